@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Benchmark: CSR SpMV effective HBM GB/s on the 300^3 7-point Poisson operand.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 300] [--kernel auto]
+
+A step is one MatMult (y = A x) of the whole operand, inputs resident in HBM.
+N = 1: the BASELINE.json configs[1] workload — 300^3 Poisson CSR (27 M rows,
+188.46 M entries, fp64 values, int32 indices) on one MI355X.
+N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL): weak
+scaling — every rank owns a 300^3 z-slab of a 300 x 300 x 300N grid (at N = 8
+this is 216 M rows, the size of BASELINE configs[3]'s 600^3), the halo planes
+exchanged over RCCL while the diagonal block multiplies (petsc-openacc_amd/
+mpiaij.py).
+
+value  = algorithmic bytes of all ranks x K / (max-over-ranks wall time of the
+         K timed steps), bytes per SpMV = 12 nnz + 4 (m+1) + 8 n + 8 m
+         (x and the matrix read once, y written once).
+roofline.achieved = the same bytes per launch / the mean duration of the
+         dominant kernel, from HIP events recorded around every launch on the
+         stream it runs on; peak 8 TB/s (MI355X_MICROARCH.md).
+cpu_baseline = the C restatement of PETSc's MatMult_SeqAIJ (oracle/, a port:
+         the reference cannot be built here) on 1 host core, bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import importlib
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md §Chip-level parameters (spec)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--grid", type=int, default=300, help="per-rank grid edge (N^3 rows per rank)")
+    p.add_argument("--kernel", default="auto", choices=["auto", "stream", "scalar", "vector", "merge"])
+    p.add_argument("--halo", default="p2p", choices=["p2p", "allgather"])
+    p.add_argument("--x", default="uniform", choices=["uniform", "exact"], help="x = splitmix(42) or generateExt")
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-cg", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(ai, aj, aa, x, seconds):
+    """Time the oracle (C restatement of MatMult_SeqAIJ) on 1 core, repeated
+    whole-operand SpMVs until `seconds` elapse (bounded sample)."""
+    build = importlib.import_module("petsc-openacc_amd.build")
+    L = ctypes.CDLL(str(build.build_oracle()))
+    P = ctypes.c_void_p
+    L.oracle_matmult_seqaij.argtypes = [ctypes.c_int32, P, P, P, P, P]
+    L.oracle_matmult_seqaij.restype = None
+    m = len(ai) - 1
+    y = np.empty(m)
+    args = (m, ai.ctypes.data, aj.ctypes.data, aa.ctypes.data, x.ctypes.data, y.ctypes.data)
+    L.oracle_matmult_seqaij(*args)  # warm-up (page-in)
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        L.oracle_matmult_seqaij(*args)
+        reps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or reps >= 50:
+            break
+    return el / reps, reps
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    pkg = importlib.import_module("petsc-openacc_amd")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (the HIP path has no CPU fallback)")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    distributed = world > 1
+    if distributed:
+        dist.init_process_group("nccl", device_id=dev)
+
+    G = args.grid
+    nx = ny = G
+    nz_global = G * world
+    row_starts = np.array([min(r * G, nz_global) * nx * ny for r in range(world + 1)], dtype=np.int64)
+    z0, z1 = rank * G, (rank + 1) * G
+    t_setup = time.perf_counter()
+    ai, aj, aa = pkg.poisson_csr(nx, ny, nz_global, z0, z1)
+    m_loc = len(ai) - 1
+    n_global = nx * ny * nz_global
+    nnz_loc = len(aj)
+
+    if args.x == "exact":
+        _, x_h = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
+    else:
+        x_h = pkg.splitmix_uniform(m_loc, 42, int(row_starts[rank]))
+    stream = torch.cuda.current_stream()
+    xd = torch.from_numpy(x_h).to(dev)
+    yd = torch.empty(m_loc, dtype=torch.float64, device=dev)
+
+    if distributed:
+        from importlib import import_module
+        mpiaij = import_module("petsc-openacc_amd.mpiaij")
+
+        def make_local(a_i, a_j, a_a, ncols):
+            return pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols, device=local_rank, kernel=args.kernel)
+
+        op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo)
+        info = op.A_d.info()
+        step = lambda: op.mult(xd, yd)  # noqa: E731
+    else:
+        A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m_loc, device=local_rank, kernel=args.kernel)
+        info = A.info()
+        step = lambda: A.mult(xd, yd, stream)  # noqa: E731
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t_setup
+
+    # global algorithmic bytes per distributed SpMV (halo bytes not counted)
+    nnz_t = torch.tensor([nnz_loc], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(nnz_t)
+    nnz_global = int(nnz_t.item())
+    bytes_global = pkg.algorithmic_bytes(n_global, n_global, nnz_global)
+    bytes_local = pkg.algorithmic_bytes(m_loc, m_loc, nnz_loc)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # per-launch HIP events on the stream the SpMV kernel runs on
+    K = args.steps
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(K):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    elapsed = float(el_t.item())
+    launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+
+    # correctness spot-check of the timed output against a fresh multiply
+    y_chk = yd.clone()
+    step()
+    torch.cuda.synchronize()
+    stable = bool(torch.equal(y_chk, yd))
+
+    cg = None
+    if not args.no_cg and not distributed:
+        try:
+            ksp = importlib.import_module("petsc-openacc_amd.ksp")
+            cg = ksp.bench_cg(pkg, A, nx, ny, nz_global, dev, iters=50)
+        except (ImportError, AttributeError):
+            cg = None
+
+    if rank == 0:
+        value = bytes_global * K / elapsed / 1e9
+        mean_launch_s = float(np.mean(launch_ms)) / 1e3
+        achieved = bytes_local / mean_launch_s / 1e9
+        out = {
+            "metric": "CSR SpMV effective HBM GB/s (300^3 7-pt Poisson, fp64 MatMult_SeqAIJ)",
+            "value": round(value, 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (generated 7-pt Poisson operand of helper.cpp; x = splitmix64 uniform[-1,1))"
+            if args.x == "uniform" else "synthetic (helper.cpp operand; x = generateExt field)",
+            "config": {
+                "workload": f"{G}x{G}x{nz_global} Poisson CSR, z-slab per GPU" if distributed
+                else f"{G}^3 Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])",
+                "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
+                "kernel": info["kernel"], "halo": args.halo if distributed else None,
+                "bytes_per_spmv": bytes_global, "flops_per_spmv_petsc": 2 * nnz_global - n_global,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "kernel_us_mean": round(mean_launch_s * 1e6, 2),
+                "kernel_us_median": round(float(np.median(launch_ms)) * 1e3, 2),
+                "kernel_us_min": round(float(np.min(launch_ms)) * 1e3, 2),
+                "bytes_per_launch": bytes_local,
+            },
+            "result_stable": stable,
+            "setup_s": round(t_setup, 2),
+        }
+        if cg is not None:
+            out["cg"] = cg
+        if not args.no_cpu_baseline and not distributed:
+            t_cpu, reps = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds)
+            out["cpu_baseline"] = {
+                "value": round(bytes_local / t_cpu / 1e9, 3),
+                "unit": "GB/s",
+                "cores": 1,
+                "kind": "port",
+                "sample": f"{reps} whole-operand {G}^3 SpMVs on 1 core ({cpu_model()}), "
+                          f"{t_cpu * 1e3:.1f} ms each; oracle/matmult_seqaij.c",
+            }
+        print(json.dumps(out), flush=True)
+
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

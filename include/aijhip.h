@@ -1,0 +1,160 @@
+/*
+ * aijhip.h — C ABI of the MI355X (gfx950) sequential-AIJ (CSR) SpMV.
+ *
+ * This is the drop-in boundary for the hot path olcf/PETSC-OpenACC offloads:
+ * PETSc 3.7.6's MatMult_SeqAIJ plus the two residency hooks the reference
+ * patches in beside it. The reference replaces three PETSc-internal C symbols
+ * at link time (/root/reference/scripts/petsc.sh:81-89 cuts them out of aij.c,
+ * /root/reference/Makefile:31,153-158 links the patched objects ahead of
+ * libpetsc.a). Those symbols take PETSc types (Mat, Vec); this ABI takes plain
+ * pointers and sizes instead, so a PETSc adapter — or any
+ * C / ctypes / FFI caller — binds it without PETSc, CUDA-compat or torch
+ * headers.
+ *
+ * Mapping (reference entry point -> this ABI):
+ *   MatAssemblyEnd_SeqAIJ hook, src/openacc-step2/MatAssemblyEnd_SeqAIJ.patch:17-44
+ *     first upload           -> aijhip_mat_create
+ *     values changed          -> aijhip_mat_update_values
+ *     structure changed       -> aijhip_mat_assembly_end
+ *   MatMult_SeqAIJ, src/openacc-step{1..4}/MatMult_SeqAIJ.patch
+ *     device-resident x, y    -> aijhip_mat_mult          (y = A x)
+ *     host x, y (step-2 form) -> aijhip_mat_mult_host     (copy x in, y out)
+ *   MatMultAdd_SeqAIJ [ext; left on the CPU by the reference, SURVEY §8f row 2]
+ *                             -> aijhip_mat_mult_add      (w = z + A x)
+ *   MatMultTranspose_SeqAIJ [ext; SURVEY §8f row 2]
+ *                             -> aijhip_mat_mult_transpose (y = A^T x)
+ *   MatDestroy_SeqAIJ hook, src/openacc-step2/MatDestroy_SeqAIJ.patch:18-34
+ *                             -> aijhip_mat_destroy
+ *
+ * Types follow the reference's PETSc build: PetscInt is int32 (no
+ * --with-64-bit-indices in scripts/petsc-release.sh:3-67), PetscScalar is
+ * real fp64 (petsc-release.sh:6,62). Offsets into aj/aa are int32 as in PETSc;
+ * all device address arithmetic is 64-bit.
+ *
+ * Error convention: every function returns 0 on success or a positive
+ * AIJHIP_ERR_* code (PetscErrorCode is an int, 0 on success; CHKERRQ-style
+ * propagation, step1 patch:16). Nothing throws across the ABI.
+ * aijhip_last_error() returns a message for the calling thread's last error.
+ *
+ * Threading: one handle = one device, one host thread at a time (PETSc 3.7
+ * objects are not thread-safe). Calls that take a `stream`
+ * (a hipStream_t passed as void*, NULL = the legacy default stream) are
+ * asynchronous with respect to the host; the ..._host variant synchronises.
+ */
+#ifndef AIJHIP_H
+#define AIJHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AIJHIP_ABI_VERSION 1
+
+enum {
+    AIJHIP_OK = 0,
+    AIJHIP_ERR_ARG = 1,      /* bad size, null pointer, malformed CSR        */
+    AIJHIP_ERR_ALLOC = 2,    /* device or host allocation failed             */
+    AIJHIP_ERR_HIP = 3,      /* a HIP runtime call failed                    */
+    AIJHIP_ERR_NODEVICE = 4, /* no usable gfx950 device                      */
+    AIJHIP_ERR_STATE = 5     /* call not valid in the handle's current state */
+};
+
+/* SpMV kernel families. AUTO picks by row-length
+ * statistics at assembly time. */
+enum {
+    AIJHIP_KERNEL_AUTO = 0,
+    AIJHIP_KERNEL_STREAM = 1, /* adaptive row blocks, products staged in LDS,
+                                 sequential per-row sum: bit-exact vs PETSc */
+    AIJHIP_KERNEL_SCALAR = 2, /* one lane per row (the reference's
+                                 `gang vector(32)` shape, step1 patch:19-21) */
+    AIJHIP_KERNEL_VECTOR = 3, /* 2..64 lanes per row, __shfl tree reduction
+                                 (64 = wavefront per row)                    */
+    AIJHIP_KERNEL_MERGE = 4   /* merge-path partition of rows+nnz, carry fix-up */
+};
+
+typedef struct aijhip_mat *aijhip_mat_t;
+
+typedef struct aijhip_info {
+    int32_t m;               /* rows                                         */
+    int32_t n;               /* columns (length of x)                        */
+    int64_t nz;              /* stored entries, explicit zeros included      */
+    int32_t nonzerorowcnt;   /* rows with >= 1 stored entry (PETSc a->nonzerorowcnt) */
+    int32_t max_row_nz;
+    int32_t compressed_row;  /* 1 if the compressed-row form is used (PETSc
+                                MatCheckCompressedRow, ratio 0.6)            */
+    int32_t kernel;          /* AIJHIP_KERNEL_* actually used by mult        */
+    int32_t vector_lanes;    /* lanes per row of the VECTOR kernel           */
+    int32_t n_blocks;        /* STREAM row blocks                            */
+    int32_t n_long_rows;     /* rows split across workgroups                 */
+    int32_t device;
+    int64_t device_bytes;    /* device memory owned by the handle            */
+    double mult_flops;       /* PETSc-logged flops per MatMult: 2nz - nonzerorowcnt
+                                (step2 MatMult patch:47)                     */
+    int64_t mult_bytes;      /* algorithmic bytes per MatMult:
+                                12 nz + 4 (m+1) + 8 n + 8 m     */
+} aijhip_info_t;
+
+/* Library / device. */
+int aijhip_abi_version(void);
+const char *aijhip_last_error(void);
+int aijhip_device_count(int *count);
+
+/* Create a device-resident copy of a host CSR matrix (ai[m+1], aj[nz],
+ * aa[nz]) on `device`. Columns must lie in [0, n) and ai must be monotone
+ * with ai[0] == 0 and ai[m] == nz; columns need not be sorted (the sum order
+ * is storage order, as in PETSc). The handle owns its device buffers; the
+ * host arrays are only read during the call. */
+int aijhip_mat_create(int device, int32_t m, int32_t n, int64_t nz,
+                      const int32_t *ai, const int32_t *aj, const double *aa,
+                      aijhip_mat_t *out);
+
+/* Same, from arrays already on `device` (e.g. a device-side assembly). The
+ * arrays are copied; the caller keeps ownership of its pointers. */
+int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
+                                  const int32_t *d_ai, const int32_t *d_aj,
+                                  const double *d_aa, aijhip_mat_t *out);
+
+/* Choose the SpMV kernel family (AIJHIP_KERNEL_*); lanes is used by VECTOR
+ * (0 = pick from the mean row length). Re-plans on the device. */
+int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
+
+/* New values, same nonzero structure (host aa[nz]): the re-upload half of
+ * MatAssemblyEnd_SeqAIJ's hook (step2 MatAssemblyEnd patch:42-44). */
+int aijhip_mat_update_values(aijhip_mat_t A, const double *aa);
+
+/* New structure and values (MAT_FINAL_ASSEMBLY after compaction): drops the
+ * device copy and re-uploads everything (step2 MatAssemblyEnd patch:21-29,
+ * :42-44). Sizes m and n are kept. */
+int aijhip_mat_assembly_end(aijhip_mat_t A, int64_t nz, const int32_t *ai,
+                            const int32_t *aj, const double *aa);
+
+/* y = A x (overwrite). x: device fp64[n], y: device fp64[m]; x and y must not
+ * alias (PETSc requires distinct Vecs). Enqueued on `stream`. */
+int aijhip_mat_mult(aijhip_mat_t A, const double *x, double *y, void *stream);
+
+/* w = z + A x. z may alias w (PETSc's yy == zz case); x must not alias w. */
+int aijhip_mat_mult_add(aijhip_mat_t A, const double *x, const double *z,
+                        double *w, void *stream);
+
+/* y = A^T x. x: device fp64[m], y: device fp64[n]. Uses a transposed copy
+ * built on first call (kept until the structure changes). */
+int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y,
+                              void *stream);
+
+/* Step-2 semantics with host vectors: x (host fp64[n]) is copied in, y
+ * (host fp64[m]) copied out; returns after y is on the host. */
+int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y);
+
+int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info);
+
+/* Free every device buffer of the handle (MatDestroy_SeqAIJ hook,
+ * step2 MatDestroy patch:18-34). NULL is a no-op. */
+int aijhip_mat_destroy(aijhip_mat_t A);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIJHIP_H */

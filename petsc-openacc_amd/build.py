@@ -1,0 +1,96 @@
+"""Build the in-tree shared libraries (gfx950 only).
+
+    python petsc-openacc_amd/build.py          # libaijhip.so (+ the oracle)
+
+libaijhip.so  — the product: HIP kernels + C ABI (include/aijhip.h) + host
+                operand producers (include/aijhip_harness.h).
+oracle/liboracle.so — the CPU checker (test infrastructure only).
+Both are git-ignored and travel to the GPU box with the gpurun snapshot.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+ROOT = PKG.parent
+CSRC = PKG / "csrc"
+LIBDIR = PKG / "lib"
+LIB = LIBDIR / "libaijhip.so"
+ORACLE_DIR = ROOT / "oracle"
+ORACLE_LIB = ORACLE_DIR / "liboracle.so"
+
+HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "dist.hip", "ksp.hip"]
+HOST_SOURCES = ["harness.cpp"]
+ARCH = os.environ.get("AIJHIP_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return c
+    raise RuntimeError("hipcc not found: the HIP path cannot be built")
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed: " + " ".join(map(str, cmd)) + "\n" + r.stdout + r.stderr)
+
+
+def build_lib(force: bool = False) -> Path:
+    LIBDIR.mkdir(exist_ok=True)
+    srcs = [CSRC / s for s in HIP_SOURCES + HOST_SOURCES if (CSRC / s).exists()]
+    deps = srcs + list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
+    if not force and not _stale(LIB, deps):
+        return LIB
+    objdir = PKG / "build"
+    objdir.mkdir(exist_ok=True)
+    hipcc = _hipcc()
+    common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"-I{ROOT / 'include'}", f"-I{CSRC}"]
+    objs = []
+    for s in srcs:
+        o = objdir / (s.stem + ".o")
+        if s.name in HOST_SOURCES:
+            cmd = ["g++", *common, "-c", str(s), "-o", str(o)]
+        else:
+            cmd = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", *common, "-c", str(s), "-o", str(o)]
+        if force or _stale(o, [s, *CSRC.glob("*.h"), *(ROOT / "include").glob("*.h")]):
+            _run(cmd)
+        objs.append(str(o))
+    tmp = LIB.with_suffix(".so.tmp")
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs])
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def build_oracle(force: bool = False) -> Path:
+    src = ORACLE_DIR / "matmult_seqaij.c"
+    if not force and not _stale(ORACLE_LIB, [src]):
+        return ORACLE_LIB
+    tmp = ORACLE_LIB.with_suffix(".so.tmp")
+    # -ffp-contract=off: each product is rounded before it is added (PETSc's
+    # x86 build has no FMA at -march=x86-64 either).
+    _run(["gcc", "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-o", str(tmp), str(src)])
+    os.replace(tmp, ORACLE_LIB)
+    return ORACLE_LIB
+
+
+def build_all(force: bool = False):
+    return build_lib(force), build_oracle(force)
+
+
+if __name__ == "__main__":
+    f = "--force" in sys.argv
+    for p in build_all(f):
+        print(p)

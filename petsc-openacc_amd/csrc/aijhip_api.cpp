@@ -1,0 +1,549 @@
+// aijhip_api.cpp — the extern "C" boundary (include/aijhip.h): device
+// residency of the CSR matrix, row-block planning and kernel dispatch.
+//
+// Residency lifecycle, as the reference's patched hooks define it:
+//   create / assembly_end  <- MatAssemblyEnd_SeqAIJ hook
+//                             (src/openacc-step2/MatAssemblyEnd_SeqAIJ.patch:17-44)
+//   destroy                <- MatDestroy_SeqAIJ hook
+//                             (src/openacc-step2/MatDestroy_SeqAIJ.patch:18-34)
+// Unlike the OpenACC present table (acc_is_present, MatAssemblyEnd patch:21-23)
+// the handle owns its device buffers explicitly: no reference counting, no
+// implicit copies on MatMult (the step-2 `enter data copyin` per call,
+// step2 MatMult patch:19-21, becomes a one-off upload here).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "aijhip_internal.h"
+
+using aijhip::BlockDesc;
+using aijhip::LongRow;
+using aijhip::LongSeg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int hipfail(hipError_t e, const char *what) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return (e == hipErrorNoDevice || e == hipErrorInvalidDevice) ? AIJHIP_ERR_NODEVICE
+                                                                 : AIJHIP_ERR_HIP;
+}
+
+// Sets the handle's device for the duration of a call, restoring the
+// caller's current device afterwards (torch keeps its own notion of it).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        err = hipGetDevice(&prev);
+        if (err == hipSuccess && prev != dev) err = hipSetDevice(dev);
+        else if (err == hipSuccess) prev = -1;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename T>
+hipError_t dmalloc(T **p, size_t count, int64_t *acct) {
+    *p = nullptr;
+    const size_t bytes = sizeof(T) * (count > 0 ? count : 1);
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+    if (e == hipSuccess && acct) *acct += (int64_t)bytes;
+    return e;
+}
+
+void free_plan(aijhip::Plan &P) {
+    hipFree(P.d_blocks);
+    hipFree(P.d_segs);
+    hipFree(P.d_longs);
+    hipFree(P.d_partials);
+    hipFree(P.d_tile_coord);
+    hipFree(P.d_carry_row);
+    hipFree(P.d_carry_val);
+    P = aijhip::Plan();
+}
+
+void free_matrix(aijhip_mat *A) {
+    free_plan(A->plan);
+    hipFree(A->d_ai);
+    hipFree(A->d_aj);
+    hipFree(A->d_aa);
+    hipFree(A->d_cai);
+    hipFree(A->d_ridx);
+    A->d_ai = A->d_aj = A->d_cai = A->d_ridx = nullptr;
+    A->d_aa = nullptr;
+    A->device_bytes = 0;
+    A->h_rai.clear();
+    A->h_rai.shrink_to_fit();
+    if (A->transpose) {
+        free_matrix(A->transpose);
+        delete A->transpose;
+        A->transpose = nullptr;
+    }
+}
+
+int validate_csr(int32_t m, int32_t n, int64_t nz, const int32_t *ai, const int32_t *aj) {
+    if (m < 0 || n < 0 || nz < 0) return fail(AIJHIP_ERR_ARG, "negative size");
+    if (nz > INT32_MAX) return fail(AIJHIP_ERR_ARG, "nz exceeds the int32 PetscInt range");
+    if (!ai) return fail(AIJHIP_ERR_ARG, "ai is NULL");
+    if (nz > 0 && !aj) return fail(AIJHIP_ERR_ARG, "aj is NULL");
+    if (ai[0] != 0) return fail(AIJHIP_ERR_ARG, "ai[0] != 0");
+    for (int32_t i = 0; i < m; ++i)
+        if (ai[i + 1] < ai[i]) return fail(AIJHIP_ERR_ARG, "ai is not monotone at row " + std::to_string(i));
+    if (ai[m] != nz) return fail(AIJHIP_ERR_ARG, "ai[m] != nz");
+    for (int64_t k = 0; k < nz; ++k)
+        if ((uint32_t)aj[k] >= (uint32_t)n)
+            return fail(AIJHIP_ERR_ARG, "column index out of range at entry " + std::to_string(k));
+    return AIJHIP_OK;
+}
+
+// CSR-stream row blocks over the handle's row list (h_rai): greedily pack
+// consecutive rows while the block holds <= kStreamNnzCap entries and
+// <= kStreamRowCap rows. A row longer than kStreamNnzCap becomes a long row,
+// split into segments of <= kLongSegNnz entries.
+int plan_stream(aijhip_mat *A) {
+    using namespace aijhip;
+    const std::vector<int32_t> &rai = A->h_rai;
+    const int32_t nr = rai.empty() ? 0 : (int32_t)rai.size() - 1;
+    std::vector<BlockDesc> blocks;
+    std::vector<LongSeg> segs;
+    std::vector<LongRow> longs;
+    blocks.reserve((size_t)nr / 64 + 8);
+    std::vector<int32_t> h_ridx;
+    if (A->compressed && A->n_crow > 0) {
+        h_ridx.resize(A->n_crow);
+        hipError_t e = hipMemcpy(h_ridx.data(), A->d_ridx, sizeof(int32_t) * A->n_crow, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hipfail(e, "plan: read ridx");
+    }
+    int32_t r = 0;
+    while (r < nr) {
+        const int32_t len = rai[r + 1] - rai[r];
+        if (len > kStreamNnzCap) {
+            LongRow lr{};
+            lr.orow = A->compressed ? h_ridx[r] : r;
+            lr.seg0 = (int32_t)segs.size();
+            for (int64_t k = rai[r]; k < rai[r + 1]; k += kLongSegNnz) {
+                const int64_t nk = std::min<int64_t>(kLongSegNnz, rai[r + 1] - k);
+                segs.push_back(LongSeg{(int32_t)k, (int32_t)nk});
+            }
+            lr.nseg = (int32_t)segs.size() - lr.seg0;
+            longs.push_back(lr);
+            ++r;
+            continue;
+        }
+        const int32_t start = r;
+        int32_t nk = 0;
+        while (r < nr && r - start < kStreamRowCap) {
+            const int32_t l = rai[r + 1] - rai[r];
+            if (l > kStreamNnzCap || nk + l > kStreamNnzCap) break;
+            nk += l;
+            ++r;
+        }
+        blocks.push_back(BlockDesc{start, r - start, rai[start], nk});
+    }
+    Plan &P = A->plan;
+    P.n_blocks = (int32_t)blocks.size();
+    P.n_segs = (int32_t)segs.size();
+    P.n_longs = (int32_t)longs.size();
+    hipError_t e;
+    if ((e = dmalloc(&P.d_blocks, blocks.size(), &P.bytes)) != hipSuccess) return hipfail(e, "plan: alloc blocks");
+    if (!blocks.empty() &&
+        (e = hipMemcpy(P.d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return hipfail(e, "plan: upload blocks");
+    if (!longs.empty()) {
+        if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
+            (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
+            (e = dmalloc(&P.d_partials, segs.size(), &P.bytes)) != hipSuccess)
+            return hipfail(e, "plan: alloc long rows");
+        if ((e = hipMemcpy(P.d_segs, segs.data(), sizeof(LongSeg) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(P.d_longs, longs.data(), sizeof(LongRow) * longs.size(), hipMemcpyHostToDevice)) != hipSuccess)
+            return hipfail(e, "plan: upload long rows");
+    }
+    return AIJHIP_OK;
+}
+
+int plan_merge(aijhip_mat *A) {
+    using namespace aijhip;
+    Plan &P = A->plan;
+    const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
+    const int64_t items = (int64_t)nr + A->nz;
+    const int64_t nt = (items + kMergeTile - 1) / kMergeTile;
+    if (nt > INT32_MAX - 2) return fail(AIJHIP_ERR_ARG, "merge plan: too many tiles");
+    P.n_tiles = (int32_t)nt;
+    hipError_t e;
+    if ((e = dmalloc(&P.d_tile_coord, (size_t)nt + 1, &P.bytes)) != hipSuccess ||
+        (e = dmalloc(&P.d_carry_row, (size_t)nt, &P.bytes)) != hipSuccess ||
+        (e = dmalloc(&P.d_carry_val, (size_t)nt, &P.bytes)) != hipSuccess)
+        return hipfail(e, "plan: alloc merge tiles");
+    if (nt > 0) {
+        if ((e = merge_plan_coords(*A, P.d_tile_coord, P.n_tiles, nullptr)) != hipSuccess ||
+            (e = hipDeviceSynchronize()) != hipSuccess)
+            return hipfail(e, "plan: merge coordinates");
+    }
+    return AIJHIP_OK;
+}
+
+int plan_build(aijhip_mat *A) {
+    free_plan(A->plan);
+    aijhip::Plan &P = A->plan;
+    int kernel = A->requested_kernel;
+    if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
+    P.kernel = kernel;
+    switch (kernel) {
+        case AIJHIP_KERNEL_STREAM:
+            return plan_stream(A);
+        case AIJHIP_KERNEL_SCALAR:
+            return AIJHIP_OK;
+        case AIJHIP_KERNEL_VECTOR: {
+            int lanes = A->requested_lanes;
+            if (lanes == 0) {
+                const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
+                const double mean = nr > 0 ? (double)A->nz / nr : 1.0;
+                lanes = 2;
+                while (lanes < 64 && lanes < mean) lanes <<= 1;
+            }
+            if (lanes != 2 && lanes != 4 && lanes != 8 && lanes != 16 && lanes != 32 && lanes != 64)
+                return fail(AIJHIP_ERR_ARG, "VECTOR lanes must be a power of two in [2, 64]");
+            P.lanes = lanes;
+            return AIJHIP_OK;
+        }
+        case AIJHIP_KERNEL_MERGE:
+            return plan_merge(A);
+        default:
+            return fail(AIJHIP_ERR_ARG, "unknown kernel " + std::to_string(kernel));
+    }
+}
+
+// Uploads a validated host CSR into A (sizes already set) and plans it.
+int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const double *aa) {
+    const int32_t m = A->m;
+    const int64_t nz = A->nz;
+    hipError_t e;
+    // structure statistics (PETSc a->nonzerorowcnt, MatCheckCompressedRow)
+    int32_t nzrows = 0, maxlen = 0;
+    for (int32_t i = 0; i < m; ++i) {
+        const int32_t l = ai[i + 1] - ai[i];
+        nzrows += l > 0;
+        maxlen = std::max(maxlen, l);
+    }
+    A->nonzerorowcnt = nzrows;
+    A->max_row_nz = maxlen;
+    // PETSc uses the compressed-row form when at least 60% of the rows are
+    // empty (MatCheckCompressedRow(..., ratio=0.6) in MatAssemblyEnd_SeqAIJ,
+    // step2 MatAssemblyEnd patch context :35 [ext]).
+    A->compressed = m > 0 && (1.0 - (double)nzrows / (double)m) >= 0.6;
+
+    if ((e = dmalloc(&A->d_ai, (size_t)m + 1, &A->device_bytes)) != hipSuccess ||
+        (e = dmalloc(&A->d_aj, (size_t)nz + 2, &A->device_bytes)) != hipSuccess ||
+        (e = dmalloc(&A->d_aa, (size_t)nz + 2, &A->device_bytes)) != hipSuccess)
+        return hipfail(e, "alloc CSR");
+    if ((e = hipMemcpy(A->d_ai, ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(A->d_aj + nz, 0, 2 * sizeof(int32_t))) != hipSuccess ||
+        (e = hipMemset(A->d_aa + nz, 0, 2 * sizeof(double))) != hipSuccess)
+        return hipfail(e, "upload ai");
+    if (nz > 0 &&
+        ((e = hipMemcpy(A->d_aj, aj, sizeof(int32_t) * (size_t)nz, hipMemcpyHostToDevice)) != hipSuccess ||
+         (e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)nz, hipMemcpyHostToDevice)) != hipSuccess))
+        return hipfail(e, "upload aj/aa");
+    if (A->compressed) {
+        std::vector<int32_t> cai, ridx;
+        cai.reserve((size_t)nzrows + 1);
+        ridx.reserve((size_t)nzrows);
+        for (int32_t i = 0; i < m; ++i)
+            if (ai[i + 1] > ai[i]) { cai.push_back(ai[i]); ridx.push_back(i); }
+        cai.push_back((int32_t)nz);
+        A->n_crow = nzrows;
+        if ((e = dmalloc(&A->d_cai, cai.size(), &A->device_bytes)) != hipSuccess ||
+            (e = dmalloc(&A->d_ridx, ridx.size(), &A->device_bytes)) != hipSuccess)
+            return hipfail(e, "alloc compressed rows");
+        if ((e = hipMemcpy(A->d_cai, cai.data(), sizeof(int32_t) * cai.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+            (!ridx.empty() &&
+             (e = hipMemcpy(A->d_ridx, ridx.data(), sizeof(int32_t) * ridx.size(), hipMemcpyHostToDevice)) != hipSuccess))
+            return hipfail(e, "upload compressed rows");
+        A->h_rai.swap(cai);
+    } else {
+        A->n_crow = 0;
+        A->h_rai.assign(ai, ai + (size_t)m + 1);
+    }
+    return plan_build(A);
+}
+
+int check_handle(aijhip_mat_t A) {
+    if (!A) return fail(AIJHIP_ERR_ARG, "NULL handle");
+    return AIJHIP_OK;
+}
+
+int mult_impl(aijhip_mat_t A, const double *x, const double *z, double *y, bool add, void *stream) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (A->m == 0) return AIJHIP_OK;
+    if (!y || (A->nz > 0 && !x) || (add && !z)) return fail(AIJHIP_ERR_ARG, "NULL vector");
+    if (x == y) return fail(AIJHIP_ERR_ARG, "x and y alias (PETSc requires distinct Vecs)");
+    DeviceGuard g(A->device);
+    if (g.err != hipSuccess) return hipfail(g.err, "set device");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipError_t e;
+    switch (A->plan.kernel) {
+        case AIJHIP_KERNEL_STREAM: e = aijhip::launch_stream(*A, x, z, y, add, s); break;
+        case AIJHIP_KERNEL_SCALAR: e = aijhip::launch_scalar(*A, x, z, y, add, s); break;
+        case AIJHIP_KERNEL_VECTOR: e = aijhip::launch_vector(*A, x, z, y, add, s); break;
+        case AIJHIP_KERNEL_MERGE: e = aijhip::launch_merge(*A, x, z, y, add, s); break;
+        default: return fail(AIJHIP_ERR_STATE, "handle has no plan");
+    }
+    if (e != hipSuccess) return hipfail(e, "SpMV launch");
+    return AIJHIP_OK;
+}
+
+int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
+                const int32_t *aj, const double *aa, aijhip_mat_t *out) {
+    if (!out) return fail(AIJHIP_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int rc = validate_csr(m, n, nz, ai, aj);
+    if (rc) return rc;
+    if (nz > 0 && !aa) return fail(AIJHIP_ERR_ARG, "aa is NULL");
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) return fail(AIJHIP_ERR_NODEVICE, "no HIP device visible");
+    if (device < 0 || device >= count) return fail(AIJHIP_ERR_ARG, "device ordinal out of range");
+    DeviceGuard g(device);
+    if (g.err != hipSuccess) return hipfail(g.err, "set device");
+    aijhip_mat *A = new (std::nothrow) aijhip_mat();
+    if (!A) return fail(AIJHIP_ERR_ALLOC, "host allocation");
+    A->device = device;
+    A->m = m;
+    A->n = n;
+    A->nz = nz;
+    rc = upload_and_plan(A, ai, aj, aa);
+    if (rc) {
+        free_matrix(A);
+        delete A;
+        return rc;
+    }
+    *out = A;
+    return AIJHIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int aijhip_abi_version(void) { return AIJHIP_ABI_VERSION; }
+
+const char *aijhip_last_error(void) { return g_err.c_str(); }
+
+int aijhip_device_count(int *count) {
+    if (!count) return fail(AIJHIP_ERR_ARG, "count is NULL");
+    *count = 0;
+    hipError_t e = hipGetDeviceCount(count);
+    if (e != hipSuccess) {
+        *count = 0;
+        return hipfail(e, "hipGetDeviceCount");
+    }
+    return AIJHIP_OK;
+}
+
+int aijhip_mat_create(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
+                      const int32_t *aj, const double *aa, aijhip_mat_t *out) {
+    return create_impl(device, m, n, nz, ai, aj, aa, out);
+}
+
+int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
+                                  const int32_t *d_ai, const int32_t *d_aj,
+                                  const double *d_aa, aijhip_mat_t *out) {
+    if (!out) return fail(AIJHIP_ERR_ARG, "out is NULL");
+    if (m < 0 || n < 0 || nz < 0 || !d_ai || (nz > 0 && (!d_aj || !d_aa)))
+        return fail(AIJHIP_ERR_ARG, "bad size or NULL array");
+    // Planning and validation read the structure on the host.
+    std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nz);
+    std::vector<double> aa((size_t)nz);
+    {
+        DeviceGuard g(device);
+        if (g.err != hipSuccess) return hipfail(g.err, "set device");
+        hipError_t e;
+        if ((e = hipMemcpy(ai.data(), d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
+            (nz > 0 && ((e = hipMemcpy(aj.data(), d_aj, sizeof(int32_t) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess ||
+                        (e = hipMemcpy(aa.data(), d_aa, sizeof(double) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess)))
+            return hipfail(e, "read device CSR");
+    }
+    return create_impl(device, m, n, nz, ai.data(), aj.data(), aa.data(), out);
+}
+
+int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (kernel < AIJHIP_KERNEL_AUTO || kernel > AIJHIP_KERNEL_MERGE)
+        return fail(AIJHIP_ERR_ARG, "unknown kernel " + std::to_string(kernel));
+    DeviceGuard g(A->device);
+    if (g.err != hipSuccess) return hipfail(g.err, "set device");
+    hipError_t e = hipDeviceSynchronize();  // in-flight launches may read the old plan
+    if (e != hipSuccess) return hipfail(e, "sync before re-plan");
+    A->requested_kernel = kernel;
+    A->requested_lanes = lanes;
+    return plan_build(A);
+}
+
+int aijhip_mat_update_values(aijhip_mat_t A, const double *aa) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (A->nz > 0 && !aa) return fail(AIJHIP_ERR_ARG, "aa is NULL");
+    DeviceGuard g(A->device);
+    if (g.err != hipSuccess) return hipfail(g.err, "set device");
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess && A->nz > 0)
+        e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)A->nz, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hipfail(e, "update values");
+    if (A->transpose) {  // A^T values are stale
+        free_matrix(A->transpose);
+        delete A->transpose;
+        A->transpose = nullptr;
+    }
+    return AIJHIP_OK;
+}
+
+int aijhip_mat_assembly_end(aijhip_mat_t A, int64_t nz, const int32_t *ai, const int32_t *aj,
+                            const double *aa) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    aijhip_mat_t B = nullptr;
+    rc = create_impl(A->device, A->m, A->n, nz, ai, aj, aa, &B);
+    if (rc) return rc;
+    rc = aijhip_mat_set_kernel(B, A->requested_kernel, A->requested_lanes);
+    if (rc) {
+        aijhip_mat_destroy(B);
+        return rc;
+    }
+    {
+        DeviceGuard g(A->device);
+        (void)hipDeviceSynchronize();
+        free_matrix(A);
+        if (A->d_xstage) hipFree(A->d_xstage);
+        if (A->d_ystage) hipFree(A->d_ystage);
+        if (A->host_stream) hipStreamDestroy(A->host_stream);
+    }
+    *A = std::move(*B);
+    B->transpose = nullptr;
+    B->d_xstage = B->d_ystage = nullptr;
+    B->host_stream = nullptr;
+    B->plan = aijhip::Plan();
+    delete B;
+    return AIJHIP_OK;
+}
+
+int aijhip_mat_mult(aijhip_mat_t A, const double *x, double *y, void *stream) {
+    return mult_impl(A, x, nullptr, y, false, stream);
+}
+
+int aijhip_mat_mult_add(aijhip_mat_t A, const double *x, const double *z, double *w,
+                        void *stream) {
+    if (A && x && x == w) return fail(AIJHIP_ERR_ARG, "x and w alias");
+    return mult_impl(A, x, z, w, true, stream);
+}
+
+int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y, void *stream) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (A->n == 0) return AIJHIP_OK;
+    if (!A->transpose) {
+        DeviceGuard g(A->device);
+        if (g.err != hipSuccess) return hipfail(g.err, "set device");
+        int32_t *tai = nullptr, *taj = nullptr;
+        double *taa = nullptr;
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = aijhip::build_transpose(*A, &tai, &taj, &taa, nullptr);
+        if (e != hipSuccess) return hipfail(e, "build transpose");
+        aijhip_mat *T = new (std::nothrow) aijhip_mat();
+        if (!T) {
+            hipFree(tai); hipFree(taj); hipFree(taa);
+            return fail(AIJHIP_ERR_ALLOC, "host allocation");
+        }
+        T->device = A->device;
+        T->m = A->n;
+        T->n = A->m;
+        T->nz = A->nz;
+        std::vector<int32_t> h_tai((size_t)T->m + 1), h_taj((size_t)T->nz);
+        std::vector<double> h_taa((size_t)T->nz);
+        e = hipMemcpy(h_tai.data(), tai, sizeof(int32_t) * h_tai.size(), hipMemcpyDeviceToHost);
+        if (e == hipSuccess && T->nz > 0) e = hipMemcpy(h_taj.data(), taj, sizeof(int32_t) * (size_t)T->nz, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && T->nz > 0) e = hipMemcpy(h_taa.data(), taa, sizeof(double) * (size_t)T->nz, hipMemcpyDeviceToHost);
+        hipFree(tai); hipFree(taj); hipFree(taa);
+        if (e != hipSuccess) { delete T; return hipfail(e, "read transpose"); }
+        T->requested_kernel = A->requested_kernel == AIJHIP_KERNEL_VECTOR ? AIJHIP_KERNEL_AUTO : A->requested_kernel;
+        rc = upload_and_plan(T, h_tai.data(), h_taj.data(), h_taa.data());
+        if (rc) { free_matrix(T); delete T; return rc; }
+        A->transpose = T;
+    }
+    return mult_impl(A->transpose, x, nullptr, y, false, stream);
+}
+
+int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (A->m == 0) return AIJHIP_OK;
+    if (!y || (A->n > 0 && !x)) return fail(AIJHIP_ERR_ARG, "NULL vector");
+    DeviceGuard g(A->device);
+    if (g.err != hipSuccess) return hipfail(g.err, "set device");
+    hipError_t e = hipSuccess;
+    if (!A->host_stream) e = hipStreamCreateWithFlags(&A->host_stream, hipStreamNonBlocking);
+    if (e == hipSuccess && !A->d_xstage) e = dmalloc(&A->d_xstage, (size_t)A->n, &A->device_bytes);
+    if (e == hipSuccess && !A->d_ystage) e = dmalloc(&A->d_ystage, (size_t)A->m, &A->device_bytes);
+    if (e != hipSuccess) return hipfail(e, "host staging");
+    // step2 MatMult patch:24 (x H2D), :27-40 (kernel), :29 (y D2H)
+    if (A->n > 0 &&
+        (e = hipMemcpyAsync(A->d_xstage, x, sizeof(double) * (size_t)A->n, hipMemcpyHostToDevice, A->host_stream)) != hipSuccess)
+        return hipfail(e, "copy x in");
+    rc = mult_impl(A, A->d_xstage, nullptr, A->d_ystage, false, A->host_stream);
+    if (rc) return rc;
+    if ((e = hipMemcpyAsync(y, A->d_ystage, sizeof(double) * (size_t)A->m, hipMemcpyDeviceToHost, A->host_stream)) != hipSuccess ||
+        (e = hipStreamSynchronize(A->host_stream)) != hipSuccess)
+        return hipfail(e, "copy y out");
+    return AIJHIP_OK;
+}
+
+int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (!info) return fail(AIJHIP_ERR_ARG, "info is NULL");
+    std::memset(info, 0, sizeof(*info));
+    info->m = A->m;
+    info->n = A->n;
+    info->nz = A->nz;
+    info->nonzerorowcnt = A->nonzerorowcnt;
+    info->max_row_nz = A->max_row_nz;
+    info->compressed_row = A->compressed ? 1 : 0;
+    info->kernel = A->plan.kernel;
+    info->vector_lanes = A->plan.lanes;
+    info->n_blocks = A->plan.n_blocks;
+    info->n_long_rows = A->plan.n_longs;
+    info->device = A->device;
+    info->device_bytes = A->device_bytes + A->plan.bytes;
+    info->mult_flops = 2.0 * (double)A->nz - (double)A->nonzerorowcnt;
+    info->mult_bytes = 12 * A->nz + 4 * ((int64_t)A->m + 1) + 8 * (int64_t)A->n + 8 * (int64_t)A->m;
+    return AIJHIP_OK;
+}
+
+int aijhip_mat_destroy(aijhip_mat_t A) {
+    if (!A) return AIJHIP_OK;
+    {
+        DeviceGuard g(A->device);
+        (void)hipDeviceSynchronize();
+        free_matrix(A);
+        hipFree(A->d_xstage);
+        hipFree(A->d_ystage);
+        if (A->host_stream) hipStreamDestroy(A->host_stream);
+    }
+    delete A;
+    return AIJHIP_OK;
+}
+
+}  // extern "C"

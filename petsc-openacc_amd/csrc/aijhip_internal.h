@@ -1,0 +1,122 @@
+// aijhip_internal.h — handle layout and kernel launchers shared by the
+// SpMV translation units. Not part of the ABI (include/aijhip.h is).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "aijhip.h"
+
+namespace aijhip {
+
+// STREAM kernel geometry: 256 lanes = 4 waves per row
+// block; up to kStreamNnzCap products staged in LDS (16 KiB fp64) and up to
+// kStreamRowCap rows, one row per lane in the reduction phase.
+constexpr int kStreamThreads = 256;
+constexpr int kStreamNnzCap = 2048;
+constexpr int kStreamRowCap = 256;
+// A row longer than kStreamNnzCap leaves the STREAM blocks and is split into
+// segments of at most kLongSegNnz entries, each summed by one workgroup.
+constexpr int kLongSegNnz = 16384;
+constexpr int kLongThreads = 256;
+// MERGE kernel: 256 lanes x kMergeItems merge-path items per workgroup.
+constexpr int kMergeThreads = 256;
+constexpr int kMergeItems = 8;
+constexpr int kMergeTile = kMergeThreads * kMergeItems;
+
+// One STREAM row block: rows [row0, row0+nrows) of the row list, entries
+// [k0, k0+nk) of aj/aa.
+struct BlockDesc {
+    int32_t row0, nrows, k0, nk;
+};
+
+// One segment of a long row: entries [k0, k0+nk), partial sum -> partials[seg].
+struct LongSeg {
+    int32_t k0, nk;
+};
+
+// A long row: output row `orow`, segments [seg0, seg0+nseg).
+struct LongRow {
+    int32_t orow, seg0, nseg, pad;
+};
+
+// Row list the kernels walk: nr rows with offsets rai[0..nr] into aj/aa and
+// (compressed-row form only) output row ids ridx[0..nr-1].
+struct RowList {
+    int32_t nr;
+    const int32_t *rai;
+    const int32_t *ridx;  // nullptr = identity
+};
+
+struct Plan {
+    int kernel = AIJHIP_KERNEL_STREAM;
+    int lanes = 0;
+    // STREAM
+    BlockDesc *d_blocks = nullptr;
+    int32_t n_blocks = 0;
+    LongSeg *d_segs = nullptr;
+    int32_t n_segs = 0;
+    LongRow *d_longs = nullptr;
+    int32_t n_longs = 0;
+    double *d_partials = nullptr;
+    // MERGE: merge-path start coordinate of every tile (+1 sentinel)
+    int2 *d_tile_coord = nullptr;
+    int32_t n_tiles = 0;
+    int2 *d_carry_row = nullptr;   // per tile: row of its carry-out (or -1)
+    double *d_carry_val = nullptr;
+    int64_t bytes = 0;  // device bytes held by the plan
+};
+
+}  // namespace aijhip
+
+struct aijhip_mat {
+    int device = 0;
+    int32_t m = 0, n = 0;
+    int64_t nz = 0;
+    int32_t nonzerorowcnt = 0;
+    int32_t max_row_nz = 0;
+    bool compressed = false;
+    int32_t *d_ai = nullptr;
+    int32_t *d_aj = nullptr;   // nz + 2 entries: the tail pad keeps 16-B loads in bounds
+    double *d_aa = nullptr;    // nz + 2 entries
+    int32_t n_crow = 0;        // compressed-row form (PETSc a->compressedrow)
+    int32_t *d_cai = nullptr;
+    int32_t *d_ridx = nullptr;
+    std::vector<int32_t> h_rai;  // host copy of the row-list offsets (planning)
+    aijhip::Plan plan;
+    int requested_kernel = AIJHIP_KERNEL_AUTO;
+    int requested_lanes = 0;
+    // host-vector staging for aijhip_mat_mult_host (allocated on first use)
+    double *d_xstage = nullptr, *d_ystage = nullptr;
+    hipStream_t host_stream = nullptr;
+    // lazily built A^T (for aijhip_mat_mult_transpose)
+    aijhip_mat *transpose = nullptr;
+    int64_t device_bytes = 0;
+};
+
+namespace aijhip {
+
+// Launchers (aijhip_kernels.hip). All enqueue on `s` and return the launch's
+// hipError_t.
+hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z,
+                         double *y, bool add, hipStream_t s);
+hipError_t launch_scalar(const aijhip_mat &A, const double *x, const double *z,
+                         double *y, bool add, hipStream_t s);
+hipError_t launch_vector(const aijhip_mat &A, const double *x, const double *z,
+                         double *y, bool add, hipStream_t s);
+hipError_t launch_merge(const aijhip_mat &A, const double *x, const double *z,
+                        double *y, bool add, hipStream_t s);
+// MERGE planning: merge-path coordinates of every tile start (device search).
+hipError_t merge_plan_coords(const aijhip_mat &A, int2 *d_coord, int32_t n_tiles,
+                             hipStream_t s);
+// Transpose (stable by row): builds At's device CSR (n x m). Returns arrays
+// allocated with hipMalloc; caller owns them.
+hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj,
+                           double **d_taa, hipStream_t s);
+
+RowList row_list(const aijhip_mat &A);
+
+}  // namespace aijhip

@@ -1,0 +1,521 @@
+// aijhip_kernels.hip — gfx950 CSR SpMV kernels (y = A x, w = z + A x).
+//
+// Replaces the PGI-generated OpenACC kernels of
+// /root/reference/src/openacc-step{1..4}/MatMult_SeqAIJ.patch. The arithmetic
+// contract is the PETSc row loop (step1 patch:22-31): per row, products
+// aa[k]*x[aj[k]] rounded to fp64 and added in storage order starting at 0.0
+// (or z[i] for MatMultAdd). The build uses -ffp-contract=off so no product is
+// fused into an add.
+//
+//  STREAM  (default) — CSR-stream row blocks: a 256-lane workgroup streams the
+//          contiguous aa/aj range of up to 256 rows / 2048 entries with
+//          16-byte loads, gathers x, stages the products in LDS, then each
+//          lane sums one row sequentially. Every global access of the matrix
+//          is a full-width coalesced load and every lane is busy in the
+//          streaming phase, independent of row length; the per-row order is
+//          PETSc's, so results are bit-identical to the CPU loop.
+//  SCALAR  — one lane per row: the reference's kernel shape (`gang vector(32)`
+//          with a sequential inner dot, step1 patch:19-31). Bit-exact, but
+//          its loads are strided by the row length (kept as a baseline).
+//  VECTOR  — L = 2..64 lanes per row (64 = one wavefront per row), strided
+//          loads, __shfl_xor tree reduction. For long uniform rows.
+//  MERGE   — merge-path (Merrill & Garland) equal split of the rows+entries
+//          merge list over lanes; rows cut by a lane or tile boundary are
+//          completed by an in-tile chain and a per-tile carry fix-up. For
+//          skewed row lengths (the Flan_1565 stress config).
+//
+// Rows longer than 2048 entries leave the STREAM blocks and are split into
+// 16K-entry segments, each reduced by one workgroup, then summed in segment
+// order by a finishing kernel (deterministic, not bit-identical).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "aijhip_internal.h"
+
+namespace aijhip {
+namespace {
+
+// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH §Workgroup
+// dispatch). Give each XCD a contiguous run of row blocks so the x window of
+// a 7-point stencil (+-N^2 rows) stays inside that XCD's 4 MiB L2. Bijective
+// for any grid size; affects speed only, never results.
+__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
+    const int q = nblk >> 3, r = nblk & 7;
+    const int xcd = bid & 7, local = bid >> 3;
+    return xcd * q + min(xcd, r) + local;
+}
+
+constexpr int kStreamIters = (kStreamNnzCap + 1 + 2 * kStreamThreads - 1) / (2 * kStreamThreads);
+
+template <bool ADD, bool CROW, bool XCD>
+__global__ __launch_bounds__(kStreamThreads) void k_spmv_stream(
+    const BlockDesc *__restrict__ blk, int nblk, const int32_t *__restrict__ rai,
+    const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
+    const double *__restrict__ aa, const double *__restrict__ x,
+    const double *z, double *y) {
+    __shared__ double prod[kStreamNnzCap];
+    const int b = XCD ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
+    const BlockDesc d = blk[b];
+    const int t = threadIdx.x;
+    const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
+
+    // Row extents and MatMultAdd seeds first: they overlap the stream below.
+    int32_t rs = 0, re = 0, orow = 0;
+    double sum = 0.0;
+    if (t < d.nrows) {
+        const int r = d.row0 + t;
+        rs = rai[r];
+        re = rai[r + 1];
+        orow = CROW ? ridx[r] : r;
+        if (ADD) sum = z[orow];
+    }
+
+    // Phase 1: coalesced 16-B loads of aa and 8-B loads of aj from an even
+    // (16-B aligned) start; the arrays carry a 2-entry tail pad.
+    const int64_t kb = k0 & ~int64_t(1);
+    double2 av[kStreamIters];
+    int2 cv[kStreamIters];
+#pragma unroll
+    for (int it = 0; it < kStreamIters; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * kStreamThreads);
+        if (k < k1) {
+            av[it] = *reinterpret_cast<const double2 *>(aa + k);
+            cv[it] = *reinterpret_cast<const int2 *>(aj + k);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kStreamIters; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * kStreamThreads);
+        if (k < k1) {
+            if (k >= k0) prod[k - k0] = av[it].x * x[cv[it].x];
+            if (k + 1 < k1) prod[k + 1 - k0] = av[it].y * x[cv[it].y];
+        }
+    }
+    __syncthreads();
+
+    // Phase 2: one lane per row, PETSc's sequential order.
+    if (t < d.nrows) {
+        for (int32_t k = rs; k < re; ++k) sum += prod[k - k0];
+        y[orow] = sum;
+    }
+}
+
+// Segments of long rows: tree-reduced partial sums.
+__global__ __launch_bounds__(kLongThreads) void k_long_partial(
+    const LongSeg *__restrict__ seg, const int32_t *__restrict__ aj,
+    const double *__restrict__ aa, const double *__restrict__ x,
+    double *__restrict__ partials) {
+    __shared__ double red[kLongThreads / 64];
+    const LongSeg s = seg[blockIdx.x];
+    const int t = threadIdx.x;
+    double acc = 0.0;
+    const int64_t k1 = (int64_t)s.k0 + s.nk;
+    for (int64_t k = (int64_t)s.k0 + t; k < k1; k += kLongThreads) acc += aa[k] * x[aj[k]];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((t & 63) == 0) red[t >> 6] = acc;
+    __syncthreads();
+    if (t == 0) {
+        double v = red[0];
+#pragma unroll
+        for (int w = 1; w < kLongThreads / 64; ++w) v += red[w];
+        partials[blockIdx.x] = v;
+    }
+}
+
+template <bool ADD>
+__global__ void k_long_finish(const LongRow *__restrict__ lr, int nl,
+                              const double *__restrict__ partials, const double *z,
+                              double *y) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nl) return;
+    const LongRow r = lr[i];
+    double s = ADD ? z[r.orow] : 0.0;
+    for (int q = 0; q < r.nseg; ++q) s += partials[r.seg0 + q];
+    y[r.orow] = s;
+}
+
+template <bool ADD, bool CROW>
+__global__ __launch_bounds__(256) void k_spmv_scalar(
+    int nr, const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx,
+    const int32_t *__restrict__ aj, const double *__restrict__ aa,
+    const double *__restrict__ x, const double *z, double *y) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nr) return;
+    const int orow = CROW ? ridx[i] : i;
+    double s = ADD ? z[orow] : 0.0;
+    const int32_t k1 = rai[i + 1];
+    for (int32_t k = rai[i]; k < k1; ++k) s += aa[k] * x[aj[k]];
+    y[orow] = s;
+}
+
+template <int L, bool ADD, bool CROW>
+__global__ __launch_bounds__(256) void k_spmv_vector(
+    int nr, const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx,
+    const int32_t *__restrict__ aj, const double *__restrict__ aa,
+    const double *__restrict__ x, const double *z, double *y) {
+    const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t row = gid / L;
+    const int lane = threadIdx.x & (L - 1);
+    if (row >= nr) return;  // uniform across the L lanes of a row group
+    double acc = 0.0;
+    const int32_t k1 = rai[row + 1];
+    for (int32_t k = rai[row] + lane; k < k1; k += L) acc += aa[k] * x[aj[k]];
+#pragma unroll
+    for (int off = L / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, L);
+    if (lane == 0) {
+        const int orow = CROW ? ridx[row] : (int)row;
+        y[orow] = ADD ? z[orow] + acc : acc;
+    }
+}
+
+// ------------------------------------------------------------ merge path
+// Global merge-path search: coordinate (row-ends consumed, entries consumed)
+// of diagonal `diag` of the merge of rai[1..nr] with 0..K-1.
+__device__ __forceinline__ int2 merge_search_global(int64_t diag, const int32_t *rai,
+                                                    int nr, int64_t K) {
+    int64_t lo = diag - K > 0 ? diag - K : 0;
+    int64_t hi = diag < nr ? diag : nr;
+    while (lo < hi) {
+        const int64_t p = (lo + hi) >> 1;
+        if ((int64_t)rai[p + 1] <= diag - p - 1) lo = p + 1;
+        else hi = p;
+    }
+    return make_int2((int)lo, (int)(diag - lo));
+}
+
+__global__ void k_merge_coords(int ntiles, const int32_t *__restrict__ rai, int nr,
+                               int64_t K, int2 *coord) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntiles) return;
+    int64_t diag = (int64_t)t * kMergeTile;
+    if (diag > nr + K) diag = nr + K;
+    coord[t] = merge_search_global(diag, rai, nr, K);
+}
+
+template <bool ADD, bool CROW>
+__global__ __launch_bounds__(kMergeThreads) void k_spmv_merge(
+    const int2 *__restrict__ coord, int nr, const int32_t *__restrict__ rai,
+    const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
+    const double *__restrict__ aa, const double *__restrict__ x, const double *z,
+    double *y, int2 *carry_row, double *carry_val) {
+    __shared__ double s_prod[kMergeTile];
+    __shared__ int32_t s_rb[kMergeTile + 2];
+    __shared__ int32_t s_tail_row[kMergeThreads];
+    __shared__ double s_tail_val[kMergeThreads];
+    const int t = threadIdx.x;
+    const int2 c0 = coord[blockIdx.x], c1 = coord[blockIdx.x + 1];
+    const int i0 = c0.x, i1 = c1.x;
+    const int64_t j0 = c0.y, j1 = c1.y;
+    const int nitems = (i1 - i0) + (int)(j1 - j0);
+    const int nrb = i1 - i0 + 2;  // s_rb[ii] = rai[i0+ii], ii in [0, i1-i0+1]
+    const int64_t K = rai[nr];
+    for (int q = t; q < nrb; q += kMergeThreads) {
+        const int r = i0 + q;
+        s_rb[q] = r <= nr ? rai[r] : (int32_t)K;
+    }
+    for (int64_t k = j0 + t; k < j1; k += kMergeThreads) s_prod[k - j0] = aa[k] * x[aj[k]];
+    __syncthreads();
+
+    // Thread-local merge-path search inside the tile.
+    const int td = min(t * kMergeItems, nitems);
+    int lo = max(0, td - (int)(j1 - j0)), hi = min(td, i1 - i0);
+    while (lo < hi) {
+        const int p = (lo + hi) >> 1;
+        if ((int64_t)s_rb[p + 1] <= j0 + td - p - 1) lo = p + 1;
+        else hi = p;
+    }
+    int ii = lo;
+    int64_t jj = j0 + td - lo;
+    double running = 0.0;
+    bool have = false, started = false;
+    int head_ii = -1;
+    double head_val = 0.0;
+    const int nmine = min(kMergeItems, nitems - td);
+    for (int it = 0; it < nmine; ++it) {
+        const int64_t rend = s_rb[ii + 1];
+        if (jj < rend) {
+            if (!have) {
+                started = (jj == s_rb[ii]);
+                running = 0.0;
+                if (ADD && started) running = z[CROW ? ridx[i0 + ii] : i0 + ii];
+                have = true;
+            }
+            running += s_prod[jj - j0];
+            ++jj;
+        } else {
+            if (!have) {
+                started = (jj == s_rb[ii]);  // empty row: its end is its first item
+                running = 0.0;
+                if (ADD && started) running = z[CROW ? ridx[i0 + ii] : i0 + ii];
+            }
+            if (started) {
+                y[CROW ? ridx[i0 + ii] : i0 + ii] = running;
+            } else {  // only the first row end of a lane can be a head
+                head_ii = ii;
+                head_val = running;
+            }
+            have = false;
+            ++ii;
+        }
+    }
+    s_tail_row[t] = have ? ii : -1;
+    s_tail_val[t] = running;
+    __syncthreads();
+
+    if (head_ii >= 0) {
+        int tf = t;
+        while (tf > 0 && s_tail_row[tf - 1] == head_ii) --tf;
+        double v;
+        if (tf < t) {
+            v = s_tail_val[tf];
+            for (int q = tf + 1; q < t; ++q) v += s_tail_val[q];
+            v += head_val;
+        } else {
+            v = head_val;
+        }
+        y[CROW ? ridx[i0 + head_ii] : i0 + head_ii] = v;
+    }
+    // Tile carry-out: the partial of the row left open at the tile's end.
+    const int tl = nitems > 0 ? (nitems - 1) / kMergeItems : 0;
+    if (t == tl) {
+        if (nitems > 0 && s_tail_row[tl] >= 0) {
+            const int row = s_tail_row[tl];
+            int tf = tl;
+            while (tf > 0 && s_tail_row[tf - 1] == row) --tf;
+            double v = s_tail_val[tf];
+            for (int q = tf + 1; q <= tl; ++q) v += s_tail_val[q];
+            carry_row[blockIdx.x] = make_int2(CROW ? ridx[i0 + row] : i0 + row, 0);
+            carry_val[blockIdx.x] = v;
+        } else {
+            carry_row[blockIdx.x] = make_int2(-1, 0);
+        }
+    }
+}
+
+// Adds tile carries into their rows. The first tile of each run of tiles
+// carrying into one row sums the run in tile order, then adds once.
+__global__ void k_merge_fixup(int ntiles, const int2 *__restrict__ carry_row,
+                              const double *__restrict__ carry_val, double *y) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= ntiles) return;
+    const int r = carry_row[b].x;
+    if (r < 0) return;
+    if (b > 0 && carry_row[b - 1].x == r) return;
+    double v = carry_val[b];
+    for (int q = b + 1; q < ntiles && carry_row[q].x == r; ++q) v += carry_val[q];
+    y[r] = y[r] + v;
+}
+
+// ------------------------------------------------------------ transpose
+__global__ void k_expand_rows(int m, const int32_t *__restrict__ ai, int32_t *rows) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    for (int32_t k = ai[i]; k < ai[i + 1]; ++k) rows[k] = i;
+}
+
+__global__ void k_iota(int64_t n, int32_t *v) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = (int32_t)i;
+}
+
+__global__ void k_gather_transpose(int64_t nz, const int32_t *__restrict__ perm,
+                                   const int32_t *__restrict__ rows,
+                                   const double *__restrict__ aa, int32_t *taj,
+                                   double *taa) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= nz) return;
+    const int32_t k = perm[p];
+    taj[p] = rows[k];
+    taa[p] = aa[k];
+}
+
+// tai[c] = first position of column c in the sorted key list (lower bound).
+__global__ void k_col_offsets(int n, int64_t nz, const int32_t *__restrict__ keys,
+                              int32_t *tai) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > n) return;
+    int64_t lo = 0, hi = nz;
+    while (lo < hi) {
+        const int64_t p = (lo + hi) >> 1;
+        if (keys[p] < c) lo = p + 1;
+        else hi = p;
+    }
+    tai[c] = (int32_t)lo;
+}
+
+inline unsigned grid_for(int64_t n, int threads) {
+    return (unsigned)((n + threads - 1) / threads);
+}
+
+}  // namespace
+
+RowList row_list(const aijhip_mat &A) {
+    if (A.compressed) return RowList{A.n_crow, A.d_cai, A.d_ridx};
+    return RowList{A.m, A.d_ai, nullptr};
+}
+
+// Compressed-row form: rows outside the list are 0 (MatMult) or z (MatMultAdd).
+static hipError_t compressed_prologue(const aijhip_mat &A, const double *z, double *y,
+                                      bool add, hipStream_t s) {
+    if (!A.compressed) return hipSuccess;
+    if (!add) return hipMemsetAsync(y, 0, sizeof(double) * (size_t)A.m, s);
+    if (z != y) return hipMemcpyAsync(y, z, sizeof(double) * (size_t)A.m, hipMemcpyDeviceToDevice, s);
+    return hipSuccess;
+}
+
+hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, double *y,
+                         bool add, hipStream_t s) {
+    hipError_t e = compressed_prologue(A, z, y, add, s);
+    if (e != hipSuccess) return e;
+    const RowList L = row_list(A);
+    const Plan &P = A.plan;
+    if (P.n_blocks > 0) {
+        const dim3 grid(P.n_blocks), block(kStreamThreads);
+#define AIJHIP_STREAM(ADD, CROW)                                                            \
+    hipLaunchKernelGGL((k_spmv_stream<ADD, CROW, true>), grid, block, 0, s, P.d_blocks,    \
+                       P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y)
+        if (add) {
+            if (L.ridx) AIJHIP_STREAM(true, true); else AIJHIP_STREAM(true, false);
+        } else {
+            if (L.ridx) AIJHIP_STREAM(false, true); else AIJHIP_STREAM(false, false);
+        }
+#undef AIJHIP_STREAM
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (P.n_longs > 0) {
+        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s,
+                           P.d_segs, A.d_aj, A.d_aa, x, P.d_partials);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        const dim3 g(grid_for(P.n_longs, 256)), b(256);
+        if (add) hipLaunchKernelGGL(k_long_finish<true>, g, b, 0, s, P.d_longs, P.n_longs, P.d_partials, z, y);
+        else hipLaunchKernelGGL(k_long_finish<false>, g, b, 0, s, P.d_longs, P.n_longs, P.d_partials, z, y);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_scalar(const aijhip_mat &A, const double *x, const double *z, double *y,
+                         bool add, hipStream_t s) {
+    hipError_t e = compressed_prologue(A, z, y, add, s);
+    if (e != hipSuccess) return e;
+    const RowList L = row_list(A);
+    if (L.nr == 0) return hipSuccess;
+    const dim3 g(grid_for(L.nr, 256)), b(256);
+#define AIJHIP_SCALAR(ADD, CROW) \
+    hipLaunchKernelGGL((k_spmv_scalar<ADD, CROW>), g, b, 0, s, L.nr, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y)
+    if (add) { if (L.ridx) AIJHIP_SCALAR(true, true); else AIJHIP_SCALAR(true, false); }
+    else { if (L.ridx) AIJHIP_SCALAR(false, true); else AIJHIP_SCALAR(false, false); }
+#undef AIJHIP_SCALAR
+    return hipGetLastError();
+}
+
+template <int LN>
+static void vector_dispatch(const aijhip_mat &A, const RowList &L, const double *x,
+                            const double *z, double *y, bool add, hipStream_t s) {
+    const dim3 g(grid_for((int64_t)L.nr * LN, 256)), b(256);
+    if (add) {
+        if (L.ridx) hipLaunchKernelGGL((k_spmv_vector<LN, true, true>), g, b, 0, s, L.nr, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y);
+        else hipLaunchKernelGGL((k_spmv_vector<LN, true, false>), g, b, 0, s, L.nr, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y);
+    } else {
+        if (L.ridx) hipLaunchKernelGGL((k_spmv_vector<LN, false, true>), g, b, 0, s, L.nr, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y);
+        else hipLaunchKernelGGL((k_spmv_vector<LN, false, false>), g, b, 0, s, L.nr, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y);
+    }
+}
+
+hipError_t launch_vector(const aijhip_mat &A, const double *x, const double *z, double *y,
+                         bool add, hipStream_t s) {
+    hipError_t e = compressed_prologue(A, z, y, add, s);
+    if (e != hipSuccess) return e;
+    const RowList L = row_list(A);
+    if (L.nr == 0) return hipSuccess;
+    switch (A.plan.lanes) {
+        case 2: vector_dispatch<2>(A, L, x, z, y, add, s); break;
+        case 4: vector_dispatch<4>(A, L, x, z, y, add, s); break;
+        case 8: vector_dispatch<8>(A, L, x, z, y, add, s); break;
+        case 16: vector_dispatch<16>(A, L, x, z, y, add, s); break;
+        case 32: vector_dispatch<32>(A, L, x, z, y, add, s); break;
+        default: vector_dispatch<64>(A, L, x, z, y, add, s); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t merge_plan_coords(const aijhip_mat &A, int2 *d_coord, int32_t n_tiles,
+                             hipStream_t s) {
+    const RowList L = row_list(A);
+    const int64_t K = A.nz;
+    hipLaunchKernelGGL(k_merge_coords, dim3(grid_for((int64_t)n_tiles + 1, 256)), dim3(256), 0, s,
+                       n_tiles, L.rai, L.nr, K, d_coord);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge(const aijhip_mat &A, const double *x, const double *z, double *y,
+                        bool add, hipStream_t s) {
+    hipError_t e = compressed_prologue(A, z, y, add, s);
+    if (e != hipSuccess) return e;
+    const RowList L = row_list(A);
+    const Plan &P = A.plan;
+    if (L.nr == 0 || P.n_tiles == 0) return hipSuccess;
+    const dim3 g(P.n_tiles), b(kMergeThreads);
+#define AIJHIP_MERGE(ADD, CROW)                                                                 \
+    hipLaunchKernelGGL((k_spmv_merge<ADD, CROW>), g, b, 0, s, P.d_tile_coord, L.nr, L.rai,     \
+                       L.ridx, A.d_aj, A.d_aa, x, z, y, P.d_carry_row, P.d_carry_val)
+    if (add) { if (L.ridx) AIJHIP_MERGE(true, true); else AIJHIP_MERGE(true, false); }
+    else { if (L.ridx) AIJHIP_MERGE(false, true); else AIJHIP_MERGE(false, false); }
+#undef AIJHIP_MERGE
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_merge_fixup, dim3(grid_for(P.n_tiles, 256)), dim3(256), 0, s,
+                       P.n_tiles, P.d_carry_row, P.d_carry_val, y);
+    return hipGetLastError();
+}
+
+hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj,
+                           double **d_taa, hipStream_t s) {
+    const int64_t nz = A.nz;
+    int32_t *rows = nullptr, *keys_out = nullptr, *perm_in = nullptr, *perm_out = nullptr;
+    void *tmp = nullptr;
+    size_t tmp_bytes = 0;
+    hipError_t e = hipSuccess;
+    *d_tai = nullptr; *d_taj = nullptr; *d_taa = nullptr;
+    const size_t nzb = sizeof(int32_t) * (size_t)(nz > 0 ? nz : 1);
+#define AIJHIP_TRY(call) do { if ((e = (call)) != hipSuccess) goto done; } while (0)
+    AIJHIP_TRY(hipMalloc(d_tai, sizeof(int32_t) * ((size_t)A.n + 1)));
+    AIJHIP_TRY(hipMalloc(d_taj, sizeof(int32_t) * (size_t)(nz + 2)));
+    AIJHIP_TRY(hipMalloc(d_taa, sizeof(double) * (size_t)(nz + 2)));
+    AIJHIP_TRY(hipMemsetAsync(*d_taj, 0, sizeof(int32_t) * (size_t)(nz + 2), s));
+    AIJHIP_TRY(hipMemsetAsync(*d_taa, 0, sizeof(double) * (size_t)(nz + 2), s));
+    if (nz > 0) {
+        AIJHIP_TRY(hipMalloc(&rows, nzb));
+        AIJHIP_TRY(hipMalloc(&keys_out, nzb));
+        AIJHIP_TRY(hipMalloc(&perm_in, nzb));
+        AIJHIP_TRY(hipMalloc(&perm_out, nzb));
+        hipLaunchKernelGGL(k_expand_rows, dim3(grid_for(A.m, 256)), dim3(256), 0, s, A.m, A.d_ai, rows);
+        hipLaunchKernelGGL(k_iota, dim3(grid_for(nz, 256)), dim3(256), 0, s, nz, perm_in);
+        // Stable LSD radix sort by column keeps each column's entries in
+        // ascending row order: exactly the order PETSc's MatMultTranspose
+        // scatters them, so a row-sequential sum over A^T reproduces it.
+        AIJHIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, A.d_aj, keys_out, perm_in,
+                                                      perm_out, (int)nz, 0, 32, s));
+        AIJHIP_TRY(hipMalloc(&tmp, tmp_bytes));
+        AIJHIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, A.d_aj, keys_out, perm_in,
+                                                      perm_out, (int)nz, 0, 32, s));
+        hipLaunchKernelGGL(k_gather_transpose, dim3(grid_for(nz, 256)), dim3(256), 0, s, nz,
+                           perm_out, rows, A.d_aa, *d_taj, *d_taa);
+        hipLaunchKernelGGL(k_col_offsets, dim3(grid_for((int64_t)A.n + 1, 256)), dim3(256), 0, s,
+                           A.n, nz, keys_out, *d_tai);
+    } else {
+        AIJHIP_TRY(hipMemsetAsync(*d_tai, 0, sizeof(int32_t) * ((size_t)A.n + 1), s));
+    }
+    AIJHIP_TRY(hipGetLastError());
+    AIJHIP_TRY(hipStreamSynchronize(s));
+done:
+#undef AIJHIP_TRY
+    hipFree(rows); hipFree(keys_out); hipFree(perm_in); hipFree(perm_out); hipFree(tmp);
+    if (e != hipSuccess) {
+        hipFree(*d_tai); hipFree(*d_taj); hipFree(*d_taa);
+        *d_tai = nullptr; *d_taj = nullptr; *d_taa = nullptr;
+    }
+    return e;
+}
+
+}  // namespace aijhip

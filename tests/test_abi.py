@@ -1,0 +1,80 @@
+"""The C-ABI library (CPU, no compute): it loads, exports every function the
+headers in include/ declare, and refuses to compute without a device."""
+import ctypes
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+
+
+def declared_functions():
+    names = set()
+    for h in (ROOT / "include").glob("*.h"):
+        src = re.sub(r"/\*.*?\*/", "", h.read_text(), flags=re.S)
+        for m in re.finditer(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(aijhip_\w+)\s*\(", src, re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_headers_declare_the_boundary():
+    names = declared_functions()
+    for f in ("aijhip_mat_create", "aijhip_mat_mult", "aijhip_mat_mult_add", "aijhip_mat_destroy",
+              "aijhip_mat_update_values", "aijhip_mat_assembly_end", "aijhip_poisson_fill"):
+        assert f in names
+
+
+def test_library_exports_every_declared_symbol(pkg):
+    lib = ctypes.CDLL(str(pkg.LIB_PATH))
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    out = subprocess.run(["nm", "-D", "--defined-only", str(pkg.LIB_PATH)], capture_output=True, text=True).stdout
+    exported = set(re.findall(r"\b(aijhip_\w+)\b", out))
+    assert declared_functions() <= exported
+    assert set(pkg.ABI_SYMBOLS + pkg.HARNESS_SYMBOLS) == declared_functions()
+
+
+def test_library_is_gfx950_code_object(pkg):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-S", str(pkg.LIB_PATH)],
+                         capture_output=True, text=True).stdout
+    assert ".hip_fatbin" in out
+    blob = pkg.LIB_PATH.read_bytes()
+    assert b"gfx950" in blob
+
+
+def test_abi_version(pkg):
+    assert pkg.lib().aijhip_abi_version() == 1
+
+
+def test_create_validates_before_touching_the_device(pkg):
+    # Malformed CSR is rejected with AIJHIP_ERR_ARG on any host.
+    ai = np.array([0, 2, 1], np.int32)
+    aj = np.array([0, 1], np.int32)
+    aa = np.ones(2)
+    with pytest.raises(pkg.AIJHIPError) as e:
+        pkg.SeqAIJHIP(ai, aj, aa)
+    assert e.value.code == pkg.AIJHIP_ERR_ARG
+    ai = np.array([0, 1], np.int32)
+    aj = np.array([5], np.int32)
+    with pytest.raises(pkg.AIJHIPError) as e:
+        pkg.SeqAIJHIP(ai, aj, np.ones(1), ncols=2)
+    assert e.value.code == pkg.AIJHIP_ERR_ARG
+
+
+def test_no_device_fails_loudly(pkg):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    ai = np.array([0, 1], np.int32)
+    with pytest.raises(pkg.AIJHIPError) as e:
+        pkg.SeqAIJHIP(ai, np.array([0], np.int32), np.ones(1))
+    assert e.value.code == pkg.AIJHIP_ERR_NODEVICE
+
+
+def test_null_handle_calls_return_errors(pkg):
+    L = pkg.lib()
+    assert L.aijhip_mat_mult(None, None, None, None) == pkg.AIJHIP_ERR_ARG
+    assert L.aijhip_mat_destroy(None) == 0
+    assert b"NULL" in L.aijhip_last_error()

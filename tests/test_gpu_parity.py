@@ -1,0 +1,227 @@
+"""GPU parity of the HIP SpMV (through the C ABI) against the oracle.
+
+Bar: the STREAM and SCALAR kernels sum each row in PETSc's
+order without FMA, so they must be BIT-IDENTICAL to the CPU restatement.
+VECTOR / MERGE / long-row segments reorder the row sum and must meet the
+componentwise fp64 bound |dy_i| <= 2 gamma(n_i) (|A||x|)_i (+ the |z| term),
+gamma(n) = n u / (1 - n u), u = 2^-53, plus ||dy||_inf / |||A||x|||_inf <= 1e-14.
+"""
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_NAMES, golden, spmv_tolerance
+from oracle import seqaij
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+BITEXACT = ("stream", "scalar")
+ALL_KERNELS = ("stream", "scalar", "vector", "merge")
+
+
+@pytest.fixture(scope="module")
+def dev(pkg):
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    assert pkg.device_count() > 0
+    return torch.device("cuda:0")
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
+
+
+def bits(a):
+    return np.ascontiguousarray(a).view(np.uint64)
+
+
+def check(y_gpu, y_ref, ai, aj, aa, x, exact, z=None):
+    if exact:
+        bad = np.nonzero(bits(y_gpu) != bits(y_ref))[0]
+        assert bad.size == 0, f"{bad.size} rows differ bitwise, first {bad[:5]}: {y_gpu[bad[:5]]} vs {y_ref[bad[:5]]}"
+        return
+    tol, absax = spmv_tolerance(ai, aj, aa, x)
+    if z is not None:
+        tol = tol + 2 * 2.0 ** -53 * (np.abs(z) + absax)
+    err = np.abs(y_gpu - y_ref)
+    assert np.all(err <= tol), f"max excess {np.max(err - tol)}"
+    scale = max(np.max(absax), 1e-300)
+    assert np.max(err) / scale <= 1e-14
+
+
+def mult(pkg, dev, ai, aj, aa, n, x, kernel, lanes=0):
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, kernel=kernel, lanes=lanes) as A:
+        xd = to_dev(x, dev)
+        yd = torch.full((len(ai) - 1,), np.nan, dtype=torch.float64, device=dev)
+        A.mult(xd, yd)
+        torch.cuda.synchronize()
+        return yd.cpu().numpy(), A.info()
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+@pytest.mark.parametrize("kernel", ALL_KERNELS)
+def test_mult_golden(pkg, dev, name, kernel):
+    g = golden(name)
+    ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
+    y, info = mult(pkg, dev, ai, aj, aa, n, g["x"], kernel)
+    long_rows = info["n_long_rows"] > 0
+    check(y, g["y"], ai, aj, aa, g["x"], exact=kernel in BITEXACT and not long_rows)
+    if long_rows:  # rows <= 2048 entries stay bit-exact even when long rows exist
+        short = np.diff(ai) <= 2048
+        assert np.array_equal(bits(y)[short], bits(g["y"])[short]) or kernel not in BITEXACT
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+@pytest.mark.parametrize("kernel", ALL_KERNELS)
+def test_mult_add_golden(pkg, dev, name, kernel):
+    g = golden(name)
+    ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, kernel=kernel) as A:
+        xd, zd = to_dev(g["x"], dev), to_dev(g["z"], dev)
+        wd = torch.empty_like(zd)
+        A.mult_add(xd, zd, wd)
+        A.mult_add(xd, zd, zd)  # z aliases w (PETSc yy == zz)
+        torch.cuda.synchronize()
+        exact = kernel in BITEXACT and A.info()["n_long_rows"] == 0
+        check(wd.cpu().numpy(), g["w"], ai, aj, aa, g["x"], exact, z=g["z"])
+        check(zd.cpu().numpy(), g["w"], ai, aj, aa, g["x"], exact, z=g["z"])
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_mult_transpose_golden(pkg, dev, name):
+    g = golden(name)
+    ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n) as A:
+        yd = torch.empty(n, dtype=torch.float64, device=dev)
+        A.mult_transpose(to_dev(g["xt"], dev), yd)
+        torch.cuda.synchronize()
+        At = (np.argsort(aj, kind="stable"))
+        # A^T row lengths = column counts; bit-exact unless a column exceeds 2048 entries
+        colcount = np.bincount(aj, minlength=n)
+        yt = yd.cpu().numpy()
+        ok = colcount <= 2048
+        assert np.array_equal(bits(yt)[ok], bits(g["yt"])[ok])
+        np.testing.assert_allclose(yt, g["yt"], rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("lanes", [2, 4, 8, 16, 32, 64])
+def test_vector_all_lane_widths(pkg, dev, lanes):
+    g = golden("skewed_small")
+    ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
+    y, info = mult(pkg, dev, ai, aj, aa, n, g["x"], "vector", lanes)
+    assert info["vector_lanes"] == lanes
+    check(y, g["y"], ai, aj, aa, g["x"], exact=False)
+
+
+def test_edge_cases(pkg, dev, coracle):
+    # empty matrix (m = 0), all-empty rows, 1x1, a single very long row
+    A = pkg.SeqAIJHIP(np.zeros(1, np.int32), np.zeros(0, np.int32), np.zeros(0), ncols=0)
+    A.mult(torch.empty(0, dtype=torch.float64, device=dev), torch.empty(0, dtype=torch.float64, device=dev))
+    A.destroy()
+    for kernel in ALL_KERNELS:
+        y, _ = mult(pkg, dev, np.zeros(11, np.int32), np.zeros(0, np.int32), np.zeros(0), 4, np.ones(4), kernel)
+        assert np.all(y == 0.0)
+        y, _ = mult(pkg, dev, np.array([0, 1], np.int32), np.array([0], np.int32), np.array([3.0]), 1,
+                    np.array([-2.0]), kernel)
+        assert y[0] == -6.0
+    rng = np.random.default_rng(5)
+    n = 300000
+    aj = np.sort(rng.choice(n, size=200000, replace=False)).astype(np.int32)
+    aa = rng.standard_normal(len(aj))
+    ai = np.array([0, 0, len(aj), len(aj)], np.int32)
+    x = rng.standard_normal(n)
+    ref = coracle.matmult(ai, aj, aa, x)
+    for kernel in ALL_KERNELS:
+        y, _ = mult(pkg, dev, ai, aj, aa, n, x, kernel)
+        check(y, ref, ai, aj, aa, x, exact=(kernel == "scalar"))
+
+
+def test_update_values_and_assembly_end(pkg, dev, coracle):
+    g = golden("poisson8")
+    ai, aj, aa = g["ai"], g["aj"], g["aa"]
+    x = g["x"]
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    xd = to_dev(x, dev)
+    yd = torch.empty_like(xd)
+    aa2 = aa * 3.0 - 1.0
+    A.update_values(aa2)
+    A.mult(xd, yd)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(yd.cpu().numpy()), bits(coracle.matmult(ai, aj, aa2, x)))
+    g2 = golden("skewed_small")
+    ai3 = g2["ai"][: len(ai)].copy()  # same row count as poisson8 (513 offsets)
+    nz3 = int(ai3[-1])
+    aj3 = np.minimum(g2["aj"][:nz3], 511).astype(np.int32)
+    aa3 = g2["aa"][:nz3]
+    A.assembly_end(ai3, aj3, aa3)
+    A.mult(xd, yd)
+    torch.cuda.synchronize()
+    assert np.array_equal(bits(yd.cpu().numpy()), bits(coracle.matmult(ai3, aj3, aa3, x)))
+    A.destroy()
+
+
+def test_mult_host_step2_semantics(pkg, dev):
+    g = golden("poisson16")
+    with pkg.SeqAIJHIP(g["ai"], g["aj"], g["aa"]) as A:
+        y = A.mult_host(g["x"])
+        assert np.array_equal(bits(y), bits(g["y"]))
+
+
+def test_alias_rejected(pkg, dev):
+    g = golden("poisson4")
+    with pkg.SeqAIJHIP(g["ai"], g["aj"], g["aa"]) as A:
+        xd = to_dev(g["x"], dev)
+        with pytest.raises(pkg.AIJHIPError):
+            A.mult(xd, xd)
+
+
+def test_stream_ordering_on_side_stream(pkg, dev):
+    g = golden("poisson16")
+    s = torch.cuda.Stream()
+    with pkg.SeqAIJHIP(g["ai"], g["aj"], g["aa"]) as A:
+        with torch.cuda.stream(s):
+            xd = to_dev(g["x"], dev)
+            yd = torch.empty_like(xd)
+            for _ in range(3):
+                A.mult(xd, yd, stream=s)
+        s.synchronize()
+        assert np.array_equal(bits(yd.cpu().numpy()), bits(g["y"]))
+
+
+@pytest.mark.parametrize("N", [100, 300])
+def test_full_size_poisson_bitexact(pkg, dev, coracle, N):
+    """BASELINE configs[0]/[1] operand at full size: STREAM vs the C oracle,
+    bit for bit, plus the size-independent properties A*1 = row sums and
+    linearity A(x + 2v) = Ax + 2Av (exact here: powers of two)."""
+    ai, aj, aa = pkg.poisson_csr(N)
+    m = N ** 3
+    x = pkg.splitmix_uniform(m, 42)
+    ref = coracle.matmult(ai, aj, aa, x, omp=True)
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        info = A.info()
+        assert info["kernel"] == "stream" and info["n_long_rows"] == 0
+        assert info["nz"] == 7 * N ** 3 - 6 * N ** 2
+        xd = to_dev(x, dev)
+        yd = torch.empty_like(xd)
+        A.mult(xd, yd)
+        torch.cuda.synchronize()
+        assert np.array_equal(bits(yd.cpu().numpy()), bits(ref))
+        ones = torch.ones(m, dtype=torch.float64, device=dev)
+        A.mult(ones, yd)
+        rs = coracle.matmult(ai, aj, aa, np.ones(m), omp=True)
+        assert np.array_equal(bits(yd.cpu().numpy()), bits(rs))
+        del xd, yd, ones
+        torch.cuda.empty_cache()
+
+
+def test_skewed_flan_standin_all_kernels(pkg, dev, coracle):
+    """Flan_1565 stand-in (BASELINE configs[4]) at a reduced row count."""
+    ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
+    x = pkg.splitmix_uniform(len(ai) - 1, 9)
+    ref = coracle.matmult(ai, aj, aa, x, omp=True)
+    for kernel in ALL_KERNELS:
+        y, info = mult(pkg, dev, ai, aj, aa, len(ai) - 1, x, kernel)
+        check(y, ref, ai, aj, aa, x, exact=False)
+        if kernel in BITEXACT:
+            short = np.diff(ai) <= 2048
+            assert np.array_equal(bits(y)[short], bits(ref)[short])
