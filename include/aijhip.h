@@ -120,6 +120,17 @@ int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
  * (0 = pick from the mean row length). Re-plans on the device. */
 int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 
+/* Speed-only knobs of the STREAM kernel; results are identical for every
+ * setting. Re-plans on the device. */
+enum {
+    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..5: lanes / LDS entries / rows per block
+                                       (DESIGN.md §Kernels); default 0      */
+    AIJHIP_OPT_XCD_REMAP = 2,       /* 1 (default): each XCD gets a contiguous
+                                       run of row blocks                    */
+    AIJHIP_OPT_NT_LOADS = 3         /* 1: non-temporal aa/aj loads (default 0) */
+};
+int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
+
 /* New values, same nonzero structure (host aa[nz]): the re-upload half of
  * MatAssemblyEnd_SeqAIJ's hook (step2 MatAssemblyEnd patch:42-44). */
 int aijhip_mat_update_values(aijhip_mat_t A, const double *aa);

@@ -22,13 +22,14 @@ LIB_PATH = _PKG / "lib" / "libaijhip.so"
 
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
+OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 
 # Every symbol include/aijhip.h and include/aijhip_harness.h declare.
 ABI_SYMBOLS = (
     "aijhip_abi_version", "aijhip_last_error", "aijhip_device_count",
-    "aijhip_mat_create", "aijhip_mat_create_from_device", "aijhip_mat_set_kernel",
+    "aijhip_mat_create", "aijhip_mat_create_from_device", "aijhip_mat_set_kernel", "aijhip_mat_set_option",
     "aijhip_mat_update_values", "aijhip_mat_assembly_end", "aijhip_mat_mult",
     "aijhip_mat_mult_add", "aijhip_mat_mult_transpose", "aijhip_mat_mult_host",
     "aijhip_mat_get_info", "aijhip_mat_destroy",
@@ -82,6 +83,7 @@ def lib() -> ctypes.CDLL:
                                         _P, _P, _P, ctypes.POINTER(_P)]
         L.aijhip_mat_create_from_device.argtypes = L.aijhip_mat_create.argtypes
         L.aijhip_mat_set_kernel.argtypes = [_P, ctypes.c_int, ctypes.c_int]
+        L.aijhip_mat_set_option.argtypes = [_P, ctypes.c_int, ctypes.c_int]
         L.aijhip_mat_update_values.argtypes = [_P, _P]
         L.aijhip_mat_assembly_end.argtypes = [_P, ctypes.c_int64, _P, _P, _P]
         L.aijhip_mat_mult.argtypes = [_P, _P, _P, _P]
@@ -165,6 +167,10 @@ class SeqAIJHIP:
     # ---- PETSc MatOps analogues
     def set_kernel(self, kernel: str, lanes: int = 0):
         _check(lib().aijhip_mat_set_kernel(self._h, KERNELS[kernel], lanes))
+
+    def set_option(self, option: str, value: int):
+        """Speed-only STREAM knobs: geometry (0..5), xcd_remap, nt_loads."""
+        _check(lib().aijhip_mat_set_option(self._h, OPTIONS[option], int(value)))
 
     def mult(self, x, y, stream=None):
         """y = A x (MatMult_SeqAIJ). x: float64[n], y: float64[m] GPU tensors."""

@@ -109,9 +109,9 @@ int validate_csr(int32_t m, int32_t n, int64_t nz, const int32_t *ai, const int3
 }
 
 // CSR-stream row blocks over the handle's row list (h_rai): greedily pack
-// consecutive rows while the block holds <= kStreamNnzCap entries and
-// <= kStreamRowCap rows. A row longer than kStreamNnzCap becomes a long row,
-// split into segments of <= kLongSegNnz entries.
+// consecutive rows while the block holds <= nnz_cap entries and <= rows rows
+// of the chosen geometry. A longer row becomes a long row, split into
+// segments of <= kLongSegNnz entries.
 int plan_stream(aijhip_mat *A) {
     using namespace aijhip;
     const std::vector<int32_t> &rai = A->h_rai;
@@ -126,10 +126,11 @@ int plan_stream(aijhip_mat *A) {
         hipError_t e = hipMemcpy(h_ridx.data(), A->d_ridx, sizeof(int32_t) * A->n_crow, hipMemcpyDeviceToHost);
         if (e != hipSuccess) return hipfail(e, "plan: read ridx");
     }
+    const StreamGeom G = kStreamGeoms[A->plan.tune.geom];
     int32_t r = 0;
     while (r < nr) {
         const int32_t len = rai[r + 1] - rai[r];
-        if (len > kStreamNnzCap) {
+        if (len > G.nnz_cap) {
             LongRow lr{};
             lr.orow = A->compressed ? h_ridx[r] : r;
             lr.seg0 = (int32_t)segs.size();
@@ -144,9 +145,9 @@ int plan_stream(aijhip_mat *A) {
         }
         const int32_t start = r;
         int32_t nk = 0;
-        while (r < nr && r - start < kStreamRowCap) {
+        while (r < nr && r - start < G.rows) {
             const int32_t l = rai[r + 1] - rai[r];
-            if (l > kStreamNnzCap || nk + l > kStreamNnzCap) break;
+            if (l > G.nnz_cap || nk + l > G.nnz_cap) break;
             nk += l;
             ++r;
         }
@@ -200,6 +201,7 @@ int plan_build(aijhip_mat *A) {
     int kernel = A->requested_kernel;
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
+    P.tune = A->requested_tune;
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM:
             return plan_stream(A);
@@ -393,6 +395,27 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes) {
     return plan_build(A);
 }
 
+int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    aijhip::Tuning t = A->requested_tune;
+    switch (option) {
+        case AIJHIP_OPT_STREAM_GEOMETRY:
+            if (value < 0 || value >= aijhip::kNumStreamGeoms) return fail(AIJHIP_ERR_ARG, "bad geometry");
+            t.geom = value;
+            break;
+        case AIJHIP_OPT_XCD_REMAP: t.xcd = value != 0; break;
+        case AIJHIP_OPT_NT_LOADS: t.nt = value != 0; break;
+        default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
+    }
+    DeviceGuard g(A->device);
+    if (g.err != hipSuccess) return hipfail(g.err, "set device");
+    hipError_t e = hipDeviceSynchronize();  // in-flight launches may read the old plan
+    if (e != hipSuccess) return hipfail(e, "sync before re-plan");
+    A->requested_tune = t;
+    return plan_build(A);
+}
+
 int aijhip_mat_update_values(aijhip_mat_t A, const double *aa) {
     int rc = check_handle(A);
     if (rc) return rc;
@@ -418,6 +441,7 @@ int aijhip_mat_assembly_end(aijhip_mat_t A, int64_t nz, const int32_t *ai, const
     aijhip_mat_t B = nullptr;
     rc = create_impl(A->device, A->m, A->n, nz, ai, aj, aa, &B);
     if (rc) return rc;
+    B->requested_tune = A->requested_tune;
     rc = aijhip_mat_set_kernel(B, A->requested_kernel, A->requested_lanes);
     if (rc) {
         aijhip_mat_destroy(B);

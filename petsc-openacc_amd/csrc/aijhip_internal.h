@@ -12,13 +12,23 @@
 
 namespace aijhip {
 
-// STREAM kernel geometry: 256 lanes = 4 waves per row
-// block; up to kStreamNnzCap products staged in LDS (16 KiB fp64) and up to
-// kStreamRowCap rows, one row per lane in the reduction phase.
-constexpr int kStreamThreads = 256;
-constexpr int kStreamNnzCap = 2048;
-constexpr int kStreamRowCap = 256;
-// A row longer than kStreamNnzCap leaves the STREAM blocks and is split into
+// STREAM kernel geometries: `threads` lanes per row
+// block, up to `nnz_cap` products staged in LDS (8 B each) and up to
+// `rows` rows (rows / threads rows per lane in the reduction phase).
+struct StreamGeom {
+    int threads, nnz_cap, rows;
+};
+constexpr StreamGeom kStreamGeoms[] = {
+    {256, 2048, 256},    // 0: 4 waves, 16 KiB LDS
+    {512, 4096, 512},    // 1: 8 waves, 32 KiB
+    {256, 4096, 512},    // 2: 4 waves, 32 KiB, 2 rows per lane
+    {128, 1024, 128},    // 3: 2 waves, 8 KiB
+    {1024, 8192, 1024},  // 4: 16 waves, 64 KiB
+    {256, 1024, 256},    // 5: 4 waves, 8 KiB
+};
+constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
+constexpr int kMaxStreamNnzCap = 8192;
+// A row longer than the geometry's nnz_cap leaves the STREAM blocks and is split into
 // segments of at most kLongSegNnz entries, each summed by one workgroup.
 constexpr int kLongSegNnz = 16384;
 constexpr int kLongThreads = 256;
@@ -51,9 +61,17 @@ struct RowList {
     const int32_t *ridx;  // nullptr = identity
 };
 
+// Speed-only knobs (aijhip_mat_set_option); they never change results.
+struct Tuning {
+    int geom = 0;      // index into kStreamGeoms
+    bool xcd = true;   // XCD-contiguous block remap
+    bool nt = false;   // non-temporal matrix loads
+};
+
 struct Plan {
     int kernel = AIJHIP_KERNEL_STREAM;
     int lanes = 0;
+    Tuning tune;
     // STREAM
     BlockDesc *d_blocks = nullptr;
     int32_t n_blocks = 0;
@@ -89,6 +107,7 @@ struct aijhip_mat {
     aijhip::Plan plan;
     int requested_kernel = AIJHIP_KERNEL_AUTO;
     int requested_lanes = 0;
+    aijhip::Tuning requested_tune;
     // host-vector staging for aijhip_mat_mult_host (allocated on first use)
     double *d_xstage = nullptr, *d_ystage = nullptr;
     hipStream_t host_stream = nullptr;

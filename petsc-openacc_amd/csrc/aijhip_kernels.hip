@@ -45,47 +45,63 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     return xcd * q + min(xcd, r) + local;
 }
 
-constexpr int kStreamIters = (kStreamNnzCap + 1 + 2 * kStreamThreads - 1) / (2 * kStreamThreads);
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 
-template <bool ADD, bool CROW, bool XCD>
-__global__ __launch_bounds__(kStreamThreads) void k_spmv_stream(
+// Matrix entries are read exactly once per SpMV: with NT the loads carry the
+// non-temporal hint so the stream does not evict the reused x window from L2.
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_stream(const T *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+template <int T, int CAP, int RPT, bool ADD, bool CROW, bool XCD, bool NT>
+__global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, const int32_t *__restrict__ rai,
     const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const double *__restrict__ x,
     const double *z, double *y) {
-    __shared__ double prod[kStreamNnzCap];
+    constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
+    __shared__ double prod[CAP];
     const int b = XCD ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
     const BlockDesc d = blk[b];
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
 
     // Row extents and MatMultAdd seeds first: they overlap the stream below.
-    int32_t rs = 0, re = 0, orow = 0;
-    double sum = 0.0;
-    if (t < d.nrows) {
-        const int r = d.row0 + t;
-        rs = rai[r];
-        re = rai[r + 1];
-        orow = CROW ? ridx[r] : r;
-        if (ADD) sum = z[orow];
+    int32_t rs[RPT], re[RPT], orow[RPT];
+    double sum[RPT];
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        rs[q] = re[q] = orow[q] = 0;
+        sum[q] = 0.0;
+        const int lr = t + q * T;
+        if (lr < d.nrows) {
+            const int r = d.row0 + lr;
+            rs[q] = rai[r];
+            re[q] = rai[r + 1];
+            orow[q] = CROW ? ridx[r] : r;
+            if (ADD) sum[q] = z[orow[q]];
+        }
     }
 
     // Phase 1: coalesced 16-B loads of aa and 8-B loads of aj from an even
     // (16-B aligned) start; the arrays carry a 2-entry tail pad.
     const int64_t kb = k0 & ~int64_t(1);
-    double2 av[kStreamIters];
-    int2 cv[kStreamIters];
+    f64x2 av[ITERS];
+    i32x2 cv[ITERS];
 #pragma unroll
-    for (int it = 0; it < kStreamIters; ++it) {
-        const int64_t k = kb + 2 * (int64_t)(t + it * kStreamThreads);
+    for (int it = 0; it < ITERS; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (k < k1) {
-            av[it] = *reinterpret_cast<const double2 *>(aa + k);
-            cv[it] = *reinterpret_cast<const int2 *>(aj + k);
+            av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
+            cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
         }
     }
 #pragma unroll
-    for (int it = 0; it < kStreamIters; ++it) {
-        const int64_t k = kb + 2 * (int64_t)(t + it * kStreamThreads);
+    for (int it = 0; it < ITERS; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (k < k1) {
             if (k >= k0) prod[k - k0] = av[it].x * x[cv[it].x];
             if (k + 1 < k1) prod[k + 1 - k0] = av[it].y * x[cv[it].y];
@@ -94,9 +110,13 @@ __global__ __launch_bounds__(kStreamThreads) void k_spmv_stream(
     __syncthreads();
 
     // Phase 2: one lane per row, PETSc's sequential order.
-    if (t < d.nrows) {
-        for (int32_t k = rs; k < re; ++k) sum += prod[k - k0];
-        y[orow] = sum;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+        if (t + q * T < d.nrows) {
+            double s = sum[q];
+            for (int32_t k = rs[q]; k < re[q]; ++k) s += prod[k - k0];
+            y[orow[q]] = s;
+        }
     }
 }
 
@@ -364,6 +384,40 @@ static hipError_t compressed_prologue(const aijhip_mat &A, const double *z, doub
     return hipSuccess;
 }
 
+template <int T, int CAP, int RPT>
+static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double *x,
+                            const double *z, double *y, bool add, hipStream_t s) {
+    const Plan &P = A.plan;
+    const int sel = (add ? 8 : 0) | (L.ridx ? 4 : 0) | (P.tune.xcd ? 2 : 0) | (P.tune.nt ? 1 : 0);
+#define AIJHIP_SL(ADD, CROW, XCD, NT)                                                          \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, ADD, CROW, XCD, NT>), dim3(P.n_blocks),    \
+                       dim3(T), 0, s, P.d_blocks, P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa,  \
+                       x, z, y);                                                               \
+    break
+    switch (sel) {
+        case 0: AIJHIP_SL(false, false, false, false);
+        case 1: AIJHIP_SL(false, false, false, true);
+        case 2: AIJHIP_SL(false, false, true, false);
+        case 3: AIJHIP_SL(false, false, true, true);
+        case 4: AIJHIP_SL(false, true, false, false);
+        case 5: AIJHIP_SL(false, true, false, true);
+        case 6: AIJHIP_SL(false, true, true, false);
+        case 7: AIJHIP_SL(false, true, true, true);
+        case 8: AIJHIP_SL(true, false, false, false);
+        case 9: AIJHIP_SL(true, false, false, true);
+        case 10: AIJHIP_SL(true, false, true, false);
+        case 11: AIJHIP_SL(true, false, true, true);
+        case 12: AIJHIP_SL(true, true, false, false);
+        case 13: AIJHIP_SL(true, true, false, true);
+        case 14: AIJHIP_SL(true, true, true, false);
+        default: AIJHIP_SL(true, true, true, true);
+    }
+#undef AIJHIP_SL
+}
+
+#define AIJHIP_GEOM(G) kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap, \
+                       kStreamGeoms[G].rows / kStreamGeoms[G].threads
+
 hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, double *y,
                          bool add, hipStream_t s) {
     hipError_t e = compressed_prologue(A, z, y, add, s);
@@ -371,16 +425,14 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     const RowList L = row_list(A);
     const Plan &P = A.plan;
     if (P.n_blocks > 0) {
-        const dim3 grid(P.n_blocks), block(kStreamThreads);
-#define AIJHIP_STREAM(ADD, CROW)                                                            \
-    hipLaunchKernelGGL((k_spmv_stream<ADD, CROW, true>), grid, block, 0, s, P.d_blocks,    \
-                       P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y)
-        if (add) {
-            if (L.ridx) AIJHIP_STREAM(true, true); else AIJHIP_STREAM(true, false);
-        } else {
-            if (L.ridx) AIJHIP_STREAM(false, true); else AIJHIP_STREAM(false, false);
+        switch (P.tune.geom) {
+            case 1: stream_dispatch<AIJHIP_GEOM(1)>(A, L, x, z, y, add, s); break;
+            case 2: stream_dispatch<AIJHIP_GEOM(2)>(A, L, x, z, y, add, s); break;
+            case 3: stream_dispatch<AIJHIP_GEOM(3)>(A, L, x, z, y, add, s); break;
+            case 4: stream_dispatch<AIJHIP_GEOM(4)>(A, L, x, z, y, add, s); break;
+            case 5: stream_dispatch<AIJHIP_GEOM(5)>(A, L, x, z, y, add, s); break;
+            default: stream_dispatch<AIJHIP_GEOM(0)>(A, L, x, z, y, add, s); break;
         }
-#undef AIJHIP_STREAM
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (P.n_longs > 0) {

@@ -239,3 +239,28 @@ def test_skewed_flan_standin_all_kernels(pkg, dev, coracle):
         if kernel in BITEXACT:
             short = np.diff(ai) <= 2048
             assert_bits(y, ref, short)
+
+
+@pytest.mark.parametrize("name", ["poisson16", "skewed_small", "compressed_small"])
+def test_stream_options_do_not_change_results(pkg, dev, name):
+    """Every STREAM geometry / XCD remap / non-temporal setting is speed-only."""
+    g = golden(name)
+    ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n) as A:
+        xd = to_dev(g["x"], dev)
+        yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
+        first = None
+        for geom in range(6):
+            for xcd in (0, 1):
+                for nt in (0, 1):
+                    A.set_option("geometry", geom)
+                    A.set_option("xcd_remap", xcd)
+                    A.set_option("nt_loads", nt)
+                    A.mult(xd, yd)
+                    torch.cuda.synchronize()
+                    y = yd.cpu().numpy()
+                    if first is None:
+                        first = y
+                    assert_bits(y, first)
+                    short = np.diff(ai) <= 1024  # below every geometry's block cap
+                    assert_bits(y, g["y"], short)

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of SpMV variants in ONE process (cdna guide §5.4
+rule 24): every round times every variant once, and the report gives the
+median and min per variant. Also times torch read/copy kernels on buffers of
+the same size as a measured-bandwidth reference, and checks that every
+variant's y is bit-identical to the first STREAM variant's.
+
+    python tools/tune.py [--grid 300] [--rounds 5] [--launches 20] [--variants all|stream]
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import itertools
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def time_launches(fn, n, stream):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return np.array([a.elapsed_time(b) * 1e3 for a, b in ev])  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grid", type=int, default=300)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--variants", default="stream")
+    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed"])
+    args = ap.parse_args()
+    pkg = importlib.import_module("petsc-openacc_amd")
+    dev = torch.device("cuda:0")
+    stream = torch.cuda.current_stream()
+    t0 = time.time()
+    if args.matrix == "poisson":
+        ai, aj, aa = pkg.poisson_csr(args.grid)
+    else:
+        ai, aj, aa = pkg.skewed_csr()
+    m = len(ai) - 1
+    nbytes = pkg.algorithmic_bytes(m, m, len(aj))
+    x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
+    y = torch.empty(m, dtype=torch.float64, device=dev)
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    print(f"# setup {time.time() - t0:.1f}s m={m} nnz={len(aj)} bytes={nbytes}", flush=True)
+
+    variants = []
+    if args.variants in ("stream", "all"):
+        for g, xcd, nt in itertools.product(range(6), (1, 0), (0, 1)):
+            variants.append(("stream", dict(geometry=g, xcd_remap=xcd, nt_loads=nt)))
+    if args.variants in ("kernels", "all"):
+        variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
+
+    def configure(kind, opts):
+        A.set_kernel(kind, opts.get("lanes", 0))
+        for k in ("geometry", "xcd_remap", "nt_loads"):
+            if k in opts:
+                A.set_option(k, opts[k])
+
+    # reference bandwidth: torch streaming kernels over the same byte count
+    buf = torch.empty(nbytes // 8, dtype=torch.float64, device=dev).uniform_()
+    half = torch.empty(nbytes // 16, dtype=torch.float64, device=dev)
+    refs = {
+        "torch_sum_read": (lambda: buf.sum(), nbytes),
+        "torch_copy": (lambda: half.copy_(buf[: nbytes // 16]), nbytes),
+    }
+
+    ref_y = None
+    results = {name: [] for name in [json.dumps([k, o]) for k, o in variants] + list(refs)}
+    for rnd in range(args.rounds):
+        for kind, opts in variants:
+            key = json.dumps([kind, opts])
+            configure(kind, opts)
+            fn = lambda: A.mult(x, y, stream)  # noqa: E731
+            time_launches(fn, 3, stream)
+            us = time_launches(fn, args.launches, stream)
+            results[key].append(float(np.median(us)))
+            if rnd == 0:
+                yy = y.cpu().numpy()
+                if ref_y is None:
+                    ref_y = yy
+                same = bool(np.array_equal(yy.view(np.uint64), ref_y.view(np.uint64)))
+                maxdiff = float(np.max(np.abs(yy - ref_y)))
+                print(json.dumps({"variant": key, "bitwise_equal_first": same, "max_abs_diff": maxdiff}), flush=True)
+        for name, (fn, nb) in refs.items():
+            time_launches(fn, 2, stream)
+            results[name].append(float(np.median(time_launches(fn, args.launches, stream))))
+    rows = []
+    for key, v in results.items():
+        nb = refs[key][1] if key in refs else nbytes
+        med, mn = float(np.median(v)), float(np.min(v))
+        rows.append({"variant": key, "us_median": round(med, 2), "us_min": round(mn, 2),
+                     "GBs_median": round(nb / med / 1e3, 1), "frac_8TBs": round(nb / med / 1e3 / 8000, 4)})
+    rows.sort(key=lambda r: r["us_median"])
+    for r in rows:
+        print(json.dumps(r), flush=True)
+
+
+if __name__ == "__main__":
+    main()
