@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--grid", type=int, default=300, help="per-rank grid edge (N^3 rows per rank)")
     p.add_argument("--kernel", default="auto", choices=["auto", "stream", "scalar", "vector", "merge"])
+    p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..5 (default: library's)")
+    p.add_argument("--xcd", type=int, default=None, help="STREAM XCD-contiguous remap 0/1")
+    p.add_argument("--nt", type=int, default=None, help="STREAM non-temporal matrix loads 0/1")
     p.add_argument("--halo", default="p2p", choices=["p2p", "allgather"])
     p.add_argument("--x", default="uniform", choices=["uniform", "exact"], help="x = splitmix(42) or generateExt")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
@@ -103,6 +106,13 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     distributed = world > 1
+
+    def configure(mat):
+        for opt, val in (("geometry", args.geometry), ("xcd_remap", args.xcd), ("nt_loads", args.nt)):
+            if val is not None:
+                mat.set_option(opt, val)
+        return mat
+
     if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
@@ -130,13 +140,13 @@ def main():
         mpiaij = import_module("petsc-openacc_amd.mpiaij")
 
         def make_local(a_i, a_j, a_a, ncols):
-            return pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols, device=local_rank, kernel=args.kernel)
+            return configure(pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols, device=local_rank, kernel=args.kernel))
 
         op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo)
         info = op.A_d.info()
         step = lambda: op.mult(xd, yd)  # noqa: E731
     else:
-        A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m_loc, device=local_rank, kernel=args.kernel)
+        A = configure(pkg.SeqAIJHIP(ai, aj, aa, ncols=m_loc, device=local_rank, kernel=args.kernel))
         info = A.info()
         step = lambda: A.mult(xd, yd, stream)  # noqa: E731
     torch.cuda.synchronize()
@@ -212,6 +222,8 @@ def main():
                 else f"{G}^3 Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])",
                 "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
                 "kernel": info["kernel"], "halo": args.halo if distributed else None,
+                "block": {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows",
+                                               "xcd_remap", "nt_loads")},
                 "bytes_per_spmv": bytes_global, "flops_per_spmv_petsc": 2 * nnz_global - n_global,
             },
             "roofline": {

@@ -94,6 +94,12 @@ typedef struct aijhip_info {
                                 (step2 MatMult patch:47)                     */
     int64_t mult_bytes;      /* algorithmic bytes per MatMult:
                                 12 nz + 4 (m+1) + 8 n + 8 m     */
+    int32_t stream_geometry; /* AIJHIP_OPT_* values in effect                */
+    int32_t xcd_remap;
+    int32_t nt_loads;
+    int32_t stream_threads;  /* lanes / entries / rows per STREAM block      */
+    int32_t stream_nnz_cap;
+    int32_t stream_rows;
 } aijhip_info_t;
 
 /* Library / device. */

@@ -55,6 +55,8 @@ class AIJInfo(ctypes.Structure):
         ("n_long_rows", ctypes.c_int32), ("device", ctypes.c_int32),
         ("device_bytes", ctypes.c_int64), ("mult_flops", ctypes.c_double),
         ("mult_bytes", ctypes.c_int64),
+        ("stream_geometry", ctypes.c_int32), ("xcd_remap", ctypes.c_int32), ("nt_loads", ctypes.c_int32),
+        ("stream_threads", ctypes.c_int32), ("stream_nnz_cap", ctypes.c_int32), ("stream_rows", ctypes.c_int32),
     ]
 
 

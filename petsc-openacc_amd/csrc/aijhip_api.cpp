@@ -553,6 +553,12 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->device_bytes = A->device_bytes + A->plan.bytes;
     info->mult_flops = 2.0 * (double)A->nz - (double)A->nonzerorowcnt;
     info->mult_bytes = 12 * A->nz + 4 * ((int64_t)A->m + 1) + 8 * (int64_t)A->n + 8 * (int64_t)A->m;
+    info->stream_geometry = A->plan.tune.geom;
+    info->xcd_remap = A->plan.tune.xcd ? 1 : 0;
+    info->nt_loads = A->plan.tune.nt ? 1 : 0;
+    info->stream_threads = aijhip::kStreamGeoms[A->plan.tune.geom].threads;
+    info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;
+    info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
     return AIJHIP_OK;
 }
 

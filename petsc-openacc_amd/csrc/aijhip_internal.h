@@ -62,9 +62,12 @@ struct RowList {
 };
 
 // Speed-only knobs (aijhip_mat_set_option); they never change results.
+// Defaults are the fastest measured on MI355X at 300^3 (profiles/r01/tune01.jsonl):
+// geometry 4, round-robin block placement (XCD-contiguous runs were 5-10 %
+// slower), plain loads (non-temporal 2-3 % slower).
 struct Tuning {
-    int geom = 0;      // index into kStreamGeoms
-    bool xcd = true;   // XCD-contiguous block remap
+    int geom = 4;      // index into kStreamGeoms
+    bool xcd = false;  // XCD-contiguous block remap
     bool nt = false;   // non-temporal matrix loads
 };
 
