@@ -50,6 +50,7 @@ def parse():
     p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..5 (default: library's)")
     p.add_argument("--xcd", type=int, default=None, help="STREAM XCD-contiguous remap 0/1")
     p.add_argument("--nt", type=int, default=None, help="STREAM non-temporal matrix loads 0/1")
+    p.add_argument("--persist", type=int, default=None, help="persistent pipelined STREAM, workgroups/CU")
     p.add_argument("--halo", default="p2p", choices=["p2p", "allgather"])
     p.add_argument("--x", default="uniform", choices=["uniform", "exact"], help="x = splitmix(42) or generateExt")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
@@ -108,7 +109,8 @@ def main():
     distributed = world > 1
 
     def configure(mat):
-        for opt, val in (("geometry", args.geometry), ("xcd_remap", args.xcd), ("nt_loads", args.nt)):
+        for opt, val in (("geometry", args.geometry), ("xcd_remap", args.xcd), ("nt_loads", args.nt),
+                         ("persistent", args.persist)):
             if val is not None:
                 mat.set_option(opt, val)
         return mat
@@ -223,7 +225,7 @@ def main():
                 "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
                 "kernel": info["kernel"], "halo": args.halo if distributed else None,
                 "block": {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows",
-                                               "xcd_remap", "nt_loads")},
+                                               "xcd_remap", "nt_loads", "persistent")},
                 "bytes_per_spmv": bytes_global, "flops_per_spmv_petsc": 2 * nnz_global - n_global,
             },
             "roofline": {

@@ -100,6 +100,7 @@ typedef struct aijhip_info {
     int32_t stream_threads;  /* lanes / entries / rows per STREAM block      */
     int32_t stream_nnz_cap;
     int32_t stream_rows;
+    int32_t persistent;      /* workgroups per CU of the pipelined STREAM (0 = off) */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -133,7 +134,9 @@ enum {
                                        (DESIGN.md §Kernels); default 0      */
     AIJHIP_OPT_XCD_REMAP = 2,       /* 1 (default): each XCD gets a contiguous
                                        run of row blocks                    */
-    AIJHIP_OPT_NT_LOADS = 3         /* 1: non-temporal aa/aj loads (default 0) */
+    AIJHIP_OPT_NT_LOADS = 3,        /* 1: non-temporal aa/aj loads (default 0) */
+    AIJHIP_OPT_PERSISTENT = 4       /* k > 0: persistent software-pipelined
+                                       STREAM, k workgroups per CU (0 = off) */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

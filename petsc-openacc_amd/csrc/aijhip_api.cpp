@@ -326,6 +326,9 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
     A->m = m;
     A->n = n;
     A->nz = nz;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        A->n_cu = cus;
     rc = upload_and_plan(A, ai, aj, aa);
     if (rc) {
         free_matrix(A);
@@ -406,6 +409,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             break;
         case AIJHIP_OPT_XCD_REMAP: t.xcd = value != 0; break;
         case AIJHIP_OPT_NT_LOADS: t.nt = value != 0; break;
+        case AIJHIP_OPT_PERSISTENT:
+            if (value < 0 || value > 16) return fail(AIJHIP_ERR_ARG, "persistent: 0..16 workgroups per CU");
+            t.persist = value;
+            break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -492,6 +499,8 @@ int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y, void *
             return fail(AIJHIP_ERR_ALLOC, "host allocation");
         }
         T->device = A->device;
+        T->n_cu = A->n_cu;
+        T->requested_tune = A->requested_tune;
         T->m = A->n;
         T->n = A->m;
         T->nz = A->nz;
@@ -559,6 +568,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->stream_threads = aijhip::kStreamGeoms[A->plan.tune.geom].threads;
     info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
+    info->persistent = A->plan.tune.persist;
     return AIJHIP_OK;
 }
 

@@ -69,6 +69,7 @@ struct Tuning {
     int geom = 4;      // index into kStreamGeoms
     bool xcd = false;  // XCD-contiguous block remap
     bool nt = false;   // non-temporal matrix loads
+    int persist = 0;   // >0: persistent pipelined STREAM, this many workgroups per CU
 };
 
 struct Plan {
@@ -95,6 +96,7 @@ struct Plan {
 
 struct aijhip_mat {
     int device = 0;
+    int n_cu = 256;  // compute units of the device (persistent grids)
     int32_t m = 0, n = 0;
     int64_t nz = 0;
     int32_t nonzerorowcnt = 0;

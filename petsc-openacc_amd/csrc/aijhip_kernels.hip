@@ -120,6 +120,89 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     }
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops,
+// not for its outstanding global loads (__syncthreads() would add
+// s_waitcnt vmcnt(0) and drain the prefetch; cdna_hip_programming.md §8).
+// The "memory" clobber keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Persistent, software-pipelined STREAM: a resident grid walks the row blocks
+// round-robin (b, b + grid, ...). The aa/aj loads of the NEXT block are issued
+// before the barrier and stay in flight while the lanes reduce the current
+// block out of LDS, so the memory pipe never drains at block boundaries.
+// Same arithmetic as k_spmv_stream (bit-identical results).
+template <int T, int CAP, bool ADD, bool CROW, bool NT>
+__global__ __launch_bounds__(T) void k_spmv_stream_pipe(
+    const BlockDesc *__restrict__ blk, int nblk, const int32_t *__restrict__ rai,
+    const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
+    const double *__restrict__ aa, const double *__restrict__ x,
+    const double *z, double *y) {
+    constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
+    __shared__ double prod[CAP];
+    const int t = threadIdx.x;
+    int b = blockIdx.x;
+    if (b >= nblk) return;
+    BlockDesc d = blk[b];
+    f64x2 av[ITERS];
+    i32x2 cv[ITERS];
+    // Every load is unconditional (lanes past the block re-read its last
+    // pair, an L1 hit), so the number of loads in flight is static and the
+    // compiler's s_waitcnt before the reduction can leave the prefetch alone.
+    auto issue = [&](const BlockDesc &dd) {
+        const int64_t kb = (int64_t)dd.k0 & ~int64_t(1), k1 = (int64_t)dd.k0 + dd.nk;
+        const int64_t klast = k1 > kb ? ((k1 - 1) & ~int64_t(1)) : kb;
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = min(kb + 2 * (int64_t)(t + it * T), klast);
+            av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
+            cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
+        }
+    };
+    issue(d);
+    for (;;) {
+        const bool own = t < d.nrows;
+        const int r = d.row0 + min(t, d.nrows - 1);
+        const int32_t rs = rai[r], re = rai[r + 1];
+        const int orow = CROW ? ridx[r] : r;
+        double sum = ADD ? z[orow] : 0.0;
+        const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk, kb = k0 & ~int64_t(1);
+        // all x gathers of the block in flight at once, then the LDS stores
+        f64x2 pv[ITERS];
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            pv[it].x = x[cv[it].x];
+            pv[it].y = x[cv[it].y];
+        }
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
+            const double p0 = av[it].x * pv[it].x;
+            const double p1 = av[it].y * pv[it].y;
+            if (k < k1) {
+                if (k >= k0) prod[k - k0] = p0;
+                if (k + 1 < k1) prod[k + 1 - k0] = p1;
+            }
+        }
+        const int bn = b + (int)gridDim.x;
+        const bool more = bn < nblk;
+        // Unconditional prefetch (the last pass re-reads its own block) keeps
+        // the in-flight count static, so the reduction waits only for rs/re.
+        const BlockDesc dn = blk[more ? bn : b];
+        issue(dn);  // in flight across the barrier and the reduction below
+        lds_barrier();
+        if (own) {
+            for (int32_t k = rs; k < re; ++k) sum += prod[k - k0];
+            y[orow] = sum;
+        }
+        if (!more) break;
+        lds_barrier();  // every lane is done reading prod before it is refilled
+        d = dn;
+        b = bn;
+    }
+}
+
 // Segments of long rows: tree-reduced partial sums.
 __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     const LongSeg *__restrict__ seg, const int32_t *__restrict__ aj,
@@ -415,6 +498,29 @@ static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double 
 #undef AIJHIP_SL
 }
 
+template <int T, int CAP>
+static void pipe_dispatch(const aijhip_mat &A, const RowList &L, const double *x,
+                          const double *z, double *y, bool add, hipStream_t s) {
+    const Plan &P = A.plan;
+    const int grid = std::min<int64_t>(P.n_blocks, (int64_t)A.n_cu * P.tune.persist);
+    const int sel = (add ? 4 : 0) | (L.ridx ? 2 : 0) | (P.tune.nt ? 1 : 0);
+#define AIJHIP_PL(ADD, CROW, NT)                                                                \
+    hipLaunchKernelGGL((k_spmv_stream_pipe<T, CAP, ADD, CROW, NT>), dim3(grid), dim3(T), 0, s, \
+                       P.d_blocks, P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y);         \
+    break
+    switch (sel) {
+        case 0: AIJHIP_PL(false, false, false);
+        case 1: AIJHIP_PL(false, false, true);
+        case 2: AIJHIP_PL(false, true, false);
+        case 3: AIJHIP_PL(false, true, true);
+        case 4: AIJHIP_PL(true, false, false);
+        case 5: AIJHIP_PL(true, false, true);
+        case 6: AIJHIP_PL(true, true, false);
+        default: AIJHIP_PL(true, true, true);
+    }
+#undef AIJHIP_PL
+}
+
 #define AIJHIP_GEOM(G) kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap, \
                        kStreamGeoms[G].rows / kStreamGeoms[G].threads
 
@@ -424,7 +530,16 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     if (e != hipSuccess) return e;
     const RowList L = row_list(A);
     const Plan &P = A.plan;
-    if (P.n_blocks > 0) {
+    if (P.n_blocks > 0 && P.tune.persist > 0 && kStreamGeoms[P.tune.geom].rows == kStreamGeoms[P.tune.geom].threads) {
+        switch (P.tune.geom) {
+            case 1: pipe_dispatch<kStreamGeoms[1].threads, kStreamGeoms[1].nnz_cap>(A, L, x, z, y, add, s); break;
+            case 3: pipe_dispatch<kStreamGeoms[3].threads, kStreamGeoms[3].nnz_cap>(A, L, x, z, y, add, s); break;
+            case 4: pipe_dispatch<kStreamGeoms[4].threads, kStreamGeoms[4].nnz_cap>(A, L, x, z, y, add, s); break;
+            case 5: pipe_dispatch<kStreamGeoms[5].threads, kStreamGeoms[5].nnz_cap>(A, L, x, z, y, add, s); break;
+            default: pipe_dispatch<kStreamGeoms[0].threads, kStreamGeoms[0].nnz_cap>(A, L, x, z, y, add, s); break;
+        }
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (P.n_blocks > 0) {
         switch (P.tune.geom) {
             case 1: stream_dispatch<AIJHIP_GEOM(1)>(A, L, x, z, y, add, s); break;
             case 2: stream_dispatch<AIJHIP_GEOM(2)>(A, L, x, z, y, add, s); break;

@@ -251,11 +251,14 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
         yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
         first = None
         for geom in range(6):
-            for xcd in (0, 1):
-                for nt in (0, 1):
+            for xcd, nt, persist in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (0, 0, 1), (0, 1, 2), (0, 0, 5)):
+                if persist and geom == 2:
+                    continue
+                for _ in range(1):
                     A.set_option("geometry", geom)
                     A.set_option("xcd_remap", xcd)
                     A.set_option("nt_loads", nt)
+                    A.set_option("persistent", persist)
                     A.mult(xd, yd)
                     torch.cuda.synchronize()
                     y = yd.cpu().numpy()

@@ -18,8 +18,8 @@ from pathlib import Path
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0]
-    return n.replace("void ", "").replace("aijhip::(anonymous namespace)::", "")
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return n.split("(")[0]
 
 
 def load_counters(d: Path):
