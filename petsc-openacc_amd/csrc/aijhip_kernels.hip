@@ -69,42 +69,51 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
 
+    // All global loads below are branch-free (addresses clamped into the
+    // block), so the compiler keeps every one of them in flight: under an
+    // `if` it waits after each pair (s_waitcnt vmcnt(1) / vmcnt(0) per
+    // iteration, seen in the ISA), leaving ~2 loads per wave outstanding.
     // Row extents and MatMultAdd seeds first: they overlap the stream below.
     int32_t rs[RPT], re[RPT], orow[RPT];
     double sum[RPT];
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
-        rs[q] = re[q] = orow[q] = 0;
-        sum[q] = 0.0;
-        const int lr = t + q * T;
-        if (lr < d.nrows) {
-            const int r = d.row0 + lr;
-            rs[q] = rai[r];
-            re[q] = rai[r + 1];
-            orow[q] = CROW ? ridx[r] : r;
-            if (ADD) sum[q] = z[orow[q]];
-        }
+        const int r = d.row0 + min(t + q * T, d.nrows - 1);
+        rs[q] = rai[r];
+        re[q] = rai[r + 1];
+        orow[q] = CROW ? ridx[r] : r;
+        sum[q] = ADD ? z[orow[q]] : 0.0;
     }
 
     // Phase 1: coalesced 16-B loads of aa and 8-B loads of aj from an even
-    // (16-B aligned) start; the arrays carry a 2-entry tail pad.
+    // (16-B aligned) start; the arrays carry a 2-entry tail pad. Lanes past
+    // the block re-read its last pair (same address: one L1 line, no HBM).
     const int64_t kb = k0 & ~int64_t(1);
+    const int64_t klast = k1 > kb ? ((k1 - 1) & ~int64_t(1)) : kb;
     f64x2 av[ITERS];
     i32x2 cv[ITERS];
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
-        const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if (k < k1) {
-            av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
-            cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
-        }
+        const int64_t k = min(kb + 2 * (int64_t)(t + it * T), klast);
+        av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
+        cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
     }
+    // every x gather of the block in flight at once
+    f64x2 xv[ITERS];
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        xv[it].x = x[cv[it].x];
+        xv[it].y = x[cv[it].y];
+    }
+    // only the LDS stores are predicated
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
+        const double p0 = av[it].x * xv[it].x;
+        const double p1 = av[it].y * xv[it].y;
         if (k < k1) {
-            if (k >= k0) prod[k - k0] = av[it].x * x[cv[it].x];
-            if (k + 1 < k1) prod[k + 1 - k0] = av[it].y * x[cv[it].y];
+            if (k >= k0) prod[k - k0] = p0;
+            if (k + 1 < k1) prod[k + 1 - k0] = p1;
         }
     }
     __syncthreads();
