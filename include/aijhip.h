@@ -130,13 +130,15 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 /* Speed-only knobs of the STREAM kernel; results are identical for every
  * setting. Re-plans on the device. */
 enum {
-    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..5: lanes / LDS entries / rows per block
-                                       (DESIGN.md §Kernels); default 0      */
+    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..8: lanes / LDS entries / rows per block
+                                       (DESIGN.md §Kernels); default 6      */
     AIJHIP_OPT_XCD_REMAP = 2,       /* 1 (default): each XCD gets a contiguous
                                        run of row blocks                    */
     AIJHIP_OPT_NT_LOADS = 3,        /* 1: non-temporal aa/aj loads (default 0) */
-    AIJHIP_OPT_PERSISTENT = 4       /* k > 0: persistent software-pipelined
+    AIJHIP_OPT_PERSISTENT = 4,      /* k > 0: persistent software-pipelined
                                        STREAM, k workgroups per CU (0 = off) */
+    AIJHIP_OPT_CLAMPED_LOADS = 5    /* 1: branch-free clamped loads instead of
+                                       predicated loads (default 0)         */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 
@@ -168,6 +170,12 @@ int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y,
 int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y);
 
 int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info);
+
+/* Borrow the handle's device CSR (read-only; valid until the next
+ * assembly_end / destroy). The analogue of PETSc's device-array getters for
+ * GPU Mat types; aj and aa carry a 2-entry zero pad past nz. */
+int aijhip_mat_get_device_csr(aijhip_mat_t A, const int32_t **ai, const int32_t **aj,
+                              const double **aa);
 
 /* Free every device buffer of the handle (MatDestroy_SeqAIJ hook,
  * step2 MatDestroy patch:18-34). NULL is a no-op. */

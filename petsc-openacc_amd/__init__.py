@@ -22,7 +22,7 @@ LIB_PATH = _PKG / "lib" / "libaijhip.so"
 
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
-OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3, "persistent": 4}
+OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3, "persistent": 4, "clamped": 5}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 
@@ -32,7 +32,7 @@ ABI_SYMBOLS = (
     "aijhip_mat_create", "aijhip_mat_create_from_device", "aijhip_mat_set_kernel", "aijhip_mat_set_option",
     "aijhip_mat_update_values", "aijhip_mat_assembly_end", "aijhip_mat_mult",
     "aijhip_mat_mult_add", "aijhip_mat_mult_transpose", "aijhip_mat_mult_host",
-    "aijhip_mat_get_info", "aijhip_mat_destroy",
+    "aijhip_mat_get_info", "aijhip_mat_get_device_csr", "aijhip_mat_destroy",
 )
 HARNESS_SYMBOLS = (
     "aijhip_poisson_nnz", "aijhip_poisson_fill", "aijhip_poisson_vectors",
@@ -94,6 +94,7 @@ def lib() -> ctypes.CDLL:
         L.aijhip_mat_mult_transpose.argtypes = [_P, _P, _P, _P]
         L.aijhip_mat_mult_host.argtypes = [_P, _P, _P]
         L.aijhip_mat_get_info.argtypes = [_P, ctypes.POINTER(AIJInfo)]
+        L.aijhip_mat_get_device_csr.argtypes = [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]
         L.aijhip_mat_destroy.argtypes = [_P]
         L.aijhip_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.aijhip_poisson_nnz.argtypes = [ctypes.c_int32] * 5 + [_I64P]
@@ -221,6 +222,12 @@ class SeqAIJHIP:
         d = {f: getattr(inf, f) for f, _ in AIJInfo._fields_}
         d["kernel"] = KERNEL_NAMES.get(d["kernel"], d["kernel"])
         return d
+
+    def device_csr(self):
+        """(ai, aj, aa) device pointers of the handle's CSR copy (borrowed)."""
+        p = [_P(), _P(), _P()]
+        _check(lib().aijhip_mat_get_device_csr(self._h, *[ctypes.byref(q) for q in p]))
+        return tuple(q.value for q in p)
 
     def destroy(self):
         if getattr(self, "_h", None) and self._h.value:

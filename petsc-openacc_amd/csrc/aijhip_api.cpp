@@ -413,6 +413,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < 0 || value > 16) return fail(AIJHIP_ERR_ARG, "persistent: 0..16 workgroups per CU");
             t.persist = value;
             break;
+        case AIJHIP_OPT_CLAMPED_LOADS: t.clamped = value != 0; break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -569,6 +570,16 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
     info->persistent = A->plan.tune.persist;
+    return AIJHIP_OK;
+}
+
+int aijhip_mat_get_device_csr(aijhip_mat_t A, const int32_t **ai, const int32_t **aj,
+                              const double **aa) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (ai) *ai = A->d_ai;
+    if (aj) *aj = A->d_aj;
+    if (aa) *aa = A->d_aa;
     return AIJHIP_OK;
 }
 

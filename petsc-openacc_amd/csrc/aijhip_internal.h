@@ -18,6 +18,9 @@ namespace aijhip {
 struct StreamGeom {
     int threads, nnz_cap, rows;
 };
+// Caps of the form 2*threads*ITERS - 2 leave exactly one pair slot for the
+// 16-B alignment of the block start, so no load iteration is wasted
+// (a fully idle 5th iteration cost 6 % at 300^3: profiles/r01/style.jsonl).
 constexpr StreamGeom kStreamGeoms[] = {
     {256, 2048, 256},    // 0: 4 waves, 16 KiB LDS
     {512, 4096, 512},    // 1: 8 waves, 32 KiB
@@ -25,6 +28,9 @@ constexpr StreamGeom kStreamGeoms[] = {
     {128, 1024, 128},    // 3: 2 waves, 8 KiB
     {1024, 8192, 1024},  // 4: 16 waves, 64 KiB
     {256, 1024, 256},    // 5: 4 waves, 8 KiB
+    {512, 4094, 512},    // 6: 8 waves, 4 pair-iterations (measured best)
+    {1024, 8190, 1024},  // 7: 16 waves, 4 pair-iterations
+    {256, 2046, 256},    // 8: 4 waves, 4 pair-iterations
 };
 constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
 constexpr int kMaxStreamNnzCap = 8192;
@@ -62,14 +68,16 @@ struct RowList {
 };
 
 // Speed-only knobs (aijhip_mat_set_option); they never change results.
-// Defaults are the fastest measured on MI355X at 300^3 (profiles/r01/tune01.jsonl):
-// geometry 4, round-robin block placement (XCD-contiguous runs were 5-10 %
-// slower), plain loads (non-temporal 2-3 % slower).
+// Defaults are the fastest measured on MI355X at 300^3 (profiles/r01/):
+// geometry 6 with predicated loads (style study), round-robin block placement
+// (XCD-contiguous runs were 5-10 % slower), plain loads (non-temporal 2-3 %
+// slower), non-persistent grid (the pipelined persistent form was 7 % slower).
 struct Tuning {
-    int geom = 4;      // index into kStreamGeoms
-    bool xcd = false;  // XCD-contiguous block remap
-    bool nt = false;   // non-temporal matrix loads
-    int persist = 0;   // >0: persistent pipelined STREAM, this many workgroups per CU
+    int geom = 6;        // index into kStreamGeoms
+    bool xcd = false;    // XCD-contiguous block remap
+    bool nt = false;     // non-temporal matrix loads
+    int persist = 0;     // >0: persistent pipelined STREAM, this many workgroups per CU
+    bool clamped = false;  // branch-free clamped loads instead of predicated loads
 };
 
 struct Plan {

@@ -56,7 +56,12 @@ __device__ __forceinline__ T ld_stream(const T *p) {
     else return *p;
 }
 
-template <int T, int CAP, int RPT, bool ADD, bool CROW, bool XCD, bool NT>
+// CLAMPED selects the load form (tools/ablate_style.py measured both):
+//  false: loads and gathers predicated on `k < k1` — lanes past the block
+//         issue no request; the compiler waits once per iteration;
+//  true:  branch-free loads, addresses clamped into the block (lanes past it
+//         re-read its last pair) — every load in flight at once.
+template <int T, int CAP, int RPT, bool ADD, bool CROW, bool XCD, bool NT, bool CLAMPED>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, const int32_t *__restrict__ rai,
     const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
@@ -69,10 +74,6 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
 
-    // All global loads below are branch-free (addresses clamped into the
-    // block), so the compiler keeps every one of them in flight: under an
-    // `if` it waits after each pair (s_waitcnt vmcnt(1) / vmcnt(0) per
-    // iteration, seen in the ISA), leaving ~2 loads per wave outstanding.
     // Row extents and MatMultAdd seeds first: they overlap the stream below.
     int32_t rs[RPT], re[RPT], orow[RPT];
     double sum[RPT];
@@ -86,34 +87,36 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     }
 
     // Phase 1: coalesced 16-B loads of aa and 8-B loads of aj from an even
-    // (16-B aligned) start; the arrays carry a 2-entry tail pad. Lanes past
-    // the block re-read its last pair (same address: one L1 line, no HBM).
+    // (16-B aligned) start; the arrays carry a 2-entry tail pad.
     const int64_t kb = k0 & ~int64_t(1);
     const int64_t klast = k1 > kb ? ((k1 - 1) & ~int64_t(1)) : kb;
     f64x2 av[ITERS];
     i32x2 cv[ITERS];
-#pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-        const int64_t k = min(kb + 2 * (int64_t)(t + it * T), klast);
-        av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
-        cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
-    }
-    // every x gather of the block in flight at once
     f64x2 xv[ITERS];
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
-        xv[it].x = x[cv[it].x];
-        xv[it].y = x[cv[it].y];
+        const int64_t k = kb + 2 * (int64_t)(t + it * T);
+        if (CLAMPED || k < k1) {
+            const int64_t kc = CLAMPED ? min(k, klast) : k;
+            av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + kc));
+            cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + kc));
+        }
     }
-    // only the LDS stores are predicated
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        const double p0 = av[it].x * xv[it].x;
-        const double p1 = av[it].y * xv[it].y;
+        if (CLAMPED || k < k1) {
+            xv[it].x = x[cv[it].x];
+            xv[it].y = x[cv[it].y];
+        }
+    }
+    // products into LDS; only the stores are predicated
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (k < k1) {
-            if (k >= k0) prod[k - k0] = p0;
-            if (k + 1 < k1) prod[k + 1 - k0] = p1;
+            if (k >= k0) prod[k - k0] = av[it].x * xv[it].x;
+            if (k + 1 < k1) prod[k + 1 - k0] = av[it].y * xv[it].y;
         }
     }
     __syncthreads();
@@ -480,29 +483,28 @@ template <int T, int CAP, int RPT>
 static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double *x,
                             const double *z, double *y, bool add, hipStream_t s) {
     const Plan &P = A.plan;
-    const int sel = (add ? 8 : 0) | (L.ridx ? 4 : 0) | (P.tune.xcd ? 2 : 0) | (P.tune.nt ? 1 : 0);
-#define AIJHIP_SL(ADD, CROW, XCD, NT)                                                          \
-    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, ADD, CROW, XCD, NT>), dim3(P.n_blocks),    \
-                       dim3(T), 0, s, P.d_blocks, P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa,  \
-                       x, z, y);                                                               \
-    break
-    switch (sel) {
-        case 0: AIJHIP_SL(false, false, false, false);
-        case 1: AIJHIP_SL(false, false, false, true);
-        case 2: AIJHIP_SL(false, false, true, false);
-        case 3: AIJHIP_SL(false, false, true, true);
-        case 4: AIJHIP_SL(false, true, false, false);
-        case 5: AIJHIP_SL(false, true, false, true);
-        case 6: AIJHIP_SL(false, true, true, false);
-        case 7: AIJHIP_SL(false, true, true, true);
-        case 8: AIJHIP_SL(true, false, false, false);
-        case 9: AIJHIP_SL(true, false, false, true);
-        case 10: AIJHIP_SL(true, false, true, false);
-        case 11: AIJHIP_SL(true, false, true, true);
-        case 12: AIJHIP_SL(true, true, false, false);
-        case 13: AIJHIP_SL(true, true, false, true);
-        case 14: AIJHIP_SL(true, true, true, false);
-        default: AIJHIP_SL(true, true, true, true);
+#define AIJHIP_SL(ADD, CROW, XCD, NT, CL)                                                          \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, ADD, CROW, XCD, NT, CL>), dim3(P.n_blocks),    \
+                       dim3(T), 0, s, P.d_blocks, P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa,      \
+                       x, z, y);                                                                   \
+    return
+    // The speed knobs (XCD remap, non-temporal, clamped loads) are compiled
+    // for the plain full-row MatMult, the benchmarked path; MatMultAdd and
+    // the compressed-row form use the default (measured-best) form.
+    if (add || L.ridx) {
+        if (add && L.ridx) { AIJHIP_SL(true, true, false, false, false); }
+        if (add) { AIJHIP_SL(true, false, false, false, false); }
+        AIJHIP_SL(false, true, false, false, false);
+    }
+    switch ((P.tune.xcd ? 4 : 0) | (P.tune.nt ? 2 : 0) | (P.tune.clamped ? 1 : 0)) {
+        case 0: AIJHIP_SL(false, false, false, false, false);
+        case 1: AIJHIP_SL(false, false, false, false, true);
+        case 2: AIJHIP_SL(false, false, false, true, false);
+        case 3: AIJHIP_SL(false, false, false, true, true);
+        case 4: AIJHIP_SL(false, false, true, false, false);
+        case 5: AIJHIP_SL(false, false, true, false, true);
+        case 6: AIJHIP_SL(false, false, true, true, false);
+        default: AIJHIP_SL(false, false, true, true, true);
     }
 #undef AIJHIP_SL
 }
@@ -539,24 +541,28 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     if (e != hipSuccess) return e;
     const RowList L = row_list(A);
     const Plan &P = A.plan;
-    if (P.n_blocks > 0 && P.tune.persist > 0 && kStreamGeoms[P.tune.geom].rows == kStreamGeoms[P.tune.geom].threads) {
-        switch (P.tune.geom) {
-            case 1: pipe_dispatch<kStreamGeoms[1].threads, kStreamGeoms[1].nnz_cap>(A, L, x, z, y, add, s); break;
-            case 3: pipe_dispatch<kStreamGeoms[3].threads, kStreamGeoms[3].nnz_cap>(A, L, x, z, y, add, s); break;
-            case 4: pipe_dispatch<kStreamGeoms[4].threads, kStreamGeoms[4].nnz_cap>(A, L, x, z, y, add, s); break;
-            case 5: pipe_dispatch<kStreamGeoms[5].threads, kStreamGeoms[5].nnz_cap>(A, L, x, z, y, add, s); break;
-            default: pipe_dispatch<kStreamGeoms[0].threads, kStreamGeoms[0].nnz_cap>(A, L, x, z, y, add, s); break;
+    // Every geometry is dispatched explicitly: the kernel's LDS size must be
+    // the one the plan's row blocks were cut for.
+    static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
+    const int g = P.tune.geom;
+    if (P.n_blocks > 0 && P.tune.persist > 0 && kStreamGeoms[g].rows == kStreamGeoms[g].threads) {
+#define AIJHIP_PG(G) \
+    case G: pipe_dispatch<kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap>(A, L, x, z, y, add, s); break
+        switch (g) {
+            AIJHIP_PG(0); AIJHIP_PG(1); AIJHIP_PG(3); AIJHIP_PG(4); AIJHIP_PG(5);
+            AIJHIP_PG(6); AIJHIP_PG(7); AIJHIP_PG(8);
+            default: return hipErrorInvalidValue;
         }
+#undef AIJHIP_PG
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (P.n_blocks > 0) {
-        switch (P.tune.geom) {
-            case 1: stream_dispatch<AIJHIP_GEOM(1)>(A, L, x, z, y, add, s); break;
-            case 2: stream_dispatch<AIJHIP_GEOM(2)>(A, L, x, z, y, add, s); break;
-            case 3: stream_dispatch<AIJHIP_GEOM(3)>(A, L, x, z, y, add, s); break;
-            case 4: stream_dispatch<AIJHIP_GEOM(4)>(A, L, x, z, y, add, s); break;
-            case 5: stream_dispatch<AIJHIP_GEOM(5)>(A, L, x, z, y, add, s); break;
-            default: stream_dispatch<AIJHIP_GEOM(0)>(A, L, x, z, y, add, s); break;
+#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, L, x, z, y, add, s); break
+        switch (g) {
+            AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
+            AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8);
+            default: return hipErrorInvalidValue;
         }
+#undef AIJHIP_SG
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (P.n_longs > 0) {

@@ -251,8 +251,9 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
         xd = to_dev(g["x"], dev)
         yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
         first = None
-        for geom in range(6):
-            for xcd, nt, persist in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (0, 0, 1), (0, 1, 2), (0, 0, 5)):
+        for geom in range(9):
+            for xcd, nt, persist, clamped in ((0, 0, 0, 0), (1, 0, 0, 1), (0, 1, 0, 0), (1, 1, 0, 1),
+                                              (0, 0, 1, 0), (0, 1, 2, 0), (0, 0, 5, 0), (0, 0, 0, 1)):
                 if persist and geom == 2:
                     continue
                 for _ in range(1):
@@ -260,6 +261,7 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
                     A.set_option("xcd_remap", xcd)
                     A.set_option("nt_loads", nt)
                     A.set_option("persistent", persist)
+                    A.set_option("clamped", clamped)
                     A.mult(xd, yd)
                     torch.cuda.synchronize()
                     y = yd.cpu().numpy()

@@ -133,6 +133,86 @@ __global__ __launch_bounds__(T) void k_block4(const BlockDesc *__restrict__ blk,
     if (t < d.nrows) y[d.row0 + t] = s + rs + re;
 }
 
+// Load-style study, full SpMV arithmetic, lanes TT, IT pair-iterations:
+//  STYLE 0: loads under `if (k < k1)` (branchy, as k_ablate<0>)
+//  STYLE 1: branch-free clamped loads + batched gathers (as the product)
+//  STYLE 2: clamped loads guarded by a block-uniform iteration count
+template <int TT, int IT, int STYLE>
+__global__ __launch_bounds__(TT) void k_style(const BlockDesc *__restrict__ blk,
+                                              const int32_t *__restrict__ rai,
+                                              const int32_t *__restrict__ aj,
+                                              const double *__restrict__ aa,
+                                              const double *__restrict__ x, double *y) {
+    __shared__ double prod[2 * TT * IT];
+    const BlockDesc d = blk[blockIdx.x];
+    const int t = threadIdx.x;
+    const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk, kb = k0 & ~int64_t(1);
+    const int r = d.row0 + min(t, d.nrows - 1);
+    const int32_t rs = rai[r], re = rai[r + 1];
+    const int64_t klast = k1 > kb ? ((k1 - 1) & ~int64_t(1)) : kb;
+    const int nit = (int)((k1 - kb + 2 * TT - 1) / (2 * TT));  // block-uniform
+    f64x2 av[IT];
+    i32x2 cv[IT];
+    f64x2 xv[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * TT);
+        if (STYLE == 0) {
+            if (k < k1) {
+                av[it] = *reinterpret_cast<const f64x2 *>(aa + k);
+                cv[it] = *reinterpret_cast<const i32x2 *>(aj + k);
+            }
+        } else if (STYLE == 1 || it < nit) {
+            const int64_t kc = min(k, klast);
+            av[it] = *reinterpret_cast<const f64x2 *>(aa + kc);
+            cv[it] = *reinterpret_cast<const i32x2 *>(aj + kc);
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * TT);
+        if (STYLE == 0) {
+            if (k < k1) {
+                xv[it].x = x[cv[it].x];
+                xv[it].y = x[cv[it].y];
+            }
+        } else if (STYLE == 1 || it < nit) {
+            xv[it].x = x[cv[it].x];
+            xv[it].y = x[cv[it].y];
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * TT);
+        if (k < k1) {
+            if (k >= k0) prod[k - k0] = av[it].x * xv[it].x;
+            if (k + 1 < k1) prod[k + 1 - k0] = av[it].y * xv[it].y;
+        }
+    }
+    __syncthreads();
+    if (t < d.nrows) {
+        double s = 0.0;
+        for (int32_t k = rs; k < re; ++k) s += prod[k - k0];
+        y[d.row0 + t] = s;
+    }
+}
+
+extern "C" int ablate_style(int tt, int it, int style, int nblk, const void *blk, const int32_t *rai,
+                            const int32_t *aj, const double *aa, const double *x, double *y,
+                            void *stream) {
+    hipStream_t s = (hipStream_t)stream;
+    const BlockDesc *b = (const BlockDesc *)blk;
+#define ST(TT, IT, S)                                                                             \
+    if (tt == TT && it == IT && style == S) {                                                     \
+        hipLaunchKernelGGL((k_style<TT, IT, S>), dim3(nblk), dim3(TT), 0, s, b, rai, aj, aa, x, y); \
+        return hipGetLastError() == hipSuccess ? 0 : 2;                                           \
+    }
+    ST(1024, 5, 0) ST(1024, 5, 1) ST(1024, 5, 2) ST(1024, 4, 0) ST(1024, 4, 1) ST(1024, 4, 2)
+    ST(512, 4, 0) ST(512, 4, 1) ST(512, 4, 2) ST(512, 5, 1) ST(256, 4, 1) ST(256, 4, 2) ST(256, 4, 0)
+#undef ST
+    return 1;
+}
+
 extern "C" int ablate_launch(int mode, int nblk, const void *blk, const int32_t *rai,
                              const int32_t *aj, const double *aa, const double *x, double *y,
                              int64_t nz, void *stream) {

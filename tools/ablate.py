@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """DIAGNOSTIC: time the ablations of tools/ablate.hip on the 300^3 operand,
-interleaved in one process (5 rounds x 20 launches, median per variant).
+interleaved in one process (rounds x launches, median per variant), next to
+the product's own MatMult and the ablation's `full` kernel run on the
+product handle's device arrays (separates code effects from allocation).
 
     hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/ablate.hip -o tools/libablate.so
     python tools/ablate.py [--grid 300]
@@ -19,7 +21,8 @@ import torch
 
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
-NAMES = ["full", "no_gather", "no_reduce", "matrix_only", "flat_matrix", "flat_read_aa", "flat4_matrix", "block4_matrix"]
+NAMES = ["full", "no_gather", "no_reduce", "matrix_only", "flat_matrix", "flat_read_aa", "flat4_matrix",
+         "block4_matrix"]
 
 
 def main():
@@ -47,32 +50,39 @@ def main():
     y = torch.empty(max(m, 256 * 8 * 256), dtype=torch.float64, device=dev)
     s = torch.cuda.current_stream()
     nblk = len(row0)
-    bytes_full = pkg.algorithmic_bytes(m, m, nz)
-    traffic = {0: bytes_full, 1: bytes_full - 8 * m, 2: bytes_full, 3: 12 * nz + 4 * (m + 1) + 8 * m,
-               4: 12 * nz, 5: 8 * nz, 6: 12 * nz, 7: 12 * nz + 4 * (m + 1) + 8 * m}
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    p_ai, p_aj, p_aa = A.device_csr()
+    full = pkg.algorithmic_bytes(m, m, nz)
+    traffic = [full, full - 8 * m, full, 12 * nz + 4 * (m + 1) + 8 * m, 12 * nz, 8 * nz, 12 * nz,
+               12 * nz + 4 * (m + 1) + 8 * m]
 
-    def launch(mode):
-        rc = L.ablate_launch(mode, nblk, blk.data_ptr(), d_ai.data_ptr(), d_aj.data_ptr(), d_aa.data_ptr(),
-                             x.data_ptr(), y.data_ptr(), nz, s.cuda_stream)
-        assert rc == 0
+    def abl(mode, pai=None, paj=None, paa=None):
+        def f():
+            rc = L.ablate_launch(mode, nblk, blk.data_ptr(), pai or d_ai.data_ptr(), paj or d_aj.data_ptr(),
+                                 paa or d_aa.data_ptr(), x.data_ptr(), y.data_ptr(), nz, s.cuda_stream)
+            assert rc == 0
+        return f
 
-    res = {k: [] for k in range(8)}
+    variants = [(NAMES[i], abl(i), traffic[i]) for i in range(8)]
+    variants.append(("full_on_product_arrays", abl(0, p_ai, p_aj, p_aa), full))
+    variants.append(("product_mult", lambda: A.mult(x, y[:m], s), full))
+    res = {v[0]: [] for v in variants}
     for _ in range(args.rounds):
-        for mode in range(8):
+        for name, fn, _ in variants:
             for _ in range(3):
-                launch(mode)
+                fn()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(args.launches)]
             for a, b in ev:
                 a.record(s)
-                launch(mode)
+                fn()
                 b.record(s)
             torch.cuda.synchronize()
-            res[mode].append(float(np.median([a.elapsed_time(b) * 1e3 for a, b in ev])))
-    for mode in range(8):
-        us = float(np.median(res[mode]))
-        print(json.dumps({"variant": NAMES[mode], "us": round(us, 1), "bytes": traffic[mode],
-                          "GBs": round(traffic[mode] / us / 1e3, 1)}), flush=True)
+            res[name].append(float(np.median([a.elapsed_time(b) * 1e3 for a, b in ev])))
+    for name, _, nb in variants:
+        us = float(np.median(res[name]))
+        print(json.dumps({"variant": name, "us": round(us, 1), "bytes": nb, "GBs": round(nb / us / 1e3, 1)}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -59,18 +59,21 @@ def main():
 
     variants = []
     if args.variants in ("stream", "all"):
-        for g, xcd, nt in itertools.product(range(6), (1, 0), (0, 1)):
-            variants.append(("stream", dict(geometry=g, xcd_remap=xcd, nt_loads=nt, persistent=0)))
+        for g, cl in itertools.product(range(9), (0, 1)):
+            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=cl)))
+        for g in (6, 7):
+            variants.append(("stream", dict(geometry=g, xcd_remap=1, nt_loads=0, persistent=0, clamped=0)))
+            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=1, persistent=0, clamped=0)))
     if args.variants in ("pipe", "all"):
         variants += [("stream", dict(geometry=g, persistent=0)) for g in (1, 4)]
-        for g, p in itertools.product((0, 1, 4, 5), (1, 2, 3, 4, 8)):
-            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=p)))
+        for g, p in itertools.product((4, 6, 7), (1, 2, 4)):
+            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=p, clamped=0)))
     if args.variants in ("kernels", "all"):
         variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
 
     def configure(kind, opts):
         A.set_kernel(kind, opts.get("lanes", 0))
-        for k in ("geometry", "xcd_remap", "nt_loads", "persistent"):
+        for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
 
