@@ -132,8 +132,10 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 enum {
     AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..8: lanes / LDS entries / rows per block
                                        (DESIGN.md §Kernels); default 6      */
-    AIJHIP_OPT_XCD_REMAP = 2,       /* 1 (default): each XCD gets a contiguous
-                                       run of row blocks                    */
+    AIJHIP_OPT_XCD_REMAP = 2,       /* 0 (default): hardware round-robin;
+                                       1: each XCD gets a contiguous run of
+                                       row blocks; C >= 2: chunks of C blocks,
+                                       chunk c of every 8C on XCD slot c     */
     AIJHIP_OPT_NT_LOADS = 3,        /* 1: non-temporal aa/aj loads (default 0) */
     AIJHIP_OPT_PERSISTENT = 4,      /* k > 0: persistent software-pipelined
                                        STREAM, k workgroups per CU (0 = off) */

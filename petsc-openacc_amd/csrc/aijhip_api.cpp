@@ -407,7 +407,11 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < 0 || value >= aijhip::kNumStreamGeoms) return fail(AIJHIP_ERR_ARG, "bad geometry");
             t.geom = value;
             break;
-        case AIJHIP_OPT_XCD_REMAP: t.xcd = value != 0; break;
+        case AIJHIP_OPT_XCD_REMAP:
+            if (value < 0) return fail(AIJHIP_ERR_ARG, "xcd_remap: 0 off, 1 contiguous, >= 2 chunk");
+            t.xcd = value != 0;
+            t.xchunk = value >= 2 ? value : 0;
+            break;
         case AIJHIP_OPT_NT_LOADS: t.nt = value != 0; break;
         case AIJHIP_OPT_PERSISTENT:
             if (value < 0 || value > 16) return fail(AIJHIP_ERR_ARG, "persistent: 0..16 workgroups per CU");
@@ -564,7 +568,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->mult_flops = 2.0 * (double)A->nz - (double)A->nonzerorowcnt;
     info->mult_bytes = 12 * A->nz + 4 * ((int64_t)A->m + 1) + 8 * (int64_t)A->n + 8 * (int64_t)A->m;
     info->stream_geometry = A->plan.tune.geom;
-    info->xcd_remap = A->plan.tune.xcd ? 1 : 0;
+    info->xcd_remap = A->plan.tune.xcd ? (A->plan.tune.xchunk ? A->plan.tune.xchunk : 1) : 0;
     info->nt_loads = A->plan.tune.nt ? 1 : 0;
     info->stream_threads = aijhip::kStreamGeoms[A->plan.tune.geom].threads;
     info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;

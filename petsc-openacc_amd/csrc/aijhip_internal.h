@@ -74,7 +74,8 @@ struct RowList {
 // slower), non-persistent grid (the pipelined persistent form was 7 % slower).
 struct Tuning {
     int geom = 6;        // index into kStreamGeoms
-    bool xcd = false;    // XCD-contiguous block remap
+    bool xcd = false;    // XCD-aware block remap
+    int xchunk = 0;      //   chunk of the chunked remap (0 = contiguous runs)
     bool nt = false;     // non-temporal matrix loads
     int persist = 0;     // >0: persistent pipelined STREAM, this many workgroups per CU
     bool clamped = false;  // branch-free clamped loads instead of predicated loads

@@ -45,6 +45,20 @@ __device__ __forceinline__ int xcd_remap(int bid, int nblk) {
     return xcd * q + min(xcd, r) + local;
 }
 
+// Chunked XCD remap: logical blocks come in chunks of C consecutive blocks,
+// chunk c of every 8C-block super-chunk runs on the same XCD (dispatch slot
+// b % 8 == c). With 8C equal to the block distance between the reuses of an
+// x line (the +-N^2 stencil offsets / rows per block), the three reads of
+// each x line land in ONE XCD's L2. chunk <= 0: contiguous runs (above).
+__device__ __forceinline__ int xcd_chunk_remap(int bid, int nblk, int chunk) {
+    if (chunk <= 0) return xcd_remap(bid, nblk);
+    const int super = 8 * chunk;
+    const int full = (nblk / super) * super;
+    if (bid >= full) return bid;  // tail: identity
+    const int s = bid / super, w = bid - s * super;
+    return s * super + chunk * (w & 7) + (w >> 3);
+}
+
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
@@ -63,13 +77,13 @@ __device__ __forceinline__ T ld_stream(const T *p) {
 //         re-read its last pair) — every load in flight at once.
 template <int T, int CAP, int RPT, bool ADD, bool CROW, bool XCD, bool NT, bool CLAMPED>
 __global__ __launch_bounds__(T) void k_spmv_stream(
-    const BlockDesc *__restrict__ blk, int nblk, const int32_t *__restrict__ rai,
+    const BlockDesc *__restrict__ blk, int nblk, int xchunk, const int32_t *__restrict__ rai,
     const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const double *__restrict__ x,
     const double *z, double *y) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
-    const int b = XCD ? xcd_remap(blockIdx.x, nblk) : (int)blockIdx.x;
+    const int b = XCD ? xcd_chunk_remap(blockIdx.x, nblk, xchunk) : (int)blockIdx.x;
     const BlockDesc d = blk[b];
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
@@ -485,7 +499,8 @@ static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double 
     const Plan &P = A.plan;
 #define AIJHIP_SL(ADD, CROW, XCD, NT, CL)                                                          \
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, ADD, CROW, XCD, NT, CL>), dim3(P.n_blocks),    \
-                       dim3(T), 0, s, P.d_blocks, P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa,      \
+                       dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, L.rai, L.ridx,       \
+                       A.d_aj, A.d_aa,                                                             \
                        x, z, y);                                                                   \
     return
     // The speed knobs (XCD remap, non-temporal, clamped loads) are compiled

@@ -64,6 +64,10 @@ def main():
         for g in (6, 7):
             variants.append(("stream", dict(geometry=g, xcd_remap=1, nt_loads=0, persistent=0, clamped=0)))
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=1, persistent=0, clamped=0)))
+    if args.variants in ("xcd", "all"):
+        for g, c in [(6, 0), (6, 1), (6, 5), (6, 11), (6, 22), (6, 44), (6, 88), (7, 0), (7, 11), (7, 22),
+                     (8, 0), (8, 44)]:
+            variants.append(("stream", dict(geometry=g, xcd_remap=c, nt_loads=0, persistent=0, clamped=0)))
     if args.variants in ("pipe", "all"):
         variants += [("stream", dict(geometry=g, persistent=0)) for g in (1, 4)]
         for g, p in itertools.product((4, 6, 7), (1, 2, 4)):
