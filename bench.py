@@ -81,6 +81,21 @@ def cpu_baseline(ai, aj, aa, x, seconds):
     return el / reps, reps
 
 
+def pmc_traffic(rows, nnz, block):
+    """HBM bytes per launch from the committed rocprofv3 PMC record
+    (profiles/pmc_latest.json, written from tools/gpu_pmc.sh), used only
+    when it was measured on the same operand with the same block geometry;
+    bench.py itself runs without the profiler, so it cannot count bytes."""
+    p = ROOT / "profiles" / "pmc_latest.json"
+    try:
+        rec = json.loads(p.read_text())
+    except (OSError, ValueError):
+        return None, None
+    if rec.get("rows") != rows or rec.get("nnz") != nnz or rec.get("block") != block:
+        return None, None
+    return rec.get("hbm_traffic_bytes_per_launch"), rec.get("source")
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -205,6 +220,9 @@ def main():
         value = bytes_global * K / elapsed / 1e9
         mean_launch_s = float(np.mean(launch_ms)) / 1e3
         achieved = bytes_local / mean_launch_s / 1e9
+        block = {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "xcd_remap", "nt_loads",
+                                      "persistent")}
+        traffic, traffic_src = (None, None) if distributed else pmc_traffic(n_global, nnz_global, block)
         out = {
             "metric": "CSR SpMV effective HBM GB/s (300^3 7-pt Poisson, fp64 MatMult_SeqAIJ)",
             "value": round(value, 2),
@@ -224,8 +242,7 @@ def main():
                 else f"{G}^3 Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])",
                 "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
                 "kernel": info["kernel"], "halo": args.halo if distributed else None,
-                "block": {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows",
-                                               "xcd_remap", "nt_loads", "persistent")},
+                "block": block,
                 "bytes_per_spmv": bytes_global, "flops_per_spmv_petsc": 2 * nnz_global - n_global,
             },
             "roofline": {
@@ -234,7 +251,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel_us_mean": round(mean_launch_s * 1e6, 2),
                 "kernel_us_median": round(float(np.median(launch_ms)) * 1e3, 2),
                 "kernel_us_min": round(float(np.min(launch_ms)) * 1e3, 2),
