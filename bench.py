@@ -56,6 +56,7 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-cg", action="store_true")
+    p.add_argument("--cg-iters", type=int, default=200, help="CG iterations timed for cg.iters_per_s")
     return p.parse_args()
 
 
@@ -79,6 +80,31 @@ def cpu_baseline(ai, aj, aa, x, seconds):
         if el >= seconds or reps >= 50:
             break
     return el / reps, reps
+
+
+def cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz, iters=8):
+    """The oracle's KSPSolve_CG restatement (numpy vector ops + the C
+    MatMult_SeqAIJ loop) on the host, a fixed small number of iterations."""
+    from oracle import ksp_cg
+    build = importlib.import_module("petsc-openacc_amd.build")
+    L = ctypes.CDLL(str(build.build_oracle()))
+    P = ctypes.c_void_p
+    L.oracle_matmult_seqaij.argtypes = [ctypes.c_int32, P, P, P, P, P]
+    L.oracle_matmult_seqaij.restype = None
+    m = len(ai) - 1
+
+    def mm(v):
+        v = np.ascontiguousarray(v)
+        y = np.empty(m)
+        L.oracle_matmult_seqaij(m, ai.ctypes.data, aj.ctypes.data, aa.ctypes.data, v.ctypes.data, y.ctypes.data)
+        return y
+
+    rhs, _ = pkg.poisson_vectors(nx, ny, nz)
+    t0 = time.perf_counter()
+    _, its, _, _ = ksp_cg.cg(ai, aj, aa, rhs, rtol=0.0, atol=0.0, max_it=iters, matmult=mm)
+    dt = time.perf_counter() - t0
+    return {"iters_per_s": round(its / dt, 3), "cores": 1, "kind": "port",
+            "sample": f"{its} CG+Jacobi iterations, oracle/ksp_cg.py + oracle/matmult_seqaij.c, 1 core"}
 
 
 def pmc_traffic(rows, nnz, block):
@@ -210,11 +236,10 @@ def main():
 
     cg = None
     if not args.no_cg and not distributed:
-        try:
-            ksp = importlib.import_module("petsc-openacc_amd.ksp")
-            cg = ksp.bench_cg(pkg, A, nx, ny, nz_global, dev, iters=50)
-        except (ImportError, AttributeError):
-            cg = None
+        ksp = importlib.import_module("petsc-openacc_amd.ksp")
+        cg = ksp.bench_cg(pkg, A, nx, ny, nz_global, dev, iters=args.cg_iters)
+        if not args.no_cpu_baseline:
+            cg["cpu_baseline"] = cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz_global)
 
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9

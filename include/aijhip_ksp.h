@@ -1,0 +1,84 @@
+/*
+ * aijhip_ksp.h — device-resident Krylov solve around the MI355X SpMV
+ * (the caller of MatMult_SeqAIJ in the reference,
+ * /root/reference/src/main_ksp.cpp:92-103 with
+ * /root/reference/configs/PETSc_SolverOptions_GAMG.info:1-4).
+ *
+ * Mirrors PETSc 3.7.6's KSPSolve_CG [ext] (src/ksp/ksp/impls/cg/cg.c) and
+ * KSPConvergedDefault [ext] (src/ksp/ksp/interface/iterativ.c): preconditioned
+ * CG with the preconditioned residual norm by default, the same breakdown
+ * checks (beta = 0, indefinite PC, indefinite matrix) and the same reason
+ * codes. Vectors are device arrays; all scalar work (alpha, beta, the
+ * convergence test) runs on the device, so iterations are launched without a
+ * host round trip. Dot products are reduced in a fixed order (deterministic
+ * run to run) but not in BLAS ddot's order, so results match PETSc to
+ * rounding, not bit for bit.
+ */
+#ifndef AIJHIP_KSP_H
+#define AIJHIP_KSP_H
+
+#include <stdint.h>
+
+#include "aijhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct aijhip_ksp *aijhip_ksp_t;
+
+/* PCType: PCNONE, PCJACOBI (= bjacobi + jacobi sub-PC on one rank,
+ * PETSc_SolverOptions_GAMG.info:16-21). */
+enum { AIJHIP_PC_NONE = 0, AIJHIP_PC_JACOBI = 1 };
+
+/* KSPNormType values as in PETSc. */
+enum {
+    AIJHIP_KSP_NORM_NONE = 0,
+    AIJHIP_KSP_NORM_PRECONDITIONED = 1,
+    AIJHIP_KSP_NORM_UNPRECONDITIONED = 2,
+    AIJHIP_KSP_NORM_NATURAL = 3
+};
+
+/* KSPConvergedReason values as in PETSc 3.7. */
+enum {
+    AIJHIP_KSP_CONVERGED_ITERATING = 0,
+    AIJHIP_KSP_CONVERGED_RTOL = 2,
+    AIJHIP_KSP_CONVERGED_ATOL = 3,
+    AIJHIP_KSP_DIVERGED_ITS = -3,
+    AIJHIP_KSP_DIVERGED_DTOL = -4,
+    AIJHIP_KSP_DIVERGED_INDEFINITE_PC = -8,
+    AIJHIP_KSP_DIVERGED_NANORINF = -9,
+    AIJHIP_KSP_DIVERGED_INDEFINITE_MAT = -10
+};
+
+/* KSPCreate + KSPSetOperators(A, A) + KSPSetType(KSPCG). A must be square;
+ * the handle borrows A (A must outlive it). Defaults as PETSc: rtol 1e-5,
+ * atol 1e-50, dtol 1e5, max_it 10000, PC Jacobi, preconditioned norm,
+ * zero initial guess. */
+int aijhip_ksp_create(aijhip_mat_t A, aijhip_ksp_t *ksp);
+int aijhip_ksp_set_tolerances(aijhip_ksp_t ksp, double rtol, double abstol, double dtol,
+                              int32_t max_it);
+int aijhip_ksp_set_pc_type(aijhip_ksp_t ksp, int pc_type);
+int aijhip_ksp_set_norm_type(aijhip_ksp_t ksp, int norm_type);
+int aijhip_ksp_set_initial_guess_nonzero(aijhip_ksp_t ksp, int flg);
+/* KSPSetUp: PC set-up (inverse diagonal) and work vectors. Called by solve
+ * if needed; call it explicitly to time set-up apart from the solve. */
+int aijhip_ksp_set_up(aijhip_ksp_t ksp);
+/* KSPSolve: b, x device fp64[m]; x is overwritten (zeroed first unless the
+ * initial guess is nonzero). Returns once the solve has finished. */
+int aijhip_ksp_solve(aijhip_ksp_t ksp, const double *b, double *x, void *stream);
+int aijhip_ksp_get_iteration_number(aijhip_ksp_t ksp, int32_t *its);
+int aijhip_ksp_get_residual_norm(aijhip_ksp_t ksp, double *rnorm);
+int aijhip_ksp_get_converged_reason(aijhip_ksp_t ksp, int *reason);
+/* KSPGetResidualHistory: copies min(na, its + 1) norms; *n = that count. */
+int aijhip_ksp_get_residual_history(aijhip_ksp_t ksp, double *hist, int32_t na, int32_t *n);
+/* Fused kernels used per iteration (1 = SpMV with the p.Ap dot in its
+ * epilogue), for reporting. */
+int aijhip_ksp_get_fused(aijhip_ksp_t ksp, int *fused);
+int aijhip_ksp_destroy(aijhip_ksp_t ksp);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIJHIP_KSP_H */

@@ -296,13 +296,7 @@ int mult_impl(aijhip_mat_t A, const double *x, const double *z, double *y, bool 
     if (g.err != hipSuccess) return hipfail(g.err, "set device");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipError_t e;
-    switch (A->plan.kernel) {
-        case AIJHIP_KERNEL_STREAM: e = aijhip::launch_stream(*A, x, z, y, add, s); break;
-        case AIJHIP_KERNEL_SCALAR: e = aijhip::launch_scalar(*A, x, z, y, add, s); break;
-        case AIJHIP_KERNEL_VECTOR: e = aijhip::launch_vector(*A, x, z, y, add, s); break;
-        case AIJHIP_KERNEL_MERGE: e = aijhip::launch_merge(*A, x, z, y, add, s); break;
-        default: return fail(AIJHIP_ERR_STATE, "handle has no plan");
-    }
+    e = aijhip::launch_mult(*A, x, z, y, add, s);
     if (e != hipSuccess) return hipfail(e, "SpMV launch");
     return AIJHIP_OK;
 }
@@ -340,6 +334,10 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
 }
 
 }  // namespace
+
+namespace aijhip {
+void set_error(const std::string &msg) { g_err = msg; }
+}  // namespace aijhip
 
 extern "C" {
 

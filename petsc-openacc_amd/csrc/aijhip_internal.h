@@ -135,7 +135,17 @@ namespace aijhip {
 // Launchers (aijhip_kernels.hip). All enqueue on `s` and return the launch's
 // hipError_t.
 hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z,
-                         double *y, bool add, hipStream_t s);
+                         double *y, bool add, hipStream_t s, double *dpart = nullptr,
+                         const int *stop = nullptr);
+// CG fusion: y = A x with the per-block partials of x . y in dpart[0..n_blocks)
+// (deterministic); every block returns at once when *stop != 0. Only for
+// square full-row STREAM plans without long rows.
+bool stream_dot_fusable(const aijhip_mat &A);
+hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, double *dpart,
+                             const int *stop, hipStream_t s);
+// Dispatch y = A x (or w = z + A x) through the handle's plan.
+hipError_t launch_mult(const aijhip_mat &A, const double *x, const double *z, double *y,
+                       bool add, hipStream_t s);
 hipError_t launch_scalar(const aijhip_mat &A, const double *x, const double *z,
                          double *y, bool add, hipStream_t s);
 hipError_t launch_vector(const aijhip_mat &A, const double *x, const double *z,
@@ -151,5 +161,8 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
                            double **d_taa, hipStream_t s);
 
 RowList row_list(const aijhip_mat &A);
+
+// Sets the calling thread's aijhip_last_error() message.
+void set_error(const std::string &msg);
 
 }  // namespace aijhip

@@ -75,14 +75,33 @@ __device__ __forceinline__ T ld_stream(const T *p) {
 //         issue no request; the compiler waits once per iteration;
 //  true:  branch-free loads, addresses clamped into the block (lanes past it
 //         re-read its last pair) — every load in flight at once.
+// Block-wide fp64 sum in a fixed order (wave __shfl_down tree, then the
+// waves' sums in wave order): deterministic run to run.
+template <int T>
+__device__ __forceinline__ double block_sum(double v, double *scratch) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    const int t = threadIdx.x;
+    __syncthreads();  // scratch may still be read by the caller's previous phase
+    if ((t & 63) == 0) scratch[t >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (t == 0) {
+#pragma unroll
+        for (int w = 0; w < T / 64; ++w) s += scratch[w];
+    }
+    return s;  // valid in thread 0
+}
+
 template <int T, int CAP, int RPT, bool ADD, bool CROW, bool XCD, bool NT, bool CLAMPED>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int xchunk, const int32_t *__restrict__ rai,
     const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const double *__restrict__ x,
-    const double *z, double *y) {
+    const double *z, double *y, double *dpart, const int *stop) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
+    if (stop && *stop) return;  // CG launched past convergence: no work
     const int b = XCD ? xcd_chunk_remap(blockIdx.x, nblk, xchunk) : (int)blockIdx.x;
     const BlockDesc d = blk[b];
     const int t = threadIdx.x;
@@ -136,13 +155,21 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     __syncthreads();
 
     // Phase 2: one lane per row, PETSc's sequential order.
+    double dotv = 0.0;
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
         if (t + q * T < d.nrows) {
             double s = sum[q];
             for (int32_t k = rs[q]; k < re[q]; ++k) s += prod[k - k0];
             y[orow[q]] = s;
+            if (dpart) dotv += x[orow[q]] * s;
         }
+    }
+    // Optional fused epilogue for CG (grid-uniform branch): the block's
+    // partial of x . y, written to dpart[b] for a fixed-order final sum.
+    if (dpart) {
+        const double v = block_sum<T>(dotv, prod);
+        if (t == 0) dpart[b] = v;
     }
 }
 
@@ -495,13 +522,14 @@ static hipError_t compressed_prologue(const aijhip_mat &A, const double *z, doub
 
 template <int T, int CAP, int RPT>
 static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double *x,
-                            const double *z, double *y, bool add, hipStream_t s) {
+                            const double *z, double *y, bool add, hipStream_t s, double *dpart,
+                            const int *stop) {
     const Plan &P = A.plan;
 #define AIJHIP_SL(ADD, CROW, XCD, NT, CL)                                                          \
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, ADD, CROW, XCD, NT, CL>), dim3(P.n_blocks),    \
                        dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, L.rai, L.ridx,       \
                        A.d_aj, A.d_aa,                                                             \
-                       x, z, y);                                                                   \
+                       x, z, y, dpart, stop);                                                      \
     return
     // The speed knobs (XCD remap, non-temporal, clamped loads) are compiled
     // for the plain full-row MatMult, the benchmarked path; MatMultAdd and
@@ -550,8 +578,20 @@ static void pipe_dispatch(const aijhip_mat &A, const RowList &L, const double *x
 #define AIJHIP_GEOM(G) kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap, \
                        kStreamGeoms[G].rows / kStreamGeoms[G].threads
 
+bool stream_dot_fusable(const aijhip_mat &A) {
+    const Plan &P = A.plan;
+    return P.kernel == AIJHIP_KERNEL_STREAM && !A.compressed && P.n_longs == 0 && P.tune.persist == 0 &&
+           A.m == A.n;
+}
+
+hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, double *dpart,
+                             const int *stop, hipStream_t s) {
+    if (!stream_dot_fusable(A)) return hipErrorInvalidValue;
+    return launch_stream(A, x, nullptr, y, false, s, dpart, stop);
+}
+
 hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, double *y,
-                         bool add, hipStream_t s) {
+                         bool add, hipStream_t s, double *dpart, const int *stop) {
     hipError_t e = compressed_prologue(A, z, y, add, s);
     if (e != hipSuccess) return e;
     const RowList L = row_list(A);
@@ -571,7 +611,7 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
 #undef AIJHIP_PG
         if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (P.n_blocks > 0) {
-#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, L, x, z, y, add, s); break
+#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, L, x, z, y, add, s, dpart, stop); break
         switch (g) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
             AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8);
@@ -664,6 +704,17 @@ hipError_t launch_merge(const aijhip_mat &A, const double *x, const double *z, d
     hipLaunchKernelGGL(k_merge_fixup, dim3(grid_for(P.n_tiles, 256)), dim3(256), 0, s,
                        P.n_tiles, P.d_carry_row, P.d_carry_val, y);
     return hipGetLastError();
+}
+
+hipError_t launch_mult(const aijhip_mat &A, const double *x, const double *z, double *y,
+                       bool add, hipStream_t s) {
+    switch (A.plan.kernel) {
+        case AIJHIP_KERNEL_STREAM: return launch_stream(A, x, z, y, add, s);
+        case AIJHIP_KERNEL_SCALAR: return launch_scalar(A, x, z, y, add, s);
+        case AIJHIP_KERNEL_VECTOR: return launch_vector(A, x, z, y, add, s);
+        case AIJHIP_KERNEL_MERGE: return launch_merge(A, x, z, y, add, s);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj,

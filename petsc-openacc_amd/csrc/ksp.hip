@@ -1,0 +1,493 @@
+// ksp.hip — device-resident preconditioned CG (include/aijhip_ksp.h).
+//
+// Restates PETSc 3.7.6 KSPSolve_CG [ext] (src/ksp/ksp/impls/cg/cg.c) with
+// KSPConvergedDefault [ext], as driven by /root/reference/src/main_ksp.cpp:92-103
+// (KSPCG, KSPSetReusePreconditioner) and the tolerances of
+// /root/reference/configs/PETSc_SolverOptions_GAMG.info:1-4. Per iteration:
+//
+//   K1  P = Z            (i = 0)      | P = Z + b P        (VecCopy / VecAYPX)
+//   K2  W = A P, partials of P.W      (KSP_MatMult + VecXDot, fused into the
+//                                      STREAM SpMV epilogue when possible)
+//   K3  scalar step: dpi, indefinite-matrix check, a = beta / dpi
+//   K4  X += a P, R -= a W, Z = D^-1 R, partials of Z.Z, Z.R, R.R
+//                                     (2 x VecAXPY + PCApply_Jacobi + dots)
+//   K5  scalar step: dp, KSPConvergedDefault, beta, indefinite-PC / beta = 0
+//                    checks, b = beta / betaold
+//
+// W shares Z's storage as in PETSc (W = Z when not single-reduction). All
+// scalars live on the device; every kernel returns at once once the device
+// flag `done` is set, so the host launches iterations in batches and polls.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "aijhip_internal.h"
+#include "aijhip_ksp.h"
+
+namespace {
+
+struct CGState {
+    double beta, betaold, dpi, dpiold, a, b, dp, rnorm0, ttol;
+    int32_t its, reason, done, i;
+};
+
+struct CGParams {
+    double rtol, abstol, dtol;
+    int32_t max_it, normtype, guess_zero, pc;
+};
+
+constexpr int kVecThreads = 256;
+constexpr int kRedThreads = 1024;
+constexpr int kNQ = 4;  // partial quantities per vector block
+
+// Block sum in a fixed order (as block_sum in aijhip_kernels.hip).
+template <int T>
+__device__ __forceinline__ double bsum(double v, double *scratch) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    const int t = threadIdx.x;
+    __syncthreads();
+    if ((t & 63) == 0) scratch[t >> 6] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (t == 0) {
+#pragma unroll
+        for (int w = 0; w < T / 64; ++w) s += scratch[w];
+    }
+    __syncthreads();
+    return s;
+}
+
+// Sum of part[0..n) in a fixed order by one 1024-lane block (valid in lane 0).
+__device__ double reduce_parts(const double *part, int n, double *scratch) {
+    double s = 0.0;
+    for (int j = threadIdx.x; j < n; j += kRedThreads) s += part[j];
+    return bsum<kRedThreads>(s, scratch);
+}
+
+// KSPConvergedDefault [ext]: the n = 0 call fixes rnorm0 and
+// ttol = max(rtol * rnorm0, abstol).
+__device__ int32_t converged(int n, double rnorm, double snorm, CGState *S, const CGParams &p) {
+    if (n == 0) {
+        S->rnorm0 = snorm;
+        S->ttol = fmax(p.rtol * snorm, p.abstol);
+    }
+    if (isnan(rnorm) || isinf(rnorm)) return AIJHIP_KSP_DIVERGED_NANORINF;
+    if (rnorm <= S->ttol) return rnorm < p.abstol ? AIJHIP_KSP_CONVERGED_ATOL : AIJHIP_KSP_CONVERGED_RTOL;
+    if (rnorm >= p.dtol * S->rnorm0) return AIJHIP_KSP_DIVERGED_DTOL;
+    return 0;
+}
+
+__device__ double norm_of(const CGParams &p, double zz, double rr, double zr) {
+    switch (p.normtype) {
+        case AIJHIP_KSP_NORM_PRECONDITIONED: return sqrt(zz);
+        case AIJHIP_KSP_NORM_UNPRECONDITIONED: return sqrt(rr);
+        case AIJHIP_KSP_NORM_NATURAL: return sqrt(fabs(zr));
+        default: return 0.0;
+    }
+}
+
+// PCSetUp_Jacobi [ext]: diag = MatGetDiagonal (first stored diagonal entry,
+// 0 if none), zero entries replaced by 1, then reciprocal.
+__global__ void k_diag_inv(int m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                           const double *__restrict__ aa, double *dinv) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= m) return;
+    double d = 0.0;
+    for (int32_t k = ai[r]; k < ai[r + 1]; ++k)
+        if (aj[k] == r) { d = aa[k]; break; }
+    if (d == 0.0) d = 1.0;
+    dinv[r] = 1.0 / d;
+}
+
+// Initial residual: r = b (zero guess) or r = b - A x (r holds A x on entry);
+// z = D^-1 r; partials Z.Z, Z.R, R.R and (nonzero guess) |D^-1 b|^2 or |b|^2.
+__global__ __launch_bounds__(kVecThreads) void k_init(int64_t n, const double *__restrict__ b,
+                                                      double *r, double *z,
+                                                      const double *__restrict__ dinv,
+                                                      double *part, CGParams p) {
+    __shared__ double scratch[kVecThreads / 64];
+    double zz = 0.0, zr = 0.0, rr = 0.0, ss = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads) {
+        const double bi = b[i];
+        const double ri = p.guess_zero ? bi : bi - r[i];  // VecAYPX(R,-1,B): r = b + (-1) r
+        const double di = p.pc ? dinv[i] : 1.0;
+        const double zi = p.pc ? di * ri : ri;
+        r[i] = ri;
+        z[i] = zi;
+        zz += zi * zi;
+        zr += zi * ri;
+        rr += ri * ri;
+        const double sb = (p.pc && p.normtype != AIJHIP_KSP_NORM_UNPRECONDITIONED) ? di * bi : bi;
+        ss += sb * sb;
+    }
+    const int nb = gridDim.x;
+    double v;
+    v = bsum<kVecThreads>(zz, scratch); if (threadIdx.x == 0) part[0 * nb + blockIdx.x] = v;
+    v = bsum<kVecThreads>(zr, scratch); if (threadIdx.x == 0) part[1 * nb + blockIdx.x] = v;
+    v = bsum<kVecThreads>(rr, scratch); if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = v;
+    v = bsum<kVecThreads>(ss, scratch); if (threadIdx.x == 0) part[3 * nb + blockIdx.x] = v;
+}
+
+__global__ __launch_bounds__(kRedThreads) void k_reduce_init(const double *part, int nb, CGState *S,
+                                                             double *hist, CGParams p) {
+    __shared__ double scratch[kRedThreads / 64];
+    const double zz = reduce_parts(part + 0 * nb, nb, scratch);
+    const double zr = reduce_parts(part + 1 * nb, nb, scratch);
+    const double rr = reduce_parts(part + 2 * nb, nb, scratch);
+    const double ss = reduce_parts(part + 3 * nb, nb, scratch);
+    if (threadIdx.x != 0) return;
+    CGState s{};
+    s.dp = norm_of(p, zz, rr, zr);
+    hist[0] = s.dp;
+    s.its = 0;
+    s.reason = converged(0, s.dp, p.guess_zero ? s.dp : sqrt(ss), &s, p);
+    s.beta = zr;
+    s.i = 0;
+    if (!s.reason) {  // top of iteration 0
+        s.its = 1;
+        if (s.beta == 0.0) s.reason = AIJHIP_KSP_CONVERGED_ATOL;
+        else if (p.max_it <= 0) { s.reason = AIJHIP_KSP_DIVERGED_ITS; s.its = 0; }
+    }
+    s.b = 0.0;
+    s.done = s.reason != 0;
+    *S = s;
+}
+
+// K1: P = Z (i = 0) or P = Z + b P (VecAYPX: y = x + alpha y, product first).
+__global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *__restrict__ z, double *p,
+                                                      const CGState *S) {
+    if (S->done) return;
+    const bool first = S->i == 0;
+    const double bb = S->b;
+    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads)
+        p[i] = first ? z[i] : z[i] + bb * p[i];
+}
+
+// Unfused dot partials of p . w (when the SpMV cannot carry the epilogue).
+__global__ __launch_bounds__(kVecThreads) void k_dot(int64_t n, const double *__restrict__ p,
+                                                     const double *__restrict__ w, double *part,
+                                                     const CGState *S) {
+    __shared__ double scratch[kVecThreads / 64];
+    if (S->done) return;
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads)
+        s += p[i] * w[i];
+    const double v = bsum<kVecThreads>(s, scratch);
+    if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+
+// K3: dpi = P.W, DIVERGED_INDEFINITE_MAT check, a = beta / dpi.
+__global__ __launch_bounds__(kRedThreads) void k_reduce_dpi(const double *part, int nb, CGState *S) {
+    __shared__ double scratch[kRedThreads / 64];
+    if (S->done) return;
+    const double dpi = reduce_parts(part, nb, scratch);
+    if (threadIdx.x != 0) return;
+    S->dpiold = S->dpi;
+    S->dpi = dpi;
+    S->betaold = S->beta;
+    if (dpi == 0.0 || (S->i > 0 && dpi * S->dpiold <= 0.0)) {
+        S->reason = AIJHIP_KSP_DIVERGED_INDEFINITE_MAT;
+        S->done = 1;
+        return;
+    }
+    S->a = S->beta / dpi;
+}
+
+// K4: X += a P; R -= a W; Z = D^-1 R (W and Z share storage: w[i] is read
+// before z[i] is written by the same lane); partials Z.Z, Z.R, R.R.
+__global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *x, const double *__restrict__ p,
+                                                        double *r, double *wz,
+                                                        const double *__restrict__ dinv, double *part,
+                                                        const CGState *S, int pc) {
+    __shared__ double scratch[kVecThreads / 64];
+    if (S->done) return;
+    const double a = S->a, na = -a;
+    double zz = 0.0, zr = 0.0, rr = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads) {
+        x[i] = x[i] + a * p[i];          // VecAXPY(X, a, P)
+        const double ri = r[i] + na * wz[i];  // VecAXPY(R, -a, W)
+        const double zi = pc ? dinv[i] * ri : ri;  // PCApply_Jacobi: VecPointwiseMult
+        r[i] = ri;
+        wz[i] = zi;
+        zz += zi * zi;
+        zr += zi * ri;
+        rr += ri * ri;
+    }
+    const int nb = gridDim.x;
+    double v;
+    v = bsum<kVecThreads>(zz, scratch); if (threadIdx.x == 0) part[0 * nb + blockIdx.x] = v;
+    v = bsum<kVecThreads>(zr, scratch); if (threadIdx.x == 0) part[1 * nb + blockIdx.x] = v;
+    v = bsum<kVecThreads>(rr, scratch); if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = v;
+}
+
+// K5: dp, convergence test at n = i + 1, beta, top-of-loop checks of i + 1.
+__global__ __launch_bounds__(kRedThreads) void k_reduce_iter(const double *part, int nb, CGState *S,
+                                                             double *hist, CGParams p) {
+    __shared__ double scratch[kRedThreads / 64];
+    if (S->done) return;
+    const double zz = reduce_parts(part + 0 * nb, nb, scratch);
+    const double zr = reduce_parts(part + 1 * nb, nb, scratch);
+    const double rr = reduce_parts(part + 2 * nb, nb, scratch);
+    if (threadIdx.x != 0) return;
+    CGState s = *S;
+    s.dp = norm_of(p, zz, rr, zr);
+    hist[s.i + 1] = s.dp;
+    s.reason = converged(s.i + 1, s.dp, 0.0, &s, p);
+    if (!s.reason) {
+        s.beta = zr;
+        s.i += 1;
+        if (s.i >= p.max_it) {
+            s.reason = AIJHIP_KSP_DIVERGED_ITS;
+        } else {
+            s.its = s.i + 1;
+            if (s.beta == 0.0) s.reason = AIJHIP_KSP_CONVERGED_ATOL;
+            else if (s.beta * s.betaold < 0.0) s.reason = AIJHIP_KSP_DIVERGED_INDEFINITE_PC;
+            else s.b = s.beta / s.betaold;
+        }
+    }
+    s.done = s.reason != 0;
+    *S = s;
+}
+
+int kfail(int code, const std::string &msg) {
+    aijhip::set_error(msg);
+    return code;
+}
+
+int khip(hipError_t e, const char *what) {
+    aijhip::set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return AIJHIP_ERR_HIP;
+}
+
+}  // namespace
+
+struct aijhip_ksp {
+    aijhip_mat *A = nullptr;
+    int pc = AIJHIP_PC_JACOBI;
+    int normtype = AIJHIP_KSP_NORM_PRECONDITIONED;
+    bool guess_nonzero = false;
+    double rtol = 1e-5, abstol = 1e-50, dtol = 1e5;
+    int32_t max_it = 10000;
+    bool set_up = false;
+    bool fused = false;
+    int vec_grid = 0;
+    double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
+    double *d_hist = nullptr;
+    int32_t hist_cap = 0;
+    CGState *d_state = nullptr;
+    CGState *h_state = nullptr;  // pinned
+    int32_t its = 0;
+    int reason = 0;
+    double rnorm = 0.0;
+    std::vector<double> hist;
+};
+
+namespace {
+
+void ksp_free(aijhip_ksp *K) {
+    hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
+    hipFree(K->d_hist); hipFree(K->d_state);
+    if (K->h_state) hipHostFree(K->h_state);
+    K->d_dinv = K->d_r = K->d_z = K->d_p = K->d_part = K->d_hist = nullptr;
+    K->d_state = nullptr;
+    K->h_state = nullptr;
+    K->set_up = false;
+}
+
+struct KDeviceGuard {
+    int prev = -1;
+    explicit KDeviceGuard(int dev) {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~KDeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+}  // namespace
+
+extern "C" {
+
+int aijhip_ksp_create(aijhip_mat_t A, aijhip_ksp_t *out) {
+    if (!out) return kfail(AIJHIP_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (!A) return kfail(AIJHIP_ERR_ARG, "NULL matrix");
+    if (A->m != A->n) return kfail(AIJHIP_ERR_ARG, "CG needs a square operator");
+    aijhip_ksp *K = new (std::nothrow) aijhip_ksp();
+    if (!K) return kfail(AIJHIP_ERR_ALLOC, "host allocation");
+    K->A = A;
+    *out = K;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_set_tolerances(aijhip_ksp_t K, double rtol, double abstol, double dtol, int32_t max_it) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (rtol < 0 || abstol < 0 || dtol <= 0 || max_it < 0) return kfail(AIJHIP_ERR_ARG, "bad tolerance");
+    K->rtol = rtol; K->abstol = abstol; K->dtol = dtol;
+    if (max_it != K->max_it) { K->max_it = max_it; K->set_up = false; }
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_set_pc_type(aijhip_ksp_t K, int pc) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI) return kfail(AIJHIP_ERR_ARG, "unknown PC type");
+    K->pc = pc;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_set_norm_type(aijhip_ksp_t K, int nt) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (nt < AIJHIP_KSP_NORM_NONE || nt > AIJHIP_KSP_NORM_NATURAL) return kfail(AIJHIP_ERR_ARG, "bad norm type");
+    K->normtype = nt;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_set_initial_guess_nonzero(aijhip_ksp_t K, int flg) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    K->guess_nonzero = flg != 0;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_set_up(aijhip_ksp_t K) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (K->set_up) return AIJHIP_OK;
+    aijhip_mat *A = K->A;
+    KDeviceGuard g(A->device);
+    ksp_free(K);
+    const int64_t m = A->m;
+    const size_t vb = sizeof(double) * (size_t)std::max<int64_t>(m, 1);
+    K->fused = aijhip::stream_dot_fusable(*A);
+    K->vec_grid = (int)std::max<int64_t>(1, std::min<int64_t>((m + kVecThreads - 1) / kVecThreads, (int64_t)A->n_cu * 8));
+    const int64_t nparts = std::max<int64_t>((int64_t)kNQ * K->vec_grid, K->fused ? A->plan.n_blocks : K->vec_grid);
+    K->hist_cap = K->max_it + 2;
+    hipError_t e;
+    if ((e = hipMalloc(&K->d_dinv, vb)) != hipSuccess || (e = hipMalloc(&K->d_r, vb)) != hipSuccess ||
+        (e = hipMalloc(&K->d_z, vb)) != hipSuccess || (e = hipMalloc(&K->d_p, vb)) != hipSuccess ||
+        (e = hipMalloc(&K->d_part, sizeof(double) * (size_t)nparts)) != hipSuccess ||
+        (e = hipMalloc(&K->d_hist, sizeof(double) * (size_t)K->hist_cap)) != hipSuccess ||
+        (e = hipMalloc(&K->d_state, sizeof(CGState))) != hipSuccess ||
+        (e = hipHostMalloc(&K->h_state, sizeof(CGState), hipHostMallocDefault)) != hipSuccess) {
+        ksp_free(K);
+        return khip(e, "ksp set-up allocation");
+    }
+    if (m > 0) {
+        hipLaunchKernelGGL(k_diag_inv, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, nullptr, A->m, A->d_ai,
+                           A->d_aj, A->d_aa, K->d_dinv);
+        if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess) {
+            ksp_free(K);
+            return khip(e, "PCSetUp_Jacobi");
+        }
+    }
+    K->set_up = true;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    int rc = aijhip_ksp_set_up(K);
+    if (rc) return rc;
+    aijhip_mat *A = K->A;
+    const int64_t m = A->m;
+    if (m > 0 && (!b || !x)) return kfail(AIJHIP_ERR_ARG, "NULL vector");
+    if (b == x) return kfail(AIJHIP_ERR_ARG, "b and x alias");
+    KDeviceGuard g(A->device);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipError_t e = hipSuccess;
+    CGParams p{K->rtol, K->abstol, K->dtol, K->max_it, K->normtype, K->guess_nonzero ? 0 : 1, K->pc};
+    const dim3 vg(K->vec_grid), vt(kVecThreads), rt(kRedThreads);
+    const int nb = K->vec_grid;
+    // KSPSolve [ext]: zero initial guess -> x = 0; else r = A x first.
+    if (!K->guess_nonzero) {
+        if (m > 0) e = hipMemsetAsync(x, 0, sizeof(double) * (size_t)m, s);
+    } else {
+        e = aijhip::launch_mult(*A, x, nullptr, K->d_r, false, s);
+    }
+    if (e != hipSuccess) return khip(e, "KSPSolve init");
+    hipLaunchKernelGGL(k_init, vg, vt, 0, s, m, b, K->d_r, K->d_z, K->d_dinv, K->d_part, p);
+    hipLaunchKernelGGL(k_reduce_init, dim3(1), rt, 0, s, K->d_part, nb, K->d_state, K->d_hist, p);
+    if ((e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve init");
+    // iterations in batches; every kernel is a no-op once `done` is set
+    const int batch = K->fused ? 8 : 1;
+    int32_t launched = 0;
+    for (;;) {
+        if ((e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess)
+            return khip(e, "KSPSolve poll");
+        if (K->h_state->done || launched >= K->max_it) break;
+        for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched) {
+            hipLaunchKernelGGL(k_aypx, vg, vt, 0, s, m, K->d_z, K->d_p, K->d_state);
+            if (K->fused) {
+                e = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, s);
+                if (e == hipSuccess)
+                    hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, A->plan.n_blocks, K->d_state);
+            } else {
+                e = aijhip::launch_mult(*A, K->d_p, nullptr, K->d_z, false, s);
+                hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
+                hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, nb, K->d_state);
+            }
+            hipLaunchKernelGGL(k_update, vg, vt, 0, s, m, x, K->d_p, K->d_r, K->d_z, K->d_dinv, K->d_part,
+                               K->d_state, K->pc);
+            hipLaunchKernelGGL(k_reduce_iter, dim3(1), rt, 0, s, K->d_part, nb, K->d_state, K->d_hist, p);
+            if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve iteration");
+        }
+    }
+    const CGState &st = *K->h_state;
+    K->its = st.its;
+    K->reason = st.reason ? st.reason : AIJHIP_KSP_DIVERGED_ITS;
+    K->rnorm = st.dp;
+    const int32_t nh = std::min<int32_t>(K->hist_cap, st.its + 1);
+    K->hist.resize((size_t)std::max(nh, 0));
+    if (nh > 0 &&
+        (e = hipMemcpy(K->hist.data(), K->d_hist, sizeof(double) * (size_t)nh, hipMemcpyDeviceToHost)) != hipSuccess)
+        return khip(e, "residual history");
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_iteration_number(aijhip_ksp_t K, int32_t *its) {
+    if (!K || !its) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    *its = K->its;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_residual_norm(aijhip_ksp_t K, double *rnorm) {
+    if (!K || !rnorm) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    *rnorm = K->rnorm;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_converged_reason(aijhip_ksp_t K, int *reason) {
+    if (!K || !reason) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    *reason = K->reason;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_residual_history(aijhip_ksp_t K, double *hist, int32_t na, int32_t *n) {
+    if (!K || !n || (na > 0 && !hist)) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    const int32_t c = std::min<int32_t>(na, (int32_t)K->hist.size());
+    std::copy(K->hist.begin(), K->hist.begin() + c, hist);
+    *n = c;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_fused(aijhip_ksp_t K, int *fused) {
+    if (!K || !fused) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    *fused = K->fused ? 1 : 0;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_destroy(aijhip_ksp_t K) {
+    if (!K) return AIJHIP_OK;
+    {
+        KDeviceGuard g(K->A->device);
+        (void)hipDeviceSynchronize();
+        ksp_free(K);
+    }
+    delete K;
+    return AIJHIP_OK;
+}
+
+}  // extern "C"

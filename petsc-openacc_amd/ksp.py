@@ -1,0 +1,158 @@
+"""Device-resident CG (include/aijhip_ksp.h) — the KSP side of the path.
+
+Mirrors the reference's solver set-up (/root/reference/src/main_ksp.cpp:92-103:
+KSPCreate, KSPSetOperators, KSPSetType(KSPCG), KSPSetFromOptions, KSPSetUp,
+KSPSolve, KSPGetConvergedReason / IterationNumber / ResidualNorm) over the
+C ABI. Options follow /root/reference/configs/PETSc_SolverOptions_GAMG.info
+(-ksp_atol 1e-12 -ksp_rtol 1e-14 -ksp_max_it 10000); the preconditioner is
+Jacobi (the reference's smoother / coarse PC) until the GAMG hierarchy lands.
+"""
+from __future__ import annotations
+
+import ctypes
+import importlib
+import time
+
+import numpy as np
+
+_pkg = importlib.import_module("petsc-openacc_amd")
+
+PC_TYPES = {"none": 0, "jacobi": 1}
+NORM_TYPES = {"none": 0, "preconditioned": 1, "unpreconditioned": 2, "natural": 3}
+REASONS = {2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
+           -8: "DIVERGED_INDEFINITE_PC", -9: "DIVERGED_NANORINF", -10: "DIVERGED_INDEFINITE_MAT"}
+KSP_SYMBOLS = (
+    "aijhip_ksp_create", "aijhip_ksp_set_tolerances", "aijhip_ksp_set_pc_type", "aijhip_ksp_set_norm_type",
+    "aijhip_ksp_set_initial_guess_nonzero", "aijhip_ksp_set_up", "aijhip_ksp_solve",
+    "aijhip_ksp_get_iteration_number", "aijhip_ksp_get_residual_norm", "aijhip_ksp_get_converged_reason",
+    "aijhip_ksp_get_residual_history", "aijhip_ksp_get_fused", "aijhip_ksp_destroy",
+)
+_P = ctypes.c_void_p
+_bound = False
+
+
+def _lib():
+    global _bound
+    L = _pkg.lib()
+    if not _bound:
+        for n in KSP_SYMBOLS:
+            getattr(L, n).restype = ctypes.c_int
+        L.aijhip_ksp_create.argtypes = [_P, ctypes.POINTER(_P)]
+        L.aijhip_ksp_set_tolerances.argtypes = [_P, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_int32]
+        L.aijhip_ksp_set_pc_type.argtypes = [_P, ctypes.c_int]
+        L.aijhip_ksp_set_norm_type.argtypes = [_P, ctypes.c_int]
+        L.aijhip_ksp_set_initial_guess_nonzero.argtypes = [_P, ctypes.c_int]
+        L.aijhip_ksp_set_up.argtypes = [_P]
+        L.aijhip_ksp_solve.argtypes = [_P, _P, _P, _P]
+        L.aijhip_ksp_get_iteration_number.argtypes = [_P, ctypes.POINTER(ctypes.c_int32)]
+        L.aijhip_ksp_get_residual_norm.argtypes = [_P, ctypes.POINTER(ctypes.c_double)]
+        L.aijhip_ksp_get_converged_reason.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
+        L.aijhip_ksp_get_residual_history.argtypes = [_P, _P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
+        L.aijhip_ksp_get_fused.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
+        L.aijhip_ksp_destroy.argtypes = [_P]
+        _bound = True
+    return L
+
+
+class KSPCG:
+    """KSPCG on a SeqAIJHIP operator (device vectors)."""
+
+    def __init__(self, A, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
+                 norm="preconditioned", guess_nonzero=False):
+        L = _lib()
+        self.A = A
+        self._h = _P()
+        _pkg._check(L.aijhip_ksp_create(A._h, ctypes.byref(self._h)))
+        self.set_tolerances(rtol, atol, dtol, max_it)
+        _pkg._check(L.aijhip_ksp_set_pc_type(self._h, PC_TYPES[pc]))
+        _pkg._check(L.aijhip_ksp_set_norm_type(self._h, NORM_TYPES[norm]))
+        _pkg._check(L.aijhip_ksp_set_initial_guess_nonzero(self._h, int(guess_nonzero)))
+
+    def set_tolerances(self, rtol, atol, dtol, max_it):
+        _pkg._check(_lib().aijhip_ksp_set_tolerances(self._h, rtol, atol, dtol, int(max_it)))
+
+    def set_up(self):
+        _pkg._check(_lib().aijhip_ksp_set_up(self._h))
+
+    def solve(self, b, x, stream=None):
+        _pkg._check(_lib().aijhip_ksp_solve(self._h, _pkg._dev_ptr(b, self.A.m, "b"),
+                                            _pkg._dev_ptr(x, self.A.m, "x"), _pkg._stream_handle(stream)))
+
+    @property
+    def its(self) -> int:
+        v = ctypes.c_int32()
+        _pkg._check(_lib().aijhip_ksp_get_iteration_number(self._h, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def reason(self) -> int:
+        v = ctypes.c_int()
+        _pkg._check(_lib().aijhip_ksp_get_converged_reason(self._h, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def rnorm(self) -> float:
+        v = ctypes.c_double()
+        _pkg._check(_lib().aijhip_ksp_get_residual_norm(self._h, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def fused(self) -> bool:
+        v = ctypes.c_int()
+        _pkg._check(_lib().aijhip_ksp_get_fused(self._h, ctypes.byref(v)))
+        return bool(v.value)
+
+    def history(self) -> np.ndarray:
+        buf = np.empty(self.its + 1)
+        n = ctypes.c_int32()
+        _pkg._check(_lib().aijhip_ksp_get_residual_history(self._h, buf.ctypes.data, len(buf), ctypes.byref(n)))
+        return buf[: n.value]
+
+    def destroy(self):
+        if getattr(self, "_h", None) and self._h.value:
+            _lib().aijhip_ksp_destroy(self._h)
+            self._h = _P()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.destroy()
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+def cg_bytes_per_iteration(m: int, nnz: int, fused: bool) -> int:
+    """Algorithmic HBM bytes of one CG iteration: SpMV (SURVEY §8d bytes) +
+    the P read of the fused dot, AYPX (2 reads + 1 write), the fused update
+    (X, P, R, W/Z, D^-1 read; X, R, Z written)."""
+    spmv = 12 * nnz + 4 * (m + 1) + 16 * m
+    dot = 8 * m if fused else 16 * m
+    return spmv + dot + 24 * m + 64 * m
+
+
+def bench_cg(pkg, A, nx, ny, nz, dev, iters=200):
+    """CG iterations/s on the device at the benchmark operand: a fixed count
+    of iterations (rtol = atol = 0, so every iteration runs), timed whole."""
+    import torch
+    rhs, _ = pkg.poisson_vectors(nx, ny, nz)
+    b = torch.from_numpy(rhs).to(dev)
+    x = torch.empty_like(b)
+    with KSPCG(A, rtol=0.0, atol=0.0, max_it=iters) as ksp:
+        ksp.set_up()
+        ksp.solve(b, x)  # warm-up
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ksp.solve(b, x)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        its, fused = ksp.its, ksp.fused
+    m = A.m
+    nb = cg_bytes_per_iteration(m, A.nz, fused)
+    return {"iters": its, "seconds": round(dt, 4), "iters_per_s": round(its / dt, 2),
+            "ms_per_iter": round(dt / its * 1e3, 4), "pc": "jacobi", "fused_spmv_dot": fused,
+            "bytes_per_iter": nb, "GBs": round(nb * its / dt / 1e9, 1)}
