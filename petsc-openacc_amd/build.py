@@ -74,6 +74,23 @@ def build_lib(force: bool = False) -> Path:
     return LIB
 
 
+MAIN_KSP = PKG / "bin" / "main_ksp"
+
+
+def build_main_ksp(force: bool = False) -> Path:
+    """The main_ksp.cpp-equivalent driver, linked against libaijhip.so."""
+    lib = build_lib(force)
+    src = CSRC / "main_ksp.cpp"
+    if not force and not _stale(MAIN_KSP, [src, lib, *(ROOT / "include").glob("*.h")]):
+        return MAIN_KSP
+    MAIN_KSP.parent.mkdir(exist_ok=True)
+    tmp = MAIN_KSP.with_suffix(".tmp")
+    _run([_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O2", "-std=c++17", f"-I{ROOT / 'include'}",
+          str(src), "-o", str(tmp), f"-L{LIBDIR}", "-laijhip", "-Wl,-rpath,$ORIGIN/../lib"])
+    os.replace(tmp, MAIN_KSP)
+    return MAIN_KSP
+
+
 def build_oracle(force: bool = False) -> Path:
     src = ORACLE_DIR / "matmult_seqaij.c"
     if not force and not _stale(ORACLE_LIB, [src]):
@@ -87,7 +104,7 @@ def build_oracle(force: bool = False) -> Path:
 
 
 def build_all(force: bool = False):
-    return build_lib(force), build_oracle(force)
+    return build_lib(force), build_main_ksp(force), build_oracle(force)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,178 @@
+// main_ksp.cpp — the reference's KSP driver (/root/reference/src/main_ksp.cpp)
+// restated over the C ABI: build the 3-D Poisson system of helper.cpp, solve
+// it with device-resident CG, print the same result block
+// (main_ksp.cpp:124-129), so scripts/generate_plots.py's regex still parses it.
+//
+//   main_ksp [-config FILE] [-da_grid_x N] [-da_grid_y N] [-da_grid_z N]
+//            [-ksp_rtol R] [-ksp_atol A] [-ksp_max_it K] [-pc_type jacobi|none]
+//            [-ksp_norm_type preconditioned|unpreconditioned|natural]
+//
+// Options come from the command line and from a PETSc options file
+// (`-key value` per line, '#' comments; PetscOptionsInsertFile,
+// main_ksp.cpp:74-77); command-line values win. Grid defaults 100^3
+// (main_ksp.cpp:33-35 "-100" = 100, overridable).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "aijhip.h"
+#include "aijhip_harness.h"
+#include "aijhip_ksp.h"
+
+namespace {
+
+double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+void parse_file(const std::string &path, std::map<std::string, std::string> &opt) {
+    std::ifstream f(path);
+    if (!f) {
+        std::fprintf(stderr, "main_ksp: cannot open options file %s\n", path.c_str());
+        std::exit(1);
+    }
+    std::string line;
+    while (std::getline(f, line)) {
+        const auto h = line.find('#');
+        if (h != std::string::npos) line.resize(h);
+        std::istringstream is(line);
+        std::string key, val;
+        if (!(is >> key) || key[0] != '-') continue;
+        is >> val;
+        if (!opt.count(key)) opt[key] = val;
+    }
+}
+
+#define CHK(call)                                                                       \
+    do {                                                                                \
+        int rc_ = (call);                                                               \
+        if (rc_) {                                                                      \
+            std::fprintf(stderr, "main_ksp: %s failed (%d): %s\n", #call, rc_,          \
+                         aijhip_last_error());                                          \
+            std::exit(rc_);                                                             \
+        }                                                                               \
+    } while (0)
+
+#define HCHK(call)                                                                      \
+    do {                                                                                \
+        hipError_t e_ = (call);                                                         \
+        if (e_ != hipSuccess) {                                                         \
+            std::fprintf(stderr, "main_ksp: %s: %s\n", #call, hipGetErrorString(e_));   \
+            std::exit(3);                                                               \
+        }                                                                               \
+    } while (0)
+
+}  // namespace
+
+int main(int argc, char **argv) {
+    std::map<std::string, std::string> opt;
+    std::string config;
+    for (int i = 1; i < argc; ++i) {
+        std::string k = argv[i];
+        if (k.size() < 2 || k[0] != '-') continue;
+        std::string v = (i + 1 < argc && argv[i + 1][0] != '-') ? argv[++i] : "";
+        if (k == "-config") config = v;
+        else opt[k] = v;
+    }
+    if (!config.empty()) parse_file(config, opt);
+    auto geti = [&](const char *k, long d) { return opt.count(k) ? std::atol(opt[k].c_str()) : d; };
+    auto getd = [&](const char *k, double d) { return opt.count(k) ? std::atof(opt[k].c_str()) : d; };
+    auto gets = [&](const char *k, const char *d) { return opt.count(k) ? opt[k] : std::string(d); };
+
+    const int32_t nx = (int32_t)geti("-da_grid_x", 100), ny = (int32_t)geti("-da_grid_y", 100),
+                  nz = (int32_t)geti("-da_grid_z", 100);
+    const std::string ksp_type = gets("-ksp_type", "cg");
+    if (ksp_type != "cg") {
+        std::fprintf(stderr, "main_ksp: -ksp_type %s not supported (cg only)\n", ksp_type.c_str());
+        return 1;
+    }
+    std::string pc_type = gets("-pc_type", "jacobi");
+    if (pc_type == "bjacobi") pc_type = "jacobi";  // one block per rank + jacobi sub-PC
+    if (pc_type == "gamg") {
+        std::fprintf(stderr, "main_ksp: -pc_type gamg is not built yet (DESIGN.md §8); using jacobi\n");
+        pc_type = "jacobi";
+    }
+    int pc = pc_type == "none" ? AIJHIP_PC_NONE : AIJHIP_PC_JACOBI;
+    if (pc_type != "none" && pc_type != "jacobi") {
+        std::fprintf(stderr, "main_ksp: -pc_type %s not supported\n", pc_type.c_str());
+        return 1;
+    }
+    const std::string nts = gets("-ksp_norm_type", "preconditioned");
+    const int normtype = nts == "unpreconditioned" ? AIJHIP_KSP_NORM_UNPRECONDITIONED
+                         : nts == "natural"        ? AIJHIP_KSP_NORM_NATURAL
+                         : nts == "none"           ? AIJHIP_KSP_NORM_NONE
+                                                   : AIJHIP_KSP_NORM_PRECONDITIONED;
+
+    // -------- createSystem (helper.cpp:22-57) + device upload
+    const double t_start = now();
+    int64_t nnz = 0;
+    CHK(aijhip_poisson_nnz(nx, ny, nz, 0, nz, &nnz));
+    const int64_t m = (int64_t)nx * ny * nz;
+    std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nnz);
+    std::vector<double> aa((size_t)nnz), rhs((size_t)m), exact((size_t)m);
+    double scale = 0.0;
+    CHK(aijhip_poisson_fill(nx, ny, nz, 0, nz, 1, ai.data(), aj.data(), aa.data(), &scale));
+    CHK(aijhip_poisson_vectors(nx, ny, nz, 0, nz, 1, rhs.data(), exact.data()));
+    aijhip_mat_t A = nullptr;
+    CHK(aijhip_mat_create(0, (int32_t)m, (int32_t)m, nnz, ai.data(), aj.data(), aa.data(), &A));
+    double *d_b = nullptr, *d_x = nullptr;
+    HCHK(hipMalloc(&d_b, sizeof(double) * (size_t)m));
+    HCHK(hipMalloc(&d_x, sizeof(double) * (size_t)m));
+    HCHK(hipMemcpy(d_b, rhs.data(), sizeof(double) * (size_t)m, hipMemcpyHostToDevice));
+    HCHK(hipMemset(d_x, 0, sizeof(double) * (size_t)m));  // VecSet(lhs, 0) (helper.cpp:48)
+    HCHK(hipDeviceSynchronize());
+    const double t_sys = now();
+
+    // -------- KSPCreate / SetOperators / SetType(CG) / SetFromOptions / SetUp (:92-97)
+    aijhip_ksp_t ksp = nullptr;
+    CHK(aijhip_ksp_create(A, &ksp));
+    CHK(aijhip_ksp_set_tolerances(ksp, getd("-ksp_rtol", 1e-5), getd("-ksp_atol", 1e-50),
+                                  getd("-ksp_divtol", 1e5), (int32_t)geti("-ksp_max_it", 10000)));
+    CHK(aijhip_ksp_set_pc_type(ksp, pc));
+    CHK(aijhip_ksp_set_norm_type(ksp, normtype));
+    CHK(aijhip_ksp_set_up(ksp));
+    HCHK(hipDeviceSynchronize());
+    const double t_solver = now();
+
+    // -------- KSPSolve (:103)
+    CHK(aijhip_ksp_solve(ksp, d_b, d_x, nullptr));
+    HCHK(hipDeviceSynchronize());
+    const double t_solve = now();
+
+    int reason = 0;
+    int32_t its = 0;
+    double res = 0.0;
+    CHK(aijhip_ksp_get_converged_reason(ksp, &reason));
+    if (reason < 0) {  // main_ksp.cpp:109-111
+        std::fprintf(stderr, "Diverger reason: %d\n", reason);
+        return 91;
+    }
+    CHK(aijhip_ksp_get_iteration_number(ksp, &its));
+    CHK(aijhip_ksp_get_residual_norm(ksp, &res));
+    // VecAXPY(lhs, -1, exact); VecNorm(lhs, NORM_INFINITY) (:119-121)
+    std::vector<double> x((size_t)m);
+    HCHK(hipMemcpy(x.data(), d_x, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost));
+    double linf = 0.0;
+    for (int64_t i = 0; i < m; ++i) linf = std::fmax(linf, std::fabs(x[i] + (-1.0) * exact[i]));
+
+    std::printf("[Nx, Ny, Nz]: [%d, %d, %d]\n" "Number of iterations: %d\n"
+                "L2 norm of final residual: %f\n" "Maximum norm of error: %f\n"
+                "Time [init, create solver, solve]: [%f, %f, %f]\n",
+                nx, ny, nz, its, res, linf, t_sys - t_start, t_solver - t_sys, t_solve - t_solver);
+    std::fflush(stdout);
+
+    CHK(aijhip_ksp_destroy(ksp));
+    CHK(aijhip_mat_destroy(A));
+    hipFree(d_b);
+    hipFree(d_x);
+    return 0;
+}

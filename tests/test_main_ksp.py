@@ -1,0 +1,51 @@
+"""The main_ksp.cpp-equivalent driver (petsc-openacc_amd/bin/main_ksp): the
+reference's printed result block (/root/reference/src/main_ksp.cpp:124-129),
+parsed with the reference plot script's regex shape
+(/root/reference/scripts/generate_plots.py:87-89), and its numbers checked
+against the oracle CG."""
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import ksp_cg, seqaij
+
+BLOCK = re.compile(r"\[Nx, Ny, Nz\]: \[(\d+), (\d+), (\d+)\]\n"
+                   r"Number of iterations: (\d+)\n"
+                   r"L2 norm of final residual: (\S+)\n"
+                   r"Maximum norm of error: (\S+)\n"
+                   r"Time \[init, create solver, solve\]: \[(\S*?), (\S*?), (\S*?)\]")
+
+
+def test_driver_builds_and_fails_cleanly_without_gpu(pkg):
+    import importlib
+    import torch
+    exe = importlib.import_module("petsc-openacc_amd.build").build_main_ksp()
+    assert exe.exists()
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    r = subprocess.run([str(exe), "-da_grid_x", "4"], capture_output=True, text=True, timeout=60)
+    assert r.returncode != 0 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_driver_output_matches_reference_format_and_oracle(pkg):
+    import importlib
+    exe = importlib.import_module("petsc-openacc_amd.build").build_main_ksp()
+    N = 20
+    r = subprocess.run([str(exe), "-config", str(ROOT / "configs" / "cg_jacobi.info"), "-da_grid_x", str(N),
+                        "-da_grid_y", str(N), "-da_grid_z", str(N)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    m = BLOCK.search(r.stdout)
+    assert m, r.stdout
+    nx, ny, nz, its = (int(m.group(i)) for i in range(1, 5))
+    res, linf = float(m.group(5)), float(m.group(6))
+    assert (nx, ny, nz) == (N, N, N)
+    ai, aj, aa, rhs, exact = seqaij.create_system(N, N, N)
+    x, its_o, reason, hist = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-14, atol=1e-12, max_it=10000)
+    assert abs(its - its_o) <= 1
+    assert abs(linf - np.max(np.abs(x - exact))) < 1e-6  # printed with %f
+    assert linf < 0.05  # second-order discretisation error at h = 1/20
+    assert res < 1e-6
