@@ -101,6 +101,7 @@ typedef struct aijhip_info {
     int32_t stream_nnz_cap;
     int32_t stream_rows;
     int32_t persistent;      /* workgroups per CU of the pipelined STREAM (0 = off) */
+    int32_t exact;           /* AIJHIP_OPT_EXACT in effect                   */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -139,8 +140,15 @@ enum {
     AIJHIP_OPT_NT_LOADS = 3,        /* 1: non-temporal aa/aj loads (default 0) */
     AIJHIP_OPT_PERSISTENT = 4,      /* k > 0: persistent software-pipelined
                                        STREAM, k workgroups per CU (0 = off) */
-    AIJHIP_OPT_CLAMPED_LOADS = 5    /* 1: branch-free clamped loads instead of
+    AIJHIP_OPT_CLAMPED_LOADS = 5,   /* 1: branch-free clamped loads instead of
                                        predicated loads (default 0)         */
+    AIJHIP_OPT_EXACT = 6            /* 1: every row summed sequentially in
+                                       PETSc's order. Default 0: row blocks
+                                       whose mean row length exceeds 16 use
+                                       2..64 lanes per row (reordered sum,
+                                       within the fp64 bound); short-row
+                                       matrices (7-pt Poisson) are bit-exact
+                                       either way                           */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

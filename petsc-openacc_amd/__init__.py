@@ -22,7 +22,7 @@ LIB_PATH = _PKG / "lib" / "libaijhip.so"
 
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
-OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3, "persistent": 4, "clamped": 5}
+OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3, "persistent": 4, "clamped": 5, "exact": 6}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 
@@ -57,7 +57,7 @@ class AIJInfo(ctypes.Structure):
         ("mult_bytes", ctypes.c_int64),
         ("stream_geometry", ctypes.c_int32), ("xcd_remap", ctypes.c_int32), ("nt_loads", ctypes.c_int32),
         ("stream_threads", ctypes.c_int32), ("stream_nnz_cap", ctypes.c_int32), ("stream_rows", ctypes.c_int32),
-        ("persistent", ctypes.c_int32),
+        ("persistent", ctypes.c_int32), ("exact", ctypes.c_int32),
     ]
 
 
@@ -154,7 +154,7 @@ class SeqAIJHIP:
     """
 
     def __init__(self, ai, aj, aa, ncols: int | None = None, device: int = 0, kernel: str = "auto",
-                 lanes: int = 0):
+                 lanes: int = 0, **options):
         ai = np.ascontiguousarray(ai, dtype=np.int32)
         aj = np.ascontiguousarray(aj, dtype=np.int32)
         aa = np.ascontiguousarray(aa, dtype=np.float64)
@@ -167,6 +167,8 @@ class SeqAIJHIP:
         self.m, self.n, self.nz, self.device = m, int(ncols), int(len(aj)), device
         if kernel != "auto" or lanes:
             self.set_kernel(kernel, lanes)
+        for k, v in options.items():  # speed / ordering knobs: geometry, exact, ...
+            self.set_option(k, v)
 
     # ---- PETSc MatOps analogues
     def set_kernel(self, kernel: str, lanes: int = 0):

@@ -416,6 +416,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             t.persist = value;
             break;
         case AIJHIP_OPT_CLAMPED_LOADS: t.clamped = value != 0; break;
+        case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -572,6 +573,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
     info->persistent = A->plan.tune.persist;
+    info->exact = A->plan.tune.exact ? 1 : 0;
     return AIJHIP_OK;
 }
 

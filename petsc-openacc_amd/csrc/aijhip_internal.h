@@ -79,7 +79,12 @@ struct Tuning {
     bool nt = false;     // non-temporal matrix loads
     int persist = 0;     // >0: persistent pipelined STREAM, this many workgroups per CU
     bool clamped = false;  // branch-free clamped loads instead of predicated loads
+    bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
 };
+
+// STREAM blocks whose mean row length exceeds this use several lanes per row
+// in the reduction phase (reordered sum) unless Tuning::exact is set.
+constexpr int kSplitMinMean = 16;
 
 struct Plan {
     int kernel = AIJHIP_KERNEL_STREAM;

@@ -95,8 +95,8 @@ __device__ __forceinline__ double block_sum(double v, double *scratch) {
 
 template <int T, int CAP, int RPT, bool ADD, bool CROW, bool XCD, bool NT, bool CLAMPED>
 __global__ __launch_bounds__(T) void k_spmv_stream(
-    const BlockDesc *__restrict__ blk, int nblk, int xchunk, const int32_t *__restrict__ rai,
-    const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
+    const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
+    const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const double *__restrict__ x,
     const double *z, double *y, double *dpart, const int *stop) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
@@ -154,15 +154,42 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     }
     __syncthreads();
 
-    // Phase 2: one lane per row, PETSc's sequential order.
+    // Phase 2. Short rows (block mean <= kSplitMinMean entries): one lane per
+    // row, PETSc's sequential order (bit-exact). Long rows: L lanes per row
+    // (strided partial sums + __shfl_xor tree; reordered, deterministic), so
+    // a block of few long rows does not leave most lanes idle on a serial
+    // LDS chain. `exact` forces the sequential form everywhere.
     double dotv = 0.0;
+    const int nr = d.nrows;
+    int L = 1;
+    if (RPT == 1 && !exact && d.nk > kSplitMinMean * nr) {
+        const int cap = min(64, T / max(nr, 1));
+        while (L * 2 <= cap) L *= 2;
+    }
+    if (L == 1) {
 #pragma unroll
-    for (int q = 0; q < RPT; ++q) {
-        if (t + q * T < d.nrows) {
-            double s = sum[q];
-            for (int32_t k = rs[q]; k < re[q]; ++k) s += prod[k - k0];
-            y[orow[q]] = s;
-            if (dpart) dotv += x[orow[q]] * s;
+        for (int q = 0; q < RPT; ++q) {
+            if (t + q * T < nr) {
+                double s = sum[q];
+                for (int32_t k = rs[q]; k < re[q]; ++k) s += prod[k - k0];
+                y[orow[q]] = s;
+                if (dpart) dotv += x[orow[q]] * s;
+            }
+        }
+    } else {
+        const int g = t / L, j = t - g * L;
+        const bool own = g < nr;
+        const int r = d.row0 + min(g, nr - 1);
+        const int32_t grs = rai[r], gre = rai[r + 1];
+        double s = 0.0;
+        if (own)
+            for (int32_t k = grs + j; k < gre; k += L) s += prod[k - k0];
+        for (int off = L >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+        if (own && j == 0) {
+            const int o = CROW ? ridx[r] : r;
+            const double v = ADD ? z[o] + s : s;
+            y[o] = v;
+            if (dpart) dotv += x[o] * v;
         }
     }
     // Optional fused epilogue for CG (grid-uniform branch): the block's
@@ -527,7 +554,8 @@ static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double 
     const Plan &P = A.plan;
 #define AIJHIP_SL(ADD, CROW, XCD, NT, CL)                                                          \
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, ADD, CROW, XCD, NT, CL>), dim3(P.n_blocks),    \
-                       dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, L.rai, L.ridx,       \
+                       dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, (int)P.tune.exact,   \
+                       L.rai, L.ridx,                                                              \
                        A.d_aj, A.d_aa,                                                             \
                        x, z, y, dpart, stop);                                                      \
     return

@@ -73,19 +73,27 @@ inline uint64_t rnd(uint64_t seed, uint64_t stream, uint64_t idx) {
 }
 inline double unit(uint64_t z) { return (double)(z >> 11) * (1.0 / 9007199254740992.0); }
 
-// Skewed stand-in row length.
-constexpr int32_t kBand = 2000;
+// Skewed stand-in. Flan_1565 is a 3-D hexahedral FEM model with 3 dofs per
+// node, so a row's columns come in runs of 3 (one per neighbouring node's
+// dofs): ordinary rows couple 15..33 nodes (45..99 entries, mean 72 ~ Flan's
+// 114.2M / 1.565M) within a band of +-kBandNodes nodes; a 1e-4 fraction of
+// hub rows (log-uniform 1e3..2e5 scattered entries) stresses load balance.
+constexpr int32_t kBandNodes = 700;
+inline bool skew_is_hub(int32_t r, uint64_t seed) { return rnd(seed, 1, (uint64_t)r) % 10000 == 0; }
+inline void skew_band(int32_t r, int32_t m, int64_t *lo, int64_t *hi) {
+    const int64_t nn = m / 3, node = std::min<int64_t>((int64_t)r / 3, std::max<int64_t>(nn - 1, 0));
+    *lo = std::max<int64_t>(0, node - kBandNodes);
+    *hi = std::min<int64_t>(nn, node + kBandNodes + 1);
+}
 inline int32_t skew_len(int32_t r, int32_t m, uint64_t seed) {
-    const uint64_t u = rnd(seed, 1, (uint64_t)r);
-    int64_t L;
-    if (u % 10000 == 0) {  // hub row: log-uniform 1e3 .. 2e5
-        L = (int64_t)(1000.0 * std::pow(200.0, unit(rnd(seed, 2, (uint64_t)r))));
+    if (skew_is_hub(r, seed)) {
+        const int64_t L = (int64_t)(1000.0 * std::pow(200.0, unit(rnd(seed, 2, (uint64_t)r))));
         return (int32_t)std::min<int64_t>(L, m);
     }
-    L = 45 + (int64_t)((u >> 20) % 55);  // 45..99, mean 72 (Flan_1565: 114.2M / 1.565M)
-    const int64_t lo = std::max<int64_t>(0, (int64_t)r - kBand);
-    const int64_t hi = std::min<int64_t>(m, (int64_t)r + kBand + 1);
-    return (int32_t)std::min<int64_t>(L, hi - lo);
+    int64_t lo, hi;
+    skew_band(r, m, &lo, &hi);
+    const int64_t nodes = 15 + (int64_t)((rnd(seed, 1, (uint64_t)r) >> 20) % 19);
+    return (int32_t)(3 * std::min<int64_t>(nodes, hi - lo));
 }
 
 }  // namespace
@@ -204,17 +212,28 @@ int aijhip_skewed_csr(int32_t m, uint64_t seed, int64_t *nnz, int32_t *ai, int32
     ai[0] = 0;
     for (int32_t r = 0; r < m; ++r) {
         const int32_t L = skew_len(r, m, seed);
-        const bool hub = L > 99;
-        const int64_t lo = hub ? 0 : std::max<int64_t>(0, (int64_t)r - kBand);
-        const int64_t hi = hub ? m : std::min<int64_t>(m, (int64_t)r + kBand + 1);
-        const int64_t W = hi - lo;
-        // one distinct column per bucket [q*W/L, (q+1)*W/L): sorted, unique
-        for (int32_t q = 0; q < L; ++q) {
-            const int64_t b0 = lo + (int64_t)q * W / L, b1 = lo + (int64_t)(q + 1) * W / L;
-            const uint64_t u = rnd(seed, 4, (uint64_t)p);
-            aj[p] = (int32_t)(b0 + (int64_t)(u % (uint64_t)(b1 - b0)));
-            aa[p] = 2.0 * unit(rnd(seed, 3, (uint64_t)p)) - 1.0;
-            ++p;
+        if (skew_is_hub(r, seed)) {
+            // one distinct column per bucket [q*m/L, (q+1)*m/L): sorted, unique
+            for (int32_t q = 0; q < L; ++q) {
+                const int64_t b0 = (int64_t)q * m / L, b1 = (int64_t)(q + 1) * m / L;
+                aj[p] = (int32_t)(b0 + (int64_t)(rnd(seed, 4, (uint64_t)p) % (uint64_t)(b1 - b0)));
+                aa[p] = 2.0 * unit(rnd(seed, 3, (uint64_t)p)) - 1.0;
+                ++p;
+            }
+        } else {
+            int64_t lo, hi;
+            skew_band(r, m, &lo, &hi);
+            const int64_t W = hi - lo, nodes = L / 3;
+            // one node per bucket of the node band, its 3 dofs consecutive
+            for (int64_t q = 0; q < nodes; ++q) {
+                const int64_t b0 = lo + q * W / nodes, b1 = lo + (q + 1) * W / nodes;
+                const int64_t node = b0 + (int64_t)(rnd(seed, 4, (uint64_t)p) % (uint64_t)(b1 - b0));
+                for (int d = 0; d < 3; ++d) {
+                    aj[p] = (int32_t)(3 * node + d);
+                    aa[p] = 2.0 * unit(rnd(seed, 3, (uint64_t)p)) - 1.0;
+                    ++p;
+                }
+            }
         }
         ai[r + 1] = (int32_t)p;
     }

@@ -57,8 +57,10 @@ def check(y_gpu, y_ref, ai, aj, aa, x, exact, z=None):
     assert np.max(err) / scale <= 1e-14
 
 
-def mult(pkg, dev, ai, aj, aa, n, x, kernel, lanes=0):
-    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, kernel=kernel, lanes=lanes) as A:
+def mult(pkg, dev, ai, aj, aa, n, x, kernel, lanes=0, **opts):
+    if kernel == "stream" and not opts:
+        opts = {"exact": 1}  # bit-exact mode; default mode is checked separately
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, kernel=kernel, lanes=lanes, **opts) as A:
         xd = to_dev(x, dev)
         yd = torch.full((len(ai) - 1,), np.nan, dtype=torch.float64, device=dev)
         A.mult(xd, yd)
@@ -81,11 +83,24 @@ def test_mult_golden(pkg, dev, name, kernel):
 
 
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_stream_default_mode(pkg, dev, name):
+    """Default STREAM (long-row blocks reduced by several lanes per row):
+    within the fp64 bound everywhere, bit-exact on short-row blocks."""
+    g = golden(name)
+    ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
+    y, info = mult(pkg, dev, ai, aj, aa, n, g["x"], "stream", exact=0)
+    assert info["exact"] == 0
+    check(y, g["y"], ai, aj, aa, g["x"], exact=False)
+    if name.startswith("poisson"):
+        assert_bits(y, g["y"])
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
 @pytest.mark.parametrize("kernel", ALL_KERNELS)
 def test_mult_add_golden(pkg, dev, name, kernel):
     g = golden(name)
     ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
-    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, kernel=kernel) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, kernel=kernel, **({"exact": 1} if kernel == "stream" else {})) as A:
         xd, zd = to_dev(g["x"], dev), to_dev(g["z"], dev)
         wd = torch.empty_like(zd)
         A.mult_add(xd, zd, wd)
@@ -100,7 +115,7 @@ def test_mult_add_golden(pkg, dev, name, kernel):
 def test_mult_transpose_golden(pkg, dev, name):
     g = golden(name)
     ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
-    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, exact=1) as A:
         yd = torch.empty(n, dtype=torch.float64, device=dev)
         A.mult_transpose(to_dev(g["xt"], dev), yd)
         torch.cuda.synchronize()
@@ -149,7 +164,7 @@ def test_update_values_and_assembly_end(pkg, dev, coracle):
     g = golden("poisson8")
     ai, aj, aa = g["ai"], g["aj"], g["aa"]
     x = g["x"]
-    A = pkg.SeqAIJHIP(ai, aj, aa)
+    A = pkg.SeqAIJHIP(ai, aj, aa, exact=1)
     xd = to_dev(x, dev)
     yd = torch.empty_like(xd)
     aa2 = aa * 3.0 - 1.0
@@ -240,6 +255,8 @@ def test_skewed_flan_standin_all_kernels(pkg, dev, coracle):
         if kernel in BITEXACT:
             short = np.diff(ai) <= 2048
             assert_bits(y, ref, short)
+    y, info = mult(pkg, dev, ai, aj, aa, len(ai) - 1, x, "stream", exact=0)  # default mode
+    check(y, ref, ai, aj, aa, x, exact=False)
 
 
 @pytest.mark.parametrize("name", ["poisson16", "skewed_small", "compressed_small"])
@@ -262,6 +279,7 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
                     A.set_option("nt_loads", nt)
                     A.set_option("persistent", persist)
                     A.set_option("clamped", clamped)
+                    A.set_option("exact", 1)
                     A.mult(xd, yd)
                     torch.cuda.synchronize()
                     y = yd.cpu().numpy()

@@ -74,6 +74,11 @@ def main():
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=p, clamped=0)))
     if args.variants in ("kernels", "all"):
         variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
+    if args.variants == "skewed":
+        for g in (0, 1, 4, 6, 7, 8):
+            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=0)))
+        variants += [("vector", {"lanes": 16}), ("vector", {"lanes": 32}), ("vector", {"lanes": 64}),
+                     ("merge", {}), ("scalar", {})]
 
     def configure(kind, opts):
         A.set_kernel(kind, opts.get("lanes", 0))
