@@ -132,7 +132,8 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
  * setting. Re-plans on the device. */
 enum {
     AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..8: lanes / LDS entries / rows per block
-                                       (DESIGN.md §Kernels); default 6      */
+                                       (DESIGN.md §Kernels); -1 (default):
+                                       6 for short rows, 1 for long rows    */
     AIJHIP_OPT_XCD_REMAP = 2,       /* 0 (default): hardware round-robin;
                                        1: each XCD gets a contiguous run of
                                        row blocks; C >= 2: chunks of C blocks,

@@ -202,6 +202,13 @@ int plan_build(aijhip_mat *A) {
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
     P.tune = A->requested_tune;
+    if (P.tune.geom < 0) {
+        // measured: 512 x 4094-entry blocks for short rows (7-pt Poisson,
+        // profiles/r01/tune04), 512 x 4096 / 512 rows for long rows (Flan
+        // stand-in, profiles/r01/skew2)
+        const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
+        P.tune.geom = (nr > 0 && A->nz > (int64_t)aijhip::kSplitMinMean * nr) ? 1 : 6;
+    }
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM:
             return plan_stream(A);
@@ -402,7 +409,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
     aijhip::Tuning t = A->requested_tune;
     switch (option) {
         case AIJHIP_OPT_STREAM_GEOMETRY:
-            if (value < 0 || value >= aijhip::kNumStreamGeoms) return fail(AIJHIP_ERR_ARG, "bad geometry");
+            if (value < -1 || value >= aijhip::kNumStreamGeoms) return fail(AIJHIP_ERR_ARG, "bad geometry");
             t.geom = value;
             break;
         case AIJHIP_OPT_XCD_REMAP:

@@ -73,7 +73,7 @@ struct RowList {
 // (XCD-contiguous runs were 5-10 % slower), plain loads (non-temporal 2-3 %
 // slower), non-persistent grid (the pipelined persistent form was 7 % slower).
 struct Tuning {
-    int geom = 6;        // index into kStreamGeoms
+    int geom = -1;       // index into kStreamGeoms; -1 = by row statistics (6 or 1)
     bool xcd = false;    // XCD-aware block remap
     int xchunk = 0;      //   chunk of the chunked remap (0 = contiguous runs)
     bool nt = false;     // non-temporal matrix loads
