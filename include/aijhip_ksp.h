@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "aijhip.h"
+#include "aijhip_gamg.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -28,8 +29,11 @@ extern "C" {
 typedef struct aijhip_ksp *aijhip_ksp_t;
 
 /* PCType: PCNONE, PCJACOBI (= bjacobi + jacobi sub-PC on one rank,
- * PETSc_SolverOptions_GAMG.info:16-21). */
-enum { AIJHIP_PC_NONE = 0, AIJHIP_PC_JACOBI = 1 };
+ * PETSc_SolverOptions_GAMG.info:16-21), PCGAMG (agg, one V-cycle per
+ * application: Richardson(1) + Jacobi smoothing down and up on every level,
+ * preonly + Jacobi on the coarsest — PETSc_SolverOptions_GAMG.info:6-21;
+ * hierarchy from include/aijhip_gamg.h). */
+enum { AIJHIP_PC_NONE = 0, AIJHIP_PC_JACOBI = 1, AIJHIP_PC_GAMG = 2 };
 
 /* KSPNormType values as in PETSc. */
 enum {
@@ -75,6 +79,13 @@ int aijhip_ksp_get_residual_history(aijhip_ksp_t ksp, double *hist, int32_t na, 
 /* Fused kernels used per iteration (1 = SpMV with the p.Ap dot in its
  * epilogue), for reporting. */
 int aijhip_ksp_get_fused(aijhip_ksp_t ksp, int *fused);
+/* GAMG options (before set-up); NULL = PETSc defaults
+ * (aijhip_gamg_params_default). */
+int aijhip_ksp_set_gamg_params(aijhip_ksp_t ksp, const aijhip_gamg_params_t *p);
+/* Multigrid levels of the set-up PC (1 for non-GAMG): rows and operator nnz
+ * per level (finest first; up to cap entries), and the host set-up time. */
+int aijhip_ksp_get_pc_levels(aijhip_ksp_t ksp, int32_t *nlevels, int32_t *rows, int64_t *nnz,
+                             int32_t cap, double *setup_seconds);
 int aijhip_ksp_destroy(aijhip_ksp_t ksp);
 
 #ifdef __cplusplus

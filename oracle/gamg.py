@@ -1,0 +1,152 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+numpy/scipy restatement of the smoothed-aggregation hierarchy of
+include/aijhip_gamg.h (PETSc 3.7.6 PCGAMG agg [ext], as configured by
+/root/reference/configs/PETSc_SolverOptions_GAMG.info:6-21) and of the
+multiplicative V-cycle PCMG applies with those options (Richardson(1) +
+Jacobi smoothing on every level, preonly + Jacobi on the coarsest).
+
+Parity unpinned w.r.t. PETSc (absent; its MIS aggregation order is not
+reproduced). This restatement pins the product's C++ set-up and device
+V-cycle: aggregates identical, operators to rounding.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import scipy.sparse as sp
+
+
+def first_diagonal(A: sp.csr_matrix) -> np.ndarray:
+    """MatGetDiagonal: first stored diagonal entry per row (0 if none)."""
+    d = np.zeros(A.shape[0])
+    for i in range(A.shape[0]):
+        for k in range(A.indptr[i], A.indptr[i + 1]):
+            if A.indices[k] == i:
+                d[i] = A.data[k]
+                break
+    return d
+
+
+def strength_graph(A, d, theta):
+    rows = np.repeat(np.arange(A.shape[0]), np.diff(A.indptr))
+    cols = A.indices
+    v = np.abs(A.data)
+    keep = (rows != cols) & (v > theta * np.sqrt(np.abs(d[rows] * d[cols])))
+    S = sp.csr_matrix((np.ones(keep.sum()), (rows[keep], cols[keep])), shape=A.shape)
+    S = ((S + S.T) != 0).astype(np.int8).tocsr()
+    S.sort_indices()
+    return S
+
+
+def aggregate(A, S):
+    m = A.shape[0]
+    agg = -np.ones(m, dtype=np.int64)
+    na = 0
+    for i in range(m):
+        nb = S.indices[S.indptr[i]:S.indptr[i + 1]]
+        if agg[i] != -1 or len(nb) == 0:
+            continue
+        if np.all(agg[nb] == -1):
+            agg[i] = na
+            agg[nb] = na
+            na += 1
+    phase1 = agg.copy()
+    for i in range(m):
+        if phase1[i] != -1:
+            continue
+        nbset = set(S.indices[S.indptr[i]:S.indptr[i + 1]].tolist())
+        best, bv = -1, -1.0
+        for k in range(A.indptr[i], A.indptr[i + 1]):
+            j = A.indices[k]
+            if j == i or phase1[j] == -1 or j not in nbset:
+                continue
+            v = abs(A.data[k])
+            if v > bv or (v == bv and j < best):
+                bv, best = v, j
+        if best >= 0:
+            agg[i] = phase1[best]
+    for i in range(m):
+        if agg[i] != -1:
+            continue
+        agg[i] = na
+        for j in S.indices[S.indptr[i]:S.indptr[i + 1]]:
+            if agg[j] == -1:
+                agg[j] = na
+        na += 1
+    return agg, na
+
+
+def _mix64(z):
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9 & 0xFFFFFFFFFFFFFFFF
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EB & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+def estimate_emax(A, dinv, its):
+    """Power iteration on D^-1 A from the same counter-based start."""
+    m = A.shape[0]
+    v = np.array([2.0 * ((_mix64((0x5EED + (i + 1) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF) >> 11)
+                         * (1.0 / 9007199254740992.0)) - 1.0 for i in range(m)])
+    v /= math.sqrt(float(np.dot(v, v)))
+    lam = 1.0
+    for _ in range(its):
+        w = dinv * (A @ v)
+        nw = math.sqrt(float(np.dot(w, w)))
+        if not nw > 0.0:
+            break
+        lam = nw
+        v = w / nw
+    return lam
+
+
+def build(A, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smooth_scale=1.4, eig_its=10):
+    """Returns a list of levels: dict(A, P, agg, emax) (P/agg absent on the coarsest)."""
+    A = sp.csr_matrix(A)
+    levels = []
+    B = np.ones(A.shape[0])
+    while len(levels) + 1 < max_levels and A.shape[0] > coarse_eq_limit:
+        d = first_diagonal(A)
+        dinv = 1.0 / np.where(d == 0.0, 1.0, d)
+        S = strength_graph(A, d, threshold)
+        agg, na = aggregate(A, S)
+        if na >= A.shape[0] or na == 0:
+            break
+        emax = estimate_emax(A, dinv, eig_its) if nsmooths > 0 else 1.0
+        Bc = np.sqrt(np.bincount(agg, weights=B * B, minlength=na))
+        p0 = np.where(Bc[agg] > 0, B / np.where(Bc[agg] > 0, Bc[agg], 1.0), 0.0)
+        P0 = sp.csr_matrix((p0, (np.arange(A.shape[0]), agg)), shape=(A.shape[0], na))
+        P = P0
+        if nsmooths > 0:
+            T = A @ P0
+            P = (-smooth_scale / emax) * (sp.diags(dinv) @ T) + P0
+        P = sp.csr_matrix(P)
+        Ac = sp.csr_matrix(P.T @ (A @ P))
+        levels.append(dict(A=A, P=P, agg=agg, emax=emax))
+        A, B = Ac, Bc
+    levels.append(dict(A=A))
+    return levels
+
+
+def vcycle(levels, b):
+    """PCApply_MG, multiplicative V-cycle: Richardson(1)+Jacobi down (zero
+    guess) and up (nonzero guess), P^T restriction, P interpolation, coarse
+    preonly + Jacobi."""
+    dinvs = []
+    for L in levels:
+        d = first_diagonal(L["A"])
+        dinvs.append(1.0 / np.where(d == 0.0, 1.0, d))
+
+    def cycle(l, bl):
+        A, dinv = levels[l]["A"], dinvs[l]
+        x = dinv * bl
+        if l == len(levels) - 1:
+            return x
+        r = bl - A @ x
+        xc = cycle(l + 1, levels[l]["P"].T @ r)
+        x = x + levels[l]["P"] @ xc
+        x = x + dinv * (bl - A @ x)
+        return x
+
+    return cycle(0, np.asarray(b, dtype=np.float64))

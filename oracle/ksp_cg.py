@@ -41,8 +41,11 @@ def cg(ai, aj, aa, b, x0=None, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc
        norm="preconditioned", matmult=None):
     """Returns (x, its, reason, history)."""
     mm = matmult or (lambda v: seqaij.matmult(ai, aj, aa, v))
-    dinv = jacobi_inverse(ai, aj, aa) if pc == "jacobi" else None
-    apply_pc = (lambda r: dinv * r) if dinv is not None else (lambda r: r.copy())
+    if callable(pc):  # e.g. oracle.gamg.vcycle bound to a hierarchy
+        apply_pc = pc
+    else:
+        dinv = jacobi_inverse(ai, aj, aa) if pc == "jacobi" else None
+        apply_pc = (lambda r: dinv * r) if dinv is not None else (lambda r: r.copy())
     guess_zero = x0 is None
     x = np.zeros_like(b) if guess_zero else x0.copy()
     r = b.copy() if guess_zero else b - mm(x)

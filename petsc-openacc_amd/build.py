@@ -24,7 +24,7 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
 HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "dist.hip", "ksp.hip"]
-HOST_SOURCES = ["harness.cpp"]
+HOST_SOURCES = ["harness.cpp", "gamg_setup.cpp"]
 ARCH = os.environ.get("AIJHIP_ARCH", "gfx950")
 
 
@@ -62,14 +62,14 @@ def build_lib(force: bool = False) -> Path:
     for s in srcs:
         o = objdir / (s.stem + ".o")
         if s.name in HOST_SOURCES:
-            cmd = ["g++", *common, "-c", str(s), "-o", str(o)]
+            cmd = ["g++", *common, "-fopenmp", "-c", str(s), "-o", str(o)]
         else:
             cmd = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", *common, "-c", str(s), "-o", str(o)]
         if force or _stale(o, [s, *CSRC.glob("*.h"), *(ROOT / "include").glob("*.h")]):
             _run(cmd)
         objs.append(str(o))
     tmp = LIB.with_suffix(".so.tmp")
-    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs])
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs, "-lgomp"])
     os.replace(tmp, LIB)
     return LIB
 

@@ -1,0 +1,430 @@
+// gamg_setup.cpp — host construction of the smoothed-aggregation hierarchy
+// (include/aijhip_gamg.h). Set-up only: the solve-phase V-cycle runs on the
+// device (ksp.hip). OpenMP over rows where the work is row-parallel; every
+// floating-point sum is accumulated in a fixed (row-traversal) order, so the
+// result does not depend on the thread count, and equals a scipy CSR
+// restatement (oracle/gamg.py) bit for bit.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <stdexcept>
+#include <vector>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "aijhip.h"
+#include "aijhip_gamg.h"
+
+namespace {
+
+struct CSR {
+    int32_t m = 0, n = 0;
+    std::vector<int32_t> ai, aj;
+    std::vector<double> aa;
+    int64_t nnz() const { return ai.empty() ? 0 : ai[m]; }
+};
+
+// Read-only view of a CSR (the caller's level-0 arrays or a stored level).
+struct View {
+    int32_t m, n;
+    const int32_t *ai, *aj;
+    const double *aa;
+};
+
+View view(const CSR &c) { return View{c.m, c.n, c.ai.data(), c.aj.data(), c.aa.data()}; }
+
+int nthreads(int req) {
+#ifdef _OPENMP
+    return req > 0 ? req : omp_get_max_threads();
+#else
+    (void)req;
+    return 1;
+#endif
+}
+
+// First stored diagonal entry of each row (0 if none) — MatGetDiagonal.
+std::vector<double> diagonal(const View &A) {
+    std::vector<double> d(A.m, 0.0);
+    for (int32_t i = 0; i < A.m; ++i)
+        for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k)
+            if (A.aj[k] == i) { d[i] = A.aa[k]; break; }
+    return d;
+}
+
+// Symmetric strength graph: j != i with |a_ij| > theta * sqrt(|a_ii a_jj|),
+// united with its transpose; rows sorted, unique.
+void strength_graph(const View &A, const std::vector<double> &d, double theta,
+                    std::vector<int32_t> &si, std::vector<int32_t> &sj) {
+    const int32_t m = A.m;
+    auto strong = [&](int32_t i, int32_t k) {
+        const int32_t j = A.aj[k];
+        if (j == i) return false;
+        const double v = std::fabs(A.aa[k]);
+        return v > theta * std::sqrt(std::fabs(d[i] * d[j]));
+    };
+    std::vector<int32_t> cnt(m + 1, 0);
+    for (int32_t i = 0; i < m; ++i)
+        for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k)
+            if (strong(i, k)) { ++cnt[i + 1]; ++cnt[A.aj[k] + 1]; }
+    std::vector<int32_t> off(m + 1, 0);
+    for (int32_t i = 0; i < m; ++i) off[i + 1] = off[i] + cnt[i + 1];
+    std::vector<int32_t> tmp(off[m]);
+    std::vector<int32_t> pos(off.begin(), off.end() - 1);
+    for (int32_t i = 0; i < m; ++i)
+        for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k)
+            if (strong(i, k)) { tmp[pos[i]++] = A.aj[k]; tmp[pos[A.aj[k]]++] = i; }
+    si.assign(m + 1, 0);
+    sj.clear();
+    sj.reserve(off[m]);
+    for (int32_t i = 0; i < m; ++i) {
+        auto b = tmp.begin() + off[i], e = tmp.begin() + off[i + 1];
+        std::sort(b, e);
+        e = std::unique(b, e);
+        sj.insert(sj.end(), b, e);
+        si[i + 1] = (int32_t)sj.size();
+    }
+}
+
+// Greedy aggregation in natural order (Vanek et al.): (1) a free node whose
+// strong neighbours are all free roots an aggregate with them; (2) a free
+// node joins the phase-1 aggregate of its strongest phase-1 neighbour
+// (lowest index on ties); (3) what is left roots aggregates with its free
+// neighbours. Isolated nodes are singletons.
+int32_t aggregate(const View &A, const std::vector<int32_t> &si, const std::vector<int32_t> &sj,
+                  std::vector<int32_t> &agg) {
+    const int32_t m = A.m;
+    agg.assign(m, -1);
+    int32_t na = 0;
+    for (int32_t i = 0; i < m; ++i) {
+        if (agg[i] != -1 || si[i] == si[i + 1]) continue;
+        bool free_all = true;
+        for (int32_t k = si[i]; k < si[i + 1] && free_all; ++k) free_all = agg[sj[k]] == -1;
+        if (!free_all) continue;
+        agg[i] = na;
+        for (int32_t k = si[i]; k < si[i + 1]; ++k) agg[sj[k]] = na;
+        ++na;
+    }
+    const std::vector<int32_t> phase1 = agg;
+    for (int32_t i = 0; i < m; ++i) {
+        if (phase1[i] != -1) continue;
+        int32_t best = -1;
+        double bv = -1.0;
+        for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) {
+            const int32_t j = A.aj[k];
+            if (j == i || phase1[j] == -1) continue;
+            if (!std::binary_search(sj.begin() + si[i], sj.begin() + si[i + 1], j)) continue;
+            const double v = std::fabs(A.aa[k]);
+            if (v > bv || (v == bv && j < best)) { bv = v; best = j; }
+        }
+        if (best >= 0) agg[i] = phase1[best];
+    }
+    for (int32_t i = 0; i < m; ++i) {
+        if (agg[i] != -1) continue;
+        agg[i] = na;
+        for (int32_t k = si[i]; k < si[i + 1]; ++k)
+            if (agg[sj[k]] == -1) agg[sj[k]] = na;
+        ++na;
+    }
+    return na;
+}
+
+uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// y = D^-1 A x (row-parallel, each row summed in storage order)
+void dinv_apply(const View &A, const std::vector<double> &dinv, const std::vector<double> &x,
+                std::vector<double> &y, int nt) {
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int32_t i = 0; i < A.m; ++i) {
+        double s = 0.0;
+        for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) s += A.aa[k] * x[A.aj[k]];
+        y[i] = dinv[i] * s;
+    }
+}
+
+double dot(const std::vector<double> &a, const std::vector<double> &b) {
+    double s = 0.0;
+    for (size_t i = 0; i < a.size(); ++i) s += a[i] * b[i];
+    return s;
+}
+
+// emax(D^-1 A) by power iteration from a counter-based random start.
+double estimate_emax(const View &A, const std::vector<double> &dinv, int its, int nt) {
+    const int32_t m = A.m;
+    if (m == 0) return 1.0;
+    std::vector<double> v(m), w(m);
+    for (int32_t i = 0; i < m; ++i)
+        v[i] = 2.0 * ((double)(mix64(0x5EEDULL + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL) >> 11) *
+                      (1.0 / 9007199254740992.0)) - 1.0;
+    double nv = std::sqrt(dot(v, v));
+    for (int32_t i = 0; i < m; ++i) v[i] /= nv;
+    double lam = 1.0;
+    for (int it = 0; it < its; ++it) {
+        dinv_apply(A, dinv, v, w, nt);
+        const double nw = std::sqrt(dot(w, w));
+        if (!(nw > 0.0)) break;
+        lam = nw;
+        for (int32_t i = 0; i < m; ++i) v[i] = w[i] / nw;
+    }
+    return lam;
+}
+
+// C = A * B (CSR x CSR). Row-parallel; per row, each product is added into
+// its column's accumulator in (A entry, B entry) traversal order starting
+// from 0.0 (the order of scipy's csr_matmat), then columns sorted.
+void spgemm(const View &A, const View &B, CSR &C, int nt) {
+    const int32_t m = A.m, n = B.n;
+    C.m = m;
+    C.n = n;
+    C.ai.assign((size_t)m + 1, 0);
+    std::vector<int32_t> cnt(m, 0);
+#pragma omp parallel num_threads(nt)
+    {
+        std::vector<int32_t> mark(n, -1);
+#pragma omp for schedule(dynamic, 4096)
+        for (int32_t i = 0; i < m; ++i) {
+            int32_t c = 0;
+            for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) {
+                const int32_t j = A.aj[k];
+                for (int32_t q = B.ai[j]; q < B.ai[j + 1]; ++q)
+                    if (mark[B.aj[q]] != i) { mark[B.aj[q]] = i; ++c; }
+            }
+            cnt[i] = c;
+        }
+    }
+    int64_t total = 0;
+    for (int32_t i = 0; i < m; ++i) total += cnt[i];
+    if (total > INT32_MAX) throw std::length_error("spgemm: product exceeds int32 indices");
+    for (int32_t i = 0; i < m; ++i) C.ai[i + 1] = C.ai[i] + cnt[i];
+    C.aj.resize(C.ai[m]);
+    C.aa.resize(C.ai[m]);
+#pragma omp parallel num_threads(nt)
+    {
+        std::vector<int32_t> mark(n, -1);
+        std::vector<double> acc(n, 0.0);
+        std::vector<int32_t> cols;
+#pragma omp for schedule(dynamic, 4096)
+        for (int32_t i = 0; i < m; ++i) {
+            cols.clear();
+            for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) {
+                const int32_t j = A.aj[k];
+                const double a = A.aa[k];
+                for (int32_t q = B.ai[j]; q < B.ai[j + 1]; ++q) {
+                    const int32_t c = B.aj[q];
+                    if (mark[c] != i) { mark[c] = i; acc[c] = 0.0; cols.push_back(c); }
+                    acc[c] += a * B.aa[q];
+                }
+            }
+            std::sort(cols.begin(), cols.end());
+            int64_t p = C.ai[i];
+            for (int32_t c : cols) { C.aj[p] = c; C.aa[p] = acc[c]; ++p; }
+        }
+    }
+}
+
+// Transpose (counting sort: each output row lists input rows ascending).
+void transpose(const View &A, CSR &T) {
+    T.m = A.n;
+    T.n = A.m;
+    T.ai.assign((size_t)A.n + 1, 0);
+    const int64_t nz = A.ai[A.m];
+    for (int64_t k = 0; k < nz; ++k) ++T.ai[A.aj[k] + 1];
+    for (int32_t c = 0; c < A.n; ++c) T.ai[c + 1] += T.ai[c];
+    T.aj.resize(nz);
+    T.aa.resize(nz);
+    std::vector<int32_t> pos(T.ai.begin(), T.ai.end() - 1);
+    for (int32_t i = 0; i < A.m; ++i)
+        for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) {
+            const int32_t p = pos[A.aj[k]]++;
+            T.aj[p] = i;
+            T.aa[p] = A.aa[k];
+        }
+}
+
+// Smoothed prolongator P = alpha * (D^-1 A P0) + P0, alpha = -scale/emax,
+// with P0(i, agg[i]) = B_i / |B restricted to agg[i]| (QR of the near-null
+// space per aggregate); returns the coarse near-null space |B|_agg.
+void prolongator(const View &A, const std::vector<double> &dinv, const std::vector<int32_t> &agg,
+                 int32_t na, const std::vector<double> &B, double alpha, int nsmooths, CSR &P,
+                 std::vector<double> &Bc, int nt) {
+    const int32_t m = A.m;
+    Bc.assign(na, 0.0);
+    for (int32_t i = 0; i < m; ++i) Bc[agg[i]] += B[i] * B[i];
+    for (int32_t a = 0; a < na; ++a) Bc[a] = std::sqrt(Bc[a]);
+    CSR P0;
+    P0.m = m;
+    P0.n = na;
+    P0.ai.resize((size_t)m + 1);
+    P0.aj.resize(m);
+    P0.aa.resize(m);
+    for (int32_t i = 0; i < m; ++i) {
+        P0.ai[i] = i;
+        P0.aj[i] = agg[i];
+        P0.aa[i] = Bc[agg[i]] > 0.0 ? B[i] / Bc[agg[i]] : 0.0;
+    }
+    P0.ai[m] = m;
+    if (nsmooths <= 0) { P = std::move(P0); return; }
+    CSR T;
+    spgemm(A, view(P0), T, nt);
+    // P = alpha * (dinv_i * T_ic) + P0_ic on the union pattern (P0's column
+    // agg[i] is in T's row whenever a_ii is stored)
+    P.m = m;
+    P.n = na;
+    P.ai.assign((size_t)m + 1, 0);
+    for (int32_t i = 0; i < m; ++i) {
+        const bool has = std::binary_search(T.aj.begin() + T.ai[i], T.aj.begin() + T.ai[i + 1], agg[i]);
+        P.ai[i + 1] = P.ai[i] + (T.ai[i + 1] - T.ai[i]) + (has ? 0 : 1);
+    }
+    P.aj.resize(P.ai[m]);
+    P.aa.resize(P.ai[m]);
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int32_t i = 0; i < m; ++i) {
+        int64_t p = P.ai[i];
+        bool placed = false;
+        const int32_t g = agg[i];
+        const double p0 = P0.aa[i];
+        for (int32_t k = T.ai[i]; k < T.ai[i + 1]; ++k) {
+            const int32_t c = T.aj[k];
+            if (!placed && g < c) { P.aj[p] = g; P.aa[p] = p0; ++p; placed = true; }
+            const double t = dinv[i] * T.aa[k];
+            P.aj[p] = c;
+            P.aa[p] = alpha * t + (c == g ? p0 : 0.0);
+            if (c == g) placed = true;
+            ++p;
+        }
+        if (!placed) { P.aj[p] = g; P.aa[p] = p0; }
+    }
+}
+
+}  // namespace
+
+struct aijhip_gamg_host {
+    std::vector<int32_t> m;          // rows per level
+    std::vector<int64_t> nnz_a;
+    std::vector<CSR> A;              // A[0] unused (the input); A[l], l >= 1
+    std::vector<CSR> P;              // P[l]: m[l] x m[l+1]
+    std::vector<std::vector<int32_t>> agg;
+    std::vector<double> emax;
+};
+
+extern "C" {
+
+int aijhip_gamg_params_default(aijhip_gamg_params_t *p) {
+    if (!p) return AIJHIP_ERR_ARG;
+    p->threshold = 0.0;
+    p->coarse_eq_limit = 50;
+    p->max_levels = 10;
+    p->nsmooths = 1;
+    p->smooth_scale = 1.4;
+    p->eig_its = 10;
+    p->threads = 0;
+    return AIJHIP_OK;
+}
+
+int aijhip_gamg_build_host(int32_t m, const int32_t *ai, const int32_t *aj, const double *aa,
+                           const aijhip_gamg_params_t *pp, aijhip_gamg_host_t *out) {
+    if (!out || m < 0 || !ai || (ai[m] > 0 && (!aj || !aa))) return AIJHIP_ERR_ARG;
+    *out = nullptr;
+    aijhip_gamg_params_t p;
+    aijhip_gamg_params_default(&p);
+    if (pp) p = *pp;
+    if (p.max_levels < 1) return AIJHIP_ERR_ARG;
+    const int nt = nthreads(p.threads);
+    aijhip_gamg_host *H = new (std::nothrow) aijhip_gamg_host();
+    if (!H) return AIJHIP_ERR_ALLOC;
+    try {
+        H->m.push_back(m);
+        H->nnz_a.push_back(ai[m]);
+        H->A.emplace_back();
+        std::vector<double> B(m, 1.0);  // near-null space of the scalar operator
+        View cur{m, m, ai, aj, aa};
+        while ((int32_t)H->m.size() < p.max_levels && cur.m > p.coarse_eq_limit) {
+            const std::vector<double> d = diagonal(cur);
+            std::vector<double> dinv(cur.m);
+            for (int32_t i = 0; i < cur.m; ++i) dinv[i] = 1.0 / (d[i] == 0.0 ? 1.0 : d[i]);
+            std::vector<int32_t> si, sj, agg;
+            strength_graph(cur, d, p.threshold, si, sj);
+            const int32_t na = aggregate(cur, si, sj, agg);
+            if (na >= cur.m || na == 0) break;  // no coarsening
+            const double emax = p.nsmooths > 0 ? estimate_emax(cur, dinv, p.eig_its, nt) : 1.0;
+            CSR P;
+            std::vector<double> Bc;
+            prolongator(cur, dinv, agg, na, B, -p.smooth_scale / emax, p.nsmooths, P, Bc, nt);
+            CSR AP, PT, Ac;
+            spgemm(cur, view(P), AP, nt);
+            transpose(view(P), PT);
+            spgemm(view(PT), view(AP), Ac, nt);
+            H->P.push_back(std::move(P));
+            H->agg.push_back(std::move(agg));
+            H->emax.push_back(emax);
+            H->m.push_back(Ac.m);
+            H->nnz_a.push_back(Ac.nnz());
+            H->A.push_back(std::move(Ac));
+            B.swap(Bc);
+            cur = view(H->A.back());
+        }
+    } catch (const std::bad_alloc &) {
+        delete H;
+        return AIJHIP_ERR_ALLOC;
+    } catch (const std::exception &) {
+        delete H;
+        return AIJHIP_ERR_ARG;
+    }
+    *out = H;
+    return AIJHIP_OK;
+}
+
+int aijhip_gamg_host_num_levels(aijhip_gamg_host_t h, int32_t *n) {
+    if (!h || !n) return AIJHIP_ERR_ARG;
+    *n = (int32_t)h->m.size();
+    return AIJHIP_OK;
+}
+
+int aijhip_gamg_host_level_info(aijhip_gamg_host_t h, int32_t l, int32_t *m, int64_t *nnz_a, int64_t *nnz_p,
+                                double *emax) {
+    if (!h || l < 0 || l >= (int32_t)h->m.size()) return AIJHIP_ERR_ARG;
+    if (m) *m = h->m[l];
+    if (nnz_a) *nnz_a = h->nnz_a[l];
+    const bool hasp = l < (int32_t)h->P.size();
+    if (nnz_p) *nnz_p = hasp ? h->P[l].nnz() : 0;
+    if (emax) *emax = hasp ? h->emax[l] : 0.0;
+    return AIJHIP_OK;
+}
+
+int aijhip_gamg_host_get_A(aijhip_gamg_host_t h, int32_t l, int32_t *ai, int32_t *aj, double *aa) {
+    if (!h || l < 1 || l >= (int32_t)h->m.size() || !ai) return AIJHIP_ERR_ARG;
+    const CSR &c = h->A[l];
+    std::copy(c.ai.begin(), c.ai.end(), ai);
+    if (aj) std::copy(c.aj.begin(), c.aj.end(), aj);
+    if (aa) std::copy(c.aa.begin(), c.aa.end(), aa);
+    return AIJHIP_OK;
+}
+
+int aijhip_gamg_host_get_P(aijhip_gamg_host_t h, int32_t l, int32_t *ai, int32_t *aj, double *aa) {
+    if (!h || l < 0 || l >= (int32_t)h->P.size() || !ai) return AIJHIP_ERR_ARG;
+    const CSR &c = h->P[l];
+    std::copy(c.ai.begin(), c.ai.end(), ai);
+    if (aj) std::copy(c.aj.begin(), c.aj.end(), aj);
+    if (aa) std::copy(c.aa.begin(), c.aa.end(), aa);
+    return AIJHIP_OK;
+}
+
+int aijhip_gamg_host_get_aggregates(aijhip_gamg_host_t h, int32_t l, int32_t *agg) {
+    if (!h || l < 0 || l >= (int32_t)h->agg.size() || !agg) return AIJHIP_ERR_ARG;
+    std::copy(h->agg[l].begin(), h->agg[l].end(), agg);
+    return AIJHIP_OK;
+}
+
+int aijhip_gamg_host_destroy(aijhip_gamg_host_t h) {
+    delete h;
+    return AIJHIP_OK;
+}
+
+}  // extern "C"

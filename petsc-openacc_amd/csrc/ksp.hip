@@ -2,29 +2,32 @@
 //
 // Restates PETSc 3.7.6 KSPSolve_CG [ext] (src/ksp/ksp/impls/cg/cg.c) with
 // KSPConvergedDefault [ext], as driven by /root/reference/src/main_ksp.cpp:92-103
-// (KSPCG, KSPSetReusePreconditioner) and the tolerances of
-// /root/reference/configs/PETSc_SolverOptions_GAMG.info:1-4. Per iteration:
+// (KSPCG, KSPSetReusePreconditioner) and the options of
+// /root/reference/configs/PETSc_SolverOptions_GAMG.info. Per iteration:
 //
 //   K1  P = Z            (i = 0)      | P = Z + b P        (VecCopy / VecAYPX)
 //   K2  W = A P, partials of P.W      (KSP_MatMult + VecXDot, fused into the
 //                                      STREAM SpMV epilogue when possible)
 //   K3  scalar step: dpi, indefinite-matrix check, a = beta / dpi
-//   K4  X += a P, R -= a W, Z = D^-1 R, partials of Z.Z, Z.R, R.R
-//                                     (2 x VecAXPY + PCApply_Jacobi + dots)
+//   K4  X += a P, R -= a W            (2 x VecAXPY), and for Jacobi / none
+//       also Z = D^-1 R with the partials of Z.Z, Z.R, R.R fused in
+//   [GAMG: Z = V-cycle(R), then the Z.Z, Z.R partials]
 //   K5  scalar step: dp, KSPConvergedDefault, beta, indefinite-PC / beta = 0
 //                    checks, b = beta / betaold
 //
 // W shares Z's storage as in PETSc (W = Z when not single-reduction). All
-// scalars live on the device; every kernel returns at once once the device
-// flag `done` is set, so the host launches iterations in batches and polls.
+// scalars live on the device; kernels return at once once the device flag
+// `done` is set, so the host launches iterations in batches and polls.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <new>
 #include <string>
 #include <vector>
 
+#include "aijhip_gamg.h"
 #include "aijhip_internal.h"
 #include "aijhip_ksp.h"
 
@@ -42,7 +45,7 @@ struct CGParams {
 
 constexpr int kVecThreads = 256;
 constexpr int kRedThreads = 1024;
-constexpr int kNQ = 4;  // partial quantities per vector block
+constexpr int kNQ = 4;  // partial quantities per vector block: zz, zr, rr, ss
 
 // Block sum in a fixed order (as block_sum in aijhip_kernels.hip).
 template <int T>
@@ -104,26 +107,34 @@ __global__ void k_diag_inv(int m, const int32_t *__restrict__ ai, const int32_t 
     dinv[r] = 1.0 / d;
 }
 
+#define GRID_STRIDE(i, n) \
+    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < (n); i += (int64_t)gridDim.x * kVecThreads)
+
 // Initial residual: r = b (zero guess) or r = b - A x (r holds A x on entry);
-// z = D^-1 r; partials Z.Z, Z.R, R.R and (nonzero guess) |D^-1 b|^2 or |b|^2.
+// Jacobi / none: z = D^-1 r; partials Z.Z, Z.R, R.R and (nonzero guess) the
+// norm of D^-1 b (or b). GAMG: z comes from the V-cycle afterwards.
 __global__ __launch_bounds__(kVecThreads) void k_init(int64_t n, const double *__restrict__ b,
                                                       double *r, double *z,
                                                       const double *__restrict__ dinv,
                                                       double *part, CGParams p) {
     __shared__ double scratch[kVecThreads / 64];
+    const bool jac = p.pc == AIJHIP_PC_JACOBI, gamg = p.pc == AIJHIP_PC_GAMG;
     double zz = 0.0, zr = 0.0, rr = 0.0, ss = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads) {
+    GRID_STRIDE(i, n) {
         const double bi = b[i];
-        const double ri = p.guess_zero ? bi : bi - r[i];  // VecAYPX(R,-1,B): r = b + (-1) r
-        const double di = p.pc ? dinv[i] : 1.0;
-        const double zi = p.pc ? di * ri : ri;
+        const double ri = p.guess_zero ? bi : bi + (-1.0) * r[i];  // VecAYPX(R,-1,B)
         r[i] = ri;
-        z[i] = zi;
-        zz += zi * zi;
-        zr += zi * ri;
         rr += ri * ri;
-        const double sb = (p.pc && p.normtype != AIJHIP_KSP_NORM_UNPRECONDITIONED) ? di * bi : bi;
-        ss += sb * sb;
+        if (!gamg) {
+            const double zi = jac ? dinv[i] * ri : ri;
+            z[i] = zi;
+            zz += zi * zi;
+            zr += zi * ri;
+            const double sb = (jac && p.normtype != AIJHIP_KSP_NORM_UNPRECONDITIONED) ? dinv[i] * bi : bi;
+            ss += sb * sb;
+        } else {
+            ss += bi * bi;  // GAMG preconditioned snorm: overwritten from V-cycle(b)
+        }
     }
     const int nb = gridDim.x;
     double v;
@@ -131,6 +142,27 @@ __global__ __launch_bounds__(kVecThreads) void k_init(int64_t n, const double *_
     v = bsum<kVecThreads>(zr, scratch); if (threadIdx.x == 0) part[1 * nb + blockIdx.x] = v;
     v = bsum<kVecThreads>(rr, scratch); if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = v;
     v = bsum<kVecThreads>(ss, scratch); if (threadIdx.x == 0) part[3 * nb + blockIdx.x] = v;
+}
+
+// partials of a.a into slot sa and a.c into slot sc (sc < 0: skip)
+__global__ __launch_bounds__(kVecThreads) void k_dots(int64_t n, const double *__restrict__ a,
+                                                      const double *__restrict__ c, double *part, int sa,
+                                                      int sc, const CGState *S) {
+    __shared__ double scratch[kVecThreads / 64];
+    if (S && S->done) return;
+    double aa = 0.0, ac = 0.0;
+    GRID_STRIDE(i, n) {
+        const double ai = a[i];
+        aa += ai * ai;
+        if (sc >= 0) ac += ai * c[i];
+    }
+    const int nb = gridDim.x;
+    double v = bsum<kVecThreads>(aa, scratch);
+    if (threadIdx.x == 0) part[sa * nb + blockIdx.x] = v;
+    if (sc >= 0) {
+        v = bsum<kVecThreads>(ac, scratch);
+        if (threadIdx.x == 0) part[sc * nb + blockIdx.x] = v;
+    }
 }
 
 __global__ __launch_bounds__(kRedThreads) void k_reduce_init(const double *part, int nb, CGState *S,
@@ -150,8 +182,8 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_init(const double *part,
     s.i = 0;
     if (!s.reason) {  // top of iteration 0
         s.its = 1;
-        if (s.beta == 0.0) s.reason = AIJHIP_KSP_CONVERGED_ATOL;
-        else if (p.max_it <= 0) { s.reason = AIJHIP_KSP_DIVERGED_ITS; s.its = 0; }
+        if (p.max_it <= 0) { s.reason = AIJHIP_KSP_DIVERGED_ITS; s.its = 0; }
+        else if (s.beta == 0.0) s.reason = AIJHIP_KSP_CONVERGED_ATOL;
     }
     s.b = 0.0;
     s.done = s.reason != 0;
@@ -164,8 +196,7 @@ __global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *_
     if (S->done) return;
     const bool first = S->i == 0;
     const double bb = S->b;
-    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads)
-        p[i] = first ? z[i] : z[i] + bb * p[i];
+    GRID_STRIDE(i, n) p[i] = first ? z[i] : z[i] + bb * p[i];
 }
 
 // Unfused dot partials of p . w (when the SpMV cannot carry the epilogue).
@@ -175,8 +206,7 @@ __global__ __launch_bounds__(kVecThreads) void k_dot(int64_t n, const double *__
     __shared__ double scratch[kVecThreads / 64];
     if (S->done) return;
     double s = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads)
-        s += p[i] * w[i];
+    GRID_STRIDE(i, n) s += p[i] * w[i];
     const double v = bsum<kVecThreads>(s, scratch);
     if (threadIdx.x == 0) part[blockIdx.x] = v;
 }
@@ -198,8 +228,9 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_dpi(const double *part, 
     S->a = S->beta / dpi;
 }
 
-// K4: X += a P; R -= a W; Z = D^-1 R (W and Z share storage: w[i] is read
-// before z[i] is written by the same lane); partials Z.Z, Z.R, R.R.
+// K4: X += a P; R -= a W; Jacobi / none: Z = D^-1 R (W and Z share storage:
+// w[i] is read before z[i] is written by the same lane); partials
+// Z.Z, Z.R, R.R (GAMG: R.R only, Z follows from the V-cycle).
 __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *x, const double *__restrict__ p,
                                                         double *r, double *wz,
                                                         const double *__restrict__ dinv, double *part,
@@ -208,20 +239,24 @@ __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *x, co
     if (S->done) return;
     const double a = S->a, na = -a;
     double zz = 0.0, zr = 0.0, rr = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kVecThreads) {
-        x[i] = x[i] + a * p[i];          // VecAXPY(X, a, P)
+    GRID_STRIDE(i, n) {
+        x[i] = x[i] + a * p[i];               // VecAXPY(X, a, P)
         const double ri = r[i] + na * wz[i];  // VecAXPY(R, -a, W)
-        const double zi = pc ? dinv[i] * ri : ri;  // PCApply_Jacobi: VecPointwiseMult
         r[i] = ri;
-        wz[i] = zi;
-        zz += zi * zi;
-        zr += zi * ri;
         rr += ri * ri;
+        if (pc != AIJHIP_PC_GAMG) {
+            const double zi = pc == AIJHIP_PC_JACOBI ? dinv[i] * ri : ri;  // PCApply_Jacobi
+            wz[i] = zi;
+            zz += zi * zi;
+            zr += zi * ri;
+        }
     }
     const int nb = gridDim.x;
     double v;
-    v = bsum<kVecThreads>(zz, scratch); if (threadIdx.x == 0) part[0 * nb + blockIdx.x] = v;
-    v = bsum<kVecThreads>(zr, scratch); if (threadIdx.x == 0) part[1 * nb + blockIdx.x] = v;
+    if (pc != AIJHIP_PC_GAMG) {
+        v = bsum<kVecThreads>(zz, scratch); if (threadIdx.x == 0) part[0 * nb + blockIdx.x] = v;
+        v = bsum<kVecThreads>(zr, scratch); if (threadIdx.x == 0) part[1 * nb + blockIdx.x] = v;
+    }
     v = bsum<kVecThreads>(rr, scratch); if (threadIdx.x == 0) part[2 * nb + blockIdx.x] = v;
 }
 
@@ -254,6 +289,26 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_iter(const double *part,
     *S = s;
 }
 
+// ------------------------------------------------------------- V-cycle
+// KSPSolve_Richardson with one iteration, scale 1, Jacobi PC [ext]:
+//   zero guess:     x = 0 + 1.0 * (D^-1 b)           = D^-1 b
+//   nonzero guess:  x = x + 1.0 * (D^-1 (b + (-1) A x))
+__global__ __launch_bounds__(kVecThreads) void k_jacobi(int64_t n, const double *__restrict__ dinv,
+                                                        const double *__restrict__ b, double *x) {
+    GRID_STRIDE(i, n) x[i] = dinv[i] * b[i];
+}
+
+// MatResidual: r = b + (-1) r, where r holds A x on entry (VecAYPX(r,-1,b)).
+__global__ __launch_bounds__(kVecThreads) void k_resid(int64_t n, const double *__restrict__ b, double *r) {
+    GRID_STRIDE(i, n) r[i] = b[i] + (-1.0) * r[i];
+}
+
+__global__ __launch_bounds__(kVecThreads) void k_richardson(int64_t n, const double *__restrict__ dinv,
+                                                            const double *__restrict__ b,
+                                                            const double *__restrict__ ax, double *x) {
+    GRID_STRIDE(i, n) x[i] = x[i] + 1.0 * (dinv[i] * (b[i] + (-1.0) * ax[i]));
+}
+
 int kfail(int code, const std::string &msg) {
     aijhip::set_error(msg);
     return code;
@@ -264,6 +319,15 @@ int khip(hipError_t e, const char *what) {
     return AIJHIP_ERR_HIP;
 }
 
+struct MGLevel {
+    aijhip_mat *A = nullptr;  // level 0: borrowed
+    aijhip_mat *P = nullptr;  // interpolation from level l+1 (owned)
+    bool own_A = false;
+    int32_t m = 0;
+    int64_t nnz = 0;
+    double *dinv = nullptr, *b = nullptr, *x = nullptr, *r = nullptr;
+};
+
 }  // namespace
 
 struct aijhip_ksp {
@@ -273,6 +337,7 @@ struct aijhip_ksp {
     bool guess_nonzero = false;
     double rtol = 1e-5, abstol = 1e-50, dtol = 1e5;
     int32_t max_it = 10000;
+    aijhip_gamg_params_t gamg;
     bool set_up = false;
     bool fused = false;
     int vec_grid = 0;
@@ -281,6 +346,8 @@ struct aijhip_ksp {
     int32_t hist_cap = 0;
     CGState *d_state = nullptr;
     CGState *h_state = nullptr;  // pinned
+    std::vector<MGLevel> mg;     // GAMG levels, finest first
+    double setup_seconds = 0.0;
     int32_t its = 0;
     int reason = 0;
     double rnorm = 0.0;
@@ -289,7 +356,17 @@ struct aijhip_ksp {
 
 namespace {
 
+void mg_free(aijhip_ksp *K) {
+    for (MGLevel &L : K->mg) {
+        if (L.own_A) aijhip_mat_destroy(L.A);
+        aijhip_mat_destroy(L.P);
+        hipFree(L.dinv); hipFree(L.b); hipFree(L.x); hipFree(L.r);
+    }
+    K->mg.clear();
+}
+
 void ksp_free(aijhip_ksp *K) {
+    mg_free(K);
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
     hipFree(K->d_hist); hipFree(K->d_state);
     if (K->h_state) hipHostFree(K->h_state);
@@ -308,6 +385,106 @@ struct KDeviceGuard {
     ~KDeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
 };
 
+dim3 vgrid(const aijhip_ksp *K, int64_t n) {
+    return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kVecThreads - 1) / kVecThreads,
+                                                                 (int64_t)K->A->n_cu * 8)));
+}
+
+// PCSetUp_GAMG: host hierarchy, device operators / interpolations / vectors.
+int gamg_setup(aijhip_ksp *K) {
+    aijhip_mat *A = K->A;
+    const int32_t m = A->m;
+    const int64_t nz = A->nz;
+    std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nz);
+    std::vector<double> aa((size_t)nz);
+    hipError_t e;
+    if ((e = hipMemcpy(ai.data(), A->d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (nz > 0 && ((e = hipMemcpy(aj.data(), A->d_aj, sizeof(int32_t) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess ||
+                    (e = hipMemcpy(aa.data(), A->d_aa, sizeof(double) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess)))
+        return khip(e, "GAMG: read operator");
+    aijhip_gamg_host_t H = nullptr;
+    int rc = aijhip_gamg_build_host(m, ai.data(), aj.data(), aa.data(), &K->gamg, &H);
+    if (rc) return kfail(rc, "GAMG: host hierarchy set-up failed");
+    ai.clear(); aj.clear(); aa.clear();
+    ai.shrink_to_fit(); aj.shrink_to_fit(); aa.shrink_to_fit();
+    int32_t nl = 0;
+    aijhip_gamg_host_num_levels(H, &nl);
+    K->mg.assign((size_t)nl, MGLevel());
+    rc = AIJHIP_OK;
+    for (int32_t l = 0; l < nl && !rc; ++l) {
+        MGLevel &L = K->mg[l];
+        int64_t nnz_a = 0, nnz_p = 0;
+        aijhip_gamg_host_level_info(H, l, &L.m, &nnz_a, &nnz_p, nullptr);
+        L.nnz = nnz_a;
+        std::vector<int32_t> xi, xj;
+        std::vector<double> xa;
+        if (l == 0) {
+            L.A = A;
+        } else {
+            xi.resize((size_t)L.m + 1); xj.resize((size_t)nnz_a); xa.resize((size_t)nnz_a);
+            aijhip_gamg_host_get_A(H, l, xi.data(), xj.data(), xa.data());
+            rc = aijhip_mat_create(A->device, L.m, L.m, nnz_a, xi.data(), xj.data(), xa.data(), &L.A);
+            L.own_A = rc == AIJHIP_OK;
+            if (rc) break;
+        }
+        if (l + 1 < nl) {
+            int32_t mc = 0;
+            aijhip_gamg_host_level_info(H, l + 1, &mc, nullptr, nullptr, nullptr);
+            xi.resize((size_t)L.m + 1); xj.resize((size_t)nnz_p); xa.resize((size_t)nnz_p);
+            aijhip_gamg_host_get_P(H, l, xi.data(), xj.data(), xa.data());
+            rc = aijhip_mat_create(A->device, L.m, mc, nnz_p, xi.data(), xj.data(), xa.data(), &L.P);
+            if (rc) break;
+        }
+        const size_t vb = sizeof(double) * (size_t)std::max<int32_t>(L.m, 1);
+        if ((e = hipMalloc(&L.dinv, vb)) != hipSuccess || (e = hipMalloc(&L.r, vb)) != hipSuccess ||
+            (l > 0 && ((e = hipMalloc(&L.b, vb)) != hipSuccess || (e = hipMalloc(&L.x, vb)) != hipSuccess))) {
+            rc = khip(e, "GAMG: level vectors");
+            break;
+        }
+        if (L.m > 0)
+            hipLaunchKernelGGL(k_diag_inv, dim3((unsigned)((L.m + 255) / 256)), dim3(256), 0, nullptr, L.m,
+                               L.A->d_ai, L.A->d_aj, L.A->d_aa, L.dinv);
+    }
+    aijhip_gamg_host_destroy(H);
+    if (rc) return rc;
+    // build every restriction (P^T) now, not inside the first solve
+    for (int32_t l = 0; l + 1 < nl; ++l) {
+        MGLevel &L = K->mg[l];
+        rc = aijhip_mat_mult_transpose(L.P, L.r, K->mg[l + 1].b, nullptr);
+        if (rc) return rc;
+    }
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return khip(e, "GAMG set-up");
+    return AIJHIP_OK;
+}
+
+// PCApply_MG (multiplicative, one V-cycle) on the finest-level input b,
+// output x.
+hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s) {
+    const int nl = (int)K->mg.size();
+    hipError_t e = hipSuccess;
+    auto B = [&](int l) { return l == 0 ? b0 : (const double *)K->mg[l].b; };
+    auto X = [&](int l) { return l == 0 ? x0 : K->mg[l].x; };
+    for (int l = 0; l < nl; ++l) {
+        MGLevel &L = K->mg[l];
+        const dim3 g = vgrid(K, L.m), t(kVecThreads);
+        hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));  // smoothd / coarse
+        if (l == nl - 1) break;
+        if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_resid, g, t, 0, s, (int64_t)L.m, B(l), L.r);
+        if ((e = aijhip::launch_mult(*L.P->transpose, L.r, nullptr, K->mg[l + 1].b, false, s)) != hipSuccess)
+            return e;  // MatRestrict = P^T r
+    }
+    for (int l = nl - 2; l >= 0; --l) {
+        MGLevel &L = K->mg[l];
+        const dim3 g = vgrid(K, L.m), t(kVecThreads);
+        // MatInterpolateAdd: x = x + P x_c
+        if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), X(l), true, s)) != hipSuccess) return e;
+        if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_richardson, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l));  // smoothu
+    }
+    return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -320,6 +497,7 @@ int aijhip_ksp_create(aijhip_mat_t A, aijhip_ksp_t *out) {
     aijhip_ksp *K = new (std::nothrow) aijhip_ksp();
     if (!K) return kfail(AIJHIP_ERR_ALLOC, "host allocation");
     K->A = A;
+    aijhip_gamg_params_default(&K->gamg);
     *out = K;
     return AIJHIP_OK;
 }
@@ -328,14 +506,35 @@ int aijhip_ksp_set_tolerances(aijhip_ksp_t K, double rtol, double abstol, double
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
     if (rtol < 0 || abstol < 0 || dtol <= 0 || max_it < 0) return kfail(AIJHIP_ERR_ARG, "bad tolerance");
     K->rtol = rtol; K->abstol = abstol; K->dtol = dtol;
-    if (max_it != K->max_it) { K->max_it = max_it; K->set_up = false; }
+    if (max_it != K->max_it) {
+        K->max_it = max_it;
+        if (K->set_up && K->hist_cap < max_it + 2) {  // regrow the history only
+            hipFree(K->d_hist);
+            K->d_hist = nullptr;
+            K->hist_cap = max_it + 2;
+            if (hipMalloc(&K->d_hist, sizeof(double) * (size_t)K->hist_cap) != hipSuccess) {
+                K->set_up = false;
+                return kfail(AIJHIP_ERR_ALLOC, "residual history");
+            }
+        }
+    }
     return AIJHIP_OK;
 }
 
 int aijhip_ksp_set_pc_type(aijhip_ksp_t K, int pc) {
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
-    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI) return kfail(AIJHIP_ERR_ARG, "unknown PC type");
+    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI && pc != AIJHIP_PC_GAMG)
+        return kfail(AIJHIP_ERR_ARG, "unknown PC type");
+    if (pc != K->pc) K->set_up = false;
     K->pc = pc;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_set_gamg_params(aijhip_ksp_t K, const aijhip_gamg_params_t *p) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (p) K->gamg = *p;
+    else aijhip_gamg_params_default(&K->gamg);
+    if (K->pc == AIJHIP_PC_GAMG) K->set_up = false;
     return AIJHIP_OK;
 }
 
@@ -355,13 +554,14 @@ int aijhip_ksp_set_initial_guess_nonzero(aijhip_ksp_t K, int flg) {
 int aijhip_ksp_set_up(aijhip_ksp_t K) {
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
     if (K->set_up) return AIJHIP_OK;
+    const auto t0 = std::chrono::steady_clock::now();
     aijhip_mat *A = K->A;
     KDeviceGuard g(A->device);
     ksp_free(K);
     const int64_t m = A->m;
     const size_t vb = sizeof(double) * (size_t)std::max<int64_t>(m, 1);
     K->fused = aijhip::stream_dot_fusable(*A);
-    K->vec_grid = (int)std::max<int64_t>(1, std::min<int64_t>((m + kVecThreads - 1) / kVecThreads, (int64_t)A->n_cu * 8));
+    K->vec_grid = (int)vgrid(K, m).x;
     const int64_t nparts = std::max<int64_t>((int64_t)kNQ * K->vec_grid, K->fused ? A->plan.n_blocks : K->vec_grid);
     K->hist_cap = K->max_it + 2;
     hipError_t e;
@@ -382,6 +582,14 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
             return khip(e, "PCSetUp_Jacobi");
         }
     }
+    if (K->pc == AIJHIP_PC_GAMG) {
+        const int rc = gamg_setup(K);
+        if (rc) {
+            ksp_free(K);
+            return rc;
+        }
+    }
+    K->setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     K->set_up = true;
     return AIJHIP_OK;
 }
@@ -397,6 +605,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     KDeviceGuard g(A->device);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     hipError_t e = hipSuccess;
+    const bool gamg = K->pc == AIJHIP_PC_GAMG;
     CGParams p{K->rtol, K->abstol, K->dtol, K->max_it, K->normtype, K->guess_nonzero ? 0 : 1, K->pc};
     const dim3 vg(K->vec_grid), vt(kVecThreads), rt(kRedThreads);
     const int nb = K->vec_grid;
@@ -408,10 +617,20 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     }
     if (e != hipSuccess) return khip(e, "KSPSolve init");
     hipLaunchKernelGGL(k_init, vg, vt, 0, s, m, b, K->d_r, K->d_z, K->d_dinv, K->d_part, p);
+    if (gamg) {
+        if (K->guess_nonzero && K->normtype != AIJHIP_KSP_NORM_UNPRECONDITIONED) {
+            // snorm = |B b| for the preconditioned-norm convergence test
+            if ((e = vcycle(K, b, K->d_z, s)) != hipSuccess) return khip(e, "GAMG V-cycle");
+            hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, nullptr, K->d_part, 3, -1, nullptr);
+        }
+        if ((e = vcycle(K, K->d_r, K->d_z, s)) != hipSuccess) return khip(e, "GAMG V-cycle");
+        hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, nullptr);
+    }
     hipLaunchKernelGGL(k_reduce_init, dim3(1), rt, 0, s, K->d_part, nb, K->d_state, K->d_hist, p);
     if ((e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve init");
-    // iterations in batches; every kernel is a no-op once `done` is set
-    const int batch = K->fused ? 8 : 1;
+    // iterations in batches; every CG kernel is a no-op once `done` is set
+    // (the V-cycle is not, so GAMG polls every iteration)
+    const int batch = (K->fused && !gamg) ? 8 : 1;
     int32_t launched = 0;
     for (;;) {
         if ((e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
@@ -431,6 +650,10 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             }
             hipLaunchKernelGGL(k_update, vg, vt, 0, s, m, x, K->d_p, K->d_r, K->d_z, K->d_dinv, K->d_part,
                                K->d_state, K->pc);
+            if (gamg && e == hipSuccess) {
+                e = vcycle(K, K->d_r, K->d_z, s);
+                hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
+            }
             hipLaunchKernelGGL(k_reduce_iter, dim3(1), rt, 0, s, K->d_part, nb, K->d_state, K->d_hist, p);
             if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve iteration");
         }
@@ -476,6 +699,24 @@ int aijhip_ksp_get_residual_history(aijhip_ksp_t K, double *hist, int32_t na, in
 int aijhip_ksp_get_fused(aijhip_ksp_t K, int *fused) {
     if (!K || !fused) return kfail(AIJHIP_ERR_ARG, "NULL argument");
     *fused = K->fused ? 1 : 0;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_pc_levels(aijhip_ksp_t K, int32_t *nlevels, int32_t *rows, int64_t *nnz, int32_t cap,
+                             double *setup_seconds) {
+    if (!K || !nlevels) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    if (K->mg.empty()) {
+        *nlevels = 1;
+        if (cap > 0 && rows) rows[0] = K->A->m;
+        if (cap > 0 && nnz) nnz[0] = K->A->nz;
+    } else {
+        *nlevels = (int32_t)K->mg.size();
+        for (int32_t l = 0; l < std::min<int32_t>(cap, *nlevels); ++l) {
+            if (rows) rows[l] = K->mg[l].m;
+            if (nnz) nnz[l] = K->mg[l].nnz;
+        }
+    }
+    if (setup_seconds) *setup_seconds = K->setup_seconds;
     return AIJHIP_OK;
 }
 

@@ -17,7 +17,7 @@ import numpy as np
 
 _pkg = importlib.import_module("petsc-openacc_amd")
 
-PC_TYPES = {"none": 0, "jacobi": 1}
+PC_TYPES = {"none": 0, "jacobi": 1, "gamg": 2}
 NORM_TYPES = {"none": 0, "preconditioned": 1, "unpreconditioned": 2, "natural": 3}
 REASONS = {2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
            -8: "DIVERGED_INDEFINITE_PC", -9: "DIVERGED_NANORINF", -10: "DIVERGED_INDEFINITE_MAT"}
@@ -26,6 +26,7 @@ KSP_SYMBOLS = (
     "aijhip_ksp_set_initial_guess_nonzero", "aijhip_ksp_set_up", "aijhip_ksp_solve",
     "aijhip_ksp_get_iteration_number", "aijhip_ksp_get_residual_norm", "aijhip_ksp_get_converged_reason",
     "aijhip_ksp_get_residual_history", "aijhip_ksp_get_fused", "aijhip_ksp_destroy",
+    "aijhip_ksp_set_gamg_params", "aijhip_ksp_get_pc_levels",
 )
 _P = ctypes.c_void_p
 _bound = False
@@ -50,6 +51,9 @@ def _lib():
         L.aijhip_ksp_get_residual_history.argtypes = [_P, _P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
         L.aijhip_ksp_get_fused.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
         L.aijhip_ksp_destroy.argtypes = [_P]
+        L.aijhip_ksp_set_gamg_params.argtypes = [_P, _P]
+        L.aijhip_ksp_get_pc_levels.argtypes = [_P, ctypes.POINTER(ctypes.c_int32), _P, _P, ctypes.c_int32,
+                                               ctypes.POINTER(ctypes.c_double)]
         _bound = True
     return L
 
@@ -58,13 +62,17 @@ class KSPCG:
     """KSPCG on a SeqAIJHIP operator (device vectors)."""
 
     def __init__(self, A, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
-                 norm="preconditioned", guess_nonzero=False):
+                 norm="preconditioned", guess_nonzero=False, gamg=None):
         L = _lib()
         self.A = A
         self._h = _P()
         _pkg._check(L.aijhip_ksp_create(A._h, ctypes.byref(self._h)))
         self.set_tolerances(rtol, atol, dtol, max_it)
         _pkg._check(L.aijhip_ksp_set_pc_type(self._h, PC_TYPES[pc]))
+        if gamg:
+            G = importlib.import_module("petsc-openacc_amd.gamg")
+            self._gp = G.default_params(**gamg)
+            _pkg._check(L.aijhip_ksp_set_gamg_params(self._h, ctypes.byref(self._gp)))
         _pkg._check(L.aijhip_ksp_set_norm_type(self._h, NORM_TYPES[norm]))
         _pkg._check(L.aijhip_ksp_set_initial_guess_nonzero(self._h, int(guess_nonzero)))
 
@@ -101,6 +109,16 @@ class KSPCG:
         v = ctypes.c_int()
         _pkg._check(_lib().aijhip_ksp_get_fused(self._h, ctypes.byref(v)))
         return bool(v.value)
+
+    def pc_levels(self):
+        """(rows per level, nnz per level, host set-up seconds) of the PC."""
+        n = ctypes.c_int32()
+        rows = np.zeros(32, np.int32)
+        nnz = np.zeros(32, np.int64)
+        secs = ctypes.c_double()
+        _pkg._check(_lib().aijhip_ksp_get_pc_levels(self._h, ctypes.byref(n), rows.ctypes.data, nnz.ctypes.data,
+                                                     32, ctypes.byref(secs)))
+        return rows[: n.value].tolist(), nnz[: n.value].tolist(), secs.value
 
     def history(self) -> np.ndarray:
         buf = np.empty(self.its + 1)

@@ -1,0 +1,134 @@
+"""GAMG hierarchy: the C++ host set-up vs the scipy restatement
+(oracle/gamg.py), CPU only; the device V-cycle and CG+GAMG are in the GPU
+section."""
+import importlib
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import gamg as ogamg
+from oracle import ksp_cg, seqaij
+
+
+def _csr(t, shape):
+    ai, aj, aa = t
+    M = sp.csr_matrix((aa, aj, ai), shape=shape)
+    M.eliminate_zeros()
+    M.sort_indices()
+    return M
+
+
+def _cmp(A, B, rtol=1e-12):
+    A = sp.csr_matrix(A); A.eliminate_zeros(); A.sort_indices()
+    B = sp.csr_matrix(B); B.eliminate_zeros(); B.sort_indices()
+    assert A.shape == B.shape
+    # structure equal up to entries that cancel to ~0 in one but not the other
+    D = (A - B).tocoo()
+    scale = max(abs(A).max(), 1e-300)
+    assert np.all(np.abs(D.data) <= rtol * scale), np.max(np.abs(D.data)) / scale
+
+
+@pytest.mark.parametrize("dims", [(8, 8, 8), (12, 12, 12), (6, 7, 5)])
+def test_host_hierarchy_matches_oracle(pkg, dims):
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    ai, aj, aa = pkg.poisson_csr(*dims)
+    m = len(ai) - 1
+    A = sp.csr_matrix((aa, aj, ai), shape=(m, m))
+    lv = G.build_host(ai, aj, aa, coarse_eq_limit=20)
+    ol = ogamg.build(A, coarse_eq_limit=20)
+    assert len(lv) == len(ol) >= 2
+    for l in range(len(lv) - 1):
+        assert np.array_equal(lv[l]["agg"], ol[l]["agg"])
+        assert lv[l]["emax"] == pytest.approx(ol[l]["emax"], rel=1e-12)
+        mc = lv[l + 1]["m"]
+        _cmp(_csr(lv[l]["P"], (lv[l]["m"], mc)), ol[l]["P"])
+        _cmp(_csr(lv[l + 1]["A"], (mc, mc)), ol[l + 1]["A"])
+
+
+def test_host_hierarchy_thread_invariant(pkg):
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    ai, aj, aa = pkg.poisson_csr(16)
+    a = G.build_host(ai, aj, aa, threads=1)
+    b = G.build_host(ai, aj, aa, threads=4)
+    for la, lb in zip(a, b):
+        for key in ("A", "P"):
+            if key in la:
+                for x, y in zip(la[key], lb[key]):
+                    assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+
+
+def test_hierarchy_galerkin_and_coarsening(pkg):
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    ai, aj, aa = pkg.poisson_csr(16)
+    lv = G.build_host(ai, aj, aa)
+    sizes = [L["m"] for L in lv]
+    assert all(b < a for a, b in zip(sizes, sizes[1:])) and sizes[-1] <= 50 or len(lv) == 10
+    # the coarse operators stay symmetric; P's columns reproduce the near-null
+    # space on the aggregates before smoothing (unit norm columns)
+    for l in range(1, len(lv)):
+        Ac = _csr(lv[l]["A"], (lv[l]["m"],) * 2)
+        assert abs(Ac - Ac.T).max() <= 1e-10 * abs(Ac).max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,norm", [(12, "preconditioned"), (20, "preconditioned"), (16, "unpreconditioned")])
+def test_gpu_cg_gamg_matches_oracle(pkg, N, norm):
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available()
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, exact = pkg.poisson_vectors(N)
+    m = len(ai) - 1
+    levels = ogamg.build(sp.csr_matrix((aa, aj, ai), shape=(m, m)), coarse_eq_limit=50)
+    tol = dict(rtol=1e-14, atol=1e-12, max_it=10000)
+    xo, its_o, reason_o, hist_o = ksp_cg.cg(ai, aj, aa, rhs, pc=lambda r: ogamg.vcycle(levels, r), norm=norm, **tol)
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    b = torch.from_numpy(rhs).cuda()
+    x = torch.empty_like(b)
+    with K.KSPCG(A, pc="gamg", norm=norm, **tol) as ksp:
+        ksp.solve(b, x)
+        rows, nnz, secs = ksp.pc_levels()
+        assert rows == [L["A"].shape[0] for L in levels]
+        assert ksp.reason == reason_o and abs(ksp.its - its_o) <= 1, (ksp.its, its_o, ksp.reason, reason_o)
+        h = ksp.history()
+        k = min(10, len(h), len(hist_o))
+        np.testing.assert_allclose(h[:k], hist_o[:k], rtol=1e-7)
+        xg = x.cpu().numpy()
+        assert np.linalg.norm(xg - xo) <= 1e-8 * np.linalg.norm(xo)
+        # fewer iterations than CG + Jacobi on the same problem
+        _, its_j, _, _ = ksp_cg.cg(ai, aj, aa, rhs, **tol)
+        assert ksp.its < its_j
+    A.destroy()
+
+
+def test_oracle_vcycle_preconditions_cg():
+    ai, aj, aa, rhs, exact = seqaij.create_system(10, 10, 10)
+    m = len(ai) - 1
+    A = sp.csr_matrix((aa, aj, ai), shape=(m, m))
+    levels = ogamg.build(A, coarse_eq_limit=20)
+    _, its_j, _, _ = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-10, max_it=1000)
+    # CG with the V-cycle as preconditioner (oracle only)
+    x = np.zeros(m)
+    r = rhs.copy()
+    z = ogamg.vcycle(levels, r)
+    p = z.copy()
+    beta = r @ z
+    its = 0
+    r0 = np.linalg.norm(z)
+    while its < 200:
+        w = A @ p
+        a = beta / (p @ w)
+        x += a * p
+        r -= a * w
+        z = ogamg.vcycle(levels, r)
+        its += 1
+        if np.linalg.norm(z) <= 1e-10 * r0:
+            break
+        bn = r @ z
+        p = z + (bn / beta) * p
+        beta = bn
+    # the reference's options (undamped Richardson+Jacobi smoothing, one
+    # Jacobi sweep as the coarse solve) make a modest V-cycle, still < half
+    # of Jacobi-CG's iterations at 10^3
+    assert its < its_j / 2, (its, its_j)
