@@ -84,16 +84,23 @@ def _mix64(z):
     return z ^ (z >> 31)
 
 
+def _seqdot(a, b):
+    """Left-to-right sum (the C++ set-up's order; np.dot is pairwise). The
+    aggregation of the next level is sensitive to the last bit of every
+    coarse entry (ties, zero threshold), so the restatement keeps the order."""
+    return float(sum((np.asarray(a) * np.asarray(b)).tolist(), 0.0))
+
+
 def estimate_emax(A, dinv, its):
     """Power iteration on D^-1 A from the same counter-based start."""
     m = A.shape[0]
     v = np.array([2.0 * ((_mix64((0x5EED + (i + 1) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF) >> 11)
                          * (1.0 / 9007199254740992.0)) - 1.0 for i in range(m)])
-    v /= math.sqrt(float(np.dot(v, v)))
+    v /= math.sqrt(_seqdot(v, v))
     lam = 1.0
     for _ in range(its):
         w = dinv * (A @ v)
-        nw = math.sqrt(float(np.dot(w, w)))
+        nw = math.sqrt(_seqdot(w, w))
         if not nw > 0.0:
             break
         lam = nw
@@ -122,7 +129,13 @@ def build(A, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smoot
             T = A @ P0
             P = (-smooth_scale / emax) * (sp.diags(dinv) @ T) + P0
         P = sp.csr_matrix(P)
-        Ac = sp.csr_matrix(P.T @ (A @ P))
+        P.sort_indices()
+        PT = sp.csr_matrix(P.T)  # rows list fine rows ascending, as the C++ transpose
+        PT.sort_indices()
+        AP = sp.csr_matrix(A @ P)
+        AP.sort_indices()
+        Ac = sp.csr_matrix(PT @ AP)  # csr x csr: scipy's csr_matmat order = the C++ spgemm's
+        Ac.sort_indices()
         levels.append(dict(A=A, P=P, agg=agg, emax=emax))
         A, B = Ac, Bc
     levels.append(dict(A=A))
