@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-cg", action="store_true")
+    p.add_argument("--no-gamg", action="store_true", help="skip the CG+GAMG solve (BASELINE configs[2])")
+    p.add_argument("--gamg-cpu-iters", type=int, default=3, help="CG+GAMG iterations in the CPU sample")
     p.add_argument("--cg-iters", type=int, default=200, help="CG iterations timed for cg.iters_per_s")
     return p.parse_args()
 
@@ -105,6 +107,40 @@ def cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz, iters=8):
     dt = time.perf_counter() - t0
     return {"iters_per_s": round(its / dt, 3), "cores": 1, "kind": "port",
             "sample": f"{its} CG+Jacobi iterations, oracle/ksp_cg.py + oracle/matmult_seqaij.c, 1 core"}
+
+
+def cpu_cg_gamg_baseline(ai, aj, aa, pkg, nx, ny, nz, its_gpu, iters=3):
+    """CG+GAMG on the host: the set-up is the library's host code (shared
+    with the device path, timed here on its own); the solve phase is the
+    oracle (oracle/ksp_cg.py + oracle/gamg.py V-cycle on scipy CSR products,
+    1 core) for a few iterations, scaled to the device's iteration count."""
+    import scipy.sparse as sp
+    from oracle import gamg as ogamg
+    from oracle import ksp_cg
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    m = len(ai) - 1
+    t0 = time.perf_counter()
+    lv = G.build_host(ai, aj, aa)
+    t_setup = time.perf_counter() - t0
+    levels = [dict(A=sp.csr_matrix((aa, aj, ai), shape=(m, m)))]
+    for l in range(1, len(lv)):
+        a_i, a_j, a_a = lv[l]["A"]
+        levels.append(dict(A=sp.csr_matrix((a_a, a_j, a_i), shape=(lv[l]["m"],) * 2)))
+        p_i, p_j, p_a = lv[l - 1]["P"]
+        levels[l - 1]["P"] = sp.csr_matrix((p_a, p_j, p_i), shape=(lv[l - 1]["m"], lv[l]["m"]))
+    del lv
+    ogamg.vcycle(levels, np.zeros(m))  # caches the Jacobi inverses (set-up work)
+    rhs, _ = pkg.poisson_vectors(nx, ny, nz)
+    A0 = levels[0]["A"]
+    t0 = time.perf_counter()
+    _, its, _, _ = ksp_cg.cg(ai, aj, aa, rhs, rtol=0.0, atol=0.0, max_it=iters, matmult=lambda v: A0 @ v,
+                             pc=lambda r: ogamg.vcycle(levels, r))
+    per_it = (time.perf_counter() - t0) / its
+    return {"s_per_iter": round(per_it, 4), "setup_s": round(t_setup, 3),
+            "time_to_solution_s_est": round(t_setup + per_it * its_gpu, 2), "cores": 1,
+            "setup_threads": int(os.environ.get("OMP_NUM_THREADS", 0)) or os.cpu_count(), "kind": "port",
+            "sample": f"{its} CG+GAMG iterations at {nx}x{ny}x{nz} (oracle CG + V-cycle, scipy CSR, 1 core), "
+                      f"scaled to the device's {its_gpu} iterations; host set-up as in the library"}
 
 
 def pmc_traffic(rows, nnz, block):
@@ -240,6 +276,15 @@ def main():
         cg = ksp.bench_cg(pkg, A, nx, ny, nz_global, dev, iters=args.cg_iters)
         if not args.no_cpu_baseline:
             cg["cpu_baseline"] = cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz_global)
+    cg_gamg = None
+    if not args.no_gamg and not distributed:
+        ksp = importlib.import_module("petsc-openacc_amd.ksp")
+        cg_gamg = ksp.bench_cg_gamg(pkg, A, nx, ny, nz_global, dev)
+        print(f"bench: CG+GAMG {cg_gamg['its']} its, solve {cg_gamg['solve_s']} s, set-up {cg_gamg['setup_s']} s",
+              file=sys.stderr, flush=True)
+        if not args.no_cpu_baseline:
+            cg_gamg["cpu_baseline"] = cpu_cg_gamg_baseline(ai, aj, aa, pkg, nx, ny, nz_global, cg_gamg["its"],
+                                                           args.gamg_cpu_iters)
 
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
@@ -288,6 +333,8 @@ def main():
         }
         if cg is not None:
             out["cg"] = cg
+        if cg_gamg is not None:
+            out["cg_gamg"] = cg_gamg
         if not args.no_cpu_baseline and not distributed:
             t_cpu, reps = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds)
             out["cpu_baseline"] = {

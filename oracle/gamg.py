@@ -20,12 +20,11 @@ import scipy.sparse as sp
 
 def first_diagonal(A: sp.csr_matrix) -> np.ndarray:
     """MatGetDiagonal: first stored diagonal entry per row (0 if none)."""
+    rows = np.repeat(np.arange(A.shape[0]), np.diff(A.indptr))
+    hit = np.flatnonzero(A.indices == rows)
+    r, first = np.unique(rows[hit], return_index=True)  # first stored hit per row
     d = np.zeros(A.shape[0])
-    for i in range(A.shape[0]):
-        for k in range(A.indptr[i], A.indptr[i + 1]):
-            if A.indices[k] == i:
-                d[i] = A.data[k]
-                break
+    d[r] = A.data[hit[first]]
     return d
 
 
@@ -84,11 +83,15 @@ def _mix64(z):
     return z ^ (z >> 31)
 
 
-def _seqdot(a, b):
-    """Left-to-right sum (the C++ set-up's order; np.dot is pairwise). The
-    aggregation of the next level is sensitive to the last bit of every
-    coarse entry (ties, zero threshold), so the restatement keeps the order."""
-    return float(sum((np.asarray(a) * np.asarray(b)).tolist(), 0.0))
+def _blockdot(a, b, block=8192):
+    """The C++ set-up's dot: left to right inside fixed 8192-entry blocks,
+    then the block sums left to right (np.cumsum accumulates sequentially;
+    np.dot is pairwise). The aggregation of the next level is sensitive to the
+    last bit of every coarse entry (ties, zero threshold), so the restatement
+    keeps the order."""
+    p = np.asarray(a, dtype=np.float64) * np.asarray(b, dtype=np.float64)
+    parts = [np.cumsum(p[i:i + block])[-1] for i in range(0, len(p), block)]
+    return float(np.cumsum(parts)[-1]) if parts else 0.0
 
 
 def estimate_emax(A, dinv, its):
@@ -96,11 +99,11 @@ def estimate_emax(A, dinv, its):
     m = A.shape[0]
     v = np.array([2.0 * ((_mix64((0x5EED + (i + 1) * 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF) >> 11)
                          * (1.0 / 9007199254740992.0)) - 1.0 for i in range(m)])
-    v /= math.sqrt(_seqdot(v, v))
+    v /= math.sqrt(_blockdot(v, v))
     lam = 1.0
     for _ in range(its):
         w = dinv * (A @ v)
-        nw = math.sqrt(_seqdot(w, w))
+        nw = math.sqrt(_blockdot(w, w))
         if not nw > 0.0:
             break
         lam = nw
@@ -145,14 +148,14 @@ def build(A, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smoot
 def vcycle(levels, b):
     """PCApply_MG, multiplicative V-cycle: Richardson(1)+Jacobi down (zero
     guess) and up (nonzero guess), P^T restriction, P interpolation, coarse
-    preonly + Jacobi."""
-    dinvs = []
+    preonly + Jacobi. The Jacobi inverses are cached in the level dicts."""
     for L in levels:
-        d = first_diagonal(L["A"])
-        dinvs.append(1.0 / np.where(d == 0.0, 1.0, d))
+        if "dinv" not in L:
+            d = first_diagonal(L["A"])
+            L["dinv"] = 1.0 / np.where(d == 0.0, 1.0, d)
 
     def cycle(l, bl):
-        A, dinv = levels[l]["A"], dinvs[l]
+        A, dinv = levels[l]["A"], levels[l]["dinv"]
         x = dinv * bl
         if l == len(levels) - 1:
             return x

@@ -5,6 +5,9 @@
 // result does not depend on the thread count, and equals a scipy CSR
 // restatement (oracle/gamg.py) bit for bit.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -37,6 +40,10 @@ struct View {
 
 View view(const CSR &c) { return View{c.m, c.n, c.ai.data(), c.aj.data(), c.aa.data()}; }
 
+double wtime() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 int nthreads(int req) {
 #ifdef _OPENMP
     return req > 0 ? req : omp_get_max_threads();
@@ -47,8 +54,9 @@ int nthreads(int req) {
 }
 
 // First stored diagonal entry of each row (0 if none) — MatGetDiagonal.
-std::vector<double> diagonal(const View &A) {
+std::vector<double> diagonal(const View &A, int nt) {
     std::vector<double> d(A.m, 0.0);
+#pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < A.m; ++i)
         for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k)
             if (A.aj[k] == i) { d[i] = A.aa[k]; break; }
@@ -56,9 +64,11 @@ std::vector<double> diagonal(const View &A) {
 }
 
 // Symmetric strength graph: j != i with |a_ij| > theta * sqrt(|a_ii a_jj|),
-// united with its transpose; rows sorted, unique.
+// united with its transpose; rows sorted, unique. Each row's set gathers its
+// own strong entries and the rows strong towards it into atomically taken
+// slots, then is sorted, so the result does not depend on the thread count.
 void strength_graph(const View &A, const std::vector<double> &d, double theta,
-                    std::vector<int32_t> &si, std::vector<int32_t> &sj) {
+                    std::vector<int32_t> &si, std::vector<int32_t> &sj, int nt) {
     const int32_t m = A.m;
     auto strong = [&](int32_t i, int32_t k) {
         const int32_t j = A.aj[k];
@@ -66,27 +76,44 @@ void strength_graph(const View &A, const std::vector<double> &d, double theta,
         const double v = std::fabs(A.aa[k]);
         return v > theta * std::sqrt(std::fabs(d[i] * d[j]));
     };
-    std::vector<int32_t> cnt(m + 1, 0);
+    std::vector<int32_t> cnt(m, 0);  // out-degree + in-degree
+#pragma omp parallel for schedule(dynamic, 4096) num_threads(nt)
     for (int32_t i = 0; i < m; ++i)
         for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k)
-            if (strong(i, k)) { ++cnt[i + 1]; ++cnt[A.aj[k] + 1]; }
-    std::vector<int32_t> off(m + 1, 0);
-    for (int32_t i = 0; i < m; ++i) off[i + 1] = off[i] + cnt[i + 1];
+            if (strong(i, k)) {
+#pragma omp atomic
+                ++cnt[i];
+#pragma omp atomic
+                ++cnt[A.aj[k]];
+            }
+    std::vector<int64_t> off((size_t)m + 1, 0);
+    for (int32_t i = 0; i < m; ++i) off[i + 1] = off[i] + cnt[i];
     std::vector<int32_t> tmp(off[m]);
-    std::vector<int32_t> pos(off.begin(), off.end() - 1);
+    std::vector<int64_t> pos(off.begin(), off.end() - 1);
+#pragma omp parallel for schedule(dynamic, 4096) num_threads(nt)
     for (int32_t i = 0; i < m; ++i)
         for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k)
-            if (strong(i, k)) { tmp[pos[i]++] = A.aj[k]; tmp[pos[A.aj[k]]++] = i; }
-    si.assign(m + 1, 0);
-    sj.clear();
-    sj.reserve(off[m]);
+            if (strong(i, k)) {
+                const int32_t j = A.aj[k];
+                int64_t a, b;
+#pragma omp atomic capture
+                a = pos[i]++;
+#pragma omp atomic capture
+                b = pos[j]++;
+                tmp[a] = j;
+                tmp[b] = i;
+            }
+#pragma omp parallel for schedule(dynamic, 4096) num_threads(nt)
     for (int32_t i = 0; i < m; ++i) {
         auto b = tmp.begin() + off[i], e = tmp.begin() + off[i + 1];
         std::sort(b, e);
-        e = std::unique(b, e);
-        sj.insert(sj.end(), b, e);
-        si[i + 1] = (int32_t)sj.size();
+        cnt[i] = (int32_t)(std::unique(b, e) - b);
     }
+    si.assign((size_t)m + 1, 0);
+    for (int32_t i = 0; i < m; ++i) si[i + 1] = si[i] + cnt[i];
+    sj.resize(si[m]);
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int32_t i = 0; i < m; ++i) std::copy_n(tmp.begin() + off[i], cnt[i], sj.begin() + si[i]);
 }
 
 // Greedy aggregation in natural order (Vanek et al.): (1) a free node whose
@@ -149,9 +176,21 @@ void dinv_apply(const View &A, const std::vector<double> &dinv, const std::vecto
     }
 }
 
-double dot(const std::vector<double> &a, const std::vector<double> &b) {
+// Deterministic blocked dot: left to right inside fixed kDotBlock-entry
+// blocks, then the block sums left to right (oracle/gamg.py _blockdot).
+constexpr int64_t kDotBlock = 8192;
+
+double dot(const std::vector<double> &a, const std::vector<double> &b, int nt) {
+    const int64_t n = (int64_t)a.size(), nb = (n + kDotBlock - 1) / kDotBlock;
+    std::vector<double> part(nb);
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int64_t q = 0; q < nb; ++q) {
+        double s = 0.0;
+        for (int64_t i = q * kDotBlock, e = std::min(n, i + kDotBlock); i < e; ++i) s += a[i] * b[i];
+        part[q] = s;
+    }
     double s = 0.0;
-    for (size_t i = 0; i < a.size(); ++i) s += a[i] * b[i];
+    for (int64_t q = 0; q < nb; ++q) s += part[q];
     return s;
 }
 
@@ -160,17 +199,20 @@ double estimate_emax(const View &A, const std::vector<double> &dinv, int its, in
     const int32_t m = A.m;
     if (m == 0) return 1.0;
     std::vector<double> v(m), w(m);
+#pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < m; ++i)
         v[i] = 2.0 * ((double)(mix64(0x5EEDULL + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL) >> 11) *
                       (1.0 / 9007199254740992.0)) - 1.0;
-    double nv = std::sqrt(dot(v, v));
+    const double nv = std::sqrt(dot(v, v, nt));
+#pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < m; ++i) v[i] /= nv;
     double lam = 1.0;
     for (int it = 0; it < its; ++it) {
         dinv_apply(A, dinv, v, w, nt);
-        const double nw = std::sqrt(dot(w, w));
+        const double nw = std::sqrt(dot(w, w, nt));
         if (!(nw > 0.0)) break;
         lam = nw;
+#pragma omp parallel for schedule(static) num_threads(nt)
         for (int32_t i = 0; i < m; ++i) v[i] = w[i] / nw;
     }
     return lam;
@@ -229,23 +271,48 @@ void spgemm(const View &A, const View &B, CSR &C, int nt) {
     }
 }
 
-// Transpose (counting sort: each output row lists input rows ascending).
-void transpose(const View &A, CSR &T) {
+// Transpose: each output row lists the input rows ascending. The input rows
+// are cut into one contiguous chunk per thread; per-(chunk, column) counts
+// give every chunk its own slots in each output row, so each thread fills
+// its slots in row order and no sort or atomic is needed.
+void transpose(const View &A, CSR &T, int nt) {
     T.m = A.n;
     T.n = A.m;
-    T.ai.assign((size_t)A.n + 1, 0);
     const int64_t nz = A.ai[A.m];
-    for (int64_t k = 0; k < nz; ++k) ++T.ai[A.aj[k] + 1];
-    for (int32_t c = 0; c < A.n; ++c) T.ai[c + 1] += T.ai[c];
+    nt = std::max(1, std::min<int>(nt, A.m / 4096 + 1));
+    std::vector<int32_t> cnt((size_t)nt * A.n, 0);  // [chunk][column]
+    auto chunk = [&](int t) { return std::make_pair((int32_t)((int64_t)A.m * t / nt),
+                                                    (int32_t)((int64_t)A.m * (t + 1) / nt)); };
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+    for (int t = 0; t < nt; ++t) {
+        const auto [r0, r1] = chunk(t);
+        int32_t *c = cnt.data() + (size_t)t * A.n;
+        for (int64_t k = A.ai[r0]; k < A.ai[r1]; ++k) ++c[A.aj[k]];
+    }
+    T.ai.assign((size_t)A.n + 1, 0);
+    int64_t run = 0;
+    for (int32_t col = 0; col < A.n; ++col) {
+        T.ai[col] = (int32_t)run;
+        for (int t = 0; t < nt; ++t) {  // counts -> starting slots
+            const int32_t k = cnt[(size_t)t * A.n + col];
+            cnt[(size_t)t * A.n + col] = (int32_t)run;
+            run += k;
+        }
+    }
+    T.ai[A.n] = (int32_t)run;
     T.aj.resize(nz);
     T.aa.resize(nz);
-    std::vector<int32_t> pos(T.ai.begin(), T.ai.end() - 1);
-    for (int32_t i = 0; i < A.m; ++i)
-        for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) {
-            const int32_t p = pos[A.aj[k]]++;
-            T.aj[p] = i;
-            T.aa[p] = A.aa[k];
-        }
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+    for (int t = 0; t < nt; ++t) {
+        const auto [r0, r1] = chunk(t);
+        int32_t *pos = cnt.data() + (size_t)t * A.n;
+        for (int32_t i = r0; i < r1; ++i)
+            for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) {
+                const int32_t p = pos[A.aj[k]]++;
+                T.aj[p] = i;
+                T.aa[p] = A.aa[k];
+            }
+    }
 }
 
 // Smoothed prolongator P = alpha * (D^-1 A P0) + P0, alpha = -scale/emax,
@@ -264,6 +331,7 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
     P0.ai.resize((size_t)m + 1);
     P0.aj.resize(m);
     P0.aa.resize(m);
+#pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < m; ++i) {
         P0.ai[i] = i;
         P0.aj[i] = agg[i];
@@ -278,10 +346,13 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
     P.m = m;
     P.n = na;
     P.ai.assign((size_t)m + 1, 0);
+    std::vector<int32_t> len(m);
+#pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < m; ++i) {
         const bool has = std::binary_search(T.aj.begin() + T.ai[i], T.aj.begin() + T.ai[i + 1], agg[i]);
-        P.ai[i + 1] = P.ai[i] + (T.ai[i + 1] - T.ai[i]) + (has ? 0 : 1);
+        len[i] = (T.ai[i + 1] - T.ai[i]) + (has ? 0 : 1);
     }
+    for (int32_t i = 0; i < m; ++i) P.ai[i + 1] = P.ai[i] + len[i];
     P.aj.resize(P.ai[m]);
     P.aa.resize(P.ai[m]);
 #pragma omp parallel for schedule(static) num_threads(nt)
@@ -345,22 +416,38 @@ int aijhip_gamg_build_host(int32_t m, const int32_t *ai, const int32_t *aj, cons
         H->A.emplace_back();
         std::vector<double> B(m, 1.0);  // near-null space of the scalar operator
         View cur{m, m, ai, aj, aa};
+        const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+        double t0 = wtime();
+        auto lap = [&](const char *what) {
+            if (!log) return;
+            const double t = wtime();
+            std::fprintf(stderr, "gamg level %zu %-12s %8.3f s\n", H->m.size() - 1, what, t - t0);
+            t0 = t;
+        };
         while ((int32_t)H->m.size() < p.max_levels && cur.m > p.coarse_eq_limit) {
-            const std::vector<double> d = diagonal(cur);
+            const std::vector<double> d = diagonal(cur, nt);
             std::vector<double> dinv(cur.m);
             for (int32_t i = 0; i < cur.m; ++i) dinv[i] = 1.0 / (d[i] == 0.0 ? 1.0 : d[i]);
             std::vector<int32_t> si, sj, agg;
-            strength_graph(cur, d, p.threshold, si, sj);
+            lap("diagonal");
+            strength_graph(cur, d, p.threshold, si, sj, nt);
+            lap("strength");
             const int32_t na = aggregate(cur, si, sj, agg);
+            lap("aggregate");
             if (na >= cur.m || na == 0) break;  // no coarsening
             const double emax = p.nsmooths > 0 ? estimate_emax(cur, dinv, p.eig_its, nt) : 1.0;
+            lap("emax");
             CSR P;
             std::vector<double> Bc;
             prolongator(cur, dinv, agg, na, B, -p.smooth_scale / emax, p.nsmooths, P, Bc, nt);
+            lap("prolongator");
             CSR AP, PT, Ac;
             spgemm(cur, view(P), AP, nt);
-            transpose(view(P), PT);
+            lap("A*P");
+            transpose(view(P), PT, nt);
+            lap("P^T");
             spgemm(view(PT), view(AP), Ac, nt);
+            lap("P^T*(AP)");
             H->P.push_back(std::move(P));
             H->agg.push_back(std::move(agg));
             H->emax.push_back(emax);

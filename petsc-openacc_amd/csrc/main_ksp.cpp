@@ -4,8 +4,10 @@
 // (main_ksp.cpp:124-129), so scripts/generate_plots.py's regex still parses it.
 //
 //   main_ksp [-config FILE] [-da_grid_x N] [-da_grid_y N] [-da_grid_z N]
-//            [-ksp_rtol R] [-ksp_atol A] [-ksp_max_it K] [-pc_type jacobi|none]
+//            [-ksp_rtol R] [-ksp_atol A] [-ksp_max_it K] [-pc_type jacobi|none|gamg]
 //            [-ksp_norm_type preconditioned|unpreconditioned|natural]
+//            [-pc_gamg_threshold T] [-pc_gamg_agg_nsmooths S]
+//            [-pc_gamg_coarse_eq_limit C] [-pc_mg_levels L]
 //
 // Options come from the command line and from a PETSc options file
 // (`-key value` per line, '#' comments; PetscOptionsInsertFile,
@@ -97,14 +99,30 @@ int main(int argc, char **argv) {
     }
     std::string pc_type = gets("-pc_type", "jacobi");
     if (pc_type == "bjacobi") pc_type = "jacobi";  // one block per rank + jacobi sub-PC
-    if (pc_type == "gamg") {
-        std::fprintf(stderr, "main_ksp: -pc_type gamg is not built yet (DESIGN.md §8); using jacobi\n");
-        pc_type = "jacobi";
-    }
-    int pc = pc_type == "none" ? AIJHIP_PC_NONE : AIJHIP_PC_JACOBI;
-    if (pc_type != "none" && pc_type != "jacobi") {
+    int pc = pc_type == "none" ? AIJHIP_PC_NONE : pc_type == "gamg" ? AIJHIP_PC_GAMG : AIJHIP_PC_JACOBI;
+    if (pc_type != "none" && pc_type != "jacobi" && pc_type != "gamg") {
         std::fprintf(stderr, "main_ksp: -pc_type %s not supported\n", pc_type.c_str());
         return 1;
+    }
+    aijhip_gamg_params_t gp;
+    aijhip_gamg_params_default(&gp);
+    if (pc == AIJHIP_PC_GAMG) {
+        // PETSc_SolverOptions_GAMG.info:6-21. The level smoother and coarse
+        // solver are fixed to that file's choice (Richardson(1) + Jacobi,
+        // preonly + Jacobi); anything else is refused, not silently changed.
+        if (gets("-pc_gamg_type", "agg") != "agg") { std::fprintf(stderr, "main_ksp: only -pc_gamg_type agg\n"); return 1; }
+        const char *fixed[][2] = {{"-mg_levels_ksp_type", "richardson"}, {"-mg_levels_ksp_max_it", "1"},
+                                  {"-mg_coarse_ksp_type", "preonly"}, {"-mg_levels_sub_pc_type", "jacobi"},
+                                  {"-mg_coarse_sub_pc_type", "jacobi"}};
+        for (auto &f : fixed)
+            if (opt.count(f[0]) && opt[f[0]] != f[1]) {
+                std::fprintf(stderr, "main_ksp: %s %s not supported (only %s)\n", f[0], opt[f[0]].c_str(), f[1]);
+                return 1;
+            }
+        gp.threshold = getd("-pc_gamg_threshold", gp.threshold);
+        gp.nsmooths = (int32_t)geti("-pc_gamg_agg_nsmooths", gp.nsmooths);
+        gp.coarse_eq_limit = (int32_t)geti("-pc_gamg_coarse_eq_limit", gp.coarse_eq_limit);
+        gp.max_levels = (int32_t)geti("-pc_mg_levels", gp.max_levels);
     }
     const std::string nts = gets("-ksp_norm_type", "preconditioned");
     const int normtype = nts == "unpreconditioned" ? AIJHIP_KSP_NORM_UNPRECONDITIONED
@@ -138,6 +156,7 @@ int main(int argc, char **argv) {
     CHK(aijhip_ksp_set_tolerances(ksp, getd("-ksp_rtol", 1e-5), getd("-ksp_atol", 1e-50),
                                   getd("-ksp_divtol", 1e5), (int32_t)geti("-ksp_max_it", 10000)));
     CHK(aijhip_ksp_set_pc_type(ksp, pc));
+    if (pc == AIJHIP_PC_GAMG) CHK(aijhip_ksp_set_gamg_params(ksp, &gp));
     CHK(aijhip_ksp_set_norm_type(ksp, normtype));
     CHK(aijhip_ksp_set_up(ksp));
     HCHK(hipDeviceSynchronize());

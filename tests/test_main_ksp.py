@@ -49,3 +49,34 @@ def test_driver_output_matches_reference_format_and_oracle(pkg):
     assert abs(linf - np.max(np.abs(x - exact))) < 1e-6  # printed with %f
     assert linf < 0.05  # second-order discretisation error at h = 1/20
     assert res < 1e-6
+
+
+@pytest.mark.gpu
+def test_driver_cg_gamg_options_file(pkg):
+    """-config configs/cg_gamg.info: CG + GAMG, iterations and error as the
+    oracle CG with the oracle V-cycle on the same hierarchy."""
+    import importlib
+    import scipy.sparse as sp
+    from oracle import gamg as ogamg
+    exe = importlib.import_module("petsc-openacc_amd.build").build_main_ksp()
+    N = 20
+    r = subprocess.run([str(exe), "-config", str(ROOT / "configs" / "cg_gamg.info"), "-da_grid_x", str(N),
+                        "-da_grid_y", str(N), "-da_grid_z", str(N)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    m = BLOCK.search(r.stdout)
+    assert m, r.stdout
+    its, linf = int(m.group(4)), float(m.group(6))
+    ai, aj, aa, rhs, exact = seqaij.create_system(N, N, N)
+    levels = ogamg.build(sp.csr_matrix((aa, aj, ai), shape=(N ** 3,) * 2))
+    x, its_o, reason, _ = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-14, atol=1e-12, max_it=10000,
+                                    pc=lambda v: ogamg.vcycle(levels, v))
+    assert reason > 0 and abs(its - its_o) <= 1, (its, its_o)
+    assert abs(linf - np.max(np.abs(x - exact))) < 1e-6
+
+
+def test_driver_refuses_unsupported_mg_smoother(pkg):
+    import importlib
+    exe = importlib.import_module("petsc-openacc_amd.build").build_main_ksp()
+    r = subprocess.run([str(exe), "-pc_type", "gamg", "-mg_levels_ksp_type", "chebyshev", "-da_grid_x", "4"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 1 and "chebyshev not supported" in r.stderr

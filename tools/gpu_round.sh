@@ -15,10 +15,10 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
  && echo "smoke ok" \
  && timeout -k 10 900 python -m pytest tests -x -q -m gpu > "$OUT/pytest_gpu.log" 2>&1 \
  && echo "pytest gpu ok" \
- && timeout -k 10 300 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" \
+ && timeout -k 10 600 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" \
  && echo "bench ok" && cat "$OUT/bench.json" \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-      -- python3 bench.py --steps 100 --no-cpu-baseline --no-cg "$@" > "$OUT/prof.log" 2>&1 \
+      -- python3 bench.py --steps 100 --no-cpu-baseline --no-cg --no-gamg "$@" > "$OUT/prof.log" 2>&1 \
  && echo "rocprof ok"
 rc=$?
 tail -5 "$OUT/pytest_gpu.log" 2>/dev/null
