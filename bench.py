@@ -62,26 +62,34 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(ai, aj, aa, x, seconds):
-    """Time the oracle (C restatement of MatMult_SeqAIJ) on 1 core, repeated
-    whole-operand SpMVs until `seconds` elapse (bounded sample)."""
+def cpu_baseline(ai, aj, aa, x, seconds, all_cores=False):
+    """Time the oracle (C restatement of MatMult_SeqAIJ) on 1 core — PETSc's
+    1 rank = 1 core — or, with all_cores, its OpenMP static-row-block form on
+    every host thread this process may use; repeated
+    whole-operand SpMVs until `seconds` elapse (bounded sample). Returns
+    (seconds per SpMV, reps, threads)."""
     build = importlib.import_module("petsc-openacc_amd.build")
     L = ctypes.CDLL(str(build.build_oracle()))
     P = ctypes.c_void_p
-    L.oracle_matmult_seqaij.argtypes = [ctypes.c_int32, P, P, P, P, P]
-    L.oracle_matmult_seqaij.restype = None
+    fn = L.oracle_matmult_seqaij_omp if all_cores else L.oracle_matmult_seqaij
+    fn.argtypes = [ctypes.c_int32, P, P, P, P, P]
+    fn.restype = None
+    threads = 1
+    if all_cores:
+        L.oracle_omp_threads.restype = ctypes.c_int
+        threads = L.oracle_omp_threads()
     m = len(ai) - 1
     y = np.empty(m)
     args = (m, ai.ctypes.data, aj.ctypes.data, aa.ctypes.data, x.ctypes.data, y.ctypes.data)
-    L.oracle_matmult_seqaij(*args)  # warm-up (page-in)
+    fn(*args)  # warm-up (page-in)
     reps, t0 = 0, time.perf_counter()
     while True:
-        L.oracle_matmult_seqaij(*args)
+        fn(*args)
         reps += 1
         el = time.perf_counter() - t0
         if el >= seconds or reps >= 50:
             break
-    return el / reps, reps
+    return el / reps, reps, threads
 
 
 def cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz, iters=8):
@@ -336,7 +344,7 @@ def main():
         if cg_gamg is not None:
             out["cg_gamg"] = cg_gamg
         if not args.no_cpu_baseline and not distributed:
-            t_cpu, reps = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds)
+            t_cpu, reps, _ = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds)
             out["cpu_baseline"] = {
                 "value": round(bytes_local / t_cpu / 1e9, 3),
                 "unit": "GB/s",
@@ -344,6 +352,15 @@ def main():
                 "kind": "port",
                 "sample": f"{reps} whole-operand {G}^3 SpMVs on 1 core ({cpu_model()}), "
                           f"{t_cpu * 1e3:.1f} ms each; oracle/matmult_seqaij.c",
+            }
+            t_all, reps_all, threads = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds / 2, all_cores=True)
+            out["cpu_baseline_all_cores"] = {
+                "value": round(bytes_local / t_all / 1e9, 3),
+                "unit": "GB/s",
+                "cores": threads,
+                "kind": "port",
+                "sample": f"{reps_all} whole-operand {G}^3 SpMVs, OpenMP static row blocks on {threads} threads, "
+                          f"{t_all * 1e3:.1f} ms each; oracle/matmult_seqaij.c oracle_matmult_seqaij_omp",
             }
         print(json.dumps(out), flush=True)
 

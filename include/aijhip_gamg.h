@@ -54,6 +54,11 @@ int aijhip_gamg_host_level_info(aijhip_gamg_host_t h, int32_t l, int32_t *m, int
 int aijhip_gamg_host_get_A(aijhip_gamg_host_t h, int32_t l, int32_t *ai, int32_t *aj, double *aa);
 int aijhip_gamg_host_get_P(aijhip_gamg_host_t h, int32_t l, int32_t *ai, int32_t *aj, double *aa);
 int aijhip_gamg_host_get_aggregates(aijhip_gamg_host_t h, int32_t l, int32_t *agg);
+/* Borrow level l's operator (which = 'A', l >= 1) or interpolation
+ * (which = 'P', l < nlevels-1) in place: the pointers stay valid until
+ * aijhip_gamg_host_destroy (no copy; the device set-up uploads from them). */
+int aijhip_gamg_host_view(aijhip_gamg_host_t h, int32_t l, char which, const int32_t **ai, const int32_t **aj,
+                          const double **aa);
 int aijhip_gamg_host_destroy(aijhip_gamg_host_t h);
 
 #ifdef __cplusplus

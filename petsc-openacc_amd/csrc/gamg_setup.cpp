@@ -509,6 +509,19 @@ int aijhip_gamg_host_get_aggregates(aijhip_gamg_host_t h, int32_t l, int32_t *ag
     return AIJHIP_OK;
 }
 
+int aijhip_gamg_host_view(aijhip_gamg_host_t h, int32_t l, char which, const int32_t **ai, const int32_t **aj,
+                          const double **aa) {
+    if (!h || !ai || !aj || !aa || l < 0) return AIJHIP_ERR_ARG;
+    const CSR *c = nullptr;
+    if (which == 'A' && l >= 1 && l < (int32_t)h->A.size()) c = &h->A[l];
+    if (which == 'P' && l < (int32_t)h->P.size()) c = &h->P[l];
+    if (!c) return AIJHIP_ERR_ARG;
+    *ai = c->ai.data();
+    *aj = c->aj.data();
+    *aa = c->aa.data();
+    return AIJHIP_OK;
+}
+
 int aijhip_gamg_host_destroy(aijhip_gamg_host_t h) {
     delete h;
     return AIJHIP_OK;

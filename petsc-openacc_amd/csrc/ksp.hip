@@ -23,6 +23,8 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <new>
 #include <string>
 #include <vector>
@@ -391,10 +393,20 @@ dim3 vgrid(const aijhip_ksp *K, int64_t n) {
 }
 
 // PCSetUp_GAMG: host hierarchy, device operators / interpolations / vectors.
+// AIJHIP_GAMG_LOG=1 prints the phases (with gamg_setup.cpp's own).
 int gamg_setup(aijhip_ksp *K) {
     aijhip_mat *A = K->A;
     const int32_t m = A->m;
     const int64_t nz = A->nz;
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!log) return;
+        (void)hipDeviceSynchronize();
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "gamg device %-22s %8.3f s\n", what, std::chrono::duration<double>(t - t0).count());
+        t0 = t;
+    };
     std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nz);
     std::vector<double> aa((size_t)nz);
     hipError_t e;
@@ -402,11 +414,14 @@ int gamg_setup(aijhip_ksp *K) {
         (nz > 0 && ((e = hipMemcpy(aj.data(), A->d_aj, sizeof(int32_t) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess ||
                     (e = hipMemcpy(aa.data(), A->d_aa, sizeof(double) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess)))
         return khip(e, "GAMG: read operator");
+    lap("read operator");
     aijhip_gamg_host_t H = nullptr;
     int rc = aijhip_gamg_build_host(m, ai.data(), aj.data(), aa.data(), &K->gamg, &H);
     if (rc) return kfail(rc, "GAMG: host hierarchy set-up failed");
-    ai.clear(); aj.clear(); aa.clear();
-    ai.shrink_to_fit(); aj.shrink_to_fit(); aa.shrink_to_fit();
+    lap("host hierarchy");
+    ai = std::vector<int32_t>();
+    aj = std::vector<int32_t>();
+    aa = std::vector<double>();
     int32_t nl = 0;
     aijhip_gamg_host_num_levels(H, &nl);
     K->mg.assign((size_t)nl, MGLevel());
@@ -416,23 +431,21 @@ int gamg_setup(aijhip_ksp *K) {
         int64_t nnz_a = 0, nnz_p = 0;
         aijhip_gamg_host_level_info(H, l, &L.m, &nnz_a, &nnz_p, nullptr);
         L.nnz = nnz_a;
-        std::vector<int32_t> xi, xj;
-        std::vector<double> xa;
+        const int32_t *xi, *xj;
+        const double *xa;
         if (l == 0) {
             L.A = A;
         } else {
-            xi.resize((size_t)L.m + 1); xj.resize((size_t)nnz_a); xa.resize((size_t)nnz_a);
-            aijhip_gamg_host_get_A(H, l, xi.data(), xj.data(), xa.data());
-            rc = aijhip_mat_create(A->device, L.m, L.m, nnz_a, xi.data(), xj.data(), xa.data(), &L.A);
+            aijhip_gamg_host_view(H, l, 'A', &xi, &xj, &xa);
+            rc = aijhip_mat_create(A->device, L.m, L.m, nnz_a, xi, xj, xa, &L.A);
             L.own_A = rc == AIJHIP_OK;
             if (rc) break;
         }
         if (l + 1 < nl) {
             int32_t mc = 0;
             aijhip_gamg_host_level_info(H, l + 1, &mc, nullptr, nullptr, nullptr);
-            xi.resize((size_t)L.m + 1); xj.resize((size_t)nnz_p); xa.resize((size_t)nnz_p);
-            aijhip_gamg_host_get_P(H, l, xi.data(), xj.data(), xa.data());
-            rc = aijhip_mat_create(A->device, L.m, mc, nnz_p, xi.data(), xj.data(), xa.data(), &L.P);
+            aijhip_gamg_host_view(H, l, 'P', &xi, &xj, &xa);
+            rc = aijhip_mat_create(A->device, L.m, mc, nnz_p, xi, xj, xa, &L.P);
             if (rc) break;
         }
         const size_t vb = sizeof(double) * (size_t)std::max<int32_t>(L.m, 1);
@@ -444,9 +457,11 @@ int gamg_setup(aijhip_ksp *K) {
         if (L.m > 0)
             hipLaunchKernelGGL(k_diag_inv, dim3((unsigned)((L.m + 255) / 256)), dim3(256), 0, nullptr, L.m,
                                L.A->d_ai, L.A->d_aj, L.A->d_aa, L.dinv);
+        if (l < 2) lap(l == 0 ? "upload level 0" : "upload level 1");
     }
     aijhip_gamg_host_destroy(H);
     if (rc) return rc;
+    lap("upload coarse levels");
     // build every restriction (P^T) now, not inside the first solve
     for (int32_t l = 0; l + 1 < nl; ++l) {
         MGLevel &L = K->mg[l];
@@ -454,6 +469,7 @@ int gamg_setup(aijhip_ksp *K) {
         if (rc) return rc;
     }
     if ((e = hipDeviceSynchronize()) != hipSuccess) return khip(e, "GAMG set-up");
+    lap("restrictions P^T");
     return AIJHIP_OK;
 }
 

@@ -12,7 +12,7 @@ _pkg = importlib.import_module("petsc-openacc_amd")
 GAMG_SYMBOLS = (
     "aijhip_gamg_params_default", "aijhip_gamg_build_host", "aijhip_gamg_host_num_levels",
     "aijhip_gamg_host_level_info", "aijhip_gamg_host_get_A", "aijhip_gamg_host_get_P",
-    "aijhip_gamg_host_get_aggregates", "aijhip_gamg_host_destroy",
+    "aijhip_gamg_host_get_aggregates", "aijhip_gamg_host_view", "aijhip_gamg_host_destroy",
 )
 
 

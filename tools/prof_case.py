@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""One workload per process, for `rocprofv3 --kernel-trace --stats -- python3
+tools/prof_case.py CASE`: the per-kernel breakdown of a case the bench line
+only reports as a total.
+
+    gamg      CG + GAMG solve at --grid^3 (reference options), after set-up
+    jacobi    --its CG + Jacobi iterations at --grid^3
+    skewed    --its SpMVs of the Flan_1565 stand-in (default kernel)
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("case", choices=["gamg", "jacobi", "skewed"])
+    ap.add_argument("--grid", type=int, default=300)
+    ap.add_argument("--its", type=int, default=50)
+    ap.add_argument("--kernel", default="auto")
+    args = ap.parse_args()
+    pkg = importlib.import_module("petsc-openacc_amd")
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    dev = torch.device("cuda:0")
+    if args.case == "skewed":
+        ai, aj, aa = pkg.skewed_csr()
+        A = pkg.SeqAIJHIP(ai, aj, aa, kernel=args.kernel)
+        x = torch.from_numpy(pkg.splitmix_uniform(A.n, 42)).to(dev)
+        y = torch.empty(A.m, dtype=torch.float64, device=dev)
+        for _ in range(args.its):
+            A.mult(x, y)
+        torch.cuda.synchronize()
+        print("skewed", A.info())
+        return
+    G = args.grid
+    ai, aj, aa = pkg.poisson_csr(G)
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    rhs, _ = pkg.poisson_vectors(G)
+    b = torch.from_numpy(rhs).to(dev)
+    x = torch.zeros_like(b)
+    if args.case == "gamg":
+        ksp = K.KSPCG(A, rtol=1e-14, atol=1e-12, pc="gamg")
+    else:
+        ksp = K.KSPCG(A, rtol=0.0, atol=0.0, max_it=args.its)
+    t0 = time.perf_counter()
+    ksp.set_up()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    ksp.solve(b, x)
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    print(f"{args.case}: set-up {t1 - t0:.3f} s, solve {t2 - t1:.4f} s, its {ksp.its}, reason {ksp.reason}")
+    ksp.destroy()
+    A.destroy()
+
+
+if __name__ == "__main__":
+    main()
