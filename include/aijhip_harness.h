@@ -21,6 +21,8 @@
 
 #include <stdint.h>
 
+#include "aijhip.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -61,6 +63,29 @@ int aijhip_split_rows(int32_t m, const int32_t *ai, const int32_t *aj, const dou
                       int32_t col_lo, int32_t col_hi, int64_t *nz_d, int64_t *nz_o,
                       int32_t *n_garray, int32_t *d_ai, int32_t *d_aj, double *d_aa,
                       int32_t *o_ai, int32_t *o_aj, double *o_aa, int32_t *garray);
+
+/* ---- Device-side producers: the same operand and vectors
+ * written straight into device memory, bit-identical to the host producers
+ * above. Arrays are device pointers sized as for aijhip_poisson_fill /
+ * _vectors; `stream` is a hipStream_t (NULL = default stream); the calls are
+ * asynchronous on it except where noted. */
+
+/* Device generateA + setRefPoint into d_ai[mloc+1], d_aj[nnz], d_aa[nnz]
+ * (nnz from aijhip_poisson_nnz); *scale as aijhip_poisson_fill. */
+int aijhip_poisson_fill_device(int32_t nx, int32_t ny, int32_t nz, int32_t z0, int32_t z1,
+                               int ref_point, int32_t *d_ai, int32_t *d_aj, double *d_aa,
+                               double *scale, void *stream);
+
+/* Device generateRHS / generateExt (+ setRefPoint's rhs update); either
+ * pointer may be NULL. Returns after the work on `stream` is done. */
+int aijhip_poisson_vectors_device(int32_t nx, int32_t ny, int32_t nz, int32_t z0, int32_t z1,
+                                  int ref_point, double *d_rhs, double *d_exact, void *stream);
+
+/* Assemble the slab operator on `device` and return it as a SeqAIJ handle
+ * (aijhip_mat_create_from_device on the assembled arrays): no host CSR, no
+ * PCIe upload of the matrix. Columns are global (n = nx*ny*nz). */
+int aijhip_mat_create_poisson(int device, int32_t nx, int32_t ny, int32_t nz, int32_t z0,
+                              int32_t z1, int ref_point, double *scale, aijhip_mat_t *out);
 
 #ifdef __cplusplus
 }

@@ -37,6 +37,7 @@ ABI_SYMBOLS = (
 HARNESS_SYMBOLS = (
     "aijhip_poisson_nnz", "aijhip_poisson_fill", "aijhip_poisson_vectors",
     "aijhip_splitmix_uniform", "aijhip_skewed_csr", "aijhip_split_rows",
+    "aijhip_poisson_fill_device", "aijhip_poisson_vectors_device", "aijhip_mat_create_poisson",
 )
 
 
@@ -102,6 +103,10 @@ def lib() -> ctypes.CDLL:
         L.aijhip_poisson_vectors.argtypes = [ctypes.c_int32] * 5 + [ctypes.c_int, _P, _P]
         L.aijhip_splitmix_uniform.argtypes = [ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64, _P]
         L.aijhip_skewed_csr.argtypes = [ctypes.c_int32, ctypes.c_uint64, _I64P, _P, _P, _P]
+        L.aijhip_poisson_fill_device.argtypes = [ctypes.c_int32] * 5 + [ctypes.c_int, _P, _P, _P, _F64P, _P]
+        L.aijhip_poisson_vectors_device.argtypes = [ctypes.c_int32] * 5 + [ctypes.c_int, _P, _P, _P]
+        L.aijhip_mat_create_poisson.argtypes = [ctypes.c_int] + [ctypes.c_int32] * 5 + [ctypes.c_int, _F64P,
+                                                                                         ctypes.POINTER(_P)]
         L.aijhip_split_rows.argtypes = [ctypes.c_int32, _P, _P, _P, ctypes.c_int32, ctypes.c_int32,
                                         _I64P, _I64P, _I32P, _P, _P, _P, _P, _P, _P, _P]
         _lib = L
@@ -145,6 +150,32 @@ def device_count() -> int:
     return c.value if rc == AIJHIP_OK else 0
 
 
+def poisson_device(nx: int, ny: int | None = None, nz: int | None = None, z0: int = 0, z1: int | None = None,
+                   ref_point: bool = True, device: int = 0):
+    """The helper.cpp operand assembled on the device (aijhip_mat_create_poisson):
+    returns (SeqAIJHIP, setRefPoint scale) with no host CSR."""
+    ny = nx if ny is None else ny
+    nz = nx if nz is None else nz
+    z1 = nz if z1 is None else z1
+    h = _P()
+    sc = ctypes.c_double()
+    _check(lib().aijhip_mat_create_poisson(device, nx, ny, nz, z0, z1, int(ref_point), ctypes.byref(sc),
+                                           ctypes.byref(h)))
+    return SeqAIJHIP(None, None, None, device=device, _handle=h), sc.value
+
+
+def poisson_vectors_device(nx: int, ny: int | None = None, nz: int | None = None, z0: int = 0,
+                           z1: int | None = None, ref_point: bool = True, rhs=None, exact=None, stream=None):
+    """generateRHS / generateExt on the device into float64 GPU tensors."""
+    ny = nx if ny is None else ny
+    nz = nx if nz is None else nz
+    z1 = nz if z1 is None else z1
+    mloc = (z1 - z0) * nx * ny
+    _check(lib().aijhip_poisson_vectors_device(
+        nx, ny, nz, z0, z1, int(ref_point), _dev_ptr(rhs, mloc, "rhs") if rhs is not None else None,
+        _dev_ptr(exact, mloc, "exact") if exact is not None else None, _stream_handle(stream)))
+
+
 class SeqAIJHIP:
     """A device-resident SeqAIJ matrix: the Mat the reference's patches act on.
 
@@ -154,7 +185,12 @@ class SeqAIJHIP:
     """
 
     def __init__(self, ai, aj, aa, ncols: int | None = None, device: int = 0, kernel: str = "auto",
-                 lanes: int = 0, **options):
+                 lanes: int = 0, _handle=None, **options):
+        if _handle is not None:  # adopt a handle made on the device (poisson_device)
+            self._h = _handle
+            inf = self.info()
+            self.m, self.n, self.nz, self.device = inf["m"], inf["n"], inf["nz"], device
+            return
         ai = np.ascontiguousarray(ai, dtype=np.int32)
         aj = np.ascontiguousarray(aj, dtype=np.int32)
         aa = np.ascontiguousarray(aa, dtype=np.float64)

@@ -97,14 +97,14 @@ int validate_csr(int32_t m, int32_t n, int64_t nz, const int32_t *ai, const int3
     if (m < 0 || n < 0 || nz < 0) return fail(AIJHIP_ERR_ARG, "negative size");
     if (nz > INT32_MAX) return fail(AIJHIP_ERR_ARG, "nz exceeds the int32 PetscInt range");
     if (!ai) return fail(AIJHIP_ERR_ARG, "ai is NULL");
-    if (nz > 0 && !aj) return fail(AIJHIP_ERR_ARG, "aj is NULL");
     if (ai[0] != 0) return fail(AIJHIP_ERR_ARG, "ai[0] != 0");
     for (int32_t i = 0; i < m; ++i)
         if (ai[i + 1] < ai[i]) return fail(AIJHIP_ERR_ARG, "ai is not monotone at row " + std::to_string(i));
     if (ai[m] != nz) return fail(AIJHIP_ERR_ARG, "ai[m] != nz");
-    for (int64_t k = 0; k < nz; ++k)
-        if ((uint32_t)aj[k] >= (uint32_t)n)
-            return fail(AIJHIP_ERR_ARG, "column index out of range at entry " + std::to_string(k));
+    if (aj)  // host columns; device columns are checked by aijhip::count_bad_columns
+        for (int64_t k = 0; k < nz; ++k)
+            if ((uint32_t)aj[k] >= (uint32_t)n)
+                return fail(AIJHIP_ERR_ARG, "column index out of range at entry " + std::to_string(k));
     return AIJHIP_OK;
 }
 
@@ -234,8 +234,9 @@ int plan_build(aijhip_mat *A) {
     }
 }
 
-// Uploads a validated host CSR into A (sizes already set) and plans it.
-int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const double *aa) {
+// Uploads a validated CSR into A (sizes already set) and plans it. ai is on
+// the host; aj/aa on the host, or on the device when dev_src (copied D2D).
+int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const double *aa, bool dev_src = false) {
     const int32_t m = A->m;
     const int64_t nz = A->nz;
     hipError_t e;
@@ -261,9 +262,10 @@ int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const d
         (e = hipMemset(A->d_aj + nz, 0, 2 * sizeof(int32_t))) != hipSuccess ||
         (e = hipMemset(A->d_aa + nz, 0, 2 * sizeof(double))) != hipSuccess)
         return hipfail(e, "upload ai");
+    const hipMemcpyKind kind = dev_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
     if (nz > 0 &&
-        ((e = hipMemcpy(A->d_aj, aj, sizeof(int32_t) * (size_t)nz, hipMemcpyHostToDevice)) != hipSuccess ||
-         (e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)nz, hipMemcpyHostToDevice)) != hipSuccess))
+        ((e = hipMemcpy(A->d_aj, aj, sizeof(int32_t) * (size_t)nz, kind)) != hipSuccess ||
+         (e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)nz, kind)) != hipSuccess))
         return hipfail(e, "upload aj/aa");
     if (A->compressed) {
         std::vector<int32_t> cai, ridx;
@@ -309,10 +311,11 @@ int mult_impl(aijhip_mat_t A, const double *x, const double *z, double *y, bool 
 }
 
 int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
-                const int32_t *aj, const double *aa, aijhip_mat_t *out) {
+                const int32_t *aj, const double *aa, aijhip_mat_t *out, bool dev_src = false) {
     if (!out) return fail(AIJHIP_ERR_ARG, "out is NULL");
     *out = nullptr;
-    int rc = validate_csr(m, n, nz, ai, aj);
+    if (nz > 0 && !aj) return fail(AIJHIP_ERR_ARG, "aj is NULL");
+    int rc = validate_csr(m, n, nz, ai, dev_src ? nullptr : aj);
     if (rc) return rc;
     if (nz > 0 && !aa) return fail(AIJHIP_ERR_ARG, "aa is NULL");
     int count = 0;
@@ -330,7 +333,13 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
         A->n_cu = cus;
-    rc = upload_and_plan(A, ai, aj, aa);
+    if (dev_src && nz > 0) {
+        int64_t bad = 0;
+        hipError_t e = aijhip::count_bad_columns(aj, nz, n, &bad);
+        if (e != hipSuccess) rc = hipfail(e, "check device columns");
+        else if (bad) rc = fail(AIJHIP_ERR_ARG, std::to_string(bad) + " column indices out of range");
+    }
+    if (!rc) rc = upload_and_plan(A, ai, aj, aa, dev_src);
     if (rc) {
         free_matrix(A);
         delete A;
@@ -374,19 +383,16 @@ int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
     if (!out) return fail(AIJHIP_ERR_ARG, "out is NULL");
     if (m < 0 || n < 0 || nz < 0 || !d_ai || (nz > 0 && (!d_aj || !d_aa)))
         return fail(AIJHIP_ERR_ARG, "bad size or NULL array");
-    // Planning and validation read the structure on the host.
-    std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nz);
-    std::vector<double> aa((size_t)nz);
+    // Planning reads the row offsets on the host (m+1 ints); the columns are
+    // range-checked on the device and aj/aa are copied device to device.
+    std::vector<int32_t> ai((size_t)m + 1);
     {
         DeviceGuard g(device);
         if (g.err != hipSuccess) return hipfail(g.err, "set device");
-        hipError_t e;
-        if ((e = hipMemcpy(ai.data(), d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
-            (nz > 0 && ((e = hipMemcpy(aj.data(), d_aj, sizeof(int32_t) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess ||
-                        (e = hipMemcpy(aa.data(), d_aa, sizeof(double) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess)))
-            return hipfail(e, "read device CSR");
+        hipError_t e = hipMemcpy(ai.data(), d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hipfail(e, "read device row offsets");
     }
-    return create_impl(device, m, n, nz, ai.data(), aj.data(), aa.data(), out);
+    return create_impl(device, m, n, nz, ai.data(), d_aj, d_aa, out, true);
 }
 
 int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes) {

@@ -166,6 +166,8 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
                            double **d_taa, hipStream_t s);
 
 RowList row_list(const aijhip_mat &A);
+// Number of device column indices outside [0, n) (synchronous).
+hipError_t count_bad_columns(const int32_t *d_aj, int64_t nz, int32_t n, int64_t *bad);
 
 // Sets the calling thread's aijhip_last_error() message.
 void set_error(const std::string &msg);

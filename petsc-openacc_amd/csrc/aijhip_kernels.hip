@@ -533,6 +533,30 @@ inline unsigned grid_for(int64_t n, int threads) {
 
 }  // namespace
 
+namespace {
+__global__ void k_count_bad_columns(const int32_t *__restrict__ aj, int64_t nz, int32_t n,
+                                    unsigned long long *bad) {
+    unsigned long long c = 0;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nz; k += (int64_t)gridDim.x * blockDim.x)
+        c += (uint32_t)aj[k] >= (uint32_t)n;
+    if (c) atomicAdd(bad, c);
+}
+}  // namespace
+
+hipError_t count_bad_columns(const int32_t *d_aj, int64_t nz, int32_t n, int64_t *bad) {
+    unsigned long long *d = nullptr, h = 0;
+    hipError_t e = hipMalloc(&d, sizeof(*d));
+    if (e != hipSuccess) return e;
+    if ((e = hipMemset(d, 0, sizeof(*d))) == hipSuccess) {
+        hipLaunchKernelGGL(k_count_bad_columns, dim3(4096), dim3(256), 0, nullptr, d_aj, nz, n, d);
+        if ((e = hipGetLastError()) == hipSuccess)
+            e = hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost);
+    }
+    hipFree(d);
+    *bad = (int64_t)h;
+    return e;
+}
+
 RowList row_list(const aijhip_mat &A) {
     if (A.compressed) return RowList{A.n_crow, A.d_cai, A.d_ridx};
     return RowList{A.m, A.d_ai, nullptr};

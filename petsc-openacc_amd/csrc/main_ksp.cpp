@@ -7,7 +7,7 @@
 //            [-ksp_rtol R] [-ksp_atol A] [-ksp_max_it K] [-pc_type jacobi|none|gamg]
 //            [-ksp_norm_type preconditioned|unpreconditioned|natural]
 //            [-pc_gamg_threshold T] [-pc_gamg_agg_nsmooths S]
-//            [-pc_gamg_coarse_eq_limit C] [-pc_mg_levels L]
+//            [-pc_gamg_coarse_eq_limit C] [-pc_mg_levels L] [-aijhip_host_assembly]
 //
 // Options come from the command line and from a PETSc options file
 // (`-key value` per line, '#' comments; PetscOptionsInsertFile,
@@ -130,22 +130,32 @@ int main(int argc, char **argv) {
                          : nts == "none"           ? AIJHIP_KSP_NORM_NONE
                                                    : AIJHIP_KSP_NORM_PRECONDITIONED;
 
-    // -------- createSystem (helper.cpp:22-57) + device upload
+    // -------- createSystem (helper.cpp:22-57): assembled on the device
+    // (csrc/poisson.hip), or on the host and uploaded with -aijhip_host_assembly
+    const bool host_asm = opt.count("-aijhip_host_assembly") > 0;
     const double t_start = now();
-    int64_t nnz = 0;
-    CHK(aijhip_poisson_nnz(nx, ny, nz, 0, nz, &nnz));
     const int64_t m = (int64_t)nx * ny * nz;
-    std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nnz);
-    std::vector<double> aa((size_t)nnz), rhs((size_t)m), exact((size_t)m);
-    double scale = 0.0;
-    CHK(aijhip_poisson_fill(nx, ny, nz, 0, nz, 1, ai.data(), aj.data(), aa.data(), &scale));
-    CHK(aijhip_poisson_vectors(nx, ny, nz, 0, nz, 1, rhs.data(), exact.data()));
+    std::vector<double> exact((size_t)m);
     aijhip_mat_t A = nullptr;
-    CHK(aijhip_mat_create(0, (int32_t)m, (int32_t)m, nnz, ai.data(), aj.data(), aa.data(), &A));
     double *d_b = nullptr, *d_x = nullptr;
     HCHK(hipMalloc(&d_b, sizeof(double) * (size_t)m));
     HCHK(hipMalloc(&d_x, sizeof(double) * (size_t)m));
-    HCHK(hipMemcpy(d_b, rhs.data(), sizeof(double) * (size_t)m, hipMemcpyHostToDevice));
+    if (host_asm) {
+        int64_t nnz = 0;
+        CHK(aijhip_poisson_nnz(nx, ny, nz, 0, nz, &nnz));
+        std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nnz);
+        std::vector<double> aa((size_t)nnz), rhs((size_t)m);
+        double scale = 0.0;
+        CHK(aijhip_poisson_fill(nx, ny, nz, 0, nz, 1, ai.data(), aj.data(), aa.data(), &scale));
+        CHK(aijhip_poisson_vectors(nx, ny, nz, 0, nz, 1, rhs.data(), exact.data()));
+        CHK(aijhip_mat_create(0, (int32_t)m, (int32_t)m, nnz, ai.data(), aj.data(), aa.data(), &A));
+        HCHK(hipMemcpy(d_b, rhs.data(), sizeof(double) * (size_t)m, hipMemcpyHostToDevice));
+    } else {
+        double scale = 0.0;
+        CHK(aijhip_mat_create_poisson(0, nx, ny, nz, 0, nz, 1, &scale, &A));
+        CHK(aijhip_poisson_vectors_device(nx, ny, nz, 0, nz, 1, d_b, d_x, nullptr));
+        HCHK(hipMemcpy(exact.data(), d_x, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost));
+    }
     HCHK(hipMemset(d_x, 0, sizeof(double) * (size_t)m));  // VecSet(lhs, 0) (helper.cpp:48)
     HCHK(hipDeviceSynchronize());
     const double t_sys = now();

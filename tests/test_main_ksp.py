@@ -80,3 +80,18 @@ def test_driver_refuses_unsupported_mg_smoother(pkg):
     r = subprocess.run([str(exe), "-pc_type", "gamg", "-mg_levels_ksp_type", "chebyshev", "-da_grid_x", "4"],
                        capture_output=True, text=True, timeout=60)
     assert r.returncode == 1 and "chebyshev not supported" in r.stderr
+
+
+@pytest.mark.gpu
+def test_driver_device_and_host_assembly_agree(pkg):
+    import importlib
+    exe = importlib.import_module("petsc-openacc_amd.build").build_main_ksp()
+    outs = []
+    for extra in ([], ["-aijhip_host_assembly"]):
+        r = subprocess.run([str(exe), "-config", str(ROOT / "configs" / "cg_jacobi.info"), "-da_grid_x", "18",
+                            "-da_grid_y", "14", "-da_grid_z", "11"] + extra, capture_output=True, text=True,
+                           timeout=300)
+        assert r.returncode == 0, r.stderr
+        m = BLOCK.search(r.stdout)
+        outs.append(m.groups()[:6])
+    assert outs[0] == outs[1]
