@@ -148,6 +148,15 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z,
 bool stream_dot_fusable(const aijhip_mat &A);
 hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, double *dpart,
                              const int *stop, hipStream_t s);
+// Fused V-cycle smoothing SpMVs on a STREAM plan (same conditions as
+// stream_dot_fusable): pre-smoothing x = D^-1 b with r = b - A x, and one
+// Richardson+Jacobi step x = t + D^-1 (b - A t) (x != t) with optional
+// z.z / z.b partials (2 x n_blocks) for CG on the finest level.
+bool stream_mg_fusable(const aijhip_mat &A);
+hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
+                         hipStream_t s);
+hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
+                          double *dpart, hipStream_t s);
 // Dispatch y = A x (or w = z + A x) through the handle's plan.
 hipError_t launch_mult(const aijhip_mat &A, const double *x, const double *z, double *y,
                        bool add, hipStream_t s);

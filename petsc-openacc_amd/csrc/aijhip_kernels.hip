@@ -93,12 +93,70 @@ __device__ __forceinline__ double block_sum(double v, double *scratch) {
     return s;  // valid in thread 0
 }
 
-template <int T, int CAP, int RPT, bool ADD, bool CROW, bool XCD, bool NT, bool CLAMPED>
+// What a STREAM launch gathers and writes. The row sum s_i = sum a_ij g(j)
+// is formed in PETSc's order (or the deterministic multi-lane order); `seed`
+// starts it (MatMultAdd's z_i), `put` stores the row's result and adds to
+// the block's dot partials d[0..kDots).
+template <bool ADD>
+struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
+    static constexpr int kDots = 1;
+    static constexpr bool kSeeded = ADD;
+    const double *x, *z;
+    double *y;
+    bool dot;
+    __device__ double gx(int32_t j) const { return x[j]; }
+    __device__ double seed(int o) const { return ADD ? z[o] : 0.0; }
+    __device__ void put(int o, double v, double *d) const {
+        y[o] = v;
+        if (dot) d[0] += x[o] * v;
+    }
+};
+
+// V-cycle pre-smoothing from a zero guess fused with the residual
+// (ksp.hip k_jacobi + SpMV + k_resid, same roundings): x = D^-1 b is gathered
+// as dinv_j * b_j, and each row stores x_i and r_i = b_i + (-1) (A x)_i.
+struct OpMgPre {
+    static constexpr int kDots = 0;
+    static constexpr bool kSeeded = false;
+    const double *b, *dinv;
+    double *x, *r;
+    __device__ double gx(int32_t j) const { return dinv[j] * b[j]; }
+    __device__ double seed(int) const { return 0.0; }
+    __device__ void put(int o, double v, double *) const {
+        const double bo = b[o];
+        x[o] = dinv[o] * bo;
+        r[o] = bo + (-1.0) * v;
+    }
+};
+
+// V-cycle post-smoothing, one Richardson step with Jacobi from the guess t
+// (SpMV + k_richardson): x_i = t_i + 1.0 (dinv_i (b_i + (-1) (A t)_i)); x
+// must not alias t. With dot, the finest level also yields CG's z.z and z.b
+// partials (z = x, b = CG's residual).
+struct OpMgPost {
+    static constexpr int kDots = 2;
+    static constexpr bool kSeeded = false;
+    const double *t, *b, *dinv;
+    double *x;
+    bool dot;
+    __device__ double gx(int32_t j) const { return t[j]; }
+    __device__ double seed(int) const { return 0.0; }
+    __device__ void put(int o, double v, double *d) const {
+        const double bo = b[o];
+        const double xo = t[o] + 1.0 * (dinv[o] * (bo + (-1.0) * v));
+        x[o] = xo;
+        if (dot) {
+            d[0] += xo * xo;
+            d[1] += xo * bo;
+        }
+    }
+};
+
+template <int T, int CAP, int RPT, bool CROW, bool XCD, bool NT, bool CLAMPED, class Op>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, const double *__restrict__ x,
-    const double *z, double *y, double *dpart, const int *stop) {
+    const double *__restrict__ aa, Op op, double *dpart, const int *stop) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
     if (stop && *stop) return;  // CG launched past convergence: no work
@@ -116,7 +174,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
         rs[q] = rai[r];
         re[q] = rai[r + 1];
         orow[q] = CROW ? ridx[r] : r;
-        sum[q] = ADD ? z[orow[q]] : 0.0;
+        sum[q] = op.seed(orow[q]);
     }
 
     // Phase 1: coalesced 16-B loads of aa and 8-B loads of aj from an even
@@ -139,8 +197,8 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (CLAMPED || k < k1) {
-            xv[it].x = x[cv[it].x];
-            xv[it].y = x[cv[it].y];
+            xv[it].x = op.gx(cv[it].x);
+            xv[it].y = op.gx(cv[it].y);
         }
     }
     // products into LDS; only the stores are predicated
@@ -159,7 +217,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     // (strided partial sums + __shfl_xor tree; reordered, deterministic), so
     // a block of few long rows does not leave most lanes idle on a serial
     // LDS chain. `exact` forces the sequential form everywhere.
-    double dotv = 0.0;
+    double dv[Op::kDots > 0 ? Op::kDots : 1] = {};
     const int nr = d.nrows;
     int L = 1;
     if (RPT == 1 && !exact && d.nk > kSplitMinMean * nr) {
@@ -172,8 +230,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             if (t + q * T < nr) {
                 double s = sum[q];
                 for (int32_t k = rs[q]; k < re[q]; ++k) s += prod[k - k0];
-                y[orow[q]] = s;
-                if (dpart) dotv += x[orow[q]] * s;
+                op.put(orow[q], s, dv);
             }
         }
     } else {
@@ -187,16 +244,17 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
         for (int off = L >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
         if (own && j == 0) {
             const int o = CROW ? ridx[r] : r;
-            const double v = ADD ? z[o] + s : s;
-            y[o] = v;
-            if (dpart) dotv += x[o] * v;
+            op.put(o, Op::kSeeded ? op.seed(o) + s : s, dv);
         }
     }
-    // Optional fused epilogue for CG (grid-uniform branch): the block's
-    // partial of x . y, written to dpart[b] for a fixed-order final sum.
-    if (dpart) {
-        const double v = block_sum<T>(dotv, prod);
-        if (t == 0) dpart[b] = v;
+    // Optional fused epilogue (grid-uniform branch): the block's dot
+    // partials, written to dpart[q * nblk + b] for a fixed-order final sum.
+    if (Op::kDots > 0 && dpart) {
+#pragma unroll
+        for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
+            const double v = block_sum<T>(dv[q], prod);
+            if (t == 0) dpart[(int64_t)q * nblk + b] = v;
+        }
     }
 }
 
@@ -577,11 +635,10 @@ static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double 
                             const int *stop) {
     const Plan &P = A.plan;
 #define AIJHIP_SL(ADD, CROW, XCD, NT, CL)                                                          \
-    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, ADD, CROW, XCD, NT, CL>), dim3(P.n_blocks),    \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, XCD, NT, CL, OpMult<ADD>>), dim3(P.n_blocks), \
                        dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, (int)P.tune.exact,   \
-                       L.rai, L.ridx,                                                              \
-                       A.d_aj, A.d_aa,                                                             \
-                       x, z, y, dpart, stop);                                                      \
+                       L.rai, L.ridx, A.d_aj, A.d_aa,                                              \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop);                      \
     return
     // The speed knobs (XCD remap, non-temporal, clamped loads) are compiled
     // for the plain full-row MatMult, the benchmarked path; MatMultAdd and
@@ -640,6 +697,39 @@ hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, do
                              const int *stop, hipStream_t s) {
     if (!stream_dot_fusable(A)) return hipErrorInvalidValue;
     return launch_stream(A, x, nullptr, y, false, s, dpart, stop);
+}
+
+bool stream_mg_fusable(const aijhip_mat &A) { return stream_dot_fusable(A); }
+
+template <class Op>
+static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dpart, hipStream_t s) {
+    if (!stream_mg_fusable(A)) return hipErrorInvalidValue;
+    const Plan &P = A.plan;
+    if (P.n_blocks == 0) return hipSuccess;
+    static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
+#define AIJHIP_OG(G)                                                                                      \
+    case G:                                                                                               \
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
+                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, 0, (int)P.tune.exact, \
+                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, nullptr);                          \
+        break
+    switch (P.tune.geom) {
+        AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
+        AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8);
+        default: return hipErrorInvalidValue;
+    }
+#undef AIJHIP_OG
+    return hipGetLastError();
+}
+
+hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
+                         hipStream_t s) {
+    return launch_stream_op(A, OpMgPre{b, dinv, x, r}, nullptr, s);
+}
+
+hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
+                          double *dpart, hipStream_t s) {
+    return launch_stream_op(A, OpMgPost{t, b, dinv, x, dpart != nullptr}, dpart, s);
 }
 
 hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, double *y,

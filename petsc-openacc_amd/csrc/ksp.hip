@@ -68,9 +68,23 @@ __device__ __forceinline__ double bsum(double v, double *scratch) {
 }
 
 // Sum of part[0..n) in a fixed order by one 1024-lane block (valid in lane 0).
+// Each lane adds part[j], part[j + 1024], ... in that order; the loads of 8
+// strides are issued together (a long partial list, e.g. one per STREAM
+// block, is otherwise latency-bound), the adds keep the order.
 __device__ double reduce_parts(const double *part, int n, double *scratch) {
+    constexpr int U = 8;
     double s = 0.0;
-    for (int j = threadIdx.x; j < n; j += kRedThreads) s += part[j];
+    for (int j0 = threadIdx.x; j0 < n; j0 += U * kRedThreads) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int j = j0 + u * kRedThreads;
+            v[u] = j < n ? part[j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j0 + u * kRedThreads < n) s += v[u];
+    }
     return bsum<kRedThreads>(s, scratch);
 }
 
@@ -263,13 +277,15 @@ __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *x, co
 }
 
 // K5: dp, convergence test at n = i + 1, beta, top-of-loop checks of i + 1.
-__global__ __launch_bounds__(kRedThreads) void k_reduce_iter(const double *part, int nb, CGState *S,
-                                                             double *hist, CGParams p) {
+// zz, zr come from pz[0, nbz) and pz[nbz, 2 nbz) (the vector kernels' slots 0
+// and 1, or the fused V-cycle's finest post-smoothing); rr from pr[0, nbr).
+__global__ __launch_bounds__(kRedThreads) void k_reduce_iter(const double *pz, int nbz, const double *pr, int nbr,
+                                                             CGState *S, double *hist, CGParams p) {
     __shared__ double scratch[kRedThreads / 64];
     if (S->done) return;
-    const double zz = reduce_parts(part + 0 * nb, nb, scratch);
-    const double zr = reduce_parts(part + 1 * nb, nb, scratch);
-    const double rr = reduce_parts(part + 2 * nb, nb, scratch);
+    const double zz = reduce_parts(pz, nbz, scratch);
+    const double zr = reduce_parts(pz + nbz, nbz, scratch);
+    const double rr = reduce_parts(pr, nbr, scratch);
     if (threadIdx.x != 0) return;
     CGState s = *S;
     s.dp = norm_of(p, zz, rr, zr);
@@ -325,6 +341,7 @@ struct MGLevel {
     aijhip_mat *A = nullptr;  // level 0: borrowed
     aijhip_mat *P = nullptr;  // interpolation from level l+1 (owned)
     bool own_A = false;
+    bool fused = false;       // smoothing passes fused into STREAM launches
     int32_t m = 0;
     int64_t nnz = 0;
     double *dinv = nullptr, *b = nullptr, *x = nullptr, *r = nullptr;
@@ -349,6 +366,7 @@ struct aijhip_ksp {
     CGState *d_state = nullptr;
     CGState *h_state = nullptr;  // pinned
     std::vector<MGLevel> mg;     // GAMG levels, finest first
+    double *d_mgpart = nullptr;  // fused finest-level z.z / z.r partials
     double setup_seconds = 0.0;
     int32_t its = 0;
     int reason = 0;
@@ -365,6 +383,8 @@ void mg_free(aijhip_ksp *K) {
         hipFree(L.dinv); hipFree(L.b); hipFree(L.x); hipFree(L.r);
     }
     K->mg.clear();
+    hipFree(K->d_mgpart);
+    K->d_mgpart = nullptr;
 }
 
 void ksp_free(aijhip_ksp *K) {
@@ -468,35 +488,61 @@ int gamg_setup(aijhip_ksp *K) {
         rc = aijhip_mat_mult_transpose(L.P, L.r, K->mg[l + 1].b, nullptr);
         if (rc) return rc;
     }
+    for (MGLevel &L : K->mg) L.fused = !std::getenv("AIJHIP_MG_UNFUSED") && aijhip::stream_mg_fusable(*L.A);
+    if (K->mg[0].fused &&
+        (e = hipMalloc(&K->d_mgpart, sizeof(double) * 2 * (size_t)std::max(1, K->mg[0].A->plan.n_blocks))) !=
+            hipSuccess)
+        return khip(e, "GAMG partials");
     if ((e = hipDeviceSynchronize()) != hipSuccess) return khip(e, "GAMG set-up");
     lap("restrictions P^T");
     return AIJHIP_OK;
 }
 
 // PCApply_MG (multiplicative, one V-cycle) on the finest-level input b,
-// output x.
-hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s) {
+// output x. On STREAM-planned levels the smoothing passes ride in the SpMV
+// (aijhip::launch_mg_pre / _post): pre-smoothing + residual is one launch,
+// and interpolation writes t = x + P x_c to the level's scratch so the
+// post-smoothing launch reads t and writes x. With dots != NULL the finest
+// post-smoothing also leaves z.z / z.b partials there (*dots_done = true).
+hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, double *dots = nullptr,
+                  bool *dots_done = nullptr) {
     const int nl = (int)K->mg.size();
     hipError_t e = hipSuccess;
+    if (dots_done) *dots_done = false;
     auto B = [&](int l) { return l == 0 ? b0 : (const double *)K->mg[l].b; };
     auto X = [&](int l) { return l == 0 ? x0 : K->mg[l].x; };
     for (int l = 0; l < nl; ++l) {
         MGLevel &L = K->mg[l];
         const dim3 g = vgrid(K, L.m), t(kVecThreads);
-        hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));  // smoothd / coarse
-        if (l == nl - 1) break;
-        if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_resid, g, t, 0, s, (int64_t)L.m, B(l), L.r);
+        if (l == nl - 1) {  // coarse: preonly + Jacobi
+            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));
+            break;
+        }
+        if (L.fused) {
+            if ((e = aijhip::launch_mg_pre(*L.A, B(l), L.dinv, X(l), L.r, s)) != hipSuccess) return e;
+        } else {
+            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));  // smoothd
+            if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_resid, g, t, 0, s, (int64_t)L.m, B(l), L.r);
+        }
         if ((e = aijhip::launch_mult(*L.P->transpose, L.r, nullptr, K->mg[l + 1].b, false, s)) != hipSuccess)
             return e;  // MatRestrict = P^T r
     }
     for (int l = nl - 2; l >= 0; --l) {
         MGLevel &L = K->mg[l];
         const dim3 g = vgrid(K, L.m), t(kVecThreads);
-        // MatInterpolateAdd: x = x + P x_c
-        if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), X(l), true, s)) != hipSuccess) return e;
-        if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_richardson, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l));  // smoothu
+        if (L.fused) {
+            // MatInterpolateAdd into the scratch: t = x + P x_c, then smoothu
+            if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), L.r, true, s)) != hipSuccess) return e;
+            double *dp = (l == 0 && dots) ? dots : nullptr;
+            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s)) != hipSuccess) return e;
+            if (dp && dots_done) *dots_done = true;
+        } else {
+            // MatInterpolateAdd: x = x + P x_c
+            if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), X(l), true, s)) != hipSuccess) return e;
+            if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_richardson, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l));  // smoothu
+        }
     }
     return hipGetLastError();
 }
@@ -666,11 +712,22 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             }
             hipLaunchKernelGGL(k_update, vg, vt, 0, s, m, x, K->d_p, K->d_r, K->d_z, K->d_dinv, K->d_part,
                                K->d_state, K->pc);
+            const double *pz = K->d_part;
+            int nbz = nb;
             if (gamg && e == hipSuccess) {
-                e = vcycle(K, K->d_r, K->d_z, s);
-                hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
+                // z = B r; z.z and z.r come from the finest post-smoothing
+                // when it is fused, else from k_dots
+                bool dots = false;
+                e = vcycle(K, K->d_r, K->d_z, s, K->d_mgpart, &dots);
+                if (dots) {
+                    pz = K->d_mgpart;
+                    nbz = K->mg[0].A->plan.n_blocks;
+                } else {
+                    hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
+                }
             }
-            hipLaunchKernelGGL(k_reduce_iter, dim3(1), rt, 0, s, K->d_part, nb, K->d_state, K->d_hist, p);
+            hipLaunchKernelGGL(k_reduce_iter, dim3(1), rt, 0, s, pz, nbz, K->d_part + 2 * nb, nb, K->d_state,
+                               K->d_hist, p);
             if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve iteration");
         }
     }

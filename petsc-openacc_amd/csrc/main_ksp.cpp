@@ -133,6 +133,11 @@ int main(int argc, char **argv) {
     // -------- createSystem (helper.cpp:22-57): assembled on the device
     // (csrc/poisson.hip), or on the host and uploaded with -aijhip_host_assembly
     const bool host_asm = opt.count("-aijhip_host_assembly") > 0;
+    int ndev = 0;
+    if (aijhip_device_count(&ndev) != AIJHIP_OK || ndev == 0) {
+        std::fprintf(stderr, "main_ksp: no HIP device visible\n");
+        return AIJHIP_ERR_NODEVICE;
+    }
     const double t_start = now();
     const int64_t m = (int64_t)nx * ny * nz;
     std::vector<double> exact((size_t)m);
