@@ -14,7 +14,8 @@
  * deterministic greedy pass in natural order (PETSc's MIS ordering is not
  * reproduced: GAMG iteration parity with PETSc is unpinned).
  * The solve-phase V-cycle runs on the device inside aijhip_ksp
- * (AIJHIP_PC_GAMG).
+ * (AIJHIP_PC_GAMG), whose set-up builds the large levels on the device
+ * (device_min_rows) with results identical to aijhip_gamg_build_host.
  */
 #ifndef AIJHIP_GAMG_H
 #define AIJHIP_GAMG_H
@@ -33,6 +34,12 @@ typedef struct aijhip_gamg_params {
     double smooth_scale;     /* 1.4 in alpha = -smooth_scale / emax          */
     int32_t eig_its;         /* iterations of the emax(D^-1 A) estimate (10) */
     int32_t threads;         /* host threads for set-up (0 = OpenMP default) */
+    int32_t device_min_rows; /* KSP set-up: levels with at least this many rows
+                              * are built on the device (strength graph, emax,
+                              * smoothing, Galerkin product; the aggregation
+                              * stays on the host); smaller ones on the host.
+                              * 0 = every level on the device, INT32_MAX = all
+                              * on the host. Same hierarchy either way.     */
 } aijhip_gamg_params_t;
 
 typedef struct aijhip_gamg_host *aijhip_gamg_host_t;

@@ -86,6 +86,12 @@ int aijhip_ksp_set_gamg_params(aijhip_ksp_t ksp, const aijhip_gamg_params_t *p);
  * per level (finest first; up to cap entries), and the host set-up time. */
 int aijhip_ksp_get_pc_levels(aijhip_ksp_t ksp, int32_t *nlevels, int32_t *rows, int64_t *nnz,
                              int32_t cap, double *setup_seconds);
+
+/* Copy out GAMG level l's operator (which = 'A') or interpolation to level
+ * l+1 ('P') from the device (PCMGGetSmoother / PCGetInterpolations
+ * introspection): sizes into m, n, nnz; with ai == NULL only the sizes. */
+int aijhip_ksp_get_pc_level(aijhip_ksp_t ksp, int32_t l, char which, int32_t *m, int32_t *n,
+                            int64_t *nnz, int32_t *ai, int32_t *aj, double *aa);
 int aijhip_ksp_destroy(aijhip_ksp_t ksp);
 
 #ifdef __cplusplus

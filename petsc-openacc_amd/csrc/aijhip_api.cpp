@@ -353,6 +353,40 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
 
 namespace aijhip {
 void set_error(const std::string &msg) { g_err = msg; }
+
+// A^T as a handle owned by A (MatMultTranspose): the device arrays of the
+// transpose (n+1 / nz+2 / nz+2, tail pad zeroed) are copied device to device
+// and freed here; only the row offsets visit the host, for planning.
+int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa) {
+    aijhip_mat *T = new (std::nothrow) aijhip_mat();
+    int rc = AIJHIP_OK;
+    if (!T) rc = fail(AIJHIP_ERR_ALLOC, "host allocation");
+    std::vector<int32_t> h_tai;
+    if (!rc) {
+        T->device = A->device;
+        T->n_cu = A->n_cu;
+        T->requested_tune = A->requested_tune;
+        T->m = A->n;
+        T->n = A->m;
+        T->nz = A->nz;
+        T->requested_kernel =
+            A->requested_kernel == AIJHIP_KERNEL_VECTOR ? AIJHIP_KERNEL_AUTO : A->requested_kernel;
+        h_tai.resize((size_t)T->m + 1);
+        const hipError_t e = hipMemcpy(h_tai.data(), tai, sizeof(int32_t) * h_tai.size(), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = hipfail(e, "read transpose offsets");
+    }
+    if (!rc) rc = upload_and_plan(T, h_tai.data(), taj, taa, true);
+    hipFree(tai);
+    hipFree(taj);
+    hipFree(taa);
+    if (rc) {
+        if (T) { free_matrix(T); delete T; }
+        return rc;
+    }
+    if (A->transpose) { free_matrix(A->transpose); delete A->transpose; }
+    A->transpose = T;
+    return AIJHIP_OK;
+}
 }  // namespace aijhip
 
 extern "C" {
@@ -510,28 +544,8 @@ int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y, void *
         hipError_t e = hipDeviceSynchronize();
         if (e == hipSuccess) e = aijhip::build_transpose(*A, &tai, &taj, &taa, nullptr);
         if (e != hipSuccess) return hipfail(e, "build transpose");
-        aijhip_mat *T = new (std::nothrow) aijhip_mat();
-        if (!T) {
-            hipFree(tai); hipFree(taj); hipFree(taa);
-            return fail(AIJHIP_ERR_ALLOC, "host allocation");
-        }
-        T->device = A->device;
-        T->n_cu = A->n_cu;
-        T->requested_tune = A->requested_tune;
-        T->m = A->n;
-        T->n = A->m;
-        T->nz = A->nz;
-        std::vector<int32_t> h_tai((size_t)T->m + 1), h_taj((size_t)T->nz);
-        std::vector<double> h_taa((size_t)T->nz);
-        e = hipMemcpy(h_tai.data(), tai, sizeof(int32_t) * h_tai.size(), hipMemcpyDeviceToHost);
-        if (e == hipSuccess && T->nz > 0) e = hipMemcpy(h_taj.data(), taj, sizeof(int32_t) * (size_t)T->nz, hipMemcpyDeviceToHost);
-        if (e == hipSuccess && T->nz > 0) e = hipMemcpy(h_taa.data(), taa, sizeof(double) * (size_t)T->nz, hipMemcpyDeviceToHost);
-        hipFree(tai); hipFree(taj); hipFree(taa);
-        if (e != hipSuccess) { delete T; return hipfail(e, "read transpose"); }
-        T->requested_kernel = A->requested_kernel == AIJHIP_KERNEL_VECTOR ? AIJHIP_KERNEL_AUTO : A->requested_kernel;
-        rc = upload_and_plan(T, h_tai.data(), h_taj.data(), h_taa.data());
-        if (rc) { free_matrix(T); delete T; return rc; }
-        A->transpose = T;
+        rc = aijhip::attach_transpose(A, tai, taj, taa);
+        if (rc) return rc;
     }
     return mult_impl(A->transpose, x, nullptr, y, false, stream);
 }

@@ -153,6 +153,8 @@ hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, do
 // Richardson+Jacobi step x = t + D^-1 (b - A t) (x != t) with optional
 // z.z / z.b partials (2 x n_blocks) for CG on the finest level.
 bool stream_mg_fusable(const aijhip_mat &A);
+// y = D^-1 A x in PETSc's row order (exact), for the GAMG set-up.
+hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s);
 hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
                          hipStream_t s);
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
@@ -175,6 +177,8 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
                            double **d_taa, hipStream_t s);
 
 RowList row_list(const aijhip_mat &A);
+// Install A^T (device arrays, freed by the call) as A's transpose handle.
+int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa);
 // Number of device column indices outside [0, n) (synchronous).
 hipError_t count_bad_columns(const int32_t *d_aj, int64_t nz, int32_t n, int64_t *bad);
 

@@ -152,6 +152,17 @@ struct OpMgPost {
     }
 };
 
+// y = D^-1 A x (the GAMG set-up's power iteration, gamg_setup.cpp dinv_apply).
+struct OpDinvMult {
+    static constexpr int kDots = 0;
+    static constexpr bool kSeeded = false;
+    const double *x, *dinv;
+    double *y;
+    __device__ double gx(int32_t j) const { return x[j]; }
+    __device__ double seed(int) const { return 0.0; }
+    __device__ void put(int o, double v, double *) const { y[o] = dinv[o] * v; }
+};
+
 template <int T, int CAP, int RPT, bool CROW, bool XCD, bool NT, bool CLAMPED, class Op>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
@@ -702,15 +713,17 @@ hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, do
 bool stream_mg_fusable(const aijhip_mat &A) { return stream_dot_fusable(A); }
 
 template <class Op>
-static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dpart, hipStream_t s) {
+static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dpart, hipStream_t s,
+                                   int exact = -1) {
     if (!stream_mg_fusable(A)) return hipErrorInvalidValue;
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
+    const int ex = exact < 0 ? (int)P.tune.exact : exact;
     static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
 #define AIJHIP_OG(G)                                                                                      \
     case G:                                                                                               \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
-                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, 0, (int)P.tune.exact, \
+                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex,                \
                            A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, nullptr);                          \
         break
     switch (P.tune.geom) {
@@ -730,6 +743,10 @@ hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *din
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
                           double *dpart, hipStream_t s) {
     return launch_stream_op(A, OpMgPost{t, b, dinv, x, dpart != nullptr}, dpart, s);
+}
+
+hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s) {
+    return launch_stream_op(A, OpDinvMult{x, dinv, y}, nullptr, s, 1);  // PETSc row order
 }
 
 hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, double *y,

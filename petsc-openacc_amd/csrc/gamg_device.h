@@ -1,0 +1,30 @@
+// gamg_device.h — the device-side smoothed-aggregation set-up
+// (gamg_device.hip), used by the KSP set-up (ksp.hip).
+#pragma once
+
+#include <vector>
+
+#include "aijhip_internal.h"
+#include "gamg_internal.h"
+
+namespace aijhip_gamg {
+
+// One level of the device hierarchy.
+struct DeviceLevel {
+    aijhip_mat *A = nullptr;  // level operator (level 0: the caller's, borrowed)
+    aijhip_mat *P = nullptr;  // prolongator to the next level, P^T attached
+    double emax = 0.0;
+};
+
+// Device set-up: levels are built on the device while the level has at least
+// p.device_min_rows rows; the greedy aggregation runs on the host from the
+// device strength graph. On return `levels` holds every level built
+// (levels[0].A = A0). *more is true when the hierarchy continues below the
+// last level (too small for the device, or a Galerkin row beyond the device
+// accumulators): B is then that level's near-null space for build_host_nns.
+int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<DeviceLevel> &levels,
+                 std::vector<double> &B, bool *more);
+
+void free_device_levels(std::vector<DeviceLevel> &levels);
+
+}  // namespace aijhip_gamg

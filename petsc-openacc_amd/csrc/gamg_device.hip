@@ -1,0 +1,715 @@
+// gamg_device.hip — the smoothed-aggregation set-up on the device
+// (gamg_internal.h build_device). Same steps, same summation orders and so
+// the same hierarchy, bit for bit, as the host builder (gamg_setup.cpp,
+// itself pinned to oracle/gamg.py):
+//   diagonal / D^-1               one lane per row
+//   strength graph S (+ S^T)      atomic slots, then per-row sort + unique
+//   aggregation                   host (sequential greedy, natural order),
+//                                 from S and per-entry |a_ij| weights
+//   emax(D^-1 A)                  power iteration on the STREAM SpMV in
+//                                 PETSc order; 8192-entry blocked dots
+//   P = (I - 1.4/emax D^-1 A) P0  row-wise product A*P0, union with P0
+//   A_c = P^T (A P)               row-wise products (below), P^T by the
+//                                 stable radix-sort transpose
+// Row-wise product C = A*B (scipy csr_matmat order): one lane per output row
+// keeps the row's distinct columns sorted in LDS and adds each product
+// a_ik * b_kj to its column's accumulator in traversal order, starting from
+// 0.0. A row with more distinct columns than the lane's capacity retries
+// with a larger capacity; past the largest the level goes to the host.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#include "gamg_device.h"
+
+namespace {
+
+using aijhip::set_error;
+
+int herr(hipError_t e, const char *what) {
+    set_error(std::string("GAMG device set-up: ") + what + ": " + hipGetErrorString(e));
+    return AIJHIP_ERR_HIP;
+}
+
+inline unsigned blocks_for(int64_t n, int t) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+// ---------------------------------------------------------------- kernels
+
+__global__ void k_diag_dinv(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                            const double *__restrict__ aa, double *d, double *dinv) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double v = 0.0;
+    for (int32_t k = ai[i]; k < ai[i + 1]; ++k)
+        if (aj[k] == i) { v = aa[k]; break; }
+    d[i] = v;
+    dinv[i] = 1.0 / (v == 0.0 ? 1.0 : v);
+}
+
+__device__ __forceinline__ bool strong(int32_t i, int32_t j, double a, const double *d, double theta) {
+    return j != i && fabs(a) > theta * sqrt(fabs(d[i] * d[j]));
+}
+
+__global__ void k_strong_count(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                               const double *__restrict__ aa, const double *__restrict__ d, double theta,
+                               unsigned long long *cnt) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    unsigned long long own = 0;
+    for (int32_t k = ai[i]; k < ai[i + 1]; ++k)
+        if (strong(i, aj[k], aa[k], d, theta)) {
+            ++own;
+            atomicAdd(&cnt[aj[k]], 1ull);
+        }
+    if (own) atomicAdd(&cnt[i], own);
+}
+
+__global__ void k_strong_fill(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                              const double *__restrict__ aa, const double *__restrict__ d, double theta,
+                              const unsigned long long *__restrict__ off, unsigned int *pos, int32_t *tmp) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    for (int32_t k = ai[i]; k < ai[i + 1]; ++k) {
+        const int32_t j = aj[k];
+        if (!strong(i, j, aa[k], d, theta)) continue;
+        tmp[off[i] + atomicAdd(&pos[i], 1u)] = j;
+        tmp[off[j] + atomicAdd(&pos[j], 1u)] = i;
+    }
+}
+
+// per-row insertion sort + unique of the gathered neighbour list
+__global__ void k_sort_unique(int32_t m, const unsigned long long *__restrict__ off, int32_t *tmp, int32_t *ucnt) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t *r = tmp + off[i];
+    const int64_t n = (int64_t)(off[i + 1] - off[i]);
+    if (n <= 64) return;  // k_sort_unique_wave's
+    for (int64_t a = 1; a < n; ++a) {
+        const int32_t v = r[a];
+        int64_t b = a - 1;
+        while (b >= 0 && r[b] > v) { r[b + 1] = r[b]; --b; }
+        r[b + 1] = v;
+    }
+    int64_t u = 0;
+    for (int64_t a = 0; a < n; ++a)
+        if (u == 0 || r[a] != r[u - 1]) r[u++] = r[a];
+    ucnt[i] = (int32_t)u;
+}
+
+// The same per row, one wavefront per row of at most 64 entries: bitonic
+// sort across the lanes, then unique by ballot. Longer rows are left to
+// k_sort_unique (it skips the short ones).
+__global__ __launch_bounds__(256) void k_sort_unique_wave(int32_t m, const unsigned long long *__restrict__ off,
+                                                          int32_t *tmp, int32_t *ucnt) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < m; i += nw) {
+        const unsigned long long o = off[i];
+        const int n = (int)(off[i + 1] - o);
+        if (n > 64) continue;
+        int32_t v = lane < n ? tmp[o + lane] : INT32_MAX;
+#pragma unroll
+        for (int k = 2; k <= 64; k <<= 1) {
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const int32_t u = __shfl_xor(v, j, 64);
+                const bool up = (lane & k) == 0, low = (lane & j) == 0;
+                v = (up == low) ? min(v, u) : max(v, u);
+            }
+        }
+        const int32_t prev = __shfl_up(v, 1, 64);
+        const bool keep = lane < n && (lane == 0 || v != prev);
+        const unsigned long long bal = __ballot(keep);
+        if (keep) tmp[o + __popcll(bal & ((1ull << lane) - 1ull))] = v;
+        if (lane == 0) ucnt[i] = __popcll(bal);
+    }
+}
+
+// compact the unique lists into S and attach the candidate weights
+// sval = max |a_ij| over stored a_ij of the row (-1: not stored)
+// (one wavefront per row, a lane per S entry, A's row scanned by all lanes)
+__global__ __launch_bounds__(256) void k_strength_compact(int32_t m, const unsigned long long *__restrict__ off,
+                                                          const int32_t *__restrict__ tmp,
+                                                          const int32_t *__restrict__ si,
+                                                          const int32_t *__restrict__ ai,
+                                                          const int32_t *__restrict__ aj,
+                                                          const double *__restrict__ aa, int32_t *sj,
+                                                          double *sval) {
+    const int lane = threadIdx.x & 63;
+    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
+    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < m; i += nw) {
+        const int32_t *r = tmp + off[i];
+        const int32_t s0 = si[i], s1 = si[i + 1], a0 = ai[i], a1 = ai[i + 1];
+        for (int32_t k0 = s0; k0 < s1; k0 += 64) {
+            const int32_t k = k0 + lane;
+            const int32_t j = k < s1 ? r[k - s0] : -1;
+            double v = -1.0;
+            for (int32_t e = a0; e < a1; ++e)
+                if (aj[e] == j) v = fmax(v, fabs(aa[e]));
+            if (k < s1) {
+                sj[k] = j;
+                sval[k] = v;
+            }
+        }
+    }
+}
+
+// Aggregation phase 2 (gamg_setup.cpp aggregate): a node phase 1 left free
+// joins the aggregate of its strongest stored phase-1 neighbour, lowest
+// index on ties.
+__global__ void k_agg_phase2(int32_t m, const int32_t *__restrict__ si, const int32_t *__restrict__ sj,
+                             const double *__restrict__ sval, const int32_t *__restrict__ phase1, int32_t *agg) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t a = phase1[i];
+    if (a == -1) {
+        int32_t best = -1;
+        double bv = -1.0;
+        for (int32_t k = si[i]; k < si[i + 1]; ++k) {
+            const int32_t j = sj[k];
+            const double v = sval[k];
+            if (phase1[j] == -1 || v < 0.0) continue;
+            if (v > bv || (v == bv && j < best)) { bv = v; best = j; }
+        }
+        if (best >= 0) a = phase1[best];
+    }
+    agg[i] = a;
+}
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// the power iteration's start (gamg_setup.cpp estimate_emax)
+__global__ void k_power_start(int32_t m, double *v) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    v[i] = 2.0 * ((double)(mix64(0x5EEDULL + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL) >> 11) *
+                  (1.0 / 9007199254740992.0)) - 1.0;
+}
+
+constexpr int64_t kDotBlock = 8192;  // gamg_setup.cpp kDotBlock
+
+// one lane per 8192-entry block, left to right (the host sums the blocks)
+__global__ void k_block_dot(int64_t n, const double *__restrict__ a, double *part) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i0 = q * kDotBlock;
+    if (i0 >= n) return;
+    const int64_t e = min(n, i0 + kDotBlock);
+    double s = 0.0;
+    for (int64_t i = i0; i < e; ++i) s += a[i] * a[i];
+    part[q] = s;
+}
+
+__global__ void k_div(int32_t m, const double *w, double nw, double *v) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) v[i] = w[i] / nw;
+}
+
+__global__ void k_iota(int32_t n, int32_t *v) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) v[i] = i;
+}
+
+__global__ void k_widen(int32_t m, const int32_t *__restrict__ c, unsigned long long *w) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) w[i] = (unsigned long long)c[i];
+}
+
+__global__ void k_narrow(int32_t n, const unsigned long long *__restrict__ w, int32_t *c) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) c[i] = (int32_t)w[i];
+}
+
+// C = A*B row by row (see the file comment). SYMBOLIC: cnt[i] = distinct
+// columns of row i, or -1 when they exceed CAP. NUMERIC: row i's sorted
+// columns and sums at ci[i].
+template <int CAP, int TPB, bool NUMERIC>
+__global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__restrict__ ai,
+                                                 const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                                                 const int32_t *__restrict__ bi, const int32_t *__restrict__ bj,
+                                                 const double *__restrict__ ba, const int32_t *__restrict__ ci,
+                                                 int32_t *cj, double *ca, int32_t *cnt) {
+    __shared__ int32_t sc[CAP * TPB];
+    __shared__ double sv[NUMERIC ? CAP * TPB : 1];
+    const int t = threadIdx.x;
+    for (int32_t i = blockIdx.x * TPB + t; i < m; i += gridDim.x * TPB) {
+        int n = 0;
+        bool over = false;
+        for (int32_t k = ai[i]; k < ai[i + 1] && !over; ++k) {
+            const int32_t j = aj[k];
+            const double a = NUMERIC ? aa[k] : 0.0;
+            for (int32_t q = bi[j]; q < bi[j + 1]; ++q) {
+                const int32_t c = bj[q];
+                int lo = 0, hi = n;
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (sc[mid * TPB + t] < c) lo = mid + 1;
+                    else hi = mid;
+                }
+                if (lo < n && sc[lo * TPB + t] == c) {
+                    if (NUMERIC) sv[lo * TPB + t] += a * ba[q];
+                    continue;
+                }
+                if (n == CAP) { over = true; break; }
+                for (int z = n; z > lo; --z) {
+                    sc[z * TPB + t] = sc[(z - 1) * TPB + t];
+                    if (NUMERIC) sv[z * TPB + t] = sv[(z - 1) * TPB + t];
+                }
+                sc[lo * TPB + t] = c;
+                if (NUMERIC) {
+                    double v0 = 0.0;
+                    v0 += a * ba[q];
+                    sv[lo * TPB + t] = v0;
+                }
+                ++n;
+            }
+        }
+        if (!NUMERIC) {
+            cnt[i] = over ? -1 : n;
+        } else {
+            const int32_t o = ci[i];
+            for (int z = 0; z < n; ++z) {
+                cj[o + z] = sc[z * TPB + t];
+                ca[o + z] = sv[z * TPB + t];
+            }
+        }
+    }
+}
+
+// P = alpha (D^-1 T) + P0 on the union pattern (gamg_setup.cpp prolongator):
+// lengths, then entries.
+__global__ void k_prolong_len(int32_t m, const int32_t *__restrict__ ti, const int32_t *__restrict__ tj,
+                              const int32_t *__restrict__ agg, int32_t *len) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    bool has = false;
+    for (int32_t k = ti[i]; k < ti[i + 1]; ++k) has |= tj[k] == agg[i];
+    len[i] = ti[i + 1] - ti[i] + (has ? 0 : 1);
+}
+
+__global__ void k_prolong_fill(int32_t m, const int32_t *__restrict__ ti, const int32_t *__restrict__ tj,
+                               const double *__restrict__ ta, const int32_t *__restrict__ agg,
+                               const double *__restrict__ p0v, const double *__restrict__ dinv, double alpha,
+                               const int32_t *__restrict__ pi, int32_t *pj, double *pa) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t p = pi[i];
+    bool placed = false;
+    const int32_t g = agg[i];
+    const double p0 = p0v[i];
+    for (int32_t k = ti[i]; k < ti[i + 1]; ++k) {
+        const int32_t c = tj[k];
+        if (!placed && g < c) { pj[p] = g; pa[p] = p0; ++p; placed = true; }
+        const double t = dinv[i] * ta[k];
+        pj[p] = c;
+        pa[p] = alpha * t + (c == g ? p0 : 0.0);
+        if (c == g) placed = true;
+        ++p;
+    }
+    if (!placed) { pj[p] = g; pa[p] = p0; }
+}
+
+// ---------------------------------------------------------------- host side
+
+// Device CSR owned by this set-up (nz + 2 entries: the SpMV handles' tail pad).
+struct DCsr {
+    int32_t m = 0, n = 0;
+    int64_t nz = 0;
+    int32_t *ai = nullptr, *aj = nullptr;
+    double *aa = nullptr;
+    void release() {
+        hipFree(ai); hipFree(aj); hipFree(aa);
+        ai = aj = nullptr;
+        aa = nullptr;
+    }
+};
+
+template <class T>
+hipError_t dalloc(T **p, int64_t count) {
+    return hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * (size_t)std::max<int64_t>(count, 1));
+}
+
+// exclusive scan of int32 counts into int32 offsets (m+1); false on overflow
+hipError_t scan_offsets(const int32_t *cnt, int32_t m, int32_t *off, int64_t *total) {
+    unsigned long long *w = nullptr, *o = nullptr;
+    void *tmp = nullptr;
+    size_t tb = 0;
+    hipError_t e;
+    if ((e = dalloc(&w, (int64_t)m + 1)) != hipSuccess || (e = dalloc(&o, (int64_t)m + 1)) != hipSuccess) goto done;
+    if ((e = hipMemset(w, 0, sizeof(unsigned long long) * ((size_t)m + 1))) != hipSuccess) goto done;
+    if (m > 0) hipLaunchKernelGGL(k_widen, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, cnt, w);
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w, o, m + 1)) != hipSuccess) goto done;
+    if ((e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) != hipSuccess) goto done;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, w, o, m + 1)) != hipSuccess) goto done;
+    {
+        unsigned long long t = 0;
+        if ((e = hipMemcpy(&t, o + m, sizeof(t), hipMemcpyDeviceToHost)) != hipSuccess) goto done;
+        *total = (int64_t)t;
+        if (t <= (unsigned long long)INT32_MAX) {  // narrow to int32 offsets (PetscInt)
+            hipLaunchKernelGGL(k_narrow, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m + 1, o, off);
+            e = hipGetLastError();
+        }
+    }
+done:
+    hipFree(w); hipFree(o); hipFree(tmp);
+    return e;
+}
+
+// C = A * B. Returns AIJHIP_OK, or AIJHIP_ERR_STATE when a row's distinct
+// columns exceed every device capacity (the caller falls back to the host).
+template <int CAP, int TPB>
+hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, const int32_t *ci, DCsr *C, bool numeric,
+                        int n_cu) {
+    const unsigned grid = (unsigned)std::min<int64_t>(blocks_for(A.m, TPB), (int64_t)n_cu * 16);
+    if (!numeric)
+        hipLaunchKernelGGL((k_rowprod<CAP, TPB, false>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj, A.aa,
+                           B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt);
+    else
+        hipLaunchKernelGGL((k_rowprod<CAP, TPB, true>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj, A.aa,
+                           B.ai, B.aj, B.aa, ci, C->aj, C->aa, nullptr);
+    return hipGetLastError();
+}
+
+int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu) {
+    C = DCsr();
+    C.m = A.m;
+    C.n = B.n;
+    int32_t *cnt = nullptr;
+    hipError_t e;
+    if ((e = dalloc(&cnt, A.m)) != hipSuccess) return herr(e, "product counts");
+    // capacities (distinct columns per row) x lanes per block, 48 KiB of LDS
+    int level = 0;
+    for (;; ++level) {
+        if (level == 0) e = rowprod_pass<64, 64>(A, B, cnt, nullptr, nullptr, false, n_cu);
+        else if (level == 1) e = rowprod_pass<256, 16>(A, B, cnt, nullptr, nullptr, false, n_cu);
+        else { hipFree(cnt); return AIJHIP_ERR_STATE; }
+        if (e != hipSuccess) { hipFree(cnt); return herr(e, "symbolic product"); }
+        int32_t mn = 0;
+        if (A.m > 0) {
+            void *tmp = nullptr;
+            size_t tb = 0;
+            int32_t *dmin = nullptr;
+            if ((e = dalloc(&dmin, 1)) == hipSuccess &&
+                (e = hipcub::DeviceReduce::Min(nullptr, tb, cnt, dmin, A.m)) == hipSuccess &&
+                (e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) == hipSuccess &&
+                (e = hipcub::DeviceReduce::Min(tmp, tb, cnt, dmin, A.m)) == hipSuccess)
+                e = hipMemcpy(&mn, dmin, sizeof(int32_t), hipMemcpyDeviceToHost);
+            hipFree(tmp);
+            hipFree(dmin);
+            if (e != hipSuccess) { hipFree(cnt); return herr(e, "product overflow check"); }
+        }
+        if (mn >= 0) break;
+    }
+    if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) { hipFree(cnt); return herr(e, "product rows"); }
+    int64_t total = 0;
+    if ((e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess) { hipFree(cnt); C.release(); return herr(e, "scan"); }
+    if (total > INT32_MAX) {
+        hipFree(cnt);
+        C.release();
+        set_error("GAMG device set-up: product exceeds int32 indices");
+        return AIJHIP_ERR_ARG;
+    }
+    C.nz = total;
+    if ((e = dalloc(&C.aj, total + 2)) != hipSuccess || (e = dalloc(&C.aa, total + 2)) != hipSuccess ||
+        (e = hipMemset(C.aj + total, 0, 2 * sizeof(int32_t))) != hipSuccess ||
+        (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess) {
+        hipFree(cnt);
+        C.release();
+        return herr(e, "product alloc");
+    }
+    e = level == 0 ? rowprod_pass<64, 64>(A, B, cnt, C.ai, &C, true, n_cu)
+                   : rowprod_pass<256, 16>(A, B, cnt, C.ai, &C, true, n_cu);
+    hipFree(cnt);
+    if (e != hipSuccess) { C.release(); return herr(e, "numeric product"); }
+    return AIJHIP_OK;
+}
+
+double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vector<double> &h_part, hipError_t *e) {
+    const int64_t nb = (n + kDotBlock - 1) / kDotBlock;
+    if (nb > 0) hipLaunchKernelGGL(k_block_dot, dim3(blocks_for(nb, 64)), dim3(64), 0, nullptr, n, d_v, d_part);
+    h_part.resize((size_t)nb);
+    *e = nb > 0 ? hipMemcpy(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost) : hipSuccess;
+    double s = 0.0;
+    for (int64_t q = 0; q < nb; ++q) s += h_part[q];
+    return std::sqrt(s);
+}
+
+// Pinned host staging for the strength graph and the aggregates (PCIe at
+// full rate, no pageable bounce), grown as needed and reused across levels.
+struct Staging {
+    void *p = nullptr;
+    size_t bytes = 0;
+    hipError_t reserve(size_t b) {
+        if (b <= bytes) return hipSuccess;
+        if (p) hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        const hipError_t e = hipHostMalloc(&p, b);
+        if (e == hipSuccess) bytes = b;
+        return e;
+    }
+    int32_t *i32() { return static_cast<int32_t *>(p); }
+    ~Staging() { if (p) hipHostFree(p); }
+};
+
+DCsr view_of(const aijhip_mat &A) {
+    DCsr v;
+    v.m = A.m;
+    v.n = A.n;
+    v.nz = A.nz;
+    v.ai = A.d_ai;
+    v.aj = A.d_aj;
+    v.aa = A.d_aa;
+    return v;
+}
+
+int make_handle(int device, DCsr &C, aijhip_mat **out) {
+    const int rc = aijhip_mat_create_from_device(device, C.m, C.n, C.nz, C.ai, C.aj, C.aa, out);
+    C.release();
+    return rc;
+}
+
+}  // namespace
+
+namespace aijhip_gamg {
+
+void free_device_levels(std::vector<DeviceLevel> &levels) {
+    for (size_t l = 0; l < levels.size(); ++l) {
+        if (l > 0) aijhip_mat_destroy(levels[l].A);
+        aijhip_mat_destroy(levels[l].P);
+    }
+    levels.clear();
+}
+
+int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<DeviceLevel> &levels,
+                 std::vector<double> &B, bool *more) {
+    levels.clear();
+    *more = false;
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!log) return;
+        (void)hipDeviceSynchronize();
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "gamg device level %zu %-14s %8.3f s\n", levels.size() - 1, what,
+                     std::chrono::duration<double>(t - t0).count());
+        t0 = t;
+    };
+    levels.push_back(DeviceLevel{A0, nullptr, 0.0});
+    B.assign((size_t)A0->m, 1.0);
+    const int n_cu = std::max(A0->n_cu, 1);
+    Staging stage;
+    int rc = AIJHIP_OK;
+    hipError_t e = hipSuccess;
+    while ((int32_t)levels.size() < p.max_levels && levels.back().A->m > p.coarse_eq_limit) {
+        aijhip_mat &A = *levels.back().A;
+        const int32_t m = A.m;
+        if (m < p.device_min_rows || !aijhip::stream_mg_fusable(A)) {
+            *more = true;  // the host takes it from here
+            break;
+        }
+        const DCsr Av = view_of(A);
+        const unsigned g256 = blocks_for(m, 256);
+        const unsigned wgrid = (unsigned)std::min<int64_t>(blocks_for((int64_t)m * 64, 256), (int64_t)n_cu * 32);
+        // ---- diagonal, strength graph
+        double *d = nullptr, *dinv = nullptr, *sval = nullptr;
+        unsigned long long *cnt = nullptr, *off = nullptr;
+        unsigned int *pos = nullptr;
+        int32_t *tmp = nullptr, *ucnt = nullptr, *si = nullptr, *sj = nullptr;
+        void *scan_tmp = nullptr;
+        size_t tb = 0;
+        int64_t nzs = 0;
+        int32_t *h_si = nullptr, *h_sj = nullptr, *agg = nullptr, *d_ph = nullptr;
+        int32_t na = 0;
+#define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto level_done; } } while (0)
+        GTRY(dalloc(&d, m), "alloc");
+        GTRY(dalloc(&dinv, m), "alloc");
+        hipLaunchKernelGGL(k_diag_dinv, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d, dinv);
+        GTRY(dalloc(&cnt, (int64_t)m + 1), "alloc");
+        GTRY(dalloc(&off, (int64_t)m + 1), "alloc");
+        GTRY(hipMemset(cnt, 0, sizeof(unsigned long long) * ((size_t)m + 1)), "memset");
+        hipLaunchKernelGGL(k_strong_count, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
+                           p.threshold, cnt);
+        GTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, m + 1), "scan");
+        GTRY(hipMalloc(&scan_tmp, std::max<size_t>(tb, 1)), "alloc");
+        GTRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, cnt, off, m + 1), "scan");
+        {
+            unsigned long long t = 0;
+            GTRY(hipMemcpy(&t, off + m, sizeof(t), hipMemcpyDeviceToHost), "read");
+            nzs = (int64_t)t;
+        }
+        GTRY(dalloc(&tmp, nzs), "alloc");
+        GTRY(dalloc(&pos, m), "alloc");
+        GTRY(hipMemset(pos, 0, sizeof(unsigned int) * (size_t)std::max(m, 1)), "memset");
+        hipLaunchKernelGGL(k_strong_fill, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
+                           p.threshold, off, pos, tmp);
+        GTRY(dalloc(&ucnt, m), "alloc");
+        hipLaunchKernelGGL(k_sort_unique_wave, dim3(wgrid), dim3(256), 0, nullptr, m, off, tmp, ucnt);
+        hipLaunchKernelGGL(k_sort_unique, dim3(g256), dim3(256), 0, nullptr, m, off, tmp, ucnt);
+        GTRY(dalloc(&si, (int64_t)m + 1), "alloc");
+        {
+            int64_t tot = 0;
+            GTRY(scan_offsets(ucnt, m, si, &tot), "scan");
+            if (tot > INT32_MAX) { rc = AIJHIP_ERR_ARG; set_error("GAMG: strength graph exceeds int32"); goto level_done; }
+            nzs = tot;
+        }
+        GTRY(dalloc(&sj, nzs), "alloc");
+        GTRY(dalloc(&sval, nzs), "alloc");
+        hipLaunchKernelGGL(k_strength_compact, dim3(wgrid), dim3(256), 0, nullptr, m, off, tmp, si, A.d_ai,
+                           A.d_aj, A.d_aa, sj, sval);
+        GTRY(hipGetLastError(), "strength kernels");
+        // ---- aggregation: phases 1 and 3 (sequential greedy) on the host from
+        // S staged in pinned memory, phase 2 on the device
+        GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
+        h_si = stage.i32();
+        h_sj = h_si + m + 1;
+        agg = h_sj + nzs;
+        GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
+        if (nzs > 0) GTRY(hipMemcpy(h_sj, sj, sizeof(int32_t) * (size_t)nzs, hipMemcpyDeviceToHost), "read S");
+        lap("strength");
+        na = aijhip_gamg::aggregate_phase1(m, h_si, h_sj, agg);
+        GTRY(dalloc(&d_ph, 2 * (int64_t)m), "alloc");
+        GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
+        hipLaunchKernelGGL(k_agg_phase2, dim3(g256), dim3(256), 0, nullptr, m, si, sj, sval, d_ph, d_ph + m);
+        GTRY(hipMemcpy(agg, d_ph + m, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
+        na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
+        lap("aggregate");
+    level_done:
+        hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(ucnt); hipFree(si); hipFree(sj);
+        hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph);
+        if (rc) { hipFree(dinv); break; }
+        if (na >= m || na == 0) { hipFree(dinv); break; }  // no coarsening: this is the coarsest level
+#undef GTRY
+#define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto prolong_done; } } while (0)
+        // ---- emax(D^-1 A)
+        double emax = 1.0;
+        DCsr P0, T, P, AP, PT, Ac;
+        int32_t *d_agg = nullptr, *plen = nullptr;
+        double *d_p0 = nullptr, *v = nullptr, *w = nullptr, *part = nullptr;
+        std::vector<double> Bc((size_t)na, 0.0), p0((size_t)m), h_part;
+        aijhip_mat *Ph = nullptr, *Ach = nullptr;
+        if (p.nsmooths > 0) {
+            GTRY(dalloc(&v, m), "alloc");
+            GTRY(dalloc(&w, m), "alloc");
+            GTRY(dalloc(&part, (m + kDotBlock - 1) / kDotBlock), "alloc");
+            hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, nullptr, m, v);
+            const double nv = host_blocked_norm(v, m, part, h_part, &e);
+            GTRY(e, "power iteration");
+            hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, v, nv, v);
+            for (int it = 0; it < p.eig_its; ++it) {
+                GTRY(aijhip::launch_dinv_mult(A, dinv, v, w, nullptr), "power iteration");
+                const double nw = host_blocked_norm(w, m, part, h_part, &e);
+                GTRY(e, "power iteration");
+                if (!(nw > 0.0)) break;
+                emax = nw;
+                hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, w, nw, v);
+            }
+            lap("emax");
+        }
+        // ---- tentative prolongator (host: the near-null space QR per aggregate)
+        for (int32_t i = 0; i < m; ++i) Bc[agg[i]] += B[i] * B[i];
+        for (int32_t a = 0; a < na; ++a) Bc[a] = std::sqrt(Bc[a]);
+        for (int32_t i = 0; i < m; ++i) p0[i] = Bc[agg[i]] > 0.0 ? B[i] / Bc[agg[i]] : 0.0;
+        GTRY(dalloc(&d_agg, m), "alloc");
+        GTRY(dalloc(&d_p0, m), "alloc");
+        GTRY(hipMemcpy(d_agg, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload");
+        GTRY(hipMemcpy(d_p0, p0.data(), sizeof(double) * (size_t)m, hipMemcpyHostToDevice), "upload");
+        P0.m = m;
+        P0.n = na;
+        P0.nz = m;
+        GTRY(dalloc(&P0.ai, (int64_t)m + 1), "alloc");
+        hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, P0.ai);
+        P0.aj = d_agg;
+        P0.aa = d_p0;
+        // ---- smoothed prolongator
+        if (p.nsmooths > 0) {
+            if ((rc = rowprod(Av, P0, T, n_cu))) goto prolong_done;
+            P.m = m;
+            P.n = na;
+            GTRY(dalloc(&plen, m), "alloc");
+            hipLaunchKernelGGL(k_prolong_len, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, d_agg, plen);
+            GTRY(dalloc(&P.ai, (int64_t)m + 1), "alloc");
+            GTRY(scan_offsets(plen, m, P.ai, &P.nz), "scan");
+            GTRY(dalloc(&P.aj, P.nz + 2), "alloc");
+            GTRY(dalloc(&P.aa, P.nz + 2), "alloc");
+            hipLaunchKernelGGL(k_prolong_fill, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, T.aa, d_agg, d_p0,
+                               dinv, -p.smooth_scale / emax, P.ai, P.aj, P.aa);
+            GTRY(hipGetLastError(), "prolongator");
+            T.release();
+        } else {
+            P.m = m;
+            P.n = na;
+            P.nz = m;
+            GTRY(dalloc(&P.ai, (int64_t)m + 1), "alloc");
+            GTRY(dalloc(&P.aj, (int64_t)m + 2), "alloc");
+            GTRY(dalloc(&P.aa, (int64_t)m + 2), "alloc");
+            GTRY(hipMemcpy(P.ai, P0.ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToDevice), "copy");
+            GTRY(hipMemcpy(P.aj, d_agg, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
+            GTRY(hipMemcpy(P.aa, d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
+        }
+        lap("prolongator");
+        // ---- Galerkin operator A_c = P^T (A P)
+        if ((rc = rowprod(Av, P, AP, n_cu))) goto prolong_done;
+        lap("A*P");
+        {
+            aijhip_mat pv;  // non-owning view for the transpose builder
+            pv.m = P.m;
+            pv.n = P.n;
+            pv.nz = P.nz;
+            pv.d_ai = P.ai;
+            pv.d_aj = P.aj;
+            pv.d_aa = P.aa;
+            PT.m = P.n;
+            PT.n = P.m;
+            PT.nz = P.nz;
+            e = aijhip::build_transpose(pv, &PT.ai, &PT.aj, &PT.aa, nullptr);
+            pv.d_ai = pv.d_aj = nullptr;
+            pv.d_aa = nullptr;
+            GTRY(e, "transpose");
+        }
+        lap("P^T");
+        if ((rc = rowprod(PT, AP, Ac, n_cu))) goto prolong_done;
+        AP.release();
+        lap("P^T*(AP)");
+        // ---- handles: P (with P^T attached for MatRestrict) and A_c
+        if ((rc = make_handle(A.device, P, &Ph))) goto prolong_done;
+        rc = aijhip::attach_transpose(Ph, PT.ai, PT.aj, PT.aa);
+        PT = DCsr();  // consumed by attach_transpose (freed on failure)
+        if (rc) goto prolong_done;
+        if ((rc = make_handle(A.device, Ac, &Ach))) goto prolong_done;
+        levels.back().P = Ph;
+        levels.back().emax = emax;
+        Ph = nullptr;
+        levels.push_back(DeviceLevel{Ach, nullptr, 0.0});
+        Ach = nullptr;
+        B.swap(Bc);
+        lap("handles");
+    prolong_done:
+#undef GTRY
+        hipFree(v); hipFree(w); hipFree(part); hipFree(dinv); hipFree(plen);
+        hipFree(P0.ai); hipFree(d_agg); hipFree(d_p0);
+        T.release(); P.release(); AP.release(); PT.release(); Ac.release();
+        if (Ph) aijhip_mat_destroy(Ph);
+        if (Ach) aijhip_mat_destroy(Ach);
+        if (rc == AIJHIP_ERR_STATE) {  // a row past the device accumulators
+            rc = AIJHIP_OK;
+            *more = true;
+            break;
+        }
+        if (rc) break;
+    }
+    if (rc) free_device_levels(levels);
+    return rc;
+}
+
+}  // namespace aijhip_gamg

@@ -1,0 +1,28 @@
+// gamg_internal.h — host pieces of the smoothed-aggregation set-up shared by
+// the host builder (gamg_setup.cpp) and the device builder (gamg_device.hip,
+// gamg_device.h).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "aijhip_gamg.h"
+
+namespace aijhip_gamg {
+
+// Greedy aggregation (gamg_setup.cpp aggregate) split around its parallel
+// middle phase, from the symmetric strength graph S (rows sorted, unique):
+// phase 1 roots aggregates at free nodes whose strong neighbours are all
+// free (returns the aggregate count so far); phase 2 (device) joins each
+// left-over node to its strongest stored phase-1 neighbour's aggregate;
+// phase 3 roots aggregates at what is left (returns the final count).
+int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg);
+int32_t aggregate_phase3(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t na);
+
+// Host continuation: the hierarchy below operator (m, ai, aj, aa) whose
+// near-null space is B (NULL = ones), at most p.max_levels levels counting
+// this one.
+int build_host_nns(int32_t m, const int32_t *ai, const int32_t *aj, const double *aa, const double *B,
+                   const aijhip_gamg_params_t &p, aijhip_gamg_host_t *out);
+
+}  // namespace aijhip_gamg

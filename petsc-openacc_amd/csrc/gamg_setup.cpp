@@ -21,6 +21,7 @@
 
 #include "aijhip.h"
 #include "aijhip_gamg.h"
+#include "gamg_internal.h"
 
 namespace {
 
@@ -376,6 +377,36 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
 
 }  // namespace
 
+namespace aijhip_gamg {
+
+int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg) {
+    std::fill(agg, agg + m, -1);
+    int32_t na = 0;
+    for (int32_t i = 0; i < m; ++i) {
+        if (agg[i] != -1 || si[i] == si[i + 1]) continue;
+        bool free_all = true;
+        for (int32_t k = si[i]; k < si[i + 1] && free_all; ++k) free_all = agg[sj[k]] == -1;
+        if (!free_all) continue;
+        agg[i] = na;
+        for (int32_t k = si[i]; k < si[i + 1]; ++k) agg[sj[k]] = na;
+        ++na;
+    }
+    return na;
+}
+
+int32_t aggregate_phase3(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t na) {
+    for (int32_t i = 0; i < m; ++i) {
+        if (agg[i] != -1) continue;
+        agg[i] = na;
+        for (int32_t k = si[i]; k < si[i + 1]; ++k)
+            if (agg[sj[k]] == -1) agg[sj[k]] = na;
+        ++na;
+    }
+    return na;
+}
+
+}  // namespace aijhip_gamg
+
 struct aijhip_gamg_host {
     std::vector<int32_t> m;          // rows per level
     std::vector<int64_t> nnz_a;
@@ -396,16 +427,24 @@ int aijhip_gamg_params_default(aijhip_gamg_params_t *p) {
     p->smooth_scale = 1.4;
     p->eig_its = 10;
     p->threads = 0;
+    p->device_min_rows = 20000;
     return AIJHIP_OK;
 }
 
 int aijhip_gamg_build_host(int32_t m, const int32_t *ai, const int32_t *aj, const double *aa,
                            const aijhip_gamg_params_t *pp, aijhip_gamg_host_t *out) {
-    if (!out || m < 0 || !ai || (ai[m] > 0 && (!aj || !aa))) return AIJHIP_ERR_ARG;
-    *out = nullptr;
     aijhip_gamg_params_t p;
     aijhip_gamg_params_default(&p);
     if (pp) p = *pp;
+    return aijhip_gamg::build_host_nns(m, ai, aj, aa, nullptr, p, out);
+}
+
+}  // extern "C"
+
+int aijhip_gamg::build_host_nns(int32_t m, const int32_t *ai, const int32_t *aj, const double *aa, const double *B0,
+                                const aijhip_gamg_params_t &p, aijhip_gamg_host_t *out) {
+    if (!out || m < 0 || !ai || (ai[m] > 0 && (!aj || !aa))) return AIJHIP_ERR_ARG;
+    *out = nullptr;
     if (p.max_levels < 1) return AIJHIP_ERR_ARG;
     const int nt = nthreads(p.threads);
     aijhip_gamg_host *H = new (std::nothrow) aijhip_gamg_host();
@@ -414,7 +453,9 @@ int aijhip_gamg_build_host(int32_t m, const int32_t *ai, const int32_t *aj, cons
         H->m.push_back(m);
         H->nnz_a.push_back(ai[m]);
         H->A.emplace_back();
-        std::vector<double> B(m, 1.0);  // near-null space of the scalar operator
+        // near-null space: the constant vector of the scalar operator, or
+        // the one the levels above handed down
+        std::vector<double> B = B0 ? std::vector<double>(B0, B0 + m) : std::vector<double>(m, 1.0);
         View cur{m, m, ai, aj, aa};
         const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
         double t0 = wtime();
@@ -467,6 +508,8 @@ int aijhip_gamg_build_host(int32_t m, const int32_t *ai, const int32_t *aj, cons
     *out = H;
     return AIJHIP_OK;
 }
+
+extern "C" {
 
 int aijhip_gamg_host_num_levels(aijhip_gamg_host_t h, int32_t *n) {
     if (!h || !n) return AIJHIP_ERR_ARG;

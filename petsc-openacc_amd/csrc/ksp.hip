@@ -30,6 +30,7 @@
 #include <vector>
 
 #include "aijhip_gamg.h"
+#include "gamg_device.h"
 #include "aijhip_internal.h"
 #include "aijhip_ksp.h"
 
@@ -412,81 +413,98 @@ dim3 vgrid(const aijhip_ksp *K, int64_t n) {
                                                                  (int64_t)K->A->n_cu * 8)));
 }
 
-// PCSetUp_GAMG: host hierarchy, device operators / interpolations / vectors.
-// AIJHIP_GAMG_LOG=1 prints the phases (with gamg_setup.cpp's own).
+// PCSetUp_GAMG. The large levels are built on the device
+// (aijhip_gamg::build_device: strength graph, emax, smoothing and Galerkin
+// product on the GPU, greedy aggregation on the host); the hierarchy below
+// device_min_rows rows (or past the device accumulators) continues on the
+// host from that level's operator and near-null space. Either way the
+// levels equal aijhip_gamg_build_host's bit for bit. AIJHIP_GAMG_LOG=1 prints
+// the phases.
 int gamg_setup(aijhip_ksp *K) {
     aijhip_mat *A = K->A;
-    const int32_t m = A->m;
-    const int64_t nz = A->nz;
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](const char *what) {
         if (!log) return;
         (void)hipDeviceSynchronize();
         const auto t = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "gamg device %-22s %8.3f s\n", what, std::chrono::duration<double>(t - t0).count());
+        std::fprintf(stderr, "gamg set-up %-22s %8.3f s\n", what, std::chrono::duration<double>(t - t0).count());
         t0 = t;
     };
-    std::vector<int32_t> ai((size_t)m + 1), aj((size_t)nz);
-    std::vector<double> aa((size_t)nz);
-    hipError_t e;
-    if ((e = hipMemcpy(ai.data(), A->d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (nz > 0 && ((e = hipMemcpy(aj.data(), A->d_aj, sizeof(int32_t) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess ||
-                    (e = hipMemcpy(aa.data(), A->d_aa, sizeof(double) * (size_t)nz, hipMemcpyDeviceToHost)) != hipSuccess)))
-        return khip(e, "GAMG: read operator");
-    lap("read operator");
+    std::vector<aijhip_gamg::DeviceLevel> dl;
+    std::vector<double> B;
+    bool more = false;
+    int rc = aijhip_gamg::build_device(A, K->gamg, dl, B, &more);
+    if (rc) return rc;
+    lap("device levels");
+    hipError_t e = hipSuccess;
     aijhip_gamg_host_t H = nullptr;
-    int rc = aijhip_gamg_build_host(m, ai.data(), aj.data(), aa.data(), &K->gamg, &H);
-    if (rc) return kfail(rc, "GAMG: host hierarchy set-up failed");
-    lap("host hierarchy");
-    ai = std::vector<int32_t>();
-    aj = std::vector<int32_t>();
-    aa = std::vector<double>();
-    int32_t nl = 0;
-    aijhip_gamg_host_num_levels(H, &nl);
+    int32_t nh = 0;
+    if (more) {  // host continuation from the last device level
+        const aijhip_mat &L = *dl.back().A;
+        std::vector<int32_t> ai((size_t)L.m + 1), aj((size_t)L.nz);
+        std::vector<double> aa((size_t)L.nz);
+        if ((e = hipMemcpy(ai.data(), L.d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
+            (L.nz > 0 &&
+             ((e = hipMemcpy(aj.data(), L.d_aj, sizeof(int32_t) * (size_t)L.nz, hipMemcpyDeviceToHost)) != hipSuccess ||
+              (e = hipMemcpy(aa.data(), L.d_aa, sizeof(double) * (size_t)L.nz, hipMemcpyDeviceToHost)) != hipSuccess))) {
+            aijhip_gamg::free_device_levels(dl);
+            return khip(e, "GAMG: read level operator");
+        }
+        aijhip_gamg_params_t hp = K->gamg;
+        hp.max_levels = K->gamg.max_levels - ((int32_t)dl.size() - 1);
+        rc = aijhip_gamg::build_host_nns(L.m, ai.data(), aj.data(), aa.data(), B.data(), hp, &H);
+        if (rc) {
+            aijhip_gamg::free_device_levels(dl);
+            return kfail(rc, "GAMG: host hierarchy set-up failed");
+        }
+        aijhip_gamg_host_num_levels(H, &nh);
+        lap("host levels");
+    }
+    const int32_t nd = (int32_t)dl.size();
+    const int32_t nl = nd + (nh > 0 ? nh - 1 : 0);
     K->mg.assign((size_t)nl, MGLevel());
-    rc = AIJHIP_OK;
-    for (int32_t l = 0; l < nl && !rc; ++l) {
-        MGLevel &L = K->mg[l];
+    for (int32_t l = 0; l < nd; ++l) {  // the device levels move into the KSP
+        K->mg[l].A = dl[l].A;
+        K->mg[l].own_A = l > 0;
+        K->mg[l].P = dl[l].P;
+    }
+    dl.clear();
+    for (int32_t hl = 1; hl < nh && !rc; ++hl) {  // host level hl = level nd - 1 + hl
+        MGLevel &L = K->mg[nd - 1 + hl];
+        MGLevel &U = K->mg[nd - 2 + hl];
+        int32_t mu = 0, mc = 0;
         int64_t nnz_a = 0, nnz_p = 0;
-        aijhip_gamg_host_level_info(H, l, &L.m, &nnz_a, &nnz_p, nullptr);
-        L.nnz = nnz_a;
+        aijhip_gamg_host_level_info(H, hl - 1, &mu, nullptr, &nnz_p, nullptr);
+        aijhip_gamg_host_level_info(H, hl, &mc, &nnz_a, nullptr, nullptr);
         const int32_t *xi, *xj;
         const double *xa;
-        if (l == 0) {
-            L.A = A;
-        } else {
-            aijhip_gamg_host_view(H, l, 'A', &xi, &xj, &xa);
-            rc = aijhip_mat_create(A->device, L.m, L.m, nnz_a, xi, xj, xa, &L.A);
-            L.own_A = rc == AIJHIP_OK;
-            if (rc) break;
-        }
-        if (l + 1 < nl) {
-            int32_t mc = 0;
-            aijhip_gamg_host_level_info(H, l + 1, &mc, nullptr, nullptr, nullptr);
-            aijhip_gamg_host_view(H, l, 'P', &xi, &xj, &xa);
-            rc = aijhip_mat_create(A->device, L.m, mc, nnz_p, xi, xj, xa, &L.P);
-            if (rc) break;
-        }
+        aijhip_gamg_host_view(H, hl - 1, 'P', &xi, &xj, &xa);
+        rc = aijhip_mat_create(A->device, mu, mc, nnz_p, xi, xj, xa, &U.P);
+        if (rc) break;
+        aijhip_gamg_host_view(H, hl, 'A', &xi, &xj, &xa);
+        rc = aijhip_mat_create(A->device, mc, mc, nnz_a, xi, xj, xa, &L.A);
+        L.own_A = rc == AIJHIP_OK;
+    }
+    if (H) aijhip_gamg_host_destroy(H);
+    if (rc) return rc;
+    for (int32_t l = 0; l < nl; ++l) {
+        MGLevel &L = K->mg[l];
+        L.m = L.A->m;
+        L.nnz = L.A->nz;
         const size_t vb = sizeof(double) * (size_t)std::max<int32_t>(L.m, 1);
         if ((e = hipMalloc(&L.dinv, vb)) != hipSuccess || (e = hipMalloc(&L.r, vb)) != hipSuccess ||
-            (l > 0 && ((e = hipMalloc(&L.b, vb)) != hipSuccess || (e = hipMalloc(&L.x, vb)) != hipSuccess))) {
-            rc = khip(e, "GAMG: level vectors");
-            break;
-        }
+            (l > 0 && ((e = hipMalloc(&L.b, vb)) != hipSuccess || (e = hipMalloc(&L.x, vb)) != hipSuccess)))
+            return khip(e, "GAMG: level vectors");
         if (L.m > 0)
             hipLaunchKernelGGL(k_diag_inv, dim3((unsigned)((L.m + 255) / 256)), dim3(256), 0, nullptr, L.m,
                                L.A->d_ai, L.A->d_aj, L.A->d_aa, L.dinv);
-        if (l < 2) lap(l == 0 ? "upload level 0" : "upload level 1");
     }
-    aijhip_gamg_host_destroy(H);
-    if (rc) return rc;
-    lap("upload coarse levels");
-    // build every restriction (P^T) now, not inside the first solve
+    // every restriction (P^T) exists before the first solve (the device
+    // levels attached theirs during the set-up)
     for (int32_t l = 0; l + 1 < nl; ++l) {
         MGLevel &L = K->mg[l];
-        rc = aijhip_mat_mult_transpose(L.P, L.r, K->mg[l + 1].b, nullptr);
-        if (rc) return rc;
+        if (!L.P->transpose && (rc = aijhip_mat_mult_transpose(L.P, L.r, K->mg[l + 1].b, nullptr))) return rc;
     }
     for (MGLevel &L : K->mg) L.fused = !std::getenv("AIJHIP_MG_UNFUSED") && aijhip::stream_mg_fusable(*L.A);
     if (K->mg[0].fused &&
@@ -494,7 +512,7 @@ int gamg_setup(aijhip_ksp *K) {
             hipSuccess)
         return khip(e, "GAMG partials");
     if ((e = hipDeviceSynchronize()) != hipSuccess) return khip(e, "GAMG set-up");
-    lap("restrictions P^T");
+    lap("level vectors, P^T");
     return AIJHIP_OK;
 }
 
@@ -791,6 +809,23 @@ int aijhip_ksp_get_pc_levels(aijhip_ksp_t K, int32_t *nlevels, int32_t *rows, in
     }
     if (setup_seconds) *setup_seconds = K->setup_seconds;
     return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_pc_level(aijhip_ksp_t K, int32_t l, char which, int32_t *m, int32_t *n, int64_t *nnz,
+                            int32_t *ai, int32_t *aj, double *aa) {
+    if (!K || l < 0 || l >= (int32_t)K->mg.size() || (which != 'A' && which != 'P'))
+        return kfail(AIJHIP_ERR_ARG, "no such PC level (set up a GAMG KSP first)");
+    const aijhip_mat *M = which == 'A' ? K->mg[l].A : K->mg[l].P;
+    if (!M) return kfail(AIJHIP_ERR_ARG, "the coarsest level has no interpolation");
+    if (m) *m = M->m;
+    if (n) *n = M->n;
+    if (nnz) *nnz = M->nz;
+    if (!ai) return AIJHIP_OK;
+    KDeviceGuard g(M->device);
+    hipError_t e = hipMemcpy(ai, M->d_ai, sizeof(int32_t) * ((size_t)M->m + 1), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && aj && M->nz > 0) e = hipMemcpy(aj, M->d_aj, sizeof(int32_t) * (size_t)M->nz, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && aa && M->nz > 0) e = hipMemcpy(aa, M->d_aa, sizeof(double) * (size_t)M->nz, hipMemcpyDeviceToHost);
+    return e == hipSuccess ? AIJHIP_OK : khip(e, "read PC level");
 }
 
 int aijhip_ksp_destroy(aijhip_ksp_t K) {

@@ -26,7 +26,7 @@ KSP_SYMBOLS = (
     "aijhip_ksp_set_initial_guess_nonzero", "aijhip_ksp_set_up", "aijhip_ksp_solve",
     "aijhip_ksp_get_iteration_number", "aijhip_ksp_get_residual_norm", "aijhip_ksp_get_converged_reason",
     "aijhip_ksp_get_residual_history", "aijhip_ksp_get_fused", "aijhip_ksp_destroy",
-    "aijhip_ksp_set_gamg_params", "aijhip_ksp_get_pc_levels",
+    "aijhip_ksp_set_gamg_params", "aijhip_ksp_get_pc_levels", "aijhip_ksp_get_pc_level",
 )
 _P = ctypes.c_void_p
 _bound = False
@@ -52,6 +52,8 @@ def _lib():
         L.aijhip_ksp_get_fused.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
         L.aijhip_ksp_destroy.argtypes = [_P]
         L.aijhip_ksp_set_gamg_params.argtypes = [_P, _P]
+        L.aijhip_ksp_get_pc_level.argtypes = [_P, ctypes.c_int32, ctypes.c_char, ctypes.POINTER(ctypes.c_int32),
+                                              ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64), _P, _P, _P]
         L.aijhip_ksp_get_pc_levels.argtypes = [_P, ctypes.POINTER(ctypes.c_int32), _P, _P, ctypes.c_int32,
                                                ctypes.POINTER(ctypes.c_double)]
         _bound = True
@@ -119,6 +121,20 @@ class KSPCG:
         _pkg._check(_lib().aijhip_ksp_get_pc_levels(self._h, ctypes.byref(n), rows.ctypes.data, nnz.ctypes.data,
                                                      32, ctypes.byref(secs)))
         return rows[: n.value].tolist(), nnz[: n.value].tolist(), secs.value
+
+    def pc_level(self, l: int, which: str = "A"):
+        """(ai, aj, aa, ncols) of GAMG level l's operator ('A') or
+        interpolation to level l+1 ('P'), copied from the device."""
+        m, n, nz = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64()
+        L = _lib()
+        _pkg._check(L.aijhip_ksp_get_pc_level(self._h, l, which.encode(), ctypes.byref(m), ctypes.byref(n),
+                                              ctypes.byref(nz), None, None, None))
+        ai = np.empty(m.value + 1, np.int32)
+        aj = np.empty(max(nz.value, 1), np.int32)
+        aa = np.empty(max(nz.value, 1), np.float64)
+        _pkg._check(L.aijhip_ksp_get_pc_level(self._h, l, which.encode(), None, None, None, ai.ctypes.data,
+                                              aj.ctypes.data, aa.ctypes.data))
+        return ai, aj[: nz.value], aa[: nz.value], n.value
 
     def history(self) -> np.ndarray:
         buf = np.empty(self.its + 1)

@@ -139,3 +139,49 @@ def test_oracle_vcycle_preconditions_cg():
     # Jacobi sweep as the coarse solve) make a modest V-cycle, still < half
     # of Jacobi-CG's iterations at 10^3
     assert its < its_j / 2, (its, its_j)
+
+
+def _bits(x):
+    return np.ascontiguousarray(x).view(np.uint64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,params", [
+    ((8, 8, 8), dict(coarse_eq_limit=20)),
+    ((12, 12, 12), dict(coarse_eq_limit=20)),
+    ((6, 7, 5), dict(coarse_eq_limit=20)),
+    ((20, 20, 20), {}),
+    ((24, 24, 24), dict(coarse_eq_limit=20)),
+    ((16, 16, 16), dict(threshold=0.05)),
+    ((16, 16, 16), dict(nsmooths=0)),
+    ((32, 32, 32), dict(device_min_rows=20000)),  # device level 0, host below
+])
+def test_gpu_device_setup_matches_host_bitwise(pkg, dims, params):
+    """The KSP's device-built hierarchy (aijhip_gamg::build_device, host
+    continuation below device_min_rows) equals the host builder's — itself
+    bit-identical to oracle/gamg.py — entry for entry."""
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available()
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    ai, aj, aa = pkg.poisson_csr(*dims)
+    prm = dict(device_min_rows=0)
+    prm.update(params)
+    lv = G.build_host(ai, aj, aa, **prm)
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    with K.KSPCG(A, pc="gamg", gamg=prm) as ksp:
+        ksp.set_up()
+        rows, nnz, _ = ksp.pc_levels()
+        assert rows == [L["m"] for L in lv]
+        for l in range(1, len(lv)):
+            dai, daj, daa, _ = ksp.pc_level(l, "A")
+            hai, haj, haa = lv[l]["A"]
+            assert np.array_equal(dai, hai) and np.array_equal(daj, haj), l
+            assert np.array_equal(_bits(daa), _bits(haa)), l
+        for l in range(len(lv) - 1):
+            pai, paj, paa, pn = ksp.pc_level(l, "P")
+            hai, haj, haa = lv[l]["P"]
+            assert pn == lv[l + 1]["m"]
+            assert np.array_equal(pai, hai) and np.array_equal(paj, haj), l
+            assert np.array_equal(_bits(paa), _bits(haa)), l
+    A.destroy()
