@@ -222,7 +222,7 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
         its, reason, rnorm = ksp.its, ksp.reason, ksp.rnorm
     err = float((x.cpu() - torch.from_numpy(exact)).abs().max())
     return {"its": its, "reason": reason, "rnorm": rnorm, "max_err": err,
-            "setup_s": round(t_setup, 3), "setup_host_s": round(t_host, 3),
+            "setup_s": round(t_setup, 3), "setup_pc_s": round(t_host, 3),
             "solve_s": round(t_solve, 4), "first_solve_s": round(t_first, 4),
             "ms_per_iter": round(t_solve / max(its, 1) * 1e3, 4),
             "time_to_solution_s": round(t_setup + t_solve, 3),
