@@ -36,7 +36,7 @@ constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
 constexpr int kMaxStreamNnzCap = 8192;
 // A row longer than the geometry's nnz_cap leaves the STREAM blocks and is split into
 // segments of at most kLongSegNnz entries, each summed by one workgroup.
-constexpr int kLongSegNnz = 16384;
+constexpr int kLongSegNnz = 4096;
 constexpr int kLongThreads = 256;
 // MERGE kernel: 256 lanes x kMergeItems merge-path items per workgroup.
 constexpr int kMergeThreads = 256;

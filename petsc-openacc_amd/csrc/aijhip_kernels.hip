@@ -171,7 +171,8 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
     if (stop && *stop) return;  // CG launched past convergence: no work
-    const int b = XCD ? xcd_chunk_remap(blockIdx.x, nblk, xchunk) : (int)blockIdx.x;
+    const int bid = (int)blockIdx.x;
+    const int b = XCD ? xcd_chunk_remap(bid, nblk, xchunk) : bid;
     const BlockDesc d = blk[b];
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
@@ -352,26 +353,44 @@ __global__ __launch_bounds__(T) void k_spmv_stream_pipe(
     }
 }
 
-// Segments of long rows: tree-reduced partial sums.
+// Segments of long rows: tree-reduced partial sums. Each lane keeps U
+// independent partial sums (entries t + (i*U + u)*T, combined u = 0..U-1 at
+// the end: a fixed order) so U loads and gathers are in flight at once — a
+// hub row's gathers are scattered over all of x, and one dependent chain per
+// lane left the kernel latency-bound.
 __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     const LongSeg *__restrict__ seg, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const double *__restrict__ x,
     double *__restrict__ partials) {
+    constexpr int U = 8;
     __shared__ double red[kLongThreads / 64];
     const LongSeg s = seg[blockIdx.x];
     const int t = threadIdx.x;
-    double acc = 0.0;
+    double acc[U] = {};
     const int64_t k1 = (int64_t)s.k0 + s.nk;
-    for (int64_t k = (int64_t)s.k0 + t; k < k1; k += kLongThreads) acc += aa[k] * x[aj[k]];
+    for (int64_t kb = (int64_t)s.k0 + t; kb < k1; kb += (int64_t)U * kLongThreads) {
+        double a[U], xv[U];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
-    if ((t & 63) == 0) red[t >> 6] = acc;
+        for (int u = 0; u < U; ++u) {
+            const int64_t k = kb + (int64_t)u * kLongThreads;
+            a[u] = k < k1 ? aa[k] : 0.0;
+            xv[u] = k < k1 ? x[aj[k]] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc[u] += a[u] * xv[u];
+    }
+    double v = acc[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) v += acc[u];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    if ((t & 63) == 0) red[t >> 6] = v;
     __syncthreads();
     if (t == 0) {
-        double v = red[0];
+        double r = red[0];
 #pragma unroll
-        for (int w = 1; w < kLongThreads / 64; ++w) v += red[w];
-        partials[blockIdx.x] = v;
+        for (int w = 1; w < kLongThreads / 64; ++w) r += red[w];
+        partials[blockIdx.x] = r;
     }
 }
 

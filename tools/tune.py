@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--variants", default="stream")
-    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed"])
+    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub"])
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
     dev = torch.device("cuda:0")
@@ -50,6 +50,11 @@ def main():
         ai, aj, aa = pkg.poisson_csr(args.grid)
     else:
         ai, aj, aa = pkg.skewed_csr()
+        if args.matrix == "skewed_nohub":  # the FEM-like rows only (hub rows emptied)
+            ln = np.diff(ai)
+            keep = np.repeat(ln <= 1000, ln)
+            ai = np.concatenate([[0], np.cumsum(np.where(ln <= 1000, ln, 0))]).astype(np.int32)
+            aj, aa = aj[keep], aa[keep]
     m = len(ai) - 1
     nbytes = pkg.algorithmic_bytes(m, m, len(aj))
     x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
@@ -77,11 +82,14 @@ def main():
     if args.variants == "skewed":
         for g in (0, 1, 4, 6, 7, 8):
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=0)))
+        for g in (1, 6):
+            variants.append(("stream", dict(geometry=g, exact=1)))
         variants += [("vector", {"lanes": 16}), ("vector", {"lanes": 32}), ("vector", {"lanes": 64}),
                      ("merge", {}), ("scalar", {})]
 
     def configure(kind, opts):
         A.set_kernel(kind, opts.get("lanes", 0))
+        A.set_option("exact", opts.get("exact", 0))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
