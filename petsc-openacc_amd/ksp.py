@@ -10,6 +10,7 @@ Jacobi (the reference's smoother / coarse PC) until the GAMG hierarchy lands.
 from __future__ import annotations
 
 import ctypes
+import math
 import importlib
 import time
 
@@ -229,3 +230,165 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
             "levels": [{"rows": r, "nnz": z} for r, z in zip(rows, nnz)],
             "options": "cg, gamg agg nsmooths 1 threshold 0, mg levels richardson(1)+jacobi, "
                        "coarse preonly+jacobi, rtol 1e-14 atol 1e-12"}
+
+
+# ----------------------------------------------------------------------------
+# Row-partitioned CG: one process per GPU, the operator an
+# MPIAIJ row block (petsc-openacc_amd/mpiaij.py), every dot product a local
+# fixed-order reduction on the device (include/aijhip_vec.h) combined across
+# ranks by one all-reduce (RCCL over xGMI with the nccl backend) — PETSc's
+# VecDot/VecNorm -> MPI_Allreduce. The iteration is KSPSolve_CG [ext] as in
+# aijhip_ksp (and oracle/ksp_cg.py): the scalar decisions run on the host
+# from the reduced values, which every rank holds identically, so all ranks
+# take the same branch. PC: Jacobi (PETSc's bjacobi + jacobi sub-PC per rank)
+# or none.
+
+VEC_SYMBOLS = ("aijhip_vec_aypx", "aijhip_vec_dot", "aijhip_vec_cg_update", "aijhip_vec_jacobi",
+               "aijhip_mat_jacobi_inverse")
+
+_vec_bound = False
+
+
+def _veclib():
+    global _vec_bound
+    L = _pkg.lib()
+    if not _vec_bound:
+        for n in VEC_SYMBOLS:
+            getattr(L, n).restype = ctypes.c_int
+        i64, d = ctypes.c_int64, ctypes.c_double
+        L.aijhip_vec_aypx.argtypes = [i64, d, _P, _P, _P]
+        L.aijhip_vec_dot.argtypes = [i64, _P, _P, _P, _P]
+        L.aijhip_vec_cg_update.argtypes = [i64, d, _P, _P, _P, _P, _P, _P, _P, _P]
+        L.aijhip_vec_jacobi.argtypes = [i64, _P, _P, _P, _P, _P]
+        L.aijhip_mat_jacobi_inverse.argtypes = [_P, _P, _P]
+        _vec_bound = True
+    return L
+
+
+class DeviceVecOps:
+    """The HIP vector kernels (aijhip_vec.h) on float64 GPU tensors; each
+    reduction lands in a small device tensor ready for the all-reduce."""
+
+    def __init__(self, device):
+        import torch
+        self.red = torch.zeros(3, dtype=torch.float64, device=device)
+
+    @staticmethod
+    def _s():
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+
+    def aypx(self, beta, x, y):
+        _pkg._check(_veclib().aijhip_vec_aypx(x.numel(), beta, x.data_ptr(), y.data_ptr(), self._s()))
+
+    def dot(self, x, y):
+        _pkg._check(_veclib().aijhip_vec_dot(x.numel(), x.data_ptr(), y.data_ptr(), self.red.data_ptr(), self._s()))
+        return self.red[:1]
+
+    def cg_update(self, a, x, p, r, w, z, dinv):
+        _pkg._check(_veclib().aijhip_vec_cg_update(x.numel(), a, x.data_ptr(), p.data_ptr(), r.data_ptr(),
+                                                   w.data_ptr(), z.data_ptr(),
+                                                   dinv.data_ptr() if dinv is not None else None,
+                                                   self.red.data_ptr(), self._s()))
+        return self.red
+
+    def jacobi(self, r, dinv, z):
+        _pkg._check(_veclib().aijhip_vec_jacobi(r.numel(), r.data_ptr(), dinv.data_ptr() if dinv is not None else None,
+                                                z.data_ptr(), self.red.data_ptr(), self._s()))
+        return self.red
+
+    @staticmethod
+    def jacobi_inverse(A_diag, dinv):
+        _pkg._check(_veclib().aijhip_mat_jacobi_inverse(A_diag._h, dinv.data_ptr(), DeviceVecOps._s()))
+
+
+class KSPCGMPI:
+    """KSPSolve_CG over a row-partitioned operator. op: object with
+    mult(x, y) on this rank's rows (MPIAIJ); dinv: this rank's Jacobi inverse
+    (None = PCNONE); ops: vector backend (DeviceVecOps on the GPU)."""
+
+    CONVERGED_RTOL, CONVERGED_ATOL = 2, 3
+    DIVERGED_ITS, DIVERGED_DTOL, DIVERGED_INDEFINITE_PC, DIVERGED_NANORINF, DIVERGED_INDEFINITE_MAT = \
+        -3, -4, -8, -9, -10
+
+    def __init__(self, op, mloc, dinv=None, ops=None, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000,
+                 norm="preconditioned", group=None, device=None):
+        import torch
+        self.op, self.m, self.dinv = op, mloc, dinv
+        self.ops = ops if ops is not None else DeviceVecOps(device)
+        self.rtol, self.atol, self.dtol, self.max_it, self.norm = rtol, atol, dtol, max_it, norm
+        self.group = group
+        dev = device if device is not None else (dinv.device if dinv is not None else None)
+        mk = lambda: torch.zeros(mloc, dtype=torch.float64, device=dev)  # noqa: E731
+        self.r, self.z, self.p = mk(), mk(), mk()
+        self.its, self.reason, self.rnorm, self.hist = 0, 0, 0.0, []
+
+    def _allreduce(self, t):
+        """Sum over ranks (in place) and return the values on the host."""
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(t, group=self.group)
+        return [float(v) for v in t.tolist()]
+
+    def _norm(self, zz, zr, rr):
+        if self.norm == "preconditioned":
+            return math.sqrt(zz)
+        if self.norm == "unpreconditioned":
+            return math.sqrt(rr)
+        return math.sqrt(abs(zr))
+
+    def _test(self, rn):
+        if math.isnan(rn) or math.isinf(rn):
+            return self.DIVERGED_NANORINF
+        if rn <= self.ttol:
+            return self.CONVERGED_ATOL if rn < self.atol else self.CONVERGED_RTOL
+        if rn >= self.dtol * self.rnorm0:
+            return self.DIVERGED_DTOL
+        return 0
+
+    def solve(self, b, x):
+        """Zero initial guess (main_ksp.cpp: VecSet(lhs, 0))."""
+        ops, r, z, p = self.ops, self.r, self.z, self.p
+        x.zero_()
+        r.copy_(b)
+        zz, zr, rr = self._allreduce(ops.jacobi(r, self.dinv, z))
+        dp = self._norm(zz, zr, rr)
+        self.hist = [dp]
+        self.rnorm0 = dp
+        self.ttol = max(self.rtol * dp, self.atol)
+        self.reason = self._test(dp)
+        self.its, self.rnorm = 0, dp
+        if self.reason:
+            return self.reason
+        beta, betaold, dpi = zr, 0.0, 0.0
+        i = 0
+        while i < self.max_it:
+            self.its = i + 1
+            if beta == 0.0:
+                self.reason = self.CONVERGED_ATOL
+                return self.reason
+            if i > 0 and beta * betaold < 0.0:
+                self.reason = self.DIVERGED_INDEFINITE_PC
+                return self.reason
+            if i == 0:
+                p.copy_(z)
+            else:
+                ops.aypx(beta / betaold, z, p)
+            self.op.mult(p, z)  # W = A P (W shares Z's storage)
+            dpiold, dpi = dpi, self._allreduce(ops.dot(p, z))[0]
+            betaold = beta
+            if dpi == 0.0 or (i > 0 and dpi * dpiold <= 0.0):
+                self.reason = self.DIVERGED_INDEFINITE_MAT
+                return self.reason
+            a = beta / dpi
+            zz, zr, rr = self._allreduce(ops.cg_update(a, x, p, r, z, z, self.dinv))
+            dp = self._norm(zz, zr, rr)
+            self.hist.append(dp)
+            self.rnorm = dp
+            self.reason = self._test(dp)
+            if self.reason:
+                return self.reason
+            beta = zr
+            i += 1
+        self.reason = self.DIVERGED_ITS
+        return self.reason

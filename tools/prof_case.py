@@ -23,7 +23,8 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("case", choices=["gamg", "jacobi", "skewed"])
+    ap.add_argument("case", choices=["gamg", "jacobi", "skewed", "skewed_nohub", "poisson"])
+    ap.add_argument("--exact", type=int, default=0)
     ap.add_argument("--grid", type=int, default=300)
     ap.add_argument("--its", type=int, default=50)
     ap.add_argument("--kernel", default="auto")
@@ -31,15 +32,24 @@ def main():
     pkg = importlib.import_module("petsc-openacc_amd")
     K = importlib.import_module("petsc-openacc_amd.ksp")
     dev = torch.device("cuda:0")
-    if args.case == "skewed":
-        ai, aj, aa = pkg.skewed_csr()
-        A = pkg.SeqAIJHIP(ai, aj, aa, kernel=args.kernel)
+    if args.case in ("skewed", "skewed_nohub", "poisson"):
+        if args.case == "poisson":
+            ai, aj, aa = pkg.poisson_csr(args.grid)
+        else:
+            ai, aj, aa = pkg.skewed_csr()
+        if args.case == "skewed_nohub":  # hub rows emptied (tools/tune.py)
+            import numpy as np
+            ln = np.diff(ai)
+            keep = np.repeat(ln <= 1000, ln)
+            ai = np.concatenate([[0], np.cumsum(np.where(ln <= 1000, ln, 0))]).astype(np.int32)
+            aj, aa = aj[keep], aa[keep]
+        A = pkg.SeqAIJHIP(ai, aj, aa, kernel=args.kernel, exact=args.exact)
         x = torch.from_numpy(pkg.splitmix_uniform(A.n, 42)).to(dev)
         y = torch.empty(A.m, dtype=torch.float64, device=dev)
         for _ in range(args.its):
             A.mult(x, y)
         torch.cuda.synchronize()
-        print("skewed", A.info())
+        print(args.case, A.info())
         return
     G = args.grid
     ai, aj, aa = pkg.poisson_csr(G)

@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--variants", default="stream")
-    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub"])
+    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx"])
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
     dev = torch.device("cuda:0")
@@ -50,11 +50,13 @@ def main():
         ai, aj, aa = pkg.poisson_csr(args.grid)
     else:
         ai, aj, aa = pkg.skewed_csr()
-        if args.matrix == "skewed_nohub":  # the FEM-like rows only (hub rows emptied)
+        if args.matrix in ("skewed_nohub", "skewed_localx"):  # the FEM-like rows only (hub rows emptied)
             ln = np.diff(ai)
             keep = np.repeat(ln <= 1000, ln)
             ai = np.concatenate([[0], np.cumsum(np.where(ln <= 1000, ln, 0))]).astype(np.int32)
             aj, aa = aj[keep], aa[keep]
+        if args.matrix == "skewed_localx":  # experiment: same stream, x gathers confined to 32 KiB
+            aj = (aj & 4095).astype(np.int32)
     m = len(ai) - 1
     nbytes = pkg.algorithmic_bytes(m, m, len(aj))
     x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
@@ -79,6 +81,12 @@ def main():
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=p, clamped=0)))
     if args.variants in ("kernels", "all"):
         variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
+    if args.variants == "skewgeom":
+        for g, ex in itertools.product(range(9), (0, 1)):
+            variants.append(("stream", dict(geometry=g, exact=ex)))
+    if args.variants == "skewpipe":
+        for g, ex, pp in itertools.product((1, 7), (0, 1), (0, 1, 2, 3)):
+            variants.append(("stream", dict(geometry=g, exact=ex, persistent=pp)))
     if args.variants == "skewed":
         for g in (0, 1, 4, 6, 7, 8):
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=0)))
