@@ -59,6 +59,9 @@ def parse():
     p.add_argument("--no-gamg", action="store_true", help="skip the CG+GAMG solve (BASELINE configs[2])")
     p.add_argument("--gamg-cpu-iters", type=int, default=3, help="CG+GAMG iterations in the CPU sample")
     p.add_argument("--cg-iters", type=int, default=200, help="CG iterations timed for cg.iters_per_s")
+    p.add_argument("--mpi", action="store_true",
+                   help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
+                        "(launch with torch.distributed.run): a one-GPU rehearsal of the N > 1 run")
     return p.parse_args()
 
 
@@ -191,7 +194,7 @@ def main():
         raise SystemExit("bench.py needs a GPU (the HIP path has no CPU fallback)")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    distributed = world > 1
+    distributed = world > 1 or args.mpi
 
     def configure(mat):
         for opt, val in (("geometry", args.geometry), ("xcd_remap", args.xcd), ("nt_loads", args.nt),
