@@ -10,7 +10,7 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT" || exit 1
 export TMPDIR=/tmp
-B="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-cg $*"
+B="bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-cg --no-gamg $*"
 run() {  # name counters...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- python3 $B \
