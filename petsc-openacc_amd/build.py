@@ -69,7 +69,8 @@ def build_lib(force: bool = False) -> Path:
             _run(cmd)
         objs.append(str(o))
     tmp = LIB.with_suffix(".so.tmp")
-    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs, "-lgomp"])
+    _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs, "-lgomp",
+          "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"])
     os.replace(tmp, LIB)
     return LIB
 

@@ -408,12 +408,14 @@ int aijhip_device_count(int *count) {
 
 int aijhip_mat_create(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
                       const int32_t *aj, const double *aa, aijhip_mat_t *out) {
+    aijhip::Range range("MatAssemblyEnd_SeqAIJHIP");
     return create_impl(device, m, n, nz, ai, aj, aa, out);
 }
 
 int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
                                   const int32_t *d_ai, const int32_t *d_aj,
                                   const double *d_aa, aijhip_mat_t *out) {
+    aijhip::Range range("MatAssemblyEnd_SeqAIJHIP (device arrays)");
     if (!out) return fail(AIJHIP_ERR_ARG, "out is NULL");
     if (m < 0 || n < 0 || nz < 0 || !d_ai || (nz > 0 && (!d_aj || !d_aa)))
         return fail(AIJHIP_ERR_ARG, "bad size or NULL array");
@@ -494,6 +496,7 @@ int aijhip_mat_update_values(aijhip_mat_t A, const double *aa) {
 
 int aijhip_mat_assembly_end(aijhip_mat_t A, int64_t nz, const int32_t *ai, const int32_t *aj,
                             const double *aa) {
+    aijhip::Range range("MatAssemblyEnd_SeqAIJHIP");
     int rc = check_handle(A);
     if (rc) return rc;
     aijhip_mat_t B = nullptr;

@@ -3,6 +3,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <stdint.h>
 
 #include <string>
@@ -11,6 +12,16 @@
 #include "aijhip.h"
 
 namespace aijhip {
+
+// roctx range for the PETSc-level phases (MatAssemblyEnd, KSPSetUp,
+// KSPSolve, the GAMG set-up levels): shown by `rocprofv3 --marker-trace`,
+// a no-op call when no tool is attached.
+struct Range {
+    explicit Range(const char *name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range &) = delete;
+    Range &operator=(const Range &) = delete;
+};
 
 // STREAM kernel geometries: `threads` lanes per row
 // block, up to `nnz_cap` products staged in LDS (8 B each) and up to

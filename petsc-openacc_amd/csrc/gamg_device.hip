@@ -514,6 +514,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     while ((int32_t)levels.size() < p.max_levels && levels.back().A->m > p.coarse_eq_limit) {
         aijhip_mat &A = *levels.back().A;
         const int32_t m = A.m;
+        aijhip::Range range("PCGAMG device level");
         if (m < p.device_min_rows || !aijhip::stream_mg_fusable(A)) {
             *more = true;  // the host takes it from here
             break;

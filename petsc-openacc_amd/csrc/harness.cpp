@@ -68,7 +68,8 @@ int aijhip_poisson_nnz(int32_t nx, int32_t ny, int32_t nz, int32_t z0, int32_t z
 int aijhip_poisson_fill(int32_t nx, int32_t ny, int32_t nz, int32_t z0, int32_t z1, int ref_point,
                         int32_t *ai, int32_t *aj, double *aa, double *scale) {
     Grid g;
-    if (!ai || !aj || !aa || make_grid(nx, ny, nz, z0, z1, &g)) return AIJHIP_ERR_ARG;
+    if (!ai || make_grid(nx, ny, nz, z0, z1, &g)) return AIJHIP_ERR_ARG;
+    if (z1 > z0 && (!aj || !aa)) return AIJHIP_ERR_ARG;  // an empty slab needs only ai
     const int64_t row0 = (int64_t)z0 * g.nxy;
     int64_t p = 0;
     int64_t lr = 0;

@@ -421,6 +421,7 @@ dim3 vgrid(const aijhip_ksp *K, int64_t n) {
 // levels equal aijhip_gamg_build_host's bit for bit. AIJHIP_GAMG_LOG=1 prints
 // the phases.
 int gamg_setup(aijhip_ksp *K) {
+    aijhip::Range range("PCSetUp_GAMG");
     aijhip_mat *A = K->A;
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
@@ -632,6 +633,7 @@ int aijhip_ksp_set_initial_guess_nonzero(aijhip_ksp_t K, int flg) {
 }
 
 int aijhip_ksp_set_up(aijhip_ksp_t K) {
+    aijhip::Range range("KSPSetUp");
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
     if (K->set_up) return AIJHIP_OK;
     const auto t0 = std::chrono::steady_clock::now();
@@ -675,6 +677,7 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
 }
 
 int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
+    aijhip::Range range("KSPSolve");
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
     int rc = aijhip_ksp_set_up(K);
     if (rc) return rc;

@@ -138,7 +138,7 @@ extern "C" {
 int aijhip_poisson_fill_device(int32_t nx, int32_t ny, int32_t nz, int32_t z0, int32_t z1, int ref_point,
                                int32_t *d_ai, int32_t *d_aj, double *d_aa, double *scale, void *stream) {
     Grid g;
-    if (!d_ai || !d_aj || !d_aa || aijhip_poisson::make_grid(nx, ny, nz, z0, z1, &g)) {
+    if (!d_ai || aijhip_poisson::make_grid(nx, ny, nz, z0, z1, &g) || (z1 > z0 && (!d_aj || !d_aa))) {
         aijhip::set_error("poisson_fill_device: bad grid or NULL array");
         return AIJHIP_ERR_ARG;
     }
