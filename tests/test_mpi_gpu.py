@@ -1,0 +1,96 @@
+"""The multi-GPU code path on one GPU: k ranks as k
+processes sharing cuda:0, torch.distributed over gloo (which takes GPU
+tensors for the halo send/recv, all-gather and all-reduce), the per-rank
+operators the product's SeqAIJHIP handles (HIP kernels), the exchange and
+the distributed CG the product's (mpiaij.py, ksp.py KSPCGMPI with the device
+vector kernels). RCCL itself runs only in the driver's multi-GPU bench."""
+import importlib
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import ksp_cg, seqaij
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, dims, halo, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg = importlib.import_module("petsc-openacc_amd")
+        mp_mod = importlib.import_module("petsc-openacc_amd.mpiaij")
+        K = importlib.import_module("petsc-openacc_amd.ksp")
+        dev = torch.device("cuda:0")
+        nx, ny, nz = dims
+        bounds = [mp_mod.slab_bounds(nz, world, r) for r in range(world)]
+        row_starts = np.array([b[0] * nx * ny for b in bounds] + [nx * ny * nz], dtype=np.int64)
+        z0, z1 = bounds[rank]
+        ai, aj, aa = pkg.poisson_csr(nx, ny, nz, z0, z1)
+
+        def make_local(a_i, a_j, a_a, ncols):
+            return pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols)
+
+        op = mp_mod.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=halo)
+        lo, hi = int(row_starts[rank]), int(row_starts[rank + 1])
+        xg = seqaij.splitmix_uniform(nx * ny * nz, 42)
+        x = torch.from_numpy(xg[lo:hi].copy()).to(dev)
+        y = torch.empty(hi - lo, dtype=torch.float64, device=dev)
+        op.mult(x, y)
+        torch.cuda.synchronize()
+        rhs, _ = pkg.poisson_vectors(nx, ny, nz, z0, z1)
+        b = torch.from_numpy(rhs).to(dev)
+        dinv = torch.empty_like(b)
+        K.DeviceVecOps.jacobi_inverse(op.A_d, dinv)
+        cg = K.KSPCGMPI(op, op.mloc, dinv=dinv, rtol=1e-10, max_it=1000, device=dev)
+        xs = torch.zeros_like(b)
+        cg.solve(b, xs)
+        torch.cuda.synchronize()
+        q.put((rank, y.cpu().numpy(), xs.cpu().numpy(), cg.its, cg.reason, list(cg.hist)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,dims,halo", [(2, (12, 10, 16), "p2p"), (3, (9, 8, 13), "allgather"),
+                                             (3, (10, 10, 12), "p2p")])
+def test_gpu_mpiaij_and_cg_on_k_ranks(world, dims, halo):
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, dims, halo, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r = q.get(timeout=300)
+        got[r[0]] = r[1:]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    nx, ny, nz = dims
+    ai, aj, aa, rhs, _ = seqaij.create_system(nx, ny, nz)
+    y_ref = seqaij.matmult(ai, aj, aa, seqaij.splitmix_uniform(nx * ny * nz, 42))
+    y = np.concatenate([got[r][0] for r in range(world)])
+    # each block's sums keep PETSc's order; the off-diagonal entries of a row
+    # are added after its diagonal-block part (MatMult_MPIAIJ), so compare to
+    # rounding
+    np.testing.assert_allclose(y, y_ref, rtol=1e-12, atol=1e-12 * np.abs(y_ref).max())
+    xo, its_o, reason_o, hist_o = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-10, max_it=1000)
+    assert len({got[r][2] for r in range(world)}) == 1
+    assert abs(got[0][2] - its_o) <= 1 and got[0][3] == reason_o
+    np.testing.assert_allclose(got[0][4][:10], hist_o[:10], rtol=1e-9)
+    x = np.concatenate([got[r][1] for r in range(world)])
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
