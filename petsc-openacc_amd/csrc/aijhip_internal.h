@@ -94,8 +94,11 @@ struct Tuning {
 };
 
 // STREAM blocks whose mean row length exceeds this use several lanes per row
-// in the reduction phase (reordered sum) unless Tuning::exact is set.
-constexpr int kSplitMinMean = 16;
+// in the reduction phase (reordered sum) unless Tuning::exact is set. Measured
+// (tools/rowlen_sweep.py, profiles/r01/rowlen_sweep.jsonl): one lane per row
+// is as fast or faster up to ~100 entries per row, several lanes win from
+// ~200 (row length 384: 346 vs 619 us).
+constexpr int kSplitMinMean = 128;
 
 struct Plan {
     int kernel = AIJHIP_KERNEL_STREAM;

@@ -95,6 +95,26 @@ def test_stream_default_mode(pkg, dev, name):
         assert_bits(y, g["y"])
 
 
+@pytest.mark.parametrize("row_len", [150, 300, 1000])
+def test_stream_multilane_long_rows(pkg, dev, row_len):
+    """Blocks of rows longer than kSplitMinMean (128) are summed by several
+    lanes per row by default (fp64 bound), sequentially with exact=1
+    (bit-exact); a ragged tail of short rows stays exact either way."""
+    rng = np.random.default_rng(row_len)
+    m = 3000
+    lens = np.where(np.arange(m) < 2500, row_len, rng.integers(1, 9, m))
+    ai = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    aj = np.concatenate([np.sort(rng.choice(m, size=l, replace=False)) for l in lens]).astype(np.int32)
+    aa = rng.uniform(-1, 1, ai[-1])
+    x = rng.uniform(-1, 1, m)
+    y_ref = seqaij.matmult(ai, aj, aa, x)
+    y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=0)
+    check(y, y_ref, ai, aj, aa, x, exact=False)
+    assert_bits(y[2600:], y_ref[2600:])  # blocks of short rows only
+    y1, _ = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=1)
+    assert_bits(y1, y_ref)
+
+
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 @pytest.mark.parametrize("kernel", ALL_KERNELS)
 def test_mult_add_golden(pkg, dev, name, kernel):
