@@ -143,16 +143,13 @@ enum {
                                        STREAM, k workgroups per CU (0 = off) */
     AIJHIP_OPT_CLAMPED_LOADS = 5,   /* 1: branch-free clamped loads instead of
                                        predicated loads (default 0)         */
-    AIJHIP_OPT_EXACT = 6,           /* 1: every row summed sequentially in
+    AIJHIP_OPT_EXACT = 6            /* 1: every row summed sequentially in
                                        PETSc's order. Default 0: row blocks
-                                       whose mean row length exceeds 128 use
+                                       whose mean row length exceeds 16 use
                                        2..64 lanes per row (reordered sum,
                                        within the fp64 bound); short-row
                                        matrices (7-pt Poisson) are bit-exact
                                        either way                           */
-    AIJHIP_OPT_PAIR_GATHER = 7      /* 1: a lane's two consecutive columns
-                                       gathered with one 16-B load (plain
-                                       MatMult); same results               */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

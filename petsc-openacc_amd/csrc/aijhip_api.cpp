@@ -466,7 +466,6 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             break;
         case AIJHIP_OPT_CLAMPED_LOADS: t.clamped = value != 0; break;
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
-        case AIJHIP_OPT_PAIR_GATHER: t.pairx = value != 0; break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);

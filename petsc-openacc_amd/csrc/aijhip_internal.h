@@ -91,7 +91,6 @@ struct Tuning {
     int persist = 0;     // >0: persistent pipelined STREAM, this many workgroups per CU
     bool clamped = false;  // branch-free clamped loads instead of predicated loads
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
-    bool pairx = false;    // consecutive column pairs gathered with one 16-B load
 };
 
 // STREAM blocks whose mean row length exceeds this use several lanes per row

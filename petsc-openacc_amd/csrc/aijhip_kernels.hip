@@ -97,9 +97,7 @@ __device__ __forceinline__ double block_sum(double v, double *scratch) {
 // is formed in PETSc's order (or the deterministic multi-lane order); `seed`
 // starts it (MatMultAdd's z_i), `put` stores the row's result and adds to
 // the block's dot partials d[0..kDots).
-typedef double f64x2a8 __attribute__((ext_vector_type(2), aligned(8)));
-
-template <bool ADD, bool PAIRX = false>
+template <bool ADD>
 struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     static constexpr int kDots = 1;
     static constexpr bool kSeeded = ADD;
@@ -107,14 +105,6 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     double *y;
     bool dot;
     __device__ double gx(int32_t j) const { return x[j]; }
-    // PAIRX: a lane's two columns, when consecutive, in one 16-B load
-    __device__ f64x2 gx2(int32_t a, int32_t b) const {
-        if (PAIRX && b == a + 1) {
-            const f64x2a8 v = *reinterpret_cast<const f64x2a8 *>(x + a);
-            return f64x2{v.x, v.y};
-        }
-        return f64x2{x[a], x[b]};
-    }
     __device__ double seed(int o) const { return ADD ? z[o] : 0.0; }
     __device__ void put(int o, double v, double *d) const {
         y[o] = v;
@@ -131,7 +121,6 @@ struct OpMgPre {
     const double *b, *dinv;
     double *x, *r;
     __device__ double gx(int32_t j) const { return dinv[j] * b[j]; }
-    __device__ f64x2 gx2(int32_t a, int32_t b) const { return f64x2{gx(a), gx(b)}; }
     __device__ double seed(int) const { return 0.0; }
     __device__ void put(int o, double v, double *) const {
         const double bo = b[o];
@@ -151,7 +140,6 @@ struct OpMgPost {
     double *x;
     bool dot;
     __device__ double gx(int32_t j) const { return t[j]; }
-    __device__ f64x2 gx2(int32_t a, int32_t b) const { return f64x2{gx(a), gx(b)}; }
     __device__ double seed(int) const { return 0.0; }
     __device__ void put(int o, double v, double *d) const {
         const double bo = b[o];
@@ -171,7 +159,6 @@ struct OpDinvMult {
     const double *x, *dinv;
     double *y;
     __device__ double gx(int32_t j) const { return x[j]; }
-    __device__ f64x2 gx2(int32_t a, int32_t b) const { return f64x2{gx(a), gx(b)}; }
     __device__ double seed(int) const { return 0.0; }
     __device__ void put(int o, double v, double *) const { y[o] = dinv[o] * v; }
 };
@@ -222,7 +209,8 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (CLAMPED || k < k1) {
-            xv[it] = op.gx2(cv[it].x, cv[it].y);
+            xv[it].x = op.gx(cv[it].x);
+            xv[it].y = op.gx(cv[it].y);
         }
     }
     // products into LDS; only the stores are predicated
@@ -689,13 +677,6 @@ static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double 
         if (add && L.ridx) { AIJHIP_SL(true, true, false, false, false); }
         if (add) { AIJHIP_SL(true, false, false, false, false); }
         AIJHIP_SL(false, true, false, false, false);
-    }
-    if (P.tune.pairx && !P.tune.xcd && !P.tune.nt && !P.tune.clamped) {
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, false, false, OpMult<false, true>>),
-                           dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk,
-                           (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,
-                           OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop);
-        return;
     }
     switch ((P.tune.xcd ? 4 : 0) | (P.tune.nt ? 2 : 0) | (P.tune.clamped ? 1 : 0)) {
         case 0: AIJHIP_SL(false, false, false, false, false);
