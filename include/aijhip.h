@@ -102,6 +102,7 @@ typedef struct aijhip_info {
     int32_t stream_rows;
     int32_t persistent;      /* workgroups per CU of the pipelined STREAM (0 = off) */
     int32_t exact;           /* AIJHIP_OPT_EXACT in effect                   */
+    int32_t x_tiled_blocks;  /* STREAM blocks gathering x from an LDS tile    */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -143,13 +144,20 @@ enum {
                                        STREAM, k workgroups per CU (0 = off) */
     AIJHIP_OPT_CLAMPED_LOADS = 5,   /* 1: branch-free clamped loads instead of
                                        predicated loads (default 0)         */
-    AIJHIP_OPT_EXACT = 6            /* 1: every row summed sequentially in
+    AIJHIP_OPT_EXACT = 6,           /* 1: every row summed sequentially in
                                        PETSc's order. Default 0: row blocks
-                                       whose mean row length exceeds 16 use
+                                       whose mean row length exceeds 128 use
                                        2..64 lanes per row (reordered sum,
-                                       within the fp64 bound); short-row
-                                       matrices (7-pt Poisson) are bit-exact
+                                       within the fp64 bound); shorter rows
+                                       (7-pt Poisson, FEM rows) are bit-exact
                                        either way                           */
+    AIJHIP_OPT_X_TILE = 7           /* 1: stage x in LDS for every block whose
+                                       columns span <= the block's LDS entries
+                                       (banded operators) and gather from
+                                       there; -1: only when half the blocks
+                                       fit; 0 (default, measured faster on
+                                       the skewed stand-in): gathers from
+                                       HBM/L2. Same results                   */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

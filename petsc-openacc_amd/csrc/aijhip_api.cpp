@@ -68,6 +68,7 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_segs);
     hipFree(P.d_longs);
     hipFree(P.d_partials);
+    hipFree(P.d_xrange);
     hipFree(P.d_tile_coord);
     hipFree(P.d_carry_row);
     hipFree(P.d_carry_val);
@@ -162,6 +163,37 @@ int plan_stream(aijhip_mat *A) {
     if (!blocks.empty() &&
         (e = hipMemcpy(P.d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return hipfail(e, "plan: upload blocks");
+    // x tiles (LDS-staged x, opt-in): where a block's columns span at most
+    // its LDS entries, x[lo, lo + span) is loaded coalesced and gathered
+    // from LDS (banded operators; never the 7-pt Poisson at scale, whose
+    // blocks span +-N^2 columns). Measured on the skewed stand-in: +3 % at
+    // geometry 6, -6 % at the default geometry 1, hence off by default.
+    P.n_xtiled = 0;
+    if (P.tune.xtile != 0 && !blocks.empty() && !A->compressed) {
+        std::vector<int2> xr(blocks.size());
+        int2 *d_xr = nullptr;
+        if ((e = dmalloc(&d_xr, blocks.size(), &P.bytes)) != hipSuccess) return hipfail(e, "plan: alloc x ranges");
+        if ((e = aijhip::block_column_ranges(*A, P.d_blocks, P.n_blocks, d_xr)) != hipSuccess ||
+            (e = hipMemcpy(xr.data(), d_xr, sizeof(int2) * xr.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
+            hipFree(d_xr);
+            return hipfail(e, "plan: x ranges");
+        }
+        int32_t fit = 0;
+        for (int2 &r : xr) {
+            if (r.y > 0 && r.y <= G.nnz_cap) ++fit;
+            else r.y = -1;
+        }
+        if (P.tune.xtile == 1 || 2 * (int64_t)fit >= (int64_t)xr.size()) {
+            if ((e = hipMemcpy(d_xr, xr.data(), sizeof(int2) * xr.size(), hipMemcpyHostToDevice)) != hipSuccess) {
+                hipFree(d_xr);
+                return hipfail(e, "plan: x ranges");
+            }
+            P.d_xrange = d_xr;
+            P.n_xtiled = fit;
+        } else {
+            hipFree(d_xr);
+        }
+    }
     if (!longs.empty()) {
         if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
@@ -207,7 +239,7 @@ int plan_build(aijhip_mat *A) {
         // profiles/r01/tune04), 512 x 4096 / 512 rows for long rows (Flan
         // stand-in, profiles/r01/skew2)
         const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
-        P.tune.geom = (nr > 0 && A->nz > (int64_t)aijhip::kSplitMinMean * nr) ? 1 : 6;
+        P.tune.geom = (nr > 0 && A->nz > (int64_t)16 * nr) ? 1 : 6;
     }
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM:
@@ -466,6 +498,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             break;
         case AIJHIP_OPT_CLAMPED_LOADS: t.clamped = value != 0; break;
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
+        case AIJHIP_OPT_X_TILE:
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "x_tile: -1 auto, 0 off, 1 on");
+            t.xtile = value;
+            break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -604,6 +640,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
     info->persistent = A->plan.tune.persist;
     info->exact = A->plan.tune.exact ? 1 : 0;
+    info->x_tiled_blocks = A->plan.n_xtiled;
     return AIJHIP_OK;
 }
 

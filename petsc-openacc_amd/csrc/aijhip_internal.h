@@ -91,6 +91,8 @@ struct Tuning {
     int persist = 0;     // >0: persistent pipelined STREAM, this many workgroups per CU
     bool clamped = false;  // branch-free clamped loads instead of predicated loads
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
+    int xtile = 0;         // x staged in LDS per block: 0 off (measured default), 1 where it fits,
+                           // -1 when half the blocks fit
 };
 
 // STREAM blocks whose mean row length exceeds this use several lanes per row
@@ -112,6 +114,10 @@ struct Plan {
     LongRow *d_longs = nullptr;
     int32_t n_longs = 0;
     double *d_partials = nullptr;
+    // x tiles: per block the first column and the span of its columns, or
+    // span -1 when they do not fit the block's LDS (gathers from HBM)
+    int2 *d_xrange = nullptr;
+    int32_t n_xtiled = 0;
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;
     int32_t n_tiles = 0;
@@ -191,6 +197,8 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
                            double **d_taa, hipStream_t s);
 
 RowList row_list(const aijhip_mat &A);
+// Per STREAM block: min column and span (max - min + 1) of its entries.
+hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out);
 // Install A^T (device arrays, freed by the call) as A's transpose handle.
 int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa);
 // Number of device column indices outside [0, n) (synchronous).

@@ -97,10 +97,11 @@ __device__ __forceinline__ double block_sum(double v, double *scratch) {
 // is formed in PETSc's order (or the deterministic multi-lane order); `seed`
 // starts it (MatMultAdd's z_i), `put` stores the row's result and adds to
 // the block's dot partials d[0..kDots).
-template <bool ADD>
+template <bool ADD, bool TILE = false>
 struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     static constexpr int kDots = 1;
     static constexpr bool kSeeded = ADD;
+    static constexpr bool kTile = TILE;  // x gathered from an LDS tile where the block fits
     const double *x, *z;
     double *y;
     bool dot;
@@ -118,6 +119,7 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
 struct OpMgPre {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
+    static constexpr bool kTile = false;
     const double *b, *dinv;
     double *x, *r;
     __device__ double gx(int32_t j) const { return dinv[j] * b[j]; }
@@ -136,6 +138,7 @@ struct OpMgPre {
 struct OpMgPost {
     static constexpr int kDots = 2;
     static constexpr bool kSeeded = false;
+    static constexpr bool kTile = false;
     const double *t, *b, *dinv;
     double *x;
     bool dot;
@@ -156,6 +159,7 @@ struct OpMgPost {
 struct OpDinvMult {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
+    static constexpr bool kTile = false;
     const double *x, *dinv;
     double *y;
     __device__ double gx(int32_t j) const { return x[j]; }
@@ -167,7 +171,7 @@ template <int T, int CAP, int RPT, bool CROW, bool XCD, bool NT, bool CLAMPED, c
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, Op op, double *dpart, const int *stop) {
+    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const int2 *__restrict__ xrange) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
     if (stop && *stop) return;  // CG launched past convergence: no work
@@ -205,13 +209,34 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + kc));
         }
     }
+    // x tile: the block's columns [xr.x, xr.x + xr.y) staged in LDS (the
+    // products' space, free until the gathers are done) with coalesced
+    // loads; the gathers then read LDS instead of issuing scattered HBM
+    // requests (banded operators; the plan decides per block).
+    int2 xr = make_int2(0, -1);
+    if constexpr (Op::kTile) xr = xrange[b];
+    const bool tiled = Op::kTile && xr.y > 0;
+    if constexpr (Op::kTile) {
+        if (tiled) {
+            for (int i = t; i < xr.y; i += T) prod[i] = op.gx(xr.x + i);
+            __syncthreads();
+        }
+    }
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (CLAMPED || k < k1) {
-            xv[it].x = op.gx(cv[it].x);
-            xv[it].y = op.gx(cv[it].y);
+            if (tiled) {
+                xv[it].x = prod[cv[it].x - xr.x];
+                xv[it].y = prod[cv[it].y - xr.x];
+            } else {
+                xv[it].x = op.gx(cv[it].x);
+                xv[it].y = op.gx(cv[it].y);
+            }
         }
+    }
+    if constexpr (Op::kTile) {
+        if (tiled) __syncthreads();  // every gather is done before the products overwrite the tile
     }
     // products into LDS; only the stores are predicated
 #pragma unroll
@@ -645,6 +670,43 @@ hipError_t count_bad_columns(const int32_t *d_aj, int64_t nz, int32_t n, int64_t
     return e;
 }
 
+namespace {
+// per block: min column and span of its entries (one workgroup per block)
+__global__ __launch_bounds__(256) void k_block_xrange(const BlockDesc *__restrict__ blk,
+                                                      const int32_t *__restrict__ aj, int2 *out) {
+    __shared__ int lo_s[4], hi_s[4];
+    const BlockDesc d = blk[blockIdx.x];
+    int lo = INT32_MAX, hi = -1;
+    for (int64_t k = d.k0 + threadIdx.x; k < (int64_t)d.k0 + d.nk; k += 256) {
+        lo = min(lo, aj[k]);
+        hi = max(hi, aj[k]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_down(lo, off, 64));
+        hi = max(hi, __shfl_down(hi, off, 64));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        lo_s[threadIdx.x >> 6] = lo;
+        hi_s[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) {
+            lo = min(lo, lo_s[w]);
+            hi = max(hi, hi_s[w]);
+        }
+        out[blockIdx.x] = hi < 0 ? make_int2(0, 0) : make_int2(lo, hi - lo + 1);
+    }
+}
+}  // namespace
+
+hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out) {
+    if (n_blocks <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_block_xrange, dim3(n_blocks), dim3(256), 0, nullptr, d_blocks, A.d_aj, d_out);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? hipDeviceSynchronize() : e;
+}
+
 RowList row_list(const aijhip_mat &A) {
     if (A.compressed) return RowList{A.n_crow, A.d_cai, A.d_ridx};
     return RowList{A.m, A.d_ai, nullptr};
@@ -668,11 +730,18 @@ static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double 
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, XCD, NT, CL, OpMult<ADD>>), dim3(P.n_blocks), \
                        dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, (int)P.tune.exact,   \
                        L.rai, L.ridx, A.d_aj, A.d_aa,                                              \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop);                      \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr);             \
     return
     // The speed knobs (XCD remap, non-temporal, clamped loads) are compiled
     // for the plain full-row MatMult, the benchmarked path; MatMultAdd and
     // the compressed-row form use the default (measured-best) form.
+    if (P.d_xrange && !add && !L.ridx && !P.tune.xcd && !P.tune.nt && !P.tune.clamped) {
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, false, false, OpMult<false, true>>),
+                           dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, P.n_blocks, 0, (int)P.tune.exact, L.rai,
+                           nullptr, A.d_aj, A.d_aa, OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop,
+                           P.d_xrange);
+        return;
+    }
     if (add || L.ridx) {
         if (add && L.ridx) { AIJHIP_SL(true, true, false, false, false); }
         if (add) { AIJHIP_SL(true, false, false, false, false); }
@@ -743,7 +812,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     case G:                                                                                               \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
                            dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex,                \
-                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, nullptr);                          \
+                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, nullptr, nullptr);                 \
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);

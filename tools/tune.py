@@ -81,6 +81,9 @@ def main():
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=p, clamped=0)))
     if args.variants in ("kernels", "all"):
         variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
+    if args.variants == "xtile":
+        for g, xt in itertools.product((1, 6), (0, 1)):
+            variants.append(("stream", dict(geometry=g, x_tile=xt)))
     if args.variants == "skewgeom":
         for g, ex in itertools.product(range(9), (0, 1)):
             variants.append(("stream", dict(geometry=g, exact=ex)))
@@ -98,6 +101,7 @@ def main():
     def configure(kind, opts):
         A.set_kernel(kind, opts.get("lanes", 0))
         A.set_option("exact", opts.get("exact", 0))
+        A.set_option("x_tile", opts.get("x_tile", -1))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
