@@ -115,6 +115,30 @@ def test_stream_multilane_long_rows(pkg, dev, row_len):
     assert_bits(y1, y_ref)
 
 
+@pytest.mark.parametrize("geometry", [1, 6, 0])
+def test_stream_x_tile_banded(pkg, dev, geometry):
+    """x staged in LDS (x_tile=1) for blocks of a banded matrix: bit-exact,
+    and the blocks that do not fit (a wide row every 997) fall back to HBM
+    gathers in the same launch."""
+    rng = np.random.default_rng(11)
+    m = 20000
+    lens = rng.integers(10, 40, m)
+    cols = []
+    for i, l in enumerate(lens):
+        lo, hi = max(0, i - 300), min(m, i + 300)
+        c = np.sort(rng.choice(np.arange(lo, hi), size=min(l, hi - lo), replace=False))
+        if i % 997 == 0:
+            c = np.unique(np.concatenate([c, [0, m - 1]]))
+        cols.append(c)
+    ai = np.concatenate([[0], np.cumsum([len(c) for c in cols])]).astype(np.int32)
+    aj = np.concatenate(cols).astype(np.int32)
+    aa = rng.uniform(-1, 1, len(aj))
+    x = rng.uniform(-1, 1, m)
+    y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=1, x_tile=1, geometry=geometry)
+    assert 0 < info["x_tiled_blocks"] < info["n_blocks"]
+    assert_bits(y, seqaij.matmult(ai, aj, aa, x))
+
+
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
 @pytest.mark.parametrize("kernel", ALL_KERNELS)
 def test_mult_add_golden(pkg, dev, name, kernel):
