@@ -23,7 +23,7 @@ LIB = LIBDIR / "libaijhip.so"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
-HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "dist.hip", "ksp.hip", "poisson.hip", "gamg_device.hip", "vec.hip"]
+HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "ksp.hip", "poisson.hip", "gamg_device.hip", "vec.hip"]
 HOST_SOURCES = ["harness.cpp", "gamg_setup.cpp"]
 ARCH = os.environ.get("AIJHIP_ARCH", "gfx950")
 
@@ -58,7 +58,7 @@ def build_lib(force: bool = False) -> Path:
     objdir.mkdir(exist_ok=True)
     hipcc = _hipcc()
     common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"-I{ROOT / 'include'}", f"-I{CSRC}"]
-    objs = []
+    objs, jobs = [], []
     for s in srcs:
         o = objdir / (s.stem + ".o")
         if s.name in HOST_SOURCES:
@@ -66,8 +66,12 @@ def build_lib(force: bool = False) -> Path:
         else:
             cmd = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", *common, "-c", str(s), "-o", str(o)]
         if force or _stale(o, [s, *CSRC.glob("*.h"), *(ROOT / "include").glob("*.h")]):
-            _run(cmd)
+            jobs.append(cmd)
         objs.append(str(o))
+    # translation units compile in parallel (at most 8 at once)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        list(ex.map(_run, jobs))
     tmp = LIB.with_suffix(".so.tmp")
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs, "-lgomp",
           "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"])

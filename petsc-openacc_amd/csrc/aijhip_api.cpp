@@ -350,9 +350,8 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
     int rc = validate_csr(m, n, nz, ai, dev_src ? nullptr : aj);
     if (rc) return rc;
     if (nz > 0 && !aa) return fail(AIJHIP_ERR_ARG, "aa is NULL");
-    int count = 0;
-    hipError_t e = hipGetDeviceCount(&count);
-    if (e != hipSuccess || count == 0) return fail(AIJHIP_ERR_NODEVICE, "no HIP device visible");
+    const int count = aijhip::visible_devices();
+    if (count <= 0) return fail(AIJHIP_ERR_NODEVICE, "no HIP device visible");
     if (device < 0 || device >= count) return fail(AIJHIP_ERR_ARG, "device ordinal out of range");
     DeviceGuard g(device);
     if (g.err != hipSuccess) return hipfail(g.err, "set device");
@@ -385,6 +384,16 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
 
 namespace aijhip {
 void set_error(const std::string &msg) { g_err = msg; }
+
+// hipGetDeviceCount costs milliseconds per call on this stack; the count of a
+// process does not change, so it is asked once.
+int visible_devices() {
+    static const int count = [] {
+        int c = 0;
+        return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+    }();
+    return count;
+}
 
 // A^T as a handle owned by A (MatMultTranspose): the device arrays of the
 // transpose (n+1 / nz+2 / nz+2, tail pad zeroed) are copied device to device

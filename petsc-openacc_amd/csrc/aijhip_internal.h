@@ -206,5 +206,6 @@ hipError_t count_bad_columns(const int32_t *d_aj, int64_t nz, int32_t n, int64_t
 
 // Sets the calling thread's aijhip_last_error() message.
 void set_error(const std::string &msg);
+int visible_devices();  // hipGetDeviceCount, cached
 
 }  // namespace aijhip

@@ -208,8 +208,7 @@ int aijhip_mat_create_poisson(int device, int32_t nx, int32_t ny, int32_t nz, in
         aijhip::set_error("mat_create_poisson: slab nnz exceeds the int32 PetscInt range");
         return AIJHIP_ERR_ARG;
     }
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) {
+    if (aijhip::visible_devices() <= 0) {
         aijhip::set_error("no HIP device visible");
         return AIJHIP_ERR_NODEVICE;
     }
