@@ -83,15 +83,21 @@ def _mix64(z):
     return z ^ (z >> 31)
 
 
-def _blockdot(a, b, block=8192):
-    """The C++ set-up's dot: left to right inside fixed 8192-entry blocks,
+def _blockdot(a, b, block=256):
+    """The C++ set-up's dot: left to right inside fixed 256-entry blocks,
     then the block sums left to right (np.cumsum accumulates sequentially;
     np.dot is pairwise). The aggregation of the next level is sensitive to the
     last bit of every coarse entry (ties, zero threshold), so the restatement
     keeps the order."""
     p = np.asarray(a, dtype=np.float64) * np.asarray(b, dtype=np.float64)
-    parts = [np.cumsum(p[i:i + block])[-1] for i in range(0, len(p), block)]
-    return float(np.cumsum(parts)[-1]) if parts else 0.0
+    n = len(p)
+    if n == 0:
+        return 0.0
+    full = (n // block) * block  # block sums left to right, vectorised over blocks
+    parts = np.cumsum(p[:full].reshape(-1, block), axis=1)[:, -1] if full else np.zeros(0)
+    if full < n:
+        parts = np.concatenate([parts, [np.cumsum(p[full:])[-1]]])
+    return float(np.cumsum(parts)[-1])
 
 
 def estimate_emax(A, dinv, its):

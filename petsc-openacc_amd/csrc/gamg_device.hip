@@ -7,7 +7,7 @@
 //   aggregation                   host (sequential greedy, natural order),
 //                                 from S and per-entry |a_ij| weights
 //   emax(D^-1 A)                  power iteration on the STREAM SpMV in
-//                                 PETSc order; 8192-entry blocked dots
+//                                 PETSc order; 256-entry blocked dots
 //   P = (I - 1.4/emax D^-1 A) P0  row-wise product A*P0, union with P0
 //   A_c = P^T (A P)               row-wise products (below), P^T by the
 //                                 stable radix-sort transpose
@@ -197,9 +197,9 @@ __global__ void k_power_start(int32_t m, double *v) {
                   (1.0 / 9007199254740992.0)) - 1.0;
 }
 
-constexpr int64_t kDotBlock = 8192;  // gamg_setup.cpp kDotBlock
+constexpr int64_t kDotBlock = 256;  // gamg_setup.cpp kDotBlock
 
-// one lane per 8192-entry block, left to right (the host sums the blocks)
+// one lane per 256-entry block, left to right (the host sums the blocks)
 __global__ void k_block_dot(int64_t n, const double *__restrict__ a, double *part) {
     const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t i0 = q * kDotBlock;

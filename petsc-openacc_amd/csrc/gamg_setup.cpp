@@ -179,7 +179,7 @@ void dinv_apply(const View &A, const std::vector<double> &dinv, const std::vecto
 
 // Deterministic blocked dot: left to right inside fixed kDotBlock-entry
 // blocks, then the block sums left to right (oracle/gamg.py _blockdot).
-constexpr int64_t kDotBlock = 8192;
+constexpr int64_t kDotBlock = 256;
 
 double dot(const std::vector<double> &a, const std::vector<double> &b, int nt) {
     const int64_t n = (int64_t)a.size(), nb = (n + kDotBlock - 1) / kDotBlock;

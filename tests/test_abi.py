@@ -82,3 +82,32 @@ def test_null_handle_calls_return_errors(pkg):
     assert L.aijhip_mat_mult(None, None, None, None) == pkg.AIJHIP_ERR_ARG
     assert L.aijhip_mat_destroy(None) == 0
     assert b"NULL" in L.aijhip_last_error()
+
+
+def test_headers_are_plain_c99(tmp_path):
+    """The boundary is a C ABI: every header compiles as strict C99 (no C++,
+    no HIP or torch types) and a C program links against the library."""
+    import shutil
+    if not shutil.which("gcc"):
+        pytest.skip("no gcc")
+    src = tmp_path / "use.c"
+    hdrs = sorted(p.name for p in (ROOT / "include").glob("*.h"))
+    src.write_text("".join(f'#include "{h}"\n' for h in hdrs) + """
+#include <stdio.h>
+int main(void) {
+    int n = -1;
+    aijhip_gamg_params_t p;
+    aijhip_gamg_params_default(&p);
+    printf("%d %d\\n", aijhip_abi_version(), p.coarse_eq_limit);
+    return aijhip_device_count(&n) == AIJHIP_OK || n == 0 ? 0 : 1;
+}
+""")
+    exe = tmp_path / "use"
+    import importlib
+    lib = importlib.import_module("petsc-openacc_amd").LIB_PATH
+    r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", f"-I{ROOT / 'include'}",
+                        str(src), "-o", str(exe), f"-L{lib.parent}", "-laijhip", f"-Wl,-rpath,{lib.parent}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert out.stdout.split()[:2] == ["1", "50"]
