@@ -39,6 +39,7 @@ namespace {
 struct CGState {
     double beta, betaold, dpi, dpiold, a, b, dp, rnorm0, ttol;
     int32_t its, reason, done, i;
+    int32_t xpend;  // X += a P of the last completed iteration not applied yet
 };
 
 struct CGParams {
@@ -208,12 +209,29 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_init(const double *part,
 }
 
 // K1: P = Z (i = 0) or P = Z + b P (VecAYPX: y = x + alpha y, product first).
+// The previous iteration's VecAXPY(X, a, P) is applied here, where P is read
+// anyway, before P is overwritten (same operation on every element, one
+// iteration later: X and P make one pass fewer per iteration).
 __global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *__restrict__ z, double *p,
-                                                      const CGState *S) {
+                                                      double *x, const CGState *S) {
     if (S->done) return;
     const bool first = S->i == 0;
-    const double bb = S->b;
-    GRID_STRIDE(i, n) p[i] = first ? z[i] : z[i] + bb * p[i];
+    const double bb = S->b, a = S->a;
+    GRID_STRIDE(i, n) {
+        const double pi = p[i];
+        if (!first) x[i] = x[i] + a * pi;
+        p[i] = first ? z[i] : z[i] + bb * pi;
+    }
+}
+
+// After the loop: the last iteration's X += a P when the solve stopped after
+// that iteration's update (converged / diverged-its / top-of-loop checks),
+// not when it stopped inside it (indefinite matrix) or before it.
+__global__ __launch_bounds__(kVecThreads) void k_final_x(int64_t n, const double *__restrict__ p, double *x,
+                                                         const CGState *S) {
+    if (!S->xpend) return;
+    const double a = S->a;
+    GRID_STRIDE(i, n) x[i] = x[i] + a * p[i];
 }
 
 // Unfused dot partials of p . w (when the SpMV cannot carry the epilogue).
@@ -240,24 +258,24 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_dpi(const double *part, 
     if (dpi == 0.0 || (S->i > 0 && dpi * S->dpiold <= 0.0)) {
         S->reason = AIJHIP_KSP_DIVERGED_INDEFINITE_MAT;
         S->done = 1;
+        S->xpend = 0;  // this iteration's X update never happens (PETSc returns first)
         return;
     }
     S->a = S->beta / dpi;
 }
 
-// K4: X += a P; R -= a W; Jacobi / none: Z = D^-1 R (W and Z share storage:
-// w[i] is read before z[i] is written by the same lane); partials
-// Z.Z, Z.R, R.R (GAMG: R.R only, Z follows from the V-cycle).
-__global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *x, const double *__restrict__ p,
-                                                        double *r, double *wz,
+// K4: R -= a W; Jacobi / none: Z = D^-1 R (W and Z share storage: w[i] is
+// read before z[i] is written by the same lane); partials Z.Z, Z.R, R.R
+// (GAMG: R.R only, Z follows from the V-cycle). VecAXPY(X, a, P) is deferred
+// to the next K1 (or k_final_x).
+__global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, double *wz,
                                                         const double *__restrict__ dinv, double *part,
                                                         const CGState *S, int pc) {
     __shared__ double scratch[kVecThreads / 64];
     if (S->done) return;
-    const double a = S->a, na = -a;
+    const double na = -S->a;
     double zz = 0.0, zr = 0.0, rr = 0.0;
     GRID_STRIDE(i, n) {
-        x[i] = x[i] + a * p[i];               // VecAXPY(X, a, P)
         const double ri = r[i] + na * wz[i];  // VecAXPY(R, -a, W)
         r[i] = ri;
         rr += ri * ri;
@@ -305,6 +323,7 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_iter(const double *pz, i
         }
     }
     s.done = s.reason != 0;
+    s.xpend = s.done;  // stopped after this iteration's update: its X += a P is due
     *S = s;
 }
 
@@ -721,7 +740,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             return khip(e, "KSPSolve poll");
         if (K->h_state->done || launched >= K->max_it) break;
         for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched) {
-            hipLaunchKernelGGL(k_aypx, vg, vt, 0, s, m, K->d_z, K->d_p, K->d_state);
+            hipLaunchKernelGGL(k_aypx, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             if (K->fused) {
                 e = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, s);
                 if (e == hipSuccess)
@@ -731,8 +750,8 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
                 hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
                 hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, nb, K->d_state);
             }
-            hipLaunchKernelGGL(k_update, vg, vt, 0, s, m, x, K->d_p, K->d_r, K->d_z, K->d_dinv, K->d_part,
-                               K->d_state, K->pc);
+            hipLaunchKernelGGL(k_update, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part, K->d_state,
+                               K->pc);
             const double *pz = K->d_part;
             int nbz = nb;
             if (gamg && e == hipSuccess) {
@@ -752,6 +771,11 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve iteration");
         }
     }
+    hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return khip(e, "KSPSolve final update");
     const CGState &st = *K->h_state;
     K->its = st.its;
     K->reason = st.reason ? st.reason : AIJHIP_KSP_DIVERGED_ITS;
