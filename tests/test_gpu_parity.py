@@ -288,6 +288,34 @@ def test_full_size_poisson_bitexact(pkg, dev, coracle, N):
         torch.cuda.empty_cache()
 
 
+def test_max_size_600_device_assembly_bitexact(pkg, dev, coracle):
+    """The largest operand of BASELINE (configs[3]'s 600^3 global grid: 216 M
+    rows, 1.51 G entries — 70 % of the int32 entry range, 18 GB of CSR) on one
+    GPU: assembled on the device, multiplied by STREAM, and compared bit for
+    bit with the C oracle on the host-assembled operand (which also checks the
+    device assembly at maximum size)."""
+    N = 600
+    m = N ** 3
+    A, _ = pkg.poisson_device(N)
+    try:
+        info = A.info()
+        assert info["nz"] == 7 * N ** 3 - 6 * N ** 2 and info["n_long_rows"] == 0
+        x = pkg.splitmix_uniform(m, 42)
+        xd = to_dev(x, dev)
+        yd = torch.empty_like(xd)
+        A.mult(xd, yd)
+        torch.cuda.synchronize()
+        y = yd.cpu().numpy()
+        del xd, yd
+    finally:
+        A.destroy()
+        torch.cuda.empty_cache()
+    ai, aj, aa = pkg.poisson_csr(N)
+    ref = coracle.matmult(ai, aj, aa, x, omp=True)
+    del ai, aj, aa
+    assert_bits(y, ref)
+
+
 def test_skewed_flan_standin_all_kernels(pkg, dev, coracle):
     """Flan_1565 stand-in (BASELINE configs[4]) at a reduced row count."""
     ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
