@@ -115,7 +115,7 @@ int validate_csr(int32_t m, int32_t n, int64_t nz, const int32_t *ai, const int3
 // segments of <= kLongSegNnz entries.
 int plan_stream(aijhip_mat *A) {
     using namespace aijhip;
-    const std::vector<int32_t> &rai = A->h_rai;
+    const auto &rai = A->h_rai;
     const int32_t nr = rai.empty() ? 0 : (int32_t)rai.size() - 1;
     std::vector<BlockDesc> blocks;
     std::vector<LongSeg> segs;
@@ -268,7 +268,9 @@ int plan_build(aijhip_mat *A) {
 
 // Uploads a validated CSR into A (sizes already set) and plans it. ai is on
 // the host; aj/aa on the host, or on the device when dev_src (copied D2D).
-int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const double *aa, bool dev_src = false) {
+// own_ai, when given, holds ai and is moved into the handle's host offsets.
+int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const double *aa, bool dev_src = false,
+                    aijhip::HostVec<int32_t> *own_ai = nullptr) {
     const int32_t m = A->m;
     const int64_t nz = A->nz;
     hipError_t e;
@@ -300,7 +302,8 @@ int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const d
          (e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)nz, kind)) != hipSuccess))
         return hipfail(e, "upload aj/aa");
     if (A->compressed) {
-        std::vector<int32_t> cai, ridx;
+        aijhip::HostVec<int32_t> cai;
+        std::vector<int32_t> ridx;
         cai.reserve((size_t)nzrows + 1);
         ridx.reserve((size_t)nzrows);
         for (int32_t i = 0; i < m; ++i)
@@ -317,7 +320,8 @@ int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const d
         A->h_rai.swap(cai);
     } else {
         A->n_crow = 0;
-        A->h_rai.assign(ai, ai + (size_t)m + 1);
+        if (own_ai && own_ai->data() == ai) A->h_rai.swap(*own_ai);
+        else A->h_rai.assign(ai, ai + (size_t)m + 1);
     }
     return plan_build(A);
 }
@@ -343,7 +347,8 @@ int mult_impl(aijhip_mat_t A, const double *x, const double *z, double *y, bool 
 }
 
 int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
-                const int32_t *aj, const double *aa, aijhip_mat_t *out, bool dev_src = false) {
+                const int32_t *aj, const double *aa, aijhip_mat_t *out, bool dev_src = false,
+                aijhip::HostVec<int32_t> *own_ai = nullptr) {
     if (!out) return fail(AIJHIP_ERR_ARG, "out is NULL");
     *out = nullptr;
     if (nz > 0 && !aj) return fail(AIJHIP_ERR_ARG, "aj is NULL");
@@ -370,7 +375,7 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
         if (e != hipSuccess) rc = hipfail(e, "check device columns");
         else if (bad) rc = fail(AIJHIP_ERR_ARG, std::to_string(bad) + " column indices out of range");
     }
-    if (!rc) rc = upload_and_plan(A, ai, aj, aa, dev_src);
+    if (!rc) rc = upload_and_plan(A, ai, aj, aa, dev_src, own_ai);
     if (rc) {
         free_matrix(A);
         delete A;
@@ -402,7 +407,7 @@ int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa) {
     aijhip_mat *T = new (std::nothrow) aijhip_mat();
     int rc = AIJHIP_OK;
     if (!T) rc = fail(AIJHIP_ERR_ALLOC, "host allocation");
-    std::vector<int32_t> h_tai;
+    aijhip::HostVec<int32_t> h_tai;
     if (!rc) {
         T->device = A->device;
         T->n_cu = A->n_cu;
@@ -416,7 +421,7 @@ int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa) {
         const hipError_t e = hipMemcpy(h_tai.data(), tai, sizeof(int32_t) * h_tai.size(), hipMemcpyDeviceToHost);
         if (e != hipSuccess) rc = hipfail(e, "read transpose offsets");
     }
-    if (!rc) rc = upload_and_plan(T, h_tai.data(), taj, taa, true);
+    if (!rc) rc = upload_and_plan(T, h_tai.data(), taj, taa, true, &h_tai);
     hipFree(tai);
     hipFree(taj);
     hipFree(taa);
@@ -462,14 +467,14 @@ int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
         return fail(AIJHIP_ERR_ARG, "bad size or NULL array");
     // Planning reads the row offsets on the host (m+1 ints); the columns are
     // range-checked on the device and aj/aa are copied device to device.
-    std::vector<int32_t> ai((size_t)m + 1);
+    aijhip::HostVec<int32_t> ai((size_t)m + 1);
     {
         DeviceGuard g(device);
         if (g.err != hipSuccess) return hipfail(g.err, "set device");
         hipError_t e = hipMemcpy(ai.data(), d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost);
         if (e != hipSuccess) return hipfail(e, "read device row offsets");
     }
-    return create_impl(device, m, n, nz, ai.data(), d_aj, d_aa, out, true);
+    return create_impl(device, m, n, nz, ai.data(), d_aj, d_aa, out, true, &ai);
 }
 
 int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes) {

@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "aijhip.h"
+#include "host_alloc.h"
 
 namespace aijhip {
 
@@ -142,7 +143,7 @@ struct aijhip_mat {
     int32_t n_crow = 0;        // compressed-row form (PETSc a->compressedrow)
     int32_t *d_cai = nullptr;
     int32_t *d_ridx = nullptr;
-    std::vector<int32_t> h_rai;  // host copy of the row-list offsets (planning)
+    aijhip::HostVec<int32_t> h_rai;  // host copy of the row-list offsets (planning)
     aijhip::Plan plan;
     int requested_kernel = AIJHIP_KERNEL_AUTO;
     int requested_lanes = 0;

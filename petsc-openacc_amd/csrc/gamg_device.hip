@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <mutex>
+
 #include <algorithm>
 #include <chrono>
 #include <cmath>
@@ -215,6 +217,47 @@ __global__ void k_div(int32_t m, const double *w, double nw, double *v) {
     if (i < m) v[i] = w[i] / nw;
 }
 
+__global__ void k_fill(int32_t m, double v, double *x) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) x[i] = v;
+}
+
+// seg[a] = first position of aggregate a in the sorted aggregate keys
+__global__ void k_seg_offsets(int32_t na, int32_t m, const int32_t *__restrict__ keys, int32_t *seg) {
+    const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a > na) return;
+    int32_t lo = 0, hi = m;
+    while (lo < hi) {
+        const int32_t q = (lo + hi) >> 1;
+        if (keys[q] < a) lo = q + 1;
+        else hi = q;
+    }
+    seg[a] = lo;
+}
+
+// The tentative prolongator's near-null space (gamg_setup.cpp prolongator):
+// B_c[a] = sqrt of the sum of B[i]^2 over the members of aggregate a in
+// ascending row order (the stable sort's order), p0[i] = B[i] / B_c[agg[i]].
+__global__ void k_agg_norm(int32_t na, const int32_t *__restrict__ seg, const int32_t *__restrict__ members,
+                           const double *__restrict__ B, double *Bc) {
+    const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= na) return;
+    double s = 0.0;
+    for (int32_t q = seg[a]; q < seg[a + 1]; ++q) {
+        const double b = B[members[q]];
+        s += b * b;
+    }
+    Bc[a] = sqrt(s);
+}
+
+__global__ void k_tentative(int32_t m, const int32_t *__restrict__ agg, const double *__restrict__ B,
+                            const double *__restrict__ Bc, double *p0) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double c = Bc[agg[i]];
+    p0[i] = c > 0.0 ? B[i] / c : 0.0;
+}
+
 __global__ void k_iota(int32_t n, int32_t *v) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i <= n) v[i] = i;
@@ -238,11 +281,14 @@ __global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__res
                                                  const int32_t *__restrict__ aj, const double *__restrict__ aa,
                                                  const int32_t *__restrict__ bi, const int32_t *__restrict__ bj,
                                                  const double *__restrict__ ba, const int32_t *__restrict__ ci,
-                                                 int32_t *cj, double *ca, int32_t *cnt) {
+                                                 int32_t *cj, double *ca, int32_t *cnt, bool redo, int32_t lo,
+                                                 int32_t hi) {
     __shared__ int32_t sc[CAP * TPB];
     __shared__ double sv[NUMERIC ? CAP * TPB : 1];
     const int t = threadIdx.x;
     for (int32_t i = blockIdx.x * TPB + t; i < m; i += gridDim.x * TPB) {
+        if (!NUMERIC && redo && cnt[i] >= 0) continue;               // counted by a smaller CAP
+        if (NUMERIC && (cnt[i] <= lo || cnt[i] > hi)) continue;     // another CAP's class
         int n = 0;
         bool over = false;
         for (int32_t k = ai[i]; k < ai[i + 1] && !over; ++k) {
@@ -250,26 +296,26 @@ __global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__res
             const double a = NUMERIC ? aa[k] : 0.0;
             for (int32_t q = bi[j]; q < bi[j + 1]; ++q) {
                 const int32_t c = bj[q];
-                int lo = 0, hi = n;
-                while (lo < hi) {
-                    const int mid = (lo + hi) >> 1;
-                    if (sc[mid * TPB + t] < c) lo = mid + 1;
-                    else hi = mid;
+                int l = 0, h = n;
+                while (l < h) {
+                    const int mid = (l + h) >> 1;
+                    if (sc[mid * TPB + t] < c) l = mid + 1;
+                    else h = mid;
                 }
-                if (lo < n && sc[lo * TPB + t] == c) {
-                    if (NUMERIC) sv[lo * TPB + t] += a * ba[q];
+                if (l < n && sc[l * TPB + t] == c) {
+                    if (NUMERIC) sv[l * TPB + t] += a * ba[q];
                     continue;
                 }
                 if (n == CAP) { over = true; break; }
-                for (int z = n; z > lo; --z) {
+                for (int z = n; z > l; --z) {
                     sc[z * TPB + t] = sc[(z - 1) * TPB + t];
                     if (NUMERIC) sv[z * TPB + t] = sv[(z - 1) * TPB + t];
                 }
-                sc[lo * TPB + t] = c;
+                sc[l * TPB + t] = c;
                 if (NUMERIC) {
                     double v0 = 0.0;
                     v0 += a * ba[q];
-                    sv[lo * TPB + t] = v0;
+                    sv[l * TPB + t] = v0;
                 }
                 ++n;
             }
@@ -460,16 +506,18 @@ done:
 
 // C = A * B. Returns AIJHIP_OK, or AIJHIP_ERR_STATE when a row's distinct
 // columns exceed every device capacity (the caller falls back to the host).
+// One pass of k_rowprod over the rows of one capacity class (each class
+// uses 48 KiB of LDS per workgroup in the numeric pass).
 template <int CAP, int TPB>
-hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, const int32_t *ci, DCsr *C, bool numeric,
-                        int n_cu) {
+hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, bool redo, int32_t lo, int32_t hi,
+                        const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
     const unsigned grid = (unsigned)std::min<int64_t>(blocks_for(A.m, TPB), (int64_t)n_cu * 16);
     if (!numeric)
         hipLaunchKernelGGL((k_rowprod<CAP, TPB, false>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt);
+                           B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, redo, 0, 0);
     else
         hipLaunchKernelGGL((k_rowprod<CAP, TPB, true>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           B.ai, B.aj, B.aa, ci, C->aj, C->aa, nullptr);
+                           B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, false, lo, hi);
     return hipGetLastError();
 }
 
@@ -527,28 +575,32 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu) {
             return AIJHIP_OK;
         }
     }
-    // some row has more columns than the wave form holds: one lane per row
-    // capacities (distinct columns per row) x lanes per block, 48 KiB of LDS
+    // one lane per row, the row's distinct columns in LDS: capacity classes
+    // 64 / 128 / 256 (a row counted -1 by a class is recounted by the next)
+    auto min_count = [&](int32_t *mn) -> hipError_t {
+        *mn = 0;
+        if (A.m == 0) return hipSuccess;
+        void *tmp = nullptr;
+        size_t tb = 0;
+        int32_t *dmin = nullptr;
+        hipError_t r;
+        if ((r = dalloc(&dmin, 1)) == hipSuccess &&
+            (r = hipcub::DeviceReduce::Min(nullptr, tb, cnt, dmin, A.m)) == hipSuccess &&
+            (r = hipMalloc(&tmp, std::max<size_t>(tb, 1))) == hipSuccess &&
+            (r = hipcub::DeviceReduce::Min(tmp, tb, cnt, dmin, A.m)) == hipSuccess)
+            r = hipMemcpy(mn, dmin, sizeof(int32_t), hipMemcpyDeviceToHost);
+        hipFree(tmp);
+        hipFree(dmin);
+        return r;
+    };
     int level = 0;
     for (;; ++level) {
-        if (level == 0) e = rowprod_pass<64, 64>(A, B, cnt, nullptr, nullptr, false, n_cu);
-        else if (level == 1) e = rowprod_pass<256, 16>(A, B, cnt, nullptr, nullptr, false, n_cu);
+        if (level == 0) e = rowprod_pass<64, 64>(A, B, cnt, false, 0, 0, nullptr, nullptr, false, n_cu);
+        else if (level == 1) e = rowprod_pass<128, 32>(A, B, cnt, true, 0, 0, nullptr, nullptr, false, n_cu);
+        else if (level == 2) e = rowprod_pass<256, 16>(A, B, cnt, true, 0, 0, nullptr, nullptr, false, n_cu);
         else { hipFree(cnt); return AIJHIP_ERR_STATE; }
-        if (e != hipSuccess) { hipFree(cnt); return herr(e, "symbolic product"); }
         int32_t mn = 0;
-        if (A.m > 0) {
-            void *tmp = nullptr;
-            size_t tb = 0;
-            int32_t *dmin = nullptr;
-            if ((e = dalloc(&dmin, 1)) == hipSuccess &&
-                (e = hipcub::DeviceReduce::Min(nullptr, tb, cnt, dmin, A.m)) == hipSuccess &&
-                (e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) == hipSuccess &&
-                (e = hipcub::DeviceReduce::Min(tmp, tb, cnt, dmin, A.m)) == hipSuccess)
-                e = hipMemcpy(&mn, dmin, sizeof(int32_t), hipMemcpyDeviceToHost);
-            hipFree(tmp);
-            hipFree(dmin);
-            if (e != hipSuccess) { hipFree(cnt); return herr(e, "product overflow check"); }
-        }
+        if (e != hipSuccess || (e = min_count(&mn)) != hipSuccess) { hipFree(cnt); return herr(e, "symbolic product"); }
         if (mn >= 0) break;
     }
     if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) { hipFree(cnt); return herr(e, "product rows"); }
@@ -568,11 +620,40 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu) {
         C.release();
         return herr(e, "product alloc");
     }
-    e = level == 0 ? rowprod_pass<64, 64>(A, B, cnt, C.ai, &C, true, n_cu)
-                   : rowprod_pass<256, 16>(A, B, cnt, C.ai, &C, true, n_cu);
+    e = rowprod_pass<64, 64>(A, B, cnt, false, -1, 64, C.ai, &C, true, n_cu);
+    if (e == hipSuccess && level >= 1) e = rowprod_pass<128, 32>(A, B, cnt, false, 64, 128, C.ai, &C, true, n_cu);
+    if (e == hipSuccess && level >= 2) e = rowprod_pass<256, 16>(A, B, cnt, false, 128, 256, C.ai, &C, true, n_cu);
     hipFree(cnt);
     if (e != hipSuccess) { C.release(); return herr(e, "numeric product"); }
     return AIJHIP_OK;
+}
+
+// B_c and p0 of the tentative prolongator from the aggregates (device).
+hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0) {
+    if (m == 0) return hipSuccess;
+    int32_t *keys = nullptr, *idx = nullptr, *members = nullptr, *seg = nullptr;
+    void *tmp = nullptr;
+    size_t tb = 0;
+    int bits = 1;
+    while (bits < 31 && (int64_t(1) << bits) < (int64_t)na) ++bits;
+    hipError_t e;
+    if ((e = dalloc(&keys, m)) != hipSuccess || (e = dalloc(&idx, m)) != hipSuccess ||
+        (e = dalloc(&members, m)) != hipSuccess || (e = dalloc(&seg, (int64_t)na + 1)) != hipSuccess)
+        goto done;
+    hipLaunchKernelGGL(k_iota, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m - 1, idx);
+    // stable: each aggregate's members stay in ascending row order
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, agg, keys, idx, members, m, 0, bits)) != hipSuccess ||
+        (e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) != hipSuccess ||
+        (e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, agg, keys, idx, members, m, 0, bits)) != hipSuccess)
+        goto done;
+    hipLaunchKernelGGL(k_seg_offsets, dim3(blocks_for((int64_t)na + 1, 256)), dim3(256), 0, nullptr, na, m, keys, seg);
+    if (na > 0)
+        hipLaunchKernelGGL(k_agg_norm, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, seg, members, B, Bc);
+    hipLaunchKernelGGL(k_tentative, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, B, Bc, p0);
+    e = hipGetLastError();
+done:
+    hipFree(keys); hipFree(idx); hipFree(members); hipFree(seg); hipFree(tmp);
+    return e;
 }
 
 double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vector<double> &h_part, hipError_t *e) {
@@ -586,8 +667,9 @@ double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vect
 }
 
 // Pinned host staging for the strength graph and the aggregates, grown as
-// needed and reused across levels (measured at 300^3: level-0 strength phase
-// 0.14 s pinned vs 0.22 s through pageable copies, allocation included).
+// needed and reused across levels and set-ups (measured at 300^3: level-0
+// strength phase 0.14 s pinned vs 0.22 s through pageable copies, allocation
+// included; the 0.86 GB allocation alone is 35 ms, paid once per process).
 struct Staging {
     void *p = nullptr;
     size_t bytes = 0;
@@ -601,8 +683,16 @@ struct Staging {
         return e;
     }
     int32_t *i32() { return static_cast<int32_t *>(p); }
-    ~Staging() { if (p) hipHostFree(p); }
 };
+
+// One per process, never freed (static destructors may run after the HIP
+// runtime is gone); set-ups take turns on it.
+Staging &process_staging(std::unique_lock<std::mutex> &lock) {
+    static std::mutex mu;
+    static Staging *st = new Staging();
+    lock = std::unique_lock<std::mutex>(mu);
+    return *st;
+}
 
 DCsr view_of(const aijhip_mat &A) {
     DCsr v;
@@ -648,11 +738,15 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         t0 = t;
     };
     levels.push_back(DeviceLevel{A0, nullptr, 0.0});
-    B.assign((size_t)A0->m, 1.0);
     const int n_cu = std::max(A0->n_cu, 1);
-    Staging stage;
+    std::unique_lock<std::mutex> stage_lock;
+    Staging &stage = process_staging(stage_lock);
     int rc = AIJHIP_OK;
     hipError_t e = hipSuccess;
+    // the near-null space of the current level, on the device (ones at the top)
+    double *d_B = nullptr;
+    if ((e = dalloc(&d_B, A0->m)) != hipSuccess) return herr(e, "alloc");
+    hipLaunchKernelGGL(k_fill, dim3(blocks_for(A0->m, 256)), dim3(256), 0, nullptr, A0->m, 1.0, d_B);
     while ((int32_t)levels.size() < p.max_levels && levels.back().A->m > p.coarse_eq_limit) {
         aijhip_mat &A = *levels.back().A;
         const int32_t m = A.m;
@@ -713,7 +807,9 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         GTRY(hipGetLastError(), "strength kernels");
         // ---- aggregation: phases 1 and 3 (sequential greedy) on the host from
         // S staged in pinned memory, phase 2 on the device
+        lap("strength kernels");
         GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
+        lap("staging alloc");
         h_si = stage.i32();
         h_sj = h_si + m + 1;
         agg = h_sj + nzs;
@@ -721,10 +817,12 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         if (nzs > 0) GTRY(hipMemcpy(h_sj, sj, sizeof(int32_t) * (size_t)nzs, hipMemcpyDeviceToHost), "read S");
         lap("strength");
         na = aijhip_gamg::aggregate_phase1(m, h_si, h_sj, agg);
+        lap("phase 1");
         GTRY(dalloc(&d_ph, 2 * (int64_t)m), "alloc");
         GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
         hipLaunchKernelGGL(k_agg_phase2, dim3(g256), dim3(256), 0, nullptr, m, si, sj, sval, d_ph, d_ph + m);
         GTRY(hipMemcpy(agg, d_ph + m, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
+        lap("phase 2");
         na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
         lap("aggregate");
     level_done:
@@ -739,8 +837,10 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         DCsr P0, T, P, AP, PT, Ac;
         int32_t *d_agg = nullptr, *plen = nullptr;
         double *d_p0 = nullptr, *v = nullptr, *w = nullptr, *part = nullptr;
-        std::vector<double> Bc((size_t)na, 0.0), p0((size_t)m), h_part;
+        double *d_Bc = nullptr;
+        std::vector<double> h_part;
         aijhip_mat *Ph = nullptr, *Ach = nullptr;
+        lap("free, vectors");
         if (p.nsmooths > 0) {
             GTRY(dalloc(&v, m), "alloc");
             GTRY(dalloc(&w, m), "alloc");
@@ -759,14 +859,13 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
             }
             lap("emax");
         }
-        // ---- tentative prolongator (host: the near-null space QR per aggregate)
-        for (int32_t i = 0; i < m; ++i) Bc[agg[i]] += B[i] * B[i];
-        for (int32_t a = 0; a < na; ++a) Bc[a] = std::sqrt(Bc[a]);
-        for (int32_t i = 0; i < m; ++i) p0[i] = Bc[agg[i]] > 0.0 ? B[i] / Bc[agg[i]] : 0.0;
+        // ---- tentative prolongator: the near-null space normalised per aggregate
         GTRY(dalloc(&d_agg, m), "alloc");
         GTRY(dalloc(&d_p0, m), "alloc");
+        GTRY(dalloc(&d_Bc, na), "alloc");
         GTRY(hipMemcpy(d_agg, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload");
-        GTRY(hipMemcpy(d_p0, p0.data(), sizeof(double) * (size_t)m, hipMemcpyHostToDevice), "upload");
+        GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0), "tentative prolongator");
+        lap("P0");
         P0.m = m;
         P0.n = na;
         P0.nz = m;
@@ -829,18 +928,19 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         rc = aijhip::attach_transpose(Ph, PT.ai, PT.aj, PT.aa);
         PT = DCsr();  // consumed by attach_transpose (freed on failure)
         if (rc) goto prolong_done;
+        lap("handle P");
         if ((rc = make_handle(A.device, Ac, &Ach))) goto prolong_done;
         levels.back().P = Ph;
         levels.back().emax = emax;
         Ph = nullptr;
         levels.push_back(DeviceLevel{Ach, nullptr, 0.0});
         Ach = nullptr;
-        B.swap(Bc);
+        std::swap(d_B, d_Bc);
         lap("handles");
     prolong_done:
 #undef GTRY
         hipFree(v); hipFree(w); hipFree(part); hipFree(dinv); hipFree(plen);
-        hipFree(P0.ai); hipFree(d_agg); hipFree(d_p0);
+        hipFree(P0.ai); hipFree(d_agg); hipFree(d_p0); hipFree(d_Bc);
         T.release(); P.release(); AP.release(); PT.release(); Ac.release();
         if (Ph) aijhip_mat_destroy(Ph);
         if (Ach) aijhip_mat_destroy(Ach);
@@ -851,6 +951,12 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         }
         if (rc) break;
     }
+    if (!rc) {  // the coarsest device level's near-null space, for the host levels
+        B.resize((size_t)levels.back().A->m);
+        if (!B.empty() && (e = hipMemcpy(B.data(), d_B, sizeof(double) * B.size(), hipMemcpyDeviceToHost)) != hipSuccess)
+            rc = herr(e, "read near-null space");
+    }
+    hipFree(d_B);
     if (rc) free_device_levels(levels);
     return rc;
 }
