@@ -19,13 +19,12 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
-#include <mutex>
-
 #include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -86,13 +85,160 @@ __global__ void k_strong_fill(int32_t m, const int32_t *__restrict__ ai, const i
     }
 }
 
-// per-row insertion sort + unique of the gathered neighbour list
-__global__ void k_sort_unique(int32_t m, const unsigned long long *__restrict__ off, int32_t *tmp, int32_t *ucnt) {
+// The weight of S entry (i, j): |a_ij| of the stored entry, or -1 when A
+// stores no (i, j) (the entry came from S^T). SORTED: A's row columns strictly
+// increase (binary search); otherwise the max over a scan of the row.
+template <bool SORTED>
+__device__ __forceinline__ double stored_weight(int32_t j, int32_t a0, int32_t a1, const int32_t *__restrict__ aj,
+                                                const double *__restrict__ aa) {
+    if (SORTED) {
+        int32_t lo = a0, hi = a1;
+        while (lo < hi) {
+            const int32_t q = (lo + hi) >> 1;
+            if (aj[q] < j) lo = q + 1;
+            else hi = q;
+        }
+        return (lo < a1 && aj[lo] == j) ? fabs(aa[lo]) : -1.0;
+    }
+    double v = -1.0;
+    for (int32_t e = a0; e < a1; ++e)
+        if (aj[e] == j) v = fmax(v, fabs(aa[e]));
+    return v;
+}
+
+// flag = 1 when some row of A has columns that do not strictly increase
+__global__ void k_rows_unsorted(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                                int32_t *flag) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
+    for (int32_t k = ai[i] + 1; k < ai[i + 1]; ++k)
+        if (aj[k] <= aj[k - 1]) { atomicOr(flag, 1); return; }
+}
+
+// Each gathered neighbour list of at most G entries sorted and made unique
+// by G lanes (bitonic across the segment's lanes, unique by ballot), with the
+// kept entries' weights: written back in place (tmp, tval), count to ucnt.
+// Longer lists are k_strength_rows_long's / k_strength_rows_huge's.
+template <int G, bool SORTED>
+__global__ __launch_bounds__(256) void k_strength_rows(int32_t m, const unsigned long long *__restrict__ off,
+                                                       int32_t *tmp, double *tval, int32_t *ucnt,
+                                                       const int32_t *__restrict__ ai,
+                                                       const int32_t *__restrict__ aj,
+                                                       const double *__restrict__ aa) {
+    const int lane = threadIdx.x & 63;
+    const int l = lane & (G - 1);
+    const unsigned long long segmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (lane & ~(G - 1));
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * (64 / G); base < m;
+         base += nw * (64 / G)) {
+        const int64_t i = base + lane / G;
+        unsigned long long o = 0;
+        int n = G + 1;
+        if (i < m) {
+            o = off[i];
+            n = (int)(off[i + 1] - o);
+        }
+        const bool mine = n <= G;
+        int32_t v = (mine && l < n) ? tmp[o + l] : INT32_MAX;
+#pragma unroll
+        for (int k = 2; k <= G; k <<= 1) {
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                const int32_t u = __shfl_xor(v, j, 64);
+                const bool up = (l & k) == 0, low = (l & j) == 0;
+                v = (up == low) ? min(v, u) : max(v, u);
+            }
+        }
+        const int32_t prev = __shfl_up(v, 1, 64);
+        const bool keep = mine && l < n && (l == 0 || v != prev);
+        const unsigned long long bal = __ballot(keep);
+        if (keep) {
+            const int pos = __popcll(bal & segmask & ((1ull << lane) - 1ull));
+            tmp[o + pos] = v;
+            tval[o + pos] = stored_weight<SORTED>(v, ai[i], ai[i + 1], aj, aa);
+        }
+        if (mine && l == 0) ucnt[i] = __popcll(bal & segmask);
+    }
+}
+
+// the rows whose gathered list is longer than lo entries and at most hi
+__global__ void k_collect_rows(int32_t m, const unsigned long long *__restrict__ off, int lo, int hi,
+                               int32_t *rows, unsigned int *count) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int64_t n = (int64_t)(off[i + 1] - off[i]);
+    if (n > lo && n <= hi) rows[atomicAdd(count, 1u)] = i;
+}
+
+constexpr int kLongList = 1024;  // k_strength_rows_long's LDS list
+
+// The same for lists of 65..1024 entries, one workgroup per row: bitonic in
+// LDS, unique by ballot with per-wave counts.
+template <bool SORTED>
+__global__ __launch_bounds__(256) void k_strength_rows_long(int32_t nrows, const int32_t *__restrict__ rows,
+                                                            const unsigned long long *__restrict__ off,
+                                                            int32_t *tmp, double *tval, int32_t *ucnt,
+                                                            const int32_t *__restrict__ ai,
+                                                            const int32_t *__restrict__ aj,
+                                                            const double *__restrict__ aa) {
+    __shared__ int32_t sv[kLongList];
+    __shared__ int wsum[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    for (int32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
+        const int32_t i = rows[q];
+        const unsigned long long o = off[i];
+        const int n = (int)(off[i + 1] - o);
+        int P = 128;
+        while (P < n) P <<= 1;
+        for (int x = t; x < P; x += 256) sv[x] = x < n ? tmp[o + x] : INT32_MAX;
+        __syncthreads();
+        for (int k = 2; k <= P; k <<= 1) {
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int x = t; x < P; x += 256) {
+                    const int y = x ^ j;
+                    if (y > x) {
+                        const int32_t a = sv[x], b = sv[y];
+                        if ((a > b) == ((x & k) == 0)) { sv[x] = b; sv[y] = a; }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        const int32_t a0 = ai[i], a1 = ai[i + 1];
+        int kept = 0;
+        for (int r = 0; r < P; r += 256) {
+            const int x = r + t;
+            const bool keep = x < n && (x == 0 || sv[x] != sv[x - 1]);
+            const unsigned long long bal = __ballot(keep);
+            if (lane == 0) wsum[w] = __popcll(bal);
+            __syncthreads();
+            int before = kept;
+            for (int z = 0; z < w; ++z) before += wsum[z];
+            const int total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+            if (keep) {
+                const int pos = before + __popcll(bal & ((1ull << lane) - 1ull));
+                tmp[o + pos] = sv[x];
+                tval[o + pos] = stored_weight<SORTED>(sv[x], a0, a1, aj, aa);
+            }
+            kept += total;
+            __syncthreads();  // wsum is rewritten by the next round
+        }
+        if (t == 0) ucnt[i] = kept;
+        __syncthreads();  // sv is refilled for the next row
+    }
+}
+
+// Lists longer than kLongList: one lane per row, insertion sort in place.
+template <bool SORTED>
+__global__ void k_strength_rows_huge(int32_t nrows, const int32_t *__restrict__ rows,
+                                     const unsigned long long *__restrict__ off, int32_t *tmp, double *tval,
+                                     int32_t *ucnt, const int32_t *__restrict__ ai,
+                                     const int32_t *__restrict__ aj, const double *__restrict__ aa) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nrows) return;
+    const int32_t i = rows[q];
     int32_t *r = tmp + off[i];
     const int64_t n = (int64_t)(off[i + 1] - off[i]);
-    if (n <= 64) return;  // k_sort_unique_wave's
     for (int64_t a = 1; a < n; ++a) {
         const int32_t v = r[a];
         int64_t b = a - 1;
@@ -102,63 +248,29 @@ __global__ void k_sort_unique(int32_t m, const unsigned long long *__restrict__ 
     int64_t u = 0;
     for (int64_t a = 0; a < n; ++a)
         if (u == 0 || r[a] != r[u - 1]) r[u++] = r[a];
+    for (int64_t a = 0; a < u; ++a) tval[off[i] + a] = stored_weight<SORTED>(r[a], ai[i], ai[i + 1], aj, aa);
     ucnt[i] = (int32_t)u;
 }
 
-// The same per row, one wavefront per row of at most 64 entries: bitonic
-// sort across the lanes, then unique by ballot. Longer rows are left to
-// k_sort_unique (it skips the short ones).
-__global__ __launch_bounds__(256) void k_sort_unique_wave(int32_t m, const unsigned long long *__restrict__ off,
-                                                          int32_t *tmp, int32_t *ucnt) {
+// S = the unique lists compacted (G lanes per row)
+template <int G>
+__global__ __launch_bounds__(256) void k_strength_copy(int32_t m, const unsigned long long *__restrict__ off,
+                                                       const int32_t *__restrict__ tmp,
+                                                       const double *__restrict__ tval,
+                                                       const int32_t *__restrict__ si, int32_t *sj,
+                                                       double *sval) {
     const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < m; i += nw) {
+    const int l = lane & (G - 1);
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * (64 / G); base < m;
+         base += nw * (64 / G)) {
+        const int64_t i = base + lane / G;
+        if (i >= m) continue;
         const unsigned long long o = off[i];
-        const int n = (int)(off[i + 1] - o);
-        if (n > 64) continue;
-        int32_t v = lane < n ? tmp[o + lane] : INT32_MAX;
-#pragma unroll
-        for (int k = 2; k <= 64; k <<= 1) {
-#pragma unroll
-            for (int j = k >> 1; j > 0; j >>= 1) {
-                const int32_t u = __shfl_xor(v, j, 64);
-                const bool up = (lane & k) == 0, low = (lane & j) == 0;
-                v = (up == low) ? min(v, u) : max(v, u);
-            }
-        }
-        const int32_t prev = __shfl_up(v, 1, 64);
-        const bool keep = lane < n && (lane == 0 || v != prev);
-        const unsigned long long bal = __ballot(keep);
-        if (keep) tmp[o + __popcll(bal & ((1ull << lane) - 1ull))] = v;
-        if (lane == 0) ucnt[i] = __popcll(bal);
-    }
-}
-
-// compact the unique lists into S and attach the candidate weights
-// sval = max |a_ij| over stored a_ij of the row (-1: not stored)
-// (one wavefront per row, a lane per S entry, A's row scanned by all lanes)
-__global__ __launch_bounds__(256) void k_strength_compact(int32_t m, const unsigned long long *__restrict__ off,
-                                                          const int32_t *__restrict__ tmp,
-                                                          const int32_t *__restrict__ si,
-                                                          const int32_t *__restrict__ ai,
-                                                          const int32_t *__restrict__ aj,
-                                                          const double *__restrict__ aa, int32_t *sj,
-                                                          double *sval) {
-    const int lane = threadIdx.x & 63;
-    const int64_t nw = (int64_t)gridDim.x * (blockDim.x >> 6);
-    for (int64_t i = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < m; i += nw) {
-        const int32_t *r = tmp + off[i];
-        const int32_t s0 = si[i], s1 = si[i + 1], a0 = ai[i], a1 = ai[i + 1];
-        for (int32_t k0 = s0; k0 < s1; k0 += 64) {
-            const int32_t k = k0 + lane;
-            const int32_t j = k < s1 ? r[k - s0] : -1;
-            double v = -1.0;
-            for (int32_t e = a0; e < a1; ++e)
-                if (aj[e] == j) v = fmax(v, fabs(aa[e]));
-            if (k < s1) {
-                sj[k] = j;
-                sval[k] = v;
-            }
+        const int32_t s0 = si[i], n = si[i + 1] - s0;
+        for (int32_t k = l; k < n; k += G) {
+            sj[s0 + k] = tmp[o + k];
+            sval[s0 + k] = tval[o + k];
         }
     }
 }
@@ -183,6 +295,13 @@ __global__ void k_agg_phase2(int32_t m, const int32_t *__restrict__ si, const in
         if (best >= 0) a = phase1[best];
     }
     agg[i] = a;
+}
+
+__global__ void k_count_value(int32_t m, const int32_t *__restrict__ x, int32_t v, unsigned long long *count) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool hit = i < m && x[i] == v;
+    const unsigned long long b = __ballot(hit);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(count, (unsigned long long)__popcll(b));
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -628,6 +747,110 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu) {
     return AIJHIP_OK;
 }
 
+// S from the gathered lists (tmp, rows at off, cnt entries each): sorted,
+// unique, weighted, compacted into (si, sj, sval) of *nzs entries.
+int strength_lists(const aijhip_mat &A, const unsigned long long *cnt, const unsigned long long *off,
+                   int32_t *tmp, int64_t ntmp, int n_cu, int32_t **si, int32_t **sj, double **sval, int64_t *nzs) {
+    const int32_t m = A.m;
+    double *tval = nullptr;
+    int32_t *ucnt = nullptr, *rows = nullptr, *flag = nullptr;
+    unsigned long long *dmax = nullptr;
+    unsigned int *nrows = nullptr;
+    void *rtmp = nullptr;
+    size_t tb = 0;
+    unsigned long long maxn = 0;
+    int32_t unsorted = 0;
+    int G = 8;
+    hipError_t e;
+    const unsigned g256 = blocks_for(m, 256);
+    *si = *sj = nullptr;
+    *sval = nullptr;
+#define STRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto done; } } while (0)
+    int rc = AIJHIP_OK;
+    STRY(dalloc(&tval, ntmp), "alloc");
+    STRY(dalloc(&ucnt, m), "alloc");
+    STRY(dalloc(&flag, 1), "alloc");
+    STRY(dalloc(&dmax, 1), "alloc");
+    STRY(hipMemset(flag, 0, sizeof(int32_t)), "memset");
+    STRY(hipMemset(dmax, 0, sizeof(unsigned long long)), "memset");
+    hipLaunchKernelGGL(k_rows_unsorted, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, flag);
+    STRY(hipcub::DeviceReduce::Max(nullptr, tb, cnt, dmax, m), "reduce");
+    STRY(hipMalloc(&rtmp, std::max<size_t>(tb, 1)), "alloc");
+    STRY(hipcub::DeviceReduce::Max(rtmp, tb, cnt, dmax, m), "reduce");
+    STRY(hipMemcpy(&maxn, dmax, sizeof(maxn), hipMemcpyDeviceToHost), "read");
+    STRY(hipMemcpy(&unsorted, flag, sizeof(unsorted), hipMemcpyDeviceToHost), "read");
+    while (G < 64 && (unsigned long long)G < maxn) G <<= 1;
+    {
+        const unsigned grid = (unsigned)std::min<int64_t>(blocks_for((int64_t)m * G, 256), (int64_t)n_cu * 32);
+#define AIJHIP_SR(GG)                                                                                          \
+    case GG:                                                                                                   \
+        if (unsorted)                                                                                          \
+            hipLaunchKernelGGL((k_strength_rows<GG, false>), dim3(grid), dim3(256), 0, nullptr, m, off, tmp,   \
+                               tval, ucnt, A.d_ai, A.d_aj, A.d_aa);                                            \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_strength_rows<GG, true>), dim3(grid), dim3(256), 0, nullptr, m, off, tmp,    \
+                               tval, ucnt, A.d_ai, A.d_aj, A.d_aa);                                            \
+        break
+        switch (G) { AIJHIP_SR(8); AIJHIP_SR(16); AIJHIP_SR(32); AIJHIP_SR(64); }
+#undef AIJHIP_SR
+    }
+    if (maxn > 64) {  // the long lists: a workgroup per row, past kLongList a lane per row
+        STRY(dalloc(&rows, m), "alloc");
+        STRY(dalloc(&nrows, 2), "alloc");
+        STRY(hipMemset(nrows, 0, 2 * sizeof(unsigned int)), "memset");
+        hipLaunchKernelGGL(k_collect_rows, dim3(g256), dim3(256), 0, nullptr, m, off, 64, kLongList, rows, nrows);
+        unsigned int nl = 0, nh = 0;
+        STRY(hipMemcpy(&nl, nrows, sizeof(nl), hipMemcpyDeviceToHost), "read");
+        if (nl > 0) {
+            const unsigned grid = (unsigned)std::min<int64_t>(nl, (int64_t)n_cu * 8);
+            if (unsorted)
+                hipLaunchKernelGGL(k_strength_rows_long<false>, dim3(grid), dim3(256), 0, nullptr, (int32_t)nl, rows,
+                                   off, tmp, tval, ucnt, A.d_ai, A.d_aj, A.d_aa);
+            else
+                hipLaunchKernelGGL(k_strength_rows_long<true>, dim3(grid), dim3(256), 0, nullptr, (int32_t)nl, rows,
+                                   off, tmp, tval, ucnt, A.d_ai, A.d_aj, A.d_aa);
+        }
+        if (maxn > (unsigned long long)kLongList) {
+            hipLaunchKernelGGL(k_collect_rows, dim3(g256), dim3(256), 0, nullptr, m, off, kLongList, INT32_MAX,
+                               rows, nrows + 1);
+            STRY(hipMemcpy(&nh, nrows + 1, sizeof(nh), hipMemcpyDeviceToHost), "read");
+            if (nh > 0) {
+                if (unsorted)
+                    hipLaunchKernelGGL(k_strength_rows_huge<false>, dim3(blocks_for(nh, 64)), dim3(64), 0, nullptr,
+                                       (int32_t)nh, rows, off, tmp, tval, ucnt, A.d_ai, A.d_aj, A.d_aa);
+                else
+                    hipLaunchKernelGGL(k_strength_rows_huge<true>, dim3(blocks_for(nh, 64)), dim3(64), 0, nullptr,
+                                       (int32_t)nh, rows, off, tmp, tval, ucnt, A.d_ai, A.d_aj, A.d_aa);
+            }
+        }
+    }
+    STRY(hipGetLastError(), "strength kernels");
+    STRY(dalloc(si, (int64_t)m + 1), "alloc");
+    STRY(scan_offsets(ucnt, m, *si, nzs), "scan");
+    if (*nzs > INT32_MAX) { rc = AIJHIP_ERR_ARG; set_error("GAMG: strength graph exceeds int32"); goto done; }
+    STRY(dalloc(sj, *nzs), "alloc");
+    STRY(dalloc(sval, *nzs), "alloc");
+    {
+        const unsigned grid = (unsigned)std::min<int64_t>(blocks_for((int64_t)m * G, 256), (int64_t)n_cu * 32);
+        switch (G) {
+            case 8: hipLaunchKernelGGL(k_strength_copy<8>, dim3(grid), dim3(256), 0, nullptr, m, off, tmp, tval, *si, *sj, *sval); break;
+            case 16: hipLaunchKernelGGL(k_strength_copy<16>, dim3(grid), dim3(256), 0, nullptr, m, off, tmp, tval, *si, *sj, *sval); break;
+            case 32: hipLaunchKernelGGL(k_strength_copy<32>, dim3(grid), dim3(256), 0, nullptr, m, off, tmp, tval, *si, *sj, *sval); break;
+            default: hipLaunchKernelGGL(k_strength_copy<64>, dim3(grid), dim3(256), 0, nullptr, m, off, tmp, tval, *si, *sj, *sval); break;
+        }
+    }
+    STRY(hipGetLastError(), "strength copy");
+done:
+#undef STRY
+    hipFree(tval); hipFree(ucnt); hipFree(rows); hipFree(flag); hipFree(dmax); hipFree(nrows); hipFree(rtmp);
+    if (rc) {
+        hipFree(*si); hipFree(*sj); hipFree(*sval);
+        *si = *sj = nullptr;
+        *sval = nullptr;
+    }
+    return rc;
+}
+
 // B_c and p0 of the tentative prolongator from the aggregates (device).
 hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0) {
     if (m == 0) return hipSuccess;
@@ -757,16 +980,17 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         }
         const DCsr Av = view_of(A);
         const unsigned g256 = blocks_for(m, 256);
-        const unsigned wgrid = (unsigned)std::min<int64_t>(blocks_for((int64_t)m * 64, 256), (int64_t)n_cu * 32);
         // ---- diagonal, strength graph
         double *d = nullptr, *dinv = nullptr, *sval = nullptr;
         unsigned long long *cnt = nullptr, *off = nullptr;
         unsigned int *pos = nullptr;
-        int32_t *tmp = nullptr, *ucnt = nullptr, *si = nullptr, *sj = nullptr;
+        int32_t *tmp = nullptr, *si = nullptr, *sj = nullptr;
         void *scan_tmp = nullptr;
         size_t tb = 0;
         int64_t nzs = 0;
         int32_t *h_si = nullptr, *h_sj = nullptr, *agg = nullptr, *d_ph = nullptr;
+        int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
+        unsigned long long *d_left = nullptr;
         int32_t na = 0;
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto level_done; } } while (0)
         GTRY(dalloc(&d, m), "alloc");
@@ -790,20 +1014,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         GTRY(hipMemset(pos, 0, sizeof(unsigned int) * (size_t)std::max(m, 1)), "memset");
         hipLaunchKernelGGL(k_strong_fill, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
                            p.threshold, off, pos, tmp);
-        GTRY(dalloc(&ucnt, m), "alloc");
-        hipLaunchKernelGGL(k_sort_unique_wave, dim3(wgrid), dim3(256), 0, nullptr, m, off, tmp, ucnt);
-        hipLaunchKernelGGL(k_sort_unique, dim3(g256), dim3(256), 0, nullptr, m, off, tmp, ucnt);
-        GTRY(dalloc(&si, (int64_t)m + 1), "alloc");
-        {
-            int64_t tot = 0;
-            GTRY(scan_offsets(ucnt, m, si, &tot), "scan");
-            if (tot > INT32_MAX) { rc = AIJHIP_ERR_ARG; set_error("GAMG: strength graph exceeds int32"); goto level_done; }
-            nzs = tot;
-        }
-        GTRY(dalloc(&sj, nzs), "alloc");
-        GTRY(dalloc(&sval, nzs), "alloc");
-        hipLaunchKernelGGL(k_strength_compact, dim3(wgrid), dim3(256), 0, nullptr, m, off, tmp, si, A.d_ai,
-                           A.d_aj, A.d_aa, sj, sval);
+        if ((rc = strength_lists(A, cnt, off, tmp, nzs, n_cu, &si, &sj, &sval, &nzs))) goto level_done;
         GTRY(hipGetLastError(), "strength kernels");
         // ---- aggregation: phases 1 and 3 (sequential greedy) on the host from
         // S staged in pinned memory, phase 2 on the device
@@ -816,26 +1027,42 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
         if (nzs > 0) GTRY(hipMemcpy(h_sj, sj, sizeof(int32_t) * (size_t)nzs, hipMemcpyDeviceToHost), "read S");
         lap("strength");
+        // (phase 1 measured on the MI355X host at 300^3: this int32 form 83 ms;
+        // bitmap or byte flags with or without early exits 87-121 ms)
         na = aijhip_gamg::aggregate_phase1(m, h_si, h_sj, agg);
         lap("phase 1");
-        GTRY(dalloc(&d_ph, 2 * (int64_t)m), "alloc");
+        GTRY(dalloc(&d_ph, m), "alloc");
+        GTRY(dalloc(&d_aggv, m), "alloc");
+        GTRY(dalloc(&d_left, 1), "alloc");
         GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
-        hipLaunchKernelGGL(k_agg_phase2, dim3(g256), dim3(256), 0, nullptr, m, si, sj, sval, d_ph, d_ph + m);
-        GTRY(hipMemcpy(agg, d_ph + m, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
-        lap("phase 2");
-        na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
+        hipLaunchKernelGGL(k_agg_phase2, dim3(g256), dim3(256), 0, nullptr, m, si, sj, sval, d_ph, d_aggv);
+        GTRY(hipMemset(d_left, 0, sizeof(unsigned long long)), "memset");
+        hipLaunchKernelGGL(k_count_value, dim3(g256), dim3(256), 0, nullptr, m, d_aggv, -1, d_left);
+        {
+            unsigned long long left = 0;
+            GTRY(hipMemcpy(&left, d_left, sizeof(left), hipMemcpyDeviceToHost), "read phase 2");
+            lap("phase 2");
+            if (left > 0) {  // phase 3 (sequential) on the host
+                GTRY(hipMemcpy(agg, d_aggv, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
+                na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
+                GTRY(hipMemcpy(d_aggv, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 3");
+            }
+        }
         lap("aggregate");
     level_done:
-        hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(ucnt); hipFree(si); hipFree(sj);
-        hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph);
-        if (rc) { hipFree(dinv); break; }
-        if (na >= m || na == 0) { hipFree(dinv); break; }  // no coarsening: this is the coarsest level
+        hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
+        hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left);
+        if (rc || na >= m || na == 0) {  // an error, or no coarsening: this is the coarsest level
+            hipFree(dinv);
+            hipFree(d_aggv);
+            break;
+        }
 #undef GTRY
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto prolong_done; } } while (0)
         // ---- emax(D^-1 A)
         double emax = 1.0;
         DCsr P0, T, P, AP, PT, Ac;
-        int32_t *d_agg = nullptr, *plen = nullptr;
+        int32_t *d_agg = d_aggv, *plen = nullptr;
         double *d_p0 = nullptr, *v = nullptr, *w = nullptr, *part = nullptr;
         double *d_Bc = nullptr;
         std::vector<double> h_part;
@@ -860,10 +1087,8 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
             lap("emax");
         }
         // ---- tentative prolongator: the near-null space normalised per aggregate
-        GTRY(dalloc(&d_agg, m), "alloc");
         GTRY(dalloc(&d_p0, m), "alloc");
         GTRY(dalloc(&d_Bc, na), "alloc");
-        GTRY(hipMemcpy(d_agg, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload");
         GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0), "tentative prolongator");
         lap("P0");
         P0.m = m;

@@ -160,11 +160,15 @@ def test_gpu_device_setup_matches_host_bitwise(pkg, dims, params):
     """The KSP's device-built hierarchy (aijhip_gamg::build_device, host
     continuation below device_min_rows) equals the host builder's — itself
     bit-identical to oracle/gamg.py — entry for entry."""
+    ai, aj, aa = pkg.poisson_csr(*dims)
+    _check_device_setup(pkg, ai, aj, aa, params)
+
+
+def _check_device_setup(pkg, ai, aj, aa, params):
     torch = pytest.importorskip("torch")
     assert torch.cuda.is_available()
     K = importlib.import_module("petsc-openacc_amd.ksp")
     G = importlib.import_module("petsc-openacc_amd.gamg")
-    ai, aj, aa = pkg.poisson_csr(*dims)
     prm = dict(device_min_rows=0)
     prm.update(params)
     lv = G.build_host(ai, aj, aa, **prm)
@@ -185,3 +189,45 @@ def test_gpu_device_setup_matches_host_bitwise(pkg, dims, params):
             assert np.array_equal(pai, hai) and np.array_equal(paj, haj), l
             assert np.array_equal(_bits(paa), _bits(haa)), l
     A.destroy()
+
+
+def _hub_operator(n_side, hubs, seed, unsorted):
+    """A 3-D Poisson operator plus `hubs` rows coupled (symmetrically, weakly)
+    to many others — strength lists of 65..1024 and of more than 1024 entries
+    — with the diagonal raised to keep it diagonally dominant."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    import importlib as _il
+    pkg = _il.import_module("petsc-openacc_amd")
+    ai, aj, aa = pkg.poisson_csr(n_side)
+    m = len(ai) - 1
+    A = sp.csr_matrix((aa, aj, ai), shape=(m, m)).tocoo()
+    r, c, v = [A.row], [A.col], [A.data]
+    for h, deg in hubs:
+        nb = rng.choice(np.setdiff1d(np.arange(m), [h]), size=deg, replace=False)
+        w = rng.uniform(1.0, 50.0, size=deg)
+        r += [np.full(deg, h), nb]
+        c += [nb, np.full(deg, h)]
+        v += [w, w]
+    B = sp.coo_matrix((np.concatenate(v), (np.concatenate(r), np.concatenate(c))), shape=(m, m)).tocsr()
+    B.sum_duplicates()
+    off = np.asarray(abs(B).sum(axis=1)).ravel() - abs(B.diagonal())
+    B.setdiag(-(off + 1.0))  # the Poisson rows' sign: negative diagonal
+    B.sort_indices()
+    ai, aj, aa = B.indptr.astype(np.int32), B.indices.astype(np.int32), B.data.astype(np.float64)
+    if unsorted:  # reverse every row's storage order
+        aj, aa = aj.copy(), aa.copy()
+        for i in range(m):
+            aj[ai[i]:ai[i + 1]] = aj[ai[i]:ai[i + 1]][::-1]
+            aa[ai[i]:ai[i + 1]] = aa[ai[i]:ai[i + 1]][::-1]
+    return ai, aj, aa
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("unsorted", [False, True])
+def test_gpu_device_setup_long_strength_lists(pkg, unsorted):
+    """Strength lists past one wavefront (a workgroup per row) and past the
+    LDS list (a lane per row), on sorted and on unsorted rows: the device
+    hierarchy still equals the host builder's bit for bit."""
+    ai, aj, aa = _hub_operator(14, [(5, 40), (100, 300), (2000, 700), (7, 1500)], 7, unsorted)
+    _check_device_setup(pkg, ai, aj, aa, dict(coarse_eq_limit=20))
