@@ -7,10 +7,13 @@ A step is one MatMult (y = A x) of the whole operand, inputs resident in HBM.
 N = 1: the BASELINE.json configs[1] workload — 300^3 Poisson CSR (27 M rows,
 188.46 M entries, fp64 values, int32 indices) on one MI355X.
 N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL): weak
-scaling — every rank owns a 300^3 z-slab of a 300 x 300 x 300N grid (at N = 8
-this is 216 M rows, the size of BASELINE configs[3]'s 600^3), the halo planes
-exchanged over RCCL while the diagonal block multiplies (petsc-openacc_amd/
-mpiaij.py).
+scaling — every rank owns a 300^3-row z-slab; the global grid doubles one
+axis per factor 2 of N (z, then y, then x): N = 2 is 300x300x600, N = 4
+300x600x600, N = 8 the 600^3 grid of BASELINE configs[3] (75 planes of
+600^2 per rank). The halo planes are exchanged over RCCL while the diagonal
+block multiplies (petsc-openacc_amd/mpiaij.py). The same line carries
+`strong_300`: the 300^3 operand itself row-partitioned over the N GPUs (the
+north star's "300^3 matrix at 1, 2, 4 and 8 GPUs").
 
 value  = algorithmic bytes of all ranks x K / (max-over-ranks wall time of the
          K timed steps), bytes per SpMV = 12 nnz + 4 (m+1) + 8 n + 8 m
@@ -59,10 +62,28 @@ def parse():
     p.add_argument("--no-gamg", action="store_true", help="skip the CG+GAMG solve (BASELINE configs[2])")
     p.add_argument("--gamg-cpu-iters", type=int, default=3, help="CG+GAMG iterations in the CPU sample")
     p.add_argument("--cg-iters", type=int, default=200, help="CG iterations timed for cg.iters_per_s")
+    p.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling 300^3 line")
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
                         "(launch with torch.distributed.run): a one-GPU rehearsal of the N > 1 run")
     return p.parse_args()
+
+
+def weak_grid(G: int, world: int):
+    """Global grid (nx, ny, nz) with G^3 rows per rank in whole z-planes:
+    each factor 2 of the world size doubles z, then y, then x (N = 8 from
+    G = 300 is 600^3); any odd factor multiplies z. Falls back to
+    G x G x G*world when the planes do not divide evenly."""
+    dims, axis, w = [G, G, G], 2, world
+    while w % 2 == 0:
+        dims[axis] *= 2
+        axis = (axis - 1) % 3
+        w //= 2
+    dims[2] *= w
+    nx, ny, nz = dims
+    if nz % world or nx * ny * (nz // world) != G ** 3:
+        return G, G, G * world
+    return nx, ny, nz
 
 
 def cpu_baseline(ai, aj, aa, x, seconds, all_cores=False):
@@ -179,6 +200,46 @@ def cpu_model():
     return "unknown"
 
 
+def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args):
+    """The G^3 operand (300^3: BASELINE configs[1]) row-partitioned over all
+    ranks in balanced whole z-planes (DMDA PETSC_DECIDE), timed like the main
+    line: K distributed SpMVs between barriers, max over ranks. Strong
+    scaling: the total work is the N = 1 workload's."""
+    import torch
+    import torch.distributed as dist
+    bounds = [mpiaij.slab_bounds(G, world, r) for r in range(world)]
+    row_starts = np.array([b[0] * G * G for b in bounds] + [G ** 3], dtype=np.int64)
+    z0, z1 = bounds[rank]
+    ai, aj, aa = pkg.poisson_csr(G, G, G, z0, z1)
+    op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo)
+    nnz_t = torch.tensor([len(aj)], dtype=torch.float64, device=dev)
+    dist.all_reduce(nnz_t)
+    nnz = int(nnz_t.item())
+    del ai, aj, aa
+    x = torch.from_numpy(pkg.splitmix_uniform(op.mloc, 42, int(row_starts[rank]))).to(dev)
+    y = torch.empty(op.mloc, dtype=torch.float64, device=dev)
+    for _ in range(args.warmup):
+        op.mult(x, y)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        op.mult(x, y)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    dt = float(el.item()) / args.steps
+    nbytes = pkg.algorithmic_bytes(G ** 3, G ** 3, nnz)
+    op.A_d.destroy()
+    if op.A_o is not None:
+        op.A_o.destroy()
+    return {"workload": f"{G}^3 Poisson CSR row-partitioned over {world} GPUs "
+                        f"({z1 - z0} of {G} z-planes on rank {rank})",
+            "scaling": "strong", "value": round(nbytes / dt / 1e9, 2), "unit": "GB/s",
+            "ms_per_step": round(dt * 1e3, 4), "rows": G ** 3, "nnz": nnz, "halo": args.halo}
+
+
 def main():
     args = parse()
     import torch
@@ -207,10 +268,10 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     G = args.grid
-    nx = ny = G
-    nz_global = G * world
-    row_starts = np.array([min(r * G, nz_global) * nx * ny for r in range(world + 1)], dtype=np.int64)
-    z0, z1 = rank * G, (rank + 1) * G
+    nx, ny, nz_global = weak_grid(G, world) if distributed else (G, G, G)
+    planes = nz_global // world
+    row_starts = np.array([r * planes * nx * ny for r in range(world + 1)], dtype=np.int64)
+    z0, z1 = rank * planes, (rank + 1) * planes
     t_setup = time.perf_counter()
     ai, aj, aa = pkg.poisson_csr(nx, ny, nz_global, z0, z1)
     m_loc = len(ai) - 1
@@ -281,6 +342,10 @@ def main():
     torch.cuda.synchronize()
     stable = bool(torch.equal(y_chk, yd))
 
+    strong = None
+    if distributed and not args.no_strong:
+        strong = strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args)
+
     cg = None
     if not args.no_cg and not distributed:
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
@@ -309,7 +374,7 @@ def main():
         cg = {"iters": cgm.its, "seconds": round(dt, 4), "iters_per_s": round(cgm.its / dt, 2),
               "ms_per_iter": round(dt / cgm.its * 1e3, 4), "pc": "jacobi (bjacobi+jacobi per rank)",
               "reductions": "2 all-reduces per iteration (RCCL)", "halo": args.halo,
-              "workload": f"{G}x{G}x{nz_global} Poisson, z-slab per GPU"}
+              "workload": f"{nx}x{ny}x{nz_global} Poisson, {planes}-plane z-slab per GPU"}
     cg_gamg = None
     if not args.no_gamg and not distributed:
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
@@ -342,7 +407,8 @@ def main():
             "data": "synthetic (generated 7-pt Poisson operand of helper.cpp; x = splitmix64 uniform[-1,1))"
             if args.x == "uniform" else "synthetic (helper.cpp operand; x = generateExt field)",
             "config": {
-                "workload": f"{G}x{G}x{nz_global} Poisson CSR, z-slab per GPU" if distributed
+                "workload": f"{nx}x{ny}x{nz_global} Poisson CSR, {planes}-plane z-slab ({m_loc} rows) per GPU"
+                if distributed
                 else f"{G}^3 Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])",
                 "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
                 "kernel": info["kernel"], "halo": args.halo if distributed else None,
@@ -365,6 +431,8 @@ def main():
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
+        if strong is not None:
+            out["strong_300"] = strong
         if cg is not None:
             out["cg"] = cg
         if cg_gamg is not None:
