@@ -93,6 +93,13 @@ __device__ __forceinline__ double block_sum(double v, double *scratch) {
     return s;  // valid in thread 0
 }
 
+// Row results are written once and not re-read by this launch: stored with the
+// non-temporal hint (`global_store … nt`). Measured on the 300^3 operand
+// (tools/ablate_buf.py, profiles/r01/ablate_buf{1,2}*.jsonl): 472 -> 450 us and
+// 491 -> 462 us on two boxes; the sc0/sc1 policy variants with nt tie, plain or
+// sc0/sc1-only stores do not gain.
+__device__ __forceinline__ void st_stream(double *p, double v) { __builtin_nontemporal_store(v, p); }
+
 // What a STREAM launch gathers and writes. The row sum s_i = sum a_ij g(j)
 // is formed in PETSc's order (or the deterministic multi-lane order); `seed`
 // starts it (MatMultAdd's z_i), `put` stores the row's result and adds to
@@ -108,7 +115,7 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int o) const { return ADD ? z[o] : 0.0; }
     __device__ void put(int o, double v, double *d) const {
-        y[o] = v;
+        st_stream(y + o, v);
         if (dot) d[0] += x[o] * v;
     }
 };
@@ -116,6 +123,7 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
 // V-cycle pre-smoothing from a zero guess fused with the residual
 // (ksp.hip k_jacobi + SpMV + k_resid, same roundings): x = D^-1 b is gathered
 // as dinv_j * b_j, and each row stores x_i and r_i = b_i + (-1) (A x)_i.
+template <bool NT>
 struct OpMgPre {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
@@ -126,8 +134,13 @@ struct OpMgPre {
     __device__ double seed(int) const { return 0.0; }
     __device__ void put(int o, double v, double *) const {
         const double bo = b[o];
-        x[o] = dinv[o] * bo;
-        r[o] = bo + (-1.0) * v;
+        if constexpr (NT) {
+            st_stream(x + o, dinv[o] * bo);
+            st_stream(r + o, bo + (-1.0) * v);
+        } else {
+            x[o] = dinv[o] * bo;
+            r[o] = bo + (-1.0) * v;
+        }
     }
 };
 
@@ -135,6 +148,7 @@ struct OpMgPre {
 // (SpMV + k_richardson): x_i = t_i + 1.0 (dinv_i (b_i + (-1) (A t)_i)); x
 // must not alias t. With dot, the finest level also yields CG's z.z and z.b
 // partials (z = x, b = CG's residual).
+template <bool NT>
 struct OpMgPost {
     static constexpr int kDots = 2;
     static constexpr bool kSeeded = false;
@@ -147,7 +161,8 @@ struct OpMgPost {
     __device__ void put(int o, double v, double *d) const {
         const double bo = b[o];
         const double xo = t[o] + 1.0 * (dinv[o] * (bo + (-1.0) * v));
-        x[o] = xo;
+        if constexpr (NT) st_stream(x + o, xo);
+        else x[o] = xo;
         if (dot) {
             d[0] += xo * xo;
             d[1] += xo * bo;
@@ -164,7 +179,7 @@ struct OpDinvMult {
     double *y;
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int) const { return 0.0; }
-    __device__ void put(int o, double v, double *) const { y[o] = dinv[o] * v; }
+    __device__ void put(int o, double v, double *) const { st_stream(y + o, dinv[o] * v); }
 };
 
 template <int T, int CAP, int RPT, bool CROW, bool XCD, bool NT, bool CLAMPED, class Op>
@@ -824,13 +839,15 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
 }
 
 hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
-                         hipStream_t s) {
-    return launch_stream_op(A, OpMgPre{b, dinv, x, r}, nullptr, s);
+                         hipStream_t s, bool nt) {
+    if (nt) return launch_stream_op(A, OpMgPre<true>{b, dinv, x, r}, nullptr, s);
+    return launch_stream_op(A, OpMgPre<false>{b, dinv, x, r}, nullptr, s);
 }
 
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
-                          double *dpart, hipStream_t s) {
-    return launch_stream_op(A, OpMgPost{t, b, dinv, x, dpart != nullptr}, dpart, s);
+                          double *dpart, hipStream_t s, bool nt) {
+    if (nt) return launch_stream_op(A, OpMgPost<true>{t, b, dinv, x, dpart != nullptr}, dpart, s);
+    return launch_stream_op(A, OpMgPost<false>{t, b, dinv, x, dpart != nullptr}, dpart, s);
 }
 
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s) {

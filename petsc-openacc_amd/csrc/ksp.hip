@@ -212,6 +212,14 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_init(const double *part,
 // The previous iteration's VecAXPY(X, a, P) is applied here, where P is read
 // anyway, before P is overwritten (same operation on every element, one
 // iteration later: X and P make one pass fewer per iteration).
+// NT: stores carry the non-temporal hint (vec_store_nt below).
+template <bool NT>
+__device__ __forceinline__ void vst(double *p, double v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <bool NT>
 __global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *__restrict__ z, double *p,
                                                       double *x, const CGState *S) {
     if (S->done) return;
@@ -219,8 +227,8 @@ __global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *_
     const double bb = S->b, a = S->a;
     GRID_STRIDE(i, n) {
         const double pi = p[i];
-        if (!first) x[i] = x[i] + a * pi;
-        p[i] = first ? z[i] : z[i] + bb * pi;
+        if (!first) vst<NT>(x + i, x[i] + a * pi);
+        vst<NT>(p + i, first ? z[i] : z[i] + bb * pi);
     }
 }
 
@@ -268,6 +276,7 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_dpi(const double *part, 
 // read before z[i] is written by the same lane); partials Z.Z, Z.R, R.R
 // (GAMG: R.R only, Z follows from the V-cycle). VecAXPY(X, a, P) is deferred
 // to the next K1 (or k_final_x).
+template <bool NT>
 __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, double *wz,
                                                         const double *__restrict__ dinv, double *part,
                                                         const CGState *S, int pc) {
@@ -277,11 +286,11 @@ __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, do
     double zz = 0.0, zr = 0.0, rr = 0.0;
     GRID_STRIDE(i, n) {
         const double ri = r[i] + na * wz[i];  // VecAXPY(R, -a, W)
-        r[i] = ri;
+        vst<NT>(r + i, ri);
         rr += ri * ri;
         if (pc != AIJHIP_PC_GAMG) {
             const double zi = pc == AIJHIP_PC_JACOBI ? dinv[i] * ri : ri;  // PCApply_Jacobi
-            wz[i] = zi;
+            vst<NT>(wz + i, zi);
             zz += zi * zi;
             zr += zi * ri;
         }
@@ -380,6 +389,9 @@ struct aijhip_ksp {
     bool set_up = false;
     bool fused = false;
     int vec_grid = 0;
+    // CG vector kernels store with the non-temporal hint; AIJHIP_VEC_NT=0/1
+    // overrides (diagnostic A/B, read at KSPCreate).
+    bool vec_nt = true;
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
     double *d_hist = nullptr;
     int32_t hist_cap = 0;
@@ -557,7 +569,7 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
             break;
         }
         if (L.fused) {
-            if ((e = aijhip::launch_mg_pre(*L.A, B(l), L.dinv, X(l), L.r, s)) != hipSuccess) return e;
+            if ((e = aijhip::launch_mg_pre(*L.A, B(l), L.dinv, X(l), L.r, s, K->vec_nt)) != hipSuccess) return e;
         } else {
             hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));  // smoothd
             if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
@@ -573,7 +585,7 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
             // MatInterpolateAdd into the scratch: t = x + P x_c, then smoothu
             if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), L.r, true, s)) != hipSuccess) return e;
             double *dp = (l == 0 && dots) ? dots : nullptr;
-            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s)) != hipSuccess) return e;
+            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s, K->vec_nt)) != hipSuccess) return e;
             if (dp && dots_done) *dots_done = true;
         } else {
             // MatInterpolateAdd: x = x + P x_c
@@ -597,6 +609,7 @@ int aijhip_ksp_create(aijhip_mat_t A, aijhip_ksp_t *out) {
     aijhip_ksp *K = new (std::nothrow) aijhip_ksp();
     if (!K) return kfail(AIJHIP_ERR_ALLOC, "host allocation");
     K->A = A;
+    if (const char *v = std::getenv("AIJHIP_VEC_NT")) K->vec_nt = std::atoi(v) != 0;
     aijhip_gamg_params_default(&K->gamg);
     *out = K;
     return AIJHIP_OK;
@@ -740,7 +753,8 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             return khip(e, "KSPSolve poll");
         if (K->h_state->done || launched >= K->max_it) break;
         for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched) {
-            hipLaunchKernelGGL(k_aypx, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
+            if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
+            else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             if (K->fused) {
                 e = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, s);
                 if (e == hipSuccess)
@@ -750,8 +764,12 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
                 hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
                 hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, nb, K->d_state);
             }
-            hipLaunchKernelGGL(k_update, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part, K->d_state,
-                               K->pc);
+            if (K->vec_nt)
+                hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
+                                   K->d_state, K->pc);
+            else
+                hipLaunchKernelGGL(k_update<false>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
+                                   K->d_state, K->pc);
             const double *pz = K->d_part;
             int nbz = nb;
             if (gamg && e == hipSuccess) {
