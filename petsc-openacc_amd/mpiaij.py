@@ -96,6 +96,11 @@ class MPIAIJ:
             oaj = self._allgather_layout(oaj, garray)
         self.A_o = make_local(oai, oaj, oaa, max(self.n_ghost_buf, 1)) if len(oaj) else None
         self.ghost = torch.zeros(max(self.n_ghost_buf, 1), dtype=torch.float64, device=device)
+        # RCCL orders its transfers after the compute stream's queued kernels;
+        # gloo moves device tensors with host-side copies that are not
+        # stream-ordered, so on that backend (the one-GPU tests) the stream is
+        # drained first: x fully written, the previous mult_add done with `ghost`.
+        self.host_ordered = dist.get_backend(group) == "gloo" and torch.device(device).type == "cuda"
 
     # -------------------------------------------------------------- layouts
     @property
@@ -125,6 +130,8 @@ class MPIAIJ:
     # ---------------------------------------------------------------- halo
     def _post_halo(self, x):
         """Start the ghost exchange; returns a list of works to wait on."""
+        if self.host_ordered:
+            torch.cuda.current_stream(x.device).synchronize()
         if self.halo == "allgather":
             if self.gather_slice is not None:
                 n = self.gather_slice.stop - self.gather_slice.start
