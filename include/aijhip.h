@@ -151,13 +151,24 @@ enum {
                                        within the fp64 bound); shorter rows
                                        (7-pt Poisson, FEM rows) are bit-exact
                                        either way                           */
-    AIJHIP_OPT_X_TILE = 7           /* 1: stage x in LDS for every block whose
+    AIJHIP_OPT_X_TILE = 7,          /* 1: stage x in LDS for every block whose
                                        columns span <= the block's LDS entries
                                        (banded operators) and gather from
                                        there; -1: only when half the blocks
                                        fit; 0 (default, measured faster on
                                        the skewed stand-in): gathers from
                                        HBM/L2. Same results                   */
+    AIJHIP_OPT_LONG_XCD = 8,        /* 1 (default): segments of long rows are
+                                       launched so that XCD q (slot % 8)
+                                       reduces those whose columns lie in the
+                                       q-th eighth of x (its L2 then holds the
+                                       x range of their scattered gathers);
+                                       0: segment order. Same results        */
+    AIJHIP_OPT_LONG_OVERLAP = 9     /* 1: long-row segments run on a side
+                                       stream concurrently with the row
+                                       blocks (forked from and joined back to
+                                       the caller's stream); 0 (default): one
+                                       stream. Same results                  */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

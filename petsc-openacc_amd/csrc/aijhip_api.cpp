@@ -68,6 +68,10 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_segs);
     hipFree(P.d_longs);
     hipFree(P.d_partials);
+    hipFree(P.d_segperm);
+    if (P.ev_fork) (void)hipEventDestroy(P.ev_fork);
+    if (P.ev_join) (void)hipEventDestroy(P.ev_join);
+    if (P.long_stream) (void)hipStreamDestroy(P.long_stream);
     hipFree(P.d_xrange);
     hipFree(P.d_tile_coord);
     hipFree(P.d_carry_row);
@@ -202,6 +206,38 @@ int plan_stream(aijhip_mat *A) {
         if ((e = hipMemcpy(P.d_segs, segs.data(), sizeof(LongSeg) * segs.size(), hipMemcpyHostToDevice)) != hipSuccess ||
             (e = hipMemcpy(P.d_longs, longs.data(), sizeof(LongRow) * longs.size(), hipMemcpyHostToDevice)) != hipSuccess)
             return hipfail(e, "plan: upload long rows");
+        if (P.tune.long_xcd && segs.size() >= 16 && A->n >= 8) {
+            // deal segments to launch slots so that slot s (XCD s % 8 under
+            // round-robin placement) gets one whose middle column lies in the
+            // (s % 8)-th eighth of x; an exhausted eighth takes from the fullest
+            std::vector<int32_t> mid(segs.size());
+            if ((e = aijhip::segment_mid_columns(*A, P.d_segs, P.n_segs, mid.data())) != hipSuccess)
+                return hipfail(e, "plan: segment columns");
+            std::vector<std::vector<int32_t>> part(8);
+            for (int32_t i = 0; i < P.n_segs; ++i)
+                part[std::min<int64_t>(7, (int64_t)mid[i] * 8 / A->n)].push_back(i);
+            std::vector<size_t> head(8, 0);
+            std::vector<int32_t> perm(segs.size());
+            for (int32_t s = 0; s < P.n_segs; ++s) {
+                int q = s & 7;
+                if (head[q] == part[q].size()) {
+                    size_t best = 0;
+                    for (int c = 0; c < 8; ++c)
+                        if (part[c].size() - head[c] > best) { best = part[c].size() - head[c]; q = c; }
+                }
+                perm[s] = part[q][head[q]++];
+            }
+            if ((e = dmalloc(&P.d_segperm, perm.size(), &P.bytes)) != hipSuccess ||
+                (e = hipMemcpy(P.d_segperm, perm.data(), sizeof(int32_t) * perm.size(), hipMemcpyHostToDevice)) !=
+                    hipSuccess)
+                return hipfail(e, "plan: segment placement");
+        }
+        if (P.tune.long_overlap && P.n_blocks > 0) {
+            if ((e = hipStreamCreateWithFlags(&P.long_stream, hipStreamNonBlocking)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming)) != hipSuccess ||
+                (e = hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming)) != hipSuccess)
+                return hipfail(e, "plan: long-row stream");
+        }
     }
     return AIJHIP_OK;
 }
@@ -516,6 +552,8 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "x_tile: -1 auto, 0 off, 1 on");
             t.xtile = value;
             break;
+        case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
+        case AIJHIP_OPT_LONG_OVERLAP: t.long_overlap = value != 0; break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);

@@ -94,6 +94,8 @@ struct Tuning {
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
     int xtile = 0;         // x staged in LDS per block: 0 off (measured default), 1 where it fits,
                            // -1 when half the blocks fit
+    bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
+    bool long_overlap = false;  // long-row segments on a side stream, concurrent with the row blocks
 };
 
 // STREAM blocks whose mean row length exceeds this use several lanes per row
@@ -115,6 +117,15 @@ struct Plan {
     LongRow *d_longs = nullptr;
     int32_t n_longs = 0;
     double *d_partials = nullptr;
+    // launch slot -> segment (nullptr = identity): slot s runs on XCD s % 8
+    // under round-robin placement, and is given a segment whose columns lie in
+    // the s % 8-th eighth of x, so each XCD's L2 holds the x range its
+    // scattered gathers hit (speed only; partials and their order unchanged)
+    int32_t *d_segperm = nullptr;
+    // Tuning::long_overlap: the long-row kernels run on a side stream forked
+    // from and joined back to the caller's stream around the STREAM launch
+    hipStream_t long_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // x tiles: per block the first column and the span of its columns, or
     // span -1 when they do not fit the block's LDS (gathers from HBM)
     int2 *d_xrange = nullptr;
@@ -198,6 +209,8 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
                            double **d_taa, hipStream_t s);
 
 RowList row_list(const aijhip_mat &A);
+// Per long-row segment: the column of its middle entry (synchronous).
+hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out);
 // Per STREAM block: min column and span (max - min + 1) of its entries.
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out);
 // Install A^T (device arrays, freed by the call) as A's transpose handle.

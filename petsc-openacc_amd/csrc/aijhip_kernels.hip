@@ -24,8 +24,9 @@
 //          completed by an in-tile chain and a per-tile carry fix-up. For
 //          skewed row lengths (the Flan_1565 stress config).
 //
-// Rows longer than 2048 entries leave the STREAM blocks and are split into
-// 16K-entry segments, each reduced by one workgroup, then summed in segment
+// Rows longer than a block's entry cap leave the STREAM blocks and are split
+// into kLongSegNnz-entry segments, each reduced by one workgroup (placed on
+// the XCD whose eighth of x its columns fall in), then summed in segment
 // order by a finishing kernel (deterministic, not bit-identical).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -401,10 +402,11 @@ __global__ __launch_bounds__(T) void k_spmv_stream_pipe(
 __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     const LongSeg *__restrict__ seg, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const double *__restrict__ x,
-    double *__restrict__ partials) {
+    double *__restrict__ partials, const int32_t *__restrict__ perm) {
     constexpr int U = 8;
     __shared__ double red[kLongThreads / 64];
-    const LongSeg s = seg[blockIdx.x];
+    const int32_t id = perm ? perm[blockIdx.x] : (int32_t)blockIdx.x;
+    const LongSeg s = seg[id];
     const int t = threadIdx.x;
     double acc[U] = {};
     const int64_t k1 = (int64_t)s.k0 + s.nk;
@@ -430,20 +432,28 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
         double r = red[0];
 #pragma unroll
         for (int w = 1; w < kLongThreads / 64; ++w) r += red[w];
-        partials[blockIdx.x] = r;
+        partials[id] = r;
     }
 }
 
+// One wavefront per long row: the lanes load 64 partials at once and the sum
+// runs through them in segment order by broadcast (a lane-per-row loop waited
+// on one dependent load per segment: 9 us for the stand-in's 119 hub rows).
 template <bool ADD>
-__global__ void k_long_finish(const LongRow *__restrict__ lr, int nl,
-                              const double *__restrict__ partials, const double *z,
-                              double *y) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(64) void k_long_finish(const LongRow *__restrict__ lr, int nl,
+                                                    const double *__restrict__ partials, const double *z,
+                                                    double *y) {
+    const int i = blockIdx.x;
     if (i >= nl) return;
     const LongRow r = lr[i];
+    const int t = threadIdx.x;
     double s = ADD ? z[r.orow] : 0.0;
-    for (int q = 0; q < r.nseg; ++q) s += partials[r.seg0 + q];
-    y[r.orow] = s;
+    for (int q0 = 0; q0 < r.nseg; q0 += 64) {
+        const int nq = min(64, r.nseg - q0);
+        const double v = t < nq ? partials[r.seg0 + q0 + t] : 0.0;
+        for (int q = 0; q < nq; ++q) s += __shfl(v, q, 64);
+    }
+    if (t == 0) y[r.orow] = s;
 }
 
 template <bool ADD, bool CROW>
@@ -722,6 +732,27 @@ hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, i
     return e == hipSuccess ? hipDeviceSynchronize() : e;
 }
 
+__global__ __launch_bounds__(256) void k_seg_midcol(const LongSeg *__restrict__ seg, int32_t ns,
+                                                    const int32_t *__restrict__ aj, int32_t *out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= ns) return;
+    const LongSeg s = seg[i];
+    out[i] = s.nk > 0 ? aj[(int64_t)s.k0 + s.nk / 2] : 0;
+}
+
+hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out) {
+    if (n_segs <= 0) return hipSuccess;
+    int32_t *d_out = nullptr;
+    hipError_t e = hipMalloc(&d_out, sizeof(int32_t) * (size_t)n_segs);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_seg_midcol, dim3(grid_for(n_segs, 256)), dim3(256), 0, nullptr, d_segs, n_segs, A.d_aj,
+                       d_out);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(h_out, d_out, sizeof(int32_t) * (size_t)n_segs, hipMemcpyDeviceToHost);
+    hipFree(d_out);
+    return e;
+}
+
 RowList row_list(const aijhip_mat &A) {
     if (A.compressed) return RowList{A.n_crow, A.d_cai, A.d_ridx};
     return RowList{A.m, A.d_ai, nullptr};
@@ -860,6 +891,25 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     if (e != hipSuccess) return e;
     const RowList L = row_list(A);
     const Plan &P = A.plan;
+    // long rows: segment partials, then their ordered sums
+    auto longs = [&](hipStream_t ls) -> hipError_t {
+        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, ls,
+                           P.d_segs, A.d_aj, A.d_aa, x, P.d_partials, P.d_segperm);
+        hipError_t le = hipGetLastError();
+        if (le != hipSuccess) return le;
+        if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, ls, P.d_longs, P.n_longs,
+                                    P.d_partials, z, y);
+        else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, ls, P.d_longs, P.n_longs,
+                                P.d_partials, z, y);
+        return hipGetLastError();
+    };
+    const bool fork = P.n_longs > 0 && P.long_stream != nullptr;
+    if (fork) {  // side stream: ordered after everything already on s
+        if ((e = hipEventRecord(P.ev_fork, s)) != hipSuccess ||
+            (e = hipStreamWaitEvent(P.long_stream, P.ev_fork, 0)) != hipSuccess ||
+            (e = longs(P.long_stream)) != hipSuccess || (e = hipEventRecord(P.ev_join, P.long_stream)) != hipSuccess)
+            return e;
+    }
     // Every geometry is dispatched explicitly: the kernel's LDS size must be
     // the one the plan's row blocks were cut for.
     static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
@@ -884,15 +934,8 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
 #undef AIJHIP_SG
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (P.n_longs > 0) {
-        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s,
-                           P.d_segs, A.d_aj, A.d_aa, x, P.d_partials);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        const dim3 g(grid_for(P.n_longs, 256)), b(256);
-        if (add) hipLaunchKernelGGL(k_long_finish<true>, g, b, 0, s, P.d_longs, P.n_longs, P.d_partials, z, y);
-        else hipLaunchKernelGGL(k_long_finish<false>, g, b, 0, s, P.d_longs, P.n_longs, P.d_partials, z, y);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
+    if (fork) return hipStreamWaitEvent(s, P.ev_join, 0);  // join: s sees the long rows' y
+    if (P.n_longs > 0) return longs(s);
     return hipSuccess;
 }
 

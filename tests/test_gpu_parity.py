@@ -331,6 +331,39 @@ def test_skewed_flan_standin_all_kernels(pkg, dev, coracle):
     check(y, ref, ai, aj, aa, x, exact=False)
 
 
+def test_long_row_xcd_placement_is_speed_only(pkg, dev, coracle):
+    """Long-row segments dealt to XCDs by column range (AIJHIP_OPT_LONG_XCD)
+    give the same bits as segment order: the same partials, summed in the
+    same order; only the workgroup that computes each one moves."""
+    ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
+    x = pkg.splitmix_uniform(len(ai) - 1, 5)
+    ref = coracle.matmult(ai, aj, aa, x, omp=True)
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        assert A.info()["n_long_rows"] > 0
+        xd = to_dev(x, dev)
+        yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
+        ys = []
+        for lx, lo in ((1, 0), (0, 0), (1, 1), (0, 1), (1, 0)):
+            A.set_option("long_xcd", lx)
+            A.set_option("long_overlap", lo)  # side stream forked from / joined to the caller's
+            yd.fill_(float("nan"))
+            A.mult(xd, yd)
+            torch.cuda.synchronize()
+            ys.append(yd.cpu().numpy())
+        for y in ys[1:]:
+            assert_bits(y, ys[0])
+        check(ys[0], ref, ai, aj, aa, x, exact=False)
+        # MatMultAdd through the forked path: w = z + A x
+        zd = to_dev(pkg.splitmix_uniform(len(ai) - 1, 6), dev)
+        A.mult_add(xd, zd, yd)
+        torch.cuda.synchronize()
+        A.set_option("long_overlap", 0)
+        wd = torch.empty_like(yd)
+        A.mult_add(xd, zd, wd)
+        torch.cuda.synchronize()
+        assert_bits(yd.cpu().numpy(), wd.cpu().numpy())
+
+
 @pytest.mark.parametrize("name", ["poisson16", "skewed_small", "compressed_small"])
 def test_stream_options_do_not_change_results(pkg, dev, name):
     """Every STREAM geometry / XCD remap / non-temporal setting is speed-only."""

@@ -84,6 +84,9 @@ def main():
     if args.variants == "xtile":
         for g, xt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
+    if args.variants == "longxcd":
+        for g, lx, lo in itertools.product((1, 6), (0, 1), (0, 1)):
+            variants.append(("stream", dict(geometry=g, long_xcd=lx, long_overlap=lo)))
     if args.variants == "skewgeom":
         for g, ex in itertools.product(range(9), (0, 1)):
             variants.append(("stream", dict(geometry=g, exact=ex)))
@@ -102,6 +105,8 @@ def main():
         A.set_kernel(kind, opts.get("lanes", 0))
         A.set_option("exact", opts.get("exact", 0))
         A.set_option("x_tile", opts.get("x_tile", -1))
+        A.set_option("long_xcd", opts.get("long_xcd", 1))
+        A.set_option("long_overlap", opts.get("long_overlap", 0))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
