@@ -41,12 +41,19 @@ def main():
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--variants", default="stream")
     ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx"])
+    ap.add_argument("--file", default=None, help="a MatrixMarket (.mtx) or PETSc binary operand, e.g. Flan_1565.mtx")
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
     dev = torch.device("cuda:0")
     stream = torch.cuda.current_stream()
     t0 = time.time()
-    if args.matrix == "poisson":
+    if args.file:
+        matio = importlib.import_module("petsc-openacc_amd.matio")
+        load = matio.load_mtx if args.file.endswith(".mtx") else matio.load_petsc_binary
+        ai, aj, aa, ncols = load(args.file)
+        if ncols != len(ai) - 1:
+            raise SystemExit("tune.py times square operands (x and y share a length)")
+    elif args.matrix == "poisson":
         ai, aj, aa = pkg.poisson_csr(args.grid)
     else:
         ai, aj, aa = pkg.skewed_csr()
