@@ -111,3 +111,21 @@ int main(void) {
     assert r.returncode == 0, r.stderr
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert out.stdout.split()[:2] == ["1", "50"]
+
+
+def test_petsc_adapter_binds_only_declared_symbols():
+    """petsc-openacc_amd/petsc/aijhip_petsc.c (compiled only against a PETSc
+    tree, absent here) calls the library through the declared ABI alone, and
+    its Makefile is a no-op without PETSC_DIR."""
+    src = (ROOT / "petsc-openacc_amd" / "petsc" / "aijhip_petsc.c").read_text()
+    used = set(re.findall(r"\b(aijhip_\w+)\s*\(", src))
+    assert {"aijhip_mat_create", "aijhip_mat_mult_host", "aijhip_mat_update_values",
+            "aijhip_mat_assembly_end", "aijhip_mat_destroy"} <= used
+    assert used <= declared_functions()
+    for sym in ("MatRegister", "MatCreate_SeqAIJ", "PetscDLLibraryRegister_aijhip_petsc",
+                "MatAssemblyEnd_SeqAIJ", "MatDestroy_SeqAIJ", "MatMult_SeqAIJ"):
+        assert sym in src
+    env = {k: v for k, v in __import__("os").environ.items() if k != "PETSC_DIR"}
+    r = subprocess.run(["make", "-s", "-C", str(ROOT / "petsc-openacc_amd" / "petsc")], capture_output=True,
+                       text=True, env=env)
+    assert r.returncode == 0 and "PETSC_DIR is not set" in r.stdout
