@@ -189,6 +189,9 @@ bool stream_mg_fusable(const aijhip_mat &A);
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s);
 hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
                          hipStream_t s, bool nt);
+// r = b - A x on a STREAM plan (residual in the SpMV epilogue).
+hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
+                           bool nt);
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
                           double *dpart, hipStream_t s, bool nt);
 // Dispatch y = A x (or w = z + A x) through the handle's plan.

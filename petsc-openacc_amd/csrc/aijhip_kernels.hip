@@ -145,6 +145,25 @@ struct OpMgPre {
     }
 };
 
+// MatResidual with the SpMV: r_i = b_i + (-1) (A x)_i (SpMV + k_resid, same
+// roundings) — the second half of the split pre-smoothing, after x = D^-1 b
+// was written by a vector pass (one gather per entry instead of OpMgPre's two).
+template <bool NT>
+struct OpMgResid {
+    static constexpr int kDots = 0;
+    static constexpr bool kSeeded = false;
+    static constexpr bool kTile = false;
+    const double *x, *b;
+    double *r;
+    __device__ double gx(int32_t j) const { return x[j]; }
+    __device__ double seed(int) const { return 0.0; }
+    __device__ void put(int o, double v, double *) const {
+        const double ro = b[o] + (-1.0) * v;
+        if constexpr (NT) st_stream(r + o, ro);
+        else r[o] = ro;
+    }
+};
+
 // V-cycle post-smoothing, one Richardson step with Jacobi from the guess t
 // (SpMV + k_richardson): x_i = t_i + 1.0 (dinv_i (b_i + (-1) (A t)_i)); x
 // must not alias t. With dot, the finest level also yields CG's z.z and z.b
@@ -873,6 +892,12 @@ hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *din
                          hipStream_t s, bool nt) {
     if (nt) return launch_stream_op(A, OpMgPre<true>{b, dinv, x, r}, nullptr, s);
     return launch_stream_op(A, OpMgPre<false>{b, dinv, x, r}, nullptr, s);
+}
+
+hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
+                           bool nt) {
+    if (nt) return launch_stream_op(A, OpMgResid<true>{x, b, r}, nullptr, s);
+    return launch_stream_op(A, OpMgResid<false>{x, b, r}, nullptr, s);
 }
 
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,

@@ -392,6 +392,13 @@ struct aijhip_ksp {
     // CG vector kernels store with the non-temporal hint; AIJHIP_VEC_NT=0/1
     // overrides (diagnostic A/B, read at KSPCreate).
     bool vec_nt = true;
+    // V-cycle pre-smoothing on fused levels: false = one launch gathering
+    // dinv_j * b_j (OpMgPre), true = x = D^-1 b pass + residual SpMV
+    // (OpMgResid). Measured at 300^3 (profiles/r01/mg_pre_split/): the split
+    // form solves in 0.205 s vs 0.221 s — the second gather per entry costs
+    // more (fine level 719 us) than writing and re-reading x (130 + 523 us).
+    // AIJHIP_MG_PRE_SPLIT=0/1 overrides (A/B).
+    bool mg_pre_split = true;
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
     double *d_hist = nullptr;
     int32_t hist_cap = 0;
@@ -568,7 +575,11 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
             hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));
             break;
         }
-        if (L.fused) {
+        if (L.fused && K->mg_pre_split) {
+            // smoothd as a vector pass, then r = b - A x in the SpMV epilogue
+            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));
+            if ((e = aijhip::launch_mg_resid(*L.A, X(l), B(l), L.r, s, K->vec_nt)) != hipSuccess) return e;
+        } else if (L.fused) {
             if ((e = aijhip::launch_mg_pre(*L.A, B(l), L.dinv, X(l), L.r, s, K->vec_nt)) != hipSuccess) return e;
         } else {
             hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));  // smoothd
@@ -610,6 +621,7 @@ int aijhip_ksp_create(aijhip_mat_t A, aijhip_ksp_t *out) {
     if (!K) return kfail(AIJHIP_ERR_ALLOC, "host allocation");
     K->A = A;
     if (const char *v = std::getenv("AIJHIP_VEC_NT")) K->vec_nt = std::atoi(v) != 0;
+    if (const char *v = std::getenv("AIJHIP_MG_PRE_SPLIT")) K->mg_pre_split = std::atoi(v) != 0;
     aijhip_gamg_params_default(&K->gamg);
     *out = K;
     return AIJHIP_OK;

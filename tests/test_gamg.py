@@ -109,6 +109,33 @@ def test_gpu_cg_gamg_matches_oracle(pkg, N, norm):
     A.destroy()
 
 
+@pytest.mark.gpu
+def test_gpu_vcycle_pre_smoothing_forms_bitwise(pkg, monkeypatch):
+    """The split pre-smoothing (x = D^-1 b pass + residual SpMV, default) and
+    the one-launch form (gathering dinv_j b_j) round identically: the whole
+    CG+GAMG solve is bit-for-bit the same."""
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available()
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    N = 24
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, _ = pkg.poisson_vectors(N)
+    b = torch.from_numpy(rhs).cuda()
+    out = []
+    monkeypatch.delenv("AIJHIP_MG_UNFUSED", raising=False)
+    for split in ("1", "0"):
+        monkeypatch.setenv("AIJHIP_MG_PRE_SPLIT", split)
+        with pkg.SeqAIJHIP(ai, aj, aa) as A:
+            x = torch.empty_like(b)
+            with K.KSPCG(A, pc="gamg", rtol=1e-14, atol=1e-12) as ksp:
+                ksp.solve(b, x)
+                out.append((ksp.its, np.array(ksp.history()), x.cpu().numpy()))
+    for its, h, xv in out[1:]:
+        assert its == out[0][0]
+        assert np.array_equal(h.view(np.uint64), out[0][1].view(np.uint64))
+        assert np.array_equal(xv.view(np.uint64), out[0][2].view(np.uint64))
+
+
 def test_oracle_vcycle_preconditions_cg():
     ai, aj, aa, rhs, exact = seqaij.create_system(10, 10, 10)
     m = len(ai) - 1
