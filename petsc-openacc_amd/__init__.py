@@ -18,7 +18,9 @@ from pathlib import Path
 import numpy as np
 
 _PKG = Path(__file__).resolve().parent
-LIB_PATH = _PKG / "lib" / "libaijhip.so"
+# AIJHIP_LIB names another build of the same library (A/B timing of two
+# builds in alternating processes, tools/build_ab.sh); default: the in-tree one
+LIB_PATH = Path(os.environ["AIJHIP_LIB"]) if os.environ.get("AIJHIP_LIB") else _PKG / "lib" / "libaijhip.so"
 
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}

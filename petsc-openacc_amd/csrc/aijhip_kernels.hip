@@ -76,16 +76,25 @@ __device__ __forceinline__ T ld_stream(const T *p) {
 //         issue no request; the compiler waits once per iteration;
 //  true:  branch-free loads, addresses clamped into the block (lanes past it
 //         re-read its last pair) — every load in flight at once.
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops,
+// not for its outstanding global loads (__syncthreads() would add
+// s_waitcnt vmcnt(0) and drain the prefetch; cdna_hip_programming.md §8).
+// The "memory" clobber keeps the compiler from moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Block-wide fp64 sum in a fixed order (wave __shfl_down tree, then the
-// waves' sums in wave order): deterministic run to run.
+// waves' sums in wave order): deterministic run to run. LDS-only barriers:
+// the row results just stored to global memory need not have landed.
 template <int T>
 __device__ __forceinline__ double block_sum(double v, double *scratch) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
     const int t = threadIdx.x;
-    __syncthreads();  // scratch may still be read by the caller's previous phase
+    lds_barrier();  // scratch may still be read by the caller's previous phase
     if ((t & 63) == 0) scratch[t >> 6] = v;
-    __syncthreads();
+    lds_barrier();
     double s = 0.0;
     if (t == 0) {
 #pragma unroll
@@ -209,10 +218,13 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     const double *__restrict__ aa, Op op, double *dpart, const int *stop, const int2 *__restrict__ xrange) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
-    if (stop && *stop) return;  // CG launched past convergence: no work
     const int bid = (int)blockIdx.x;
     const int b = XCD ? xcd_chunk_remap(bid, nblk, xchunk) : bid;
     const BlockDesc d = blk[b];
+    // CG launched past convergence: no work. The test also reads the
+    // descriptor (d.nk is never negative), so both scalar loads are issued
+    // before one wait instead of the descriptor load waiting for the branch.
+    if ((stop ? *stop : 0) != 0 || d.nk < 0) return;
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
 
@@ -328,14 +340,6 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             if (t == 0) dpart[(int64_t)q * nblk + b] = v;
         }
     }
-}
-
-// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops,
-// not for its outstanding global loads (__syncthreads() would add
-// s_waitcnt vmcnt(0) and drain the prefetch; cdna_hip_programming.md §8).
-// The "memory" clobber keeps the compiler from moving LDS accesses across it.
-__device__ __forceinline__ void lds_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
 // Persistent, software-pipelined STREAM: a resident grid walks the row blocks

@@ -88,6 +88,8 @@ def main():
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=p, clamped=0)))
     if args.variants in ("kernels", "all"):
         variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
+    if args.variants == "default":  # the product's defaults only
+        variants.append(("stream", {}))
     if args.variants == "xtile":
         for g, xt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
@@ -111,7 +113,7 @@ def main():
     def configure(kind, opts):
         A.set_kernel(kind, opts.get("lanes", 0))
         A.set_option("exact", opts.get("exact", 0))
-        A.set_option("x_tile", opts.get("x_tile", -1))
+        A.set_option("x_tile", opts.get("x_tile", -1 if opts else 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
         A.set_option("long_overlap", opts.get("long_overlap", 0))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
