@@ -93,6 +93,9 @@ def main():
     if args.variants == "xtile":
         for g, xt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
+    if args.variants == "xtile_big":  # larger blocks amortise the tile load over more entries
+        for g, xt in ((1, 0), (7, 0), (7, 1), (4, 0), (4, 1), (6, 1)):
+            variants.append(("stream", dict(geometry=g, x_tile=xt)))
     if args.variants == "longxcd":
         for g, lx, lo in itertools.product((1, 6), (0, 1), (0, 1)):
             variants.append(("stream", dict(geometry=g, long_xcd=lx, long_overlap=lo)))
