@@ -54,6 +54,15 @@ void aijhip_splitmix_uniform(int64_t n, uint64_t seed, int64_t offset, double *x
 int aijhip_skewed_csr(int32_t m, uint64_t seed, int64_t *nnz, int32_t *ai, int32_t *aj,
                       double *aa);
 
+/* Seeded FEM-structured CSR (the other Flan_1565 stand-in: Flan is a 3-D
+ * hexahedral mesh with 3 dofs per node): nodes on an nx x ny x nz grid in
+ * natural order, `dofs` unknowns per node numbered node*dofs + d, and every
+ * row coupling all dofs of the (up to) 27 neighbouring nodes, columns sorted;
+ * values uniform [-1, 1) from (seed, entry index). Interior rows hold
+ * 27*dofs entries. Pass ai/aj/aa = NULL to get nnz only. */
+int aijhip_fem_hex_csr(int32_t nx, int32_t ny, int32_t nz, int32_t dofs, uint64_t seed,
+                       int64_t *nnz, int32_t *ai, int32_t *aj, double *aa);
+
 /* Split local rows into PETSc MPIAIJ blocks: columns in [col_lo, col_hi) go to
  * the diagonal block (renumbered c - col_lo); the others to the off-diagonal
  * block, renumbered by position in garray (the sorted unique off-block global

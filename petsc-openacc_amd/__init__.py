@@ -39,7 +39,7 @@ ABI_SYMBOLS = (
 )
 HARNESS_SYMBOLS = (
     "aijhip_poisson_nnz", "aijhip_poisson_fill", "aijhip_poisson_vectors",
-    "aijhip_splitmix_uniform", "aijhip_skewed_csr", "aijhip_split_rows",
+    "aijhip_splitmix_uniform", "aijhip_skewed_csr", "aijhip_fem_hex_csr", "aijhip_split_rows",
     "aijhip_poisson_fill_device", "aijhip_poisson_vectors_device", "aijhip_mat_create_poisson",
 )
 
@@ -106,6 +106,7 @@ def lib() -> ctypes.CDLL:
         L.aijhip_poisson_vectors.argtypes = [ctypes.c_int32] * 5 + [ctypes.c_int, _P, _P]
         L.aijhip_splitmix_uniform.argtypes = [ctypes.c_int64, ctypes.c_uint64, ctypes.c_int64, _P]
         L.aijhip_skewed_csr.argtypes = [ctypes.c_int32, ctypes.c_uint64, _I64P, _P, _P, _P]
+        L.aijhip_fem_hex_csr.argtypes = [ctypes.c_int32] * 4 + [ctypes.c_uint64, _I64P, _P, _P, _P]
         L.aijhip_poisson_fill_device.argtypes = [ctypes.c_int32] * 5 + [ctypes.c_int, _P, _P, _P, _F64P, _P]
         L.aijhip_poisson_vectors_device.argtypes = [ctypes.c_int32] * 5 + [ctypes.c_int, _P, _P, _P]
         L.aijhip_mat_create_poisson.argtypes = [ctypes.c_int] + [ctypes.c_int32] * 5 + [ctypes.c_int, _F64P,
@@ -342,6 +343,25 @@ def skewed_csr(m: int = FLAN_1565_ROWS, seed: int = 1565):
     aa = np.empty(nnz.value, np.float64)
     _check_h(L.aijhip_skewed_csr(m, seed, ctypes.byref(nnz), ai.ctypes.data, aj.ctypes.data, aa.ctypes.data),
              "skewed_csr")
+    return ai, aj, aa
+
+
+FLAN_HEX_GRID = (81, 80, 80)  # 518,400 nodes x 3 dofs = 1,555,200 rows (Flan_1565: 1,564,794)
+
+
+def fem_hex_csr(nx: int = FLAN_HEX_GRID[0], ny: int = FLAN_HEX_GRID[1], nz: int = FLAN_HEX_GRID[2],
+                dofs: int = 3, seed: int = 1565):
+    """Seeded FEM-structured CSR standing in for Flan_1565's mesh structure
+    (3-D hexahedral, 3 dofs per node, 27-node coupling)."""
+    L = lib()
+    nnz = ctypes.c_int64()
+    _check_h(L.aijhip_fem_hex_csr(nx, ny, nz, dofs, seed, ctypes.byref(nnz), None, None, None), "fem_hex_csr")
+    m = nx * ny * nz * dofs
+    ai = np.empty(m + 1, np.int32)
+    aj = np.empty(nnz.value, np.int32)
+    aa = np.empty(nnz.value, np.float64)
+    _check_h(L.aijhip_fem_hex_csr(nx, ny, nz, dofs, seed, ctypes.byref(nnz), ai.ctypes.data, aj.ctypes.data,
+                                  aa.ctypes.data), "fem_hex_csr")
     return ai, aj, aa
 
 

@@ -193,6 +193,44 @@ int aijhip_skewed_csr(int32_t m, uint64_t seed, int64_t *nnz, int32_t *ai, int32
     return AIJHIP_OK;
 }
 
+int aijhip_fem_hex_csr(int32_t nx, int32_t ny, int32_t nz, int32_t dofs, uint64_t seed, int64_t *nnz,
+                       int32_t *ai, int32_t *aj, double *aa) {
+    if (nx < 1 || ny < 1 || nz < 1 || dofs < 1 || !nnz) return AIJHIP_ERR_ARG;
+    // couplings per axis: 3 neighbours inside, 2 at a face (1 on a 1-wide axis)
+    auto pairs = [](int64_t n) { return n == 1 ? (int64_t)1 : 3 * n - 2; };
+    const int64_t nodes = (int64_t)nx * ny * nz, m = nodes * dofs;
+    const int64_t total = pairs(nx) * pairs(ny) * pairs(nz) * dofs * dofs;
+    if (m > INT32_MAX || total > INT32_MAX) return AIJHIP_ERR_ARG;
+    *nnz = total;
+    if (!ai) return AIJHIP_OK;
+    if (!aj || !aa) return AIJHIP_ERR_ARG;
+    int64_t p = 0, r = 0;
+    ai[0] = 0;
+    for (int32_t k = 0; k < nz; ++k)
+        for (int32_t j = 0; j < ny; ++j)
+            for (int32_t i = 0; i < nx; ++i)
+                for (int32_t d = 0; d < dofs; ++d) {
+                    // the 27 neighbouring nodes in ascending node order, all
+                    // their dofs: the row's columns come out sorted
+                    for (int32_t dk = -1; dk <= 1; ++dk) {
+                        if (k + dk < 0 || k + dk >= nz) continue;
+                        for (int32_t dj = -1; dj <= 1; ++dj) {
+                            if (j + dj < 0 || j + dj >= ny) continue;
+                            for (int32_t di = -1; di <= 1; ++di) {
+                                if (i + di < 0 || i + di >= nx) continue;
+                                const int64_t node = (i + di) + (int64_t)nx * ((j + dj) + (int64_t)ny * (k + dk));
+                                for (int32_t e = 0; e < dofs; ++e, ++p) {
+                                    aj[p] = (int32_t)(node * dofs + e);
+                                    aa[p] = 2.0 * unit(rnd(seed, 5, (uint64_t)p)) - 1.0;
+                                }
+                            }
+                        }
+                    }
+                    ai[++r] = (int32_t)p;
+                }
+    return AIJHIP_OK;
+}
+
 int aijhip_split_rows(int32_t m, const int32_t *ai, const int32_t *aj, const double *aa,
                       int32_t col_lo, int32_t col_hi, int64_t *nz_d, int64_t *nz_o,
                       int32_t *n_garray, int32_t *d_ai, int32_t *d_aj, double *d_aa,

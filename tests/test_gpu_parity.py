@@ -394,3 +394,16 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
                     assert_bits(y, first, short)
                     assert_bits(y, g["y"], short)
                     check(y, g["y"], ai, aj, aa, g["x"], exact=False)
+
+
+def test_fem_hex_flan_standin_all_kernels(pkg, dev, coracle):
+    """Flan_1565's mesh structure (BASELINE configs[4]; hexahedral, 3 dofs per
+    node, 81-entry interior rows) at a reduced grid: STREAM and SCALAR keep
+    PETSc's order (rows fit one block), the others meet the fp64 bound."""
+    ai, aj, aa = pkg.fem_hex_csr(21, 20, 19)
+    assert np.diff(ai).max() == 81
+    x = pkg.splitmix_uniform(len(ai) - 1, 11)
+    ref = coracle.matmult(ai, aj, aa, x, omp=True)
+    for kernel in ALL_KERNELS:
+        y, _ = mult(pkg, dev, ai, aj, aa, len(ai) - 1, x, kernel)
+        check(y, ref, ai, aj, aa, x, exact=kernel in BITEXACT)

@@ -1,5 +1,7 @@
 """Host-side operand producers (CPU): the C++ restatement of helper.cpp used
 by the benchmark must equal the numpy oracle bit for bit."""
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -79,3 +81,42 @@ def test_split_rows_is_mpiaij_split(pkg):
     y_d = seqaij.matmult(dai, daj, daa, x[lo:hi])
     y = seqaij.matmult_add(oai, oaj, oaa, x[garray], y_d)
     np.testing.assert_allclose(y, y_ref, rtol=1e-14, atol=1e-10)
+
+
+def _fem_hex_reference(nx, ny, nz, dofs, seed):
+    """Loop restatement of aijhip_fem_hex_csr (include/aijhip_harness.h)."""
+    ai, aj = [0], []
+    for k in range(nz):
+        for j in range(ny):
+            for i in range(nx):
+                for _ in range(dofs):
+                    for dk in (-1, 0, 1):
+                        for dj in (-1, 0, 1):
+                            for di in (-1, 0, 1):
+                                a, b, c = i + di, j + dj, k + dk
+                                if 0 <= a < nx and 0 <= b < ny and 0 <= c < nz:
+                                    node = a + nx * (b + ny * c)
+                                    aj.extend(node * dofs + e for e in range(dofs))
+                    ai.append(len(aj))
+    # entry p's value is rnd(seed, 5, p) = splitmix(seed + 5 * 0xD1B54A32D192ED03, p)
+    aa = seqaij.splitmix_uniform(len(aj), (seed + 5 * 0xD1B54A32D192ED03) % (1 << 64), 0)
+    return np.array(ai, np.int32), np.array(aj, np.int32), aa
+
+
+@pytest.mark.parametrize("dims", [(4, 3, 5, 3), (1, 2, 3, 2), (3, 3, 3, 1)])
+def test_fem_hex_csr_matches_loop_restatement(pkg, dims):
+    ai, aj, aa = pkg.fem_hex_csr(*dims, seed=1565)
+    ri, rj, ra = _fem_hex_reference(*dims, seed=1565)
+    assert np.array_equal(ai, ri) and np.array_equal(aj, rj)
+    assert np.array_equal(aa.view(np.uint64), ra.view(np.uint64))
+
+
+def test_fem_hex_csr_flan_shape(pkg):
+    nx, ny, nz = pkg.FLAN_HEX_GRID
+    L = pkg.lib()
+    nnz = ctypes.c_int64()
+    assert L.aijhip_fem_hex_csr(nx, ny, nz, 3, 1565, ctypes.byref(nnz), None, None, None) == 0
+    m = nx * ny * nz * 3
+    assert abs(m - pkg.FLAN_1565_ROWS) / pkg.FLAN_1565_ROWS < 0.01
+    assert nnz.value == 9 * (3 * nx - 2) * (3 * ny - 2) * (3 * nz - 2)
+    assert 70 < nnz.value / m <= 81  # Flan_1565: 114.2 M / 1.565 M = 73 per row

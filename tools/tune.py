@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--variants", default="stream")
-    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx"])
+    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx", "fem_hex"])
     ap.add_argument("--file", default=None, help="a MatrixMarket (.mtx) or PETSc binary operand, e.g. Flan_1565.mtx")
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
@@ -55,6 +55,8 @@ def main():
             raise SystemExit("tune.py times square operands (x and y share a length)")
     elif args.matrix == "poisson":
         ai, aj, aa = pkg.poisson_csr(args.grid)
+    elif args.matrix == "fem_hex":  # Flan_1565's structure: hexahedral mesh, 3 dofs per node
+        ai, aj, aa = pkg.fem_hex_csr()
     else:
         ai, aj, aa = pkg.skewed_csr()
         if args.matrix in ("skewed_nohub", "skewed_localx"):  # the FEM-like rows only (hub rows emptied)
