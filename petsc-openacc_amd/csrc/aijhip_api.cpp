@@ -271,11 +271,20 @@ int plan_build(aijhip_mat *A) {
     P.kernel = kernel;
     P.tune = A->requested_tune;
     if (P.tune.geom < 0) {
-        // measured: 512 x 4094-entry blocks for short rows (7-pt Poisson,
-        // profiles/r01/tune04), 512 x 4096 / 512 rows for long rows (Flan
-        // stand-in, profiles/r01/skew2)
+        // measured: 512 x 4094-entry blocks (geometry 6, 8 waves/SIMD) for
+        // short rows (7-pt Poisson, profiles/r01/tune04) and for long rows
+        // whose gathers run along x lines (FEM-structured stand-in: 283 vs
+        // 313 us); 512 x 4096 (geometry 1: 76 VGPRs, 6 waves/SIMD) for long
+        // rows with scattered gathers (skewed stand-in 405 vs 449 us, GAMG's
+        // coarse operators) — profiles/r01/rowsum/
         const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
-        P.tune.geom = (nr > 0 && A->nz > (int64_t)16 * nr) ? 1 : 6;
+        P.tune.geom = 6;
+        if (nr > 0 && A->nz > (int64_t)16 * nr) {
+            double lpe = 1.0;
+            const hipError_t e = aijhip::gather_lines_per_entry(*A, &lpe);
+            if (e != hipSuccess) return hipfail(e, "plan: gather locality");
+            if (lpe > aijhip::kScatteredLinesPerEntry) P.tune.geom = 1;
+        }
     }
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM:

@@ -85,7 +85,7 @@ struct RowList {
 // (XCD-contiguous runs were 5-10 % slower), plain loads (non-temporal 2-3 %
 // slower), non-persistent grid (the pipelined persistent form was 7 % slower).
 struct Tuning {
-    int geom = -1;       // index into kStreamGeoms; -1 = by row statistics (6 or 1)
+    int geom = -1;       // index into kStreamGeoms; -1 = by row length and gather locality (6 or 1)
     bool xcd = false;    // XCD-aware block remap
     int xchunk = 0;      //   chunk of the chunked remap (0 = contiguous runs)
     bool nt = false;     // non-temporal matrix loads
@@ -104,6 +104,16 @@ struct Tuning {
 // is as fast or faster up to ~100 entries per row, several lanes win from
 // ~200 (row length 384: 346 vs 619 us).
 constexpr int kSplitMinMean = 128;
+// One-lane-per-row blocks whose mean row length exceeds this read their LDS
+// products eight at a time ahead of the sequential adds (row_sum_seq; same
+// order, same bits). Measured (profiles/r01/rowsum/): FEM-structured stand-in
+// 310 -> 280 us at geometry 6, skewed stand-in 429 -> 405 us at geometry 1.
+constexpr int kBatchMinMean = 16;
+// Automatic geometry for long rows (mean > 16): above this many distinct x
+// lines per entry the gathers count as scattered (geometry 1), below it they
+// run along lines (geometry 6). Measured: 7-pt 0.73, GAMG coarse operators
+// 0.51-0.68, skewed stand-in 0.40, FEM-structured stand-in 0.17.
+constexpr double kScatteredLinesPerEntry = 0.25;
 
 struct Plan {
     int kernel = AIJHIP_KERNEL_STREAM;
@@ -216,6 +226,9 @@ RowList row_list(const aijhip_mat &A);
 hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out);
 // Per STREAM block: min column and span (max - min + 1) of its entries.
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out);
+// Distinct 128-B x lines per entry over a row sample (at most 65536 rows):
+// ~0.7 for the 7-point stencil, ~0.17 for a 3-dof hexahedral FEM operator.
+hipError_t gather_lines_per_entry(const aijhip_mat &A, double *out);
 // Install A^T (device arrays, freed by the call) as A's transpose handle.
 int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa);
 // Number of device column indices outside [0, n) (synchronous).

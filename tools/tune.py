@@ -92,6 +92,8 @@ def main():
         variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
     if args.variants == "default":  # the product's defaults only
         variants.append(("stream", {}))
+    if args.variants == "rowsum":  # default plus the small geometries (medium-length rows)
+        variants += [("stream", {})] + [("stream", dict(geometry=g, x_tile=xt)) for g in (0, 1, 6, 8) for xt in (0, -1)]
     if args.variants == "xtile":
         for g, xt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
@@ -117,6 +119,7 @@ def main():
 
     def configure(kind, opts):
         A.set_kernel(kind, opts.get("lanes", 0))
+        A.set_option("geometry", opts.get("geometry", -1))  # -1: the library's choice
         A.set_option("exact", opts.get("exact", 0))
         A.set_option("x_tile", opts.get("x_tile", -1 if opts else 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
@@ -149,7 +152,10 @@ def main():
                     ref_y = yy
                 same = bool(np.array_equal(yy.view(np.uint64), ref_y.view(np.uint64)))
                 maxdiff = float(np.max(np.abs(yy - ref_y)))
-                print(json.dumps({"variant": key, "bitwise_equal_first": same, "max_abs_diff": maxdiff}), flush=True)
+                inf = A.info()
+                print(json.dumps({"variant": key, "bitwise_equal_first": same, "max_abs_diff": maxdiff,
+                                  "geometry": inf["stream_geometry"], "x_tiled_blocks": inf["x_tiled_blocks"],
+                                  "n_blocks": inf["n_blocks"]}), flush=True)
         for name, (fn, nb) in refs.items():
             time_launches(fn, 2, stream)
             results[name].append(float(np.median(time_launches(fn, args.launches, stream))))
