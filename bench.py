@@ -66,6 +66,9 @@ def parse():
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
                         "(launch with torch.distributed.run): a one-GPU rehearsal of the N > 1 run")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="N > 1 control-flow rehearsal on a one-GPU box: every rank on cuda:0 over gloo "
+                        "(RCCL refuses two ranks on one device); timings are not scaling numbers")
     return p.parse_args()
 
 
@@ -253,6 +256,8 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the HIP path has no CPU fallback)")
+    if args.rehearse_one_gpu:
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     distributed = world > 1 or args.mpi
@@ -265,7 +270,10 @@ def main():
         return mat
 
     if distributed:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     G = args.grid
     nx, ny, nz_global = weak_grid(G, world) if distributed else (G, G, G)
@@ -384,7 +392,7 @@ def main():
         dt = float(el.item())
         return {"iters": cgm.its, "seconds": round(dt, 4), "iters_per_s": round(cgm.its / dt, 2),
                 "ms_per_iter": round(dt / cgm.its * 1e3, 4), "pc": "jacobi (bjacobi+jacobi per rank)",
-                "reductions": "2 all-reduces per iteration (RCCL)", "halo": args.halo,
+                "reductions": f"2 all-reduces per iteration ({'gloo' if args.rehearse_one_gpu else 'RCCL'})", "halo": args.halo,
                 "workload": f"{nx}x{ny}x{nz_global} Poisson, {planes}-plane z-slab per GPU"}
 
     def single_cg_gamg():
@@ -450,6 +458,8 @@ def main():
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
+        if args.rehearse_one_gpu:
+            out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
         if strong is not None:
             out["strong_300"] = strong
         if cg is not None:
