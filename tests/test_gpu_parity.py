@@ -407,3 +407,12 @@ def test_fem_hex_flan_standin_all_kernels(pkg, dev, coracle):
     for kernel in ALL_KERNELS:
         y, _ = mult(pkg, dev, ai, aj, aa, len(ai) - 1, x, kernel)
         check(y, ref, ai, aj, aa, x, exact=kernel in BITEXACT)
+
+
+def test_auto_geometry_follows_gather_locality(pkg, dev):
+    """Automatic STREAM geometry (aijhip_api.cpp plan_build): short rows and
+    long rows gathered along x lines -> 6; long scattered rows -> 1."""
+    cases = [(pkg.poisson_csr(12), 6), (pkg.fem_hex_csr(21, 20, 19), 6), (pkg.skewed_csr(300000, seed=1565), 1)]
+    for (ai, aj, aa), geom in cases:
+        with pkg.SeqAIJHIP(ai, aj, aa) as A:
+            assert A.info()["stream_geometry"] == geom
