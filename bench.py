@@ -240,6 +240,7 @@ def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args):
     return {"workload": f"{G}^3 Poisson CSR row-partitioned over {world} GPUs "
                         f"({z1 - z0} of {G} z-planes on rank {rank})",
             "scaling": "strong", "value": round(nbytes / dt / 1e9, 2), "unit": "GB/s",
+            "roofline_frac": round(nbytes / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
             "ms_per_step": round(dt * 1e3, 4), "rows": G ** 3, "nnz": nnz, "halo": args.halo}
 
 
@@ -458,6 +459,8 @@ def main():
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
+        if distributed:  # whole-job rate against N HBM peaks (roofline.frac is rank 0's kernel alone)
+            out["aggregate_roofline_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
         if args.rehearse_one_gpu:
             out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
         if strong is not None:
