@@ -219,16 +219,18 @@ __device__ __forceinline__ void vst(double *p, double v) {
     else *p = v;
 }
 
+// x == nullptr: X += a P is applied in k_update instead (x_in_update).
 template <bool NT>
 __global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *__restrict__ z, double *p,
                                                       double *x, const CGState *S) {
     if (S->done) return;
-    const bool first = S->i == 0;
+    const bool first = S->i == 0 || x == nullptr;
     const double bb = S->b, a = S->a;
+    const bool p_first = S->i == 0;
     GRID_STRIDE(i, n) {
         const double pi = p[i];
         if (!first) vst<NT>(x + i, x[i] + a * pi);
-        vst<NT>(p + i, first ? z[i] : z[i] + bb * pi);
+        vst<NT>(p + i, p_first ? z[i] : z[i] + bb * pi);
     }
 }
 
@@ -279,12 +281,14 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_dpi(const double *part, 
 template <bool NT>
 __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, double *wz,
                                                         const double *__restrict__ dinv, double *part,
-                                                        const CGState *S, int pc) {
+                                                        const CGState *S, int pc,
+                                                        const double *__restrict__ p, double *x) {
     __shared__ double scratch[kVecThreads / 64];
     if (S->done) return;
-    const double na = -S->a;
+    const double a = S->a, na = -S->a;
     double zz = 0.0, zr = 0.0, rr = 0.0;
     GRID_STRIDE(i, n) {
+        if (x) vst<NT>(x + i, x[i] + a * p[i]);  // VecAXPY(X, a, P) (x_in_update)
         const double ri = r[i] + na * wz[i];  // VecAXPY(R, -a, W)
         vst<NT>(r + i, ri);
         rr += ri * ri;
@@ -399,6 +403,12 @@ struct aijhip_ksp {
     // more (fine level 719 us) than writing and re-reading x (130 + 523 us).
     // AIJHIP_MG_PRE_SPLIT=0/1 overrides (A/B).
     bool mg_pre_split = true;
+    // X += a P in the r/z update after the SpMV (PETSc's place) instead of
+    // deferred into the next p = z + b p pass: same bytes, but the kernel
+    // before each SpMV leaves only p dirty. AIJHIP_CG_X_IN_UPDATE=0/1 (A/B).
+    // Measured (profiles/r01/x_in_update/, 3 alternating rounds): CG+Jacobi
+    // 400 its 0.376 -> 0.392 s, CG+GAMG 0.205 -> 0.207 s, hence off.
+    bool x_in_update = false;
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
     double *d_hist = nullptr;
     int32_t hist_cap = 0;
@@ -622,6 +632,7 @@ int aijhip_ksp_create(aijhip_mat_t A, aijhip_ksp_t *out) {
     K->A = A;
     if (const char *v = std::getenv("AIJHIP_VEC_NT")) K->vec_nt = std::atoi(v) != 0;
     if (const char *v = std::getenv("AIJHIP_MG_PRE_SPLIT")) K->mg_pre_split = std::atoi(v) != 0;
+    if (const char *v = std::getenv("AIJHIP_CG_X_IN_UPDATE")) K->x_in_update = std::atoi(v) != 0;
     aijhip_gamg_params_default(&K->gamg);
     *out = K;
     return AIJHIP_OK;
@@ -765,8 +776,9 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             return khip(e, "KSPSolve poll");
         if (K->h_state->done || launched >= K->max_it) break;
         for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched) {
-            if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
-            else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
+            double *xa = K->x_in_update ? nullptr : x, *xu = K->x_in_update ? x : nullptr;
+            if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, xa, K->d_state);
+            else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, xa, K->d_state);
             if (K->fused) {
                 e = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, s);
                 if (e == hipSuccess)
@@ -778,10 +790,10 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             }
             if (K->vec_nt)
                 hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
-                                   K->d_state, K->pc);
+                                   K->d_state, K->pc, K->d_p, xu);
             else
                 hipLaunchKernelGGL(k_update<false>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
-                                   K->d_state, K->pc);
+                                   K->d_state, K->pc, K->d_p, xu);
             const double *pz = K->d_part;
             int nbz = nb;
             if (gamg && e == hipSuccess) {
@@ -801,7 +813,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve iteration");
         }
     }
-    hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
+    if (!K->x_in_update) hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
     if ((e = hipGetLastError()) != hipSuccess ||
         (e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)
