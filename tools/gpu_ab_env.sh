@@ -14,6 +14,6 @@ for r in $(seq 1 "$R"); do
     v=$VA; [[ $side == B ]] && v=$VB
     env "$VAR=$v" timeout -k 10 120 python -u tools/prof_case.py jacobi --its 400 > "$OUT/jac_${side}_$r.log" 2>&1 || exit 1
     env "$VAR=$v" timeout -k 10 200 python -u tools/prof_case.py gamg > "$OUT/gamg_${side}_$r.log" 2>&1 || exit 1
-    echo "$side ($VAR=$v) r$r $(grep -h 'jacobi:' "$OUT/jac_${side}_$r.log" | cut -d, -f2) | $(grep -h 'gamg: set-up' "$OUT/gamg_${side}_$r.log" | cut -d, -f2,3)"
+    echo "$side ($VAR=$v) r$r $(grep -h 'jacobi:' "$OUT/jac_${side}_$r.log" | cut -d, -f2) | $(grep -h 'gamg: set-up' "$OUT/gamg_${side}_$r.log" | cut -d, -f1,2)"
   done
 done
