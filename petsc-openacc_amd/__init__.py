@@ -18,9 +18,17 @@ from pathlib import Path
 import numpy as np
 
 _PKG = Path(__file__).resolve().parent
-# AIJHIP_LIB names another build of the same library (A/B timing of two
-# builds in alternating processes, tools/build_ab.sh); default: the in-tree one
-LIB_PATH = Path(os.environ["AIJHIP_LIB"]) if os.environ.get("AIJHIP_LIB") else _PKG / "lib" / "libaijhip.so"
+LIB_PATH = _PKG / "lib" / "libaijhip.so"
+# A/B timing of two builds in alternating processes (tools/build_ab.sh) may
+# name another build of the same library, but only with AIJHIP_AB=1 set too,
+# and the process says so on stderr: nothing loads a foreign build silently.
+if os.environ.get("AIJHIP_LIB"):
+    if os.environ.get("AIJHIP_AB") != "1":
+        raise RuntimeError("AIJHIP_LIB is set without AIJHIP_AB=1: refusing to load a build other than "
+                           f"{LIB_PATH}")
+    LIB_PATH = Path(os.environ["AIJHIP_LIB"]).resolve()
+    import sys as _sys
+    print(f"[aijhip] A/B run: loading {LIB_PATH}", file=_sys.stderr)
 
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}

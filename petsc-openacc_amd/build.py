@@ -35,11 +35,30 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the HIP path cannot be built")
 
 
-def _stale(target: Path, deps) -> bool:
-    if not target.exists():
+def _digest(deps, extra=()) -> str:
+    """sha256 over the sources (names and contents) and the compile lines."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in sorted(Path(p) for p in deps):
+        h.update(d.name.encode() + b"\0" + d.read_bytes() + b"\0")
+    for e in extra:
+        h.update(str(e).encode() + b"\0")
+    return h.hexdigest()
+
+
+def _stale(target: Path, deps, extra=()) -> bool:
+    """A target is stale unless the digest recorded beside it when it was built
+    equals the digest of its sources now. Content, not mtime: a snapshot copied
+    to another machine keeps its prebuilt library only if it was built from
+    exactly these sources and flags."""
+    stamp = target.with_name(target.name + ".sha256")
+    if not target.exists() or not stamp.exists():
         return True
-    t = target.stat().st_mtime
-    return any(Path(d).stat().st_mtime > t for d in deps)
+    return stamp.read_text().strip() != _digest(deps, extra)
+
+
+def _stamp(target: Path, deps, extra=()) -> None:
+    target.with_name(target.name + ".sha256").write_text(_digest(deps, extra) + "\n")
 
 
 def _run(cmd):
@@ -52,12 +71,13 @@ def build_lib(force: bool = False) -> Path:
     LIBDIR.mkdir(exist_ok=True)
     srcs = [CSRC / s for s in HIP_SOURCES + HOST_SOURCES if (CSRC / s).exists()]
     deps = srcs + list(CSRC.glob("*.h")) + list((ROOT / "include").glob("*.h"))
-    if not force and not _stale(LIB, deps):
+    common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"-I{ROOT / 'include'}", f"-I{CSRC}"]
+    flags = (ARCH, *common)
+    if not force and not _stale(LIB, deps, flags):
         return LIB
     objdir = PKG / "build"
     objdir.mkdir(exist_ok=True)
     hipcc = _hipcc()
-    common = ["-O3", "-fPIC", "-std=c++17", "-ffp-contract=off", f"-I{ROOT / 'include'}", f"-I{CSRC}"]
     objs, jobs = [], []
     for s in srcs:
         o = objdir / (s.stem + ".o")
@@ -65,17 +85,25 @@ def build_lib(force: bool = False) -> Path:
             cmd = ["g++", *common, "-fopenmp", "-c", str(s), "-o", str(o)]
         else:
             cmd = [hipcc, "-x", "hip", f"--offload-arch={ARCH}", *common, "-c", str(s), "-o", str(o)]
-        if force or _stale(o, [s, *CSRC.glob("*.h"), *(ROOT / "include").glob("*.h")]):
-            jobs.append(cmd)
+        odeps = [s, *CSRC.glob("*.h"), *(ROOT / "include").glob("*.h")]
+        if force or _stale(o, odeps, cmd):
+            jobs.append((cmd, o, odeps))
         objs.append(str(o))
+
+    def _compile(job):
+        cmd, o, odeps = job
+        _run(cmd)
+        _stamp(o, odeps, cmd)
+
     # translation units compile in parallel (at most 8 at once)
     from concurrent.futures import ThreadPoolExecutor
     with ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
-        list(ex.map(_run, jobs))
+        list(ex.map(_compile, jobs))
     tmp = LIB.with_suffix(".so.tmp")
     _run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs, "-lgomp",
           "-L/opt/rocm/lib", "-lrocprofiler-sdk-roctx", "-Wl,-rpath,/opt/rocm/lib"])
     os.replace(tmp, LIB)
+    _stamp(LIB, deps, flags)
     return LIB
 
 
@@ -86,13 +114,15 @@ def build_main_ksp(force: bool = False) -> Path:
     """The main_ksp.cpp-equivalent driver, linked against libaijhip.so."""
     lib = build_lib(force)
     src = CSRC / "main_ksp.cpp"
-    if not force and not _stale(MAIN_KSP, [src, lib, *(ROOT / "include").glob("*.h")]):
+    mdeps = [src, lib.with_name(lib.name + ".sha256"), *(ROOT / "include").glob("*.h")]
+    if not force and not _stale(MAIN_KSP, mdeps, (ARCH,)):
         return MAIN_KSP
     MAIN_KSP.parent.mkdir(exist_ok=True)
     tmp = MAIN_KSP.with_suffix(".tmp")
     _run([_hipcc(), "-x", "hip", f"--offload-arch={ARCH}", "-O2", "-std=c++17", f"-I{ROOT / 'include'}",
           str(src), "-o", str(tmp), f"-L{LIBDIR}", "-laijhip", "-Wl,-rpath,$ORIGIN/../lib"])
     os.replace(tmp, MAIN_KSP)
+    _stamp(MAIN_KSP, mdeps, (ARCH,))
     return MAIN_KSP
 
 
@@ -105,6 +135,7 @@ def build_oracle(force: bool = False) -> Path:
     # x86 build has no FMA at -march=x86-64 either).
     _run(["gcc", "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-o", str(tmp), str(src)])
     os.replace(tmp, ORACLE_LIB)
+    _stamp(ORACLE_LIB, [src])
     return ORACLE_LIB
 
 

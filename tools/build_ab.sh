@@ -1,13 +1,13 @@
 #!/bin/bash
-# Build scratch/ab/<tag>/libaijhip.so from the working tree with ONE source
+# Build ablibs/<tag>/libaijhip.so from the working tree with ONE source
 # file taken from a git revision (default HEAD), for A/B timing of two builds
-# in alternating processes: AIJHIP_LIB=scratch/ab/<tag>/libaijhip.so python ...
+# in alternating processes: AIJHIP_LIB=ablibs/<tag>/libaijhip.so python ...
 #   usage: tools/build_ab.sh TAG FILE [REV]     (FILE relative to csrc/)
 set -euo pipefail
 TAG=$1; FILE=$2; REV=${3:-HEAD}
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CSRC=$ROOT/petsc-openacc_amd/csrc
-OUT=$ROOT/scratch/ab/$TAG
+OUT=$ROOT/ablibs/$TAG
 mkdir -p "$OUT"
 python3 -c "import sys; sys.path.insert(0, '$ROOT'); import importlib; importlib.import_module('petsc-openacc_amd.build').build_lib()"
 git -C "$ROOT" show "$REV:petsc-openacc_amd/csrc/$FILE" > "$OUT/$FILE"

@@ -1,12 +1,12 @@
 #!/bin/bash
-# Build scratch/ab/<tag>/libaijhip.so from the working tree with ONE source
+# Build ablibs/<tag>/libaijhip.so from the working tree with ONE source
 # file replaced by a given variant file (A/B of an edit not yet committed).
 #   usage: tools/build_variant.sh TAG FILE VARIANT_PATH     (FILE relative to csrc/)
 set -euo pipefail
 TAG=$1; FILE=$2; SRC=$3
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 CSRC=$ROOT/petsc-openacc_amd/csrc
-OUT=$ROOT/scratch/ab/$TAG
+OUT=$ROOT/ablibs/$TAG
 mkdir -p "$OUT"
 python3 -c "import sys; sys.path.insert(0, '$ROOT'); import importlib; importlib.import_module('petsc-openacc_amd.build').build_lib()"
 cp "$SRC" "$OUT/$FILE"

@@ -14,7 +14,7 @@ for r in $(seq 1 "$R"); do
     for side in A B; do
       lib=$LA; [[ $side == B ]] && lib=$LB
       f="$OUT/${mat}_${side}_$r.jsonl"
-      AIJHIP_LIB=$lib timeout -k 10 240 python -u tools/tune.py --matrix "$mat" --variants "$V" --rounds 3 > "$f" 2>&1 \
+      AIJHIP_AB=1 AIJHIP_LIB=$lib timeout -k 10 240 python -u tools/tune.py --matrix "$mat" --variants "$V" --rounds 3 > "$f" 2>&1 \
         || { tail -20 "$f"; exit 1; }
       echo "$mat $side r$r: $(python3 tools/tune_summary.py "$f")"
       grep -h '"bitwise_equal_first": false' "$f" | head -3
