@@ -92,6 +92,15 @@ int aijhip_ksp_get_pc_levels(aijhip_ksp_t ksp, int32_t *nlevels, int32_t *rows, 
  * introspection): sizes into m, n, nnz; with ai == NULL only the sizes. */
 int aijhip_ksp_get_pc_level(aijhip_ksp_t ksp, int32_t l, char which, int32_t *m, int32_t *n,
                             int64_t *nnz, int32_t *ai, int32_t *aj, double *aa);
+/* How the GAMG set-up built each coarsening l -> l+1 (up to cap entries,
+ * one per level but the coarsest): path[l] = 1 on the device
+ * (aijhip_gamg build_device), 0 on the host builder; product_cols[l] = the
+ * widest accumulator the device Galerkin products needed (0 = the wavefront
+ * form, else 64 / 128 / 256 LDS columns per row; -1 on the host).
+ * *host_fallback = 1 when a level the device would have built went to the
+ * host because a product row exceeded 256 distinct columns. */
+int aijhip_ksp_get_gamg_setup_path(aijhip_ksp_t ksp, int32_t cap, int32_t *path, int32_t *product_cols,
+                                   int32_t *host_fallback);
 int aijhip_ksp_destroy(aijhip_ksp_t ksp);
 
 #ifdef __cplusplus

@@ -14,6 +14,9 @@ struct DeviceLevel {
     aijhip_mat *A = nullptr;  // level operator (level 0: the caller's, borrowed)
     aijhip_mat *P = nullptr;  // prolongator to the next level, P^T attached
     double emax = 0.0;
+    // the widest accumulator class the Galerkin products building P and
+    // A_{l+1} needed: 0 = wavefront form, else 64 / 128 / 256 LDS columns
+    int product_cols = 0;
 };
 
 // Device set-up: levels are built on the device while the level has at least
@@ -22,8 +25,10 @@ struct DeviceLevel {
 // (levels[0].A = A0). *more is true when the hierarchy continues below the
 // last level (too small for the device, or a Galerkin row beyond the device
 // accumulators): B is then that level's near-null space for build_host_nns.
+// *overflow is true when that hand-over happened at a level the device
+// would otherwise have built (a product row past every device class).
 int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<DeviceLevel> &levels,
-                 std::vector<double> &B, bool *more);
+                 std::vector<double> &B, bool *more, bool *overflow = nullptr);
 
 void free_device_levels(std::vector<DeviceLevel> &levels);
 

@@ -640,7 +640,7 @@ hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, bool redo, i
     return hipGetLastError();
 }
 
-int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu) {
+int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nullptr) {
     C = DCsr();
     C.m = A.m;
     C.n = B.n;
@@ -691,7 +691,7 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu) {
                                A.aa, B.ai, B.aj, B.aa, C.ai, C.aj, C.aa, nullptr);
             hipFree(cnt);
             if ((e = hipGetLastError()) != hipSuccess) { C.release(); return herr(e, "numeric product"); }
-            return AIJHIP_OK;
+            return AIJHIP_OK;  // the wavefront form: *cols_used stays as it was
         }
     }
     // one lane per row, the row's distinct columns in LDS: capacity classes
@@ -744,6 +744,7 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu) {
     if (e == hipSuccess && level >= 2) e = rowprod_pass<256, 16>(A, B, cnt, false, 128, 256, C.ai, &C, true, n_cu);
     hipFree(cnt);
     if (e != hipSuccess) { C.release(); return herr(e, "numeric product"); }
+    if (cols_used) *cols_used = std::max(*cols_used, 64 << level);
     return AIJHIP_OK;
 }
 
@@ -947,9 +948,10 @@ void free_device_levels(std::vector<DeviceLevel> &levels) {
 }
 
 int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<DeviceLevel> &levels,
-                 std::vector<double> &B, bool *more) {
+                 std::vector<double> &B, bool *more, bool *overflow) {
     levels.clear();
     *more = false;
+    if (overflow) *overflow = false;
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](const char *what) {
@@ -1061,6 +1063,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto prolong_done; } } while (0)
         // ---- emax(D^-1 A)
         double emax = 1.0;
+        int cols_used = 0;
         DCsr P0, T, P, AP, PT, Ac;
         int32_t *d_agg = d_aggv, *plen = nullptr;
         double *d_p0 = nullptr, *v = nullptr, *w = nullptr, *part = nullptr;
@@ -1100,7 +1103,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         P0.aa = d_p0;
         // ---- smoothed prolongator
         if (p.nsmooths > 0) {
-            if ((rc = rowprod(Av, P0, T, n_cu))) goto prolong_done;
+            if ((rc = rowprod(Av, P0, T, n_cu, &cols_used))) goto prolong_done;
             P.m = m;
             P.n = na;
             GTRY(dalloc(&plen, m), "alloc");
@@ -1126,7 +1129,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         }
         lap("prolongator");
         // ---- Galerkin operator A_c = P^T (A P)
-        if ((rc = rowprod(Av, P, AP, n_cu))) goto prolong_done;
+        if ((rc = rowprod(Av, P, AP, n_cu, &cols_used))) goto prolong_done;
         lap("A*P");
         {
             aijhip_mat pv;  // non-owning view for the transpose builder
@@ -1145,7 +1148,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
             GTRY(e, "transpose");
         }
         lap("P^T");
-        if ((rc = rowprod(PT, AP, Ac, n_cu))) goto prolong_done;
+        if ((rc = rowprod(PT, AP, Ac, n_cu, &cols_used))) goto prolong_done;
         AP.release();
         lap("P^T*(AP)");
         // ---- handles: P (with P^T attached for MatRestrict) and A_c
@@ -1157,6 +1160,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         if ((rc = make_handle(A.device, Ac, &Ach))) goto prolong_done;
         levels.back().P = Ph;
         levels.back().emax = emax;
+        levels.back().product_cols = cols_used;
         Ph = nullptr;
         levels.push_back(DeviceLevel{Ach, nullptr, 0.0});
         Ach = nullptr;
@@ -1172,6 +1176,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         if (rc == AIJHIP_ERR_STATE) {  // a row past the device accumulators
             rc = AIJHIP_OK;
             *more = true;
+            if (overflow) *overflow = true;
             break;
         }
         if (rc) break;

@@ -417,6 +417,9 @@ struct aijhip_ksp {
     std::vector<MGLevel> mg;     // GAMG levels, finest first
     double *d_mgpart = nullptr;  // fused finest-level z.z / z.r partials
     double setup_seconds = 0.0;
+    // how each level's coarsening was built (aijhip_ksp_get_gamg_setup_path)
+    std::vector<int32_t> setup_path, setup_cols;
+    bool setup_overflow = false;
     int32_t its = 0;
     int reason = 0;
     double rnorm = 0.0;
@@ -482,9 +485,16 @@ int gamg_setup(aijhip_ksp *K) {
     };
     std::vector<aijhip_gamg::DeviceLevel> dl;
     std::vector<double> B;
-    bool more = false;
-    int rc = aijhip_gamg::build_device(A, K->gamg, dl, B, &more);
+    bool more = false, overflow = false;
+    int rc = aijhip_gamg::build_device(A, K->gamg, dl, B, &more, &overflow);
     if (rc) return rc;
+    K->setup_path.clear();
+    K->setup_cols.clear();
+    for (size_t l = 0; l + 1 < dl.size(); ++l) {
+        K->setup_path.push_back(1);
+        K->setup_cols.push_back(dl[l].product_cols);
+    }
+    K->setup_overflow = overflow;
     lap("device levels");
     hipError_t e = hipSuccess;
     aijhip_gamg_host_t H = nullptr;
@@ -512,6 +522,10 @@ int gamg_setup(aijhip_ksp *K) {
     }
     const int32_t nd = (int32_t)dl.size();
     const int32_t nl = nd + (nh > 0 ? nh - 1 : 0);
+    for (int32_t hl = 1; hl < nh; ++hl) {
+        K->setup_path.push_back(0);
+        K->setup_cols.push_back(-1);
+    }
     K->mg.assign((size_t)nl, MGLevel());
     for (int32_t l = 0; l < nd; ++l) {  // the device levels move into the KSP
         K->mg[l].A = dl[l].A;
@@ -895,6 +909,19 @@ int aijhip_ksp_get_pc_level(aijhip_ksp_t K, int32_t l, char which, int32_t *m, i
     if (e == hipSuccess && aj && M->nz > 0) e = hipMemcpy(aj, M->d_aj, sizeof(int32_t) * (size_t)M->nz, hipMemcpyDeviceToHost);
     if (e == hipSuccess && aa && M->nz > 0) e = hipMemcpy(aa, M->d_aa, sizeof(double) * (size_t)M->nz, hipMemcpyDeviceToHost);
     return e == hipSuccess ? AIJHIP_OK : khip(e, "read PC level");
+}
+
+int aijhip_ksp_get_gamg_setup_path(aijhip_ksp_t K, int32_t cap, int32_t *path, int32_t *product_cols,
+                                   int32_t *host_fallback) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "null ksp");
+    if (!K->set_up || K->pc != AIJHIP_PC_GAMG) return kfail(AIJHIP_ERR_STATE, "GAMG not set up");
+    const size_t n = std::min<size_t>(K->setup_path.size(), (size_t)std::max(cap, 0));
+    for (size_t l = 0; l < n; ++l) {
+        if (path) path[l] = K->setup_path[l];
+        if (product_cols) product_cols[l] = K->setup_cols[l];
+    }
+    if (host_fallback) *host_fallback = K->setup_overflow ? 1 : 0;
+    return AIJHIP_OK;
 }
 
 int aijhip_ksp_destroy(aijhip_ksp_t K) {

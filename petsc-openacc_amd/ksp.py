@@ -28,6 +28,7 @@ KSP_SYMBOLS = (
     "aijhip_ksp_get_iteration_number", "aijhip_ksp_get_residual_norm", "aijhip_ksp_get_converged_reason",
     "aijhip_ksp_get_residual_history", "aijhip_ksp_get_fused", "aijhip_ksp_destroy",
     "aijhip_ksp_set_gamg_params", "aijhip_ksp_get_pc_levels", "aijhip_ksp_get_pc_level",
+    "aijhip_ksp_get_gamg_setup_path",
 )
 _P = ctypes.c_void_p
 _bound = False
@@ -57,6 +58,7 @@ def _lib():
                                               ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int64), _P, _P, _P]
         L.aijhip_ksp_get_pc_levels.argtypes = [_P, ctypes.POINTER(ctypes.c_int32), _P, _P, ctypes.c_int32,
                                                ctypes.POINTER(ctypes.c_double)]
+        L.aijhip_ksp_get_gamg_setup_path.argtypes = [_P, ctypes.c_int32, _P, _P, ctypes.POINTER(ctypes.c_int32)]
         _bound = True
     return L
 
@@ -122,6 +124,18 @@ class KSPCG:
         _pkg._check(_lib().aijhip_ksp_get_pc_levels(self._h, ctypes.byref(n), rows.ctypes.data, nnz.ctypes.data,
                                                      32, ctypes.byref(secs)))
         return rows[: n.value].tolist(), nnz[: n.value].tolist(), secs.value
+
+    def setup_path(self):
+        """Per coarsening l -> l+1: ("device"|"host", widest product
+        accumulator: 0 = wavefront form, 64/128/256 LDS columns, -1 host), and
+        whether a device level overflowed to the host builder."""
+        path = np.zeros(32, np.int32)
+        cols = np.zeros(32, np.int32)
+        fb = ctypes.c_int32()
+        _pkg._check(_lib().aijhip_ksp_get_gamg_setup_path(self._h, 32, path.ctypes.data, cols.ctypes.data,
+                                                           ctypes.byref(fb)))
+        n = len(self.pc_levels()[0]) - 1
+        return [("device" if path[l] else "host", int(cols[l])) for l in range(n)], bool(fb.value)
 
     def pc_level(self, l: int, which: str = "A"):
         """(ai, aj, aa, ncols) of GAMG level l's operator ('A') or
