@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
                         "(launch with torch.distributed.run): a one-GPU rehearsal of the N > 1 run")
+    p.add_argument("--comm-timeout", type=float, default=600.0,
+                   help="seconds before a stuck collective aborts the run (process group and RCCL waits)")
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="N > 1 control-flow rehearsal on a one-GPU box: every rank on cuda:0 over gloo "
                         "(RCCL refuses two ranks on one device); timings are not scaling numbers")
@@ -203,7 +205,7 @@ def cpu_model():
     return "unknown"
 
 
-def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args):
+def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm):
     """The G^3 operand (300^3: BASELINE configs[1]) row-partitioned over all
     ranks in balanced whole z-planes (DMDA PETSC_DECIDE), timed like the main
     line: K distributed SpMVs between barriers, max over ranks. Strong
@@ -214,7 +216,7 @@ def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args):
     row_starts = np.array([b[0] * G * G for b in bounds] + [G ** 3], dtype=np.int64)
     z0, z1 = bounds[rank]
     ai, aj, aa = pkg.poisson_csr(G, G, G, z0, z1)
-    op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo)
+    op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo, comm=comm)
     nnz_t = torch.tensor([len(aj)], dtype=torch.float64, device=dev)
     dist.all_reduce(nnz_t)
     nnz = int(nnz_t.item())
@@ -234,6 +236,7 @@ def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args):
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     dt = float(el.item()) / args.steps
     nbytes = pkg.algorithmic_bytes(G ** 3, G ** 3, nnz)
+    op.native.destroy()
     op.A_d.destroy()
     if op.A_o is not None:
         op.A_o.destroy()
@@ -270,11 +273,19 @@ def main():
                 mat.set_option(opt, val)
         return mat
 
+    comm = None
     if distributed:
+        from datetime import timedelta
+        to = timedelta(seconds=args.comm_timeout)
         if args.rehearse_one_gpu:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=to)
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=to)
+        # the library's own communicator (include/aijhip_mpi.h): RCCL, or the
+        # host transport when the ranks share one GPU (RCCL refuses that)
+        C = importlib.import_module("petsc-openacc_amd.comm")
+        comm = (C.Comm.host(device=local_rank, timeout_s=args.comm_timeout) if args.rehearse_one_gpu
+                else C.Comm.rccl(device=local_rank, timeout_s=args.comm_timeout))
 
     G = args.grid
     nx, ny, nz_global = weak_grid(G, world) if distributed else (G, G, G)
@@ -302,7 +313,7 @@ def main():
         def make_local(a_i, a_j, a_a, ncols):
             return configure(pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols, device=local_rank, kernel=args.kernel))
 
-        op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo)
+        op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo, comm=comm)
         info = op.A_d.info()
         step = lambda: op.mult(xd, yd)  # noqa: E731
     else:
@@ -345,6 +356,27 @@ def main():
     elapsed = float(el_t.item())
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
 
+    ranks = None
+    if distributed:
+        # Evidence the exchange hides behind the diagonal block: the same K
+        # launches of A_d alone (no halo, no A_o) on the same stream.
+        ev_d = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        y_diag = torch.empty_like(yd)
+        for i in range(K):
+            ev_d[i][0].record(stream)
+            op.A_d.mult(xd, y_diag, stream)
+            ev_d[i][1].record(stream)
+        torch.cuda.synchronize()
+        diag_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_d]))
+        del y_diag
+        mine = {"rank": rank, "device": torch.cuda.current_device(),
+                "pci_bus": getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None), "rows": m_loc, "nnz": nnz_loc, "ghosts": op.n_ghost,
+            "spmv_us_mean": round(float(np.mean(launch_ms)) * 1e3, 2),
+            "diag_block_us_mean": round(diag_ms * 1e3, 2),
+            "halo_exposed_us": round((float(np.mean(launch_ms)) - diag_ms) * 1e3, 2)}
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+
     # correctness spot-check of the timed output against a fresh multiply
     y_chk = yd.clone()
     step()
@@ -356,14 +388,20 @@ def main():
     # in the line instead of discarding the headline measurement.
     def guarded(name, fn):
         try:
-            return fn()
+            res, ok = fn(), 1.0
         except Exception as e:  # noqa: BLE001
             print(f"bench: {name} failed: {e!r}", file=sys.stderr, flush=True)
-            return {"error": f"{type(e).__name__}: {e}"[:300]}
+            res, ok = {"error": f"{type(e).__name__}: {e}"[:300]}, 0.0
+        if distributed:  # every rank learns whether any rank failed, so none waits on a peer that gave up
+            flag = torch.tensor([ok], dtype=torch.float64, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if float(flag.item()) < 1.0 and ok:
+                res = {"error": "failed on another rank"}
+        return res
 
     strong = None
     if distributed and not args.no_strong:
-        strong = guarded("strong_300", lambda: strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args))
+        strong = guarded("strong_300", lambda: strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm))
 
     def single_cg():
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
@@ -374,15 +412,14 @@ def main():
 
     def distributed_cg():
         # row-partitioned CG+Jacobi: dots all-reduced over RCCL
-        ksp = importlib.import_module("petsc-openacc_amd.ksp")
+        # aijhip_kspmpi: scalar steps on the device, RCCL all-reduces of device
+        # doubles on the compute stream, host polls every 8 iterations
         rhs_h, _ = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
         b = torch.from_numpy(rhs_h).to(dev)
-        dinv = torch.empty_like(b)
-        ksp.DeviceVecOps.jacobi_inverse(op.A_d, dinv)
         xs = torch.zeros_like(b)
-        cgm = ksp.KSPCGMPI(op, m_loc, dinv=dinv, rtol=0.0, atol=0.0, max_it=5, device=dev)
+        cgm = C.KSPCGMPINative(op.native, rtol=0.0, atol=0.0, max_it=5)
         cgm.solve(b, xs)  # warm-up
-        cgm.max_it = args.cg_iters
+        cgm.set_tolerances(0.0, 0.0, 1e5, args.cg_iters)
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -391,10 +428,16 @@ def main():
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dt = float(el.item())
-        return {"iters": cgm.its, "seconds": round(dt, 4), "iters_per_s": round(cgm.its / dt, 2),
-                "ms_per_iter": round(dt / cgm.its * 1e3, 4), "pc": "jacobi (bjacobi+jacobi per rank)",
-                "reductions": f"2 all-reduces per iteration ({'gloo' if args.rehearse_one_gpu else 'RCCL'})", "halo": args.halo,
-                "workload": f"{nx}x{ny}x{nz_global} Poisson, {planes}-plane z-slab per GPU"}
+        its = cgm.its
+        out = {"iters": its, "seconds": round(dt, 4), "iters_per_s": round(its / dt, 2),
+               "ms_per_iter": round(dt / its * 1e3, 4), "pc": "jacobi (bjacobi+jacobi per rank)",
+               "reductions": "2 all-reduces per iteration (" + ("host transport over gloo" if args.rehearse_one_gpu
+                                                                 else "RCCL, device doubles") +
+                             ("; skipped at one rank" if world == 1 else "") + ")",
+               "host_syncs": cgm.host_syncs, "halo": args.halo, "solver": "aijhip_kspmpi (native)",
+               "workload": f"{nx}x{ny}x{nz_global} Poisson, {planes}-plane z-slab per GPU"}
+        cgm.destroy()
+        return out
 
     def single_cg_gamg():
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
@@ -461,6 +504,14 @@ def main():
         }
         if distributed:  # whole-job rate against N HBM peaks (roofline.frac is rank 0's kernel alone)
             out["aggregate_roofline_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
+            ci = comm.info()
+            out["distributed"] = {
+                "world_size": world, "backend": dist.get_backend(), "comm": ci["kind"],
+                "rccl_version": ci["version"] or None, "comm_timeout_s": args.comm_timeout,
+                "ranks": ranks,
+                "halo_hidden": "spmv_us_mean vs diag_block_us_mean per rank: the exchange runs on a second "
+                               "stream while A_d multiplies; halo_exposed_us is what it adds (A_o product "
+                               "included)"}
         if args.rehearse_one_gpu:
             out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
         if strong is not None:

@@ -1,0 +1,138 @@
+/*
+ * aijhip_mpi.h — the row-partitioned path on MI355X: one process per GPU,
+ * the communicator RCCL (over xGMI) or the caller's own host transport,
+ * MatMult_MPIAIJ over it, and KSPSolve_CG over that.
+ *
+ * Reference mapping. The reference runs PETSc's MPIAIJ on 1-16 MPI ranks
+ * (/root/reference/runs/single-node-scaling.pbs:56-67); its patched
+ * MatMult_SeqAIJ (src/openacc-step{1..4}/MatMult_SeqAIJ.patch) is the
+ * diagonal-block product inside PETSc's MatMult_MPIAIJ [ext]:
+ *     VecScatterBegin(x -> lvec); (*A->ops->mult)(A_d, x, y);
+ *     VecScatterEnd;              (*B->ops->multadd)(A_o, lvec, y, y)
+ * and its KSPSolve_CG [ext] reduces every dot with MPI_Allreduce
+ * (/root/reference/src/main_ksp.cpp:103). Here:
+ *     VecScatter        -> grouped RCCL send/recv (or all-gather) of the
+ *                          ghost rows on a second HIP stream, overlapped with
+ *                          the A_d product on the caller's stream
+ *     MPI_Allreduce     -> RCCL all-reduce of 1-3 device doubles, enqueued on
+ *                          the caller's stream (no host round trip)
+ *     CG scalar logic   -> device kernels on the reduced values (every rank
+ *                          holds the same sums, so every rank branches alike);
+ *                          the host polls a stop flag every few iterations.
+ *
+ * The local blocks are ordinary aijhip_mat_t handles (include/aijhip.h): A_d
+ * with local columns, A_o with columns numbered into the ghost vector
+ * (PETSc's garray order). The handles here borrow them.
+ *
+ * Error convention as aijhip.h; AIJHIP_ERR_COMM for a failed or timed-out
+ * collective (the communicator is aborted and every later call on it fails).
+ */
+#ifndef AIJHIP_MPI_H
+#define AIJHIP_MPI_H
+
+#include <stdint.h>
+
+#include "aijhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AIJHIP_ERR_COMM 6
+
+typedef struct aijhip_comm *aijhip_comm_t;
+typedef struct aijhip_mpiaij *aijhip_mpiaij_t;
+typedef struct aijhip_kspmpi *aijhip_kspmpi_t;
+
+enum { AIJHIP_COMM_RCCL = 1, AIJHIP_COMM_HOST = 2 };
+enum { AIJHIP_HALO_P2P = 0, AIJHIP_HALO_ALLGATHER = 1 };
+
+/* ---------------------------------------------------------------- comm */
+
+/* RCCL's 128-byte ncclUniqueId, made on one rank and handed to all others by
+ * the caller (e.g. over torch.distributed or MPI_Bcast). */
+int aijhip_comm_rccl_unique_id(unsigned char id[128]);
+/* ncclCommInitRank on `device` (collective over all nranks). RCCL is
+ * resolved at run time from the process (the librccl.so.1 already loaded,
+ * e.g. by PyTorch) or from /opt/rocm/lib. */
+int aijhip_comm_create_rccl(const unsigned char id[128], int32_t nranks, int32_t rank, int32_t device,
+                            aijhip_comm_t *out);
+
+/* A host transport supplied by the caller (MPI, gloo, ...). Buffers are HOST
+ * memory; the library stages device data through pinned buffers around each
+ * call. allreduce: in-place sum of n doubles over all ranks (every rank must
+ * end with identical values). exchange: the halo of operator `op` — `send` holds this rank's
+ * packed send rows (peers in the order given to aijhip_mpiaij_create,
+ * send_off delimiting them), `recv` receives the ghost vector (p2p: peer
+ * segments at recv_off; all-gather: nranks x gather_len). Return 0 on
+ * success. */
+typedef int (*aijhip_host_allreduce_fn)(void *ctx, double *buf, int32_t n);
+typedef int (*aijhip_host_exchange_fn)(void *ctx, aijhip_mpiaij_t op, const double *send, int64_t nsend,
+                                       double *recv, int64_t nrecv);
+int aijhip_comm_create_host(int32_t nranks, int32_t rank, int32_t device, aijhip_host_allreduce_fn allreduce,
+                            aijhip_host_exchange_fn exchange, void *ctx, aijhip_comm_t *out);
+
+/* kind: AIJHIP_COMM_*; version: RCCL's ncclGetVersion code (0 for host). */
+int aijhip_comm_info(aijhip_comm_t comm, int32_t *nranks, int32_t *rank, int32_t *kind, int32_t *version);
+/* In-place sum of n device doubles over all ranks, enqueued on `stream`
+ * (MPI_Allreduce(MPI_SUM) of VecDot / VecNorm). */
+int aijhip_comm_allreduce_sum(aijhip_comm_t comm, double *d_buf, int32_t n, void *stream);
+/* Seconds a blocking wait inside a solve may take before the communicator
+ * is aborted and AIJHIP_ERR_COMM returned (default 300; <= 0 = forever). */
+int aijhip_comm_set_timeout(aijhip_comm_t comm, double seconds);
+int aijhip_comm_destroy(aijhip_comm_t comm);
+
+/* ---------------------------------------------------- MatMult_MPIAIJ */
+
+/* This rank's row block: A_d (mloc x mloc, local columns), A_o (mloc x
+ * n_ghost_buf, may be NULL when no row has off-block entries).
+ * Send side: peers send_peer[0..n_send) in that order; the local rows sent
+ * to peer q are send_rows[send_off[q] .. send_off[q+1]).
+ * Receive side, halo AIJHIP_HALO_P2P: ghost[recv_off[p] .. recv_off[p+1])
+ * comes from recv_peer[p] (ghost length recv_off[n_recv]).
+ * AIJHIP_HALO_ALLGATHER: n_send must be 1 with send_peer[0] = -1 (the rows
+ * every other rank needs from this one, padded by the library to
+ * gather_len); the ghost vector is the all-gather, nranks x gather_len
+ * (recv_* ignored). */
+int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o, int32_t halo,
+                         int32_t n_send, const int32_t *send_peer, const int64_t *send_off,
+                         const int32_t *send_rows, int32_t n_recv, const int32_t *recv_peer,
+                         const int64_t *recv_off, int32_t gather_len, aijhip_mpiaij_t *out);
+/* y = A_d x + A_o x_ghost (MatMult_MPIAIJ): the ghost exchange runs on the
+ * handle's exchange stream while A_d multiplies on `stream`. x, y: device
+ * fp64[mloc], distinct. */
+int aijhip_mpiaij_mult(aijhip_mpiaij_t M, const double *x, double *y, void *stream);
+/* The ghost vector of the last mult (device fp64, *n entries), for tests. */
+int aijhip_mpiaij_get_ghost(aijhip_mpiaij_t M, const double **ghost, int64_t *n);
+int aijhip_mpiaij_destroy(aijhip_mpiaij_t M);
+
+/* ------------------------------------------------- KSPSolve_CG over it */
+
+/* KSPCG on the distributed operator; PC none or Jacobi (PETSc's bjacobi +
+ * jacobi sub-PC on each rank: the inverse diagonal of A_d). Options,
+ * reasons and norms as aijhip_ksp.h; defaults as PETSc. */
+int aijhip_kspmpi_create(aijhip_mpiaij_t M, aijhip_kspmpi_t *out);
+int aijhip_kspmpi_set_tolerances(aijhip_kspmpi_t K, double rtol, double abstol, double dtol, int32_t max_it);
+int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc_type);
+int aijhip_kspmpi_set_norm_type(aijhip_kspmpi_t K, int norm_type);
+/* Iterations launched between two host polls of the device stop flag
+ * (default 8). Every kernel of an iteration is a no-op once the flag is set,
+ * and every rank polls at the same iterations, so the collectives stay
+ * matched. */
+int aijhip_kspmpi_set_poll_interval(aijhip_kspmpi_t K, int32_t iters);
+/* KSPSolve from x = 0 (main_ksp.cpp: VecSet(lhs, 0)); b, x device
+ * fp64[mloc]. Returns once the solve has finished on this rank. */
+int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *stream);
+int aijhip_kspmpi_get_iteration_number(aijhip_kspmpi_t K, int32_t *its);
+int aijhip_kspmpi_get_residual_norm(aijhip_kspmpi_t K, double *rnorm);
+int aijhip_kspmpi_get_converged_reason(aijhip_kspmpi_t K, int *reason);
+int aijhip_kspmpi_get_residual_history(aijhip_kspmpi_t K, double *hist, int32_t na, int32_t *n);
+/* Host synchronisations made by the last solve (polls + the final read). */
+int aijhip_kspmpi_get_host_syncs(aijhip_kspmpi_t K, int32_t *n);
+int aijhip_kspmpi_destroy(aijhip_kspmpi_t K);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIJHIP_MPI_H */

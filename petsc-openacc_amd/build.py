@@ -23,7 +23,8 @@ LIB = LIBDIR / "libaijhip.so"
 ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
-HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "ksp.hip", "poisson.hip", "gamg_device.hip", "vec.hip"]
+HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "ksp.hip", "poisson.hip", "gamg_device.hip", "vec.hip",
+               "ksp_mpi.hip"]
 HOST_SOURCES = ["harness.cpp", "gamg_setup.cpp"]
 ARCH = os.environ.get("AIJHIP_ARCH", "gfx950")
 

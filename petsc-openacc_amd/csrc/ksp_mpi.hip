@@ -1,0 +1,901 @@
+// ksp_mpi.hip — the row-partitioned path (include/aijhip_mpi.h): the
+// communicator, MatMult_MPIAIJ and KSPSolve_CG over it, one process per GPU.
+//
+// PETSc's MatMult_MPIAIJ [ext] and KSPSolve_CG [ext] with
+// its MPI_Allreduce per dot (/root/reference/src/main_ksp.cpp:103 on
+// /root/reference/runs/single-node-scaling.pbs:56-67's 1-16 ranks), laid out
+// for MI355X:
+//
+//   caller stream s   : [aypx] -- A_d p (+ p.w partials) ------ wait(halo) -- A_o g (+ correction) -- ...
+//   exchange stream xs:   wait(s) -- pack -- RCCL send/recv ----^
+//   s (cont.)         : reduce partials -> RCCL all-reduce (1 double) -> scalar step -> update ->
+//                       reduce -> RCCL all-reduce (3 doubles) -> scalar step
+//
+// No iteration needs the host: the reduced sums are identical on every rank
+// (an all-reduce leaves one value everywhere), so the scalar steps
+// (cg_device.h) take the same branch on every rank, and the host reads the
+// stop flag every `poll` iterations. Kernels return at once after the flag
+// is set; the halo exchange and the all-reduces keep running so that every
+// rank issues the same collectives.
+//
+// RCCL is resolved with dlopen at communicator creation: the librccl.so.1
+// the process already holds (PyTorch's) or /opt/rocm/lib's; libaijhip.so
+// itself has no link-time RCCL dependency and loads on machines without it.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <thread>
+#include <type_traits>
+#include <vector>
+
+#include "aijhip_internal.h"
+#include "aijhip_mpi.h"
+#include "cg_device.h"
+
+namespace {
+
+int mfail(int code, const std::string &msg) {
+    aijhip::set_error(msg);
+    return code;
+}
+
+int mhip(hipError_t e, const char *what) {
+    aijhip::set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return AIJHIP_ERR_HIP;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~DeviceGuard() { if (prev >= 0) (void)hipSetDevice(prev); }
+};
+
+// ------------------------------------------------------------ RCCL table
+struct Rccl {
+    decltype(&ncclGetVersion) GetVersion = nullptr;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;
+    decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+    decltype(&ncclAllReduce) AllReduce = nullptr;
+    decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    bool ok = false;
+    std::string why;
+};
+
+const Rccl &rccl() {
+    static Rccl R;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // already in the process (PyTorch's)
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW);
+        if (!h) {
+            const char *d = dlerror();
+            R.why = std::string("librccl.so.1 not loadable: ") + (d ? d : "?");
+            return;
+        }
+        bool all = true;
+        auto sym = [&](auto &f, const char *name) {
+            f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+            if (!f) {
+                all = false;
+                R.why += std::string(" missing ") + name;
+            }
+        };
+        sym(R.GetVersion, "ncclGetVersion");
+        sym(R.GetUniqueId, "ncclGetUniqueId");
+        sym(R.CommInitRank, "ncclCommInitRank");
+        sym(R.CommDestroy, "ncclCommDestroy");
+        sym(R.CommAbort, "ncclCommAbort");
+        sym(R.CommGetAsyncError, "ncclCommGetAsyncError");
+        sym(R.AllReduce, "ncclAllReduce");
+        sym(R.AllGather, "ncclAllGather");
+        sym(R.Send, "ncclSend");
+        sym(R.Recv, "ncclRecv");
+        sym(R.GroupStart, "ncclGroupStart");
+        sym(R.GroupEnd, "ncclGroupEnd");
+        sym(R.GetErrorString, "ncclGetErrorString");
+        R.ok = all;
+    });
+    return R;
+}
+
+int nfail(ncclResult_t r, const char *what) {
+    const Rccl &R = rccl();
+    aijhip::set_error(std::string(what) + ": " + (R.GetErrorString ? R.GetErrorString(r) : "RCCL error"));
+    return AIJHIP_ERR_COMM;
+}
+
+}  // namespace
+
+struct aijhip_comm {
+    int kind = 0;
+    int32_t nranks = 1, rank = 0, device = 0;
+    int version = 0;
+    ncclComm_t nc = nullptr;
+    aijhip_host_allreduce_fn har = nullptr;
+    aijhip_host_exchange_fn hex = nullptr;
+    void *ctx = nullptr;
+    double timeout_s = 300.0;
+    bool aborted = false;
+    double *h_red = nullptr;  // pinned staging of host all-reduces
+    hipEvent_t ev_wait = nullptr;
+    int64_t waits = 0;  // host waits made (polls, host-transport collectives)
+};
+
+namespace {
+
+constexpr int kMaxRed = 64;
+
+void comm_abort(aijhip_comm *C) {
+    if (C->aborted) return;
+    C->aborted = true;
+    if (C->kind == AIJHIP_COMM_RCCL && C->nc) {
+        rccl().CommAbort(C->nc);
+        C->nc = nullptr;
+    }
+}
+
+// Block the host until `s` has drained up to now, failing (and aborting the
+// communicator) if a collective reports an error or the wait exceeds the
+// timeout: a stuck peer makes the solve return AIJHIP_ERR_COMM instead of
+// hanging the process.
+int wait_stream(aijhip_comm *C, hipStream_t s) {
+    ++C->waits;
+    hipError_t e = hipEventRecord(C->ev_wait, s);
+    if (e != hipSuccess) return mhip(e, "comm wait");
+    if (C->timeout_s <= 0.0) {
+        e = hipEventSynchronize(C->ev_wait);
+        return e == hipSuccess ? AIJHIP_OK : mhip(e, "comm wait");
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        e = hipEventQuery(C->ev_wait);
+        if (e == hipSuccess) return AIJHIP_OK;
+        if (e != hipErrorNotReady) return mhip(e, "comm wait");
+        if (C->kind == AIJHIP_COMM_RCCL && C->nc && (spin & 255) == 255) {
+            ncclResult_t ae = ncclSuccess;
+            rccl().CommGetAsyncError(C->nc, &ae);
+            if (ae != ncclSuccess && ae != ncclInProgress) {
+                comm_abort(C);
+                return nfail(ae, "RCCL asynchronous error");
+            }
+        }
+        const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (el > C->timeout_s) {
+            comm_abort(C);
+            return mfail(AIJHIP_ERR_COMM, "collective timed out after " + std::to_string(C->timeout_s) +
+                                              " s (communicator aborted)");
+        }
+        if (el > 1e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
+
+int comm_allreduce(aijhip_comm *C, double *d_buf, int32_t n, hipStream_t s) {
+    if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
+    if (n <= 0) return AIJHIP_OK;
+    if (C->kind == AIJHIP_COMM_RCCL) {
+        const ncclResult_t r = rccl().AllReduce(d_buf, d_buf, (size_t)n, ncclFloat64, ncclSum, C->nc, s);
+        return r == ncclSuccess ? AIJHIP_OK : nfail(r, "ncclAllReduce");
+    }
+    if (n > kMaxRed) return mfail(AIJHIP_ERR_ARG, "host all-reduce of more than 64 values");
+    hipError_t e = hipMemcpyAsync(C->h_red, d_buf, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, s);
+    if (e != hipSuccess) return mhip(e, "all-reduce staging");
+    int rc = wait_stream(C, s);
+    if (rc) return rc;
+    if (C->har(C->ctx, C->h_red, n) != 0) {
+        comm_abort(C);
+        return mfail(AIJHIP_ERR_COMM, "host all-reduce callback failed");
+    }
+    e = hipMemcpyAsync(d_buf, C->h_red, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, s);
+    return e == hipSuccess ? AIJHIP_OK : mhip(e, "all-reduce staging");
+}
+
+// ------------------------------------------------------------- kernels
+// Pack the send rows: buf[i] = x[rows[i]] (zero past n up to n_pad).
+__global__ __launch_bounds__(256) void k_pack(int64_t n, int64_t n_pad, const int32_t *__restrict__ rows,
+                                              const double *__restrict__ x, double *buf) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * 256)
+        buf[i] = i < n ? x[rows[i]] : 0.0;
+}
+
+// w[o] += (A_o g)_o for every row o of A_o's row list (MatMultAdd_SeqAIJ
+// order: the sum starts from w[o] and adds the products in storage order),
+// and, in the CG, the partials of p_o w_o(new) - p_o w_o(old): the A_d
+// epilogue already summed p_o w_o(old), so the two give p . w.
+__global__ __launch_bounds__(kVecThreads) void k_offdiag(int32_t nr, const int32_t *__restrict__ rai,
+                                                         const int32_t *__restrict__ ridx,
+                                                         const int32_t *__restrict__ aj,
+                                                         const double *__restrict__ aa,
+                                                         const double *__restrict__ g,
+                                                         const double *__restrict__ p, double *w, double *part,
+                                                         const CGState *S) {
+    __shared__ double scratch[kVecThreads / 64];
+    if (S && S->done) return;
+    double d = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < nr; i += (int64_t)gridDim.x * kVecThreads) {
+        const int32_t o = ridx ? ridx[i] : (int32_t)i;
+        const double old = w[o];
+        double s = old;
+        for (int32_t k = rai[i]; k < rai[i + 1]; ++k) s += aa[k] * g[aj[k]];
+        w[o] = s;
+        if (part) {
+            const double po = p[o];
+            d += po * s + (-(po * old));
+        }
+    }
+    if (!part) return;
+    const double v = bsum<kVecThreads>(d, scratch);
+    if (threadIdx.x == 0) part[blockIdx.x] = v;
+}
+
+// red[q] = this device's fixed-order sum of part[q*nb .. (q+1)*nb), q < nq
+// (the single-GPU solver's k_reduce_* sums). step: one rank, no all-reduce
+// in between — apply the scalar step here (1: init, 2: iteration) as the
+// single-GPU solver's fused reduce kernels do.
+__global__ __launch_bounds__(kRedThreads) void k_local_sums(const double *part, int nb, int nq, double *red,
+                                                            int step, CGState *S, double *hist, CGParams p) {
+    __shared__ double scratch[kRedThreads / 64];
+    if (step == 2 && S->done) return;
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < nq; ++q) v[q] = reduce_parts(part + (size_t)q * nb, nb, scratch);
+    if (threadIdx.x != 0) return;
+    if (step == 1) step_init(v[0], v[1], v[2], v[3], S, hist, p);
+    else if (step == 2) step_iter(v[0], v[1], v[2], S, hist, p);
+    else for (int q = 0; q < nq; ++q) red[q] = v[q];
+}
+
+// dpi's local sum: the A_d epilogue's partials, then the A_o corrections
+// (step: apply step_dpi here, one rank).
+__global__ __launch_bounds__(kRedThreads) void k_local_dpi(const double *part, int nb, const double *opart,
+                                                           int nob, double *red, CGState *S, int step) {
+    __shared__ double scratch[kRedThreads / 64];
+    if (S->done) return;
+    double v = reduce_parts(part, nb, scratch);
+    if (nob > 0) {
+        const double o = reduce_parts(opart, nob, scratch);
+        v += o;
+    }
+    if (threadIdx.x != 0) return;
+    if (step) step_dpi(v, S);
+    else red[0] = v;
+}
+
+__global__ void k_step_init(const double *red, CGState *S, double *hist, CGParams p) {
+    if (threadIdx.x == 0) step_init(red[0], red[1], red[2], red[3], S, hist, p);
+}
+
+__global__ void k_step_dpi(const double *red, CGState *S) {
+    if (threadIdx.x == 0 && !S->done) step_dpi(red[0], S);
+}
+
+__global__ void k_step_iter(const double *red, CGState *S, double *hist, CGParams p) {
+    if (threadIdx.x == 0 && !S->done) step_iter(red[0], red[1], red[2], S, hist, p);
+}
+
+int grid_of(int64_t n, int cap) {
+    return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, cap));
+}
+
+}  // namespace
+
+struct aijhip_mpiaij {
+    aijhip_comm *comm = nullptr;
+    aijhip_mat *Ad = nullptr, *Ao = nullptr;
+    int halo = AIJHIP_HALO_P2P;
+    int32_t mloc = 0;
+    int64_t n_ghost = 0;
+    std::vector<int32_t> send_peer, recv_peer;
+    std::vector<int64_t> send_off, recv_off;
+    std::vector<int64_t> send_first;  // per send peer: first row if its rows are one contiguous run, else -1
+    int32_t gather_len = 0;
+    int64_t n_send = 0;     // packed send entries (all-gather: gather_len)
+    bool pack_all = false;  // every send row goes through the packed buffer
+    int32_t *d_send_rows = nullptr;
+    double *d_sendbuf = nullptr, *d_ghost = nullptr;
+    double *h_send = nullptr, *h_ghost = nullptr;  // host transport staging (pinned)
+    hipStream_t xs = nullptr;
+    hipEvent_t ev_x = nullptr, ev_halo = nullptr;
+    int o_grid = 1;
+};
+
+namespace {
+
+void mpiaij_free(aijhip_mpiaij *M) {
+    hipFree(M->d_send_rows); hipFree(M->d_sendbuf); hipFree(M->d_ghost);
+    if (M->h_send) hipHostFree(M->h_send);
+    if (M->h_ghost) hipHostFree(M->h_ghost);
+    if (M->xs) hipStreamDestroy(M->xs);
+    if (M->ev_x) hipEventDestroy(M->ev_x);
+    if (M->ev_halo) hipEventDestroy(M->ev_halo);
+}
+
+// Start the ghost exchange on the exchange stream (ordered after everything
+// already enqueued on s, i.e. after x is written and the previous A_o
+// product has read the ghost vector).
+int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
+    aijhip_comm *C = M->comm;
+    if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
+    hipError_t e;
+    if ((e = hipEventRecord(M->ev_x, s)) != hipSuccess || (e = hipStreamWaitEvent(M->xs, M->ev_x, 0)) != hipSuccess)
+        return mhip(e, "halo order");
+    const int64_t npack = M->halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send;
+    const int64_t nrows = M->send_off.empty() ? 0 : M->send_off.back();
+    if (npack > 0 && (M->pack_all || M->halo == AIJHIP_HALO_ALLGATHER)) {
+        hipLaunchKernelGGL(k_pack, dim3(grid_of(npack, 1024)), dim3(256), 0, M->xs, nrows, npack, M->d_send_rows,
+                           x, M->d_sendbuf);
+    } else if (npack > 0) {  // RCCL p2p: only the non-contiguous peers are packed
+        for (size_t q = 0; q < M->send_peer.size(); ++q) {
+            if (M->send_first[q] >= 0) continue;
+            const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
+            hipLaunchKernelGGL(k_pack, dim3(grid_of(n, 1024)), dim3(256), 0, M->xs, n, n, M->d_send_rows + a, x,
+                               M->d_sendbuf + a);
+        }
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return mhip(e, "halo pack");
+    if (C->kind == AIJHIP_COMM_RCCL) {
+        const Rccl &R = rccl();
+        ncclResult_t r;
+        if (M->halo == AIJHIP_HALO_ALLGATHER) {
+            r = R.AllGather(M->d_sendbuf, M->d_ghost, (size_t)M->gather_len, ncclFloat64, C->nc, M->xs);
+            if (r != ncclSuccess) return nfail(r, "ncclAllGather");
+        } else {
+            if ((r = R.GroupStart()) != ncclSuccess) return nfail(r, "ncclGroupStart");
+            for (size_t q = 0; q < M->send_peer.size(); ++q) {
+                const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
+                const double *src = M->send_first[q] >= 0 ? x + M->send_first[q] : M->d_sendbuf + a;
+                if (n > 0 && (r = R.Send(src, (size_t)n, ncclFloat64, M->send_peer[q], C->nc, M->xs)) != ncclSuccess)
+                    break;
+            }
+            for (size_t p = 0; r == ncclSuccess && p < M->recv_peer.size(); ++p) {
+                const int64_t a = M->recv_off[p], n = M->recv_off[p + 1] - a;
+                if (n > 0 && (r = R.Recv(M->d_ghost + a, (size_t)n, ncclFloat64, M->recv_peer[p], C->nc, M->xs)) !=
+                                 ncclSuccess)
+                    break;
+            }
+            const ncclResult_t r2 = R.GroupEnd();
+            if (r != ncclSuccess) return nfail(r, "ncclSend/ncclRecv");
+            if (r2 != ncclSuccess) return nfail(r2, "ncclGroupEnd");
+        }
+        if ((e = hipEventRecord(M->ev_halo, M->xs)) != hipSuccess) return mhip(e, "halo event");
+    } else if (npack > 0) {
+        if ((e = hipMemcpyAsync(M->h_send, M->d_sendbuf, sizeof(double) * (size_t)npack, hipMemcpyDeviceToHost,
+                                M->xs)) != hipSuccess)
+            return mhip(e, "halo staging");
+    }
+    return AIJHIP_OK;
+}
+
+// Finish the exchange (host transport: the callback, then the ghost upload)
+// and order s after it.
+int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
+    aijhip_comm *C = M->comm;
+    hipError_t e;
+    if (C->kind == AIJHIP_COMM_HOST) {
+        const int64_t npack = M->halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send;
+        int rc = wait_stream(C, M->xs);
+        if (rc) return rc;
+        if (C->hex(C->ctx, M, M->h_send, npack, M->h_ghost, M->n_ghost) != 0) {
+            comm_abort(C);
+            return mfail(AIJHIP_ERR_COMM, "host exchange callback failed");
+        }
+        if (M->n_ghost > 0 && (e = hipMemcpyAsync(M->d_ghost, M->h_ghost, sizeof(double) * (size_t)M->n_ghost,
+                                                  hipMemcpyHostToDevice, M->xs)) != hipSuccess)
+            return mhip(e, "ghost upload");
+        if ((e = hipEventRecord(M->ev_halo, M->xs)) != hipSuccess) return mhip(e, "halo event");
+    }
+    if ((e = hipStreamWaitEvent(s, M->ev_halo, 0)) != hipSuccess) return mhip(e, "halo wait");
+    return AIJHIP_OK;
+}
+
+// y = A_d x + A_o g; with dot: W = y and the p.w partials (p = x) into
+// part (A_d blocks, fused when A_d's plan allows) and opart (A_o rows).
+int mpiaij_apply(aijhip_mpiaij *M, const double *x, double *y, hipStream_t s, double *part, double *opart,
+                 const CGState *S, bool fused) {
+    // nothing to send or receive (one rank, or a block with no coupling):
+    // no exchange, no second stream
+    const bool exchange = M->n_send > 0 || M->n_ghost > 0 || M->halo == AIJHIP_HALO_ALLGATHER;
+    int rc = exchange ? halo_post(M, x, s) : AIJHIP_OK;
+    if (rc) return rc;
+    hipError_t e;
+    if (part && fused) e = aijhip::launch_stream_dot(*M->Ad, x, y, part, S ? &S->done : nullptr, s);
+    else e = aijhip::launch_mult(*M->Ad, x, nullptr, y, false, s);
+    if (e != hipSuccess) return mhip(e, "A_d product");
+    if (exchange && (rc = halo_finish(M, s))) return rc;
+    if (M->Ao) {
+        const aijhip::RowList L = aijhip::row_list(*M->Ao);
+        if (part) {
+            if (L.nr > 0)
+                hipLaunchKernelGGL(k_offdiag, dim3(M->o_grid), dim3(kVecThreads), 0, s, L.nr, L.rai, L.ridx,
+                                   M->Ao->d_aj, M->Ao->d_aa, M->d_ghost, x, y, opart, S);
+            e = hipGetLastError();
+        } else {
+            e = aijhip::launch_mult(*M->Ao, M->d_ghost, y, y, true, s);  // MatMultAdd_SeqAIJ(A_o, g, y, y)
+        }
+        if (e != hipSuccess) return mhip(e, "A_o product");
+    }
+    return AIJHIP_OK;
+}
+
+}  // namespace
+
+struct aijhip_kspmpi {
+    aijhip_mpiaij *M = nullptr;
+    double rtol = 1e-5, abstol = 1e-50, dtol = 1e5;
+    int32_t max_it = 10000;
+    int pc = AIJHIP_PC_JACOBI;
+    int normtype = AIJHIP_KSP_NORM_PRECONDITIONED;
+    int32_t poll = 8;
+    bool set_up = false, fused = false, vec_nt = true;
+    int vec_grid = 1, n_dparts = 1;
+    double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr,
+           *d_opart = nullptr, *d_red = nullptr, *d_hist = nullptr;
+    int32_t hist_cap = 0;
+    CGState *d_state = nullptr, *h_state = nullptr;
+    int32_t its = 0, host_syncs = 0;
+    int reason = 0;
+    double rnorm = 0.0;
+    std::vector<double> hist;
+};
+
+namespace {
+
+void kspmpi_free(aijhip_kspmpi *K) {
+    hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
+    hipFree(K->d_opart); hipFree(K->d_red); hipFree(K->d_hist); hipFree(K->d_state);
+    if (K->h_state) hipHostFree(K->h_state);
+    K->d_dinv = K->d_r = K->d_z = K->d_p = K->d_part = K->d_opart = K->d_red = K->d_hist = nullptr;
+    K->d_state = K->h_state = nullptr;
+    K->set_up = false;
+}
+
+int kspmpi_set_up(aijhip_kspmpi *K) {
+    if (K->set_up) return AIJHIP_OK;
+    kspmpi_free(K);
+    aijhip_mpiaij *M = K->M;
+    aijhip_mat *A = M->Ad;
+    const int64_t m = A->m;
+    K->fused = aijhip::stream_dot_fusable(*A);
+    K->vec_grid = (int)std::max<int64_t>(1, std::min<int64_t>((m + kVecThreads - 1) / kVecThreads,
+                                                              (int64_t)A->n_cu * 8));
+    K->n_dparts = K->fused ? std::max(1, A->plan.n_blocks) : K->vec_grid;
+    const int64_t nparts = std::max<int64_t>((int64_t)kNQ * K->vec_grid, K->n_dparts);
+    K->hist_cap = K->max_it + 2;
+    const size_t vb = sizeof(double) * (size_t)std::max<int64_t>(m, 1);
+    hipError_t e;
+    if ((e = hipMalloc(&K->d_dinv, vb)) != hipSuccess || (e = hipMalloc(&K->d_r, vb)) != hipSuccess ||
+        (e = hipMalloc(&K->d_z, vb)) != hipSuccess || (e = hipMalloc(&K->d_p, vb)) != hipSuccess ||
+        (e = hipMalloc(&K->d_part, sizeof(double) * (size_t)nparts)) != hipSuccess ||
+        (e = hipMalloc(&K->d_opart, sizeof(double) * (size_t)M->o_grid)) != hipSuccess ||
+        (e = hipMalloc(&K->d_red, sizeof(double) * 8)) != hipSuccess ||
+        (e = hipMalloc(&K->d_hist, sizeof(double) * (size_t)K->hist_cap)) != hipSuccess ||
+        (e = hipMalloc(&K->d_state, sizeof(CGState))) != hipSuccess ||
+        (e = hipHostMalloc(&K->h_state, sizeof(CGState), hipHostMallocDefault)) != hipSuccess) {
+        kspmpi_free(K);
+        return mhip(e, "KSPSetUp (distributed) allocation");
+    }
+    if (m > 0) {
+        hipLaunchKernelGGL(k_diag_inv, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, nullptr, A->m, A->d_ai,
+                           A->d_aj, A->d_aa, K->d_dinv);
+        if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess) {
+            kspmpi_free(K);
+            return mhip(e, "PCSetUp_Jacobi (distributed)");
+        }
+    }
+    K->set_up = true;
+    return AIJHIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ---------------------------------------------------------------- comm
+int aijhip_comm_rccl_unique_id(unsigned char id[128]) {
+    if (!id) return mfail(AIJHIP_ERR_ARG, "NULL id");
+    const Rccl &R = rccl();
+    if (!R.ok) return mfail(AIJHIP_ERR_COMM, "RCCL unavailable: " + R.why);
+    ncclUniqueId u;
+    const ncclResult_t r = R.GetUniqueId(&u);
+    if (r != ncclSuccess) return nfail(r, "ncclGetUniqueId");
+    std::memcpy(id, u.internal, NCCL_UNIQUE_ID_BYTES);
+    return AIJHIP_OK;
+}
+
+static int comm_new(int kind, int32_t nranks, int32_t rank, int32_t device, aijhip_comm **out) {
+    if (!out) return mfail(AIJHIP_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (nranks < 1 || rank < 0 || rank >= nranks) return mfail(AIJHIP_ERR_ARG, "bad rank / size");
+    int ndev = aijhip::visible_devices();
+    if (device < 0 || device >= ndev) return mfail(AIJHIP_ERR_NODEVICE, "no such device");
+    aijhip_comm *C = new (std::nothrow) aijhip_comm();
+    if (!C) return mfail(AIJHIP_ERR_ALLOC, "host allocation");
+    C->kind = kind; C->nranks = nranks; C->rank = rank; C->device = device;
+    DeviceGuard g(device);
+    hipError_t e;
+    if ((e = hipEventCreateWithFlags(&C->ev_wait, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipHostMalloc(&C->h_red, sizeof(double) * kMaxRed, hipHostMallocDefault)) != hipSuccess) {
+        if (C->ev_wait) hipEventDestroy(C->ev_wait);
+        delete C;
+        return mhip(e, "communicator set-up");
+    }
+    *out = C;
+    return AIJHIP_OK;
+}
+
+int aijhip_comm_destroy(aijhip_comm_t C) {
+    if (!C) return AIJHIP_OK;
+    {
+        DeviceGuard g(C->device);
+        if (C->kind == AIJHIP_COMM_RCCL && C->nc) rccl().CommDestroy(C->nc);
+        if (C->ev_wait) hipEventDestroy(C->ev_wait);
+        if (C->h_red) hipHostFree(C->h_red);
+    }
+    delete C;
+    return AIJHIP_OK;
+}
+
+int aijhip_comm_create_rccl(const unsigned char id[128], int32_t nranks, int32_t rank, int32_t device,
+                            aijhip_comm_t *out) {
+    if (!id) return mfail(AIJHIP_ERR_ARG, "NULL id");
+    const Rccl &R = rccl();
+    if (!R.ok) return mfail(AIJHIP_ERR_COMM, "RCCL unavailable: " + R.why);
+    aijhip_comm *C = nullptr;
+    int rc = comm_new(AIJHIP_COMM_RCCL, nranks, rank, device, &C);
+    if (rc) return rc;
+    DeviceGuard g(device);
+    ncclUniqueId u;
+    std::memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclResult_t r = R.CommInitRank(&C->nc, nranks, u, rank);
+    if (r != ncclSuccess) {
+        C->nc = nullptr;
+        aijhip_comm_destroy(C);
+        return nfail(r, "ncclCommInitRank");
+    }
+    R.GetVersion(&C->version);
+    *out = C;
+    return AIJHIP_OK;
+}
+
+int aijhip_comm_create_host(int32_t nranks, int32_t rank, int32_t device, aijhip_host_allreduce_fn allreduce,
+                            aijhip_host_exchange_fn exchange, void *ctx, aijhip_comm_t *out) {
+    if (!allreduce || !exchange) return mfail(AIJHIP_ERR_ARG, "NULL callback");
+    aijhip_comm *C = nullptr;
+    int rc = comm_new(AIJHIP_COMM_HOST, nranks, rank, device, &C);
+    if (rc) return rc;
+    C->har = allreduce;
+    C->hex = exchange;
+    C->ctx = ctx;
+    *out = C;
+    return AIJHIP_OK;
+}
+
+int aijhip_comm_info(aijhip_comm_t C, int32_t *nranks, int32_t *rank, int32_t *kind, int32_t *version) {
+    if (!C) return mfail(AIJHIP_ERR_ARG, "NULL comm");
+    if (nranks) *nranks = C->nranks;
+    if (rank) *rank = C->rank;
+    if (kind) *kind = C->kind;
+    if (version) *version = C->version;
+    return AIJHIP_OK;
+}
+
+int aijhip_comm_allreduce_sum(aijhip_comm_t C, double *d_buf, int32_t n, void *stream) {
+    if (!C || (n > 0 && !d_buf) || n < 0) return mfail(AIJHIP_ERR_ARG, "bad all-reduce arguments");
+    DeviceGuard g(C->device);
+    return comm_allreduce(C, d_buf, n, reinterpret_cast<hipStream_t>(stream));
+}
+
+int aijhip_comm_set_timeout(aijhip_comm_t C, double seconds) {
+    if (!C) return mfail(AIJHIP_ERR_ARG, "NULL comm");
+    C->timeout_s = seconds;
+    return AIJHIP_OK;
+}
+
+// ---------------------------------------------------- MatMult_MPIAIJ
+int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o, int32_t halo, int32_t n_send,
+                         const int32_t *send_peer, const int64_t *send_off, const int32_t *send_rows,
+                         int32_t n_recv, const int32_t *recv_peer, const int64_t *recv_off, int32_t gather_len,
+                         aijhip_mpiaij_t *out) {
+    if (!out) return mfail(AIJHIP_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (!comm || !A_d) return mfail(AIJHIP_ERR_ARG, "NULL comm or diagonal block");
+    if (A_d->m != A_d->n) return mfail(AIJHIP_ERR_ARG, "diagonal block must be square");
+    if (A_d->device != comm->device || (A_o && A_o->device != comm->device))
+        return mfail(AIJHIP_ERR_ARG, "blocks and communicator on different devices");
+    if (A_o && A_o->m != A_d->m) return mfail(AIJHIP_ERR_ARG, "off-diagonal block row count");
+    if (halo != AIJHIP_HALO_P2P && halo != AIJHIP_HALO_ALLGATHER) return mfail(AIJHIP_ERR_ARG, "bad halo kind");
+    if (n_send < 0 || n_recv < 0 || (n_send > 0 && (!send_peer || !send_off)) ||
+        (halo == AIJHIP_HALO_P2P && n_recv > 0 && (!recv_peer || !recv_off)))
+        return mfail(AIJHIP_ERR_ARG, "bad exchange plan");
+    aijhip_mpiaij *M = new (std::nothrow) aijhip_mpiaij();
+    if (!M) return mfail(AIJHIP_ERR_ALLOC, "host allocation");
+    M->comm = comm; M->Ad = A_d; M->Ao = A_o; M->halo = halo; M->mloc = A_d->m;
+    auto bad = [&](const std::string &msg) {
+        mpiaij_free(M);
+        delete M;
+        return mfail(AIJHIP_ERR_ARG, msg);
+    };
+    M->send_off.assign(1, 0);
+    std::vector<int32_t> rows;
+    if (n_send > 0) {
+        if (send_off[0] != 0) return bad("send_off[0] must be 0");
+        for (int32_t q = 0; q < n_send; ++q) {
+            const int64_t a = send_off[q], b = send_off[q + 1];
+            if (b < a || (b > a && !send_rows)) return bad("bad send_off");
+            if (halo == AIJHIP_HALO_P2P && (send_peer[q] < 0 || send_peer[q] >= comm->nranks || send_peer[q] == comm->rank))
+                return bad("bad send peer");
+            bool contig = b > a;
+            for (int64_t i = a; i < b; ++i) {
+                if (send_rows[i] < 0 || send_rows[i] >= A_d->m) return bad("send row out of range");
+                if (i > a && send_rows[i] != send_rows[i - 1] + 1) contig = false;
+            }
+            M->send_peer.push_back(send_peer[q]);
+            M->send_off.push_back(b);
+            M->send_first.push_back(contig ? send_rows[a] : -1);
+        }
+        rows.assign(send_rows, send_rows + send_off[n_send]);
+    }
+    M->n_send = M->send_off.back();
+    if (halo == AIJHIP_HALO_ALLGATHER) {
+        if (n_send > 1 || gather_len < std::max<int64_t>(M->n_send, 1)) return bad("all-gather plan");
+        M->gather_len = gather_len;
+        M->n_ghost = (int64_t)gather_len * comm->nranks;
+    } else {
+        M->recv_off.assign(1, 0);
+        if (n_recv > 0 && recv_off[0] != 0) return bad("recv_off[0] must be 0");
+        for (int32_t p = 0; p < n_recv; ++p) {
+            if (recv_off[p + 1] < recv_off[p]) return bad("bad recv_off");
+            if (recv_peer[p] < 0 || recv_peer[p] >= comm->nranks || recv_peer[p] == comm->rank)
+                return bad("bad recv peer");
+            M->recv_peer.push_back(recv_peer[p]);
+            M->recv_off.push_back(recv_off[p + 1]);
+        }
+        M->n_ghost = M->recv_off.back();
+    }
+    if (A_o && A_o->n != std::max<int64_t>(M->n_ghost, 1) && A_o->n != M->n_ghost)
+        return bad("off-diagonal block columns != ghost length");
+    M->pack_all = comm->kind == AIJHIP_COMM_HOST;
+    DeviceGuard g(comm->device);
+    hipError_t e = hipSuccess;
+    const int64_t nbuf = std::max<int64_t>(1, halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send);
+    const int64_t ng = std::max<int64_t>(1, M->n_ghost);
+    if ((e = hipMalloc(&M->d_send_rows, sizeof(int32_t) * (size_t)std::max<int64_t>(1, M->n_send))) != hipSuccess ||
+        (e = hipMalloc(&M->d_sendbuf, sizeof(double) * (size_t)nbuf)) != hipSuccess ||
+        (e = hipMalloc(&M->d_ghost, sizeof(double) * (size_t)ng)) != hipSuccess ||
+        (e = hipMemset(M->d_ghost, 0, sizeof(double) * (size_t)ng)) != hipSuccess ||
+        (e = hipMemset(M->d_sendbuf, 0, sizeof(double) * (size_t)nbuf)) != hipSuccess ||
+        (M->n_send > 0 && (e = hipMemcpy(M->d_send_rows, rows.data(), sizeof(int32_t) * (size_t)M->n_send,
+                                         hipMemcpyHostToDevice)) != hipSuccess) ||
+        (e = hipStreamCreateWithFlags(&M->xs, hipStreamNonBlocking)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&M->ev_x, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&M->ev_halo, hipEventDisableTiming)) != hipSuccess ||
+        (M->pack_all && ((e = hipHostMalloc(&M->h_send, sizeof(double) * (size_t)nbuf, hipHostMallocDefault)) !=
+                             hipSuccess ||
+                         (e = hipHostMalloc(&M->h_ghost, sizeof(double) * (size_t)ng, hipHostMallocDefault)) !=
+                             hipSuccess))) {
+        mpiaij_free(M);
+        delete M;
+        return mhip(e, "MPIAIJ set-up");
+    }
+    if (A_o) {
+        const aijhip::RowList L = aijhip::row_list(*A_o);
+        M->o_grid = grid_of(L.nr, A_o->n_cu * 4);
+    }
+    *out = M;
+    return AIJHIP_OK;
+}
+
+int aijhip_mpiaij_mult(aijhip_mpiaij_t M, const double *x, double *y, void *stream) {
+    if (!M) return mfail(AIJHIP_ERR_ARG, "NULL matrix");
+    if (M->mloc > 0 && (!x || !y)) return mfail(AIJHIP_ERR_ARG, "NULL vector");
+    if (x == y) return mfail(AIJHIP_ERR_ARG, "x and y alias");
+    DeviceGuard g(M->comm->device);
+    return mpiaij_apply(M, x, y, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr, nullptr, false);
+}
+
+int aijhip_mpiaij_get_ghost(aijhip_mpiaij_t M, const double **ghost, int64_t *n) {
+    if (!M) return mfail(AIJHIP_ERR_ARG, "NULL matrix");
+    if (ghost) *ghost = M->d_ghost;
+    if (n) *n = M->n_ghost;
+    return AIJHIP_OK;
+}
+
+int aijhip_mpiaij_destroy(aijhip_mpiaij_t M) {
+    if (!M) return AIJHIP_OK;
+    {
+        DeviceGuard g(M->comm->device);
+        (void)hipStreamSynchronize(M->xs);
+        mpiaij_free(M);
+    }
+    delete M;
+    return AIJHIP_OK;
+}
+
+// ------------------------------------------------- KSPSolve_CG over it
+int aijhip_kspmpi_create(aijhip_mpiaij_t M, aijhip_kspmpi_t *out) {
+    if (!out) return mfail(AIJHIP_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    if (!M) return mfail(AIJHIP_ERR_ARG, "NULL operator");
+    if (M->Ad->compressed) return mfail(AIJHIP_ERR_ARG, "diagonal block in compressed-row form");
+    aijhip_kspmpi *K = new (std::nothrow) aijhip_kspmpi();
+    if (!K) return mfail(AIJHIP_ERR_ALLOC, "host allocation");
+    K->M = M;
+    if (const char *v = std::getenv("AIJHIP_VEC_NT")) K->vec_nt = std::atoi(v) != 0;
+    *out = K;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_set_tolerances(aijhip_kspmpi_t K, double rtol, double abstol, double dtol, int32_t max_it) {
+    if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (rtol < 0 || abstol < 0 || dtol <= 0 || max_it < 0) return mfail(AIJHIP_ERR_ARG, "bad tolerance");
+    K->rtol = rtol; K->abstol = abstol; K->dtol = dtol;
+    if (max_it + 2 > K->hist_cap) K->set_up = false;  // regrow the history
+    K->max_it = max_it;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc) {
+    if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI)
+        return mfail(AIJHIP_ERR_ARG, "distributed CG: PC none or jacobi");
+    K->pc = pc;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_set_norm_type(aijhip_kspmpi_t K, int nt) {
+    if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
+    if (nt < AIJHIP_KSP_NORM_NONE || nt > AIJHIP_KSP_NORM_NATURAL) return mfail(AIJHIP_ERR_ARG, "bad norm type");
+    K->normtype = nt;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_set_poll_interval(aijhip_kspmpi_t K, int32_t iters) {
+    if (!K || iters < 1) return mfail(AIJHIP_ERR_ARG, "bad poll interval");
+    K->poll = iters;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *stream) {
+    aijhip::Range range("KSPSolve (MPIAIJ)");
+    if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
+    aijhip_mpiaij *M = K->M;
+    aijhip_comm *C = M->comm;
+    DeviceGuard g(C->device);
+    int rc = kspmpi_set_up(K);
+    if (rc) return rc;
+    const int64_t m = M->mloc;
+    if (m > 0 && (!b || !x)) return mfail(AIJHIP_ERR_ARG, "NULL vector");
+    if (b == x) return mfail(AIJHIP_ERR_ARG, "b and x alias");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool multi = C->nranks > 1;
+    CGParams p{K->rtol, K->abstol, K->dtol, K->max_it, K->normtype, 1, K->pc};
+    const dim3 vg(K->vec_grid), vt(kVecThreads), rt(kRedThreads);
+    const int nb = K->vec_grid;
+    const double *dinv = K->pc == AIJHIP_PC_JACOBI ? K->d_dinv : nullptr;
+    const int64_t waits0 = C->waits;
+    hipError_t e = hipSuccess;
+    if (m > 0 && (e = hipMemsetAsync(x, 0, sizeof(double) * (size_t)m, s)) != hipSuccess) return mhip(e, "x = 0");
+    // r = b, z = B r, then ||z|| etc. summed over all ranks
+    hipLaunchKernelGGL(k_init, vg, vt, 0, s, m, b, K->d_r, K->d_z, dinv, K->d_part, p);
+    hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 4, K->d_red, multi ? 0 : 1, K->d_state,
+                       K->d_hist, p);
+    if (multi) {
+        if ((rc = comm_allreduce(C, K->d_red, 4, s))) return rc;
+        hipLaunchKernelGGL(k_step_init, dim3(1), dim3(64), 0, s, K->d_red, K->d_state, K->d_hist, p);
+    }
+    if ((e = hipGetLastError()) != hipSuccess) return mhip(e, "KSPSolve init");
+    const bool have_o = M->Ao && aijhip::row_list(*M->Ao).nr > 0;
+    int32_t launched = 0;
+    for (;;) {
+        if ((e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess)
+            return mhip(e, "KSPSolve poll");
+        if ((rc = wait_stream(C, s))) return rc;
+        if (K->h_state->done || launched >= K->max_it) break;
+        for (int j = 0; j < K->poll && launched < K->max_it; ++j, ++launched) {
+            if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
+            else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
+            // W = A P with the p.w partials (W shares Z's storage)
+            if ((rc = mpiaij_apply(M, K->d_p, K->d_z, s, K->d_part, have_o ? K->d_opart : nullptr, K->d_state,
+                                   K->fused)))
+                return rc;
+            if (!K->fused) hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
+            hipLaunchKernelGGL(k_local_dpi, dim3(1), rt, 0, s, K->d_part, K->n_dparts, K->d_opart,
+                               have_o ? M->o_grid : 0, K->d_red, K->d_state, multi ? 0 : 1);
+            if (multi) {
+                if ((rc = comm_allreduce(C, K->d_red, 1, s))) return rc;
+                hipLaunchKernelGGL(k_step_dpi, dim3(1), dim3(64), 0, s, K->d_red, K->d_state);
+            }
+            if (K->vec_nt)
+                hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state,
+                                   K->pc, K->d_p, nullptr);
+            else
+                hipLaunchKernelGGL(k_update<false>, vg, vt, 0, s, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state,
+                                   K->pc, K->d_p, nullptr);
+            hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 3, K->d_red, multi ? 0 : 2,
+                               K->d_state, K->d_hist, p);
+            if (multi) {
+                if ((rc = comm_allreduce(C, K->d_red, 3, s))) return rc;
+                hipLaunchKernelGGL(k_step_iter, dim3(1), dim3(64), 0, s, K->d_red, K->d_state, K->d_hist, p);
+            }
+            if ((e = hipGetLastError()) != hipSuccess) return mhip(e, "KSPSolve iteration");
+        }
+    }
+    hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return mhip(e, "KSPSolve final update");
+    if ((rc = wait_stream(C, s))) return rc;
+    K->host_syncs = (int32_t)(C->waits - waits0);
+    const CGState &st = *K->h_state;
+    K->its = st.its;
+    K->reason = st.reason ? st.reason : AIJHIP_KSP_DIVERGED_ITS;
+    K->rnorm = st.dp;
+    const int32_t nh = std::min<int32_t>(K->hist_cap, st.its + 1);
+    K->hist.resize((size_t)std::max(nh, 0));
+    if (nh > 0 &&
+        (e = hipMemcpy(K->hist.data(), K->d_hist, sizeof(double) * (size_t)nh, hipMemcpyDeviceToHost)) != hipSuccess)
+        return mhip(e, "residual history");
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_iteration_number(aijhip_kspmpi_t K, int32_t *its) {
+    if (!K || !its) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    *its = K->its;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_residual_norm(aijhip_kspmpi_t K, double *rnorm) {
+    if (!K || !rnorm) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    *rnorm = K->rnorm;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_converged_reason(aijhip_kspmpi_t K, int *reason) {
+    if (!K || !reason) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    *reason = K->reason;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_residual_history(aijhip_kspmpi_t K, double *hist, int32_t na, int32_t *n) {
+    if (!K || !n || (na > 0 && !hist)) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    const int32_t c = std::min<int32_t>(na, (int32_t)K->hist.size());
+    std::copy(K->hist.begin(), K->hist.begin() + c, hist);
+    *n = c;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_host_syncs(aijhip_kspmpi_t K, int32_t *n) {
+    if (!K || !n) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    *n = K->host_syncs;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_destroy(aijhip_kspmpi_t K) {
+    if (!K) return AIJHIP_OK;
+    {
+        DeviceGuard g(K->M->comm->device);
+        (void)hipDeviceSynchronize();
+        kspmpi_free(K);
+    }
+    delete K;
+    return AIJHIP_OK;
+}
+
+}  // extern "C"

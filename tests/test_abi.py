@@ -36,8 +36,9 @@ def test_library_exports_every_declared_symbol(pkg):
     import importlib
     ksp = importlib.import_module("petsc-openacc_amd.ksp")
     gamg = importlib.import_module("petsc-openacc_amd.gamg")
+    comm = importlib.import_module("petsc-openacc_amd.comm")
     assert set(pkg.ABI_SYMBOLS + pkg.HARNESS_SYMBOLS + ksp.KSP_SYMBOLS + ksp.VEC_SYMBOLS +
-               gamg.GAMG_SYMBOLS) == declared_functions()
+               gamg.GAMG_SYMBOLS + comm.MPI_SYMBOLS) == declared_functions()
 
 
 def test_library_is_gfx950_code_object(pkg):
@@ -82,6 +83,26 @@ def test_null_handle_calls_return_errors(pkg):
     assert L.aijhip_mat_mult(None, None, None, None) == pkg.AIJHIP_ERR_ARG
     assert L.aijhip_mat_destroy(None) == 0
     assert b"NULL" in L.aijhip_last_error()
+
+
+def test_mpi_boundary_validates_without_a_device(pkg):
+    """include/aijhip_mpi.h: null handles and bad ranks are refused before
+    any device or RCCL call; destroy(NULL) is a no-op."""
+    import importlib
+    C = importlib.import_module("petsc-openacc_amd.comm")
+    L = C._lib()
+    h = ctypes.c_void_p()
+    assert L.aijhip_mpiaij_mult(None, None, None, None) == pkg.AIJHIP_ERR_ARG
+    assert L.aijhip_kspmpi_solve(None, None, None, None) == pkg.AIJHIP_ERR_ARG
+    assert L.aijhip_comm_allreduce_sum(None, None, 1, None) == pkg.AIJHIP_ERR_ARG
+    assert L.aijhip_mpiaij_create(None, None, None, 0, 0, None, None, None, 0, None, None, 0,
+                                  ctypes.byref(h)) == pkg.AIJHIP_ERR_ARG
+    noop_ar = C.ALLREDUCE_FN(lambda *a: 0)
+    noop_ex = C.EXCHANGE_FN(lambda *a: 0)
+    assert L.aijhip_comm_create_host(2, 2, 0, noop_ar, noop_ex, None, ctypes.byref(h)) == pkg.AIJHIP_ERR_ARG
+    assert L.aijhip_comm_create_host(2, 0, 0, C.ALLREDUCE_FN(), C.EXCHANGE_FN(), None, ctypes.byref(h)) == pkg.AIJHIP_ERR_ARG
+    for f in ("aijhip_comm_destroy", "aijhip_mpiaij_destroy", "aijhip_kspmpi_destroy"):
+        assert getattr(L, f)(None) == 0
 
 
 def test_headers_are_plain_c99(tmp_path):

@@ -43,12 +43,19 @@ def _worker(rank, world, port, dims, halo, q):
             return pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols)
 
         op = mp_mod.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=halo)
+        C = importlib.import_module("petsc-openacc_amd.comm")
+        comm = C.Comm.host(device=0, timeout_s=120)
+        op_n = mp_mod.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=halo, comm=comm)
         lo, hi = int(row_starts[rank]), int(row_starts[rank + 1])
         xg = seqaij.splitmix_uniform(nx * ny * nz, 42)
         x = torch.from_numpy(xg[lo:hi].copy()).to(dev)
         y = torch.empty(hi - lo, dtype=torch.float64, device=dev)
         op.mult(x, y)
+        y_n = torch.full_like(y, float("nan"))
+        op_n.mult(x, y_n)
+        op_n.mult(x, y_n)  # twice: the ghost buffer is reused
         torch.cuda.synchronize()
+        same = bool(torch.equal(y, y_n))
         rhs, _ = pkg.poisson_vectors(nx, ny, nz, z0, z1)
         b = torch.from_numpy(rhs).to(dev)
         dinv = torch.empty_like(b)
@@ -57,7 +64,11 @@ def _worker(rank, world, port, dims, halo, q):
         xs = torch.zeros_like(b)
         cg.solve(b, xs)
         torch.cuda.synchronize()
-        q.put((rank, y.cpu().numpy(), xs.cpu().numpy(), cg.its, cg.reason, list(cg.hist)))
+        xn = torch.full_like(b, float("nan"))
+        with C.KSPCGMPINative(op_n.native, rtol=1e-10, max_it=1000, poll=3) as kn:
+            kn.solve(b, xn)
+            native = (xn.cpu().numpy(), kn.its, kn.reason, kn.hist.tolist())
+        q.put((rank, y.cpu().numpy(), xs.cpu().numpy(), cg.its, cg.reason, list(cg.hist), same, native))
     finally:
         dist.destroy_process_group()
 
@@ -94,3 +105,11 @@ def test_gpu_mpiaij_and_cg_on_k_ranks(world, dims, halo):
     np.testing.assert_allclose(got[0][4][:10], hist_o[:10], rtol=1e-9)
     x = np.concatenate([got[r][1] for r in range(world)])
     assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
+    # the native path (aijhip_mpiaij / aijhip_kspmpi over the host transport)
+    assert all(got[r][5] for r in range(world)), "native MatMult_MPIAIJ differs from the stream-ordered path"
+    nat = [got[r][6] for r in range(world)]
+    assert len({n[1] for n in nat}) == 1 and len({n[2] for n in nat}) == 1  # every rank took the same path
+    assert abs(nat[0][1] - its_o) <= 1 and nat[0][2] == reason_o
+    np.testing.assert_allclose(nat[0][3][:10], hist_o[:10], rtol=1e-9)
+    xn = np.concatenate([n[0] for n in nat])
+    assert np.linalg.norm(xn - xo) <= 1e-8 * np.linalg.norm(xo)
