@@ -60,8 +60,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-cg", action="store_true")
     p.add_argument("--no-gamg", action="store_true", help="skip the CG+GAMG solve (BASELINE configs[2])")
-    p.add_argument("--gamg-cpu-iters", type=int, default=3, help="CG+GAMG iterations in the CPU sample")
     p.add_argument("--cg-iters", type=int, default=200, help="CG iterations timed for cg.iters_per_s")
+    p.add_argument("--no-host-vec", action="store_true", help="skip the host-vector MatMult timing")
     p.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling 300^3 line")
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
@@ -146,38 +146,63 @@ def cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz, iters=8):
             "sample": f"{its} CG+Jacobi iterations, oracle/ksp_cg.py + oracle/matmult_seqaij.c, 1 core"}
 
 
-def cpu_cg_gamg_baseline(ai, aj, aa, pkg, nx, ny, nz, its_gpu, iters=3):
-    """CG+GAMG on the host: the set-up is the library's host code (shared
-    with the device path, timed here on its own); the solve phase is the
-    oracle (oracle/ksp_cg.py + oracle/gamg.py V-cycle on scipy CSR products,
-    1 core) for a few iterations, scaled to the device's iteration count."""
-    import scipy.sparse as sp
-    from oracle import gamg as ogamg
-    from oracle import ksp_cg
-    G = importlib.import_module("petsc-openacc_amd.gamg")
-    m = len(ai) - 1
-    t0 = time.perf_counter()
-    lv = G.build_host(ai, aj, aa)
-    t_setup = time.perf_counter() - t0
-    levels = [dict(A=sp.csr_matrix((aa, aj, ai), shape=(m, m)))]
-    for l in range(1, len(lv)):
-        a_i, a_j, a_a = lv[l]["A"]
-        levels.append(dict(A=sp.csr_matrix((a_a, a_j, a_i), shape=(lv[l]["m"],) * 2)))
-        p_i, p_j, p_a = lv[l - 1]["P"]
-        levels[l - 1]["P"] = sp.csr_matrix((p_a, p_j, p_i), shape=(lv[l - 1]["m"], lv[l]["m"]))
-    del lv
-    ogamg.vcycle(levels, np.zeros(m))  # caches the Jacobi inverses (set-up work)
-    rhs, _ = pkg.poisson_vectors(nx, ny, nz)
-    A0 = levels[0]["A"]
-    t0 = time.perf_counter()
-    _, its, _, _ = ksp_cg.cg(ai, aj, aa, rhs, rtol=0.0, atol=0.0, max_it=iters, matmult=lambda v: A0 @ v,
-                             pc=lambda r: ogamg.vcycle(levels, r))
-    per_it = (time.perf_counter() - t0) / its
-    return {"s_per_iter": round(per_it, 4), "setup_s": round(t_setup, 3),
-            "time_to_solution_s_est": round(t_setup + per_it * its_gpu, 2), "cores": 1,
-            "setup_threads": int(os.environ.get("OMP_NUM_THREADS", 0)) or os.cpu_count(), "kind": "port",
-            "sample": f"{its} CG+GAMG iterations at {nx}x{ny}x{nz} (oracle CG + V-cycle, scipy CSR, 1 core), "
-                      f"scaled to the device's {its_gpu} iterations; host set-up as in the library"}
+def cpu_cg_gamg_baseline(ai, aj, aa, pkg, nx, ny, nz, small=100):
+    """The reference's CPU configuration, measured: CG + GAMG to rtol 1e-14 /
+    atol 1e-12 from x = 0 on the host (oracle/cg_gamg.c: OpenMP row blocks,
+    the library's host hierarchy builder), (i) on every host thread this
+    process may use at the benchmark operand — the analogue of the reference's
+    16-rank node run (/root/reference/runs/single-node-scaling.pbs:56-67) —
+    and (ii) on 1 core at {small}^3 (BASELINE configs[0], the reference's
+    plumbing configuration: 1 rank)."""
+    from oracle import host_cg_gamg
+    rhs, exact = pkg.poisson_vectors(nx, ny, nz)
+    h = host_cg_gamg.solve(ai, aj, aa, rhs)
+    out = {"time_to_solution_s": round(h["setup_s"] + h["solve_s"], 3), "setup_s": round(h["setup_s"], 3),
+           "solve_s": round(h["solve_s"], 3), "its": h["its"], "reason": h["reason"],
+           "max_err": float(np.abs(h["x"] - exact).max()), "cores": h["threads"], "cpu": cpu_model(),
+           "kind": "port",
+           "sample": f"full solve at {nx}x{ny}x{nz}: oracle/cg_gamg.c (CG + V-cycle, OpenMP, {h['threads']} threads) "
+                     f"over the library's host GAMG hierarchy (built with the same threads)"}
+    del h
+    s_ai, s_aj, s_aa = pkg.poisson_csr(small)
+    s_rhs, s_exact = pkg.poisson_vectors(small)
+    h1 = host_cg_gamg.solve(s_ai, s_aj, s_aa, s_rhs, threads=1)
+    out["one_core_configs0"] = {
+        "workload": f"{small}^3 Poisson CG+GAMG (BASELINE configs[0])", "cores": 1,
+        "time_to_solution_s": round(h1["setup_s"] + h1["solve_s"], 3), "setup_s": round(h1["setup_s"], 3),
+        "solve_s": round(h1["solve_s"], 3), "its": h1["its"], "reason": h1["reason"],
+        "max_err": float(np.abs(h1["x"] - s_exact).max()), "kind": "port"}
+    return out
+
+
+def host_vec_mult(A, x_h, reps=10):
+    """MatMult with HOST x and y (aijhip_mat_mult_host: the path an unchanged
+    PETSc caller with host Vecs takes), PCIe included: the
+    serial step-2 form, the pipelined step-3/4 analogue from pageable arrays
+    (staged through pinned slots) and from pinned arrays (direct DMA). The
+    three results must be bit-identical."""
+    import torch
+    out, ys = {}, []
+    for name, chunk, pin in (("serial_pageable", 0, False), ("pipelined_pageable", -1, False),
+                             ("pipelined_pinned", -1, True)):
+        A.set_option("host_pipeline", chunk)
+        if pin:
+            xp = torch.from_numpy(x_h).pin_memory().numpy()
+            yp = torch.empty(A.m, dtype=torch.float64).pin_memory().numpy()
+        else:
+            xp, yp = x_h, np.empty(A.m)
+        A.mult_host(xp, out=yp)  # warm-up (builds the pipeline)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            A.mult_host(xp, out=yp)
+        dt = (time.perf_counter() - t0) / reps
+        out[name] = {"ms": round(dt * 1e3, 3), "pcie_GBs": round((8 * A.n + 8 * A.m) / dt / 1e9, 2)}
+        ys.append(np.array(yp, copy=True))
+    A.set_option("host_pipeline", -1)
+    out["bitwise_equal"] = bool(all(np.array_equal(ys[0].view(np.uint64), y.view(np.uint64)) for y in ys[1:]))
+    out["speedup_pipelined_pageable"] = round(out["serial_pageable"]["ms"] / out["pipelined_pageable"]["ms"], 3)
+    out["note"] = "ms per MatMult with x, y in host memory (x H2D + product + y D2H), whole-call wall time"
+    return out
 
 
 def pmc_traffic(rows, nnz, block):
@@ -444,9 +469,14 @@ def main():
         out = ksp.bench_cg_gamg(pkg, A, nx, ny, nz_global, dev)
         print(f"bench: CG+GAMG {out['its']} its, solve {out['solve_s']} s, set-up {out['setup_s']} s",
               file=sys.stderr, flush=True)
+        # BASELINE configs[0] (100^3) on the device as well, beside its 1-core host solve
+        s_ai, s_aj, s_aa = pkg.poisson_csr(100)
+        with pkg.SeqAIJHIP(s_ai, s_aj, s_aa, device=local_rank) as A100:
+            small = ksp.bench_cg_gamg(pkg, A100, 100, 100, 100, dev)
+        out["configs0_device"] = {k: small[k] for k in ("its", "reason", "max_err", "setup_s", "solve_s",
+                                                        "time_to_solution_s")}
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_cg_gamg_baseline(ai, aj, aa, pkg, nx, ny, nz_global, out["its"],
-                                                       args.gamg_cpu_iters)
+            out["cpu_baseline"] = cpu_cg_gamg_baseline(ai, aj, aa, pkg, nx, ny, nz_global)
         return out
 
     cg = None
@@ -455,6 +485,9 @@ def main():
     cg_gamg = None
     if not args.no_gamg and not distributed:
         cg_gamg = guarded("cg_gamg", single_cg_gamg)
+    host_vec = None
+    if not distributed and not args.no_host_vec:
+        host_vec = guarded("host_vec", lambda: host_vec_mult(A, x_h))
 
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
@@ -520,6 +553,8 @@ def main():
             out["cg"] = cg
         if cg_gamg is not None:
             out["cg_gamg"] = cg_gamg
+        if host_vec is not None:
+            out["host_vec"] = host_vec
         if not args.no_cpu_baseline and not distributed:
             t_cpu, reps, _ = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds)
             out["cpu_baseline"] = {

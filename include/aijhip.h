@@ -164,6 +164,13 @@ enum {
                                        q-th eighth of x (its L2 then holds the
                                        x range of their scattered gathers);
                                        0: segment order. Same results        */
+    AIJHIP_OPT_HOST_PIPELINE = 10,  /* aijhip_mat_mult_host: -1 (default) x
+                                       uploads in ~983,040-row chunks while
+                                       the row blocks whose columns have
+                                       arrived multiply and their y chunks
+                                       download (step3/step4 analogue); k > 0:
+                                       chunks of >= k rows; 0: the serial
+                                       step-2 form. Same results              */
     AIJHIP_OPT_LONG_OVERLAP = 9     /* 1: long-row segments run on a side
                                        stream concurrently with the row
                                        blocks (forked from and joined back to
@@ -196,7 +203,11 @@ int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y,
                               void *stream);
 
 /* Step-2 semantics with host vectors: x (host fp64[n]) is copied in, y
- * (host fp64[m]) copied out; returns after y is on the host. */
+ * (host fp64[m]) copied out; returns after y is on the host. The copies are
+ * pipelined with the product (AIJHIP_OPT_HOST_PIPELINE, the reference's
+ * step3/step4: src/openacc-step4/MatMult_SeqAIJ.patch:51-91): host arrays
+ * that are already pinned (hipHostMalloc / hipHostRegister) are DMA'd
+ * directly, pageable ones through pinned staging slots. */
 int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y);
 
 int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info);

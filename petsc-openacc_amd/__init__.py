@@ -33,7 +33,7 @@ if os.environ.get("AIJHIP_LIB"):
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
 OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3, "persistent": 4, "clamped": 5, "exact": 6, "x_tile": 7,
-           "long_xcd": 8, "long_overlap": 9}
+           "long_xcd": 8, "long_overlap": 9, "host_pipeline": 10}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 
@@ -241,12 +241,16 @@ class SeqAIJHIP:
         _check(lib().aijhip_mat_mult_transpose(self._h, _dev_ptr(x, self.m, "x"),
                                                _dev_ptr(y, self.n, "y"), _stream_handle(stream)))
 
-    def mult_host(self, x: np.ndarray) -> np.ndarray:
-        """Step-2 semantics: host x in, host y out (copies over PCIe)."""
+    def mult_host(self, x: np.ndarray, out: np.ndarray | None = None) -> np.ndarray:
+        """Step-2 semantics: host x in, host y out (copies over PCIe,
+        pipelined with the product as steps 3/4 do; pinned arrays, e.g. numpy
+        views of torch pin_memory tensors, are DMA'd without staging)."""
         x = np.ascontiguousarray(x, dtype=np.float64)
         if x.shape[0] < self.n:
             raise ValueError("x too short")
-        y = np.empty(self.m)
+        y = np.empty(self.m) if out is None else out
+        if y.shape[0] < self.m:
+            raise ValueError("out too short")
         _check(lib().aijhip_mat_mult_host(self._h, _np_ptr(x, np.float64), _np_ptr(y, np.float64)))
         return y
 

@@ -24,7 +24,7 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
 HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "ksp.hip", "poisson.hip", "gamg_device.hip", "vec.hip",
-               "ksp_mpi.hip"]
+               "ksp_mpi.hip", "host_pipe.cpp"]
 HOST_SOURCES = ["harness.cpp", "gamg_setup.cpp"]
 ARCH = os.environ.get("AIJHIP_ARCH", "gfx950")
 
@@ -128,15 +128,15 @@ def build_main_ksp(force: bool = False) -> Path:
 
 
 def build_oracle(force: bool = False) -> Path:
-    src = ORACLE_DIR / "matmult_seqaij.c"
-    if not force and not _stale(ORACLE_LIB, [src]):
+    srcs = [ORACLE_DIR / "matmult_seqaij.c", ORACLE_DIR / "cg_gamg.c"]
+    if not force and not _stale(ORACLE_LIB, srcs):
         return ORACLE_LIB
     tmp = ORACLE_LIB.with_suffix(".so.tmp")
     # -ffp-contract=off: each product is rounded before it is added (PETSc's
     # x86 build has no FMA at -march=x86-64 either).
-    _run(["gcc", "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-o", str(tmp), str(src)])
+    _run(["gcc", "-O2", "-fPIC", "-shared", "-fopenmp", "-ffp-contract=off", "-o", str(tmp), *map(str, srcs), "-lm"])
     os.replace(tmp, ORACLE_LIB)
-    _stamp(ORACLE_LIB, [src])
+    _stamp(ORACLE_LIB, srcs)
     return ORACLE_LIB
 
 

@@ -76,6 +76,7 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_tile_coord);
     hipFree(P.d_carry_row);
     hipFree(P.d_carry_val);
+    aijhip::host_pipe_free(P.hpipe);
     P = aijhip::Plan();
 }
 
@@ -563,6 +564,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
         case AIJHIP_OPT_LONG_OVERLAP: t.long_overlap = value != 0; break;
+        case AIJHIP_OPT_HOST_PIPELINE:
+            if (value < -1) return fail(AIJHIP_ERR_ARG, "host_pipeline: -1 auto, 0 serial, k > 0 chunk rows");
+            t.host_chunk = value;
+            break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -662,16 +667,9 @@ int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y) {
     if (e == hipSuccess && !A->d_xstage) e = dmalloc(&A->d_xstage, (size_t)A->n, &A->device_bytes);
     if (e == hipSuccess && !A->d_ystage) e = dmalloc(&A->d_ystage, (size_t)A->m, &A->device_bytes);
     if (e != hipSuccess) return hipfail(e, "host staging");
-    // step2 MatMult patch:24 (x H2D), :27-40 (kernel), :29 (y D2H)
-    if (A->n > 0 &&
-        (e = hipMemcpyAsync(A->d_xstage, x, sizeof(double) * (size_t)A->n, hipMemcpyHostToDevice, A->host_stream)) != hipSuccess)
-        return hipfail(e, "copy x in");
-    rc = mult_impl(A, A->d_xstage, nullptr, A->d_ystage, false, A->host_stream);
-    if (rc) return rc;
-    if ((e = hipMemcpyAsync(y, A->d_ystage, sizeof(double) * (size_t)A->m, hipMemcpyDeviceToHost, A->host_stream)) != hipSuccess ||
-        (e = hipStreamSynchronize(A->host_stream)) != hipSuccess)
-        return hipfail(e, "copy y out");
-    return AIJHIP_OK;
+    // step2 MatMult patch:24 (x H2D), :27-40 (kernel), :29 (y D2H), pipelined
+    // as steps 3/4 overlap them (host_pipe.cpp)
+    return aijhip::host_pipe_mult(A, x, y);
 }
 
 int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {

@@ -96,7 +96,11 @@ struct Tuning {
                            // -1 when half the blocks fit
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
     bool long_overlap = false;  // long-row segments on a side stream, concurrent with the row blocks
+    int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
+                           // k > 0 pipelined in chunks of >= k rows
 };
+
+struct HostPipe;  // host-vector MatMult pipeline state (host_pipe.cpp)
 
 // STREAM blocks whose mean row length exceeds this use several lanes per row
 // in the reduction phase (reordered sum) unless Tuning::exact is set. Measured
@@ -146,6 +150,7 @@ struct Plan {
     int2 *d_carry_row = nullptr;   // per tile: row of its carry-out (or -1)
     double *d_carry_val = nullptr;
     int64_t bytes = 0;  // device bytes held by the plan
+    HostPipe *hpipe = nullptr;  // built on the first host-vector MatMult
 };
 
 }  // namespace aijhip
@@ -233,6 +238,16 @@ hipError_t gather_lines_per_entry(const aijhip_mat &A, double *out);
 int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa);
 // Number of device column indices outside [0, n) (synchronous).
 hipError_t count_bad_columns(const int32_t *d_aj, int64_t nz, int32_t n, int64_t *bad);
+
+// y = A x over the STREAM row blocks [b0, b0 + nb) only (default speed
+// knobs; full-row, no long rows).
+hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, const double *x, double *y,
+                                hipStream_t s);
+// Host-vector MatMult (aijhip_mat_mult_host), host_pipe.cpp: x uploaded in
+// chunks while the row blocks whose columns have arrived multiply and their y
+// chunks download (step-3/4 analogue). Returns an AIJHIP_* code.
+int host_pipe_mult(aijhip_mat *A, const double *x, double *y);
+void host_pipe_free(HostPipe *p);
 
 // Sets the calling thread's aijhip_last_error() message.
 void set_error(const std::string &msg);

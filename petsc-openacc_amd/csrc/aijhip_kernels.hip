@@ -971,6 +971,29 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     return hipGetLastError();
 }
 
+hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, const double *x, double *y,
+                                hipStream_t s) {
+    const Plan &P = A.plan;
+    if (P.kernel != AIJHIP_KERNEL_STREAM || A.compressed || P.n_longs > 0 || b0 < 0 || b0 + nb > P.n_blocks)
+        return hipErrorInvalidValue;
+    if (nb <= 0) return hipSuccess;
+    static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
+#define AIJHIP_BG(G)                                                                                            \
+    case G:                                                                                                     \
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, OpMult<false>>), dim3(nb), \
+                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks + b0, nb, 0, (int)P.tune.exact,       \
+                           A.d_ai, nullptr, A.d_aj, A.d_aa, OpMult<false>{x, nullptr, y, false}, nullptr, nullptr, \
+                           nullptr);                                                                             \
+        break
+    switch (P.tune.geom) {
+        AIJHIP_BG(0); AIJHIP_BG(1); AIJHIP_BG(2); AIJHIP_BG(3); AIJHIP_BG(4);
+        AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8);
+        default: return hipErrorInvalidValue;
+    }
+#undef AIJHIP_BG
+    return hipGetLastError();
+}
+
 hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
                          hipStream_t s, bool nt) {
     if (nt) return launch_stream_op(A, OpMgPre<true>{b, dinv, x, r}, nullptr, s);

@@ -32,7 +32,8 @@
  *
  * Vectors: PETSc 3.7 Vecs are host arrays, so MatMult has the reference's
  * step-2 semantics (matrix resident on the device, x in and y out over PCIe
- * per call: aijhip_mat_mult_host). MatMultAdd / MatMultTranspose stay on
+ * per call: aijhip_mat_mult_host, which pipelines the two copies with the
+ * product the way steps 3/4 do). MatMultAdd / MatMultTranspose stay on
  * the CPU, as in the reference. A device Vec type is what removes the PCIe
  * traffic.
  */
@@ -64,8 +65,12 @@ static PetscErrorCode AIJHIPDevice(Mat A, int *dev)
 
 /* The device half of MatAssemblyEnd (step2 MatAssemblyEnd patch:17-44):
  * first assembly uploads; same nonzero structure -> new values only;
- * changed structure -> drop and re-upload. Flush assembly does nothing. */
-static PetscErrorCode AIJHIPUpload(Mat A, MatAssemblyType mode)
+ * changed structure -> drop and re-upload. Flush assembly does nothing.
+ * bump: 1 when called from inside ops->assemblyend — PETSc's MatAssemblyEnd
+ * raises the object state once more after the hook returns, so the state the
+ * upload corresponds to is the current one + 1 (else the first MatMult would
+ * see a "changed" matrix and upload every value a second time). */
+static PetscErrorCode AIJHIPUpload(Mat A, MatAssemblyType mode, PetscObjectState bump)
 {
   Mat_SeqAIJ     *a = (Mat_SeqAIJ*)A->data;
   Mat_AIJHIP     *d = (Mat_AIJHIP*)A->spptr;
@@ -89,6 +94,7 @@ static PetscErrorCode AIJHIPUpload(Mat A, MatAssemblyType mode)
   if (rc) SETERRQ1(PetscObjectComm((PetscObject)A), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
   d->nonzerostate = A->nonzerostate;
   ierr = PetscObjectStateGet((PetscObject)A, &d->state);CHKERRQ(ierr);
+  d->state += bump;
   PetscFunctionReturn(0);
 }
 
@@ -120,7 +126,7 @@ static PetscErrorCode AIJHIPMult(Mat A, Vec xx, Vec yy)
   ierr = PetscObjectStateGet((PetscObject)A, &state);CHKERRQ(ierr);
   if (!d || !d->h || d->state != state) { /* never uploaded, or host values changed since */
     if (!A->assembled) SETERRQ(PetscObjectComm((PetscObject)A), PETSC_ERR_ARG_WRONGSTATE, "aijhip: MatMult on an unassembled matrix");
-    ierr = AIJHIPUpload(A, MAT_FINAL_ASSEMBLY);CHKERRQ(ierr);
+    ierr = AIJHIPUpload(A, MAT_FINAL_ASSEMBLY, 0);CHKERRQ(ierr);
     d = (Mat_AIJHIP*)A->spptr;
   }
   ierr = VecGetArrayRead(xx, &x);CHKERRQ(ierr);
@@ -145,7 +151,11 @@ static PetscErrorCode MatAssemblyEnd_SeqAIJHIP(Mat A, MatAssemblyType mode)
 
   PetscFunctionBegin;
   ierr = (*seqaij_assemblyend)(A, mode);CHKERRQ(ierr); /* compaction, compressed rows, inodes */
-  ierr = AIJHIPUpload(A, mode);CHKERRQ(ierr);
+  /* MatAssemblyEnd_SeqAIJ_Inode [ext] points ops->mult at MatMult_SeqAIJ_Inode
+   * when it finds identical-pattern rows (multi-dof FEM operators such as
+   * Flan_1565): take MatMult back, or such matrices would multiply on the CPU */
+  A->ops->mult = AIJHIPMult;
+  ierr = AIJHIPUpload(A, mode, 1);CHKERRQ(ierr);
   PetscFunctionReturn(0);
 }
 
@@ -218,13 +228,16 @@ PETSC_EXTERN PetscErrorCode PetscDLLibraryRegister_aijhip_petsc(void)
 #include "original/MatDestroy_SeqAIJ.c"
 #undef MatDestroy_SeqAIJ
 
+PetscErrorCode MatMult_SeqAIJ(Mat, Vec, Vec);
+
 PetscErrorCode MatAssemblyEnd_SeqAIJ(Mat A, MatAssemblyType mode)
 {
   PetscErrorCode ierr;
 
   PetscFunctionBegin;
   ierr = MatAssemblyEnd_SeqAIJ_Original(A, mode);CHKERRQ(ierr);
-  ierr = AIJHIPUpload(A, mode);CHKERRQ(ierr);
+  A->ops->mult = MatMult_SeqAIJ; /* the inode check may have installed MatMult_SeqAIJ_Inode */
+  ierr = AIJHIPUpload(A, mode, 1);CHKERRQ(ierr);
   PetscFunctionReturn(0);
 }
 

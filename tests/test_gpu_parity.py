@@ -241,6 +241,37 @@ def test_mult_host_step2_semantics(pkg, dev):
         assert_bits(y, g["y"])
 
 
+@pytest.mark.parametrize("operand,chunk", [("poisson", 5000), ("poisson", -1), ("poisson", 0), ("random", 3000)])
+def test_mult_host_pipeline_bitwise(pkg, dev, operand, chunk):
+    """The host-vector MatMult (step-3/4 analogue, host_pipe.cpp) with many
+    chunks, the default chunking and the serial form, on a banded operand
+    and a scattered one (every row chunk waits for all of x): bit-identical
+    to the device-vector product, with pageable and with pinned host arrays."""
+    if operand == "poisson":
+        ai, aj, aa = pkg.poisson_csr(40, 40, 40)
+    else:
+        rng = np.random.default_rng(7)  # columns anywhere: every row chunk needs all of x
+        m, k = 60000, 9
+        ai = np.arange(m + 1, dtype=np.int32) * k
+        aj = np.sort(rng.integers(0, m, size=(m, k)), axis=1).astype(np.int32).ravel()
+        aa = rng.standard_normal(m * k)
+    n = len(ai) - 1
+    x = seqaij.splitmix_uniform(n, 42)
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        if A.info()["n_long_rows"]:
+            pytest.skip("long rows take the serial form")
+        A.set_option("host_pipeline", chunk)
+        y_dev = torch.empty(n, dtype=torch.float64, device=dev)
+        A.mult(to_dev(x, dev), y_dev)
+        ref = y_dev.cpu().numpy()
+        assert_bits(A.mult_host(x), ref)
+        assert_bits(A.mult_host(x), ref)  # staging reused
+        xp = torch.from_numpy(x).pin_memory()
+        yp = torch.full((n,), float("nan"), dtype=torch.float64).pin_memory()
+        A.mult_host(xp.numpy(), out=yp.numpy())
+        assert_bits(yp.numpy(), ref)
+
+
 def test_alias_rejected(pkg, dev):
     g = golden("poisson4")
     with pkg.SeqAIJHIP(g["ai"], g["aj"], g["aa"]) as A:

@@ -73,3 +73,30 @@ def test_splitmix_known_values():
     x = seqaij.splitmix_uniform(4, seed=42)
     assert np.all((x >= -1) & (x < 1))
     assert len(set(x.tolist())) == 4
+
+
+def test_host_cg_gamg_matches_numpy_restatement():
+    """oracle/cg_gamg.c (the measured host CG+GAMG baseline) against
+    oracle/ksp_cg.py + oracle/gamg.py's V-cycle on the same host hierarchy."""
+    import importlib
+
+    import scipy.sparse as sp
+
+    from oracle import gamg as ogamg
+    from oracle import host_cg_gamg, ksp_cg, seqaij
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    ai, aj, aa, rhs, exact = seqaij.create_system(14, 14, 14)
+    lv = G.build_host(ai, aj, aa)
+    levels = [dict(A=sp.csr_matrix((aa, aj, ai), shape=(lv[0]["m"],) * 2))]
+    for l in range(1, len(lv)):
+        a_i, a_j, a_a = lv[l]["A"]
+        levels.append(dict(A=sp.csr_matrix((a_a, a_j, a_i), shape=(lv[l]["m"],) * 2)))
+        p_i, p_j, p_a = lv[l - 1]["P"]
+        levels[l - 1]["P"] = sp.csr_matrix((p_a, p_j, p_i), shape=(lv[l - 1]["m"], lv[l]["m"]))
+    xo, its_o, reason_o, hist_o = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-12, atol=1e-50,
+                                            pc=lambda r: ogamg.vcycle(levels, r))
+    for threads in (1, 3):
+        h = host_cg_gamg.solve(ai, aj, aa, rhs, rtol=1e-12, atol=1e-50, threads=threads, levels=lv)
+        assert h["reason"] == reason_o and abs(h["its"] - its_o) <= 1
+        np.testing.assert_allclose(h["hist"][:its_o], hist_o[:its_o], rtol=1e-8)
+        assert np.linalg.norm(h["x"] - xo) <= 1e-9 * np.linalg.norm(xo)
