@@ -205,6 +205,28 @@ def host_vec_mult(A, x_h, reps=10):
     return out
 
 
+def read_ceiling(nbytes, dev, reps=20):
+    """The achievable HBM read rate on this box, timed in the same run:
+    aijhip_read_probe over a buffer of the SpMV's byte count (16-B loads,
+    each byte once per launch), mean of `reps` launches by HIP events."""
+    import torch
+    ksp = importlib.import_module("petsc-openacc_amd.ksp")
+    L = ksp._veclib()
+    buf = torch.ones(nbytes // 8, dtype=torch.float64, device=dev)
+    s = torch.cuda.current_stream()
+    for _ in range(3):
+        L.aijhip_read_probe(buf.data_ptr(), buf.numel(), s.cuda_stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(s)
+        L.aijhip_read_probe(buf.data_ptr(), buf.numel(), s.cuda_stream)
+        b.record(s)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    del buf
+    return round(nbytes / (ms / 1e3) / 1e9, 1), round(ms * 1e3, 2)
+
+
 def pmc_traffic(rows, nnz, block):
     """HBM bytes per launch from the committed rocprofv3 PMC record
     (profiles/pmc_latest.json, written from tools/gpu_pmc.sh), used only
@@ -489,6 +511,10 @@ def main():
     if not distributed and not args.no_host_vec:
         host_vec = guarded("host_vec", lambda: host_vec_mult(A, x_h))
 
+    ceiling = None
+    if not distributed:
+        ceiling = guarded("read_ceiling", lambda: read_ceiling(bytes_local, dev))
+
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
         mean_launch_s = float(np.mean(launch_ms)) / 1e3
@@ -535,6 +561,10 @@ def main():
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
+        if isinstance(ceiling, tuple):  # same-run flat-read ceiling: fraction of what HBM delivers here
+            out["roofline"]["ceiling_flat_read"] = {
+                "GBs": ceiling[0], "us": ceiling[1], "frac_of_ceiling": round(achieved / ceiling[0], 4),
+                "probe": "aijhip_read_probe: the SpMV's byte count read once with 16-B loads"}
         if distributed:  # whole-job rate against N HBM peaks (roofline.frac is rank 0's kernel alone)
             out["aggregate_roofline_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
             ci = comm.info()

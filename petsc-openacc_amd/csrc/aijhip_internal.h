@@ -43,6 +43,8 @@ constexpr StreamGeom kStreamGeoms[] = {
     {512, 4094, 512},    // 6: 8 waves, 4 pair-iterations (measured best)
     {1024, 8190, 1024},  // 7: 16 waves, 4 pair-iterations
     {256, 2046, 256},    // 8: 4 waves, 4 pair-iterations
+    {512, 6142, 512},    // 9: 8 waves, 6 pair-iterations, 48 KiB: an x tile of a +-2100-column band fits
+    {512, 8190, 512},    // 10: 8 waves, 8 pair-iterations, 64 KiB
 };
 constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
 constexpr int kMaxStreamNnzCap = 8192;

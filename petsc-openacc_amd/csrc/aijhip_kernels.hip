@@ -955,7 +955,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
-    static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 11, "update the geometry dispatch");
 #define AIJHIP_OG(G)                                                                                      \
     case G:                                                                                               \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
@@ -964,7 +964,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
-        AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8);
+        AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8); AIJHIP_OG(9); AIJHIP_OG(10);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_OG
@@ -977,7 +977,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
     if (P.kernel != AIJHIP_KERNEL_STREAM || A.compressed || P.n_longs > 0 || b0 < 0 || b0 + nb > P.n_blocks)
         return hipErrorInvalidValue;
     if (nb <= 0) return hipSuccess;
-    static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 11, "update the geometry dispatch");
 #define AIJHIP_BG(G)                                                                                            \
     case G:                                                                                                     \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, OpMult<false>>), dim3(nb), \
@@ -987,7 +987,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
         break
     switch (P.tune.geom) {
         AIJHIP_BG(0); AIJHIP_BG(1); AIJHIP_BG(2); AIJHIP_BG(3); AIJHIP_BG(4);
-        AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8);
+        AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8); AIJHIP_BG(9); AIJHIP_BG(10);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_BG
@@ -1043,14 +1043,14 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     }
     // Every geometry is dispatched explicitly: the kernel's LDS size must be
     // the one the plan's row blocks were cut for.
-    static_assert(kNumStreamGeoms == 9, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 11, "update the geometry dispatch");
     const int g = P.tune.geom;
     if (P.n_blocks > 0 && P.tune.persist > 0 && kStreamGeoms[g].rows == kStreamGeoms[g].threads) {
 #define AIJHIP_PG(G) \
     case G: pipe_dispatch<kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap>(A, L, x, z, y, add, s); break
         switch (g) {
             AIJHIP_PG(0); AIJHIP_PG(1); AIJHIP_PG(3); AIJHIP_PG(4); AIJHIP_PG(5);
-            AIJHIP_PG(6); AIJHIP_PG(7); AIJHIP_PG(8);
+            AIJHIP_PG(6); AIJHIP_PG(7); AIJHIP_PG(8); AIJHIP_PG(9); AIJHIP_PG(10);
             default: return hipErrorInvalidValue;
         }
 #undef AIJHIP_PG
@@ -1059,7 +1059,7 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
 #define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, L, x, z, y, add, s, dpart, stop); break
         switch (g) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
-            AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8);
+            AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10);
             default: return hipErrorInvalidValue;
         }
 #undef AIJHIP_SG

@@ -130,6 +130,27 @@ double *partials(hipError_t *e) {
     return per_dev[dev];
 }
 
+// HBM read ceiling: n doubles read once, in the STREAM kernel's access shape
+// (a 512-lane workgroup per contiguous 32 KiB tile, four 16-B loads per lane
+// issued before any use), a partial sum per workgroup so no load is dropped.
+constexpr int kProbeThreads = 512, kProbeIters = 4;
+__global__ __launch_bounds__(kProbeThreads) void k_read_probe(int64_t n2, const double2 *__restrict__ v,
+                                                              double *part) {
+    __shared__ double scratch[kProbeThreads / 64];
+    const int64_t base = (int64_t)blockIdx.x * kProbeThreads * kProbeIters + threadIdx.x;
+    double2 r[kProbeIters];
+#pragma unroll
+    for (int it = 0; it < kProbeIters; ++it) {
+        const int64_t i = base + (int64_t)it * kProbeThreads;
+        r[it] = i < n2 ? v[i] : make_double2(0.0, 0.0);
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int it = 0; it < kProbeIters; ++it) s += r[it].x + r[it].y;
+    const double t = bsum<kProbeThreads>(s, scratch);
+    if (threadIdx.x == 0) part[blockIdx.x & (kMaxBlocks - 1)] = t;
+}
+
 int grid_for(int64_t n) {
     return (int)std::max<int64_t>(1, std::min<int64_t>((n + kThreads - 1) / kThreads, kMaxBlocks));
 }
@@ -190,6 +211,18 @@ int aijhip_vec_jacobi(int64_t n, const double *r, const double *dinv, double *z,
     hipLaunchKernelGGL(k_jacobi, dim3(nb), dim3(kThreads), 0, s, n, r, dinv, z, part);
     hipLaunchKernelGGL(k_finish, dim3(1), dim3(kRedThreads), 0, s, part, nb, 3, d_result);
     return vhip(hipGetLastError(), "vec_jacobi");
+}
+
+int aijhip_read_probe(const double *d_buf, int64_t n, void *stream) {
+    if (n < 0 || (n > 0 && !d_buf) || ((uintptr_t)d_buf & 15)) return verr(AIJHIP_ERR_ARG, "read_probe: bad arguments");
+    if (n < 2) return AIJHIP_OK;
+    hipError_t e;
+    double *part = partials(&e);
+    if (!part) return vhip(e, "read_probe scratch");
+    const int64_t n2 = n / 2, per = (int64_t)kProbeThreads * kProbeIters;
+    hipLaunchKernelGGL(k_read_probe, dim3((unsigned)((n2 + per - 1) / per)), dim3(kProbeThreads), 0,
+                       (hipStream_t)stream, n2, reinterpret_cast<const double2 *>(d_buf), part);
+    return vhip(hipGetLastError(), "read_probe");
 }
 
 int aijhip_mat_jacobi_inverse(aijhip_mat_t A, double *d_dinv, void *stream) {

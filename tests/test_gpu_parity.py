@@ -115,7 +115,7 @@ def test_stream_multilane_long_rows(pkg, dev, row_len):
     assert_bits(y1, y_ref)
 
 
-@pytest.mark.parametrize("geometry", [1, 6, 0])
+@pytest.mark.parametrize("geometry", [1, 6, 0, 9, 10])
 def test_stream_x_tile_banded(pkg, dev, geometry):
     """x staged in LDS (x_tile=1) for blocks of a banded matrix: bit-exact,
     and the blocks that do not fit (a wide row every 997) fall back to HBM
@@ -404,7 +404,7 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
         xd = to_dev(g["x"], dev)
         yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
         first = None
-        for geom in range(9):
+        for geom in range(11):
             for xcd, nt, persist, clamped in ((0, 0, 0, 0), (1, 0, 0, 1), (0, 1, 0, 0), (22, 1, 0, 1), (3, 0, 0, 0),
                                               (0, 0, 1, 0), (0, 1, 2, 0), (0, 0, 5, 0), (0, 0, 0, 1)):
                 if persist and geom == 2:

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--grid", type=int, default=300)
     ap.add_argument("--its", type=int, default=50)
     ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--opt", action="append", default=[], help="set_option NAME=VALUE (repeatable)")
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
     K = importlib.import_module("petsc-openacc_amd.ksp")
@@ -44,6 +45,9 @@ def main():
             ai = np.concatenate([[0], np.cumsum(np.where(ln <= 1000, ln, 0))]).astype(np.int32)
             aj, aa = aj[keep], aa[keep]
         A = pkg.SeqAIJHIP(ai, aj, aa, kernel=args.kernel, exact=args.exact)
+        for o in args.opt:
+            k, v = o.split("=")
+            A.set_option(k, int(v))
         x = torch.from_numpy(pkg.splitmix_uniform(A.n, 42)).to(dev)
         y = torch.empty(A.m, dtype=torch.float64, device=dev)
         for _ in range(args.its):

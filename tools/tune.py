@@ -97,6 +97,9 @@ def main():
     if args.variants == "xtile":
         for g, xt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
+    if args.variants == "xtile_band":  # LDS x tiles of a +-2100-column band (geometries 9/10 fit it)
+        for g, xt in ((1, 0), (6, 0), (9, 0), (9, 1), (10, 0), (10, 1)):
+            variants.append(("stream", dict(geometry=g, x_tile=xt)))
     if args.variants == "xtile_big":  # larger blocks amortise the tile load over more entries
         for g, xt in ((1, 0), (7, 0), (7, 1), (4, 0), (4, 1), (6, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
