@@ -33,6 +33,7 @@
 #include <stdint.h>
 
 #include "aijhip.h"
+#include "aijhip_gamg.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -108,12 +109,18 @@ int aijhip_mpiaij_destroy(aijhip_mpiaij_t M);
 
 /* ------------------------------------------------- KSPSolve_CG over it */
 
-/* KSPCG on the distributed operator; PC none or Jacobi (PETSc's bjacobi +
- * jacobi sub-PC on each rank: the inverse diagonal of A_d). Options,
- * reasons and norms as aijhip_ksp.h; defaults as PETSc. */
+/* KSPCG on the distributed operator. PC (aijhip_ksp.h values): NONE; JACOBI
+ * = PETSc's bjacobi + jacobi sub-PC (the inverse diagonal of A_d); GAMG =
+ * bjacobi + gamg sub-PC (-pc_type bjacobi -sub_pc_type gamg): each rank's
+ * diagonal block gets its own smoothed-aggregation hierarchy
+ * (aijhip_ksp.h's set-up, parameters from aijhip_kspmpi_set_gamg_params) and
+ * one V-cycle per application, with no communication inside the PC; at one
+ * rank it is PCGAMG itself. Options, reasons and norms as aijhip_ksp.h;
+ * defaults as PETSc. */
 int aijhip_kspmpi_create(aijhip_mpiaij_t M, aijhip_kspmpi_t *out);
 int aijhip_kspmpi_set_tolerances(aijhip_kspmpi_t K, double rtol, double abstol, double dtol, int32_t max_it);
 int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc_type);
+int aijhip_kspmpi_set_gamg_params(aijhip_kspmpi_t K, const aijhip_gamg_params_t *p);
 int aijhip_kspmpi_set_norm_type(aijhip_kspmpi_t K, int norm_type);
 /* Iterations launched between two host polls of the device stop flag
  * (default 8). Every kernel of an iteration is a no-op once the flag is set,

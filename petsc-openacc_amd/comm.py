@@ -41,6 +41,7 @@ MPI_SYMBOLS = (
     "aijhip_comm_allreduce_sum", "aijhip_comm_set_timeout", "aijhip_comm_destroy",
     "aijhip_mpiaij_create", "aijhip_mpiaij_mult", "aijhip_mpiaij_get_ghost", "aijhip_mpiaij_destroy",
     "aijhip_kspmpi_create", "aijhip_kspmpi_set_tolerances", "aijhip_kspmpi_set_pc_type",
+    "aijhip_kspmpi_set_gamg_params",
     "aijhip_kspmpi_set_norm_type", "aijhip_kspmpi_set_poll_interval", "aijhip_kspmpi_solve",
     "aijhip_kspmpi_get_iteration_number", "aijhip_kspmpi_get_residual_norm", "aijhip_kspmpi_get_converged_reason",
     "aijhip_kspmpi_get_residual_history", "aijhip_kspmpi_get_host_syncs", "aijhip_kspmpi_destroy",
@@ -68,6 +69,7 @@ def _lib():
         L.aijhip_kspmpi_create.argtypes = [_P, ctypes.POINTER(_P)]
         L.aijhip_kspmpi_set_tolerances.argtypes = [_P, _d, _d, _d, _i32]
         L.aijhip_kspmpi_set_pc_type.argtypes = [_P, ctypes.c_int]
+        L.aijhip_kspmpi_set_gamg_params.argtypes = [_P, _P]
         L.aijhip_kspmpi_set_norm_type.argtypes = [_P, ctypes.c_int]
         L.aijhip_kspmpi_set_poll_interval.argtypes = [_P, _i32]
         L.aijhip_kspmpi_solve.argtypes = [_P, _P, _P, _P]
@@ -245,7 +247,9 @@ class KSPCGMPINative:
     (bjacobi + jacobi per rank), every scalar decision on the device."""
 
     def __init__(self, op: NativeMPIAIJ, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
-                 norm="preconditioned", poll: int = 8):
+                 norm="preconditioned", poll: int = 8, gamg=None):
+        """pc: "none", "jacobi" (bjacobi + jacobi) or "gamg" (bjacobi + gamg:
+        a GAMG hierarchy per rank's diagonal block; gamg = its parameters)."""
         K = importlib.import_module("petsc-openacc_amd.ksp")
         L = _lib()
         self.op = op
@@ -253,6 +257,10 @@ class KSPCGMPINative:
         _pkg._check(L.aijhip_kspmpi_create(op._h, ctypes.byref(self._h)))
         self.set_tolerances(rtol, atol, dtol, max_it)
         _pkg._check(L.aijhip_kspmpi_set_pc_type(self._h, K.PC_TYPES[pc]))
+        if gamg:
+            G = importlib.import_module("petsc-openacc_amd.gamg")
+            self._gp = G.default_params(**gamg)
+            _pkg._check(L.aijhip_kspmpi_set_gamg_params(self._h, ctypes.byref(self._gp)))
         _pkg._check(L.aijhip_kspmpi_set_norm_type(self._h, K.NORM_TYPES[norm]))
         _pkg._check(L.aijhip_kspmpi_set_poll_interval(self._h, int(poll)))
 

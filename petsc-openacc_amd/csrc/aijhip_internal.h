@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "aijhip.h"
+#include "aijhip_ksp.h"
 #include "host_alloc.h"
 
 namespace aijhip {
@@ -250,6 +251,13 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
 // chunks download (step-3/4 analogue). Returns an AIJHIP_* code.
 int host_pipe_mult(aijhip_mat *A, const double *x, double *y);
 void host_pipe_free(HostPipe *p);
+
+// The V-cycle of a set-up GAMG KSP (ksp.hip) as a preconditioner of another
+// solver (the distributed CG's block-Jacobi sub-PC, ksp_mpi.hip): x = B b on
+// `s`. When the finest post-smoothing carried the z.z / z.b partials, *dots
+// points at them (2 x *nbz doubles), else NULL.
+hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t s, const double **dots,
+                         int *nbz);
 
 // Sets the calling thread's aijhip_last_error() message.
 void set_error(const std::string &msg);

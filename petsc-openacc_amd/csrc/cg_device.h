@@ -248,6 +248,27 @@ __global__ __launch_bounds__(kVecThreads) void k_dot(int64_t n, const double *__
     if (threadIdx.x == 0) part[blockIdx.x] = v;
 }
 
+// partials of a.a into slot sa and a.c into slot sc (sc < 0: skip)
+__global__ __launch_bounds__(kVecThreads) void k_dots(int64_t n, const double *__restrict__ a,
+                                                      const double *__restrict__ c, double *part, int sa,
+                                                      int sc, const CGState *S) {
+    __shared__ double scratch[kVecThreads / 64];
+    if (S && S->done) return;
+    double aa = 0.0, ac = 0.0;
+    GRID_STRIDE(i, n) {
+        const double ai = a[i];
+        aa += ai * ai;
+        if (sc >= 0) ac += ai * c[i];
+    }
+    const int nb = gridDim.x;
+    double v = bsum<kVecThreads>(aa, scratch);
+    if (threadIdx.x == 0) part[sa * nb + blockIdx.x] = v;
+    if (sc >= 0) {
+        v = bsum<kVecThreads>(ac, scratch);
+        if (threadIdx.x == 0) part[sc * nb + blockIdx.x] = v;
+    }
+}
+
 // K4: R -= a W; Jacobi / none: Z = D^-1 R (W and Z share storage: w[i] is
 // read before z[i] is written by the same lane); partials Z.Z, Z.R, R.R
 // (GAMG: R.R only, Z follows from the V-cycle). VecAXPY(X, a, P) is deferred

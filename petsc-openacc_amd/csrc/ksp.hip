@@ -37,27 +37,6 @@
 
 namespace {
 
-// partials of a.a into slot sa and a.c into slot sc (sc < 0: skip)
-__global__ __launch_bounds__(kVecThreads) void k_dots(int64_t n, const double *__restrict__ a,
-                                                      const double *__restrict__ c, double *part, int sa,
-                                                      int sc, const CGState *S) {
-    __shared__ double scratch[kVecThreads / 64];
-    if (S && S->done) return;
-    double aa = 0.0, ac = 0.0;
-    GRID_STRIDE(i, n) {
-        const double ai = a[i];
-        aa += ai * ai;
-        if (sc >= 0) ac += ai * c[i];
-    }
-    const int nb = gridDim.x;
-    double v = bsum<kVecThreads>(aa, scratch);
-    if (threadIdx.x == 0) part[sa * nb + blockIdx.x] = v;
-    if (sc >= 0) {
-        v = bsum<kVecThreads>(ac, scratch);
-        if (threadIdx.x == 0) part[sc * nb + blockIdx.x] = v;
-    }
-}
-
 // K3 / K5 / init: this device's partials summed in a fixed order, then the
 // scalar step (cg_device.h).
 __global__ __launch_bounds__(kRedThreads) void k_reduce_init(const double *part, int nb, CGState *S,
@@ -382,6 +361,19 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
 }
 
 }  // namespace
+
+namespace aijhip {
+
+hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t s, const double **dots,
+                         int *nbz) {
+    bool done = false;
+    const hipError_t e = vcycle(K, b, x, s, K->d_mgpart, &done);
+    *dots = done ? K->d_mgpart : nullptr;
+    *nbz = done ? K->mg[0].A->plan.n_blocks : 0;
+    return e;
+}
+
+}  // namespace aijhip
 
 extern "C" {
 

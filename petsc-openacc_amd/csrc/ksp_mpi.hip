@@ -278,6 +278,22 @@ __global__ __launch_bounds__(kRedThreads) void k_local_dpi(const double *part, i
     else red[0] = v;
 }
 
+// GAMG sub-PC: zz, zr from pz[0, nbz) and pz[nbz, 2 nbz) (the V-cycle's fused
+// finest post-smoothing, or k_dots), rr from pr[0, nbr) — ksp.hip
+// k_reduce_iter's sums; step: apply step_iter here (one rank).
+__global__ __launch_bounds__(kRedThreads) void k_local_iter(const double *pz, int nbz, const double *pr, int nbr,
+                                                            double *red, int step, CGState *S, double *hist,
+                                                            CGParams p) {
+    __shared__ double scratch[kRedThreads / 64];
+    if (S->done) return;
+    const double zz = reduce_parts(pz, nbz, scratch);
+    const double zr = reduce_parts(pz + nbz, nbz, scratch);
+    const double rr = reduce_parts(pr, nbr, scratch);
+    if (threadIdx.x != 0) return;
+    if (step) step_iter(zz, zr, rr, S, hist, p);
+    else { red[0] = zz; red[1] = zr; red[2] = rr; }
+}
+
 __global__ void k_step_init(const double *red, CGState *S, double *hist, CGParams p) {
     if (threadIdx.x == 0) step_init(red[0], red[1], red[2], red[3], S, hist, p);
 }
@@ -444,6 +460,12 @@ struct aijhip_kspmpi {
     int normtype = AIJHIP_KSP_NORM_PRECONDITIONED;
     int32_t poll = 8;
     bool set_up = false, fused = false, vec_nt = true;
+    // PC GAMG = PETSc's -pc_type bjacobi -sub_pc_type gamg: a GAMG hierarchy of
+    // this rank's diagonal block (a single-GPU KSP's set-up), one V-cycle per
+    // application, no communication inside the preconditioner
+    aijhip_ksp_t sub = nullptr;
+    aijhip_gamg_params_t gamg{};
+    bool gamg_set = false;
     int vec_grid = 1, n_dparts = 1;
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr,
            *d_opart = nullptr, *d_red = nullptr, *d_hist = nullptr;
@@ -461,6 +483,8 @@ void kspmpi_free(aijhip_kspmpi *K) {
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
     hipFree(K->d_opart); hipFree(K->d_red); hipFree(K->d_hist); hipFree(K->d_state);
     if (K->h_state) hipHostFree(K->h_state);
+    if (K->sub) aijhip_ksp_destroy(K->sub);
+    K->sub = nullptr;
     K->d_dinv = K->d_r = K->d_z = K->d_p = K->d_part = K->d_opart = K->d_red = K->d_hist = nullptr;
     K->d_state = K->h_state = nullptr;
     K->set_up = false;
@@ -497,6 +521,16 @@ int kspmpi_set_up(aijhip_kspmpi *K) {
         if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess) {
             kspmpi_free(K);
             return mhip(e, "PCSetUp_Jacobi (distributed)");
+        }
+    }
+    if (K->pc == AIJHIP_PC_GAMG) {  // PCSetUp_BJacobi + the sub-PC's PCSetUp_GAMG on A_d
+        int rc = aijhip_ksp_create(A, &K->sub);
+        if (!rc) rc = aijhip_ksp_set_pc_type(K->sub, AIJHIP_PC_GAMG);
+        if (!rc && K->gamg_set) rc = aijhip_ksp_set_gamg_params(K->sub, &K->gamg);
+        if (!rc) rc = aijhip_ksp_set_up(K->sub);
+        if (rc) {
+            kspmpi_free(K);
+            return rc;
         }
     }
     K->set_up = true;
@@ -753,9 +787,18 @@ int aijhip_kspmpi_set_tolerances(aijhip_kspmpi_t K, double rtol, double abstol, 
 
 int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc) {
     if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
-    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI)
-        return mfail(AIJHIP_ERR_ARG, "distributed CG: PC none or jacobi");
+    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI && pc != AIJHIP_PC_GAMG)
+        return mfail(AIJHIP_ERR_ARG, "distributed CG: PC none, jacobi or gamg (block Jacobi with GAMG blocks)");
+    if (pc != K->pc) K->set_up = false;
     K->pc = pc;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_set_gamg_params(aijhip_kspmpi_t K, const aijhip_gamg_params_t *p) {
+    if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
+    K->gamg_set = p != nullptr;
+    if (p) K->gamg = *p;
+    if (K->pc == AIJHIP_PC_GAMG) K->set_up = false;
     return AIJHIP_OK;
 }
 
@@ -793,7 +836,15 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
     hipError_t e = hipSuccess;
     if (m > 0 && (e = hipMemsetAsync(x, 0, sizeof(double) * (size_t)m, s)) != hipSuccess) return mhip(e, "x = 0");
     // r = b, z = B r, then ||z|| etc. summed over all ranks
+    const bool gamg = K->pc == AIJHIP_PC_GAMG;
     hipLaunchKernelGGL(k_init, vg, vt, 0, s, m, b, K->d_r, K->d_z, dinv, K->d_part, p);
+    if (gamg) {  // z = B r, then its z.z, z.r partials (as ksp.hip with a zero guess)
+        const double *dots = nullptr;
+        int nbz = 0;
+        if ((e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, &dots, &nbz)) != hipSuccess)
+            return mhip(e, "GAMG V-cycle");
+        hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, nullptr);
+    }
     hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 4, K->d_red, multi ? 0 : 1, K->d_state,
                        K->d_hist, p);
     if (multi) {
@@ -808,7 +859,8 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
             return mhip(e, "KSPSolve poll");
         if ((rc = wait_stream(C, s))) return rc;
         if (K->h_state->done || launched >= K->max_it) break;
-        for (int j = 0; j < K->poll && launched < K->max_it; ++j, ++launched) {
+        const int32_t poll = gamg ? 1 : K->poll;  // the V-cycle does not stop at the flag
+        for (int j = 0; j < poll && launched < K->max_it; ++j, ++launched) {
             if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             // W = A P with the p.w partials (W shares Z's storage)
@@ -828,8 +880,22 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
             else
                 hipLaunchKernelGGL(k_update<false>, vg, vt, 0, s, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state,
                                    K->pc, K->d_p, nullptr);
-            hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 3, K->d_red, multi ? 0 : 2,
-                               K->d_state, K->d_hist, p);
+            if (gamg) {  // z = B r; z.z and z.r from the fused finest post-smoothing, else k_dots
+                const double *dots = nullptr;
+                int nbz = 0;
+                if ((e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, &dots, &nbz)) != hipSuccess)
+                    return mhip(e, "GAMG V-cycle");
+                if (!dots) {
+                    hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
+                    dots = K->d_part;
+                    nbz = nb;
+                }
+                hipLaunchKernelGGL(k_local_iter, dim3(1), rt, 0, s, dots, nbz, K->d_part + 2 * nb, nb, K->d_red,
+                                   multi ? 0 : 1, K->d_state, K->d_hist, p);
+            } else {
+                hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 3, K->d_red, multi ? 0 : 2,
+                                   K->d_state, K->d_hist, p);
+            }
             if (multi) {
                 if ((rc = comm_allreduce(C, K->d_red, 3, s))) return rc;
                 hipLaunchKernelGGL(k_step_iter, dim3(1), dim3(64), 0, s, K->d_red, K->d_state, K->d_hist, p);

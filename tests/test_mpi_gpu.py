@@ -68,7 +68,12 @@ def _worker(rank, world, port, dims, halo, q):
         with C.KSPCGMPINative(op_n.native, rtol=1e-10, max_it=1000, poll=3) as kn:
             kn.solve(b, xn)
             native = (xn.cpu().numpy(), kn.its, kn.reason, kn.hist.tolist())
-        q.put((rank, y.cpu().numpy(), xs.cpu().numpy(), cg.its, cg.reason, list(cg.hist), same, native))
+        xg = torch.full_like(b, float("nan"))  # CG + bjacobi/GAMG (one hierarchy per diagonal block)
+        with C.KSPCGMPINative(op_n.native, rtol=1e-10, max_it=1000, pc="gamg") as kg:
+            kg.solve(b, xg)
+            native_gamg = (xg.cpu().numpy(), kg.its, kg.reason, kg.hist.tolist())
+        q.put((rank, y.cpu().numpy(), xs.cpu().numpy(), cg.its, cg.reason, list(cg.hist), same, native,
+               native_gamg))
     finally:
         dist.destroy_process_group()
 
@@ -113,3 +118,29 @@ def test_gpu_mpiaij_and_cg_on_k_ranks(world, dims, halo):
     np.testing.assert_allclose(nat[0][3][:10], hist_o[:10], rtol=1e-9)
     xn = np.concatenate([n[0] for n in nat])
     assert np.linalg.norm(xn - xo) <= 1e-8 * np.linalg.norm(xo)
+    # CG + bjacobi/GAMG against the oracle CG preconditioned by one oracle
+    # V-cycle per rank's diagonal block (PETSc -pc_type bjacobi -sub_pc_type gamg)
+    import importlib
+    import scipy.sparse as sp
+    from oracle import gamg as ogamg
+    pkg = importlib.import_module("petsc-openacc_amd")
+    mp_mod = importlib.import_module("petsc-openacc_amd.mpiaij")
+    bounds = [mp_mod.slab_bounds(nz, world, r) for r in range(world)]
+    starts = [b[0] * nx * ny for b in bounds] + [nx * ny * nz]
+    blocks = []
+    for r in range(world):
+        lo, hi = starts[r], starts[r + 1]
+        (dai, daj, daa), _, _ = pkg.split_rows(*pkg.poisson_csr(nx, ny, nz, *bounds[r]), lo, hi)
+        blocks.append((lo, hi, ogamg.build(sp.csr_matrix((daa, daj, dai), shape=(hi - lo, hi - lo)))))
+
+    def bjacobi(rv):
+        return np.concatenate([ogamg.vcycle(lv, rv[lo:hi]) for lo, hi, lv in blocks])
+
+    xg_o, its_g, reason_g, hist_g = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-10, max_it=1000, pc=bjacobi)
+    gm = [got[r][7] for r in range(world)]
+    assert len({g[1] for g in gm}) == 1 and len({g[2] for g in gm}) == 1
+    print(f"\nbjacobi/GAMG: {gm[0][1]} its (oracle {its_g}), CG/Jacobi {nat[0][1]} its")
+    assert abs(gm[0][1] - its_g) <= 1 and gm[0][2] == reason_g
+    np.testing.assert_allclose(gm[0][3][:10], hist_g[:10], rtol=1e-7)
+    xgm = np.concatenate([g[0] for g in gm])
+    assert np.linalg.norm(xgm - xg_o) <= 1e-8 * np.linalg.norm(xg_o)
