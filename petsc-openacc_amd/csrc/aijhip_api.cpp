@@ -16,6 +16,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "aijhip_internal.h"
@@ -27,6 +28,8 @@ using aijhip::LongSeg;
 namespace {
 
 thread_local std::string g_err;
+// row lists at least this long are planned on several host threads
+constexpr int32_t kParallelPlanRows = 1 << 20;
 
 int fail(int code, const std::string &msg) {
     g_err = msg;
@@ -118,27 +121,17 @@ int validate_csr(int32_t m, int32_t n, int64_t nz, const int32_t *ai, const int3
 // consecutive rows while the block holds <= nnz_cap entries and <= rows rows
 // of the chosen geometry. A longer row becomes a long row, split into
 // segments of <= kLongSegNnz entries.
-int plan_stream(aijhip_mat *A) {
+// Greedy row blocks of rows [r0, r1) of the row list (see plan_stream).
+void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *h_ridx, int32_t r0, int32_t r1,
+               std::vector<BlockDesc> &blocks, std::vector<LongSeg> &segs, std::vector<LongRow> &longs) {
     using namespace aijhip;
     const auto &rai = A->h_rai;
-    const int32_t nr = rai.empty() ? 0 : (int32_t)rai.size() - 1;
-    std::vector<BlockDesc> blocks;
-    std::vector<LongSeg> segs;
-    std::vector<LongRow> longs;
-    blocks.reserve((size_t)nr / 64 + 8);
-    std::vector<int32_t> h_ridx;
-    if (A->compressed && A->n_crow > 0) {
-        h_ridx.resize(A->n_crow);
-        hipError_t e = hipMemcpy(h_ridx.data(), A->d_ridx, sizeof(int32_t) * A->n_crow, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) return hipfail(e, "plan: read ridx");
-    }
-    const StreamGeom G = kStreamGeoms[A->plan.tune.geom];
-    int32_t r = 0;
-    while (r < nr) {
+    int32_t r = r0;
+    while (r < r1) {
         const int32_t len = rai[r + 1] - rai[r];
         if (len > G.nnz_cap) {
             LongRow lr{};
-            lr.orow = A->compressed ? h_ridx[r] : r;
+            lr.orow = h_ridx ? h_ridx[r] : r;
             lr.seg0 = (int32_t)segs.size();
             for (int64_t k = rai[r]; k < rai[r + 1]; k += kLongSegNnz) {
                 const int64_t nk = std::min<int64_t>(kLongSegNnz, rai[r + 1] - k);
@@ -151,13 +144,59 @@ int plan_stream(aijhip_mat *A) {
         }
         const int32_t start = r;
         int32_t nk = 0;
-        while (r < nr && r - start < G.rows) {
+        while (r < r1 && r - start < G.rows) {
             const int32_t l = rai[r + 1] - rai[r];
             if (l > G.nnz_cap || nk + l > G.nnz_cap) break;
             nk += l;
             ++r;
         }
         blocks.push_back(BlockDesc{start, r - start, rai[start], nk});
+    }
+}
+
+int plan_stream(aijhip_mat *A) {
+    using namespace aijhip;
+    const auto &rai = A->h_rai;
+    const int32_t nr = rai.empty() ? 0 : (int32_t)rai.size() - 1;
+    std::vector<BlockDesc> blocks;
+    std::vector<LongSeg> segs;
+    std::vector<LongRow> longs;
+    std::vector<int32_t> h_ridx;
+    if (A->compressed && A->n_crow > 0) {
+        h_ridx.resize(A->n_crow);
+        hipError_t e = hipMemcpy(h_ridx.data(), A->d_ridx, sizeof(int32_t) * A->n_crow, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return hipfail(e, "plan: read ridx");
+    }
+    const StreamGeom G = kStreamGeoms[A->plan.tune.geom];
+    const int32_t *ridx = h_ridx.empty() ? nullptr : h_ridx.data();
+    // Large operands are planned in row ranges on host threads (a block
+    // boundary at each range start: speed-only, the sums do not change);
+    // 27 M rows take ~30 ms on one thread.
+    const int nt = nr >= kParallelPlanRows ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()))
+                                          : 1;
+    if (nt <= 1) {
+        blocks.reserve((size_t)nr / 64 + 8);
+        plan_rows(A, G, ridx, 0, nr, blocks, segs, longs);
+    } else {
+        std::vector<std::vector<BlockDesc>> pb(nt);
+        std::vector<std::vector<LongSeg>> ps(nt);
+        std::vector<std::vector<LongRow>> pl(nt);
+        std::vector<std::thread> th;
+        for (int t = 0; t < nt; ++t)
+            th.emplace_back([&, t] {
+                const int32_t r0 = (int32_t)((int64_t)nr * t / nt), r1 = (int32_t)((int64_t)nr * (t + 1) / nt);
+                pb[t].reserve((size_t)(r1 - r0) / 64 + 8);
+                plan_rows(A, G, ridx, r0, r1, pb[t], ps[t], pl[t]);
+            });
+        for (auto &x : th) x.join();
+        for (int t = 0; t < nt; ++t) {
+            blocks.insert(blocks.end(), pb[t].begin(), pb[t].end());
+            for (LongRow lr : pl[t]) {
+                lr.seg0 += (int32_t)segs.size();
+                longs.push_back(lr);
+            }
+            segs.insert(segs.end(), ps[t].begin(), ps[t].end());
+        }
     }
     Plan &P = A->plan;
     P.n_blocks = (int32_t)blocks.size();
@@ -315,8 +354,10 @@ int plan_build(aijhip_mat *A) {
 // Uploads a validated CSR into A (sizes already set) and plans it. ai is on
 // the host; aj/aa on the host, or on the device when dev_src (copied D2D).
 // own_ai, when given, holds ai and is moved into the handle's host offsets.
-int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const double *aa, bool dev_src = false,
-                    aijhip::HostVec<int32_t> *own_ai = nullptr) {
+// Structure statistics, PETSc's compressed-row form and the host row list,
+// then the plan — from the host row offsets ai (adopted when own_ai holds
+// them). The device CSR is already in place.
+int structure_and_plan(aijhip_mat *A, const int32_t *ai, aijhip::HostVec<int32_t> *own_ai) {
     const int32_t m = A->m;
     const int64_t nz = A->nz;
     hipError_t e;
@@ -333,20 +374,6 @@ int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const d
     // empty (MatCheckCompressedRow(..., ratio=0.6) in MatAssemblyEnd_SeqAIJ,
     // step2 MatAssemblyEnd patch context :35 [ext]).
     A->compressed = m > 0 && (1.0 - (double)nzrows / (double)m) >= 0.6;
-
-    if ((e = dmalloc(&A->d_ai, (size_t)m + 1, &A->device_bytes)) != hipSuccess ||
-        (e = dmalloc(&A->d_aj, (size_t)nz + 2, &A->device_bytes)) != hipSuccess ||
-        (e = dmalloc(&A->d_aa, (size_t)nz + 2, &A->device_bytes)) != hipSuccess)
-        return hipfail(e, "alloc CSR");
-    if ((e = hipMemcpy(A->d_ai, ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemset(A->d_aj + nz, 0, 2 * sizeof(int32_t))) != hipSuccess ||
-        (e = hipMemset(A->d_aa + nz, 0, 2 * sizeof(double))) != hipSuccess)
-        return hipfail(e, "upload ai");
-    const hipMemcpyKind kind = dev_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
-    if (nz > 0 &&
-        ((e = hipMemcpy(A->d_aj, aj, sizeof(int32_t) * (size_t)nz, kind)) != hipSuccess ||
-         (e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)nz, kind)) != hipSuccess))
-        return hipfail(e, "upload aj/aa");
     if (A->compressed) {
         aijhip::HostVec<int32_t> cai;
         std::vector<int32_t> ridx;
@@ -370,6 +397,27 @@ int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const d
         else A->h_rai.assign(ai, ai + (size_t)m + 1);
     }
     return plan_build(A);
+}
+
+int upload_and_plan(aijhip_mat *A, const int32_t *ai, const int32_t *aj, const double *aa, bool dev_src = false,
+                    aijhip::HostVec<int32_t> *own_ai = nullptr) {
+    const int32_t m = A->m;
+    const int64_t nz = A->nz;
+    hipError_t e;
+    if ((e = dmalloc(&A->d_ai, (size_t)m + 1, &A->device_bytes)) != hipSuccess ||
+        (e = dmalloc(&A->d_aj, (size_t)nz + 2, &A->device_bytes)) != hipSuccess ||
+        (e = dmalloc(&A->d_aa, (size_t)nz + 2, &A->device_bytes)) != hipSuccess)
+        return hipfail(e, "alloc CSR");
+    if ((e = hipMemcpy(A->d_ai, ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(A->d_aj + nz, 0, 2 * sizeof(int32_t))) != hipSuccess ||
+        (e = hipMemset(A->d_aa + nz, 0, 2 * sizeof(double))) != hipSuccess)
+        return hipfail(e, "upload ai");
+    const hipMemcpyKind kind = dev_src ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice;
+    if (nz > 0 &&
+        ((e = hipMemcpy(A->d_aj, aj, sizeof(int32_t) * (size_t)nz, kind)) != hipSuccess ||
+         (e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)nz, kind)) != hipSuccess))
+        return hipfail(e, "upload aj/aa");
+    return structure_and_plan(A, ai, own_ai);
 }
 
 int check_handle(aijhip_mat_t A) {
@@ -446,35 +494,58 @@ int visible_devices() {
     return count;
 }
 
-// A^T as a handle owned by A (MatMultTranspose): the device arrays of the
-// transpose (n+1 / nz+2 / nz+2, tail pad zeroed) are copied device to device
-// and freed here; only the row offsets visit the host, for planning.
-int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa) {
-    aijhip_mat *T = new (std::nothrow) aijhip_mat();
-    int rc = AIJHIP_OK;
-    if (!T) rc = fail(AIJHIP_ERR_ALLOC, "host allocation");
-    aijhip::HostVec<int32_t> h_tai;
-    if (!rc) {
-        T->device = A->device;
-        T->n_cu = A->n_cu;
-        T->requested_tune = A->requested_tune;
-        T->m = A->n;
-        T->n = A->m;
-        T->nz = A->nz;
-        T->requested_kernel =
-            A->requested_kernel == AIJHIP_KERNEL_VECTOR ? AIJHIP_KERNEL_AUTO : A->requested_kernel;
-        h_tai.resize((size_t)T->m + 1);
-        const hipError_t e = hipMemcpy(h_tai.data(), tai, sizeof(int32_t) * h_tai.size(), hipMemcpyDeviceToHost);
-        if (e != hipSuccess) rc = hipfail(e, "read transpose offsets");
+int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai, int32_t *d_aj, double *d_aa,
+                     const aijhip_mat *like, aijhip_mat **out) {
+    *out = nullptr;
+    aijhip_mat *A = new (std::nothrow) aijhip_mat();
+    if (!A) {
+        hipFree(d_ai); hipFree(d_aj); hipFree(d_aa);
+        return fail(AIJHIP_ERR_ALLOC, "host allocation");
     }
-    if (!rc) rc = upload_and_plan(T, h_tai.data(), taj, taa, true, &h_tai);
-    hipFree(tai);
-    hipFree(taj);
-    hipFree(taa);
+    A->device = device;
+    A->m = m;
+    A->n = n;
+    A->nz = nz;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+        A->n_cu = cus;
+    if (like) {
+        A->requested_tune = like->requested_tune;
+        A->requested_kernel =
+            like->requested_kernel == AIJHIP_KERNEL_VECTOR ? AIJHIP_KERNEL_AUTO : like->requested_kernel;
+    }
+    A->d_ai = d_ai;
+    A->d_aj = d_aj;
+    A->d_aa = d_aa;
+    A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
+    aijhip::HostVec<int32_t> h_ai;
+    int rc = AIJHIP_OK;
+    hipError_t e = hipSuccess;
+    try {
+        h_ai.resize((size_t)m + 1);
+    } catch (const std::bad_alloc &) {
+        rc = fail(AIJHIP_ERR_ALLOC, "host row offsets");
+    }
+    if (!rc && ((e = hipMemsetAsync(d_aj + nz, 0, 2 * sizeof(int32_t), nullptr)) != hipSuccess ||
+                (e = hipMemsetAsync(d_aa + nz, 0, 2 * sizeof(double), nullptr)) != hipSuccess ||
+                (e = hipMemcpy(h_ai.data(), d_ai, sizeof(int32_t) * h_ai.size(), hipMemcpyDeviceToHost)) != hipSuccess))
+        rc = hipfail(e, "read device row offsets");
+    if (!rc) rc = structure_and_plan(A, h_ai.data(), &h_ai);
     if (rc) {
-        if (T) { free_matrix(T); delete T; }
+        free_matrix(A);
+        delete A;
         return rc;
     }
+    *out = A;
+    return AIJHIP_OK;
+}
+
+// A^T as a handle owned by A (MatMultTranspose), adopting the transpose's
+// device arrays (n+1 / nz+2 / nz+2).
+int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa) {
+    aijhip_mat *T = nullptr;
+    const int rc = adopt_device_csr(A->device, A->n, A->m, A->nz, tai, taj, taa, A, &T);
+    if (rc) return rc;
     if (A->transpose) { free_matrix(A->transpose); delete A->transpose; }
     A->transpose = T;
     return AIJHIP_OK;

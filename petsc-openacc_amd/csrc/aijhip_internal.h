@@ -237,7 +237,13 @@ hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, i
 // Distinct 128-B x lines per entry over a row sample (at most 65536 rows):
 // ~0.7 for the 7-point stencil, ~0.17 for a 3-dof hexahedral FEM operator.
 hipError_t gather_lines_per_entry(const aijhip_mat &A, double *out);
-// Install A^T (device arrays, freed by the call) as A's transpose handle.
+// A handle that takes ownership of device CSR arrays made inside the library
+// (aj / aa allocated with nz + 2 entries; trusted: no column check, no copy).
+// Tuning and kernel choice copied from `like` when given. The arrays are
+// freed on failure.
+int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai, int32_t *d_aj, double *d_aa,
+                     const aijhip_mat *like, aijhip_mat **out);
+// Install A^T (device arrays, adopted) as A's transpose handle.
 int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa);
 // Number of device column indices outside [0, n) (synchronous).
 hipError_t count_bad_columns(const int32_t *d_aj, int64_t nz, int32_t n, int64_t *bad);

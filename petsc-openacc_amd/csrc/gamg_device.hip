@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gamg_device.h"
@@ -929,9 +930,56 @@ DCsr view_of(const aijhip_mat &A) {
     return v;
 }
 
+// The power iteration for emax(D^-1 A) (10 steps from a fixed start, norms
+// summed on the host in 256-entry blocks: the host builder's order) on a
+// host thread of its own.
+struct EmaxJob {
+    std::thread th;
+    double emax = 1.0;
+    hipError_t e = hipSuccess;
+    double *v = nullptr, *w = nullptr, *part = nullptr;
+    void start(const aijhip_mat &A, const double *dinv, int its) {
+        th = std::thread([this, &A, dinv, its] {
+            (void)hipSetDevice(A.device);
+            const int32_t m = A.m;
+            const unsigned g256 = blocks_for(m, 256);
+            std::vector<double> h_part;
+            if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
+                (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
+                return;
+            hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, nullptr, m, v);
+            const double nv = host_blocked_norm(v, m, part, h_part, &e);
+            if (e != hipSuccess) return;
+            hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, v, nv, v);
+            for (int it = 0; it < its; ++it) {
+                if ((e = aijhip::launch_dinv_mult(A, dinv, v, w, nullptr)) != hipSuccess) return;
+                const double nw = host_blocked_norm(w, m, part, h_part, &e);
+                if (e != hipSuccess) return;
+                if (!(nw > 0.0)) break;
+                emax = nw;
+                hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, w, nw, v);
+            }
+        });
+    }
+    void join() {
+        if (th.joinable()) th.join();
+    }
+    void release() {
+        hipFree(v); hipFree(w); hipFree(part);
+        v = w = part = nullptr;
+    }
+    ~EmaxJob() {
+        join();
+        release();
+    }
+};
+
+// The level's handle adopts the set-up's device arrays (no copy, no host
+// column check: they were made here).
 int make_handle(int device, DCsr &C, aijhip_mat **out) {
-    const int rc = aijhip_mat_create_from_device(device, C.m, C.n, C.nz, C.ai, C.aj, C.aa, out);
-    C.release();
+    const int rc = aijhip::adopt_device_csr(device, C.m, C.n, C.nz, C.ai, C.aj, C.aa, nullptr, out);
+    C.ai = C.aj = nullptr;  // owned by the handle now (or freed on failure)
+    C.aa = nullptr;
     return rc;
 }
 
@@ -994,6 +1042,9 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
         unsigned long long *d_left = nullptr;
         int32_t na = 0;
+        // emax(D^-1 A) needs only A: its power iteration runs from a second
+        // host thread while this one stages S and aggregates on the CPU
+        EmaxJob job;
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto level_done; } } while (0)
         GTRY(dalloc(&d, m), "alloc");
         GTRY(dalloc(&dinv, m), "alloc");
@@ -1021,6 +1072,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         // ---- aggregation: phases 1 and 3 (sequential greedy) on the host from
         // S staged in pinned memory, phase 2 on the device
         lap("strength kernels");
+        if (p.nsmooths > 0) job.start(A, dinv, p.eig_its);
         GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
         lap("staging alloc");
         h_si = stage.i32();
@@ -1052,11 +1104,13 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         }
         lap("aggregate");
     level_done:
+        job.join();
         hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
         hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left);
         if (rc || na >= m || na == 0) {  // an error, or no coarsening: this is the coarsest level
             hipFree(dinv);
             hipFree(d_aggv);
+            job.release();
             break;
         }
 #undef GTRY
@@ -1071,22 +1125,13 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         std::vector<double> h_part;
         aijhip_mat *Ph = nullptr, *Ach = nullptr;
         lap("free, vectors");
-        if (p.nsmooths > 0) {
-            GTRY(dalloc(&v, m), "alloc");
-            GTRY(dalloc(&w, m), "alloc");
-            GTRY(dalloc(&part, (m + kDotBlock - 1) / kDotBlock), "alloc");
-            hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, nullptr, m, v);
-            const double nv = host_blocked_norm(v, m, part, h_part, &e);
-            GTRY(e, "power iteration");
-            hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, v, nv, v);
-            for (int it = 0; it < p.eig_its; ++it) {
-                GTRY(aijhip::launch_dinv_mult(A, dinv, v, w, nullptr), "power iteration");
-                const double nw = host_blocked_norm(w, m, part, h_part, &e);
-                GTRY(e, "power iteration");
-                if (!(nw > 0.0)) break;
-                emax = nw;
-                hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, w, nw, v);
-            }
+        if (p.nsmooths > 0) {  // joined at level_done
+            v = job.v;
+            w = job.w;
+            part = job.part;
+            job.v = job.w = job.part = nullptr;  // freed at prolong_done
+            GTRY(job.e, "power iteration");
+            emax = job.emax;
             lap("emax");
         }
         // ---- tentative prolongator: the near-null space normalised per aggregate
