@@ -207,24 +207,30 @@ def host_vec_mult(A, x_h, reps=10):
 
 def read_ceiling(nbytes, dev, reps=20):
     """The achievable HBM read rate on this box, timed in the same run:
-    aijhip_read_probe over a buffer of the SpMV's byte count (16-B loads,
-    each byte once per launch), mean of `reps` launches by HIP events."""
+    aijhip_read_probe over a buffer of the SpMV's byte count, each byte read
+    once per launch; mean of `reps` launches by HIP events. Returns
+    {mode: (GB/s, us)} for mode 0 (the fastest shape measured: non-temporal
+    16-B loads, two per lane) and mode 1 (the STREAM kernel's shape: plain
+    loads, four per lane)."""
     import torch
     ksp = importlib.import_module("petsc-openacc_amd.ksp")
     L = ksp._veclib()
-    buf = torch.ones(nbytes // 8, dtype=torch.float64, device=dev)
+    buf = torch.rand(nbytes // 8, dtype=torch.float64, device=dev)
     s = torch.cuda.current_stream()
-    for _ in range(3):
-        L.aijhip_read_probe(buf.data_ptr(), buf.numel(), s.cuda_stream)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for a, b in ev:
-        a.record(s)
-        L.aijhip_read_probe(buf.data_ptr(), buf.numel(), s.cuda_stream)
-        b.record(s)
-    torch.cuda.synchronize()
-    ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    out = {}
+    for mode in (0, 1):
+        for _ in range(3):
+            L.aijhip_read_probe(buf.data_ptr(), buf.numel(), mode, s.cuda_stream)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            a.record(s)
+            L.aijhip_read_probe(buf.data_ptr(), buf.numel(), mode, s.cuda_stream)
+            b.record(s)
+        torch.cuda.synchronize()
+        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        out[mode] = (round(nbytes / (ms / 1e3) / 1e9, 1), round(ms * 1e3, 2))
     del buf
-    return round(nbytes / (ms / 1e3) / 1e9, 1), round(ms * 1e3, 2)
+    return out
 
 
 def pmc_traffic(rows, nnz, block):
@@ -594,10 +600,14 @@ def main():
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
-        if isinstance(ceiling, tuple):  # same-run flat-read ceiling: fraction of what HBM delivers here
+        if isinstance(ceiling, dict) and "error" not in ceiling:  # same-run flat reads of the same bytes
             out["roofline"]["ceiling_flat_read"] = {
-                "GBs": ceiling[0], "us": ceiling[1], "frac_of_ceiling": round(achieved / ceiling[0], 4),
-                "probe": "aijhip_read_probe: the SpMV's byte count read once with 16-B loads"}
+                "GBs": ceiling[0][0], "us": ceiling[0][1], "frac_of_ceiling": round(achieved / ceiling[0][0], 4),
+                "probe": "aijhip_read_probe mode 0: the SpMV's byte count read once, non-temporal 16-B loads, "
+                         "512-lane workgroups of two loads per lane (the fastest shape, tools/read_sweep.hip)",
+                "stream_shape_read": {"GBs": ceiling[1][0], "us": ceiling[1][1],
+                                      "frac": round(achieved / ceiling[1][0], 4),
+                                      "probe": "mode 1: plain loads, four per lane (the STREAM kernel's shape)"}}
         if distributed:  # whole-job rate against N HBM peaks (roofline.frac is rank 0's kernel alone)
             out["aggregate_roofline_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
             ci = comm.info()

@@ -132,14 +132,19 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 /* Speed-only knobs of the STREAM kernel; results are identical for every
  * setting. Re-plans on the device. */
 enum {
-    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..10: lanes / LDS entries / rows per block
+    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..11: lanes / LDS entries / rows per block
                                        (DESIGN.md §Kernels); -1 (default):
                                        6 for short rows, 1 for long rows    */
     AIJHIP_OPT_XCD_REMAP = 2,       /* 0 (default): hardware round-robin;
                                        1: each XCD gets a contiguous run of
                                        row blocks; C >= 2: chunks of C blocks,
                                        chunk c of every 8C on XCD slot c     */
-    AIJHIP_OPT_NT_LOADS = 3,        /* 1: non-temporal aa/aj loads (default 0) */
+    AIJHIP_OPT_NT_LOADS = 3,        /* -1 (default): non-temporal for long rows
+                                       with scattered gathers (the geometry-1
+                                       operands), plain otherwise; 0 plain;
+                                       1 non-temporal aa/aj loads; 2 a lane's
+                                       aj loads first, then non-temporal aa;
+                                       3 aj first, plain                    */
     AIJHIP_OPT_PERSISTENT = 4,      /* k > 0: persistent software-pipelined
                                        STREAM, k workgroups per CU (0 = off) */
     AIJHIP_OPT_CLAMPED_LOADS = 5,   /* 1: branch-free clamped loads instead of

@@ -43,12 +43,14 @@ int aijhip_vec_cg_update(int64_t n, double alpha, double *x, const double *p, do
 int aijhip_vec_jacobi(int64_t n, const double *r, const double *dinv, double *z, double *d_result,
                       void *stream);
 
-/* Diagnostic: reads d_buf[0 .. n & ~1) once with 16-B loads in the STREAM
- * SpMV's access shape (512-lane workgroups, each a contiguous 32 KiB tile,
- * four loads in flight per lane): the achievable HBM read rate the SpMV's
- * roofline fraction is read against (bench.py roofline.ceiling_flat_read).
- * d_buf 16-B aligned. */
-int aijhip_read_probe(const double *d_buf, int64_t n, void *stream);
+/* Diagnostic: reads d_buf[0 .. n & ~1) once with 16-B loads by 512-lane
+ * workgroups streaming contiguous tiles — the achievable HBM read rate the
+ * SpMV's roofline fraction is read against (bench.py
+ * roofline.ceiling_flat_read). mode 0: the fastest shape measured
+ * (non-temporal loads, two per lane, tools/read_sweep.hip); mode 1: the
+ * STREAM kernel's own shape (plain loads, four per lane). d_buf 16-B
+ * aligned. */
+int aijhip_read_probe(const double *d_buf, int64_t n, int mode, void *stream);
 
 /* PCSetUp_Jacobi on A's rows: d_dinv[i] = 1 / (first stored a_ii, 0 -> 1). */
 int aijhip_mat_jacobi_inverse(aijhip_mat_t A, double *d_dinv, void *stream);

@@ -310,21 +310,25 @@ int plan_build(aijhip_mat *A) {
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
     P.tune = A->requested_tune;
-    if (P.tune.geom < 0) {
+    if (P.tune.geom < 0 || P.tune.nt < 0) {
         // measured: 512 x 4094-entry blocks (geometry 6, 8 waves/SIMD) for
         // short rows (7-pt Poisson, profiles/r01/tune04) and for long rows
         // whose gathers run along x lines (FEM-structured stand-in: 283 vs
         // 313 us); 512 x 4096 (geometry 1: 76 VGPRs, 6 waves/SIMD) for long
         // rows with scattered gathers (skewed stand-in 405 vs 449 us, GAMG's
-        // coarse operators) — profiles/r01/rowsum/
+        // coarse operators) — profiles/r01/rowsum/. Non-temporal matrix
+        // loads for the scattered ones (skewed 398 vs 411 us; Poisson and the
+        // FEM stand-in are neutral to slower: profiles/r02/ntlong/)
         const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
-        P.tune.geom = 6;
+        bool scattered = false;
         if (nr > 0 && A->nz > (int64_t)16 * nr) {
             double lpe = 1.0;
             const hipError_t e = aijhip::gather_lines_per_entry(*A, &lpe);
             if (e != hipSuccess) return hipfail(e, "plan: gather locality");
-            if (lpe > aijhip::kScatteredLinesPerEntry) P.tune.geom = 1;
+            scattered = lpe > aijhip::kScatteredLinesPerEntry;
         }
+        if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
+        if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
     }
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM:
@@ -622,7 +626,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             t.xcd = value != 0;
             t.xchunk = value >= 2 ? value : 0;
             break;
-        case AIJHIP_OPT_NT_LOADS: t.nt = value != 0; break;
+        case AIJHIP_OPT_NT_LOADS:
+            if (value < -1 || value > 3) return fail(AIJHIP_ERR_ARG, "nt_loads: -1 (auto), 0..3");
+            t.nt = value;
+            break;
         case AIJHIP_OPT_PERSISTENT:
             if (value < 0 || value > 16) return fail(AIJHIP_ERR_ARG, "persistent: 0..16 workgroups per CU");
             t.persist = value;
@@ -764,7 +771,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->mult_bytes = 12 * A->nz + 4 * ((int64_t)A->m + 1) + 8 * (int64_t)A->n + 8 * (int64_t)A->m;
     info->stream_geometry = A->plan.tune.geom;
     info->xcd_remap = A->plan.tune.xcd ? (A->plan.tune.xchunk ? A->plan.tune.xchunk : 1) : 0;
-    info->nt_loads = A->plan.tune.nt ? 1 : 0;
+    info->nt_loads = A->plan.tune.nt;
     info->stream_threads = aijhip::kStreamGeoms[A->plan.tune.geom].threads;
     info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;

@@ -46,6 +46,7 @@ constexpr StreamGeom kStreamGeoms[] = {
     {256, 2046, 256},    // 8: 4 waves, 4 pair-iterations
     {512, 6142, 512},    // 9: 8 waves, 6 pair-iterations, 48 KiB: an x tile of a +-2100-column band fits
     {512, 8190, 512},    // 10: 8 waves, 8 pair-iterations, 64 KiB
+    {512, 2046, 512},    // 11: 8 waves, 2 pair-iterations, 16 KiB
 };
 constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
 constexpr int kMaxStreamNnzCap = 8192;
@@ -91,7 +92,8 @@ struct Tuning {
     int geom = -1;       // index into kStreamGeoms; -1 = by row length and gather locality (6 or 1)
     bool xcd = false;    // XCD-aware block remap
     int xchunk = 0;      //   chunk of the chunked remap (0 = contiguous runs)
-    bool nt = false;     // non-temporal matrix loads
+    int nt = -1;         // matrix loads: -1 by gather locality (non-temporal for scattered long rows),
+                         // 0 plain, 1 non-temporal, 2 aj first + aa non-temporal, 3 aj first
     int persist = 0;     // >0: persistent pipelined STREAM, this many workgroups per CU
     bool clamped = false;  // branch-free clamped loads instead of predicated loads
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones

@@ -236,7 +236,9 @@ __device__ __forceinline__ double row_sum_seq(const double *p, int32_t n, double
     return s;
 }
 
-template <int T, int CAP, int RPT, bool CROW, bool XCD, bool NT, bool CLAMPED, class Op>
+// NT (load mode): 0 plain loads, aa/aj interleaved per iteration; 1 both
+// non-temporal; 2 all aj loads first, then aa non-temporal; 3 aj first, plain.
+template <int T, int CAP, int RPT, bool CROW, bool XCD, int NT, bool CLAMPED, class Op>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
@@ -272,13 +274,27 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     f64x2 av[ITERS];
     i32x2 cv[ITERS];
     f64x2 xv[ITERS];
+    if constexpr (NT >= 2) {  // the columns first: the gathers need only them
 #pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-        const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if (CLAMPED || k < k1) {
-            const int64_t kc = CLAMPED ? min(k, klast) : k;
-            av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + kc));
-            cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + kc));
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
+            if (CLAMPED || k < k1) cv[it] = *reinterpret_cast<const i32x2 *>(aj + (CLAMPED ? min(k, klast) : k));
+        }
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
+            if (CLAMPED || k < k1)
+                av[it] = ld_stream<NT == 2>(reinterpret_cast<const f64x2 *>(aa + (CLAMPED ? min(k, klast) : k)));
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
+            if (CLAMPED || k < k1) {
+                const int64_t kc = CLAMPED ? min(k, klast) : k;
+                av[it] = ld_stream<NT == 1>(reinterpret_cast<const f64x2 *>(aa + kc));
+                cv[it] = ld_stream<NT == 1>(reinterpret_cast<const i32x2 *>(aj + kc));
+            }
         }
     }
     // x tile: the block's columns [xr.x, xr.x + xr.y) staged in LDS (the
@@ -895,6 +911,10 @@ static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double 
         if (add) { AIJHIP_SL(true, false, false, false, false); }
         AIJHIP_SL(false, true, false, false, false);
     }
+    if (P.tune.nt >= 2 && !P.tune.xcd && !P.tune.clamped) {  // load-order study modes
+        if (P.tune.nt == 2) { AIJHIP_SL(false, false, false, 2, false); }
+        AIJHIP_SL(false, false, false, 3, false);
+    }
     switch ((P.tune.xcd ? 4 : 0) | (P.tune.nt ? 2 : 0) | (P.tune.clamped ? 1 : 0)) {
         case 0: AIJHIP_SL(false, false, false, false, false);
         case 1: AIJHIP_SL(false, false, false, false, true);
@@ -955,7 +975,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
-    static_assert(kNumStreamGeoms == 11, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
 #define AIJHIP_OG(G)                                                                                      \
     case G:                                                                                               \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
@@ -964,7 +984,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
-        AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8); AIJHIP_OG(9); AIJHIP_OG(10);
+        AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8); AIJHIP_OG(9); AIJHIP_OG(10); AIJHIP_OG(11);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_OG
@@ -977,7 +997,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
     if (P.kernel != AIJHIP_KERNEL_STREAM || A.compressed || P.n_longs > 0 || b0 < 0 || b0 + nb > P.n_blocks)
         return hipErrorInvalidValue;
     if (nb <= 0) return hipSuccess;
-    static_assert(kNumStreamGeoms == 11, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
 #define AIJHIP_BG(G)                                                                                            \
     case G:                                                                                                     \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, OpMult<false>>), dim3(nb), \
@@ -987,7 +1007,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
         break
     switch (P.tune.geom) {
         AIJHIP_BG(0); AIJHIP_BG(1); AIJHIP_BG(2); AIJHIP_BG(3); AIJHIP_BG(4);
-        AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8); AIJHIP_BG(9); AIJHIP_BG(10);
+        AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8); AIJHIP_BG(9); AIJHIP_BG(10); AIJHIP_BG(11);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_BG
@@ -1043,14 +1063,14 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     }
     // Every geometry is dispatched explicitly: the kernel's LDS size must be
     // the one the plan's row blocks were cut for.
-    static_assert(kNumStreamGeoms == 11, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
     const int g = P.tune.geom;
     if (P.n_blocks > 0 && P.tune.persist > 0 && kStreamGeoms[g].rows == kStreamGeoms[g].threads) {
 #define AIJHIP_PG(G) \
     case G: pipe_dispatch<kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap>(A, L, x, z, y, add, s); break
         switch (g) {
             AIJHIP_PG(0); AIJHIP_PG(1); AIJHIP_PG(3); AIJHIP_PG(4); AIJHIP_PG(5);
-            AIJHIP_PG(6); AIJHIP_PG(7); AIJHIP_PG(8); AIJHIP_PG(9); AIJHIP_PG(10);
+            AIJHIP_PG(6); AIJHIP_PG(7); AIJHIP_PG(8); AIJHIP_PG(9); AIJHIP_PG(10); AIJHIP_PG(11);
             default: return hipErrorInvalidValue;
         }
 #undef AIJHIP_PG
@@ -1059,7 +1079,7 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
 #define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, L, x, z, y, add, s, dpart, stop); break
         switch (g) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
-            AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10);
+            AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
             default: return hipErrorInvalidValue;
         }
 #undef AIJHIP_SG

@@ -130,23 +130,35 @@ double *partials(hipError_t *e) {
     return per_dev[dev];
 }
 
-// HBM read ceiling: n doubles read once, in the STREAM kernel's access shape
-// (a 512-lane workgroup per contiguous 32 KiB tile, four 16-B loads per lane
-// issued before any use), a partial sum per workgroup so no load is dropped.
-constexpr int kProbeThreads = 512, kProbeIters = 4;
+// HBM read ceiling: n doubles read once by 512-lane workgroups, each a
+// contiguous tile of U 16-B loads per lane issued before any use, a partial
+// sum per workgroup so no load is dropped. tools/read_sweep.hip measured the
+// shapes: non-temporal loads with U = 2 read fastest (7.3 TB/s at 2.8 GB);
+// U = 4 plain loads is the STREAM kernel's own shape (6.1 TB/s).
+constexpr int kProbeThreads = 512;
+template <int U, bool NT>
 __global__ __launch_bounds__(kProbeThreads) void k_read_probe(int64_t n2, const double2 *__restrict__ v,
                                                               double *part) {
     __shared__ double scratch[kProbeThreads / 64];
-    const int64_t base = (int64_t)blockIdx.x * kProbeThreads * kProbeIters + threadIdx.x;
-    double2 r[kProbeIters];
+    const int64_t base = (int64_t)blockIdx.x * kProbeThreads * U + threadIdx.x;
+    double2 r[U];
 #pragma unroll
-    for (int it = 0; it < kProbeIters; ++it) {
+    for (int it = 0; it < U; ++it) {
         const int64_t i = base + (int64_t)it * kProbeThreads;
-        r[it] = i < n2 ? v[i] : make_double2(0.0, 0.0);
+        if (i < n2) {
+            if constexpr (NT) {
+                r[it].x = __builtin_nontemporal_load(&v[i].x);
+                r[it].y = __builtin_nontemporal_load(&v[i].y);
+            } else {
+                r[it] = v[i];
+            }
+        } else {
+            r[it] = make_double2(0.0, 0.0);
+        }
     }
     double s = 0.0;
 #pragma unroll
-    for (int it = 0; it < kProbeIters; ++it) s += r[it].x + r[it].y;
+    for (int it = 0; it < U; ++it) s += r[it].x + r[it].y;
     const double t = bsum<kProbeThreads>(s, scratch);
     if (threadIdx.x == 0) part[blockIdx.x & (kMaxBlocks - 1)] = t;
 }
@@ -213,15 +225,25 @@ int aijhip_vec_jacobi(int64_t n, const double *r, const double *dinv, double *z,
     return vhip(hipGetLastError(), "vec_jacobi");
 }
 
-int aijhip_read_probe(const double *d_buf, int64_t n, void *stream) {
-    if (n < 0 || (n > 0 && !d_buf) || ((uintptr_t)d_buf & 15)) return verr(AIJHIP_ERR_ARG, "read_probe: bad arguments");
+int aijhip_read_probe(const double *d_buf, int64_t n, int mode, void *stream) {
+    if (n < 0 || (n > 0 && !d_buf) || ((uintptr_t)d_buf & 15) || mode < 0 || mode > 1)
+        return verr(AIJHIP_ERR_ARG, "read_probe: bad arguments");
     if (n < 2) return AIJHIP_OK;
     hipError_t e;
     double *part = partials(&e);
     if (!part) return vhip(e, "read_probe scratch");
-    const int64_t n2 = n / 2, per = (int64_t)kProbeThreads * kProbeIters;
-    hipLaunchKernelGGL(k_read_probe, dim3((unsigned)((n2 + per - 1) / per)), dim3(kProbeThreads), 0,
-                       (hipStream_t)stream, n2, reinterpret_cast<const double2 *>(d_buf), part);
+    const int64_t n2 = n / 2;
+    const double2 *v = reinterpret_cast<const double2 *>(d_buf);
+    hipStream_t s = (hipStream_t)stream;
+    if (mode == 0) {
+        const int64_t per = (int64_t)kProbeThreads * 2;
+        hipLaunchKernelGGL((k_read_probe<2, true>), dim3((unsigned)((n2 + per - 1) / per)), dim3(kProbeThreads), 0, s,
+                           n2, v, part);
+    } else {
+        const int64_t per = (int64_t)kProbeThreads * 4;
+        hipLaunchKernelGGL((k_read_probe<4, false>), dim3((unsigned)((n2 + per - 1) / per)), dim3(kProbeThreads), 0,
+                           s, n2, v, part);
+    }
     return vhip(hipGetLastError(), "read_probe");
 }
 

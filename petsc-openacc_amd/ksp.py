@@ -275,7 +275,7 @@ def _veclib():
         L.aijhip_vec_cg_update.argtypes = [i64, d, _P, _P, _P, _P, _P, _P, _P, _P]
         L.aijhip_vec_jacobi.argtypes = [i64, _P, _P, _P, _P, _P]
         L.aijhip_mat_jacobi_inverse.argtypes = [_P, _P, _P]
-        L.aijhip_read_probe.argtypes = [_P, i64, _P]
+        L.aijhip_read_probe.argtypes = [_P, i64, ctypes.c_int, _P]
         _vec_bound = True
     return L
 

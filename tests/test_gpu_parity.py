@@ -404,7 +404,7 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
         xd = to_dev(g["x"], dev)
         yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
         first = None
-        for geom in range(11):
+        for geom in range(12):
             for xcd, nt, persist, clamped in ((0, 0, 0, 0), (1, 0, 0, 1), (0, 1, 0, 0), (22, 1, 0, 1), (3, 0, 0, 0),
                                               (0, 0, 1, 0), (0, 1, 2, 0), (0, 0, 5, 0), (0, 0, 0, 1)):
                 if persist and geom == 2:

@@ -97,6 +97,15 @@ def main():
     if args.variants == "xtile":
         for g, xt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
+    if args.variants == "ntlong":  # non-temporal matrix loads for long-row operands, both automatic geometries
+        for g, nt in itertools.product((1, 6), (0, 1)):
+            variants.append(("stream", dict(geometry=g, nt_loads=nt)))
+    if args.variants == "loadorder":  # aj-first load order and non-temporal aa (nt_loads 2/3)
+        for nt in (0, 1, 2, 3):
+            variants.append(("stream", dict(geometry=6, nt_loads=nt)))
+    if args.variants == "ntgeom":  # non-temporal matrix loads x load depth (tools/read_sweep.hip: nt reads 6.8 TB/s)
+        for g, nt in itertools.product((6, 11, 8, 0), (0, 1)):
+            variants.append(("stream", dict(geometry=g, nt_loads=nt)))
     if args.variants == "xtile_band":  # LDS x tiles of a +-2100-column band (geometries 9/10 fit it)
         for g, xt in ((1, 0), (6, 0), (9, 0), (9, 1), (10, 0), (10, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
