@@ -18,7 +18,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
  && timeout -k 10 600 python bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" \
  && echo "bench ok" && cat "$OUT/bench.json" \
  && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-      -- python3 bench.py --steps 100 --no-cpu-baseline --no-cg --no-gamg "$@" > "$OUT/prof.log" 2>&1 \
+      -- python3 bench.py --steps 100 --no-cpu-baseline --no-cg --no-gamg --no-host-vec "$@" > "$OUT/prof.log" 2>&1 \
  && echo "rocprof ok"
 rc=$?
 tail -5 "$OUT/pytest_gpu.log" 2>/dev/null
