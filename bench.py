@@ -91,6 +91,27 @@ def weak_grid(G: int, world: int):
     return nx, ny, nz
 
 
+def rank_record(rank, device, pci_bus, rows, nnz, ghosts, spmv_ms, diag_ms):
+    """One rank's entry of the N > 1 line: where it ran and how much of its
+    distributed SpMV the exchange (+ the A_o product) adds on top of the
+    diagonal block alone."""
+    return {"rank": rank, "device": device, "pci_bus": pci_bus, "rows": rows, "nnz": nnz, "ghosts": ghosts,
+            "spmv_us_mean": round(spmv_ms * 1e3, 2), "diag_block_us_mean": round(diag_ms * 1e3, 2),
+            "halo_exposed_us": round((spmv_ms - diag_ms) * 1e3, 2)}
+
+
+def distributed_block(world, backend, comm_info, timeout_s, ranks):
+    """The `distributed` object of the N > 1 line: world
+    size, backends, RCCL version, the collective timeout and every rank's
+    record, slowest exposed halo first in `worst_rank`."""
+    worst = max(ranks, key=lambda r: r["halo_exposed_us"]) if ranks else None
+    return {"world_size": world, "backend": backend, "comm": comm_info["kind"],
+            "rccl_version": comm_info["version"] or None, "comm_timeout_s": timeout_s, "ranks": ranks,
+            "worst_rank": None if worst is None else worst["rank"],
+            "halo_hidden": "spmv_us_mean vs diag_block_us_mean per rank: the exchange runs on a second "
+                           "stream while A_d multiplies; halo_exposed_us is what it adds (A_o product included)"}
+
+
 def cpu_baseline(ai, aj, aa, x, seconds, all_cores=False):
     """Time the oracle (C restatement of MatMult_SeqAIJ) on 1 core — PETSc's
     1 rank = 1 core — or, with all_cores, its OpenMP static-row-block form on
@@ -422,11 +443,9 @@ def main():
         torch.cuda.synchronize()
         diag_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_d]))
         del y_diag
-        mine = {"rank": rank, "device": torch.cuda.current_device(),
-                "pci_bus": getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None), "rows": m_loc, "nnz": nnz_loc, "ghosts": op.n_ghost,
-            "spmv_us_mean": round(float(np.mean(launch_ms)) * 1e3, 2),
-            "diag_block_us_mean": round(diag_ms * 1e3, 2),
-            "halo_exposed_us": round((float(np.mean(launch_ms)) - diag_ms) * 1e3, 2)}
+        mine = rank_record(rank, torch.cuda.current_device(),
+                           getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None), m_loc, nnz_loc,
+                           op.n_ghost, float(np.mean(launch_ms)), diag_ms)
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
 
@@ -610,14 +629,7 @@ def main():
                                       "probe": "mode 1: plain loads, four per lane (the STREAM kernel's shape)"}}
         if distributed:  # whole-job rate against N HBM peaks (roofline.frac is rank 0's kernel alone)
             out["aggregate_roofline_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
-            ci = comm.info()
-            out["distributed"] = {
-                "world_size": world, "backend": dist.get_backend(), "comm": ci["kind"],
-                "rccl_version": ci["version"] or None, "comm_timeout_s": args.comm_timeout,
-                "ranks": ranks,
-                "halo_hidden": "spmv_us_mean vs diag_block_us_mean per rank: the exchange runs on a second "
-                               "stream while A_d multiplies; halo_exposed_us is what it adds (A_o product "
-                               "included)"}
+            out["distributed"] = distributed_block(world, dist.get_backend(), comm.info(), args.comm_timeout, ranks)
         if args.rehearse_one_gpu:
             out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
         if strong is not None:
