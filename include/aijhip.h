@@ -215,6 +215,19 @@ int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y,
  * directly, pageable ones through pinned staging slots. */
 int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y);
 
+/* w = z + A x with host vectors (MatMultAdd_SeqAIJ, aij.c [ext]: the
+ * off-diagonal product of MatMult_MPIAIJ and PCMG's interpolation reach it);
+ * each row sum starts from z[i], as PETSc's does. z may alias w; x must not.
+ * The reference leaves this on the CPU; the PETSc adapter
+ * routes it here for matrices above a size threshold. */
+int aijhip_mat_mult_add_host(aijhip_mat_t A, const double *x, const double *z,
+                             double *w);
+
+/* y = A^T x with host vectors (MatMultTranspose_SeqAIJ [ext]: PCMG's
+ * restriction). Same transposed copy and scatter order as
+ * aijhip_mat_mult_transpose; the copies are pipelined as for mult_host. */
+int aijhip_mat_mult_transpose_host(aijhip_mat_t A, const double *x, double *y);
+
 int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info);
 
 /* Borrow the handle's device CSR (read-only; valid until the next

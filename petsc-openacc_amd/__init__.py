@@ -43,6 +43,7 @@ ABI_SYMBOLS = (
     "aijhip_mat_create", "aijhip_mat_create_from_device", "aijhip_mat_set_kernel", "aijhip_mat_set_option",
     "aijhip_mat_update_values", "aijhip_mat_assembly_end", "aijhip_mat_mult",
     "aijhip_mat_mult_add", "aijhip_mat_mult_transpose", "aijhip_mat_mult_host",
+    "aijhip_mat_mult_add_host", "aijhip_mat_mult_transpose_host",
     "aijhip_mat_get_info", "aijhip_mat_get_device_csr", "aijhip_mat_destroy",
 )
 HARNESS_SYMBOLS = (
@@ -105,6 +106,8 @@ def lib() -> ctypes.CDLL:
         L.aijhip_mat_mult_add.argtypes = [_P, _P, _P, _P, _P]
         L.aijhip_mat_mult_transpose.argtypes = [_P, _P, _P, _P]
         L.aijhip_mat_mult_host.argtypes = [_P, _P, _P]
+        L.aijhip_mat_mult_add_host.argtypes = [_P, _P, _P, _P]
+        L.aijhip_mat_mult_transpose_host.argtypes = [_P, _P, _P]
         L.aijhip_mat_get_info.argtypes = [_P, ctypes.POINTER(AIJInfo)]
         L.aijhip_mat_get_device_csr.argtypes = [_P, ctypes.POINTER(_P), ctypes.POINTER(_P), ctypes.POINTER(_P)]
         L.aijhip_mat_destroy.argtypes = [_P]
@@ -252,6 +255,30 @@ class SeqAIJHIP:
         if y.shape[0] < self.m:
             raise ValueError("out too short")
         _check(lib().aijhip_mat_mult_host(self._h, _np_ptr(x, np.float64), _np_ptr(y, np.float64)))
+        return y
+
+    def mult_add_host(self, x: np.ndarray, z: np.ndarray, out: np.ndarray | None = None) -> np.ndarray:
+        """w = z + A x with host arrays (MatMultAdd_SeqAIJ); out may be z."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        z = np.ascontiguousarray(z, dtype=np.float64)
+        if x.shape[0] < self.n or z.shape[0] < self.m:
+            raise ValueError("x or z too short")
+        w = np.empty(self.m) if out is None else out
+        if w.shape[0] < self.m:
+            raise ValueError("out too short")
+        _check(lib().aijhip_mat_mult_add_host(self._h, _np_ptr(x, np.float64), _np_ptr(z, np.float64),
+                                              _np_ptr(w, np.float64)))
+        return w
+
+    def mult_transpose_host(self, x: np.ndarray, out: np.ndarray | None = None) -> np.ndarray:
+        """y = A^T x with host arrays (MatMultTranspose_SeqAIJ)."""
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        if x.shape[0] < self.m:
+            raise ValueError("x too short")
+        y = np.empty(self.n) if out is None else out
+        if y.shape[0] < self.n:
+            raise ValueError("out too short")
+        _check(lib().aijhip_mat_mult_transpose_host(self._h, _np_ptr(x, np.float64), _np_ptr(y, np.float64)))
         return y
 
     def update_values(self, aa):

@@ -715,10 +715,10 @@ int aijhip_mat_mult_add(aijhip_mat_t A, const double *x, const double *z, double
     return mult_impl(A, x, z, w, true, stream);
 }
 
-int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y, void *stream) {
-    int rc = check_handle(A);
-    if (rc) return rc;
-    if (A->n == 0) return AIJHIP_OK;
+namespace {
+
+// A^T, built on first use (kept until the structure changes).
+int ensure_transpose(aijhip_mat *A) {
     if (!A->transpose) {
         DeviceGuard g(A->device);
         if (g.err != hipSuccess) return hipfail(g.err, "set device");
@@ -727,9 +727,27 @@ int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y, void *
         hipError_t e = hipDeviceSynchronize();
         if (e == hipSuccess) e = aijhip::build_transpose(*A, &tai, &taj, &taa, nullptr);
         if (e != hipSuccess) return hipfail(e, "build transpose");
-        rc = aijhip::attach_transpose(A, tai, taj, taa);
-        if (rc) return rc;
+        return aijhip::attach_transpose(A, tai, taj, taa);
     }
+    return AIJHIP_OK;
+}
+
+// The handle's host-vector staging buffers and stream (first use).
+int ensure_host_staging(aijhip_mat *A) {
+    hipError_t e = hipSuccess;
+    if (!A->host_stream) e = hipStreamCreateWithFlags(&A->host_stream, hipStreamNonBlocking);
+    if (e == hipSuccess && !A->d_xstage) e = dmalloc(&A->d_xstage, (size_t)A->n, &A->device_bytes);
+    if (e == hipSuccess && !A->d_ystage) e = dmalloc(&A->d_ystage, (size_t)A->m, &A->device_bytes);
+    return e == hipSuccess ? AIJHIP_OK : hipfail(e, "host staging");
+}
+
+}  // namespace
+
+int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y, void *stream) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (A->n == 0) return AIJHIP_OK;
+    if ((rc = ensure_transpose(A))) return rc;
     return mult_impl(A->transpose, x, nullptr, y, false, stream);
 }
 
@@ -740,14 +758,51 @@ int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y) {
     if (!y || (A->n > 0 && !x)) return fail(AIJHIP_ERR_ARG, "NULL vector");
     DeviceGuard g(A->device);
     if (g.err != hipSuccess) return hipfail(g.err, "set device");
-    hipError_t e = hipSuccess;
-    if (!A->host_stream) e = hipStreamCreateWithFlags(&A->host_stream, hipStreamNonBlocking);
-    if (e == hipSuccess && !A->d_xstage) e = dmalloc(&A->d_xstage, (size_t)A->n, &A->device_bytes);
-    if (e == hipSuccess && !A->d_ystage) e = dmalloc(&A->d_ystage, (size_t)A->m, &A->device_bytes);
-    if (e != hipSuccess) return hipfail(e, "host staging");
+    if ((rc = ensure_host_staging(A))) return rc;
     // step2 MatMult patch:24 (x H2D), :27-40 (kernel), :29 (y D2H), pipelined
     // as steps 3/4 overlap them (host_pipe.cpp)
     return aijhip::host_pipe_mult(A, x, y);
+}
+
+int aijhip_mat_mult_add_host(aijhip_mat_t A, const double *x, const double *z, double *w) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (A->m == 0) return AIJHIP_OK;
+    if (!z || !w || (A->n > 0 && !x)) return fail(AIJHIP_ERR_ARG, "NULL vector");
+    if (x == w) return fail(AIJHIP_ERR_ARG, "x and w alias");
+    DeviceGuard g(A->device);
+    if (g.err != hipSuccess) return hipfail(g.err, "set device");
+    if ((rc = ensure_host_staging(A))) return rc;
+    // z goes up before w comes down, so z == w (PETSc's yy == zz) is fine;
+    // the row sums start from z[i] in the kernel (MatMultAdd_SeqAIJ's order)
+    hipStream_t s = A->host_stream;
+    hipError_t e = hipSuccess;
+    if (A->n > 0) e = hipMemcpyAsync(A->d_xstage, x, sizeof(double) * (size_t)A->n, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(A->d_ystage, z, sizeof(double) * (size_t)A->m, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hipfail(e, "copy x, z in");
+    if ((e = aijhip::launch_mult(*A, A->d_xstage, A->d_ystage, A->d_ystage, true, s)) != hipSuccess)
+        return hipfail(e, "MatMultAdd launch");
+    if ((e = hipMemcpyAsync(w, A->d_ystage, sizeof(double) * (size_t)A->m, hipMemcpyDeviceToHost, s)) !=
+            hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hipfail(e, "copy w out");
+    return AIJHIP_OK;
+}
+
+int aijhip_mat_mult_transpose_host(aijhip_mat_t A, const double *x, double *y) {
+    int rc = check_handle(A);
+    if (rc) return rc;
+    if (A->n == 0) return AIJHIP_OK;
+    if (!y || (A->m > 0 && !x)) return fail(AIJHIP_ERR_ARG, "NULL vector");
+    {
+        DeviceGuard g(A->device);
+        if (g.err != hipSuccess) return hipfail(g.err, "set device");
+        if ((rc = ensure_transpose(A))) return rc;
+    }
+    // A^T is a handle of its own: its MatMult with host vectors is the
+    // pipelined one above
+    return aijhip_mat_mult_host(A->transpose, x, y);
 }
 
 int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {

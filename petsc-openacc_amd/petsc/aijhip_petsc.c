@@ -33,9 +33,13 @@
  * Vectors: PETSc 3.7 Vecs are host arrays, so MatMult has the reference's
  * step-2 semantics (matrix resident on the device, x in and y out over PCIe
  * per call: aijhip_mat_mult_host, which pipelines the two copies with the
- * product the way steps 3/4 do). MatMultAdd / MatMultTranspose stay on
- * the CPU, as in the reference. A device Vec type is what removes the PCIe
- * traffic.
+ * product the way steps 3/4 do). MatMultAdd (MatMult_MPIAIJ's off-diagonal
+ * product, PCMG's interpolation) and MatMultTranspose (PCMG's restriction),
+ * which the reference leaves on the CPU, run on the device too when the
+ * matrix has at least -aijhip_transfer_min_nz entries (default 262144:
+ * below that PETSc's own loop beats a PCIe round trip); smaller ones keep
+ * PETSc's SeqAIJ (or Inode) bodies. A device Vec type is what removes the
+ * PCIe traffic.
  */
 #include <petsc/private/matimpl.h>
 #include <../src/mat/impls/aij/seq/aij.h>
@@ -48,7 +52,26 @@ typedef struct {
   PetscObjectState state;        /* object state at the last upload: values
                                     changed without an assembly (MatScale,
                                     MatShift, MatDuplicate, ...) raise it */
+  /* PETSc's CPU bodies the assembly left in the ops table (SeqAIJ or Inode),
+     for matrices below the transfer threshold */
+  PetscErrorCode (*cpu_multadd)(Mat, Vec, Vec, Vec);
+  PetscErrorCode (*cpu_multtranspose)(Mat, Vec, Vec);
 } Mat_AIJHIP;
+
+static PetscInt transfer_min_nz = -1; /* -aijhip_transfer_min_nz, read once */
+
+static PetscErrorCode AIJHIPTransferMinNz(PetscInt *out)
+{
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  if (transfer_min_nz < 0) {
+    transfer_min_nz = 262144;
+    ierr = PetscOptionsGetInt(NULL, NULL, "-aijhip_transfer_min_nz", &transfer_min_nz, NULL);CHKERRQ(ierr);
+  }
+  *out = transfer_min_nz;
+  PetscFunctionReturn(0);
+}
 
 static PetscErrorCode AIJHIPDevice(Mat A, int *dev)
 {
@@ -112,6 +135,8 @@ static PetscErrorCode AIJHIPFree(Mat A)
   PetscFunctionReturn(0);
 }
 
+static PetscErrorCode AIJHIPCurrent(Mat, Mat_AIJHIP**);
+
 /* y = A x with the device-resident matrix; x and y are host arrays. */
 static PetscErrorCode AIJHIPMult(Mat A, Vec xx, Vec yy)
 {
@@ -119,22 +144,111 @@ static PetscErrorCode AIJHIPMult(Mat A, Vec xx, Vec yy)
   Mat_AIJHIP        *d = (Mat_AIJHIP*)A->spptr;
   const PetscScalar *x;
   PetscScalar       *y;
-  PetscObjectState  state;
   PetscErrorCode    ierr;
 
   PetscFunctionBegin;
-  ierr = PetscObjectStateGet((PetscObject)A, &state);CHKERRQ(ierr);
-  if (!d || !d->h || d->state != state) { /* never uploaded, or host values changed since */
-    if (!A->assembled) SETERRQ(PetscObjectComm((PetscObject)A), PETSC_ERR_ARG_WRONGSTATE, "aijhip: MatMult on an unassembled matrix");
-    ierr = AIJHIPUpload(A, MAT_FINAL_ASSEMBLY, 0);CHKERRQ(ierr);
-    d = (Mat_AIJHIP*)A->spptr;
-  }
+  ierr = AIJHIPCurrent(A, &d);CHKERRQ(ierr); /* never uploaded, or host values changed since */
   ierr = VecGetArrayRead(xx, &x);CHKERRQ(ierr);
   ierr = VecGetArray(yy, &y);CHKERRQ(ierr);
   if (aijhip_mat_mult_host(d->h, x, y)) SETERRQ1(PetscObjectComm((PetscObject)A), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
   ierr = VecRestoreArrayRead(xx, &x);CHKERRQ(ierr);
   ierr = VecRestoreArray(yy, &y);CHKERRQ(ierr);
   ierr = PetscLogFlops(2.0*a->nz - a->nonzerorowcnt);CHKERRQ(ierr); /* step2 MatMult patch:47 */
+  PetscFunctionReturn(0);
+}
+
+/* Bring the device copy up to date before a product (first use, or host
+ * values changed since the last upload). */
+static PetscErrorCode AIJHIPCurrent(Mat A, Mat_AIJHIP **out)
+{
+  Mat_AIJHIP       *d = (Mat_AIJHIP*)A->spptr;
+  PetscObjectState state;
+  PetscErrorCode   ierr;
+
+  PetscFunctionBegin;
+  ierr = PetscObjectStateGet((PetscObject)A, &state);CHKERRQ(ierr);
+  if (!d || !d->h || d->state != state) {
+    if (!A->assembled) SETERRQ(PetscObjectComm((PetscObject)A), PETSC_ERR_ARG_WRONGSTATE, "aijhip: product with an unassembled matrix");
+    ierr = AIJHIPUpload(A, MAT_FINAL_ASSEMBLY, 0);CHKERRQ(ierr);
+  }
+  *out = (Mat_AIJHIP*)A->spptr;
+  PetscFunctionReturn(0);
+}
+
+/* zz = yy + A xx (MatMultAdd_SeqAIJ: each row sum starts from yy[i]). */
+static PetscErrorCode AIJHIPMultAdd(Mat A, Vec xx, Vec yy, Vec zz)
+{
+  Mat_SeqAIJ        *a = (Mat_SeqAIJ*)A->data;
+  Mat_AIJHIP        *d = (Mat_AIJHIP*)A->spptr;
+  const PetscScalar *x, *y;
+  PetscScalar       *z;
+  PetscInt          min_nz;
+  PetscErrorCode    ierr;
+
+  PetscFunctionBegin;
+  ierr = AIJHIPTransferMinNz(&min_nz);CHKERRQ(ierr);
+  if (a->nz < min_nz && d && d->cpu_multadd) {
+    ierr = (*d->cpu_multadd)(A, xx, yy, zz);CHKERRQ(ierr);
+    PetscFunctionReturn(0);
+  }
+  ierr = AIJHIPCurrent(A, &d);CHKERRQ(ierr);
+  ierr = VecGetArrayRead(xx, &x);CHKERRQ(ierr);
+  if (yy == zz) {
+    ierr = VecGetArray(zz, &z);CHKERRQ(ierr);
+    y = z;
+  } else {
+    ierr = VecGetArrayRead(yy, &y);CHKERRQ(ierr);
+    ierr = VecGetArray(zz, &z);CHKERRQ(ierr);
+  }
+  if (aijhip_mat_mult_add_host(d->h, x, y, z)) SETERRQ1(PetscObjectComm((PetscObject)A), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
+  ierr = VecRestoreArrayRead(xx, &x);CHKERRQ(ierr);
+  if (yy != zz) {
+    ierr = VecRestoreArrayRead(yy, &y);CHKERRQ(ierr);
+  }
+  ierr = VecRestoreArray(zz, &z);CHKERRQ(ierr);
+  ierr = PetscLogFlops(2.0*a->nz);CHKERRQ(ierr);
+  PetscFunctionReturn(0);
+}
+
+/* yy = A^T xx (MatMultTranspose_SeqAIJ's scatter order, kept by the device
+ * transpose). */
+static PetscErrorCode AIJHIPMultTranspose(Mat A, Vec xx, Vec yy)
+{
+  Mat_SeqAIJ        *a = (Mat_SeqAIJ*)A->data;
+  Mat_AIJHIP        *d = (Mat_AIJHIP*)A->spptr;
+  const PetscScalar *x;
+  PetscScalar       *y;
+  PetscInt          min_nz;
+  PetscErrorCode    ierr;
+
+  PetscFunctionBegin;
+  ierr = AIJHIPTransferMinNz(&min_nz);CHKERRQ(ierr);
+  if (a->nz < min_nz && d && d->cpu_multtranspose) {
+    ierr = (*d->cpu_multtranspose)(A, xx, yy);CHKERRQ(ierr);
+    PetscFunctionReturn(0);
+  }
+  ierr = AIJHIPCurrent(A, &d);CHKERRQ(ierr);
+  ierr = VecGetArrayRead(xx, &x);CHKERRQ(ierr);
+  ierr = VecGetArray(yy, &y);CHKERRQ(ierr);
+  if (aijhip_mat_mult_transpose_host(d->h, x, y)) SETERRQ1(PetscObjectComm((PetscObject)A), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
+  ierr = VecRestoreArrayRead(xx, &x);CHKERRQ(ierr);
+  ierr = VecRestoreArray(yy, &y);CHKERRQ(ierr);
+  ierr = PetscLogFlops(2.0*a->nz);CHKERRQ(ierr);
+  PetscFunctionReturn(0);
+}
+
+/* After PETSc's assembly: remember the CPU multadd / multtranspose it
+ * installed (the Inode check may pick its own), then point the ops table at
+ * the device forms. */
+static PetscErrorCode AIJHIPInstallOps(Mat A)
+{
+  Mat_AIJHIP *d = (Mat_AIJHIP*)A->spptr;
+
+  PetscFunctionBegin;
+  if (A->ops->multadd != AIJHIPMultAdd) d->cpu_multadd = A->ops->multadd;
+  if (A->ops->multtranspose != AIJHIPMultTranspose) d->cpu_multtranspose = A->ops->multtranspose;
+  A->ops->multadd       = AIJHIPMultAdd;
+  A->ops->multtranspose = AIJHIPMultTranspose;
   PetscFunctionReturn(0);
 }
 
@@ -156,6 +270,9 @@ static PetscErrorCode MatAssemblyEnd_SeqAIJHIP(Mat A, MatAssemblyType mode)
    * Flan_1565): take MatMult back, or such matrices would multiply on the CPU */
   A->ops->mult = AIJHIPMult;
   ierr = AIJHIPUpload(A, mode, 1);CHKERRQ(ierr);
+  if (mode == MAT_FINAL_ASSEMBLY) {
+    ierr = AIJHIPInstallOps(A);CHKERRQ(ierr);
+  }
   PetscFunctionReturn(0);
 }
 
@@ -238,6 +355,9 @@ PetscErrorCode MatAssemblyEnd_SeqAIJ(Mat A, MatAssemblyType mode)
   ierr = MatAssemblyEnd_SeqAIJ_Original(A, mode);CHKERRQ(ierr);
   A->ops->mult = MatMult_SeqAIJ; /* the inode check may have installed MatMult_SeqAIJ_Inode */
   ierr = AIJHIPUpload(A, mode, 1);CHKERRQ(ierr);
+  if (mode == MAT_FINAL_ASSEMBLY) { /* MatMultAdd_SeqAIJ / MatMultTranspose_SeqAIJ stay in aij.o: only the ops table changes */
+    ierr = AIJHIPInstallOps(A);CHKERRQ(ierr);
+  }
   PetscFunctionReturn(0);
 }
 

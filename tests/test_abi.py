@@ -141,10 +141,12 @@ def test_petsc_adapter_binds_only_declared_symbols():
     src = (ROOT / "petsc-openacc_amd" / "petsc" / "aijhip_petsc.c").read_text()
     used = set(re.findall(r"\b(aijhip_\w+)\s*\(", src))
     assert {"aijhip_mat_create", "aijhip_mat_mult_host", "aijhip_mat_update_values",
-            "aijhip_mat_assembly_end", "aijhip_mat_destroy"} <= used
+            "aijhip_mat_assembly_end", "aijhip_mat_destroy", "aijhip_mat_mult_add_host",
+            "aijhip_mat_mult_transpose_host"} <= used
     assert used <= declared_functions()
     for sym in ("MatRegister", "MatCreate_SeqAIJ", "PetscDLLibraryRegister_aijhip_petsc",
-                "MatAssemblyEnd_SeqAIJ", "MatDestroy_SeqAIJ", "MatMult_SeqAIJ"):
+                "MatAssemblyEnd_SeqAIJ", "MatDestroy_SeqAIJ", "MatMult_SeqAIJ", "ops->multadd",
+                "ops->multtranspose", "-aijhip_transfer_min_nz"):
         assert sym in src
     env = {k: v for k, v in __import__("os").environ.items() if k != "PETSC_DIR"}
     r = subprocess.run(["make", "-s", "-C", str(ROOT / "petsc-openacc_amd" / "petsc")], capture_output=True,

@@ -98,5 +98,8 @@ def test_host_cg_gamg_matches_numpy_restatement():
     for threads in (1, 3):
         h = host_cg_gamg.solve(ai, aj, aa, rhs, rtol=1e-12, atol=1e-50, threads=threads, levels=lv)
         assert h["reason"] == reason_o and abs(h["its"] - its_o) <= 1
-        np.testing.assert_allclose(h["hist"][:its_o], hist_o[:its_o], rtol=1e-8)
+        # threaded dots sum in another order: the late, 1e-12-reduced norms
+        # carry round-off relative to the initial one, not to themselves
+        n = min(its_o, len(h["hist"]))
+        np.testing.assert_allclose(h["hist"][:n], hist_o[:n], rtol=1e-8, atol=1e-14 * hist_o[0])
         assert np.linalg.norm(h["x"] - xo) <= 1e-9 * np.linalg.norm(xo)
