@@ -1,0 +1,419 @@
+// gamg_aggregate.hip — phases 1 and 3 of the greedy aggregation
+// (gamg_setup.cpp aggregate) on the device, with the same result as the
+// sequential passes, node for node.
+//
+// Phase 1 walks the nodes in natural order and roots an aggregate at a free
+// node whose strong neighbours are all free; the root takes them. A node is
+// free at its turn exactly when no earlier root lies within two steps of it
+// in S (a root at distance 1 took it, one at distance 2 took a neighbour), so
+// the roots are the lexicographically-first distance-2 independent set of
+// the nodes with strong neighbours, and that set is unique: node i is a root
+// iff every lower node within two steps of it is not. That rule runs in
+// parallel as an event-driven sweep (a topological order on the "lower
+// node within two steps" relation):
+//   cnt[i]  = the number of walks of length 1 and 2 from i to lower nodes;
+//   a root marks every higher node within two steps OUT (compare-and-swap:
+//           the first root to reach it wins; all that matters is that it is
+//           OUT);
+//   an OUT node takes one off cnt[k] for every walk to a higher, still
+//           undecided k; the walk that brings cnt[k] to 0 makes k a root
+//           (all its lower neighbours are decided and none is a root: a
+//           root never decrements, so a node next to one never gets to 0).
+// Decisions are final, so the order in which concurrent lanes act cannot
+// change the outcome. Each round is two launches (roots mark, OUT nodes
+// count down); the rounds needed grow with the longest chain of roots the
+// natural order forces (about 2 N on an N^3 grid: ~650 at 300^3). Deep
+// chains (a path graph needs m / 3 rounds) are handed back to the host pass.
+// Aggregate numbers follow the roots' index order (a scan), as the host's
+// counter does.
+//
+// Phase 3 (the few nodes phases 1 and 2 leave) stays the host's sequential
+// pass, over those nodes and their S rows only, gathered on the device.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <vector>
+
+#include "gamg_device.h"
+
+namespace {
+
+constexpr int32_t kUndecided = 0, kRoot = 1, kOut = 2;
+constexpr unsigned kRoundGrid = 512;  // workgroups of 256 lanes per round launch
+
+inline unsigned blocks_for(int64_t n, int t) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+// f(k) for every walk i -> j (k = j) and i -> j -> k (k != i) in S
+template <class F>
+__device__ __forceinline__ void for_walks(int32_t i, const int32_t *__restrict__ si, const int32_t *__restrict__ sj,
+                                          F f) {
+    const int32_t a1 = si[i + 1];
+    for (int32_t a = si[i]; a < a1; ++a) {
+        const int32_t j = sj[a];
+        f(j);
+        const int32_t b1 = si[j + 1];
+        for (int32_t b = si[j]; b < b1; ++b) {
+            const int32_t k = sj[b];
+            if (k != i) f(k);
+        }
+    }
+}
+
+__global__ void k_lf_init(int32_t m, const int32_t *__restrict__ si, const int32_t *__restrict__ sj, int32_t *state,
+                          int32_t *cnt) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    if (si[i] == si[i + 1]) {  // no strong neighbour: never a root, in nobody's walks
+        state[i] = kOut;
+        cnt[i] = 0;
+        return;
+    }
+    int32_t c = 0;
+    for_walks(i, si, sj, [&](int32_t k) { c += k < i; });
+    state[i] = kUndecided;
+    cnt[i] = c;
+}
+
+// round 0's roots: undecided nodes with no lower node within two steps
+__global__ void k_lf_seed(int32_t m, int32_t *state, const int32_t *__restrict__ cnt, int32_t *roots,
+                          unsigned *tails) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m || state[i] != kUndecided || cnt[i] != 0) return;
+    state[i] = kRoot;
+    roots[atomicAdd(&tails[0], 1u)] = i;
+}
+
+// Append v to list for the lanes with p set: one atomic per wavefront (the
+// tails are single counters every lane of a round appends to).
+__device__ __forceinline__ void wave_push(bool p, int32_t v, int32_t *list, unsigned *tail) {
+    const unsigned long long mask = __ballot(p);
+    if (!mask) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(tail, (unsigned)__popcll(mask));
+    base = (unsigned)__shfl((int)base, leader, 64);
+    if (p) list[base + (unsigned)__popcll(mask & ((1ull << lane) - 1ull))] = v;
+}
+
+constexpr int kGroup = 8;   // lanes per frontier node: its strong neighbours split over them
+constexpr int kBatch2 = 8;  // second-step nodes loaded together before acting on them
+
+// The walks of frontier node i handled by one lane of its group: neighbours
+// j = S(i)[l], S(i)[l + kGroup], ... and their rows, in batches of kBatch2
+// (loads first, then the state reads, then act(k, state), so a lane's chain
+// is a few dependent steps per batch rather than per node).
+template <class Act>
+__device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int32_t *__restrict__ si,
+                                            const int32_t *__restrict__ sj, const int32_t *state, Act act) {
+    const int32_t a0 = on ? si[i] : 0, a1 = on ? si[i + 1] : 0;
+    // every lane of the wavefront runs the same number of batches, so that
+    // act() may vote across the wavefront
+    int32_t deg = a1 - a0;
+    for (int o = 32; o > 0; o >>= 1) deg = max(deg, __shfl_xor(deg, o, 64));
+    for (int32_t a_base = 0; a_base < deg; a_base += kGroup) {
+        const int32_t a = a_base + l;
+        const bool has_j = a < a1 - a0;
+        const int32_t j = has_j ? sj[a0 + a] : 0;
+        const int32_t b0 = has_j ? si[j] : 0, b1 = has_j ? si[j + 1] : 0;
+        int32_t len = b1 - b0 + 1;  // the neighbour itself, then its row
+        int32_t mx = len;
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
+        for (int32_t c = 0; c < mx; c += kBatch2) {
+            int32_t k[kBatch2], st[kBatch2];
+#pragma unroll
+            for (int u = 0; u < kBatch2; ++u) {
+                const int32_t e = c + u;
+                k[u] = e < len ? (e == 0 ? j : sj[b0 + e - 1]) : -1;
+            }
+#pragma unroll
+            for (int u = 0; u < kBatch2; ++u) st[u] = k[u] > i ? state[k[u]] : kOut;
+#pragma unroll
+            for (int u = 0; u < kBatch2; ++u) act(k[u], st[u]);
+        }
+    }
+}
+
+// Round t, first half: the roots found last round mark the higher nodes
+// within two steps OUT. rstart[t] .. tails[0] are this round's roots (only
+// the second half appends roots, so tails[0] is stable here).
+__global__ __launch_bounds__(256) void k_lf_mark(int t, const int32_t *__restrict__ si,
+                                                 const int32_t *__restrict__ sj, int32_t *state,
+                                                 const int32_t *__restrict__ roots, int32_t *outs, unsigned *tails,
+                                                 unsigned *rstart) {
+    const unsigned lo = rstart[t], hi = tails[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) rstart[t + 1] = hi;
+    const int l = threadIdx.x % kGroup;
+    const unsigned groups = gridDim.x * (blockDim.x / kGroup);
+    const unsigned g0 = blockIdx.x * (blockDim.x / kGroup) + threadIdx.x / kGroup;
+    // wavefront-uniform trip count (wave_push votes across the wavefront)
+    for (unsigned q0 = lo; q0 < hi; q0 += groups) {
+        const unsigned q = q0 + g0;
+        const bool on = q < hi;
+        const int32_t r = on ? roots[q] : 0;
+        group_walks(r, l, on, si, sj, state, [&](int32_t k, int32_t st) {
+            const bool p = on && st == kUndecided && atomicCAS(&state[k], kUndecided, kOut) == kUndecided;
+            wave_push(p, k, outs, &tails[1]);
+        });
+    }
+}
+
+// Round t, second half: the nodes just marked OUT count down their higher
+// undecided nodes; a count reaching 0 makes a root for round t + 1.
+__global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restrict__ si,
+                                                  const int32_t *__restrict__ sj, int32_t *state, int32_t *cnt,
+                                                  int32_t *roots, const int32_t *__restrict__ outs, unsigned *tails,
+                                                  unsigned *ostart) {
+    const unsigned lo = ostart[t], hi = tails[1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) ostart[t + 1] = hi;
+    const int l = threadIdx.x % kGroup;
+    const unsigned groups = gridDim.x * (blockDim.x / kGroup);
+    const unsigned g0 = blockIdx.x * (blockDim.x / kGroup) + threadIdx.x / kGroup;
+    for (unsigned q0 = lo; q0 < hi; q0 += groups) {
+        const unsigned q = q0 + g0;
+        const bool on = q < hi;
+        const int32_t j = on ? outs[q] : 0;
+        group_walks(j, l, on, si, sj, state, [&](int32_t k, int32_t st) {
+            bool p = false;
+            if (on && st == kUndecided && atomicSub(&cnt[k], 1) == 1) {
+                state[k] = kRoot;
+                p = true;
+            }
+            wave_push(p, k, roots, &tails[0]);
+        });
+    }
+}
+
+__global__ void k_lf_flags(int32_t m, const int32_t *__restrict__ state, int32_t *flag, unsigned *undecided) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int32_t s = state[i];
+    flag[i] = s == kRoot;
+    if (s == kUndecided) atomicAdd(undecided, 1u);
+}
+
+// phase-1 aggregates: the root and its strong neighbours (disjoint: roots
+// are at least three steps apart)
+__global__ void k_lf_assign(int32_t m, const int32_t *__restrict__ si, const int32_t *__restrict__ sj,
+                            const int32_t *__restrict__ state, const int32_t *__restrict__ id, int32_t *agg) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m || state[i] != kRoot) return;
+    const int32_t a = id[i];
+    agg[i] = a;
+    for (int32_t k = si[i]; k < si[i + 1]; ++k) agg[sj[k]] = a;
+}
+
+__global__ void k_fill_i32(int32_t m, int32_t v, int32_t *x) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) x[i] = v;
+}
+
+__global__ void k_free_flags(int32_t m, const int32_t *__restrict__ agg, int32_t *flag) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) flag[i] = agg[i] == -1;
+}
+
+// the free nodes in index order, and their S row lengths
+__global__ void k_free_list(int32_t m, const int32_t *__restrict__ flag, const int32_t *__restrict__ pos,
+                            const int32_t *__restrict__ si, int32_t *list, int32_t *len) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m || !flag[i]) return;
+    list[pos[i]] = i;
+    len[pos[i]] = si[i + 1] - si[i];
+}
+
+__global__ void k_free_rows(int32_t nf, const int32_t *__restrict__ list, const int32_t *__restrict__ roff,
+                            const int32_t *__restrict__ si, const int32_t *__restrict__ sj, int32_t *rows) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nf) return;
+    const int32_t i = list[q], s0 = si[i], n = si[i + 1] - s0, o = roff[q];
+    for (int32_t k = 0; k < n; ++k) rows[o + k] = sj[s0 + k];
+}
+
+__global__ void k_scatter_i32(int32_t nf, const int32_t *__restrict__ list, const int32_t *__restrict__ v,
+                              int32_t *agg) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < nf) agg[list[q]] = v[q];
+}
+
+template <class T>
+hipError_t dalloc(T **p, int64_t n) {
+    return hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * (size_t)std::max<int64_t>(n, 1));
+}
+
+// exclusive sum of n int32 (hipcub, temp allocated here)
+hipError_t exclusive_sum(const int32_t *in, int32_t *out, int32_t n, hipStream_t s) {
+    size_t tb = 0;
+    void *tmp = nullptr;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s);
+    if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tb, 1));
+    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, n, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    hipFree(tmp);
+    return e;
+}
+
+}  // namespace
+
+namespace aijhip_gamg {
+
+hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *sj, int32_t max_rounds,
+                                   int32_t *phase1, int32_t *na, int32_t *rounds, bool *done) {
+    *done = false;
+    *na = 0;
+    *rounds = 0;
+    if (m <= 0) {
+        *done = true;
+        return hipSuccess;
+    }
+    hipStream_t s = nullptr;
+    int32_t *state = nullptr, *cnt = nullptr, *roots = nullptr, *outs = nullptr;
+    unsigned *tails = nullptr, *rstart = nullptr, *ostart = nullptr, *h_ctl = nullptr;
+    const unsigned g = blocks_for(m, 256);
+    constexpr int kBatch = 32;  // rounds launched between two looks at the tails
+    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) e = dalloc(&state, m);
+    if (e == hipSuccess) e = dalloc(&cnt, m);
+    if (e == hipSuccess) e = dalloc(&roots, m);
+    if (e == hipSuccess) e = dalloc(&outs, m);
+    if (e == hipSuccess) e = dalloc(&tails, 4);
+    if (e == hipSuccess) e = dalloc(&rstart, (int64_t)max_rounds + kBatch + 2);
+    if (e == hipSuccess) e = dalloc(&ostart, (int64_t)max_rounds + kBatch + 2);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_ctl), sizeof(unsigned) * 4);
+    if (e == hipSuccess) e = hipMemsetAsync(tails, 0, sizeof(unsigned) * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(rstart, 0, sizeof(unsigned), s);
+    if (e == hipSuccess) e = hipMemsetAsync(ostart, 0, sizeof(unsigned), s);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_lf_init, dim3(g), dim3(256), 0, s, m, si, sj, state, cnt);
+        hipLaunchKernelGGL(k_lf_seed, dim3(g), dim3(256), 0, s, m, state, cnt, roots, tails);
+        e = hipGetLastError();
+    }
+    int t = 0;
+    while (e == hipSuccess && t < max_rounds) {
+        for (int b = 0; b < kBatch; ++b, ++t) {
+            hipLaunchKernelGGL(k_lf_mark, dim3(kRoundGrid), dim3(256), 0, s, t, si, sj, state, roots, outs, tails,
+                               rstart);
+            hipLaunchKernelGGL(k_lf_count, dim3(kRoundGrid), dim3(256), 0, s, t, si, sj, state, cnt, roots, outs,
+                               tails, ostart);
+        }
+        // finished when the last round found no new root: rstart[t] holds the
+        // root count the last mark launch saw
+        if ((e = hipGetLastError()) != hipSuccess) break;
+        if ((e = hipMemcpyAsync(h_ctl, tails, sizeof(unsigned), hipMemcpyDeviceToHost, s)) != hipSuccess) break;
+        if ((e = hipMemcpyAsync(h_ctl + 1, rstart + t, sizeof(unsigned), hipMemcpyDeviceToHost, s)) != hipSuccess)
+            break;
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) break;
+        if (h_ctl[0] == h_ctl[1]) {
+            *done = true;
+            break;
+        }
+    }
+    *rounds = t;
+    if (e == hipSuccess && *done) {
+        // every node decided (a check on the rule above), aggregate numbers in
+        // root order
+        int32_t *flag = cnt, *id = outs;  // reused: the sweep is over
+        if ((e = hipMemsetAsync(tails + 2, 0, sizeof(unsigned), s)) == hipSuccess) {
+            hipLaunchKernelGGL(k_lf_flags, dim3(g), dim3(256), 0, s, m, state, flag, tails + 2);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) e = exclusive_sum(flag, id, m, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(h_ctl + 2, tails + 2, sizeof(unsigned), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess && h_ctl[2] != 0) *done = false;  // unreachable if the rule holds: the host redoes it
+        int32_t last_id = 0, last_flag = 0;
+        if (e == hipSuccess && *done) {
+            e = hipMemcpy(&last_id, id + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(&last_flag, flag + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+        }
+        if (e == hipSuccess && *done) {
+            *na = last_id + last_flag;
+            hipLaunchKernelGGL(k_fill_i32, dim3(g), dim3(256), 0, s, m, -1, phase1);
+            hipLaunchKernelGGL(k_lf_assign, dim3(g), dim3(256), 0, s, m, si, sj, state, id, phase1);
+            e = hipGetLastError();
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+        }
+    }
+    hipFree(state); hipFree(cnt); hipFree(roots); hipFree(outs);
+    hipFree(tails); hipFree(rstart); hipFree(ostart);
+    if (h_ctl) hipHostFree(h_ctl);
+    if (s) hipStreamDestroy(s);
+    return e;
+}
+
+hipError_t aggregate_phase3_device(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t *na) {
+    int32_t *flag = nullptr, *pos = nullptr, *list = nullptr, *len = nullptr, *roff = nullptr, *rows = nullptr,
+            *val = nullptr;
+    const unsigned g = blocks_for(m, 256);
+    int32_t nf = 0, nrow = 0;
+    std::vector<int32_t> h_list, h_roff, h_rows, h_val;
+    hipError_t e = dalloc(&flag, m);
+    if (e == hipSuccess) e = dalloc(&pos, m);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_free_flags, dim3(g), dim3(256), 0, nullptr, m, agg, flag);
+        e = exclusive_sum(flag, pos, m, nullptr);
+    }
+    if (e == hipSuccess) {
+        int32_t lp = 0, lf = 0;
+        e = hipMemcpy(&lp, pos + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(&lf, flag + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+        nf = lp + lf;
+    }
+    if (e == hipSuccess && nf > 0) {
+        if ((e = dalloc(&list, nf)) == hipSuccess && (e = dalloc(&len, nf)) == hipSuccess &&
+            (e = dalloc(&roff, nf)) == hipSuccess) {
+            hipLaunchKernelGGL(k_free_list, dim3(g), dim3(256), 0, nullptr, m, flag, pos, si, list, len);
+            e = exclusive_sum(len, roff, nf, nullptr);
+        }
+        if (e == hipSuccess) {
+            int32_t lo = 0, ll = 0;
+            e = hipMemcpy(&lo, roff + (nf - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(&ll, len + (nf - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+            nrow = lo + ll;
+        }
+        if (e == hipSuccess && (e = dalloc(&rows, nrow)) == hipSuccess) {
+            hipLaunchKernelGGL(k_free_rows, dim3(blocks_for(nf, 256)), dim3(256), 0, nullptr, nf, list, roff, si, sj,
+                               rows);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess) {
+            h_list.resize(nf);
+            h_roff.resize((size_t)nf + 1);
+            h_rows.resize((size_t)std::max(nrow, 1));
+            e = hipMemcpy(h_list.data(), list, sizeof(int32_t) * (size_t)nf, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(h_roff.data(), roff, sizeof(int32_t) * (size_t)nf, hipMemcpyDeviceToHost);
+            if (e == hipSuccess && nrow > 0)
+                e = hipMemcpy(h_rows.data(), rows, sizeof(int32_t) * (size_t)nrow, hipMemcpyDeviceToHost);
+            h_roff[nf] = nrow;
+        }
+        if (e == hipSuccess) {
+            // gamg_setup.cpp aggregate phase 3 over the free nodes alone: a node
+            // outside the list already has an aggregate
+            h_val.assign(nf, -1);
+            int32_t n = *na;
+            for (int32_t q = 0; q < nf; ++q) {
+                if (h_val[q] != -1) continue;
+                h_val[q] = n;
+                for (int32_t k = h_roff[q]; k < h_roff[q + 1]; ++k) {
+                    const auto it = std::lower_bound(h_list.begin(), h_list.end(), h_rows[k]);
+                    if (it != h_list.end() && *it == h_rows[k] && h_val[it - h_list.begin()] == -1)
+                        h_val[it - h_list.begin()] = n;
+                }
+                ++n;
+            }
+            *na = n;
+            if ((e = dalloc(&val, nf)) == hipSuccess &&
+                (e = hipMemcpy(val, h_val.data(), sizeof(int32_t) * (size_t)nf, hipMemcpyHostToDevice)) ==
+                    hipSuccess) {
+                hipLaunchKernelGGL(k_scatter_i32, dim3(blocks_for(nf, 256)), dim3(256), 0, nullptr, nf, list, val,
+                                   agg);
+                e = hipGetLastError();
+            }
+        }
+    }
+    hipFree(flag); hipFree(pos); hipFree(list); hipFree(len); hipFree(roff); hipFree(rows); hipFree(val);
+    return e;
+}
+
+}  // namespace aijhip_gamg

@@ -32,4 +32,17 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
 
 void free_device_levels(std::vector<DeviceLevel> &levels);
 
+// Aggregation phase 1 on the device (gamg_aggregate.hip), from the symmetric
+// strength graph S (device CSR, rows sorted, unique, no diagonal): phase1[i]
+// = the phase-1 aggregate of node i or -1, *na = their count, identical to
+// aggregate_phase1. *done is false when the sweep needed more than
+// max_rounds rounds (the caller then runs the host pass).
+hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *sj, int32_t max_rounds,
+                                   int32_t *phase1, int32_t *na, int32_t *rounds, bool *done);
+// Phase 3 for the nodes agg[] still has at -1 (aggregate_phase3 restricted to
+// them): their S rows are gathered on the device, the sequential pass runs on
+// the host, the result is scattered back. *na in: the count so far; out: the
+// final count.
+hipError_t aggregate_phase3_device(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t *na);
+
 }  // namespace aijhip_gamg

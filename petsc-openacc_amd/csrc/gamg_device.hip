@@ -4,8 +4,10 @@
 // itself pinned to oracle/gamg.py):
 //   diagonal / D^-1               one lane per row
 //   strength graph S (+ S^T)      atomic slots, then per-row sort + unique
-//   aggregation                   host (sequential greedy, natural order),
-//                                 from S and per-entry |a_ij| weights
+//   aggregation                   greedy, natural order: phase 1 as a
+//                                 device sweep (gamg_aggregate.hip) or the
+//                                 host pass, phase 2 on the device, phase 3
+//                                 sequential over the nodes left
 //   emax(D^-1 A)                  power iteration on the STREAM SpMV in
 //                                 PETSc order; 256-entry blocked dots
 //   P = (I - 1.4/emax D^-1 A) P0  row-wise product A*P0, union with P0
@@ -983,6 +985,23 @@ int make_handle(int device, DCsr &C, aijhip_mat **out) {
     return rc;
 }
 
+// Which side runs aggregation phase 1 (both give the same aggregates): the
+// device sweep for levels of at least 2^20 rows whose S averages at most 16
+// strong neighbours (the sweep follows walks of length 2, ~deg^2 per node),
+// with a round budget near the host pass's cost (a round ~ 10-20 us, the pass
+// ~ 3 ns per node); AIJHIP_GAMG_AGG=host|device overrides (device: no round
+// budget).
+bool device_phase1(int32_t m, int64_t nzs, int32_t *max_rounds) {
+    const char *f = std::getenv("AIJHIP_GAMG_AGG");
+    if (f && std::string(f) == "host") return false;
+    if (f && std::string(f) == "device") {
+        *max_rounds = m + 2;
+        return true;
+    }
+    *max_rounds = std::max<int32_t>(256, m / 8192);
+    return m >= (1 << 20) && nzs <= 16 * (int64_t)m;
+}
+
 }  // namespace
 
 namespace aijhip_gamg {
@@ -1042,6 +1061,8 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
         unsigned long long *d_left = nullptr;
         int32_t na = 0;
+        bool dev_agg = false;  // phase 1 ran on the device (else the host pass)
+        int32_t sweep_rounds = 0;
         // emax(D^-1 A) needs only A: its power iteration runs from a second
         // host thread while this one stages S and aggregates on the CPU
         EmaxJob job;
@@ -1069,26 +1090,41 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
                            p.threshold, off, pos, tmp);
         if ((rc = strength_lists(A, cnt, off, tmp, nzs, n_cu, &si, &sj, &sval, &nzs))) goto level_done;
         GTRY(hipGetLastError(), "strength kernels");
-        // ---- aggregation: phases 1 and 3 (sequential greedy) on the host from
-        // S staged in pinned memory, phase 2 on the device
+        // ---- aggregation. Phase 1: the device sweep (gamg_aggregate.hip) on
+        // large levels with a sparse S, else -- or when the sweep would run too
+        // deep -- the sequential pass on the host from S staged in pinned
+        // memory; the same aggregates either way. Phase 2 on the device; phase
+        // 3 (sequential) over the nodes left.
         lap("strength kernels");
         if (p.nsmooths > 0) job.start(A, dinv, p.eig_its);
-        GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
-        lap("staging alloc");
-        h_si = stage.i32();
-        h_sj = h_si + m + 1;
-        agg = h_sj + nzs;
-        GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
-        if (nzs > 0) GTRY(hipMemcpy(h_sj, sj, sizeof(int32_t) * (size_t)nzs, hipMemcpyDeviceToHost), "read S");
-        lap("strength");
-        // (phase 1 measured on the MI355X host at 300^3: this int32 form 83 ms;
-        // bitmap or byte flags with or without early exits 87-121 ms)
-        na = aijhip_gamg::aggregate_phase1(m, h_si, h_sj, agg);
-        lap("phase 1");
         GTRY(dalloc(&d_ph, m), "alloc");
         GTRY(dalloc(&d_aggv, m), "alloc");
         GTRY(dalloc(&d_left, 1), "alloc");
-        GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
+        {
+            int32_t max_rounds = 0;
+            if (device_phase1(m, nzs, &max_rounds)) {
+                GTRY(aijhip_gamg::aggregate_phase1_device(m, si, sj, max_rounds, d_ph, &na, &sweep_rounds, &dev_agg),
+                     "phase 1 sweep");
+                if (log)
+                    std::fprintf(stderr, "gamg device level %zu phase 1 sweep: %d rounds%s\n", levels.size() - 1,
+                                 sweep_rounds, dev_agg ? "" : " (too deep: host pass)");
+            }
+        }
+        if (!dev_agg) {
+            GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
+            lap("staging alloc");
+            h_si = stage.i32();
+            h_sj = h_si + m + 1;
+            agg = h_sj + nzs;
+            GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
+            if (nzs > 0) GTRY(hipMemcpy(h_sj, sj, sizeof(int32_t) * (size_t)nzs, hipMemcpyDeviceToHost), "read S");
+            lap("strength");
+            // (phase 1 measured on the MI355X host at 300^3: this int32 form 83 ms;
+            // bitmap or byte flags with or without early exits 87-121 ms)
+            na = aijhip_gamg::aggregate_phase1(m, h_si, h_sj, agg);
+            GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
+        }
+        lap("phase 1");
         hipLaunchKernelGGL(k_agg_phase2, dim3(g256), dim3(256), 0, nullptr, m, si, sj, sval, d_ph, d_aggv);
         GTRY(hipMemset(d_left, 0, sizeof(unsigned long long)), "memset");
         hipLaunchKernelGGL(k_count_value, dim3(g256), dim3(256), 0, nullptr, m, d_aggv, -1, d_left);
@@ -1096,7 +1132,9 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
             unsigned long long left = 0;
             GTRY(hipMemcpy(&left, d_left, sizeof(left), hipMemcpyDeviceToHost), "read phase 2");
             lap("phase 2");
-            if (left > 0) {  // phase 3 (sequential) on the host
+            if (left > 0 && dev_agg) {  // phase 3 over the left-over nodes' rows only
+                GTRY(aijhip_gamg::aggregate_phase3_device(m, si, sj, d_aggv, &na), "phase 3");
+            } else if (left > 0) {  // phase 3 (sequential) on the host
                 GTRY(hipMemcpy(agg, d_aggv, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
                 na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
                 GTRY(hipMemcpy(d_aggv, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 3");

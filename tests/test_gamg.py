@@ -183,10 +183,15 @@ def _bits(x):
     ((16, 16, 16), dict(nsmooths=0)),
     ((32, 32, 32), dict(device_min_rows=20000)),  # device level 0, host below
 ])
-def test_gpu_device_setup_matches_host_bitwise(pkg, dims, params):
+@pytest.mark.parametrize("agg", ["auto", "device"])
+def test_gpu_device_setup_matches_host_bitwise(pkg, dims, params, agg, monkeypatch):
     """The KSP's device-built hierarchy (aijhip_gamg::build_device, host
     continuation below device_min_rows) equals the host builder's — itself
-    bit-identical to oracle/gamg.py — entry for entry."""
+    bit-identical to oracle/gamg.py — entry for entry. agg = device: the
+    aggregation's phase 1 as the device sweep on every level (automatic only
+    from 2^20 rows), phase 3 over the gathered left-over rows."""
+    if agg == "device":
+        monkeypatch.setenv("AIJHIP_GAMG_AGG", "device")
     ai, aj, aa = pkg.poisson_csr(*dims)
     _check_device_setup(pkg, ai, aj, aa, params)
 
@@ -252,9 +257,13 @@ def _hub_operator(n_side, hubs, seed, unsorted):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("unsorted", [False, True])
-def test_gpu_device_setup_long_strength_lists(pkg, unsorted):
+@pytest.mark.parametrize("agg", ["auto", "device"])
+def test_gpu_device_setup_long_strength_lists(pkg, unsorted, agg, monkeypatch):
     """Strength lists past one wavefront (a workgroup per row) and past the
     LDS list (a lane per row), on sorted and on unsorted rows: the device
-    hierarchy still equals the host builder's bit for bit."""
+    hierarchy still equals the host builder's bit for bit (with the phase-1
+    sweep too: hub rows make long walks and irregular root chains)."""
+    if agg == "device":
+        monkeypatch.setenv("AIJHIP_GAMG_AGG", "device")
     ai, aj, aa = _hub_operator(14, [(5, 40), (100, 300), (2000, 700), (7, 1500)], 7, unsorted)
     _check_device_setup(pkg, ai, aj, aa, dict(coarse_eq_limit=20))
