@@ -33,6 +33,9 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "gamg_device.h"
@@ -84,26 +87,43 @@ __global__ void k_lf_seed(int32_t m, int32_t *state, const int32_t *__restrict__
     roots[atomicAdd(&tails[0], 1u)] = i;
 }
 
-// Append v to list for the lanes with p set: one atomic per wavefront (the
-// tails are single counters every lane of a round appends to).
-__device__ __forceinline__ void wave_push(bool p, int32_t v, int32_t *list, unsigned *tail) {
-    const unsigned long long mask = __ballot(p);
-    if (!mask) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    unsigned base = 0;
-    if (lane == leader) base = atomicAdd(tail, (unsigned)__popcll(mask));
-    base = (unsigned)__shfl((int)base, leader, 64);
-    if (p) list[base + (unsigned)__popcll(mask & ((1ull << lane) - 1ull))] = v;
-}
-
 constexpr int kGroup = 8;   // lanes per frontier node: its strong neighbours split over them
 constexpr int kBatch2 = 8;  // second-step nodes loaded together before acting on them
 
+// Append k[u] for every (lane, u) with p[u] set to list: one atomic per
+// wavefront and batch (the tails are single counters every lane of a round
+// appends to), slots in (u, lane) order.
+__device__ __forceinline__ void wave_push(const bool (&p)[kBatch2], const int32_t (&k)[kBatch2], int32_t *list,
+                                          unsigned *tail) {
+    unsigned long long mask[kBatch2];
+    unsigned total = 0;
+#pragma unroll
+    for (int u = 0; u < kBatch2; ++u) {
+        mask[u] = __ballot(p[u]);
+        total += (unsigned)__popcll(mask[u]);
+    }
+    if (total == 0) return;
+    const int lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    unsigned long long any = 0;
+#pragma unroll
+    for (int u = 0; u < kBatch2; ++u) any |= mask[u];
+    const int leader = __ffsll(any) - 1;
+    unsigned base = 0;
+    if (lane == leader) base = atomicAdd(tail, total);
+    base = (unsigned)__shfl((int)base, leader, 64);
+#pragma unroll
+    for (int u = 0; u < kBatch2; ++u) {
+        if (p[u]) list[base + (unsigned)__popcll(mask[u] & below)] = k[u];
+        base += (unsigned)__popcll(mask[u]);
+    }
+}
+
 // The walks of frontier node i handled by one lane of its group: neighbours
-// j = S(i)[l], S(i)[l + kGroup], ... and their rows, in batches of kBatch2
-// (loads first, then the state reads, then act(k, state), so a lane's chain
-// is a few dependent steps per batch rather than per node).
+// j = S(i)[l], S(i)[l + kGroup], ... and their rows, in batches of kBatch2:
+// the batch's nodes, then their states, then act(k, st) on the whole batch,
+// whose atomics are independent of one another (a lane's chain is a few
+// dependent steps per batch, not per node).
 template <class Act>
 __device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int32_t *__restrict__ si,
                                             const int32_t *__restrict__ sj, const int32_t *state, Act act) {
@@ -117,7 +137,7 @@ __device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int
         const bool has_j = a < a1 - a0;
         const int32_t j = has_j ? sj[a0 + a] : 0;
         const int32_t b0 = has_j ? si[j] : 0, b1 = has_j ? si[j + 1] : 0;
-        int32_t len = b1 - b0 + 1;  // the neighbour itself, then its row
+        const int32_t len = has_j ? b1 - b0 + 1 : 0;  // the neighbour itself, then its row
         int32_t mx = len;
         for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o, 64));
         for (int32_t c = 0; c < mx; c += kBatch2) {
@@ -129,8 +149,7 @@ __device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int
             }
 #pragma unroll
             for (int u = 0; u < kBatch2; ++u) st[u] = k[u] > i ? state[k[u]] : kOut;
-#pragma unroll
-            for (int u = 0; u < kBatch2; ++u) act(k[u], st[u]);
+            act(k, st);
         }
     }
 }
@@ -152,8 +171,11 @@ __global__ __launch_bounds__(256) void k_lf_mark(int t, const int32_t *__restric
         const unsigned q = q0 + g0;
         const bool on = q < hi;
         const int32_t r = on ? roots[q] : 0;
-        group_walks(r, l, on, si, sj, state, [&](int32_t k, int32_t st) {
-            const bool p = on && st == kUndecided && atomicCAS(&state[k], kUndecided, kOut) == kUndecided;
+        group_walks(r, l, on, si, sj, state, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
+            bool p[kBatch2];
+#pragma unroll
+            for (int u = 0; u < kBatch2; ++u)
+                p[u] = on && st[u] == kUndecided && atomicCAS(&state[k[u]], kUndecided, kOut) == kUndecided;
             wave_push(p, k, outs, &tails[1]);
         });
     }
@@ -174,12 +196,13 @@ __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restri
         const unsigned q = q0 + g0;
         const bool on = q < hi;
         const int32_t j = on ? outs[q] : 0;
-        group_walks(j, l, on, si, sj, state, [&](int32_t k, int32_t st) {
-            bool p = false;
-            if (on && st == kUndecided && atomicSub(&cnt[k], 1) == 1) {
-                state[k] = kRoot;
-                p = true;
-            }
+        group_walks(j, l, on, si, sj, state, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
+            bool p[kBatch2];
+#pragma unroll
+            for (int u = 0; u < kBatch2; ++u) p[u] = on && st[u] == kUndecided && atomicSub(&cnt[k[u]], 1) == 1;
+#pragma unroll
+            for (int u = 0; u < kBatch2; ++u)
+                if (p[u]) state[k[u]] = kRoot;
             wave_push(p, k, roots, &tails[0]);
         });
     }
@@ -267,6 +290,10 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
         *done = true;
         return hipSuccess;
     }
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    const char *gs = std::getenv("AIJHIP_LF_GRID");
+    const unsigned grid = gs ? (unsigned)std::atoi(gs) : kRoundGrid;
+    auto clk = std::chrono::steady_clock::now();
     hipStream_t s = nullptr;
     int32_t *state = nullptr, *cnt = nullptr, *roots = nullptr, *outs = nullptr;
     unsigned *tails = nullptr, *rstart = nullptr, *ostart = nullptr, *h_ctl = nullptr;
@@ -289,12 +316,21 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
         hipLaunchKernelGGL(k_lf_seed, dim3(g), dim3(256), 0, s, m, state, cnt, roots, tails);
         e = hipGetLastError();
     }
+    auto lap = [&](const char *what) {
+        if (!log) return;
+        (void)hipStreamSynchronize(s);
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "  phase 1 sweep %-10s %8.3f ms\n", what,
+                     std::chrono::duration<double, std::milli>(now - clk).count());
+        clk = now;
+    };
+    lap("init");
     int t = 0;
     while (e == hipSuccess && t < max_rounds) {
         for (int b = 0; b < kBatch; ++b, ++t) {
-            hipLaunchKernelGGL(k_lf_mark, dim3(kRoundGrid), dim3(256), 0, s, t, si, sj, state, roots, outs, tails,
+            hipLaunchKernelGGL(k_lf_mark, dim3(grid), dim3(256), 0, s, t, si, sj, state, roots, outs, tails,
                                rstart);
-            hipLaunchKernelGGL(k_lf_count, dim3(kRoundGrid), dim3(256), 0, s, t, si, sj, state, cnt, roots, outs,
+            hipLaunchKernelGGL(k_lf_count, dim3(grid), dim3(256), 0, s, t, si, sj, state, cnt, roots, outs,
                                tails, ostart);
         }
         // finished when the last round found no new root: rstart[t] holds the
@@ -310,6 +346,7 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
         }
     }
     *rounds = t;
+    lap("rounds");
     if (e == hipSuccess && *done) {
         // every node decided (a check on the rule above), aggregate numbers in
         // root order
@@ -335,6 +372,7 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
             if (e == hipSuccess) e = hipStreamSynchronize(s);
         }
     }
+    lap("numbering");
     hipFree(state); hipFree(cnt); hipFree(roots); hipFree(outs);
     hipFree(tails); hipFree(rstart); hipFree(ostart);
     if (h_ctl) hipHostFree(h_ctl);
