@@ -90,7 +90,9 @@ int aijhip_comm_destroy(aijhip_comm_t comm);
  * Send side: peers send_peer[0..n_send) in that order; the local rows sent
  * to peer q are send_rows[send_off[q] .. send_off[q+1]).
  * Receive side, halo AIJHIP_HALO_P2P: ghost[recv_off[p] .. recv_off[p+1])
- * comes from recv_peer[p] (ghost length recv_off[n_recv]).
+ * comes from recv_peer[p] (ghost length recv_off[n_recv]). A peer may be
+ * this rank itself (a send/receive pair with itself is a local copy; PETSc's
+ * VecScatter does the same for self entries).
  * AIJHIP_HALO_ALLGATHER: n_send must be 1 with send_peer[0] = -1 (the rows
  * every other rank needs from this one, padded by the library to
  * gather_len); the ghost vector is the all-gather, nranks x gather_len

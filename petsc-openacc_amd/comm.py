@@ -138,11 +138,17 @@ class Comm:
                     outs = [torch.from_numpy(r[q * g:(q + 1) * g]) for q in range(world)]
                     dist.all_gather(outs, torch.from_numpy(s[:g].copy()), group=group)
                     return 0
-                works, bufs = [], []
+                works, bufs, own = [], [], None
                 for q, a, b in plan["send"]:
+                    if q == rank:  # a segment for this rank itself: a local copy
+                        own = s[a:b].copy()
+                        continue
                     bufs.append(torch.from_numpy(s[a:b].copy()))
                     works.append(dist.isend(bufs[-1], q, group=group))
                 for p, a, b in plan["recv"]:
+                    if p == rank:
+                        r[a:b] = own
+                        continue
                     works.append(dist.irecv(torch.from_numpy(r[a:b]), p, group=group))
                 for w in works:
                     w.wait()

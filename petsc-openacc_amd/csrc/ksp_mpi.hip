@@ -673,7 +673,7 @@ int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o,
         for (int32_t q = 0; q < n_send; ++q) {
             const int64_t a = send_off[q], b = send_off[q + 1];
             if (b < a || (b > a && !send_rows)) return bad("bad send_off");
-            if (halo == AIJHIP_HALO_P2P && (send_peer[q] < 0 || send_peer[q] >= comm->nranks || send_peer[q] == comm->rank))
+            if (halo == AIJHIP_HALO_P2P && (send_peer[q] < 0 || send_peer[q] >= comm->nranks))
                 return bad("bad send peer");
             bool contig = b > a;
             for (int64_t i = a; i < b; ++i) {
@@ -696,7 +696,7 @@ int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o,
         if (n_recv > 0 && recv_off[0] != 0) return bad("recv_off[0] must be 0");
         for (int32_t p = 0; p < n_recv; ++p) {
             if (recv_off[p + 1] < recv_off[p]) return bad("bad recv_off");
-            if (recv_peer[p] < 0 || recv_peer[p] >= comm->nranks || recv_peer[p] == comm->rank)
+            if (recv_peer[p] < 0 || recv_peer[p] >= comm->nranks)
                 return bad("bad recv peer");
             M->recv_peer.push_back(recv_peer[p]);
             M->recv_off.push_back(recv_off[p + 1]);

@@ -1,0 +1,144 @@
+"""The RCCL halo code paths at world size 1 (include/aijhip_mpi.h): RCCL
+refuses two ranks on one device, so a one-GPU box cannot run a real N > 1
+exchange; but a rank may send to and receive from itself, and an all-gather
+over one rank is a copy. Here the "ghost" columns are rows the rank owns
+(A_o holds the entries in those columns, A_d the rest), so the grouped
+ncclSend/ncclRecv (contiguous rows sent in place, scattered rows packed),
+the all-gather, the exchange stream and its events, and the distributed CG
+around them all run over a real RCCL communicator. Each result must equal,
+bit for bit, the same plan over the host transport (same kernels, same
+order) and the device's A_d x then A_o g product, and the CG must match the
+oracle's on the operator they represent (A)."""
+import importlib
+import os
+import socket
+
+import numpy as np
+import pytest
+
+from oracle import ksp_cg, seqaij
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def split_self(ai, aj, aa, G):
+    """A_d: the entries outside columns G (diagonal kept), columns unchanged;
+    A_o: the entries in columns G (off the diagonal), columns renumbered to
+    their position in G. Storage order kept in both."""
+    m = len(ai) - 1
+    pos = np.full(m, -1, np.int64)
+    pos[G] = np.arange(len(G))
+    rows = np.repeat(np.arange(m), np.diff(ai))
+    off = (pos[aj] >= 0) & (aj != rows)
+    d_cnt = np.bincount(rows[~off], minlength=m)
+    o_cnt = np.bincount(rows[off], minlength=m)
+    dai = np.concatenate([[0], np.cumsum(d_cnt)]).astype(np.int32)
+    oai = np.concatenate([[0], np.cumsum(o_cnt)]).astype(np.int32)
+    return (dai, aj[~off].astype(np.int32), aa[~off]), (oai, pos[aj[off]].astype(np.int32), aa[off])
+
+
+def _worker(port, N, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    out = {}
+    try:
+        pkg = importlib.import_module("petsc-openacc_amd")
+        C = importlib.import_module("petsc-openacc_amd.comm")
+        dev = torch.device("cuda:0")
+        comm_r = C.Comm.rccl(device=0, timeout_s=60)
+        comm_h = C.Comm.host(device=0, timeout_s=60)
+        ai, aj, aa = pkg.poisson_csr(N)
+        m = N ** 3
+        rhs, _ = pkg.poisson_vectors(N)
+        x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
+        b = torch.from_numpy(rhs).to(dev)
+        variants = {
+            "p2p_contiguous": ("p2p", np.arange(m - 2 * N * N, m)),
+            "p2p_scattered": ("p2p", np.arange(3, m, 7)),
+            "allgather": ("allgather", np.arange(0, m, 5)),
+        }
+        for name, (halo, G) in variants.items():
+            (dai, daj, daa), (oai, oaj, oaa) = split_self(ai, aj, aa, G)
+            Ad = pkg.SeqAIJHIP(dai, daj, daa, ncols=m)
+            Ao = pkg.SeqAIJHIP(oai, oaj, oaa, ncols=len(G))
+            if halo == "p2p":
+                send, recv, glen = [(0, G)], [(0, 0, len(G))], 0
+            else:
+                send, recv, glen = [(-1, G)], [], len(G)
+            res = {}
+            for kind, comm in (("rccl", comm_r), ("host", comm_h)):
+                op = C.NativeMPIAIJ(comm, Ad, Ao, halo, send, recv, glen)
+                y = torch.full_like(x, float("nan"))
+                op.mult(x, y)
+                op.mult(x, y)  # the ghost buffer and the send rows reused
+                torch.cuda.synchronize()
+                runs = {}
+                for pc in ("jacobi", "none"):
+                    xs = torch.full_like(b, float("nan"))
+                    with C.KSPCGMPINative(op, rtol=1e-10, max_it=2000, pc=pc) as kn:
+                        kn.solve(b, xs)
+                        runs[pc] = dict(its=kn.its, reason=kn.reason, hist=kn.hist.copy(), x=xs.cpu().numpy())
+                res[kind] = dict(y=y.cpu().numpy(), runs=runs)
+                op.destroy()
+            # the device's own A_d x, then A_o g added (MatMult_MPIAIJ's order)
+            yd = torch.empty_like(x)
+            Ad.mult(x, yd)
+            g = x[torch.from_numpy(G).to(dev)].contiguous()
+            ye = torch.empty_like(x)
+            Ao.mult_add(g, yd, ye)
+            torch.cuda.synchronize()
+            res["device"] = ye.cpu().numpy()
+            out[name] = res
+            Ad.destroy()
+            Ao.destroy()
+        out["info"] = comm_r.info()
+        comm_r.destroy()
+        comm_h.destroy()
+        q.put(out)
+    except Exception as e:  # noqa: BLE001
+        q.put({"error": repr(e)})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_rccl_self_exchange_paths_match_host_transport_bitwise():
+    import torch.multiprocessing as mp
+    N = 20
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_worker, args=(_free_port(), N, q))
+    p.start()
+    r = q.get(timeout=300)
+    p.join(timeout=120)
+    assert "error" not in r, r.get("error")
+    assert p.exitcode == 0
+    assert r["info"]["kind"] == "rccl" and r["info"]["nranks"] == 1
+    ai, aj, aa, rhs, _ = seqaij.create_system(N, N, N)
+    y_ref = seqaij.matmult(ai, aj, aa, seqaij.splitmix_uniform(N ** 3, 42))
+    for name in ("p2p_contiguous", "p2p_scattered", "allgather"):
+        res = r[name]
+        yr, yh = res["rccl"]["y"], res["host"]["y"]
+        assert np.array_equal(yr.view(np.uint64), yh.view(np.uint64)), name
+        assert np.array_equal(yr.view(np.uint64), res["device"].view(np.uint64)), name
+        # A_d + A_o = A; the A_o part of each row is added after A_d's: rounding
+        np.testing.assert_allclose(yr, y_ref, rtol=1e-12, atol=1e-12 * np.abs(y_ref).max())
+        for pc in ("jacobi", "none"):
+            a, h = res["rccl"]["runs"][pc], res["host"]["runs"][pc]
+            assert a["its"] == h["its"] and a["reason"] == h["reason"], (name, pc)
+            np.testing.assert_array_equal(a["hist"], h["hist"])
+            assert np.array_equal(a["x"].view(np.uint64), h["x"].view(np.uint64)), (name, pc)
+            xo, its_o, reason_o, hist_o = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-10, max_it=2000, pc=pc)
+            assert a["reason"] == reason_o and abs(a["its"] - its_o) <= 1, (name, pc, a["its"], its_o)
+            np.testing.assert_allclose(a["hist"][:10], hist_o[:10], rtol=1e-9)
+            assert np.linalg.norm(a["x"] - xo) <= 1e-8 * np.linalg.norm(xo)
