@@ -81,6 +81,23 @@ _I64P = ctypes.POINTER(ctypes.c_int64)
 _F64P = ctypes.POINTER(ctypes.c_double)
 
 
+def _bind_process_hip_runtime() -> None:
+    """One HIP runtime per process. PyTorch ships its own libamdhip64 under
+    the same soname (libamdhip64.so.7) as /opt/rocm's and loads it by path. If
+    this library came first it would bind ROCm's copy, torch would then load
+    its own, and whichever of the two initialised second would find no device
+    ("no ROCm-capable device is detected"; tests/test_runtime_binding_gpu.py).
+    Loading torch's copy first (without importing torch) makes the soname
+    resolve to it for both."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    hip = Path(spec.origin).parent / "lib" / "libamdhip64.so"
+    if hip.exists():
+        ctypes.CDLL(str(hip), mode=ctypes.RTLD_GLOBAL)
+
+
 def lib() -> ctypes.CDLL:
     """Load lib/libaijhip.so (built by build.py); fail loudly if absent."""
     global _lib
@@ -88,6 +105,7 @@ def lib() -> ctypes.CDLL:
         if not LIB_PATH.exists():
             raise AIJHIPError(AIJHIP_ERR_STATE, f"{LIB_PATH} is missing — run petsc-openacc_amd/build.py "
                                                 "(there is no CPU fallback)")
+        _bind_process_hip_runtime()
         L = ctypes.CDLL(str(LIB_PATH))
         L.aijhip_last_error.restype = ctypes.c_char_p
         for name in ABI_SYMBOLS + HARNESS_SYMBOLS:

@@ -454,7 +454,7 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
     if (rc) return rc;
     if (nz > 0 && !aa) return fail(AIJHIP_ERR_ARG, "aa is NULL");
     const int count = aijhip::visible_devices();
-    if (count <= 0) return fail(AIJHIP_ERR_NODEVICE, "no HIP device visible");
+    if (count <= 0) return fail(AIJHIP_ERR_NODEVICE, aijhip::no_device_reason());
     if (device < 0 || device >= count) return fail(AIJHIP_ERR_ARG, "device ordinal out of range");
     DeviceGuard g(device);
     if (g.err != hipSuccess) return hipfail(g.err, "set device");
@@ -490,12 +490,23 @@ void set_error(const std::string &msg) { g_err = msg; }
 
 // hipGetDeviceCount costs milliseconds per call on this stack; the count of a
 // process does not change, so it is asked once.
+namespace {
+hipError_t g_count_err = hipSuccess;  // why hipGetDeviceCount failed, if it did
+}
+
 int visible_devices() {
     static const int count = [] {
         int c = 0;
-        return hipGetDeviceCount(&c) == hipSuccess ? c : 0;
+        g_count_err = hipGetDeviceCount(&c);
+        return g_count_err == hipSuccess ? c : 0;
     }();
     return count;
+}
+
+std::string no_device_reason() {
+    return g_count_err == hipSuccess ? std::string("no HIP device visible")
+                                     : std::string("no HIP device visible (hipGetDeviceCount: ") +
+                                           hipGetErrorString(g_count_err) + ")";
 }
 
 int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai, int32_t *d_aj, double *d_aa,

@@ -270,5 +270,6 @@ hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t 
 // Sets the calling thread's aijhip_last_error() message.
 void set_error(const std::string &msg);
 int visible_devices();  // hipGetDeviceCount, cached
+std::string no_device_reason();  // the error text when visible_devices() is 0
 
 }  // namespace aijhip
