@@ -90,11 +90,20 @@ __global__ void k_lf_seed(int32_t m, int32_t *state, const int32_t *__restrict__
 constexpr int kGroup = 8;   // lanes per frontier node: its strong neighbours split over them
 constexpr int kBatch2 = 8;  // second-step nodes loaded together before acting on them
 
-// Append k[u] for every (lane, u) with p[u] set to list: one atomic per
-// wavefront and batch (the tails are single counters every lane of a round
-// appends to), slots in (u, lane) order.
-__device__ __forceinline__ void wave_push(const bool (&p)[kBatch2], const int32_t (&k)[kBatch2], int32_t *list,
-                                          unsigned *tail) {
+// A workgroup's appends gather in LDS and go to the global list with one
+// atomic on its tail per workgroup and pass (the tails are single counters
+// every workgroup of a round appends to; per-lane or per-wavefront atomics on
+// them serialise the middle rounds, whose frontiers are the largest).
+constexpr int kWgBuf = 2048;
+struct WgList {
+    int32_t v[kWgBuf];
+    unsigned n, base;
+};
+
+// Append k[u] for every (lane, u) with p[u] set: one LDS atomic per
+// wavefront and batch; past the buffer, straight to the global list.
+__device__ __forceinline__ void wg_add(WgList &L, const bool (&p)[kBatch2], const int32_t (&k)[kBatch2],
+                                       int32_t *list, unsigned *tail) {
     unsigned long long mask[kBatch2];
     unsigned total = 0;
 #pragma unroll
@@ -109,14 +118,30 @@ __device__ __forceinline__ void wave_push(const bool (&p)[kBatch2], const int32_
 #pragma unroll
     for (int u = 0; u < kBatch2; ++u) any |= mask[u];
     const int leader = __ffsll(any) - 1;
-    unsigned base = 0;
-    if (lane == leader) base = atomicAdd(tail, total);
-    base = (unsigned)__shfl((int)base, leader, 64);
+    unsigned pos = 0;
+    if (lane == leader) pos = atomicAdd(&L.n, total);
+    pos = (unsigned)__shfl((int)pos, leader, 64);
 #pragma unroll
     for (int u = 0; u < kBatch2; ++u) {
-        if (p[u]) list[base + (unsigned)__popcll(mask[u] & below)] = k[u];
-        base += (unsigned)__popcll(mask[u]);
+        if (p[u]) {
+            const unsigned idx = pos + (unsigned)__popcll(mask[u] & below);
+            if (idx < (unsigned)kWgBuf) L.v[idx] = k[u];
+            else list[atomicAdd(tail, 1u)] = k[u];
+        }
+        pos += (unsigned)__popcll(mask[u]);
     }
+}
+
+// Workgroup-uniform: the buffered appends to list[tail ...), coalesced.
+__device__ __forceinline__ void wg_flush(WgList &L, int32_t *list, unsigned *tail) {
+    __syncthreads();
+    const unsigned n = min(L.n, (unsigned)kWgBuf);
+    if (threadIdx.x == 0) L.base = n ? atomicAdd(tail, n) : 0u;
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < n; i += blockDim.x) list[L.base + i] = L.v[i];
+    __syncthreads();
+    if (threadIdx.x == 0) L.n = 0;
+    __syncthreads();
 }
 
 // The walks of frontier node i handled by one lane of its group: neighbours
@@ -126,7 +151,7 @@ __device__ __forceinline__ void wave_push(const bool (&p)[kBatch2], const int32_
 // dependent steps per batch, not per node).
 template <class Act>
 __device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int32_t *__restrict__ si,
-                                            const int32_t *__restrict__ sj, const int32_t *state, Act act) {
+                                            const int32_t *__restrict__ sj, const int32_t *state, bool pre, Act act) {
     const int32_t a0 = on ? si[i] : 0, a1 = on ? si[i + 1] : 0;
     // every lane of the wavefront runs the same number of batches, so that
     // act() may vote across the wavefront
@@ -148,7 +173,7 @@ __device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int
                 k[u] = e < len ? (e == 0 ? j : sj[b0 + e - 1]) : -1;
             }
 #pragma unroll
-            for (int u = 0; u < kBatch2; ++u) st[u] = k[u] > i ? state[k[u]] : kOut;
+            for (int u = 0; u < kBatch2; ++u) st[u] = k[u] > i ? (pre ? state[k[u]] : kUndecided) : kOut;
             act(k, st);
         }
     }
@@ -160,24 +185,29 @@ __device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int
 __global__ __launch_bounds__(256) void k_lf_mark(int t, const int32_t *__restrict__ si,
                                                  const int32_t *__restrict__ sj, int32_t *state,
                                                  const int32_t *__restrict__ roots, int32_t *outs, unsigned *tails,
-                                                 unsigned *rstart) {
+                                                 unsigned *rstart, int pre) {
     const unsigned lo = rstart[t], hi = tails[0];
     if (blockIdx.x == 0 && threadIdx.x == 0) rstart[t + 1] = hi;
+    if (lo >= hi) return;  // grid-uniform
+    __shared__ WgList L;
+    if (threadIdx.x == 0) L.n = 0;
+    __syncthreads();
     const int l = threadIdx.x % kGroup;
     const unsigned groups = gridDim.x * (blockDim.x / kGroup);
     const unsigned g0 = blockIdx.x * (blockDim.x / kGroup) + threadIdx.x / kGroup;
-    // wavefront-uniform trip count (wave_push votes across the wavefront)
+    // workgroup-uniform trip count (wg_flush synchronises the workgroup)
     for (unsigned q0 = lo; q0 < hi; q0 += groups) {
         const unsigned q = q0 + g0;
         const bool on = q < hi;
         const int32_t r = on ? roots[q] : 0;
-        group_walks(r, l, on, si, sj, state, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
+        group_walks(r, l, on, si, sj, state, pre != 0, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
             bool p[kBatch2];
 #pragma unroll
             for (int u = 0; u < kBatch2; ++u)
                 p[u] = on && st[u] == kUndecided && atomicCAS(&state[k[u]], kUndecided, kOut) == kUndecided;
-            wave_push(p, k, outs, &tails[1]);
+            wg_add(L, p, k, outs, &tails[1]);
         });
+        wg_flush(L, outs, &tails[1]);
     }
 }
 
@@ -186,9 +216,13 @@ __global__ __launch_bounds__(256) void k_lf_mark(int t, const int32_t *__restric
 __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restrict__ si,
                                                   const int32_t *__restrict__ sj, int32_t *state, int32_t *cnt,
                                                   int32_t *roots, const int32_t *__restrict__ outs, unsigned *tails,
-                                                  unsigned *ostart) {
+                                                  unsigned *ostart, int pre) {
     const unsigned lo = ostart[t], hi = tails[1];
     if (blockIdx.x == 0 && threadIdx.x == 0) ostart[t + 1] = hi;
+    if (lo >= hi) return;  // grid-uniform
+    __shared__ WgList L;
+    if (threadIdx.x == 0) L.n = 0;
+    __syncthreads();
     const int l = threadIdx.x % kGroup;
     const unsigned groups = gridDim.x * (blockDim.x / kGroup);
     const unsigned g0 = blockIdx.x * (blockDim.x / kGroup) + threadIdx.x / kGroup;
@@ -196,15 +230,16 @@ __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restri
         const unsigned q = q0 + g0;
         const bool on = q < hi;
         const int32_t j = on ? outs[q] : 0;
-        group_walks(j, l, on, si, sj, state, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
+        group_walks(j, l, on, si, sj, state, pre != 0, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
             bool p[kBatch2];
 #pragma unroll
             for (int u = 0; u < kBatch2; ++u) p[u] = on && st[u] == kUndecided && atomicSub(&cnt[k[u]], 1) == 1;
 #pragma unroll
             for (int u = 0; u < kBatch2; ++u)
                 if (p[u]) state[k[u]] = kRoot;
-            wave_push(p, k, roots, &tails[0]);
+            wg_add(L, p, k, roots, &tails[0]);
         });
+        wg_flush(L, roots, &tails[0]);
     }
 }
 
@@ -293,6 +328,12 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     const char *gs = std::getenv("AIJHIP_LF_GRID");
     const unsigned grid = gs ? (unsigned)std::atoi(gs) : kRoundGrid;
+    // read a node's state before its atomic (skips decided nodes; one more
+    // dependent load per round) or go straight to the atomic (a decided
+    // node's CAS fails; an OUT node's count never reaches 0, a root's gets no
+    // further walks)
+    const char *ps = std::getenv("AIJHIP_LF_PREREAD");
+    const int pre = ps ? std::atoi(ps) : 1;
     auto clk = std::chrono::steady_clock::now();
     hipStream_t s = nullptr;
     int32_t *state = nullptr, *cnt = nullptr, *roots = nullptr, *outs = nullptr;
@@ -329,9 +370,9 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     while (e == hipSuccess && t < max_rounds) {
         for (int b = 0; b < kBatch; ++b, ++t) {
             hipLaunchKernelGGL(k_lf_mark, dim3(grid), dim3(256), 0, s, t, si, sj, state, roots, outs, tails,
-                               rstart);
+                               rstart, pre);
             hipLaunchKernelGGL(k_lf_count, dim3(grid), dim3(256), 0, s, t, si, sj, state, cnt, roots, outs,
-                               tails, ostart);
+                               tails, ostart, pre);
         }
         // finished when the last round found no new root: rstart[t] holds the
         // root count the last mark launch saw
