@@ -96,7 +96,7 @@ int aijhip_ksp_get_pc_level(aijhip_ksp_t ksp, int32_t l, char which, int32_t *m,
  * one per level but the coarsest): path[l] = 1 on the device
  * (aijhip_gamg build_device), 0 on the host builder; product_cols[l] = the
  * widest accumulator the device Galerkin products needed (0 = the wavefront
- * form, else 64 / 128 / 256 LDS columns per row; -1 on the host).
+ * form, else 32 / 64 / 128 / 256 LDS columns per row; -1 on the host).
  * *host_fallback = 1 when a level the device would have built went to the
  * host because a product row exceeded 256 distinct columns. */
 int aijhip_ksp_get_gamg_setup_path(aijhip_ksp_t ksp, int32_t cap, int32_t *path, int32_t *product_cols,

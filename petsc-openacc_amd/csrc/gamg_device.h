@@ -15,7 +15,7 @@ struct DeviceLevel {
     aijhip_mat *P = nullptr;  // prolongator to the next level, P^T attached
     double emax = 0.0;
     // the widest accumulator class the Galerkin products building P and
-    // A_{l+1} needed: 0 = wavefront form, else 64 / 128 / 256 LDS columns
+    // A_{l+1} needed: 0 = wavefront form, else 32 / 64 / 128 / 256 LDS columns
     int product_cols = 0;
 };
 

@@ -650,11 +650,23 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
     int32_t *cnt = nullptr;
     hipError_t e;
     if ((e = dalloc(&cnt, A.m)) != hipSuccess) return herr(e, "product counts");
+    // products per row (mean): A's row length x B's
+    double per_row = 0.0;
+    {
+        int32_t bnz = 0;
+        if ((e = hipMemcpy(&bnz, B.ai + B.m, sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess) {
+            hipFree(cnt);
+            return herr(e, "product sizes");
+        }
+        per_row = B.m > 0 ? (double)A.nz * ((double)bnz / (double)B.m) / std::max<int32_t>(A.m, 1) : 0.0;
+    }
     constexpr int kWaveK = 16;  // columns per lane: up to 1024 per row
     const unsigned gw = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.m + 3) / 4, (int64_t)n_cu * 16));
     // the wave form pays off for few, heavy rows (coarse Galerkin products:
     // 744 rows of ~20k products, 34 -> 15 ms at 300^3); for many light rows
     // one lane per row keeps every lane busy (27 M rows: 27 vs 288 ms)
+    // (for many heavy rows as well: P^T (A P) at 300^3, 3.27 M rows of ~290
+    // products, 43 ms one lane per row, 322 ms one wave per row)
     if (A.m <= 8192) {
         hipLaunchKernelGGL((k_rowprod_wave<kWaveK, false>), dim3(gw), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
                            B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt);
@@ -715,9 +727,14 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
         hipFree(dmin);
         return r;
     };
-    int level = 0;
+    // light products (A*P0, A*P on the finest level: ~4 and ~25 products
+    // per row) start in a 32-column class: 24 KiB of LDS per 64-row
+    // workgroup in the numeric pass instead of 48, twice the waves per CU
+    const bool small = per_row <= 48.0;
+    int level = small ? -1 : 0;
     for (;; ++level) {
-        if (level == 0) e = rowprod_pass<64, 64>(A, B, cnt, false, 0, 0, nullptr, nullptr, false, n_cu);
+        if (level == -1) e = rowprod_pass<32, 64>(A, B, cnt, false, 0, 0, nullptr, nullptr, false, n_cu);
+        else if (level == 0) e = rowprod_pass<64, 64>(A, B, cnt, small, 0, 0, nullptr, nullptr, false, n_cu);
         else if (level == 1) e = rowprod_pass<128, 32>(A, B, cnt, true, 0, 0, nullptr, nullptr, false, n_cu);
         else if (level == 2) e = rowprod_pass<256, 16>(A, B, cnt, true, 0, 0, nullptr, nullptr, false, n_cu);
         else { hipFree(cnt); return AIJHIP_ERR_STATE; }
@@ -742,12 +759,13 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
         C.release();
         return herr(e, "product alloc");
     }
-    e = rowprod_pass<64, 64>(A, B, cnt, false, -1, 64, C.ai, &C, true, n_cu);
+    if (small) e = rowprod_pass<32, 64>(A, B, cnt, false, -1, 32, C.ai, &C, true, n_cu);
+    if (e == hipSuccess && level >= 0) e = rowprod_pass<64, 64>(A, B, cnt, false, small ? 32 : -1, 64, C.ai, &C, true, n_cu);
     if (e == hipSuccess && level >= 1) e = rowprod_pass<128, 32>(A, B, cnt, false, 64, 128, C.ai, &C, true, n_cu);
     if (e == hipSuccess && level >= 2) e = rowprod_pass<256, 16>(A, B, cnt, false, 128, 256, C.ai, &C, true, n_cu);
     hipFree(cnt);
     if (e != hipSuccess) { C.release(); return herr(e, "numeric product"); }
-    if (cols_used) *cols_used = std::max(*cols_used, 64 << level);
+    if (cols_used) *cols_used = std::max(*cols_used, level < 0 ? 32 : 64 << level);
     return AIJHIP_OK;
 }
 
