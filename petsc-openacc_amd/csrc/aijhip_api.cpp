@@ -365,12 +365,36 @@ int structure_and_plan(aijhip_mat *A, const int32_t *ai, aijhip::HostVec<int32_t
     const int32_t m = A->m;
     const int64_t nz = A->nz;
     hipError_t e;
-    // structure statistics (PETSc a->nonzerorowcnt, MatCheckCompressedRow)
+    // structure statistics (PETSc a->nonzerorowcnt, MatCheckCompressedRow);
+    // row ranges on host threads for large operands, as the planning below
     int32_t nzrows = 0, maxlen = 0;
-    for (int32_t i = 0; i < m; ++i) {
-        const int32_t l = ai[i + 1] - ai[i];
-        nzrows += l > 0;
-        maxlen = std::max(maxlen, l);
+    {
+        const int nt = m >= kParallelPlanRows
+                           ? (int)std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()))
+                           : 1;
+        std::vector<int32_t> pz(nt, 0), pm(nt, 0);
+        auto stats = [&](int t) {
+            const int32_t r0 = (int32_t)((int64_t)m * t / nt), r1 = (int32_t)((int64_t)m * (t + 1) / nt);
+            int32_t z = 0, x = 0;
+            for (int32_t i = r0; i < r1; ++i) {
+                const int32_t l = ai[i + 1] - ai[i];
+                z += l > 0;
+                x = std::max(x, l);
+            }
+            pz[t] = z;
+            pm[t] = x;
+        };
+        if (nt <= 1) {
+            stats(0);
+        } else {
+            std::vector<std::thread> th;
+            for (int t = 0; t < nt; ++t) th.emplace_back(stats, t);
+            for (auto &x : th) x.join();
+        }
+        for (int t = 0; t < nt; ++t) {
+            nzrows += pz[t];
+            maxlen = std::max(maxlen, pm[t]);
+        }
     }
     A->nonzerorowcnt = nzrows;
     A->max_row_nz = maxlen;

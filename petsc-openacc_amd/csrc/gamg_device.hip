@@ -1084,22 +1084,6 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         // emax(D^-1 A) needs only A: its power iteration runs from a second
         // host thread while this one stages S and aggregates on the CPU
         EmaxJob job;
-        // A level that will aggregate on the host needs S in pinned memory: the
-        // (first-time) pinned allocation runs on a second host thread while
-        // the strength kernels run, sized from A's off-diagonal count (S's
-        // size when A's pattern is symmetric; reserve() grows it if not).
-        std::thread stage_th;
-        hipError_t stage_e = hipSuccess;
-        {
-            int32_t rounds_guess = 0;
-            if (!device_phase1(m, std::max<int64_t>(A.nz - m, 0), &rounds_guess)) {
-                const size_t want = sizeof(int32_t) * ((size_t)m + 1 + (size_t)std::max<int64_t>(A.nz - m, 0) + (size_t)m);
-                stage_th = std::thread([&stage, &stage_e, want, dev = A.device] {
-                    (void)hipSetDevice(dev);
-                    stage_e = stage.reserve(want);
-                });
-            }
-        }
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto level_done; } } while (0)
         GTRY(dalloc(&d, m), "alloc");
         GTRY(dalloc(&dinv, m), "alloc");
@@ -1144,8 +1128,6 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
                                  sweep_rounds, dev_agg ? "" : " (too deep: host pass)");
             }
         }
-        if (stage_th.joinable()) stage_th.join();
-        GTRY(stage_e, "pinned staging");
         if (!dev_agg) {
             GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
             lap("staging alloc");
@@ -1179,7 +1161,6 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         lap("aggregate");
     level_done:
         job.join();
-        if (stage_th.joinable()) stage_th.join();
         hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
         hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left);
         if (rc || na >= m || na == 0) {  // an error, or no coarsening: this is the coarsest level
