@@ -118,6 +118,93 @@ __global__ void k_rows_unsorted(int32_t m, const int32_t *__restrict__ ai, const
         if (aj[k] <= aj[k - 1]) { atomicOr(flag, 1); return; }
 }
 
+// S straight from A when A's rows are sorted and the strong pattern is
+// symmetric (Galerkin operators of a symmetric operand, the 7-point one):
+// then S u S^T = S, already sorted and unique, every entry a stored one.
+// G lanes per row (rows of up to a few G entries; a wave holds 64 / G rows).
+#define AIJHIP_ROW_LANES                                                                                      \
+    const int lane = threadIdx.x & 63;                                                                        \
+    const int l = lane & (G - 1);                                                                             \
+    const unsigned long long segmask = (G == 64 ? ~0ull : ((1ull << G) - 1ull)) << (lane & ~(G - 1));         \
+    const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;                                                \
+    for (int64_t base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * (64 / G); base < m;         \
+         base += nw * (64 / G))
+
+template <int G>
+__global__ __launch_bounds__(256) void k_strong_direct_count(int32_t m, const int32_t *__restrict__ ai,
+                                                             const int32_t *__restrict__ aj,
+                                                             const double *__restrict__ aa,
+                                                             const double *__restrict__ d, double theta,
+                                                             int32_t *cnt) {
+    AIJHIP_ROW_LANES {
+        const int64_t i = base + lane / G;
+        const bool on = i < m;
+        const int32_t a0 = on ? ai[i] : 0, a1 = on ? ai[i + 1] : 0;
+        int32_t c = 0;
+        for (int32_t k = a0 + l; k < a1; k += G) c += strong((int32_t)i, aj[k], aa[k], d, theta);
+        for (int o = G / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (on && l == 0) cnt[i] = c;
+    }
+}
+
+// the strong entries in A's order: lanes take entries l, l + G, ... and
+// place them by a ballot over the row's lanes
+template <int G>
+__global__ __launch_bounds__(256) void k_strong_direct_fill(int32_t m, const int32_t *__restrict__ ai,
+                                                            const int32_t *__restrict__ aj,
+                                                            const double *__restrict__ aa,
+                                                            const double *__restrict__ d, double theta,
+                                                            const int32_t *__restrict__ si, int32_t *sj,
+                                                            double *sval) {
+    AIJHIP_ROW_LANES {
+        const int64_t i = base + lane / G;
+        const bool on = i < m;
+        const int32_t a0 = on ? ai[i] : 0, a1 = on ? ai[i + 1] : 0;
+        int32_t len = a1 - a0;
+        for (int o = 32; o > 0; o >>= 1) len = max(len, __shfl_xor(len, o, 64));
+        int32_t o = on ? si[i] : 0;
+        for (int32_t r = 0; r < len; r += G) {  // wavefront-uniform rounds
+            const int32_t k = a0 + r + l;
+            const bool in = k < a1;
+            const int32_t j = in ? aj[k] : 0;
+            const double a = in ? aa[k] : 0.0;
+            const bool keep = in && strong((int32_t)i, j, a, d, theta);
+            const unsigned long long bal = __ballot(keep) & segmask;
+            if (keep) {
+                const int pos = __popcll(bal & ((1ull << lane) - 1ull));
+                sj[o + pos] = j;
+                sval[o + pos] = fabs(a);
+            }
+            o += __popcll(bal);
+        }
+    }
+}
+
+// flag = 1 when some (i, j) of S has no (j, i)
+template <int G>
+__global__ __launch_bounds__(256) void k_strong_asymmetric(int32_t m, const int32_t *__restrict__ si,
+                                                           const int32_t *__restrict__ sj, int32_t *flag) {
+    AIJHIP_ROW_LANES {
+        const int64_t i = base + lane / G;
+        if (i >= m) continue;
+        (void)segmask;
+        bool bad = false;
+        for (int32_t k = si[i] + l; k < si[i + 1] && !bad; k += G) {
+            const int32_t j = sj[k];
+            const int32_t e = si[j + 1];
+            int32_t lo = si[j], hi = e;
+            while (lo < hi) {
+                const int32_t q = (lo + hi) >> 1;
+                if (sj[q] < (int32_t)i) lo = q + 1;
+                else hi = q;
+            }
+            bad = lo == e || sj[lo] != (int32_t)i;
+        }
+        if (bad) atomicOr(flag, 1);
+    }
+}
+#undef AIJHIP_ROW_LANES
+
 // Each gathered neighbour list of at most G entries sorted and made unique
 // by G lanes (bitonic across the segment's lanes, unique by ballot), with the
 // kept entries' weights: written back in place (tmp, tval), count to ucnt.
@@ -769,6 +856,69 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
     return AIJHIP_OK;
 }
 
+// S directly from A (k_strong_direct_*): *ok = false, nothing allocated,
+// when A has an unsorted row or the strong pattern is not symmetric (the
+// caller then gathers S u S^T).
+int strength_direct(const aijhip_mat &A, const double *d, double theta, int32_t **si, int32_t **sj,
+                    double **sval, int64_t *nzs, bool *ok) {
+    const int32_t m = A.m;
+    const unsigned g256 = blocks_for(m, 256);
+    int32_t *cnt = nullptr, *flag = nullptr;
+    int32_t h_flag = 0;
+    hipError_t e;
+    int rc = AIJHIP_OK;
+    *ok = false;
+    *si = *sj = nullptr;
+    *sval = nullptr;
+#define DTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto done; } } while (0)
+    DTRY(dalloc(&flag, 1), "alloc");
+    DTRY(hipMemset(flag, 0, sizeof(int32_t)), "memset");
+    hipLaunchKernelGGL(k_rows_unsorted, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, flag);
+    DTRY(hipMemcpy(&h_flag, flag, sizeof(h_flag), hipMemcpyDeviceToHost), "read");
+    if (h_flag) goto done;
+    {
+        // lanes per row: the mean row length rounded up to a power of two
+        const double mean = m > 0 ? (double)A.nz / m : 1.0;
+        int G = 4;
+        while (G < 64 && G < mean) G <<= 1;
+        const unsigned grid = (unsigned)std::min<int64_t>(blocks_for((int64_t)m * G, 256), (int64_t)A.n_cu * 64);
+        DTRY(dalloc(&cnt, m), "alloc");
+#define AIJHIP_SD(GG)                                                                                         \
+    case GG:                                                                                                  \
+        hipLaunchKernelGGL((k_strong_direct_count<GG>), dim3(grid), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj,  \
+                           A.d_aa, d, theta, cnt);                                                            \
+        break
+        switch (G) { AIJHIP_SD(4); AIJHIP_SD(8); AIJHIP_SD(16); AIJHIP_SD(32); AIJHIP_SD(64); }
+#undef AIJHIP_SD
+        DTRY(dalloc(si, (int64_t)m + 1), "alloc");
+        DTRY(scan_offsets(cnt, m, *si, nzs), "scan");
+        if (*nzs > INT32_MAX) { rc = AIJHIP_ERR_ARG; set_error("GAMG: strength graph exceeds int32"); goto done; }
+        DTRY(dalloc(sj, *nzs), "alloc");
+        DTRY(dalloc(sval, *nzs), "alloc");
+#define AIJHIP_SD(GG)                                                                                         \
+    case GG:                                                                                                  \
+        hipLaunchKernelGGL((k_strong_direct_fill<GG>), dim3(grid), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj,   \
+                           A.d_aa, d, theta, *si, *sj, *sval);                                                \
+        hipLaunchKernelGGL((k_strong_asymmetric<GG>), dim3(grid), dim3(256), 0, nullptr, m, *si, *sj, flag);  \
+        break
+        switch (G) { AIJHIP_SD(4); AIJHIP_SD(8); AIJHIP_SD(16); AIJHIP_SD(32); AIJHIP_SD(64); }
+#undef AIJHIP_SD
+    }
+    DTRY(hipGetLastError(), "strength kernels");
+    DTRY(hipMemcpy(&h_flag, flag, sizeof(h_flag), hipMemcpyDeviceToHost), "read");
+    *ok = h_flag == 0;
+done:
+#undef DTRY
+    hipFree(cnt);
+    hipFree(flag);
+    if (rc || !*ok) {
+        hipFree(*si); hipFree(*sj); hipFree(*sval);
+        *si = *sj = nullptr;
+        *sval = nullptr;
+    }
+    return rc;
+}
+
 // S from the gathered lists (tmp, rows at off, cnt entries each): sorted,
 // unique, weighted, compacted into (si, sj, sval) of *nzs entries.
 int strength_lists(const aijhip_mat &A, const unsigned long long *cnt, const unsigned long long *off,
@@ -1088,6 +1238,14 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         GTRY(dalloc(&d, m), "alloc");
         GTRY(dalloc(&dinv, m), "alloc");
         hipLaunchKernelGGL(k_diag_dinv, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d, dinv);
+        {
+            bool direct = false;  // S straight from A (sorted rows, symmetric strong pattern)
+            if ((rc = strength_direct(A, d, p.threshold, &si, &sj, &sval, &nzs, &direct))) goto level_done;
+            if (log)
+                std::fprintf(stderr, "gamg device level %zu strength graph: %s\n", levels.size() - 1,
+                             direct ? "direct (symmetric)" : "gathered (S u S^T)");
+            if (direct) goto strength_done;
+        }
         GTRY(dalloc(&cnt, (int64_t)m + 1), "alloc");
         GTRY(dalloc(&off, (int64_t)m + 1), "alloc");
         GTRY(hipMemset(cnt, 0, sizeof(unsigned long long) * ((size_t)m + 1)), "memset");
@@ -1107,6 +1265,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         hipLaunchKernelGGL(k_strong_fill, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
                            p.threshold, off, pos, tmp);
         if ((rc = strength_lists(A, cnt, off, tmp, nzs, n_cu, &si, &sj, &sval, &nzs))) goto level_done;
+    strength_done:
         GTRY(hipGetLastError(), "strength kernels");
         // ---- aggregation. Phase 1: the device sweep (gamg_aggregate.hip) on
         // large levels with a sparse S, else -- or when the sweep would run too
