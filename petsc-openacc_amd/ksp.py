@@ -127,7 +127,7 @@ class KSPCG:
 
     def setup_path(self):
         """Per coarsening l -> l+1: ("device"|"host", widest product
-        accumulator: 0 = wavefront form, 64/128/256 LDS columns, -1 host), and
+        accumulator: 0 = wavefront form, 32/64/128/256 LDS columns, -1 host), and
         whether a device level overflowed to the host builder."""
         path = np.zeros(32, np.int32)
         cols = np.zeros(32, np.int32)

@@ -220,7 +220,9 @@ def _check_device_setup(pkg, ai, aj, aa, params):
             assert pn == lv[l + 1]["m"]
             assert np.array_equal(pai, hai) and np.array_equal(paj, haj), l
             assert np.array_equal(_bits(paa), _bits(haa)), l
+        path, _ = ksp.setup_path()
     A.destroy()
+    return path
 
 
 def _hub_operator(n_side, hubs, seed, unsorted):
@@ -267,3 +269,53 @@ def test_gpu_device_setup_long_strength_lists(pkg, unsorted, agg, monkeypatch):
         monkeypatch.setenv("AIJHIP_GAMG_AGG", "device")
     ai, aj, aa = _hub_operator(14, [(5, 40), (100, 300), (2000, 700), (7, 1500)], 7, unsorted)
     _check_device_setup(pkg, ai, aj, aa, dict(coarse_eq_limit=20))
+
+
+def _spd_from_pattern(m, rows, cols, seed):
+    """Symmetric, diagonally dominant (negative diagonal, as the Poisson
+    rows) from an off-diagonal pattern; rows sorted."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    w = rng.uniform(0.5, 2.0, size=len(rows))
+    B = sp.coo_matrix((np.concatenate([w, w]), (np.concatenate([rows, cols]), np.concatenate([cols, rows]))),
+                      shape=(m, m)).tocsr()
+    B.sum_duplicates()
+    off = np.asarray(abs(B).sum(axis=1)).ravel()
+    B = B + sp.diags(-(off + 1.0))
+    B = sp.csr_matrix(B)
+    B.sort_indices()
+    return B.indptr.astype(np.int32), B.indices.astype(np.int32), B.data.astype(np.float64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["path", "random", "isolated"])
+def test_gpu_device_aggregation_sweep_on_irregular_graphs(pkg, case, monkeypatch):
+    """The phase-1 device sweep (gamg_aggregate.hip, forced on every level)
+    on graphs unlike the 7-point lattice: a path (a chain of ~m/3 roots, one
+    per round), a random symmetric graph, and a lattice with isolated rows
+    (no strong neighbour: never a root, phase 3 singletons). The hierarchy
+    must equal the host builder's bit for bit."""
+    monkeypatch.setenv("AIJHIP_GAMG_AGG", "device")
+    if case == "path":
+        m = 6000
+        r = np.arange(m - 1)
+        ai, aj, aa = _spd_from_pattern(m, r, r + 1, 1)
+    elif case == "random":
+        m = 30000
+        rng = np.random.default_rng(3)
+        r = rng.integers(0, m, size=m)  # mean degree 2 (wider Galerkin rows outgrow the device classes)
+        c = rng.integers(0, m, size=m)
+        keep = r != c
+        ai, aj, aa = _spd_from_pattern(m, r[keep], c[keep], 2)
+    else:
+        import scipy.sparse as sp
+        pai, paj, paa = pkg.poisson_csr(12)
+        P = sp.csr_matrix((paa, paj, pai), shape=(1728, 1728))
+        iso = sp.diags(np.full(200, -3.0))
+        B = sp.csr_matrix(sp.block_diag([P, iso]))
+        perm = np.random.default_rng(5).permutation(B.shape[0])  # isolated rows spread through the order
+        B = sp.csr_matrix(B[perm][:, perm])
+        B.sort_indices()
+        ai, aj, aa = B.indptr.astype(np.int32), B.indices.astype(np.int32), B.data.astype(np.float64)
+    path = _check_device_setup(pkg, ai, aj, aa, dict(coarse_eq_limit=20))
+    assert path[0][0] == "device", path  # the finest coarsening was built on the device: the sweep ran
