@@ -500,33 +500,63 @@ __global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__res
         if (NUMERIC && (cnt[i] <= lo || cnt[i] > hi)) continue;     // another CAP's class
         int n = 0;
         bool over = false;
-        for (int32_t k = ai[i]; k < ai[i + 1] && !over; ++k) {
-            const int32_t j = aj[k];
-            const double a = NUMERIC ? aa[k] : 0.0;
-            for (int32_t q = bi[j]; q < bi[j + 1]; ++q) {
-                const int32_t c = bj[q];
-                int l = 0, h = n;
-                while (l < h) {
-                    const int mid = (l + h) >> 1;
-                    if (sc[mid * TPB + t] < c) l = mid + 1;
-                    else h = mid;
+        // the row's products in traversal order, their operands loaded in
+        // batches (KB entries of A, then QB entries of each B row) ahead of
+        // the LDS work: one exposed memory latency per batch, not per product
+        constexpr int KB = 4, QB = 8;
+        const int32_t k1 = ai[i + 1];
+        for (int32_t kb = ai[i]; kb < k1 && !over; kb += KB) {
+            int32_t jj[KB], q0[KB], q1[KB];
+            double av[KB];
+#pragma unroll
+            for (int u = 0; u < KB; ++u) {
+                const bool in = kb + u < k1;
+                jj[u] = in ? aj[kb + u] : 0;
+                av[u] = (NUMERIC && in) ? aa[kb + u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < KB; ++u) {
+                const bool in = kb + u < k1;
+                q0[u] = in ? bi[jj[u]] : 0;
+                q1[u] = in ? bi[jj[u] + 1] : 0;
+            }
+            for (int u = 0; u < KB && !over; ++u) {
+                const double a = av[u];
+                for (int32_t qb = q0[u]; qb < q1[u] && !over; qb += QB) {
+                    int32_t cc[QB];
+                    double bv[QB];
+#pragma unroll
+                    for (int w = 0; w < QB; ++w) {
+                        const bool in = qb + w < q1[u];
+                        cc[w] = in ? bj[qb + w] : 0;
+                        bv[w] = (NUMERIC && in) ? ba[qb + w] : 0.0;
+                    }
+                    for (int w = 0; w < QB && qb + w < q1[u]; ++w) {
+                        const int32_t c = cc[w];
+                        int l = 0, h = n;
+                        while (l < h) {
+                            const int mid = (l + h) >> 1;
+                            if (sc[mid * TPB + t] < c) l = mid + 1;
+                            else h = mid;
+                        }
+                        if (l < n && sc[l * TPB + t] == c) {
+                            if (NUMERIC) sv[l * TPB + t] += a * bv[w];
+                            continue;
+                        }
+                        if (n == CAP) { over = true; break; }
+                        for (int z = n; z > l; --z) {
+                            sc[z * TPB + t] = sc[(z - 1) * TPB + t];
+                            if (NUMERIC) sv[z * TPB + t] = sv[(z - 1) * TPB + t];
+                        }
+                        sc[l * TPB + t] = c;
+                        if (NUMERIC) {
+                            double v0 = 0.0;
+                            v0 += a * bv[w];
+                            sv[l * TPB + t] = v0;
+                        }
+                        ++n;
+                    }
                 }
-                if (l < n && sc[l * TPB + t] == c) {
-                    if (NUMERIC) sv[l * TPB + t] += a * ba[q];
-                    continue;
-                }
-                if (n == CAP) { over = true; break; }
-                for (int z = n; z > l; --z) {
-                    sc[z * TPB + t] = sc[(z - 1) * TPB + t];
-                    if (NUMERIC) sv[z * TPB + t] = sv[(z - 1) * TPB + t];
-                }
-                sc[l * TPB + t] = c;
-                if (NUMERIC) {
-                    double v0 = 0.0;
-                    v0 += a * ba[q];
-                    sv[l * TPB + t] = v0;
-                }
-                ++n;
             }
         }
         if (!NUMERIC) {
