@@ -503,7 +503,7 @@ __global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__res
         // the row's products in traversal order, their operands loaded in
         // batches (KB entries of A, then QB entries of each B row) ahead of
         // the LDS work: one exposed memory latency per batch, not per product
-        constexpr int KB = 4, QB = 8;
+        constexpr int KB = 8, QB = 16;
         const int32_t k1 = ai[i + 1];
         for (int32_t kb = ai[i]; kb < k1 && !over; kb += KB) {
             int32_t jj[KB], q0[KB], q1[KB];
