@@ -782,8 +782,12 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
     // the wave form pays off for few, heavy rows (coarse Galerkin products:
     // 744 rows of ~20k products, 34 -> 15 ms at 300^3); for many light rows
     // one lane per row keeps every lane busy (27 M rows: 27 vs 288 ms)
-    // (for many heavy rows as well: P^T (A P) at 300^3, 3.27 M rows of ~290
-    // products, 43 ms one lane per row, 322 ms one wave per row)
+    // (for many heavy rows too: at 300^3 the finest P^T (A P), 3.27 M rows of
+    // ~270 products, 43 ms one lane per row vs 322 ms one wave per row; the
+    // next level's, 71.7 K rows of ~3460 products, 34 vs 89 ms)
+    if (std::getenv("AIJHIP_GAMG_LOG"))
+        std::fprintf(stderr, "  product %d x %d: %.0f products per row -> %s\n", A.m, B.n, per_row,
+                     A.m <= 8192 ? "wavefront per row" : "lane per row");
     if (A.m <= 8192) {
         hipLaunchKernelGGL((k_rowprod_wave<kWaveK, false>), dim3(gw), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
                            B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt);
