@@ -1328,11 +1328,38 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
             h_sj = h_si + m + 1;
             agg = h_sj + nzs;
             GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
-            if (nzs > 0) GTRY(hipMemcpy(h_sj, sj, sizeof(int32_t) * (size_t)nzs, hipMemcpyDeviceToHost), "read S");
             lap("strength");
-            // (phase 1 measured on the MI355X host at 300^3: this int32 form 83 ms;
-            // bitmap or byte flags with or without early exits 87-121 ms)
-            na = aijhip_gamg::aggregate_phase1(m, h_si, h_sj, agg);
+            // S's columns come down in row chunks while the pass works through
+            // the rows already here (a node reads only its own row). (Phase 1
+            // measured on the MI355X host at 300^3 level 0: this int32 form
+            // 83 ms; bitmap or byte flags with or without early exits 87-121 ms.)
+            {
+                constexpr int kChunks = 16;
+                hipStream_t cs = nullptr;
+                hipEvent_t ev[kChunks] = {};
+                GTRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
+                int32_t r[kChunks + 1];
+                for (int c = 0; c <= kChunks; ++c) r[c] = (int32_t)((int64_t)m * c / kChunks);
+                for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
+                    const int64_t a = h_si[r[c]], b = h_si[r[c + 1]];
+                    if (b > a)
+                        e = hipMemcpyAsync(h_sj + a, sj + a, sizeof(int32_t) * (size_t)(b - a), hipMemcpyDeviceToHost,
+                                           cs);
+                    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[c], hipEventDisableTiming);
+                    if (e == hipSuccess) e = hipEventRecord(ev[c], cs);
+                }
+                std::fill(agg, agg + m, -1);
+                na = 0;
+                for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
+                    if ((e = hipEventSynchronize(ev[c])) == hipSuccess)
+                        na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_sj, agg, na);
+                }
+                (void)hipStreamSynchronize(cs);
+                for (hipEvent_t x : ev)
+                    if (x) (void)hipEventDestroy(x);
+                (void)hipStreamDestroy(cs);
+                GTRY(e, "read S");
+            }
             GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
         }
         lap("phase 1");

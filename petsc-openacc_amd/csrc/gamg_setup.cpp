@@ -379,10 +379,9 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
 
 namespace aijhip_gamg {
 
-int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg) {
-    std::fill(agg, agg + m, -1);
-    int32_t na = 0;
-    for (int32_t i = 0; i < m; ++i) {
+int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const int32_t *sj, int32_t *agg,
+                              int32_t na) {
+    for (int32_t i = r0; i < r1; ++i) {
         if (agg[i] != -1 || si[i] == si[i + 1]) continue;
         bool free_all = true;
         for (int32_t k = si[i]; k < si[i + 1] && free_all; ++k) free_all = agg[sj[k]] == -1;
@@ -392,6 +391,11 @@ int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_
         ++na;
     }
     return na;
+}
+
+int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg) {
+    std::fill(agg, agg + m, -1);
+    return aggregate_phase1_rows(0, m, si, sj, agg, 0);
 }
 
 int32_t aggregate_phase3(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t na) {
