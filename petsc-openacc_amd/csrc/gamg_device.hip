@@ -595,35 +595,47 @@ __global__ __launch_bounds__(256) void k_rowprod_wave(int32_t m, const int32_t *
         int n = 0;
         bool over = false;
         const int32_t k1 = ai[i + 1];
+        constexpr int QB = 16;  // B entries loaded together: one exposed latency per batch
         for (int32_t k = ai[i]; k < k1; ++k) {
             const int32_t j = aj[k];
             const double a = WRITE ? aa[k] : 0.0;
             const int32_t q1 = bi[j + 1];
-            for (int32_t q = bi[j]; q < q1; ++q) {
-                const int32_t c = bj[q];
-                if ((int)(((uint32_t)c * 0x9E3779B1u) >> 26) != lane) continue;
-                bool hit = false;
+            for (int32_t qb = bi[j]; qb < q1; qb += QB) {
+                int32_t cc[QB];
+                double bv[QB];
 #pragma unroll
-                for (int e = 0; e < K; ++e) {
-                    if (e < n && col[e] == c) {
-                        if (WRITE) val[e] += a * ba[q];
-                        hit = true;
-                    }
+                for (int w = 0; w < QB; ++w) {
+                    const bool in = qb + w < q1;
+                    cc[w] = in ? bj[qb + w] : -1;
+                    bv[w] = (WRITE && in) ? ba[qb + w] : 0.0;
                 }
-                if (hit) continue;
-                if (n == K) { over = true; continue; }
 #pragma unroll
-                for (int e = 0; e < K; ++e) {
-                    if (e == n) {
-                        col[e] = c;
-                        if (WRITE) {
-                            double v0 = 0.0;
-                            v0 += a * ba[q];
-                            val[e] = v0;
+                for (int w = 0; w < QB; ++w) {
+                    const int32_t c = cc[w];
+                    if (c < 0 || (int)(((uint32_t)c * 0x9E3779B1u) >> 26) != lane) continue;
+                    bool hit = false;
+#pragma unroll
+                    for (int e = 0; e < K; ++e) {
+                        if (e < n && col[e] == c) {
+                            if (WRITE) val[e] += a * bv[w];
+                            hit = true;
                         }
                     }
+                    if (hit) continue;
+                    if (n == K) { over = true; continue; }
+#pragma unroll
+                    for (int e = 0; e < K; ++e) {
+                        if (e == n) {
+                            col[e] = c;
+                            if (WRITE) {
+                                double v0 = 0.0;
+                                v0 += a * bv[w];
+                                val[e] = v0;
+                            }
+                        }
+                    }
+                    ++n;
                 }
-                ++n;
             }
         }
         // distinct columns of the row = sum over lanes
