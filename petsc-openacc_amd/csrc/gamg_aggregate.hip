@@ -43,7 +43,7 @@
 namespace {
 
 constexpr int32_t kUndecided = 0, kRoot = 1, kOut = 2;
-constexpr unsigned kRoundGrid = 512;  // workgroups of 256 lanes per round launch
+constexpr unsigned kRoundGrid = 2048;  // workgroups of 256 lanes per round launch (512: 10 % slower)
 
 inline unsigned blocks_for(int64_t n, int t) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
 
@@ -130,6 +130,46 @@ __device__ __forceinline__ void wg_add(WgList &L, const bool (&p)[kBatch2], cons
         }
         pos += (unsigned)__popcll(mask[u]);
     }
+}
+
+// Append k to list when p (one element per lane; every lane of the
+// workgroup calls it at the same point).
+__device__ __forceinline__ void wg_add1(WgList &L, bool p, int32_t k, int32_t *list, unsigned *tail) {
+    const unsigned long long mask = __ballot(p);
+    if (!mask) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll(mask) - 1;
+    unsigned pos = 0;
+    if (lane == leader) pos = atomicAdd(&L.n, (unsigned)__popcll(mask));
+    pos = (unsigned)__shfl((int)pos, leader, 64);
+    if (p) {
+        const unsigned idx = pos + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
+        if (idx < (unsigned)kWgBuf) L.v[idx] = k;
+        else list[atomicAdd(tail, 1u)] = k;
+    }
+}
+
+// A workgroup's count-downs of one pass, combined per node in an LDS hash
+// table (open addressing, 8 probes) and applied with one global atomic per
+// distinct node (the OUT nodes of a round share most of their higher
+// neighbours): 35 -> 31 ms over the 704 rounds at 300^3.
+constexpr int kHashBits = 11, kHash = 1 << kHashBits;
+struct WgCounts {
+    int32_t key[kHash];
+    int32_t n[kHash];
+};
+
+__device__ __forceinline__ bool wg_count_add(WgCounts &H, int32_t k) {
+    const uint32_t h = ((uint32_t)k * 0x9E3779B1u) >> (32 - kHashBits);
+    for (int probe = 0; probe < 8; ++probe) {
+        const uint32_t s = (h + (uint32_t)probe) & (kHash - 1);
+        const int32_t prev = atomicCAS(&H.key[s], -1, k);
+        if (prev == -1 || prev == k) {
+            atomicAdd(&H.n[s], 1);
+            return true;
+        }
+    }
+    return false;  // the caller counts down in global memory directly
 }
 
 // Workgroup-uniform: the buffered appends to list[tail ...), coalesced.
@@ -221,7 +261,12 @@ __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restri
     if (blockIdx.x == 0 && threadIdx.x == 0) ostart[t + 1] = hi;
     if (lo >= hi) return;  // grid-uniform
     __shared__ WgList L;
+    __shared__ WgCounts H;
     if (threadIdx.x == 0) L.n = 0;
+    for (int s = threadIdx.x; s < kHash; s += blockDim.x) {
+        H.key[s] = -1;
+        H.n[s] = 0;
+    }
     __syncthreads();
     const int l = threadIdx.x % kGroup;
     const unsigned groups = gridDim.x * (blockDim.x / kGroup);
@@ -233,12 +278,31 @@ __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restri
         group_walks(j, l, on, si, sj, state, pre != 0, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
             bool p[kBatch2];
 #pragma unroll
-            for (int u = 0; u < kBatch2; ++u) p[u] = on && st[u] == kUndecided && atomicSub(&cnt[k[u]], 1) == 1;
+            for (int u = 0; u < kBatch2; ++u) {
+                p[u] = false;
+                if (on && st[u] == kUndecided && !wg_count_add(H, k[u])) p[u] = atomicSub(&cnt[k[u]], 1) == 1;
+            }
 #pragma unroll
             for (int u = 0; u < kBatch2; ++u)
                 if (p[u]) state[k[u]] = kRoot;
             wg_add(L, p, k, roots, &tails[0]);
         });
+        __syncthreads();
+        // the combined count-downs: the one that brings a count to 0 (its old
+        // value equals what it subtracts) makes the root
+        for (int s0 = 0; s0 < kHash; s0 += blockDim.x) {
+            const int s = s0 + threadIdx.x;
+            const int32_t key = s < kHash ? H.key[s] : -1;
+            bool pr = false;
+            if (key >= 0) {
+                const int32_t c = H.n[s];
+                pr = atomicSub(&cnt[key], c) == c;
+                if (pr) state[key] = kRoot;
+                H.key[s] = -1;
+                H.n[s] = 0;
+            }
+            wg_add1(L, pr, key, roots, &tails[0]);
+        }
         wg_flush(L, roots, &tails[0]);
     }
 }
@@ -333,7 +397,7 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     // node's CAS fails; an OUT node's count never reaches 0, a root's gets no
     // further walks)
     const char *ps = std::getenv("AIJHIP_LF_PREREAD");
-    const int pre = ps ? std::atoi(ps) : 1;
+    const int pre = ps ? std::atoi(ps) : 0;  // measured: 0 is 5-10 % faster (fewer dependent loads)
     auto clk = std::chrono::steady_clock::now();
     hipStream_t s = nullptr;
     int32_t *state = nullptr, *cnt = nullptr, *roots = nullptr, *outs = nullptr;
