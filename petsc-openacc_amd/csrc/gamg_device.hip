@@ -482,22 +482,30 @@ __global__ void k_narrow(int32_t n, const unsigned long long *__restrict__ w, in
     if (i < n) c[i] = (int32_t)w[i];
 }
 
-// C = A*B row by row (see the file comment). SYMBOLIC: cnt[i] = distinct
-// columns of row i, or -1 when they exceed CAP. NUMERIC: row i's sorted
-// columns and sums at ci[i].
-template <int CAP, int TPB, bool NUMERIC>
+// C = A*B row by row (see the file comment), TEAM lanes per row: with two,
+// each lane owns the columns of one hash half and keeps only those (a list
+// of at most CAP), both walk all the row's products in traversal order and
+// the owner adds each — per column the same order as one lane alone, so the
+// same bits — with half the list to search and shift. SYMBOLIC: cnt[i] =
+// distinct columns of row i, or -1 when a lane's list would pass CAP (the
+// next class recounts it); klass[i] = this class when it fits. NUMERIC: the
+// rows of this class, sorted columns (the team's two lists merged by rank)
+// and sums at ci[i].
+template <int CAP, int TPB, bool NUMERIC, int TEAM>
 __global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__restrict__ ai,
                                                  const int32_t *__restrict__ aj, const double *__restrict__ aa,
                                                  const int32_t *__restrict__ bi, const int32_t *__restrict__ bj,
                                                  const double *__restrict__ ba, const int32_t *__restrict__ ci,
-                                                 int32_t *cj, double *ca, int32_t *cnt, bool redo, int32_t lo,
-                                                 int32_t hi) {
+                                                 int32_t *cj, double *ca, int32_t *cnt, bool redo,
+                                                 int32_t *klass, int32_t myclass) {
+    static_assert(TEAM == 1 || TEAM == 2, "one or two lanes per row");
     __shared__ int32_t sc[CAP * TPB];
     __shared__ double sv[NUMERIC ? CAP * TPB : 1];
     const int t = threadIdx.x;
-    for (int32_t i = blockIdx.x * TPB + t; i < m; i += gridDim.x * TPB) {
-        if (!NUMERIC && redo && cnt[i] >= 0) continue;               // counted by a smaller CAP
-        if (NUMERIC && (cnt[i] <= lo || cnt[i] > hi)) continue;     // another CAP's class
+    const int me = t % TEAM;
+    for (int32_t i = (blockIdx.x * TPB + t) / TEAM; i < m; i += gridDim.x * (TPB / TEAM)) {
+        if (!NUMERIC && redo && cnt[i] >= 0) continue;    // counted by a smaller class
+        if (NUMERIC && klass[i] != myclass) continue;     // another class's row
         int n = 0;
         bool over = false;
         // the row's products in traversal order, their operands loaded in
@@ -533,6 +541,7 @@ __global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__res
                     }
                     for (int w = 0; w < QB && qb + w < q1[u]; ++w) {
                         const int32_t c = cc[w];
+                        if (TEAM == 2 && (int)(((uint32_t)c * 0x9E3779B1u) >> 31) != me) continue;
                         int l = 0, h = n;
                         while (l < h) {
                             const int mid = (l + h) >> 1;
@@ -560,12 +569,37 @@ __global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__res
             }
         }
         if (!NUMERIC) {
-            cnt[i] = over ? -1 : n;
+            int tot = n;
+            if (TEAM == 2) {
+                tot += __shfl_xor(n, 1, 64);
+                over = (__shfl_xor((int)over, 1, 64) != 0) || over;
+            }
+            if (me == 0) {
+                cnt[i] = over ? -1 : tot;
+                if (!over) klass[i] = myclass;
+            }
         } else {
             const int32_t o = ci[i];
-            for (int z = 0; z < n; ++z) {
-                cj[o + z] = sc[z * TPB + t];
-                ca[o + z] = sv[z * TPB + t];
+            if (TEAM == 1) {
+                for (int z = 0; z < n; ++z) {
+                    cj[o + z] = sc[z * TPB + t];
+                    ca[o + z] = sv[z * TPB + t];
+                }
+            } else {
+                // rank = own position + the partner's columns below it
+                const int np = __shfl_xor(n, 1, 64);
+                const int tp = t ^ 1;
+                for (int z = 0; z < n; ++z) {
+                    const int32_t c = sc[z * TPB + t];
+                    int l = 0, h = np;
+                    while (l < h) {
+                        const int mid = (l + h) >> 1;
+                        if (sc[mid * TPB + tp] < c) l = mid + 1;
+                        else h = mid;
+                    }
+                    cj[o + z + l] = c;
+                    ca[o + z + l] = sv[z * TPB + t];
+                }
             }
         }
     }
@@ -759,17 +793,35 @@ done:
 // columns exceed every device capacity (the caller falls back to the host).
 // One pass of k_rowprod over the rows of one capacity class (each class
 // uses 48 KiB of LDS per workgroup in the numeric pass).
-template <int CAP, int TPB>
-hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, bool redo, int32_t lo, int32_t hi,
+template <int CAP, int TPB, int TEAM>
+hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, int32_t myclass, bool redo,
                         const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
-    const unsigned grid = (unsigned)std::min<int64_t>(blocks_for(A.m, TPB), (int64_t)n_cu * 16);
+    const unsigned grid = (unsigned)std::min<int64_t>(blocks_for((int64_t)A.m * TEAM, TPB), (int64_t)n_cu * 16);
     if (!numeric)
-        hipLaunchKernelGGL((k_rowprod<CAP, TPB, false>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, redo, 0, 0);
+        hipLaunchKernelGGL((k_rowprod<CAP, TPB, false, TEAM>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj,
+                           A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, redo, klass, myclass);
     else
-        hipLaunchKernelGGL((k_rowprod<CAP, TPB, true>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, false, lo, hi);
+        hipLaunchKernelGGL((k_rowprod<CAP, TPB, true, TEAM>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj,
+                           A.aa, B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, false, klass, myclass);
     return hipGetLastError();
+}
+
+// The lane-per-row capacity classes, tried in order (each numeric pass uses
+// at most 48 KiB of LDS per workgroup): columns per row 32 (one lane), ~64,
+// ~128, ~256 (two lanes, a hash half each), 256 (one lane: rows whose halves
+// are too uneven for the two-lane class).
+constexpr int kProdClasses = 5;
+constexpr int kProdClassCols[kProdClasses] = {32, 64, 128, 256, 256};
+
+hipError_t rowprod_class(int c, const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, bool redo,
+                         const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
+    switch (c) {
+        case 0: return rowprod_pass<32, 64, 1>(A, B, cnt, klass, 0, redo, ci, C, numeric, n_cu);
+        case 1: return rowprod_pass<32, 128, 2>(A, B, cnt, klass, 1, redo, ci, C, numeric, n_cu);
+        case 2: return rowprod_pass<64, 64, 2>(A, B, cnt, klass, 2, redo, ci, C, numeric, n_cu);
+        case 3: return rowprod_pass<128, 32, 2>(A, B, cnt, klass, 3, redo, ci, C, numeric, n_cu);
+        default: return rowprod_pass<256, 16, 1>(A, B, cnt, klass, 4, redo, ci, C, numeric, n_cu);
+    }
 }
 
 int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nullptr) {
@@ -861,25 +913,34 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
         return r;
     };
     // light products (A*P0, A*P on the finest level: ~4 and ~25 products
-    // per row) start in a 32-column class: 24 KiB of LDS per 64-row
+    // per row) start in the 32-column class: 24 KiB of LDS per 64-row
     // workgroup in the numeric pass instead of 48, twice the waves per CU
-    const bool small = per_row <= 48.0;
-    int level = small ? -1 : 0;
-    for (;; ++level) {
-        if (level == -1) e = rowprod_pass<32, 64>(A, B, cnt, false, 0, 0, nullptr, nullptr, false, n_cu);
-        else if (level == 0) e = rowprod_pass<64, 64>(A, B, cnt, small, 0, 0, nullptr, nullptr, false, n_cu);
-        else if (level == 1) e = rowprod_pass<128, 32>(A, B, cnt, true, 0, 0, nullptr, nullptr, false, n_cu);
-        else if (level == 2) e = rowprod_pass<256, 16>(A, B, cnt, true, 0, 0, nullptr, nullptr, false, n_cu);
-        else { hipFree(cnt); return AIJHIP_ERR_STATE; }
+    int32_t *klass = nullptr;
+    if ((e = dalloc(&klass, A.m)) != hipSuccess) { hipFree(cnt); return herr(e, "product classes"); }
+    const int first = per_row <= 48.0 ? 0 : 1;
+    int last = first;
+    for (;; ++last) {
+        if (last >= kProdClasses) { hipFree(cnt); hipFree(klass); return AIJHIP_ERR_STATE; }
+        e = rowprod_class(last, A, B, cnt, klass, last > first, nullptr, nullptr, false, n_cu);
         int32_t mn = 0;
-        if (e != hipSuccess || (e = min_count(&mn)) != hipSuccess) { hipFree(cnt); return herr(e, "symbolic product"); }
+        if (e != hipSuccess || (e = min_count(&mn)) != hipSuccess) {
+            hipFree(cnt); hipFree(klass);
+            return herr(e, "symbolic product");
+        }
         if (mn >= 0) break;
     }
-    if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) { hipFree(cnt); return herr(e, "product rows"); }
+    auto bail = [&](hipError_t r, const char *what) {
+        hipFree(cnt);
+        hipFree(klass);
+        C.release();
+        return herr(r, what);
+    };
+    if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) return bail(e, "product rows");
     int64_t total = 0;
-    if ((e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess) { hipFree(cnt); C.release(); return herr(e, "scan"); }
+    if ((e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess) return bail(e, "scan");
     if (total > INT32_MAX) {
         hipFree(cnt);
+        hipFree(klass);
         C.release();
         set_error("GAMG device set-up: product exceeds int32 indices");
         return AIJHIP_ERR_ARG;
@@ -887,18 +948,14 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
     C.nz = total;
     if ((e = dalloc(&C.aj, total + 2)) != hipSuccess || (e = dalloc(&C.aa, total + 2)) != hipSuccess ||
         (e = hipMemset(C.aj + total, 0, 2 * sizeof(int32_t))) != hipSuccess ||
-        (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess) {
-        hipFree(cnt);
-        C.release();
-        return herr(e, "product alloc");
-    }
-    if (small) e = rowprod_pass<32, 64>(A, B, cnt, false, -1, 32, C.ai, &C, true, n_cu);
-    if (e == hipSuccess && level >= 0) e = rowprod_pass<64, 64>(A, B, cnt, false, small ? 32 : -1, 64, C.ai, &C, true, n_cu);
-    if (e == hipSuccess && level >= 1) e = rowprod_pass<128, 32>(A, B, cnt, false, 64, 128, C.ai, &C, true, n_cu);
-    if (e == hipSuccess && level >= 2) e = rowprod_pass<256, 16>(A, B, cnt, false, 128, 256, C.ai, &C, true, n_cu);
+        (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess)
+        return bail(e, "product alloc");
+    for (int c = first; c <= last && e == hipSuccess; ++c)
+        e = rowprod_class(c, A, B, cnt, klass, false, C.ai, &C, true, n_cu);
+    if (e != hipSuccess) return bail(e, "numeric product");
     hipFree(cnt);
-    if (e != hipSuccess) { C.release(); return herr(e, "numeric product"); }
-    if (cols_used) *cols_used = std::max(*cols_used, level < 0 ? 32 : 64 << level);
+    hipFree(klass);
+    if (cols_used) *cols_used = std::max(*cols_used, kProdClassCols[last]);
     return AIJHIP_OK;
 }
 
