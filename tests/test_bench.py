@@ -53,7 +53,8 @@ def test_distributed_block_schema(bench):
     assert bench.distributed_block(1, "gloo", {"kind": "host", "version": 0}, 60.0, [])["rccl_version"] is None
 
 
-@pytest.mark.parametrize("name", ["bench_rehearse_n2_r02e.json", "bench_mpi_n1_r02e.json"])
+@pytest.mark.parametrize("name", ["bench_rehearse_n2_r02e.json", "bench_mpi_n1_r02e.json",
+                                  "bench_rehearse_n2_r02j.json", "bench_mpi_n1_r02j.json"])
 def test_committed_rehearsal_lines_carry_the_n_gt_1_fields(name):
     """The rehearsals committed under profiles/r02/ were produced by this
     bench.py: one JSON line with the contract fields plus the distributed
@@ -70,3 +71,5 @@ def test_committed_rehearsal_lines_carry_the_n_gt_1_fields(name):
     assert line["cg_gamg"]["its"] > 0
     if line["n_gpus"] > 1:
         assert line["strong_300"]["unit"] == "GB/s" and 0 < line["strong_300"]["roofline_frac"] < 1
+    if "worst_rank" in d:  # written by distributed_block (round 2 onwards)
+        assert d["worst_rank"] in [r["rank"] for r in d["ranks"]]
