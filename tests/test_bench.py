@@ -54,7 +54,8 @@ def test_distributed_block_schema(bench):
 
 
 @pytest.mark.parametrize("name", ["bench_rehearse_n2_r02e.json", "bench_mpi_n1_r02e.json",
-                                  "bench_rehearse_n2_r02j.json", "bench_mpi_n1_r02j.json"])
+                                  "bench_rehearse_n2_r02j.json", "bench_mpi_n1_r02j.json",
+                                  "bench_rehearse_n2_r02n.json", "bench_mpi_n1_r02n.json"])
 def test_committed_rehearsal_lines_carry_the_n_gt_1_fields(name):
     """The rehearsals committed under profiles/r02/ were produced by this
     bench.py: one JSON line with the contract fields plus the distributed
