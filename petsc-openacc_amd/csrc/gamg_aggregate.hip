@@ -22,8 +22,13 @@
 // Decisions are final, so the order in which concurrent lanes act cannot
 // change the outcome. Each round is two launches (roots mark, OUT nodes
 // count down); the rounds needed grow with the longest chain of roots the
-// natural order forces (about 2 N on an N^3 grid: ~650 at 300^3). Deep
-// chains (a path graph needs m / 3 rounds) are handed back to the host pass.
+// natural order forces (about 2.35 N on an N^3 grid: 704 at 300^3). Deep
+// chains (a path graph needs m / 3 rounds) are handed back to the host pass
+// past a round budget. A workgroup gathers its list appends in LDS and
+// combines its count-downs per node in an LDS hash table, so the global
+// atomics are one per workgroup and pass on the list tails and one per
+// distinct node on the counts (the middle rounds, whose frontiers are the
+// largest, are where the time goes).
 // Aggregate numbers follow the roots' index order (a scan), as the host's
 // counter does.
 //
