@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--no-gamg", action="store_true", help="skip the CG+GAMG solve (BASELINE configs[2])")
     p.add_argument("--cg-iters", type=int, default=200, help="CG iterations timed for cg.iters_per_s")
     p.add_argument("--no-host-vec", action="store_true", help="skip the host-vector MatMult timing")
+    p.add_argument("--no-flan", action="store_true", help="skip the configs[4] Flan_1565 stand-in legs")
+    p.add_argument("--roofline-reps", type=int, default=50,
+                   help="launches timed by HIP events for roofline.achieved (at least this many, SURVEY §8d)")
     p.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling 300^3 line")
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
@@ -200,7 +203,8 @@ def host_vec_mult(A, x_h, reps=10):
     """MatMult with HOST x and y (aijhip_mat_mult_host: the path an unchanged
     PETSc caller with host Vecs takes), PCIe included: the
     serial step-2 form, the pipelined step-3/4 analogue from pageable arrays
-    (staged through pinned slots) and from pinned arrays (direct DMA). The
+    (copied directly: one H2D stream, and a second host thread issuing the D2H
+    of y chunks) and from pinned arrays (direct DMA). The
     three results must be bit-identical."""
     import torch
     out, ys = {}, []
@@ -267,6 +271,73 @@ def pmc_traffic(rows, nnz, block):
     if rec.get("rows") != rows or rec.get("nnz") != nnz or rec.get("block") != block:
         return None, None
     return rec.get("hbm_traffic_bytes_per_launch"), rec.get("source")
+
+
+def time_launches(fn, stream, reps):
+    """Per-launch HIP events on `stream` around `reps` calls of fn():
+    (mean us, median us, min us)."""
+    import torch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    us = np.array([a.elapsed_time(b) for a, b in ev]) * 1e3
+    return float(np.mean(us)), float(np.median(us)), float(np.min(us))
+
+
+def flan_standins(pkg, dev, reps, cpu_sample):
+    """BASELINE configs[4] (SuiteSparse Flan_1565, absent offline) through its
+    two stand-ins at full size, each timed like the headline kernel (HIP events
+    on the launch stream, `reps` launches after warm-up) beside a flat read of
+    the same byte count in the same run:
+      skewed — 1,564,794 rows of 45-99 banded entries plus 1e-4 hub rows of
+               1e3-2e5 scattered entries (seed 1565): the merge-path
+               load-balance stress; STREAM (default), STREAM exact (PETSc's
+               order in every row that fits a block) and MERGE;
+      fem_hex — Flan_1565's own structure: a hexahedral mesh of 81x80x80
+               nodes, 3 dofs per node, 81-entry interior rows.
+    Parity is the -m gpu tests' job (tests/test_flan_standins_gpu.py)."""
+    import torch
+    stream = torch.cuda.current_stream()
+    out = {}
+    for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(), ("stream", "stream_exact", "merge")),
+                                ("fem_hex", lambda: pkg.fem_hex_csr(), ("stream",))):
+        ai, aj, aa = make()
+        m, nnz = len(ai) - 1, len(aj)
+        nbytes = pkg.algorithmic_bytes(m, m, nnz)
+        x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
+        y = torch.empty_like(x)
+        rec = {"rows": m, "nnz": nnz, "max_row": int(np.diff(ai).max()), "bytes_per_spmv": nbytes}
+        for kern in kernels:
+            A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="merge" if kern == "merge" else "stream")
+            try:
+                if kern == "stream_exact":
+                    A.set_option("exact", 1)
+                info = A.info()
+                for _ in range(5):
+                    A.mult(x, y, stream)
+                mean, med, mn = time_launches(lambda: A.mult(x, y, stream), stream, reps)
+            finally:
+                A.destroy()
+            rec[kern] = {"us_mean": round(mean, 2), "us_median": round(med, 2), "us_min": round(mn, 2),
+                         "GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
+                         "frac": round(nbytes / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                         "geometry": info.get("stream_geometry"), "long_rows": info.get("n_long_rows")}
+        del x, y
+        flat = read_ceiling(nbytes, dev)
+        rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],
+                                    "frac_of_ceiling": round(rec["stream"]["GBs"] / flat[0][0], 4)}
+        if cpu_sample:
+            t_cpu, reps_cpu, _ = cpu_baseline(ai, aj, aa, pkg.splitmix_uniform(m, 42), 3.0)
+            rec["cpu_baseline"] = {"value": round(nbytes / t_cpu / 1e9, 3), "unit": "GB/s", "cores": 1,
+                                   "kind": "port", "sample": f"{reps_cpu} SpMVs on 1 core, oracle/matmult_seqaij.c"}
+        out[name] = rec
+        del ai, aj, aa
+    out["note"] = ("Flan_1565 itself is not in the image (no network); matio.load_mtx reads it when present. "
+                   "GBs = algorithmic bytes / mean HIP-event launch time; frac of 8 TB/s")
+    return out
 
 
 def cpu_model():
@@ -449,6 +520,18 @@ def main():
         ranks = [None] * world
         dist.all_gather_object(ranks, mine)
 
+    # roofline sample: at least --roofline-reps launches (SURVEY §8d asks
+    # for the median of >= 50), the K timed ones plus more if K is smaller
+    extra = max(0, args.roofline_reps - K)
+    if extra and not distributed:
+        ev_x = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(extra)]
+        for a, b in ev_x:
+            a.record(stream)
+            step()
+            b.record(stream)
+        torch.cuda.synchronize()
+        launch_ms = np.concatenate([launch_ms, [a.elapsed_time(b) for a, b in ev_x]])
+
     # correctness spot-check of the timed output against a fresh multiply
     y_chk = yd.clone()
     step()
@@ -572,6 +655,10 @@ def main():
     ceiling = None
     if not distributed:
         ceiling = guarded("read_ceiling", lambda: read_ceiling(bytes_local, dev))
+    flan = None
+    if not distributed and not args.no_flan:
+        flan = guarded("flan_standin", lambda: flan_standins(pkg, dev, max(args.roofline_reps, 50),
+                                                             not args.no_cpu_baseline))
 
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
@@ -588,6 +675,7 @@ def main():
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 4),
+            "ms_per_step_median_launch": round(float(np.median(launch_ms[:K])), 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -614,6 +702,8 @@ def main():
                 "kernel_us_mean": round(mean_launch_s * 1e6, 2),
                 "kernel_us_median": round(float(np.median(launch_ms)) * 1e3, 2),
                 "kernel_us_min": round(float(np.min(launch_ms)) * 1e3, 2),
+                "launches_timed": int(len(launch_ms)),
+                "achieved_from_median": round(bytes_local / (float(np.median(launch_ms)) / 1e3) / 1e9, 1),
                 "bytes_per_launch": bytes_local,
             },
             "result_stable": stable,
@@ -640,6 +730,8 @@ def main():
             out["cg_gamg"] = cg_gamg
         if host_vec is not None:
             out["host_vec"] = host_vec
+        if flan is not None:
+            out["flan_standin"] = flan
         if not args.no_cpu_baseline and not distributed:
             t_cpu, reps, _ = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds)
             out["cpu_baseline"] = {

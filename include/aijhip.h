@@ -176,11 +176,21 @@ enum {
                                        download (step3/step4 analogue); k > 0:
                                        chunks of >= k rows; 0: the serial
                                        step-2 form. Same results              */
-    AIJHIP_OPT_LONG_OVERLAP = 9     /* 1: long-row segments run on a side
+    AIJHIP_OPT_LONG_OVERLAP = 9,    /* 1: long-row segments run on a side
                                        stream concurrently with the row
                                        blocks (forked from and joined back to
                                        the caller's stream); 0 (default): one
                                        stream. Same results                  */
+    AIJHIP_OPT_ROW_GROUP = 11       /* MatMult / MatMultAdd of row blocks whose
+                                       mean row length is at least 24, when
+                                       AIJHIP_OPT_EXACT is 0: 1 = a register
+                                       kernel, 2..64 lanes per row summing
+                                       strided 16-B pairs, __shfl_xor
+                                       combine, no LDS staging (reordered sum,
+                                       within the fp64 bound; deterministic);
+                                       0 = the LDS STREAM block; -1 (default)
+                                       = automatic. Rows of shorter blocks
+                                       stay bit-exact either way            */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 
@@ -212,7 +222,10 @@ int aijhip_mat_mult_transpose(aijhip_mat_t A, const double *x, double *y,
  * pipelined with the product (AIJHIP_OPT_HOST_PIPELINE, the reference's
  * step3/step4: src/openacc-step4/MatMult_SeqAIJ.patch:51-91): host arrays
  * that are already pinned (hipHostMalloc / hipHostRegister) are DMA'd
- * directly, pageable ones through pinned staging slots. */
+ * directly; pageable ones are copied straight from and to the caller's arrays
+ * as well (the runtime's pageable path measured faster than staging through
+ * pinned slots): x chunks upload on one stream, y chunks download on another,
+ * issued from a second host thread. */
 int aijhip_mat_mult_host(aijhip_mat_t A, const double *x, double *y);
 
 /* w = z + A x with host vectors (MatMultAdd_SeqAIJ, aij.c [ext]: the

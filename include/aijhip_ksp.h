@@ -79,6 +79,10 @@ int aijhip_ksp_get_residual_history(aijhip_ksp_t ksp, double *hist, int32_t na, 
 /* Fused kernels used per iteration (1 = SpMV with the p.Ap dot in its
  * epilogue), for reporting. */
 int aijhip_ksp_get_fused(aijhip_ksp_t ksp, int *fused);
+/* Host synchronisations made by the last solve: the polls of the device stop
+ * flag (one per batch of 8 iterations, AIJHIP_KSP_POLL overrides) plus the
+ * final read. */
+int aijhip_ksp_get_host_syncs(aijhip_ksp_t ksp, int32_t *n);
 /* GAMG options (before set-up); NULL = PETSc defaults
  * (aijhip_gamg_params_default). */
 int aijhip_ksp_set_gamg_params(aijhip_ksp_t ksp, const aijhip_gamg_params_t *p);

@@ -76,6 +76,8 @@ void free_plan(aijhip::Plan &P) {
     if (P.ev_join) (void)hipEventDestroy(P.ev_join);
     if (P.long_stream) (void)hipStreamDestroy(P.long_stream);
     hipFree(P.d_xrange);
+    hipFree(P.d_sblocks);
+    hipFree(P.d_gblocks);
     hipFree(P.d_tile_coord);
     hipFree(P.d_carry_row);
     hipFree(P.d_carry_val);
@@ -207,6 +209,29 @@ int plan_stream(aijhip_mat *A) {
     if (!blocks.empty() &&
         (e = hipMemcpy(P.d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return hipfail(e, "plan: upload blocks");
+    // Register row-group blocks (Tuning::group): the plain MatMult launch
+    // runs blocks of long enough rows through k_spmv_rowgroup and the rest
+    // through the LDS STREAM kernel; exact mode and compressed rows keep the
+    // one launch. (The decision is per block; the sums of the other blocks do
+    // not change.)
+    P.n_sblocks = P.n_gblocks = 0;
+    if (P.tune.group > 0 && !P.tune.exact && !blocks.empty() && P.tune.persist == 0 && !A->compressed) {
+        std::vector<BlockDesc> sb, gb;
+        for (const BlockDesc &d : blocks)
+            (d.nk >= (int64_t)kGroupMinMean * d.nrows ? gb : sb).push_back(d);
+        if (!gb.empty()) {
+            if ((e = dmalloc(&P.d_sblocks, sb.size(), &P.bytes)) != hipSuccess ||
+                (e = dmalloc(&P.d_gblocks, gb.size(), &P.bytes)) != hipSuccess)
+                return hipfail(e, "plan: alloc row-group blocks");
+            if ((!sb.empty() && (e = hipMemcpy(P.d_sblocks, sb.data(), sizeof(BlockDesc) * sb.size(),
+                                               hipMemcpyHostToDevice)) != hipSuccess) ||
+                (e = hipMemcpy(P.d_gblocks, gb.data(), sizeof(BlockDesc) * gb.size(), hipMemcpyHostToDevice)) !=
+                    hipSuccess)
+                return hipfail(e, "plan: upload row-group blocks");
+            P.n_sblocks = (int32_t)sb.size();
+            P.n_gblocks = (int32_t)gb.size();
+        }
+    }
     // x tiles (LDS-staged x, opt-in): where a block's columns span at most
     // its LDS entries, x[lo, lo + span) is loaded coalesced and gathered
     // from LDS (banded operators; never the 7-pt Poisson at scale, whose
@@ -330,6 +355,7 @@ int plan_build(aijhip_mat *A) {
         if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
         if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
     }
+    if (P.tune.group < 0) P.tune.group = 0;  // automatic choice: off until measured
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM:
             return plan_stream(A);
@@ -680,6 +706,11 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_HOST_PIPELINE:
             if (value < -1) return fail(AIJHIP_ERR_ARG, "host_pipeline: -1 auto, 0 serial, k > 0 chunk rows");
             t.host_chunk = value;
+            break;
+        case AIJHIP_OPT_ROW_GROUP:
+            if (value < -1 || value > 2)
+                return fail(AIJHIP_ERR_ARG, "row_group: -1 auto, 0 off, 1 on (256 lanes), 2 on (512 lanes)");
+            t.group = value;
             break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }

@@ -103,6 +103,8 @@ struct Tuning {
     bool long_overlap = false;  // long-row segments on a side stream, concurrent with the row blocks
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
+    int group = -1;        // register row-group kernel for blocks of mean row length >= kGroupMinMean
+                           // (plain MatMult / MatMultAdd, exact = 0): -1 auto, 0 off, 1 on
 };
 
 struct HostPipe;  // host-vector MatMult pipeline state (host_pipe.cpp)
@@ -123,6 +125,11 @@ constexpr int kBatchMinMean = 16;
 // run along lines (geometry 6). Measured: 7-pt 0.73, GAMG coarse operators
 // 0.51-0.68, skewed stand-in 0.40, FEM-structured stand-in 0.17.
 constexpr double kScatteredLinesPerEntry = 0.25;
+// Row blocks whose mean row length is at least this are eligible for the
+// register row-group kernel (Tuning::group): L lanes per row accumulate
+// strided 16-B pairs in registers, no LDS product buffer.
+constexpr int kGroupMinMean = 24;
+constexpr int kGroupThreads = 256;
 
 struct Plan {
     int kernel = AIJHIP_KERNEL_STREAM;
@@ -149,6 +156,11 @@ struct Plan {
     // span -1 when they do not fit the block's LDS (gathers from HBM)
     int2 *d_xrange = nullptr;
     int32_t n_xtiled = 0;
+    // Tuning::group: the row blocks split into the LDS STREAM ones (d_sblocks)
+    // and the register row-group ones (d_gblocks), for the plain MatMult /
+    // MatMultAdd launch; d_blocks keeps all of them (fused epilogues)
+    BlockDesc *d_sblocks = nullptr, *d_gblocks = nullptr;
+    int32_t n_sblocks = 0, n_gblocks = 0;
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;
     int32_t n_tiles = 0;
@@ -208,15 +220,16 @@ bool stream_mg_fusable(const aijhip_mat &A);
 // y = D^-1 A x in PETSc's row order (exact), for the GAMG set-up.
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s);
 hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
-                         hipStream_t s, bool nt);
+                         hipStream_t s, bool nt, const int *stop = nullptr);
 // r = b - A x on a STREAM plan (residual in the SpMV epilogue).
 hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
-                           bool nt);
+                           bool nt, const int *stop = nullptr);
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
-                          double *dpart, hipStream_t s, bool nt);
-// Dispatch y = A x (or w = z + A x) through the handle's plan.
+                          double *dpart, hipStream_t s, bool nt, const int *stop = nullptr);
+// Dispatch y = A x (or w = z + A x) through the handle's plan. stop: a device
+// flag (CG's `done`); STREAM row blocks return at once once it is set.
 hipError_t launch_mult(const aijhip_mat &A, const double *x, const double *z, double *y,
-                       bool add, hipStream_t s);
+                       bool add, hipStream_t s, const int *stop = nullptr);
 hipError_t launch_scalar(const aijhip_mat &A, const double *x, const double *z,
                          double *y, bool add, hipStream_t s);
 hipError_t launch_vector(const aijhip_mat &A, const double *x, const double *z,
@@ -265,7 +278,7 @@ void host_pipe_free(HostPipe *p);
 // `s`. When the finest post-smoothing carried the z.z / z.b partials, *dots
 // points at them (2 x *nbz doubles), else NULL.
 hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t s, const double **dots,
-                         int *nbz);
+                         int *nbz, const int *stop = nullptr);
 
 // Sets the calling thread's aijhip_last_error() message.
 void set_error(const std::string &msg);

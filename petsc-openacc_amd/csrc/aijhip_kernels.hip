@@ -466,11 +466,14 @@ __global__ __launch_bounds__(T) void k_spmv_stream_pipe(
     }
 }
 
-// Segments of long rows: tree-reduced partial sums. Each lane keeps U
-// independent partial sums (entries t + (i*U + u)*T, combined u = 0..U-1 at
-// the end: a fixed order) so U loads and gathers are in flight at once — a
-// hub row's gathers are scattered over all of x, and one dependent chain per
-// lane left the kernel latency-bound.
+// Segments of long rows: tree-reduced partial sums. A lane takes 16-B pairs
+// (aa as f64x2, aj as i32x2 from an even start, as the STREAM blocks do) at
+// pair stride kLongThreads and keeps U pairs in flight: a 4096-entry segment
+// is 2048 pairs, so every load and gather of the segment is issued before the
+// first product is needed (the previous form, 8 scalar entries per round,
+// waited on two dependent latencies per round: 2.66 TB/s). The
+// lane's U partial sums are combined u = 0..U-1, then the wave tree, then the
+// waves in order: a fixed order.
 __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     const LongSeg *__restrict__ seg, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const double *__restrict__ x,
@@ -481,17 +484,31 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     const LongSeg s = seg[id];
     const int t = threadIdx.x;
     double acc[U] = {};
-    const int64_t k1 = (int64_t)s.k0 + s.nk;
-    for (int64_t kb = (int64_t)s.k0 + t; kb < k1; kb += (int64_t)U * kLongThreads) {
-        double a[U], xv[U];
+    const int64_t k0 = s.k0, k1 = (int64_t)s.k0 + s.nk, kb = k0 & ~int64_t(1);
+    for (int64_t k = kb + 2 * t; k < k1; k += (int64_t)2 * U * kLongThreads) {
+        f64x2 a[U];
+        i32x2 c[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t k = kb + (int64_t)u * kLongThreads;
-            a[u] = k < k1 ? aa[k] : 0.0;
-            xv[u] = k < k1 ? x[aj[k]] : 0.0;
+            const int64_t kk = k + (int64_t)2 * u * kLongThreads;
+            if (kk < k1) {
+                a[u] = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(aa + kk));
+                c[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(aj + kk));
+            }
+        }
+        double x0[U], x1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t kk = k + (int64_t)2 * u * kLongThreads;
+            x0[u] = (kk < k1 && kk >= k0) ? x[c[u].x] : 0.0;
+            x1[u] = (kk + 1 < k1) ? x[c[u].y] : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) acc[u] += a[u] * xv[u];
+        for (int u = 0; u < U; ++u) {
+            const int64_t kk = k + (int64_t)2 * u * kLongThreads;
+            if (kk < k1 && kk >= k0) acc[u] += a[u].x * x0[u];
+            if (kk + 1 < k1) acc[u] += a[u].y * x1[u];
+        }
     }
     double v = acc[0];
 #pragma unroll
@@ -506,6 +523,66 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
         for (int w = 1; w < kLongThreads / 64; ++w) r += red[w];
         partials[id] = r;
     }
+}
+
+// Register row groups (Tuning::group): a workgroup takes one STREAM row block
+// of long-enough rows (mean >= kGroupMinMean) and gives each row L lanes
+// (the largest power of two <= min(64, T / rows)). Lane j of a row sums the
+// row's 16-B pairs j, j + L, j + 2L, ... (U pairs in flight) into two
+// registers; the row's lanes combine with __shfl_xor. No LDS product buffer,
+// no barrier and no serial per-row phase: the LDS STREAM block holds 32 KiB
+// and reduces each row on one lane, which leaves ~1/8 of its lanes working
+// on rows of 45-100 entries. The sum is reordered (within the fp64 bound of
+// SURVEY §8d) and deterministic (L and the pair order follow the plan).
+template <int T, bool ADD, bool NT>
+__global__ __launch_bounds__(T) void k_spmv_rowgroup(const BlockDesc *__restrict__ blk,
+                                                     const int32_t *__restrict__ rai,
+                                                     const int32_t *__restrict__ aj,
+                                                     const double *__restrict__ aa,
+                                                     const double *__restrict__ x, const double *z, double *y,
+                                                     const int *stop) {
+    constexpr int U = 4;
+    const BlockDesc d = blk[blockIdx.x];
+    if ((stop ? *stop : 0) != 0) return;
+    const int t = threadIdx.x, nr = d.nrows;
+    const int cap = min(64, T / max(nr, 1));
+    int L = 1;
+    while (L * 2 <= cap) L *= 2;
+    const int g = t / L, j = t - g * L;
+    const bool own = g < nr;
+    const int r = d.row0 + min(g, nr - 1);
+    const int64_t rs = rai[r], re = rai[r + 1];
+    double acc0 = 0.0, acc1 = 0.0;
+    if (own) {
+        for (int64_t k = (rs & ~int64_t(1)) + 2 * j; k < re; k += (int64_t)2 * L * U) {
+            f64x2 a[U];
+            i32x2 c[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t kk = k + (int64_t)2 * L * u;
+                if (kk < re) {
+                    a[u] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + kk));
+                    c[u] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + kk));
+                }
+            }
+            double x0[U], x1[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t kk = k + (int64_t)2 * L * u;
+                x0[u] = (kk < re && kk >= rs) ? x[c[u].x] : 0.0;
+                x1[u] = (kk + 1 < re) ? x[c[u].y] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t kk = k + (int64_t)2 * L * u;
+                if (kk < re && kk >= rs) acc0 += a[u].x * x0[u];
+                if (kk + 1 < re) acc1 += a[u].y * x1[u];
+            }
+        }
+    }
+    double sv = acc0 + acc1;
+    for (int off = L >> 1; off > 0; off >>= 1) sv += __shfl_xor(sv, off, 64);
+    if (own && j == 0) st_stream(y + r, ADD ? z[r] + sv : sv);
 }
 
 // One wavefront per long row: the lanes load 64 partials at once and the sum
@@ -805,13 +882,16 @@ hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, i
 }
 
 // Gather locality of a row sample: distinct 16-column (128-B) x lines per
-// entry, counted along each sampled row (columns are sorted within a row).
+// entry, counted along each sampled row (columns are sorted within a row)
+// over its first kRowLinesWalk entries: a lane that walked a whole 2e5-entry
+// hub row serially made this planning kernel 30x the SpMV (12.4 ms).
+constexpr int32_t kRowLinesWalk = 512;
 __global__ __launch_bounds__(256) void k_row_lines(const int32_t *__restrict__ rai, int32_t nr, int32_t stride,
                                                    const int32_t *__restrict__ aj, unsigned long long *out) {
     const int64_t r = ((int64_t)blockIdx.x * 256 + threadIdx.x) * stride;
     long long ent = 0, lines = 0;
     if (r < nr) {
-        const int32_t k0 = rai[r], k1 = rai[r + 1];
+        const int32_t k0 = rai[r], k1 = min(rai[r + 1], rai[r] + kRowLinesWalk);
         int32_t prev = -1;
         for (int32_t k = k0; k < k1; ++k) {
             const int32_t l = aj[k] >> 4;
@@ -886,10 +966,9 @@ static hipError_t compressed_prologue(const aijhip_mat &A, const double *z, doub
 }
 
 template <int T, int CAP, int RPT>
-static void stream_dispatch(const aijhip_mat &A, const RowList &L, const double *x,
+static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L, const double *x,
                             const double *z, double *y, bool add, hipStream_t s, double *dpart,
                             const int *stop) {
-    const Plan &P = A.plan;
 #define AIJHIP_SL(ADD, CROW, XCD, NT, CL)                                                          \
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, XCD, NT, CL, OpMult<ADD>>), dim3(P.n_blocks), \
                        dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, (int)P.tune.exact,   \
@@ -970,7 +1049,7 @@ bool stream_mg_fusable(const aijhip_mat &A) { return stream_dot_fusable(A); }
 
 template <class Op>
 static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dpart, hipStream_t s,
-                                   int exact = -1) {
+                                   int exact = -1, const int *stop = nullptr) {
     if (!stream_mg_fusable(A)) return hipErrorInvalidValue;
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
@@ -980,7 +1059,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     case G:                                                                                               \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
                            dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex,                \
-                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, nullptr, nullptr);                 \
+                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, stop, nullptr);                    \
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
@@ -1015,21 +1094,21 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
 }
 
 hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
-                         hipStream_t s, bool nt) {
-    if (nt) return launch_stream_op(A, OpMgPre<true>{b, dinv, x, r}, nullptr, s);
-    return launch_stream_op(A, OpMgPre<false>{b, dinv, x, r}, nullptr, s);
+                         hipStream_t s, bool nt, const int *stop) {
+    if (nt) return launch_stream_op(A, OpMgPre<true>{b, dinv, x, r}, nullptr, s, -1, stop);
+    return launch_stream_op(A, OpMgPre<false>{b, dinv, x, r}, nullptr, s, -1, stop);
 }
 
 hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
-                           bool nt) {
-    if (nt) return launch_stream_op(A, OpMgResid<true>{x, b, r}, nullptr, s);
-    return launch_stream_op(A, OpMgResid<false>{x, b, r}, nullptr, s);
+                           bool nt, const int *stop) {
+    if (nt) return launch_stream_op(A, OpMgResid<true>{x, b, r}, nullptr, s, -1, stop);
+    return launch_stream_op(A, OpMgResid<false>{x, b, r}, nullptr, s, -1, stop);
 }
 
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
-                          double *dpart, hipStream_t s, bool nt) {
-    if (nt) return launch_stream_op(A, OpMgPost<true>{t, b, dinv, x, dpart != nullptr}, dpart, s);
-    return launch_stream_op(A, OpMgPost<false>{t, b, dinv, x, dpart != nullptr}, dpart, s);
+                          double *dpart, hipStream_t s, bool nt, const int *stop) {
+    if (nt) return launch_stream_op(A, OpMgPost<true>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
+    return launch_stream_op(A, OpMgPost<false>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
 }
 
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s) {
@@ -1075,8 +1154,37 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
         }
 #undef AIJHIP_PG
         if ((e = hipGetLastError()) != hipSuccess) return e;
+    } else if (P.n_gblocks > 0 && !dpart) {
+        // LDS STREAM blocks of short rows, then the register row groups
+        if (P.n_sblocks > 0) {
+            Plan view = P;  // the same plan over the short-row block list (a non-owning copy)
+            view.d_blocks = P.d_sblocks;
+            view.n_blocks = P.n_sblocks;
+            view.d_xrange = nullptr;
+#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, view, L, x, z, y, add, s, nullptr, stop); break
+            switch (g) {
+                AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
+                AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
+                default: return hipErrorInvalidValue;
+            }
+#undef AIJHIP_SG
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        const bool nt = P.tune.nt == 1;
+#define AIJHIP_RG(TT, ADD, NT)                                                                                \
+    hipLaunchKernelGGL((k_spmv_rowgroup<TT, ADD, NT>), dim3(P.n_gblocks), dim3(TT), 0, s, P.d_gblocks, L.rai, \
+                       A.d_aj, A.d_aa, x, z, y, stop)
+        if (P.tune.group == 2) {
+            if (add) { if (nt) AIJHIP_RG(512, true, true); else AIJHIP_RG(512, true, false); }
+            else { if (nt) AIJHIP_RG(512, false, true); else AIJHIP_RG(512, false, false); }
+        } else {
+            if (add) { if (nt) AIJHIP_RG(256, true, true); else AIJHIP_RG(256, true, false); }
+            else { if (nt) AIJHIP_RG(256, false, true); else AIJHIP_RG(256, false, false); }
+        }
+#undef AIJHIP_RG
+        if ((e = hipGetLastError()) != hipSuccess) return e;
     } else if (P.n_blocks > 0) {
-#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, L, x, z, y, add, s, dpart, stop); break
+#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, P, L, x, z, y, add, s, dpart, stop); break
         switch (g) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
             AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
@@ -1165,9 +1273,11 @@ hipError_t launch_merge(const aijhip_mat &A, const double *x, const double *z, d
 }
 
 hipError_t launch_mult(const aijhip_mat &A, const double *x, const double *z, double *y,
-                       bool add, hipStream_t s) {
+                       bool add, hipStream_t s, const int *stop) {
     switch (A.plan.kernel) {
-        case AIJHIP_KERNEL_STREAM: return launch_stream(A, x, z, y, add, s);
+        // the stop flag reaches the STREAM row blocks (the long-row, SCALAR,
+        // VECTOR and MERGE kernels ignore it: they recompute the same values)
+        case AIJHIP_KERNEL_STREAM: return launch_stream(A, x, z, y, add, s, nullptr, stop);
         case AIJHIP_KERNEL_SCALAR: return launch_scalar(A, x, z, y, add, s);
         case AIJHIP_KERNEL_VECTOR: return launch_vector(A, x, z, y, add, s);
         case AIJHIP_KERNEL_MERGE: return launch_merge(A, x, z, y, add, s);

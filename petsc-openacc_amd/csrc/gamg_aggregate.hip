@@ -409,7 +409,11 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     unsigned *tails = nullptr, *rstart = nullptr, *ostart = nullptr, *h_ctl = nullptr;
     const unsigned g = blocks_for(m, 256);
     constexpr int kBatch = 32;  // rounds launched between two looks at the tails
-    hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    // s does not synchronise with the null stream, on which the strength
+    // kernels wrote si/sj: drain it first, so the sweep's reads are ordered
+    // after their producers explicitly
+    hipError_t e = hipStreamSynchronize(nullptr);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
     if (e == hipSuccess) e = dalloc(&state, m);
     if (e == hipSuccess) e = dalloc(&cnt, m);
     if (e == hipSuccess) e = dalloc(&roots, m);

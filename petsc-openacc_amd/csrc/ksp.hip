@@ -72,19 +72,28 @@ __global__ __launch_bounds__(kRedThreads) void k_reduce_iter(const double *pz, i
 // KSPSolve_Richardson with one iteration, scale 1, Jacobi PC [ext]:
 //   zero guess:     x = 0 + 1.0 * (D^-1 b)           = D^-1 b
 //   nonzero guess:  x = x + 1.0 * (D^-1 (b + (-1) A x))
+// Every V-cycle kernel takes CG's stop flag (`done`, NULL outside a solve):
+// once it is set they return at once, so the solver can launch iterations in
+// batches between host polls as CG+Jacobi does.
 __global__ __launch_bounds__(kVecThreads) void k_jacobi(int64_t n, const double *__restrict__ dinv,
-                                                        const double *__restrict__ b, double *x) {
+                                                        const double *__restrict__ b, double *x,
+                                                        const int *stop) {
+    if (stop && *stop) return;
     GRID_STRIDE(i, n) x[i] = dinv[i] * b[i];
 }
 
 // MatResidual: r = b + (-1) r, where r holds A x on entry (VecAYPX(r,-1,b)).
-__global__ __launch_bounds__(kVecThreads) void k_resid(int64_t n, const double *__restrict__ b, double *r) {
+__global__ __launch_bounds__(kVecThreads) void k_resid(int64_t n, const double *__restrict__ b, double *r,
+                                                       const int *stop) {
+    if (stop && *stop) return;
     GRID_STRIDE(i, n) r[i] = b[i] + (-1.0) * r[i];
 }
 
 __global__ __launch_bounds__(kVecThreads) void k_richardson(int64_t n, const double *__restrict__ dinv,
                                                             const double *__restrict__ b,
-                                                            const double *__restrict__ ax, double *x) {
+                                                            const double *__restrict__ ax, double *x,
+                                                            const int *stop) {
+    if (stop && *stop) return;
     GRID_STRIDE(i, n) x[i] = x[i] + 1.0 * (dinv[i] * (b[i] + (-1.0) * ax[i]));
 }
 
@@ -148,7 +157,7 @@ struct aijhip_ksp {
     // how each level's coarsening was built (aijhip_ksp_get_gamg_setup_path)
     std::vector<int32_t> setup_path, setup_cols;
     bool setup_overflow = false;
-    int32_t its = 0;
+    int32_t its = 0, host_syncs = 0;
     int reason = 0;
     double rnorm = 0.0;
     std::vector<double> hist;
@@ -314,7 +323,7 @@ int gamg_setup(aijhip_ksp *K) {
 // post-smoothing launch reads t and writes x. With dots != NULL the finest
 // post-smoothing also leaves z.z / z.b partials there (*dots_done = true).
 hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, double *dots = nullptr,
-                  bool *dots_done = nullptr) {
+                  bool *dots_done = nullptr, const int *stop = nullptr) {
     const int nl = (int)K->mg.size();
     hipError_t e = hipSuccess;
     if (dots_done) *dots_done = false;
@@ -324,21 +333,22 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
         MGLevel &L = K->mg[l];
         const dim3 g = vgrid(K, L.m), t(kVecThreads);
         if (l == nl - 1) {  // coarse: preonly + Jacobi
-            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));
+            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
             break;
         }
         if (L.fused && K->mg_pre_split) {
             // smoothd as a vector pass, then r = b - A x in the SpMV epilogue
-            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));
-            if ((e = aijhip::launch_mg_resid(*L.A, X(l), B(l), L.r, s, K->vec_nt)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
+            if ((e = aijhip::launch_mg_resid(*L.A, X(l), B(l), L.r, s, K->vec_nt, stop)) != hipSuccess) return e;
         } else if (L.fused) {
-            if ((e = aijhip::launch_mg_pre(*L.A, B(l), L.dinv, X(l), L.r, s, K->vec_nt)) != hipSuccess) return e;
+            if ((e = aijhip::launch_mg_pre(*L.A, B(l), L.dinv, X(l), L.r, s, K->vec_nt, stop)) != hipSuccess)
+                return e;
         } else {
-            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l));  // smoothd
-            if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_resid, g, t, 0, s, (int64_t)L.m, B(l), L.r);
+            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);  // smoothd
+            if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s, stop)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_resid, g, t, 0, s, (int64_t)L.m, B(l), L.r, stop);
         }
-        if ((e = aijhip::launch_mult(*L.P->transpose, L.r, nullptr, K->mg[l + 1].b, false, s)) != hipSuccess)
+        if ((e = aijhip::launch_mult(*L.P->transpose, L.r, nullptr, K->mg[l + 1].b, false, s, stop)) != hipSuccess)
             return e;  // MatRestrict = P^T r
     }
     for (int l = nl - 2; l >= 0; --l) {
@@ -346,15 +356,16 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
         const dim3 g = vgrid(K, L.m), t(kVecThreads);
         if (L.fused) {
             // MatInterpolateAdd into the scratch: t = x + P x_c, then smoothu
-            if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), L.r, true, s)) != hipSuccess) return e;
+            if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), L.r, true, s, stop)) != hipSuccess) return e;
             double *dp = (l == 0 && dots) ? dots : nullptr;
-            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s, K->vec_nt)) != hipSuccess) return e;
+            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s, K->vec_nt, stop)) != hipSuccess)
+                return e;
             if (dp && dots_done) *dots_done = true;
         } else {
             // MatInterpolateAdd: x = x + P x_c
-            if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), X(l), true, s)) != hipSuccess) return e;
-            if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s)) != hipSuccess) return e;
-            hipLaunchKernelGGL(k_richardson, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l));  // smoothu
+            if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), X(l), true, s, stop)) != hipSuccess) return e;
+            if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s, stop)) != hipSuccess) return e;
+            hipLaunchKernelGGL(k_richardson, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l), stop);  // smoothu
         }
     }
     return hipGetLastError();
@@ -365,9 +376,9 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
 namespace aijhip {
 
 hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t s, const double **dots,
-                         int *nbz) {
+                         int *nbz, const int *stop) {
     bool done = false;
-    const hipError_t e = vcycle(K, b, x, s, K->d_mgpart, &done);
+    const hipError_t e = vcycle(K, b, x, s, K->d_mgpart, &done, stop);
     *dots = done ? K->d_mgpart : nullptr;
     *nbz = done ? K->mg[0].A->plan.n_blocks : 0;
     return e;
@@ -521,11 +532,14 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     }
     hipLaunchKernelGGL(k_reduce_init, dim3(1), rt, 0, s, K->d_part, nb, K->d_state, K->d_hist, p);
     if ((e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve init");
-    // iterations in batches; every CG kernel is a no-op once `done` is set
-    // (the V-cycle is not, so GAMG polls every iteration)
-    const int batch = (K->fused && !gamg) ? 8 : 1;
+    // iterations in batches; every CG and V-cycle kernel is a no-op once
+    // `done` is set (AIJHIP_KSP_POLL overrides the batch, for A/B)
+    int batch = 8;
+    if (const char *v = std::getenv("AIJHIP_KSP_POLL")) batch = std::max(1, std::atoi(v));
     int32_t launched = 0;
+    K->host_syncs = 0;
     for (;;) {
+        ++K->host_syncs;
         if ((e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return khip(e, "KSPSolve poll");
@@ -539,7 +553,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
                 if (e == hipSuccess)
                     hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, A->plan.n_blocks, K->d_state);
             } else {
-                e = aijhip::launch_mult(*A, K->d_p, nullptr, K->d_z, false, s);
+                e = aijhip::launch_mult(*A, K->d_p, nullptr, K->d_z, false, s, &K->d_state->done);
                 hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
                 hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, nb, K->d_state);
             }
@@ -555,7 +569,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
                 // z = B r; z.z and z.r come from the finest post-smoothing
                 // when it is fused, else from k_dots
                 bool dots = false;
-                e = vcycle(K, K->d_r, K->d_z, s, K->d_mgpart, &dots);
+                e = vcycle(K, K->d_r, K->d_z, s, K->d_mgpart, &dots, &K->d_state->done);
                 if (dots) {
                     pz = K->d_mgpart;
                     nbz = K->mg[0].A->plan.n_blocks;
@@ -573,6 +587,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
         (e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)
         return khip(e, "KSPSolve final update");
+    ++K->host_syncs;
     const CGState &st = *K->h_state;
     K->its = st.its;
     K->reason = st.reason ? st.reason : AIJHIP_KSP_DIVERGED_ITS;
@@ -608,6 +623,12 @@ int aijhip_ksp_get_residual_history(aijhip_ksp_t K, double *hist, int32_t na, in
     const int32_t c = std::min<int32_t>(na, (int32_t)K->hist.size());
     std::copy(K->hist.begin(), K->hist.begin() + c, hist);
     *n = c;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_get_host_syncs(aijhip_ksp_t K, int32_t *n) {
+    if (!K || !n) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    *n = K->host_syncs;
     return AIJHIP_OK;
 }
 

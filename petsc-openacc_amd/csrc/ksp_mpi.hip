@@ -780,8 +780,17 @@ int aijhip_kspmpi_set_tolerances(aijhip_kspmpi_t K, double rtol, double abstol, 
     if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
     if (rtol < 0 || abstol < 0 || dtol <= 0 || max_it < 0) return mfail(AIJHIP_ERR_ARG, "bad tolerance");
     K->rtol = rtol; K->abstol = abstol; K->dtol = dtol;
-    if (max_it + 2 > K->hist_cap) K->set_up = false;  // regrow the history
     K->max_it = max_it;
+    if (K->set_up && max_it + 2 > K->hist_cap) {  // regrow the history only (keeps dinv and the sub-PC)
+        DeviceGuard g(K->M->comm->device);
+        hipFree(K->d_hist);
+        K->d_hist = nullptr;
+        K->hist_cap = max_it + 2;
+        if (hipMalloc(&K->d_hist, sizeof(double) * (size_t)K->hist_cap) != hipSuccess) {
+            K->set_up = false;
+            return mfail(AIJHIP_ERR_ALLOC, "residual history");
+        }
+    }
     return AIJHIP_OK;
 }
 
@@ -853,23 +862,27 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
     }
     if ((e = hipGetLastError()) != hipSuccess) return mhip(e, "KSPSolve init");
     const bool have_o = M->Ao && aijhip::row_list(*M->Ao).nr > 0;
+    // The A_o correction partials (p_o w_o(new) - p_o w_o(old)) complete p.w
+    // only when the A_d epilogue summed p_o w_o(old), i.e. in the fused path;
+    // otherwise k_dot sums p.w over the final w and the A_o rows are already
+    // in it (counting them twice broke conjugacy).
+    double *opart = (have_o && K->fused) ? K->d_opart : nullptr;
+    const int nob = opart ? M->o_grid : 0;
     int32_t launched = 0;
     for (;;) {
         if ((e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess)
             return mhip(e, "KSPSolve poll");
         if ((rc = wait_stream(C, s))) return rc;
         if (K->h_state->done || launched >= K->max_it) break;
-        const int32_t poll = gamg ? 1 : K->poll;  // the V-cycle does not stop at the flag
+        const int32_t poll = K->poll;  // every CG and V-cycle kernel returns at once past the flag
         for (int j = 0; j < poll && launched < K->max_it; ++j, ++launched) {
             if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             // W = A P with the p.w partials (W shares Z's storage)
-            if ((rc = mpiaij_apply(M, K->d_p, K->d_z, s, K->d_part, have_o ? K->d_opart : nullptr, K->d_state,
-                                   K->fused)))
-                return rc;
+            if ((rc = mpiaij_apply(M, K->d_p, K->d_z, s, K->d_part, opart, K->d_state, K->fused))) return rc;
             if (!K->fused) hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
-            hipLaunchKernelGGL(k_local_dpi, dim3(1), rt, 0, s, K->d_part, K->n_dparts, K->d_opart,
-                               have_o ? M->o_grid : 0, K->d_red, K->d_state, multi ? 0 : 1);
+            hipLaunchKernelGGL(k_local_dpi, dim3(1), rt, 0, s, K->d_part, K->n_dparts, opart, nob, K->d_red,
+                               K->d_state, multi ? 0 : 1);
             if (multi) {
                 if ((rc = comm_allreduce(C, K->d_red, 1, s))) return rc;
                 hipLaunchKernelGGL(k_step_dpi, dim3(1), dim3(64), 0, s, K->d_red, K->d_state);
@@ -883,7 +896,8 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
             if (gamg) {  // z = B r; z.z and z.r from the fused finest post-smoothing, else k_dots
                 const double *dots = nullptr;
                 int nbz = 0;
-                if ((e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, &dots, &nbz)) != hipSuccess)
+                if ((e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, &dots, &nbz, &K->d_state->done)) !=
+                    hipSuccess)
                     return mhip(e, "GAMG V-cycle");
                 if (!dots) {
                     hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);

@@ -28,7 +28,7 @@ KSP_SYMBOLS = (
     "aijhip_ksp_get_iteration_number", "aijhip_ksp_get_residual_norm", "aijhip_ksp_get_converged_reason",
     "aijhip_ksp_get_residual_history", "aijhip_ksp_get_fused", "aijhip_ksp_destroy",
     "aijhip_ksp_set_gamg_params", "aijhip_ksp_get_pc_levels", "aijhip_ksp_get_pc_level",
-    "aijhip_ksp_get_gamg_setup_path",
+    "aijhip_ksp_get_gamg_setup_path", "aijhip_ksp_get_host_syncs",
 )
 _P = ctypes.c_void_p
 _bound = False
@@ -52,6 +52,7 @@ def _lib():
         L.aijhip_ksp_get_converged_reason.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
         L.aijhip_ksp_get_residual_history.argtypes = [_P, _P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
         L.aijhip_ksp_get_fused.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
+        L.aijhip_ksp_get_host_syncs.argtypes = [_P, ctypes.POINTER(ctypes.c_int32)]
         L.aijhip_ksp_destroy.argtypes = [_P]
         L.aijhip_ksp_set_gamg_params.argtypes = [_P, _P]
         L.aijhip_ksp_get_pc_level.argtypes = [_P, ctypes.c_int32, ctypes.c_char, ctypes.POINTER(ctypes.c_int32),
@@ -107,6 +108,13 @@ class KSPCG:
     def rnorm(self) -> float:
         v = ctypes.c_double()
         _pkg._check(_lib().aijhip_ksp_get_residual_norm(self._h, ctypes.byref(v)))
+        return v.value
+
+    @property
+    def host_syncs(self) -> int:
+        """Host synchronisations of the last solve (polls + the final read)."""
+        v = ctypes.c_int32()
+        _pkg._check(_lib().aijhip_ksp_get_host_syncs(self._h, ctypes.byref(v)))
         return v.value
 
     @property

@@ -52,6 +52,8 @@ typedef struct {
   PetscObjectState state;        /* object state at the last upload: values
                                     changed without an assembly (MatScale,
                                     MatShift, MatDuplicate, ...) raise it */
+  PetscBool        stale;        /* set by the assembly hook: the next product
+                                    re-uploads and records the state it sees */
   /* PETSc's CPU bodies the assembly left in the ops table (SeqAIJ or Inode),
      for matrices below the transfer threshold */
   PetscErrorCode (*cpu_multadd)(Mat, Vec, Vec, Vec);
@@ -86,14 +88,14 @@ static PetscErrorCode AIJHIPDevice(Mat A, int *dev)
   PetscFunctionReturn(0);
 }
 
-/* The device half of MatAssemblyEnd (step2 MatAssemblyEnd patch:17-44):
- * first assembly uploads; same nonzero structure -> new values only;
- * changed structure -> drop and re-upload. Flush assembly does nothing.
- * bump: 1 when called from inside ops->assemblyend — PETSc's MatAssemblyEnd
- * raises the object state once more after the hook returns, so the state the
- * upload corresponds to is the current one + 1 (else the first MatMult would
- * see a "changed" matrix and upload every value a second time). */
-static PetscErrorCode AIJHIPUpload(Mat A, MatAssemblyType mode, PetscObjectState bump)
+/* The device copy brought up to date (step2 MatAssemblyEnd patch:17-44, done
+ * at the first product after the assembly as step 2's MatMult copyin does,
+ * step2 MatMult patch:19-21): first use creates; same nonzero structure ->
+ * new values only; changed structure -> drop and re-upload. The state
+ * recorded is the one read here, at product time, so it is exact whatever
+ * PETSc raised after the assembly hook returned (the public MatAssemblyEnd
+ * raises it once more; an internal direct call does not). */
+static PetscErrorCode AIJHIPUpload(Mat A)
 {
   Mat_SeqAIJ     *a = (Mat_SeqAIJ*)A->data;
   Mat_AIJHIP     *d = (Mat_AIJHIP*)A->spptr;
@@ -101,7 +103,6 @@ static PetscErrorCode AIJHIPUpload(Mat A, MatAssemblyType mode, PetscObjectState
   PetscErrorCode ierr;
 
   PetscFunctionBegin;
-  if (mode == MAT_FLUSH_ASSEMBLY) PetscFunctionReturn(0);
   if (!d) {
     ierr = PetscNew(&d);CHKERRQ(ierr);
     A->spptr = d;
@@ -117,7 +118,24 @@ static PetscErrorCode AIJHIPUpload(Mat A, MatAssemblyType mode, PetscObjectState
   if (rc) SETERRQ1(PetscObjectComm((PetscObject)A), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
   d->nonzerostate = A->nonzerostate;
   ierr = PetscObjectStateGet((PetscObject)A, &d->state);CHKERRQ(ierr);
-  d->state += bump;
+  d->stale = PETSC_FALSE;
+  PetscFunctionReturn(0);
+}
+
+/* The assembly hook's device half: a final assembly makes the device copy
+ * stale (flush assembly does nothing, step2 MatAssemblyEnd patch:15). */
+static PetscErrorCode AIJHIPMarkStale(Mat A, MatAssemblyType mode)
+{
+  Mat_AIJHIP     *d = (Mat_AIJHIP*)A->spptr;
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  if (mode == MAT_FLUSH_ASSEMBLY) PetscFunctionReturn(0);
+  if (!d) {
+    ierr = PetscNew(&d);CHKERRQ(ierr);
+    A->spptr = d;
+  }
+  d->stale = PETSC_TRUE;
   PetscFunctionReturn(0);
 }
 
@@ -167,9 +185,9 @@ static PetscErrorCode AIJHIPCurrent(Mat A, Mat_AIJHIP **out)
 
   PetscFunctionBegin;
   ierr = PetscObjectStateGet((PetscObject)A, &state);CHKERRQ(ierr);
-  if (!d || !d->h || d->state != state) {
+  if (!d || !d->h || d->stale || d->state != state) {
     if (!A->assembled) SETERRQ(PetscObjectComm((PetscObject)A), PETSC_ERR_ARG_WRONGSTATE, "aijhip: product with an unassembled matrix");
-    ierr = AIJHIPUpload(A, MAT_FINAL_ASSEMBLY, 0);CHKERRQ(ierr);
+    ierr = AIJHIPUpload(A);CHKERRQ(ierr);
   }
   *out = (Mat_AIJHIP*)A->spptr;
   PetscFunctionReturn(0);
@@ -269,7 +287,7 @@ static PetscErrorCode MatAssemblyEnd_SeqAIJHIP(Mat A, MatAssemblyType mode)
    * when it finds identical-pattern rows (multi-dof FEM operators such as
    * Flan_1565): take MatMult back, or such matrices would multiply on the CPU */
   A->ops->mult = AIJHIPMult;
-  ierr = AIJHIPUpload(A, mode, 1);CHKERRQ(ierr);
+  ierr = AIJHIPMarkStale(A, mode);CHKERRQ(ierr);
   if (mode == MAT_FINAL_ASSEMBLY) {
     ierr = AIJHIPInstallOps(A);CHKERRQ(ierr);
   }
@@ -354,7 +372,7 @@ PetscErrorCode MatAssemblyEnd_SeqAIJ(Mat A, MatAssemblyType mode)
   PetscFunctionBegin;
   ierr = MatAssemblyEnd_SeqAIJ_Original(A, mode);CHKERRQ(ierr);
   A->ops->mult = MatMult_SeqAIJ; /* the inode check may have installed MatMult_SeqAIJ_Inode */
-  ierr = AIJHIPUpload(A, mode, 1);CHKERRQ(ierr);
+  ierr = AIJHIPMarkStale(A, mode);CHKERRQ(ierr);
   if (mode == MAT_FINAL_ASSEMBLY) { /* MatMultAdd_SeqAIJ / MatMultTranspose_SeqAIJ stay in aij.o: only the ops table changes */
     ierr = AIJHIPInstallOps(A);CHKERRQ(ierr);
   }

@@ -476,3 +476,47 @@ def test_auto_geometry_follows_gather_locality(pkg, dev):
     for (ai, aj, aa), geom in cases:
         with pkg.SeqAIJHIP(ai, aj, aa) as A:
             assert A.info()["stream_geometry"] == geom
+
+
+@pytest.mark.parametrize("case", ["skewed", "fem_hex", "mixed"])
+@pytest.mark.parametrize("group", [1, 2])
+def test_row_group_kernel(pkg, dev, coracle, case, group):
+    """Register row groups (row_group 1 = 256 lanes, 2 = 512): blocks of mean
+    row length >= 24 are summed by L lanes per row in registers (reordered,
+    fp64 bound, deterministic); blocks of shorter rows keep the LDS STREAM
+    kernel and stay bit-exact; MatMultAdd alike."""
+    if case == "skewed":
+        ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
+    elif case == "fem_hex":
+        ai, aj, aa = pkg.fem_hex_csr(21, 20, 19)
+    else:  # 7-point rows, then rows of 30-90 entries
+        rng = np.random.default_rng(7)
+        p_ai, p_aj, p_aa = pkg.poisson_csr(20)
+        m0 = len(p_ai) - 1
+        lens = rng.integers(30, 90, 5000)
+        m = m0 + len(lens)
+        rows = [np.sort(rng.choice(m, size=l, replace=False)) for l in lens]
+        ai = np.concatenate([p_ai, p_ai[-1] + np.cumsum(lens)]).astype(np.int32)
+        aj = np.concatenate([p_aj] + rows).astype(np.int32)
+        aa = np.concatenate([p_aa, rng.uniform(-1, 1, int(lens.sum()))])
+    m = len(ai) - 1
+    x = pkg.splitmix_uniform(m, 21)
+    z = pkg.splitmix_uniform(m, 22)
+    ref = coracle.matmult(ai, aj, aa, x, omp=True)
+    with pkg.SeqAIJHIP(ai, aj, aa, row_group=group) as A:
+        xd, zd = to_dev(x, dev), to_dev(z, dev)
+        y1 = torch.full((m,), float("nan"), dtype=torch.float64, device=dev)
+        y2 = torch.empty_like(y1)
+        w = torch.empty_like(y1)
+        A.mult(xd, y1)
+        A.mult(xd, y2)
+        A.mult_add(xd, zd, w)
+        torch.cuda.synchronize()
+        y = y1.cpu().numpy()
+        assert torch.equal(y1, y2)
+        check(y, ref, ai, aj, aa, x, exact=False)
+        wref = coracle.matmult_add(ai, aj, aa, x, z)
+        check(w.cpu().numpy(), wref, ai, aj, aa, x, exact=False, z=z)
+        if case == "mixed":  # the Poisson rows sit in short-row blocks: PETSc's order
+            n0 = len(p_ai) - 1 - 600
+            assert_bits(y[:n0], ref[:n0])

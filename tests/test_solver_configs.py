@@ -75,6 +75,7 @@ def test_gpu_cg_gamg_300_configs2(pkg, coracle):
         its, reason, rnorm = ksp.its, ksp.reason, ksp.rnorm
         hist = ksp.history()
         path, overflow = ksp.setup_path()
+        syncs = ksp.host_syncs
     finally:
         ksp.destroy()
         A.destroy()
@@ -91,6 +92,39 @@ def test_gpu_cg_gamg_300_configs2(pkg, coracle):
     assert rel <= 1e-11, rel
     assert err <= C_H2 / (N * N), err
     assert all(p == "device" for p, _ in path[:2]), path  # the two big levels are built on the GPU
+    # the V-cycle honours the device stop flag: iterations go out in batches
+    # of 8 between host polls (57 iterations -> 8 polls + the final read)
+    assert syncs <= 10, syncs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pc", ["gamg", "jacobi"])
+def test_gpu_batched_polling_is_bitwise(pkg, pc, monkeypatch):
+    """Polling the stop flag every 8 iterations (default) or every iteration
+    (AIJHIP_KSP_POLL=1) gives the same residual history and x bit for bit:
+    kernels launched past convergence return at once."""
+    torch = pytest.importorskip("torch")
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    N = 48
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, _ = pkg.poisson_vectors(N)
+    out = {}
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    try:
+        with K.KSPCG(A, pc=pc, **TOL) as ksp:
+            for poll in ("1", "8"):
+                monkeypatch.setenv("AIJHIP_KSP_POLL", poll)
+                b = torch.from_numpy(rhs).cuda()
+                x = torch.empty_like(b)
+                ksp.solve(b, x)
+                torch.cuda.synchronize()
+                out[poll] = (ksp.its, ksp.history(), x.cpu().numpy(), ksp.host_syncs)
+    finally:
+        A.destroy()
+    (i1, h1, x1, s1), (i8, h8, x8, s8) = out["1"], out["8"]
+    assert i1 == i8 and i1 > 8
+    assert np.array_equal(_bits(h1), _bits(h8)) and np.array_equal(_bits(x1), _bits(x8))
+    assert s1 >= i1 and s8 <= i8 // 8 + 3, (s1, s8, i1)
 
 
 @pytest.mark.gpu

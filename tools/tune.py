@@ -121,6 +121,10 @@ def main():
     if args.variants == "skewpipe":
         for g, ex, pp in itertools.product((1, 7), (0, 1), (0, 1, 2, 3)):
             variants.append(("stream", dict(geometry=g, exact=ex, persistent=pp)))
+    if args.variants == "group":  # register row-group kernel (AIJHIP_OPT_ROW_GROUP) vs the LDS blocks
+        for g, rg, nt in ((-1, 0, -1), (-1, 1, -1), (-1, 2, -1), (-1, 1, 0), (-1, 1, 1), (6, 1, -1), (6, 0, -1),
+                          (1, 2, 1), (6, 2, 0)):
+            variants.append(("stream", dict(geometry=g, row_group=rg, nt_loads=nt)))
     if args.variants == "skewed":
         for g in (0, 1, 4, 6, 7, 8):
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=0)))
@@ -136,6 +140,7 @@ def main():
         A.set_option("x_tile", opts.get("x_tile", -1 if opts else 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
         A.set_option("long_overlap", opts.get("long_overlap", 0))
+        A.set_option("row_group", opts.get("row_group", 0))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
