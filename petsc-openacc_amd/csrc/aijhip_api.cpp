@@ -688,7 +688,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             t.xchunk = value >= 2 ? value : 0;
             break;
         case AIJHIP_OPT_NT_LOADS:
-            if (value < -1 || value > 3) return fail(AIJHIP_ERR_ARG, "nt_loads: -1 (auto), 0..3");
+            if (value < -1 || value > 5) return fail(AIJHIP_ERR_ARG, "nt_loads: -1 (auto), 0..5");
             t.nt = value;
             break;
         case AIJHIP_OPT_PERSISTENT:

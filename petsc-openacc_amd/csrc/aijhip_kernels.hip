@@ -236,13 +236,21 @@ __device__ __forceinline__ double row_sum_seq(const double *p, int32_t n, double
     return s;
 }
 
-// NT (load mode): 0 plain loads, aa/aj interleaved per iteration; 1 both
-// non-temporal; 2 all aj loads first, then aa non-temporal; 3 aj first, plain.
-template <int T, int CAP, int RPT, bool CROW, bool XCD, int NT, bool CLAMPED, class Op>
+// NT (load mode), bits 0-1: 0 plain loads, aa/aj interleaved per iteration;
+// 1 both non-temporal; 2 all aj loads first, then aa non-temporal; 3 aj
+// first, plain. Bit 2 (SHUF): gathers in lane-stride order — the wave's
+// 128-entry window is gathered as entries [0, 64) then [64, 128) (columns
+// moved across lanes with __shfl, the values moved back to the lanes that
+// hold the pairs), so one gather instruction touches the x lines of ~64
+// consecutive entries instead of every other entry of 128: about half as
+// many distinct lines per instruction, the matrix loads still 16-B pairs.
+template <int T, int CAP, int RPT, bool CROW, bool XCD, int NTMODE, bool CLAMPED, class Op>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, Op op, double *dpart, const int *stop, const int2 *__restrict__ xrange) {
+    constexpr int NT = NTMODE & 3;
+    constexpr bool SHUF = (NTMODE & 4) != 0;
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
     const int bid = (int)blockIdx.x;
@@ -310,16 +318,37 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             __syncthreads();
         }
     }
+    if constexpr (SHUF && !Op::kTile) {
+        const int lane = t & 63;
+        const int half = lane >> 1;
 #pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-        const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if (CLAMPED || k < k1) {
-            if (tiled) {
-                xv[it].x = prod[cv[it].x - xr.x];
-                xv[it].y = prod[cv[it].y - xr.x];
-            } else {
-                xv[it].x = op.gx(cv[it].x);
-                xv[it].y = op.gx(cv[it].y);
+        for (int it = 0; it < ITERS; ++it) {
+            // first pair index of this wave's window in this iteration
+            const int64_t kw = kb + 2 * (int64_t)((t & ~63) + it * T);
+            const int ca0 = __shfl(cv[it].x, half, 64), ca1 = __shfl(cv[it].y, half, 64);
+            const int cb0 = __shfl(cv[it].x, 32 + half, 64), cb1 = __shfl(cv[it].y, 32 + half, 64);
+            const int ca = (lane & 1) ? ca1 : ca0, cb = (lane & 1) ? cb1 : cb0;
+            // an entry is gathered when the lane holding its pair loaded it
+            const bool va = CLAMPED || kw + 2 * half < k1, vb = CLAMPED || kw + 2 * (32 + half) < k1;
+            const double xa = va ? op.gx(ca) : 0.0, xb = vb ? op.gx(cb) : 0.0;
+            const int e0 = (2 * lane) & 63, e1 = (2 * lane + 1) & 63;
+            const double a0 = __shfl(xa, e0, 64), b0 = __shfl(xb, e0, 64);
+            const double a1 = __shfl(xa, e1, 64), b1 = __shfl(xb, e1, 64);
+            xv[it].x = lane < 32 ? a0 : b0;
+            xv[it].y = lane < 32 ? a1 : b1;
+        }
+    } else {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
+            if (CLAMPED || k < k1) {
+                if (tiled) {
+                    xv[it].x = prod[cv[it].x - xr.x];
+                    xv[it].y = prod[cv[it].y - xr.x];
+                } else {
+                    xv[it].x = op.gx(cv[it].x);
+                    xv[it].y = op.gx(cv[it].y);
+                }
             }
         }
     }
@@ -990,8 +1019,10 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         if (add) { AIJHIP_SL(true, false, false, false, false); }
         AIJHIP_SL(false, true, false, false, false);
     }
-    if (P.tune.nt >= 2 && !P.tune.xcd && !P.tune.clamped) {  // load-order study modes
+    if (P.tune.nt >= 2 && !P.tune.xcd && !P.tune.clamped) {  // load-order study modes, lane-stride gathers
         if (P.tune.nt == 2) { AIJHIP_SL(false, false, false, 2, false); }
+        if (P.tune.nt == 4) { AIJHIP_SL(false, false, false, 4, false); }
+        if (P.tune.nt == 5) { AIJHIP_SL(false, false, false, 5, false); }
         AIJHIP_SL(false, false, false, 3, false);
     }
     switch ((P.tune.xcd ? 4 : 0) | (P.tune.nt ? 2 : 0) | (P.tune.clamped ? 1 : 0)) {

@@ -435,7 +435,8 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
         first = None
         for geom in range(12):
             for xcd, nt, persist, clamped in ((0, 0, 0, 0), (1, 0, 0, 1), (0, 1, 0, 0), (22, 1, 0, 1), (3, 0, 0, 0),
-                                              (0, 0, 1, 0), (0, 1, 2, 0), (0, 0, 5, 0), (0, 0, 0, 1)):
+                                              (0, 0, 1, 0), (0, 1, 2, 0), (0, 0, 5, 0), (0, 0, 0, 1), (0, 4, 0, 0),
+                                              (0, 5, 0, 0)):
                 if persist and geom == 2:
                     continue
                 for _ in range(1):

@@ -125,6 +125,9 @@ def main():
         for g, rg, nt in ((-1, 0, -1), (-1, 1, -1), (-1, 2, -1), (-1, 1, 0), (-1, 1, 1), (6, 1, -1), (6, 0, -1),
                           (1, 2, 1), (6, 2, 0)):
             variants.append(("stream", dict(geometry=g, row_group=rg, nt_loads=nt)))
+    if args.variants == "shuf":  # lane-stride gathers through __shfl (nt_loads 4 plain / 5 non-temporal)
+        for g, nt in ((-1, -1), (-1, 4), (-1, 5), (6, 0), (6, 4), (6, 5), (1, 1), (1, 5), (1, 4), (0, 4), (8, 4)):
+            variants.append(("stream", dict(geometry=g, nt_loads=nt)))
     if args.variants == "skewed":
         for g in (0, 1, 4, 6, 7, 8):
             variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=0)))
