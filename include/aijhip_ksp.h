@@ -33,7 +33,16 @@ typedef struct aijhip_ksp *aijhip_ksp_t;
  * application: Richardson(1) + Jacobi smoothing down and up on every level,
  * preonly + Jacobi on the coarsest — PETSc_SolverOptions_GAMG.info:6-21;
  * hierarchy from include/aijhip_gamg.h). */
-enum { AIJHIP_PC_NONE = 0, AIJHIP_PC_JACOBI = 1, AIJHIP_PC_GAMG = 2 };
+enum {
+    AIJHIP_PC_NONE = 0,
+    AIJHIP_PC_JACOBI = 1,
+    AIJHIP_PC_GAMG = 2,         /* PCGAMG; on a distributed operator (aijhip_kspmpi,
+                                   more than one rank) the hierarchy spans the
+                                   ranks, as PETSc's agg GAMG does             */
+    AIJHIP_PC_BJACOBI_GAMG = 3  /* distributed operator only: -pc_type bjacobi
+                                   -sub_pc_type gamg (one hierarchy per rank's
+                                   diagonal block, no coupling)               */
+};
 
 /* KSPNormType values as in PETSc. */
 enum {

@@ -73,6 +73,18 @@ typedef int (*aijhip_host_exchange_fn)(void *ctx, aijhip_mpiaij_t op, const doub
 int aijhip_comm_create_host(int32_t nranks, int32_t rank, int32_t device, aijhip_host_allreduce_fn allreduce,
                             aijhip_host_exchange_fn exchange, void *ctx, aijhip_comm_t *out);
 
+/* The host transport's point-to-point exchange of variable-size messages,
+ * used by the distributed GAMG set-up (aggregate ids, ghost rows of P,
+ * Galerkin contributions to other ranks' coarse rows): send segment q —
+ * send[send_off[q] .. send_off[q+1]), 8-byte words — to send_peer[q];
+ * receive segment p into recv[recv_off[p] .. recv_off[p+1]) from
+ * recv_peer[p]. Sizes are known on both sides (the library exchanges them
+ * first); this rank never appears as a peer. Return 0 on success. */
+typedef int (*aijhip_host_sendrecv_fn)(void *ctx, int32_t n_send, const int32_t *send_peer,
+                                       const int64_t *send_off, const double *send, int32_t n_recv,
+                                       const int32_t *recv_peer, const int64_t *recv_off, double *recv);
+int aijhip_comm_set_host_sendrecv(aijhip_comm_t comm, aijhip_host_sendrecv_fn fn);
+
 /* kind: AIJHIP_COMM_*; version: RCCL's ncclGetVersion code (0 for host). */
 int aijhip_comm_info(aijhip_comm_t comm, int32_t *nranks, int32_t *rank, int32_t *kind, int32_t *version);
 /* In-place sum of n device doubles over all ranks, enqueued on `stream`
@@ -113,12 +125,16 @@ int aijhip_mpiaij_destroy(aijhip_mpiaij_t M);
 
 /* KSPCG on the distributed operator. PC (aijhip_ksp.h values): NONE; JACOBI
  * = PETSc's bjacobi + jacobi sub-PC (the inverse diagonal of A_d); GAMG =
- * bjacobi + gamg sub-PC (-pc_type bjacobi -sub_pc_type gamg): each rank's
- * diagonal block gets its own smoothed-aggregation hierarchy
- * (aijhip_ksp.h's set-up, parameters from aijhip_kspmpi_set_gamg_params) and
- * one V-cycle per application, with no communication inside the PC; at one
- * rank it is PCGAMG itself. Options, reasons and norms as aijhip_ksp.h;
- * defaults as PETSc. */
+ * PETSc's agg GAMG over the whole operator (-pc_type gamg on an MPIAIJ
+ * matrix): aggregates local to each rank, the prolongator smoothed and the
+ * Galerkin products formed across ranks (ghost rows of P exchanged, coarse
+ * contributions sent to their owners), every level a distributed operator
+ * with its own p2p halo, one multiplicative V-cycle per application with
+ * the halo exchanges inside (the operator must use AIJHIP_HALO_P2P); at one
+ * rank the single-GPU PCGAMG set-up (bit-identical to aijhip_ksp's).
+ * BJACOBI_GAMG = -pc_type bjacobi -sub_pc_type gamg: a hierarchy per rank's
+ * diagonal block, no communication inside the PC. Options, reasons and norms
+ * as aijhip_ksp.h; defaults as PETSc. */
 int aijhip_kspmpi_create(aijhip_mpiaij_t M, aijhip_kspmpi_t *out);
 int aijhip_kspmpi_set_tolerances(aijhip_kspmpi_t K, double rtol, double abstol, double dtol, int32_t max_it);
 int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc_type);
@@ -138,6 +154,13 @@ int aijhip_kspmpi_get_converged_reason(aijhip_kspmpi_t K, int *reason);
 int aijhip_kspmpi_get_residual_history(aijhip_kspmpi_t K, double *hist, int32_t na, int32_t *n);
 /* Host synchronisations made by the last solve (polls + the final read). */
 int aijhip_kspmpi_get_host_syncs(aijhip_kspmpi_t K, int32_t *n);
+/* The preconditioner's multigrid levels after set-up: global rows and
+ * global operator entries per level (GAMG across ranks); BJACOBI_GAMG: this
+ * rank's block hierarchy; other PCs: the operator alone. Collective for
+ * GAMG (nnz is summed over the ranks). */
+int aijhip_kspmpi_get_pc_levels(aijhip_kspmpi_t K, int32_t *nlevels, int64_t *rows, int64_t *nnz, int32_t cap);
+/* Seconds the last set-up took on this rank. */
+int aijhip_kspmpi_get_setup_seconds(aijhip_kspmpi_t K, double *seconds);
 int aijhip_kspmpi_destroy(aijhip_kspmpi_t K);
 
 #ifdef __cplusplus

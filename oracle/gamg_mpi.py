@@ -1,0 +1,73 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+numpy/scipy restatement of the distributed smoothed-aggregation hierarchy of
+petsc-openacc_amd/csrc/gamg_mpi.hip (PCGAMG across ranks, the agg GAMG the
+reference runs on 1-16 MPI ranks: /root/reference/runs/single-node-scaling.pbs
+:56-67 with /root/reference/configs/PETSc_SolverOptions_GAMG.info:6-21),
+computed globally:
+
+  - rank r owns rows [starts[r], starts[r+1]) of every level;
+  - aggregates are formed on each rank's diagonal block with oracle/gamg.py's
+    greedy aggregation, numbered rank by rank (coarse rows of rank r =
+    [cstarts[r], cstarts[r+1]));
+  - emax by power iteration on the global D^-1 A from oracle/gamg.py's start
+    vector at global indices;
+  - P0, P = P0 - 1.4/emax D^-1 A P0 and A_c = P^T A P over the whole operator;
+  - the hierarchy stops where the single-GPU one does, with global counts.
+
+The V-cycle is oracle/gamg.py's (global operators; the distributed one is the
+same arithmetic up to summation order). Parity unpinned w.r.t. PETSc, as for
+oracle/gamg.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+from oracle import gamg as og
+
+
+def build(A, starts, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smooth_scale=1.4, eig_its=10):
+    """A: global operator; starts: row ownership (len = ranks + 1). Returns
+    a list of levels dict(A, P, starts, emax) in oracle/gamg.py's format
+    (vcycle-compatible)."""
+    A = sp.csr_matrix(A)
+    starts = np.asarray(starts, dtype=np.int64)
+    levels = []
+    B = np.ones(A.shape[0])
+    while len(levels) + 1 < max_levels and A.shape[0] > coarse_eq_limit:
+        d = og.first_diagonal(A)
+        dinv = 1.0 / np.where(d == 0.0, 1.0, d)
+        aggs, nas = [], []
+        for r in range(len(starts) - 1):
+            lo, hi = starts[r], starts[r + 1]
+            Ad = sp.csr_matrix(A[lo:hi, lo:hi])
+            Ad.sort_indices()
+            S = og.strength_graph(Ad, d[lo:hi], threshold)
+            agg, na = og.aggregate(Ad, S)
+            aggs.append(agg)
+            nas.append(na)
+        cstarts = np.concatenate([[0], np.cumsum(nas)]).astype(np.int64)
+        NA = int(cstarts[-1])
+        if NA == 0 or NA >= A.shape[0]:
+            break
+        agg = np.concatenate([a + cstarts[r] for r, a in enumerate(aggs)])
+        emax = og.estimate_emax(A, dinv, eig_its) if nsmooths > 0 else 1.0
+        Bc = np.sqrt(np.bincount(agg, weights=B * B, minlength=NA))
+        p0 = np.where(Bc[agg] > 0, B / np.where(Bc[agg] > 0, Bc[agg], 1.0), 0.0)
+        P0 = sp.csr_matrix((p0, (np.arange(A.shape[0]), agg)), shape=(A.shape[0], NA))
+        P = P0
+        if nsmooths > 0:
+            P = (-smooth_scale / emax) * (sp.diags(dinv) @ (A @ P0)) + P0
+        P = sp.csr_matrix(P)
+        P.sort_indices()
+        Ac = sp.csr_matrix(P.T @ (A @ P))
+        Ac.sort_indices()
+        levels.append(dict(A=A, P=P, starts=starts, emax=emax, agg=agg))
+        A, B, starts = Ac, Bc, cstarts
+    levels.append(dict(A=A, starts=starts))
+    return levels
+
+
+def vcycle(levels, b):
+    return og.vcycle(levels, b)

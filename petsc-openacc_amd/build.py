@@ -24,7 +24,7 @@ ORACLE_DIR = ROOT / "oracle"
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 
 HIP_SOURCES = ["aijhip_kernels.hip", "aijhip_api.cpp", "ksp.hip", "poisson.hip", "gamg_device.hip", "vec.hip",
-               "ksp_mpi.hip", "host_pipe.cpp", "gamg_aggregate.hip"]
+               "ksp_mpi.hip", "host_pipe.cpp", "gamg_aggregate.hip", "gamg_mpi.hip"]
 HOST_SOURCES = ["harness.cpp", "gamg_setup.cpp"]
 ARCH = os.environ.get("AIJHIP_ARCH", "gfx950")
 

@@ -35,6 +35,8 @@ AIJHIP_ERR_COMM = 6
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, _P, _DP, _i32)
 EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, _P, _P, _DP, _i64, _DP, _i64)
+_I32P, _I64P = ctypes.POINTER(_i32), ctypes.POINTER(_i64)
+SENDRECV_FN = ctypes.CFUNCTYPE(ctypes.c_int, _P, _i32, _I32P, _I64P, _DP, _i32, _I32P, _I64P, _DP)
 
 MPI_SYMBOLS = (
     "aijhip_comm_rccl_unique_id", "aijhip_comm_create_rccl", "aijhip_comm_create_host", "aijhip_comm_info",
@@ -45,6 +47,7 @@ MPI_SYMBOLS = (
     "aijhip_kspmpi_set_norm_type", "aijhip_kspmpi_set_poll_interval", "aijhip_kspmpi_solve",
     "aijhip_kspmpi_get_iteration_number", "aijhip_kspmpi_get_residual_norm", "aijhip_kspmpi_get_converged_reason",
     "aijhip_kspmpi_get_residual_history", "aijhip_kspmpi_get_host_syncs", "aijhip_kspmpi_destroy",
+    "aijhip_comm_set_host_sendrecv", "aijhip_kspmpi_get_pc_levels", "aijhip_kspmpi_get_setup_seconds",
 )
 _bound = False
 
@@ -79,6 +82,9 @@ def _lib():
         L.aijhip_kspmpi_get_residual_history.argtypes = [_P, _P, _i32, ctypes.POINTER(_i32)]
         L.aijhip_kspmpi_get_host_syncs.argtypes = [_P, ctypes.POINTER(_i32)]
         L.aijhip_kspmpi_destroy.argtypes = [_P]
+        L.aijhip_comm_set_host_sendrecv.argtypes = [_P, SENDRECV_FN]
+        L.aijhip_kspmpi_get_pc_levels.argtypes = [_P, ctypes.POINTER(_i32), _P, _P, _i32]
+        L.aijhip_kspmpi_get_setup_seconds.argtypes = [_P, ctypes.POINTER(_d)]
         _bound = True
     return L
 
@@ -156,9 +162,34 @@ class Comm:
             except Exception:  # noqa: BLE001
                 return 1
 
-        cb = (ALLREDUCE_FN(allreduce), EXCHANGE_FN(exchange))
+        def sendrecv(_ctx, ns, speer, soff, send, nr, rpeer, roff, recv):
+            """The library's own point-to-point plans (the distributed GAMG's
+            set-up messages and the halos of the operators it makes)."""
+            try:
+                works, outs = [], []
+                sall = np.ctypeslib.as_array(send, shape=(max(int(soff[ns]), 1),)) if ns else None
+                for i in range(ns):
+                    buf = torch.from_numpy(sall[int(soff[i]):int(soff[i + 1])].copy())
+                    outs.append(buf)
+                    works.append(dist.isend(buf, int(speer[i]), group=group))
+                rall = np.ctypeslib.as_array(recv, shape=(max(int(roff[nr]), 1),)) if nr else None
+                ins = []
+                for i in range(nr):
+                    buf = torch.empty(int(roff[i + 1]) - int(roff[i]), dtype=torch.float64)
+                    ins.append((int(roff[i]), buf))
+                    works.append(dist.irecv(buf, int(rpeer[i]), group=group))
+                for w in works:
+                    w.wait()
+                for a, buf in ins:
+                    rall[a:a + buf.numel()] = buf.numpy()
+                return 0
+            except Exception:  # noqa: BLE001
+                return 1
+
+        cb = (ALLREDUCE_FN(allreduce), EXCHANGE_FN(exchange), SENDRECV_FN(sendrecv))
         h = _P()
         _pkg._check(_lib().aijhip_comm_create_host(world, rank, device, cb[0], cb[1], None, ctypes.byref(h)))
+        _pkg._check(_lib().aijhip_comm_set_host_sendrecv(h, cb[2]))
         c = cls(h, COMM_HOST, rank, world, device, keep=(cb, state))
         c.set_timeout(timeout_s)
         return c
@@ -254,8 +285,9 @@ class KSPCGMPINative:
 
     def __init__(self, op: NativeMPIAIJ, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
                  norm="preconditioned", poll: int = 8, gamg=None):
-        """pc: "none", "jacobi" (bjacobi + jacobi) or "gamg" (bjacobi + gamg:
-        a GAMG hierarchy per rank's diagonal block; gamg = its parameters)."""
+        """pc: "none", "jacobi" (bjacobi + jacobi), "gamg" (PCGAMG across the
+        ranks: one distributed hierarchy) or "bjacobi_gamg" (a GAMG hierarchy
+        per rank's diagonal block); gamg = the GAMG parameters."""
         K = importlib.import_module("petsc-openacc_amd.ksp")
         L = _lib()
         self.op = op
@@ -299,6 +331,20 @@ class KSPCGMPINative:
     @property
     def host_syncs(self) -> int:
         return self._get(_lib().aijhip_kspmpi_get_host_syncs, _i32)
+
+    @property
+    def setup_seconds(self) -> float:
+        return self._get(_lib().aijhip_kspmpi_get_setup_seconds, _d)
+
+    def pc_levels(self):
+        """(global rows, global entries) per level of the set-up PC
+        (collective for GAMG across ranks)."""
+        n = _i32()
+        rows = np.zeros(32, np.int64)
+        nnz = np.zeros(32, np.int64)
+        _pkg._check(_lib().aijhip_kspmpi_get_pc_levels(self._h, ctypes.byref(n), rows.ctypes.data, nnz.ctypes.data,
+                                                        32))
+        return rows[: n.value].tolist(), nnz[: n.value].tolist()
 
     @property
     def hist(self) -> np.ndarray:

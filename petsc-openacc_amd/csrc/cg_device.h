@@ -14,8 +14,8 @@
 
 #include "aijhip_ksp.h"
 
-namespace {
-
+// The device scalar state (external linkage: the distributed GAMG's
+// translation unit passes it to MatMult_MPIAIJ, mpi_internal.h).
 struct CGState {
     double beta, betaold, dpi, dpiold, a, b, dp, rnorm0, ttol;
     int32_t its, reason, done, i;
@@ -26,6 +26,8 @@ struct CGParams {
     double rtol, abstol, dtol;
     int32_t max_it, normtype, guess_zero, pc;
 };
+
+namespace {
 
 constexpr int kVecThreads = 256;
 constexpr int kRedThreads = 1024;

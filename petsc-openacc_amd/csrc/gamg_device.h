@@ -2,12 +2,31 @@
 // (gamg_device.hip), used by the KSP set-up (ksp.hip).
 #pragma once
 
+#include <algorithm>
 #include <vector>
 
 #include "aijhip_internal.h"
 #include "gamg_internal.h"
 
 namespace aijhip_gamg {
+
+// Device CSR owned by a set-up (nz + 2 entries: the SpMV handles' tail pad).
+struct DCsr {
+    int32_t m = 0, n = 0;
+    int64_t nz = 0;
+    int32_t *ai = nullptr, *aj = nullptr;
+    double *aa = nullptr;
+    void release() {
+        hipFree(ai); hipFree(aj); hipFree(aa);
+        ai = aj = nullptr;
+        aa = nullptr;
+    }
+};
+
+template <class T>
+hipError_t dalloc(T **p, int64_t count) {
+    return hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * (size_t)std::max<int64_t>(count, 1));
+}
 
 // One level of the device hierarchy.
 struct DeviceLevel {
@@ -31,6 +50,32 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
                  std::vector<double> &B, bool *more, bool *overflow = nullptr);
 
 void free_device_levels(std::vector<DeviceLevel> &levels);
+
+// The steps of one coarsening, shared by build_device and the distributed
+// set-up (gamg_mpi.hip):
+//  aggregate_level: D^-1, strength graph and aggregates of A's rows (device
+//    agg ids in [0, *na)); with emax_its > 0 also emax(D^-1 A) of A itself
+//    (the power iteration on a second host thread);
+//  smooth_level: the tentative P0 from the near-null space B (Bc = the next
+//    level's) and P = P0 + alpha D^-1 (A P0), columns = agg ids;
+//  galerkin_level: A_c = P^T (A P) and P^T (ap_out: keep A P as well).
+int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_agg, int32_t *na, double **dinv,
+                    int emax_its, double *emax, hipError_t *emax_err, size_t level);
+int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, const double *dinv, double alpha,
+                 int nsmooths, int n_cu, double **d_p0, double **d_Bc, DCsr &P, int *cols_used);
+int galerkin_level(const DCsr &Av, const DCsr &P, DCsr &PT, DCsr &Ac, int n_cu, int *cols_used, DCsr *ap_out);
+// A handle adopting C's arrays (C is emptied).
+int make_level_handle(int device, DCsr &C, aijhip_mat **out);
+// C = A B, the row-traversal product (scipy csr_matmat order).
+int rowprod_device(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used);
+// The tentative prolongator's values: Bc[a] = ||B over aggregate a||, p0[i] =
+// B[i] / Bc[agg[i]] (device arrays).
+hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0);
+// P = P0 + alpha D^-1 T on the union pattern of T and P0 (P0: one entry per
+// row, column agg[i], value p0[i]); T's columns may extend past the local
+// aggregates (the distributed set-up's ghost coarse columns).
+int prolong_from_T(const DCsr &T, const int32_t *d_agg, const double *d_p0, const double *dinv, double alpha,
+                   DCsr &P);
 
 // Aggregation phase 1 on the device (gamg_aggregate.hip), from the symmetric
 // strength graph S (device CSR, rows sorted, unique, no diagonal): phase1[i]

@@ -745,23 +745,8 @@ __global__ void k_prolong_fill(int32_t m, const int32_t *__restrict__ ti, const 
 
 // ---------------------------------------------------------------- host side
 
-// Device CSR owned by this set-up (nz + 2 entries: the SpMV handles' tail pad).
-struct DCsr {
-    int32_t m = 0, n = 0;
-    int64_t nz = 0;
-    int32_t *ai = nullptr, *aj = nullptr;
-    double *aa = nullptr;
-    void release() {
-        hipFree(ai); hipFree(aj); hipFree(aa);
-        ai = aj = nullptr;
-        aa = nullptr;
-    }
-};
-
-template <class T>
-hipError_t dalloc(T **p, int64_t count) {
-    return hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * (size_t)std::max<int64_t>(count, 1));
-}
+using aijhip_gamg::DCsr;
+using aijhip_gamg::dalloc;
 
 // exclusive scan of int32 counts into int32 offsets (m+1); false on overflow
 hipError_t scan_offsets(const int32_t *cnt, int32_t m, int32_t *off, int64_t *total) {
@@ -1285,6 +1270,318 @@ void free_device_levels(std::vector<DeviceLevel> &levels) {
     levels.clear();
 }
 
+// Diagonal, strength graph and aggregates of one level (the first half of a
+// coarsening; build_device's and the distributed set-up's). With emax_its >
+// 0 the power iteration for emax(D^-1 A) runs on a second host thread
+// meanwhile (*emax on return).
+int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_agg_out, int32_t *na_out,
+                    double **dinv_out, int emax_its, double *emax, hipError_t *emax_err, size_t level) {
+    *d_agg_out = nullptr;
+    *dinv_out = nullptr;
+    *na_out = 0;
+    const int32_t m = A.m;
+    const int n_cu = std::max(A.n_cu, 1);
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!log) return;
+        (void)hipDeviceSynchronize();
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "gamg device level %zu %-14s %8.3f s\n", level, what,
+                     std::chrono::duration<double>(t - t0).count());
+        t0 = t;
+    };
+    std::unique_lock<std::mutex> stage_lock;
+    Staging &stage = process_staging(stage_lock);
+    int rc = AIJHIP_OK;
+    hipError_t e = hipSuccess;
+    const unsigned g256 = blocks_for(m, 256);
+    double *d = nullptr, *dinv = nullptr, *sval = nullptr;
+    unsigned long long *cnt = nullptr, *off = nullptr;
+    unsigned int *pos = nullptr;
+    int32_t *tmp = nullptr, *si = nullptr, *sj = nullptr;
+    void *scan_tmp = nullptr;
+    size_t tb = 0;
+    int64_t nzs = 0;
+    int32_t *h_si = nullptr, *h_sj = nullptr, *agg = nullptr, *d_ph = nullptr;
+    int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
+    unsigned long long *d_left = nullptr;
+    int32_t na = 0;
+    bool dev_agg = false;  // phase 1 ran on the device (else the host pass)
+    int32_t sweep_rounds = 0;
+    // emax(D^-1 A) needs only A: its power iteration runs from a second
+    // host thread while this one stages S and aggregates on the CPU
+    EmaxJob job;
+#define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto level_done; } } while (0)
+    GTRY(dalloc(&d, m), "alloc");
+    GTRY(dalloc(&dinv, m), "alloc");
+    hipLaunchKernelGGL(k_diag_dinv, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d, dinv);
+    {
+        bool direct = false;  // S straight from A (sorted rows, symmetric strong pattern)
+        if ((rc = strength_direct(A, d, p.threshold, &si, &sj, &sval, &nzs, &direct))) goto level_done;
+        if (log)
+            std::fprintf(stderr, "gamg device level %zu strength graph: %s\n", level,
+                         direct ? "direct (symmetric)" : "gathered (S u S^T)");
+        if (direct) goto strength_done;
+    }
+    GTRY(dalloc(&cnt, (int64_t)m + 1), "alloc");
+    GTRY(dalloc(&off, (int64_t)m + 1), "alloc");
+    GTRY(hipMemset(cnt, 0, sizeof(unsigned long long) * ((size_t)m + 1)), "memset");
+    hipLaunchKernelGGL(k_strong_count, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
+                       p.threshold, cnt);
+    GTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, m + 1), "scan");
+    GTRY(hipMalloc(&scan_tmp, std::max<size_t>(tb, 1)), "alloc");
+    GTRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, cnt, off, m + 1), "scan");
+    {
+        unsigned long long t = 0;
+        GTRY(hipMemcpy(&t, off + m, sizeof(t), hipMemcpyDeviceToHost), "read");
+        nzs = (int64_t)t;
+    }
+    GTRY(dalloc(&tmp, nzs), "alloc");
+    GTRY(dalloc(&pos, m), "alloc");
+    GTRY(hipMemset(pos, 0, sizeof(unsigned int) * (size_t)std::max(m, 1)), "memset");
+    hipLaunchKernelGGL(k_strong_fill, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
+                       p.threshold, off, pos, tmp);
+    if ((rc = strength_lists(A, cnt, off, tmp, nzs, n_cu, &si, &sj, &sval, &nzs))) goto level_done;
+strength_done:
+    GTRY(hipGetLastError(), "strength kernels");
+    // ---- aggregation. Phase 1: the device sweep (gamg_aggregate.hip) on
+    // large levels with a sparse S, else -- or when the sweep would run too
+    // deep -- the sequential pass on the host from S staged in pinned
+    // memory; the same aggregates either way. Phase 2 on the device; phase
+    // 3 (sequential) over the nodes left.
+    lap("strength kernels");
+    if (emax_its > 0) job.start(A, dinv, emax_its);
+    GTRY(dalloc(&d_ph, m), "alloc");
+    GTRY(dalloc(&d_aggv, m), "alloc");
+    GTRY(dalloc(&d_left, 1), "alloc");
+    {
+        int32_t max_rounds = 0;
+        if (device_phase1(m, nzs, &max_rounds)) {
+            GTRY(aijhip_gamg::aggregate_phase1_device(m, si, sj, max_rounds, d_ph, &na, &sweep_rounds, &dev_agg),
+                 "phase 1 sweep");
+            if (log)
+                std::fprintf(stderr, "gamg device level %zu phase 1 sweep: %d rounds%s\n", level, sweep_rounds,
+                             dev_agg ? "" : " (too deep: host pass)");
+        }
+    }
+    if (!dev_agg) {
+        GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
+        lap("staging alloc");
+        h_si = stage.i32();
+        h_sj = h_si + m + 1;
+        agg = h_sj + nzs;
+        GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
+        lap("strength");
+        // S's columns come down in row chunks while the pass works through
+        // the rows already here (a node reads only its own row). (Phase 1
+        // measured on the MI355X host at 300^3 level 0: this int32 form
+        // 83 ms; bitmap or byte flags with or without early exits 87-121 ms.)
+        {
+            constexpr int kChunks = 16;
+            hipStream_t cs = nullptr;
+            hipEvent_t ev[kChunks] = {};
+            GTRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
+            int32_t r[kChunks + 1];
+            for (int c = 0; c <= kChunks; ++c) r[c] = (int32_t)((int64_t)m * c / kChunks);
+            for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
+                const int64_t a = h_si[r[c]], b = h_si[r[c + 1]];
+                if (b > a)
+                    e = hipMemcpyAsync(h_sj + a, sj + a, sizeof(int32_t) * (size_t)(b - a), hipMemcpyDeviceToHost,
+                                       cs);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[c], hipEventDisableTiming);
+                if (e == hipSuccess) e = hipEventRecord(ev[c], cs);
+            }
+            std::fill(agg, agg + m, -1);
+            na = 0;
+            for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
+                if ((e = hipEventSynchronize(ev[c])) == hipSuccess)
+                    na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_sj, agg, na);
+            }
+            (void)hipStreamSynchronize(cs);
+            for (hipEvent_t x : ev)
+                if (x) (void)hipEventDestroy(x);
+            (void)hipStreamDestroy(cs);
+            GTRY(e, "read S");
+        }
+        GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
+    }
+    lap("phase 1");
+    hipLaunchKernelGGL(k_agg_phase2, dim3(g256), dim3(256), 0, nullptr, m, si, sj, sval, d_ph, d_aggv);
+    GTRY(hipMemset(d_left, 0, sizeof(unsigned long long)), "memset");
+    hipLaunchKernelGGL(k_count_value, dim3(g256), dim3(256), 0, nullptr, m, d_aggv, -1, d_left);
+    {
+        unsigned long long left = 0;
+        GTRY(hipMemcpy(&left, d_left, sizeof(left), hipMemcpyDeviceToHost), "read phase 2");
+        lap("phase 2");
+        if (left > 0 && dev_agg) {  // phase 3 over the left-over nodes' rows only
+            GTRY(aijhip_gamg::aggregate_phase3_device(m, si, sj, d_aggv, &na), "phase 3");
+        } else if (left > 0) {  // phase 3 (sequential) on the host
+            GTRY(hipMemcpy(agg, d_aggv, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
+            na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
+            GTRY(hipMemcpy(d_aggv, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 3");
+        }
+    }
+    lap("aggregate");
+level_done:
+#undef GTRY
+    job.join();
+    hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
+    hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left);
+    if (emax_its > 0) {
+        *emax = job.emax;
+        if (emax_err) *emax_err = job.e;
+    }
+    job.release();
+    if (rc) {
+        hipFree(dinv);
+        hipFree(d_aggv);
+        return rc;
+    }
+    *d_agg_out = d_aggv;
+    *dinv_out = dinv;
+    *na_out = na;
+    return AIJHIP_OK;
+}
+
+// The tentative prolongator (near-null space B normalised per aggregate:
+// Bc = the next level's B, p0) and the smoothed P = P0 + alpha D^-1 (A P0)
+// with local columns (agg ids). d_p0 (m) and d_Bc (na) are returned for the
+// caller to free; P owns its arrays.
+int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, const double *dinv, double alpha,
+                 int nsmooths, int n_cu, double **d_p0_out, double **d_Bc_out, DCsr &P, int *cols_used) {
+    const int32_t m = Av.m;
+    const unsigned g256 = blocks_for(m, 256);
+    int rc = AIJHIP_OK;
+    hipError_t e = hipSuccess;
+    double *d_p0 = nullptr, *d_Bc = nullptr;
+    int32_t *plen = nullptr;
+    DCsr P0, T;
+#define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto done; } } while (0)
+    GTRY(dalloc(&d_p0, m), "alloc");
+    GTRY(dalloc(&d_Bc, na), "alloc");
+    GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0), "tentative prolongator");
+    P0.m = m;
+    P0.n = na;
+    P0.nz = m;
+    GTRY(dalloc(&P0.ai, (int64_t)m + 1), "alloc");
+    hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, P0.ai);
+    P0.aj = d_agg;
+    P0.aa = d_p0;
+    if (nsmooths > 0) {
+        if ((rc = rowprod(Av, P0, T, n_cu, cols_used))) goto done;
+        P.m = m;
+        P.n = na;
+        GTRY(dalloc(&plen, m), "alloc");
+        hipLaunchKernelGGL(k_prolong_len, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, d_agg, plen);
+        GTRY(dalloc(&P.ai, (int64_t)m + 1), "alloc");
+        GTRY(scan_offsets(plen, m, P.ai, &P.nz), "scan");
+        GTRY(dalloc(&P.aj, P.nz + 2), "alloc");
+        GTRY(dalloc(&P.aa, P.nz + 2), "alloc");
+        hipLaunchKernelGGL(k_prolong_fill, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, T.aa, d_agg, d_p0,
+                           dinv, alpha, P.ai, P.aj, P.aa);
+        GTRY(hipGetLastError(), "prolongator");
+    } else {
+        P.m = m;
+        P.n = na;
+        P.nz = m;
+        GTRY(dalloc(&P.ai, (int64_t)m + 1), "alloc");
+        GTRY(dalloc(&P.aj, (int64_t)m + 2), "alloc");
+        GTRY(dalloc(&P.aa, (int64_t)m + 2), "alloc");
+        GTRY(hipMemcpy(P.ai, P0.ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToDevice), "copy");
+        GTRY(hipMemcpy(P.aj, d_agg, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
+        GTRY(hipMemcpy(P.aa, d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
+    }
+done:
+#undef GTRY
+    hipFree(P0.ai);
+    hipFree(plen);
+    T.release();
+    if (rc) {
+        P.release();
+        hipFree(d_p0);
+        hipFree(d_Bc);
+        return rc;
+    }
+    *d_p0_out = d_p0;
+    *d_Bc_out = d_Bc;
+    return AIJHIP_OK;
+}
+
+// The Galerkin operator A_c = P^T (A P) of local blocks (PT = P^T returned:
+// the MatRestrict operator); AP is released unless ap_out is given.
+int galerkin_level(const DCsr &Av, const DCsr &P, DCsr &PT, DCsr &Ac, int n_cu, int *cols_used, DCsr *ap_out) {
+    DCsr AP;
+    int rc = rowprod(Av, P, AP, n_cu, cols_used);
+    if (rc) return rc;
+    {
+        aijhip_mat pv;  // non-owning view for the transpose builder
+        pv.m = P.m;
+        pv.n = P.n;
+        pv.nz = P.nz;
+        pv.d_ai = P.ai;
+        pv.d_aj = P.aj;
+        pv.d_aa = P.aa;
+        PT.m = P.n;
+        PT.n = P.m;
+        PT.nz = P.nz;
+        const hipError_t e = aijhip::build_transpose(pv, &PT.ai, &PT.aj, &PT.aa, nullptr);
+        pv.d_ai = pv.d_aj = nullptr;
+        pv.d_aa = nullptr;
+        if (e != hipSuccess) {
+            AP.release();
+            return herr(e, "transpose");
+        }
+    }
+    if ((rc = rowprod(PT, AP, Ac, n_cu, cols_used))) {
+        AP.release();
+        PT.release();
+        return rc;
+    }
+    if (ap_out) *ap_out = AP;
+    else AP.release();
+    return AIJHIP_OK;
+}
+
+int make_level_handle(int device, DCsr &C, aijhip_mat **out) { return make_handle(device, C, out); }
+
+int rowprod_device(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
+    return rowprod(A, B, C, n_cu, cols_used);
+}
+
+hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0) {
+    return tentative(m, na, agg, B, Bc, p0);
+}
+
+int prolong_from_T(const DCsr &T, const int32_t *d_agg, const double *d_p0, const double *dinv, double alpha,
+                   DCsr &P) {
+    const int32_t m = T.m;
+    const unsigned g256 = blocks_for(m, 256);
+    int32_t *plen = nullptr;
+    hipError_t e;
+    P = DCsr();
+    P.m = m;
+    P.n = T.n;
+    if ((e = dalloc(&plen, m)) != hipSuccess) return herr(e, "alloc");
+    if (m > 0) hipLaunchKernelGGL(k_prolong_len, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, d_agg, plen);
+    if ((e = dalloc(&P.ai, (int64_t)m + 1)) != hipSuccess || (e = scan_offsets(plen, m, P.ai, &P.nz)) != hipSuccess ||
+        (e = dalloc(&P.aj, P.nz + 2)) != hipSuccess || (e = dalloc(&P.aa, P.nz + 2)) != hipSuccess) {
+        hipFree(plen);
+        P.release();
+        return herr(e, "prolongator");
+    }
+    if (m > 0)
+        hipLaunchKernelGGL(k_prolong_fill, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, T.aa, d_agg, d_p0, dinv,
+                           alpha, P.ai, P.aj, P.aa);
+    e = hipGetLastError();
+    hipFree(plen);
+    if (e != hipSuccess) {
+        P.release();
+        return herr(e, "prolongator");
+    }
+    return AIJHIP_OK;
+}
+
 int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<DeviceLevel> &levels,
                  std::vector<double> &B, bool *more, bool *overflow) {
     levels.clear();
@@ -1302,8 +1599,6 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     };
     levels.push_back(DeviceLevel{A0, nullptr, 0.0});
     const int n_cu = std::max(A0->n_cu, 1);
-    std::unique_lock<std::mutex> stage_lock;
-    Staging &stage = process_staging(stage_lock);
     int rc = AIJHIP_OK;
     hipError_t e = hipSuccess;
     // the near-null space of the current level, on the device (ones at the top)
@@ -1318,249 +1613,54 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
             *more = true;  // the host takes it from here
             break;
         }
-        const DCsr Av = view_of(A);
-        const unsigned g256 = blocks_for(m, 256);
-        // ---- diagonal, strength graph
-        double *d = nullptr, *dinv = nullptr, *sval = nullptr;
-        unsigned long long *cnt = nullptr, *off = nullptr;
-        unsigned int *pos = nullptr;
-        int32_t *tmp = nullptr, *si = nullptr, *sj = nullptr;
-        void *scan_tmp = nullptr;
-        size_t tb = 0;
-        int64_t nzs = 0;
-        int32_t *h_si = nullptr, *h_sj = nullptr, *agg = nullptr, *d_ph = nullptr;
-        int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
-        unsigned long long *d_left = nullptr;
-        int32_t na = 0;
-        bool dev_agg = false;  // phase 1 ran on the device (else the host pass)
-        int32_t sweep_rounds = 0;
-        // emax(D^-1 A) needs only A: its power iteration runs from a second
-        // host thread while this one stages S and aggregates on the CPU
-        EmaxJob job;
-#define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto level_done; } } while (0)
-        GTRY(dalloc(&d, m), "alloc");
-        GTRY(dalloc(&dinv, m), "alloc");
-        hipLaunchKernelGGL(k_diag_dinv, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d, dinv);
-        {
-            bool direct = false;  // S straight from A (sorted rows, symmetric strong pattern)
-            if ((rc = strength_direct(A, d, p.threshold, &si, &sj, &sval, &nzs, &direct))) goto level_done;
-            if (log)
-                std::fprintf(stderr, "gamg device level %zu strength graph: %s\n", levels.size() - 1,
-                             direct ? "direct (symmetric)" : "gathered (S u S^T)");
-            if (direct) goto strength_done;
-        }
-        GTRY(dalloc(&cnt, (int64_t)m + 1), "alloc");
-        GTRY(dalloc(&off, (int64_t)m + 1), "alloc");
-        GTRY(hipMemset(cnt, 0, sizeof(unsigned long long) * ((size_t)m + 1)), "memset");
-        hipLaunchKernelGGL(k_strong_count, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
-                           p.threshold, cnt);
-        GTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, m + 1), "scan");
-        GTRY(hipMalloc(&scan_tmp, std::max<size_t>(tb, 1)), "alloc");
-        GTRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, cnt, off, m + 1), "scan");
-        {
-            unsigned long long t = 0;
-            GTRY(hipMemcpy(&t, off + m, sizeof(t), hipMemcpyDeviceToHost), "read");
-            nzs = (int64_t)t;
-        }
-        GTRY(dalloc(&tmp, nzs), "alloc");
-        GTRY(dalloc(&pos, m), "alloc");
-        GTRY(hipMemset(pos, 0, sizeof(unsigned int) * (size_t)std::max(m, 1)), "memset");
-        hipLaunchKernelGGL(k_strong_fill, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
-                           p.threshold, off, pos, tmp);
-        if ((rc = strength_lists(A, cnt, off, tmp, nzs, n_cu, &si, &sj, &sval, &nzs))) goto level_done;
-    strength_done:
-        GTRY(hipGetLastError(), "strength kernels");
-        // ---- aggregation. Phase 1: the device sweep (gamg_aggregate.hip) on
-        // large levels with a sparse S, else -- or when the sweep would run too
-        // deep -- the sequential pass on the host from S staged in pinned
-        // memory; the same aggregates either way. Phase 2 on the device; phase
-        // 3 (sequential) over the nodes left.
-        lap("strength kernels");
-        if (p.nsmooths > 0) job.start(A, dinv, p.eig_its);
-        GTRY(dalloc(&d_ph, m), "alloc");
-        GTRY(dalloc(&d_aggv, m), "alloc");
-        GTRY(dalloc(&d_left, 1), "alloc");
-        {
-            int32_t max_rounds = 0;
-            if (device_phase1(m, nzs, &max_rounds)) {
-                GTRY(aijhip_gamg::aggregate_phase1_device(m, si, sj, max_rounds, d_ph, &na, &sweep_rounds, &dev_agg),
-                     "phase 1 sweep");
-                if (log)
-                    std::fprintf(stderr, "gamg device level %zu phase 1 sweep: %d rounds%s\n", levels.size() - 1,
-                                 sweep_rounds, dev_agg ? "" : " (too deep: host pass)");
-            }
-        }
-        if (!dev_agg) {
-            GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
-            lap("staging alloc");
-            h_si = stage.i32();
-            h_sj = h_si + m + 1;
-            agg = h_sj + nzs;
-            GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
-            lap("strength");
-            // S's columns come down in row chunks while the pass works through
-            // the rows already here (a node reads only its own row). (Phase 1
-            // measured on the MI355X host at 300^3 level 0: this int32 form
-            // 83 ms; bitmap or byte flags with or without early exits 87-121 ms.)
-            {
-                constexpr int kChunks = 16;
-                hipStream_t cs = nullptr;
-                hipEvent_t ev[kChunks] = {};
-                GTRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
-                int32_t r[kChunks + 1];
-                for (int c = 0; c <= kChunks; ++c) r[c] = (int32_t)((int64_t)m * c / kChunks);
-                for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
-                    const int64_t a = h_si[r[c]], b = h_si[r[c + 1]];
-                    if (b > a)
-                        e = hipMemcpyAsync(h_sj + a, sj + a, sizeof(int32_t) * (size_t)(b - a), hipMemcpyDeviceToHost,
-                                           cs);
-                    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[c], hipEventDisableTiming);
-                    if (e == hipSuccess) e = hipEventRecord(ev[c], cs);
-                }
-                std::fill(agg, agg + m, -1);
-                na = 0;
-                for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
-                    if ((e = hipEventSynchronize(ev[c])) == hipSuccess)
-                        na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_sj, agg, na);
-                }
-                (void)hipStreamSynchronize(cs);
-                for (hipEvent_t x : ev)
-                    if (x) (void)hipEventDestroy(x);
-                (void)hipStreamDestroy(cs);
-                GTRY(e, "read S");
-            }
-            GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
-        }
-        lap("phase 1");
-        hipLaunchKernelGGL(k_agg_phase2, dim3(g256), dim3(256), 0, nullptr, m, si, sj, sval, d_ph, d_aggv);
-        GTRY(hipMemset(d_left, 0, sizeof(unsigned long long)), "memset");
-        hipLaunchKernelGGL(k_count_value, dim3(g256), dim3(256), 0, nullptr, m, d_aggv, -1, d_left);
-        {
-            unsigned long long left = 0;
-            GTRY(hipMemcpy(&left, d_left, sizeof(left), hipMemcpyDeviceToHost), "read phase 2");
-            lap("phase 2");
-            if (left > 0 && dev_agg) {  // phase 3 over the left-over nodes' rows only
-                GTRY(aijhip_gamg::aggregate_phase3_device(m, si, sj, d_aggv, &na), "phase 3");
-            } else if (left > 0) {  // phase 3 (sequential) on the host
-                GTRY(hipMemcpy(agg, d_aggv, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
-                na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
-                GTRY(hipMemcpy(d_aggv, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 3");
-            }
-        }
-        lap("aggregate");
-    level_done:
-        job.join();
-        hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
-        hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left);
+        int32_t *d_agg = nullptr, na = 0;
+        double *dinv = nullptr, emax = 1.0;
+        hipError_t emax_err = hipSuccess;
+        rc = aggregate_level(A, p, &d_agg, &na, &dinv, p.nsmooths > 0 ? p.eig_its : 0, &emax, &emax_err,
+                             levels.size() - 1);
         if (rc || na >= m || na == 0) {  // an error, or no coarsening: this is the coarsest level
             hipFree(dinv);
-            hipFree(d_aggv);
-            job.release();
+            hipFree(d_agg);
             break;
         }
-#undef GTRY
-#define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto prolong_done; } } while (0)
-        // ---- emax(D^-1 A)
-        double emax = 1.0;
+        if (emax_err != hipSuccess) {
+            hipFree(dinv);
+            hipFree(d_agg);
+            rc = herr(emax_err, "power iteration");
+            break;
+        }
+        lap("emax");
         int cols_used = 0;
-        DCsr P0, T, P, AP, PT, Ac;
-        int32_t *d_agg = d_aggv, *plen = nullptr;
-        double *d_p0 = nullptr, *v = nullptr, *w = nullptr, *part = nullptr;
-        double *d_Bc = nullptr;
-        std::vector<double> h_part;
+        const DCsr Av = view_of(A);
+        DCsr P, PT, Ac;
+        double *d_p0 = nullptr, *d_Bc = nullptr;
         aijhip_mat *Ph = nullptr, *Ach = nullptr;
-        lap("free, vectors");
-        if (p.nsmooths > 0) {  // joined at level_done
-            v = job.v;
-            w = job.w;
-            part = job.part;
-            job.v = job.w = job.part = nullptr;  // freed at prolong_done
-            GTRY(job.e, "power iteration");
-            emax = job.emax;
-            lap("emax");
-        }
-        // ---- tentative prolongator: the near-null space normalised per aggregate
-        GTRY(dalloc(&d_p0, m), "alloc");
-        GTRY(dalloc(&d_Bc, na), "alloc");
-        GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0), "tentative prolongator");
-        lap("P0");
-        P0.m = m;
-        P0.n = na;
-        P0.nz = m;
-        GTRY(dalloc(&P0.ai, (int64_t)m + 1), "alloc");
-        hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, P0.ai);
-        P0.aj = d_agg;
-        P0.aa = d_p0;
-        // ---- smoothed prolongator
-        if (p.nsmooths > 0) {
-            if ((rc = rowprod(Av, P0, T, n_cu, &cols_used))) goto prolong_done;
-            P.m = m;
-            P.n = na;
-            GTRY(dalloc(&plen, m), "alloc");
-            hipLaunchKernelGGL(k_prolong_len, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, d_agg, plen);
-            GTRY(dalloc(&P.ai, (int64_t)m + 1), "alloc");
-            GTRY(scan_offsets(plen, m, P.ai, &P.nz), "scan");
-            GTRY(dalloc(&P.aj, P.nz + 2), "alloc");
-            GTRY(dalloc(&P.aa, P.nz + 2), "alloc");
-            hipLaunchKernelGGL(k_prolong_fill, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, T.aa, d_agg, d_p0,
-                               dinv, -p.smooth_scale / emax, P.ai, P.aj, P.aa);
-            GTRY(hipGetLastError(), "prolongator");
-            T.release();
-        } else {
-            P.m = m;
-            P.n = na;
-            P.nz = m;
-            GTRY(dalloc(&P.ai, (int64_t)m + 1), "alloc");
-            GTRY(dalloc(&P.aj, (int64_t)m + 2), "alloc");
-            GTRY(dalloc(&P.aa, (int64_t)m + 2), "alloc");
-            GTRY(hipMemcpy(P.ai, P0.ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToDevice), "copy");
-            GTRY(hipMemcpy(P.aj, d_agg, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
-            GTRY(hipMemcpy(P.aa, d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
-        }
+        // ---- tentative + smoothed prolongator
+        rc = smooth_level(Av, na, d_agg, d_B, dinv, -p.smooth_scale / emax, p.nsmooths, n_cu, &d_p0, &d_Bc, P,
+                          &cols_used);
         lap("prolongator");
         // ---- Galerkin operator A_c = P^T (A P)
-        if ((rc = rowprod(Av, P, AP, n_cu, &cols_used))) goto prolong_done;
-        lap("A*P");
-        {
-            aijhip_mat pv;  // non-owning view for the transpose builder
-            pv.m = P.m;
-            pv.n = P.n;
-            pv.nz = P.nz;
-            pv.d_ai = P.ai;
-            pv.d_aj = P.aj;
-            pv.d_aa = P.aa;
-            PT.m = P.n;
-            PT.n = P.m;
-            PT.nz = P.nz;
-            e = aijhip::build_transpose(pv, &PT.ai, &PT.aj, &PT.aa, nullptr);
-            pv.d_ai = pv.d_aj = nullptr;
-            pv.d_aa = nullptr;
-            GTRY(e, "transpose");
-        }
-        lap("P^T");
-        if ((rc = rowprod(PT, AP, Ac, n_cu, &cols_used))) goto prolong_done;
-        AP.release();
+        if (!rc) rc = galerkin_level(Av, P, PT, Ac, n_cu, &cols_used, nullptr);
         lap("P^T*(AP)");
         // ---- handles: P (with P^T attached for MatRestrict) and A_c
-        if ((rc = make_handle(A.device, P, &Ph))) goto prolong_done;
-        rc = aijhip::attach_transpose(Ph, PT.ai, PT.aj, PT.aa);
-        PT = DCsr();  // consumed by attach_transpose (freed on failure)
-        if (rc) goto prolong_done;
-        lap("handle P");
-        if ((rc = make_handle(A.device, Ac, &Ach))) goto prolong_done;
-        levels.back().P = Ph;
-        levels.back().emax = emax;
-        levels.back().product_cols = cols_used;
-        Ph = nullptr;
-        levels.push_back(DeviceLevel{Ach, nullptr, 0.0});
-        Ach = nullptr;
-        std::swap(d_B, d_Bc);
-        lap("handles");
-    prolong_done:
-#undef GTRY
-        hipFree(v); hipFree(w); hipFree(part); hipFree(dinv); hipFree(plen);
-        hipFree(P0.ai); hipFree(d_agg); hipFree(d_p0); hipFree(d_Bc);
-        T.release(); P.release(); AP.release(); PT.release(); Ac.release();
+        if (!rc) rc = make_handle(A.device, P, &Ph);
+        if (!rc) {
+            rc = aijhip::attach_transpose(Ph, PT.ai, PT.aj, PT.aa);
+            PT = DCsr();  // consumed by attach_transpose (freed on failure)
+        }
+        if (!rc) rc = make_handle(A.device, Ac, &Ach);
+        if (!rc) {
+            levels.back().P = Ph;
+            levels.back().emax = emax;
+            levels.back().product_cols = cols_used;
+            Ph = nullptr;
+            levels.push_back(DeviceLevel{Ach, nullptr, 0.0});
+            Ach = nullptr;
+            std::swap(d_B, d_Bc);
+            lap("handles");
+        }
+        hipFree(dinv); hipFree(d_agg); hipFree(d_p0); hipFree(d_Bc);
+        P.release(); PT.release(); Ac.release();
         if (Ph) aijhip_mat_destroy(Ph);
         if (Ach) aijhip_mat_destroy(Ach);
         if (rc == AIJHIP_ERR_STATE) {  // a row past the device accumulators

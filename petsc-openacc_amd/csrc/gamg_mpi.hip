@@ -1,0 +1,1146 @@
+// gamg_mpi.hip — PCGAMG across ranks: the smoothed-aggregation hierarchy of
+// a row-distributed operator and its V-cycle (aijhip_kspmpi with
+// AIJHIP_PC_GAMG at more than one rank).
+//
+// The reference runs CG + PETSc's agg GAMG on 1-16 MPI ranks
+// (/root/reference/runs/single-node-scaling.pbs:56-67 with
+// /root/reference/configs/PETSc_SolverOptions_GAMG.info:6-21): its
+// aggregation, prolongator smoothing and Galerkin products span the MPIAIJ
+// operator [ext]. The same structure here, MI355X-first:
+//
+//   aggregates   local to each rank (PETSc's agg GAMG keeps aggregates on
+//                their owner too): the single-GPU steps (gamg_device.hip
+//                aggregate_level) on the diagonal block A_d;
+//   emax         power iteration on the distributed D^-1 A (MatMult_MPIAIJ +
+//                all-reduced norms), from the single-GPU start vector taken at
+//                global indices;
+//   P            = P0 + alpha D^-1 (A P0) over the whole operator: A_ext = [A_d |
+//                A_o] times P0 extended by its ghost rows (aggregate id and
+//                value of each ghost fine node, exchanged through the halo);
+//   A_c          = P^T (A P): P's rows of the ghost fine nodes are exchanged
+//                (variable length), A P = A_ext P_ext and P^T (A P) are the
+//                device row-wise products over an extended coarse numbering
+//                (own coarse rows first, then the off-rank ones); the rows
+//                that belong to other ranks' coarse nodes are sent to their
+//                owners and added there;
+//   level l+1    C_d (own columns) and C_o (ghost columns) with a p2p halo
+//                plan; P = [P_d | P_o] and R = P^T = [P_d^T | R_o], R_o built
+//                from the ghost fine rows of P.
+// Bulk work (the large products, the transposes, the V-cycle) is on the
+// device; the host handles boundary-sized data (ghost rows, contributions).
+// The V-cycle is PETSc's multiplicative PCMG with the reference's options
+// (Richardson(1)+Jacobi down and up, P^T restriction, coarse Jacobi), every
+// SpMV a MatMult_MPIAIJ-shaped product with its halo on the operator's
+// exchange stream.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "gamg_device.h"
+#include "gamg_mpi.h"
+#include "mpi_internal.h"
+
+namespace {
+
+using aijhip_gamg::DCsr;
+using aijhip_gamg::dalloc;
+using aijhip_mpi::mfail;
+using aijhip_mpi::mhip;
+
+inline unsigned nblk(int64_t n, int t = 256) { return (unsigned)std::max<int64_t>(1, (n + t - 1) / t); }
+
+// ---------------------------------------------------------------- kernels
+__device__ __forceinline__ uint64_t mix64d(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// the single-GPU power iteration's start vector at global indices off + i
+__global__ void k_power_start_off(int32_t m, int64_t off, double *v) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    v[i] = 2.0 * ((double)(mix64d(0x5EEDULL + (uint64_t)(off + i + 1) * 0x9E3779B97F4A7C15ULL) >> 11) *
+                  (1.0 / 9007199254740992.0)) - 1.0;
+}
+
+constexpr int64_t kDotBlock = 256;
+
+__global__ void k_sumsq_blocks(int64_t n, const double *__restrict__ a, double *part) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i0 = q * kDotBlock;
+    if (i0 >= n) return;
+    const int64_t e = min(n, i0 + kDotBlock);
+    double s = 0.0;
+    for (int64_t i = i0; i < e; ++i) s += a[i] * a[i];
+    part[q] = s;
+}
+
+__global__ void k_scale_by(int32_t m, const double *__restrict__ d, double *w) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) w[i] = d[i] * w[i];
+}
+
+__global__ void k_divide(int32_t m, const double *w, double nw, double *v) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) v[i] = w[i] / nw;
+}
+
+__global__ void k_coarse_gid(int32_t m, int64_t off, const int32_t *__restrict__ agg, double *out) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[i] = (double)(off + agg[i]);
+}
+
+__global__ void k_iota32(int32_t n, int32_t *v) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i <= n) v[i] = i;
+}
+
+// rows of [A | B] (B's columns shifted by boff; B given by a full row pointer)
+__global__ void k_hcat_len(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ bi, int32_t *len) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) len[i] = (ai[i + 1] - ai[i]) + (bi ? bi[i + 1] - bi[i] : 0);
+}
+
+__global__ void k_hcat_fill(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                            const double *__restrict__ aa, const int32_t *__restrict__ bi,
+                            const int32_t *__restrict__ bj, const double *__restrict__ ba, int32_t boff,
+                            const int32_t *__restrict__ ci, int32_t *cj, double *ca) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t p = ci[i];
+    for (int32_t k = ai[i]; k < ai[i + 1]; ++k, ++p) {
+        cj[p] = aj[k];
+        ca[p] = aa[k];
+    }
+    if (bi)
+        for (int32_t k = bi[i]; k < bi[i + 1]; ++k, ++p) {
+            cj[p] = bj[k] + boff;
+            ca[p] = ba[k];
+        }
+}
+
+__global__ void k_add_offset(int32_t n, int32_t off, const int32_t *__restrict__ src, int32_t *dst) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] = src[i] + off;
+}
+
+__global__ void k_remap(int64_t n, const int32_t *__restrict__ table, int32_t *cols) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) cols[k] = table[cols[k]];
+}
+
+// rows [r0, r0 + n) of a CSR: lengths, then a compact copy
+__global__ void k_rows_len(int32_t n, const int32_t *__restrict__ rows, const int32_t *__restrict__ ai, int32_t *len) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) len[q] = ai[rows[q] + 1] - ai[rows[q]];
+}
+
+__global__ void k_rows_copy(int32_t n, const int32_t *__restrict__ rows, const int32_t *__restrict__ ai,
+                            const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                            const int32_t *__restrict__ off, int32_t *oj, double *oa) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    int32_t p = off[q];
+    for (int32_t k = ai[rows[q]]; k < ai[rows[q] + 1]; ++k, ++p) {
+        oj[p] = aj[k];
+        oa[p] = aa[k];
+    }
+}
+
+// C = A + B (rows sorted by column; a column in both: a + b)
+__global__ void k_add_len(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                          const int32_t *__restrict__ bi, const int32_t *__restrict__ bj, int32_t *len) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t p = ai[i], q = bi[i], n = 0;
+    const int32_t pe = ai[i + 1], qe = bi[i + 1];
+    while (p < pe || q < qe) {
+        if (q >= qe || (p < pe && aj[p] < bj[q])) ++p;
+        else if (p >= pe || bj[q] < aj[p]) ++q;
+        else { ++p; ++q; }
+        ++n;
+    }
+    len[i] = n;
+}
+
+__global__ void k_add_fill(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                           const double *__restrict__ aa, const int32_t *__restrict__ bi,
+                           const int32_t *__restrict__ bj, const double *__restrict__ ba,
+                           const int32_t *__restrict__ ci, int32_t *cj, double *ca) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t p = ai[i], q = bi[i], o = ci[i];
+    const int32_t pe = ai[i + 1], qe = bi[i + 1];
+    while (p < pe || q < qe) {
+        if (q >= qe || (p < pe && aj[p] < bj[q])) { cj[o] = aj[p]; ca[o] = aa[p]; ++p; }
+        else if (p >= pe || bj[q] < aj[p]) { cj[o] = bj[q]; ca[o] = ba[q]; ++q; }
+        else { cj[o] = aj[p]; ca[o] = aa[p] + ba[q]; ++p; ++q; }
+        ++o;
+    }
+}
+
+// split columns: < nloc -> D (same ids), >= nloc -> O (id - nloc)
+__global__ void k_split_len(int32_t m, const int32_t *__restrict__ ci, const int32_t *__restrict__ cj, int32_t nloc,
+                            int32_t *ld, int32_t *lo) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t d = 0;
+    for (int32_t k = ci[i]; k < ci[i + 1]; ++k) d += cj[k] < nloc;
+    ld[i] = d;
+    lo[i] = ci[i + 1] - ci[i] - d;
+}
+
+__global__ void k_split_fill(int32_t m, const int32_t *__restrict__ ci, const int32_t *__restrict__ cj,
+                             const double *__restrict__ ca, int32_t nloc, const int32_t *__restrict__ di,
+                             int32_t *dj, double *da, const int32_t *__restrict__ oi, int32_t *oj, double *oa) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t pd = di[i], po = oi[i];
+    for (int32_t k = ci[i]; k < ci[i + 1]; ++k) {
+        if (cj[k] < nloc) { dj[pd] = cj[k]; da[pd] = ca[k]; ++pd; }
+        else { oj[po] = cj[k] - nloc; oa[po] = ca[k]; ++po; }
+    }
+}
+
+// V-cycle vector passes (ksp.hip's, with CG's stop flag)
+__global__ __launch_bounds__(256) void k_mg_jacobi(int64_t n, const double *__restrict__ dinv,
+                                                   const double *__restrict__ b, double *x, const int *stop) {
+    if (stop && *stop) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        x[i] = dinv[i] * b[i];
+}
+
+__global__ __launch_bounds__(256) void k_mg_resid(int64_t n, const double *__restrict__ b, double *r,
+                                                  const int *stop) {
+    if (stop && *stop) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        r[i] = b[i] + (-1.0) * r[i];
+}
+
+__global__ __launch_bounds__(256) void k_mg_richardson(int64_t n, const double *__restrict__ dinv,
+                                                       const double *__restrict__ b, const double *__restrict__ ax,
+                                                       double *x, const int *stop) {
+    if (stop && *stop) return;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        x[i] = x[i] + 1.0 * (dinv[i] * (b[i] + (-1.0) * ax[i]));
+}
+
+// ---------------------------------------------------------------- host side
+int gerr(hipError_t e, const char *what) { return mhip(e, (std::string("distributed GAMG: ") + what).c_str()); }
+
+// Host CSR with 64-bit column ids (global or extended numbering).
+struct HCsr {
+    std::vector<int64_t> ai{0};
+    std::vector<int64_t> aj;
+    std::vector<double> aa;
+    int64_t rows() const { return (int64_t)ai.size() - 1; }
+};
+
+// exclusive prefix over ranks of one value per rank (every rank learns all)
+int all_values(aijhip_comm *C, int64_t v, std::vector<int64_t> &all) {
+    std::vector<std::vector<uint64_t>> out((size_t)C->nranks), in;
+    for (auto &o : out) o.assign(1, (uint64_t)v);
+    int rc = aijhip_mpi::comm_sendrecv(C, out, in);
+    if (rc) return rc;
+    all.assign((size_t)C->nranks, 0);
+    for (int p = 0; p < C->nranks; ++p) all[p] = in[p].empty() ? 0 : (int64_t)in[p][0];
+    return AIJHIP_OK;
+}
+
+int owner_of(const std::vector<int64_t> &starts, int64_t gid) {
+    return (int)(std::upper_bound(starts.begin(), starts.end(), gid) - starts.begin()) - 1;
+}
+
+// Rows `rows` of a device CSR down to the host (columns as stored).
+int download_rows(const int32_t *d_ai, const int32_t *d_aj, const double *d_aa, const std::vector<int32_t> &rows,
+                  std::vector<int32_t> &off, std::vector<int32_t> &cols, std::vector<double> &vals) {
+    const int32_t n = (int32_t)rows.size();
+    off.assign((size_t)n + 1, 0);
+    cols.clear();
+    vals.clear();
+    if (n == 0) return AIJHIP_OK;
+    int32_t *d_rows = nullptr, *d_len = nullptr, *d_off = nullptr, *d_oj = nullptr;
+    double *d_oa = nullptr;
+    hipError_t e;
+    int rc = AIJHIP_OK;
+    std::vector<int32_t> len((size_t)n);
+    if ((e = dalloc(&d_rows, n)) != hipSuccess || (e = dalloc(&d_len, n)) != hipSuccess ||
+        (e = hipMemcpy(d_rows, rows.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice)) != hipSuccess) {
+        rc = gerr(e, "row gather");
+        goto done;
+    }
+    hipLaunchKernelGGL(k_rows_len, dim3(nblk(n)), dim3(256), 0, nullptr, n, d_rows, d_ai, d_len);
+    if ((e = hipMemcpy(len.data(), d_len, sizeof(int32_t) * n, hipMemcpyDeviceToHost)) != hipSuccess) {
+        rc = gerr(e, "row gather");
+        goto done;
+    }
+    for (int32_t q = 0; q < n; ++q) off[q + 1] = off[q] + len[q];
+    cols.resize((size_t)off[n]);
+    vals.resize((size_t)off[n]);
+    if ((e = dalloc(&d_off, (int64_t)n + 1)) != hipSuccess || (e = dalloc(&d_oj, off[n])) != hipSuccess ||
+        (e = dalloc(&d_oa, off[n])) != hipSuccess ||
+        (e = hipMemcpy(d_off, off.data(), sizeof(int32_t) * ((size_t)n + 1), hipMemcpyHostToDevice)) != hipSuccess) {
+        rc = gerr(e, "row gather");
+        goto done;
+    }
+    hipLaunchKernelGGL(k_rows_copy, dim3(nblk(n)), dim3(256), 0, nullptr, n, d_rows, d_ai, d_aj, d_aa, d_off, d_oj,
+                       d_oa);
+    if (off[n] > 0 &&
+        ((e = hipMemcpy(cols.data(), d_oj, sizeof(int32_t) * (size_t)off[n], hipMemcpyDeviceToHost)) != hipSuccess ||
+         (e = hipMemcpy(vals.data(), d_oa, sizeof(double) * (size_t)off[n], hipMemcpyDeviceToHost)) != hipSuccess))
+        rc = gerr(e, "row gather");
+done:
+    hipFree(d_rows); hipFree(d_len); hipFree(d_off); hipFree(d_oj); hipFree(d_oa);
+    return rc;
+}
+
+// Host CSR (int32 columns) -> device DCsr with the +2 tail pad.
+int upload_csr(int32_t m, int32_t n, const std::vector<int32_t> &ai, const std::vector<int32_t> &aj,
+               const std::vector<double> &aa, DCsr &D) {
+    D = DCsr();
+    D.m = m;
+    D.n = n;
+    D.nz = ai.empty() ? 0 : ai.back();
+    hipError_t e;
+    if ((e = dalloc(&D.ai, (int64_t)m + 1)) != hipSuccess || (e = dalloc(&D.aj, D.nz + 2)) != hipSuccess ||
+        (e = dalloc(&D.aa, D.nz + 2)) != hipSuccess ||
+        (e = hipMemcpy(D.ai, ai.data(), sizeof(int32_t) * ((size_t)m + 1), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(D.aj, 0, sizeof(int32_t) * (size_t)(D.nz + 2))) != hipSuccess ||
+        (e = hipMemset(D.aa, 0, sizeof(double) * (size_t)(D.nz + 2))) != hipSuccess ||
+        (D.nz > 0 &&
+         ((e = hipMemcpy(D.aj, aj.data(), sizeof(int32_t) * (size_t)D.nz, hipMemcpyHostToDevice)) != hipSuccess ||
+          (e = hipMemcpy(D.aa, aa.data(), sizeof(double) * (size_t)D.nz, hipMemcpyHostToDevice)) != hipSuccess))) {
+        D.release();
+        return gerr(e, "upload");
+    }
+    return AIJHIP_OK;
+}
+
+// exclusive scan of device int32 lengths into device offsets (host round trip)
+int scan_lengths(const int32_t *d_len, int32_t m, int32_t **d_off, int64_t *total) {
+    std::vector<int32_t> len((size_t)m), off((size_t)m + 1, 0);
+    hipError_t e;
+    if (m > 0 && (e = hipMemcpy(len.data(), d_len, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost)) != hipSuccess)
+        return gerr(e, "lengths");
+    int64_t t = 0;
+    for (int32_t i = 0; i < m; ++i) {
+        off[i] = (int32_t)t;
+        t += len[i];
+    }
+    if (t > INT32_MAX) return mfail(AIJHIP_ERR_STATE, "distributed GAMG: a local operator past int32 entries");
+    off[m] = (int32_t)t;
+    *total = t;
+    if ((e = dalloc(d_off, (int64_t)m + 1)) != hipSuccess ||
+        (e = hipMemcpy(*d_off, off.data(), sizeof(int32_t) * ((size_t)m + 1), hipMemcpyHostToDevice)) != hipSuccess)
+        return gerr(e, "offsets");
+    return AIJHIP_OK;
+}
+
+// C = [A | B] (B: full row pointer bi, columns shifted by boff); bi may be null
+int hcat(const DCsr &A, const int32_t *bi, const int32_t *bj, const double *ba, int32_t boff, int32_t ncols,
+         DCsr &C) {
+    C = DCsr();
+    C.m = A.m;
+    C.n = ncols;
+    int32_t *len = nullptr;
+    hipError_t e;
+    if ((e = dalloc(&len, A.m)) != hipSuccess) return gerr(e, "alloc");
+    if (A.m > 0) hipLaunchKernelGGL(k_hcat_len, dim3(nblk(A.m)), dim3(256), 0, nullptr, A.m, A.ai, bi, len);
+    int rc = scan_lengths(len, A.m, &C.ai, &C.nz);
+    hipFree(len);
+    if (rc) return rc;
+    if ((e = dalloc(&C.aj, C.nz + 2)) != hipSuccess || (e = dalloc(&C.aa, C.nz + 2)) != hipSuccess) {
+        C.release();
+        return gerr(e, "alloc");
+    }
+    if (A.m > 0)
+        hipLaunchKernelGGL(k_hcat_fill, dim3(nblk(A.m)), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa, bi, bj, ba,
+                           boff, C.ai, C.aj, C.aa);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        C.release();
+        return gerr(e, "concatenate");
+    }
+    return AIJHIP_OK;
+}
+
+// C = A + B (same shape, sorted rows)
+int csr_add(const DCsr &A, const DCsr &B, DCsr &C) {
+    C = DCsr();
+    C.m = A.m;
+    C.n = A.n;
+    int32_t *len = nullptr;
+    hipError_t e;
+    if ((e = dalloc(&len, A.m)) != hipSuccess) return gerr(e, "alloc");
+    if (A.m > 0) hipLaunchKernelGGL(k_add_len, dim3(nblk(A.m)), dim3(256), 0, nullptr, A.m, A.ai, A.aj, B.ai, B.aj, len);
+    int rc = scan_lengths(len, A.m, &C.ai, &C.nz);
+    hipFree(len);
+    if (rc) return rc;
+    if ((e = dalloc(&C.aj, C.nz + 2)) != hipSuccess || (e = dalloc(&C.aa, C.nz + 2)) != hipSuccess) {
+        C.release();
+        return gerr(e, "alloc");
+    }
+    if (A.m > 0)
+        hipLaunchKernelGGL(k_add_fill, dim3(nblk(A.m)), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa, B.ai, B.aj, B.aa,
+                           C.ai, C.aj, C.aa);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        C.release();
+        return gerr(e, "sum");
+    }
+    return AIJHIP_OK;
+}
+
+// D = columns < nloc, O = the others shifted by -nloc (nghost columns)
+int csr_split(const DCsr &C, int32_t nloc, int32_t nghost, DCsr &D, DCsr &O) {
+    D = DCsr();
+    O = DCsr();
+    D.m = O.m = C.m;
+    D.n = nloc;
+    O.n = nghost;
+    int32_t *ld = nullptr, *lo = nullptr;
+    hipError_t e;
+    if ((e = dalloc(&ld, C.m)) != hipSuccess || (e = dalloc(&lo, C.m)) != hipSuccess) {
+        hipFree(ld);
+        return gerr(e, "alloc");
+    }
+    if (C.m > 0)
+        hipLaunchKernelGGL(k_split_len, dim3(nblk(C.m)), dim3(256), 0, nullptr, C.m, C.ai, C.aj, nloc, ld, lo);
+    int rc = scan_lengths(ld, C.m, &D.ai, &D.nz);
+    if (!rc) rc = scan_lengths(lo, C.m, &O.ai, &O.nz);
+    hipFree(ld);
+    hipFree(lo);
+    if (rc) {
+        D.release();
+        O.release();
+        return rc;
+    }
+    if ((e = dalloc(&D.aj, D.nz + 2)) != hipSuccess || (e = dalloc(&D.aa, D.nz + 2)) != hipSuccess ||
+        (e = dalloc(&O.aj, O.nz + 2)) != hipSuccess || (e = dalloc(&O.aa, O.nz + 2)) != hipSuccess) {
+        D.release();
+        O.release();
+        return gerr(e, "alloc");
+    }
+    if (C.m > 0)
+        hipLaunchKernelGGL(k_split_fill, dim3(nblk(C.m)), dim3(256), 0, nullptr, C.m, C.ai, C.aj, C.aa, nloc, D.ai,
+                           D.aj, D.aa, O.ai, O.aj, O.aa);
+    if ((e = hipGetLastError()) != hipSuccess) {
+        D.release();
+        O.release();
+        return gerr(e, "split");
+    }
+    return AIJHIP_OK;
+}
+
+int remap_cols(DCsr &C, const std::vector<int32_t> &table) {
+    if (C.nz == 0) return AIJHIP_OK;
+    int32_t *d_t = nullptr;
+    hipError_t e;
+    if ((e = dalloc(&d_t, (int64_t)table.size())) != hipSuccess ||
+        (e = hipMemcpy(d_t, table.data(), sizeof(int32_t) * table.size(), hipMemcpyHostToDevice)) != hipSuccess) {
+        hipFree(d_t);
+        return gerr(e, "column map");
+    }
+    hipLaunchKernelGGL(k_remap, dim3(nblk(C.nz)), dim3(256), 0, nullptr, C.nz, d_t, C.aj);
+    e = hipGetLastError();
+    hipFree(d_t);
+    return e == hipSuccess ? AIJHIP_OK : gerr(e, "column map");
+}
+
+// copy a handle's CSR into a DCsr view (not owned)
+DCsr view(const aijhip_mat &A) {
+    DCsr v;
+    v.m = A.m;
+    v.n = A.n;
+    v.nz = A.nz;
+    v.ai = A.d_ai;
+    v.aj = A.d_aj;
+    v.aa = A.d_aa;
+    return v;
+}
+
+// A handle's CSR on the host with a full row pointer (compressed-row form expanded)
+int host_full_rows(const aijhip_mat &A, std::vector<int32_t> &ai, std::vector<int32_t> &aj,
+                   std::vector<double> &aa) {
+    ai.assign((size_t)A.m + 1, 0);
+    aj.resize((size_t)A.nz);
+    aa.resize((size_t)A.nz);
+    hipError_t e;
+    if (A.nz > 0 && ((e = hipMemcpy(aj.data(), A.d_aj, sizeof(int32_t) * (size_t)A.nz, hipMemcpyDeviceToHost)) !=
+                         hipSuccess ||
+                     (e = hipMemcpy(aa.data(), A.d_aa, sizeof(double) * (size_t)A.nz, hipMemcpyDeviceToHost)) !=
+                         hipSuccess))
+        return gerr(e, "read block");
+    if (!A.compressed) {
+        if ((e = hipMemcpy(ai.data(), A.d_ai, sizeof(int32_t) * ai.size(), hipMemcpyDeviceToHost)) != hipSuccess)
+            return gerr(e, "read block");
+        return AIJHIP_OK;
+    }
+    std::vector<int32_t> cai((size_t)A.n_crow + 1), ridx((size_t)A.n_crow);
+    if ((e = hipMemcpy(cai.data(), A.d_cai, sizeof(int32_t) * cai.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (A.n_crow > 0 &&
+         (e = hipMemcpy(ridx.data(), A.d_ridx, sizeof(int32_t) * ridx.size(), hipMemcpyDeviceToHost)) != hipSuccess))
+        return gerr(e, "read block");
+    std::vector<int32_t> len((size_t)A.m, 0);
+    for (int32_t q = 0; q < A.n_crow; ++q) len[ridx[q]] = cai[q + 1] - cai[q];
+    for (int32_t i = 0; i < A.m; ++i) ai[i + 1] = ai[i] + len[i];
+    return AIJHIP_OK;
+}
+
+// Ghost values of a device vector through an operator's halo (host copy).
+int halo_values(aijhip_mpiaij *M, const double *d_x, std::vector<double> &out) {
+    out.assign((size_t)M->n_ghost, 0.0);
+    int rc = aijhip_mpi::halo_post(M, d_x, nullptr);
+    if (!rc) rc = aijhip_mpi::halo_finish(M, nullptr);
+    if (rc) return rc;
+    hipError_t e;
+    if ((e = hipStreamSynchronize(nullptr)) != hipSuccess ||
+        (M->n_ghost > 0 && (e = hipMemcpy(out.data(), M->d_ghost, sizeof(double) * out.size(),
+                                          hipMemcpyDeviceToHost)) != hipSuccess))
+        return gerr(e, "ghost values");
+    return AIJHIP_OK;
+}
+
+// sqrt of the sum over all ranks of the 256-blocked local sums of squares
+int global_norm(aijhip_comm *C, const double *d_v, int32_t m, double *d_part, double *out) {
+    const int64_t nb = (m + kDotBlock - 1) / kDotBlock;
+    std::vector<double> h((size_t)nb);
+    hipError_t e;
+    if (nb > 0) {
+        hipLaunchKernelGGL(k_sumsq_blocks, dim3(nblk(nb, 64)), dim3(64), 0, nullptr, (int64_t)m, d_v, d_part);
+        if ((e = hipMemcpy(h.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost)) != hipSuccess)
+            return gerr(e, "norm");
+    }
+    double s = 0.0;
+    for (int64_t q = 0; q < nb; ++q) s += h[q];
+    int rc = aijhip_mpi::comm_allreduce_host(C, &s, 1);
+    if (rc) return rc;
+    *out = std::sqrt(s);
+    return AIJHIP_OK;
+}
+
+}  // namespace
+
+namespace aijhip_gamg_mpi {
+
+void Hierarchy::destroy() {
+    for (size_t l = 0; l < lv.size(); ++l) {
+        Level &L = lv[l];
+        if (L.op && l > 0) aijhip_mpiaij_destroy(L.op);
+        if (l > 0) {
+            aijhip_mat_destroy(L.Ad);
+            aijhip_mat_destroy(L.Ao);
+        }
+        aijhip_mat_destroy(L.Pd);
+        aijhip_mat_destroy(L.Po);
+        aijhip_mat_destroy(L.Ro);
+        hipFree(L.dinv); hipFree(L.b); hipFree(L.x); hipFree(L.r);
+    }
+    lv.clear();
+}
+
+// The p2p halo plan of a level from its sorted ghost list: requests to the
+// owners (ghost order = owner order), send lists from what others request.
+static int make_operator(aijhip_comm *C, aijhip_mat *Ad, aijhip_mat *Ao, const std::vector<int64_t> &ghosts,
+                         const std::vector<int64_t> &starts, aijhip_mpiaij **out) {
+    const int P = C->nranks;
+    std::vector<std::vector<uint64_t>> req((size_t)P), got;
+    std::vector<int32_t> recv_peer;
+    std::vector<int64_t> recv_off{0};
+    for (size_t s = 0; s < ghosts.size();) {
+        const int q = owner_of(starts, ghosts[s]);
+        size_t e = s;
+        while (e < ghosts.size() && owner_of(starts, ghosts[e]) == q) {
+            req[q].push_back((uint64_t)(ghosts[e] - starts[q]));
+            ++e;
+        }
+        recv_peer.push_back(q);
+        recv_off.push_back((int64_t)e);
+        s = e;
+    }
+    int rc = aijhip_mpi::comm_sendrecv(C, req, got);
+    if (rc) return rc;
+    std::vector<int32_t> send_peer, send_rows;
+    std::vector<int64_t> send_off{0};
+    for (int q = 0; q < P; ++q) {
+        if (q == C->rank || got[q].empty()) continue;
+        send_peer.push_back(q);
+        for (uint64_t r : got[q]) send_rows.push_back((int32_t)r);
+        send_off.push_back((int64_t)send_rows.size());
+    }
+    return aijhip_mpiaij_create(C, Ad, Ao, AIJHIP_HALO_P2P, (int32_t)send_peer.size(), send_peer.data(),
+                                send_off.data(), send_rows.empty() ? nullptr : send_rows.data(),
+                                (int32_t)recv_peer.size(), recv_peer.data(), recv_off.data(), 0, out);
+}
+
+int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
+    aijhip::Range range("PCSetUp_GAMG (MPIAIJ)");
+    H.destroy();
+    aijhip_comm *C = M0->comm;
+    if (M0->halo != AIJHIP_HALO_P2P)
+        return mfail(AIJHIP_ERR_ARG, "distributed GAMG: the operator needs the p2p halo (AIJHIP_HALO_P2P)");
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](size_t l, const char *what) {
+        if (!log) return;
+        (void)hipDeviceSynchronize();
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[rank %d] gamg mpi level %zu %-22s %8.3f s\n", C->rank, l, what,
+                     std::chrono::duration<double>(t - t0).count());
+        t0 = t;
+    };
+    const int P = C->nranks, me = C->rank;
+    const int n_cu = std::max(M0->Ad->n_cu, 1);
+    hipError_t e;
+    int rc = AIJHIP_OK;
+    // ---- level 0: the caller's operator and its ghost global ids
+    H.lv.emplace_back();
+    {
+        Level &L0 = H.lv[0];
+        L0.Ad = M0->Ad;
+        L0.Ao = M0->Ao;
+        L0.op = M0;
+        L0.m = M0->mloc;
+        std::vector<int64_t> all;
+        if ((rc = all_values(C, L0.m, all))) return rc;
+        L0.starts.assign((size_t)P + 1, 0);
+        for (int q = 0; q < P; ++q) L0.starts[q + 1] = L0.starts[q] + all[q];
+        L0.rstart = L0.starts[me];
+        double *gid = nullptr;
+        if ((e = dalloc(&gid, L0.m)) != hipSuccess) return gerr(e, "alloc");
+        std::vector<int32_t> agg_id;  // gid = rstart + i
+        int32_t *iota = nullptr;
+        if ((e = dalloc(&iota, (int64_t)L0.m + 1)) != hipSuccess) {
+            hipFree(gid);
+            return gerr(e, "alloc");
+        }
+        hipLaunchKernelGGL(k_iota32, dim3(nblk((int64_t)L0.m + 1)), dim3(256), 0, nullptr, L0.m, iota);
+        if (L0.m > 0) hipLaunchKernelGGL(k_coarse_gid, dim3(nblk(L0.m)), dim3(256), 0, nullptr, L0.m, L0.rstart, iota, gid);
+        std::vector<double> g;
+        rc = halo_values(M0, gid, g);
+        hipFree(gid);
+        hipFree(iota);
+        if (rc) return rc;
+        L0.ghost_gid.resize(g.size());
+        for (size_t s = 0; s < g.size(); ++s) L0.ghost_gid[s] = (int64_t)g[s];
+    }
+    // the near-null space of the current level (ones at the top)
+    double *d_B = nullptr;
+    if ((e = dalloc(&d_B, H.lv[0].m)) != hipSuccess) return gerr(e, "alloc");
+    {
+        std::vector<double> ones((size_t)std::max(H.lv[0].m, 1), 1.0);
+        if ((e = hipMemcpy(d_B, ones.data(), sizeof(double) * (size_t)H.lv[0].m, hipMemcpyHostToDevice)) != hipSuccess) {
+            hipFree(d_B);
+            return gerr(e, "near-null space");
+        }
+    }
+    for (;;) {
+        const size_t l = H.lv.size() - 1;
+        Level &L = H.lv[l];
+        const int32_t m = L.m;
+        const int64_t M = L.starts[P];
+        if ((int32_t)H.lv.size() >= p.max_levels || M <= p.coarse_eq_limit) break;
+        // ---- local aggregates
+        int32_t *d_agg = nullptr, na = 0;
+        double *dinv = nullptr;
+        if ((rc = aijhip_gamg::aggregate_level(*L.Ad, p, &d_agg, &na, &dinv, 0, nullptr, nullptr, l))) break;
+        std::vector<int64_t> na_all;
+        if ((rc = all_values(C, na, na_all))) {
+            hipFree(d_agg); hipFree(dinv);
+            break;
+        }
+        int64_t NA = 0, cstart = 0;
+        std::vector<int64_t> cstarts((size_t)P + 1, 0);
+        for (int q = 0; q < P; ++q) cstarts[q + 1] = cstarts[q] + na_all[q];
+        NA = cstarts[P];
+        cstart = cstarts[me];
+        lap(l, "aggregates");
+        if (NA == 0 || NA >= M) {  // no coarsening anywhere: this is the coarsest level
+            hipFree(d_agg); hipFree(dinv);
+            break;
+        }
+        // ---- emax(D^-1 A) of the distributed operator
+        double emax = 1.0;
+        if (p.nsmooths > 0) {
+            double *v = nullptr, *w = nullptr, *part = nullptr;
+            if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
+                (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
+                rc = gerr(e, "alloc");
+            double nv = 0.0;
+            if (!rc) {
+                if (m > 0) hipLaunchKernelGGL(k_power_start_off, dim3(nblk(m)), dim3(256), 0, nullptr, m, L.rstart, v);
+                rc = global_norm(C, v, m, part, &nv);
+            }
+            if (!rc && m > 0) hipLaunchKernelGGL(k_divide, dim3(nblk(m)), dim3(256), 0, nullptr, m, v, nv, v);
+            for (int it = 0; !rc && it < p.eig_its; ++it) {
+                if ((rc = aijhip_mpi::mpiaij_apply(L.op, v, w, nullptr, nullptr, nullptr, nullptr, false))) break;
+                if (m > 0) hipLaunchKernelGGL(k_scale_by, dim3(nblk(m)), dim3(256), 0, nullptr, m, dinv, w);
+                double nw = 0.0;
+                if ((rc = global_norm(C, w, m, part, &nw))) break;
+                if (!(nw > 0.0)) break;
+                emax = nw;
+                if (m > 0) hipLaunchKernelGGL(k_divide, dim3(nblk(m)), dim3(256), 0, nullptr, m, w, nw, v);
+            }
+            hipFree(v); hipFree(w); hipFree(part);
+            if (rc) {
+                hipFree(d_agg); hipFree(dinv);
+                break;
+            }
+        }
+        lap(l, "emax");
+        const double alpha = -p.smooth_scale / emax;
+        // ---- tentative prolongator and its ghost rows (aggregate gid, value)
+        double *d_p0 = nullptr, *d_Bc = nullptr, *d_v = nullptr;
+        std::vector<double> g_agg, g_p0;
+        if ((e = dalloc(&d_p0, m)) != hipSuccess || (e = dalloc(&d_Bc, na)) != hipSuccess ||
+            (e = dalloc(&d_v, m)) != hipSuccess || (e = aijhip_gamg::tentative_device(m, na, d_agg, d_B, d_Bc, d_p0)) !=
+                                                       hipSuccess)
+            rc = gerr(e, "tentative prolongator");
+        if (!rc) {
+            if (m > 0) hipLaunchKernelGGL(k_coarse_gid, dim3(nblk(m)), dim3(256), 0, nullptr, m, cstart, d_agg, d_v);
+            rc = halo_values(L.op, d_v, g_agg);
+        }
+        if (!rc) rc = halo_values(L.op, d_p0, g_p0);
+        hipFree(d_v);
+        const int32_t ng = (int32_t)L.ghost_gid.size();
+        // extended coarse numbering E1: own aggregates, then the off-rank ones of the ghosts (sorted)
+        std::vector<int64_t> e1_off;
+        for (int32_t s = 0; s < ng; ++s) e1_off.push_back((int64_t)g_agg[s]);
+        std::sort(e1_off.begin(), e1_off.end());
+        e1_off.erase(std::unique(e1_off.begin(), e1_off.end()), e1_off.end());
+        auto e1_id = [&](int64_t gidc) -> int32_t {
+            if (gidc >= cstart && gidc < cstart + na) return (int32_t)(gidc - cstart);
+            return na + (int32_t)(std::lower_bound(e1_off.begin(), e1_off.end(), gidc) - e1_off.begin());
+        };
+        // A_ext = [A_d | A_o] (ghost columns after the local ones)
+        DCsr Aext, P0ext, T, Plocal;
+        std::vector<int32_t> oai, oaj;
+        std::vector<double> oaa;
+        bool aext_owned = false;
+        if (!rc && L.Ao && ng > 0) {
+            rc = host_full_rows(*L.Ao, oai, oaj, oaa);
+            DCsr Ofull;
+            if (!rc) rc = upload_csr(m, ng, oai, oaj, oaa, Ofull);
+            if (!rc) rc = hcat(view(*L.Ad), Ofull.ai, Ofull.aj, Ofull.aa, m, m + ng, Aext);
+            Ofull.release();
+            aext_owned = true;
+        } else if (!rc) {
+            Aext = view(*L.Ad);
+            Aext.n = m + ng;
+        }
+        lap(l, "A_ext");
+        // P0 extended by the ghost rows: rows m + ng, columns E1
+        if (!rc) {
+            std::vector<int32_t> gcol((size_t)ng);
+            for (int32_t s = 0; s < ng; ++s) gcol[s] = e1_id((int64_t)g_agg[s]);
+            P0ext.m = m + ng;
+            P0ext.n = na + (int32_t)e1_off.size();
+            P0ext.nz = m + ng;
+            if ((e = dalloc(&P0ext.ai, (int64_t)m + ng + 1)) != hipSuccess ||
+                (e = dalloc(&P0ext.aj, (int64_t)m + ng + 2)) != hipSuccess ||
+                (e = dalloc(&P0ext.aa, (int64_t)m + ng + 2)) != hipSuccess ||
+                (e = hipMemset(P0ext.aj, 0, sizeof(int32_t) * (size_t)(m + ng + 2))) != hipSuccess ||
+                (e = hipMemset(P0ext.aa, 0, sizeof(double) * (size_t)(m + ng + 2))) != hipSuccess ||
+                (m > 0 && ((e = hipMemcpy(P0ext.aj, d_agg, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToDevice)) !=
+                               hipSuccess ||
+                           (e = hipMemcpy(P0ext.aa, d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice)) !=
+                               hipSuccess)) ||
+                (ng > 0 && ((e = hipMemcpy(P0ext.aj + m, gcol.data(), sizeof(int32_t) * (size_t)ng,
+                                           hipMemcpyHostToDevice)) != hipSuccess ||
+                            (e = hipMemcpy(P0ext.aa + m, g_p0.data(), sizeof(double) * (size_t)ng,
+                                           hipMemcpyHostToDevice)) != hipSuccess)))
+                rc = gerr(e, "P0 extended");
+            if (!rc) hipLaunchKernelGGL(k_iota32, dim3(nblk((int64_t)m + ng + 1)), dim3(256), 0, nullptr, m + ng,
+                                        P0ext.ai);
+        }
+        // ---- P = P0 + alpha D^-1 (A P0) on the local rows (columns E1)
+        int cols_used = 0;
+        if (!rc) {
+            if (p.nsmooths > 0) {
+                rc = aijhip_gamg::rowprod_device(Aext, P0ext, T, n_cu, &cols_used);
+                if (!rc) rc = aijhip_gamg::prolong_from_T(T, d_agg, d_p0, dinv, alpha, Plocal);
+                T.release();
+            } else {  // P = P0 (local rows)
+                std::vector<int32_t> ai((size_t)m + 1), aj((size_t)m);
+                std::vector<double> aa((size_t)m);
+                std::iota(ai.begin(), ai.end(), 0);
+                if ((m > 0 && ((e = hipMemcpy(aj.data(), d_agg, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost)) !=
+                                   hipSuccess ||
+                               (e = hipMemcpy(aa.data(), d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost)) !=
+                                   hipSuccess)))
+                    rc = gerr(e, "P0");
+                if (!rc) rc = upload_csr(m, P0ext.n, ai, aj, aa, Plocal);
+            }
+        }
+        P0ext.release();
+        lap(l, "prolongator");
+        // ---- P's rows of the ghost fine nodes (global coarse ids): each
+        // rank sends the rows its neighbours hold as ghosts
+        auto e1_gid = [&](int32_t c) -> int64_t { return c < na ? cstart + c : e1_off[c - na]; };
+        std::vector<std::vector<int64_t>> gcols((size_t)ng);  // ghost row s: global coarse ids
+        std::vector<std::vector<double>> gvals((size_t)ng);
+        if (!rc) {
+            std::vector<std::vector<uint64_t>> out((size_t)P), in;
+            for (size_t q = 0; q < L.op->send_peer.size() && !rc; ++q) {
+                const int64_t a = L.op->send_off[q], b = L.op->send_off[q + 1];
+                std::vector<int32_t> rows(L.op->h_send_rows.begin() + a, L.op->h_send_rows.begin() + b), off, cols;
+                std::vector<double> vals;
+                if ((rc = download_rows(Plocal.ai, Plocal.aj, Plocal.aa, rows, off, cols, vals))) break;
+                auto &o = out[L.op->send_peer[q]];
+                for (size_t r = 0; r < rows.size(); ++r) {
+                    o.push_back((uint64_t)(off[r + 1] - off[r]));
+                    for (int32_t k = off[r]; k < off[r + 1]; ++k) {
+                        o.push_back((uint64_t)e1_gid(cols[k]));
+                        uint64_t bitsv;
+                        std::memcpy(&bitsv, &vals[k], 8);
+                        o.push_back(bitsv);
+                    }
+                }
+            }
+            if (!rc) rc = aijhip_mpi::comm_sendrecv(C, out, in);
+            for (size_t pp = 0; !rc && pp < L.op->recv_peer.size(); ++pp) {
+                const auto &w = in[L.op->recv_peer[pp]];
+                size_t k = 0;
+                for (int64_t s = L.op->recv_off[pp]; s < L.op->recv_off[pp + 1]; ++s) {
+                    if (k >= w.size()) {
+                        rc = mfail(AIJHIP_ERR_COMM, "distributed GAMG: short ghost-row message");
+                        break;
+                    }
+                    const uint64_t len = w[k++];
+                    for (uint64_t t = 0; t < len; ++t) {
+                        gcols[s].push_back((int64_t)w[k++]);
+                        double v;
+                        std::memcpy(&v, &w[k++], 8);
+                        gvals[s].push_back(v);
+                    }
+                }
+            }
+        }
+        lap(l, "ghost rows of P");
+        // extended coarse numbering E2: own, then every off-rank id of P's local and ghost rows
+        std::vector<int64_t> e2_off(e1_off);
+        for (int32_t s = 0; s < ng; ++s)
+            for (int64_t c : gcols[s])
+                if (c < cstart || c >= cstart + na) e2_off.push_back(c);
+        std::sort(e2_off.begin(), e2_off.end());
+        e2_off.erase(std::unique(e2_off.begin(), e2_off.end()), e2_off.end());
+        const int32_t n2 = na + (int32_t)e2_off.size();
+        auto e2_id = [&](int64_t gidc) -> int32_t {
+            if (gidc >= cstart && gidc < cstart + na) return (int32_t)(gidc - cstart);
+            return na + (int32_t)(std::lower_bound(e2_off.begin(), e2_off.end(), gidc) - e2_off.begin());
+        };
+        // P_local: E1 -> E2; P_ext2 = [P_local; P_ghost]
+        DCsr Pext, AP, PT, Cext;
+        if (!rc) {
+            std::vector<int32_t> t1((size_t)P0ext.n);
+            for (int32_t c = 0; c < (int32_t)t1.size(); ++c) t1[c] = c < na ? c : e2_id(e1_off[c - na]);
+            rc = remap_cols(Plocal, t1);
+            Plocal.n = n2;
+        }
+        if (!rc) {
+            std::vector<int32_t> gi{0}, gj;
+            std::vector<double> ga;
+            for (int32_t s = 0; s < ng; ++s) {
+                std::vector<std::pair<int32_t, double>> row;
+                for (size_t k = 0; k < gcols[s].size(); ++k) row.emplace_back(e2_id(gcols[s][k]), gvals[s][k]);
+                std::sort(row.begin(), row.end(),
+                          [](const std::pair<int32_t, double> &a, const std::pair<int32_t, double> &b) {
+                              return a.first < b.first;
+                          });
+                for (auto &x : row) {
+                    gj.push_back(x.first);
+                    ga.push_back(x.second);
+                }
+                gi.push_back((int32_t)gj.size());
+            }
+            // vertical stack on the device
+            const int64_t nzl = Plocal.nz, nzg = (int64_t)gj.size();
+            Pext.m = m + ng;
+            Pext.n = n2;
+            Pext.nz = nzl + nzg;
+            int32_t *d_gi = nullptr;
+            if ((e = dalloc(&Pext.ai, (int64_t)m + ng + 1)) != hipSuccess || (e = dalloc(&Pext.aj, Pext.nz + 2)) != hipSuccess ||
+                (e = dalloc(&Pext.aa, Pext.nz + 2)) != hipSuccess ||
+                (e = hipMemset(Pext.aj, 0, sizeof(int32_t) * (size_t)(Pext.nz + 2))) != hipSuccess ||
+                (e = hipMemset(Pext.aa, 0, sizeof(double) * (size_t)(Pext.nz + 2))) != hipSuccess ||
+                (e = hipMemcpy(Pext.ai, Plocal.ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToDevice)) != hipSuccess ||
+                (nzl > 0 && ((e = hipMemcpy(Pext.aj, Plocal.aj, sizeof(int32_t) * (size_t)nzl, hipMemcpyDeviceToDevice)) !=
+                                 hipSuccess ||
+                             (e = hipMemcpy(Pext.aa, Plocal.aa, sizeof(double) * (size_t)nzl, hipMemcpyDeviceToDevice)) !=
+                                 hipSuccess)) ||
+                (nzg > 0 && ((e = hipMemcpy(Pext.aj + nzl, gj.data(), sizeof(int32_t) * (size_t)nzg,
+                                            hipMemcpyHostToDevice)) != hipSuccess ||
+                             (e = hipMemcpy(Pext.aa + nzl, ga.data(), sizeof(double) * (size_t)nzg,
+                                            hipMemcpyHostToDevice)) != hipSuccess)) ||
+                (e = dalloc(&d_gi, (int64_t)ng + 1)) != hipSuccess ||
+                (e = hipMemcpy(d_gi, gi.data(), sizeof(int32_t) * gi.size(), hipMemcpyHostToDevice)) != hipSuccess)
+                rc = gerr(e, "P extended");
+            if (!rc && ng > 0)
+                hipLaunchKernelGGL(k_add_offset, dim3(nblk(ng)), dim3(256), 0, nullptr, ng, (int32_t)nzl, d_gi + 1,
+                                   Pext.ai + m + 1);
+            hipFree(d_gi);
+            // R_o rows (own coarse c): the ghost fine rows' entries in own columns, by slot
+            if (!rc) {
+                std::vector<std::vector<std::pair<int32_t, double>>> rrows((size_t)na);
+                for (int32_t s = 0; s < ng; ++s)
+                    for (size_t k = 0; k < gcols[s].size(); ++k) {
+                        const int64_t c = gcols[s][k];
+                        if (c >= cstart && c < cstart + na) rrows[c - cstart].emplace_back(s, gvals[s][k]);
+                    }
+                std::vector<int32_t> ri{0}, rj;
+                std::vector<double> ra;
+                for (auto &row : rrows) {
+                    for (auto &x : row) {
+                        rj.push_back(x.first);
+                        ra.push_back(x.second);
+                    }
+                    ri.push_back((int32_t)rj.size());
+                }
+                if (!rj.empty())
+                    rc = aijhip_mat_create(L.Ad->device, na, ng, (int64_t)rj.size(), ri.data(), rj.data(), ra.data(),
+                                           &L.Ro);
+            }
+        }
+        lap(l, "P extended, R_o");
+        // ---- A P and P^T (A P)
+        if (!rc) rc = aijhip_gamg::rowprod_device(Aext, Pext, AP, n_cu, &cols_used);
+        Pext.release();
+        if (aext_owned) Aext.release();
+        lap(l, "A*P");
+        if (!rc) {
+            aijhip_mat pv;  // non-owning view for the transpose builder
+            pv.m = Plocal.m;
+            pv.n = Plocal.n;
+            pv.nz = Plocal.nz;
+            pv.d_ai = Plocal.ai;
+            pv.d_aj = Plocal.aj;
+            pv.d_aa = Plocal.aa;
+            PT.m = Plocal.n;
+            PT.n = Plocal.m;
+            PT.nz = Plocal.nz;
+            e = aijhip::build_transpose(pv, &PT.ai, &PT.aj, &PT.aa, nullptr);
+            pv.d_ai = pv.d_aj = nullptr;
+            pv.d_aa = nullptr;
+            if (e != hipSuccess) rc = gerr(e, "transpose");
+        }
+        if (!rc) rc = aijhip_gamg::rowprod_device(PT, AP, Cext, n_cu, &cols_used);
+        PT.release();
+        AP.release();
+        lap(l, "P^T*(AP)");
+        // ---- rows [na, n2) of Cext belong to other ranks: send them to their owners
+        std::vector<int64_t> gnew;  // level l+1 ghost list
+        std::vector<int32_t> corr_i{0}, corr_j;
+        std::vector<double> corr_a;
+        if (!rc) {
+            std::vector<int32_t> rows;
+            for (int32_t r = na; r < n2; ++r) rows.push_back(r);
+            std::vector<int32_t> off, cols;
+            std::vector<double> vals;
+            rc = download_rows(Cext.ai, Cext.aj, Cext.aa, rows, off, cols, vals);
+            auto e2_gid = [&](int32_t c) -> int64_t { return c < na ? cstart + c : e2_off[c - na]; };
+            std::vector<std::vector<uint64_t>> out((size_t)P), in;
+            for (size_t q = 0; !rc && q < rows.size(); ++q) {
+                const int64_t rg = e2_off[q];
+                auto &o = out[owner_of(cstarts, rg)];
+                o.push_back((uint64_t)rg);
+                o.push_back((uint64_t)(off[q + 1] - off[q]));
+                for (int32_t k = off[q]; k < off[q + 1]; ++k) {
+                    o.push_back((uint64_t)e2_gid(cols[k]));
+                    uint64_t bitsv;
+                    std::memcpy(&bitsv, &vals[k], 8);
+                    o.push_back(bitsv);
+                }
+            }
+            if (!rc) rc = aijhip_mpi::comm_sendrecv(C, out, in);
+            // received (row, col, value) for own rows, in (peer, message) order
+            struct Trip {
+                int32_t r;
+                int64_t c;
+                double v;
+            };
+            std::vector<Trip> trips;
+            for (int q = 0; !rc && q < P; ++q) {
+                if (q == me) continue;
+                const auto &w = in[q];
+                size_t k = 0;
+                while (k < w.size()) {
+                    const int64_t rg = (int64_t)w[k++];
+                    const uint64_t len = w[k++];
+                    for (uint64_t t = 0; t < len; ++t) {
+                        Trip tr;
+                        tr.r = (int32_t)(rg - cstart);
+                        tr.c = (int64_t)w[k++];
+                        std::memcpy(&tr.v, &w[k++], 8);
+                        trips.push_back(tr);
+                    }
+                }
+            }
+            // level l+1 ghosts: E2's off-rank ids and every off-rank column received
+            gnew = e2_off;
+            for (const Trip &t : trips)
+                if (t.c < cstart || t.c >= cstart + na) gnew.push_back(t.c);
+            std::sort(gnew.begin(), gnew.end());
+            gnew.erase(std::unique(gnew.begin(), gnew.end()), gnew.end());
+            auto u_id = [&](int64_t gidc) -> int32_t {  // unified: own [0, na), ghost slot na + s
+                if (gidc >= cstart && gidc < cstart + na) return (int32_t)(gidc - cstart);
+                return na + (int32_t)(std::lower_bound(gnew.begin(), gnew.end(), gidc) - gnew.begin());
+            };
+            std::stable_sort(trips.begin(), trips.end(), [&](const Trip &a, const Trip &b) {
+                if (a.r != b.r) return a.r < b.r;
+                return u_id(a.c) < u_id(b.c);
+            });
+            std::vector<int32_t> cnt((size_t)na, 0);
+            for (size_t k = 0; k < trips.size();) {
+                size_t j = k;
+                double v = 0.0;
+                const int32_t cu = u_id(trips[k].c);
+                while (j < trips.size() && trips[j].r == trips[k].r && u_id(trips[j].c) == cu) v += trips[j++].v;
+                ++cnt[trips[k].r];
+                corr_j.push_back(cu);
+                corr_a.push_back(v);
+                k = j;
+            }
+            corr_i.assign((size_t)na + 1, 0);
+            for (int32_t r = 0; r < na; ++r) corr_i[r + 1] = corr_i[r] + cnt[r];
+            // E2 -> unified numbering for the own rows of Cext and for P
+            std::vector<int32_t> t2((size_t)n2);
+            for (int32_t c = 0; c < n2; ++c) t2[c] = c < na ? c : u_id(e2_off[c - na]);
+            if (!rc) rc = remap_cols(Cext, t2);
+            if (!rc) rc = remap_cols(Plocal, t2);
+        }
+        lap(l, "Galerkin contributions");
+        // ---- the coarse operator's own rows: Cext[0, na) + received, split
+        DCsr Cown, Corr, Ctot, Cd, Co, Pd, Po;
+        const int32_t ngn = (int32_t)gnew.size();
+        if (!rc) {
+            Cown.m = na;
+            Cown.n = na + ngn;
+            Cown.ai = Cext.ai;
+            Cown.aj = Cext.aj;
+            Cown.aa = Cext.aa;
+            int32_t nz_own = 0;
+            if ((e = hipMemcpy(&nz_own, Cext.ai + na, sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
+                rc = gerr(e, "coarse rows");
+            Cown.nz = nz_own;
+            if (!rc) rc = upload_csr(na, na + ngn, corr_i, corr_j, corr_a, Corr);
+            if (!rc) rc = csr_add(Cown, Corr, Ctot);
+            Cown = DCsr();  // a view of Cext
+            Corr.release();
+            if (!rc) rc = csr_split(Ctot, na, ngn, Cd, Co);
+            Ctot.release();
+            Plocal.n = na + ngn;
+            if (!rc) rc = csr_split(Plocal, na, ngn, Pd, Po);
+        }
+        Cext.release();
+        Plocal.release();
+        // ---- handles of level l+1 and the transfer operators of level l
+        aijhip_mat *Adn = nullptr, *Aon = nullptr;
+        if (!rc) rc = aijhip_gamg::make_level_handle(L.Ad->device, Cd, &Adn);
+        if (!rc && Co.nz > 0) rc = aijhip_gamg::make_level_handle(L.Ad->device, Co, &Aon);
+        Co.release();
+        if (!rc) rc = aijhip_gamg::make_level_handle(L.Ad->device, Pd, &L.Pd);
+        if (!rc) {  // R_d = P_d^T attached for the restriction
+            int32_t *ti = nullptr, *tj = nullptr;
+            double *ta = nullptr;
+            if ((e = aijhip::build_transpose(*L.Pd, &ti, &tj, &ta, nullptr)) != hipSuccess) rc = gerr(e, "P^T");
+            else rc = aijhip::attach_transpose(L.Pd, ti, tj, ta);
+        }
+        if (!rc && Po.nz > 0) rc = aijhip_gamg::make_level_handle(L.Ad->device, Po, &L.Po);
+        Po.release();
+        Pd.release();
+        Cd.release();
+        hipFree(d_agg);
+        hipFree(dinv);
+        hipFree(d_p0);
+        lap(l, "handles");
+        if (rc) {
+            aijhip_mat_destroy(Adn);
+            aijhip_mat_destroy(Aon);
+            hipFree(d_Bc);
+            break;
+        }
+        H.lv.emplace_back();
+        Level &N = H.lv.back();
+        Level &Lp = H.lv[l];  // (reference refreshed after the push)
+        N.Ad = Adn;
+        N.Ao = Aon;
+        N.m = na;
+        N.starts = cstarts;
+        N.rstart = cstart;
+        N.ghost_gid = gnew;
+        rc = make_operator(C, Adn, Aon, gnew, cstarts, &N.op);
+        Lp.emax = emax;
+        std::swap(d_B, d_Bc);
+        hipFree(d_Bc);
+        lap(l, "halo plan");
+        if (rc) break;
+    }
+    hipFree(d_B);
+    // level vectors and D^-1
+    for (size_t l = 0; !rc && l < H.lv.size(); ++l) {
+        Level &L = H.lv[l];
+        const size_t vb = sizeof(double) * (size_t)std::max<int32_t>(L.m, 1);
+        if ((e = hipMalloc(&L.dinv, vb)) != hipSuccess || (e = hipMalloc(&L.r, vb)) != hipSuccess ||
+            (l > 0 && ((e = hipMalloc(&L.b, vb)) != hipSuccess || (e = hipMalloc(&L.x, vb)) != hipSuccess))) {
+            rc = gerr(e, "level vectors");
+            break;
+        }
+        if (L.m > 0)
+            hipLaunchKernelGGL(k_diag_inv, dim3(nblk(L.m)), dim3(256), 0, nullptr, L.m, L.Ad->d_ai, L.Ad->d_aj,
+                               L.Ad->d_aa, L.dinv);
+    }
+    if (!rc && (e = hipDeviceSynchronize()) != hipSuccess) rc = gerr(e, "set-up");
+    if (rc) H.destroy();
+    return rc;
+}
+
+// y = B x (+ z) through the halo of `halo_op`: the exchange of x overlaps B_d x
+static int transfer(aijhip_mpiaij *halo_op, const aijhip_mat *Bd, const aijhip_mat *Bo, const double *x,
+                    const double *z, double *y, bool add, hipStream_t s, const int *stop) {
+    const bool exch = halo_op->n_send > 0 || halo_op->n_ghost > 0;
+    int rc = exch ? aijhip_mpi::halo_post(halo_op, x, s) : AIJHIP_OK;
+    if (rc) return rc;
+    hipError_t e = aijhip::launch_mult(*Bd, x, z, y, add, s, stop);
+    if (e != hipSuccess) return gerr(e, "transfer product");
+    if (exch && (rc = aijhip_mpi::halo_finish(halo_op, s))) return rc;
+    if (Bo && (e = aijhip::launch_mult(*Bo, halo_op->d_ghost, y, y, true, s, stop)) != hipSuccess)
+        return gerr(e, "transfer ghost product");
+    return AIJHIP_OK;
+}
+
+int vcycle(Hierarchy &H, const double *b0, double *x0, hipStream_t s, const int *stop) {
+    const int nl = (int)H.lv.size();
+    auto B = [&](int l) { return l == 0 ? b0 : (const double *)H.lv[l].b; };
+    auto X = [&](int l) { return l == 0 ? x0 : H.lv[l].x; };
+    auto grid = [](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048))); };
+    int rc;
+    for (int l = 0; l < nl; ++l) {
+        Level &L = H.lv[l];
+        hipLaunchKernelGGL(k_mg_jacobi, grid(L.m), dim3(256), 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
+        if (l == nl - 1) break;  // coarse: preonly + Jacobi
+        // r = b - A x (MatMult_MPIAIJ, then the residual)
+        if ((rc = aijhip_mpi::mpiaij_apply(L.op, X(l), L.r, s, nullptr, nullptr, nullptr, false, stop))) return rc;
+        hipLaunchKernelGGL(k_mg_resid, grid(L.m), dim3(256), 0, s, (int64_t)L.m, B(l), L.r, stop);
+        // MatRestrict: b_{l+1} = P^T r = P_d^T r + R_o r_ghost
+        if ((rc = transfer(L.op, L.Pd->transpose, L.Ro, L.r, nullptr, H.lv[l + 1].b, false, s, stop))) return rc;
+    }
+    for (int l = nl - 2; l >= 0; --l) {
+        Level &L = H.lv[l];
+        // MatInterpolateAdd: x = x + P x_c (P_d x_c + P_o x_c ghost)
+        if ((rc = transfer(H.lv[l + 1].op, L.Pd, L.Po, X(l + 1), X(l), X(l), true, s, stop))) return rc;
+        // smoothu: x = x + D^-1 (b - A x)
+        if ((rc = aijhip_mpi::mpiaij_apply(L.op, X(l), L.r, s, nullptr, nullptr, nullptr, false, stop))) return rc;
+        hipLaunchKernelGGL(k_mg_richardson, grid(L.m), dim3(256), 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l), stop);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? AIJHIP_OK : gerr(e, "V-cycle");
+}
+
+}  // namespace aijhip_gamg_mpi

@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -38,8 +39,10 @@
 #include "aijhip_internal.h"
 #include "aijhip_mpi.h"
 #include "cg_device.h"
+#include "gamg_mpi.h"
+#include "mpi_internal.h"
 
-namespace {
+namespace aijhip_mpi {
 
 int mfail(int code, const std::string &msg) {
     aijhip::set_error(msg);
@@ -50,6 +53,12 @@ int mhip(hipError_t e, const char *what) {
     aijhip::set_error(std::string(what) + ": " + hipGetErrorString(e));
     return AIJHIP_ERR_HIP;
 }
+
+}  // namespace aijhip_mpi
+
+using namespace aijhip_mpi;
+
+namespace {
 
 struct DeviceGuard {
     int prev = -1;
@@ -125,24 +134,12 @@ int nfail(ncclResult_t r, const char *what) {
 
 }  // namespace
 
-struct aijhip_comm {
-    int kind = 0;
-    int32_t nranks = 1, rank = 0, device = 0;
-    int version = 0;
-    ncclComm_t nc = nullptr;
-    aijhip_host_allreduce_fn har = nullptr;
-    aijhip_host_exchange_fn hex = nullptr;
-    void *ctx = nullptr;
-    double timeout_s = 300.0;
-    bool aborted = false;
-    double *h_red = nullptr;  // pinned staging of host all-reduces
-    hipEvent_t ev_wait = nullptr;
-    int64_t waits = 0;  // host waits made (polls, host-transport collectives)
-};
 
 namespace {
-
 constexpr int kMaxRed = 64;
+}  // namespace
+
+namespace aijhip_mpi {
 
 void comm_abort(aijhip_comm *C) {
     if (C->aborted) return;
@@ -207,6 +204,128 @@ int comm_allreduce(aijhip_comm *C, double *d_buf, int32_t n, hipStream_t s) {
     e = hipMemcpyAsync(d_buf, C->h_red, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, s);
     return e == hipSuccess ? AIJHIP_OK : mhip(e, "all-reduce staging");
 }
+
+int comm_allreduce_host(aijhip_comm *C, double *v, int32_t n) {
+    if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
+    if (n <= 0 || C->nranks == 1) return AIJHIP_OK;
+    if (C->kind == AIJHIP_COMM_HOST) {
+        if (n > kMaxRed) return mfail(AIJHIP_ERR_ARG, "host all-reduce of more than 64 values");
+        std::memcpy(C->h_red, v, sizeof(double) * (size_t)n);
+        ++C->waits;
+        if (C->har(C->ctx, C->h_red, n) != 0) {
+            comm_abort(C);
+            return mfail(AIJHIP_ERR_COMM, "host all-reduce callback failed");
+        }
+        std::memcpy(v, C->h_red, sizeof(double) * (size_t)n);
+        return AIJHIP_OK;
+    }
+    double *d = nullptr;
+    hipError_t e = hipMalloc(&d, sizeof(double) * (size_t)n);
+    if (e != hipSuccess) return mhip(e, "all-reduce buffer");
+    int rc = AIJHIP_OK;
+    if (!C->xs && (e = hipStreamCreateWithFlags(&C->xs, hipStreamNonBlocking)) != hipSuccess) rc = mhip(e, "stream");
+    if (!rc && (e = hipMemcpyAsync(d, v, sizeof(double) * (size_t)n, hipMemcpyHostToDevice, C->xs)) != hipSuccess)
+        rc = mhip(e, "all-reduce upload");
+    if (!rc) rc = comm_allreduce(C, d, n, C->xs);
+    if (!rc && (e = hipMemcpyAsync(v, d, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost, C->xs)) != hipSuccess)
+        rc = mhip(e, "all-reduce download");
+    if (!rc) rc = wait_stream(C, C->xs);
+    hipFree(d);
+    return rc;
+}
+
+// Counts first (one word per peer pair), then the payloads: RCCL grouped
+// send/recv of device copies, or the host transport's sendrecv callback.
+int comm_sendrecv(aijhip_comm *C, const std::vector<std::vector<uint64_t>> &out,
+                  std::vector<std::vector<uint64_t>> &in) {
+    const int P = C->nranks, me = C->rank;
+    in.assign((size_t)P, {});
+    if ((int)out.size() != P) return mfail(AIJHIP_ERR_ARG, "sendrecv: one list per rank");
+    in[me] = out[me];
+    if (P == 1) return AIJHIP_OK;
+    if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
+    // the counts: word q of my row goes to rank q
+    std::vector<std::vector<uint64_t>> cnt_out((size_t)P), cnt_in;
+    std::vector<int64_t> nin((size_t)P, 0);
+    auto exchange = [&](const std::vector<std::vector<uint64_t>> &o, std::vector<std::vector<uint64_t>> &i,
+                        const std::vector<int64_t> &isize) -> int {
+        std::vector<int32_t> sp, rp;
+        std::vector<int64_t> so{0}, ro{0};
+        std::vector<uint64_t> sbuf;
+        for (int q = 0; q < P; ++q) {
+            if (q == me || o[q].empty()) continue;
+            sp.push_back(q);
+            sbuf.insert(sbuf.end(), o[q].begin(), o[q].end());
+            so.push_back((int64_t)sbuf.size());
+        }
+        for (int p = 0; p < P; ++p) {
+            if (p == me || isize[p] == 0) continue;
+            rp.push_back(p);
+            ro.push_back(ro.back() + isize[p]);
+        }
+        std::vector<uint64_t> rbuf((size_t)ro.back());
+        if (C->kind == AIJHIP_COMM_HOST) {
+            if (!C->hsr) return mfail(AIJHIP_ERR_STATE, "host transport without a sendrecv callback "
+                                                        "(aijhip_comm_set_host_sendrecv)");
+            ++C->waits;
+            if (C->hsr(C->ctx, (int32_t)sp.size(), sp.data(), so.data(), reinterpret_cast<const double *>(sbuf.data()),
+                       (int32_t)rp.size(), rp.data(), ro.data(), reinterpret_cast<double *>(rbuf.data())) != 0) {
+                comm_abort(C);
+                return mfail(AIJHIP_ERR_COMM, "host sendrecv callback failed");
+            }
+        } else {
+            const Rccl &R = rccl();
+            hipError_t e;
+            if (!C->xs && (e = hipStreamCreateWithFlags(&C->xs, hipStreamNonBlocking)) != hipSuccess)
+                return mhip(e, "stream");
+            uint64_t *ds = nullptr, *dr = nullptr;
+            if ((e = hipMalloc(&ds, sizeof(uint64_t) * std::max<size_t>(1, sbuf.size()))) != hipSuccess ||
+                (e = hipMalloc(&dr, sizeof(uint64_t) * std::max<size_t>(1, rbuf.size()))) != hipSuccess) {
+                hipFree(ds);
+                return mhip(e, "sendrecv buffers");
+            }
+            int rc = AIJHIP_OK;
+            if (!sbuf.empty() && (e = hipMemcpyAsync(ds, sbuf.data(), sizeof(uint64_t) * sbuf.size(),
+                                                     hipMemcpyHostToDevice, C->xs)) != hipSuccess)
+                rc = mhip(e, "sendrecv upload");
+            if (!rc) {
+                ncclResult_t r = R.GroupStart();
+                for (size_t q = 0; r == ncclSuccess && q < sp.size(); ++q)
+                    r = R.Send(ds + so[q], (size_t)(so[q + 1] - so[q]), ncclUint64, sp[q], C->nc, C->xs);
+                for (size_t p = 0; r == ncclSuccess && p < rp.size(); ++p)
+                    r = R.Recv(dr + ro[p], (size_t)(ro[p + 1] - ro[p]), ncclUint64, rp[p], C->nc, C->xs);
+                const ncclResult_t r2 = R.GroupEnd();
+                if (r != ncclSuccess) rc = nfail(r, "set-up ncclSend/ncclRecv");
+                else if (r2 != ncclSuccess) rc = nfail(r2, "ncclGroupEnd");
+            }
+            if (!rc && !rbuf.empty() && (e = hipMemcpyAsync(rbuf.data(), dr, sizeof(uint64_t) * rbuf.size(),
+                                                            hipMemcpyDeviceToHost, C->xs)) != hipSuccess)
+                rc = mhip(e, "sendrecv download");
+            if (!rc) rc = wait_stream(C, C->xs);
+            hipFree(ds);
+            hipFree(dr);
+            if (rc) return rc;
+        }
+        for (size_t p = 0; p < rp.size(); ++p) i[rp[p]].assign(rbuf.begin() + ro[p], rbuf.begin() + ro[p + 1]);
+        return AIJHIP_OK;
+    };
+    for (int q = 0; q < P; ++q) cnt_out[q].assign(1, (uint64_t)out[q].size());
+    std::vector<int64_t> ones((size_t)P, 1);
+    ones[me] = 0;
+    cnt_in.assign((size_t)P, {});
+    int rc = exchange(cnt_out, cnt_in, ones);
+    if (rc) return rc;
+    for (int p = 0; p < P; ++p) nin[p] = p == me ? 0 : (int64_t)cnt_in[p][0];
+    std::vector<std::vector<uint64_t>> got((size_t)P);
+    if ((rc = exchange(out, got, nin))) return rc;
+    for (int p = 0; p < P; ++p)
+        if (p != me) in[p] = std::move(got[p]);
+    return AIJHIP_OK;
+}
+
+}  // namespace aijhip_mpi
+
+namespace {
 
 // ------------------------------------------------------------- kernels
 // Pack the send rows: buf[i] = x[rows[i]] (zero past n up to n_pad).
@@ -312,25 +431,6 @@ int grid_of(int64_t n, int cap) {
 
 }  // namespace
 
-struct aijhip_mpiaij {
-    aijhip_comm *comm = nullptr;
-    aijhip_mat *Ad = nullptr, *Ao = nullptr;
-    int halo = AIJHIP_HALO_P2P;
-    int32_t mloc = 0;
-    int64_t n_ghost = 0;
-    std::vector<int32_t> send_peer, recv_peer;
-    std::vector<int64_t> send_off, recv_off;
-    std::vector<int64_t> send_first;  // per send peer: first row if its rows are one contiguous run, else -1
-    int32_t gather_len = 0;
-    int64_t n_send = 0;     // packed send entries (all-gather: gather_len)
-    bool pack_all = false;  // every send row goes through the packed buffer
-    int32_t *d_send_rows = nullptr;
-    double *d_sendbuf = nullptr, *d_ghost = nullptr;
-    double *h_send = nullptr, *h_ghost = nullptr;  // host transport staging (pinned)
-    hipStream_t xs = nullptr;
-    hipEvent_t ev_x = nullptr, ev_halo = nullptr;
-    int o_grid = 1;
-};
 
 namespace {
 
@@ -342,6 +442,10 @@ void mpiaij_free(aijhip_mpiaij *M) {
     if (M->ev_x) hipEventDestroy(M->ev_x);
     if (M->ev_halo) hipEventDestroy(M->ev_halo);
 }
+
+}  // namespace
+
+namespace aijhip_mpi {
 
 // Start the ghost exchange on the exchange stream (ordered after everything
 // already enqueued on s, i.e. after x is written and the previous A_o
@@ -408,7 +512,43 @@ int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
         const int64_t npack = M->halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send;
         int rc = wait_stream(C, M->xs);
         if (rc) return rc;
-        if (C->hex(C->ctx, M, M->h_send, npack, M->h_ghost, M->n_ghost) != 0) {
+        int bad = 0;
+        if (C->hsr && M->halo == AIJHIP_HALO_P2P) {
+            // the library's own plan over the generic point-to-point callback
+            // (operators the library made itself have no plan on the caller's
+            // side); segments for this rank itself are local copies
+            std::vector<int32_t> sp, rp;
+            std::vector<int64_t> so{0}, ro{0};
+            std::vector<double> sb, rb;
+            for (size_t q = 0; q < M->send_peer.size(); ++q) {
+                if (M->send_peer[q] == C->rank) continue;
+                sp.push_back(M->send_peer[q]);
+                sb.insert(sb.end(), M->h_send + M->send_off[q], M->h_send + M->send_off[q + 1]);
+                so.push_back((int64_t)sb.size());
+            }
+            for (size_t pp = 0; pp < M->recv_peer.size(); ++pp) {
+                if (M->recv_peer[pp] == C->rank) continue;
+                rp.push_back(M->recv_peer[pp]);
+                ro.push_back(ro.back() + (M->recv_off[pp + 1] - M->recv_off[pp]));
+            }
+            rb.resize((size_t)ro.back());
+            bad = C->hsr(C->ctx, (int32_t)sp.size(), sp.data(), so.data(), sb.data(), (int32_t)rp.size(), rp.data(),
+                         ro.data(), rb.data());
+            for (size_t pp = 0, k = 0; !bad && pp < M->recv_peer.size(); ++pp) {
+                const int64_t a = M->recv_off[pp], n = M->recv_off[pp + 1] - a;
+                if (M->recv_peer[pp] == C->rank) {
+                    for (size_t q = 0; q < M->send_peer.size(); ++q)
+                        if (M->send_peer[q] == C->rank)
+                            std::memcpy(M->h_ghost + a, M->h_send + M->send_off[q], sizeof(double) * (size_t)n);
+                } else {
+                    std::memcpy(M->h_ghost + a, rb.data() + ro[k], sizeof(double) * (size_t)n);
+                    ++k;
+                }
+            }
+        } else {
+            bad = C->hex(C->ctx, M, M->h_send, npack, M->h_ghost, M->n_ghost);
+        }
+        if (bad != 0) {
             comm_abort(C);
             return mfail(AIJHIP_ERR_COMM, "host exchange callback failed");
         }
@@ -424,7 +564,7 @@ int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
 // y = A_d x + A_o g; with dot: W = y and the p.w partials (p = x) into
 // part (A_d blocks, fused when A_d's plan allows) and opart (A_o rows).
 int mpiaij_apply(aijhip_mpiaij *M, const double *x, double *y, hipStream_t s, double *part, double *opart,
-                 const CGState *S, bool fused) {
+                 const CGState *S, bool fused, const int *stop) {
     // nothing to send or receive (one rank, or a block with no coupling):
     // no exchange, no second stream
     const bool exchange = M->n_send > 0 || M->n_ghost > 0 || M->halo == AIJHIP_HALO_ALLGATHER;
@@ -432,7 +572,7 @@ int mpiaij_apply(aijhip_mpiaij *M, const double *x, double *y, hipStream_t s, do
     if (rc) return rc;
     hipError_t e;
     if (part && fused) e = aijhip::launch_stream_dot(*M->Ad, x, y, part, S ? &S->done : nullptr, s);
-    else e = aijhip::launch_mult(*M->Ad, x, nullptr, y, false, s);
+    else e = aijhip::launch_mult(*M->Ad, x, nullptr, y, false, s, stop);
     if (e != hipSuccess) return mhip(e, "A_d product");
     if (exchange && (rc = halo_finish(M, s))) return rc;
     if (M->Ao) {
@@ -443,14 +583,14 @@ int mpiaij_apply(aijhip_mpiaij *M, const double *x, double *y, hipStream_t s, do
                                    M->Ao->d_aj, M->Ao->d_aa, M->d_ghost, x, y, opart, S);
             e = hipGetLastError();
         } else {
-            e = aijhip::launch_mult(*M->Ao, M->d_ghost, y, y, true, s);  // MatMultAdd_SeqAIJ(A_o, g, y, y)
+            e = aijhip::launch_mult(*M->Ao, M->d_ghost, y, y, true, s, stop);  // MatMultAdd_SeqAIJ(A_o, g, y, y)
         }
         if (e != hipSuccess) return mhip(e, "A_o product");
     }
     return AIJHIP_OK;
 }
 
-}  // namespace
+}  // namespace aijhip_mpi
 
 struct aijhip_kspmpi {
     aijhip_mpiaij *M = nullptr;
@@ -464,6 +604,9 @@ struct aijhip_kspmpi {
     // this rank's diagonal block (a single-GPU KSP's set-up), one V-cycle per
     // application, no communication inside the preconditioner
     aijhip_ksp_t sub = nullptr;
+    // PC GAMG across ranks (gamg_mpi.hip)
+    aijhip_gamg_mpi::Hierarchy *dh = nullptr;
+    double setup_seconds = 0.0;
     aijhip_gamg_params_t gamg{};
     bool gamg_set = false;
     int vec_grid = 1, n_dparts = 1;
@@ -485,6 +628,11 @@ void kspmpi_free(aijhip_kspmpi *K) {
     if (K->h_state) hipHostFree(K->h_state);
     if (K->sub) aijhip_ksp_destroy(K->sub);
     K->sub = nullptr;
+    if (K->dh) {
+        K->dh->destroy();
+        delete K->dh;
+        K->dh = nullptr;
+    }
     K->d_dinv = K->d_r = K->d_z = K->d_p = K->d_part = K->d_opart = K->d_red = K->d_hist = nullptr;
     K->d_state = K->h_state = nullptr;
     K->set_up = false;
@@ -492,6 +640,7 @@ void kspmpi_free(aijhip_kspmpi *K) {
 
 int kspmpi_set_up(aijhip_kspmpi *K) {
     if (K->set_up) return AIJHIP_OK;
+    const auto t_setup = std::chrono::steady_clock::now();
     kspmpi_free(K);
     aijhip_mpiaij *M = K->M;
     aijhip_mat *A = M->Ad;
@@ -523,7 +672,22 @@ int kspmpi_set_up(aijhip_kspmpi *K) {
             return mhip(e, "PCSetUp_Jacobi (distributed)");
         }
     }
-    if (K->pc == AIJHIP_PC_GAMG) {  // PCSetUp_BJacobi + the sub-PC's PCSetUp_GAMG on A_d
+    // GAMG across ranks: more than one rank (AIJHIP_GAMG_DIST=1 forces the
+    // distributed set-up at one rank too, for tests)
+    const char *force = std::getenv("AIJHIP_GAMG_DIST");
+    const bool dist = K->pc == AIJHIP_PC_GAMG && (M->comm->nranks > 1 || (force && std::atoi(force) != 0));
+    if (dist) {
+        aijhip_gamg_params_t gp;
+        if (K->gamg_set) gp = K->gamg;
+        else aijhip_gamg_params_default(&gp);
+        K->dh = new (std::nothrow) aijhip_gamg_mpi::Hierarchy();
+        int rc = K->dh ? aijhip_gamg_mpi::build(M, gp, *K->dh) : mfail(AIJHIP_ERR_ALLOC, "host allocation");
+        if (rc) {
+            kspmpi_free(K);
+            return rc;
+        }
+    } else if (K->pc == AIJHIP_PC_GAMG || K->pc == AIJHIP_PC_BJACOBI_GAMG) {
+        // PCSetUp_BJacobi + the sub-PC's PCSetUp_GAMG on A_d (at one rank: PCGAMG itself)
         int rc = aijhip_ksp_create(A, &K->sub);
         if (!rc) rc = aijhip_ksp_set_pc_type(K->sub, AIJHIP_PC_GAMG);
         if (!rc && K->gamg_set) rc = aijhip_ksp_set_gamg_params(K->sub, &K->gamg);
@@ -533,8 +697,19 @@ int kspmpi_set_up(aijhip_kspmpi *K) {
             return rc;
         }
     }
+    K->setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_setup).count();
     K->set_up = true;
     return AIJHIP_OK;
+}
+
+// z = B r with the GAMG PC: the distributed hierarchy or the per-rank one.
+// *dots: the fused finest post-smoothing's z.z / z.r partials, or NULL.
+int pc_gamg_apply(aijhip_kspmpi *K, hipStream_t s, const double **dots, int *nbz) {
+    *dots = nullptr;
+    *nbz = 0;
+    if (K->dh) return aijhip_gamg_mpi::vcycle(*K->dh, K->d_r, K->d_z, s, &K->d_state->done);
+    const hipError_t e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, dots, nbz, &K->d_state->done);
+    return e == hipSuccess ? AIJHIP_OK : mhip(e, "GAMG V-cycle");
 }
 
 }  // namespace
@@ -579,6 +754,7 @@ int aijhip_comm_destroy(aijhip_comm_t C) {
     {
         DeviceGuard g(C->device);
         if (C->kind == AIJHIP_COMM_RCCL && C->nc) rccl().CommDestroy(C->nc);
+        if (C->xs) hipStreamDestroy(C->xs);
         if (C->ev_wait) hipEventDestroy(C->ev_wait);
         if (C->h_red) hipHostFree(C->h_red);
     }
@@ -618,6 +794,13 @@ int aijhip_comm_create_host(int32_t nranks, int32_t rank, int32_t device, aijhip
     C->hex = exchange;
     C->ctx = ctx;
     *out = C;
+    return AIJHIP_OK;
+}
+
+int aijhip_comm_set_host_sendrecv(aijhip_comm_t C, aijhip_host_sendrecv_fn fn) {
+    if (!C) return mfail(AIJHIP_ERR_ARG, "NULL comm");
+    if (C->kind != AIJHIP_COMM_HOST) return mfail(AIJHIP_ERR_ARG, "not a host-transport communicator");
+    C->hsr = fn;
     return AIJHIP_OK;
 }
 
@@ -685,6 +868,7 @@ int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o,
             M->send_first.push_back(contig ? send_rows[a] : -1);
         }
         rows.assign(send_rows, send_rows + send_off[n_send]);
+        M->h_send_rows = rows;
     }
     M->n_send = M->send_off.back();
     if (halo == AIJHIP_HALO_ALLGATHER) {
@@ -796,8 +980,8 @@ int aijhip_kspmpi_set_tolerances(aijhip_kspmpi_t K, double rtol, double abstol, 
 
 int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc) {
     if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
-    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI && pc != AIJHIP_PC_GAMG)
-        return mfail(AIJHIP_ERR_ARG, "distributed CG: PC none, jacobi or gamg (block Jacobi with GAMG blocks)");
+    if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI && pc != AIJHIP_PC_GAMG && pc != AIJHIP_PC_BJACOBI_GAMG)
+        return mfail(AIJHIP_ERR_ARG, "distributed CG: PC none, jacobi, gamg or bjacobi_gamg");
     if (pc != K->pc) K->set_up = false;
     K->pc = pc;
     return AIJHIP_OK;
@@ -845,13 +1029,12 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
     hipError_t e = hipSuccess;
     if (m > 0 && (e = hipMemsetAsync(x, 0, sizeof(double) * (size_t)m, s)) != hipSuccess) return mhip(e, "x = 0");
     // r = b, z = B r, then ||z|| etc. summed over all ranks
-    const bool gamg = K->pc == AIJHIP_PC_GAMG;
+    const bool gamg = K->pc == AIJHIP_PC_GAMG || K->pc == AIJHIP_PC_BJACOBI_GAMG;
     hipLaunchKernelGGL(k_init, vg, vt, 0, s, m, b, K->d_r, K->d_z, dinv, K->d_part, p);
     if (gamg) {  // z = B r, then its z.z, z.r partials (as ksp.hip with a zero guess)
         const double *dots = nullptr;
         int nbz = 0;
-        if ((e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, &dots, &nbz)) != hipSuccess)
-            return mhip(e, "GAMG V-cycle");
+        if ((rc = pc_gamg_apply(K, s, &dots, &nbz))) return rc;
         hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, nullptr);
     }
     hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 4, K->d_red, multi ? 0 : 1, K->d_state,
@@ -896,9 +1079,7 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
             if (gamg) {  // z = B r; z.z and z.r from the fused finest post-smoothing, else k_dots
                 const double *dots = nullptr;
                 int nbz = 0;
-                if ((e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, &dots, &nbz, &K->d_state->done)) !=
-                    hipSuccess)
-                    return mhip(e, "GAMG V-cycle");
+                if ((rc = pc_gamg_apply(K, s, &dots, &nbz))) return rc;
                 if (!dots) {
                     hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
                     dots = K->d_part;
@@ -964,6 +1145,51 @@ int aijhip_kspmpi_get_residual_history(aijhip_kspmpi_t K, double *hist, int32_t 
 int aijhip_kspmpi_get_host_syncs(aijhip_kspmpi_t K, int32_t *n) {
     if (!K || !n) return mfail(AIJHIP_ERR_ARG, "NULL argument");
     *n = K->host_syncs;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_pc_levels(aijhip_kspmpi_t K, int32_t *nlevels, int64_t *rows, int64_t *nnz, int32_t cap) {
+    if (!K || !nlevels) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    if (!K->set_up) return mfail(AIJHIP_ERR_STATE, "KSP not set up");
+    if (K->dh) {
+        const auto &lv = K->dh->lv;
+        *nlevels = (int32_t)lv.size();
+        const int32_t n = std::min<int32_t>(cap, *nlevels);
+        std::vector<double> z((size_t)std::max(n, 1), 0.0);
+        for (int32_t l = 0; l < n; ++l) {
+            if (rows) rows[l] = lv[l].starts.back();
+            z[l] = (double)lv[l].Ad->nz + (lv[l].Ao ? (double)lv[l].Ao->nz : 0.0);
+        }
+        DeviceGuard g(K->M->comm->device);
+        for (int32_t l0 = 0; l0 < n; l0 += 64) {  // the host transport reduces 64 values at a time
+            const int32_t c = std::min<int32_t>(64, n - l0);
+            int rc = aijhip_mpi::comm_allreduce_host(K->M->comm, z.data() + l0, c);
+            if (rc) return rc;
+        }
+        for (int32_t l = 0; l < n; ++l)
+            if (nnz) nnz[l] = (int64_t)z[l];
+        return AIJHIP_OK;
+    }
+    if (K->sub) {
+        std::vector<int32_t> r((size_t)std::max(cap, 1));
+        std::vector<int64_t> z((size_t)std::max(cap, 1));
+        int rc = aijhip_ksp_get_pc_levels(K->sub, nlevels, r.data(), z.data(), cap, nullptr);
+        if (rc) return rc;
+        for (int32_t l = 0; l < std::min(cap, *nlevels); ++l) {
+            if (rows) rows[l] = r[l];
+            if (nnz) nnz[l] = z[l];
+        }
+        return AIJHIP_OK;
+    }
+    *nlevels = 1;
+    if (cap > 0 && rows) rows[0] = K->M->mloc;
+    if (cap > 0 && nnz) nnz[0] = K->M->Ad->nz + (K->M->Ao ? K->M->Ao->nz : 0);
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_setup_seconds(aijhip_kspmpi_t K, double *seconds) {
+    if (!K || !seconds) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    *seconds = K->setup_seconds;
     return AIJHIP_OK;
 }
 

@@ -18,7 +18,7 @@ import numpy as np
 
 _pkg = importlib.import_module("petsc-openacc_amd")
 
-PC_TYPES = {"none": 0, "jacobi": 1, "gamg": 2}
+PC_TYPES = {"none": 0, "jacobi": 1, "gamg": 2, "bjacobi_gamg": 3}
 NORM_TYPES = {"none": 0, "preconditioned": 1, "unpreconditioned": 2, "natural": 3}
 REASONS = {2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
            -8: "DIVERGED_INDEFINITE_PC", -9: "DIVERGED_NANORINF", -10: "DIVERGED_INDEFINITE_MAT"}

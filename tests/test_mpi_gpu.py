@@ -69,7 +69,7 @@ def _worker(rank, world, port, dims, halo, q):
             kn.solve(b, xn)
             native = (xn.cpu().numpy(), kn.its, kn.reason, kn.hist.tolist())
         xg = torch.full_like(b, float("nan"))  # CG + bjacobi/GAMG (one hierarchy per diagonal block)
-        with C.KSPCGMPINative(op_n.native, rtol=1e-10, max_it=1000, pc="gamg") as kg:
+        with C.KSPCGMPINative(op_n.native, rtol=1e-10, max_it=1000, pc="bjacobi_gamg") as kg:
             kg.solve(b, xg)
             native_gamg = (xg.cpu().numpy(), kg.its, kg.reason, kg.hist.tolist())
         q.put((rank, y.cpu().numpy(), xs.cpu().numpy(), cg.its, cg.reason, list(cg.hist), same, native,
