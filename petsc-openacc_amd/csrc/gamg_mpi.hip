@@ -156,20 +156,35 @@ __global__ void k_rows_copy(int32_t n, const int32_t *__restrict__ rows, const i
     }
 }
 
-// C = A + B (rows sorted by column; a column in both: a + b)
-__global__ void k_add_len(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
-                          const int32_t *__restrict__ bi, const int32_t *__restrict__ bj, int32_t *len) {
-    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
+// C = A + B (rows sorted by column; a column in both: a + b). An exact zero
+// sum is not stored, as scipy's csr_matmat (and the single-GPU row products)
+// drop the zeros of a product row: the ranks' partial Galerkin sums of an
+// entry that cancels globally leave no explicit zero.
+template <bool FILL>
+__device__ __forceinline__ int32_t add_row(int32_t i, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                                           const double *__restrict__ aa, const int32_t *__restrict__ bi,
+                                           const int32_t *__restrict__ bj, const double *__restrict__ ba, int32_t o,
+                                           int32_t *cj, double *ca) {
     int32_t p = ai[i], q = bi[i], n = 0;
     const int32_t pe = ai[i + 1], qe = bi[i + 1];
     while (p < pe || q < qe) {
-        if (q >= qe || (p < pe && aj[p] < bj[q])) ++p;
-        else if (p >= pe || bj[q] < aj[p]) ++q;
-        else { ++p; ++q; }
+        int32_t c;
+        double v;
+        if (q >= qe || (p < pe && aj[p] < bj[q])) { c = aj[p]; v = aa[p]; ++p; }
+        else if (p >= pe || bj[q] < aj[p]) { c = bj[q]; v = ba[q]; ++q; }
+        else { c = aj[p]; v = aa[p] + ba[q]; ++p; ++q; }
+        if (v == 0.0) continue;
+        if (FILL) { cj[o + n] = c; ca[o + n] = v; }
         ++n;
     }
-    len[i] = n;
+    return n;
+}
+
+__global__ void k_add_len(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                          const double *__restrict__ aa, const int32_t *__restrict__ bi,
+                          const int32_t *__restrict__ bj, const double *__restrict__ ba, int32_t *len) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) len[i] = add_row<false>(i, ai, aj, aa, bi, bj, ba, 0, nullptr, nullptr);
 }
 
 __global__ void k_add_fill(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
@@ -177,15 +192,7 @@ __global__ void k_add_fill(int32_t m, const int32_t *__restrict__ ai, const int3
                            const int32_t *__restrict__ bj, const double *__restrict__ ba,
                            const int32_t *__restrict__ ci, int32_t *cj, double *ca) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    int32_t p = ai[i], q = bi[i], o = ci[i];
-    const int32_t pe = ai[i + 1], qe = bi[i + 1];
-    while (p < pe || q < qe) {
-        if (q >= qe || (p < pe && aj[p] < bj[q])) { cj[o] = aj[p]; ca[o] = aa[p]; ++p; }
-        else if (p >= pe || bj[q] < aj[p]) { cj[o] = bj[q]; ca[o] = ba[q]; ++q; }
-        else { cj[o] = aj[p]; ca[o] = aa[p] + ba[q]; ++p; ++q; }
-        ++o;
-    }
+    if (i < m) add_row<true>(i, ai, aj, aa, bi, bj, ba, ci[i], cj, ca);
 }
 
 // split columns: < nloc -> D (same ids), >= nloc -> O (id - nloc)
@@ -380,7 +387,9 @@ int csr_add(const DCsr &A, const DCsr &B, DCsr &C) {
     int32_t *len = nullptr;
     hipError_t e;
     if ((e = dalloc(&len, A.m)) != hipSuccess) return gerr(e, "alloc");
-    if (A.m > 0) hipLaunchKernelGGL(k_add_len, dim3(nblk(A.m)), dim3(256), 0, nullptr, A.m, A.ai, A.aj, B.ai, B.aj, len);
+    if (A.m > 0)
+        hipLaunchKernelGGL(k_add_len, dim3(nblk(A.m)), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa, B.ai, B.aj, B.aa,
+                           len);
     int rc = scan_lengths(len, A.m, &C.ai, &C.nz);
     hipFree(len);
     if (rc) return rc;
