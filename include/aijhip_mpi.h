@@ -159,6 +159,13 @@ int aijhip_kspmpi_get_host_syncs(aijhip_kspmpi_t K, int32_t *n);
  * rank's block hierarchy; other PCs: the operator alone. Collective for
  * GAMG (nnz is summed over the ranks). */
 int aijhip_kspmpi_get_pc_levels(aijhip_kspmpi_t K, int32_t *nlevels, int64_t *rows, int64_t *nnz, int32_t cap);
+/* GAMG across ranks, after set-up: this rank's rows of level l's operator
+ * (which = 'A') or interpolation (which = 'P', l below the coarsest) with
+ * GLOBAL column ids of their level; *rstart = the first global row, *m rows,
+ * *nnz entries. Call with ai = NULL for the sizes, then with arrays of
+ * m + 1 / nnz / nnz entries. For tests and inspection. */
+int aijhip_kspmpi_get_pc_level(aijhip_kspmpi_t K, int32_t l, char which, int64_t *rstart, int32_t *m, int64_t *nnz,
+                               int64_t *ai, int64_t *aj, double *aa);
 /* Seconds the last set-up took on this rank. */
 int aijhip_kspmpi_get_setup_seconds(aijhip_kspmpi_t K, double *seconds);
 int aijhip_kspmpi_destroy(aijhip_kspmpi_t K);

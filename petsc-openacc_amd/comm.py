@@ -48,6 +48,7 @@ MPI_SYMBOLS = (
     "aijhip_kspmpi_get_iteration_number", "aijhip_kspmpi_get_residual_norm", "aijhip_kspmpi_get_converged_reason",
     "aijhip_kspmpi_get_residual_history", "aijhip_kspmpi_get_host_syncs", "aijhip_kspmpi_destroy",
     "aijhip_comm_set_host_sendrecv", "aijhip_kspmpi_get_pc_levels", "aijhip_kspmpi_get_setup_seconds",
+    "aijhip_kspmpi_get_pc_level",
 )
 _bound = False
 
@@ -85,6 +86,8 @@ def _lib():
         L.aijhip_comm_set_host_sendrecv.argtypes = [_P, SENDRECV_FN]
         L.aijhip_kspmpi_get_pc_levels.argtypes = [_P, ctypes.POINTER(_i32), _P, _P, _i32]
         L.aijhip_kspmpi_get_setup_seconds.argtypes = [_P, ctypes.POINTER(_d)]
+        L.aijhip_kspmpi_get_pc_level.argtypes = [_P, _i32, ctypes.c_char, ctypes.POINTER(_i64), ctypes.POINTER(_i32),
+                                                 ctypes.POINTER(_i64), _P, _P, _P]
         _bound = True
     return L
 
@@ -335,6 +338,21 @@ class KSPCGMPINative:
     @property
     def setup_seconds(self) -> float:
         return self._get(_lib().aijhip_kspmpi_get_setup_seconds, _d)
+
+    def pc_level(self, l: int, which: str = "A"):
+        """This rank's rows of level l's operator ('A') or interpolation ('P')
+        of the distributed GAMG hierarchy: (rstart, ai, aj, aa) with global
+        columns."""
+        L = _lib()
+        r0, m, nnz = _i64(), _i32(), _i64()
+        _pkg._check(L.aijhip_kspmpi_get_pc_level(self._h, l, which.encode(), ctypes.byref(r0), ctypes.byref(m),
+                                                 ctypes.byref(nnz), None, None, None))
+        ai = np.zeros(m.value + 1, np.int64)
+        aj = np.zeros(max(nnz.value, 1), np.int64)
+        aa = np.zeros(max(nnz.value, 1))
+        _pkg._check(L.aijhip_kspmpi_get_pc_level(self._h, l, which.encode(), ctypes.byref(r0), ctypes.byref(m),
+                                                 ctypes.byref(nnz), ai.ctypes.data, aj.ctypes.data, aa.ctypes.data))
+        return r0.value, ai, aj[: nnz.value], aa[: nnz.value]
 
     def pc_levels(self):
         """(global rows, global entries) per level of the set-up PC

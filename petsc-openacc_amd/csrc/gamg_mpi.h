@@ -37,6 +37,10 @@ struct Hierarchy {
 
 // PCSetUp_GAMG over the distributed operator M0 (p2p halo). Collective.
 int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H);
+// This rank's rows of level l's operator ('A') or interpolation ('P') on the
+// host, columns in the global numbering of their level (tests).
+int get_level(const Hierarchy &H, int32_t l, char which, int64_t *rstart, int32_t *m, std::vector<int64_t> &ai,
+              std::vector<int64_t> &aj, std::vector<double> &aa);
 // One multiplicative V-cycle x = B b on `s` (every halo exchange is issued on
 // every rank whatever the stop flag says; the kernels return at once past it).
 int vcycle(Hierarchy &H, const double *b, double *x, hipStream_t s, const int *stop);

@@ -1110,6 +1110,52 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
     return rc;
 }
 
+// Rows of [Bd | Bo] on the host with global columns: Bd's column c -> doff +
+// c, Bo's column s -> ghost[s]; each row sorted by global column.
+int level_rows(const aijhip_mat *Bd, const aijhip_mat *Bo, int64_t doff, const std::vector<int64_t> &ghost,
+               std::vector<int64_t> &ai, std::vector<int64_t> &aj, std::vector<double> &aa) {
+    std::vector<int32_t> di, dj, oi, oj;
+    std::vector<double> da, oa;
+    int rc = host_full_rows(*Bd, di, dj, da);
+    if (!rc && Bo) rc = host_full_rows(*Bo, oi, oj, oa);
+    if (rc) return rc;
+    const int32_t m = Bd->m;
+    ai.assign((size_t)m + 1, 0);
+    aj.clear();
+    aa.clear();
+    std::vector<std::pair<int64_t, double>> row;
+    for (int32_t i = 0; i < m; ++i) {
+        row.clear();
+        for (int32_t k = di[i]; k < di[i + 1]; ++k) row.emplace_back(doff + dj[k], da[k]);
+        if (Bo)
+            for (int32_t k = oi[i]; k < oi[i + 1]; ++k) row.emplace_back(ghost[oj[k]], oa[k]);
+        std::sort(row.begin(), row.end(), [](const std::pair<int64_t, double> &a, const std::pair<int64_t, double> &b) {
+            return a.first < b.first;
+        });
+        for (auto &x : row) {
+            aj.push_back(x.first);
+            aa.push_back(x.second);
+        }
+        ai[i + 1] = (int64_t)aj.size();
+    }
+    return AIJHIP_OK;
+}
+
+int get_level(const Hierarchy &H, int32_t l, char which, int64_t *rstart, int32_t *m, std::vector<int64_t> &ai,
+              std::vector<int64_t> &aj, std::vector<double> &aa) {
+    if (l < 0 || l >= (int32_t)H.lv.size()) return mfail(AIJHIP_ERR_ARG, "no such level");
+    const Level &L = H.lv[l];
+    *rstart = L.rstart;
+    *m = L.m;
+    if (which == 'A') return level_rows(L.Ad, L.Ao, L.rstart, L.ghost_gid, ai, aj, aa);
+    if (which == 'P') {
+        if (l + 1 >= (int32_t)H.lv.size()) return mfail(AIJHIP_ERR_ARG, "the coarsest level has no interpolation");
+        const Level &N = H.lv[l + 1];
+        return level_rows(L.Pd, L.Po, N.rstart, N.ghost_gid, ai, aj, aa);
+    }
+    return mfail(AIJHIP_ERR_ARG, "which: 'A' or 'P'");
+}
+
 // y = B x (+ z) through the halo of `halo_op`: the exchange of x overlaps B_d x
 static int transfer(aijhip_mpiaij *halo_op, const aijhip_mat *Bd, const aijhip_mat *Bo, const double *x,
                     const double *z, double *y, bool add, hipStream_t s, const int *stop) {

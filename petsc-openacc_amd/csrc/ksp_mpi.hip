@@ -704,11 +704,13 @@ int kspmpi_set_up(aijhip_kspmpi *K) {
 
 // z = B r with the GAMG PC: the distributed hierarchy or the per-rank one.
 // *dots: the fused finest post-smoothing's z.z / z.r partials, or NULL.
-int pc_gamg_apply(aijhip_kspmpi *K, hipStream_t s, const double **dots, int *nbz) {
+// stop: CG's flag, NULL for the V-cycle before the first scalar step (the
+// device state is initialised by that step).
+int pc_gamg_apply(aijhip_kspmpi *K, hipStream_t s, const double **dots, int *nbz, const int *stop) {
     *dots = nullptr;
     *nbz = 0;
-    if (K->dh) return aijhip_gamg_mpi::vcycle(*K->dh, K->d_r, K->d_z, s, &K->d_state->done);
-    const hipError_t e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, dots, nbz, &K->d_state->done);
+    if (K->dh) return aijhip_gamg_mpi::vcycle(*K->dh, K->d_r, K->d_z, s, stop);
+    const hipError_t e = aijhip::ksp_pc_vcycle(K->sub, K->d_r, K->d_z, s, dots, nbz, stop);
     return e == hipSuccess ? AIJHIP_OK : mhip(e, "GAMG V-cycle");
 }
 
@@ -1034,7 +1036,7 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
     if (gamg) {  // z = B r, then its z.z, z.r partials (as ksp.hip with a zero guess)
         const double *dots = nullptr;
         int nbz = 0;
-        if ((rc = pc_gamg_apply(K, s, &dots, &nbz))) return rc;
+        if ((rc = pc_gamg_apply(K, s, &dots, &nbz, nullptr))) return rc;
         hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, nullptr);
     }
     hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 4, K->d_red, multi ? 0 : 1, K->d_state,
@@ -1079,7 +1081,7 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
             if (gamg) {  // z = B r; z.z and z.r from the fused finest post-smoothing, else k_dots
                 const double *dots = nullptr;
                 int nbz = 0;
-                if ((rc = pc_gamg_apply(K, s, &dots, &nbz))) return rc;
+                if ((rc = pc_gamg_apply(K, s, &dots, &nbz, &K->d_state->done))) return rc;
                 if (!dots) {
                     hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
                     dots = K->d_part;
@@ -1184,6 +1186,22 @@ int aijhip_kspmpi_get_pc_levels(aijhip_kspmpi_t K, int32_t *nlevels, int64_t *ro
     *nlevels = 1;
     if (cap > 0 && rows) rows[0] = K->M->mloc;
     if (cap > 0 && nnz) nnz[0] = K->M->Ad->nz + (K->M->Ao ? K->M->Ao->nz : 0);
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_pc_level(aijhip_kspmpi_t K, int32_t l, char which, int64_t *rstart, int32_t *m, int64_t *nnz,
+                               int64_t *ai, int64_t *aj, double *aa) {
+    if (!K || !rstart || !m || !nnz) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    if (!K->set_up || !K->dh) return mfail(AIJHIP_ERR_STATE, "no distributed GAMG hierarchy (set up a GAMG solve)");
+    DeviceGuard g(K->M->comm->device);
+    std::vector<int64_t> vi, vj;
+    std::vector<double> va;
+    const int rc = aijhip_gamg_mpi::get_level(*K->dh, l, which, rstart, m, vi, vj, va);
+    if (rc) return rc;
+    *nnz = (int64_t)vj.size();
+    if (ai) std::copy(vi.begin(), vi.end(), ai);
+    if (aj) std::copy(vj.begin(), vj.end(), aj);
+    if (aa) std::copy(va.begin(), va.end(), aa);
     return AIJHIP_OK;
 }
 

@@ -68,6 +68,9 @@ def _worker(rank, world, port, dims, pcs, env, q):
                 rows, nnz = k.pc_levels()
                 out[pc] = dict(x=x.cpu().numpy(), its=k.its, reason=k.reason, hist=k.hist.tolist(), rows=rows,
                                nnz=nnz, syncs=k.host_syncs)
+                if pc == "gamg" and (world > 1 or env):
+                    out[pc]["A"] = [k.pc_level(l, "A") for l in range(len(rows))]
+                    out[pc]["P"] = [k.pc_level(l, "P") for l in range(len(rows) - 1)]
         q.put((rank, out))
     except Exception as e:  # noqa: BLE001
         q.put((rank, {"error": repr(e)}))
@@ -124,6 +127,22 @@ def test_gpu_gamg_across_ranks_matches_oracle(world, dims):
     # exact arithmetic may round to a tiny value instead of 0 (then stored)
     for got_nnz, L in zip(g[0]["nnz"], levels):
         assert abs(got_nnz - L["A"].nnz) <= max(2, 0.002 * L["A"].nnz), (g[0]["nnz"], [L["A"].nnz for L in levels])
+    # the hierarchy itself, level by level, against the oracle's operators
+    def glue(parts, shape):
+        rows, cols, vals = [], [], []
+        for r0, ai, aj, aa in parts:
+            rows.append(r0 + np.repeat(np.arange(len(ai) - 1), np.diff(ai)))
+            cols.append(aj)
+            vals.append(aa)
+        return sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=shape)
+
+    for l, L in enumerate(levels):
+        Ag = glue([got[r]["gamg"]["A"][l] for r in range(world)], L["A"].shape)
+        scale = abs(L["A"]).max()
+        assert abs(Ag - L["A"]).max() <= 1e-12 * scale, (l, "A", abs(Ag - L["A"]).max(), scale)
+        if "P" in L:
+            Pg = glue([got[r]["gamg"]["P"][l] for r in range(world)], L["P"].shape)
+            assert abs(Pg - L["P"]).max() <= 1e-12 * abs(L["P"]).max(), (l, "P", abs(Pg - L["P"]).max())
     bj = got[0]["bjacobi_gamg"]["its"]
     print(f"\n{world} ranks {dims}: GAMG across ranks {g[0]['its']} its (oracle {its_o}), levels {g[0]['rows']}, "
           f"bjacobi+GAMG {bj} its, host syncs {g[0]['syncs']}")
