@@ -27,14 +27,15 @@ import scipy.sparse as sp
 from oracle import gamg as og
 
 
-def build(A, starts, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smooth_scale=1.4, eig_its=10):
-    """A: global operator; starts: row ownership (len = ranks + 1). Returns
-    a list of levels dict(A, P, starts, emax) in oracle/gamg.py's format
-    (vcycle-compatible)."""
+def build(A, starts, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smooth_scale=1.4, eig_its=10,
+          B=None):
+    """A: global operator; starts: row ownership (len = ranks + 1); B: the
+    near-null space (ones). Returns a list of levels dict(A, P, starts, emax,
+    agg, Bc) in oracle/gamg.py's format (vcycle-compatible)."""
     A = sp.csr_matrix(A)
     starts = np.asarray(starts, dtype=np.int64)
     levels = []
-    B = np.ones(A.shape[0])
+    B = np.ones(A.shape[0]) if B is None else np.asarray(B, dtype=np.float64)
     while len(levels) + 1 < max_levels and A.shape[0] > coarse_eq_limit:
         d = og.first_diagonal(A)
         dinv = 1.0 / np.where(d == 0.0, 1.0, d)
@@ -63,7 +64,7 @@ def build(A, starts, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=
         P.sort_indices()
         Ac = sp.csr_matrix(P.T @ (A @ P))
         Ac.sort_indices()
-        levels.append(dict(A=A, P=P, starts=starts, emax=emax, agg=agg))
+        levels.append(dict(A=A, P=P, starts=starts, emax=emax, agg=agg, Bc=Bc))
         A, B, starts = Ac, Bc, cstarts
     levels.append(dict(A=A, starts=starts))
     return levels

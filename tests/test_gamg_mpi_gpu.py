@@ -142,6 +142,7 @@ def test_gpu_gamg_across_ranks_matches_oracle(world, dims):
     # other aggregates where phase 2 compares strengths that are equal in
     # exact arithmetic and differ in their last bit.)
     nl = len(g[0]["rows"])
+    B = None  # the near-null space the device coarsens level l with (ones, then the Bc chain)
     for l in range(nl):
         parts = [got[r]["gamg"]["A"][l] for r in range(world)]
         n_l = g[0]["rows"][l]
@@ -151,7 +152,8 @@ def test_gpu_gamg_across_ranks_matches_oracle(world, dims):
         if l + 1 == nl:
             break
         starts = [p[0] for p in parts] + [n_l]
-        sub = ogm.build(Al, starts, max_levels=2, coarse_eq_limit=0)
+        sub = ogm.build(Al, starts, max_levels=2, coarse_eq_limit=0, B=B)
+        B = sub[0]["Bc"]
         n_c = g[0]["rows"][l + 1]
         assert sub[1]["A"].shape[0] == n_c, (l, sub[1]["A"].shape, n_c)
         Pg = glue([got[r]["gamg"]["P"][l] for r in range(world)], (n_l, n_c))
