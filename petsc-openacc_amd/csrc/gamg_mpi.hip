@@ -156,10 +156,9 @@ __global__ void k_rows_copy(int32_t n, const int32_t *__restrict__ rows, const i
     }
 }
 
-// C = A + B (rows sorted by column; a column in both: a + b). An exact zero
-// sum is not stored, as scipy's csr_matmat (and the single-GPU row products)
-// drop the zeros of a product row: the ranks' partial Galerkin sums of an
-// entry that cancels globally leave no explicit zero.
+// C = A + B (rows sorted by column; a column in both: a + b). Every
+// structural entry is kept, zero sums included, as the single-GPU row
+// products keep them (so one rank reproduces the single-GPU hierarchy).
 template <bool FILL>
 __device__ __forceinline__ int32_t add_row(int32_t i, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
                                            const double *__restrict__ aa, const int32_t *__restrict__ bi,
@@ -173,7 +172,6 @@ __device__ __forceinline__ int32_t add_row(int32_t i, const int32_t *__restrict_
         if (q >= qe || (p < pe && aj[p] < bj[q])) { c = aj[p]; v = aa[p]; ++p; }
         else if (p >= pe || bj[q] < aj[p]) { c = bj[q]; v = ba[q]; ++q; }
         else { c = aj[p]; v = aa[p] + ba[q]; ++p; ++q; }
-        if (v == 0.0) continue;
         if (FILL) { cj[o + n] = c; ca[o + n] = v; }
         ++n;
     }
