@@ -59,6 +59,33 @@ __global__ __launch_bounds__(T) void k_tile(int64_t n2, const double2 *__restric
     if (threadIdx.x == 0) out[blockIdx.x & 4095] = s;
 }
 
+// the STREAM shape with the tile moved by LDS-DMA (global_load_lds_dwordx4:
+// no VGPR destination), then read back from LDS; AUX 2 = non-temporal
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void glob_void;
+template <int T, int U, int AUX>
+__global__ __launch_bounds__(T) void k_tile_glds(int64_t n2, const double2 *__restrict__ v, double *out) {
+    __shared__ double2 buf[T * U];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t base = (int64_t)blockIdx.x * T * U;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * T + w * 64 + lane;
+        const double2 *src = v + (i < n2 ? i : n2 - 1);
+        __builtin_amdgcn_global_load_lds((glob_void *)src, (lds_void *)&buf[u * T + w * 64], 16, 0, AUX);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const double2 r = buf[u * T + threadIdx.x];
+        s += r.x + r.y;
+    }
+    s = block_sum<T>(s);
+    if (threadIdx.x == 0) out[blockIdx.x & 4095] = s;
+}
+
 // persistent grid-stride, U loads in flight per lane
 template <int T, int U>
 __global__ __launch_bounds__(T) void k_stride(int64_t n2, const double2 *__restrict__ v, double *out) {
@@ -131,6 +158,13 @@ int main(int argc, char **argv) {
     TILE(512, 2, true); TILE(512, 4, true); TILE(512, 8, true);
     TILE(1024, 1, true); TILE(1024, 2, false); TILE(1024, 4, false); TILE(1024, 8, false); TILE(1024, 2, true);
     TILE(1024, 4, true);
+#define GLDS(T, U, AUX)                                                                                     \
+    report("glds T=" #T " U=" #U " aux=" #AUX, time_us([&] {                                                \
+               hipLaunchKernelGGL((k_tile_glds<T, U, AUX>), dim3((unsigned)((n2 + T * U - 1) / (T * U))), dim3(T), \
+                                  0, nullptr, n2, v, out);                                                   \
+           }, 20))
+    GLDS(512, 2, 0); GLDS(512, 4, 0); GLDS(512, 2, 2); GLDS(512, 4, 2); GLDS(256, 4, 2); GLDS(256, 8, 2);
+    GLDS(512, 8, 2); GLDS(1024, 2, 2);
 #define STRIDE(T, U, W)                                                                                      \
     report("stride T=" #T " U=" #U " wg/CU=" #W, time_us([&] {                                              \
                hipLaunchKernelGGL((k_stride<T, U>), dim3(cus * W), dim3(T), 0, nullptr, n2, v, out);          \
