@@ -8,10 +8,10 @@ OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd "$ROOT" || exit 1
 export TMPDIR=/tmp
-timeout -k 10 120 tools/read_sweep > "$OUT/read_sweep.jsonl" 2>&1 || { tail -5 "$OUT/read_sweep.jsonl"; exit 1; }
-grep -E "glds|T=512 U=2 nt=true|T=512 U=4 nt=false" "$OUT/read_sweep.jsonl"
+true
+true
 export MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 RANK=0 WORLD_SIZE=1 LOCAL_RANK=0
-for P in 37 38; do
+for P in 37 38 300; do
   timeout -k 10 300 python3 -u tools/slab_probe.py --planes $P > "$OUT/slab_$P.json" 2> "$OUT/slab_$P.err" || { tail -20 "$OUT/slab_$P.err"; exit 1; }
   cat "$OUT/slab_$P.json"
 done

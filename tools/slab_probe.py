@@ -70,7 +70,7 @@ def main():
     nb = pkg.algorithmic_bytes(m, m, len(daj))
     out["A_d_us"] = {"median": round(med, 2), "mean": round(mean, 2), "GBs": round(nb / (med * 1e-6) / 1e9, 1)}
     med, mean = med_us(lambda: A_o.mult_add(g, y, y, s), s)
-    out["A_o_multadd_us"] = {"median": round(med, 2), "mean": round(mean, 2), "compressed": A_o.info()["compressed"]}
+    out["A_o_multadd_us"] = {"median": round(med, 2), "mean": round(mean, 2), "info": {k: v for k, v in A_o.info().items() if k in ("m", "nz", "kernel", "n_blocks")}}
     idx = torch.from_numpy(np.concatenate([np.arange(G * G), np.arange(m - G * G, m)])).to(dev)
     buf = torch.empty(2 * G * G, dtype=torch.float64, device=dev)
     med, mean = med_us(lambda: torch.index_select(x, 0, idx, out=buf), s)
