@@ -239,6 +239,22 @@ __global__ __launch_bounds__(256) void k_mg_richardson(int64_t n, const double *
         x[i] = x[i] + 1.0 * (dinv[i] * (b[i] + (-1.0) * ax[i]));
 }
 
+// y[o] = y[o] + scale[o] * (-(A_o g)_o) over A_o's rows (scale NULL: 1): the
+// off-diagonal block's share of a fused residual (r = b - A_d x - A_o g) or
+// post-smoothing (x = t + D^-1 (b - A_d t - A_o g)) on the boundary rows
+__global__ __launch_bounds__(256) void k_offdiag_axpy(int32_t nr, const int32_t *__restrict__ rai,
+                                                      const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
+                                                      const double *__restrict__ aa, const double *__restrict__ g,
+                                                      const double *__restrict__ scale, double *y, const int *stop) {
+    if (stop && *stop) return;
+    for (int32_t q = blockIdx.x * 256 + threadIdx.x; q < nr; q += gridDim.x * 256) {
+        const int32_t o = ridx ? ridx[q] : q;
+        double sum = 0.0;
+        for (int32_t k = rai[q]; k < rai[q + 1]; ++k) sum += aa[k] * g[aj[k]];
+        y[o] = y[o] + (scale ? scale[o] : 1.0) * (-sum);
+    }
+}
+
 // ---------------------------------------------------------------- host side
 int gerr(hipError_t e, const char *what) { return mhip(e, (std::string("distributed GAMG: ") + what).c_str()); }
 
@@ -968,7 +984,7 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
             if (!rc) rc = aijhip_mpi::comm_sendrecv(C, out, in);
             // received (row, col, value) for own rows, in (peer, message) order
             struct Trip {
-                int32_t r;
+                int32_t r, cu;  // own coarse row; column in the unified numbering (set below)
                 int64_t c;
                 double v;
             };
@@ -999,16 +1015,16 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
                 if (gidc >= cstart && gidc < cstart + na) return (int32_t)(gidc - cstart);
                 return na + (int32_t)(std::lower_bound(gnew.begin(), gnew.end(), gidc) - gnew.begin());
             };
-            std::stable_sort(trips.begin(), trips.end(), [&](const Trip &a, const Trip &b) {
-                if (a.r != b.r) return a.r < b.r;
-                return u_id(a.c) < u_id(b.c);
+            for (Trip &t : trips) t.cu = u_id(t.c);
+            std::stable_sort(trips.begin(), trips.end(), [](const Trip &a, const Trip &b) {
+                return a.r != b.r ? a.r < b.r : a.cu < b.cu;
             });
             std::vector<int32_t> cnt((size_t)na, 0);
             for (size_t k = 0; k < trips.size();) {
                 size_t j = k;
                 double v = 0.0;
-                const int32_t cu = u_id(trips[k].c);
-                while (j < trips.size() && trips[j].r == trips[k].r && u_id(trips[j].c) == cu) v += trips[j++].v;
+                const int32_t cu = trips[k].cu;
+                while (j < trips.size() && trips[j].r == trips[k].r && trips[j].cu == cu) v += trips[j++].v;
                 ++cnt[trips[k].r];
                 corr_j.push_back(cu);
                 corr_a.push_back(v);
@@ -1168,31 +1184,71 @@ static int transfer(aijhip_mpiaij *halo_op, const aijhip_mat *Bd, const aijhip_m
     return AIJHIP_OK;
 }
 
+// The A_o correction of a fused smoothing launch (after the halo landed).
+static int offdiag_axpy(const Level &L, const double *scale, double *y, hipStream_t s, const int *stop) {
+    if (!L.Ao) return AIJHIP_OK;
+    const aijhip::RowList R = aijhip::row_list(*L.Ao);
+    if (R.nr == 0) return AIJHIP_OK;
+    hipLaunchKernelGGL(k_offdiag_axpy, dim3(nblk(R.nr)), dim3(256), 0, s, R.nr, R.rai, R.ridx, L.Ao->d_aj,
+                       L.Ao->d_aa, L.op->d_ghost, scale, y, stop);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? AIJHIP_OK : gerr(e, "off-diagonal smoothing share");
+}
+
 int vcycle(Hierarchy &H, const double *b0, double *x0, hipStream_t s, const int *stop) {
     const int nl = (int)H.lv.size();
     auto B = [&](int l) { return l == 0 ? b0 : (const double *)H.lv[l].b; };
     auto X = [&](int l) { return l == 0 ? x0 : H.lv[l].x; };
     auto grid = [](int64_t n) { return dim3((unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 2048))); };
+    // smoothing SpMVs fused with their vector passes on STREAM-planned blocks
+    // (ksp.hip's launch_mg_resid / launch_mg_post over A_d while the halo
+    // moves, then A_o's share on the boundary rows); AIJHIP_MG_UNFUSED=1 for A/B
+    static const bool unfused = std::getenv("AIJHIP_MG_UNFUSED") != nullptr;
+    auto fused = [&](const Level &L) { return !unfused && aijhip::stream_mg_fusable(*L.Ad); };
+    auto exchanges = [](const aijhip_mpiaij *M) { return M->n_send > 0 || M->n_ghost > 0; };
     int rc;
+    hipError_t e;
     for (int l = 0; l < nl; ++l) {
         Level &L = H.lv[l];
         hipLaunchKernelGGL(k_mg_jacobi, grid(L.m), dim3(256), 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
         if (l == nl - 1) break;  // coarse: preonly + Jacobi
-        // r = b - A x (MatMult_MPIAIJ, then the residual)
-        if ((rc = aijhip_mpi::mpiaij_apply(L.op, X(l), L.r, s, nullptr, nullptr, nullptr, false, stop))) return rc;
-        hipLaunchKernelGGL(k_mg_resid, grid(L.m), dim3(256), 0, s, (int64_t)L.m, B(l), L.r, stop);
+        // r = b - A x
+        if (fused(L)) {
+            const bool ex = exchanges(L.op);
+            if (ex && (rc = aijhip_mpi::halo_post(L.op, X(l), s))) return rc;
+            if ((e = aijhip::launch_mg_resid(*L.Ad, X(l), B(l), L.r, s, true, stop)) != hipSuccess)
+                return gerr(e, "residual");
+            if (ex && (rc = aijhip_mpi::halo_finish(L.op, s))) return rc;
+            if ((rc = offdiag_axpy(L, nullptr, L.r, s, stop))) return rc;
+        } else {  // MatMult_MPIAIJ, then the residual
+            if ((rc = aijhip_mpi::mpiaij_apply(L.op, X(l), L.r, s, nullptr, nullptr, nullptr, false, stop))) return rc;
+            hipLaunchKernelGGL(k_mg_resid, grid(L.m), dim3(256), 0, s, (int64_t)L.m, B(l), L.r, stop);
+        }
         // MatRestrict: b_{l+1} = P^T r = P_d^T r + R_o r_ghost
         if ((rc = transfer(L.op, L.Pd->transpose, L.Ro, L.r, nullptr, H.lv[l + 1].b, false, s, stop))) return rc;
     }
     for (int l = nl - 2; l >= 0; --l) {
         Level &L = H.lv[l];
-        // MatInterpolateAdd: x = x + P x_c (P_d x_c + P_o x_c ghost)
-        if ((rc = transfer(H.lv[l + 1].op, L.Pd, L.Po, X(l + 1), X(l), X(l), true, s, stop))) return rc;
-        // smoothu: x = x + D^-1 (b - A x)
-        if ((rc = aijhip_mpi::mpiaij_apply(L.op, X(l), L.r, s, nullptr, nullptr, nullptr, false, stop))) return rc;
-        hipLaunchKernelGGL(k_mg_richardson, grid(L.m), dim3(256), 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l), stop);
+        if (fused(L)) {
+            // MatInterpolateAdd into the scratch: t = x + P x_c, then smoothu
+            // x = t + D^-1 (b - A t) in the SpMV epilogue over A_d
+            if ((rc = transfer(H.lv[l + 1].op, L.Pd, L.Po, X(l + 1), X(l), L.r, true, s, stop))) return rc;
+            const bool ex = exchanges(L.op);
+            if (ex && (rc = aijhip_mpi::halo_post(L.op, L.r, s))) return rc;
+            if ((e = aijhip::launch_mg_post(*L.Ad, L.r, B(l), L.dinv, X(l), nullptr, s, true, stop)) != hipSuccess)
+                return gerr(e, "post-smoothing");
+            if (ex && (rc = aijhip_mpi::halo_finish(L.op, s))) return rc;
+            if ((rc = offdiag_axpy(L, L.dinv, X(l), s, stop))) return rc;
+        } else {
+            // MatInterpolateAdd: x = x + P x_c (P_d x_c + P_o x_c ghost)
+            if ((rc = transfer(H.lv[l + 1].op, L.Pd, L.Po, X(l + 1), X(l), X(l), true, s, stop))) return rc;
+            // smoothu: x = x + D^-1 (b - A x)
+            if ((rc = aijhip_mpi::mpiaij_apply(L.op, X(l), L.r, s, nullptr, nullptr, nullptr, false, stop))) return rc;
+            hipLaunchKernelGGL(k_mg_richardson, grid(L.m), dim3(256), 0, s, (int64_t)L.m, L.dinv, B(l), L.r, X(l),
+                               stop);
+        }
     }
-    const hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     return e == hipSuccess ? AIJHIP_OK : gerr(e, "V-cycle");
 }
 
