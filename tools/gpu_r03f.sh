@@ -17,4 +17,4 @@ timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run -
     && echo "prof ok" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
 timeout -k 10 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_ANY SQ_WAIT_INST_ANY \
     SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES --output-format csv -d "$OUT/sq_skewed" -o run \
-    -- python3 tools/prof_case.py skewed --its 20 > "$OUT/sq_skewed.log" 2>&1 && echo "sq ok"
+    -- python3 tools/prof_case.py skewed --its 20 > "$OUT/sq_skewed.log" 2>&1 && echo "sq ok" && timeout -k 10 300 python3 tools/tune.py --matrix skewed --variants skewgeom --rounds 3 > "$OUT/skewgeom.jsonl" 2>&1 && grep us_median "$OUT/skewgeom.jsonl" | head -8
