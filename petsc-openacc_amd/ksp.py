@@ -242,7 +242,7 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
         ksp.solve(b, x)
         torch.cuda.synchronize()
         t_solve = time.perf_counter() - t0
-        its, reason, rnorm = ksp.its, ksp.reason, ksp.rnorm
+        its, reason, rnorm, syncs = ksp.its, ksp.reason, ksp.rnorm, ksp.host_syncs
     err = float((x.cpu() - torch.from_numpy(exact)).abs().max())
     # the same set-up again in this process (a caller that rebuilds the
     # hierarchy after new values): the first one above also pays one-time
@@ -256,7 +256,7 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
     return {"its": its, "reason": reason, "rnorm": rnorm, "max_err": err,
             "setup_s": round(t_setup, 3), "setup_again_s": round(t_again, 3), "setup_pc_s": round(t_host, 3),
             "solve_s": round(t_solve, 4), "first_solve_s": round(t_first, 4),
-            "ms_per_iter": round(t_solve / max(its, 1) * 1e3, 4),
+            "ms_per_iter": round(t_solve / max(its, 1) * 1e3, 4), "host_syncs": syncs,
             "time_to_solution_s": round(t_setup + t_solve, 3),
             "levels": [{"rows": r, "nnz": z} for r, z in zip(rows, nnz)],
             "options": "cg, gamg agg nsmooths 1 threshold 0, mg levels richardson(1)+jacobi, "
