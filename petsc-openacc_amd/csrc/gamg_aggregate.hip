@@ -413,7 +413,15 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     // kernels wrote si/sj: drain it first, so the sweep's reads are ordered
     // after their producers explicitly
     hipError_t e = hipStreamSynchronize(nullptr);
+    auto mark = [&](const char *what) {
+        if (!log) return;
+        const auto now = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "  phase 1 sweep %-10s %8.3f ms (host)\n", what,
+                     std::chrono::duration<double, std::milli>(now - clk).count());
+    };
+    mark("drained");
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    mark("stream");
     if (e == hipSuccess) e = dalloc(&state, m);
     if (e == hipSuccess) e = dalloc(&cnt, m);
     if (e == hipSuccess) e = dalloc(&roots, m);
@@ -422,6 +430,7 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     if (e == hipSuccess) e = dalloc(&rstart, (int64_t)max_rounds + kBatch + 2);
     if (e == hipSuccess) e = dalloc(&ostart, (int64_t)max_rounds + kBatch + 2);
     if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_ctl), sizeof(unsigned) * 4);
+    mark("allocs");
     if (e == hipSuccess) e = hipMemsetAsync(tails, 0, sizeof(unsigned) * 4, s);
     if (e == hipSuccess) e = hipMemsetAsync(rstart, 0, sizeof(unsigned), s);
     if (e == hipSuccess) e = hipMemsetAsync(ostart, 0, sizeof(unsigned), s);
@@ -430,6 +439,7 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
         hipLaunchKernelGGL(k_lf_seed, dim3(g), dim3(256), 0, s, m, state, cnt, roots, tails);
         e = hipGetLastError();
     }
+    mark("launched");
     auto lap = [&](const char *what) {
         if (!log) return;
         (void)hipStreamSynchronize(s);

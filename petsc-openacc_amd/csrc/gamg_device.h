@@ -3,6 +3,9 @@
 #pragma once
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "aijhip_internal.h"
@@ -25,7 +28,14 @@ struct DCsr {
 
 template <class T>
 hipError_t dalloc(T **p, int64_t count) {
-    return hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * (size_t)std::max<int64_t>(count, 1));
+    static const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    const size_t bytes = sizeof(T) * (size_t)std::max<int64_t>(count, 1);
+    if (!log) return hipMalloc(reinterpret_cast<void **>(p), bytes);
+    const auto t0 = std::chrono::steady_clock::now();
+    const hipError_t e = hipMalloc(reinterpret_cast<void **>(p), bytes);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > 1.0) std::fprintf(stderr, "  slow hipMalloc %.1f MB: %.2f ms\n", bytes / 1e6, ms);
+    return e;
 }
 
 // One level of the device hierarchy.

@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -710,6 +711,154 @@ __global__ __launch_bounds__(256) void k_rowprod_wave(int32_t m, const int32_t *
     }
 }
 
+// The same product, G lanes per output row sharing an LDS hash table of T
+// column slots (round 3). The row's terms a_ik are taken in order; for each,
+// the G lanes cover B row k's entries side by side, each adding its product
+// to its column's slot. A row of B holds every column once, so no two lanes
+// of one step touch the same slot, and the steps run in k order (the group
+// is one wavefront's lanes, whose LDS operations complete in program order):
+// per column, the sum runs in traversal order from 0.0, as with one lane
+// alone — the same bits. Keys are claimed with an LDS compare-and-swap and
+// linear probing; values need no atomics. A_i's terms come in chunks of G
+// (one lane each: a_ik, k and B row k's extent) and are broadcast by shuffle.
+// Count mode: cnt[i] = distinct columns, or -1 when the table could pass T
+// (checked against an upper bound, recounted exactly only when it says so);
+// klass[i] = myclass when it fits. Write mode: the rows of myclass, their
+// keys compacted and ranked (sorted columns) and written with the sums.
+template <int G, int T, int NG, bool WRITE>
+__global__ __launch_bounds__(G *NG) void k_rowprod_hash(int32_t m, const int32_t *__restrict__ ai,
+                                                        const int32_t *__restrict__ aj,
+                                                        const double *__restrict__ aa,
+                                                        const int32_t *__restrict__ bi,
+                                                        const int32_t *__restrict__ bj,
+                                                        const double *__restrict__ ba, const int32_t *__restrict__ ci,
+                                                        int32_t *cj, double *ca, int32_t *cnt, int32_t *klass,
+                                                        int32_t myclass, bool redo, bool pipe) {
+    static_assert(G >= 1 && G <= 64 && 64 % G == 0, "a group lies within one wavefront");
+    static_assert((T & (T - 1)) == 0 && T >= 2 * G, "power-of-two table, at least two slots per lane");
+    constexpr int LOGT = __builtin_ctz(T);
+    __shared__ int32_t s_key[NG * T];
+    __shared__ double s_val[WRITE ? NG * T : 1];
+    __shared__ int32_t s_ck[WRITE ? NG * T : 1];
+    const int g = threadIdx.x / G, l = threadIdx.x % G;
+    const int gbase = (threadIdx.x & 63) - l;  // the group's first lane within the wavefront
+    int32_t *key = s_key + g * T;
+    double *val = s_val + (WRITE ? g * T : 0);
+    int32_t *ck = s_ck + (WRITE ? g * T : 0);
+    auto group_sum = [&](int v) {
+#pragma unroll
+        for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        return v;
+    };
+    for (int64_t i = (int64_t)blockIdx.x * NG + g; i < m; i += (int64_t)gridDim.x * NG) {
+        if (!WRITE && redo && cnt[i] >= 0) continue;  // counted by a smaller class
+        if (WRITE && klass[i] != myclass) continue;    // another class's row
+        for (int s = l; s < T; s += G) {
+            key[s] = -1;
+            if (WRITE) val[s] = 0.0;
+        }
+        __builtin_amdgcn_wave_barrier();
+        int mine = 0;     // keys this lane claimed
+        int bound = 0;    // (group-uniform) at least the keys in the table
+        bool over = false;
+        const int32_t k1 = ai[i + 1];
+        for (int32_t kc = ai[i]; kc < k1 && !over; kc += G) {
+            int32_t q0 = 0, q1 = 0;
+            double a = 0.0;
+            if (kc + l < k1) {
+                const int32_t j = aj[kc + l];
+                if (WRITE) a = aa[kc + l];
+                q0 = bi[j];
+                q1 = bi[j + 1];
+            }
+            const int nk = min(G, k1 - kc);
+            auto insert = [&](int32_t c, double p) {
+                uint32_t h = ((uint32_t)c * 0x9E3779B1u) >> (32 - LOGT);
+                for (;;) {
+                    const int32_t old = atomicCAS(&key[h], -1, c);
+                    if (old == -1) {
+                        ++mine;
+                        break;
+                    }
+                    if (old == c) break;
+                    h = (h + 1) & (T - 1);
+                }
+                if (WRITE) val[h] += p;
+            };
+            // B row k's first G entries are loaded one step ahead (software
+            // pipelined: the next row's load in flight while this one's
+            // products go into the table; the LDS order is unchanged)
+            int32_t nb0 = __shfl(q0, gbase, 64), nb1 = __shfl(q1, gbase, 64);
+            double nav = WRITE ? __shfl(a, gbase, 64) : 0.0;
+            int32_t nc = -1;
+            double nv = 0.0;
+            if (pipe && nb0 + l < nb1) {
+                nc = bj[nb0 + l];
+                if (WRITE) nv = ba[nb0 + l];
+            }
+            for (int t = 0; t < nk; ++t) {
+                const int32_t b0 = nb0, b1 = nb1, c0 = nc;
+                const double av = nav, v0 = nv;
+                if (t + 1 < nk) {
+                    nb0 = __shfl(q0, gbase + t + 1, 64);
+                    nb1 = __shfl(q1, gbase + t + 1, 64);
+                    if (WRITE) nav = __shfl(a, gbase + t + 1, 64);
+                    nc = -1;
+                    if (pipe && nb0 + l < nb1) {
+                        nc = bj[nb0 + l];
+                        if (WRITE) nv = ba[nb0 + l];
+                    }
+                }
+                const int len = b1 - b0;
+                if (bound + len > T - 1) {  // the table could fill: count exactly
+                    bound = group_sum(mine);
+                    if (bound + len > T - 1) {
+                        over = true;
+                        break;
+                    }
+                }
+                bound += len;
+                // (pipelined: the first entry came with the previous step)
+                if (pipe && c0 >= 0) insert(c0, WRITE ? av * v0 : 0.0);
+                for (int32_t q = b0 + l + (pipe ? G : 0); q < b1; q += G) insert(bj[q], WRITE ? av * ba[q] : 0.0);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (!WRITE) {
+            const int tot = group_sum(mine);
+            if (l == 0) {
+                cnt[i] = over ? -1 : tot;
+                if (!over) klass[i] = myclass;
+            }
+            __builtin_amdgcn_wave_barrier();  // the table is cleared for the group's next row
+            continue;
+        }
+        // compact the keys, rank each against them (sorted columns), write
+        const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1ull);
+        const unsigned long long below = (1ull << l) - 1ull;
+        int n = 0;
+        for (int s0 = 0; s0 < T; s0 += G) {
+            const int32_t c = key[s0 + l];
+            const bool occ = c != -1;
+            const unsigned long long b = (__ballot(occ) >> gbase) & gmask;
+            if (occ) ck[n + __popcll(b & below)] = c;
+            n += __popcll(b);
+        }
+        __builtin_amdgcn_wave_barrier();
+        const int32_t o = ci[i];
+        for (int s0 = 0; s0 < T; s0 += G) {
+            const int32_t c = key[s0 + l];
+            if (c != -1) {
+                int r = 0;
+                for (int z = 0; z < n; ++z) r += ck[z] < c;
+                cj[o + r] = c;
+                ca[o + r] = val[s0 + l];
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
 // P = alpha (D^-1 T) + P0 on the union pattern (gamg_setup.cpp prolongator):
 // lengths, then entries.
 __global__ void k_prolong_len(int32_t m, const int32_t *__restrict__ ti, const int32_t *__restrict__ tj,
@@ -798,6 +947,62 @@ hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *kla
 constexpr int kProdClasses = 5;
 constexpr int kProdClassCols[kProdClasses] = {32, 64, 128, 256, 256};
 
+// The hash-table classes (k_rowprod_hash): table sizes tried in order; a
+// row counted -1 at one size is recounted at the next. Groups per workgroup:
+// at least a wavefront, at most 256 lanes and 64 KiB of LDS (16 B per slot
+// in the numeric pass).
+constexpr int kHashClasses = 6;
+constexpr int kHashT[kHashClasses] = {16, 32, 64, 128, 256, 1024};
+constexpr int kHashClassId = 16;  // klass ids kHashClassId + t (the lane classes use 0..4)
+
+template <int G, int T>
+constexpr int hash_groups() {
+    return std::max(64 / G, std::min(256 / G, 65536 / (16 * T)));
+}
+
+template <int G, int T>
+hipError_t rowprod_hash_pass(const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, int32_t myclass, bool redo,
+                             const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
+    constexpr int NG = hash_groups<G, T>();
+    static_assert(NG * T * 16 <= 65536, "LDS per workgroup");
+    const unsigned grid = (unsigned)std::min<int64_t>(blocks_for(A.m, NG), (int64_t)n_cu * 32);
+    static const bool pipe = [] {
+        const char *v = std::getenv("AIJHIP_GAMG_HASH_PIPE");
+        return !(v && v[0] == '0');
+    }();
+    if (!numeric)
+        hipLaunchKernelGGL((k_rowprod_hash<G, T, NG, false>), dim3(grid), dim3(G * NG), 0, nullptr, A.m, A.ai, A.aj,
+                           A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, klass, myclass, redo, pipe);
+    else
+        hipLaunchKernelGGL((k_rowprod_hash<G, T, NG, true>), dim3(grid), dim3(G * NG), 0, nullptr, A.m, A.ai, A.aj,
+                           A.aa, B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, klass, myclass, false, pipe);
+    return hipGetLastError();
+}
+
+// lanes per row for table t given the preferred G (at most half the table;
+// at least 16 for the largest table, whose groups would not fit otherwise)
+int hash_lanes(int G, int t) {
+    const int T = kHashT[t];
+    if (G > T / 2) G = T / 2;
+    if (T == 1024 && G < 16) G = 16;
+    return G;
+}
+
+hipError_t rowprod_hash_class(int t, int G, const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, bool redo,
+                              const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
+    const int id = kHashClassId + t;
+#define AIJHIP_HASH(GG, TT)                                                                                   \
+    if (G == GG && kHashT[t] == TT) return rowprod_hash_pass<GG, TT>(A, B, cnt, klass, id, redo, ci, C, numeric, n_cu)
+    AIJHIP_HASH(4, 16); AIJHIP_HASH(8, 16); AIJHIP_HASH(4, 32); AIJHIP_HASH(8, 32); AIJHIP_HASH(16, 32);
+    AIJHIP_HASH(4, 64); AIJHIP_HASH(4, 128); AIJHIP_HASH(4, 256);
+    AIJHIP_HASH(8, 64); AIJHIP_HASH(8, 128); AIJHIP_HASH(8, 256);
+    AIJHIP_HASH(16, 64); AIJHIP_HASH(16, 128); AIJHIP_HASH(16, 256); AIJHIP_HASH(16, 1024);
+    AIJHIP_HASH(32, 64); AIJHIP_HASH(32, 128); AIJHIP_HASH(32, 256); AIJHIP_HASH(32, 1024);
+    AIJHIP_HASH(64, 128); AIJHIP_HASH(64, 256); AIJHIP_HASH(64, 1024);
+#undef AIJHIP_HASH
+    return hipErrorInvalidValue;
+}
+
 hipError_t rowprod_class(int c, const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, bool redo,
                          const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
     switch (c) {
@@ -809,6 +1014,30 @@ hipError_t rowprod_class(int c, const DCsr &A, const DCsr &B, int32_t *cnt, int3
     }
 }
 
+// AIJHIP_GAMG_HASH=0: the round-2 product forms (lane per row, wavefront
+// per row for small A) instead of the hash-table groups; the same bits
+bool hash_off() {
+    const char *v = std::getenv("AIJHIP_GAMG_HASH");
+    return v && v[0] == '0';
+}
+
+// the minimum of cnt[0..m) (0 when m = 0)
+hipError_t min_of(const int32_t *cnt, int32_t m, int32_t *mn) {
+    *mn = 0;
+    if (m == 0) return hipSuccess;
+    void *tmp = nullptr;
+    size_t tb = 0;
+    int32_t *dmin = nullptr;
+    hipError_t r;
+    if ((r = dalloc(&dmin, 1)) == hipSuccess && (r = hipcub::DeviceReduce::Min(nullptr, tb, cnt, dmin, m)) == hipSuccess &&
+        (r = hipMalloc(&tmp, std::max<size_t>(tb, 1))) == hipSuccess &&
+        (r = hipcub::DeviceReduce::Min(tmp, tb, cnt, dmin, m)) == hipSuccess)
+        r = hipMemcpy(mn, dmin, sizeof(int32_t), hipMemcpyDeviceToHost);
+    hipFree(tmp);
+    hipFree(dmin);
+    return r;
+}
+
 int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nullptr) {
     C = DCsr();
     C.m = A.m;
@@ -817,7 +1046,7 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
     hipError_t e;
     if ((e = dalloc(&cnt, A.m)) != hipSuccess) return herr(e, "product counts");
     // products per row (mean): A's row length x B's
-    double per_row = 0.0;
+    double per_row = 0.0, b_row = 0.0;
     {
         int32_t bnz = 0;
         if ((e = hipMemcpy(&bnz, B.ai + B.m, sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess) {
@@ -825,6 +1054,74 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
             return herr(e, "product sizes");
         }
         per_row = B.m > 0 ? (double)A.nz * ((double)bnz / (double)B.m) / std::max<int32_t>(A.m, 1) : 0.0;
+        b_row = B.m > 0 ? (double)bnz / (double)B.m : 0.0;
+    }
+    if (!hash_off()) {
+        // G lanes per row: B's mean row length rounded up to a power of two
+        int G = 4;
+        while (G < 64 && G < b_row) G <<= 1;
+        if (const char *v = std::getenv("AIJHIP_GAMG_HASH_G")) G = std::max(4, std::min(64, std::atoi(v)));
+        const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        int32_t *klass = nullptr;
+        auto bail = [&](hipError_t r, const char *what) {
+            hipFree(cnt);
+            hipFree(klass);
+            C.release();
+            return herr(r, what);
+        };
+        if ((e = dalloc(&klass, A.m)) != hipSuccess) return bail(e, "product classes");
+        // the first table: the smallest above the mean products per row
+        // (their bound on the distinct columns), at most 64 slots; rows that
+        // overflow it are recounted with the next
+        int first = 0;
+        while (first + 1 < kHashClasses && kHashT[first] <= std::min(per_row, 48.0)) ++first;
+        if (const char *v = std::getenv("AIJHIP_GAMG_HASH_T0")) first = std::max(0, std::min(kHashClasses - 1, std::atoi(v)));
+        int last = -1;
+        for (int t = first; t < kHashClasses; ++t) {
+            if ((e = rowprod_hash_class(t, hash_lanes(G, t), A, B, cnt, klass, t > first, nullptr, nullptr, false,
+                                        n_cu)) != hipSuccess)
+                return bail(e, "symbolic product");
+            int32_t mn = 0;
+            if ((e = min_of(cnt, A.m, &mn)) != hipSuccess) return bail(e, "symbolic product");
+            if (mn >= 0) {
+                last = t;
+                break;
+            }
+        }
+        if (last < 0) {  // a row past the largest table: the host builder takes the level
+            hipFree(cnt);
+            hipFree(klass);
+            return AIJHIP_ERR_STATE;
+        }
+        if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) return bail(e, "product rows");
+        int64_t total = 0;
+        if ((e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess) return bail(e, "scan");
+        if (total > INT32_MAX) {
+            hipFree(cnt);
+            hipFree(klass);
+            C.release();
+            set_error("GAMG device set-up: product exceeds int32 indices");
+            return AIJHIP_ERR_ARG;
+        }
+        C.nz = total;
+        if ((e = dalloc(&C.aj, total + 2)) != hipSuccess || (e = dalloc(&C.aa, total + 2)) != hipSuccess ||
+            (e = hipMemset(C.aj + total, 0, 2 * sizeof(int32_t))) != hipSuccess ||
+            (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess)
+            return bail(e, "product alloc");
+        for (int t = first; t <= last && e == hipSuccess; ++t)
+            e = rowprod_hash_class(t, hash_lanes(G, t), A, B, cnt, klass, false, C.ai, &C, true, n_cu);
+        if (e != hipSuccess) return bail(e, "numeric product");
+        hipFree(cnt);
+        hipFree(klass);
+        if (cols_used) *cols_used = std::max(*cols_used, kHashT[last]);
+        if (log) {
+            (void)hipDeviceSynchronize();
+            std::fprintf(stderr, "  product %d x %d: %.0f products per row, B rows %.1f -> hash, %d lanes, "
+                         "tables %d-%d: %.2f ms\n", A.m, B.n, per_row, b_row, G, kHashT[first], kHashT[last],
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3);
+        }
+        return AIJHIP_OK;
     }
     constexpr int kWaveK = 16;  // columns per lane: up to 1024 per row
     const unsigned gw = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.m + 3) / 4, (int64_t)n_cu * 16));
@@ -1198,6 +1495,15 @@ struct EmaxJob {
     double *v = nullptr, *w = nullptr, *part = nullptr;
     void start(const aijhip_mat &A, const double *dinv, int its) {
         th = std::thread([this, &A, dinv, its] {
+            const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+            auto c0 = std::chrono::steady_clock::now();
+            auto mark = [&](const char *what) {
+                if (!log) return;
+                const auto now = std::chrono::steady_clock::now();
+                std::fprintf(stderr, "  emax job %-12s %8.3f ms\n", what,
+                             std::chrono::duration<double, std::milli>(now - c0).count());
+                c0 = now;
+            };
             (void)hipSetDevice(A.device);
             const int32_t m = A.m;
             const unsigned g256 = blocks_for(m, 256);
@@ -1205,18 +1511,22 @@ struct EmaxJob {
             if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
                 (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
                 return;
+            mark("alloc");
             hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, nullptr, m, v);
             const double nv = host_blocked_norm(v, m, part, h_part, &e);
             if (e != hipSuccess) return;
+            mark("start");
             hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, v, nv, v);
             for (int it = 0; it < its; ++it) {
                 if ((e = aijhip::launch_dinv_mult(A, dinv, v, w, nullptr)) != hipSuccess) return;
                 const double nw = host_blocked_norm(w, m, part, h_part, &e);
                 if (e != hipSuccess) return;
+                if (it == 0) mark("iteration 0");
                 if (!(nw > 0.0)) break;
                 emax = nw;
                 hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, w, nw, v);
             }
+            mark("iterations");
         });
     }
     void join() {
@@ -1239,6 +1549,46 @@ int make_handle(int device, DCsr &C, aijhip_mat **out) {
     C.ai = C.aj = nullptr;  // owned by the handle now (or freed on failure)
     C.aa = nullptr;
     return rc;
+}
+
+// The interpolation handle of one level (P, with P^T attached for
+// MatRestrict) made on a second host thread: its planning reads P's row
+// offsets back to the host (27 M rows at 300^3, ~14 ms) and nothing before
+// the V-cycle needs it, so it overlaps the next level's aggregation, whose
+// phase 1 keeps the GPU idle on coarse levels. Joined before build_device
+// returns. AIJHIP_GAMG_HANDLE_SYNC=1: made in line (A/B).
+struct HandleJob {
+    std::thread th;
+    size_t level = 0;
+    int rc = AIJHIP_OK;
+    std::string err;
+    aijhip_mat *P = nullptr;
+    void start(int device, size_t l, DCsr Pm, DCsr PTm) {
+        level = l;
+        th = std::thread([this, device, Pm, PTm]() mutable {
+            (void)hipSetDevice(device);
+            rc = make_handle(device, Pm, &P);
+            if (!rc) rc = aijhip::attach_transpose(P, PTm.ai, PTm.aj, PTm.aa);  // consumes PT
+            else PTm.release();
+            if (rc) {
+                err = aijhip_last_error();
+                if (P) aijhip_mat_destroy(P);
+                P = nullptr;
+            }
+        });
+    }
+    void join() {
+        if (th.joinable()) th.join();
+    }
+    ~HandleJob() {
+        join();
+        if (P) aijhip_mat_destroy(P);
+    }
+};
+
+bool handles_in_line() {
+    const char *v = std::getenv("AIJHIP_GAMG_HANDLE_SYNC");
+    return v && v[0] == '1';
 }
 
 // Which side runs aggregation phase 1 (both give the same aggregates): the
@@ -1303,7 +1653,7 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
     void *scan_tmp = nullptr;
     size_t tb = 0;
     int64_t nzs = 0;
-    int32_t *h_si = nullptr, *h_sj = nullptr, *agg = nullptr, *d_ph = nullptr;
+    int32_t *h_si = nullptr, *agg = nullptr, *d_ph = nullptr;
     int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
     unsigned long long *d_left = nullptr;
     int32_t na = 0;
@@ -1366,37 +1716,53 @@ strength_done:
         }
     }
     if (!dev_agg) {
-        GTRY(stage.reserve(sizeof(int32_t) * ((size_t)m + 1 + (size_t)nzs + (size_t)m)), "pinned staging");
-        lap("staging alloc");
-        h_si = stage.i32();
-        h_sj = h_si + m + 1;
-        agg = h_sj + nzs;
-        GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
-        lap("strength");
-        // S's columns come down in row chunks while the pass works through
-        // the rows already here (a node reads only its own row). (Phase 1
+        // S's columns come down in row chunks through two pinned slots while
+        // the pass works through the rows already here (a node reads only its
+        // own row of S; the aggregate ids of all). Pinned: the row offsets,
+        // the ids and the two slots (~50 MB at 300^3 level 1, where a whole
+        // copy of S took 0.37 GB and 20 ms to pin on first use). (Phase 1
         // measured on the MI355X host at 300^3 level 0: this int32 form
         // 83 ms; bitmap or byte flags with or without early exits 87-121 ms.)
+        constexpr int kChunks = 32;
+        int32_t r[kChunks + 1];
+        for (int c = 0; c <= kChunks; ++c) r[c] = (int32_t)((int64_t)m * c / kChunks);
+        int32_t *h_off = nullptr;
+        GTRY(hipHostMalloc(reinterpret_cast<void **>(&h_off), sizeof(int32_t) * (kChunks + 1)), "pinned offsets");
+        for (int c = 0; c <= kChunks && e == hipSuccess; ++c)
+            e = hipMemcpyAsync(h_off + c, si + r[c], sizeof(int32_t), hipMemcpyDeviceToHost, nullptr);
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+        int64_t slot = 0;
+        for (int c = 0; c < kChunks; ++c) slot = std::max<int64_t>(slot, (int64_t)h_off[c + 1] - h_off[c]);
+        (void)hipHostFree(h_off);
+        GTRY(e, "read S offsets");
+        GTRY(stage.reserve(sizeof(int32_t) * (2 * (size_t)m + 1 + 2 * (size_t)slot)), "pinned staging");
+        lap("staging alloc");
+        h_si = stage.i32();
+        agg = h_si + m + 1;
+        int32_t *h_slot[2] = {agg + m, agg + m + slot};
+        GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
+        lap("strength");
         {
-            constexpr int kChunks = 16;
             hipStream_t cs = nullptr;
-            hipEvent_t ev[kChunks] = {};
+            hipEvent_t ev[2] = {};
             GTRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
-            int32_t r[kChunks + 1];
-            for (int c = 0; c <= kChunks; ++c) r[c] = (int32_t)((int64_t)m * c / kChunks);
-            for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
+            auto fetch = [&](int c) {  // chunk c into slot c % 2
                 const int64_t a = h_si[r[c]], b = h_si[r[c + 1]];
+                hipError_t x = hipSuccess;
                 if (b > a)
-                    e = hipMemcpyAsync(h_sj + a, sj + a, sizeof(int32_t) * (size_t)(b - a), hipMemcpyDeviceToHost,
-                                       cs);
-                if (e == hipSuccess) e = hipEventCreateWithFlags(&ev[c], hipEventDisableTiming);
-                if (e == hipSuccess) e = hipEventRecord(ev[c], cs);
-            }
+                    x = hipMemcpyAsync(h_slot[c & 1], sj + a, sizeof(int32_t) * (size_t)(b - a),
+                                       hipMemcpyDeviceToHost, cs);
+                if (x == hipSuccess) x = hipEventRecord(ev[c & 1], cs);
+                return x;
+            };
+            for (int z = 0; z < 2 && e == hipSuccess; ++z) e = hipEventCreateWithFlags(&ev[z], hipEventDisableTiming);
+            for (int c = 0; c < 2 && c < kChunks && e == hipSuccess; ++c) e = fetch(c);
             std::fill(agg, agg + m, -1);
             na = 0;
             for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
-                if ((e = hipEventSynchronize(ev[c])) == hipSuccess)
-                    na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_sj, agg, na);
+                if ((e = hipEventSynchronize(ev[c & 1])) != hipSuccess) break;
+                na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_slot[c & 1], agg, na, h_si[r[c]]);
+                if (c + 2 < kChunks) e = fetch(c + 2);
             }
             (void)hipStreamSynchronize(cs);
             for (hipEvent_t x : ev)
@@ -1414,20 +1780,17 @@ strength_done:
         unsigned long long left = 0;
         GTRY(hipMemcpy(&left, d_left, sizeof(left), hipMemcpyDeviceToHost), "read phase 2");
         lap("phase 2");
-        if (left > 0 && dev_agg) {  // phase 3 over the left-over nodes' rows only
+        if (left > 0)  // phase 3 over the left-over nodes' rows only (the host pass's order)
             GTRY(aijhip_gamg::aggregate_phase3_device(m, si, sj, d_aggv, &na), "phase 3");
-        } else if (left > 0) {  // phase 3 (sequential) on the host
-            GTRY(hipMemcpy(agg, d_aggv, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost), "read phase 2");
-            na = aijhip_gamg::aggregate_phase3(m, h_si, h_sj, agg, na);
-            GTRY(hipMemcpy(d_aggv, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 3");
-        }
     }
     lap("aggregate");
 level_done:
 #undef GTRY
     job.join();
+    lap("emax joined");
     hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
     hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left);
+    lap("freed");
     if (emax_its > 0) {
         *emax = job.emax;
         if (emax_err) *emax_err = job.e;
@@ -1511,8 +1874,18 @@ done:
 // The Galerkin operator A_c = P^T (A P) of local blocks (PT = P^T returned:
 // the MatRestrict operator); AP is released unless ap_out is given.
 int galerkin_level(const DCsr &Av, const DCsr &P, DCsr &PT, DCsr &Ac, int n_cu, int *cols_used, DCsr *ap_out) {
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!log) return;
+        (void)hipDeviceSynchronize();
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "  galerkin %-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    };
     DCsr AP;
     int rc = rowprod(Av, P, AP, n_cu, cols_used);
+    lap("A*P");
     if (rc) return rc;
     {
         aijhip_mat pv;  // non-owning view for the transpose builder
@@ -1528,6 +1901,7 @@ int galerkin_level(const DCsr &Av, const DCsr &P, DCsr &PT, DCsr &Ac, int n_cu, 
         const hipError_t e = aijhip::build_transpose(pv, &PT.ai, &PT.aj, &PT.aa, nullptr);
         pv.d_ai = pv.d_aj = nullptr;
         pv.d_aa = nullptr;
+        lap("P^T");
         if (e != hipSuccess) {
             AP.release();
             return herr(e, "transpose");
@@ -1538,8 +1912,10 @@ int galerkin_level(const DCsr &Av, const DCsr &P, DCsr &PT, DCsr &Ac, int n_cu, 
         PT.release();
         return rc;
     }
+    lap("P^T*(AP)");
     if (ap_out) *ap_out = AP;
     else AP.release();
+    lap("released");
     return AIJHIP_OK;
 }
 
@@ -1601,6 +1977,8 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     const int n_cu = std::max(A0->n_cu, 1);
     int rc = AIJHIP_OK;
     hipError_t e = hipSuccess;
+    const bool in_line = handles_in_line();
+    std::vector<std::unique_ptr<HandleJob>> jobs;
     // the near-null space of the current level, on the device (ones at the top)
     double *d_B = nullptr;
     if ((e = dalloc(&d_B, A0->m)) != hipSuccess) return herr(e, "alloc");
@@ -1643,8 +2021,14 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         if (!rc) rc = galerkin_level(Av, P, PT, Ac, n_cu, &cols_used, nullptr);
         lap("P^T*(AP)");
         // ---- handles: P (with P^T attached for MatRestrict) and A_c
-        if (!rc) rc = make_handle(A.device, P, &Ph);
-        if (!rc) {
+        if (!rc && !in_line) {
+            jobs.emplace_back(new HandleJob());
+            jobs.back()->start(A.device, levels.size() - 1, P, PT);
+            P = DCsr();  // owned by the job now
+            PT = DCsr();
+        }
+        if (!rc && in_line) rc = make_handle(A.device, P, &Ph);
+        if (!rc && in_line) {
             rc = aijhip::attach_transpose(Ph, PT.ai, PT.aj, PT.aa);
             PT = DCsr();  // consumed by attach_transpose (freed on failure)
         }
@@ -1671,6 +2055,20 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         }
         if (rc) break;
     }
+    for (auto &j : jobs) {  // the interpolation handles made meanwhile
+        j->join();
+        if (j->rc) {
+            if (!rc) {
+                rc = j->rc;
+                set_error(j->err);
+            }
+            continue;
+        }
+        levels[j->level].P = j->P;
+        j->P = nullptr;
+    }
+    jobs.clear();
+    lap("P handles");
     if (!rc) {  // the coarsest device level's near-null space, for the host levels
         B.resize((size_t)levels.back().A->m);
         if (!B.empty() && (e = hipMemcpy(B.data(), d_B, sizeof(double) * B.size(), hipMemcpyDeviceToHost)) != hipSuccess)

@@ -380,14 +380,16 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
 namespace aijhip_gamg {
 
 int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const int32_t *sj, int32_t *agg,
-                              int32_t na) {
+                              int32_t na, int64_t sj0) {
     for (int32_t i = r0; i < r1; ++i) {
         if (agg[i] != -1 || si[i] == si[i + 1]) continue;
+        const int32_t *row = sj + (si[i] - sj0);
+        const int32_t len = si[i + 1] - si[i];
         bool free_all = true;
-        for (int32_t k = si[i]; k < si[i + 1] && free_all; ++k) free_all = agg[sj[k]] == -1;
+        for (int32_t k = 0; k < len && free_all; ++k) free_all = agg[row[k]] == -1;
         if (!free_all) continue;
         agg[i] = na;
-        for (int32_t k = si[i]; k < si[i + 1]; ++k) agg[sj[k]] = na;
+        for (int32_t k = 0; k < len; ++k) agg[row[k]] = na;
         ++na;
     }
     return na;
