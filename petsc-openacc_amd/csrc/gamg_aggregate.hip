@@ -35,7 +35,6 @@
 // Phase 3 (the few nodes phases 1 and 2 leave) stays the host's sequential
 // pass, over those nodes and their S rows only, gathered on the device.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -43,6 +42,7 @@
 #include <cstdlib>
 #include <vector>
 
+#include "dscan.h"
 #include "gamg_device.h"
 
 namespace {
@@ -369,13 +369,11 @@ hipError_t dalloc(T **p, int64_t n) {
     return hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * (size_t)std::max<int64_t>(n, 1));
 }
 
-// exclusive sum of n int32 (hipcub, temp allocated here)
+// exclusive sum of n int32 (temp allocated here)
 hipError_t exclusive_sum(const int32_t *in, int32_t *out, int32_t n, hipStream_t s) {
-    size_t tb = 0;
-    void *tmp = nullptr;
-    hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, in, out, n, s);
-    if (e == hipSuccess) e = hipMalloc(&tmp, std::max<size_t>(tb, 1));
-    if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, in, out, n, s);
+    int32_t *tmp = nullptr;
+    hipError_t e = dalloc(&tmp, aijhip_dscan::scan_tmp_elems(n));
+    if (e == hipSuccess) e = aijhip_dscan::exclusive_scan(in, out, (int64_t)n, tmp, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     hipFree(tmp);
     return e;
@@ -420,7 +418,12 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
                      std::chrono::duration<double, std::milli>(now - clk).count());
     };
     mark("drained");
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        s = aijhip_gamg::setup_stream(dev, 0);
+        if (!s) e = hipErrorOutOfMemory;
+    }
     mark("stream");
     if (e == hipSuccess) e = dalloc(&state, m);
     if (e == hipSuccess) e = dalloc(&cnt, m);
@@ -500,7 +503,7 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     hipFree(state); hipFree(cnt); hipFree(roots); hipFree(outs);
     hipFree(tails); hipFree(rstart); hipFree(ostart);
     if (h_ctl) hipHostFree(h_ctl);
-    if (s) hipStreamDestroy(s);
+    // (s is the process's set-up stream: kept)
     return e;
 }
 

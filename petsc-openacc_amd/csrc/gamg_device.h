@@ -38,6 +38,10 @@ hipError_t dalloc(T **p, int64_t count) {
     return e;
 }
 
+// The set-up's process-wide streams (device, slot 0 or 1), created on first
+// use and kept.
+hipStream_t setup_stream(int device, int slot);
+
 // One level of the device hierarchy.
 struct DeviceLevel {
     aijhip_mat *A = nullptr;  // level operator (level 0: the caller's, borrowed)

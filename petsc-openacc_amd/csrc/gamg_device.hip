@@ -19,7 +19,6 @@
 // 0.0. A row with more distinct columns than the lane's capacity retries
 // with a larger capacity; past the largest the level goes to the host.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <chrono>
@@ -32,6 +31,7 @@
 #include <thread>
 #include <vector>
 
+#include "dscan.h"
 #include "gamg_device.h"
 
 namespace {
@@ -433,28 +433,16 @@ __global__ void k_fill(int32_t m, double v, double *x) {
 }
 
 // seg[a] = first position of aggregate a in the sorted aggregate keys
-__global__ void k_seg_offsets(int32_t na, int32_t m, const int32_t *__restrict__ keys, int32_t *seg) {
-    const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
-    if (a > na) return;
-    int32_t lo = 0, hi = m;
-    while (lo < hi) {
-        const int32_t q = (lo + hi) >> 1;
-        if (keys[q] < a) lo = q + 1;
-        else hi = q;
-    }
-    seg[a] = lo;
-}
-
 // The tentative prolongator's near-null space (gamg_setup.cpp prolongator):
 // B_c[a] = sqrt of the sum of B[i]^2 over the members of aggregate a in
 // ascending row order (the stable sort's order), p0[i] = B[i] / B_c[agg[i]].
-__global__ void k_agg_norm(int32_t na, const int32_t *__restrict__ seg, const int32_t *__restrict__ members,
-                           const double *__restrict__ B, double *Bc) {
+__global__ void k_agg_norm(int32_t na, const int32_t *__restrict__ seg, const double *__restrict__ bm,
+                           double *Bc) {
     const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
     if (a >= na) return;
     double s = 0.0;
     for (int32_t q = seg[a]; q < seg[a + 1]; ++q) {
-        const double b = B[members[q]];
+        const double b = bm[q];
         s += b * b;
     }
     Bc[a] = sqrt(s);
@@ -899,16 +887,13 @@ using aijhip_gamg::dalloc;
 
 // exclusive scan of int32 counts into int32 offsets (m+1); false on overflow
 hipError_t scan_offsets(const int32_t *cnt, int32_t m, int32_t *off, int64_t *total) {
-    unsigned long long *w = nullptr, *o = nullptr;
-    void *tmp = nullptr;
-    size_t tb = 0;
+    unsigned long long *w = nullptr, *o = nullptr, *stmp = nullptr;
     hipError_t e;
     if ((e = dalloc(&w, (int64_t)m + 1)) != hipSuccess || (e = dalloc(&o, (int64_t)m + 1)) != hipSuccess) goto done;
     if ((e = hipMemset(w, 0, sizeof(unsigned long long) * ((size_t)m + 1))) != hipSuccess) goto done;
     if (m > 0) hipLaunchKernelGGL(k_widen, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, cnt, w);
-    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, w, o, m + 1)) != hipSuccess) goto done;
-    if ((e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) != hipSuccess) goto done;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, w, o, m + 1)) != hipSuccess) goto done;
+    if ((e = dalloc(&stmp, aijhip_dscan::scan_tmp_elems((int64_t)m + 1))) != hipSuccess) goto done;
+    if ((e = aijhip_dscan::exclusive_scan(w, o, (int64_t)m + 1, stmp, nullptr)) != hipSuccess) goto done;
     {
         unsigned long long t = 0;
         if ((e = hipMemcpy(&t, o + m, sizeof(t), hipMemcpyDeviceToHost)) != hipSuccess) goto done;
@@ -919,7 +904,7 @@ hipError_t scan_offsets(const int32_t *cnt, int32_t m, int32_t *off, int64_t *to
         }
     }
 done:
-    hipFree(w); hipFree(o); hipFree(tmp);
+    hipFree(w); hipFree(o); hipFree(stmp);
     return e;
 }
 
@@ -1025,15 +1010,14 @@ bool hash_off() {
 hipError_t min_of(const int32_t *cnt, int32_t m, int32_t *mn) {
     *mn = 0;
     if (m == 0) return hipSuccess;
-    void *tmp = nullptr;
-    size_t tb = 0;
     int32_t *dmin = nullptr;
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     hipError_t r;
-    if ((r = dalloc(&dmin, 1)) == hipSuccess && (r = hipcub::DeviceReduce::Min(nullptr, tb, cnt, dmin, m)) == hipSuccess &&
-        (r = hipMalloc(&tmp, std::max<size_t>(tb, 1))) == hipSuccess &&
-        (r = hipcub::DeviceReduce::Min(tmp, tb, cnt, dmin, m)) == hipSuccess)
+    if ((r = dalloc(&dmin, 1)) == hipSuccess &&
+        (r = aijhip_dscan::extreme<int32_t, false>(cnt, m, dmin, cus, nullptr)) == hipSuccess)
         r = hipMemcpy(mn, dmin, sizeof(int32_t), hipMemcpyDeviceToHost);
-    hipFree(tmp);
     hipFree(dmin);
     return r;
 }
@@ -1138,18 +1122,7 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
         hipLaunchKernelGGL((k_rowprod_wave<kWaveK, false>), dim3(gw), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
                            B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt);
         int32_t mn = 0;
-        if ((e = hipGetLastError()) == hipSuccess && A.m > 0) {
-            void *tmp = nullptr;
-            size_t tb = 0;
-            int32_t *dmin = nullptr;
-            if ((e = dalloc(&dmin, 1)) == hipSuccess &&
-                (e = hipcub::DeviceReduce::Min(nullptr, tb, cnt, dmin, A.m)) == hipSuccess &&
-                (e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) == hipSuccess &&
-                (e = hipcub::DeviceReduce::Min(tmp, tb, cnt, dmin, A.m)) == hipSuccess)
-                e = hipMemcpy(&mn, dmin, sizeof(int32_t), hipMemcpyDeviceToHost);
-            hipFree(tmp);
-            hipFree(dmin);
-        }
+        if ((e = hipGetLastError()) == hipSuccess && A.m > 0) e = min_of(cnt, A.m, &mn);
         if (e != hipSuccess) { hipFree(cnt); return herr(e, "symbolic product"); }
         if (mn >= 0) {  // every row fits the wave form
             if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) { hipFree(cnt); return herr(e, "product rows"); }
@@ -1178,22 +1151,7 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
     }
     // one lane per row, the row's distinct columns in LDS: capacity classes
     // 64 / 128 / 256 (a row counted -1 by a class is recounted by the next)
-    auto min_count = [&](int32_t *mn) -> hipError_t {
-        *mn = 0;
-        if (A.m == 0) return hipSuccess;
-        void *tmp = nullptr;
-        size_t tb = 0;
-        int32_t *dmin = nullptr;
-        hipError_t r;
-        if ((r = dalloc(&dmin, 1)) == hipSuccess &&
-            (r = hipcub::DeviceReduce::Min(nullptr, tb, cnt, dmin, A.m)) == hipSuccess &&
-            (r = hipMalloc(&tmp, std::max<size_t>(tb, 1))) == hipSuccess &&
-            (r = hipcub::DeviceReduce::Min(tmp, tb, cnt, dmin, A.m)) == hipSuccess)
-            r = hipMemcpy(mn, dmin, sizeof(int32_t), hipMemcpyDeviceToHost);
-        hipFree(tmp);
-        hipFree(dmin);
-        return r;
-    };
+    auto min_count = [&](int32_t *mn) -> hipError_t { return min_of(cnt, A.m, mn); };
     // light products (A*P0, A*P on the finest level: ~4 and ~25 products
     // per row) start in the 32-column class: 24 KiB of LDS per 64-row
     // workgroup in the numeric pass instead of 48, twice the waves per CU
@@ -1313,8 +1271,6 @@ int strength_lists(const aijhip_mat &A, const unsigned long long *cnt, const uns
     int32_t *ucnt = nullptr, *rows = nullptr, *flag = nullptr;
     unsigned long long *dmax = nullptr;
     unsigned int *nrows = nullptr;
-    void *rtmp = nullptr;
-    size_t tb = 0;
     unsigned long long maxn = 0;
     int32_t unsorted = 0;
     int G = 8;
@@ -1331,9 +1287,7 @@ int strength_lists(const aijhip_mat &A, const unsigned long long *cnt, const uns
     STRY(hipMemset(flag, 0, sizeof(int32_t)), "memset");
     STRY(hipMemset(dmax, 0, sizeof(unsigned long long)), "memset");
     hipLaunchKernelGGL(k_rows_unsorted, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, flag);
-    STRY(hipcub::DeviceReduce::Max(nullptr, tb, cnt, dmax, m), "reduce");
-    STRY(hipMalloc(&rtmp, std::max<size_t>(tb, 1)), "alloc");
-    STRY(hipcub::DeviceReduce::Max(rtmp, tb, cnt, dmax, m), "reduce");
+    if (m > 0) STRY((aijhip_dscan::extreme<unsigned long long, true>(cnt, m, dmax, n_cu, nullptr)), "reduce");
     STRY(hipMemcpy(&maxn, dmax, sizeof(maxn), hipMemcpyDeviceToHost), "read");
     STRY(hipMemcpy(&unsorted, flag, sizeof(unsorted), hipMemcpyDeviceToHost), "read");
     while (G < 64 && (unsigned long long)G < maxn) G <<= 1;
@@ -1399,7 +1353,7 @@ int strength_lists(const aijhip_mat &A, const unsigned long long *cnt, const uns
     STRY(hipGetLastError(), "strength copy");
 done:
 #undef STRY
-    hipFree(tval); hipFree(ucnt); hipFree(rows); hipFree(flag); hipFree(dmax); hipFree(nrows); hipFree(rtmp);
+    hipFree(tval); hipFree(ucnt); hipFree(rows); hipFree(flag); hipFree(dmax); hipFree(nrows);
     if (rc) {
         hipFree(*si); hipFree(*sj); hipFree(*sval);
         *si = *sj = nullptr;
@@ -1409,30 +1363,34 @@ done:
 }
 
 // B_c and p0 of the tentative prolongator from the aggregates (device).
+// The members of each aggregate in ascending row order, with their B, are
+// the transpose of P0's pattern (one entry per row, column agg[i], value
+// B[i]): the library's stable transpose gives exactly that.
 hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0) {
     if (m == 0) return hipSuccess;
-    int32_t *keys = nullptr, *idx = nullptr, *members = nullptr, *seg = nullptr;
-    void *tmp = nullptr;
-    size_t tb = 0;
-    int bits = 1;
-    while (bits < 31 && (int64_t(1) << bits) < (int64_t)na) ++bits;
+    int32_t *ai = nullptr, *tai = nullptr, *taj = nullptr;
+    double *taa = nullptr;
     hipError_t e;
-    if ((e = dalloc(&keys, m)) != hipSuccess || (e = dalloc(&idx, m)) != hipSuccess ||
-        (e = dalloc(&members, m)) != hipSuccess || (e = dalloc(&seg, (int64_t)na + 1)) != hipSuccess)
-        goto done;
-    hipLaunchKernelGGL(k_iota, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m - 1, idx);
-    // stable: each aggregate's members stay in ascending row order
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, agg, keys, idx, members, m, 0, bits)) != hipSuccess ||
-        (e = hipMalloc(&tmp, std::max<size_t>(tb, 1))) != hipSuccess ||
-        (e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, agg, keys, idx, members, m, 0, bits)) != hipSuccess)
-        goto done;
-    hipLaunchKernelGGL(k_seg_offsets, dim3(blocks_for((int64_t)na + 1, 256)), dim3(256), 0, nullptr, na, m, keys, seg);
-    if (na > 0)
-        hipLaunchKernelGGL(k_agg_norm, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, seg, members, B, Bc);
-    hipLaunchKernelGGL(k_tentative, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, B, Bc, p0);
-    e = hipGetLastError();
-done:
-    hipFree(keys); hipFree(idx); hipFree(members); hipFree(seg); hipFree(tmp);
+    if ((e = dalloc(&ai, (int64_t)m + 1)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, ai);
+    {
+        aijhip_mat v;  // non-owning view
+        v.m = m;
+        v.n = na;
+        v.nz = m;
+        v.d_ai = ai;
+        v.d_aj = const_cast<int32_t *>(agg);
+        v.d_aa = const_cast<double *>(B);
+        e = aijhip::build_transpose(v, &tai, &taj, &taa, nullptr);
+        v.d_ai = v.d_aj = nullptr;
+        v.d_aa = nullptr;
+    }
+    if (e == hipSuccess) {
+        if (na > 0) hipLaunchKernelGGL(k_agg_norm, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, tai, taa, Bc);
+        hipLaunchKernelGGL(k_tentative, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, B, Bc, p0);
+        e = hipGetLastError();
+    }
+    hipFree(ai); hipFree(tai); hipFree(taj); hipFree(taa);
     return e;
 }
 
@@ -1612,6 +1570,27 @@ bool device_phase1(int32_t m, int64_t nzs, int32_t *max_rounds) {
 
 namespace aijhip_gamg {
 
+// Process-wide set-up streams, per device and slot (0: the phase-1 sweep,
+// 1: the host pass's staging copies): created once, kept for the life of the
+// process like the pinned staging (a first stream creation costs ~5 ms on the
+// MI355X; set_pc_type(GAMG) makes them ahead of the set-up).
+hipStream_t setup_stream(int device, int slot) {
+    static std::mutex mu;
+    static std::vector<hipStream_t> *cache = new std::vector<hipStream_t>();
+    std::lock_guard<std::mutex> g(mu);
+    const size_t k = (size_t)device * 2 + (size_t)(slot & 1);
+    if (cache->size() <= k) cache->resize(k + 1, nullptr);
+    if (!(*cache)[k]) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != device) (void)hipSetDevice(device);
+        hipStream_t st = nullptr;
+        if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) (*cache)[k] = st;
+        if (cur != device) (void)hipSetDevice(cur);
+    }
+    return (*cache)[k];
+}
+
 void free_device_levels(std::vector<DeviceLevel> &levels) {
     for (size_t l = 0; l < levels.size(); ++l) {
         if (l > 0) aijhip_mat_destroy(levels[l].A);
@@ -1650,8 +1629,7 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
     unsigned long long *cnt = nullptr, *off = nullptr;
     unsigned int *pos = nullptr;
     int32_t *tmp = nullptr, *si = nullptr, *sj = nullptr;
-    void *scan_tmp = nullptr;
-    size_t tb = 0;
+    unsigned long long *scan_tmp = nullptr;
     int64_t nzs = 0;
     int32_t *h_si = nullptr, *agg = nullptr, *d_ph = nullptr;
     int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
@@ -1679,9 +1657,8 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
     GTRY(hipMemset(cnt, 0, sizeof(unsigned long long) * ((size_t)m + 1)), "memset");
     hipLaunchKernelGGL(k_strong_count, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d,
                        p.threshold, cnt);
-    GTRY(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, off, m + 1), "scan");
-    GTRY(hipMalloc(&scan_tmp, std::max<size_t>(tb, 1)), "alloc");
-    GTRY(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, cnt, off, m + 1), "scan");
+    GTRY(dalloc(&scan_tmp, aijhip_dscan::scan_tmp_elems((int64_t)m + 1)), "alloc");
+    GTRY(aijhip_dscan::exclusive_scan(cnt, off, (int64_t)m + 1, scan_tmp, nullptr), "scan");
     {
         unsigned long long t = 0;
         GTRY(hipMemcpy(&t, off + m, sizeof(t), hipMemcpyDeviceToHost), "read");
@@ -1743,9 +1720,9 @@ strength_done:
         GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
         lap("strength");
         {
-            hipStream_t cs = nullptr;
             hipEvent_t ev[2] = {};
-            GTRY(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
+            hipStream_t cs = setup_stream(A.device, 1);
+            if (!cs) GTRY(hipErrorOutOfMemory, "stream");
             auto fetch = [&](int c) {  // chunk c into slot c % 2
                 const int64_t a = h_si[r[c]], b = h_si[r[c + 1]];
                 hipError_t x = hipSuccess;
@@ -1767,7 +1744,6 @@ strength_done:
             (void)hipStreamSynchronize(cs);
             for (hipEvent_t x : ev)
                 if (x) (void)hipEventDestroy(x);
-            (void)hipStreamDestroy(cs);
             GTRY(e, "read S");
         }
         GTRY(hipMemcpy(d_ph, agg, sizeof(int32_t) * (size_t)m, hipMemcpyHostToDevice), "upload phase 1");
@@ -1983,6 +1959,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     double *d_B = nullptr;
     if ((e = dalloc(&d_B, A0->m)) != hipSuccess) return herr(e, "alloc");
     hipLaunchKernelGGL(k_fill, dim3(blocks_for(A0->m, 256)), dim3(256), 0, nullptr, A0->m, 1.0, d_B);
+    lap("first kernel");
     while ((int32_t)levels.size() < p.max_levels && levels.back().A->m > p.coarse_eq_limit) {
         aijhip_mat &A = *levels.back().A;
         const int32_t m = A.m;

@@ -429,6 +429,8 @@ int aijhip_ksp_set_pc_type(aijhip_ksp_t K, int pc) {
         return kfail(AIJHIP_ERR_ARG, "unknown PC type");
     if (pc != K->pc) K->set_up = false;
     K->pc = pc;
+    if (pc == AIJHIP_PC_GAMG)  // the set-up's streams, made once per process
+        for (int slot = 0; slot < 2; ++slot) (void)aijhip_gamg::setup_stream(K->A->device, slot);
     return AIJHIP_OK;
 }
 

@@ -39,6 +39,7 @@
 #include "aijhip_internal.h"
 #include "aijhip_mpi.h"
 #include "cg_device.h"
+#include "gamg_device.h"
 #include "gamg_mpi.h"
 #include "mpi_internal.h"
 
@@ -986,6 +987,8 @@ int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc) {
         return mfail(AIJHIP_ERR_ARG, "distributed CG: PC none, jacobi, gamg or bjacobi_gamg");
     if (pc != K->pc) K->set_up = false;
     K->pc = pc;
+    if (pc == AIJHIP_PC_GAMG || pc == AIJHIP_PC_BJACOBI_GAMG)  // the set-up's streams, made once per process
+        for (int slot = 0; slot < 2; ++slot) (void)aijhip_gamg::setup_stream(K->M->comm->device, slot);
     return AIJHIP_OK;
 }
 
