@@ -1341,11 +1341,15 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
         // Stable LSD radix sort by column keeps each column's entries in
         // ascending row order: exactly the order PETSc's MatMultTranspose
         // scatters them, so a row-sequential sum over A^T reproduces it.
+        // (only the bits a column index can have: 22 for 3.27 M columns,
+        // three 8-bit passes instead of four)
+        int bits = 1;
+        while (bits < 32 && (int64_t(1) << bits) < (int64_t)A.n) ++bits;
         AIJHIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, A.d_aj, keys_out, perm_in,
-                                                      perm_out, (int)nz, 0, 32, s));
+                                                      perm_out, (int)nz, 0, bits, s));
         AIJHIP_TRY(hipMalloc(&tmp, tmp_bytes));
         AIJHIP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, A.d_aj, keys_out, perm_in,
-                                                      perm_out, (int)nz, 0, 32, s));
+                                                      perm_out, (int)nz, 0, bits, s));
         hipLaunchKernelGGL(k_gather_transpose, dim3(grid_for(nz, 256)), dim3(256), 0, s, nz,
                            perm_out, rows, A.d_aa, *d_taj, *d_taa);
         hipLaunchKernelGGL(k_col_offsets, dim3(grid_for((int64_t)A.n + 1, 256)), dim3(256), 0, s,

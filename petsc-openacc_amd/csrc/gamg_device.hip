@@ -847,6 +847,72 @@ __global__ __launch_bounds__(G *NG) void k_rowprod_hash(int32_t m, const int32_t
     }
 }
 
+// T = A * P0 where P0 has one entry per row (column agg[k], value p0[k]):
+// one lane per row, the row's distinct columns (at most CAP) in registers,
+// each product added to its column in traversal order from 0.0 (the order
+// of the general forms, so the same bits); sorted by rank on the way out.
+// Count mode: cnt[i] = distinct columns, or -1 past CAP (the general form
+// takes the product then).
+template <int CAP, bool WRITE>
+__global__ __launch_bounds__(256) void k_rowprod_p0(int32_t m, const int32_t *__restrict__ ai,
+                                                    const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                                                    const int32_t *__restrict__ agg, const double *__restrict__ p0,
+                                                    const int32_t *__restrict__ ci, int32_t *cj, double *ca,
+                                                    int32_t *cnt) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int32_t col[CAP];
+    double val[CAP];
+#pragma unroll
+    for (int e = 0; e < CAP; ++e) {
+        col[e] = -1;
+        val[e] = 0.0;
+    }
+    int n = 0;
+    bool over = false;
+    const int32_t k1 = ai[i + 1];
+    for (int32_t k = ai[i]; k < k1; ++k) {
+        const int32_t j = aj[k];
+        const int32_t c = agg[j];
+        const double p = WRITE ? aa[k] * p0[j] : 0.0;
+        bool hit = false;
+#pragma unroll
+        for (int e = 0; e < CAP; ++e)
+            if (col[e] == c) {
+                if (WRITE) val[e] += p;
+                hit = true;
+            }
+        if (hit) continue;
+        if (n == CAP) {
+            over = true;
+            break;
+        }
+#pragma unroll
+        for (int e = 0; e < CAP; ++e)
+            if (e == n) {
+                col[e] = c;
+                if (WRITE) val[e] += p;  // from 0.0
+            }
+        ++n;
+    }
+    if (!WRITE) {
+        cnt[i] = over ? -1 : n;
+        return;
+    }
+    if (cnt[i] < 0) return;  // the general form's row
+    const int32_t o = ci[i];
+#pragma unroll
+    for (int e = 0; e < CAP; ++e) {
+        if (e < n) {
+            int r = 0;
+#pragma unroll
+            for (int z = 0; z < CAP; ++z) r += (z < n && col[z] < col[e]);
+            cj[o + r] = col[e];
+            ca[o + r] = val[e];
+        }
+    }
+}
+
 // P = alpha (D^-1 T) + P0 on the union pattern (gamg_setup.cpp prolongator):
 // lengths, then entries.
 __global__ void k_prolong_len(int32_t m, const int32_t *__restrict__ ti, const int32_t *__restrict__ tj,
@@ -1022,7 +1088,58 @@ hipError_t min_of(const int32_t *cnt, int32_t m, int32_t *mn) {
     return r;
 }
 
-int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nullptr) {
+int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nullptr);
+
+// T = A * P0 (P0: one entry per row, column agg, value p0) by k_rowprod_p0;
+// a row with more than kP0Cap distinct columns sends the whole product to
+// the general form (same bits either way).
+constexpr int kP0Cap = 8;
+int rowprod_p0(const DCsr &A, const DCsr &P0, DCsr &C, int n_cu, int *cols_used) {
+    // (rows of A longer than the list on average: the hash form directly)
+    if (hash_off() || A.nz > (int64_t)kP0Cap * std::max<int32_t>(A.m, 1)) return rowprod(A, P0, C, n_cu, cols_used);
+    C = DCsr();
+    C.m = A.m;
+    C.n = P0.n;
+    int32_t *cnt = nullptr;
+    hipError_t e;
+    const unsigned g = blocks_for(A.m, 256);
+    if ((e = dalloc(&cnt, A.m)) != hipSuccess) return herr(e, "product counts");
+    if (A.m > 0)
+        hipLaunchKernelGGL((k_rowprod_p0<kP0Cap, false>), dim3(g), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
+                           P0.aj, P0.aa, nullptr, nullptr, nullptr, cnt);
+    int32_t mn = 0;
+    if ((e = hipGetLastError()) != hipSuccess || (e = min_of(cnt, A.m, &mn)) != hipSuccess) {
+        hipFree(cnt);
+        return herr(e, "symbolic product");
+    }
+    if (mn < 0) {
+        hipFree(cnt);
+        return rowprod(A, P0, C, n_cu, cols_used);
+    }
+    int64_t total = 0;
+    if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess || (e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess ||
+        (e = dalloc(&C.aj, total + 2)) != hipSuccess || (e = dalloc(&C.aa, total + 2)) != hipSuccess ||
+        (e = hipMemset(C.aj + total, 0, 2 * sizeof(int32_t))) != hipSuccess ||
+        (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess) {
+        hipFree(cnt);
+        C.release();
+        return herr(e, "product alloc");
+    }
+    C.nz = total;
+    if (A.m > 0)
+        hipLaunchKernelGGL((k_rowprod_p0<kP0Cap, true>), dim3(g), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
+                           P0.aj, P0.aa, C.ai, C.aj, C.aa, cnt);
+    e = hipGetLastError();
+    hipFree(cnt);
+    if (e != hipSuccess) {
+        C.release();
+        return herr(e, "numeric product");
+    }
+    if (cols_used) *cols_used = std::max(*cols_used, kP0Cap);
+    return AIJHIP_OK;
+}
+
+int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
     C = DCsr();
     C.m = A.m;
     C.n = B.n;
@@ -1796,10 +1913,20 @@ int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, 
     double *d_p0 = nullptr, *d_Bc = nullptr;
     int32_t *plen = nullptr;
     DCsr P0, T;
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    auto t0 = std::chrono::steady_clock::now();
+    auto lap = [&](const char *what) {
+        if (!log) return;
+        (void)hipDeviceSynchronize();
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "  smooth %-12s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+        t0 = t;
+    };
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto done; } } while (0)
     GTRY(dalloc(&d_p0, m), "alloc");
     GTRY(dalloc(&d_Bc, na), "alloc");
     GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0), "tentative prolongator");
+    lap("tentative");
     P0.m = m;
     P0.n = na;
     P0.nz = m;
@@ -1808,7 +1935,8 @@ int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, 
     P0.aj = d_agg;
     P0.aa = d_p0;
     if (nsmooths > 0) {
-        if ((rc = rowprod(Av, P0, T, n_cu, cols_used))) goto done;
+        if ((rc = rowprod_p0(Av, P0, T, n_cu, cols_used))) goto done;
+        lap("A*P0");
         P.m = m;
         P.n = na;
         GTRY(dalloc(&plen, m), "alloc");
@@ -1820,6 +1948,7 @@ int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, 
         hipLaunchKernelGGL(k_prolong_fill, dim3(g256), dim3(256), 0, nullptr, m, T.ai, T.aj, T.aa, d_agg, d_p0,
                            dinv, alpha, P.ai, P.aj, P.aa);
         GTRY(hipGetLastError(), "prolongator");
+        lap("P fill");
     } else {
         P.m = m;
         P.n = na;
@@ -1836,6 +1965,7 @@ done:
     hipFree(P0.ai);
     hipFree(plen);
     T.release();
+    lap("freed");
     if (rc) {
         P.release();
         hipFree(d_p0);
