@@ -144,3 +144,74 @@ def test_gpu_mpiaij_and_cg_on_k_ranks(world, dims, halo):
     np.testing.assert_allclose(gm[0][3][:10], hist_g[:10], rtol=1e-7)
     xgm = np.concatenate([g[0] for g in gm])
     assert np.linalg.norm(xgm - xg_o) <= 1e-8 * np.linalg.norm(xg_o)
+
+
+def _unfused_worker(rank, world, port, dims, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pkg = importlib.import_module("petsc-openacc_amd")
+        mp_mod = importlib.import_module("petsc-openacc_amd.mpiaij")
+        C = importlib.import_module("petsc-openacc_amd.comm")
+        dev = torch.device("cuda:0")
+        nx, ny, nz = dims
+        bounds = [mp_mod.slab_bounds(nz, world, r) for r in range(world)]
+        row_starts = np.array([b[0] * nx * ny for b in bounds] + [nx * ny * nz], dtype=np.int64)
+        z0, z1 = bounds[rank]
+        ai, aj, aa = pkg.poisson_csr(nx, ny, nz, z0, z1)
+        rhs, _ = pkg.poisson_vectors(nx, ny, nz, z0, z1)
+        b = torch.from_numpy(rhs).to(dev)
+        comm = C.Comm.host(device=0, timeout_s=120)
+        out = {}
+        for kernel in ("stream", "vector"):
+            def make_local(a_i, a_j, a_a, ncols, kernel=kernel):
+                return pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols, kernel=kernel)
+
+            op = mp_mod.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, comm=comm)
+            x = torch.full_like(b, float("nan"))
+            with C.KSPCGMPINative(op.native, rtol=1e-10, max_it=1000) as k:
+                k.solve(b, x)
+                torch.cuda.synchronize()
+                out[kernel] = (x.cpu().numpy(), k.its, k.reason, k.hist.tolist(), op.A_d.info()["kernel"])
+        q.put((rank, out))
+    except Exception as e:  # noqa: BLE001
+        q.put((rank, {"error": repr(e)}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gpu_kspmpi_unfused_dot_matches_fused_and_oracle():
+    """with a diagonal block the STREAM epilogue cannot carry p.w
+    (here the VECTOR kernel), the distributed CG takes the unfused dot, which
+    must not add the off-diagonal correction a second time: same iterations
+    and residual history as the fused run and the oracle CG."""
+    import torch.multiprocessing as mp
+    world, dims = 2, (12, 10, 16)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unfused_worker, args=(r, world, port, dims, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, out = q.get(timeout=300)
+        got[r] = out
+    for p in procs:
+        p.join(timeout=120)
+    for r in range(world):
+        assert "error" not in got[r], got[r]["error"]
+    nx, ny, nz = dims
+    ai, aj, aa, rhs, _ = seqaij.create_system(nx, ny, nz)
+    xo, its_o, reason_o, hist_o = ksp_cg.cg(ai, aj, aa, rhs, rtol=1e-10, max_it=1000)
+    fused, unfused = got[0]["stream"], got[0]["vector"]
+    assert fused[4] == "stream" and unfused[4] == "vector"
+    assert unfused[2] == reason_o and abs(unfused[1] - its_o) <= 1 and abs(unfused[1] - fused[1]) <= 1
+    np.testing.assert_allclose(unfused[3][:10], hist_o[:10], rtol=1e-9)
+    np.testing.assert_allclose(unfused[3][:10], fused[3][:10], rtol=1e-9)
+    x = np.concatenate([got[r]["vector"][0] for r in range(world)])
+    assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)

@@ -118,6 +118,9 @@ def main():
     if args.variants == "skewgeom":
         for g, ex in itertools.product(range(9), (0, 1)):
             variants.append(("stream", dict(geometry=g, exact=ex)))
+    if args.variants == "skewgeom2":  # the geometries the skewgeom sweep left out (9-11) against 1
+        for g, nt in itertools.product((1, 9, 10, 11), (0, 1)):
+            variants.append(("stream", dict(geometry=g, nt_loads=nt)))
     if args.variants == "skewpipe":
         for g, ex, pp in itertools.product((1, 7), (0, 1), (0, 1, 2, 3)):
             variants.append(("stream", dict(geometry=g, exact=ex, persistent=pp)))
