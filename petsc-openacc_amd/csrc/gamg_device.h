@@ -76,7 +76,8 @@ void free_device_levels(std::vector<DeviceLevel> &levels);
 int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_agg, int32_t *na, double **dinv,
                     int emax_its, double *emax, hipError_t *emax_err, size_t level);
 int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, const double *dinv, double alpha,
-                 int nsmooths, int n_cu, double **d_p0, double **d_Bc, DCsr &P, int *cols_used);
+                 int nsmooths, int n_cu, double **d_p0, double **d_Bc, DCsr &P, int *cols_used,
+                 bool b_ones = false);  // b_ones: d_B is all 1.0 (the finest level's near-null space)
 int galerkin_level(const DCsr &Av, const DCsr &P, DCsr &PT, DCsr &Ac, int n_cu, int *cols_used, DCsr *ap_out);
 // A handle adopting C's arrays (C is emptied).
 int make_level_handle(int device, DCsr &C, aijhip_mat **out);

@@ -448,6 +448,18 @@ __global__ void k_agg_norm(int32_t na, const int32_t *__restrict__ seg, const do
     Bc[a] = sqrt(s);
 }
 
+// B = 1 (the finest level): the member counts, and B_c = sqrt(count) (the sum
+// of count ones is count exactly, whatever the order)
+__global__ void k_agg_count(int32_t m, const int32_t *__restrict__ agg, int32_t *count) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) atomicAdd(&count[agg[i]], 1);
+}
+
+__global__ void k_agg_norm_count(int32_t na, const int32_t *__restrict__ count, double *Bc) {
+    const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a < na) Bc[a] = sqrt((double)count[a]);
+}
+
 __global__ void k_tentative(int32_t m, const int32_t *__restrict__ agg, const double *__restrict__ B,
                             const double *__restrict__ Bc, double *p0) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1483,11 +1495,24 @@ done:
 // The members of each aggregate in ascending row order, with their B, are
 // the transpose of P0's pattern (one entry per row, column agg[i], value
 // B[i]): the library's stable transpose gives exactly that.
-hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0) {
+hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0,
+                     bool b_ones = false) {
     if (m == 0) return hipSuccess;
     int32_t *ai = nullptr, *tai = nullptr, *taj = nullptr;
     double *taa = nullptr;
     hipError_t e;
+    if (b_ones) {  // B = 1: each sum of B^2 is its member count, exact in any order
+        int32_t *count = nullptr;
+        if ((e = dalloc(&count, std::max(na, 1))) != hipSuccess) return e;
+        if ((e = hipMemset(count, 0, sizeof(int32_t) * (size_t)std::max(na, 1))) == hipSuccess) {
+            hipLaunchKernelGGL(k_agg_count, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, count);
+            if (na > 0) hipLaunchKernelGGL(k_agg_norm_count, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, count, Bc);
+            hipLaunchKernelGGL(k_tentative, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, B, Bc, p0);
+            e = hipGetLastError();
+        }
+        hipFree(count);
+        return e;
+    }
     if ((e = dalloc(&ai, (int64_t)m + 1)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, ai);
     {
@@ -1905,7 +1930,8 @@ level_done:
 // with local columns (agg ids). d_p0 (m) and d_Bc (na) are returned for the
 // caller to free; P owns its arrays.
 int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, const double *dinv, double alpha,
-                 int nsmooths, int n_cu, double **d_p0_out, double **d_Bc_out, DCsr &P, int *cols_used) {
+                 int nsmooths, int n_cu, double **d_p0_out, double **d_Bc_out, DCsr &P, int *cols_used,
+                 bool b_ones) {
     const int32_t m = Av.m;
     const unsigned g256 = blocks_for(m, 256);
     int rc = AIJHIP_OK;
@@ -1925,7 +1951,7 @@ int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, 
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto done; } } while (0)
     GTRY(dalloc(&d_p0, m), "alloc");
     GTRY(dalloc(&d_Bc, na), "alloc");
-    GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0), "tentative prolongator");
+    GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0, b_ones), "tentative prolongator");
     lap("tentative");
     P0.m = m;
     P0.n = na;
@@ -2122,7 +2148,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         aijhip_mat *Ph = nullptr, *Ach = nullptr;
         // ---- tentative + smoothed prolongator
         rc = smooth_level(Av, na, d_agg, d_B, dinv, -p.smooth_scale / emax, p.nsmooths, n_cu, &d_p0, &d_Bc, P,
-                          &cols_used);
+                          &cols_used, levels.size() == 1);
         lap("prolongator");
         // ---- Galerkin operator A_c = P^T (A P)
         if (!rc) rc = galerkin_level(Av, P, PT, Ac, n_cu, &cols_used, nullptr);
