@@ -85,7 +85,8 @@ int make_level_handle(int device, DCsr &C, aijhip_mat **out);
 int rowprod_device(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used);
 // The tentative prolongator's values: Bc[a] = ||B over aggregate a||, p0[i] =
 // B[i] / Bc[agg[i]] (device arrays).
-hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0);
+hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0,
+                            bool b_ones = false);  // b_ones: B is all 1.0
 // P = P0 + alpha D^-1 T on the union pattern of T and P0 (P0: one entry per
 // row, column agg[i], value p0[i]); T's columns may extend past the local
 // aggregates (the distributed set-up's ghost coarse columns).

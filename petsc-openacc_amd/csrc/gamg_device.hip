@@ -2057,8 +2057,9 @@ int rowprod_device(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_us
     return rowprod(A, B, C, n_cu, cols_used);
 }
 
-hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0) {
-    return tentative(m, na, agg, B, Bc, p0);
+hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0,
+                            bool b_ones) {
+    return tentative(m, na, agg, B, Bc, p0, b_ones);
 }
 
 int prolong_from_T(const DCsr &T, const int32_t *d_agg, const double *d_p0, const double *dinv, double alpha,

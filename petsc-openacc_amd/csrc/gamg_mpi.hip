@@ -41,9 +41,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
+#include "dscan.h"
 #include "gamg_device.h"
 #include "gamg_mpi.h"
 #include "mpi_internal.h"
@@ -346,24 +349,58 @@ int upload_csr(int32_t m, int32_t n, const std::vector<int32_t> &ai, const std::
     return AIJHIP_OK;
 }
 
-// exclusive scan of device int32 lengths into device offsets (host round trip)
+__global__ void k_fill_value(int32_t m, double v, double *x) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) x[i] = v;
+}
+
+__global__ void k_len_total(int32_t m, const int32_t *__restrict__ len, unsigned long long *off) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) off[m] = m > 0 ? off[m - 1] + (unsigned long long)len[m - 1] : 0ull;
+}
+
+__global__ void k_narrow_off(int32_t n, const unsigned long long *__restrict__ w, int32_t *o) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) o[i] = (int32_t)w[i];
+}
+
+// exclusive scan of device int32 lengths into device int32 offsets (m + 1),
+// on the device in 64-bit (dscan.h), one 8-byte read for the total
 int scan_lengths(const int32_t *d_len, int32_t m, int32_t **d_off, int64_t *total) {
-    std::vector<int32_t> len((size_t)m), off((size_t)m + 1, 0);
+    unsigned long long *w = nullptr, *tmp = nullptr;
     hipError_t e;
-    if (m > 0 && (e = hipMemcpy(len.data(), d_len, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost)) != hipSuccess)
-        return gerr(e, "lengths");
-    int64_t t = 0;
-    for (int32_t i = 0; i < m; ++i) {
-        off[i] = (int32_t)t;
-        t += len[i];
+    int rc = AIJHIP_OK;
+    unsigned long long t = 0;
+    *d_off = nullptr;
+    if ((e = dalloc(&w, (int64_t)m + 1)) != hipSuccess ||
+        (e = dalloc(&tmp, aijhip_dscan::scan_tmp_elems(std::max<int64_t>(m, 1)))) != hipSuccess ||
+        (m > 0 && (e = aijhip_dscan::exclusive_scan(d_len, w, (int64_t)m, tmp, nullptr)) != hipSuccess)) {
+        rc = gerr(e, "lengths");
+        goto done;
     }
-    if (t > INT32_MAX) return mfail(AIJHIP_ERR_STATE, "distributed GAMG: a local operator past int32 entries");
-    off[m] = (int32_t)t;
-    *total = t;
-    if ((e = dalloc(d_off, (int64_t)m + 1)) != hipSuccess ||
-        (e = hipMemcpy(*d_off, off.data(), sizeof(int32_t) * ((size_t)m + 1), hipMemcpyHostToDevice)) != hipSuccess)
-        return gerr(e, "offsets");
-    return AIJHIP_OK;
+    hipLaunchKernelGGL(k_len_total, dim3(1), dim3(64), 0, nullptr, m, d_len, w);
+    if ((e = hipMemcpy(&t, w + m, sizeof(t), hipMemcpyDeviceToHost)) != hipSuccess) {
+        rc = gerr(e, "lengths");
+        goto done;
+    }
+    if (t > (unsigned long long)INT32_MAX) {
+        rc = mfail(AIJHIP_ERR_STATE, "distributed GAMG: a local operator past int32 entries");
+        goto done;
+    }
+    *total = (int64_t)t;
+    if ((e = dalloc(d_off, (int64_t)m + 1)) != hipSuccess) {
+        rc = gerr(e, "offsets");
+        goto done;
+    }
+    hipLaunchKernelGGL(k_narrow_off, dim3(nblk((int64_t)m + 1)), dim3(256), 0, nullptr, m + 1, w, *d_off);
+    if ((e = hipGetLastError()) != hipSuccess) rc = gerr(e, "offsets");
+done:
+    hipFree(w);
+    hipFree(tmp);
+    if (rc) {
+        hipFree(*d_off);
+        *d_off = nullptr;
+    }
+    return rc;
 }
 
 // C = [A | B] (B: full row pointer bi, columns shifted by boff); bi may be null
@@ -603,6 +640,48 @@ static int make_operator(aijhip_comm *C, aijhip_mat *Ad, aijhip_mat *Ao, const s
                                 (int32_t)recv_peer.size(), recv_peer.data(), recv_off.data(), 0, out);
 }
 
+// A level's interpolation handles (P_d with R_d = P_d^T attached, and P_o)
+// made on a second host thread, as the single-GPU set-up does: planning
+// P_d's STREAM handle reads its row offsets back to the host, and nothing
+// needs the handles before the V-cycle. No communication inside.
+struct PJob {
+    std::thread th;
+    size_t level = 0;
+    int rc = AIJHIP_OK;
+    std::string err;
+    aijhip_mat *Pd = nullptr, *Po = nullptr;
+    void start(int device, size_t l, DCsr pd, DCsr po) {
+        level = l;
+        th = std::thread([this, device, pd, po]() mutable {
+            (void)hipSetDevice(device);
+            rc = aijhip_gamg::make_level_handle(device, pd, &Pd);
+            if (!rc) {
+                int32_t *ti = nullptr, *tj = nullptr;
+                double *ta = nullptr;
+                const hipError_t e = aijhip::build_transpose(*Pd, &ti, &tj, &ta, nullptr);
+                rc = e != hipSuccess ? gerr(e, "P^T") : aijhip::attach_transpose(Pd, ti, tj, ta);
+            }
+            if (!rc && po.nz > 0) rc = aijhip_gamg::make_level_handle(device, po, &Po);
+            po.release();
+            pd.release();
+            if (rc) {
+                err = aijhip_last_error();
+                aijhip_mat_destroy(Pd);
+                aijhip_mat_destroy(Po);
+                Pd = Po = nullptr;
+            }
+        });
+    }
+    void join() {
+        if (th.joinable()) th.join();
+    }
+    ~PJob() {
+        join();
+        aijhip_mat_destroy(Pd);
+        aijhip_mat_destroy(Po);
+    }
+};
+
 int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
     aijhip::Range range("PCSetUp_GAMG (MPIAIJ)");
     H.destroy();
@@ -621,6 +700,9 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
     };
     const int P = C->nranks, me = C->rank;
     const int n_cu = std::max(M0->Ad->n_cu, 1);
+    const char *hs = std::getenv("AIJHIP_GAMG_HANDLE_SYNC");
+    const bool in_line = hs && hs[0] == '1';
+    std::vector<std::unique_ptr<PJob>> jobs;
     hipError_t e;
     int rc = AIJHIP_OK;
     // ---- level 0: the caller's operator and its ghost global ids
@@ -657,23 +739,74 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
     // the near-null space of the current level (ones at the top)
     double *d_B = nullptr;
     if ((e = dalloc(&d_B, H.lv[0].m)) != hipSuccess) return gerr(e, "alloc");
-    {
-        std::vector<double> ones((size_t)std::max(H.lv[0].m, 1), 1.0);
-        if ((e = hipMemcpy(d_B, ones.data(), sizeof(double) * (size_t)H.lv[0].m, hipMemcpyHostToDevice)) != hipSuccess) {
-            hipFree(d_B);
-            return gerr(e, "near-null space");
-        }
-    }
+    if (H.lv[0].m > 0)
+        hipLaunchKernelGGL(k_fill_value, dim3(nblk(H.lv[0].m)), dim3(256), 0, nullptr, H.lv[0].m, 1.0, d_B);
+    lap(0, "ghost ids, B");
     for (;;) {
         const size_t l = H.lv.size() - 1;
         Level &L = H.lv[l];
         const int32_t m = L.m;
         const int64_t M = L.starts[P];
         if ((int32_t)H.lv.size() >= p.max_levels || M <= p.coarse_eq_limit) break;
+        // ---- emax(D^-1 A) of the distributed operator, on a second host
+        // thread while this one forms the local aggregates (which need no
+        // communication; the thread's halo exchanges and all-reduces are the
+        // only collectives in flight, in the same order on every rank, and it
+        // is joined before the next one below)
+        double emax = 1.0;
+        int emax_rc = AIJHIP_OK;
+        std::string emax_err;
+        double *dinv_e = nullptr;
+        std::thread emax_th;
+        if (p.nsmooths > 0) {
+            if ((e = dalloc(&dinv_e, m)) != hipSuccess) {
+                rc = gerr(e, "alloc");
+                break;
+            }
+            if (m > 0)
+                hipLaunchKernelGGL(k_diag_inv, dim3(nblk(m)), dim3(256), 0, nullptr, m, L.Ad->d_ai, L.Ad->d_aj,
+                                   L.Ad->d_aa, dinv_e);
+            emax_th = std::thread([&, dev = L.Ad->device]() {
+                (void)hipSetDevice(dev);
+                double *v = nullptr, *w = nullptr, *part = nullptr;
+                hipError_t x;
+                if ((x = dalloc(&v, m)) != hipSuccess || (x = dalloc(&w, m)) != hipSuccess ||
+                    (x = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
+                    emax_rc = gerr(x, "alloc");
+                double nv = 0.0;
+                if (!emax_rc) {
+                    if (m > 0) hipLaunchKernelGGL(k_power_start_off, dim3(nblk(m)), dim3(256), 0, nullptr, m, L.rstart, v);
+                    emax_rc = global_norm(C, v, m, part, &nv);
+                }
+                if (!emax_rc && m > 0) hipLaunchKernelGGL(k_divide, dim3(nblk(m)), dim3(256), 0, nullptr, m, v, nv, v);
+                for (int it = 0; !emax_rc && it < p.eig_its; ++it) {
+                    if ((emax_rc = aijhip_mpi::mpiaij_apply(L.op, v, w, nullptr, nullptr, nullptr, nullptr, false))) break;
+                    if (m > 0) hipLaunchKernelGGL(k_scale_by, dim3(nblk(m)), dim3(256), 0, nullptr, m, dinv_e, w);
+                    double nw = 0.0;
+                    if ((emax_rc = global_norm(C, w, m, part, &nw))) break;
+                    if (!(nw > 0.0)) break;
+                    emax = nw;
+                    if (m > 0) hipLaunchKernelGGL(k_divide, dim3(nblk(m)), dim3(256), 0, nullptr, m, w, nw, v);
+                }
+                (void)hipStreamSynchronize(nullptr);
+                hipFree(v); hipFree(w); hipFree(part);
+                if (emax_rc) emax_err = aijhip_last_error();
+            });
+        }
         // ---- local aggregates
         int32_t *d_agg = nullptr, na = 0;
         double *dinv = nullptr;
-        if ((rc = aijhip_gamg::aggregate_level(*L.Ad, p, &d_agg, &na, &dinv, 0, nullptr, nullptr, l))) break;
+        rc = aijhip_gamg::aggregate_level(*L.Ad, p, &d_agg, &na, &dinv, 0, nullptr, nullptr, l);
+        if (emax_th.joinable()) emax_th.join();
+        hipFree(dinv_e);
+        if (!rc && emax_rc) {
+            rc = emax_rc;
+            aijhip::set_error(emax_err);
+        }
+        if (rc) {
+            hipFree(d_agg); hipFree(dinv);
+            break;
+        }
         std::vector<int64_t> na_all;
         if ((rc = all_values(C, na, na_all))) {
             hipFree(d_agg); hipFree(dinv);
@@ -689,41 +822,13 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
             hipFree(d_agg); hipFree(dinv);
             break;
         }
-        // ---- emax(D^-1 A) of the distributed operator
-        double emax = 1.0;
-        if (p.nsmooths > 0) {
-            double *v = nullptr, *w = nullptr, *part = nullptr;
-            if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
-                (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
-                rc = gerr(e, "alloc");
-            double nv = 0.0;
-            if (!rc) {
-                if (m > 0) hipLaunchKernelGGL(k_power_start_off, dim3(nblk(m)), dim3(256), 0, nullptr, m, L.rstart, v);
-                rc = global_norm(C, v, m, part, &nv);
-            }
-            if (!rc && m > 0) hipLaunchKernelGGL(k_divide, dim3(nblk(m)), dim3(256), 0, nullptr, m, v, nv, v);
-            for (int it = 0; !rc && it < p.eig_its; ++it) {
-                if ((rc = aijhip_mpi::mpiaij_apply(L.op, v, w, nullptr, nullptr, nullptr, nullptr, false))) break;
-                if (m > 0) hipLaunchKernelGGL(k_scale_by, dim3(nblk(m)), dim3(256), 0, nullptr, m, dinv, w);
-                double nw = 0.0;
-                if ((rc = global_norm(C, w, m, part, &nw))) break;
-                if (!(nw > 0.0)) break;
-                emax = nw;
-                if (m > 0) hipLaunchKernelGGL(k_divide, dim3(nblk(m)), dim3(256), 0, nullptr, m, w, nw, v);
-            }
-            hipFree(v); hipFree(w); hipFree(part);
-            if (rc) {
-                hipFree(d_agg); hipFree(dinv);
-                break;
-            }
-        }
         lap(l, "emax");
         const double alpha = -p.smooth_scale / emax;
         // ---- tentative prolongator and its ghost rows (aggregate gid, value)
         double *d_p0 = nullptr, *d_Bc = nullptr, *d_v = nullptr;
         std::vector<double> g_agg, g_p0;
         if ((e = dalloc(&d_p0, m)) != hipSuccess || (e = dalloc(&d_Bc, na)) != hipSuccess ||
-            (e = dalloc(&d_v, m)) != hipSuccess || (e = aijhip_gamg::tentative_device(m, na, d_agg, d_B, d_Bc, d_p0)) !=
+            (e = dalloc(&d_v, m)) != hipSuccess || (e = aijhip_gamg::tentative_device(m, na, d_agg, d_B, d_Bc, d_p0, l == 0)) !=
                                                        hipSuccess)
             rc = gerr(e, "tentative prolongator");
         if (!rc) {
@@ -909,23 +1014,25 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
                 hipLaunchKernelGGL(k_add_offset, dim3(nblk(ng)), dim3(256), 0, nullptr, ng, (int32_t)nzl, d_gi + 1,
                                    Pext.ai + m + 1);
             hipFree(d_gi);
-            // R_o rows (own coarse c): the ghost fine rows' entries in own columns, by slot
-            if (!rc) {
-                std::vector<std::vector<std::pair<int32_t, double>>> rrows((size_t)na);
+            // R_o rows (own coarse c): the ghost fine rows' entries in own
+            // columns, by slot (a counting pass, then the entries in (slot,
+            // entry) order; nothing when the rank has no ghosts)
+            if (!rc && ng > 0) {
+                std::vector<int32_t> ri((size_t)na + 1, 0);
+                for (int32_t s = 0; s < ng; ++s)
+                    for (int64_t c : gcols[s])
+                        if (c >= cstart && c < cstart + na) ++ri[c - cstart + 1];
+                for (int32_t c = 0; c < na; ++c) ri[c + 1] += ri[c];
+                std::vector<int32_t> rj((size_t)ri[na]), pos(ri.begin(), ri.end() - 1);
+                std::vector<double> ra((size_t)ri[na]);
                 for (int32_t s = 0; s < ng; ++s)
                     for (size_t k = 0; k < gcols[s].size(); ++k) {
                         const int64_t c = gcols[s][k];
-                        if (c >= cstart && c < cstart + na) rrows[c - cstart].emplace_back(s, gvals[s][k]);
+                        if (c < cstart || c >= cstart + na) continue;
+                        const int32_t q = pos[c - cstart]++;
+                        rj[q] = s;
+                        ra[q] = gvals[s][k];
                     }
-                std::vector<int32_t> ri{0}, rj;
-                std::vector<double> ra;
-                for (auto &row : rrows) {
-                    for (auto &x : row) {
-                        rj.push_back(x.first);
-                        ra.push_back(x.second);
-                    }
-                    ri.push_back((int32_t)rj.size());
-                }
                 if (!rj.empty())
                     rc = aijhip_mat_create(L.Ad->device, na, ng, (int64_t)rj.size(), ri.data(), rj.data(), ra.data(),
                                            &L.Ro);
@@ -1068,14 +1175,20 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
         if (!rc) rc = aijhip_gamg::make_level_handle(L.Ad->device, Cd, &Adn);
         if (!rc && Co.nz > 0) rc = aijhip_gamg::make_level_handle(L.Ad->device, Co, &Aon);
         Co.release();
-        if (!rc) rc = aijhip_gamg::make_level_handle(L.Ad->device, Pd, &L.Pd);
-        if (!rc) {  // R_d = P_d^T attached for the restriction
+        if (!rc && !in_line) {  // P_d (with R_d = P_d^T) and P_o on a second host thread
+            jobs.emplace_back(new PJob());
+            jobs.back()->start(L.Ad->device, l, Pd, Po);
+            Pd = DCsr();  // owned by the job now
+            Po = DCsr();
+        }
+        if (!rc && in_line) rc = aijhip_gamg::make_level_handle(L.Ad->device, Pd, &L.Pd);
+        if (!rc && in_line) {  // R_d = P_d^T attached for the restriction
             int32_t *ti = nullptr, *tj = nullptr;
             double *ta = nullptr;
             if ((e = aijhip::build_transpose(*L.Pd, &ti, &tj, &ta, nullptr)) != hipSuccess) rc = gerr(e, "P^T");
             else rc = aijhip::attach_transpose(L.Pd, ti, tj, ta);
         }
-        if (!rc && Po.nz > 0) rc = aijhip_gamg::make_level_handle(L.Ad->device, Po, &L.Po);
+        if (!rc && in_line && Po.nz > 0) rc = aijhip_gamg::make_level_handle(L.Ad->device, Po, &L.Po);
         Po.release();
         Pd.release();
         Cd.release();
@@ -1106,6 +1219,20 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
         if (rc) break;
     }
     hipFree(d_B);
+    for (auto &j : jobs) {  // the interpolation handles made meanwhile
+        j->join();
+        if (j->rc) {
+            if (!rc) {
+                rc = j->rc;
+                aijhip::set_error(j->err);
+            }
+            continue;
+        }
+        H.lv[j->level].Pd = j->Pd;
+        H.lv[j->level].Po = j->Po;
+        j->Pd = j->Po = nullptr;
+    }
+    jobs.clear();
     // level vectors and D^-1
     for (size_t l = 0; !rc && l < H.lv.size(); ++l) {
         Level &L = H.lv[l];
