@@ -103,6 +103,10 @@ typedef struct aijhip_info {
     int32_t persistent;      /* workgroups per CU of the pipelined STREAM (0 = off) */
     int32_t exact;           /* AIJHIP_OPT_EXACT in effect                   */
     int32_t x_tiled_blocks;  /* STREAM blocks gathering x from an LDS tile    */
+    int32_t gather_sorted;   /* MatMult reads the gather-ordered copy of the
+                                row blocks (AIJHIP_OPT_GATHER_SORT): 1 with
+                                32-bit columns, 2 with 16-bit block-relative
+                                columns (every block spans < 2^16); 0 off   */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -181,7 +185,7 @@ enum {
                                        blocks (forked from and joined back to
                                        the caller's stream); 0 (default): one
                                        stream. Same results                  */
-    AIJHIP_OPT_ROW_GROUP = 11       /* MatMult / MatMultAdd of row blocks whose
+    AIJHIP_OPT_ROW_GROUP = 11,      /* MatMult / MatMultAdd of row blocks whose
                                        mean row length is at least 24, when
                                        AIJHIP_OPT_EXACT is 0: 1 = a register
                                        kernel, 2..64 lanes per row summing
@@ -191,6 +195,17 @@ enum {
                                        0 = the LDS STREAM block; -1 (default)
                                        = automatic. Rows of shorter blocks
                                        stay bit-exact either way            */
+    AIJHIP_OPT_GATHER_SORT = 12     /* MatMult / MatMultAdd from a copy of the
+                                       row blocks with each block's entries
+                                       sorted by column and their positions
+                                       in the block: x is gathered in column
+                                       order, the products are summed in the
+                                       rows' storage order (the same bits).
+                                       1 on, 0 off, -1 (default): on for
+                                       operands with scattered gathers (long
+                                       rows, > 0.25 distinct x lines per
+                                       entry); costs a second copy of the
+                                       entries plus 2 bytes each            */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

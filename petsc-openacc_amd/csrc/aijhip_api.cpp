@@ -76,6 +76,13 @@ void free_plan(aijhip::Plan &P) {
     if (P.ev_join) (void)hipEventDestroy(P.ev_join);
     if (P.long_stream) (void)hipStreamDestroy(P.long_stream);
     hipFree(P.d_xrange);
+    hipFree(P.d_saj);
+    hipFree(P.d_saa);
+    hipFree(P.d_sslot);
+    hipFree(P.d_sidx);
+    hipFree(P.d_sbase);
+    hipFree(P.d_nblocks);
+    hipFree(P.d_wblocks);
     hipFree(P.d_sblocks);
     hipFree(P.d_gblocks);
     hipFree(P.d_tile_coord);
@@ -263,6 +270,84 @@ int plan_stream(aijhip_mat *A) {
             hipFree(d_xr);
         }
     }
+    // gather-ordered copy of the row blocks (Tuning::gsort): for the plain
+    // MatMult / MatMultAdd launch (not with the x tiles, the row groups or
+    // the persistent kernel, which read the original order)
+    if (P.tune.gsort > 0 && !blocks.empty() && P.d_xrange == nullptr && P.n_gblocks == 0 && P.tune.persist == 0) {
+        const size_t nzp = (size_t)A->nz + 2;
+        if ((e = dmalloc(&P.d_saj, nzp, &P.bytes)) != hipSuccess || (e = dmalloc(&P.d_saa, nzp, &P.bytes)) != hipSuccess ||
+            (e = dmalloc(&P.d_sslot, nzp, &P.bytes)) != hipSuccess ||
+            (e = hipMemset(P.d_saj, 0, sizeof(int32_t) * nzp)) != hipSuccess ||
+            (e = hipMemset(P.d_saa, 0, sizeof(double) * nzp)) != hipSuccess ||
+            (e = hipMemset(P.d_sslot, 0, sizeof(uint16_t) * nzp)) != hipSuccess ||
+            (e = aijhip::build_gather_order(*A, P, false)) != hipSuccess)
+            return hipfail(e, "plan: gather-ordered blocks");
+        // 16-bit columns when every block's columns span < 2^16 (banded
+        // operators): the packed form replaces the 32-bit sorted columns
+        int32_t *d_base = nullptr, *d_span = nullptr;
+        std::vector<int32_t> span((size_t)P.n_blocks);
+        if ((e = dmalloc(&d_base, (size_t)P.n_blocks, nullptr)) != hipSuccess ||
+            (e = dmalloc(&d_span, (size_t)P.n_blocks, nullptr)) != hipSuccess ||
+            (e = aijhip::gather_order_spans(P, d_base, d_span)) != hipSuccess ||
+            (e = hipMemcpy(span.data(), d_span, sizeof(int32_t) * span.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
+            hipFree(d_base);
+            hipFree(d_span);
+            return hipfail(e, "plan: gather-ordered spans");
+        }
+        hipFree(d_span);
+        // blocks whose columns span < 2^16 take the 16-bit form; when most
+        // do, the others (a wide row within the block cap) are launched from
+        // the original arrays
+        int64_t narrow_nz = 0, nz_all = 0;
+        for (size_t b = 0; b < blocks.size(); ++b) {
+            nz_all += blocks[b].nk;
+            if (span[b] < 65536) narrow_nz += blocks[b].nk;
+        }
+        if (narrow_nz > 0 && 10 * narrow_nz >= 9 * nz_all) {
+            std::vector<BlockDesc> nb, wb;
+            std::vector<int32_t> nbase, base((size_t)P.n_blocks);
+            if ((e = hipMemcpy(base.data(), d_base, sizeof(int32_t) * base.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
+                hipFree(d_base);
+                return hipfail(e, "plan: gather-ordered spans");
+            }
+            for (size_t b = 0; b < blocks.size(); ++b) {
+                if (span[b] < 65536) {
+                    nb.push_back(blocks[b]);
+                    nbase.push_back(base[b]);
+                } else {
+                    wb.push_back(blocks[b]);
+                }
+            }
+            hipFree(d_base);
+            const size_t words = 4 * ((size_t)A->nz / 2 + 2);
+            if ((e = dmalloc(&P.d_sidx, words, &P.bytes)) != hipSuccess ||
+                (e = hipMemset(P.d_sidx, 0, sizeof(uint16_t) * words)) != hipSuccess ||
+                (e = dmalloc(&P.d_sbase, nbase.size(), &P.bytes)) != hipSuccess ||
+                (e = hipMemcpy(P.d_sbase, nbase.data(), sizeof(int32_t) * nbase.size(), hipMemcpyHostToDevice)) !=
+                    hipSuccess)
+                return hipfail(e, "plan: gather-ordered 16-bit form");
+            if (!wb.empty()) {
+                if ((e = dmalloc(&P.d_nblocks, nb.size(), &P.bytes)) != hipSuccess ||
+                    (e = dmalloc(&P.d_wblocks, wb.size(), &P.bytes)) != hipSuccess ||
+                    (e = hipMemcpy(P.d_nblocks, nb.data(), sizeof(BlockDesc) * nb.size(), hipMemcpyHostToDevice)) !=
+                        hipSuccess ||
+                    (e = hipMemcpy(P.d_wblocks, wb.data(), sizeof(BlockDesc) * wb.size(), hipMemcpyHostToDevice)) !=
+                        hipSuccess)
+                    return hipfail(e, "plan: gather-ordered block lists");
+                P.n_nblocks = (int32_t)nb.size();
+                P.n_wblocks = (int32_t)wb.size();
+            }
+            if ((e = aijhip::pack_gather_order(P, wb.empty() ? P.d_blocks : P.d_nblocks, (int32_t)nb.size(), P.d_sbase,
+                                               P.d_sidx)) != hipSuccess ||
+                (e = hipDeviceSynchronize()) != hipSuccess)
+                return hipfail(e, "plan: gather-ordered 16-bit form");
+            hipFree(P.d_saj);  // (d_sslot stays: it re-orders new values, aijhip_mat_update_values)
+            P.bytes -= (int64_t)sizeof(int32_t) * (int64_t)nzp;
+            P.d_saj = nullptr;
+        } else {
+            hipFree(d_base);
+        }
+    }
     if (!longs.empty()) {
         if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
@@ -335,7 +420,9 @@ int plan_build(aijhip_mat *A) {
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
     P.tune = A->requested_tune;
-    if (P.tune.geom < 0 || P.tune.nt < 0) {
+    const bool auto_sort = P.tune.gsort < 0;
+    bool scattered = false;
+    if (P.tune.geom < 0 || P.tune.nt < 0 || P.tune.gsort < 0) {
         // measured: 512 x 4094-entry blocks (geometry 6, 8 waves/SIMD) for
         // short rows (7-pt Poisson, profiles/r01/tune04) and for long rows
         // whose gathers run along x lines (FEM-structured stand-in: 283 vs
@@ -345,20 +432,46 @@ int plan_build(aijhip_mat *A) {
         // loads for the scattered ones (skewed 398 vs 411 us; Poisson and the
         // FEM stand-in are neutral to slower: profiles/r02/ntlong/)
         const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
-        bool scattered = false;
-        if (nr > 0 && A->nz > (int64_t)16 * nr) {
+        const bool long_rows = nr > 0 && A->nz > (int64_t)16 * nr;
+        if (long_rows) {
             double lpe = 1.0;
             const hipError_t e = aijhip::gather_lines_per_entry(*A, &lpe);
             if (e != hipSuccess) return hipfail(e, "plan: gather locality");
             scattered = lpe > aijhip::kScatteredLinesPerEntry;
         }
-        if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
-        if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
+        // Long rows on a caller's handle: the gather-ordered copy of the row
+        // blocks (Tuning::gsort; x read in column order within a block, the
+        // sums unchanged) at geometry 6, plain loads, when its 16-bit form
+        // fits (below) — measured: skewed stand-in 406 -> 325 us, its
+        // ordinary rows 342 -> 256, the FEM-structured one 287 -> 271
+        // (profiles/r03/gsort_*.jsonl); the 7-pt Poisson (short rows) stays
+        // unsorted (sorted: 551 vs 492 us). The set-up's own operators (GAMG
+        // levels: gsort 0) keep one copy of their entries.
+        if (P.tune.gsort < 0) P.tune.gsort = long_rows ? 1 : 0;
+        const bool sorted = P.tune.gsort > 0;
+        if (P.tune.geom < 0) P.tune.geom = (scattered && !sorted) ? 1 : 6;
+        if (P.tune.nt < 0) P.tune.nt = (scattered && !sorted) ? 1 : 0;
     }
     if (P.tune.group < 0) P.tune.group = 0;  // automatic choice: off until measured
     switch (kernel) {
-        case AIJHIP_KERNEL_STREAM:
-            return plan_stream(A);
+        case AIJHIP_KERNEL_STREAM: {
+            int rc = plan_stream(A);
+            if (!rc && auto_sort && P.tune.gsort > 0 && !P.d_sidx) {
+                // automatic and the 16-bit form did not fit (blocks spanning
+                // 2^16 columns and more): the original layout, the geometry
+                // and loads the gather locality picks without it
+                const aijhip::Tuning req = A->requested_tune;
+                free_plan(A->plan);
+                P.kernel = kernel;
+                P.tune = req;
+                P.tune.gsort = 0;
+                if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
+                if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
+                if (P.tune.group < 0) P.tune.group = 0;
+                rc = plan_stream(A);
+            }
+            return rc;
+        }
         case AIJHIP_KERNEL_SCALAR:
             return AIJHIP_OK;
         case AIJHIP_KERNEL_VECTOR: {
@@ -583,6 +696,7 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
     A->d_aj = d_aj;
     A->d_aa = d_aa;
     A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
+    if (!like) A->requested_tune.gsort = 0;  // the set-up's own operators: one copy of the entries
     aijhip::HostVec<int32_t> h_ai;
     int rc = AIJHIP_OK;
     hipError_t e = hipSuccess;
@@ -712,6 +826,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
                 return fail(AIJHIP_ERR_ARG, "row_group: -1 auto, 0 off, 1 on (256 lanes), 2 on (512 lanes)");
             t.group = value;
             break;
+        case AIJHIP_OPT_GATHER_SORT:
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "gather_sort: -1 auto, 0 off, 1 on");
+            t.gsort = value;
+            break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -731,6 +849,8 @@ int aijhip_mat_update_values(aijhip_mat_t A, const double *aa) {
     hipError_t e = hipDeviceSynchronize();
     if (e == hipSuccess && A->nz > 0)
         e = hipMemcpy(A->d_aa, aa, sizeof(double) * (size_t)A->nz, hipMemcpyHostToDevice);
+    if (e == hipSuccess && A->plan.d_sslot)  // the gather-ordered copy of the values
+        e = aijhip::build_gather_order(*A, A->plan, true);
     if (e != hipSuccess) return hipfail(e, "update values");
     if (A->transpose) {  // A^T values are stale
         free_matrix(A->transpose);
@@ -899,6 +1019,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->persistent = A->plan.tune.persist;
     info->exact = A->plan.tune.exact ? 1 : 0;
     info->x_tiled_blocks = A->plan.n_xtiled;
+    info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
     return AIJHIP_OK;
 }
 

@@ -105,6 +105,8 @@ struct Tuning {
                            // k > 0 pipelined in chunks of >= k rows
     int group = -1;        // register row-group kernel for blocks of mean row length >= kGroupMinMean
                            // (plain MatMult / MatMultAdd, exact = 0): -1 auto, 0 off, 1 on
+    int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
+                           // (operands with scattered gathers, caller's handles), 0 off, 1 on
 };
 
 struct HostPipe;  // host-vector MatMult pipeline state (host_pipe.cpp)
@@ -161,6 +163,22 @@ struct Plan {
     // MatMultAdd launch; d_blocks keeps all of them (fused epilogues)
     BlockDesc *d_sblocks = nullptr, *d_gblocks = nullptr;
     int32_t n_sblocks = 0, n_gblocks = 0;
+    // Tuning::gsort: each row block's entries sorted by column (columns,
+    // values) and their positions in the block (the products' LDS slots)
+    int32_t *d_saj = nullptr;
+    double *d_saa = nullptr;
+    uint16_t *d_sslot = nullptr;
+    // ... or, when every block's columns span < 2^16, 16-bit columns
+    // (relative to the block's first, d_sbase) and slots packed four per
+    // entry pair in d_sidx (d_saj / d_sslot then freed): 12 bytes per entry
+    uint16_t *d_sidx = nullptr;
+    int32_t *d_sbase = nullptr;
+    // ... and when only some blocks are that narrow (a wide row within the
+    // block cap: the skewed stand-in's shorter hub rows), the narrow blocks
+    // in d_nblocks (d_sbase follows their order) and the others in
+    // d_wblocks, launched from the original arrays
+    BlockDesc *d_nblocks = nullptr, *d_wblocks = nullptr;
+    int32_t n_nblocks = 0, n_wblocks = 0;
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;
     int32_t n_tiles = 0;
@@ -249,6 +267,16 @@ RowList row_list(const aijhip_mat &A);
 hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out);
 // Per STREAM block: min column and span (max - min + 1) of its entries.
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out);
+// The gather-ordered copy of the plan's row blocks (Plan::d_saj/d_saa/
+// d_sslot, allocated by the caller); values_only: the values again, in the
+// order already built.
+hipError_t build_gather_order(const aijhip_mat &A, const Plan &P, bool values_only);
+// Per block: first sorted column and the span of its columns (after build_gather_order).
+hipError_t gather_order_spans(const Plan &P, int32_t *d_base, int32_t *d_span);
+// The 16-bit packed form of the sorted columns and slots of blocks
+// d_blk[0, nblk) (d_base: their first columns, in that order).
+hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk, const int32_t *d_base,
+                             uint16_t *d_sidx);
 // Distinct 128-B x lines per entry over a row sample (at most 65536 rows):
 // ~0.7 for the 7-point stencil, ~0.17 for a 3-dof hexahedral FEM operator.
 hipError_t gather_lines_per_entry(const aijhip_mat &A, double *out);

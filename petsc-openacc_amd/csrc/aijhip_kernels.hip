@@ -248,9 +248,19 @@ template <int T, int CAP, int RPT, bool CROW, bool XCD, int NTMODE, bool CLAMPED
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const int2 *__restrict__ xrange) {
+    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const int2 *__restrict__ xrange,
+    const uint16_t *__restrict__ sslot, const int32_t *__restrict__ sbase) {
     constexpr int NT = NTMODE & 3;
     constexpr bool SHUF = (NTMODE & 4) != 0;
+    // bit 3: gather-ordered blocks (Plan::d_saj/d_saa): aj/aa hold each
+    // block's entries sorted by column, sslot their positions in the block,
+    // where the products go; the row sums below read them in storage order
+    constexpr bool SORTED = (NTMODE & 8) != 0;
+    // bit 4: the same with 16-bit columns and slots packed per entry pair in
+    // aj's place (aj[k], aj[k+1] = cols | slots << 16 ... see pack below):
+    // one 8-B load per pair as in CSR, columns relative to the block's
+    // first (sbase[b]); 12 bytes per entry like the original arrays
+    constexpr bool S16 = (NTMODE & 16) != 0;
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     __shared__ double prod[CAP];
     const int bid = (int)blockIdx.x;
@@ -303,6 +313,24 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
                 av[it] = ld_stream<NT == 1>(reinterpret_cast<const f64x2 *>(aa + kc));
                 cv[it] = ld_stream<NT == 1>(reinterpret_cast<const i32x2 *>(aj + kc));
             }
+        }
+    }
+    uint32_t sv[(SORTED || S16) ? ITERS : 1];  // the pairs' product slots (two 16-bit positions)
+    if constexpr (S16) {  // unpack: .x = two 16-bit columns (block-relative), .y = two slots
+        const int32_t base = sbase[b];
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const uint32_t c = (uint32_t)cv[it].x;
+            sv[it] = (uint32_t)cv[it].y;
+            cv[it].x = base + (int32_t)(c & 0xffffu);
+            cv[it].y = base + (int32_t)(c >> 16);
+        }
+    }
+    if constexpr (SORTED) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
+            if (k < k1) sv[it] = *reinterpret_cast<const uint32_t *>(sslot + k);
         }
     }
     // x tile: the block's columns [xr.x, xr.x + xr.y) staged in LDS (the
@@ -360,8 +388,10 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (k < k1) {
-            if (k >= k0) prod[k - k0] = av[it].x * xv[it].x;
-            if (k + 1 < k1) prod[k + 1 - k0] = av[it].y * xv[it].y;
+            const int s0 = (SORTED || S16) ? (int)(sv[it] & 0xffffu) : (int)(k - k0);
+            const int s1 = (SORTED || S16) ? (int)(sv[it] >> 16) : (int)(k + 1 - k0);
+            if (k >= k0) prod[s0] = av[it].x * xv[it].x;
+            if (k + 1 < k1) prod[s1] = av[it].y * xv[it].y;
         }
     }
     __syncthreads();
@@ -903,6 +933,122 @@ __global__ __launch_bounds__(256) void k_block_xrange(const BlockDesc *__restric
 }
 }  // namespace
 
+// Gather-ordered row blocks (Tuning::gsort): one workgroup sorts its
+// block's entries by column (ties by position; bitonic over the next power
+// of two) and writes the sorted columns, the values in that order and each
+// entry's position in the block. x is then gathered in column order — a
+// wave's 64 lanes read a few x lines instead of one per scattered node —
+// while the products land at their storage positions, so the row sums (and
+// their bits) are the unsorted kernel's.
+template <int N>
+__global__ __launch_bounds__(256) void k_block_gather_order(const BlockDesc *__restrict__ blk,
+                                                            const int32_t *__restrict__ aj,
+                                                            const double *__restrict__ aa, int32_t *saj,
+                                                            double *saa, uint16_t *sslot) {
+    __shared__ unsigned long long key[N];
+    const BlockDesc d = blk[blockIdx.x];
+    const int t = threadIdx.x;
+    int n2 = 2;
+    while (n2 < d.nk) n2 <<= 1;
+    for (int i = t; i < n2; i += 256)
+        key[i] = i < d.nk ? ((unsigned long long)(uint32_t)aj[(int64_t)d.k0 + i] << 16) | (unsigned)i : ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < n2; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const unsigned long long a = key[i], b = key[ixj];
+                    if ((a > b) == ((i & k) == 0)) {
+                        key[i] = b;
+                        key[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = t; i < d.nk; i += 256) {
+        const unsigned long long v = key[i];
+        const int slot = (int)(v & 0xffffu);
+        const int64_t k = (int64_t)d.k0 + i;
+        saj[k] = (int32_t)(v >> 16);
+        sslot[k] = (uint16_t)slot;
+        saa[k] = aa[(int64_t)d.k0 + slot];
+    }
+}
+
+// The block's column span after the sort: (first column, last - first)
+__global__ void k_block_col_span(const BlockDesc *__restrict__ blk, int32_t nblk, const int32_t *__restrict__ saj,
+                                 int32_t *base, int32_t *span) {
+    const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nblk) return;
+    const BlockDesc d = blk[b];
+    const int32_t lo = d.nk > 0 ? saj[d.k0] : 0, hi = d.nk > 0 ? saj[(int64_t)d.k0 + d.nk - 1] : 0;
+    base[b] = lo;
+    span[b] = hi - lo;
+}
+
+// 16-bit form: entry k of pair p = k / 2 at half h = k % 2 -> column
+// (relative to the block's first) in sidx[4p + h], slot in sidx[4p + 2 + h];
+// a pair shared by two blocks gets one half from each
+__global__ __launch_bounds__(256) void k_pack_gather_order(const BlockDesc *__restrict__ blk,
+                                                           const int32_t *__restrict__ saj,
+                                                           const uint16_t *__restrict__ sslot,
+                                                           const int32_t *__restrict__ base, uint16_t *sidx) {
+    const BlockDesc d = blk[blockIdx.x];
+    const int32_t b0 = base[blockIdx.x];
+    for (int i = threadIdx.x; i < d.nk; i += 256) {
+        const int64_t k = (int64_t)d.k0 + i, p = k >> 1, h = k & 1;
+        sidx[4 * p + h] = (uint16_t)(saj[k] - b0);
+        sidx[4 * p + 2 + h] = sslot[k];
+    }
+}
+
+// The sorted values again after new values (aijhip_mat_update_values)
+__global__ __launch_bounds__(256) void k_gather_order_values(const BlockDesc *__restrict__ blk,
+                                                             const uint16_t *__restrict__ sslot,
+                                                             const double *__restrict__ aa, double *saa) {
+    const BlockDesc d = blk[blockIdx.x];
+    for (int i = threadIdx.x; i < d.nk; i += 256) {
+        const int64_t k = (int64_t)d.k0 + i;
+        saa[k] = aa[(int64_t)d.k0 + sslot[k]];
+    }
+}
+
+hipError_t build_gather_order(const aijhip_mat &A, const Plan &P, bool values_only) {
+    if (P.n_blocks == 0) return hipSuccess;
+    if (values_only) {
+        hipLaunchKernelGGL(k_gather_order_values, dim3(P.n_blocks), dim3(256), 0, nullptr, P.d_blocks, P.d_sslot,
+                           A.d_aa, P.d_saa);
+        return hipGetLastError();
+    }
+    const int cap = kStreamGeoms[P.tune.geom].nnz_cap;
+#define AIJHIP_GO(NN)                                                                                       \
+    hipLaunchKernelGGL(k_block_gather_order<NN>, dim3(P.n_blocks), dim3(256), 0, nullptr, P.d_blocks, A.d_aj, \
+                       A.d_aa, P.d_saj, P.d_saa, P.d_sslot)
+    if (cap <= 1024) AIJHIP_GO(1024);
+    else if (cap <= 2048) AIJHIP_GO(2048);
+    else if (cap <= 4096) AIJHIP_GO(4096);
+    else AIJHIP_GO(8192);
+#undef AIJHIP_GO
+    return hipGetLastError();
+}
+
+hipError_t gather_order_spans(const Plan &P, int32_t *d_base, int32_t *d_span) {
+    if (P.n_blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_block_col_span, dim3(grid_for(P.n_blocks, 256)), dim3(256), 0, nullptr, P.d_blocks,
+                       P.n_blocks, P.d_saj, d_base, d_span);
+    return hipGetLastError();
+}
+
+hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk, const int32_t *d_base,
+                             uint16_t *d_sidx) {
+    if (nblk == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_gather_order, dim3(nblk), dim3(256), 0, nullptr, d_blk, P.d_saj, P.d_sslot, d_base,
+                       d_sidx);
+    return hipGetLastError();
+}
+
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out) {
     if (n_blocks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_block_xrange, dim3(n_blocks), dim3(256), 0, nullptr, d_blocks, A.d_aj, d_out);
@@ -1002,8 +1148,49 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, XCD, NT, CL, OpMult<ADD>>), dim3(P.n_blocks), \
                        dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, (int)P.tune.exact,   \
                        L.rai, L.ridx, A.d_aj, A.d_aa,                                              \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr);             \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, nullptr); \
     return
+    // Gather-ordered blocks (Plan::d_sslot): the sorted copy, every variant
+    // (MatMult / MatMultAdd, full or compressed rows, dot epilogue)
+    // (with the narrow / wide split, the dot epilogue's partials would come
+    // from two launches: the CG's fused product takes the original arrays)
+    if (P.d_sidx && (P.n_wblocks == 0 || !dpart)) {  // 16-bit columns and slots packed per pair
+        const BlockDesc *nb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
+        const int32_t nn = P.n_wblocks ? P.n_nblocks : P.n_blocks;
+#define AIJHIP_SS(ADD, CROW)                                                                                  \
+    if (nn > 0)                                                                                               \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, false, 16, false, OpMult<ADD>>), dim3(nn), dim3(T), 0, \
+                           s, nb, nn, 0, (int)P.tune.exact, L.rai, L.ridx,                                    \
+                           reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa,                               \
+                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, P.d_sbase); \
+    if (P.n_wblocks > 0)                                                                                      \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, false, 0, false, OpMult<ADD>>), dim3(P.n_wblocks), \
+                           dim3(T), 0, s, P.d_wblocks, P.n_wblocks, 0, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, \
+                           A.d_aa, OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);    \
+    return
+        if (add && L.ridx) { AIJHIP_SS(true, true); }
+        if (add) { AIJHIP_SS(true, false); }
+        if (L.ridx) { AIJHIP_SS(false, true); }
+        AIJHIP_SS(false, false);
+#undef AIJHIP_SS
+    }
+    if (P.d_sidx) {  // split plan, fused dot: the original arrays in one launch
+        if (L.ridx) { AIJHIP_SL(false, true, false, false, false); }
+        AIJHIP_SL(false, false, false, false, false);
+    }
+    if (P.d_sslot) {
+#define AIJHIP_SS(ADD, CROW)                                                                            \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, false, 8, false, OpMult<ADD>>), dim3(P.n_blocks), \
+                       dim3(T), 0, s, P.d_blocks, P.n_blocks, 0, (int)P.tune.exact, L.rai, L.ridx, P.d_saj,  \
+                       P.d_saa, OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sslot,    \
+                       nullptr);                                                                        \
+    return
+        if (add && L.ridx) { AIJHIP_SS(true, true); }
+        if (add) { AIJHIP_SS(true, false); }
+        if (L.ridx) { AIJHIP_SS(false, true); }
+        AIJHIP_SS(false, false);
+#undef AIJHIP_SS
+    }
     // The speed knobs (XCD remap, non-temporal, clamped loads) are compiled
     // for the plain full-row MatMult, the benchmarked path; MatMultAdd and
     // the compressed-row form use the default (measured-best) form.
@@ -1011,7 +1198,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, false, false, OpMult<false, true>>),
                            dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, P.n_blocks, 0, (int)P.tune.exact, L.rai,
                            nullptr, A.d_aj, A.d_aa, OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop,
-                           P.d_xrange);
+                           P.d_xrange, nullptr, nullptr);
         return;
     }
     if (add || L.ridx) {
@@ -1090,7 +1277,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     case G:                                                                                               \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
                            dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex,                \
-                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, stop, nullptr);                    \
+                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, stop, nullptr, nullptr, nullptr);  \
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
@@ -1113,7 +1300,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, OpMult<false>>), dim3(nb), \
                            dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks + b0, nb, 0, (int)P.tune.exact,       \
                            A.d_ai, nullptr, A.d_aj, A.d_aa, OpMult<false>{x, nullptr, y, false}, nullptr, nullptr, \
-                           nullptr);                                                                             \
+                           nullptr, nullptr, nullptr);                                                           \
         break
     switch (P.tune.geom) {
         AIJHIP_BG(0); AIJHIP_BG(1); AIJHIP_BG(2); AIJHIP_BG(3); AIJHIP_BG(4);

@@ -455,6 +455,24 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
                     assert_bits(y, first, short)
                     assert_bits(y, g["y"], short)
                     check(y, g["y"], ai, aj, aa, g["x"], exact=False)
+        # the gather-ordered copy at every geometry (block caps 1024..8190),
+        # exact and default modes
+        for o, v in (("xcd_remap", 0), ("nt_loads", -1), ("persistent", 0), ("clamped", 0)):
+            A.set_option(o, v)
+        short = np.diff(ai) <= 1024
+        for geom in range(12):
+            ys = {}
+            for gs, ex in ((1, 1), (1, 0), (0, 0)):
+                A.set_option("geometry", geom)
+                A.set_option("gather_sort", gs)
+                A.set_option("exact", ex)
+                assert (A.info()["gather_sorted"] > 0) == bool(gs and A.info()["n_blocks"] > 0)
+                A.mult(xd, yd)
+                torch.cuda.synchronize()
+                ys[gs, ex] = y = yd.cpu().numpy()
+                check(y, g["y"], ai, aj, aa, g["x"], exact=False)
+            assert_bits(ys[1, 1], g["y"], short)
+            assert_bits(ys[1, 0], ys[0, 0])  # same row sums, sorted gathers or not
 
 
 def test_fem_hex_flan_standin_all_kernels(pkg, dev, coracle):
@@ -470,13 +488,84 @@ def test_fem_hex_flan_standin_all_kernels(pkg, dev, coracle):
         check(y, ref, ai, aj, aa, x, exact=kernel in BITEXACT)
 
 
-def test_auto_geometry_follows_gather_locality(pkg, dev):
-    """Automatic STREAM geometry (aijhip_api.cpp plan_build): short rows and
-    long rows gathered along x lines -> 6; long scattered rows -> 1."""
-    cases = [(pkg.poisson_csr(12), 6), (pkg.fem_hex_csr(21, 20, 19), 6), (pkg.skewed_csr(300000, seed=1565), 1)]
-    for (ai, aj, aa), geom in cases:
+def test_auto_geometry_follows_gather_locality(pkg, dev, coracle):
+    """Automatic STREAM layout (aijhip_api.cpp plan_build): short rows -> the
+    original order at geometry 6; long rows -> the gather-ordered copy in its
+    16-bit form at geometry 6; without it (gather_sort 0), long rows gathered
+    along x lines -> 6 and long scattered rows -> 1. The gather-ordered
+    product equals the unsorted one and the oracle bit for bit (rows within
+    the block cap)."""
+    cases = [(pkg.poisson_csr(12), 6, 0, 6), (pkg.fem_hex_csr(21, 20, 19), 6, 2, 6),
+             (pkg.skewed_csr(300000, seed=1565), 6, 2, 1)]  # 2: 16-bit block-relative columns
+    for (ai, aj, aa), geom, sorted_, geom_unsorted in cases:
         with pkg.SeqAIJHIP(ai, aj, aa) as A:
-            assert A.info()["stream_geometry"] == geom
+            info = A.info()
+            assert (info["stream_geometry"], info["gather_sorted"]) == (geom, sorted_)
+            if not sorted_:
+                continue
+            x = torch.from_numpy(pkg.splitmix_uniform(A.n, 42)).to(dev)
+            y1 = torch.empty(A.m, dtype=torch.float64, device=dev)
+            A.mult(x, y1)
+            A.set_option("gather_sort", 0)
+            assert A.info()["gather_sorted"] == 0 and A.info()["stream_geometry"] == geom_unsorted
+            y0 = torch.empty_like(y1)
+            A.mult(x, y0)
+            torch.cuda.synchronize()
+            assert torch.equal(y0, y1)
+            A.set_option("gather_sort", -1)
+            A.set_option("exact", 1)  # every row within the block cap in PETSc's order
+            assert A.info()["gather_sorted"] == 2
+            A.mult(x, y1)
+            torch.cuda.synchronize()
+            ref = coracle.matmult(ai, aj, aa, x.cpu().numpy(), omp=True)
+            short = np.diff(ai) <= info["stream_nnz_cap"]
+            assert np.array_equal(y1.cpu().numpy()[short].view(np.uint64), ref[short].view(np.uint64))
+
+
+@pytest.mark.parametrize("wide,form", [(0, 2), (40, 1), (4999, 2)])
+def test_gather_sort_32_and_16_bit_columns(pkg, dev, coracle, wide, form):
+    """The gather-ordered copy with 16-bit block-relative columns (every
+    block's columns within 2^16), with 32-bit columns (a row every 40
+    reaching both ends of a 90,000-column x: every block wide), and split (a
+    wide row every 4999: those blocks from the original arrays, the rest
+    16-bit): MatMult and MatMultAdd equal the unsorted kernel and the oracle
+    bit for bit (exact mode), and new values (aijhip_mat_update_values) reach
+    the sorted copy."""
+    rng = np.random.default_rng(21)
+    m = 90000
+    lens = rng.integers(40, 100, m)
+    cols = []
+    for i, l in enumerate(lens):
+        lo, hi = max(0, i - 3000), min(m, i + 3000)
+        c = np.sort(rng.choice(np.arange(lo, hi), size=l, replace=False))
+        if wide and i % wide == 0:
+            c = np.unique(np.concatenate([c, [0, m - 1]]))
+        cols.append(c)
+    ai = np.concatenate([[0], np.cumsum([len(c) for c in cols])]).astype(np.int32)
+    aj = np.concatenate(cols).astype(np.int32)
+    aa = rng.uniform(-1, 1, len(aj))
+    x = rng.uniform(-1, 1, m)
+    z = rng.uniform(-1, 1, m)
+    with pkg.SeqAIJHIP(ai, aj, aa, exact=1, gather_sort=1) as A:
+        assert A.info()["gather_sorted"] == form
+        xd, zd = to_dev(x, dev), to_dev(z, dev)
+        y = torch.empty(m, dtype=torch.float64, device=dev)
+        w = torch.empty_like(y)
+        A.mult(xd, y)
+        A.mult_add(xd, zd, w)
+        torch.cuda.synchronize()
+        assert_bits(y.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True))
+        A.set_option("gather_sort", 0)
+        w0 = torch.empty_like(y)
+        A.mult_add(xd, zd, w0)
+        torch.cuda.synchronize()
+        assert torch.equal(w, w0)
+        A.set_option("gather_sort", 1)
+        aa2 = rng.uniform(-1, 1, len(aj))
+        A.update_values(aa2)
+        A.mult(xd, y)
+        torch.cuda.synchronize()
+        assert_bits(y.cpu().numpy(), coracle.matmult(ai, aj, aa2, x, omp=True))
 
 
 @pytest.mark.parametrize("case", ["skewed", "fem_hex", "mixed"])

@@ -40,7 +40,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--variants", default="stream")
-    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx", "fem_hex"])
+    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx", "skewed_blocksort", "fem_hex"])
     ap.add_argument("--file", default=None, help="a MatrixMarket (.mtx) or PETSc binary operand, e.g. Flan_1565.mtx")
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
@@ -59,13 +59,28 @@ def main():
         ai, aj, aa = pkg.fem_hex_csr()
     else:
         ai, aj, aa = pkg.skewed_csr()
-        if args.matrix in ("skewed_nohub", "skewed_localx"):  # the FEM-like rows only (hub rows emptied)
+        if args.matrix in ("skewed_nohub", "skewed_localx", "skewed_blocksort"):  # the FEM-like rows only (hub rows emptied)
             ln = np.diff(ai)
             keep = np.repeat(ln <= 1000, ln)
             ai = np.concatenate([[0], np.cumsum(np.where(ln <= 1000, ln, 0))]).astype(np.int32)
             aj, aa = aj[keep], aa[keep]
         if args.matrix == "skewed_localx":  # experiment: same stream, x gathers confined to 32 KiB
             aj = (aj & 4095).astype(np.int32)
+        if args.matrix == "skewed_blocksort":  # experiment: each ~4096-entry row block's columns sorted
+            # across the block (the gather pattern a column-sorted in-block
+            # layout would give; the rows' sums change, the stream does not)
+            ln = np.diff(ai)
+            aj = aj.copy()
+            r0 = 0
+            while r0 < len(ln):
+                r1, nk = r0, 0
+                while r1 < len(ln) and r1 - r0 < 512 and nk + ln[r1] <= 4096:
+                    nk += ln[r1]
+                    r1 += 1
+                r1 = max(r1, r0 + 1)
+                a, b = ai[r0], ai[r1]
+                aj[a:b] = np.sort(aj[a:b])
+                r0 = r1
     m = len(ai) - 1
     nbytes = pkg.algorithmic_bytes(m, m, len(aj))
     x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
@@ -118,6 +133,12 @@ def main():
     if args.variants == "skewgeom":
         for g, ex in itertools.product(range(9), (0, 1)):
             variants.append(("stream", dict(geometry=g, exact=ex)))
+    if args.variants == "gsort":  # gather-ordered row blocks (AIJHIP_OPT_GATHER_SORT) against the unsorted
+        for g, gs, nt in ((-1, -1, -1), (-1, 0, -1), (6, 1, 0), (1, 1, 0), (6, 1, 1), (6, 0, 0), (1, 0, 1)):
+            variants.append(("stream", dict(geometry=g, gather_sort=gs, nt_loads=nt)))
+    if args.variants == "geo16":  # the two automatic geometries
+        for g in (1, 6):
+            variants.append(("stream", dict(geometry=g)))
     if args.variants == "skewgeom2":  # the geometries the skewgeom sweep left out (9-11) against 1
         for g, nt in itertools.product((1, 9, 10, 11), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
@@ -147,6 +168,7 @@ def main():
         A.set_option("long_xcd", opts.get("long_xcd", 1))
         A.set_option("long_overlap", opts.get("long_overlap", 0))
         A.set_option("row_group", opts.get("row_group", 0))
+        A.set_option("gather_sort", opts.get("gather_sort", -1))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
