@@ -317,13 +317,17 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     }
     uint32_t sv[(SORTED || S16) ? ITERS : 1];  // the pairs' product slots (two 16-bit positions)
     if constexpr (S16) {  // unpack: .x = two 16-bit columns (block-relative), .y = two slots
+        // A pair straddling a block edge carries the neighbour's half,
+        // relative to the neighbour's first column: that half is gathered
+        // (never stored) at this block's first column instead, which exists.
         const int32_t base = sbase[b];
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
             const uint32_t c = (uint32_t)cv[it].x;
             sv[it] = (uint32_t)cv[it].y;
-            cv[it].x = base + (int32_t)(c & 0xffffu);
-            cv[it].y = base + (int32_t)(c >> 16);
+            cv[it].x = base + (k >= k0 && k < k1 ? (int32_t)(c & 0xffffu) : 0);
+            cv[it].y = base + (k + 1 < k1 ? (int32_t)(c >> 16) : 0);
         }
     }
     if constexpr (SORTED) {
