@@ -136,6 +136,9 @@ def main():
     if args.variants == "gsort":  # gather-ordered row blocks (AIJHIP_OPT_GATHER_SORT) against the unsorted
         for g, gs, nt in ((-1, -1, -1), (-1, 0, -1), (6, 1, 0), (1, 1, 0), (6, 1, 1), (6, 0, 0), (1, 0, 1)):
             variants.append(("stream", dict(geometry=g, gather_sort=gs, nt_loads=nt)))
+    if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
+        for lx, lo in ((1, 0), (1, 1), (0, 0), (0, 1)):
+            variants.append(("stream", dict(long_xcd=lx, long_overlap=lo)))
     if args.variants == "geo16":  # the two automatic geometries
         for g in (1, 6):
             variants.append(("stream", dict(geometry=g)))
