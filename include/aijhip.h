@@ -107,6 +107,10 @@ typedef struct aijhip_info {
                                 row blocks (AIJHIP_OPT_GATHER_SORT): 1 with
                                 32-bit columns, 2 with 16-bit block-relative
                                 columns (every block spans < 2^16); 0 off   */
+    int32_t column_codes;    /* MatMult reads 16-bit column codes instead of
+                                aj (AIJHIP_OPT_COLUMN_CODES): the row blocks
+                                whose columns the codes cover (10 bytes per
+                                entry instead of 12); 0 off                  */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -195,7 +199,7 @@ enum {
                                        0 = the LDS STREAM block; -1 (default)
                                        = automatic. Rows of shorter blocks
                                        stay bit-exact either way            */
-    AIJHIP_OPT_GATHER_SORT = 12     /* MatMult / MatMultAdd from a copy of the
+    AIJHIP_OPT_GATHER_SORT = 12,    /* MatMult / MatMultAdd from a copy of the
                                        row blocks with each block's entries
                                        sorted by column and their positions
                                        in the block: x is gathered in column
@@ -206,6 +210,19 @@ enum {
                                        rows, > 0.25 distinct x lines per
                                        entry); costs a second copy of the
                                        entries plus 2 bytes each            */
+    AIJHIP_OPT_COLUMN_CODES = 13    /* MatMult / MatMultAdd / the CG and V-cycle
+                                       epilogues read a 16-bit code per entry
+                                       instead of aj: (row in block << b) |
+                                       index into the block's dictionary of
+                                       column - row offsets (a stencil has a
+                                       handful per block), aa unchanged, the
+                                       same sums. 1 on, 0 off, -1 (default):
+                                       tried first at geometry 6 (gather
+                                       order off) and kept where the row
+                                       blocks' offsets fit (>= 90 % of the
+                                       entries), else the automatic layout
+                                       without them; costs 2 bytes per entry
+                                       of device memory                      */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

@@ -83,6 +83,8 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_sbase);
     hipFree(P.d_nblocks);
     hipFree(P.d_wblocks);
+    hipFree(P.d_code);
+    hipFree(P.d_cmeta);
     hipFree(P.d_sblocks);
     hipFree(P.d_gblocks);
     hipFree(P.d_tile_coord);
@@ -348,6 +350,71 @@ int plan_stream(aijhip_mat *A) {
             hipFree(d_base);
         }
     }
+    // column codes (Tuning::codes): a 16-bit code per entry in aj's place
+    // for the row blocks whose offset dictionaries fit (geometry 6, plain
+    // full-row launches: not with the x tiles, row groups, gather order,
+    // XCD remap, clamped loads or the persistent kernel); when some do not
+    // fit, they are launched from aj
+    if (P.tune.codes > 0 && P.tune.geom == 6 && !blocks.empty() && !A->compressed && P.d_xrange == nullptr &&
+        P.n_gblocks == 0 && P.d_sslot == nullptr && P.tune.persist == 0 && P.tune.nt <= 1 && !P.tune.clamped &&
+        !P.tune.xcd) {
+        int32_t *d_cnt = nullptr;
+        std::vector<int32_t> cnt(blocks.size());
+        if ((e = dmalloc(&d_cnt, blocks.size(), nullptr)) != hipSuccess ||
+            (e = aijhip::column_code_counts(*A, P.d_blocks, P.n_blocks, d_cnt)) != hipSuccess ||
+            (e = hipMemcpy(cnt.data(), d_cnt, sizeof(int32_t) * cnt.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
+            hipFree(d_cnt);
+            return hipfail(e, "plan: column code counts");
+        }
+        hipFree(d_cnt);
+        int64_t fit_nz = 0, nz_all = 0, dict = 0;
+        std::vector<char> fit(blocks.size());
+        for (size_t b = 0; b < blocks.size(); ++b) {
+            fit[b] = cnt[b] <= (1 << aijhip::code_index_bits(blocks[b].nrows));
+            nz_all += blocks[b].nk;
+            if (fit[b]) {
+                fit_nz += blocks[b].nk;
+                dict += cnt[b];
+            }
+        }
+        if (fit_nz > 0 && 10 * fit_nz >= 9 * nz_all) {
+            std::vector<BlockDesc> nb, wb;
+            std::vector<int32_t> meta;
+            for (size_t b = 0; b < blocks.size(); ++b) (fit[b] ? nb : wb).push_back(blocks[b]);
+            meta.resize(2 * nb.size());
+            int64_t pos = (int64_t)meta.size();
+            for (size_t b = 0, j = 0; b < blocks.size(); ++b)
+                if (fit[b]) {
+                    meta[2 * j] = (int32_t)pos;
+                    meta[2 * j + 1] = cnt[b];
+                    pos += cnt[b];
+                    ++j;
+                }
+            if (pos > INT32_MAX) return fail(AIJHIP_ERR_ARG, "plan: column code dictionaries too large");
+            const size_t ncode = (size_t)A->nz + 2;
+            if ((e = dmalloc(&P.d_cmeta, (size_t)pos, &P.bytes)) != hipSuccess ||
+                (e = hipMemcpy(P.d_cmeta, meta.data(), sizeof(int32_t) * meta.size(), hipMemcpyHostToDevice)) !=
+                    hipSuccess ||
+                (e = dmalloc(&P.d_code, ncode, &P.bytes)) != hipSuccess ||
+                (e = hipMemset(P.d_code, 0, sizeof(uint16_t) * ncode)) != hipSuccess)
+                return hipfail(e, "plan: column codes");
+            if (!wb.empty()) {
+                if ((e = dmalloc(&P.d_nblocks, nb.size(), &P.bytes)) != hipSuccess ||
+                    (e = dmalloc(&P.d_wblocks, wb.size(), &P.bytes)) != hipSuccess ||
+                    (e = hipMemcpy(P.d_nblocks, nb.data(), sizeof(BlockDesc) * nb.size(), hipMemcpyHostToDevice)) !=
+                        hipSuccess ||
+                    (e = hipMemcpy(P.d_wblocks, wb.data(), sizeof(BlockDesc) * wb.size(), hipMemcpyHostToDevice)) !=
+                        hipSuccess)
+                    return hipfail(e, "plan: column code block lists");
+                P.n_nblocks = (int32_t)nb.size();
+                P.n_wblocks = (int32_t)wb.size();
+            }
+            if ((e = aijhip::column_code_write(*A, wb.empty() ? P.d_blocks : P.d_nblocks, (int32_t)nb.size(),
+                                               P.d_cmeta, P.d_code)) != hipSuccess ||
+                (e = hipDeviceSynchronize()) != hipSuccess)
+                return hipfail(e, "plan: column codes");
+        }
+    }
     if (!longs.empty()) {
         if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
@@ -421,6 +488,7 @@ int plan_build(aijhip_mat *A) {
     P.kernel = kernel;
     P.tune = A->requested_tune;
     const bool auto_sort = P.tune.gsort < 0;
+    const bool auto_codes = P.tune.codes < 0;
     bool scattered = false;
     if (P.tune.geom < 0 || P.tune.nt < 0 || P.tune.gsort < 0) {
         // measured: 512 x 4094-entry blocks (geometry 6, 8 waves/SIMD) for
@@ -453,8 +521,30 @@ int plan_build(aijhip_mat *A) {
         if (P.tune.nt < 0) P.tune.nt = (scattered && !sorted) ? 1 : 0;
     }
     if (P.tune.group < 0) P.tune.group = 0;  // automatic choice: off until measured
+    if (P.tune.codes < 0) P.tune.codes = 0;  // automatic: tried below (STREAM)
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM: {
+            // Automatic column codes: tried first on every full-row operand
+            // the coded launch serves (geometry 6, gather order off, no other
+            // layout knob); kept when the blocks' offset dictionaries fit
+            // (>= 90 % of the entries), else the choice above without them.
+            // Measured in one process (profiles/r03/codes/): 300^3 Poisson
+            // 486.6 -> 433.8 us, FEM stand-in 267.4 (gather-ordered) ->
+            // 263.4 us; the skewed stand-in's blocks never fit.
+            const aijhip::Tuning &rq = A->requested_tune;
+            if (auto_codes && !A->compressed && rq.gsort <= 0 && (rq.geom < 0 || rq.geom == 6) && rq.xtile == 0 &&
+                rq.group <= 0 && rq.persist == 0 && !rq.xcd && !rq.clamped && rq.nt <= 1) {
+                const aijhip::Tuning keep = P.tune;
+                P.tune.codes = 1;
+                P.tune.gsort = 0;
+                P.tune.geom = 6;
+                if (rq.nt < 0) P.tune.nt = 0;
+                const int rc = plan_stream(A);
+                if (rc || P.d_code) return rc;
+                free_plan(A->plan);
+                P.kernel = kernel;
+                P.tune = keep;
+            }
             int rc = plan_stream(A);
             if (!rc && auto_sort && P.tune.gsort > 0 && !P.d_sidx) {
                 // automatic and the 16-bit form did not fit (blocks spanning
@@ -468,6 +558,7 @@ int plan_build(aijhip_mat *A) {
                 if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
                 if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
                 if (P.tune.group < 0) P.tune.group = 0;
+                if (P.tune.codes < 0) P.tune.codes = 0;
                 rc = plan_stream(A);
             }
             return rc;
@@ -696,7 +787,10 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
     A->d_aj = d_aj;
     A->d_aa = d_aa;
     A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
-    if (!like) A->requested_tune.gsort = 0;  // the set-up's own operators: one copy of the entries
+    if (!like) {  // the set-up's own operators: one copy of the entries, no codes (plan time)
+        A->requested_tune.gsort = 0;
+        A->requested_tune.codes = 0;
+    }
     aijhip::HostVec<int32_t> h_ai;
     int rc = AIJHIP_OK;
     hipError_t e = hipSuccess;
@@ -829,6 +923,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_GATHER_SORT:
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "gather_sort: -1 auto, 0 off, 1 on");
             t.gsort = value;
+            break;
+        case AIJHIP_OPT_COLUMN_CODES:
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "column_codes: -1 auto, 0 off, 1 on");
+            t.codes = value;
             break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
@@ -1020,6 +1118,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->exact = A->plan.tune.exact ? 1 : 0;
     info->x_tiled_blocks = A->plan.n_xtiled;
     info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
+    info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
     return AIJHIP_OK;
 }
 

@@ -107,7 +107,23 @@ struct Tuning {
                            // (plain MatMult / MatMultAdd, exact = 0): -1 auto, 0 off, 1 on
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
                            // (operands with scattered gathers, caller's handles), 0 off, 1 on
+    int codes = -1;        // 16-bit column codes instead of aj (Plan::d_code): -1 auto (where the
+                           // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
 };
+
+// Column codes (Tuning::codes): entry k of a row block starting at row0 is
+// coded as (r << b) | i, r = its row - row0, i = the index of aj[k] - row in
+// the block's sorted dictionary of distinct column - row offsets. b is a
+// function of the block's row count only (the rows need 16 - b bits), capped
+// so the dictionary fits kCodeDictMax LDS entries: 512-row blocks get 7 bits
+// (128 offsets; a 7-point stencil has 7), 50-row blocks of FEM rows 9
+// (512; a block of the FEM stand-in has ~135).
+constexpr int kCodeDictMax = 512;
+__host__ __device__ inline int code_index_bits(int nrows) {
+    int rb = 0;
+    while (rb < 16 && (1 << rb) < nrows) ++rb;
+    return 16 - rb < 9 ? 16 - rb : 9;
+}
 
 struct HostPipe;  // host-vector MatMult pipeline state (host_pipe.cpp)
 
@@ -179,6 +195,12 @@ struct Plan {
     // d_wblocks, launched from the original arrays
     BlockDesc *d_nblocks = nullptr, *d_wblocks = nullptr;
     int32_t n_nblocks = 0, n_wblocks = 0;
+    // Tuning::codes: one 16-bit code per entry (nz + 2, pairs read as one
+    // 4-B word) and d_cmeta = per coded block {dictionary start, size} then
+    // the dictionaries; the coded blocks are d_blocks, or d_nblocks with the
+    // others in d_wblocks (launched from aj) when some do not fit
+    uint16_t *d_code = nullptr;
+    int32_t *d_cmeta = nullptr;
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;
     int32_t n_tiles = 0;
@@ -277,6 +299,12 @@ hipError_t gather_order_spans(const Plan &P, int32_t *d_base, int32_t *d_span);
 // d_blk[0, nblk) (d_base: their first columns, in that order).
 hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk, const int32_t *d_base,
                              uint16_t *d_sidx);
+// Column codes: pass 0 counts each block's distinct column - row offsets
+// into d_cnt[0, nblk); pass 1 (d_cmeta laid out by the caller) writes the
+// dictionaries and the codes of blocks d_blk[0, nblk).
+hipError_t column_code_counts(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt);
+hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cmeta,
+                             uint16_t *d_code);
 // Distinct 128-B x lines per entry over a row sample (at most 65536 rows):
 // ~0.7 for the 7-point stencil, ~0.17 for a 3-dof hexahedral FEM operator.
 hipError_t gather_lines_per_entry(const aijhip_mat &A, double *out);

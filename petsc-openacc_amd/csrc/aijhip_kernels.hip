@@ -261,17 +261,39 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     // one 8-B load per pair as in CSR, columns relative to the block's
     // first (sbase[b]); 12 bytes per entry like the original arrays
     constexpr bool S16 = (NTMODE & 16) != 0;
+    // bit 5: column codes (Plan::d_code, full-row lists only): aj holds one
+    // 16-bit code per entry, (row - row0) << b | index into the block's
+    // dictionary of column - row offsets; sbase holds per block {dictionary
+    // start, size} and then the dictionaries. 10 bytes per entry instead of
+    // 12; the products, their slots and the sums are the plain kernel's
+    constexpr bool CODES = (NTMODE & 32) != 0;
+    static_assert(!(CODES && (S16 || SORTED || SHUF || CROW || NT >= 2 || Op::kTile)),
+                  "column codes: plain full-row form only");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
+    constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     __shared__ double prod[CAP];
+    __shared__ int32_t cdict[CODES ? kCodeDictMax : 1];
     const int bid = (int)blockIdx.x;
     const int b = XCD ? xcd_chunk_remap(bid, nblk, xchunk) : bid;
     const BlockDesc d = blk[b];
+    int32_t nd = 0, dbase = 0;
+    if constexpr (CODES) {
+        dbase = sbase[2 * b];
+        nd = sbase[2 * b + 1];
+    }
     // CG launched past convergence: no work. The test also reads the
     // descriptor (d.nk is never negative), so both scalar loads are issued
     // before one wait instead of the descriptor load waiting for the branch.
     if ((stop ? *stop : 0) != 0 || d.nk < 0) return;
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
+    // the block's offset dictionary, loaded ahead of the stream (to LDS below)
+    int32_t dval[DPT];
+    if constexpr (CODES) {
+#pragma unroll
+        for (int i = 0; i < DPT; ++i)
+            if (t + i * T < nd) dval[i] = sbase[dbase + t + i * T];
+    }
 
     // Row extents and MatMultAdd seeds first: they overlap the stream below.
     int32_t rs[RPT], re[RPT], orow[RPT];
@@ -305,13 +327,43 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
                 av[it] = ld_stream<NT == 2>(reinterpret_cast<const f64x2 *>(aa + (CLAMPED ? min(k, klast) : k)));
         }
     } else {
+        uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
             if (CLAMPED || k < k1) {
                 const int64_t kc = CLAMPED ? min(k, klast) : k;
                 av[it] = ld_stream<NT == 1>(reinterpret_cast<const f64x2 *>(aa + kc));
-                cv[it] = ld_stream<NT == 1>(reinterpret_cast<const i32x2 *>(aj + kc));
+                if constexpr (CODES)
+                    cw[it] = ld_stream<NT == 1>(reinterpret_cast<const uint32_t *>(aj) + (kc >> 1));
+                else
+                    cv[it] = ld_stream<NT == 1>(reinterpret_cast<const i32x2 *>(aj + kc));
+            }
+        }
+        if constexpr (CODES) {
+#pragma unroll
+            for (int i = 0; i < DPT; ++i)
+                if (t + i * T < nd) cdict[t + i * T] = dval[i];
+            lds_barrier();
+            // decoded and gathered pair by pair (one pair's columns live at a
+            // time: decoding all first took 70 VGPRs, 7 waves/SIMD)
+            const int ib = code_index_bits(d.nrows);
+            const uint32_t im = (1u << ib) - 1u;
+            const int e0 = (int)(k0 - kb), ne = (int)(k1 - kb);  // the block's entries relative to kb
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) {
+                const int e = 2 * (t + it * T);
+                if (e < ne) {
+                    const uint32_t lo = cw[it] & 0xffffu, hi = cw[it] >> 16;
+                    int32_t c0 = d.row0 + (int32_t)(lo >> ib) + cdict[lo & im];
+                    int32_t c1 = d.row0 + (int32_t)(hi >> ib) + cdict[hi & im];
+                    // a pair straddling a block edge carries the neighbour's
+                    // code: that half gathers this half's column (never stored)
+                    if (e < e0) c0 = c1;
+                    if (e + 1 >= ne) c1 = c0;
+                    xv[it].x = op.gx(c0);
+                    xv[it].y = op.gx(c1);
+                }
             }
         }
     }
@@ -350,7 +402,9 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             __syncthreads();
         }
     }
-    if constexpr (SHUF && !Op::kTile) {
+    if constexpr (CODES) {
+        // gathered with the decode above
+    } else if constexpr (SHUF && !Op::kTile) {
         const int lane = t & 63;
         const int half = lane >> 1;
 #pragma unroll
@@ -1008,6 +1062,81 @@ __global__ __launch_bounds__(256) void k_pack_gather_order(const BlockDesc *__re
     }
 }
 
+// Column codes (Tuning::codes), one workgroup per row block: the offsets
+// aj[k] - row of its entries (a lane per row) are sorted (bitonic over the
+// next power of two) and made unique by wave 0 (ballot compaction). Pass 0
+// stores the number of distinct offsets; pass 1 stores the dictionary at
+// cmeta[cmeta[2b]] and each entry's code (row - row0) << b | rank, the rank
+// found by binary search. A block whose count exceeds 2^b is never passed
+// to pass 1 (the host splits it off).
+template <int N>
+__global__ __launch_bounds__(256) void k_block_codes(const BlockDesc *__restrict__ blk,
+                                                     const int32_t *__restrict__ rai,
+                                                     const int32_t *__restrict__ aj, int32_t *cnt, int32_t *cmeta,
+                                                     uint16_t *code) {
+    __shared__ int32_t key[N];
+    __shared__ int32_t uq[kCodeDictMax];
+    __shared__ int32_t s_nd;
+    const BlockDesc d = blk[blockIdx.x];
+    const int t = threadIdx.x;
+    int n2 = 2;
+    while (n2 < d.nk) n2 <<= 1;
+    for (int r = t; r < d.nrows; r += 256) {
+        const int32_t row = d.row0 + r;
+        for (int32_t k = rai[row]; k < rai[row + 1]; ++k) key[k - d.k0] = aj[k] - row;
+    }
+    for (int i = d.nk + t; i < n2; i += 256) key[i] = INT32_MAX;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < n2; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int32_t a = key[i], c = key[ixj];
+                    if ((a > c) == ((i & k) == 0)) {
+                        key[i] = c;
+                        key[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    if (t < 64) {
+        int n = 0;
+        for (int i0 = 0; i0 < d.nk; i0 += 64) {
+            const int i = i0 + t;
+            const bool f = i < d.nk && (i == 0 || key[i] != key[i - 1]);
+            const unsigned long long m = __ballot(f);
+            const int pos = n + __popcll(m & ((1ull << t) - 1ull));
+            if (f && pos < kCodeDictMax) uq[pos] = key[i];
+            n += __popcll(m);
+        }
+        if (t == 0) s_nd = n;
+    }
+    __syncthreads();
+    const int nd = s_nd;
+    if (cmeta == nullptr) {
+        if (t == 0) cnt[blockIdx.x] = nd;
+        return;
+    }
+    const int32_t base = cmeta[2 * blockIdx.x];
+    for (int i = t; i < nd; i += 256) cmeta[base + i] = uq[i];
+    const int ib = code_index_bits(d.nrows);
+    for (int r = t; r < d.nrows; r += 256) {
+        const int32_t row = d.row0 + r;
+        for (int32_t k = rai[row]; k < rai[row + 1]; ++k) {
+            const int32_t off = aj[k] - row;
+            int lo = 0, hi = nd - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (uq[mid] < off) lo = mid + 1;
+                else hi = mid;
+            }
+            code[k] = (uint16_t)(((uint32_t)r << ib) | (uint32_t)lo);
+        }
+    }
+}
+
 // The sorted values again after new values (aijhip_mat_update_values)
 __global__ __launch_bounds__(256) void k_gather_order_values(const BlockDesc *__restrict__ blk,
                                                              const uint16_t *__restrict__ sslot,
@@ -1051,6 +1180,31 @@ hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk
     hipLaunchKernelGGL(k_pack_gather_order, dim3(nblk), dim3(256), 0, nullptr, d_blk, P.d_saj, P.d_sslot, d_base,
                        d_sidx);
     return hipGetLastError();
+}
+
+template <bool WRITE>
+static hipError_t launch_block_codes(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt,
+                                     int32_t *d_cmeta, uint16_t *d_code, int cap) {
+    if (nblk <= 0) return hipSuccess;
+    int32_t *meta = WRITE ? d_cmeta : nullptr;
+#define AIJHIP_BC(NN) \
+    hipLaunchKernelGGL(k_block_codes<NN>, dim3(nblk), dim3(256), 0, nullptr, d_blk, A.d_ai, A.d_aj, d_cnt, meta, d_code)
+    if (cap <= 1024) AIJHIP_BC(1024);
+    else if (cap <= 2048) AIJHIP_BC(2048);
+    else if (cap <= 4096) AIJHIP_BC(4096);
+    else AIJHIP_BC(8192);
+#undef AIJHIP_BC
+    return hipGetLastError();
+}
+
+hipError_t column_code_counts(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt) {
+    return launch_block_codes<false>(A, d_blk, nblk, d_cnt, nullptr, nullptr,
+                                     kStreamGeoms[A.plan.tune.geom].nnz_cap);
+}
+
+hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cmeta,
+                             uint16_t *d_code) {
+    return launch_block_codes<true>(A, d_blk, nblk, nullptr, d_cmeta, d_code, kStreamGeoms[A.plan.tune.geom].nnz_cap);
 }
 
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out) {
@@ -1154,6 +1308,33 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                        L.rai, L.ridx, A.d_aj, A.d_aa,                                              \
                        OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, nullptr); \
     return
+    // Column codes (Plan::d_code; geometry 6, full-row lists): MatMult,
+    // MatMultAdd and the CG's fused dot; with a coded / uncoded split the dot's
+    // partials would come from two launches, so that case takes aj
+    if constexpr (T == 512 && CAP == 4094 && RPT == 1) {
+        if (P.d_code && !L.ridx && (P.n_wblocks == 0 || !dpart)) {
+            const BlockDesc *cb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
+            const int32_t nc = P.n_wblocks ? P.n_nblocks : P.n_blocks;
+#define AIJHIP_SC(ADD, NTM)                                                                                       \
+    if (nc > 0)                                                                                                   \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, NTM, false, OpMult<ADD>>), dim3(nc), dim3(T), 0, \
+                           s, cb, nc, 0, (int)P.tune.exact, L.rai, nullptr,                                        \
+                           reinterpret_cast<const int32_t *>(P.d_code), A.d_aa,                                   \
+                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, P.d_cmeta);     \
+    if (P.n_wblocks > 0)                                                                                          \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, 0, false, OpMult<ADD>>), dim3(P.n_wblocks),  \
+                           dim3(T), 0, s, P.d_wblocks, P.n_wblocks, 0, (int)P.tune.exact, L.rai, nullptr, A.d_aj, \
+                           A.d_aa, OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);        \
+    return
+            if (add) {
+                if (P.tune.nt == 1) { AIJHIP_SC(true, 33); }
+                AIJHIP_SC(true, 32);
+            }
+            if (P.tune.nt == 1) { AIJHIP_SC(false, 33); }
+            AIJHIP_SC(false, 32);
+#undef AIJHIP_SC
+        }
+    }
     // Gather-ordered blocks (Plan::d_sslot): the sorted copy, every variant
     // (MatMult / MatMultAdd, full or compressed rows, dot epilogue)
     // (with the narrow / wide split, the dot epilogue's partials would come
@@ -1276,6 +1457,13 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
+    if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, false, 32, false, Op>), dim3(P.n_blocks),
+                           dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex, A.d_ai, nullptr,
+                           reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, op, dpart, stop, nullptr, nullptr,
+                           P.d_cmeta);
+        return hipGetLastError();
+    }
     static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
 #define AIJHIP_OG(G)                                                                                      \
     case G:                                                                                               \

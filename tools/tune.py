@@ -136,6 +136,9 @@ def main():
     if args.variants == "gsort":  # gather-ordered row blocks (AIJHIP_OPT_GATHER_SORT) against the unsorted
         for g, gs, nt in ((-1, -1, -1), (-1, 0, -1), (6, 1, 0), (1, 1, 0), (6, 1, 1), (6, 0, 0), (1, 0, 1)):
             variants.append(("stream", dict(geometry=g, gather_sort=gs, nt_loads=nt)))
+    if args.variants == "codes":  # 16-bit column codes (AIJHIP_OPT_COLUMN_CODES) against aj, gather order off/on
+        for gs, cc, nt in ((0, 0, 0), (0, 1, 0), (0, 1, 1), (-1, 0, -1), (0, 0, 1)):
+            variants.append(("stream", dict(geometry=6, gather_sort=gs, column_codes=cc, nt_loads=nt)))
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
         for lx, lo in ((1, 0), (1, 1), (0, 0), (0, 1)):
             variants.append(("stream", dict(long_xcd=lx, long_overlap=lo)))
@@ -172,6 +175,7 @@ def main():
         A.set_option("long_overlap", opts.get("long_overlap", 0))
         A.set_option("row_group", opts.get("row_group", 0))
         A.set_option("gather_sort", opts.get("gather_sort", -1))
+        A.set_option("column_codes", opts.get("column_codes", -1))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
