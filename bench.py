@@ -754,6 +754,10 @@ def main():
         if aj_leg is not None:
             out["roofline"]["aj_layout"] = aj_leg
         if isinstance(ceiling, dict) and "error" not in ceiling:  # same-run flat reads of the same bytes
+            if info.get("column_codes"):  # the coded kernel against the same reads, on the bytes it moves
+                out["roofline"]["moved_frac_of_flat_read"] = round(out["roofline"]["moved_GBs"] / ceiling[0][0], 4)
+                out["roofline"]["moved_frac_of_stream_shape_read"] = round(
+                    out["roofline"]["moved_GBs"] / ceiling[1][0], 4)
             out["roofline"]["ceiling_flat_read"] = {
                 "GBs": ceiling[0][0], "us": ceiling[0][1], "frac_of_ceiling": round(achieved / ceiling[0][0], 4),
                 "probe": "aijhip_read_probe mode 0: the SpMV's byte count read once, non-temporal 16-B loads, "

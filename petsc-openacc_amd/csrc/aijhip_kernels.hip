@@ -801,7 +801,41 @@ __global__ __launch_bounds__(kMergeThreads) void k_spmv_merge(
         const int r = i0 + q;
         s_rb[q] = r <= nr ? rai[r] : (int32_t)K;
     }
-    for (int64_t k = j0 + t; k < j1; k += kMergeThreads) s_prod[k - j0] = aa[k] * x[aj[k]];
+    // The tile's entries as in STREAM: 16-B aa / 8-B aj pairs from an even
+    // start (the arrays carry a 2-entry tail pad), every load of a lane in
+    // flight before its gathers (one entry per lane and loop trip, as this
+    // loop was first written, left each lane waiting on one load at a time)
+    {
+        constexpr int MI = (kMergeTile + 1 + 2 * kMergeThreads - 1) / (2 * kMergeThreads);
+        const int64_t kb = j0 & ~int64_t(1);
+        f64x2 av[MI];
+        i32x2 cv[MI];
+        f64x2 xv[MI];
+#pragma unroll
+        for (int it = 0; it < MI; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * kMergeThreads);
+            if (k < j1) {
+                av[it] = *reinterpret_cast<const f64x2 *>(aa + k);
+                cv[it] = *reinterpret_cast<const i32x2 *>(aj + k);
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < MI; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * kMergeThreads);
+            if (k < j1) {
+                xv[it].x = x[k >= j0 ? cv[it].x : cv[it].y];  // a pair's half before the tile: never stored
+                xv[it].y = x[k + 1 < j1 ? cv[it].y : cv[it].x];  // ... or after it
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < MI; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * kMergeThreads);
+            if (k < j1) {
+                if (k >= j0) s_prod[k - j0] = av[it].x * xv[it].x;
+                if (k + 1 < j1) s_prod[k + 1 - j0] = av[it].y * xv[it].y;
+            }
+        }
+    }
     __syncthreads();
 
     // Thread-local merge-path search inside the tile.
