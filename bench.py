@@ -627,7 +627,9 @@ def main():
         rhs_h, exact_h = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
         b = torch.from_numpy(rhs_h).to(dev)
         xs = torch.zeros_like(b)
-        kg = C.KSPCGMPINative(op.native, rtol=1e-14, atol=1e-12, max_it=10000, pc="gamg")
+        # (with --halo allgather the hierarchy is built over the operator's
+        # p2p twin, which shares A_d: the set-up's level halos are p2p plans)
+        kg = C.KSPCGMPINative(op.p2p_native(), rtol=1e-14, atol=1e-12, max_it=10000, pc="gamg")
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -655,7 +657,8 @@ def main():
                "levels": [{"rows": int(r), "nnz": int(z)} for r, z in zip(rows_l, nnz_l)],
                "pc": ("PCGAMG across ranks (aggregates per rank, P and Galerkin products over the MPIAIJ "
                       "operator, csrc/gamg_mpi.hip)" if world > 1 else "PCGAMG (single-GPU set-up)"),
-               "options": "rtol 1e-14 atol 1e-12", "workload": f"{nx}x{ny}x{nz_global} Poisson"}
+               "options": "rtol 1e-14 atol 1e-12", "workload": f"{nx}x{ny}x{nz_global} Poisson",
+               "halo": "p2p" if args.halo == "p2p" else "p2p twin of the all-gather operator (shares A_d)"}
         kg.destroy()
         return out
 

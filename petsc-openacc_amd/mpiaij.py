@@ -94,7 +94,9 @@ class MPIAIJ:
         self.nz_d, self.nz_o, self.n_ghost = len(daj), len(oaj), len(garray)
         self.plan = HaloPlan(garray, self.row_starts, self.rank, self.world, group)
         self.A_d = make_local(dai, daj, daa, self.mloc)
+        self._comm, self._make_local, self._twin = comm, make_local, None
         if halo == "allgather":
+            self._o_p2p = (oai, oaj, oaa)  # ghost-numbered A_o, for p2p_native()
             oaj = self._allgather_layout(oaj, garray)
         self.A_o = make_local(oai, oaj, oaa, max(self.n_ghost_buf, 1)) if len(oaj) else None
         self.ghost = torch.zeros(max(self.n_ghost_buf, 1), dtype=torch.float64, device=device)
@@ -116,6 +118,25 @@ class MPIAIJ:
                 recv = [(p, a, b) for p, (a, b, _) in sorted(self.plan.recv.items(), key=lambda kv: kv[1][0])]
             self.native = C.NativeMPIAIJ(comm, self.A_d, self.A_o, halo, send, recv,
                                          getattr(self, "gather_len", 0))
+
+    def p2p_native(self):
+        """The native operator with the point-to-point halo: `native` itself,
+        or (all-gather halo) a twin sharing A_d, with A_o in ghost numbering
+        and the p2p plan. The distributed GAMG set-up (csrc/gamg_mpi.hip)
+        builds every level's exchange from p2p plans, so PCGAMG across ranks
+        runs on this; the product is the same either way."""
+        if self.native is None:
+            raise RuntimeError("p2p_native needs the library's communicator (comm=...)")
+        if self.halo == "p2p":
+            return self.native
+        if self._twin is None:
+            C = importlib.import_module("petsc-openacc_amd.comm")
+            oai, oaj, oaa = self._o_p2p
+            A_o = self._make_local(oai, oaj, oaa, max(self.n_ghost, 1)) if len(oaj) else None
+            send = [(q, idx) for q, idx in sorted(self.plan.send.items())]
+            recv = [(p, a, b) for p, (a, b, _) in sorted(self.plan.recv.items(), key=lambda kv: kv[1][0])]
+            self._twin = (A_o, C.NativeMPIAIJ(self._comm, self.A_d, A_o, "p2p", send, recv, 0))
+        return self._twin[1]
 
     # -------------------------------------------------------------- layouts
     @property

@@ -34,7 +34,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, dims, pcs, env, q):
+def _worker(rank, world, port, dims, pcs, env, q, halo="p2p"):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -56,13 +56,13 @@ def _worker(rank, world, port, dims, pcs, env, q):
             return pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols)
 
         comm = C.Comm.host(device=0, timeout_s=120)
-        op = mp_mod.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, comm=comm)
+        op = mp_mod.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=halo, comm=comm)
         rhs, _ = pkg.poisson_vectors(nx, ny, nz, z0, z1)
         b = torch.from_numpy(rhs).to(dev)
         out = {}
         for pc in pcs:
             x = torch.full_like(b, float("nan"))
-            with C.KSPCGMPINative(op.native, max_it=1000, pc=pc, **TOL) as k:
+            with C.KSPCGMPINative(op.p2p_native() if pc == "gamg" else op.native, max_it=1000, pc=pc, **TOL) as k:
                 k.solve(b, x)
                 torch.cuda.synchronize()
                 rows, nnz = k.pc_levels()
@@ -78,12 +78,12 @@ def _worker(rank, world, port, dims, pcs, env, q):
         dist.destroy_process_group()
 
 
-def _run(world, dims, pcs, env=None):
+def _run(world, dims, pcs, env=None, halo="p2p"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, dims, pcs, env or {}, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, dims, pcs, env or {}, q, halo)) for r in range(world)]
     for p in procs:
         p.start()
     got = {}
@@ -189,3 +189,17 @@ def test_gpu_gamg_distributed_setup_at_one_rank_matches_pcgamg():
     assert dist_run["its"] == single["its"]
     np.testing.assert_allclose(dist_run["hist"], single["hist"], rtol=1e-6, atol=1e-15 * single["hist"][0])
     np.testing.assert_allclose(dist_run["x"], single["x"], rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_gamg_on_allgather_operator():
+    """An operator with the north star's all-gather halo: CG + Jacobi runs on
+    it as built, PCGAMG across ranks on its p2p twin (MPIAIJ.p2p_native, which
+    shares A_d); both equal the p2p operator's solves bit for bit."""
+    dims = (12, 12, 16)
+    ag = _run(2, dims, ("gamg", "jacobi"), halo="allgather")
+    pp = _run(2, dims, ("gamg", "jacobi"))
+    for r in range(2):
+        for pc in ("gamg", "jacobi"):
+            assert ag[r][pc]["its"] == pp[r][pc]["its"], (r, pc)
+            assert np.array_equal(ag[r][pc]["x"].view(np.uint64), pp[r][pc]["x"].view(np.uint64)), (r, pc)
