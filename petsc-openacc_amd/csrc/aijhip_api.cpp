@@ -351,11 +351,13 @@ int plan_stream(aijhip_mat *A) {
         }
     }
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
-    // for the row blocks whose offset dictionaries fit (geometry 6, plain
+    // for the row blocks whose offset dictionaries fit (geometry 6 — 7 and 9
+    // for MatMult / MatMultAdd only, A/B —, plain
     // full-row launches: not with the x tiles, row groups, gather order,
     // XCD remap, clamped loads or the persistent kernel); when some do not
     // fit, they are launched from aj
-    if (P.tune.codes > 0 && P.tune.geom == 6 && !blocks.empty() && !A->compressed && P.d_xrange == nullptr &&
+    if (P.tune.codes > 0 && (P.tune.geom == 6 || P.tune.geom == 7 || P.tune.geom == 9) && !blocks.empty() &&
+        !A->compressed && P.d_xrange == nullptr &&
         P.n_gblocks == 0 && P.d_sslot == nullptr && P.tune.persist == 0 && P.tune.nt <= 1 && !P.tune.clamped &&
         !P.tune.xcd) {
         int32_t *d_cnt = nullptr;

@@ -1345,7 +1345,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // Column codes (Plan::d_code; geometry 6, full-row lists): MatMult,
     // MatMultAdd and the CG's fused dot; with a coded / uncoded split the dot's
     // partials would come from two launches, so that case takes aj
-    if constexpr (T == 512 && CAP == 4094 && RPT == 1) {
+    if constexpr (RPT == 1 && ((T == 512 && (CAP == 4094 || CAP == 6142)) || (T == 1024 && CAP == 8190))) {
         if (P.d_code && !L.ridx && (P.n_wblocks == 0 || !dpart)) {
             const BlockDesc *cb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
             const int32_t nc = P.n_wblocks ? P.n_nblocks : P.n_blocks;

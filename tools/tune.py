@@ -139,6 +139,9 @@ def main():
     if args.variants == "codes":  # 16-bit column codes (AIJHIP_OPT_COLUMN_CODES) against aj, gather order off/on
         for gs, cc, nt in ((0, 0, 0), (0, 1, 0), (0, 1, 1), (-1, 0, -1), (0, 0, 1)):
             variants.append(("stream", dict(geometry=6, gather_sort=gs, column_codes=cc, nt_loads=nt)))
+    if args.variants == "codesgeom":  # column codes at the geometries the coded launch is built for
+        for g, cc, nt in ((6, 1, 0), (6, 1, 1), (7, 1, 0), (7, 1, 1), (9, 1, 0), (9, 1, 1), (6, 0, 0)):
+            variants.append(("stream", dict(geometry=g, gather_sort=0, column_codes=cc, nt_loads=nt)))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
