@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--persist", type=int, default=None, help="persistent pipelined STREAM, workgroups/CU")
     p.add_argument("--codes", type=int, default=None,
                    help="STREAM column codes -1 (library default: automatic) / 0 (aj) / 1")
+    p.add_argument("--patterns", type=int, default=None,
+                   help="STREAM row patterns -1 (library default: automatic) / 0 / 1")
     p.add_argument("--halo", default="p2p", choices=["p2p", "allgather"])
     p.add_argument("--x", default="uniform", choices=["uniform", "exact"], help="x = splitmix(42) or generateExt")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
@@ -327,7 +329,8 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                          "GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
                          "frac": round(nbytes / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                          "geometry": info.get("stream_geometry"), "long_rows": info.get("n_long_rows"),
-                         "column_codes": info.get("column_codes"), "gather_sorted": info.get("gather_sorted")}
+                         "column_codes": info.get("column_codes"), "gather_sorted": info.get("gather_sorted"),
+                         "row_patterns": info.get("row_patterns")}
         del x, y
         flat = read_ceiling(nbytes, dev)
         rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],
@@ -416,7 +419,8 @@ def main():
 
     def configure(mat):
         for opt, val in (("geometry", args.geometry), ("xcd_remap", args.xcd), ("nt_loads", args.nt),
-                         ("persistent", args.persist), ("column_codes", args.codes)):
+                         ("persistent", args.persist), ("column_codes", args.codes),
+                         ("row_patterns", args.patterns)):
             if val is not None:
                 mat.set_option(opt, val)
         return mat
@@ -541,12 +545,13 @@ def main():
     torch.cuda.synchronize()
     stable = bool(torch.equal(y_chk, yd))
 
-    # With column codes in the plan (the automatic layout), the same SpMV
-    # from PETSc's aj array in the same run: the uncoded kernel's time and
-    # fraction, and whether its y is the same bits (it must be).
+    # With row patterns or column codes in the plan (the automatic layouts),
+    # the same SpMV from PETSc's aj array in the same run: the plain kernel's
+    # time and fraction, and whether its y is the same bits (it must be).
     aj_leg = None
-    if not distributed and info.get("column_codes"):
+    if not distributed and (info.get("column_codes") or info.get("row_patterns")):
         def aj_layout():
+            A.set_option("row_patterns", 0)
             A.set_option("column_codes", 0)
             try:
                 y_aj = torch.empty_like(yd)
@@ -557,11 +562,13 @@ def main():
                 del y_aj
             finally:
                 A.set_option("column_codes", -1 if args.codes is None else args.codes)
+                A.set_option("row_patterns", -1 if args.patterns is None else args.patterns)
             return {"us_mean": round(mean, 2), "us_median": round(med, 2), "us_min": round(mn, 2),
                     "GBs": round(bytes_local / (mean * 1e-6) / 1e9, 1),
                     "frac": round(bytes_local / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                     "bitwise_equal_coded": same,
-                    "note": "the same MatMult reading PETSc's aj (12 bytes per entry), column codes off"}
+                    "note": "the same MatMult reading PETSc's aj (12 bytes per entry): row patterns and "
+                            "column codes off"}
         aj_leg = aj_layout()
 
     # The measurements beside the headline one are guarded: an exception
@@ -700,7 +707,7 @@ def main():
         mean_launch_s = float(np.mean(launch_ms)) / 1e3
         achieved = bytes_local / mean_launch_s / 1e9
         block = {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "xcd_remap", "nt_loads",
-                                      "persistent", "column_codes")}
+                                      "persistent", "column_codes", "row_patterns")}
         traffic, traffic_src = (None, None) if distributed else pmc_traffic(n_global, nnz_global, block)
         out = {
             "metric": "CSR SpMV effective HBM GB/s (300^3 7-pt Poisson, fp64 MatMult_SeqAIJ)",
@@ -744,20 +751,27 @@ def main():
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
-        if info.get("column_codes"):
-            # the coded layout reads 2 B of code per entry instead of aj's 4 B
-            # (plus the blocks' offset dictionaries, < 0.1 %): `achieved`
-            # keeps SURVEY §8d's CSR bytes, as the metric defines it; this is
-            # the rate on the bytes the kernel moves
-            moved = bytes_local - 2 * nnz_loc
-            out["roofline"]["layout"] = "column codes (16-bit per entry, aa verbatim)"
+        if info.get("column_codes") or info.get("row_patterns"):
+            # `achieved` keeps SURVEY §8d's CSR bytes, as the metric defines
+            # effective bandwidth; these are the bytes the kernel moves and
+            # its rate on them. Column codes read 2 B per entry instead of
+            # aj's 4 B (plus the blocks' offset dictionaries, < 0.1 %); row
+            # patterns read no column per entry, 1 B of pattern id per row
+            # (plus a table of <= 1024 words, L2-resident)
+            if info.get("row_patterns"):
+                moved = bytes_local - 4 * nnz_loc + m_loc
+                out["roofline"]["layout"] = (f"row patterns ({info['row_patterns']} column - row offset lists, "
+                                             "a 1-byte id per row, aa verbatim; cf. PETSc's inode rows)")
+            else:
+                moved = bytes_local - 2 * nnz_loc
+                out["roofline"]["layout"] = "column codes (16-bit per entry, aa verbatim)"
             out["roofline"]["bytes_moved_per_launch"] = moved
             out["roofline"]["moved_GBs"] = round(moved / mean_launch_s / 1e9, 1)
             out["roofline"]["frac_of_moved_bytes"] = round(moved / mean_launch_s / 1e9 / HBM_PEAK_GBS, 4)
         if aj_leg is not None:
             out["roofline"]["aj_layout"] = aj_leg
         if isinstance(ceiling, dict) and "error" not in ceiling:  # same-run flat reads of the same bytes
-            if info.get("column_codes"):  # the coded kernel against the same reads, on the bytes it moves
+            if "moved_GBs" in out["roofline"]:  # the kernel against the same reads, on the bytes it moves
                 out["roofline"]["moved_frac_of_flat_read"] = round(out["roofline"]["moved_GBs"] / ceiling[0][0], 4)
                 out["roofline"]["moved_frac_of_stream_shape_read"] = round(
                     out["roofline"]["moved_GBs"] / ceiling[1][0], 4)

@@ -111,6 +111,9 @@ typedef struct aijhip_info {
                                 aj (AIJHIP_OPT_COLUMN_CODES): the row blocks
                                 whose columns the codes cover (10 bytes per
                                 entry instead of 12); 0 off                  */
+    int32_t row_patterns;    /* MatMult reads a pattern id per row instead of
+                                aj (AIJHIP_OPT_ROW_PATTERNS): the number of
+                                distinct column - row offset lists; 0 off    */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -210,7 +213,7 @@ enum {
                                        rows, > 0.25 distinct x lines per
                                        entry); costs a second copy of the
                                        entries plus 2 bytes each            */
-    AIJHIP_OPT_COLUMN_CODES = 13    /* MatMult / MatMultAdd / the CG and V-cycle
+    AIJHIP_OPT_COLUMN_CODES = 13,   /* MatMult / MatMultAdd / the CG and V-cycle
                                        epilogues read a 16-bit code per entry
                                        instead of aj: (row in block << b) |
                                        index into the block's dictionary of
@@ -223,6 +226,15 @@ enum {
                                        entries), else the automatic layout
                                        without them; costs 2 bytes per entry
                                        of device memory                      */
+    AIJHIP_OPT_ROW_PATTERNS = 14    /* short-row operands whose rows follow at
+                                       most 256 distinct column - row offset
+                                       lists (stencils): no per-entry column
+                                       at all — a pattern id per row (1 byte),
+                                       the lists staged in LDS, x gathered by
+                                       one lane per row; aa unchanged, the same
+                                       sums. 1 on, 0 off, -1 (default): tried
+                                       first where the mean row is at most 16
+                                       entries; costs 1 byte per row          */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

@@ -34,7 +34,7 @@ KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
 OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3, "persistent": 4, "clamped": 5, "exact": 6, "x_tile": 7,
            "long_xcd": 8, "long_overlap": 9, "host_pipeline": 10, "row_group": 11, "gather_sort": 12,
-           "column_codes": 13}
+           "column_codes": 13, "row_patterns": 14}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 
@@ -73,6 +73,7 @@ class AIJInfo(ctypes.Structure):
         ("stream_threads", ctypes.c_int32), ("stream_nnz_cap", ctypes.c_int32), ("stream_rows", ctypes.c_int32),
         ("persistent", ctypes.c_int32), ("exact", ctypes.c_int32), ("x_tiled_blocks", ctypes.c_int32),
         ("gather_sorted", ctypes.c_int32), ("column_codes", ctypes.c_int32),
+        ("row_patterns", ctypes.c_int32),
     ]
 
 

@@ -85,6 +85,8 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_wblocks);
     hipFree(P.d_code);
     hipFree(P.d_cmeta);
+    hipFree(P.d_pid);
+    hipFree(P.d_ptab);
     hipFree(P.d_sblocks);
     hipFree(P.d_gblocks);
     hipFree(P.d_tile_coord);
@@ -350,6 +352,16 @@ int plan_stream(aijhip_mat *A) {
             hipFree(d_base);
         }
     }
+    // row patterns (Tuning::patterns): a pattern id per row in aj's place
+    // for short-row operands whose rows follow few offset lists (stencils);
+    // geometry 6, plain full-row launches, no long rows
+    const int32_t nrl = rai.empty() ? 0 : (int32_t)rai.size() - 1;
+    if (P.tune.patterns > 0 && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed &&
+        A->nz <= (int64_t)kBatchMinMean * nrl && P.d_xrange == nullptr && P.n_gblocks == 0 && P.d_sslot == nullptr &&
+        P.tune.persist == 0 && !P.tune.clamped && !P.tune.xcd) {
+        bool ok = false;
+        if ((e = aijhip::build_row_patterns(*A, P, &ok)) != hipSuccess) return hipfail(e, "plan: row patterns");
+    }
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
     // for the row blocks whose offset dictionaries fit (geometry 6 — 7 and 9
     // for MatMult / MatMultAdd only, A/B —, plain
@@ -357,7 +369,7 @@ int plan_stream(aijhip_mat *A) {
     // XCD remap, clamped loads or the persistent kernel); when some do not
     // fit, they are launched from aj
     if (P.tune.codes > 0 && (P.tune.geom == 6 || P.tune.geom == 7 || P.tune.geom == 9) && !blocks.empty() &&
-        !A->compressed && P.d_xrange == nullptr &&
+        P.d_pid == nullptr && !A->compressed && P.d_xrange == nullptr &&
         P.n_gblocks == 0 && P.d_sslot == nullptr && P.tune.persist == 0 && P.tune.nt <= 1 && !P.tune.clamped &&
         !P.tune.xcd) {
         int32_t *d_cnt = nullptr;
@@ -491,6 +503,7 @@ int plan_build(aijhip_mat *A) {
     P.tune = A->requested_tune;
     const bool auto_sort = P.tune.gsort < 0;
     const bool auto_codes = P.tune.codes < 0;
+    const bool auto_patterns = P.tune.patterns < 0;
     bool scattered = false;
     if (P.tune.geom < 0 || P.tune.nt < 0 || P.tune.gsort < 0) {
         // measured: 512 x 4094-entry blocks (geometry 6, 8 waves/SIMD) for
@@ -524,6 +537,7 @@ int plan_build(aijhip_mat *A) {
     }
     if (P.tune.group < 0) P.tune.group = 0;  // automatic choice: off until measured
     if (P.tune.codes < 0) P.tune.codes = 0;  // automatic: tried below (STREAM)
+    if (P.tune.patterns < 0) P.tune.patterns = 0;
     switch (kernel) {
         case AIJHIP_KERNEL_STREAM: {
             // Automatic column codes: tried first on every full-row operand
@@ -533,16 +547,19 @@ int plan_build(aijhip_mat *A) {
             // Measured in one process (profiles/r03/codes/): 300^3 Poisson
             // 486.6 -> 433.8 us, FEM stand-in 267.4 (gather-ordered) ->
             // 263.4 us; the skewed stand-in's blocks never fit.
+            // Row patterns are tried the same way, before the codes, for
+            // short rows (a stencil: no per-entry column at all).
             const aijhip::Tuning &rq = A->requested_tune;
-            if (auto_codes && !A->compressed && rq.gsort <= 0 && (rq.geom < 0 || rq.geom == 6) && rq.xtile == 0 &&
-                rq.group <= 0 && rq.persist == 0 && !rq.xcd && !rq.clamped && rq.nt <= 1) {
+            if ((auto_codes || auto_patterns) && !A->compressed && rq.gsort <= 0 && (rq.geom < 0 || rq.geom == 6) &&
+                rq.xtile <= 0 && rq.group <= 0 && rq.persist == 0 && !rq.xcd && !rq.clamped && rq.nt <= 1) {
                 const aijhip::Tuning keep = P.tune;
-                P.tune.codes = 1;
+                if (auto_codes) P.tune.codes = 1;
+                if (auto_patterns) P.tune.patterns = 1;
                 P.tune.gsort = 0;
                 P.tune.geom = 6;
                 if (rq.nt < 0) P.tune.nt = 0;
                 const int rc = plan_stream(A);
-                if (rc || P.d_code) return rc;
+                if (rc || P.d_code || P.d_pid) return rc;
                 free_plan(A->plan);
                 P.kernel = kernel;
                 P.tune = keep;
@@ -561,6 +578,7 @@ int plan_build(aijhip_mat *A) {
                 if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
                 if (P.tune.group < 0) P.tune.group = 0;
                 if (P.tune.codes < 0) P.tune.codes = 0;
+                if (P.tune.patterns < 0) P.tune.patterns = 0;
                 rc = plan_stream(A);
             }
             return rc;
@@ -789,9 +807,10 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
     A->d_aj = d_aj;
     A->d_aa = d_aa;
     A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
-    if (!like) {  // the set-up's own operators: one copy of the entries, no codes (plan time)
+    if (!like) {  // the set-up's own operators: one copy of the entries, no codes or patterns (plan time)
         A->requested_tune.gsort = 0;
         A->requested_tune.codes = 0;
+        A->requested_tune.patterns = 0;
     }
     aijhip::HostVec<int32_t> h_ai;
     int rc = AIJHIP_OK;
@@ -929,6 +948,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_COLUMN_CODES:
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "column_codes: -1 auto, 0 off, 1 on");
             t.codes = value;
+            break;
+        case AIJHIP_OPT_ROW_PATTERNS:
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "row_patterns: -1 auto, 0 off, 1 on");
+            t.patterns = value;
             break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
@@ -1121,6 +1144,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->x_tiled_blocks = A->plan.n_xtiled;
     info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
     info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
+    info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
     return AIJHIP_OK;
 }
 

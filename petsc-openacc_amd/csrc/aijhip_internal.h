@@ -109,6 +109,8 @@ struct Tuning {
                            // (operands with scattered gathers, caller's handles), 0 off, 1 on
     int codes = -1;        // 16-bit column codes instead of aj (Plan::d_code): -1 auto (where the
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
+    int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
+                           // offset lists are few), 0 off, 1 on
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is
@@ -119,6 +121,11 @@ struct Tuning {
 // (128 offsets; a 7-point stencil has 7), 50-row blocks of FEM rows 9
 // (512; a block of the FEM stand-in has ~135).
 constexpr int kCodeDictMax = 512;
+// Row patterns (Tuning::patterns): at most 256 distinct column - row offset
+// lists per operand, their table (a start | length word per pattern, then
+// the offsets) at most kPatTableMax words, staged in LDS by every block.
+constexpr int kPatTableMax = 1024;
+constexpr int kPatMax = 256;
 __host__ __device__ inline int code_index_bits(int nrows) {
     int rb = 0;
     while (rb < 16 && (1 << rb) < nrows) ++rb;
@@ -201,6 +208,11 @@ struct Plan {
     // others in d_wblocks (launched from aj) when some do not fit
     uint16_t *d_code = nullptr;
     int32_t *d_cmeta = nullptr;
+    // Tuning::patterns: a pattern id per row and the pattern table (start |
+    // length << 16 per pattern, then the offsets); geometry 6, full rows
+    uint8_t *d_pid = nullptr;
+    int32_t *d_ptab = nullptr;
+    int32_t n_ptab = 0, n_pat = 0;
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;
     int32_t n_tiles = 0;
@@ -302,6 +314,11 @@ hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk
 // Column codes: pass 0 counts each block's distinct column - row offsets
 // into d_cnt[0, nblk); pass 1 (d_cmeta laid out by the caller) writes the
 // dictionaries and the codes of blocks d_blk[0, nblk).
+// Row patterns: when the operand's rows follow at most kPatMax distinct
+// column - row offset lists (64-bit hashes, verified entry by entry) whose
+// table fits kPatTableMax words, allocates and fills P.d_pid / P.d_ptab and
+// sets *ok; otherwise leaves them null.
+hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok);
 hipError_t column_code_counts(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt);
 hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cmeta,
                              uint16_t *d_code);

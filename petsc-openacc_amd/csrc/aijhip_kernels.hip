@@ -31,6 +31,9 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+#include <vector>
+
 #include "aijhip_internal.h"
 
 namespace aijhip {
@@ -504,6 +507,86 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
         for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
             const double v = block_sum<T>(dv[q], prod);
             if (t == 0) dpart[(int64_t)q * nblk + b] = v;
+        }
+    }
+}
+
+// Row patterns (Tuning::patterns; short-row operands whose rows follow a
+// few column - row offset lists: stencils): the STREAM row blocks, but the
+// columns are not stored per entry. Each row has a pattern id (1 byte), the
+// pattern table (offsets in storage order) is staged in LDS per block, and
+// the matrix stream is aa alone, staged in LDS by coalesced 16-B loads.
+// Phase 2 takes one lane per row: column = row + offset, x gathered by the
+// row's lane (neighbouring lanes gather neighbouring x for a stencil), and
+// s += aa * x in storage order from s = seed — the arithmetic and order of
+// the STREAM kernel's phase 1 + phase 2, so the result is bit-identical.
+// ptab: [0, npat) = start | len << 16 of each pattern's offsets, then the
+// offsets; ntab entries in all (<= kPatTableMax).
+template <int T, int CAP, class Op>
+__global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
+                                                    const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
+                                                    int ntab, int npat, const double *__restrict__ aa, Op op,
+                                                    double *dpart, const int *stop) {
+    constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
+    constexpr int TPT = (kPatTableMax + T - 1) / T;
+    __shared__ double av[CAP];
+    __shared__ int32_t tab[kPatTableMax];
+    const int b = (int)blockIdx.x;
+    const BlockDesc d = blk[b];
+    if ((stop ? *stop : 0) != 0 || d.nk < 0) return;
+    const int t = threadIdx.x;
+    const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
+    int32_t tv[TPT];
+#pragma unroll
+    for (int i = 0; i < TPT; ++i)
+        if (t + i * T < ntab) tv[i] = ptab[t + i * T];
+    const int r = d.row0 + min(t, d.nrows - 1);
+    const int32_t rs = rai[r], re = rai[r + 1];
+    const int p = pid[r];
+    const double seed = op.seed(r);
+    // the block's values: 16-B loads from an even start (2-entry tail pad)
+    const int64_t kb = k0 & ~int64_t(1);
+    f64x2 a2[ITERS];
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * T);
+        if (k < k1) a2[it] = *reinterpret_cast<const f64x2 *>(aa + k);
+    }
+#pragma unroll
+    for (int i = 0; i < TPT; ++i)
+        if (t + i * T < ntab) tab[t + i * T] = tv[i];
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * T);
+        if (k < k1) {
+            if (k >= k0) av[k - k0] = a2[it].x;
+            if (k + 1 < k1) av[k + 1 - k0] = a2[it].y;
+        }
+    }
+    __syncthreads();
+    double dv[Op::kDots > 0 ? Op::kDots : 1] = {};
+    if (t < d.nrows) {
+        const int32_t pm = tab[min(p, npat - 1)];
+        const int32_t* off = tab + (pm & 0xffff);
+        const int32_t n = re - rs;  // == the pattern's length
+        const double *ar = av + (rs - k0);
+        double s = seed;
+        for (int32_t j0 = 0; j0 < n; j0 += 8) {
+            double xv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j0 + j < n) xv[j] = op.gx(r + off[j0 + j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j0 + j < n) s += ar[j0 + j] * xv[j];
+        }
+        op.put(r, s, dv);
+    }
+    if (Op::kDots > 0 && dpart) {
+#pragma unroll
+        for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
+            const double v = block_sum<T>(dv[q], av);
+            if (t == 0) dpart[(int64_t)q * gridDim.x + b] = v;
         }
     }
 }
@@ -1216,6 +1299,177 @@ hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk
     return hipGetLastError();
 }
 
+// ---- row patterns (Tuning::patterns) -----------------------------------
+__device__ __forceinline__ unsigned long long pat_mix(unsigned long long h) {
+    h ^= h >> 30;
+    h *= 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 27;
+    h *= 0x94d049bb133111ebull;
+    return h ^ (h >> 31);
+}
+
+// 64-bit hash of each row's length and column - row offsets (never 0)
+__global__ __launch_bounds__(256) void k_pat_hash(int32_t m, const int32_t *__restrict__ ai,
+                                                  const int32_t *__restrict__ aj, unsigned long long *hash) {
+    const int32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    const int32_t k0 = ai[r], k1 = ai[r + 1];
+    unsigned long long h = pat_mix(0x9e3779b97f4a7c15ull + (unsigned long long)(k1 - k0));
+    for (int32_t k = k0; k < k1; ++k) h = pat_mix(h ^ (unsigned long long)(uint32_t)(aj[k] - r));
+    hash[r] = h | 1ull;
+}
+
+// Distinct hashes into an open-addressing table of `ts` slots (a power of
+// two): a lane whose wave neighbour holds the same hash leaves the insert to
+// it, and a slot already holding the hash is read before any CAS, so the
+// ~all-interior rows of a stencil cost one atomic per new pattern.
+constexpr int kPatTableSlots = 4096;
+__global__ __launch_bounds__(256) void k_pat_insert(int32_t m, const unsigned long long *__restrict__ hash,
+                                                    unsigned long long *table, int *overflow) {
+    const int32_t r = blockIdx.x * 256 + threadIdx.x;
+    const unsigned long long h = r < m ? hash[r] : 0ull;
+    const unsigned long long hp = __shfl_up(h, 1, 64);
+    if (r >= m || ((threadIdx.x & 63) != 0 && hp == h)) return;
+    unsigned int slot = (unsigned int)(h >> 20) & (kPatTableSlots - 1);
+    for (int probe = 0; probe < kPatTableSlots; ++probe) {
+        const unsigned long long cur = __atomic_load_n(table + slot, __ATOMIC_RELAXED);
+        if (cur == h) return;
+        if (cur == 0ull) {
+            const unsigned long long prev = atomicCAS(table + slot, 0ull, h);
+            if (prev == 0ull || prev == h) return;
+        }
+        slot = (slot + 1) & (kPatTableSlots - 1);
+    }
+    atomicExch(overflow, 1);
+}
+
+// Pattern id of each row (binary search in the sorted distinct hashes) and
+// each pattern's first row
+__global__ __launch_bounds__(256) void k_pat_assign(int32_t m, const unsigned long long *__restrict__ hash,
+                                                    const unsigned long long *__restrict__ sorted, int npat,
+                                                    uint8_t *pid, int32_t *rep) {
+    const int32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    const unsigned long long h = hash[r];
+    int lo = 0, hi = npat - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (sorted[mid] < h) lo = mid + 1;
+        else hi = mid;
+    }
+    pid[r] = (uint8_t)lo;
+    if (__atomic_load_n(rep + lo, __ATOMIC_RELAXED) > r) atomicMin(rep + lo, r);
+}
+
+// The offsets of each pattern's first row (at most kPatTableMax per row)
+__global__ void k_pat_rows(int npat, const int32_t *__restrict__ rep, const int32_t *__restrict__ ai,
+                           const int32_t *__restrict__ aj, int32_t *len, int32_t *off) {
+    const int p = blockIdx.x;
+    const int32_t r = rep[p], k0 = ai[r], n = ai[r + 1] - k0;
+    if (threadIdx.x == 0) len[p] = n;
+    for (int j = threadIdx.x; j < n && j < kPatTableMax; j += blockDim.x) off[p * kPatTableMax + j] = aj[k0 + j] - r;
+}
+
+// Rows whose entries differ from their pattern's (a hash collision)
+__global__ __launch_bounds__(256) void k_pat_verify(int32_t m, const int32_t *__restrict__ ai,
+                                                    const int32_t *__restrict__ aj, const uint8_t *__restrict__ pid,
+                                                    const int32_t *__restrict__ ptab, int *bad) {
+    const int32_t r = blockIdx.x * 256 + threadIdx.x;
+    if (r >= m) return;
+    const int32_t pm = ptab[pid[r]], st = pm & 0xffff, len = pm >> 16;
+    const int32_t k0 = ai[r], n = ai[r + 1] - k0;
+    bool ok = n == len;
+    for (int32_t j = 0; ok && j < n; ++j) ok = aj[k0 + j] - r == ptab[st + j];
+    if (!ok) atomicAdd(bad, 1);
+}
+
+hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
+    *ok = false;
+    const int32_t m = A.m;
+    if (m <= 0 || A.compressed) return hipSuccess;
+    const int g = (int)((m + 255) / 256);
+    unsigned long long *d_hash = nullptr, *d_table = nullptr, *d_sorted = nullptr;
+    int *d_flag = nullptr;
+    int32_t *d_rep = nullptr, *d_len = nullptr, *d_off = nullptr;
+    hipError_t e;
+    auto done = [&](hipError_t r) {
+        hipFree(d_hash); hipFree(d_table); hipFree(d_sorted); hipFree(d_flag);
+        hipFree(d_rep); hipFree(d_len); hipFree(d_off);
+        return r;
+    };
+    if ((e = hipMalloc(&d_hash, sizeof(unsigned long long) * (size_t)m)) != hipSuccess ||
+        (e = hipMalloc(&d_table, sizeof(unsigned long long) * kPatTableSlots)) != hipSuccess ||
+        (e = hipMalloc(&d_flag, sizeof(int) * 2)) != hipSuccess ||
+        (e = hipMemset(d_table, 0, sizeof(unsigned long long) * kPatTableSlots)) != hipSuccess ||
+        (e = hipMemset(d_flag, 0, sizeof(int) * 2)) != hipSuccess)
+        return done(e);
+    hipLaunchKernelGGL(k_pat_hash, dim3(g), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, d_hash);
+    hipLaunchKernelGGL(k_pat_insert, dim3(g), dim3(256), 0, nullptr, m, d_hash, d_table, d_flag);
+    std::vector<unsigned long long> table(kPatTableSlots);
+    int flag[2] = {0, 0};
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpy(table.data(), d_table, sizeof(unsigned long long) * table.size(), hipMemcpyDeviceToHost)) !=
+            hipSuccess ||
+        (e = hipMemcpy(flag, d_flag, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess)
+        return done(e);
+    std::vector<unsigned long long> hs;
+    for (unsigned long long h : table)
+        if (h) hs.push_back(h);
+    if (flag[0] || hs.empty() || (int)hs.size() > kPatMax) return done(hipSuccess);
+    std::sort(hs.begin(), hs.end());  // pattern ids in hash order: the same ids run to run
+    const int npat = (int)hs.size();
+    std::vector<int32_t> rep_init(npat, INT32_MAX);
+    if ((e = hipMalloc(&d_sorted, sizeof(unsigned long long) * npat)) != hipSuccess ||
+        (e = hipMalloc(&d_rep, sizeof(int32_t) * npat)) != hipSuccess ||
+        (e = hipMalloc(&d_len, sizeof(int32_t) * npat)) != hipSuccess ||
+        (e = hipMalloc(&d_off, sizeof(int32_t) * (size_t)npat * kPatTableMax)) != hipSuccess ||
+        (e = hipMalloc(&P.d_pid, (size_t)m + 256)) != hipSuccess ||
+        (e = hipMemcpy(d_sorted, hs.data(), sizeof(unsigned long long) * npat, hipMemcpyHostToDevice)) !=
+            hipSuccess ||
+        (e = hipMemcpy(d_rep, rep_init.data(), sizeof(int32_t) * npat, hipMemcpyHostToDevice)) != hipSuccess)
+        return done(e);
+    hipLaunchKernelGGL(k_pat_assign, dim3(g), dim3(256), 0, nullptr, m, d_hash, d_sorted, npat, P.d_pid, d_rep);
+    hipLaunchKernelGGL(k_pat_rows, dim3(npat), dim3(64), 0, nullptr, npat, d_rep, A.d_ai, A.d_aj, d_len, d_off);
+    std::vector<int32_t> len(npat);
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpy(len.data(), d_len, sizeof(int32_t) * npat, hipMemcpyDeviceToHost)) != hipSuccess)
+        return done(e);
+    std::vector<int32_t> tab(npat);
+    int64_t total = npat;
+    for (int p = 0; p < npat; ++p) total += len[p];
+    if (total > kPatTableMax) {
+        hipFree(P.d_pid);
+        P.d_pid = nullptr;
+        return done(hipSuccess);
+    }
+    std::vector<int32_t> off((size_t)npat * kPatTableMax);
+    if ((e = hipMemcpy(off.data(), d_off, sizeof(int32_t) * off.size(), hipMemcpyDeviceToHost)) != hipSuccess)
+        return done(e);
+    for (int p = 0; p < npat; ++p) {
+        tab[p] = (int32_t)tab.size() | (len[p] << 16);
+        for (int j = 0; j < len[p]; ++j) tab.push_back(off[(size_t)p * kPatTableMax + j]);
+    }
+    if ((e = hipMalloc(&P.d_ptab, sizeof(int32_t) * tab.size())) != hipSuccess ||
+        (e = hipMemcpy(P.d_ptab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
+        return done(e);
+    hipLaunchKernelGGL(k_pat_verify, dim3(g), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, P.d_pid, P.d_ptab, d_flag + 1);
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpy(flag, d_flag, sizeof(int) * 2, hipMemcpyDeviceToHost)) != hipSuccess)
+        return done(e);
+    if (flag[1] != 0) {  // a collision: keep aj
+        hipFree(P.d_pid);
+        hipFree(P.d_ptab);
+        P.d_pid = nullptr;
+        P.d_ptab = nullptr;
+        return done(hipSuccess);
+    }
+    P.n_ptab = (int32_t)tab.size();
+    P.n_pat = npat;
+    P.bytes += (int64_t)m + 256 + 4 * (int64_t)tab.size();
+    *ok = true;
+    return done(hipSuccess);
+}
+
 template <bool WRITE>
 static hipError_t launch_block_codes(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt,
                                      int32_t *d_cmeta, uint16_t *d_code, int cap) {
@@ -1342,6 +1596,20 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                        L.rai, L.ridx, A.d_aj, A.d_aa,                                              \
                        OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, nullptr); \
     return
+    // Row patterns (Plan::d_pid; geometry 6, full-row lists, short rows)
+    if constexpr (T == 512 && CAP == 4094 && RPT == 1) {
+        if (P.d_pid && !L.ridx) {
+            if (add)
+                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, OpMult<true>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks,
+                                   L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
+                                   OpMult<true>{x, z, y, dpart != nullptr}, dpart, stop);
+            else
+                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, OpMult<false>>), dim3(P.n_blocks), dim3(T), 0, s,
+                                   P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
+                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop);
+            return;
+        }
+    }
     // Column codes (Plan::d_code; geometry 6, full-row lists): MatMult,
     // MatMultAdd and the CG's fused dot; with a coded / uncoded split the dot's
     // partials would come from two launches, so that case takes aj
@@ -1491,6 +1759,11 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
+    if (P.d_pid && P.tune.geom == 6) {  // row patterns (planned at geometry 6)
+        hipLaunchKernelGGL((k_spmv_pattern<512, 4094, Op>), dim3(P.n_blocks), dim3(512), 0, s, P.d_blocks, A.d_ai,
+                           P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop);
+        return hipGetLastError();
+    }
     if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, false, 32, false, Op>), dim3(P.n_blocks),
                            dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex, A.d_ai, nullptr,

@@ -52,7 +52,7 @@ def test_poisson_codes_bitwise(pkg, dev, coracle):
     ai, aj, aa = pkg.poisson_csr(37)
     m = len(ai) - 1
     x, z = pkg.splitmix_uniform(m, 42), pkg.splitmix_uniform(m, 7)
-    with pkg.SeqAIJHIP(ai, aj, aa, column_codes=1) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=0, column_codes=1) as A:
         info = A.info()
         assert info["column_codes"] == 1 and info["stream_geometry"] == 6
         y1, w1 = products(A, x, z, dev)
@@ -77,7 +77,7 @@ def test_golden_codes(pkg, dev, name):
     bit-identical to the fixture (exact mode)."""
     g = golden(name)
     ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
-    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, column_codes=1, exact=1) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, row_patterns=0, column_codes=1, exact=1) as A:
         xd = to_dev(g["x"], dev)
         y = torch.full((A.m,), np.nan, dtype=torch.float64, device=dev)
         A.mult(xd, y)
@@ -109,7 +109,7 @@ def test_split_coded_and_uncoded_blocks(pkg, dev, coracle):
     aj = np.concatenate([c for c, _ in rows]).astype(np.int32)
     aa = np.concatenate([v for _, v in rows])
     x, z = pkg.splitmix_uniform(m, 1), pkg.splitmix_uniform(m, 2)
-    with pkg.SeqAIJHIP(ai, aj, aa, column_codes=1, exact=1) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=0, column_codes=1, exact=1) as A:
         assert A.info()["column_codes"] == 1
         y1, w1 = products(A, x, z, dev)
         assert_bits(y1, coracle.matmult(ai, aj, aa, x, omp=True))
@@ -160,7 +160,7 @@ def test_cg_and_gamg_with_codes_bitwise(pkg, dev):
     for pc, kw in (("jacobi", dict(rtol=1e-10, max_it=500)), ("gamg", dict(rtol=1e-14, atol=1e-12))):
         out = {}
         for codes in (0, 1):
-            with pkg.SeqAIJHIP(ai, aj, aa, column_codes=codes) as A:
+            with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=0, column_codes=codes) as A:
                 assert A.info()["column_codes"] == codes
                 x = torch.zeros_like(b)
                 with K.KSPCG(A, pc=pc, **kw) as ksp:

@@ -489,18 +489,20 @@ def test_fem_hex_flan_standin_all_kernels(pkg, dev, coracle):
 
 
 def test_auto_geometry_follows_gather_locality(pkg, dev, coracle):
-    """Automatic STREAM layout (aijhip_api.cpp plan_build): column codes at
-    geometry 6 wherever the row blocks' offset dictionaries fit (the 7-point
-    stencil, the FEM rows); otherwise long rows -> the gather-ordered copy in
-    its 16-bit form at geometry 6, and without it (gather_sort 0) long
-    scattered rows -> geometry 1. The gather-ordered product equals the
-    unsorted one and the oracle bit for bit (rows within the block cap)."""
-    cases = [(pkg.poisson_csr(12), 6, 0, 1, 6), (pkg.fem_hex_csr(21, 20, 19), 6, 0, 1, 6),
-             (pkg.skewed_csr(300000, seed=1565), 6, 2, 0, 1)]  # 2: 16-bit block-relative columns
-    for (ai, aj, aa), geom, sorted_, codes, geom_unsorted in cases:
+    """Automatic STREAM layout (aijhip_api.cpp plan_build): row patterns at
+    geometry 6 for short rows that follow few offset lists (the 7-point
+    stencil); column codes wherever the row blocks' offset dictionaries fit
+    (the FEM rows); otherwise long rows -> the gather-ordered copy in its
+    16-bit form at geometry 6, and without it (gather_sort 0) long scattered
+    rows -> geometry 1. The gather-ordered product equals the unsorted one
+    and the oracle bit for bit (rows within the block cap)."""
+    cases = [(pkg.poisson_csr(12), 6, 0, 0, True, 6), (pkg.fem_hex_csr(21, 20, 19), 6, 0, 1, False, 6),
+             (pkg.skewed_csr(300000, seed=1565), 6, 2, 0, False, 1)]  # 2: 16-bit block-relative columns
+    for (ai, aj, aa), geom, sorted_, codes, pats, geom_unsorted in cases:
         with pkg.SeqAIJHIP(ai, aj, aa) as A:
             info = A.info()
-            assert (info["stream_geometry"], info["gather_sorted"], info["column_codes"]) == (geom, sorted_, codes)
+            assert (info["stream_geometry"], info["gather_sorted"], info["column_codes"],
+                    info["row_patterns"] > 0) == (geom, sorted_, codes, pats)
             if not sorted_:
                 continue
             x = torch.from_numpy(pkg.splitmix_uniform(A.n, 42)).to(dev)

@@ -1,0 +1,133 @@
+"""Row patterns (AIJHIP_OPT_ROW_PATTERNS): for short-row operands whose rows
+follow at most 256 distinct column - row offset lists (a stencil), the STREAM
+row blocks read no column per entry — a pattern id per row, the lists staged
+in LDS, x gathered by one lane per row. aa and the summation (s = seed, then
+s += aa[k] * x[col] in storage order) are the plain kernel's, so every result
+must be BIT-IDENTICAL to the aj layout and to the oracle (the PETSc row loop,
+/root/reference/src/openacc-step1/MatMult_SeqAIJ.patch:22-31)."""
+import importlib
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN_NAMES, golden
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev(pkg):
+    assert torch.cuda.is_available(), "GPU tests need a visible MI355X"
+    return torch.device("cuda:0")
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).to(dev)
+
+
+def assert_bits(a, b, mask=None):
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    if mask is not None:
+        a, b = a[mask], b[mask]
+    bad = np.nonzero(a.view(np.uint64) != b.view(np.uint64))[0]
+    assert bad.size == 0, f"{bad.size}/{a.size} entries differ bitwise; first {bad[:4]}: {a[bad[:4]]} vs {b[bad[:4]]}"
+
+
+def products(A, x, z, dev):
+    xd, zd = to_dev(x, dev), to_dev(z, dev)
+    y = torch.full((A.m,), np.nan, dtype=torch.float64, device=dev)
+    w = torch.full((A.m,), np.nan, dtype=torch.float64, device=dev)
+    A.mult(xd, y)
+    A.mult_add(xd, zd, w)
+    torch.cuda.synchronize()
+    return y.cpu().numpy(), w.cpu().numpy()
+
+
+@pytest.mark.parametrize("dims", [(37, 37, 37), (20, 17, 13), (1, 9, 40), (300, 2, 3)])
+def test_poisson_patterns_bitwise(pkg, dev, coracle, dims):
+    """7-point Poisson with the reference point (helper.cpp:161-279), cubes,
+    boxes and thin grids: the automatic layout takes row patterns (interior,
+    faces, edges, corners, the reference rows); MatMult and MatMultAdd equal
+    the oracle and the aj layout bit for bit, also after new values."""
+    ai, aj, aa = pkg.poisson_csr(*dims)
+    m = len(ai) - 1
+    x, z = pkg.splitmix_uniform(m, 42), pkg.splitmix_uniform(m, 7)
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        info = A.info()
+        assert 0 < info["row_patterns"] <= 256 and info["column_codes"] == 0
+        y1, w1 = products(A, x, z, dev)
+        assert_bits(y1, coracle.matmult(ai, aj, aa, x, omp=True))
+        A.set_option("row_patterns", 0)
+        A.set_option("column_codes", 0)
+        assert A.info()["row_patterns"] == 0
+        y0, w0 = products(A, x, z, dev)
+        assert_bits(y1, y0)
+        assert_bits(w1, w0)
+        A.set_option("row_patterns", -1)
+        aa2 = np.random.default_rng(5).uniform(-1, 1, len(aa))
+        A.update_values(aa2)  # the patterns do not depend on the values
+        y2, _ = products(A, x, z, dev)
+        assert_bits(y2, coracle.matmult(ai, aj, aa2, x, omp=True))
+
+
+@pytest.mark.parametrize("name", GOLDEN_NAMES)
+def test_golden_patterns(pkg, dev, name):
+    """Every golden fixture with patterns requested (taken where they fit):
+    rows within the block cap stay bit-identical to the fixture."""
+    g = golden(name)
+    ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, row_patterns=1, exact=1) as A:
+        xd = to_dev(g["x"], dev)
+        y = torch.full((A.m,), np.nan, dtype=torch.float64, device=dev)
+        A.mult(xd, y)
+        torch.cuda.synchronize()
+        short = np.diff(ai) <= A.info()["stream_nnz_cap"]
+        assert_bits(y.cpu().numpy(), g["y"], short)
+
+
+def test_many_patterns_fall_back(pkg, dev, coracle):
+    """Short random rows (>256 distinct offset lists): no patterns; the plan
+    keeps another layout and the product stays the oracle's."""
+    rng = np.random.default_rng(9)
+    m = 50000
+    lens = rng.integers(3, 9, m)
+    cols = [np.unique(np.clip(i + rng.integers(-40, 41, l), 0, m - 1)) for i, l in enumerate(lens)]
+    ai = np.concatenate([[0], np.cumsum([len(c) for c in cols])]).astype(np.int32)
+    aj = np.concatenate(cols).astype(np.int32)
+    aa = rng.uniform(-1, 1, len(aj))
+    x = rng.uniform(-1, 1, m)
+    with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=1) as A:
+        assert A.info()["row_patterns"] == 0
+        xd = to_dev(x, dev)
+        y = torch.empty(m, dtype=torch.float64, device=dev)
+        A.mult(xd, y)
+        torch.cuda.synchronize()
+        assert_bits(y.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True))
+
+
+def test_cg_and_gamg_with_patterns_bitwise(pkg, dev):
+    """The solver path on a patterned operator: CG + Jacobi (the fused
+    SpMV + p.w epilogue) and CG + GAMG (the fused V-cycle smoothers and the
+    set-up's power iteration on the fine level) give the aj run's residual
+    history and solution bit for bit."""
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    ai, aj, aa = pkg.poisson_csr(40)
+    rhs, _ = pkg.poisson_vectors(40, 40, 40)
+    b = torch.from_numpy(rhs).to(dev)
+    for pc, kw in (("jacobi", dict(rtol=1e-10, max_it=500)), ("gamg", dict(rtol=1e-14, atol=1e-12))):
+        out = {}
+        for pats in (0, 1):
+            with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=pats, column_codes=0) as A:
+                assert (A.info()["row_patterns"] > 0) == bool(pats)
+                x = torch.zeros_like(b)
+                with K.KSPCG(A, pc=pc, **kw) as ksp:
+                    ksp.set_up()
+                    ksp.solve(b, x)
+                    torch.cuda.synchronize()
+                    assert ksp.fused
+                    out[pats] = (ksp.its, ksp.history(), x.cpu().numpy())
+        assert out[0][0] == out[1][0]
+        assert_bits(out[0][1], out[1][1])
+        assert_bits(out[0][2], out[1][2])

@@ -142,6 +142,9 @@ def main():
     if args.variants == "codesgeom":  # column codes at the geometries the coded launch is built for
         for g, cc, nt in ((6, 1, 0), (6, 1, 1), (7, 1, 0), (7, 1, 1), (9, 1, 0), (9, 1, 1), (6, 0, 0)):
             variants.append(("stream", dict(geometry=g, gather_sort=0, column_codes=cc, nt_loads=nt)))
+    if args.variants == "layouts":  # the automatic layout (row patterns / codes) against codes and aj
+        for rp, cc, nt in ((-1, -1, 0), (0, 1, 0), (0, 0, 0), (1, 0, 1)):
+            variants.append(("stream", dict(geometry=6, gather_sort=0, row_patterns=rp, column_codes=cc, nt_loads=nt)))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
@@ -181,6 +184,7 @@ def main():
         A.set_option("row_group", opts.get("row_group", 0))
         A.set_option("gather_sort", opts.get("gather_sort", -1))
         A.set_option("column_codes", opts.get("column_codes", -1))
+        A.set_option("row_patterns", opts.get("row_patterns", -1))
         for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
             if k in opts:
                 A.set_option(k, opts[k])
