@@ -18,9 +18,13 @@ north star's "300^3 matrix at 1, 2, 4 and 8 GPUs").
 value  = algorithmic bytes of all ranks x K / (max-over-ranks wall time of the
          K timed steps), bytes per SpMV = 12 nnz + 4 (m+1) + 8 n + 8 m
          (x and the matrix read once, y written once).
-roofline.achieved = the same bytes per launch / the mean duration of the
-         dominant kernel, from HIP events recorded around every launch on the
-         stream it runs on; peak 8 TB/s (MI355X_MICROARCH.md).
+roofline.achieved = the compulsory bytes of the layout the plan chose (row
+         patterns / column codes / CSR, roofline.layout) per launch / the
+         mean duration of the dominant kernel, from HIP events recorded
+         around every launch on the stream it runs on; peak 8 TB/s
+         (MI355X_MICROARCH.md). roofline.csr_effective: the CSR bytes / the
+         same time (value's effective rate); roofline.aj_layout: the same
+         MatMult from aj in the same run.
 cpu_baseline = the C restatement of PETSc's MatMult_SeqAIJ (oracle/, a port:
          the reference cannot be built here) on 1 host core, bounded sample.
 """
@@ -705,7 +709,22 @@ def main():
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
         mean_launch_s = float(np.mean(launch_ms)) / 1e3
-        achieved = bytes_local / mean_launch_s / 1e9
+        # The roofline is the kernel's own: the compulsory bytes of the
+        # layout the plan chose (row patterns: no column per entry, a 1-byte
+        # id per row; column codes: 2 B per entry instead of aj's 4 B; else
+        # SURVEY §8d's CSR bytes). `value` stays the metric's effective rate
+        # on the CSR bytes (roofline.csr_effective beside it).
+        if info.get("row_patterns") and not distributed:
+            layout_bytes = bytes_local - 4 * nnz_loc + m_loc
+            layout = (f"row patterns ({info['row_patterns']} column - row offset lists, a 1-byte id per row, aa "
+                      "verbatim, no column per entry; cf. PETSc's inode rows)")
+        elif info.get("column_codes") and not distributed:
+            layout_bytes = bytes_local - 2 * nnz_loc
+            layout = "column codes (a 16-bit code per entry in aj's place, aa verbatim)"
+        else:
+            layout_bytes, layout = bytes_local, "CSR (PETSc's ai / aj / aa)"
+        achieved = layout_bytes / mean_launch_s / 1e9
+        achieved_csr = bytes_local / mean_launch_s / 1e9
         block = {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "xcd_remap", "nt_loads",
                                       "persistent", "column_codes", "row_patterns")}
         traffic, traffic_src = (None, None) if distributed else pmc_traffic(n_global, nnz_global, block)
@@ -745,40 +764,27 @@ def main():
                 "kernel_us_median": round(float(np.median(launch_ms)) * 1e3, 2),
                 "kernel_us_min": round(float(np.min(launch_ms)) * 1e3, 2),
                 "launches_timed": int(len(launch_ms)),
-                "achieved_from_median": round(bytes_local / (float(np.median(launch_ms)) / 1e3) / 1e9, 1),
-                "bytes_per_launch": bytes_local,
+                "achieved_from_median": round(layout_bytes / (float(np.median(launch_ms)) / 1e3) / 1e9, 1),
+                "bytes_per_launch": layout_bytes,
+                "layout": layout,
+                "csr_effective": {
+                    "bytes_per_launch": bytes_local, "achieved": round(achieved_csr, 1),
+                    "frac": round(achieved_csr / HBM_PEAK_GBS, 4),
+                    "note": "SURVEY §8d's CSR bytes (12 nnz + 4 (m+1) + 8 n + 8 m) / the same mean launch time: "
+                            "the metric's effective bandwidth (value); above the HBM peak when the layout reads "
+                            "fewer bytes than CSR"},
             },
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
-        if info.get("column_codes") or info.get("row_patterns"):
-            # `achieved` keeps SURVEY §8d's CSR bytes, as the metric defines
-            # effective bandwidth; these are the bytes the kernel moves and
-            # its rate on them. Column codes read 2 B per entry instead of
-            # aj's 4 B (plus the blocks' offset dictionaries, < 0.1 %); row
-            # patterns read no column per entry, 1 B of pattern id per row
-            # (plus a table of <= 1024 words, L2-resident)
-            if info.get("row_patterns"):
-                moved = bytes_local - 4 * nnz_loc + m_loc
-                out["roofline"]["layout"] = (f"row patterns ({info['row_patterns']} column - row offset lists, "
-                                             "a 1-byte id per row, aa verbatim; cf. PETSc's inode rows)")
-            else:
-                moved = bytes_local - 2 * nnz_loc
-                out["roofline"]["layout"] = "column codes (16-bit per entry, aa verbatim)"
-            out["roofline"]["bytes_moved_per_launch"] = moved
-            out["roofline"]["moved_GBs"] = round(moved / mean_launch_s / 1e9, 1)
-            out["roofline"]["frac_of_moved_bytes"] = round(moved / mean_launch_s / 1e9 / HBM_PEAK_GBS, 4)
         if aj_leg is not None:
             out["roofline"]["aj_layout"] = aj_leg
         if isinstance(ceiling, dict) and "error" not in ceiling:  # same-run flat reads of the same bytes
-            if "moved_GBs" in out["roofline"]:  # the kernel against the same reads, on the bytes it moves
-                out["roofline"]["moved_frac_of_flat_read"] = round(out["roofline"]["moved_GBs"] / ceiling[0][0], 4)
-                out["roofline"]["moved_frac_of_stream_shape_read"] = round(
-                    out["roofline"]["moved_GBs"] / ceiling[1][0], 4)
             out["roofline"]["ceiling_flat_read"] = {
                 "GBs": ceiling[0][0], "us": ceiling[0][1], "frac_of_ceiling": round(achieved / ceiling[0][0], 4),
-                "probe": "aijhip_read_probe mode 0: the SpMV's byte count read once, non-temporal 16-B loads, "
-                         "512-lane workgroups of two loads per lane (the fastest shape, tools/read_sweep.hip)",
+                "probe": "aijhip_read_probe mode 0: the SpMV's CSR byte count read once, non-temporal 16-B loads, "
+                         "512-lane workgroups of two loads per lane (the fastest shape, tools/read_sweep.hip); "
+                         "frac_of_ceiling = roofline.achieved (the layout's bytes) / this rate",
                 "stream_shape_read": {"GBs": ceiling[1][0], "us": ceiling[1][1],
                                       "frac": round(achieved / ceiling[1][0], 4),
                                       "probe": "mode 1: plain loads, four per lane (the STREAM kernel's shape)"}}
