@@ -361,6 +361,12 @@ int plan_stream(aijhip_mat *A) {
         P.tune.persist == 0 && !P.tune.clamped && !P.tune.xcd) {
         bool ok = false;
         if ((e = aijhip::build_row_patterns(*A, P, &ok)) != hipSuccess) return hipfail(e, "plan: row patterns");
+        // row starts from ai (default) or from the scan of the patterns'
+        // lengths (AIJHIP_PAT_AI=0; measured slower: 368.4 vs 358.3 us at
+        // 300^3, profiles/r03/patterns/patai_poisson.jsonl — the scan waits
+        // on the pattern id and the table, where ai's loads were in flight)
+        const char *pa = std::getenv("AIJHIP_PAT_AI");
+        P.pat_ai = !(pa && pa[0] == '0');
     }
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
     // for the row blocks whose offset dictionaries fit (geometry 6 — 7 and 9

@@ -213,6 +213,7 @@ struct Plan {
     uint8_t *d_pid = nullptr;
     int32_t *d_ptab = nullptr;
     int32_t n_ptab = 0, n_pat = 0;
+    bool pat_ai = true;  // row starts from ai; AIJHIP_PAT_AI=0 at planning: from the lengths' scan (A/B)
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;
     int32_t n_tiles = 0;

@@ -522,7 +522,10 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // the STREAM kernel's phase 1 + phase 2, so the result is bit-identical.
 // ptab: [0, npat) = start | len << 16 of each pattern's offsets, then the
 // offsets; ntab entries in all (<= kPatTableMax).
-template <int T, int CAP, class Op>
+// SCAN: the rows' starts are the block's k0 plus the prefix sums of their
+// patterns' lengths (a wave scan and the wave totals through LDS), so ai is
+// not read at all; otherwise from ai (A/B).
+template <int T, int CAP, bool SCAN, class Op>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
@@ -531,6 +534,7 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     constexpr int TPT = (kPatTableMax + T - 1) / T;
     __shared__ double av[CAP];
     __shared__ int32_t tab[kPatTableMax];
+    __shared__ int32_t wsum[T / 64];
     const int b = (int)blockIdx.x;
     const BlockDesc d = blk[b];
     if ((stop ? *stop : 0) != 0 || d.nk < 0) return;
@@ -540,9 +544,14 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
 #pragma unroll
     for (int i = 0; i < TPT; ++i)
         if (t + i * T < ntab) tv[i] = ptab[t + i * T];
+    const bool own = t < d.nrows;
     const int r = d.row0 + min(t, d.nrows - 1);
-    const int32_t rs = rai[r], re = rai[r + 1];
-    const int p = pid[r];
+    const int p = min((int)pid[r], npat - 1);
+    int32_t rs = 0, n = 0;
+    if constexpr (!SCAN) {
+        rs = rai[r];
+        n = rai[r + 1] - rs;
+    }
     const double seed = op.seed(r);
     // the block's values: 16-B loads from an even start (2-entry tail pad)
     const int64_t kb = k0 & ~int64_t(1);
@@ -551,6 +560,19 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (k < k1) a2[it] = *reinterpret_cast<const f64x2 *>(aa + k);
+    }
+    int32_t pm = 0, excl = 0;
+    if constexpr (SCAN) {
+        pm = ptab[p];  // (the table is L2-resident)
+        n = own ? pm >> 16 : 0;
+        int32_t inc = n;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t v = __shfl_up(inc, o, 64);
+            if ((t & 63) >= o) inc += v;
+        }
+        excl = inc - n;
+        if ((t & 63) == 63) wsum[t >> 6] = inc;
     }
 #pragma unroll
     for (int i = 0; i < TPT; ++i)
@@ -565,10 +587,14 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     }
     __syncthreads();
     double dv[Op::kDots > 0 ? Op::kDots : 1] = {};
-    if (t < d.nrows) {
-        const int32_t pm = tab[min(p, npat - 1)];
-        const int32_t* off = tab + (pm & 0xffff);
-        const int32_t n = re - rs;  // == the pattern's length
+    if constexpr (SCAN) {
+        for (int w = 0; w < (t >> 6); ++w) excl += wsum[w];
+        rs = (int32_t)k0 + excl;
+    } else {
+        pm = tab[p];
+    }
+    if (own) {
+        const int32_t *off = tab + (pm & 0xffff);
         const double *ar = av + (rs - k0);
         double s = seed;
         for (int32_t j0 = 0; j0 < n; j0 += 8) {
@@ -1599,15 +1625,18 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // Row patterns (Plan::d_pid; geometry 6, full-row lists, short rows)
     if constexpr (T == 512 && CAP == 4094 && RPT == 1) {
         if (P.d_pid && !L.ridx) {
-            if (add)
-                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, OpMult<true>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks,
-                                   L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
-                                   OpMult<true>{x, z, y, dpart != nullptr}, dpart, stop);
-            else
-                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, OpMult<false>>), dim3(P.n_blocks), dim3(T), 0, s,
-                                   P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
-                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop);
-            return;
+#define AIJHIP_PT(ADD, SC)                                                                                   \
+    hipLaunchKernelGGL((k_spmv_pattern<T, CAP, SC, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, \
+                       L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,                                     \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop);                                    \
+    return
+            if (add) {
+                if (P.pat_ai) { AIJHIP_PT(true, false); }
+                AIJHIP_PT(true, true);
+            }
+            if (P.pat_ai) { AIJHIP_PT(false, false); }
+            AIJHIP_PT(false, true);
+#undef AIJHIP_PT
         }
     }
     // Column codes (Plan::d_code; geometry 6, full-row lists): MatMult,
@@ -1760,8 +1789,8 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
     if (P.d_pid && P.tune.geom == 6) {  // row patterns (planned at geometry 6)
-        hipLaunchKernelGGL((k_spmv_pattern<512, 4094, Op>), dim3(P.n_blocks), dim3(512), 0, s, P.d_blocks, A.d_ai,
-                           P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop);
+        hipLaunchKernelGGL((k_spmv_pattern<512, 4094, false, Op>), dim3(P.n_blocks), dim3(512), 0, s, P.d_blocks,
+                           A.d_ai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop);
         return hipGetLastError();
     }
     if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)

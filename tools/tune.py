@@ -13,6 +13,7 @@ import argparse
 import importlib
 import itertools
 import json
+import os
 import sys
 import time
 from pathlib import Path
@@ -145,6 +146,10 @@ def main():
     if args.variants == "layouts":  # the automatic layout (row patterns / codes) against codes and aj
         for rp, cc, nt in ((-1, -1, 0), (0, 1, 0), (0, 0, 0), (1, 0, 1)):
             variants.append(("stream", dict(geometry=6, gather_sort=0, row_patterns=rp, column_codes=cc, nt_loads=nt)))
+    if args.variants == "patai":  # row patterns: row starts from the lengths' scan vs from ai
+        for ai_ in ("0", "1"):
+            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_AI": ai_})))
+        variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_PAT_AI": "0"})))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
@@ -175,6 +180,8 @@ def main():
                      ("merge", {}), ("scalar", {})]
 
     def configure(kind, opts):
+        for k, v in opts.get("env", {}).items():  # read by the planner (the set_option calls below re-plan)
+            os.environ[k] = v
         A.set_kernel(kind, opts.get("lanes", 0))
         A.set_option("geometry", opts.get("geometry", -1))  # -1: the library's choice
         A.set_option("exact", opts.get("exact", 0))
