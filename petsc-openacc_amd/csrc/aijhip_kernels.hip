@@ -525,7 +525,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // SCAN: the rows' starts are the block's k0 plus the prefix sums of their
 // patterns' lengths (a wave scan and the wave totals through LDS), so ai is
 // not read at all; otherwise from ai (A/B).
-template <int T, int CAP, bool SCAN, class Op>
+template <int T, int CAP, bool SCAN, class Op, bool NT = false>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if (k < k1) a2[it] = *reinterpret_cast<const f64x2 *>(aa + k);
+        if (k < k1) a2[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
     }
     int32_t pm = 0, excl = 0;
     if constexpr (SCAN) {
@@ -1633,6 +1633,12 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
             if (add) {
                 if (P.pat_ai) { AIJHIP_PT(true, false); }
                 AIJHIP_PT(true, true);
+            }
+            if (P.pat_ai && P.tune.nt == 1) {  // A/B: non-temporal aa loads
+                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, true>), dim3(P.n_blocks), dim3(T), 0,
+                                   s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
+                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop);
+                return;
             }
             if (P.pat_ai) { AIJHIP_PT(false, false); }
             AIJHIP_PT(false, true);

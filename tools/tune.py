@@ -146,6 +146,9 @@ def main():
     if args.variants == "layouts":  # the automatic layout (row patterns / codes) against codes and aj
         for rp, cc, nt in ((-1, -1, 0), (0, 1, 0), (0, 0, 0), (1, 0, 1)):
             variants.append(("stream", dict(geometry=6, gather_sort=0, row_patterns=rp, column_codes=cc, nt_loads=nt)))
+    if args.variants == "patnt":  # row patterns: plain vs non-temporal aa loads
+        for nt in (0, 1, 0, 1):
+            variants.append(("stream", dict(row_patterns=1, nt_loads=nt)))
     if args.variants == "patai":  # row patterns: row starts from the lengths' scan vs from ai
         for ai_ in ("0", "1"):
             variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_AI": ai_})))
