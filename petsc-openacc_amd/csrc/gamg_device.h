@@ -38,8 +38,7 @@ hipError_t dalloc(T **p, int64_t count) {
     return e;
 }
 
-// The set-up's process-wide streams (device, slot 0: the phase-1 sweep, 1: S
-// downloads, 2: the emax power iteration), non-blocking, created on first
+// The set-up's process-wide streams (device, slot 0 or 1), created on first
 // use and kept.
 hipStream_t setup_stream(int device, int slot);
 

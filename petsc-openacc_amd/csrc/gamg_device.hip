@@ -427,55 +427,6 @@ __global__ void k_div(int32_t m, const double *w, double nw, double *v) {
     if (i < m) v[i] = w[i] / nw;
 }
 
-// The power iteration on its own stream, without host round trips: the
-// blocked dot's partials summed left to right on the device (one wavefront
-// streams them; the adds stay sequential, as the host's loop), then the
-// norm's square root, the stop test and the division read device scalars.
-struct EmaxDev {
-    double nv, nw, emax;
-    int stop;
-};
-
-// mode 0: the start vector's norm (nv); mode 1: an iteration's (nw, emax,
-// stop once a norm is not positive: the host loop's break)
-__global__ __launch_bounds__(64) void k_seq_norm(int64_t nb, const double *__restrict__ part, EmaxDev *st, int mode) {
-    const int lane = threadIdx.x;
-    double s = 0.0;
-    double v = lane < nb ? part[lane] : 0.0;
-    for (int64_t c = 0; c < nb; c += 64) {
-        const double nxt = c + 64 + lane < nb ? part[c + 64 + lane] : 0.0;  // the next chunk in flight
-        const int n = (int)min((int64_t)64, nb - c);
-        const long long bits = __double_as_longlong(v);
-        const int lo = (int)bits, hi = (int)(bits >> 32);
-        for (int j = 0; j < n; ++j) {
-            const unsigned l = (unsigned)__builtin_amdgcn_readlane(lo, j);
-            const long long h = (long long)__builtin_amdgcn_readlane(hi, j);
-            s += __longlong_as_double((h << 32) | (long long)l);
-        }
-        v = nxt;
-    }
-    if (lane != 0) return;
-    const double r = sqrt(s);
-    if (mode == 0) {
-        st->nv = r;
-    } else if (!st->stop) {
-        if (!(r > 0.0)) {
-            st->stop = 1;
-        } else {
-            st->nw = r;
-            st->emax = r;
-        }
-    }
-}
-
-// mode 0: v = w / nv; mode 1: v = w / nw unless stopped
-__global__ void k_div_dev(int32_t m, const double *w, const EmaxDev *st, int mode, double *v) {
-    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (mode == 1 && st->stop) return;
-    const double d = mode == 0 ? st->nv : st->nw;
-    if (i < m) v[i] = w[i] / d;
-}
-
 __global__ void k_fill(int32_t m, double v, double *x) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) x[i] = v;
@@ -1585,7 +1536,6 @@ hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B,
     return e;
 }
 
-
 double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vector<double> &h_part, hipError_t *e) {
     const int64_t nb = (n + kDotBlock - 1) / kDotBlock;
     if (nb > 0) hipLaunchKernelGGL(k_block_dot, dim3(blocks_for(nb, 64)), dim3(64), 0, nullptr, n, d_v, d_part);
@@ -1643,27 +1593,7 @@ struct EmaxJob {
     double emax = 1.0;
     hipError_t e = hipSuccess;
     double *v = nullptr, *w = nullptr, *part = nullptr;
-    EmaxDev *st = nullptr;
-    hipEvent_t ready = nullptr;
-    // Two forms, the same bits. Levels whose blocked dot has at most
-    // kEmaxDeviceSum partials (level 1 and below at 300^3) run on a set-up
-    // stream of their own (slot 2), after the caller's null-stream work so
-    // far (A and dinv), with the partials summed on the device and one
-    // 32-byte read at the end: their per-iteration downloads queued behind the
-    // level's S downloads (level 1 at 300^3: 27 -> 8 ms). Larger levels sum
-    // on the host, one iteration at a time on the null stream: the device
-    // sum of 105 K partials is a serial chain (~1 ms a norm), and a queue of
-    // its iterations slowed the concurrent phase-1 sweep and the allocations
-    // that synchronise the device (level 0: 46 -> 70 ms measured).
-    static constexpr int64_t kEmaxDeviceSum = 16384;
     void start(const aijhip_mat &A, const double *dinv, int its) {
-        if ((A.m + kDotBlock - 1) / kDotBlock > kEmaxDeviceSum) {
-            start_host(A, dinv, its);
-            return;
-        }
-        if ((e = hipEventCreateWithFlags(&ready, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventRecord(ready, nullptr)) != hipSuccess)
-            return;
         th = std::thread([this, &A, dinv, its] {
             const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
             auto c0 = std::chrono::steady_clock::now();
@@ -1671,54 +1601,6 @@ struct EmaxJob {
                 if (!log) return;
                 const auto now = std::chrono::steady_clock::now();
                 std::fprintf(stderr, "  emax job %-12s %8.3f ms\n", what,
-                             std::chrono::duration<double, std::milli>(now - c0).count());
-                c0 = now;
-            };
-            (void)hipSetDevice(A.device);
-            const int32_t m = A.m;
-            const unsigned g256 = blocks_for(m, 256);
-            const int64_t nb = (m + kDotBlock - 1) / kDotBlock;
-            hipStream_t es = aijhip_gamg::setup_stream(A.device, 2);
-            if (!es) {
-                e = hipErrorOutOfMemory;
-                return;
-            }
-            const EmaxDev init{0.0, 0.0, 1.0, 0};
-            if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
-                (e = dalloc(&part, nb)) != hipSuccess || (e = dalloc(&st, 1)) != hipSuccess ||
-                (e = hipStreamWaitEvent(es, ready, 0)) != hipSuccess ||
-                (e = hipMemcpyAsync(st, &init, sizeof(init), hipMemcpyHostToDevice, es)) != hipSuccess)
-                return;
-            mark("alloc");
-            hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, es, m, v);
-            if (nb > 0) {
-                hipLaunchKernelGGL(k_block_dot, dim3(blocks_for(nb, 64)), dim3(64), 0, es, (int64_t)m, v, part);
-                hipLaunchKernelGGL(k_seq_norm, dim3(1), dim3(64), 0, es, nb, part, st, 0);
-                hipLaunchKernelGGL(k_div_dev, dim3(g256), dim3(256), 0, es, m, v, st, 0, v);
-            }
-            for (int it = 0; it < its && nb > 0; ++it) {
-                if ((e = aijhip::launch_dinv_mult(A, dinv, v, w, es)) != hipSuccess) return;
-                hipLaunchKernelGGL(k_block_dot, dim3(blocks_for(nb, 64)), dim3(64), 0, es, (int64_t)m, w, part);
-                hipLaunchKernelGGL(k_seq_norm, dim3(1), dim3(64), 0, es, nb, part, st, 1);
-                hipLaunchKernelGGL(k_div_dev, dim3(g256), dim3(256), 0, es, m, w, st, 1, v);
-            }
-            EmaxDev out = init;
-            if ((e = hipGetLastError()) != hipSuccess ||
-                (e = hipMemcpyAsync(&out, st, sizeof(out), hipMemcpyDeviceToHost, es)) != hipSuccess ||
-                (e = hipStreamSynchronize(es)) != hipSuccess)
-                return;
-            emax = out.emax;
-            mark("iterations");
-        });
-    }
-    void start_host(const aijhip_mat &A, const double *dinv, int its) {
-        th = std::thread([this, &A, dinv, its] {
-            const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
-            auto c0 = std::chrono::steady_clock::now();
-            auto mark = [&](const char *what) {
-                if (!log) return;
-                const auto now = std::chrono::steady_clock::now();
-                std::fprintf(stderr, "  emax job %-12s %8.3f ms (host sums)\n", what,
                              std::chrono::duration<double, std::milli>(now - c0).count());
                 c0 = now;
             };
@@ -1733,11 +1615,13 @@ struct EmaxJob {
             hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, nullptr, m, v);
             const double nv = host_blocked_norm(v, m, part, h_part, &e);
             if (e != hipSuccess) return;
+            mark("start");
             hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, v, nv, v);
             for (int it = 0; it < its; ++it) {
                 if ((e = aijhip::launch_dinv_mult(A, dinv, v, w, nullptr)) != hipSuccess) return;
                 const double nw = host_blocked_norm(w, m, part, h_part, &e);
                 if (e != hipSuccess) return;
+                if (it == 0) mark("iteration 0");
                 if (!(nw > 0.0)) break;
                 emax = nw;
                 hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, w, nw, v);
@@ -1749,11 +1633,8 @@ struct EmaxJob {
         if (th.joinable()) th.join();
     }
     void release() {
-        hipFree(v); hipFree(w); hipFree(part); hipFree(st);
+        hipFree(v); hipFree(w); hipFree(part);
         v = w = part = nullptr;
-        st = nullptr;
-        if (ready) (void)hipEventDestroy(ready);
-        ready = nullptr;
     }
     ~EmaxJob() {
         join();
@@ -1839,7 +1720,7 @@ hipStream_t setup_stream(int device, int slot) {
     static std::mutex mu;
     static std::vector<hipStream_t> *cache = new std::vector<hipStream_t>();
     std::lock_guard<std::mutex> g(mu);
-    const size_t k = (size_t)device * 3 + (size_t)(slot % 3);  // slots: sweep, S downloads, emax job
+    const size_t k = (size_t)device * 2 + (size_t)(slot & 1);
     if (cache->size() <= k) cache->resize(k + 1, nullptr);
     if (!(*cache)[k]) {
         int cur = 0;
