@@ -139,6 +139,12 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
                std::vector<BlockDesc> &blocks, std::vector<LongSeg> &segs, std::vector<LongRow> &longs) {
     using namespace aijhip;
     const auto &rai = A->h_rai;
+    // segment length: kLongSegNnz; AIJHIP_LONG_SEG=n for A/B (tools/tune.py longseg)
+    static const int64_t seg_nnz = [] {
+        const char *v = std::getenv("AIJHIP_LONG_SEG");
+        const int64_t n = v ? std::atoll(v) : 0;
+        return n >= 256 && n <= (1 << 20) ? n : (int64_t)kLongSegNnz;
+    }();
     int32_t r = r0;
     while (r < r1) {
         const int32_t len = rai[r + 1] - rai[r];
@@ -146,8 +152,8 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
             LongRow lr{};
             lr.orow = h_ridx ? h_ridx[r] : r;
             lr.seg0 = (int32_t)segs.size();
-            for (int64_t k = rai[r]; k < rai[r + 1]; k += kLongSegNnz) {
-                const int64_t nk = std::min<int64_t>(kLongSegNnz, rai[r + 1] - k);
+            for (int64_t k = rai[r]; k < rai[r + 1]; k += seg_nnz) {
+                const int64_t nk = std::min<int64_t>(seg_nnz, rai[r + 1] - k);
                 segs.push_back(LongSeg{(int32_t)k, (int32_t)nk});
             }
             lr.nseg = (int32_t)segs.size() - lr.seg0;
