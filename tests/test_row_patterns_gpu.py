@@ -54,9 +54,11 @@ def test_poisson_patterns_bitwise(pkg, dev, coracle, dims):
     ai, aj, aa = pkg.poisson_csr(*dims)
     m = len(ai) - 1
     x, z = pkg.splitmix_uniform(m, 42), pkg.splitmix_uniform(m, 7)
+    rows = np.repeat(np.arange(m), np.diff(ai))
+    lists = {tuple(aj[ai[i]:ai[i + 1]] - rows[ai[i]:ai[i + 1]]) for i in range(m)}  # the distinct offset lists
     with pkg.SeqAIJHIP(ai, aj, aa) as A:
         info = A.info()
-        assert 0 < info["row_patterns"] <= 256 and info["column_codes"] == 0
+        assert info["row_patterns"] == len(lists) and info["column_codes"] == 0
         y1, w1 = products(A, x, z, dev)
         assert_bits(y1, coracle.matmult(ai, aj, aa, x, omp=True))
         A.set_option("row_patterns", 0)
