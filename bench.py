@@ -398,7 +398,9 @@ def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm):
     return {"workload": f"{G}^3 Poisson CSR row-partitioned over {world} GPUs "
                         f"({z1 - z0} of {G} z-planes on rank {rank})",
             "scaling": "strong", "value": round(nbytes / dt / 1e9, 2), "unit": "GB/s",
-            "roofline_frac": round(nbytes / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
+            # SURVEY §8d's CSR bytes over N HBM peaks: an effective fraction,
+            # above 1 when the ranks' diagonal blocks read row patterns
+            "csr_effective_frac": round(nbytes / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
             "ms_per_step": round(dt * 1e3, 4), "rows": G ** 3, "nnz": nnz, "halo": args.halo}
 
 
@@ -788,8 +790,8 @@ def main():
                 "stream_shape_read": {"GBs": ceiling[1][0], "us": ceiling[1][1],
                                       "frac": round(achieved / ceiling[1][0], 4),
                                       "probe": "mode 1: plain loads, four per lane (the STREAM kernel's shape)"}}
-        if distributed:  # whole-job rate against N HBM peaks (roofline.frac is rank 0's kernel alone)
-            out["aggregate_roofline_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
+        if distributed:  # whole-job CSR-effective rate against N HBM peaks (roofline.frac: rank 0's kernel alone)
+            out["aggregate_csr_effective_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
             out["distributed"] = distributed_block(world, dist.get_backend(), comm.info(), args.comm_timeout, ranks)
         if args.rehearse_one_gpu:
             out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
