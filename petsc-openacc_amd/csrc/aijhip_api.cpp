@@ -13,6 +13,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -171,6 +173,27 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
         }
         blocks.push_back(BlockDesc{start, r - start, rai[start], nk});
     }
+}
+
+// XCD placement of the row-pattern launch. Blocks are dealt round-robin over
+// the 8 XCDs, so a block's +-1 / +-N in-plane x window reaches into blocks
+// run by other XCDs: at 300^3 each x line is fetched into ~2.2 of the 8 L2s
+// (PMC: 2.36 GB per launch against 2.07 GB). Chunks of C consecutive blocks
+// per XCD, with 8·C blocks spanning the plane distance dmax (so the +-dmax
+// reads of a line land in the same XCD's chunk), keep the in-plane window
+// on one XCD except at chunk edges. AIJHIP_PAT_XCHUNK: "auto" (C from dmax
+// and the mean rows per block, 0 when no C fits within 1/8 of a chunk),
+// -1 contiguous runs, C > 0 a fixed chunk, 0 hardware order; unset: "auto"
+// when kPatXchunkAuto, else hardware order.
+constexpr bool kPatXchunkAuto = false;
+static int32_t pattern_xchunk(const aijhip::Plan &P, int32_t nrows) {
+    const char *env = std::getenv("AIJHIP_PAT_XCHUNK");
+    if (env && std::strcmp(env, "auto") != 0) return (int32_t)std::strtol(env, nullptr, 10);
+    if ((!env && !kPatXchunkAuto) || P.n_blocks <= 0 || P.pat_dmax <= 0) return 0;
+    const double rpb = (double)nrows / P.n_blocks;
+    const int64_t c = std::llround(P.pat_dmax / (8.0 * rpb));
+    if (c < 1 || 8 * c > P.n_blocks) return 0;
+    return std::fabs(8.0 * c * rpb - P.pat_dmax) <= 0.125 * c * rpb ? (int32_t)c : 0;
 }
 
 int plan_stream(aijhip_mat *A) {
@@ -373,6 +396,7 @@ int plan_stream(aijhip_mat *A) {
         // on the pattern id and the table, where ai's loads were in flight)
         const char *pa = std::getenv("AIJHIP_PAT_AI");
         P.pat_ai = !(pa && pa[0] == '0');
+        P.pat_xchunk = ok ? pattern_xchunk(P, nrl) : 0;
     }
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
     // for the row blocks whose offset dictionaries fit (geometry 6 — 7 and 9

@@ -529,13 +529,16 @@ template <int T, int CAP, bool SCAN, class Op, bool NT = false>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
-                                                    double *dpart, const int *stop) {
+                                                    double *dpart, const int *stop, int xchunk = 0) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int TPT = (kPatTableMax + T - 1) / T;
     __shared__ double av[CAP];
     __shared__ int32_t tab[kPatTableMax];
     __shared__ int32_t wsum[T / 64];
-    const int b = (int)blockIdx.x;
+    // xchunk (Plan::pat_xchunk): the XCD placement of the row blocks — a
+    // bijection, so the dot partials keep their logical slots and order
+    const int b = xchunk == 0 ? (int)blockIdx.x
+                              : xcd_chunk_remap((int)blockIdx.x, (int)gridDim.x, xchunk < 0 ? 0 : xchunk);
     const BlockDesc d = blk[b];
     if ((stop ? *stop : 0) != 0 || d.nk < 0) return;
     const int t = threadIdx.x;
@@ -1471,10 +1474,16 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
     std::vector<int32_t> off((size_t)npat * kPatTableMax);
     if ((e = hipMemcpy(off.data(), d_off, sizeof(int32_t) * off.size(), hipMemcpyDeviceToHost)) != hipSuccess)
         return done(e);
+    int32_t dmax = 0;
     for (int p = 0; p < npat; ++p) {
         tab[p] = (int32_t)tab.size() | (len[p] << 16);
-        for (int j = 0; j < len[p]; ++j) tab.push_back(off[(size_t)p * kPatTableMax + j]);
+        for (int j = 0; j < len[p]; ++j) {
+            const int32_t o = off[(size_t)p * kPatTableMax + j];
+            tab.push_back(o);
+            dmax = std::max(dmax, o < 0 ? -o : o);
+        }
     }
+    P.pat_dmax = dmax;
     if ((e = hipMalloc(&P.d_ptab, sizeof(int32_t) * tab.size())) != hipSuccess ||
         (e = hipMemcpy(P.d_ptab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return done(e);
@@ -1628,7 +1637,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
 #define AIJHIP_PT(ADD, SC)                                                                                   \
     hipLaunchKernelGGL((k_spmv_pattern<T, CAP, SC, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, \
                        L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,                                     \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop);                                    \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);                      \
     return
             if (add) {
                 if (P.pat_ai) { AIJHIP_PT(true, false); }
@@ -1637,7 +1646,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
             if (P.pat_ai && P.tune.nt == 1) {  // A/B: non-temporal aa loads
                 hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, true>), dim3(P.n_blocks), dim3(T), 0,
                                    s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
-                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop);
+                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);
                 return;
             }
             if (P.pat_ai) { AIJHIP_PT(false, false); }
@@ -1796,7 +1805,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
     if (P.d_pid && P.tune.geom == 6) {  // row patterns (planned at geometry 6)
         hipLaunchKernelGGL((k_spmv_pattern<512, 4094, false, Op>), dim3(P.n_blocks), dim3(512), 0, s, P.d_blocks,
-                           A.d_ai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop);
+                           A.d_ai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop, P.pat_xchunk);
         return hipGetLastError();
     }
     if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)

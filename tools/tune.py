@@ -153,6 +153,9 @@ def main():
         for ai_ in ("0", "1"):
             variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_AI": ai_})))
         variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_PAT_AI": "0"})))
+    if args.variants == "patxcd":  # row patterns: XCD placement of the blocks (AIJHIP_PAT_XCHUNK)
+        for xc in ("0", "auto", "-1", "11", "44", "0", "auto"):
+            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_XCHUNK": xc})))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
