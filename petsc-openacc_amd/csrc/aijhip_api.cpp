@@ -385,7 +385,7 @@ int plan_stream(aijhip_mat *A) {
     // for short-row operands whose rows follow few offset lists (stencils);
     // geometry 6, plain full-row launches, no long rows
     const int32_t nrl = rai.empty() ? 0 : (int32_t)rai.size() - 1;
-    if (P.tune.patterns > 0 && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed &&
+    if (P.tune.patterns > 0 && (P.tune.geom == 6 || P.tune.geom == 7 || P.tune.geom == 8) && !blocks.empty() && longs.empty() && !A->compressed &&
         A->nz <= (int64_t)kBatchMinMean * nrl && P.d_xrange == nullptr && P.n_gblocks == 0 && P.d_sslot == nullptr &&
         P.tune.persist == 0 && !P.tune.clamped && !P.tune.xcd) {
         bool ok = false;
@@ -397,6 +397,8 @@ int plan_stream(aijhip_mat *A) {
         const char *pa = std::getenv("AIJHIP_PAT_AI");
         P.pat_ai = !(pa && pa[0] == '0');
         P.pat_xchunk = ok ? pattern_xchunk(P, nrl) : 0;
+        const char *pp = std::getenv("AIJHIP_PAT_PIPE");
+        P.pat_pipe = pp && pp[0] == '1';
     }
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
     // for the row blocks whose offset dictionaries fit (geometry 6 — 7 and 9

@@ -620,6 +620,107 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     }
 }
 
+// Row patterns, persistent and software-pipelined (A/B, AIJHIP_PAT_PIPE=1;
+// MatMult only): a resident grid walks the row blocks b, b + grid, ...; each
+// lane issues its row's x gathers of the current block, THEN the aa loads of
+// the next block (vmcnt completes in issue order, so the sums wait on the
+// gathers only), so a workgroup keeps matrix bytes in flight through its
+// gather phase instead of draining at every block. Same per-row arithmetic
+// and order as k_spmv_pattern (bit-identical).
+template <int T, int CAP>
+__global__ __launch_bounds__(T) void k_spmv_pattern_pipe(const BlockDesc *__restrict__ blk, int nblk,
+                                                         const int32_t *__restrict__ rai,
+                                                         const uint8_t *__restrict__ pid,
+                                                         const int32_t *__restrict__ ptab, int ntab, int npat,
+                                                         const double *__restrict__ aa,
+                                                         const double *__restrict__ x, double *__restrict__ y) {
+    constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
+    constexpr int TPT = (kPatTableMax + T - 1) / T;
+    __shared__ double av[CAP];
+    __shared__ int32_t tab[kPatTableMax];
+    const int t = threadIdx.x;
+    int b = (int)blockIdx.x;
+    if (b >= nblk) return;  // uniform per workgroup
+#pragma unroll
+    for (int i = 0; i < TPT; ++i)
+        if (t + i * T < ntab) tab[t + i * T] = ptab[t + i * T];
+    BlockDesc d = blk[b];
+    f64x2 a2[ITERS];
+    int64_t kb = d.k0 & ~int64_t(1);
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+        const int64_t k = kb + 2 * (int64_t)(t + it * T);
+        if (k < (int64_t)d.k0 + d.nk) a2[it] = ld_stream<false>(reinterpret_cast<const f64x2 *>(aa + k));
+    }
+    int r = d.row0 + min(t, d.nrows - 1);
+    int p = min((int)pid[r], npat - 1);
+    int32_t rs = rai[r], n = rai[r + 1] - rs;
+    for (;;) {
+        const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int64_t k = kb + 2 * (int64_t)(t + it * T);
+            if (k < k1) {
+                if (k >= k0) av[k - k0] = a2[it].x;
+                if (k + 1 < k1) av[k + 1 - k0] = a2[it].y;
+            }
+        }
+        const int bn = b + (int)gridDim.x;
+        const bool more = bn < nblk;
+        BlockDesc dn = d;
+        if (more) dn = blk[bn];
+        __syncthreads();
+        const bool own = t < d.nrows && d.nk >= 0;
+        const int32_t pm = tab[p];
+        const int32_t *off = tab + (pm & 0xffff);
+        const double *ar = av + (rs - k0);
+        const int32_t n0 = own ? min(n, 8) : 0;
+        double xv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (j < n0) xv[j] = x[r + off[j]];
+        // the next block's loads, behind the gathers
+        int rn = r, pn = p;
+        int32_t rsn = rs, nn = n;
+        if (more) {
+            kb = dn.k0 & ~int64_t(1);
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) {
+                const int64_t k = kb + 2 * (int64_t)(t + it * T);
+                if (k < (int64_t)dn.k0 + dn.nk) a2[it] = ld_stream<false>(reinterpret_cast<const f64x2 *>(aa + k));
+            }
+            rn = dn.row0 + min(t, dn.nrows - 1);
+            pn = min((int)pid[rn], npat - 1);
+            rsn = rai[rn];
+            nn = rai[rn + 1] - rsn;
+        }
+        if (own) {
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j < n0) s += ar[j] * xv[j];
+            for (int32_t j0 = 8; j0 < n; j0 += 8) {
+                double xw[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j0 + j < n) xw[j] = x[r + off[j0 + j]];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j0 + j < n) s += ar[j0 + j] * xw[j];
+            }
+            st_stream(y + r, s);
+        }
+        __syncthreads();  // av is rewritten next
+        if (!more) break;
+        b = bn;
+        d = dn;
+        r = rn;
+        p = pn;
+        rs = rsn;
+        n = nn;
+    }
+}
+
 // Persistent, software-pipelined STREAM: a resident grid walks the row blocks
 // round-robin (b, b + grid, ...). The aa/aj loads of the NEXT block are issued
 // before the barrier and stay in flight while the lanes reduce the current
@@ -1632,7 +1733,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                        OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, nullptr); \
     return
     // Row patterns (Plan::d_pid; geometry 6, full-row lists, short rows)
-    if constexpr (T == 512 && CAP == 4094 && RPT == 1) {
+    if constexpr (RPT == 1 && ((T == 512 && CAP == 4094) || (T == 256 && CAP == 2046) || (T == 1024 && CAP == 8190))) {
         if (P.d_pid && !L.ridx) {
 #define AIJHIP_PT(ADD, SC)                                                                                   \
     hipLaunchKernelGGL((k_spmv_pattern<T, CAP, SC, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, \
@@ -1642,6 +1743,22 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
             if (add) {
                 if (P.pat_ai) { AIJHIP_PT(true, false); }
                 AIJHIP_PT(true, true);
+            }
+            if constexpr (T == 512 && CAP == 4094) {
+                if (P.pat_ai && P.pat_pipe && !dpart && !stop) {  // A/B: persistent, pipelined
+                    static int grid = 0;
+                    if (grid == 0) {
+                        int dev = 0, cus = 0, occ = 0;
+                        (void)hipGetDevice(&dev);
+                        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+                        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_spmv_pattern_pipe<T, CAP>, T, 0);
+                        grid = std::max(1, cus * std::max(1, occ));
+                    }
+                    const int g = std::min(grid, (int)P.n_blocks);
+                    hipLaunchKernelGGL((k_spmv_pattern_pipe<T, CAP>), dim3(g), dim3(T), 0, s, P.d_blocks, P.n_blocks,
+                                       L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, x, y);
+                    return;
+                }
             }
             if (P.pat_ai && P.tune.nt == 1) {  // A/B: non-temporal aa loads
                 hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, true>), dim3(P.n_blocks), dim3(T), 0,
@@ -1803,9 +1920,16 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
-    if (P.d_pid && P.tune.geom == 6) {  // row patterns (planned at geometry 6)
-        hipLaunchKernelGGL((k_spmv_pattern<512, 4094, false, Op>), dim3(P.n_blocks), dim3(512), 0, s, P.d_blocks,
-                           A.d_ai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop, P.pat_xchunk);
+    if (P.d_pid) {  // row patterns (planned at geometry 6; 7 and 8 for A/B)
+#define AIJHIP_PO(G)                                                                                        \
+    hipLaunchKernelGGL((k_spmv_pattern<kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap, false, Op>),       \
+                       dim3(P.n_blocks), dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, A.d_ai, P.d_pid,   \
+                       P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop, P.pat_xchunk)
+        if (P.tune.geom == 6) AIJHIP_PO(6);
+        else if (P.tune.geom == 7) AIJHIP_PO(7);
+        else if (P.tune.geom == 8) AIJHIP_PO(8);
+        else return hipErrorInvalidValue;
+#undef AIJHIP_PO
         return hipGetLastError();
     }
     if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)

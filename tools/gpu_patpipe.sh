@@ -1,0 +1,12 @@
+#!/bin/bash
+# Row patterns: persistent pipelined MatMult A/B (AIJHIP_PAT_PIPE) at 300^3.
+#   usage: tools/gpu_patpipe.sh TAG
+set -o pipefail
+TAG=${1:-patpipe}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT" || exit 1
+export TMPDIR=/tmp
+timeout -k 10 400 python -u tools/tune.py --variants patpipe --rounds 5 --launches 20 > "$OUT/tune_poisson.jsonl" 2>&1 || { tail -5 "$OUT/tune_poisson.jsonl"; exit 1; }
+grep -E "us_median|bitwise" "$OUT/tune_poisson.jsonl"
