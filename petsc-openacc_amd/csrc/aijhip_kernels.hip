@@ -601,13 +601,20 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
         const double *ar = av + (rs - k0);
         double s = seed;
         for (int32_t j0 = 0; j0 < n; j0 += 8) {
-            double xv[8];
+            // branch-free: slots past the row's end repeat its last entry
+            // (loaded, not summed), so the 8 offset reads, the 8 gathers and
+            // the 8 value reads issue back to back under one wait each
+            const int32_t last = n - 1 - j0;
+            int32_t o[8];
+            double xv[8], av8[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j0 + j < n) xv[j] = op.gx(r + off[j0 + j]);
+            for (int j = 0; j < 8; ++j) o[j] = off[j0 + min(j, last)];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j0 + j < n) s += ar[j0 + j] * xv[j];
+            for (int j = 0; j < 8; ++j) xv[j] = op.gx(r + o[j]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) av8[j] = ar[j0 + min(j, last)];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s = j <= last ? s + av8[j] * xv[j] : s;
         }
         op.put(r, s, dv);
     }
@@ -674,50 +681,60 @@ __global__ __launch_bounds__(T) void k_spmv_pattern_pipe(const BlockDesc *__rest
         const int32_t pm = tab[p];
         const int32_t *off = tab + (pm & 0xffff);
         const double *ar = av + (rs - k0);
-        const int32_t n0 = own ? min(n, 8) : 0;
+        __builtin_assume(n >= 1);  // launched only when no pattern is empty (Plan::pat_minlen)
+        const int32_t l0 = min(n, 8) - 1;  // branch-free as in k_spmv_pattern
+        int32_t o[8];
         double xv[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-            if (j < n0) xv[j] = x[r + off[j]];
-        // the next block's loads, behind the gathers
-        int rn = r, pn = p;
-        int32_t rsn = rs, nn = n;
-        if (more) {
+        for (int j = 0; j < 8; ++j) o[j] = off[max(min(j, l0), 0)];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xv[j] = x[r + o[j]];
+        __builtin_amdgcn_sched_barrier(0);  // the next block's loads stay behind the gathers
+        {  // unpredicated (past the block's end: its first pair again), so the
+           // compiler's wait counts know these loads follow the gathers
             kb = dn.k0 & ~int64_t(1);
+            const int64_t k1n = more ? (int64_t)dn.k0 + dn.nk : 0;
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) {
                 const int64_t k = kb + 2 * (int64_t)(t + it * T);
-                if (k < (int64_t)dn.k0 + dn.nk) a2[it] = ld_stream<false>(reinterpret_cast<const f64x2 *>(aa + k));
+                a2[it] = ld_stream<false>(reinterpret_cast<const f64x2 *>(aa + (k < k1n ? k : kb)));
             }
-            rn = dn.row0 + min(t, dn.nrows - 1);
-            pn = min((int)pid[rn], npat - 1);
-            rsn = rai[rn];
-            nn = rai[rn + 1] - rsn;
         }
-        if (own) {
+        // the next rows' id and starts, raw (used after the barrier below)
+        const int rn = dn.row0 + min(t, dn.nrows - 1);
+        const int pidn = pid[rn];
+        const int32_t ra0 = rai[rn], ra1 = rai[rn + 1];
+        __builtin_amdgcn_sched_barrier(0);
+        {  // every lane sums (the gathers stay unpredicated); owners store
             double s = 0.0;
+            double av8[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                if (j < n0) s += ar[j] * xv[j];
+            for (int j = 0; j < 8; ++j) av8[j] = ar[max(min(j, l0), 0)];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) s += j <= l0 ? av8[j] * xv[j] : -0.0;  // s + -0.0 == s, bit for bit
             for (int32_t j0 = 8; j0 < n; j0 += 8) {
+                const int32_t last = n - 1 - j0;
+                int32_t ow[8];
                 double xw[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j0 + j < n) xw[j] = x[r + off[j0 + j]];
+                for (int j = 0; j < 8; ++j) ow[j] = off[j0 + min(j, last)];
 #pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j0 + j < n) s += ar[j0 + j] * xw[j];
+                for (int j = 0; j < 8; ++j) xw[j] = x[r + ow[j]];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) av8[j] = ar[j0 + min(j, last)];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) s += j <= last ? av8[j] * xw[j] : -0.0;
             }
-            st_stream(y + r, s);
+            if (own) st_stream(y + r, s);
         }
         __syncthreads();  // av is rewritten next
         if (!more) break;
         b = bn;
         d = dn;
         r = rn;
-        p = pn;
-        rs = rsn;
-        n = nn;
+        p = min(pidn, npat - 1);
+        rs = ra0;
+        n = ra1 - ra0;
     }
 }
 
@@ -1575,8 +1592,9 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
     std::vector<int32_t> off((size_t)npat * kPatTableMax);
     if ((e = hipMemcpy(off.data(), d_off, sizeof(int32_t) * off.size(), hipMemcpyDeviceToHost)) != hipSuccess)
         return done(e);
-    int32_t dmax = 0;
+    int32_t dmax = 0, minlen = INT32_MAX;
     for (int p = 0; p < npat; ++p) {
+        minlen = std::min(minlen, len[p]);
         tab[p] = (int32_t)tab.size() | (len[p] << 16);
         for (int j = 0; j < len[p]; ++j) {
             const int32_t o = off[(size_t)p * kPatTableMax + j];
@@ -1585,6 +1603,7 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
         }
     }
     P.pat_dmax = dmax;
+    P.pat_minlen = minlen;
     if ((e = hipMalloc(&P.d_ptab, sizeof(int32_t) * tab.size())) != hipSuccess ||
         (e = hipMemcpy(P.d_ptab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return done(e);
@@ -1745,7 +1764,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                 AIJHIP_PT(true, true);
             }
             if constexpr (T == 512 && CAP == 4094) {
-                if (P.pat_ai && P.pat_pipe && !dpart && !stop) {  // A/B: persistent, pipelined
+                if (P.pat_ai && P.pat_pipe && P.pat_minlen >= 1 && !dpart && !stop) {  // A/B: persistent, pipelined
                     static int grid = 0;
                     if (grid == 0) {
                         int dev = 0, cus = 0, occ = 0;
