@@ -214,9 +214,8 @@ struct Plan {
     int32_t *d_ptab = nullptr;
     int32_t n_ptab = 0, n_pat = 0;
     bool pat_ai = true;  // row starts from ai; AIJHIP_PAT_AI=0 at planning: from the lengths' scan (A/B)
-    int32_t pat_minlen = 0;  // shortest offset list (0: some rows are empty)
+    bool pat_bf = true;      // branch-free gathers; AIJHIP_PAT_BF=0 at planning: predicated (A/B)
     int32_t pat_dmax = 0;    // largest |column - row| offset in the table (the stencil's plane distance)
-    bool pat_pipe = false;   // AIJHIP_PAT_PIPE=1 at planning: persistent pipelined MatMult (A/B)
     int32_t pat_xchunk = 0;  // XCD chunk of the row-pattern launch: 0 hardware order, -1 contiguous, C > 0 chunked
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;

@@ -525,7 +525,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // SCAN: the rows' starts are the block's k0 plus the prefix sums of their
 // patterns' lengths (a wave scan and the wave totals through LDS), so ai is
 // not read at all; otherwise from ai (A/B).
-template <int T, int CAP, bool SCAN, class Op, bool NT = false>
+template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = true>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
@@ -600,6 +600,17 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
         const int32_t *off = tab + (pm & 0xffff);
         const double *ar = av + (rs - k0);
         double s = seed;
+        if constexpr (!BF) {  // A/B (AIJHIP_PAT_BF=0): the predicated form
+            for (int32_t j0 = 0; j0 < n; j0 += 8) {
+                double xv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j0 + j < n) xv[j] = op.gx(r + off[j0 + j]);
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j0 + j < n) s += ar[j0 + j] * xv[j];
+            }
+        } else
         for (int32_t j0 = 0; j0 < n; j0 += 8) {
             // branch-free: slots past the row's end repeat its last entry
             // (loaded, not summed), so the 8 offset reads, the 8 gathers and
@@ -624,117 +635,6 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
             const double v = block_sum<T>(dv[q], av);
             if (t == 0) dpart[(int64_t)q * gridDim.x + b] = v;
         }
-    }
-}
-
-// Row patterns, persistent and software-pipelined (A/B, AIJHIP_PAT_PIPE=1;
-// MatMult only): a resident grid walks the row blocks b, b + grid, ...; each
-// lane issues its row's x gathers of the current block, THEN the aa loads of
-// the next block (vmcnt completes in issue order, so the sums wait on the
-// gathers only), so a workgroup keeps matrix bytes in flight through its
-// gather phase instead of draining at every block. Same per-row arithmetic
-// and order as k_spmv_pattern (bit-identical).
-template <int T, int CAP>
-__global__ __launch_bounds__(T) void k_spmv_pattern_pipe(const BlockDesc *__restrict__ blk, int nblk,
-                                                         const int32_t *__restrict__ rai,
-                                                         const uint8_t *__restrict__ pid,
-                                                         const int32_t *__restrict__ ptab, int ntab, int npat,
-                                                         const double *__restrict__ aa,
-                                                         const double *__restrict__ x, double *__restrict__ y) {
-    constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
-    constexpr int TPT = (kPatTableMax + T - 1) / T;
-    __shared__ double av[CAP];
-    __shared__ int32_t tab[kPatTableMax];
-    const int t = threadIdx.x;
-    int b = (int)blockIdx.x;
-    if (b >= nblk) return;  // uniform per workgroup
-#pragma unroll
-    for (int i = 0; i < TPT; ++i)
-        if (t + i * T < ntab) tab[t + i * T] = ptab[t + i * T];
-    BlockDesc d = blk[b];
-    f64x2 a2[ITERS];
-    int64_t kb = d.k0 & ~int64_t(1);
-#pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-        const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if (k < (int64_t)d.k0 + d.nk) a2[it] = ld_stream<false>(reinterpret_cast<const f64x2 *>(aa + k));
-    }
-    int r = d.row0 + min(t, d.nrows - 1);
-    int p = min((int)pid[r], npat - 1);
-    int32_t rs = rai[r], n = rai[r + 1] - rs;
-    for (;;) {
-        const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            if (k < k1) {
-                if (k >= k0) av[k - k0] = a2[it].x;
-                if (k + 1 < k1) av[k + 1 - k0] = a2[it].y;
-            }
-        }
-        const int bn = b + (int)gridDim.x;
-        const bool more = bn < nblk;
-        BlockDesc dn = d;
-        if (more) dn = blk[bn];
-        __syncthreads();
-        const bool own = t < d.nrows && d.nk >= 0;
-        const int32_t pm = tab[p];
-        const int32_t *off = tab + (pm & 0xffff);
-        const double *ar = av + (rs - k0);
-        __builtin_assume(n >= 1);  // launched only when no pattern is empty (Plan::pat_minlen)
-        const int32_t l0 = min(n, 8) - 1;  // branch-free as in k_spmv_pattern
-        int32_t o[8];
-        double xv[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = off[max(min(j, l0), 0)];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[j] = x[r + o[j]];
-        __builtin_amdgcn_sched_barrier(0);  // the next block's loads stay behind the gathers
-        {  // unpredicated (past the block's end: its first pair again), so the
-           // compiler's wait counts know these loads follow the gathers
-            kb = dn.k0 & ~int64_t(1);
-            const int64_t k1n = more ? (int64_t)dn.k0 + dn.nk : 0;
-#pragma unroll
-            for (int it = 0; it < ITERS; ++it) {
-                const int64_t k = kb + 2 * (int64_t)(t + it * T);
-                a2[it] = ld_stream<false>(reinterpret_cast<const f64x2 *>(aa + (k < k1n ? k : kb)));
-            }
-        }
-        // the next rows' id and starts, raw (used after the barrier below)
-        const int rn = dn.row0 + min(t, dn.nrows - 1);
-        const int pidn = pid[rn];
-        const int32_t ra0 = rai[rn], ra1 = rai[rn + 1];
-        __builtin_amdgcn_sched_barrier(0);
-        {  // every lane sums (the gathers stay unpredicated); owners store
-            double s = 0.0;
-            double av8[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) av8[j] = ar[max(min(j, l0), 0)];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s += j <= l0 ? av8[j] * xv[j] : -0.0;  // s + -0.0 == s, bit for bit
-            for (int32_t j0 = 8; j0 < n; j0 += 8) {
-                const int32_t last = n - 1 - j0;
-                int32_t ow[8];
-                double xw[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) ow[j] = off[j0 + min(j, last)];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) xw[j] = x[r + ow[j]];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) av8[j] = ar[j0 + min(j, last)];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) s += j <= last ? av8[j] * xw[j] : -0.0;
-            }
-            if (own) st_stream(y + r, s);
-        }
-        __syncthreads();  // av is rewritten next
-        if (!more) break;
-        b = bn;
-        d = dn;
-        r = rn;
-        p = min(pidn, npat - 1);
-        rs = ra0;
-        n = ra1 - ra0;
     }
 }
 
@@ -1592,9 +1492,8 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
     std::vector<int32_t> off((size_t)npat * kPatTableMax);
     if ((e = hipMemcpy(off.data(), d_off, sizeof(int32_t) * off.size(), hipMemcpyDeviceToHost)) != hipSuccess)
         return done(e);
-    int32_t dmax = 0, minlen = INT32_MAX;
+    int32_t dmax = 0;
     for (int p = 0; p < npat; ++p) {
-        minlen = std::min(minlen, len[p]);
         tab[p] = (int32_t)tab.size() | (len[p] << 16);
         for (int j = 0; j < len[p]; ++j) {
             const int32_t o = off[(size_t)p * kPatTableMax + j];
@@ -1603,7 +1502,6 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
         }
     }
     P.pat_dmax = dmax;
-    P.pat_minlen = minlen;
     if ((e = hipMalloc(&P.d_ptab, sizeof(int32_t) * tab.size())) != hipSuccess ||
         (e = hipMemcpy(P.d_ptab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return done(e);
@@ -1763,21 +1661,11 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                 if (P.pat_ai) { AIJHIP_PT(true, false); }
                 AIJHIP_PT(true, true);
             }
-            if constexpr (T == 512 && CAP == 4094) {
-                if (P.pat_ai && P.pat_pipe && P.pat_minlen >= 1 && !dpart && !stop) {  // A/B: persistent, pipelined
-                    static int grid = 0;
-                    if (grid == 0) {
-                        int dev = 0, cus = 0, occ = 0;
-                        (void)hipGetDevice(&dev);
-                        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_spmv_pattern_pipe<T, CAP>, T, 0);
-                        grid = std::max(1, cus * std::max(1, occ));
-                    }
-                    const int g = std::min(grid, (int)P.n_blocks);
-                    hipLaunchKernelGGL((k_spmv_pattern_pipe<T, CAP>), dim3(g), dim3(T), 0, s, P.d_blocks, P.n_blocks,
-                                       L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, x, y);
-                    return;
-                }
+            if (P.pat_ai && !P.pat_bf) {  // A/B: the predicated gathers
+                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, false>), dim3(P.n_blocks),
+                                   dim3(T), 0, s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
+                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);
+                return;
             }
             if (P.pat_ai && P.tune.nt == 1) {  // A/B: non-temporal aa loads
                 hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, true>), dim3(P.n_blocks), dim3(T), 0,

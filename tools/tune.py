@@ -159,9 +159,9 @@ def main():
     if args.variants == "patgeom":  # row patterns at geometries 6 (512 rows), 8 (256) and 7 (1024)
         for g, nt in ((6, 0), (8, 0), (7, 0), (8, 1), (6, 0)):
             variants.append(("stream", dict(row_patterns=1, geometry=g, nt_loads=nt, env={"AIJHIP_PAT_XCHUNK": "0"})))
-    if args.variants == "patpipe":  # row patterns: persistent pipelined MatMult (AIJHIP_PAT_PIPE) vs one block per WG
-        for pp in ("0", "1", "0", "1"):
-            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_PIPE": pp, "AIJHIP_PAT_XCHUNK": "0"})))
+    if args.variants == "patbf":  # row patterns: branch-free vs predicated gathers (AIJHIP_PAT_BF)
+        for bf in ("1", "0", "1", "0"):
+            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_BF": bf, "AIJHIP_PAT_XCHUNK": "0"})))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
