@@ -525,7 +525,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // SCAN: the rows' starts are the block's k0 plus the prefix sums of their
 // patterns' lengths (a wave scan and the wave totals through LDS), so ai is
 // not read at all; otherwise from ai (A/B).
-template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = true>
+template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = false>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
@@ -600,7 +600,7 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
         const int32_t *off = tab + (pm & 0xffff);
         const double *ar = av + (rs - k0);
         double s = seed;
-        if constexpr (!BF) {  // A/B (AIJHIP_PAT_BF=0): the predicated form
+        if constexpr (!BF) {  // predicated gathers (default; the branch-free form below: AIJHIP_PAT_BF=1)
             for (int32_t j0 = 0; j0 < n; j0 += 8) {
                 double xv[8];
 #pragma unroll
@@ -612,9 +612,12 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
             }
         } else
         for (int32_t j0 = 0; j0 < n; j0 += 8) {
-            // branch-free: slots past the row's end repeat its last entry
-            // (loaded, not summed), so the 8 offset reads, the 8 gathers and
-            // the 8 value reads issue back to back under one wait each
+            // branch-free (A/B): slots past the row's end repeat its last
+            // entry (loaded, not summed), so the 8 offset reads, the 8
+            // gathers and the 8 value reads issue back to back under one wait
+            // each. Measured slower at 300^3 (370.4 vs 360.3 us,
+            // profiles/r03/patterns/patbf_poisson.jsonl): the 8th gather of a
+            // 7-entry row is a wasted load
             const int32_t last = n - 1 - j0;
             int32_t o[8];
             double xv[8], av8[8];
@@ -1661,8 +1664,8 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                 if (P.pat_ai) { AIJHIP_PT(true, false); }
                 AIJHIP_PT(true, true);
             }
-            if (P.pat_ai && !P.pat_bf) {  // A/B: the predicated gathers
-                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, false>), dim3(P.n_blocks),
+            if (P.pat_ai && P.pat_bf) {  // A/B: the branch-free gathers
+                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, true>), dim3(P.n_blocks),
                                    dim3(T), 0, s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
                                    OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);
                 return;
