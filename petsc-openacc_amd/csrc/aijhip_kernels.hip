@@ -525,7 +525,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // SCAN: the rows' starts are the block's k0 plus the prefix sums of their
 // patterns' lengths (a wave scan and the wave totals through LDS), so ai is
 // not read at all; otherwise from ai (A/B).
-template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = false>
+template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = false, bool NB = false>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
@@ -596,11 +596,34 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     } else {
         pm = tab[p];
     }
+    // NB (A/B, AIJHIP_PAT_NB=1): x[r - 1] and x[r + 1] taken from the
+    // neighbouring lanes' x[r] (rows are consecutive lanes), gathered only by
+    // the lanes at a wave's or the block's edge
+    double xd = 0.0, xl = 0.0, xr = 0.0;
+    if constexpr (NB) {
+        xd = op.gx(r);
+        xl = __shfl_up(xd, 1, 64);
+        xr = __shfl_down(xd, 1, 64);
+    }
     if (own) {
         const int32_t *off = tab + (pm & 0xffff);
         const double *ar = av + (rs - k0);
         double s = seed;
-        if constexpr (!BF) {  // predicated gathers (default; the branch-free form below: AIJHIP_PAT_BF=1)
+        if constexpr (NB) {
+            const bool okl = (t & 63) != 0, okr = (t & 63) != 63 && t + 1 < d.nrows;
+            for (int32_t j0 = 0; j0 < n; j0 += 8) {
+                double xv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j0 + j < n) {
+                        const int32_t o = off[j0 + j];
+                        xv[j] = o == 0 ? xd : (o == -1 && okl) ? xl : (o == 1 && okr) ? xr : op.gx(r + o);
+                    }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (j0 + j < n) s += ar[j0 + j] * xv[j];
+            }
+        } else if constexpr (!BF) {  // predicated gathers (default; the branch-free form below: AIJHIP_PAT_BF=1)
             for (int32_t j0 = 0; j0 < n; j0 += 8) {
                 double xv[8];
 #pragma unroll
@@ -1663,6 +1686,12 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
             if (add) {
                 if (P.pat_ai) { AIJHIP_PT(true, false); }
                 AIJHIP_PT(true, true);
+            }
+            if (P.pat_ai && P.pat_nb) {  // A/B: x[r +- 1] from the neighbouring lanes
+                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, false, true>), dim3(P.n_blocks),
+                                   dim3(T), 0, s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
+                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);
+                return;
             }
             if (P.pat_ai && P.pat_bf) {  // A/B: the branch-free gathers
                 hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, true>), dim3(P.n_blocks),

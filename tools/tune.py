@@ -162,6 +162,10 @@ def main():
     if args.variants == "patbf":  # row patterns: branch-free vs predicated gathers (AIJHIP_PAT_BF)
         for bf in ("1", "0", "1", "0"):
             variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_BF": bf, "AIJHIP_PAT_XCHUNK": "0"})))
+    if args.variants == "patnb":  # row patterns: x[r +- 1] from neighbouring lanes (AIJHIP_PAT_NB) vs gathered
+        for nb in ("0", "1", "0", "1"):
+            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_NB": nb, "AIJHIP_PAT_BF": "0",
+                                                                 "AIJHIP_PAT_XCHUNK": "0"})))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
