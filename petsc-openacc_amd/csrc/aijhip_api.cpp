@@ -401,6 +401,8 @@ int plan_stream(aijhip_mat *A) {
         P.pat_bf = bf && bf[0] == '1';
         const char *nb = std::getenv("AIJHIP_PAT_NB");
         P.pat_nb = nb && nb[0] == '1';
+        const char *w16 = std::getenv("AIJHIP_PAT_W16");
+        P.pat_w16 = w16 && w16[0] == '1';
     }
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
     // for the row blocks whose offset dictionaries fit (geometry 6 — 7 and 9

@@ -214,6 +214,7 @@ struct Plan {
     int32_t *d_ptab = nullptr;
     int32_t n_ptab = 0, n_pat = 0;
     bool pat_ai = true;  // row starts from ai; AIJHIP_PAT_AI=0 at planning: from the lengths' scan (A/B)
+    bool pat_w16 = false;    // AIJHIP_PAT_W16=1 at planning: one 16-B LDS write per staged pair (A/B, slower)
     bool pat_nb = false;     // AIJHIP_PAT_NB=1 at planning: x[r +- 1] from neighbouring lanes (A/B)
     bool pat_bf = false;     // AIJHIP_PAT_BF=1 at planning: branch-free gathers (A/B, measured slower)
     int32_t pat_dmax = 0;    // largest |column - row| offset in the table (the stencil's plane distance)

@@ -525,14 +525,19 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // SCAN: the rows' starts are the block's k0 plus the prefix sums of their
 // patterns' lengths (a wave scan and the wave totals through LDS), so ai is
 // not read at all; otherwise from ai (A/B).
-template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = false, bool NB = false>
+template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = false, bool NB = false, bool W16 = false>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
                                                     double *dpart, const int *stop, int xchunk = 0) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int TPT = (kPatTableMax + T - 1) / T;
-    __shared__ double av[CAP];
+    // W16 (A/B, AIJHIP_PAT_W16=1): the staged values sit at (k - kb), kb =
+    // the even start of the block's pairs, so every pair is one aligned 16-B
+    // LDS write (slots outside [k0, k1) hold neighbours' values, never read).
+    // Measured slower at 300^3: 403.3 vs 360.7 us with two 8-B writes at
+    // (k - k0) (profiles/r03/patterns/patw16_poisson.jsonl)
+    __shared__ __attribute__((aligned(16))) double av[W16 ? CAP + 2 : CAP];
     __shared__ int32_t tab[kPatTableMax];
     __shared__ int32_t wsum[T / 64];
     // xchunk (Plan::pat_xchunk): the XCD placement of the row blocks — a
@@ -583,7 +588,9 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if (k < k1) {
+        if constexpr (W16) {
+            if (k < k1) *reinterpret_cast<f64x2 *>(av + (k - kb)) = a2[it];
+        } else if (k < k1) {
             if (k >= k0) av[k - k0] = a2[it].x;
             if (k + 1 < k1) av[k + 1 - k0] = a2[it].y;
         }
@@ -607,7 +614,7 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     }
     if (own) {
         const int32_t *off = tab + (pm & 0xffff);
-        const double *ar = av + (rs - k0);
+        const double *ar = av + (rs - (W16 ? kb : k0));
         double s = seed;
         if constexpr (NB) {
             const bool okl = (t & 63) != 0, okr = (t & 63) != 63 && t + 1 < d.nrows;
@@ -1686,6 +1693,13 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
             if (add) {
                 if (P.pat_ai) { AIJHIP_PT(true, false); }
                 AIJHIP_PT(true, true);
+            }
+            if (P.pat_ai && P.pat_w16) {  // A/B: one 16-B LDS write per pair
+                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, false, false, true>),
+                                   dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab,
+                                   P.n_pat, A.d_aa, OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop,
+                                   P.pat_xchunk);
+                return;
             }
             if (P.pat_ai && P.pat_nb) {  // A/B: x[r +- 1] from the neighbouring lanes
                 hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, false, true>), dim3(P.n_blocks),

@@ -166,6 +166,9 @@ def main():
         for nb in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_NB": nb, "AIJHIP_PAT_BF": "0",
                                                                  "AIJHIP_PAT_XCHUNK": "0"})))
+    if args.variants == "patw16":  # row patterns: 16-B vs two 8-B LDS writes per staged pair (AIJHIP_PAT_W16)
+        for w in ("0", "1", "0", "1"):
+            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_W16": w, "AIJHIP_PAT_XCHUNK": "0"})))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
