@@ -1,30 +1,38 @@
 #!/usr/bin/env python3
 """Benchmark: CSR SpMV effective HBM GB/s on the 300^3 7-point Poisson operand.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 300] [--kernel auto]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 300] [--layout csr|auto]
 
 A step is one MatMult (y = A x) of the whole operand, inputs resident in HBM.
 N = 1: the BASELINE.json configs[1] workload — 300^3 Poisson CSR (27 M rows,
 188.46 M entries, fp64 values, int32 indices) on one MI355X.
-N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL): weak
-scaling — every rank owns a 300^3-row z-slab; the global grid doubles one
-axis per factor 2 of N (z, then y, then x): N = 2 is 300x300x600, N = 4
-300x600x600, N = 8 the 600^3 grid of BASELINE configs[3] (75 planes of
-600^2 per rank). The halo planes are exchanged over RCCL while the diagonal
-block multiplies (petsc-openacc_amd/mpiaij.py). The same line carries
-`strong_300`: the 300^3 operand itself row-partitioned over the N GPUs (the
-north star's "300^3 matrix at 1, 2, 4 and 8 GPUs").
+N > 1: one rank per GPU over RCCL. Launched by torch.distributed.run, or by
+this script itself: `python bench.py --gpus N` with no WORLD_SIZE in the
+environment starts the N rank processes (before any GPU call) and prints rank
+0's line (the reference's rank sweep, runs/single-node-scaling.pbs:56-67, is
+its job script's; here the bench owns it). Weak scaling — every rank owns a
+300^3-row z-slab; the global grid doubles one axis per factor 2 of N (z, then
+y, then x): N = 2 is 300x300x600, N = 4 300x600x600, N = 8 the 600^3 grid of
+BASELINE configs[3] (75 planes of 600^2 per rank). The halo planes are
+exchanged over RCCL while the diagonal block multiplies (csrc/ksp_mpi.hip).
+The same line carries `strong_300`: the 300^3 operand itself row-partitioned
+over the N GPUs (the north star's "300^3 matrix at 1, 2, 4 and 8 GPUs"), and
+per rank the halo cost of both exchange forms (p2p send/recv, all-gather).
+
+The headline MatMult reads PETSc's CSR as stored (ai / aj / aa; --layout
+csr, the default): the metric is a CSR SpMV. The library's automatic layout
+(row patterns for a stencil: no aj at all) is timed beside it in the
+`effective` block, on its own bytes, and is never `value`.
 
 value  = algorithmic bytes of all ranks x K / (max-over-ranks wall time of the
          K timed steps), bytes per SpMV = 12 nnz + 4 (m+1) + 8 n + 8 m
          (x and the matrix read once, y written once).
-roofline.achieved = the compulsory bytes of the layout the plan chose (row
-         patterns / column codes / CSR, roofline.layout) per launch / the
-         mean duration of the dominant kernel, from HIP events recorded
-         around every launch on the stream it runs on; peak 8 TB/s
-         (MI355X_MICROARCH.md). roofline.csr_effective: the CSR bytes / the
-         same time (value's effective rate); roofline.aj_layout: the same
-         MatMult from aj in the same run.
+roofline.achieved = the compulsory bytes of the layout the timed kernel reads
+         (aijhip_info_t.mult_layout_bytes: the CSR bytes above for --layout
+         csr) per launch / the mean duration of the launch, from HIP events
+         recorded around every launch on the stream it runs on; peak 8 TB/s
+         (MI355X_MICROARCH.md). Every `frac` in the line is bytes the timed
+         kernel moves / its time / 8 TB/s.
 cpu_baseline = the C restatement of PETSc's MatMult_SeqAIJ (oracle/, a port:
          the reference cannot be built here) on 1 host core, bounded sample.
 """
@@ -55,9 +63,10 @@ def parse():
     p.add_argument("--grid", type=int, default=300, help="per-rank grid edge (N^3 rows per rank)")
     p.add_argument("--kernel", default="auto", choices=["auto", "stream", "scalar", "vector", "merge"])
     p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..5 (default: library's)")
-    p.add_argument("--xcd", type=int, default=None, help="STREAM XCD-contiguous remap 0/1")
     p.add_argument("--nt", type=int, default=None, help="STREAM non-temporal matrix loads 0/1")
-    p.add_argument("--persist", type=int, default=None, help="persistent pipelined STREAM, workgroups/CU")
+    p.add_argument("--layout", default="csr", choices=["csr", "auto"],
+                   help="what the headline MatMult reads: csr = PETSc's aj/aa (the metric's CSR SpMV; default), "
+                        "auto = the library's automatic layout (row patterns / column codes where they fit)")
     p.add_argument("--codes", type=int, default=None,
                    help="STREAM column codes -1 (library default: automatic) / 0 (aj) / 1")
     p.add_argument("--patterns", type=int, default=None,
@@ -100,6 +109,66 @@ def weak_grid(G: int, world: int):
     if nz % world or nx * ny * (nz // world) != G ** 3:
         return G, G, G * world
     return nx, ny, nz
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def rank_plan(n: int, argv, port: int, child=None, env=None):
+    """The N rank processes `python bench.py --gpus N` starts when no launcher
+    set WORLD_SIZE (the driver may run the bench plainly at every N): one per
+    GPU, the torch.distributed env contract of torch.distributed.run (RANK,
+    LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR 127.0.0.1,
+    MASTER_PORT), the same arguments. Returns [(cmd, env)] in rank order."""
+    cmd = list(child) if child is not None else [sys.executable, "-u", str(Path(__file__).resolve())] + list(argv)
+    base = dict(os.environ if env is None else env)
+    out = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0",
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        out.append((cmd, e))
+    return out
+
+
+def launch_ranks(n: int, argv, child=None, poll_s: float = 0.2) -> int:
+    """Start the N ranks (rank_plan) as child processes of this one — no exec,
+    and nothing here has touched the GPU — and wait for them. Rank 0's stdout
+    is this process's stdout (its one JSON line); the other ranks' stdout goes
+    to stderr, so exactly one line reaches the driver. If a rank fails, the
+    others are stopped (by their own Popen handles) and its exit code is
+    returned."""
+    import subprocess
+    plan = rank_plan(n, argv, free_port(), child)
+    procs = []
+    for r, (cmd, env) in enumerate(plan):
+        procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except Exception:  # noqa: BLE001
+                p.kill()
+                p.wait()
+    return rc
 
 
 def rank_record(rank, device, pci_bus, rows, nnz, ghosts, spmv_ms, diag_ms):
@@ -268,7 +337,7 @@ def read_ceiling(nbytes, dev, reps=20):
 
 def pmc_traffic(rows, nnz, block):
     """HBM bytes per launch from the committed rocprofv3 PMC record
-    (profiles/pmc_latest.json, written from tools/gpu_pmc.sh), used only
+    (profiles/pmc_latest.json, written from tools/gpu_pmc_case.sh), used only
     when it was measured on the same operand with the same block geometry;
     bench.py itself runs without the profiler, so it cannot count bytes."""
     p = ROOT / "profiles" / "pmc_latest.json"
@@ -329,16 +398,19 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                 mean, med, mn = time_launches(lambda: A.mult(x, y, stream), stream, reps)
             finally:
                 A.destroy()
+            lb = info["mult_layout_bytes"]
             rec[kern] = {"us_mean": round(mean, 2), "us_median": round(med, 2), "us_min": round(mn, 2),
-                         "GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
-                         "frac": round(nbytes / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                         "layout_bytes": lb, "GBs": round(lb / (mean * 1e-6) / 1e9, 1),
+                         "frac": round(lb / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                         "csr_effective_GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
                          "geometry": info.get("stream_geometry"), "long_rows": info.get("n_long_rows"),
                          "column_codes": info.get("column_codes"), "gather_sorted": info.get("gather_sorted"),
                          "row_patterns": info.get("row_patterns")}
         del x, y
         flat = read_ceiling(nbytes, dev)
         rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],
-                                    "frac_of_ceiling": round(rec["stream"]["GBs"] / flat[0][0], 4)}
+                                    "frac_of_ceiling": round(rec["stream"]["GBs"] / flat[0][0], 4),
+                                    "note": "the CSR byte count read once by aijhip_read_probe (mode 0)"}
         if cpu_sample:
             t_cpu, reps_cpu, _ = cpu_baseline(ai, aj, aa, pkg.splitmix_uniform(m, 42), 3.0)
             rec["cpu_baseline"] = {"value": round(nbytes / t_cpu / 1e9, 3), "unit": "GB/s", "cores": 1,
@@ -346,7 +418,9 @@ def flan_standins(pkg, dev, reps, cpu_sample):
         out[name] = rec
         del ai, aj, aa
     out["note"] = ("Flan_1565 itself is not in the image (no network); matio.load_mtx reads it when present. "
-                   "GBs = algorithmic bytes / mean HIP-event launch time; frac of 8 TB/s")
+                   "GBs / frac = the bytes of the layout the launch reads (layout_bytes: column codes 10 B per "
+                   "coded entry, the gather-ordered copy 12 B, CSR 12 B) / mean HIP-event launch time, of 8 TB/s; "
+                   "csr_effective_GBs = SURVEY §8d's CSR bytes / the same time")
     return out
 
 
@@ -360,61 +434,122 @@ def cpu_model():
     return "unknown"
 
 
+def halo_forms(op, x, stream, reps, rank, dev, m_loc, nnz_loc):
+    """Per rank, what each exchange form adds on top of the diagonal block:
+    `reps` distributed SpMVs through the all-gather operator (op.native, built
+    with halo="allgather") and through its p2p twin (op.p2p_native(): same A_d,
+    ghost-numbered A_o, ncclSend/ncclRecv to the slab neighbours), against
+    the same launches of A_d alone. Returns {form: this rank's record}."""
+    import torch
+    y = torch.empty(op.mloc, dtype=torch.float64, device=dev)
+    diag_us, _, _ = time_launches(lambda: op.A_d.mult(x, y, stream), stream, reps)
+    out = {}
+    for form, nat in (("p2p", op.p2p_native()), ("allgather", op.native)):
+        for _ in range(3):
+            nat.mult(x, y, stream)
+        us, _, _ = time_launches(lambda: nat.mult(x, y, stream), stream, reps)
+        out[form] = rank_record(rank, torch.cuda.current_device(),
+                                getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None), m_loc, nnz_loc,
+                                op.n_ghost, us / 1e3, diag_us / 1e3)
+    del y
+    return out
+
+
+def gather_forms(mine, world):
+    """All ranks' halo_forms records, per form, worst exposed rank named."""
+    import torch.distributed as dist
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    res = {}
+    for form in ("p2p", "allgather"):
+        ranks = [r[form] for r in allr]
+        worst = max(ranks, key=lambda q: q["halo_exposed_us"])
+        res[form] = {"ranks": ranks, "worst_rank": worst["rank"], "worst_halo_exposed_us": worst["halo_exposed_us"]}
+    return res
+
+
 def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm):
     """The G^3 operand (300^3: BASELINE configs[1]) row-partitioned over all
     ranks in balanced whole z-planes (DMDA PETSC_DECIDE), timed like the main
     line: K distributed SpMVs between barriers, max over ranks. Strong
-    scaling: the total work is the N = 1 workload's."""
+    scaling: the total work is the N = 1 workload's. Both halo forms are
+    timed per rank (halo_forms); the headline form is --halo."""
     import torch
     import torch.distributed as dist
     bounds = [mpiaij.slab_bounds(G, world, r) for r in range(world)]
     row_starts = np.array([b[0] * G * G for b in bounds] + [G ** 3], dtype=np.int64)
     z0, z1 = bounds[rank]
     ai, aj, aa = pkg.poisson_csr(G, G, G, z0, z1)
-    op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo, comm=comm)
+    nnz_loc = len(aj)
+    op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo="allgather", comm=comm)
+    nat = op.native if args.halo == "allgather" else op.p2p_native()
+    layout_local = op.A_d.info()["mult_layout_bytes"]
     nnz_t = torch.tensor([len(aj)], dtype=torch.float64, device=dev)
     dist.all_reduce(nnz_t)
     nnz = int(nnz_t.item())
     del ai, aj, aa
+    stream = torch.cuda.current_stream()
     x = torch.from_numpy(pkg.splitmix_uniform(op.mloc, 42, int(row_starts[rank]))).to(dev)
     y = torch.empty(op.mloc, dtype=torch.float64, device=dev)
     for _ in range(args.warmup):
-        op.mult(x, y)
+        nat.mult(x, y, stream)
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        op.mult(x, y)
+        nat.mult(x, y, stream)
     torch.cuda.synchronize()
     dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
     dt = float(el.item()) / args.steps
+    forms = gather_forms(halo_forms(op, x, stream, max(args.steps, 20), rank, dev, op.mloc, nnz_loc), world)
     nbytes = pkg.algorithmic_bytes(G ** 3, G ** 3, nnz)
+    lt = torch.tensor([float(layout_local)], dtype=torch.float64, device=dev)
+    dist.all_reduce(lt)
     op.native.destroy()
+    if op._twin is not None:
+        op._twin[1].destroy()
+        if op._twin[0] is not None:
+            op._twin[0].destroy()
     op.A_d.destroy()
     if op.A_o is not None:
         op.A_o.destroy()
     return {"workload": f"{G}^3 Poisson CSR row-partitioned over {world} GPUs "
                         f"({z1 - z0} of {G} z-planes on rank {rank})",
             "scaling": "strong", "value": round(nbytes / dt / 1e9, 2), "unit": "GB/s",
-            # SURVEY §8d's CSR bytes over N HBM peaks: an effective fraction,
-            # above 1 when the ranks' diagonal blocks read row patterns
-            "csr_effective_frac": round(nbytes / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
-            "ms_per_step": round(dt * 1e3, 4), "rows": G ** 3, "nnz": nnz, "halo": args.halo}
+            # the bytes the ranks' diagonal blocks read (CSR with --layout csr)
+            # over N HBM peaks
+            "frac": round(float(lt.item()) / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
+            "ms_per_step": round(dt * 1e3, 4), "rows": G ** 3, "nnz": nnz, "halo": args.halo,
+            "halo_forms": forms}
+
+
+def layout_name(info) -> str:
+    if info.get("row_patterns"):
+        return (f"row patterns ({info['row_patterns']} column - row offset lists, a 1-byte id per row, aa "
+                "verbatim, no column per entry; cf. PETSc's inode rows) — not CSR")
+    if info.get("column_codes"):
+        return "column codes (a 16-bit code per entry in aj's place, aa verbatim) — not CSR"
+    if info.get("gather_sorted"):
+        return "gather-ordered copy of the CSR row blocks"
+    return "CSR (PETSc's ai / aj / aa as stored)"
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher: start the N ranks here, before anything touches the GPU
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     import torch
     import torch.distributed as dist
 
     pkg = importlib.import_module("petsc-openacc_amd")
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the HIP path has no CPU fallback)")
     if args.rehearse_one_gpu:
@@ -422,13 +557,20 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
     distributed = world > 1 or args.mpi
+    csr_forced = args.layout == "csr"
 
-    def configure(mat):
-        for opt, val in (("geometry", args.geometry), ("xcd_remap", args.xcd), ("nt_loads", args.nt),
-                         ("persistent", args.persist), ("column_codes", args.codes),
-                         ("row_patterns", args.patterns)):
+    def set_layout(mat, csr):
+        """csr: the MatMult reads PETSc's aj (row patterns and column codes
+        off); else the library's automatic layout (or what --codes /
+        --patterns force)."""
+        mat.set_option("column_codes", 0 if csr else (-1 if args.codes is None else args.codes))
+        mat.set_option("row_patterns", 0 if csr else (-1 if args.patterns is None else args.patterns))
+
+    def configure(mat, csr=csr_forced):
+        for opt, val in (("geometry", args.geometry), ("nt_loads", args.nt)):
             if val is not None:
                 mat.set_option(opt, val)
+        set_layout(mat, csr)
         return mat
 
     comm = None
@@ -471,9 +613,12 @@ def main():
         def make_local(a_i, a_j, a_a, ncols):
             return configure(pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols, device=local_rank, kernel=args.kernel))
 
-        op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo=args.halo, comm=comm)
+        # built with the all-gather halo; its p2p twin shares A_d, so both
+        # exchange forms are timed on one diagonal block (halo_forms)
+        op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo="allgather", comm=comm)
+        nat = op.native if args.halo == "allgather" else op.p2p_native()
         info = op.A_d.info()
-        step = lambda: op.mult(xd, yd)  # noqa: E731
+        step = lambda: nat.mult(xd, yd, stream)  # noqa: E731
     else:
         A = configure(pkg.SeqAIJHIP(ai, aj, aa, ncols=m_loc, device=local_rank, kernel=args.kernel))
         info = A.info()
@@ -488,6 +633,13 @@ def main():
     nnz_global = int(nnz_t.item())
     bytes_global = pkg.algorithmic_bytes(n_global, n_global, nnz_global)
     bytes_local = pkg.algorithmic_bytes(m_loc, m_loc, nnz_loc)
+    # what the timed kernel moves: the layout's compulsory bytes (the CSR
+    # bytes above for --layout csr; distributed: A_d's layout + A_o as CSR)
+    if distributed:
+        layout_bytes = info["mult_layout_bytes"] + (pkg.algorithmic_bytes(m_loc, m_loc, op.nz_o) - 4 * (m_loc + 1)
+                                                     - 16 * m_loc + 8 * op.n_ghost if op.nz_o else 0)
+    else:
+        layout_bytes = info["mult_layout_bytes"]
 
     for _ in range(args.warmup):
         step()
@@ -514,24 +666,13 @@ def main():
     elapsed = float(el_t.item())
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
 
-    ranks = None
+    ranks = forms = None
     if distributed:
-        # Evidence the exchange hides behind the diagonal block: the same K
-        # launches of A_d alone (no halo, no A_o) on the same stream.
-        ev_d = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
-        y_diag = torch.empty_like(yd)
-        for i in range(K):
-            ev_d[i][0].record(stream)
-            op.A_d.mult(xd, y_diag, stream)
-            ev_d[i][1].record(stream)
-        torch.cuda.synchronize()
-        diag_ms = float(np.mean([a.elapsed_time(b) for a, b in ev_d]))
-        del y_diag
-        mine = rank_record(rank, torch.cuda.current_device(),
-                           getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None), m_loc, nnz_loc,
-                           op.n_ghost, float(np.mean(launch_ms)), diag_ms)
-        ranks = [None] * world
-        dist.all_gather_object(ranks, mine)
+        # Evidence the exchange hides behind the diagonal block: both halo
+        # forms against the same launches of A_d alone, per rank
+        mine = halo_forms(op, xd, stream, K, rank, dev, m_loc, nnz_loc)
+        forms = gather_forms(mine, world)
+        ranks = forms[args.halo]["ranks"]
 
     # roofline sample: at least --roofline-reps launches (SURVEY §8d asks
     # for the median of >= 50), the K timed ones plus more if K is smaller
@@ -551,31 +692,34 @@ def main():
     torch.cuda.synchronize()
     stable = bool(torch.equal(y_chk, yd))
 
-    # With row patterns or column codes in the plan (the automatic layouts),
-    # the same SpMV from PETSc's aj array in the same run: the plain kernel's
-    # time and fraction, and whether its y is the same bits (it must be).
-    aj_leg = None
-    if not distributed and (info.get("column_codes") or info.get("row_patterns")):
-        def aj_layout():
-            A.set_option("row_patterns", 0)
-            A.set_option("column_codes", 0)
-            try:
-                y_aj = torch.empty_like(yd)
-                for _ in range(5):
-                    A.mult(xd, y_aj, stream)
-                mean, med, mn = time_launches(lambda: A.mult(xd, y_aj, stream), stream, max(args.roofline_reps, 50))
-                same = bool(torch.equal(y_aj, y_chk))
-                del y_aj
-            finally:
-                A.set_option("column_codes", -1 if args.codes is None else args.codes)
-                A.set_option("row_patterns", -1 if args.patterns is None else args.patterns)
-            return {"us_mean": round(mean, 2), "us_median": round(med, 2), "us_min": round(mn, 2),
-                    "GBs": round(bytes_local / (mean * 1e-6) / 1e9, 1),
-                    "frac": round(bytes_local / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                    "bitwise_equal_coded": same,
-                    "note": "the same MatMult reading PETSc's aj (12 bytes per entry): row patterns and "
-                            "column codes off"}
-        aj_leg = aj_layout()
+    # The library's automatic layout (row patterns for the stencil: no aj)
+    # timed beside the CSR headline in the same run, on ITS bytes; its y must
+    # be the headline's bits. It is not a CSR measurement and never `value`.
+    effective = None
+    if not distributed and csr_forced:
+        def effective_layout():
+            set_layout(A, False)
+            inf = A.info()
+            if inf["mult_layout_bytes"] == bytes_local and not inf.get("row_patterns") and \
+                    not inf.get("column_codes"):
+                return {"layout": layout_name(inf), "note": "the automatic layout is CSR here"}
+            y_e = torch.empty_like(yd)
+            for _ in range(5):
+                A.mult(xd, y_e, stream)
+            mean, med, mn = time_launches(lambda: A.mult(xd, y_e, stream), stream, max(args.roofline_reps, 50))
+            same = bool(torch.equal(y_e, y_chk))
+            del y_e
+            lb = inf["mult_layout_bytes"]
+            return {"layout": layout_name(inf), "bytes_per_launch": lb,
+                    "us_mean": round(mean, 2), "us_median": round(med, 2), "us_min": round(mn, 2),
+                    "achieved": round(lb / (mean * 1e-6) / 1e9, 1),
+                    "frac": round(lb / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                    "csr_equivalent_GBs": round(bytes_local / (mean * 1e-6) / 1e9, 1),
+                    "bitwise_equal_csr": same,
+                    "note": "NOT a CSR SpMV: this layout does not read aj (the bytes it moves are bytes_per_launch; "
+                            "frac is on those). csr_equivalent_GBs = the CSR bytes over the same time, for "
+                            "comparison only. The CG / CG+GAMG legs below run on this layout."}
+        effective = effective_layout()
 
     # The measurements beside the headline one are guarded: an exception
     # raised alike on every rank (a bug, an allocation failure) is recorded
@@ -597,9 +741,17 @@ def main():
     if distributed and not args.no_strong:
         strong = guarded("strong_300", lambda: strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm))
 
+    # the solver legs run on the automatic layout (what a caller gets)
+    if distributed and csr_forced:
+        set_layout(op.A_d, False)
+    elif not distributed:
+        set_layout(A, False)
+    solver_layout = layout_name((op.A_d if distributed else A).info())
+
     def single_cg():
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
         out = ksp.bench_cg(pkg, A, nx, ny, nz_global, dev, iters=args.cg_iters)
+        out["layout"] = solver_layout
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz_global)
         return out
@@ -611,7 +763,7 @@ def main():
         rhs_h, _ = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
         b = torch.from_numpy(rhs_h).to(dev)
         xs = torch.zeros_like(b)
-        cgm = C.KSPCGMPINative(op.native, rtol=0.0, atol=0.0, max_it=5)
+        cgm = C.KSPCGMPINative(nat, rtol=0.0, atol=0.0, max_it=5)
         cgm.solve(b, xs)  # warm-up
         cgm.set_tolerances(0.0, 0.0, 1e5, args.cg_iters)
         dist.barrier()
@@ -629,6 +781,7 @@ def main():
                                                                  else "RCCL, device doubles") +
                              ("; skipped at one rank" if world == 1 else "") + ")",
                "host_syncs": cgm.host_syncs, "halo": args.halo, "solver": "aijhip_kspmpi (native)",
+               "layout": solver_layout,
                "workload": f"{nx}x{ny}x{nz_global} Poisson, {planes}-plane z-slab per GPU"}
         cgm.destroy()
         return out
@@ -636,12 +789,10 @@ def main():
     def distributed_cg_gamg():
         # CG + PCGAMG across the ranks (csrc/gamg_mpi.hip: one distributed
         # hierarchy, as PETSc's agg GAMG on MPIAIJ), the reference's
-        # tolerances, from x = 0
+        # tolerances, from x = 0; the hierarchy's level halos are p2p plans
         rhs_h, exact_h = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
         b = torch.from_numpy(rhs_h).to(dev)
         xs = torch.zeros_like(b)
-        # (with --halo allgather the hierarchy is built over the operator's
-        # p2p twin, which shares A_d: the set-up's level halos are p2p plans)
         kg = C.KSPCGMPINative(op.p2p_native(), rtol=1e-14, atol=1e-12, max_it=10000, pc="gamg")
         dist.barrier()
         torch.cuda.synchronize()
@@ -671,13 +822,14 @@ def main():
                "pc": ("PCGAMG across ranks (aggregates per rank, P and Galerkin products over the MPIAIJ "
                       "operator, csrc/gamg_mpi.hip)" if world > 1 else "PCGAMG (single-GPU set-up)"),
                "options": "rtol 1e-14 atol 1e-12", "workload": f"{nx}x{ny}x{nz_global} Poisson",
-               "halo": "p2p" if args.halo == "p2p" else "p2p twin of the all-gather operator (shares A_d)"}
+               "layout": solver_layout, "halo": "p2p (the p2p twin of the operator; shares A_d)"}
         kg.destroy()
         return out
 
     def single_cg_gamg():
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
         out = ksp.bench_cg_gamg(pkg, A, nx, ny, nz_global, dev)
+        out["layout"] = solver_layout
         print(f"bench: CG+GAMG {out['its']} its, solve {out['solve_s']} s, set-up {out['setup_s']} s",
               file=sys.stderr, flush=True)
         # BASELINE configs[0] (100^3) on the device as well, beside its 1-core host solve
@@ -711,24 +863,9 @@ def main():
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
         mean_launch_s = float(np.mean(launch_ms)) / 1e3
-        # The roofline is the kernel's own: the compulsory bytes of the
-        # layout the plan chose (row patterns: no column per entry, a 1-byte
-        # id per row; column codes: 2 B per entry instead of aj's 4 B; else
-        # SURVEY §8d's CSR bytes). `value` stays the metric's effective rate
-        # on the CSR bytes (roofline.csr_effective beside it).
-        if info.get("row_patterns") and not distributed:
-            layout_bytes = bytes_local - 4 * nnz_loc + m_loc
-            layout = (f"row patterns ({info['row_patterns']} column - row offset lists, a 1-byte id per row, aa "
-                      "verbatim, no column per entry; cf. PETSc's inode rows)")
-        elif info.get("column_codes") and not distributed:
-            layout_bytes = bytes_local - 2 * nnz_loc
-            layout = "column codes (a 16-bit code per entry in aj's place, aa verbatim)"
-        else:
-            layout_bytes, layout = bytes_local, "CSR (PETSc's ai / aj / aa)"
         achieved = layout_bytes / mean_launch_s / 1e9
-        achieved_csr = bytes_local / mean_launch_s / 1e9
-        block = {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "xcd_remap", "nt_loads",
-                                      "persistent", "column_codes", "row_patterns")}
+        block = {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "nt_loads", "column_codes",
+                                      "row_patterns")}
         traffic, traffic_src = (None, None) if distributed else pmc_traffic(n_global, nnz_global, block)
         out = {
             "metric": "CSR SpMV effective HBM GB/s (300^3 7-pt Poisson, fp64 MatMult_SeqAIJ)",
@@ -750,7 +887,7 @@ def main():
                 if distributed
                 else f"{G}^3 Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])",
                 "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
-                "kernel": info["kernel"], "halo": args.halo if distributed else None,
+                "kernel": info["kernel"], "layout": layout_name(info), "halo": args.halo if distributed else None,
                 "block": block,
                 "bytes_per_spmv": bytes_global, "flops_per_spmv_petsc": 2 * nnz_global - n_global,
             },
@@ -762,37 +899,36 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "kernel": ("k_spmv_stream (CSR: aj / aa pairs, x gathered, LDS row sums)"
+                           if not (info.get("row_patterns") or info.get("column_codes")) else layout_name(info)),
                 "kernel_us_mean": round(mean_launch_s * 1e6, 2),
                 "kernel_us_median": round(float(np.median(launch_ms)) * 1e3, 2),
                 "kernel_us_min": round(float(np.min(launch_ms)) * 1e3, 2),
                 "launches_timed": int(len(launch_ms)),
                 "achieved_from_median": round(layout_bytes / (float(np.median(launch_ms)) / 1e3) / 1e9, 1),
                 "bytes_per_launch": layout_bytes,
-                "layout": layout,
-                "csr_effective": {
-                    "bytes_per_launch": bytes_local, "achieved": round(achieved_csr, 1),
-                    "frac": round(achieved_csr / HBM_PEAK_GBS, 4),
-                    "note": "SURVEY §8d's CSR bytes (12 nnz + 4 (m+1) + 8 n + 8 m) / the same mean launch time: "
-                            "the metric's effective bandwidth (value); above the HBM peak when the layout reads "
-                            "fewer bytes than CSR"},
+                "layout": layout_name(info),
+                "note": ("rank 0's distributed MatMult (exchange + A_d + A_o) on rank 0's bytes"
+                         if distributed else "bytes the timed kernel moves / mean HIP-event launch time"),
             },
             "result_stable": stable,
             "setup_s": round(t_setup, 2),
         }
-        if aj_leg is not None:
-            out["roofline"]["aj_layout"] = aj_leg
+        if effective is not None:
+            out["effective"] = effective
         if isinstance(ceiling, dict) and "error" not in ceiling:  # same-run flat reads of the same bytes
             out["roofline"]["ceiling_flat_read"] = {
                 "GBs": ceiling[0][0], "us": ceiling[0][1], "frac_of_ceiling": round(achieved / ceiling[0][0], 4),
                 "probe": "aijhip_read_probe mode 0: the SpMV's CSR byte count read once, non-temporal 16-B loads, "
                          "512-lane workgroups of two loads per lane (the fastest shape, tools/read_sweep.hip); "
-                         "frac_of_ceiling = roofline.achieved (the layout's bytes) / this rate",
+                         "frac_of_ceiling = roofline.achieved / this rate",
                 "stream_shape_read": {"GBs": ceiling[1][0], "us": ceiling[1][1],
                                       "frac": round(achieved / ceiling[1][0], 4),
                                       "probe": "mode 1: plain loads, four per lane (the STREAM kernel's shape)"}}
-        if distributed:  # whole-job CSR-effective rate against N HBM peaks (roofline.frac: rank 0's kernel alone)
-            out["aggregate_csr_effective_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
+        if distributed:  # whole-job rate against N HBM peaks (roofline.frac: rank 0's launch alone)
+            out["aggregate_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
             out["distributed"] = distributed_block(world, dist.get_backend(), comm.info(), args.comm_timeout, ranks)
+            out["distributed"]["halo_forms"] = forms
         if args.rehearse_one_gpu:
             out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
         if strong is not None:

@@ -50,7 +50,11 @@
 extern "C" {
 #endif
 
-#define AIJHIP_ABI_VERSION 1
+/* 2: aijhip_info_t gained mult_layout_bytes; the A/B-only options
+ * AIJHIP_OPT_XCD_REMAP / _PERSISTENT / _CLAMPED_LOADS / _LONG_OVERLAP /
+ * _ROW_GROUP were withdrawn (measured slower) and return
+ * AIJHIP_ERR_ARG. */
+#define AIJHIP_ABI_VERSION 2
 
 enum {
     AIJHIP_OK = 0,
@@ -114,6 +118,15 @@ typedef struct aijhip_info {
     int32_t row_patterns;    /* MatMult reads a pattern id per row instead of
                                 aj (AIJHIP_OPT_ROW_PATTERNS): the number of
                                 distinct column - row offset lists; 0 off    */
+    int32_t pad0;
+    int64_t mult_layout_bytes; /* compulsory bytes one MatMult of the plan in
+                                effect moves: mult_bytes for CSR (aj read);
+                                less where the plan reads column codes (10 B
+                                per coded entry) or row patterns (8 B per
+                                entry + 1 B per row + the offset table);
+                                more for the 32-bit gather-ordered copy
+                                (14 B per entry). x and the matrix read once,
+                                y written once (ABI 2)                        */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -146,20 +159,16 @@ enum {
     AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..11: lanes / LDS entries / rows per block
                                        (DESIGN.md §Kernels); -1 (default):
                                        6 for short rows, 1 for long rows    */
-    AIJHIP_OPT_XCD_REMAP = 2,       /* 0 (default): hardware round-robin;
-                                       1: each XCD gets a contiguous run of
-                                       row blocks; C >= 2: chunks of C blocks,
-                                       chunk c of every 8C on XCD slot c     */
+    AIJHIP_OPT_XCD_REMAP = 2,       /* withdrawn in ABI 2 (XCD-contiguous block
+                                       placement measured 3-10 % slower)     */
     AIJHIP_OPT_NT_LOADS = 3,        /* -1 (default): non-temporal for long rows
                                        with scattered gathers (the geometry-1
                                        operands), plain otherwise; 0 plain;
-                                       1 non-temporal aa/aj loads; 2 a lane's
-                                       aj loads first, then non-temporal aa;
-                                       3 aj first, plain                    */
-    AIJHIP_OPT_PERSISTENT = 4,      /* k > 0: persistent software-pipelined
-                                       STREAM, k workgroups per CU (0 = off) */
-    AIJHIP_OPT_CLAMPED_LOADS = 5,   /* 1: branch-free clamped loads instead of
-                                       predicated loads (default 0)         */
+                                       1 non-temporal aa/aj loads            */
+    AIJHIP_OPT_PERSISTENT = 4,      /* withdrawn in ABI 2 (the persistent
+                                       pipelined STREAM measured 7-28 % slower) */
+    AIJHIP_OPT_CLAMPED_LOADS = 5,   /* withdrawn in ABI 2 (branch-free clamped
+                                       loads measured slower)                */
     AIJHIP_OPT_EXACT = 6,           /* 1: every row summed sequentially in
                                        PETSc's order. Default 0: row blocks
                                        whose mean row length exceeds 128 use
@@ -187,21 +196,10 @@ enum {
                                        download (step3/step4 analogue); k > 0:
                                        chunks of >= k rows; 0: the serial
                                        step-2 form. Same results              */
-    AIJHIP_OPT_LONG_OVERLAP = 9,    /* 1: long-row segments run on a side
-                                       stream concurrently with the row
-                                       blocks (forked from and joined back to
-                                       the caller's stream); 0 (default): one
-                                       stream. Same results                  */
-    AIJHIP_OPT_ROW_GROUP = 11,      /* MatMult / MatMultAdd of row blocks whose
-                                       mean row length is at least 24, when
-                                       AIJHIP_OPT_EXACT is 0: 1 = a register
-                                       kernel, 2..64 lanes per row summing
-                                       strided 16-B pairs, __shfl_xor
-                                       combine, no LDS staging (reordered sum,
-                                       within the fp64 bound; deterministic);
-                                       0 = the LDS STREAM block; -1 (default)
-                                       = automatic. Rows of shorter blocks
-                                       stay bit-exact either way            */
+    AIJHIP_OPT_LONG_OVERLAP = 9,    /* withdrawn in ABI 2 (a side stream for
+                                       the long-row segments measured neutral) */
+    AIJHIP_OPT_ROW_GROUP = 11,      /* withdrawn in ABI 2 (register row groups
+                                       measured slower on every operand)     */
     AIJHIP_OPT_GATHER_SORT = 12,    /* MatMult / MatMultAdd from a copy of the
                                        row blocks with each block's entries
                                        sorted by column and their positions

@@ -32,9 +32,10 @@ if os.environ.get("AIJHIP_LIB"):
 
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
-OPTIONS = {"geometry": 1, "xcd_remap": 2, "nt_loads": 3, "persistent": 4, "clamped": 5, "exact": 6, "x_tile": 7,
-           "long_xcd": 8, "long_overlap": 9, "host_pipeline": 10, "row_group": 11, "gather_sort": 12,
-           "column_codes": 13, "row_patterns": 14}
+OPTIONS = {"geometry": 1, "nt_loads": 3, "exact": 6, "x_tile": 7, "long_xcd": 8, "host_pipeline": 10,
+           "gather_sort": 12, "column_codes": 13, "row_patterns": 14}
+# withdrawn in ABI 2 (measured slower); the library refuses them
+WITHDRAWN_OPTIONS = {"xcd_remap": 2, "persistent": 4, "clamped": 5, "long_overlap": 9, "row_group": 11}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 
@@ -73,7 +74,8 @@ class AIJInfo(ctypes.Structure):
         ("stream_threads", ctypes.c_int32), ("stream_nnz_cap", ctypes.c_int32), ("stream_rows", ctypes.c_int32),
         ("persistent", ctypes.c_int32), ("exact", ctypes.c_int32), ("x_tiled_blocks", ctypes.c_int32),
         ("gather_sorted", ctypes.c_int32), ("column_codes", ctypes.c_int32),
-        ("row_patterns", ctypes.c_int32),
+        ("row_patterns", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("mult_layout_bytes", ctypes.c_int64),
     ]
 
 
@@ -247,8 +249,13 @@ class SeqAIJHIP:
         _check(lib().aijhip_mat_set_kernel(self._h, KERNELS[kernel], lanes))
 
     def set_option(self, option: str, value: int):
-        """Speed-only STREAM knobs: geometry (0..5), xcd_remap, nt_loads."""
-        _check(lib().aijhip_mat_set_option(self._h, OPTIONS[option], int(value)))
+        """Speed-only STREAM knobs (include/aijhip.h AIJHIP_OPT_*): geometry,
+        nt_loads, exact, x_tile, long_xcd, host_pipeline, gather_sort,
+        column_codes, row_patterns. Results never depend on them."""
+        code = OPTIONS.get(option, WITHDRAWN_OPTIONS.get(option))
+        if code is None:
+            raise KeyError(f"unknown option {option!r}")
+        _check(lib().aijhip_mat_set_option(self._h, code, int(value)))
 
     def mult(self, x, y, stream=None):
         """y = A x (MatMult_SeqAIJ). x: float64[n], y: float64[m] GPU tensors."""

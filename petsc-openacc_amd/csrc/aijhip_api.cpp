@@ -74,9 +74,6 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_longs);
     hipFree(P.d_partials);
     hipFree(P.d_segperm);
-    if (P.ev_fork) (void)hipEventDestroy(P.ev_fork);
-    if (P.ev_join) (void)hipEventDestroy(P.ev_join);
-    if (P.long_stream) (void)hipStreamDestroy(P.long_stream);
     hipFree(P.d_xrange);
     hipFree(P.d_saj);
     hipFree(P.d_saa);
@@ -89,8 +86,6 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_cmeta);
     hipFree(P.d_pid);
     hipFree(P.d_ptab);
-    hipFree(P.d_sblocks);
-    hipFree(P.d_gblocks);
     hipFree(P.d_tile_coord);
     hipFree(P.d_carry_row);
     hipFree(P.d_carry_val);
@@ -141,12 +136,9 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
                std::vector<BlockDesc> &blocks, std::vector<LongSeg> &segs, std::vector<LongRow> &longs) {
     using namespace aijhip;
     const auto &rai = A->h_rai;
-    // segment length: kLongSegNnz; AIJHIP_LONG_SEG=n for A/B (tools/tune.py longseg)
-    static const int64_t seg_nnz = [] {
-        const char *v = std::getenv("AIJHIP_LONG_SEG");
-        const int64_t n = v ? std::atoll(v) : 0;
-        return n >= 256 && n <= (1 << 20) ? n : (int64_t)kLongSegNnz;
-    }();
+    // segment length: 1024-16384 measured within 3 % on the skewed stand-in
+    // (profiles/r03/longseg/)
+    constexpr int64_t seg_nnz = kLongSegNnz;
     int32_t r = r0;
     while (r < r1) {
         const int32_t len = rai[r + 1] - rai[r];
@@ -173,27 +165,6 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
         }
         blocks.push_back(BlockDesc{start, r - start, rai[start], nk});
     }
-}
-
-// XCD placement of the row-pattern launch. Blocks are dealt round-robin over
-// the 8 XCDs, so a block's +-1 / +-N in-plane x window reaches into blocks
-// run by other XCDs: at 300^3 each x line is fetched into ~2.2 of the 8 L2s
-// (PMC: 2.36 GB per launch against 2.07 GB). Chunks of C consecutive blocks
-// per XCD, with 8·C blocks spanning the plane distance dmax (so the +-dmax
-// reads of a line land in the same XCD's chunk), keep the in-plane window
-// on one XCD except at chunk edges. AIJHIP_PAT_XCHUNK: "auto" (C from dmax
-// and the mean rows per block, 0 when no C fits within 1/8 of a chunk),
-// -1 contiguous runs, C > 0 a fixed chunk, 0 hardware order; unset: "auto"
-// when kPatXchunkAuto, else hardware order.
-constexpr bool kPatXchunkAuto = false;
-static int32_t pattern_xchunk(const aijhip::Plan &P, int32_t nrows) {
-    const char *env = std::getenv("AIJHIP_PAT_XCHUNK");
-    if (env && std::strcmp(env, "auto") != 0) return (int32_t)std::strtol(env, nullptr, 10);
-    if ((!env && !kPatXchunkAuto) || P.n_blocks <= 0 || P.pat_dmax <= 0) return 0;
-    const double rpb = (double)nrows / P.n_blocks;
-    const int64_t c = std::llround(P.pat_dmax / (8.0 * rpb));
-    if (c < 1 || 8 * c > P.n_blocks) return 0;
-    return std::fabs(8.0 * c * rpb - P.pat_dmax) <= 0.125 * c * rpb ? (int32_t)c : 0;
 }
 
 int plan_stream(aijhip_mat *A) {
@@ -249,29 +220,6 @@ int plan_stream(aijhip_mat *A) {
     if (!blocks.empty() &&
         (e = hipMemcpy(P.d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return hipfail(e, "plan: upload blocks");
-    // Register row-group blocks (Tuning::group): the plain MatMult launch
-    // runs blocks of long enough rows through k_spmv_rowgroup and the rest
-    // through the LDS STREAM kernel; exact mode and compressed rows keep the
-    // one launch. (The decision is per block; the sums of the other blocks do
-    // not change.)
-    P.n_sblocks = P.n_gblocks = 0;
-    if (P.tune.group > 0 && !P.tune.exact && !blocks.empty() && P.tune.persist == 0 && !A->compressed) {
-        std::vector<BlockDesc> sb, gb;
-        for (const BlockDesc &d : blocks)
-            (d.nk >= (int64_t)kGroupMinMean * d.nrows ? gb : sb).push_back(d);
-        if (!gb.empty()) {
-            if ((e = dmalloc(&P.d_sblocks, sb.size(), &P.bytes)) != hipSuccess ||
-                (e = dmalloc(&P.d_gblocks, gb.size(), &P.bytes)) != hipSuccess)
-                return hipfail(e, "plan: alloc row-group blocks");
-            if ((!sb.empty() && (e = hipMemcpy(P.d_sblocks, sb.data(), sizeof(BlockDesc) * sb.size(),
-                                               hipMemcpyHostToDevice)) != hipSuccess) ||
-                (e = hipMemcpy(P.d_gblocks, gb.data(), sizeof(BlockDesc) * gb.size(), hipMemcpyHostToDevice)) !=
-                    hipSuccess)
-                return hipfail(e, "plan: upload row-group blocks");
-            P.n_sblocks = (int32_t)sb.size();
-            P.n_gblocks = (int32_t)gb.size();
-        }
-    }
     // x tiles (LDS-staged x, opt-in): where a block's columns span at most
     // its LDS entries, x[lo, lo + span) is loaded coalesced and gathered
     // from LDS (banded operators; never the 7-pt Poisson at scale, whose
@@ -304,9 +252,9 @@ int plan_stream(aijhip_mat *A) {
         }
     }
     // gather-ordered copy of the row blocks (Tuning::gsort): for the plain
-    // MatMult / MatMultAdd launch (not with the x tiles, the row groups or
-    // the persistent kernel, which read the original order)
-    if (P.tune.gsort > 0 && !blocks.empty() && P.d_xrange == nullptr && P.n_gblocks == 0 && P.tune.persist == 0) {
+    // MatMult / MatMultAdd launch (not with the x tiles, which read the
+    // original order)
+    if (P.tune.gsort > 0 && !blocks.empty() && P.d_xrange == nullptr) {
         const size_t nzp = (size_t)A->nz + 2;
         if ((e = dmalloc(&P.d_saj, nzp, &P.bytes)) != hipSuccess || (e = dmalloc(&P.d_saa, nzp, &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_sslot, nzp, &P.bytes)) != hipSuccess ||
@@ -369,6 +317,7 @@ int plan_stream(aijhip_mat *A) {
                     return hipfail(e, "plan: gather-ordered block lists");
                 P.n_nblocks = (int32_t)nb.size();
                 P.n_wblocks = (int32_t)wb.size();
+                for (const BlockDesc &d : wb) P.nz_wide += d.nk;
             }
             if ((e = aijhip::pack_gather_order(P, wb.empty() ? P.d_blocks : P.d_nblocks, (int32_t)nb.size(), P.d_sbase,
                                                P.d_sidx)) != hipSuccess ||
@@ -385,35 +334,17 @@ int plan_stream(aijhip_mat *A) {
     // for short-row operands whose rows follow few offset lists (stencils);
     // geometry 6, plain full-row launches, no long rows
     const int32_t nrl = rai.empty() ? 0 : (int32_t)rai.size() - 1;
-    if (P.tune.patterns > 0 && (P.tune.geom == 6 || P.tune.geom == 7 || P.tune.geom == 8) && !blocks.empty() && longs.empty() && !A->compressed &&
-        A->nz <= (int64_t)kBatchMinMean * nrl && P.d_xrange == nullptr && P.n_gblocks == 0 && P.d_sslot == nullptr &&
-        P.tune.persist == 0 && !P.tune.clamped && !P.tune.xcd) {
+    if (P.tune.patterns > 0 && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed &&
+        A->nz <= (int64_t)kBatchMinMean * nrl && P.d_xrange == nullptr && P.d_sslot == nullptr) {
         bool ok = false;
         if ((e = aijhip::build_row_patterns(*A, P, &ok)) != hipSuccess) return hipfail(e, "plan: row patterns");
-        // row starts from ai (default) or from the scan of the patterns'
-        // lengths (AIJHIP_PAT_AI=0; measured slower: 368.4 vs 358.3 us at
-        // 300^3, profiles/r03/patterns/patai_poisson.jsonl — the scan waits
-        // on the pattern id and the table, where ai's loads were in flight)
-        const char *pa = std::getenv("AIJHIP_PAT_AI");
-        P.pat_ai = !(pa && pa[0] == '0');
-        P.pat_xchunk = ok ? pattern_xchunk(P, nrl) : 0;
-        const char *bf = std::getenv("AIJHIP_PAT_BF");
-        P.pat_bf = bf && bf[0] == '1';
-        const char *nb = std::getenv("AIJHIP_PAT_NB");
-        P.pat_nb = nb && nb[0] == '1';
-        const char *w16 = std::getenv("AIJHIP_PAT_W16");
-        P.pat_w16 = w16 && w16[0] == '1';
     }
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
-    // for the row blocks whose offset dictionaries fit (geometry 6 — 7 and 9
-    // for MatMult / MatMultAdd only, A/B —, plain
-    // full-row launches: not with the x tiles, row groups, gather order,
-    // XCD remap, clamped loads or the persistent kernel); when some do not
-    // fit, they are launched from aj
-    if (P.tune.codes > 0 && (P.tune.geom == 6 || P.tune.geom == 7 || P.tune.geom == 9) && !blocks.empty() &&
-        P.d_pid == nullptr && !A->compressed && P.d_xrange == nullptr &&
-        P.n_gblocks == 0 && P.d_sslot == nullptr && P.tune.persist == 0 && P.tune.nt <= 1 && !P.tune.clamped &&
-        !P.tune.xcd) {
+    // for the row blocks whose offset dictionaries fit (geometry 6, plain
+    // full-row launches: not with the x tiles or the gather order); when
+    // some do not fit, they are launched from aj
+    if (P.tune.codes > 0 && P.tune.geom == 6 && !blocks.empty() && P.d_pid == nullptr && !A->compressed &&
+        P.d_xrange == nullptr && P.d_sslot == nullptr) {
         int32_t *d_cnt = nullptr;
         std::vector<int32_t> cnt(blocks.size());
         if ((e = dmalloc(&d_cnt, blocks.size(), nullptr)) != hipSuccess ||
@@ -447,6 +378,7 @@ int plan_stream(aijhip_mat *A) {
                     ++j;
                 }
             if (pos > INT32_MAX) return fail(AIJHIP_ERR_ARG, "plan: column code dictionaries too large");
+            P.n_cmeta = pos;
             const size_t ncode = (size_t)A->nz + 2;
             if ((e = dmalloc(&P.d_cmeta, (size_t)pos, &P.bytes)) != hipSuccess ||
                 (e = hipMemcpy(P.d_cmeta, meta.data(), sizeof(int32_t) * meta.size(), hipMemcpyHostToDevice)) !=
@@ -464,6 +396,7 @@ int plan_stream(aijhip_mat *A) {
                     return hipfail(e, "plan: column code block lists");
                 P.n_nblocks = (int32_t)nb.size();
                 P.n_wblocks = (int32_t)wb.size();
+                for (const BlockDesc &d : wb) P.nz_wide += d.nk;
             }
             if ((e = aijhip::column_code_write(*A, wb.empty() ? P.d_blocks : P.d_nblocks, (int32_t)nb.size(),
                                                P.d_cmeta, P.d_code)) != hipSuccess ||
@@ -504,12 +437,6 @@ int plan_stream(aijhip_mat *A) {
                 (e = hipMemcpy(P.d_segperm, perm.data(), sizeof(int32_t) * perm.size(), hipMemcpyHostToDevice)) !=
                     hipSuccess)
                 return hipfail(e, "plan: segment placement");
-        }
-        if (P.tune.long_overlap && P.n_blocks > 0) {
-            if ((e = hipStreamCreateWithFlags(&P.long_stream, hipStreamNonBlocking)) != hipSuccess ||
-                (e = hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming)) != hipSuccess ||
-                (e = hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming)) != hipSuccess)
-                return hipfail(e, "plan: long-row stream");
         }
     }
     return AIJHIP_OK;
@@ -577,7 +504,6 @@ int plan_build(aijhip_mat *A) {
         if (P.tune.geom < 0) P.tune.geom = (scattered && !sorted) ? 1 : 6;
         if (P.tune.nt < 0) P.tune.nt = (scattered && !sorted) ? 1 : 0;
     }
-    if (P.tune.group < 0) P.tune.group = 0;  // automatic choice: off until measured
     if (P.tune.codes < 0) P.tune.codes = 0;  // automatic: tried below (STREAM)
     if (P.tune.patterns < 0) P.tune.patterns = 0;
     switch (kernel) {
@@ -593,7 +519,7 @@ int plan_build(aijhip_mat *A) {
             // short rows (a stencil: no per-entry column at all).
             const aijhip::Tuning &rq = A->requested_tune;
             if ((auto_codes || auto_patterns) && !A->compressed && rq.gsort <= 0 && (rq.geom < 0 || rq.geom == 6) &&
-                rq.xtile <= 0 && rq.group <= 0 && rq.persist == 0 && !rq.xcd && !rq.clamped && rq.nt <= 1) {
+                rq.xtile <= 0 && rq.nt <= 1) {
                 const aijhip::Tuning keep = P.tune;
                 if (auto_codes) P.tune.codes = 1;
                 if (auto_patterns) P.tune.patterns = 1;
@@ -618,7 +544,6 @@ int plan_build(aijhip_mat *A) {
                 P.tune.gsort = 0;
                 if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
                 if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
-                if (P.tune.group < 0) P.tune.group = 0;
                 if (P.tune.codes < 0) P.tune.codes = 0;
                 if (P.tune.patterns < 0) P.tune.patterns = 0;
                 rc = plan_stream(A);
@@ -888,6 +813,29 @@ int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa) {
 }
 }  // namespace aijhip
 
+namespace {
+// Compulsory bytes of one MatMult under the plan in effect: the arrays the
+// launched kernels stream (each read once), x read once, y written once —
+// SURVEY §8d's count for the layout actually read. Block descriptors,
+// dictionaries and pattern tables are included where the layout needs them.
+int64_t layout_bytes(const aijhip_mat &A) {
+    const aijhip::Plan &P = A.plan;
+    const int64_t m = A.m, n = A.n, nz = A.nz;
+    const int64_t rows = A.compressed ? (4 * ((int64_t)A.n_crow + 1) + 4 * (int64_t)A.n_crow) : 4 * (m + 1);
+    const int64_t vec = 8 * n + 8 * m;
+    if (P.kernel != AIJHIP_KERNEL_STREAM) return 12 * nz + rows + vec;
+    if (P.d_pid)  // aa, ai, a pattern id per row and the offset table
+        return 8 * nz + rows + m + 4 * (int64_t)P.n_ptab + vec;
+    if (P.d_code)  // coded entries 10 B, blocks launched from aj 12 B, the dictionaries
+        return 10 * (nz - P.nz_wide) + 12 * P.nz_wide + rows + vec + 4 * P.n_cmeta;
+    if (P.d_sidx)  // 16-bit columns and slots per entry pair (4 B per entry), sorted values, block bases
+        return 12 * nz + rows + vec + 4 * (int64_t)(P.n_blocks - P.n_wblocks);
+    if (P.d_sslot)  // sorted 32-bit columns + sorted values + 16-bit slots
+        return 14 * nz + rows + vec;
+    return 12 * nz + rows + vec;
+}
+}  // namespace
+
 extern "C" {
 
 int aijhip_abi_version(void) { return AIJHIP_ABI_VERSION; }
@@ -954,34 +902,25 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             t.geom = value;
             break;
         case AIJHIP_OPT_XCD_REMAP:
-            if (value < 0) return fail(AIJHIP_ERR_ARG, "xcd_remap: 0 off, 1 contiguous, >= 2 chunk");
-            t.xcd = value != 0;
-            t.xchunk = value >= 2 ? value : 0;
-            break;
+        case AIJHIP_OPT_PERSISTENT:
+        case AIJHIP_OPT_CLAMPED_LOADS:
+        case AIJHIP_OPT_LONG_OVERLAP:
+        case AIJHIP_OPT_ROW_GROUP:
+            return fail(AIJHIP_ERR_ARG, "option " + std::to_string(option) +
+                                            " was withdrawn in ABI 2 (measured slower; DESIGN.md §5)");
         case AIJHIP_OPT_NT_LOADS:
-            if (value < -1 || value > 5) return fail(AIJHIP_ERR_ARG, "nt_loads: -1 (auto), 0..5");
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "nt_loads: -1 (auto), 0, 1");
             t.nt = value;
             break;
-        case AIJHIP_OPT_PERSISTENT:
-            if (value < 0 || value > 16) return fail(AIJHIP_ERR_ARG, "persistent: 0..16 workgroups per CU");
-            t.persist = value;
-            break;
-        case AIJHIP_OPT_CLAMPED_LOADS: t.clamped = value != 0; break;
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
         case AIJHIP_OPT_X_TILE:
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "x_tile: -1 auto, 0 off, 1 on");
             t.xtile = value;
             break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
-        case AIJHIP_OPT_LONG_OVERLAP: t.long_overlap = value != 0; break;
         case AIJHIP_OPT_HOST_PIPELINE:
             if (value < -1) return fail(AIJHIP_ERR_ARG, "host_pipeline: -1 auto, 0 serial, k > 0 chunk rows");
             t.host_chunk = value;
-            break;
-        case AIJHIP_OPT_ROW_GROUP:
-            if (value < -1 || value > 2)
-                return fail(AIJHIP_ERR_ARG, "row_group: -1 auto, 0 off, 1 on (256 lanes), 2 on (512 lanes)");
-            t.group = value;
             break;
         case AIJHIP_OPT_GATHER_SORT:
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "gather_sort: -1 auto, 0 off, 1 on");
@@ -1176,17 +1115,18 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->mult_flops = 2.0 * (double)A->nz - (double)A->nonzerorowcnt;
     info->mult_bytes = 12 * A->nz + 4 * ((int64_t)A->m + 1) + 8 * (int64_t)A->n + 8 * (int64_t)A->m;
     info->stream_geometry = A->plan.tune.geom;
-    info->xcd_remap = A->plan.tune.xcd ? (A->plan.tune.xchunk ? A->plan.tune.xchunk : 1) : 0;
+    info->xcd_remap = 0;
     info->nt_loads = A->plan.tune.nt;
     info->stream_threads = aijhip::kStreamGeoms[A->plan.tune.geom].threads;
     info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
-    info->persistent = A->plan.tune.persist;
+    info->persistent = 0;
     info->exact = A->plan.tune.exact ? 1 : 0;
     info->x_tiled_blocks = A->plan.n_xtiled;
     info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
     info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
     info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
+    info->mult_layout_bytes = layout_bytes(*A);
     return AIJHIP_OK;
 }
 

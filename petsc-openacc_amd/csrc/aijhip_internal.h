@@ -84,27 +84,23 @@ struct RowList {
 };
 
 // Speed-only knobs (aijhip_mat_set_option); they never change results.
-// Defaults are the fastest measured on MI355X at 300^3 (profiles/r01/):
-// geometry 6 with predicated loads (style study), round-robin block placement
-// (XCD-contiguous runs were 5-10 % slower), plain loads (non-temporal 2-3 %
-// slower), non-persistent grid (the pipelined persistent form was 7 % slower).
+// Defaults are the fastest measured on MI355X: geometry 6 for
+// short rows and for long rows whose gathers run along x lines, geometry 1 for
+// scattered long rows; plain loads except for those (non-temporal); hardware
+// round-robin block placement. The A/B-only variants measured slower
+// (XCD-contiguous placement, the persistent pipelined grid, clamped loads,
+// register row groups, a side stream for the long rows) were withdrawn in
+// ABI 2; profiles/r01-r03 keep their records.
 struct Tuning {
     int geom = -1;       // index into kStreamGeoms; -1 = by row length and gather locality (6 or 1)
-    bool xcd = false;    // XCD-aware block remap
-    int xchunk = 0;      //   chunk of the chunked remap (0 = contiguous runs)
     int nt = -1;         // matrix loads: -1 by gather locality (non-temporal for scattered long rows),
-                         // 0 plain, 1 non-temporal, 2 aj first + aa non-temporal, 3 aj first
-    int persist = 0;     // >0: persistent pipelined STREAM, this many workgroups per CU
-    bool clamped = false;  // branch-free clamped loads instead of predicated loads
+                         // 0 plain, 1 non-temporal
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
     int xtile = 0;         // x staged in LDS per block: 0 off (measured default), 1 where it fits,
                            // -1 when half the blocks fit
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
-    bool long_overlap = false;  // long-row segments on a side stream, concurrent with the row blocks
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
-    int group = -1;        // register row-group kernel for blocks of mean row length >= kGroupMinMean
-                           // (plain MatMult / MatMultAdd, exact = 0): -1 auto, 0 off, 1 on
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
                            // (operands with scattered gathers, caller's handles), 0 off, 1 on
     int codes = -1;        // 16-bit column codes instead of aj (Plan::d_code): -1 auto (where the
@@ -150,12 +146,6 @@ constexpr int kBatchMinMean = 16;
 // run along lines (geometry 6). Measured: 7-pt 0.73, GAMG coarse operators
 // 0.51-0.68, skewed stand-in 0.40, FEM-structured stand-in 0.17.
 constexpr double kScatteredLinesPerEntry = 0.25;
-// Row blocks whose mean row length is at least this are eligible for the
-// register row-group kernel (Tuning::group): L lanes per row accumulate
-// strided 16-B pairs in registers, no LDS product buffer.
-constexpr int kGroupMinMean = 24;
-constexpr int kGroupThreads = 256;
-
 struct Plan {
     int kernel = AIJHIP_KERNEL_STREAM;
     int lanes = 0;
@@ -173,19 +163,10 @@ struct Plan {
     // the s % 8-th eighth of x, so each XCD's L2 holds the x range its
     // scattered gathers hit (speed only; partials and their order unchanged)
     int32_t *d_segperm = nullptr;
-    // Tuning::long_overlap: the long-row kernels run on a side stream forked
-    // from and joined back to the caller's stream around the STREAM launch
-    hipStream_t long_stream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // x tiles: per block the first column and the span of its columns, or
     // span -1 when they do not fit the block's LDS (gathers from HBM)
     int2 *d_xrange = nullptr;
     int32_t n_xtiled = 0;
-    // Tuning::group: the row blocks split into the LDS STREAM ones (d_sblocks)
-    // and the register row-group ones (d_gblocks), for the plain MatMult /
-    // MatMultAdd launch; d_blocks keeps all of them (fused epilogues)
-    BlockDesc *d_sblocks = nullptr, *d_gblocks = nullptr;
-    int32_t n_sblocks = 0, n_gblocks = 0;
     // Tuning::gsort: each row block's entries sorted by column (columns,
     // values) and their positions in the block (the products' LDS slots)
     int32_t *d_saj = nullptr;
@@ -202,23 +183,20 @@ struct Plan {
     // d_wblocks, launched from the original arrays
     BlockDesc *d_nblocks = nullptr, *d_wblocks = nullptr;
     int32_t n_nblocks = 0, n_wblocks = 0;
+    int64_t nz_wide = 0;  // entries of the d_wblocks (read from aj / aa)
     // Tuning::codes: one 16-bit code per entry (nz + 2, pairs read as one
     // 4-B word) and d_cmeta = per coded block {dictionary start, size} then
     // the dictionaries; the coded blocks are d_blocks, or d_nblocks with the
     // others in d_wblocks (launched from aj) when some do not fit
     uint16_t *d_code = nullptr;
     int32_t *d_cmeta = nullptr;
+    int64_t n_cmeta = 0;  // int32 words of d_cmeta (per-block meta + dictionaries)
     // Tuning::patterns: a pattern id per row and the pattern table (start |
     // length << 16 per pattern, then the offsets); geometry 6, full rows
     uint8_t *d_pid = nullptr;
     int32_t *d_ptab = nullptr;
     int32_t n_ptab = 0, n_pat = 0;
-    bool pat_ai = true;  // row starts from ai; AIJHIP_PAT_AI=0 at planning: from the lengths' scan (A/B)
-    bool pat_w16 = false;    // AIJHIP_PAT_W16=1 at planning: one 16-B LDS write per staged pair (A/B, slower)
-    bool pat_nb = false;     // AIJHIP_PAT_NB=1 at planning: x[r +- 1] from neighbouring lanes (A/B)
-    bool pat_bf = false;     // AIJHIP_PAT_BF=1 at planning: branch-free gathers (A/B, measured slower)
     int32_t pat_dmax = 0;    // largest |column - row| offset in the table (the stencil's plane distance)
-    int32_t pat_xchunk = 0;  // XCD chunk of the row-pattern launch: 0 hardware order, -1 contiguous, C > 0 chunked
     // MERGE: merge-path start coordinate of every tile (+1 sentinel)
     int2 *d_tile_coord = nullptr;
     int32_t n_tiles = 0;
@@ -232,7 +210,7 @@ struct Plan {
 
 struct aijhip_mat {
     int device = 0;
-    int n_cu = 256;  // compute units of the device (persistent grids)
+    int n_cu = 256;  // compute units of the device
     int32_t m = 0, n = 0;
     int64_t nz = 0;
     int32_t nonzerorowcnt = 0;

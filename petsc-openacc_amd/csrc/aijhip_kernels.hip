@@ -39,30 +39,11 @@
 namespace aijhip {
 namespace {
 
-// Blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH §Workgroup
-// dispatch). Give each XCD a contiguous run of row blocks so the x window of
-// a 7-point stencil (+-N^2 rows) stays inside that XCD's 4 MiB L2. Bijective
-// for any grid size; affects speed only, never results.
-__device__ __forceinline__ int xcd_remap(int bid, int nblk) {
-    const int q = nblk >> 3, r = nblk & 7;
-    const int xcd = bid & 7, local = bid >> 3;
-    return xcd * q + min(xcd, r) + local;
-}
-
-// Chunked XCD remap: logical blocks come in chunks of C consecutive blocks,
-// chunk c of every 8C-block super-chunk runs on the same XCD (dispatch slot
-// b % 8 == c). With 8C equal to the block distance between the reuses of an
-// x line (the +-N^2 stencil offsets / rows per block), the three reads of
-// each x line land in ONE XCD's L2. chunk <= 0: contiguous runs (above).
-__device__ __forceinline__ int xcd_chunk_remap(int bid, int nblk, int chunk) {
-    if (chunk <= 0) return xcd_remap(bid, nblk);
-    const int super = 8 * chunk;
-    const int full = (nblk / super) * super;
-    if (bid >= full) return bid;  // tail: identity
-    const int s = bid / super, w = bid - s * super;
-    return s * super + chunk * (w & 7) + (w >> 3);
-}
-
+// Row blocks run in launch order; the hardware deals them round-robin over
+// the 8 XCDs (MI355X_MICROARCH §Workgroup dispatch). XCD-contiguous and
+// chunked remaps of that order were measured 1-10 % slower at 300^3 (DESIGN
+// §5; withdrawn in ABI 2): the cross-XCD x re-reads they remove are served by
+// the Infinity Cache.
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
@@ -74,11 +55,8 @@ __device__ __forceinline__ T ld_stream(const T *p) {
     else return *p;
 }
 
-// CLAMPED selects the load form (tools/ablate_style.py measured both):
-//  false: loads and gathers predicated on `k < k1` — lanes past the block
-//         issue no request; the compiler waits once per iteration;
-//  true:  branch-free loads, addresses clamped into the block (lanes past it
-//         re-read its last pair) — every load in flight at once.
+// Loads and gathers are predicated on `k < k1`: lanes past the block issue no
+// request (branch-free clamped loads measured slower, tools/ablate_style.py).
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops,
 // not for its outstanding global loads (__syncthreads() would add
 // s_waitcnt vmcnt(0) and drain the prefetch; cdna_hip_programming.md §8).
@@ -239,22 +217,14 @@ __device__ __forceinline__ double row_sum_seq(const double *p, int32_t n, double
     return s;
 }
 
-// NT (load mode), bits 0-1: 0 plain loads, aa/aj interleaved per iteration;
-// 1 both non-temporal; 2 all aj loads first, then aa non-temporal; 3 aj
-// first, plain. Bit 2 (SHUF): gathers in lane-stride order — the wave's
-// 128-entry window is gathered as entries [0, 64) then [64, 128) (columns
-// moved across lanes with __shfl, the values moved back to the lanes that
-// hold the pairs), so one gather instruction touches the x lines of ~64
-// consecutive entries instead of every other entry of 128: about half as
-// many distinct lines per instruction, the matrix loads still 16-B pairs.
-template <int T, int CAP, int RPT, bool CROW, bool XCD, int NTMODE, bool CLAMPED, class Op>
+// NTMODE bit 0: non-temporal matrix loads (scattered long-row operands).
+template <int T, int CAP, int RPT, bool CROW, int NTMODE, class Op>
 __global__ __launch_bounds__(T) void k_spmv_stream(
-    const BlockDesc *__restrict__ blk, int nblk, int xchunk, int exact,
+    const BlockDesc *__restrict__ blk, int nblk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, Op op, double *dpart, const int *stop, const int2 *__restrict__ xrange,
     const uint16_t *__restrict__ sslot, const int32_t *__restrict__ sbase) {
-    constexpr int NT = NTMODE & 3;
-    constexpr bool SHUF = (NTMODE & 4) != 0;
+    constexpr bool NT = (NTMODE & 1) != 0;
     // bit 3: gather-ordered blocks (Plan::d_saj/d_saa): aj/aa hold each
     // block's entries sorted by column, sslot their positions in the block,
     // where the products go; the row sums below read them in storage order
@@ -270,14 +240,12 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     // start, size} and then the dictionaries. 10 bytes per entry instead of
     // 12; the products, their slots and the sums are the plain kernel's
     constexpr bool CODES = (NTMODE & 32) != 0;
-    static_assert(!(CODES && (S16 || SORTED || SHUF || CROW || NT >= 2 || Op::kTile)),
-                  "column codes: plain full-row form only");
+    static_assert(!(CODES && (S16 || SORTED || CROW || Op::kTile)), "column codes: plain full-row form only");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     __shared__ double prod[CAP];
     __shared__ int32_t cdict[CODES ? kCodeDictMax : 1];
-    const int bid = (int)blockIdx.x;
-    const int b = XCD ? xcd_chunk_remap(bid, nblk, xchunk) : bid;
+    const int b = (int)blockIdx.x;
     const BlockDesc d = blk[b];
     int32_t nd = 0, dbase = 0;
     if constexpr (CODES) {
@@ -313,34 +281,20 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     // Phase 1: coalesced 16-B loads of aa and 8-B loads of aj from an even
     // (16-B aligned) start; the arrays carry a 2-entry tail pad.
     const int64_t kb = k0 & ~int64_t(1);
-    const int64_t klast = k1 > kb ? ((k1 - 1) & ~int64_t(1)) : kb;
     f64x2 av[ITERS];
     i32x2 cv[ITERS];
     f64x2 xv[ITERS];
-    if constexpr (NT >= 2) {  // the columns first: the gathers need only them
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            if (CLAMPED || k < k1) cv[it] = *reinterpret_cast<const i32x2 *>(aj + (CLAMPED ? min(k, klast) : k));
-        }
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            if (CLAMPED || k < k1)
-                av[it] = ld_stream<NT == 2>(reinterpret_cast<const f64x2 *>(aa + (CLAMPED ? min(k, klast) : k)));
-        }
-    } else {
+    {
         uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            if (CLAMPED || k < k1) {
-                const int64_t kc = CLAMPED ? min(k, klast) : k;
-                av[it] = ld_stream<NT == 1>(reinterpret_cast<const f64x2 *>(aa + kc));
+            if (k < k1) {
+                av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
                 if constexpr (CODES)
-                    cw[it] = ld_stream<NT == 1>(reinterpret_cast<const uint32_t *>(aj) + (kc >> 1));
+                    cw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aj) + (k >> 1));
                 else
-                    cv[it] = ld_stream<NT == 1>(reinterpret_cast<const i32x2 *>(aj + kc));
+                    cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
             }
         }
         if constexpr (CODES) {
@@ -405,32 +359,11 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             __syncthreads();
         }
     }
-    if constexpr (CODES) {
-        // gathered with the decode above
-    } else if constexpr (SHUF && !Op::kTile) {
-        const int lane = t & 63;
-        const int half = lane >> 1;
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            // first pair index of this wave's window in this iteration
-            const int64_t kw = kb + 2 * (int64_t)((t & ~63) + it * T);
-            const int ca0 = __shfl(cv[it].x, half, 64), ca1 = __shfl(cv[it].y, half, 64);
-            const int cb0 = __shfl(cv[it].x, 32 + half, 64), cb1 = __shfl(cv[it].y, 32 + half, 64);
-            const int ca = (lane & 1) ? ca1 : ca0, cb = (lane & 1) ? cb1 : cb0;
-            // an entry is gathered when the lane holding its pair loaded it
-            const bool va = CLAMPED || kw + 2 * half < k1, vb = CLAMPED || kw + 2 * (32 + half) < k1;
-            const double xa = va ? op.gx(ca) : 0.0, xb = vb ? op.gx(cb) : 0.0;
-            const int e0 = (2 * lane) & 63, e1 = (2 * lane + 1) & 63;
-            const double a0 = __shfl(xa, e0, 64), b0 = __shfl(xb, e0, 64);
-            const double a1 = __shfl(xa, e1, 64), b1 = __shfl(xb, e1, 64);
-            xv[it].x = lane < 32 ? a0 : b0;
-            xv[it].y = lane < 32 ? a1 : b1;
-        }
-    } else {
+    if constexpr (!CODES) {  // (the coded form gathered with the decode above)
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            if (CLAMPED || k < k1) {
+            if (k < k1) {
                 if (tiled) {
                     xv[it].x = prod[cv[it].x - xr.x];
                     xv[it].y = prod[cv[it].y - xr.x];
@@ -521,29 +454,20 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // s += aa * x in storage order from s = seed — the arithmetic and order of
 // the STREAM kernel's phase 1 + phase 2, so the result is bit-identical.
 // ptab: [0, npat) = start | len << 16 of each pattern's offsets, then the
-// offsets; ntab entries in all (<= kPatTableMax).
-// SCAN: the rows' starts are the block's k0 plus the prefix sums of their
-// patterns' lengths (a wave scan and the wave totals through LDS), so ai is
-// not read at all; otherwise from ai (A/B).
-template <int T, int CAP, bool SCAN, class Op, bool NT = false, bool BF = false, bool NB = false, bool W16 = false>
+// offsets; ntab entries in all (<= kPatTableMax). The row starts come from
+// ai (a scan of the patterns' lengths, branch-free 8-slot gathers, x[r +- 1]
+// from the neighbouring lanes, one 16-B LDS write per pair and XCD-chunked
+// block placement were all measured slower: DESIGN §5, profiles/r03/patterns/).
+template <int T, int CAP, class Op>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
                                                     int ntab, int npat, const double *__restrict__ aa, Op op,
-                                                    double *dpart, const int *stop, int xchunk = 0) {
+                                                    double *dpart, const int *stop) {
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int TPT = (kPatTableMax + T - 1) / T;
-    // W16 (A/B, AIJHIP_PAT_W16=1): the staged values sit at (k - kb), kb =
-    // the even start of the block's pairs, so every pair is one aligned 16-B
-    // LDS write (slots outside [k0, k1) hold neighbours' values, never read).
-    // Measured slower at 300^3: 403.3 vs 360.7 us with two 8-B writes at
-    // (k - k0) (profiles/r03/patterns/patw16_poisson.jsonl)
-    __shared__ __attribute__((aligned(16))) double av[W16 ? CAP + 2 : CAP];
+    __shared__ double av[CAP];
     __shared__ int32_t tab[kPatTableMax];
-    __shared__ int32_t wsum[T / 64];
-    // xchunk (Plan::pat_xchunk): the XCD placement of the row blocks — a
-    // bijection, so the dot partials keep their logical slots and order
-    const int b = xchunk == 0 ? (int)blockIdx.x
-                              : xcd_chunk_remap((int)blockIdx.x, (int)gridDim.x, xchunk < 0 ? 0 : xchunk);
+    const int b = (int)blockIdx.x;
     const BlockDesc d = blk[b];
     if ((stop ? *stop : 0) != 0 || d.nk < 0) return;
     const int t = threadIdx.x;
@@ -555,11 +479,7 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     const bool own = t < d.nrows;
     const int r = d.row0 + min(t, d.nrows - 1);
     const int p = min((int)pid[r], npat - 1);
-    int32_t rs = 0, n = 0;
-    if constexpr (!SCAN) {
-        rs = rai[r];
-        n = rai[r + 1] - rs;
-    }
+    const int32_t rs = rai[r], n = rai[r + 1] - rs;
     const double seed = op.seed(r);
     // the block's values: 16-B loads from an even start (2-entry tail pad)
     const int64_t kb = k0 & ~int64_t(1);
@@ -567,20 +487,7 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if (k < k1) a2[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
-    }
-    int32_t pm = 0, excl = 0;
-    if constexpr (SCAN) {
-        pm = ptab[p];  // (the table is L2-resident)
-        n = own ? pm >> 16 : 0;
-        int32_t inc = n;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t v = __shfl_up(inc, o, 64);
-            if ((t & 63) >= o) inc += v;
-        }
-        excl = inc - n;
-        if ((t & 63) == 63) wsum[t >> 6] = inc;
+        if (k < k1) a2[it] = *reinterpret_cast<const f64x2 *>(aa + k);
     }
 #pragma unroll
     for (int i = 0; i < TPT; ++i)
@@ -588,77 +495,26 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        if constexpr (W16) {
-            if (k < k1) *reinterpret_cast<f64x2 *>(av + (k - kb)) = a2[it];
-        } else if (k < k1) {
+        if (k < k1) {
             if (k >= k0) av[k - k0] = a2[it].x;
             if (k + 1 < k1) av[k + 1 - k0] = a2[it].y;
         }
     }
     __syncthreads();
     double dv[Op::kDots > 0 ? Op::kDots : 1] = {};
-    if constexpr (SCAN) {
-        for (int w = 0; w < (t >> 6); ++w) excl += wsum[w];
-        rs = (int32_t)k0 + excl;
-    } else {
-        pm = tab[p];
-    }
-    // NB (A/B, AIJHIP_PAT_NB=1): x[r - 1] and x[r + 1] taken from the
-    // neighbouring lanes' x[r] (rows are consecutive lanes), gathered only by
-    // the lanes at a wave's or the block's edge
-    double xd = 0.0, xl = 0.0, xr = 0.0;
-    if constexpr (NB) {
-        xd = op.gx(r);
-        xl = __shfl_up(xd, 1, 64);
-        xr = __shfl_down(xd, 1, 64);
-    }
+    const int32_t pm = tab[p];
     if (own) {
         const int32_t *off = tab + (pm & 0xffff);
-        const double *ar = av + (rs - (W16 ? kb : k0));
+        const double *ar = av + (rs - k0);
         double s = seed;
-        if constexpr (NB) {
-            const bool okl = (t & 63) != 0, okr = (t & 63) != 63 && t + 1 < d.nrows;
-            for (int32_t j0 = 0; j0 < n; j0 += 8) {
-                double xv[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j0 + j < n) {
-                        const int32_t o = off[j0 + j];
-                        xv[j] = o == 0 ? xd : (o == -1 && okl) ? xl : (o == 1 && okr) ? xr : op.gx(r + o);
-                    }
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j0 + j < n) s += ar[j0 + j] * xv[j];
-            }
-        } else if constexpr (!BF) {  // predicated gathers (default; the branch-free form below: AIJHIP_PAT_BF=1)
-            for (int32_t j0 = 0; j0 < n; j0 += 8) {
-                double xv[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j0 + j < n) xv[j] = op.gx(r + off[j0 + j]);
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    if (j0 + j < n) s += ar[j0 + j] * xv[j];
-            }
-        } else
         for (int32_t j0 = 0; j0 < n; j0 += 8) {
-            // branch-free (A/B): slots past the row's end repeat its last
-            // entry (loaded, not summed), so the 8 offset reads, the 8
-            // gathers and the 8 value reads issue back to back under one wait
-            // each. Measured slower at 300^3 (370.4 vs 360.3 us,
-            // profiles/r03/patterns/patbf_poisson.jsonl): the 8th gather of a
-            // 7-entry row is a wasted load
-            const int32_t last = n - 1 - j0;
-            int32_t o[8];
-            double xv[8], av8[8];
+            double xv[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = off[j0 + min(j, last)];
+            for (int j = 0; j < 8; ++j)
+                if (j0 + j < n) xv[j] = op.gx(r + off[j0 + j]);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) xv[j] = op.gx(r + o[j]);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) av8[j] = ar[j0 + min(j, last)];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) s = j <= last ? s + av8[j] * xv[j] : s;
+            for (int j = 0; j < 8; ++j)
+                if (j0 + j < n) s += ar[j0 + j] * xv[j];
         }
         op.put(r, s, dv);
     }
@@ -668,81 +524,6 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
             const double v = block_sum<T>(dv[q], av);
             if (t == 0) dpart[(int64_t)q * gridDim.x + b] = v;
         }
-    }
-}
-
-// Persistent, software-pipelined STREAM: a resident grid walks the row blocks
-// round-robin (b, b + grid, ...). The aa/aj loads of the NEXT block are issued
-// before the barrier and stay in flight while the lanes reduce the current
-// block out of LDS, so the memory pipe never drains at block boundaries.
-// Same arithmetic as k_spmv_stream (bit-identical results).
-template <int T, int CAP, bool ADD, bool CROW, bool NT>
-__global__ __launch_bounds__(T) void k_spmv_stream_pipe(
-    const BlockDesc *__restrict__ blk, int nblk, const int32_t *__restrict__ rai,
-    const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, const double *__restrict__ x,
-    const double *z, double *y) {
-    constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
-    __shared__ double prod[CAP];
-    const int t = threadIdx.x;
-    int b = blockIdx.x;
-    if (b >= nblk) return;
-    BlockDesc d = blk[b];
-    f64x2 av[ITERS];
-    i32x2 cv[ITERS];
-    // Every load is unconditional (lanes past the block re-read its last
-    // pair, an L1 hit), so the number of loads in flight is static and the
-    // compiler's s_waitcnt before the reduction can leave the prefetch alone.
-    auto issue = [&](const BlockDesc &dd) {
-        const int64_t kb = (int64_t)dd.k0 & ~int64_t(1), k1 = (int64_t)dd.k0 + dd.nk;
-        const int64_t klast = k1 > kb ? ((k1 - 1) & ~int64_t(1)) : kb;
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int64_t k = min(kb + 2 * (int64_t)(t + it * T), klast);
-            av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
-            cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
-        }
-    };
-    issue(d);
-    for (;;) {
-        const bool own = t < d.nrows;
-        const int r = d.row0 + min(t, d.nrows - 1);
-        const int32_t rs = rai[r], re = rai[r + 1];
-        const int orow = CROW ? ridx[r] : r;
-        double sum = ADD ? z[orow] : 0.0;
-        const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk, kb = k0 & ~int64_t(1);
-        // all x gathers of the block in flight at once, then the LDS stores
-        f64x2 pv[ITERS];
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            pv[it].x = x[cv[it].x];
-            pv[it].y = x[cv[it].y];
-        }
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            const double p0 = av[it].x * pv[it].x;
-            const double p1 = av[it].y * pv[it].y;
-            if (k < k1) {
-                if (k >= k0) prod[k - k0] = p0;
-                if (k + 1 < k1) prod[k + 1 - k0] = p1;
-            }
-        }
-        const int bn = b + (int)gridDim.x;
-        const bool more = bn < nblk;
-        // Unconditional prefetch (the last pass re-reads its own block) keeps
-        // the in-flight count static, so the reduction waits only for rs/re.
-        const BlockDesc dn = blk[more ? bn : b];
-        issue(dn);  // in flight across the barrier and the reduction below
-        lds_barrier();
-        if (own) {
-            for (int32_t k = rs; k < re; ++k) sum += prod[k - k0];
-            y[orow] = sum;
-        }
-        if (!more) break;
-        lds_barrier();  // every lane is done reading prod before it is refilled
-        d = dn;
-        b = bn;
     }
 }
 
@@ -803,66 +584,6 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
         for (int w = 1; w < kLongThreads / 64; ++w) r += red[w];
         partials[id] = r;
     }
-}
-
-// Register row groups (Tuning::group): a workgroup takes one STREAM row block
-// of long-enough rows (mean >= kGroupMinMean) and gives each row L lanes
-// (the largest power of two <= min(64, T / rows)). Lane j of a row sums the
-// row's 16-B pairs j, j + L, j + 2L, ... (U pairs in flight) into two
-// registers; the row's lanes combine with __shfl_xor. No LDS product buffer,
-// no barrier and no serial per-row phase: the LDS STREAM block holds 32 KiB
-// and reduces each row on one lane, which leaves ~1/8 of its lanes working
-// on rows of 45-100 entries. The sum is reordered (within the fp64 bound of
-// SURVEY §8d) and deterministic (L and the pair order follow the plan).
-template <int T, bool ADD, bool NT>
-__global__ __launch_bounds__(T) void k_spmv_rowgroup(const BlockDesc *__restrict__ blk,
-                                                     const int32_t *__restrict__ rai,
-                                                     const int32_t *__restrict__ aj,
-                                                     const double *__restrict__ aa,
-                                                     const double *__restrict__ x, const double *z, double *y,
-                                                     const int *stop) {
-    constexpr int U = 4;
-    const BlockDesc d = blk[blockIdx.x];
-    if ((stop ? *stop : 0) != 0) return;
-    const int t = threadIdx.x, nr = d.nrows;
-    const int cap = min(64, T / max(nr, 1));
-    int L = 1;
-    while (L * 2 <= cap) L *= 2;
-    const int g = t / L, j = t - g * L;
-    const bool own = g < nr;
-    const int r = d.row0 + min(g, nr - 1);
-    const int64_t rs = rai[r], re = rai[r + 1];
-    double acc0 = 0.0, acc1 = 0.0;
-    if (own) {
-        for (int64_t k = (rs & ~int64_t(1)) + 2 * j; k < re; k += (int64_t)2 * L * U) {
-            f64x2 a[U];
-            i32x2 c[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t kk = k + (int64_t)2 * L * u;
-                if (kk < re) {
-                    a[u] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + kk));
-                    c[u] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + kk));
-                }
-            }
-            double x0[U], x1[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t kk = k + (int64_t)2 * L * u;
-                x0[u] = (kk < re && kk >= rs) ? x[c[u].x] : 0.0;
-                x1[u] = (kk + 1 < re) ? x[c[u].y] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const int64_t kk = k + (int64_t)2 * L * u;
-                if (kk < re && kk >= rs) acc0 += a[u].x * x0[u];
-                if (kk + 1 < re) acc1 += a[u].y * x1[u];
-            }
-        }
-    }
-    double sv = acc0 + acc1;
-    for (int off = L >> 1; off > 0; off >>= 1) sv += __shfl_xor(sv, off, 64);
-    if (own && j == 0) st_stream(y + r, ADD ? z[r] + sv : sv);
 }
 
 // One wavefront per long row: the lanes load 64 partials at once and the sum
@@ -1402,22 +1123,33 @@ __global__ __launch_bounds__(256) void k_pat_hash(int32_t m, const int32_t *__re
 // Distinct hashes into an open-addressing table of `ts` slots (a power of
 // two): a lane whose wave neighbour holds the same hash leaves the insert to
 // it, and a slot already holding the hash is read before any CAS, so the
-// ~all-interior rows of a stencil cost one atomic per new pattern.
+// ~all-interior rows of a stencil cost one atomic per new pattern. Every
+// successful insert is counted (counts[0]); once more than kPatMax distinct
+// hashes are in, the operand cannot use row patterns: the inserting lane
+// raises `overflow` and every lane that sees it leaves, so a large
+// unstructured operand costs ~kPatMax inserts, not m walks of a full table
+// (ADVICE r03).
 constexpr int kPatTableSlots = 4096;
 __global__ __launch_bounds__(256) void k_pat_insert(int32_t m, const unsigned long long *__restrict__ hash,
-                                                    unsigned long long *table, int *overflow) {
+                                                    unsigned long long *table, int *overflow, int *count) {
     const int32_t r = blockIdx.x * 256 + threadIdx.x;
     const unsigned long long h = r < m ? hash[r] : 0ull;
     const unsigned long long hp = __shfl_up(h, 1, 64);
     if (r >= m || ((threadIdx.x & 63) != 0 && hp == h)) return;
+    if (__atomic_load_n(overflow, __ATOMIC_RELAXED)) return;
     unsigned int slot = (unsigned int)(h >> 20) & (kPatTableSlots - 1);
     for (int probe = 0; probe < kPatTableSlots; ++probe) {
         const unsigned long long cur = __atomic_load_n(table + slot, __ATOMIC_RELAXED);
         if (cur == h) return;
         if (cur == 0ull) {
             const unsigned long long prev = atomicCAS(table + slot, 0ull, h);
-            if (prev == 0ull || prev == h) return;
+            if (prev == h) return;
+            if (prev == 0ull) {
+                if (atomicAdd(count, 1) >= kPatMax) atomicExch(overflow, 1);
+                return;
+            }
         }
+        if ((probe & 15) == 15 && __atomic_load_n(overflow, __ATOMIC_RELAXED)) return;
         slot = (slot + 1) & (kPatTableSlots - 1);
     }
     atomicExch(overflow, 1);
@@ -1479,12 +1211,12 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
     };
     if ((e = hipMalloc(&d_hash, sizeof(unsigned long long) * (size_t)m)) != hipSuccess ||
         (e = hipMalloc(&d_table, sizeof(unsigned long long) * kPatTableSlots)) != hipSuccess ||
-        (e = hipMalloc(&d_flag, sizeof(int) * 2)) != hipSuccess ||
+        (e = hipMalloc(&d_flag, sizeof(int) * 3)) != hipSuccess ||
         (e = hipMemset(d_table, 0, sizeof(unsigned long long) * kPatTableSlots)) != hipSuccess ||
-        (e = hipMemset(d_flag, 0, sizeof(int) * 2)) != hipSuccess)
+        (e = hipMemset(d_flag, 0, sizeof(int) * 3)) != hipSuccess)
         return done(e);
     hipLaunchKernelGGL(k_pat_hash, dim3(g), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, d_hash);
-    hipLaunchKernelGGL(k_pat_insert, dim3(g), dim3(256), 0, nullptr, m, d_hash, d_table, d_flag);
+    hipLaunchKernelGGL(k_pat_insert, dim3(g), dim3(256), 0, nullptr, m, d_hash, d_table, d_flag, d_flag + 2);
     std::vector<unsigned long long> table(kPatTableSlots);
     int flag[2] = {0, 0};
     if ((e = hipGetLastError()) != hipSuccess ||
@@ -1676,71 +1408,41 @@ template <int T, int CAP, int RPT>
 static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L, const double *x,
                             const double *z, double *y, bool add, hipStream_t s, double *dpart,
                             const int *stop) {
-#define AIJHIP_SL(ADD, CROW, XCD, NT, CL)                                                          \
-    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, XCD, NT, CL, OpMult<ADD>>), dim3(P.n_blocks), \
-                       dim3(T), 0, s, P.d_blocks, P.n_blocks, P.tune.xchunk, (int)P.tune.exact,   \
-                       L.rai, L.ridx, A.d_aj, A.d_aa,                                              \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, nullptr); \
+    constexpr bool kGeom6 = T == kStreamGeoms[6].threads && CAP == kStreamGeoms[6].nnz_cap && RPT == 1;
+#define AIJHIP_SL(ADD, CROW, NT)                                                                             \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, NT, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
+                       P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,             \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, nullptr);       \
     return
     // Row patterns (Plan::d_pid; geometry 6, full-row lists, short rows)
-    if constexpr (RPT == 1 && ((T == 512 && CAP == 4094) || (T == 256 && CAP == 2046) || (T == 1024 && CAP == 8190))) {
+    if constexpr (kGeom6) {
         if (P.d_pid && !L.ridx) {
-#define AIJHIP_PT(ADD, SC)                                                                                   \
-    hipLaunchKernelGGL((k_spmv_pattern<T, CAP, SC, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, \
-                       L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,                                     \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);                      \
+#define AIJHIP_PT(ADD)                                                                                     \
+    hipLaunchKernelGGL((k_spmv_pattern<T, CAP, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, \
+                       L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,                                 \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop);                                \
     return
-            if (add) {
-                if (P.pat_ai) { AIJHIP_PT(true, false); }
-                AIJHIP_PT(true, true);
-            }
-            if (P.pat_ai && P.pat_w16) {  // A/B: one 16-B LDS write per pair
-                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, false, false, true>),
-                                   dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab,
-                                   P.n_pat, A.d_aa, OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop,
-                                   P.pat_xchunk);
-                return;
-            }
-            if (P.pat_ai && P.pat_nb) {  // A/B: x[r +- 1] from the neighbouring lanes
-                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, false, true>), dim3(P.n_blocks),
-                                   dim3(T), 0, s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
-                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);
-                return;
-            }
-            if (P.pat_ai && P.pat_bf) {  // A/B: the branch-free gathers
-                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, false, true>), dim3(P.n_blocks),
-                                   dim3(T), 0, s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
-                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);
-                return;
-            }
-            if (P.pat_ai && P.tune.nt == 1) {  // A/B: non-temporal aa loads
-                hipLaunchKernelGGL((k_spmv_pattern<T, CAP, false, OpMult<false>, true>), dim3(P.n_blocks), dim3(T), 0,
-                                   s, P.d_blocks, L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,
-                                   OpMult<false>{x, z, y, dpart != nullptr}, dpart, stop, P.pat_xchunk);
-                return;
-            }
-            if (P.pat_ai) { AIJHIP_PT(false, false); }
-            AIJHIP_PT(false, true);
+            if (add) { AIJHIP_PT(true); }
+            AIJHIP_PT(false);
 #undef AIJHIP_PT
         }
     }
     // Column codes (Plan::d_code; geometry 6, full-row lists): MatMult,
     // MatMultAdd and the CG's fused dot; with a coded / uncoded split the dot's
     // partials would come from two launches, so that case takes aj
-    if constexpr (RPT == 1 && ((T == 512 && (CAP == 4094 || CAP == 6142)) || (T == 1024 && CAP == 8190))) {
+    if constexpr (kGeom6) {
         if (P.d_code && !L.ridx && (P.n_wblocks == 0 || !dpart)) {
             const BlockDesc *cb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
             const int32_t nc = P.n_wblocks ? P.n_nblocks : P.n_blocks;
 #define AIJHIP_SC(ADD, NTM)                                                                                       \
     if (nc > 0)                                                                                                   \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, NTM, false, OpMult<ADD>>), dim3(nc), dim3(T), 0, \
-                           s, cb, nc, 0, (int)P.tune.exact, L.rai, nullptr,                                        \
-                           reinterpret_cast<const int32_t *>(P.d_code), A.d_aa,                                   \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, NTM, OpMult<ADD>>), dim3(nc), dim3(T), 0, s, cb, nc, \
+                           (int)P.tune.exact, L.rai, nullptr, reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, \
                            OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, P.d_cmeta);     \
     if (P.n_wblocks > 0)                                                                                          \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, 0, false, OpMult<ADD>>), dim3(P.n_wblocks),  \
-                           dim3(T), 0, s, P.d_wblocks, P.n_wblocks, 0, (int)P.tune.exact, L.rai, nullptr, A.d_aj, \
-                           A.d_aa, OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);        \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, s, \
+                           P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,           \
+                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);                \
     return
             if (add) {
                 if (P.tune.nt == 1) { AIJHIP_SC(true, 33); }
@@ -1758,16 +1460,15 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     if (P.d_sidx && (P.n_wblocks == 0 || !dpart)) {  // 16-bit columns and slots packed per pair
         const BlockDesc *nb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
         const int32_t nn = P.n_wblocks ? P.n_nblocks : P.n_blocks;
-#define AIJHIP_SS(ADD, CROW)                                                                                  \
-    if (nn > 0)                                                                                               \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, false, 16, false, OpMult<ADD>>), dim3(nn), dim3(T), 0, \
-                           s, nb, nn, 0, (int)P.tune.exact, L.rai, L.ridx,                                    \
-                           reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa,                               \
-                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, P.d_sbase); \
-    if (P.n_wblocks > 0)                                                                                      \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, false, 0, false, OpMult<ADD>>), dim3(P.n_wblocks), \
-                           dim3(T), 0, s, P.d_wblocks, P.n_wblocks, 0, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, \
-                           A.d_aa, OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);    \
+#define AIJHIP_SS(ADD, CROW)                                                                                   \
+    if (nn > 0)                                                                                                \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 16, OpMult<ADD>>), dim3(nn), dim3(T), 0, s, nb, nn, \
+                           (int)P.tune.exact, L.rai, L.ridx, reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa, \
+                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, P.d_sbase);  \
+    if (P.n_wblocks > 0)                                                                                       \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, s, \
+                           P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,         \
+                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);             \
     return
         if (add && L.ridx) { AIJHIP_SS(true, true); }
         if (add) { AIJHIP_SS(true, false); }
@@ -1776,15 +1477,14 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
 #undef AIJHIP_SS
     }
     if (P.d_sidx) {  // split plan, fused dot: the original arrays in one launch
-        if (L.ridx) { AIJHIP_SL(false, true, false, false, false); }
-        AIJHIP_SL(false, false, false, false, false);
+        if (L.ridx) { AIJHIP_SL(false, true, 0); }
+        AIJHIP_SL(false, false, 0);
     }
     if (P.d_sslot) {
-#define AIJHIP_SS(ADD, CROW)                                                                            \
-    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, false, 8, false, OpMult<ADD>>), dim3(P.n_blocks), \
-                       dim3(T), 0, s, P.d_blocks, P.n_blocks, 0, (int)P.tune.exact, L.rai, L.ridx, P.d_saj,  \
-                       P.d_saa, OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sslot,    \
-                       nullptr);                                                                        \
+#define AIJHIP_SS(ADD, CROW)                                                                                \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 8, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
+                       P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, L.ridx, P.d_saj, P.d_saa,          \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sslot, nullptr);   \
     return
         if (add && L.ridx) { AIJHIP_SS(true, true); }
         if (add) { AIJHIP_SS(true, false); }
@@ -1792,61 +1492,24 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         AIJHIP_SS(false, false);
 #undef AIJHIP_SS
     }
-    // The speed knobs (XCD remap, non-temporal, clamped loads) are compiled
-    // for the plain full-row MatMult, the benchmarked path; MatMultAdd and
-    // the compressed-row form use the default (measured-best) form.
-    if (P.d_xrange && !add && !L.ridx && !P.tune.xcd && !P.tune.nt && !P.tune.clamped) {
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, false, false, false, OpMult<false, true>>),
-                           dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, P.n_blocks, 0, (int)P.tune.exact, L.rai,
-                           nullptr, A.d_aj, A.d_aa, OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop,
-                           P.d_xrange, nullptr, nullptr);
+    // LDS x tiles: the plain full-row MatMult only
+    if (P.d_xrange && !add && !L.ridx && P.tune.nt != 1) {
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<false, true>>), dim3(P.n_blocks), dim3(T), 0,
+                           s, P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,
+                           OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop, P.d_xrange, nullptr, nullptr);
         return;
     }
-    if (add || L.ridx) {
-        if (add && L.ridx) { AIJHIP_SL(true, true, false, false, false); }
-        if (add) { AIJHIP_SL(true, false, false, false, false); }
-        AIJHIP_SL(false, true, false, false, false);
+    // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
+    // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)
+    if (P.tune.nt == 1 && !L.ridx) {
+        if (add) { AIJHIP_SL(true, false, 1); }
+        AIJHIP_SL(false, false, 1);
     }
-    if (P.tune.nt >= 2 && !P.tune.xcd && !P.tune.clamped) {  // load-order study modes, lane-stride gathers
-        if (P.tune.nt == 2) { AIJHIP_SL(false, false, false, 2, false); }
-        if (P.tune.nt == 4) { AIJHIP_SL(false, false, false, 4, false); }
-        if (P.tune.nt == 5) { AIJHIP_SL(false, false, false, 5, false); }
-        AIJHIP_SL(false, false, false, 3, false);
-    }
-    switch ((P.tune.xcd ? 4 : 0) | (P.tune.nt ? 2 : 0) | (P.tune.clamped ? 1 : 0)) {
-        case 0: AIJHIP_SL(false, false, false, false, false);
-        case 1: AIJHIP_SL(false, false, false, false, true);
-        case 2: AIJHIP_SL(false, false, false, true, false);
-        case 3: AIJHIP_SL(false, false, false, true, true);
-        case 4: AIJHIP_SL(false, false, true, false, false);
-        case 5: AIJHIP_SL(false, false, true, false, true);
-        case 6: AIJHIP_SL(false, false, true, true, false);
-        default: AIJHIP_SL(false, false, true, true, true);
-    }
+    if (add && L.ridx) { AIJHIP_SL(true, true, 0); }
+    if (add) { AIJHIP_SL(true, false, 0); }
+    if (L.ridx) { AIJHIP_SL(false, true, 0); }
+    AIJHIP_SL(false, false, 0);
 #undef AIJHIP_SL
-}
-
-template <int T, int CAP>
-static void pipe_dispatch(const aijhip_mat &A, const RowList &L, const double *x,
-                          const double *z, double *y, bool add, hipStream_t s) {
-    const Plan &P = A.plan;
-    const int grid = std::min<int64_t>(P.n_blocks, (int64_t)A.n_cu * P.tune.persist);
-    const int sel = (add ? 4 : 0) | (L.ridx ? 2 : 0) | (P.tune.nt ? 1 : 0);
-#define AIJHIP_PL(ADD, CROW, NT)                                                                \
-    hipLaunchKernelGGL((k_spmv_stream_pipe<T, CAP, ADD, CROW, NT>), dim3(grid), dim3(T), 0, s, \
-                       P.d_blocks, P.n_blocks, L.rai, L.ridx, A.d_aj, A.d_aa, x, z, y);         \
-    break
-    switch (sel) {
-        case 0: AIJHIP_PL(false, false, false);
-        case 1: AIJHIP_PL(false, false, true);
-        case 2: AIJHIP_PL(false, true, false);
-        case 3: AIJHIP_PL(false, true, true);
-        case 4: AIJHIP_PL(true, false, false);
-        case 5: AIJHIP_PL(true, false, true);
-        case 6: AIJHIP_PL(true, true, false);
-        default: AIJHIP_PL(true, true, true);
-    }
-#undef AIJHIP_PL
 }
 
 #define AIJHIP_GEOM(G) kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap, \
@@ -1854,8 +1517,7 @@ static void pipe_dispatch(const aijhip_mat &A, const RowList &L, const double *x
 
 bool stream_dot_fusable(const aijhip_mat &A) {
     const Plan &P = A.plan;
-    return P.kernel == AIJHIP_KERNEL_STREAM && !A.compressed && P.n_longs == 0 && P.tune.persist == 0 &&
-           A.m == A.n;
+    return P.kernel == AIJHIP_KERNEL_STREAM && !A.compressed && P.n_longs == 0 && A.m == A.n;
 }
 
 hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, double *dpart,
@@ -1873,31 +1535,26 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
-    if (P.d_pid) {  // row patterns (planned at geometry 6; 7 and 8 for A/B)
-#define AIJHIP_PO(G)                                                                                        \
-    hipLaunchKernelGGL((k_spmv_pattern<kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap, false, Op>),       \
-                       dim3(P.n_blocks), dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, A.d_ai, P.d_pid,   \
-                       P.d_ptab, P.n_ptab, P.n_pat, A.d_aa, op, dpart, stop, P.pat_xchunk)
-        if (P.tune.geom == 6) AIJHIP_PO(6);
-        else if (P.tune.geom == 7) AIJHIP_PO(7);
-        else if (P.tune.geom == 8) AIJHIP_PO(8);
-        else return hipErrorInvalidValue;
-#undef AIJHIP_PO
+    if (P.d_pid) {  // row patterns (planned at geometry 6)
+        if (P.tune.geom != 6) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((k_spmv_pattern<kStreamGeoms[6].threads, kStreamGeoms[6].nnz_cap, Op>), dim3(P.n_blocks),
+                           dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, A.d_ai, P.d_pid, P.d_ptab, P.n_ptab,
+                           P.n_pat, A.d_aa, op, dpart, stop);
         return hipGetLastError();
     }
     if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)
-        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, false, 32, false, Op>), dim3(P.n_blocks),
-                           dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex, A.d_ai, nullptr,
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, 32, Op>), dim3(P.n_blocks),
+                           dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,
                            reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, op, dpart, stop, nullptr, nullptr,
                            P.d_cmeta);
         return hipGetLastError();
     }
     static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
-#define AIJHIP_OG(G)                                                                                      \
-    case G:                                                                                               \
-        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, Op>), dim3(P.n_blocks), \
-                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, 0, ex,                \
-                           A.d_ai, nullptr, A.d_aj, A.d_aa, op, dpart, stop, nullptr, nullptr, nullptr);  \
+#define AIJHIP_OG(G)                                                                                             \
+    case G:                                                                                                      \
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_blocks),                      \
+                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr, A.d_aj, \
+                           A.d_aa, op, dpart, stop, nullptr, nullptr, nullptr);                                  \
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
@@ -1915,11 +1572,11 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
         return hipErrorInvalidValue;
     if (nb <= 0) return hipSuccess;
     static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
-#define AIJHIP_BG(G)                                                                                            \
-    case G:                                                                                                     \
-        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, false, false, false, OpMult<false>>), dim3(nb), \
-                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks + b0, nb, 0, (int)P.tune.exact,       \
-                           A.d_ai, nullptr, A.d_aj, A.d_aa, OpMult<false>{x, nullptr, y, false}, nullptr, nullptr, \
+#define AIJHIP_BG(G)                                                                                             \
+    case G:                                                                                                      \
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, OpMult<false>>), dim3(nb),                   \
+                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks + b0, nb, (int)P.tune.exact, A.d_ai,  \
+                           nullptr, A.d_aj, A.d_aa, OpMult<false>{x, nullptr, y, false}, nullptr, nullptr,       \
                            nullptr, nullptr, nullptr);                                                           \
         break
     switch (P.tune.geom) {
@@ -1959,71 +1616,12 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     if (e != hipSuccess) return e;
     const RowList L = row_list(A);
     const Plan &P = A.plan;
-    // long rows: segment partials, then their ordered sums
-    auto longs = [&](hipStream_t ls) -> hipError_t {
-        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, ls,
-                           P.d_segs, A.d_aj, A.d_aa, x, P.d_partials, P.d_segperm);
-        hipError_t le = hipGetLastError();
-        if (le != hipSuccess) return le;
-        if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, ls, P.d_longs, P.n_longs,
-                                    P.d_partials, z, y);
-        else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, ls, P.d_longs, P.n_longs,
-                                P.d_partials, z, y);
-        return hipGetLastError();
-    };
-    const bool fork = P.n_longs > 0 && P.long_stream != nullptr;
-    if (fork) {  // side stream: ordered after everything already on s
-        if ((e = hipEventRecord(P.ev_fork, s)) != hipSuccess ||
-            (e = hipStreamWaitEvent(P.long_stream, P.ev_fork, 0)) != hipSuccess ||
-            (e = longs(P.long_stream)) != hipSuccess || (e = hipEventRecord(P.ev_join, P.long_stream)) != hipSuccess)
-            return e;
-    }
     // Every geometry is dispatched explicitly: the kernel's LDS size must be
     // the one the plan's row blocks were cut for.
     static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
-    const int g = P.tune.geom;
-    if (P.n_blocks > 0 && P.tune.persist > 0 && kStreamGeoms[g].rows == kStreamGeoms[g].threads) {
-#define AIJHIP_PG(G) \
-    case G: pipe_dispatch<kStreamGeoms[G].threads, kStreamGeoms[G].nnz_cap>(A, L, x, z, y, add, s); break
-        switch (g) {
-            AIJHIP_PG(0); AIJHIP_PG(1); AIJHIP_PG(3); AIJHIP_PG(4); AIJHIP_PG(5);
-            AIJHIP_PG(6); AIJHIP_PG(7); AIJHIP_PG(8); AIJHIP_PG(9); AIJHIP_PG(10); AIJHIP_PG(11);
-            default: return hipErrorInvalidValue;
-        }
-#undef AIJHIP_PG
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if (P.n_gblocks > 0 && !dpart) {
-        // LDS STREAM blocks of short rows, then the register row groups
-        if (P.n_sblocks > 0) {
-            Plan view = P;  // the same plan over the short-row block list (a non-owning copy)
-            view.d_blocks = P.d_sblocks;
-            view.n_blocks = P.n_sblocks;
-            view.d_xrange = nullptr;
-#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, view, L, x, z, y, add, s, nullptr, stop); break
-            switch (g) {
-                AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
-                AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
-                default: return hipErrorInvalidValue;
-            }
-#undef AIJHIP_SG
-            if ((e = hipGetLastError()) != hipSuccess) return e;
-        }
-        const bool nt = P.tune.nt == 1;
-#define AIJHIP_RG(TT, ADD, NT)                                                                                \
-    hipLaunchKernelGGL((k_spmv_rowgroup<TT, ADD, NT>), dim3(P.n_gblocks), dim3(TT), 0, s, P.d_gblocks, L.rai, \
-                       A.d_aj, A.d_aa, x, z, y, stop)
-        if (P.tune.group == 2) {
-            if (add) { if (nt) AIJHIP_RG(512, true, true); else AIJHIP_RG(512, true, false); }
-            else { if (nt) AIJHIP_RG(512, false, true); else AIJHIP_RG(512, false, false); }
-        } else {
-            if (add) { if (nt) AIJHIP_RG(256, true, true); else AIJHIP_RG(256, true, false); }
-            else { if (nt) AIJHIP_RG(256, false, true); else AIJHIP_RG(256, false, false); }
-        }
-#undef AIJHIP_RG
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    } else if (P.n_blocks > 0) {
+    if (P.n_blocks > 0) {
 #define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, P, L, x, z, y, add, s, dpart, stop); break
-        switch (g) {
+        switch (P.tune.geom) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
             AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
             default: return hipErrorInvalidValue;
@@ -2031,8 +1629,18 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
 #undef AIJHIP_SG
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    if (fork) return hipStreamWaitEvent(s, P.ev_join, 0);  // join: s sees the long rows' y
-    if (P.n_longs > 0) return longs(s);
+    // long rows: segment partials, then their ordered sums (one stream: a
+    // forked side stream measured neutral)
+    if (P.n_longs > 0) {
+        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s, P.d_segs, A.d_aj, A.d_aa, x,
+                           P.d_partials, P.d_segperm);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
+                                    P.d_partials, z, y);
+        else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
+                                P.d_partials, z, y);
+        return hipGetLastError();
+    }
     return hipSuccess;
 }
 

@@ -85,7 +85,7 @@ int phip(hipError_t e, const char *what) {
 
 bool pipelinable(const aijhip_mat &A) {
     const Plan &P = A.plan;
-    return P.kernel == AIJHIP_KERNEL_STREAM && !A.compressed && P.n_longs == 0 && P.tune.persist == 0 &&
+    return P.kernel == AIJHIP_KERNEL_STREAM && !A.compressed && P.n_longs == 0 &&
            P.tune.host_chunk != 0 && P.n_blocks > 0;
 }
 

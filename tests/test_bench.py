@@ -71,7 +71,79 @@ def test_committed_rehearsal_lines_carry_the_n_gt_1_fields(name):
     assert line["cg"]["solver"] == "aijhip_kspmpi (native)" and "host_syncs" in line["cg"]
     assert line["cg_gamg"]["its"] > 0
     if line["n_gpus"] > 1:
-        s3 = line["strong_300"]  # (round 2's lines: roofline_frac; from round 3: csr_effective_frac)
-        assert s3["unit"] == "GB/s" and 0 < s3.get("csr_effective_frac", s3.get("roofline_frac", 0)) < 2
+        s3 = line["strong_300"]  # (round 2's lines: roofline_frac; from round 4: frac)
+        assert s3["unit"] == "GB/s" and 0 < s3.get("frac", s3.get("roofline_frac", 0)) <= 1
+    assert_fracs_at_most_one(line)
     if "worst_rank" in d:  # written by distributed_block (round 2 onwards)
         assert d["worst_rank"] in [r["rank"] for r in d["ranks"]]
+
+
+def _fracs(o, path=""):
+    if isinstance(o, dict):
+        for k, v in o.items():
+            if "frac" in k and isinstance(v, (int, float)) and not isinstance(v, bool):
+                yield f"{path}/{k}", v
+            yield from _fracs(v, f"{path}/{k}")
+    elif isinstance(o, list):
+        for i, v in enumerate(o):
+            yield from _fracs(v, f"{path}[{i}]")
+
+
+def assert_fracs_at_most_one(line):
+    """Every fraction of 8 TB/s a bench line reports is the bytes the timed
+    kernel moves over its time: none can exceed 1."""
+    bad = [(p, v) for p, v in _fracs(line) if v > 1.0]
+    assert not bad, bad
+
+
+def test_fraction_check_catches_an_effective_rate():
+    assert_fracs_at_most_one({"roofline": {"frac": 0.74, "aj_layout": {"frac": 0.73}}, "flan": [{"frac": 0.6}]})
+    with pytest.raises(AssertionError):
+        assert_fracs_at_most_one({"roofline": {"csr_effective": {"frac": 1.02}}})
+
+
+def test_round4_lines_have_no_fraction_above_one():
+    """Lines this round's bench.py wrote (profiles/r04/bench_*.json) carry
+    only fractions of the bytes each timed kernel moves."""
+    import json
+    for f in sorted((ROOT / "profiles" / "r04").glob("bench_*.json")):
+        for raw in f.read_text().strip().splitlines():
+            if raw.startswith("{"):
+                assert_fracs_at_most_one(json.loads(raw))
+
+
+def test_rank_plan_env_contract(bench):
+    """`python bench.py --gpus N` without a launcher starts N ranks with the
+    torch.distributed.run environment."""
+    plan = bench.rank_plan(4, ["--gpus", "4", "--steps", "5"], 29511, env={"PATH": "/bin", "HSA_ENABLE_IPC_MODE_LEGACY": "0"})
+    assert len(plan) == 4
+    for r, (cmd, env) in enumerate(plan):
+        assert cmd[-4:] == ["--gpus", "4", "--steps", "5"] and cmd[-5].endswith("bench.py")
+        assert env["RANK"] == env["LOCAL_RANK"] == str(r)
+        assert env["WORLD_SIZE"] == env["LOCAL_WORLD_SIZE"] == "4"
+        assert env["MASTER_ADDR"] == "127.0.0.1" and env["MASTER_PORT"] == "29511"
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["PATH"] == "/bin"
+
+
+CHILD = ("import json, os, sys\n"
+         "r = int(os.environ['RANK'])\n"
+         "print('rank', r, 'noise')\n"
+         "if r == int(os.environ.get('FAIL_RANK', '-1')): sys.exit(3)\n"
+         "if r == 0: print(json.dumps({'n_gpus': int(os.environ['WORLD_SIZE']), 'rank': r}))\n")
+
+
+def test_launch_ranks_prints_exactly_one_json_line(bench, capfd):
+    import json
+    import sys
+    rc = bench.launch_ranks(3, [], child=[sys.executable, "-c", CHILD])
+    assert rc == 0
+    out = capfd.readouterr().out.strip().splitlines()
+    lines = [json.loads(x) for x in out if x.startswith("{")]
+    assert lines == [{"n_gpus": 3, "rank": 0}]
+    assert out == ["rank 0 noise", '{"n_gpus": 3, "rank": 0}']  # the other ranks' stdout went to stderr
+
+
+def test_launch_ranks_propagates_a_failure(bench, monkeypatch):
+    import sys
+    monkeypatch.setenv("FAIL_RANK", "1")
+    assert bench.launch_ranks(2, [], child=[sys.executable, "-c", CHILD]) == 3

@@ -403,9 +403,8 @@ def test_long_row_xcd_placement_is_speed_only(pkg, dev, coracle):
         xd = to_dev(x, dev)
         yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
         ys = []
-        for lx, lo in ((1, 0), (0, 0), (1, 1), (0, 1), (1, 0)):
+        for lx in (1, 0, 1):
             A.set_option("long_xcd", lx)
-            A.set_option("long_overlap", lo)  # side stream forked from / joined to the caller's
             yd.fill_(float("nan"))
             A.mult(xd, yd)
             torch.cuda.synchronize()
@@ -413,11 +412,11 @@ def test_long_row_xcd_placement_is_speed_only(pkg, dev, coracle):
         for y in ys[1:]:
             assert_bits(y, ys[0])
         check(ys[0], ref, ai, aj, aa, x, exact=False)
-        # MatMultAdd through the forked path: w = z + A x
+        # MatMultAdd: w = z + A x, both placements
         zd = to_dev(pkg.splitmix_uniform(len(ai) - 1, 6), dev)
         A.mult_add(xd, zd, yd)
         torch.cuda.synchronize()
-        A.set_option("long_overlap", 0)
+        A.set_option("long_xcd", 0)
         wd = torch.empty_like(yd)
         A.mult_add(xd, zd, wd)
         torch.cuda.synchronize()
@@ -426,39 +425,34 @@ def test_long_row_xcd_placement_is_speed_only(pkg, dev, coracle):
 
 @pytest.mark.parametrize("name", ["poisson16", "skewed_small", "compressed_small"])
 def test_stream_options_do_not_change_results(pkg, dev, name):
-    """Every STREAM geometry / XCD remap / non-temporal setting is speed-only."""
+    """Every STREAM geometry / non-temporal setting is speed-only; the
+    options withdrawn in ABI 2 are refused."""
     g = golden(name)
     ai, aj, aa, n = g["ai"], g["aj"], g["aa"], int(g["ncols"])
     with pkg.SeqAIJHIP(ai, aj, aa, ncols=n) as A:
         xd = to_dev(g["x"], dev)
         yd = torch.empty(len(ai) - 1, dtype=torch.float64, device=dev)
+        for opt in pkg.WITHDRAWN_OPTIONS:
+            with pytest.raises(pkg.AIJHIPError, match="withdrawn"):
+                A.set_option(opt, 1)
         first = None
         for geom in range(12):
-            for xcd, nt, persist, clamped in ((0, 0, 0, 0), (1, 0, 0, 1), (0, 1, 0, 0), (22, 1, 0, 1), (3, 0, 0, 0),
-                                              (0, 0, 1, 0), (0, 1, 2, 0), (0, 0, 5, 0), (0, 0, 0, 1), (0, 4, 0, 0),
-                                              (0, 5, 0, 0)):
-                if persist and geom == 2:
-                    continue
-                for _ in range(1):
-                    A.set_option("geometry", geom)
-                    A.set_option("xcd_remap", xcd)
-                    A.set_option("nt_loads", nt)
-                    A.set_option("persistent", persist)
-                    A.set_option("clamped", clamped)
-                    A.set_option("exact", 1)
-                    A.mult(xd, yd)
-                    torch.cuda.synchronize()
-                    y = yd.cpu().numpy()
-                    if first is None:
-                        first = y
-                    short = np.diff(ai) <= 1024  # below every geometry's block cap
-                    assert_bits(y, first, short)
-                    assert_bits(y, g["y"], short)
-                    check(y, g["y"], ai, aj, aa, g["x"], exact=False)
+            for nt in (0, 1):
+                A.set_option("geometry", geom)
+                A.set_option("nt_loads", nt)
+                A.set_option("exact", 1)
+                A.mult(xd, yd)
+                torch.cuda.synchronize()
+                y = yd.cpu().numpy()
+                if first is None:
+                    first = y
+                short = np.diff(ai) <= 1024  # below every geometry's block cap
+                assert_bits(y, first, short)
+                assert_bits(y, g["y"], short)
+                check(y, g["y"], ai, aj, aa, g["x"], exact=False)
         # the gather-ordered copy at every geometry (block caps 1024..8190),
         # exact and default modes
-        for o, v in (("xcd_remap", 0), ("nt_loads", -1), ("persistent", 0), ("clamped", 0)):
-            A.set_option(o, v)
+        A.set_option("nt_loads", -1)
         short = np.diff(ai) <= 1024
         for geom in range(12):
             ys = {}
@@ -568,47 +562,3 @@ def test_gather_sort_32_and_16_bit_columns(pkg, dev, coracle, wide, form):
         A.mult(xd, y)
         torch.cuda.synchronize()
         assert_bits(y.cpu().numpy(), coracle.matmult(ai, aj, aa2, x, omp=True))
-
-
-@pytest.mark.parametrize("case", ["skewed", "fem_hex", "mixed"])
-@pytest.mark.parametrize("group", [1, 2])
-def test_row_group_kernel(pkg, dev, coracle, case, group):
-    """Register row groups (row_group 1 = 256 lanes, 2 = 512): blocks of mean
-    row length >= 24 are summed by L lanes per row in registers (reordered,
-    fp64 bound, deterministic); blocks of shorter rows keep the LDS STREAM
-    kernel and stay bit-exact; MatMultAdd alike."""
-    if case == "skewed":
-        ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
-    elif case == "fem_hex":
-        ai, aj, aa = pkg.fem_hex_csr(21, 20, 19)
-    else:  # 7-point rows, then rows of 30-90 entries
-        rng = np.random.default_rng(7)
-        p_ai, p_aj, p_aa = pkg.poisson_csr(20)
-        m0 = len(p_ai) - 1
-        lens = rng.integers(30, 90, 5000)
-        m = m0 + len(lens)
-        rows = [np.sort(rng.choice(m, size=l, replace=False)) for l in lens]
-        ai = np.concatenate([p_ai, p_ai[-1] + np.cumsum(lens)]).astype(np.int32)
-        aj = np.concatenate([p_aj] + rows).astype(np.int32)
-        aa = np.concatenate([p_aa, rng.uniform(-1, 1, int(lens.sum()))])
-    m = len(ai) - 1
-    x = pkg.splitmix_uniform(m, 21)
-    z = pkg.splitmix_uniform(m, 22)
-    ref = coracle.matmult(ai, aj, aa, x, omp=True)
-    with pkg.SeqAIJHIP(ai, aj, aa, row_group=group) as A:
-        xd, zd = to_dev(x, dev), to_dev(z, dev)
-        y1 = torch.full((m,), float("nan"), dtype=torch.float64, device=dev)
-        y2 = torch.empty_like(y1)
-        w = torch.empty_like(y1)
-        A.mult(xd, y1)
-        A.mult(xd, y2)
-        A.mult_add(xd, zd, w)
-        torch.cuda.synchronize()
-        y = y1.cpu().numpy()
-        assert torch.equal(y1, y2)
-        check(y, ref, ai, aj, aa, x, exact=False)
-        wref = coracle.matmult_add(ai, aj, aa, x, z)
-        check(w.cpu().numpy(), wref, ai, aj, aa, x, exact=False, z=z)
-        if case == "mixed":  # the Poisson rows sit in short-row blocks: PETSc's order
-            n0 = len(p_ai) - 1 - 600
-            assert_bits(y[:n0], ref[:n0])

@@ -91,19 +91,8 @@ def main():
 
     variants = []
     if args.variants in ("stream", "all"):
-        for g, cl in itertools.product(range(9), (0, 1)):
-            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=cl)))
-        for g in (6, 7):
-            variants.append(("stream", dict(geometry=g, xcd_remap=1, nt_loads=0, persistent=0, clamped=0)))
-            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=1, persistent=0, clamped=0)))
-    if args.variants in ("xcd", "all"):
-        for g, c in [(6, 0), (6, 1), (6, 5), (6, 11), (6, 22), (6, 44), (6, 88), (7, 0), (7, 11), (7, 22),
-                     (8, 0), (8, 44)]:
-            variants.append(("stream", dict(geometry=g, xcd_remap=c, nt_loads=0, persistent=0, clamped=0)))
-    if args.variants in ("pipe", "all"):
-        variants += [("stream", dict(geometry=g, persistent=0)) for g in (1, 4)]
-        for g, p in itertools.product((4, 6, 7), (1, 2, 4)):
-            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=p, clamped=0)))
+        for g, nt in itertools.product(range(12), (0, 1)):
+            variants.append(("stream", dict(geometry=g, nt_loads=nt)))
     if args.variants in ("kernels", "all"):
         variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
     if args.variants == "default":  # the product's defaults only
@@ -116,9 +105,6 @@ def main():
     if args.variants == "ntlong":  # non-temporal matrix loads for long-row operands, both automatic geometries
         for g, nt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
-    if args.variants == "loadorder":  # aj-first load order and non-temporal aa (nt_loads 2/3)
-        for nt in (0, 1, 2, 3):
-            variants.append(("stream", dict(geometry=6, nt_loads=nt)))
     if args.variants == "ntgeom":  # non-temporal matrix loads x load depth (tools/read_sweep.hip: nt reads 6.8 TB/s)
         for g, nt in itertools.product((6, 11, 8, 0), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
@@ -129,8 +115,8 @@ def main():
         for g, xt in ((1, 0), (7, 0), (7, 1), (4, 0), (4, 1), (6, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
     if args.variants == "longxcd":
-        for g, lx, lo in itertools.product((1, 6), (0, 1), (0, 1)):
-            variants.append(("stream", dict(geometry=g, long_xcd=lx, long_overlap=lo)))
+        for g, lx in itertools.product((1, 6), (0, 1)):
+            variants.append(("stream", dict(geometry=g, long_xcd=lx)))
     if args.variants == "skewgeom":
         for g, ex in itertools.product(range(9), (0, 1)):
             variants.append(("stream", dict(geometry=g, exact=ex)))
@@ -149,50 +135,20 @@ def main():
     if args.variants == "patnt":  # row patterns: plain vs non-temporal aa loads
         for nt in (0, 1, 0, 1):
             variants.append(("stream", dict(row_patterns=1, nt_loads=nt)))
-    if args.variants == "patai":  # row patterns: row starts from the lengths' scan vs from ai
-        for ai_ in ("0", "1"):
-            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_AI": ai_})))
-        variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_PAT_AI": "0"})))
-    if args.variants == "patxcd":  # row patterns: XCD placement of the blocks (AIJHIP_PAT_XCHUNK)
-        for xc in ("0", "auto", "-1", "11", "44", "0", "auto"):
-            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_XCHUNK": xc})))
-    if args.variants == "patgeom":  # row patterns at geometries 6 (512 rows), 8 (256) and 7 (1024)
-        for g, nt in ((6, 0), (8, 0), (7, 0), (8, 1), (6, 0)):
-            variants.append(("stream", dict(row_patterns=1, geometry=g, nt_loads=nt, env={"AIJHIP_PAT_XCHUNK": "0"})))
-    if args.variants == "patbf":  # row patterns: branch-free vs predicated gathers (AIJHIP_PAT_BF)
-        for bf in ("1", "0", "1", "0"):
-            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_BF": bf, "AIJHIP_PAT_XCHUNK": "0"})))
-    if args.variants == "patnb":  # row patterns: x[r +- 1] from neighbouring lanes (AIJHIP_PAT_NB) vs gathered
-        for nb in ("0", "1", "0", "1"):
-            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_NB": nb, "AIJHIP_PAT_BF": "0",
-                                                                 "AIJHIP_PAT_XCHUNK": "0"})))
-    if args.variants == "patw16":  # row patterns: 16-B vs two 8-B LDS writes per staged pair (AIJHIP_PAT_W16)
-        for w in ("0", "1", "0", "1"):
-            variants.append(("stream", dict(row_patterns=1, env={"AIJHIP_PAT_W16": w, "AIJHIP_PAT_XCHUNK": "0"})))
     if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
         variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
-    if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: serial vs side stream
-        for lx, lo in ((1, 0), (1, 1), (0, 0), (0, 1)):
-            variants.append(("stream", dict(long_xcd=lx, long_overlap=lo)))
+    if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: XCD placement on / off
+        for lx in (1, 0):
+            variants.append(("stream", dict(long_xcd=lx)))
     if args.variants == "geo16":  # the two automatic geometries
         for g in (1, 6):
             variants.append(("stream", dict(geometry=g)))
     if args.variants == "skewgeom2":  # the geometries the skewgeom sweep left out (9-11) against 1
         for g, nt in itertools.product((1, 9, 10, 11), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
-    if args.variants == "skewpipe":
-        for g, ex, pp in itertools.product((1, 7), (0, 1), (0, 1, 2, 3)):
-            variants.append(("stream", dict(geometry=g, exact=ex, persistent=pp)))
-    if args.variants == "group":  # register row-group kernel (AIJHIP_OPT_ROW_GROUP) vs the LDS blocks
-        for g, rg, nt in ((-1, 0, -1), (-1, 1, -1), (-1, 2, -1), (-1, 1, 0), (-1, 1, 1), (6, 1, -1), (6, 0, -1),
-                          (1, 2, 1), (6, 2, 0)):
-            variants.append(("stream", dict(geometry=g, row_group=rg, nt_loads=nt)))
-    if args.variants == "shuf":  # lane-stride gathers through __shfl (nt_loads 4 plain / 5 non-temporal)
-        for g, nt in ((-1, -1), (-1, 4), (-1, 5), (6, 0), (6, 4), (6, 5), (1, 1), (1, 5), (1, 4), (0, 4), (8, 4)):
-            variants.append(("stream", dict(geometry=g, nt_loads=nt)))
     if args.variants == "skewed":
         for g in (0, 1, 4, 6, 7, 8):
-            variants.append(("stream", dict(geometry=g, xcd_remap=0, nt_loads=0, persistent=0, clamped=0)))
+            variants.append(("stream", dict(geometry=g, nt_loads=0)))
         for g in (1, 6):
             variants.append(("stream", dict(geometry=g, exact=1)))
         variants += [("vector", {"lanes": 16}), ("vector", {"lanes": 32}), ("vector", {"lanes": 64}),
@@ -206,12 +162,10 @@ def main():
         A.set_option("exact", opts.get("exact", 0))
         A.set_option("x_tile", opts.get("x_tile", -1 if opts else 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
-        A.set_option("long_overlap", opts.get("long_overlap", 0))
-        A.set_option("row_group", opts.get("row_group", 0))
         A.set_option("gather_sort", opts.get("gather_sort", -1))
         A.set_option("column_codes", opts.get("column_codes", -1))
         A.set_option("row_patterns", opts.get("row_patterns", -1))
-        for k in ("geometry", "xcd_remap", "nt_loads", "persistent", "clamped"):
+        for k in ("geometry", "nt_loads"):
             if k in opts:
                 A.set_option(k, opts[k])
 
