@@ -118,7 +118,9 @@ typedef struct aijhip_info {
     int32_t row_patterns;    /* MatMult reads a pattern id per row instead of
                                 aj (AIJHIP_OPT_ROW_PATTERNS): the number of
                                 distinct column - row offset lists; 0 off    */
-    int32_t pad0;
+    int32_t long_windows;    /* rows longer than a block summed by x column
+                                window (AIJHIP_OPT_LONG_WINDOW): the number
+                                of windows; 0 = 4096-entry segments        */
     int64_t mult_layout_bytes; /* compulsory bytes one MatMult of the plan in
                                 effect moves: mult_bytes for CSR (aj read);
                                 less where the plan reads column codes (10 B
@@ -224,6 +226,17 @@ enum {
                                        entries), else the automatic layout
                                        without them; costs 2 bytes per entry
                                        of device memory                      */
+    AIJHIP_OPT_LONG_WINDOW = 15,    /* rows longer than a STREAM block: 1 =
+                                       by x column window (each workgroup
+                                       stages 2048 x entries in LDS and sums
+                                       every long row's entries in that
+                                       window; the rows' window sums are added
+                                       in window order), 0 = 4096-entry
+                                       segments; -1 (default): windows when
+                                       the long rows are column-sorted, at
+                                       most 512 and >= 2048 of their entries
+                                       per window. Reordered, deterministic,
+                                       within the fp64 bound either way      */
     AIJHIP_OPT_ROW_PATTERNS = 14    /* short-row operands whose rows follow at
                                        most 256 distinct column - row offset
                                        lists (stencils): no per-entry column

@@ -33,7 +33,7 @@ if os.environ.get("AIJHIP_LIB"):
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
 OPTIONS = {"geometry": 1, "nt_loads": 3, "exact": 6, "x_tile": 7, "long_xcd": 8, "host_pipeline": 10,
-           "gather_sort": 12, "column_codes": 13, "row_patterns": 14}
+           "gather_sort": 12, "column_codes": 13, "row_patterns": 14, "long_window": 15}
 # withdrawn in ABI 2 (measured slower); the library refuses them
 WITHDRAWN_OPTIONS = {"xcd_remap": 2, "persistent": 4, "clamped": 5, "long_overlap": 9, "row_group": 11}
 
@@ -74,7 +74,7 @@ class AIJInfo(ctypes.Structure):
         ("stream_threads", ctypes.c_int32), ("stream_nnz_cap", ctypes.c_int32), ("stream_rows", ctypes.c_int32),
         ("persistent", ctypes.c_int32), ("exact", ctypes.c_int32), ("x_tiled_blocks", ctypes.c_int32),
         ("gather_sorted", ctypes.c_int32), ("column_codes", ctypes.c_int32),
-        ("row_patterns", ctypes.c_int32), ("pad0", ctypes.c_int32),
+        ("row_patterns", ctypes.c_int32), ("long_windows", ctypes.c_int32),
         ("mult_layout_bytes", ctypes.c_int64),
     ]
 

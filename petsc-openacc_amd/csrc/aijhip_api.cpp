@@ -74,6 +74,7 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_longs);
     hipFree(P.d_partials);
     hipFree(P.d_segperm);
+    hipFree(P.d_wbnd);
     hipFree(P.d_xrange);
     hipFree(P.d_saj);
     hipFree(P.d_saa);
@@ -404,7 +405,13 @@ int plan_stream(aijhip_mat *A) {
                 return hipfail(e, "plan: column codes");
         }
     }
-    if (!longs.empty()) {
+    bool windowed = false;
+    if (!longs.empty() && P.tune.long_window != 0) {
+        if ((e = aijhip::build_long_windows(*A, P, longs, P.tune.long_window > 0, &windowed)) != hipSuccess)
+            return hipfail(e, "plan: long-row windows");
+        if (windowed) P.n_segs = 0;
+    }
+    if (!longs.empty() && !windowed) {
         if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_partials, segs.size(), &P.bytes)) != hipSuccess)
@@ -918,6 +925,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             t.xtile = value;
             break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
+        case AIJHIP_OPT_LONG_WINDOW:
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "long_window: -1 auto, 0 segments, 1 windows");
+            t.long_window = value;
+            break;
         case AIJHIP_OPT_HOST_PIPELINE:
             if (value < -1) return fail(AIJHIP_ERR_ARG, "host_pipeline: -1 auto, 0 serial, k > 0 chunk rows");
             t.host_chunk = value;
@@ -1126,6 +1137,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
     info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
     info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
+    info->long_windows = A->plan.d_wbnd != nullptr ? A->plan.n_win : 0;
     info->mult_layout_bytes = layout_bytes(*A);
     return AIJHIP_OK;
 }

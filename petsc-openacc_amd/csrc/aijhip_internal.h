@@ -54,6 +54,11 @@ constexpr int kMaxStreamNnzCap = 8192;
 // segments of at most kLongSegNnz entries, each summed by one workgroup.
 constexpr int kLongSegNnz = 4096;
 constexpr int kLongThreads = 256;
+// Windowed long rows (Tuning::long_window): x column windows of kWinCols
+// doubles staged in LDS, one workgroup per window; at most kWinMaxRows long
+// rows, their columns sorted.
+constexpr int kWinCols = 2048;
+constexpr int kWinMaxRows = 512;
 // MERGE kernel: 256 lanes x kMergeItems merge-path items per workgroup.
 constexpr int kMergeThreads = 256;
 constexpr int kMergeItems = 8;
@@ -99,6 +104,8 @@ struct Tuning {
     int xtile = 0;         // x staged in LDS per block: 0 off (measured default), 1 where it fits,
                            // -1 when half the blocks fit
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
+    int long_window = -1;  // long rows by x column window (k_long_window) instead of segments: -1 auto
+                           // (sorted rows, >= 2048 long-row entries per window), 0 segments, 1 windows
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
@@ -163,6 +170,11 @@ struct Plan {
     // the s % 8-th eighth of x, so each XCD's L2 holds the x range its
     // scattered gathers hit (speed only; partials and their order unchanged)
     int32_t *d_segperm = nullptr;
+    // Tuning::long_window: per long row i and window w the first entry with
+    // column >= w kWinCols (n_win + 1 per row); then d_partials holds
+    // n_longs x n_win window sums and d_longs[i] = {orow, i n_win, n_win}
+    int32_t *d_wbnd = nullptr;
+    int32_t n_win = 0;
     // x tiles: per block the first column and the span of its columns, or
     // span -1 when they do not fit the block's LDS (gathers from HBM)
     int2 *d_xrange = nullptr;
@@ -249,14 +261,12 @@ bool stream_dot_fusable(const aijhip_mat &A);
 hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, double *dpart,
                              const int *stop, hipStream_t s);
 // Fused V-cycle smoothing SpMVs on a STREAM plan (same conditions as
-// stream_dot_fusable): pre-smoothing x = D^-1 b with r = b - A x, and one
+// stream_dot_fusable): the pre-smoothing residual r = b - A x, and one
 // Richardson+Jacobi step x = t + D^-1 (b - A t) (x != t) with optional
 // z.z / z.b partials (2 x n_blocks) for CG on the finest level.
 bool stream_mg_fusable(const aijhip_mat &A);
 // y = D^-1 A x in PETSc's row order (exact), for the GAMG set-up.
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s);
-hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
-                         hipStream_t s, bool nt, const int *stop = nullptr);
 // r = b - A x on a STREAM plan (residual in the SpMV epilogue).
 hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
                            bool nt, const int *stop = nullptr);
@@ -281,6 +291,10 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
                            double **d_taa, hipStream_t s);
 
 RowList row_list(const aijhip_mat &A);
+// Windowed long rows: *ok when every long row is sorted and (unless force)
+// the rows carry >= 2048 entries per window; fills P.d_wbnd / n_win,
+// P.d_longs and P.d_partials (the caller has not allocated them).
+hipError_t build_long_windows(const aijhip_mat &A, Plan &P, const std::vector<LongRow> &longs, bool force, bool *ok);
 // Per long-row segment: the column of its middle entry (synchronous).
 hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out);
 // Per STREAM block: min column and span (max - min + 1) of its entries.

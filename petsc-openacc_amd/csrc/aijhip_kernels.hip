@@ -111,33 +111,9 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     }
 };
 
-// V-cycle pre-smoothing from a zero guess fused with the residual
-// (ksp.hip k_jacobi + SpMV + k_resid, same roundings): x = D^-1 b is gathered
-// as dinv_j * b_j, and each row stores x_i and r_i = b_i + (-1) (A x)_i.
-template <bool NT>
-struct OpMgPre {
-    static constexpr int kDots = 0;
-    static constexpr bool kSeeded = false;
-    static constexpr bool kTile = false;
-    const double *b, *dinv;
-    double *x, *r;
-    __device__ double gx(int32_t j) const { return dinv[j] * b[j]; }
-    __device__ double seed(int) const { return 0.0; }
-    __device__ void put(int o, double v, double *) const {
-        const double bo = b[o];
-        if constexpr (NT) {
-            st_stream(x + o, dinv[o] * bo);
-            st_stream(r + o, bo + (-1.0) * v);
-        } else {
-            x[o] = dinv[o] * bo;
-            r[o] = bo + (-1.0) * v;
-        }
-    }
-};
-
 // MatResidual with the SpMV: r_i = b_i + (-1) (A x)_i (SpMV + k_resid, same
-// roundings) — the second half of the split pre-smoothing, after x = D^-1 b
-// was written by a vector pass (one gather per entry instead of OpMgPre's two).
+// roundings) — the second half of the pre-smoothing, after x = D^-1 b was
+// written by a vector pass.
 template <bool NT>
 struct OpMgResid {
     static constexpr int kDots = 0;
@@ -584,6 +560,164 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
         for (int w = 1; w < kLongThreads / 64; ++w) r += red[w];
         partials[id] = r;
     }
+}
+
+// Windowed long rows (Plan::d_wbnd; Tuning::long_window): the hub rows of a
+// skewed operand scatter their gathers over all of x, one 128-B line per
+// entry, so the segment form above moves ~16x more L2 -> CU bytes for x than
+// for the matrix (the stand-in: 6.8 M hub entries, ~47 us against ~13 us of
+// their stream). Here workgroup w owns x's column window [w W, (w + 1) W),
+// loads it into LDS once with coalesced loads, and takes every long row's
+// entries whose columns fall in it (the rows' columns are sorted, so they are
+// one contiguous run per row: bnd[i (nw + 1) + w, + w + 1)). The runs are
+// walked as one flat list (prefix offsets in LDS), T * U entries per pass:
+// coalesced aa / aj loads, x from the LDS window, products to LDS, then per
+// row a wavefront sums the pass's slice (strided lanes + __shfl_down tree)
+// into acc[i] in pass order. partials[i nw + w] = the row's sum over the
+// window; k_long_finish adds them in window order. Deterministic (the lanes'
+// shares and the orders are fixed by the plan), reordered like the segments.
+template <int W, int T, int U>
+__global__ __launch_bounds__(T) void k_long_window(int32_t nl, int32_t nw, int32_t n, const int32_t *__restrict__ bnd,
+                                                   const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                                                   const double *__restrict__ x, double *__restrict__ partials) {
+    __shared__ double xs[W];
+    __shared__ double prod[T * U];
+    __shared__ int32_t pre[kWinMaxRows + 1];
+    __shared__ int32_t kst[kWinMaxRows];
+    __shared__ double acc[kWinMaxRows];
+    __shared__ int32_t wtot[T / 64];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    const int32_t w = (int32_t)blockIdx.x;
+    const int64_t c0 = (int64_t)w * W;
+    const int32_t cn = (int32_t)min<int64_t>(W, (int64_t)n - c0);
+    // the x window (16-B loads when x is 16-B aligned: W, c0 are even)
+    const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    for (int32_t i = 2 * t; i < cn; i += 2 * T) {
+        if (i + 1 < cn && al) {
+            const f64x2 v = *reinterpret_cast<const f64x2 *>(x + c0 + i);
+            xs[i] = v.x;
+            xs[i + 1] = v.y;
+        } else if (i + 1 < cn) {
+            xs[i] = x[c0 + i];
+            xs[i + 1] = x[c0 + i + 1];
+        } else {
+            xs[i] = x[c0 + i];
+        }
+    }
+    // each row's run in this window; flat offsets by a block scan (rows
+    // T at a time, the running total carried in register `base`)
+    int32_t base = 0;
+    for (int32_t i0 = 0; i0 < nl; i0 += T) {
+        const int32_t i = i0 + t;
+        int32_t len = 0;
+        if (i < nl) {
+            const int32_t a = bnd[(int64_t)i * (nw + 1) + w], b = bnd[(int64_t)i * (nw + 1) + w + 1];
+            kst[i] = a;
+            len = b - a;
+            acc[i] = 0.0;
+        }
+        int32_t inc = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int32_t v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) wtot[wave] = inc;
+        __syncthreads();
+        int32_t off = base;
+        for (int q = 0; q < wave; ++q) off += wtot[q];
+        if (i < nl) pre[i] = off + inc - len;
+        for (int q = 0; q < T / 64; ++q) base += wtot[q];
+        __syncthreads();
+    }
+    if (t == 0) pre[nl] = base;
+    __syncthreads();
+    const int32_t E = base;
+    for (int32_t e0 = 0; e0 < E; e0 += T * U) {
+        double av[U];
+        int32_t cv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t e = e0 + t + u * T;
+            if (e < E) {
+                int32_t lo = 0, hi = nl - 1;  // the row whose run holds flat entry e
+                while (lo < hi) {
+                    const int32_t mid = (lo + hi + 1) >> 1;
+                    if (pre[mid] <= e) lo = mid;
+                    else hi = mid - 1;
+                }
+                const int64_t k = (int64_t)kst[lo] + (e - pre[lo]);
+                av[u] = __builtin_nontemporal_load(aa + k);
+                cv[u] = __builtin_nontemporal_load(aj + k);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t e = e0 + t + u * T;
+            if (e < E) prod[t + u * T] = av[u] * xs[cv[u] - c0];
+        }
+        __syncthreads();
+        // the rows whose runs meet [e0, e1): a wavefront each, in row order
+        const int32_t e1 = min(E, e0 + T * U);
+        int32_t r0 = 0, r1 = nl - 1;
+        {
+            int32_t lo = 0, hi = nl - 1;
+            while (lo < hi) {
+                const int32_t mid = (lo + hi + 1) >> 1;
+                if (pre[mid] <= e0) lo = mid;
+                else hi = mid - 1;
+            }
+            r0 = lo;
+            lo = 0, hi = nl - 1;
+            while (lo < hi) {
+                const int32_t mid = (lo + hi + 1) >> 1;
+                if (pre[mid] <= e1 - 1) lo = mid;
+                else hi = mid - 1;
+            }
+            r1 = lo;
+        }
+        for (int32_t i = r0 + wave; i <= r1; i += T / 64) {
+            const int32_t a = max(pre[i], e0) - e0, b = min(pre[i + 1], e1) - e0;
+            double s = 0.0;
+            for (int32_t j = a + lane; j < b; j += 64) s += prod[j];
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+            if (lane == 0 && b > a) acc[i] += s;
+        }
+        __syncthreads();
+    }
+    for (int32_t i = t; i < nl; i += T) partials[(int64_t)i * nw + w] = acc[i];
+}
+
+// bnd[i (nw + 1) + w] = the first entry of long row rows[i] whose column is
+// >= w W (w = nw: the row's end); the row's columns must be sorted
+__global__ void k_window_bounds(int32_t nl, int32_t nw, int32_t W, const int32_t *__restrict__ rows,
+                                const int32_t *__restrict__ ai, const int32_t *__restrict__ aj, int32_t *bnd) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= (int64_t)nl * (nw + 1)) return;
+    const int32_t i = (int32_t)(g / (nw + 1)), w = (int32_t)(g - (int64_t)i * (nw + 1));
+    const int32_t r = rows[i];
+    int32_t lo = ai[r], hi = ai[r + 1];
+    if (w < nw) {
+        const int64_t c = (int64_t)w * W;
+        while (lo < hi) {
+            const int32_t mid = lo + ((hi - lo) >> 1);
+            if ((int64_t)aj[mid] < c) lo = mid + 1;
+            else hi = mid;
+        }
+    }
+    bnd[g] = lo;
+}
+
+// long rows whose columns are not in ascending order (then: segments)
+__global__ void k_rows_unsorted(int32_t nl, const int32_t *__restrict__ rows, const int32_t *__restrict__ ai,
+                                const int32_t *__restrict__ aj, int *bad) {
+    const int32_t i = blockIdx.x;
+    if (i >= nl) return;
+    const int32_t r = rows[i];
+    int c = 0;
+    for (int32_t k = ai[r] + threadIdx.x; k + 1 < ai[r + 1]; k += blockDim.x) c += aj[k + 1] < aj[k];
+    if (c) atomicAdd(bad, c);
 }
 
 // One wavefront per long row: the lanes load 64 partials at once and the sum
@@ -1377,6 +1511,62 @@ __global__ __launch_bounds__(256) void k_seg_midcol(const LongSeg *__restrict__ 
     out[i] = s.nk > 0 ? aj[(int64_t)s.k0 + s.nk / 2] : 0;
 }
 
+hipError_t build_long_windows(const aijhip_mat &A, Plan &P, const std::vector<LongRow> &longs, bool force, bool *ok) {
+    *ok = false;
+    const int32_t nl = (int32_t)longs.size();
+    if (nl == 0 || nl > kWinMaxRows || A.compressed || A.n <= 0 || A.h_rai.empty()) return hipSuccess;
+    const int32_t nw = (int32_t)(((int64_t)A.n + kWinCols - 1) / kWinCols);
+    int64_t total = 0;
+    std::vector<int32_t> rows(nl);
+    for (int32_t i = 0; i < nl; ++i) {
+        rows[i] = longs[i].orow;
+        total += A.h_rai[rows[i] + 1] - A.h_rai[rows[i]];
+    }
+    // enough entries per window to pay for staging it (the skewed stand-in:
+    // ~8,800 per window; a few long rows over a wide x keep their segments)
+    if (!force && total < (int64_t)2048 * nw) return hipSuccess;
+    int32_t *d_rows = nullptr, *d_bnd = nullptr;
+    int *d_bad = nullptr, bad = 0;
+    hipError_t e;
+    auto done = [&](hipError_t r) {
+        hipFree(d_rows);
+        hipFree(d_bad);
+        if (!*ok) hipFree(d_bnd);
+        return r;
+    };
+    if ((e = hipMalloc(&d_rows, sizeof(int32_t) * nl)) != hipSuccess ||
+        (e = hipMalloc(&d_bad, sizeof(int))) != hipSuccess || (e = hipMemset(d_bad, 0, sizeof(int))) != hipSuccess ||
+        (e = hipMemcpy(d_rows, rows.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice)) != hipSuccess)
+        return done(e);
+    hipLaunchKernelGGL(k_rows_unsorted, dim3(nl), dim3(256), 0, nullptr, nl, d_rows, A.d_ai, A.d_aj, d_bad);
+    if ((e = hipGetLastError()) != hipSuccess || (e = hipMemcpy(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost)) !=
+                                                     hipSuccess)
+        return done(e);
+    if (bad) return done(hipSuccess);  // unsorted long rows: segments
+    const int64_t nb = (int64_t)nl * (nw + 1);
+    if ((e = hipMalloc(&d_bnd, sizeof(int32_t) * nb)) != hipSuccess) return done(e);
+    hipLaunchKernelGGL(k_window_bounds, dim3(grid_for(nb, 256)), dim3(256), 0, nullptr, nl, nw, kWinCols, d_rows,
+                       A.d_ai, A.d_aj, d_bnd);
+    std::vector<LongRow> lr(nl);
+    for (int32_t i = 0; i < nl; ++i) lr[i] = LongRow{longs[i].orow, i * nw, nw, 0};
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMalloc(&P.d_longs, sizeof(LongRow) * nl)) != hipSuccess ||
+        (e = hipMemcpy(P.d_longs, lr.data(), sizeof(LongRow) * nl, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMalloc(&P.d_partials, sizeof(double) * (size_t)nl * nw)) != hipSuccess ||
+        (e = hipDeviceSynchronize()) != hipSuccess) {
+        hipFree(P.d_longs);
+        hipFree(P.d_partials);
+        P.d_longs = nullptr;
+        P.d_partials = nullptr;
+        return done(e);
+    }
+    P.d_wbnd = d_bnd;
+    P.n_win = nw;
+    P.bytes += (int64_t)sizeof(int32_t) * nb + (int64_t)sizeof(LongRow) * nl + (int64_t)sizeof(double) * nl * nw;
+    *ok = true;
+    return done(hipSuccess);
+}
+
 hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out) {
     if (n_segs <= 0) return hipSuccess;
     int32_t *d_out = nullptr;
@@ -1588,12 +1778,6 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
     return hipGetLastError();
 }
 
-hipError_t launch_mg_pre(const aijhip_mat &A, const double *b, const double *dinv, double *x, double *r,
-                         hipStream_t s, bool nt, const int *stop) {
-    if (nt) return launch_stream_op(A, OpMgPre<true>{b, dinv, x, r}, nullptr, s, -1, stop);
-    return launch_stream_op(A, OpMgPre<false>{b, dinv, x, r}, nullptr, s, -1, stop);
-}
-
 hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
                            bool nt, const int *stop) {
     if (nt) return launch_stream_op(A, OpMgResid<true>{x, b, r}, nullptr, s, -1, stop);
@@ -1632,8 +1816,12 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     // long rows: segment partials, then their ordered sums (one stream: a
     // forked side stream measured neutral)
     if (P.n_longs > 0) {
-        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s, P.d_segs, A.d_aj, A.d_aa, x,
-                           P.d_partials, P.d_segperm);
+        if (P.d_wbnd)  // by x column window
+            hipLaunchKernelGGL((k_long_window<kWinCols, 512, 4>), dim3(P.n_win), dim3(512), 0, s, P.n_longs, P.n_win,
+                               A.n, P.d_wbnd, A.d_aj, A.d_aa, x, P.d_partials);
+        else
+            hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s, P.d_segs, A.d_aj, A.d_aa, x,
+                               P.d_partials, P.d_segperm);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
                                     P.d_partials, z, y);

@@ -393,14 +393,11 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
         return hipSuccess;
     }
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
-    const char *gs = std::getenv("AIJHIP_LF_GRID");
-    const unsigned grid = gs ? (unsigned)std::atoi(gs) : kRoundGrid;
-    // read a node's state before its atomic (skips decided nodes; one more
-    // dependent load per round) or go straight to the atomic (a decided
+    const unsigned grid = kRoundGrid;
+    // straight to the atomic, no read of a node's state first (a decided
     // node's CAS fails; an OUT node's count never reaches 0, a root's gets no
-    // further walks)
-    const char *ps = std::getenv("AIJHIP_LF_PREREAD");
-    const int pre = ps ? std::atoi(ps) : 0;  // measured: 0 is 5-10 % faster (fewer dependent loads)
+    // further walks): 5-10 % faster than pre-reading (fewer dependent loads)
+    constexpr int pre = 0;
     auto clk = std::chrono::steady_clock::now();
     hipStream_t s = nullptr;
     int32_t *state = nullptr, *cnt = nullptr, *roots = nullptr, *outs = nullptr;

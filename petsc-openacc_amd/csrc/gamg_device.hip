@@ -483,234 +483,6 @@ __global__ void k_narrow(int32_t n, const unsigned long long *__restrict__ w, in
     if (i < n) c[i] = (int32_t)w[i];
 }
 
-// C = A*B row by row (see the file comment), TEAM lanes per row: with two,
-// each lane owns the columns of one hash half and keeps only those (a list
-// of at most CAP), both walk all the row's products in traversal order and
-// the owner adds each — per column the same order as one lane alone, so the
-// same bits — with half the list to search and shift. SYMBOLIC: cnt[i] =
-// distinct columns of row i, or -1 when a lane's list would pass CAP (the
-// next class recounts it); klass[i] = this class when it fits. NUMERIC: the
-// rows of this class, sorted columns (the team's two lists merged by rank)
-// and sums at ci[i].
-template <int CAP, int TPB, bool NUMERIC, int TEAM>
-__global__ __launch_bounds__(TPB) void k_rowprod(int32_t m, const int32_t *__restrict__ ai,
-                                                 const int32_t *__restrict__ aj, const double *__restrict__ aa,
-                                                 const int32_t *__restrict__ bi, const int32_t *__restrict__ bj,
-                                                 const double *__restrict__ ba, const int32_t *__restrict__ ci,
-                                                 int32_t *cj, double *ca, int32_t *cnt, bool redo,
-                                                 int32_t *klass, int32_t myclass) {
-    static_assert(TEAM == 1 || TEAM == 2, "one or two lanes per row");
-    __shared__ int32_t sc[CAP * TPB];
-    __shared__ double sv[NUMERIC ? CAP * TPB : 1];
-    const int t = threadIdx.x;
-    const int me = t % TEAM;
-    for (int32_t i = (blockIdx.x * TPB + t) / TEAM; i < m; i += gridDim.x * (TPB / TEAM)) {
-        if (!NUMERIC && redo && cnt[i] >= 0) continue;    // counted by a smaller class
-        if (NUMERIC && klass[i] != myclass) continue;     // another class's row
-        int n = 0;
-        bool over = false;
-        // the row's products in traversal order, their operands loaded in
-        // batches (KB entries of A, then QB entries of each B row) ahead of
-        // the LDS work: one exposed memory latency per batch, not per product
-        constexpr int KB = 8, QB = 16;
-        const int32_t k1 = ai[i + 1];
-        for (int32_t kb = ai[i]; kb < k1 && !over; kb += KB) {
-            int32_t jj[KB], q0[KB], q1[KB];
-            double av[KB];
-#pragma unroll
-            for (int u = 0; u < KB; ++u) {
-                const bool in = kb + u < k1;
-                jj[u] = in ? aj[kb + u] : 0;
-                av[u] = (NUMERIC && in) ? aa[kb + u] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < KB; ++u) {
-                const bool in = kb + u < k1;
-                q0[u] = in ? bi[jj[u]] : 0;
-                q1[u] = in ? bi[jj[u] + 1] : 0;
-            }
-            for (int u = 0; u < KB && !over; ++u) {
-                const double a = av[u];
-                for (int32_t qb = q0[u]; qb < q1[u] && !over; qb += QB) {
-                    int32_t cc[QB];
-                    double bv[QB];
-#pragma unroll
-                    for (int w = 0; w < QB; ++w) {
-                        const bool in = qb + w < q1[u];
-                        cc[w] = in ? bj[qb + w] : 0;
-                        bv[w] = (NUMERIC && in) ? ba[qb + w] : 0.0;
-                    }
-                    for (int w = 0; w < QB && qb + w < q1[u]; ++w) {
-                        const int32_t c = cc[w];
-                        if (TEAM == 2 && (int)(((uint32_t)c * 0x9E3779B1u) >> 31) != me) continue;
-                        int l = 0, h = n;
-                        while (l < h) {
-                            const int mid = (l + h) >> 1;
-                            if (sc[mid * TPB + t] < c) l = mid + 1;
-                            else h = mid;
-                        }
-                        if (l < n && sc[l * TPB + t] == c) {
-                            if (NUMERIC) sv[l * TPB + t] += a * bv[w];
-                            continue;
-                        }
-                        if (n == CAP) { over = true; break; }
-                        for (int z = n; z > l; --z) {
-                            sc[z * TPB + t] = sc[(z - 1) * TPB + t];
-                            if (NUMERIC) sv[z * TPB + t] = sv[(z - 1) * TPB + t];
-                        }
-                        sc[l * TPB + t] = c;
-                        if (NUMERIC) {
-                            double v0 = 0.0;
-                            v0 += a * bv[w];
-                            sv[l * TPB + t] = v0;
-                        }
-                        ++n;
-                    }
-                }
-            }
-        }
-        if (!NUMERIC) {
-            int tot = n;
-            if (TEAM == 2) {
-                tot += __shfl_xor(n, 1, 64);
-                over = (__shfl_xor((int)over, 1, 64) != 0) || over;
-            }
-            if (me == 0) {
-                cnt[i] = over ? -1 : tot;
-                if (!over) klass[i] = myclass;
-            }
-        } else {
-            const int32_t o = ci[i];
-            if (TEAM == 1) {
-                for (int z = 0; z < n; ++z) {
-                    cj[o + z] = sc[z * TPB + t];
-                    ca[o + z] = sv[z * TPB + t];
-                }
-            } else {
-                // rank = own position + the partner's columns below it
-                const int np = __shfl_xor(n, 1, 64);
-                const int tp = t ^ 1;
-                for (int z = 0; z < n; ++z) {
-                    const int32_t c = sc[z * TPB + t];
-                    int l = 0, h = np;
-                    while (l < h) {
-                        const int mid = (l + h) >> 1;
-                        if (sc[mid * TPB + tp] < c) l = mid + 1;
-                        else h = mid;
-                    }
-                    cj[o + z + l] = c;
-                    ca[o + z + l] = sv[z * TPB + t];
-                }
-            }
-        }
-    }
-}
-
-// The same product, one wavefront per output row with the row's columns
-// owned by lanes (hash of the column): every lane walks the row's products
-// in traversal order (uniform loads) and the owner of each product's column
-// adds it to that column's accumulator held in its registers — per column,
-// the same order as one lane walking alone, so the same bits — while the
-// wave covers up to 64*K distinct columns and a row's products are not
-// serialised behind one lane's LDS search. Count mode: cnt[i] = distinct
-// columns or -1 (a lane over K). Write mode: the columns ranked across the
-// wave (sorted) and written with their sums at ci[i].
-template <int K, bool WRITE>
-__global__ __launch_bounds__(256) void k_rowprod_wave(int32_t m, const int32_t *__restrict__ ai,
-                                                      const int32_t *__restrict__ aj, const double *__restrict__ aa,
-                                                      const int32_t *__restrict__ bi, const int32_t *__restrict__ bj,
-                                                      const double *__restrict__ ba, const int32_t *__restrict__ ci,
-                                                      int32_t *cj, double *ca, int32_t *cnt) {
-    __shared__ int32_t s_col[4][64 * K];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int64_t nwaves = (int64_t)gridDim.x * 4;
-    for (int64_t i = (int64_t)blockIdx.x * 4 + w; i < m; i += nwaves) {
-        int32_t col[K];
-        double val[K];
-        int n = 0;
-        bool over = false;
-        const int32_t k1 = ai[i + 1];
-        constexpr int QB = 16;  // B entries loaded together: one exposed latency per batch
-        for (int32_t k = ai[i]; k < k1; ++k) {
-            const int32_t j = aj[k];
-            const double a = WRITE ? aa[k] : 0.0;
-            const int32_t q1 = bi[j + 1];
-            for (int32_t qb = bi[j]; qb < q1; qb += QB) {
-                int32_t cc[QB];
-                double bv[QB];
-#pragma unroll
-                for (int w = 0; w < QB; ++w) {
-                    const bool in = qb + w < q1;
-                    cc[w] = in ? bj[qb + w] : -1;
-                    bv[w] = (WRITE && in) ? ba[qb + w] : 0.0;
-                }
-#pragma unroll
-                for (int w = 0; w < QB; ++w) {
-                    const int32_t c = cc[w];
-                    if (c < 0 || (int)(((uint32_t)c * 0x9E3779B1u) >> 26) != lane) continue;
-                    bool hit = false;
-#pragma unroll
-                    for (int e = 0; e < K; ++e) {
-                        if (e < n && col[e] == c) {
-                            if (WRITE) val[e] += a * bv[w];
-                            hit = true;
-                        }
-                    }
-                    if (hit) continue;
-                    if (n == K) { over = true; continue; }
-#pragma unroll
-                    for (int e = 0; e < K; ++e) {
-                        if (e == n) {
-                            col[e] = c;
-                            if (WRITE) {
-                                double v0 = 0.0;
-                                v0 += a * bv[w];
-                                val[e] = v0;
-                            }
-                        }
-                    }
-                    ++n;
-                }
-            }
-        }
-        // distinct columns of the row = sum over lanes
-        int tot = n;
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) tot += __shfl_xor(tot, off, 64);
-        const bool any_over = __ballot(over) != 0ull;
-        if (!WRITE) {
-            if (lane == 0) cnt[i] = any_over ? -1 : tot;
-            continue;
-        }
-        // rank every column against the wave's columns, packed in LDS
-        // (lane L's columns at the exclusive prefix of the lanes' counts)
-        int32_t *sc = s_col[w];
-        int start = n;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int v = __shfl_up(start, off, 64);
-            if (lane >= off) start += v;
-        }
-        start -= n;
-#pragma unroll
-        for (int e = 0; e < K; ++e)
-            if (e < n) sc[start + e] = col[e];
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS stores are visible
-        const int32_t o = ci[i];
-#pragma unroll
-        for (int e = 0; e < K; ++e) {
-            if (e < n) {
-                int r = 0;
-                for (int z = 0; z < tot; ++z) r += sc[z] < col[e];
-                cj[o + r] = col[e];
-                ca[o + r] = val[e];
-            }
-        }
-        __builtin_amdgcn_wave_barrier();  // the LDS slots are reused by the wave's next row
-    }
-}
-
 // The same product, G lanes per output row sharing an LDS hash table of T
 // column slots (round 3). The row's terms a_ik are taken in order; for each,
 // the G lanes cover B row k's entries side by side, each adding its product
@@ -988,35 +760,13 @@ done:
 
 // C = A * B. Returns AIJHIP_OK, or AIJHIP_ERR_STATE when a row's distinct
 // columns exceed every device capacity (the caller falls back to the host).
-// One pass of k_rowprod over the rows of one capacity class (each class
-// uses 48 KiB of LDS per workgroup in the numeric pass).
-template <int CAP, int TPB, int TEAM>
-hipError_t rowprod_pass(const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, int32_t myclass, bool redo,
-                        const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
-    const unsigned grid = (unsigned)std::min<int64_t>(blocks_for((int64_t)A.m * TEAM, TPB), (int64_t)n_cu * 16);
-    if (!numeric)
-        hipLaunchKernelGGL((k_rowprod<CAP, TPB, false, TEAM>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj,
-                           A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, redo, klass, myclass);
-    else
-        hipLaunchKernelGGL((k_rowprod<CAP, TPB, true, TEAM>), dim3(grid), dim3(TPB), 0, nullptr, A.m, A.ai, A.aj,
-                           A.aa, B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, false, klass, myclass);
-    return hipGetLastError();
-}
-
-// The lane-per-row capacity classes, tried in order (each numeric pass uses
-// at most 48 KiB of LDS per workgroup): columns per row 32 (one lane), ~64,
-// ~128, ~256 (two lanes, a hash half each), 256 (one lane: rows whose halves
-// are too uneven for the two-lane class).
-constexpr int kProdClasses = 5;
-constexpr int kProdClassCols[kProdClasses] = {32, 64, 128, 256, 256};
-
 // The hash-table classes (k_rowprod_hash): table sizes tried in order; a
 // row counted -1 at one size is recounted at the next. Groups per workgroup:
 // at least a wavefront, at most 256 lanes and 64 KiB of LDS (16 B per slot
 // in the numeric pass).
 constexpr int kHashClasses = 6;
 constexpr int kHashT[kHashClasses] = {16, 32, 64, 128, 256, 1024};
-constexpr int kHashClassId = 16;  // klass ids kHashClassId + t (the lane classes use 0..4)
+constexpr int kHashClassId = 16;  // klass ids kHashClassId + t
 
 template <int G, int T>
 constexpr int hash_groups() {
@@ -1029,10 +779,7 @@ hipError_t rowprod_hash_pass(const DCsr &A, const DCsr &B, int32_t *cnt, int32_t
     constexpr int NG = hash_groups<G, T>();
     static_assert(NG * T * 16 <= 65536, "LDS per workgroup");
     const unsigned grid = (unsigned)std::min<int64_t>(blocks_for(A.m, NG), (int64_t)n_cu * 32);
-    static const bool pipe = [] {
-        const char *v = std::getenv("AIJHIP_GAMG_HASH_PIPE");
-        return !(v && v[0] == '0');
-    }();
+    constexpr bool pipe = true;  // the next B row's first entries loaded while the current one's go in (-10 %)
     if (!numeric)
         hipLaunchKernelGGL((k_rowprod_hash<G, T, NG, false>), dim3(grid), dim3(G * NG), 0, nullptr, A.m, A.ai, A.aj,
                            A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, klass, myclass, redo, pipe);
@@ -1066,24 +813,6 @@ hipError_t rowprod_hash_class(int t, int G, const DCsr &A, const DCsr &B, int32_
     return hipErrorInvalidValue;
 }
 
-hipError_t rowprod_class(int c, const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, bool redo,
-                         const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
-    switch (c) {
-        case 0: return rowprod_pass<32, 64, 1>(A, B, cnt, klass, 0, redo, ci, C, numeric, n_cu);
-        case 1: return rowprod_pass<32, 128, 2>(A, B, cnt, klass, 1, redo, ci, C, numeric, n_cu);
-        case 2: return rowprod_pass<64, 64, 2>(A, B, cnt, klass, 2, redo, ci, C, numeric, n_cu);
-        case 3: return rowprod_pass<128, 32, 2>(A, B, cnt, klass, 3, redo, ci, C, numeric, n_cu);
-        default: return rowprod_pass<256, 16, 1>(A, B, cnt, klass, 4, redo, ci, C, numeric, n_cu);
-    }
-}
-
-// AIJHIP_GAMG_HASH=0: the round-2 product forms (lane per row, wavefront
-// per row for small A) instead of the hash-table groups; the same bits
-bool hash_off() {
-    const char *v = std::getenv("AIJHIP_GAMG_HASH");
-    return v && v[0] == '0';
-}
-
 // the minimum of cnt[0..m) (0 when m = 0)
 hipError_t min_of(const int32_t *cnt, int32_t m, int32_t *mn) {
     *mn = 0;
@@ -1108,7 +837,7 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
 constexpr int kP0Cap = 8;
 int rowprod_p0(const DCsr &A, const DCsr &P0, DCsr &C, int n_cu, int *cols_used) {
     // (rows of A longer than the list on average: the hash form directly)
-    if (hash_off() || A.nz > (int64_t)kP0Cap * std::max<int32_t>(A.m, 1)) return rowprod(A, P0, C, n_cu, cols_used);
+    if (A.nz > (int64_t)kP0Cap * std::max<int32_t>(A.m, 1)) return rowprod(A, P0, C, n_cu, cols_used);
     C = DCsr();
     C.m = A.m;
     C.n = P0.n;
@@ -1169,11 +898,10 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
         per_row = B.m > 0 ? (double)A.nz * ((double)bnz / (double)B.m) / std::max<int32_t>(A.m, 1) : 0.0;
         b_row = B.m > 0 ? (double)bnz / (double)B.m : 0.0;
     }
-    if (!hash_off()) {
+    {
         // G lanes per row: B's mean row length rounded up to a power of two
         int G = 4;
         while (G < 64 && G < b_row) G <<= 1;
-        if (const char *v = std::getenv("AIJHIP_GAMG_HASH_G")) G = std::max(4, std::min(64, std::atoi(v)));
         const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
         int32_t *klass = nullptr;
@@ -1189,7 +917,6 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
         // overflow it are recounted with the next
         int first = 0;
         while (first + 1 < kHashClasses && kHashT[first] <= std::min(per_row, 48.0)) ++first;
-        if (const char *v = std::getenv("AIJHIP_GAMG_HASH_T0")) first = std::max(0, std::min(kHashClasses - 1, std::atoi(v)));
         int last = -1;
         for (int t = first; t < kHashClasses; ++t) {
             if ((e = rowprod_hash_class(t, hash_lanes(G, t), A, B, cnt, klass, t > first, nullptr, nullptr, false,
@@ -1236,96 +963,6 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
         }
         return AIJHIP_OK;
     }
-    constexpr int kWaveK = 16;  // columns per lane: up to 1024 per row
-    const unsigned gw = (unsigned)std::max<int64_t>(1, std::min<int64_t>((A.m + 3) / 4, (int64_t)n_cu * 16));
-    // the wave form pays off for few, heavy rows (coarse Galerkin products:
-    // 744 rows of ~20k products, 34 -> 15 ms at 300^3); for many light rows
-    // one lane per row keeps every lane busy (27 M rows: 27 vs 288 ms)
-    // (for many heavy rows too: at 300^3 the finest P^T (A P), 3.27 M rows of
-    // ~270 products, 43 ms one lane per row vs 322 ms one wave per row; the
-    // next level's, 71.7 K rows of ~3460 products, 34 vs 89 ms)
-    if (std::getenv("AIJHIP_GAMG_LOG"))
-        std::fprintf(stderr, "  product %d x %d: %.0f products per row -> %s\n", A.m, B.n, per_row,
-                     A.m <= 8192 ? "wavefront per row" : "lane per row");
-    if (A.m <= 8192) {
-        hipLaunchKernelGGL((k_rowprod_wave<kWaveK, false>), dim3(gw), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt);
-        int32_t mn = 0;
-        if ((e = hipGetLastError()) == hipSuccess && A.m > 0) e = min_of(cnt, A.m, &mn);
-        if (e != hipSuccess) { hipFree(cnt); return herr(e, "symbolic product"); }
-        if (mn >= 0) {  // every row fits the wave form
-            if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) { hipFree(cnt); return herr(e, "product rows"); }
-            int64_t total = 0;
-            if ((e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess) { hipFree(cnt); C.release(); return herr(e, "scan"); }
-            if (total > INT32_MAX) {
-                hipFree(cnt);
-                C.release();
-                set_error("GAMG device set-up: product exceeds int32 indices");
-                return AIJHIP_ERR_ARG;
-            }
-            C.nz = total;
-            if ((e = dalloc(&C.aj, total + 2)) != hipSuccess || (e = dalloc(&C.aa, total + 2)) != hipSuccess ||
-                (e = hipMemset(C.aj + total, 0, 2 * sizeof(int32_t))) != hipSuccess ||
-                (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess) {
-                hipFree(cnt);
-                C.release();
-                return herr(e, "product alloc");
-            }
-            hipLaunchKernelGGL((k_rowprod_wave<kWaveK, true>), dim3(gw), dim3(256), 0, nullptr, A.m, A.ai, A.aj,
-                               A.aa, B.ai, B.aj, B.aa, C.ai, C.aj, C.aa, nullptr);
-            hipFree(cnt);
-            if ((e = hipGetLastError()) != hipSuccess) { C.release(); return herr(e, "numeric product"); }
-            return AIJHIP_OK;  // the wavefront form: *cols_used stays as it was
-        }
-    }
-    // one lane per row, the row's distinct columns in LDS: capacity classes
-    // 64 / 128 / 256 (a row counted -1 by a class is recounted by the next)
-    auto min_count = [&](int32_t *mn) -> hipError_t { return min_of(cnt, A.m, mn); };
-    // light products (A*P0, A*P on the finest level: ~4 and ~25 products
-    // per row) start in the 32-column class: 24 KiB of LDS per 64-row
-    // workgroup in the numeric pass instead of 48, twice the waves per CU
-    int32_t *klass = nullptr;
-    if ((e = dalloc(&klass, A.m)) != hipSuccess) { hipFree(cnt); return herr(e, "product classes"); }
-    const int first = per_row <= 48.0 ? 0 : 1;
-    int last = first;
-    for (;; ++last) {
-        if (last >= kProdClasses) { hipFree(cnt); hipFree(klass); return AIJHIP_ERR_STATE; }
-        e = rowprod_class(last, A, B, cnt, klass, last > first, nullptr, nullptr, false, n_cu);
-        int32_t mn = 0;
-        if (e != hipSuccess || (e = min_count(&mn)) != hipSuccess) {
-            hipFree(cnt); hipFree(klass);
-            return herr(e, "symbolic product");
-        }
-        if (mn >= 0) break;
-    }
-    auto bail = [&](hipError_t r, const char *what) {
-        hipFree(cnt);
-        hipFree(klass);
-        C.release();
-        return herr(r, what);
-    };
-    if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess) return bail(e, "product rows");
-    int64_t total = 0;
-    if ((e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess) return bail(e, "scan");
-    if (total > INT32_MAX) {
-        hipFree(cnt);
-        hipFree(klass);
-        C.release();
-        set_error("GAMG device set-up: product exceeds int32 indices");
-        return AIJHIP_ERR_ARG;
-    }
-    C.nz = total;
-    if ((e = dalloc(&C.aj, total + 2)) != hipSuccess || (e = dalloc(&C.aa, total + 2)) != hipSuccess ||
-        (e = hipMemset(C.aj + total, 0, 2 * sizeof(int32_t))) != hipSuccess ||
-        (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess)
-        return bail(e, "product alloc");
-    for (int c = first; c <= last && e == hipSuccess; ++c)
-        e = rowprod_class(c, A, B, cnt, klass, false, C.ai, &C, true, n_cu);
-    if (e != hipSuccess) return bail(e, "numeric product");
-    hipFree(cnt);
-    hipFree(klass);
-    if (cols_used) *cols_used = std::max(*cols_used, kProdClassCols[last]);
-    return AIJHIP_OK;
 }
 
 // S directly from A (k_strong_direct_*): *ok = false, nothing allocated,
@@ -1656,7 +1293,7 @@ int make_handle(int device, DCsr &C, aijhip_mat **out) {
 // offsets back to the host (27 M rows at 300^3, ~14 ms) and nothing before
 // the V-cycle needs it, so it overlaps the next level's aggregation, whose
 // phase 1 keeps the GPU idle on coarse levels. Joined before build_device
-// returns. AIJHIP_GAMG_HANDLE_SYNC=1: made in line (A/B).
+// returns.
 struct HandleJob {
     std::thread th;
     size_t level = 0;
@@ -1686,10 +1323,6 @@ struct HandleJob {
     }
 };
 
-bool handles_in_line() {
-    const char *v = std::getenv("AIJHIP_GAMG_HANDLE_SYNC");
-    return v && v[0] == '1';
-}
 
 // Which side runs aggregation phase 1 (both give the same aggregates): the
 // device sweep for levels of at least 2^20 rows whose S averages at most 16
@@ -2110,7 +1743,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     const int n_cu = std::max(A0->n_cu, 1);
     int rc = AIJHIP_OK;
     hipError_t e = hipSuccess;
-    const bool in_line = handles_in_line();
+    constexpr bool in_line = false;  // (in line measured ~14 ms slower at 300^3)
     std::vector<std::unique_ptr<HandleJob>> jobs;
     // the near-null space of the current level, on the device (ones at the top)
     double *d_B = nullptr;

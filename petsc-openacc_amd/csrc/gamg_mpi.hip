@@ -700,8 +700,7 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
     };
     const int P = C->nranks, me = C->rank;
     const int n_cu = std::max(M0->Ad->n_cu, 1);
-    const char *hs = std::getenv("AIJHIP_GAMG_HANDLE_SYNC");
-    const bool in_line = hs && hs[0] == '1';
+    constexpr bool in_line = false;  // the interpolation handles come from a second host thread
     std::vector<std::unique_ptr<PJob>> jobs;
     hipError_t e;
     int rc = AIJHIP_OK;

@@ -130,22 +130,14 @@ struct aijhip_ksp {
     bool set_up = false;
     bool fused = false;
     int vec_grid = 0;
-    // CG vector kernels store with the non-temporal hint; AIJHIP_VEC_NT=0/1
-    // overrides (diagnostic A/B, read at KSPCreate).
-    bool vec_nt = true;
-    // V-cycle pre-smoothing on fused levels: false = one launch gathering
-    // dinv_j * b_j (OpMgPre), true = x = D^-1 b pass + residual SpMV
-    // (OpMgResid). Measured at 300^3 (profiles/r01/mg_pre_split/): the split
-    // form solves in 0.205 s vs 0.221 s — the second gather per entry costs
-    // more (fine level 719 us) than writing and re-reading x (130 + 523 us).
-    // AIJHIP_MG_PRE_SPLIT=0/1 overrides (A/B).
-    bool mg_pre_split = true;
-    // X += a P in the r/z update after the SpMV (PETSc's place) instead of
-    // deferred into the next p = z + b p pass: same bytes, but the kernel
-    // before each SpMV leaves only p dirty. AIJHIP_CG_X_IN_UPDATE=0/1 (A/B).
-    // Measured (profiles/r01/x_in_update/, 3 alternating rounds): CG+Jacobi
-    // 400 its 0.376 -> 0.392 s, CG+GAMG 0.205 -> 0.207 s, hence off.
-    bool x_in_update = false;
+    // CG vector kernels store with the non-temporal hint (tools: CG+Jacobi
+    // 1053 -> 1093 it/s). V-cycle pre-smoothing on fused levels is x = D^-1 b
+    // as a vector pass, then r = b - A x in the SpMV epilogue (OpMgResid):
+    // one launch gathering dinv_j * b_j solved in 0.221 s against 0.205 s
+    // (profiles/r01/mg_pre_split/). X += a P is deferred into the next
+    // p = z + b p pass: in the r/z update (PETSc's place) CG+Jacobi took
+    // 0.392 s against 0.376 s per 400 iterations (profiles/r01/x_in_update/).
+    // (Those A/B forms were withdrawn in round 4.)
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
     double *d_hist = nullptr;
     int32_t hist_cap = 0;
@@ -318,7 +310,8 @@ int gamg_setup(aijhip_ksp *K) {
 
 // PCApply_MG (multiplicative, one V-cycle) on the finest-level input b,
 // output x. On STREAM-planned levels the smoothing passes ride in the SpMV
-// (aijhip::launch_mg_pre / _post): pre-smoothing + residual is one launch,
+// (aijhip::launch_mg_resid / _post): the residual rides in the SpMV after
+// the x = D^-1 b vector pass,
 // and interpolation writes t = x + P x_c to the level's scratch so the
 // post-smoothing launch reads t and writes x. With dots != NULL the finest
 // post-smoothing also leaves z.z / z.b partials there (*dots_done = true).
@@ -336,13 +329,10 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
             hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
             break;
         }
-        if (L.fused && K->mg_pre_split) {
+        if (L.fused) {
             // smoothd as a vector pass, then r = b - A x in the SpMV epilogue
             hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
-            if ((e = aijhip::launch_mg_resid(*L.A, X(l), B(l), L.r, s, K->vec_nt, stop)) != hipSuccess) return e;
-        } else if (L.fused) {
-            if ((e = aijhip::launch_mg_pre(*L.A, B(l), L.dinv, X(l), L.r, s, K->vec_nt, stop)) != hipSuccess)
-                return e;
+            if ((e = aijhip::launch_mg_resid(*L.A, X(l), B(l), L.r, s, true, stop)) != hipSuccess) return e;
         } else {
             hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);  // smoothd
             if ((e = aijhip::launch_mult(*L.A, X(l), nullptr, L.r, false, s, stop)) != hipSuccess) return e;
@@ -358,7 +348,7 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
             // MatInterpolateAdd into the scratch: t = x + P x_c, then smoothu
             if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), L.r, true, s, stop)) != hipSuccess) return e;
             double *dp = (l == 0 && dots) ? dots : nullptr;
-            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s, K->vec_nt, stop)) != hipSuccess)
+            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s, true, stop)) != hipSuccess)
                 return e;
             if (dp && dots_done) *dots_done = true;
         } else {
@@ -396,9 +386,6 @@ int aijhip_ksp_create(aijhip_mat_t A, aijhip_ksp_t *out) {
     aijhip_ksp *K = new (std::nothrow) aijhip_ksp();
     if (!K) return kfail(AIJHIP_ERR_ALLOC, "host allocation");
     K->A = A;
-    if (const char *v = std::getenv("AIJHIP_VEC_NT")) K->vec_nt = std::atoi(v) != 0;
-    if (const char *v = std::getenv("AIJHIP_MG_PRE_SPLIT")) K->mg_pre_split = std::atoi(v) != 0;
-    if (const char *v = std::getenv("AIJHIP_CG_X_IN_UPDATE")) K->x_in_update = std::atoi(v) != 0;
     aijhip_gamg_params_default(&K->gamg);
     *out = K;
     return AIJHIP_OK;
@@ -547,9 +534,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             return khip(e, "KSPSolve poll");
         if (K->h_state->done || launched >= K->max_it) break;
         for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched) {
-            double *xa = K->x_in_update ? nullptr : x, *xu = K->x_in_update ? x : nullptr;
-            if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, xa, K->d_state);
-            else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, xa, K->d_state);
+            hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             if (K->fused) {
                 e = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, s);
                 if (e == hipSuccess)
@@ -559,12 +544,8 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
                 hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
                 hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, nb, K->d_state);
             }
-            if (K->vec_nt)
-                hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
-                                   K->d_state, K->pc, K->d_p, xu);
-            else
-                hipLaunchKernelGGL(k_update<false>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
-                                   K->d_state, K->pc, K->d_p, xu);
+            hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
+                               K->d_state, K->pc, K->d_p, nullptr);
             const double *pz = K->d_part;
             int nbz = nb;
             if (gamg && e == hipSuccess) {
@@ -584,7 +565,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve iteration");
         }
     }
-    if (!K->x_in_update) hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
+    hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
     if ((e = hipGetLastError()) != hipSuccess ||
         (e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)

@@ -600,7 +600,7 @@ struct aijhip_kspmpi {
     int pc = AIJHIP_PC_JACOBI;
     int normtype = AIJHIP_KSP_NORM_PRECONDITIONED;
     int32_t poll = 8;
-    bool set_up = false, fused = false, vec_nt = true;
+    bool set_up = false, fused = false;
     // PC GAMG = PETSc's -pc_type bjacobi -sub_pc_type gamg: a GAMG hierarchy of
     // this rank's diagonal block (a single-GPU KSP's set-up), one V-cycle per
     // application, no communication inside the preconditioner
@@ -958,7 +958,6 @@ int aijhip_kspmpi_create(aijhip_mpiaij_t M, aijhip_kspmpi_t *out) {
     aijhip_kspmpi *K = new (std::nothrow) aijhip_kspmpi();
     if (!K) return mfail(AIJHIP_ERR_ALLOC, "host allocation");
     K->M = M;
-    if (const char *v = std::getenv("AIJHIP_VEC_NT")) K->vec_nt = std::atoi(v) != 0;
     *out = K;
     return AIJHIP_OK;
 }
@@ -1064,8 +1063,7 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
         if (K->h_state->done || launched >= K->max_it) break;
         const int32_t poll = K->poll;  // every CG and V-cycle kernel returns at once past the flag
         for (int j = 0; j < poll && launched < K->max_it; ++j, ++launched) {
-            if (K->vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
-            else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
+            hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
             // W = A P with the p.w partials (W shares Z's storage)
             if ((rc = mpiaij_apply(M, K->d_p, K->d_z, s, K->d_part, opart, K->d_state, K->fused))) return rc;
             if (!K->fused) hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
@@ -1075,12 +1073,8 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
                 if ((rc = comm_allreduce(C, K->d_red, 1, s))) return rc;
                 hipLaunchKernelGGL(k_step_dpi, dim3(1), dim3(64), 0, s, K->d_red, K->d_state);
             }
-            if (K->vec_nt)
-                hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state,
-                                   K->pc, K->d_p, nullptr);
-            else
-                hipLaunchKernelGGL(k_update<false>, vg, vt, 0, s, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state,
-                                   K->pc, K->d_p, nullptr);
+            hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state,
+                               K->pc, K->d_p, nullptr);
             if (gamg) {  // z = B r; z.z and z.r from the fused finest post-smoothing, else k_dots
                 const double *dots = nullptr;
                 int nbz = 0;

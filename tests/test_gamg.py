@@ -110,10 +110,11 @@ def test_gpu_cg_gamg_matches_oracle(pkg, N, norm):
 
 
 @pytest.mark.gpu
-def test_gpu_vcycle_pre_smoothing_forms_bitwise(pkg, monkeypatch):
-    """The split pre-smoothing (x = D^-1 b pass + residual SpMV, default) and
-    the one-launch form (gathering dinv_j b_j) round identically: the whole
-    CG+GAMG solve is bit-for-bit the same."""
+def test_gpu_vcycle_fused_smoothers_bitwise(pkg, monkeypatch):
+    """The fused V-cycle smoothers (residual and Richardson+Jacobi step in the
+    SpMV epilogue, default) and the unfused kernels (PCMG's separate
+    smoother, MatResidual and vector passes; AIJHIP_MG_UNFUSED=1) round
+    identically on one GPU: the whole CG+GAMG solve is bit-for-bit the same."""
     torch = pytest.importorskip("torch")
     assert torch.cuda.is_available()
     K = importlib.import_module("petsc-openacc_amd.ksp")
@@ -122,9 +123,11 @@ def test_gpu_vcycle_pre_smoothing_forms_bitwise(pkg, monkeypatch):
     rhs, _ = pkg.poisson_vectors(N)
     b = torch.from_numpy(rhs).cuda()
     out = []
-    monkeypatch.delenv("AIJHIP_MG_UNFUSED", raising=False)
-    for split in ("1", "0"):
-        monkeypatch.setenv("AIJHIP_MG_PRE_SPLIT", split)
+    for unfused in (None, "1"):
+        if unfused is None:
+            monkeypatch.delenv("AIJHIP_MG_UNFUSED", raising=False)
+        else:
+            monkeypatch.setenv("AIJHIP_MG_UNFUSED", unfused)
         with pkg.SeqAIJHIP(ai, aj, aa) as A:
             x = torch.empty_like(b)
             with K.KSPCG(A, pc="gamg", rtol=1e-14, atol=1e-12) as ksp:

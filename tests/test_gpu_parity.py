@@ -423,6 +423,79 @@ def test_long_row_xcd_placement_is_speed_only(pkg, dev, coracle):
         assert_bits(yd.cpu().numpy(), wd.cpu().numpy())
 
 
+@pytest.mark.parametrize("force", [-1, 1])
+def test_long_rows_by_x_window(pkg, dev, coracle, force):
+    """Long rows summed by x column window (AIJHIP_OPT_LONG_WINDOW; automatic
+    on the skewed stand-in, whose hub rows are column-sorted): MatMult and
+    MatMultAdd within the fp64 bound, the same bits launch after launch, the
+    short rows bit-exact, and the same values as the segment form to the
+    bound; an MPIAIJ-style unaligned x (offset by one entry) too."""
+    ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
+    m = len(ai) - 1
+    x = pkg.splitmix_uniform(m + 1, 7)
+    z = pkg.splitmix_uniform(m, 8)
+    ref = coracle.matmult(ai, aj, aa, x[:m], omp=True)
+    short = np.diff(ai) <= 2048
+    with pkg.SeqAIJHIP(ai, aj, aa, exact=1, long_window=force) as A:
+        info = A.info()
+        assert info["n_long_rows"] > 0 and info["long_windows"] == (m + 2047) // 2048
+        xd = to_dev(x, dev)
+        zd = to_dev(z, dev)
+        y1 = torch.full((m,), np.nan, dtype=torch.float64, device=dev)
+        y2 = torch.empty_like(y1)
+        w = torch.empty_like(y1)
+        A.mult(xd, y1)
+        A.mult(xd, y2)
+        A.mult_add(xd, zd, w)
+        torch.cuda.synchronize()
+        y = y1.cpu().numpy()
+        assert torch.equal(y1, y2)
+        check(y, ref, ai, aj, aa, x[:m], exact=False)
+        assert_bits(y, ref, short)
+        check(w.cpu().numpy(), coracle.matmult_add(ai, aj, aa, x[:m], z), ai, aj, aa, x[:m], exact=False, z=z)
+        # x at an 8-byte offset (a ghost buffer inside a larger tensor)
+        xo = torch.zeros(m + 2, dtype=torch.float64, device=dev)
+        xo[1:m + 1] = xd[:m]
+        A.mult(xo[1:m + 1], y2)
+        torch.cuda.synchronize()
+        assert torch.equal(y1, y2)
+        A.set_option("long_window", 0)
+        assert A.info()["long_windows"] == 0
+        A.mult(xd, y2)
+        torch.cuda.synchronize()
+        check(y2.cpu().numpy(), ref, ai, aj, aa, x[:m], exact=False)
+
+
+def test_long_window_needs_sorted_rows(pkg, dev, coracle):
+    """A long row whose columns are not ascending keeps the segment form even
+    when windows are asked for (its window runs would not be contiguous)."""
+    rng = np.random.default_rng(3)
+    m = 50000
+    lens = np.full(m, 5)
+    lens[[100, 20000]] = 30000
+    ai = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    rows = [np.sort(rng.choice(m, size=l, replace=False)) for l in lens]
+    rows[20000] = rows[20000][::-1].copy()  # descending
+    aj = np.concatenate(rows).astype(np.int32)
+    aa = rng.uniform(-1, 1, ai[-1])
+    x = rng.uniform(-1, 1, m)
+    with pkg.SeqAIJHIP(ai, aj, aa, long_window=1) as A:
+        assert A.info()["n_long_rows"] == 2 and A.info()["long_windows"] == 0
+        xd = to_dev(x, dev)
+        yd = torch.empty(m, dtype=torch.float64, device=dev)
+        A.mult(xd, yd)
+        torch.cuda.synchronize()
+        check(yd.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True), ai, aj, aa, x, exact=False)
+    rows[20000] = rows[20000][::-1].copy()
+    aj = np.concatenate(rows).astype(np.int32)
+    with pkg.SeqAIJHIP(ai, aj, aa, long_window=1) as A:
+        assert A.info()["long_windows"] == (m + 2047) // 2048  # forced: sorted now
+        yd = torch.empty(m, dtype=torch.float64, device=dev)
+        A.mult(to_dev(x, dev), yd)
+        torch.cuda.synchronize()
+        check(yd.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True), ai, aj, aa, x, exact=False)
+
+
 @pytest.mark.parametrize("name", ["poisson16", "skewed_small", "compressed_small"])
 def test_stream_options_do_not_change_results(pkg, dev, name):
     """Every STREAM geometry / non-temporal setting is speed-only; the
