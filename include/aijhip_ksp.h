@@ -92,6 +92,17 @@ int aijhip_ksp_get_fused(aijhip_ksp_t ksp, int *fused);
  * flag (one per batch of 8 iterations, AIJHIP_KSP_POLL overrides) plus the
  * final read. */
 int aijhip_ksp_get_host_syncs(aijhip_ksp_t ksp, int32_t *n);
+/* Compulsory HBM bytes one CG iteration of the set-up solver moves (the
+ * roofline of the solve): every SpMV at its plan's layout bytes
+ * (aijhip_info_t.mult_layout_bytes: matrix, x once, y once) plus the vector
+ * passes' reads and writes — CG's p = z + b p (with the deferred x += a p),
+ * the r update, and for GAMG per level the Jacobi pass, the residual and
+ * post-smoothing SpMVs with their b / D^-1 reads, MatRestrict (P^T),
+ * MatInterpolateAdd (P, reading the level's x) and the coarse Jacobi. The
+ * per-part split: *spmv_bytes of the total are matrix launches, *level0 of
+ * the total belong to the finest level (its SpMVs and vectors). Valid after
+ * set-up; the first iteration moves a little less. */
+int aijhip_ksp_get_iteration_bytes(aijhip_ksp_t ksp, int64_t *bytes, int64_t *spmv_bytes, int64_t *level0);
 /* GAMG options (before set-up); NULL = PETSc defaults
  * (aijhip_gamg_params_default). */
 int aijhip_ksp_set_gamg_params(aijhip_ksp_t ksp, const aijhip_gamg_params_t *p);

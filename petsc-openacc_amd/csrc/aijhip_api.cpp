@@ -820,12 +820,12 @@ int attach_transpose(aijhip_mat *A, int32_t *tai, int32_t *taj, double *taa) {
 }
 }  // namespace aijhip
 
-namespace {
+namespace aijhip {
 // Compulsory bytes of one MatMult under the plan in effect: the arrays the
 // launched kernels stream (each read once), x read once, y written once —
 // SURVEY §8d's count for the layout actually read. Block descriptors,
 // dictionaries and pattern tables are included where the layout needs them.
-int64_t layout_bytes(const aijhip_mat &A) {
+int64_t mult_layout_bytes(const aijhip_mat &A) {
     const aijhip::Plan &P = A.plan;
     const int64_t m = A.m, n = A.n, nz = A.nz;
     const int64_t rows = A.compressed ? (4 * ((int64_t)A.n_crow + 1) + 4 * (int64_t)A.n_crow) : 4 * (m + 1);
@@ -841,7 +841,7 @@ int64_t layout_bytes(const aijhip_mat &A) {
         return 14 * nz + rows + vec;
     return 12 * nz + rows + vec;
 }
-}  // namespace
+}  // namespace aijhip
 
 extern "C" {
 
@@ -1138,7 +1138,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
     info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
     info->long_windows = A->plan.d_wbnd != nullptr ? A->plan.n_win : 0;
-    info->mult_layout_bytes = layout_bytes(*A);
+    info->mult_layout_bytes = aijhip::mult_layout_bytes(*A);
     return AIJHIP_OK;
 }
 

@@ -351,6 +351,9 @@ void host_pipe_free(HostPipe *p);
 hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t s, const double **dots,
                          int *nbz, const int *stop = nullptr);
 
+// Compulsory bytes one MatMult under A's plan moves (aijhip_info_t.mult_layout_bytes).
+int64_t mult_layout_bytes(const aijhip_mat &A);
+
 // Sets the calling thread's aijhip_last_error() message.
 void set_error(const std::string &msg);
 int visible_devices();  // hipGetDeviceCount, cached

@@ -698,7 +698,9 @@ __global__ void k_window_bounds(int32_t nl, int32_t nw, int32_t W, const int32_t
     const int32_t i = (int32_t)(g / (nw + 1)), w = (int32_t)(g - (int64_t)i * (nw + 1));
     const int32_t r = rows[i];
     int32_t lo = ai[r], hi = ai[r + 1];
-    if (w < nw) {
+    if (w == nw) {
+        lo = hi;
+    } else {
         const int64_t c = (int64_t)w * W;
         while (lo < hi) {
             const int32_t mid = lo + ((hi - lo) >> 1);

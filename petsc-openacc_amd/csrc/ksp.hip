@@ -615,6 +615,45 @@ int aijhip_ksp_get_host_syncs(aijhip_ksp_t K, int32_t *n) {
     return AIJHIP_OK;
 }
 
+int aijhip_ksp_get_iteration_bytes(aijhip_ksp_t K, int64_t *bytes, int64_t *spmv_bytes, int64_t *level0) {
+    if (!K || !bytes) return kfail(AIJHIP_ERR_ARG, "NULL argument");
+    if (!K->set_up) return kfail(AIJHIP_ERR_STATE, "KSP is not set up");
+    const int64_t m = K->A->m;
+    const int64_t a0 = aijhip::mult_layout_bytes(*K->A);
+    // CG: p = z + b p with x += a p (reads z, p, x; writes p, x), the SpMV
+    // (p . w in its epilogue), the r update (Jacobi: reads r, w, D^-1,
+    // writes r, z; GAMG: reads r, w, writes r; z from the V-cycle)
+    int64_t spmv = a0, vec = 40 * m + (K->pc == AIJHIP_PC_GAMG ? 24 * m : 40 * m);
+    if (!K->fused) vec += 16 * m;  // p . w in its own pass
+    int64_t lev0 = a0 + vec;
+    if (K->pc == AIJHIP_PC_GAMG) {
+        const int nl = (int)K->mg.size();
+        for (int l = 0; l < nl; ++l) {
+            const MGLevel &L = K->mg[l];
+            const int64_t ml = L.m;
+            int64_t sp = 0, v = 0;
+            if (l == nl - 1) {
+                v = 24 * ml;  // coarse: x = D^-1 b
+            } else {
+                const int64_t la = aijhip::mult_layout_bytes(*L.A);
+                const int64_t lp = aijhip::mult_layout_bytes(*L.P);
+                const int64_t lt = L.P->transpose ? aijhip::mult_layout_bytes(*L.P->transpose) : lp;
+                if (L.fused)  // D^-1 b pass; r = b - A x (+ b); P^T r; t = x + P x_c (+ x); x = t + D^-1 (b - A t) (+ b, D^-1)
+                    sp = la + lt + lp + la, v = 24 * ml + 8 * ml + 8 * ml + 16 * ml;
+                else  // the same with the residual and Richardson passes separate
+                    sp = la + lt + lp + la, v = 24 * ml + 24 * ml + 8 * ml + 40 * ml;
+            }
+            spmv += sp;
+            vec += v;
+            if (l == 0) lev0 += sp + v;
+        }
+    }
+    *bytes = spmv + vec;
+    if (spmv_bytes) *spmv_bytes = spmv;
+    if (level0) *level0 = lev0;
+    return AIJHIP_OK;
+}
+
 int aijhip_ksp_get_fused(aijhip_ksp_t K, int *fused) {
     if (!K || !fused) return kfail(AIJHIP_ERR_ARG, "NULL argument");
     *fused = K->fused ? 1 : 0;

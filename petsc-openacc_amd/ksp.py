@@ -28,7 +28,7 @@ KSP_SYMBOLS = (
     "aijhip_ksp_get_iteration_number", "aijhip_ksp_get_residual_norm", "aijhip_ksp_get_converged_reason",
     "aijhip_ksp_get_residual_history", "aijhip_ksp_get_fused", "aijhip_ksp_destroy",
     "aijhip_ksp_set_gamg_params", "aijhip_ksp_get_pc_levels", "aijhip_ksp_get_pc_level",
-    "aijhip_ksp_get_gamg_setup_path", "aijhip_ksp_get_host_syncs",
+    "aijhip_ksp_get_gamg_setup_path", "aijhip_ksp_get_host_syncs", "aijhip_ksp_get_iteration_bytes",
 )
 _P = ctypes.c_void_p
 _bound = False
@@ -53,6 +53,8 @@ def _lib():
         L.aijhip_ksp_get_residual_history.argtypes = [_P, _P, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]
         L.aijhip_ksp_get_fused.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
         L.aijhip_ksp_get_host_syncs.argtypes = [_P, ctypes.POINTER(ctypes.c_int32)]
+        L.aijhip_ksp_get_iteration_bytes.argtypes = [_P, ctypes.POINTER(ctypes.c_int64),
+                                                     ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]
         L.aijhip_ksp_destroy.argtypes = [_P]
         L.aijhip_ksp_set_gamg_params.argtypes = [_P, _P]
         L.aijhip_ksp_get_pc_level.argtypes = [_P, ctypes.c_int32, ctypes.c_char, ctypes.POINTER(ctypes.c_int32),
@@ -116,6 +118,14 @@ class KSPCG:
         v = ctypes.c_int32()
         _pkg._check(_lib().aijhip_ksp_get_host_syncs(self._h, ctypes.byref(v)))
         return v.value
+
+    def iteration_bytes(self):
+        """(total, SpMV part, finest-level part): compulsory HBM bytes of one
+        CG iteration of the set-up solver (aijhip_ksp_get_iteration_bytes)."""
+        t, sp, l0 = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        _pkg._check(_lib().aijhip_ksp_get_iteration_bytes(self._h, ctypes.byref(t), ctypes.byref(sp),
+                                                          ctypes.byref(l0)))
+        return t.value, sp.value, l0.value
 
     @property
     def fused(self) -> bool:
@@ -183,15 +193,6 @@ class KSPCG:
             pass
 
 
-def cg_bytes_per_iteration(m: int, nnz: int, fused: bool) -> int:
-    """Algorithmic HBM bytes of one CG iteration: SpMV (SURVEY §8d bytes) +
-    the P read of the fused dot, AYPX (2 reads + 1 write), the fused update
-    (X, P, R, W/Z, D^-1 read; X, R, Z written)."""
-    spmv = 12 * nnz + 4 * (m + 1) + 16 * m
-    dot = 8 * m if fused else 16 * m
-    return spmv + dot + 24 * m + 64 * m
-
-
 def bench_cg(pkg, A, nx, ny, nz, dev, iters=200):
     """CG iterations/s on the device at the benchmark operand: a fixed count
     of iterations (rtol = atol = 0, so every iteration runs), timed whole."""
@@ -208,11 +209,15 @@ def bench_cg(pkg, A, nx, ny, nz, dev, iters=200):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         its, fused = ksp.its, ksp.fused
-    m = A.m
-    nb = cg_bytes_per_iteration(m, A.nz, fused)
+        nb, nb_spmv, _ = ksp.iteration_bytes()
     return {"iters": its, "seconds": round(dt, 4), "iters_per_s": round(its / dt, 2),
             "ms_per_iter": round(dt / its * 1e3, 4), "pc": "jacobi", "fused_spmv_dot": fused,
-            "bytes_per_iter": nb, "GBs": round(nb * its / dt / 1e9, 1)}
+            "bytes_per_iter": nb, "GBs": round(nb * its / dt / 1e9, 1),
+            "roofline": {"bound": "hbm", "bytes_per_iter": nb, "spmv_bytes_per_iter": nb_spmv,
+                         "achieved": round(nb * its / dt / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                         "frac": round(nb * its / dt / 1e9 / 8000.0, 4),
+                         "note": "aijhip_ksp_get_iteration_bytes: the SpMV at its layout's bytes + the vector "
+                                 "passes, per iteration, over the measured wall time of the iterations"}}
 
 
 def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000):
@@ -243,6 +248,7 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
         torch.cuda.synchronize()
         t_solve = time.perf_counter() - t0
         its, reason, rnorm, syncs = ksp.its, ksp.reason, ksp.rnorm, ksp.host_syncs
+        nb, nb_spmv, nb_l0 = ksp.iteration_bytes()
     err = float((x.cpu() - torch.from_numpy(exact)).abs().max())
     # the same set-up again in this process (a caller that rebuilds the
     # hierarchy after new values): the first one above also pays one-time
@@ -259,6 +265,13 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
             "ms_per_iter": round(t_solve / max(its, 1) * 1e3, 4), "host_syncs": syncs,
             "time_to_solution_s": round(t_setup + t_solve, 3),
             "levels": [{"rows": r, "nnz": z} for r, z in zip(rows, nnz)],
+            "roofline": {"bound": "hbm", "bytes_per_iter": nb, "spmv_bytes_per_iter": nb_spmv,
+                         "finest_level_bytes_per_iter": nb_l0,
+                         "achieved": round(nb * its / t_solve / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+                         "frac": round(nb * its / t_solve / 1e9 / 8000.0, 4),
+                         "note": "aijhip_ksp_get_iteration_bytes (every SpMV of the hierarchy at its layout's "
+                                 "bytes — A_l twice, P, P^T per level — plus CG's and the V-cycle's vector passes) "
+                                 "x iterations / the solve's wall time (polls and launch gaps included)"},
             "options": "cg, gamg agg nsmooths 1 threshold 0, mg levels richardson(1)+jacobi, "
                        "coarse preonly+jacobi, rtol 1e-14 atol 1e-12"}
 
