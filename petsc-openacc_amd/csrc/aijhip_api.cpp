@@ -75,7 +75,7 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_partials);
     hipFree(P.d_segperm);
     hipFree(P.d_wbnd);
-    hipFree(P.d_xrange);
+    hipFree(P.d_xwin);
     hipFree(P.d_saj);
     hipFree(P.d_saa);
     hipFree(P.d_sslot);
@@ -228,34 +228,28 @@ int plan_stream(aijhip_mat *A) {
     // geometry 6, -6 % at the default geometry 1, hence off by default.
     P.n_xtiled = 0;
     if (P.tune.xtile != 0 && !blocks.empty() && !A->compressed) {
-        std::vector<int2> xr(blocks.size());
-        int2 *d_xr = nullptr;
-        if ((e = dmalloc(&d_xr, blocks.size(), &P.bytes)) != hipSuccess) return hipfail(e, "plan: alloc x ranges");
-        if ((e = aijhip::block_column_ranges(*A, P.d_blocks, P.n_blocks, d_xr)) != hipSuccess ||
-            (e = hipMemcpy(xr.data(), d_xr, sizeof(int2) * xr.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
-            hipFree(d_xr);
-            return hipfail(e, "plan: x ranges");
+        std::vector<aijhip::XWin> xw(blocks.size());
+        aijhip::XWin *d_xw = nullptr;
+        if ((e = dmalloc(&d_xw, blocks.size(), &P.bytes)) != hipSuccess) return hipfail(e, "plan: alloc x windows");
+        if ((e = aijhip::block_x_windows(*A, P.d_blocks, P.n_blocks, G.nnz_cap, d_xw)) != hipSuccess ||
+            (e = hipMemcpy(xw.data(), d_xw, sizeof(aijhip::XWin) * xw.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
+            hipFree(d_xw);
+            return hipfail(e, "plan: x windows");
         }
         int32_t fit = 0;
-        for (int2 &r : xr) {
-            if (r.y > 0 && r.y <= G.nnz_cap) ++fit;
-            else r.y = -1;
-        }
-        if (P.tune.xtile == 1 || 2 * (int64_t)fit >= (int64_t)xr.size()) {
-            if ((e = hipMemcpy(d_xr, xr.data(), sizeof(int2) * xr.size(), hipMemcpyHostToDevice)) != hipSuccess) {
-                hipFree(d_xr);
-                return hipfail(e, "plan: x ranges");
-            }
-            P.d_xrange = d_xr;
+        for (const aijhip::XWin &w : xw) fit += w.n[0] >= 0;
+        if (P.tune.xtile == 1 || 2 * (int64_t)fit >= (int64_t)xw.size()) {
+            P.d_xwin = d_xw;
             P.n_xtiled = fit;
         } else {
-            hipFree(d_xr);
+            hipFree(d_xw);
+            P.bytes -= (int64_t)sizeof(aijhip::XWin) * (int64_t)xw.size();
         }
     }
     // gather-ordered copy of the row blocks (Tuning::gsort): for the plain
     // MatMult / MatMultAdd launch (not with the x tiles, which read the
     // original order)
-    if (P.tune.gsort > 0 && !blocks.empty() && P.d_xrange == nullptr) {
+    if (P.tune.gsort > 0 && !blocks.empty() && P.d_xwin == nullptr) {
         const size_t nzp = (size_t)A->nz + 2;
         if ((e = dmalloc(&P.d_saj, nzp, &P.bytes)) != hipSuccess || (e = dmalloc(&P.d_saa, nzp, &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_sslot, nzp, &P.bytes)) != hipSuccess ||
@@ -336,7 +330,7 @@ int plan_stream(aijhip_mat *A) {
     // geometry 6, plain full-row launches, no long rows
     const int32_t nrl = rai.empty() ? 0 : (int32_t)rai.size() - 1;
     if (P.tune.patterns > 0 && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed &&
-        A->nz <= (int64_t)kBatchMinMean * nrl && P.d_xrange == nullptr && P.d_sslot == nullptr) {
+        A->nz <= (int64_t)kBatchMinMean * nrl && P.d_xwin == nullptr && P.d_sslot == nullptr) {
         bool ok = false;
         if ((e = aijhip::build_row_patterns(*A, P, &ok)) != hipSuccess) return hipfail(e, "plan: row patterns");
     }
@@ -345,7 +339,7 @@ int plan_stream(aijhip_mat *A) {
     // full-row launches: not with the x tiles or the gather order); when
     // some do not fit, they are launched from aj
     if (P.tune.codes > 0 && P.tune.geom == 6 && !blocks.empty() && P.d_pid == nullptr && !A->compressed &&
-        P.d_xrange == nullptr && P.d_sslot == nullptr) {
+        P.d_xwin == nullptr && P.d_sslot == nullptr) {
         int32_t *d_cnt = nullptr;
         std::vector<int32_t> cnt(blocks.size());
         if ((e = dmalloc(&d_cnt, blocks.size(), nullptr)) != hipSuccess ||

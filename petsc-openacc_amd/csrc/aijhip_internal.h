@@ -70,6 +70,17 @@ struct BlockDesc {
     int32_t row0, nrows, k0, nk;
 };
 
+// LDS x tile of a row block (Tuning::xtile): up to kXWin column windows
+// [s[w], s[w] + n[w]) of x, ascending, staged one after another in the
+// block's LDS; n[0] < 0: the block gathers from global memory. A 7-point
+// stencil block has three (the planes below and above, its own plane +- N).
+constexpr int kXWin = 4;
+struct XWin {
+    int32_t s[kXWin], n[kXWin];
+};
+// Columns closer than this (in x entries) share a window.
+constexpr int kXWinGap = 64;
+
 // One segment of a long row: entries [k0, k0+nk), partial sum -> partials[seg].
 struct LongSeg {
     int32_t k0, nk;
@@ -101,8 +112,8 @@ struct Tuning {
     int nt = -1;         // matrix loads: -1 by gather locality (non-temporal for scattered long rows),
                          // 0 plain, 1 non-temporal
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
-    int xtile = 0;         // x staged in LDS per block: 0 off (measured default), 1 where it fits,
-                           // -1 when half the blocks fit
+    int xtile = 0;         // x staged in LDS per block (up to kXWin column windows): 0 off, 1 where
+                           // it fits, -1 when half the blocks fit
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
     int long_window = -1;  // long rows by x column window (k_long_window) instead of segments: -1 auto
                            // (sorted rows, >= 2048 long-row entries per window), 0 segments, 1 windows
@@ -175,9 +186,9 @@ struct Plan {
     // n_longs x n_win window sums and d_longs[i] = {orow, i n_win, n_win}
     int32_t *d_wbnd = nullptr;
     int32_t n_win = 0;
-    // x tiles: per block the first column and the span of its columns, or
-    // span -1 when they do not fit the block's LDS (gathers from HBM)
-    int2 *d_xrange = nullptr;
+    // x tiles: per block its column windows (XWin), or n[0] = -1 when they do
+    // not fit the block's LDS (gathers from global memory)
+    XWin *d_xwin = nullptr;
     int32_t n_xtiled = 0;
     // Tuning::gsort: each row block's entries sorted by column (columns,
     // values) and their positions in the block (the products' LDS slots)
@@ -299,6 +310,9 @@ hipError_t build_long_windows(const aijhip_mat &A, Plan &P, const std::vector<Lo
 hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out);
 // Per STREAM block: min column and span (max - min + 1) of its entries.
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out);
+// Per STREAM block: its x column windows (k_block_xwindows), n[0] = -1 when
+// they are more than kXWin or span more than `cap` entries (synchronous).
+hipError_t block_x_windows(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int cap, XWin *d_out);
 // The gather-ordered copy of the plan's row blocks (Plan::d_saj/d_saa/
 // d_sslot, allocated by the caller); values_only: the values again, in the
 // order already built.

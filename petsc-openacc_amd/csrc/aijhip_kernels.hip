@@ -198,7 +198,7 @@ template <int T, int CAP, int RPT, bool CROW, int NTMODE, class Op>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const int2 *__restrict__ xrange,
+    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const XWin *__restrict__ xwin,
     const uint16_t *__restrict__ sslot, const int32_t *__restrict__ sbase) {
     constexpr bool NT = (NTMODE & 1) != 0;
     // bit 3: gather-ordered blocks (Plan::d_saj/d_saa): aj/aa hold each
@@ -322,27 +322,43 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             if (k < k1) sv[it] = *reinterpret_cast<const uint32_t *>(sslot + k);
         }
     }
-    // x tile: the block's columns [xr.x, xr.x + xr.y) staged in LDS (the
-    // products' space, free until the gathers are done) with coalesced
-    // loads; the gathers then read LDS instead of issuing scattered HBM
-    // requests (banded operators; the plan decides per block).
-    int2 xr = make_int2(0, -1);
-    if constexpr (Op::kTile) xr = xrange[b];
-    const bool tiled = Op::kTile && xr.y > 0;
+    // x tile: the block's column windows (Plan::d_xwin) staged in LDS one
+    // after another (the products' space, free until the gathers are done)
+    // with coalesced loads; the gathers then read LDS instead of issuing
+    // scattered requests through L1/L2 (the plan decides per block).
+    XWin xw{};
+    if constexpr (Op::kTile) xw = xwin[b];
+    const bool tiled = Op::kTile && xw.n[0] >= 0;
+    int32_t wo[kXWin] = {};  // each window's first LDS slot
     if constexpr (Op::kTile) {
         if (tiled) {
-            for (int i = t; i < xr.y; i += T) prod[i] = op.gx(xr.x + i);
+            int32_t o = 0;
+#pragma unroll
+            for (int w = 0; w < kXWin; ++w) {
+                wo[w] = o;
+                for (int32_t i = t; i < xw.n[w]; i += T) prod[o + i] = op.gx(xw.s[w] + i);
+                o += max(xw.n[w], 0);
+            }
             __syncthreads();
         }
     }
+    // LDS slot of column c: the last window starting at or below it
+    auto tslot = [&](int32_t c) {
+        int32_t q = c - xw.s[0];
+#pragma unroll
+        for (int w = 1; w < kXWin; ++w)
+            if (xw.n[w] > 0 && c >= xw.s[w]) q = c - xw.s[w] + wo[w];
+        return q;
+    };
     if constexpr (!CODES) {  // (the coded form gathered with the decode above)
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
             if (k < k1) {
                 if (tiled) {
-                    xv[it].x = prod[cv[it].x - xr.x];
-                    xv[it].y = prod[cv[it].y - xr.x];
+                    // a pair's half outside the block (edge) reads slot 0, never stored
+                    xv[it].x = prod[k >= k0 ? tslot(cv[it].x) : 0];
+                    xv[it].y = prod[k + 1 < k1 ? tslot(cv[it].y) : 0];
                 } else {
                     xv[it].x = op.gx(cv[it].x);
                     xv[it].y = op.gx(cv[it].y);
@@ -1045,6 +1061,69 @@ __global__ __launch_bounds__(256) void k_block_xrange(const BlockDesc *__restric
 }
 }  // namespace
 
+// x windows of a row block (Tuning::xtile): its columns sorted in LDS
+// (bitonic over the next power of two), split where two consecutive columns
+// are more than kXWinGap apart; up to kXWin windows whose lengths add up to
+// at most `cap` LDS entries, else n[0] = -1 (the block gathers from memory).
+template <int N>
+__global__ __launch_bounds__(256) void k_block_xwindows(const BlockDesc *__restrict__ blk,
+                                                        const int32_t *__restrict__ aj, int cap, XWin *out) {
+    __shared__ int32_t key[N];
+    __shared__ int32_t st[kXWin + 1];
+    __shared__ int32_t s_nc;
+    const BlockDesc d = blk[blockIdx.x];
+    const int t = threadIdx.x;
+    int n2 = 2;
+    while (n2 < d.nk) n2 <<= 1;
+    for (int i = t; i < n2; i += 256) key[i] = i < d.nk ? aj[(int64_t)d.k0 + i] : INT32_MAX;
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = t; i < n2; i += 256) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const int32_t a = key[i], c = key[ixj];
+                    if ((a > c) == ((i & k) == 0)) {
+                        key[i] = c;
+                        key[ixj] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    if (t < 64) {  // cluster starts, in order (wave 0)
+        int nc = 0;
+        for (int i0 = 0; i0 < d.nk; i0 += 64) {
+            const int i = i0 + t;
+            const bool f = i < d.nk && (i == 0 || (int64_t)key[i] - key[i - 1] > kXWinGap);
+            const unsigned long long msk = __ballot(f);
+            const int pos = nc + __popcll(msk & ((1ull << t) - 1ull));
+            if (f && pos <= kXWin) st[pos] = i;
+            nc += __popcll(msk);
+        }
+        if (t == 0) s_nc = nc;
+    }
+    __syncthreads();
+    if (t == 0) {
+        XWin w;
+        const int nc = s_nc;
+        int64_t tot = 0;
+        for (int q = 0; q < kXWin; ++q) {
+            if (q < nc && nc <= kXWin) {
+                const int a = st[q], e = q + 1 < nc ? st[q + 1] - 1 : d.nk - 1;
+                w.s[q] = key[a];
+                w.n[q] = key[e] - key[a] + 1;
+                tot += w.n[q];
+            } else {
+                w.s[q] = INT32_MAX;
+                w.n[q] = 0;
+            }
+        }
+        if (nc == 0 || nc > kXWin || tot > cap) w.n[0] = -1;
+        out[blockIdx.x] = w;
+    }
+}
+
 // Gather-ordered row blocks (Tuning::gsort): one workgroup sorts its
 // block's entries by column (ties by position; bitonic over the next power
 // of two) and writes the sorted columns, the values in that order and each
@@ -1449,6 +1528,19 @@ hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_
     return launch_block_codes<true>(A, d_blk, nblk, nullptr, d_cmeta, d_code, kStreamGeoms[A.plan.tune.geom].nnz_cap);
 }
 
+hipError_t block_x_windows(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int cap, XWin *d_out) {
+    if (n_blocks <= 0) return hipSuccess;
+#define AIJHIP_XW(NN) \
+    hipLaunchKernelGGL(k_block_xwindows<NN>, dim3(n_blocks), dim3(256), 0, nullptr, d_blocks, A.d_aj, cap, d_out)
+    if (cap <= 1024) AIJHIP_XW(1024);
+    else if (cap <= 2048) AIJHIP_XW(2048);
+    else if (cap <= 4096) AIJHIP_XW(4096);
+    else AIJHIP_XW(8192);
+#undef AIJHIP_XW
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? hipDeviceSynchronize() : e;
+}
+
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out) {
     if (n_blocks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_block_xrange, dim3(n_blocks), dim3(256), 0, nullptr, d_blocks, A.d_aj, d_out);
@@ -1685,10 +1777,10 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
 #undef AIJHIP_SS
     }
     // LDS x tiles: the plain full-row MatMult only
-    if (P.d_xrange && !add && !L.ridx && P.tune.nt != 1) {
+    if (P.d_xwin && !add && !L.ridx && P.tune.nt != 1) {
         hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<false, true>>), dim3(P.n_blocks), dim3(T), 0,
                            s, P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,
-                           OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop, P.d_xrange, nullptr, nullptr);
+                           OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop, P.d_xwin, nullptr, nullptr);
         return;
     }
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd

@@ -118,8 +118,9 @@ def test_stream_multilane_long_rows(pkg, dev, row_len):
 @pytest.mark.parametrize("geometry", [1, 6, 0, 9, 10])
 def test_stream_x_tile_banded(pkg, dev, geometry):
     """x staged in LDS (x_tile=1) for blocks of a banded matrix: bit-exact,
-    and the blocks that do not fit (a wide row every 997) fall back to HBM
-    gathers in the same launch."""
+    and the blocks that do not fit (a row every 997 reaching five more
+    places of x: more windows than a block stages) fall back to gathers
+    from memory in the same launch."""
     rng = np.random.default_rng(11)
     m = 20000
     lens = rng.integers(10, 40, m)
@@ -128,7 +129,7 @@ def test_stream_x_tile_banded(pkg, dev, geometry):
         lo, hi = max(0, i - 300), min(m, i + 300)
         c = np.sort(rng.choice(np.arange(lo, hi), size=min(l, hi - lo), replace=False))
         if i % 997 == 0:
-            c = np.unique(np.concatenate([c, [0, m - 1]]))
+            c = np.unique(np.concatenate([c, [0, m // 4, m // 2, 3 * m // 4, m - 1]]))
         cols.append(c)
     ai = np.concatenate([[0], np.cumsum([len(c) for c in cols])]).astype(np.int32)
     aj = np.concatenate(cols).astype(np.int32)
@@ -137,6 +138,24 @@ def test_stream_x_tile_banded(pkg, dev, geometry):
     y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=1, x_tile=1, geometry=geometry)
     assert 0 < info["x_tiled_blocks"] < info["n_blocks"]
     assert_bits(y, seqaij.matmult(ai, aj, aa, x))
+
+
+@pytest.mark.parametrize("grid", [(16, 16, 16), (40, 40, 40), (300, 7, 5), (3, 200, 60)])
+def test_stream_x_windows_poisson(pkg, dev, coracle, grid):
+    """The 7-point operand's row blocks gather x from LDS windows (x_tile=1,
+    the CSR kernel reading aj): each block stages the planes below and above
+    and its own plane +- N (<= 4 windows); the result is PETSc's loop bit for
+    bit, and so is the plain gather."""
+    ai, aj, aa = pkg.poisson_csr(*grid)
+    m = len(ai) - 1
+    x = pkg.splitmix_uniform(m, 17)
+    ref = coracle.matmult(ai, aj, aa, x, omp=True)
+    y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", x_tile=1, row_patterns=0, column_codes=0)
+    assert info["x_tiled_blocks"] > 0 and info["row_patterns"] == 0 and info["column_codes"] == 0
+    assert_bits(y, ref)
+    y0, info0 = mult(pkg, dev, ai, aj, aa, m, x, "stream", x_tile=0, row_patterns=0, column_codes=0)
+    assert info0["x_tiled_blocks"] == 0
+    assert_bits(y0, ref)
 
 
 @pytest.mark.parametrize("name", GOLDEN_NAMES)

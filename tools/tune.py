@@ -102,6 +102,10 @@ def main():
     if args.variants == "xtile":
         for g, xt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, x_tile=xt)))
+    if args.variants == "xwin":  # the CSR kernel (aj read) gathering x from LDS column windows vs from memory
+        for xt in (0, 1, 0, 1):
+            variants.append(("stream", dict(geometry=6, x_tile=xt, nt_loads=0, row_patterns=0, column_codes=0,
+                                            gather_sort=0)))
     if args.variants == "ntlong":  # non-temporal matrix loads for long-row operands, both automatic geometries
         for g, nt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
