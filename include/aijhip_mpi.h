@@ -130,8 +130,13 @@ int aijhip_mpiaij_destroy(aijhip_mpiaij_t M);
  * Galerkin products formed across ranks (ghost rows of P exchanged, coarse
  * contributions sent to their owners), every level a distributed operator
  * with its own p2p halo, one multiplicative V-cycle per application with
- * the halo exchanges inside (the operator must use AIJHIP_HALO_P2P); at one
- * rank the single-GPU PCGAMG set-up (bit-identical to aijhip_ksp's).
+ * the halo exchanges inside (the operator must use AIJHIP_HALO_P2P:
+ * set_pc_type refuses an all-gather operator at more than one rank); at one
+ * rank the single-GPU PCGAMG set-up (bit-identical to aijhip_ksp's). The
+ * V-cycle's smoothing SpMVs are fused with their vector passes on A_d and add
+ * A_o's share afterwards, r = (b - A_d x) - A_o g, where PETSc's MatResidual
+ * forms A_d x + A_o g first: boundary rows round differently (same
+ * iterations, history within 1e-10; AIJHIP_MG_UNFUSED=1 keeps PETSc's order).
  * BJACOBI_GAMG = -pc_type bjacobi -sub_pc_type gamg: a hierarchy per rank's
  * diagonal block, no communication inside the PC. Options, reasons and norms
  * as aijhip_ksp.h; defaults as PETSc. */

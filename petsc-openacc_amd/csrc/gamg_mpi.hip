@@ -802,14 +802,23 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
             rc = emax_rc;
             aijhip::set_error(emax_err);
         }
-        if (rc) {
-            hipFree(d_agg); hipFree(dinv);
-            break;
-        }
+        // the level's first collective carries this rank's outcome (-1 =
+        // failed): a failure on one rank (allocation, aggregation, emax) ends
+        // the set-up on every rank here, instead of leaving the others in the
+        // level's exchanges until the communicator times out
         std::vector<int64_t> na_all;
-        if ((rc = all_values(C, na, na_all))) {
-            hipFree(d_agg); hipFree(dinv);
-            break;
+        {
+            const int lrc = rc;
+            const int crc = all_values(C, lrc ? -1 : (int64_t)na, na_all);
+            bool peer = false;
+            if (!crc)
+                for (int64_t v : na_all) peer = peer || v < 0;
+            if (lrc || crc || peer) {
+                hipFree(d_agg); hipFree(dinv);
+                rc = lrc ? lrc : crc ? crc : mfail(AIJHIP_ERR_COMM, ("distributed GAMG: another rank failed at level " +
+                                                                   std::to_string(l)).c_str());
+                break;
+            }
         }
         int64_t NA = 0, cstart = 0;
         std::vector<int64_t> cstarts((size_t)P + 1, 0);

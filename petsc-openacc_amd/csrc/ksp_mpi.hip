@@ -984,6 +984,14 @@ int aijhip_kspmpi_set_pc_type(aijhip_kspmpi_t K, int pc) {
     if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
     if (pc != AIJHIP_PC_NONE && pc != AIJHIP_PC_JACOBI && pc != AIJHIP_PC_GAMG && pc != AIJHIP_PC_BJACOBI_GAMG)
         return mfail(AIJHIP_ERR_ARG, "distributed CG: PC none, jacobi, gamg or bjacobi_gamg");
+    // PCGAMG across ranks builds every level's exchange from the operator's
+    // p2p plan: refuse an all-gather-halo operator here, with the way out,
+    // rather than at KSPSetUp
+    if (pc == AIJHIP_PC_GAMG && K->M->comm->nranks > 1 && K->M->halo != AIJHIP_HALO_P2P)
+        return mfail(AIJHIP_ERR_ARG,
+                     "PC gamg across ranks needs the operator's p2p halo: create a p2p twin of this all-gather "
+                     "operator sharing A_d (aijhip_mpiaij_create with AIJHIP_HALO_P2P; mpiaij.MPIAIJ.p2p_native()), "
+                     "or use AIJHIP_PC_BJACOBI_GAMG");
     if (pc != K->pc) K->set_up = false;
     K->pc = pc;
     if (pc == AIJHIP_PC_GAMG || pc == AIJHIP_PC_BJACOBI_GAMG)  // the set-up's streams, made once per process
