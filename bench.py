@@ -86,7 +86,7 @@ def parse():
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
                         "(launch with torch.distributed.run): a one-GPU rehearsal of the N > 1 run")
-    p.add_argument("--comm-timeout", type=float, default=600.0,
+    p.add_argument("--comm-timeout", type=float, default=300.0,
                    help="seconds before a stuck collective aborts the run (process group and RCCL waits)")
     p.add_argument("--rehearse-one-gpu", action="store_true",
                    help="N > 1 control-flow rehearsal on a one-GPU box: every rank on cuda:0 over gloo "
