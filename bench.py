@@ -61,7 +61,7 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--grid", type=int, default=300, help="per-rank grid edge (N^3 rows per rank)")
-    p.add_argument("--kernel", default="auto", choices=["auto", "stream", "scalar", "vector", "merge"])
+    p.add_argument("--kernel", default="auto", choices=["auto", "stream", "scalar", "vector"])
     p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..5 (default: library's)")
     p.add_argument("--nt", type=int, default=None, help="STREAM non-temporal matrix loads 0/1")
     p.add_argument("--layout", default="csr", choices=["csr", "auto"],
@@ -371,15 +371,16 @@ def flan_standins(pkg, dev, reps, cpu_sample):
     the same byte count in the same run:
       skewed — 1,564,794 rows of 45-99 banded entries plus 1e-4 hub rows of
                1e3-2e5 scattered entries (seed 1565): the merge-path
-               load-balance stress; STREAM (default), STREAM exact (PETSc's
-               order in every row that fits a block) and MERGE;
+               load-balance stress; STREAM (default: hub rows by x column
+               window), STREAM exact (PETSc's order in every row that fits a
+               block) and the hub rows as 4096-entry segments;
       fem_hex — Flan_1565's own structure: a hexahedral mesh of 81x80x80
                nodes, 3 dofs per node, 81-entry interior rows.
     Parity is the -m gpu tests' job (tests/test_flan_standins_gpu.py)."""
     import torch
     stream = torch.cuda.current_stream()
     out = {}
-    for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(), ("stream", "stream_exact", "merge")),
+    for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(), ("stream", "stream_exact", "stream_segments")),
                                 ("fem_hex", lambda: pkg.fem_hex_csr(), ("stream",))):
         ai, aj, aa = make()
         m, nnz = len(ai) - 1, len(aj)
@@ -388,10 +389,12 @@ def flan_standins(pkg, dev, reps, cpu_sample):
         y = torch.empty_like(x)
         rec = {"rows": m, "nnz": nnz, "max_row": int(np.diff(ai).max()), "bytes_per_spmv": nbytes}
         for kern in kernels:
-            A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="merge" if kern == "merge" else "stream")
+            A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="stream")
             try:
                 if kern == "stream_exact":
                     A.set_option("exact", 1)
+                if kern == "stream_segments":  # hub rows as 4096-entry segments instead of x windows
+                    A.set_option("long_window", 0)
                 info = A.info()
                 for _ in range(5):
                     A.mult(x, y, stream)
@@ -405,7 +408,7 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                          "csr_effective_GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
                          "geometry": info.get("stream_geometry"), "long_rows": info.get("n_long_rows"),
                          "column_codes": info.get("column_codes"), "gather_sorted": info.get("gather_sorted"),
-                         "row_patterns": info.get("row_patterns")}
+                         "row_patterns": info.get("row_patterns"), "long_windows": info.get("long_windows")}
         del x, y
         flat = read_ceiling(nbytes, dev)
         rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],

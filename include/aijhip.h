@@ -50,10 +50,10 @@
 extern "C" {
 #endif
 
-/* 2: aijhip_info_t gained mult_layout_bytes; the A/B-only options
- * AIJHIP_OPT_XCD_REMAP / _PERSISTENT / _CLAMPED_LOADS / _LONG_OVERLAP /
- * _ROW_GROUP were withdrawn (measured slower) and return
- * AIJHIP_ERR_ARG. */
+/* 2: aijhip_info_t gained long_windows and mult_layout_bytes; the A/B-only
+ * options AIJHIP_OPT_XCD_REMAP / _PERSISTENT / _CLAMPED_LOADS /
+ * _LONG_OVERLAP / _ROW_GROUP and AIJHIP_KERNEL_MERGE were withdrawn
+ * (measured slower) and return AIJHIP_ERR_ARG. */
 #define AIJHIP_ABI_VERSION 2
 
 enum {
@@ -75,7 +75,13 @@ enum {
                                  `gang vector(32)` shape, step1 patch:19-21) */
     AIJHIP_KERNEL_VECTOR = 3, /* 2..64 lanes per row, __shfl tree reduction
                                  (64 = wavefront per row)                    */
-    AIJHIP_KERNEL_MERGE = 4   /* merge-path partition of rows+nnz, carry fix-up */
+    AIJHIP_KERNEL_MERGE = 4   /* withdrawn in ABI 2 (aijhip_mat_set_kernel
+                                 returns AIJHIP_ERR_ARG): STREAM's planner
+                                 cuts the merge list of row ends and entries
+                                 into blocks of <= 512 rows and <= 4094
+                                 entries, rows longer than a block into x
+                                 windows or segments; an explicit merge-path
+                                 kernel measured 1.6x slower */
 };
 
 typedef struct aijhip_mat *aijhip_mat_t;

@@ -87,9 +87,6 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_cmeta);
     hipFree(P.d_pid);
     hipFree(P.d_ptab);
-    hipFree(P.d_tile_coord);
-    hipFree(P.d_carry_row);
-    hipFree(P.d_carry_val);
     aijhip::host_pipe_free(P.hpipe);
     P = aijhip::Plan();
 }
@@ -443,27 +440,6 @@ int plan_stream(aijhip_mat *A) {
     return AIJHIP_OK;
 }
 
-int plan_merge(aijhip_mat *A) {
-    using namespace aijhip;
-    Plan &P = A->plan;
-    const int32_t nr = A->h_rai.empty() ? 0 : (int32_t)A->h_rai.size() - 1;
-    const int64_t items = (int64_t)nr + A->nz;
-    const int64_t nt = (items + kMergeTile - 1) / kMergeTile;
-    if (nt > INT32_MAX - 2) return fail(AIJHIP_ERR_ARG, "merge plan: too many tiles");
-    P.n_tiles = (int32_t)nt;
-    hipError_t e;
-    if ((e = dmalloc(&P.d_tile_coord, (size_t)nt + 1, &P.bytes)) != hipSuccess ||
-        (e = dmalloc(&P.d_carry_row, (size_t)nt, &P.bytes)) != hipSuccess ||
-        (e = dmalloc(&P.d_carry_val, (size_t)nt, &P.bytes)) != hipSuccess)
-        return hipfail(e, "plan: alloc merge tiles");
-    if (nt > 0) {
-        if ((e = merge_plan_coords(*A, P.d_tile_coord, P.n_tiles, nullptr)) != hipSuccess ||
-            (e = hipDeviceSynchronize()) != hipSuccess)
-            return hipfail(e, "plan: merge coordinates");
-    }
-    return AIJHIP_OK;
-}
-
 int plan_build(aijhip_mat *A) {
     free_plan(A->plan);
     aijhip::Plan &P = A->plan;
@@ -566,8 +542,6 @@ int plan_build(aijhip_mat *A) {
             P.lanes = lanes;
             return AIJHIP_OK;
         }
-        case AIJHIP_KERNEL_MERGE:
-            return plan_merge(A);
         default:
             return fail(AIJHIP_ERR_ARG, "unknown kernel " + std::to_string(kernel));
     }
@@ -882,7 +856,10 @@ int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
 int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes) {
     int rc = check_handle(A);
     if (rc) return rc;
-    if (kernel < AIJHIP_KERNEL_AUTO || kernel > AIJHIP_KERNEL_MERGE)
+    if (kernel == AIJHIP_KERNEL_MERGE)
+        return fail(AIJHIP_ERR_ARG, "the MERGE kernel was withdrawn in ABI 2: STREAM's row blocks are the "
+                                    "merge-path decomposition (DESIGN.md §5)");
+    if (kernel < AIJHIP_KERNEL_AUTO || kernel > AIJHIP_KERNEL_VECTOR)
         return fail(AIJHIP_ERR_ARG, "unknown kernel " + std::to_string(kernel));
     DeviceGuard g(A->device);
     if (g.err != hipSuccess) return hipfail(g.err, "set device");

@@ -59,10 +59,6 @@ constexpr int kLongThreads = 256;
 // rows, their columns sorted.
 constexpr int kWinCols = 2048;
 constexpr int kWinMaxRows = 512;
-// MERGE kernel: 256 lanes x kMergeItems merge-path items per workgroup.
-constexpr int kMergeThreads = 256;
-constexpr int kMergeItems = 8;
-constexpr int kMergeTile = kMergeThreads * kMergeItems;
 
 // One STREAM row block: rows [row0, row0+nrows) of the row list, entries
 // [k0, k0+nk) of aj/aa.
@@ -220,11 +216,6 @@ struct Plan {
     int32_t *d_ptab = nullptr;
     int32_t n_ptab = 0, n_pat = 0;
     int32_t pat_dmax = 0;    // largest |column - row| offset in the table (the stencil's plane distance)
-    // MERGE: merge-path start coordinate of every tile (+1 sentinel)
-    int2 *d_tile_coord = nullptr;
-    int32_t n_tiles = 0;
-    int2 *d_carry_row = nullptr;   // per tile: row of its carry-out (or -1)
-    double *d_carry_val = nullptr;
     int64_t bytes = 0;  // device bytes held by the plan
     HostPipe *hpipe = nullptr;  // built on the first host-vector MatMult
 };
@@ -291,11 +282,6 @@ hipError_t launch_scalar(const aijhip_mat &A, const double *x, const double *z,
                          double *y, bool add, hipStream_t s);
 hipError_t launch_vector(const aijhip_mat &A, const double *x, const double *z,
                          double *y, bool add, hipStream_t s);
-hipError_t launch_merge(const aijhip_mat &A, const double *x, const double *z,
-                        double *y, bool add, hipStream_t s);
-// MERGE planning: merge-path coordinates of every tile start (device search).
-hipError_t merge_plan_coords(const aijhip_mat &A, int2 *d_coord, int32_t n_tiles,
-                             hipStream_t s);
 // Transpose (stable by row): builds At's device CSR (n x m). Returns arrays
 // allocated with hipMalloc; caller owns them.
 hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj,

@@ -19,10 +19,9 @@
 //          its loads are strided by the row length (kept as a baseline).
 //  VECTOR  — L = 2..64 lanes per row (64 = one wavefront per row), strided
 //          loads, __shfl_xor tree reduction. For long uniform rows.
-//  MERGE   — merge-path (Merrill & Garland) equal split of the rows+entries
-//          merge list over lanes; rows cut by a lane or tile boundary are
-//          completed by an in-tile chain and a per-tile carry fix-up. For
-//          skewed row lengths (the Flan_1565 stress config).
+//  (MERGE, an explicit merge-path kernel, was withdrawn in ABI 2: the STREAM
+//  planner already cuts the merge list of rows and entries into balanced
+//  blocks, and the kernel measured 1.6x slower on its own stress operand.)
 //
 // Rows longer than a block's entry cap leave the STREAM blocks and are split
 // into kLongSegNnz-entry segments, each reduced by one workgroup (placed on
@@ -790,178 +789,6 @@ __global__ __launch_bounds__(256) void k_spmv_vector(
         const int orow = CROW ? ridx[row] : (int)row;
         y[orow] = ADD ? z[orow] + acc : acc;
     }
-}
-
-// ------------------------------------------------------------ merge path
-// Global merge-path search: coordinate (row-ends consumed, entries consumed)
-// of diagonal `diag` of the merge of rai[1..nr] with 0..K-1.
-__device__ __forceinline__ int2 merge_search_global(int64_t diag, const int32_t *rai,
-                                                    int nr, int64_t K) {
-    int64_t lo = diag - K > 0 ? diag - K : 0;
-    int64_t hi = diag < nr ? diag : nr;
-    while (lo < hi) {
-        const int64_t p = (lo + hi) >> 1;
-        if ((int64_t)rai[p + 1] <= diag - p - 1) lo = p + 1;
-        else hi = p;
-    }
-    return make_int2((int)lo, (int)(diag - lo));
-}
-
-__global__ void k_merge_coords(int ntiles, const int32_t *__restrict__ rai, int nr,
-                               int64_t K, int2 *coord) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t > ntiles) return;
-    int64_t diag = (int64_t)t * kMergeTile;
-    if (diag > nr + K) diag = nr + K;
-    coord[t] = merge_search_global(diag, rai, nr, K);
-}
-
-template <bool ADD, bool CROW>
-__global__ __launch_bounds__(kMergeThreads) void k_spmv_merge(
-    const int2 *__restrict__ coord, int nr, const int32_t *__restrict__ rai,
-    const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, const double *__restrict__ x, const double *z,
-    double *y, int2 *carry_row, double *carry_val) {
-    __shared__ double s_prod[kMergeTile];
-    __shared__ int32_t s_rb[kMergeTile + 2];
-    __shared__ int32_t s_tail_row[kMergeThreads];
-    __shared__ double s_tail_val[kMergeThreads];
-    const int t = threadIdx.x;
-    const int2 c0 = coord[blockIdx.x], c1 = coord[blockIdx.x + 1];
-    const int i0 = c0.x, i1 = c1.x;
-    const int64_t j0 = c0.y, j1 = c1.y;
-    const int nitems = (i1 - i0) + (int)(j1 - j0);
-    const int nrb = i1 - i0 + 2;  // s_rb[ii] = rai[i0+ii], ii in [0, i1-i0+1]
-    const int64_t K = rai[nr];
-    for (int q = t; q < nrb; q += kMergeThreads) {
-        const int r = i0 + q;
-        s_rb[q] = r <= nr ? rai[r] : (int32_t)K;
-    }
-    // The tile's entries as in STREAM: 16-B aa / 8-B aj pairs from an even
-    // start (the arrays carry a 2-entry tail pad), every load of a lane in
-    // flight before its gathers (one entry per lane and loop trip, as this
-    // loop was first written, left each lane waiting on one load at a time)
-    {
-        constexpr int MI = (kMergeTile + 1 + 2 * kMergeThreads - 1) / (2 * kMergeThreads);
-        const int64_t kb = j0 & ~int64_t(1);
-        f64x2 av[MI];
-        i32x2 cv[MI];
-        f64x2 xv[MI];
-#pragma unroll
-        for (int it = 0; it < MI; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * kMergeThreads);
-            if (k < j1) {
-                av[it] = *reinterpret_cast<const f64x2 *>(aa + k);
-                cv[it] = *reinterpret_cast<const i32x2 *>(aj + k);
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < MI; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * kMergeThreads);
-            if (k < j1) {
-                xv[it].x = x[k >= j0 ? cv[it].x : cv[it].y];  // a pair's half before the tile: never stored
-                xv[it].y = x[k + 1 < j1 ? cv[it].y : cv[it].x];  // ... or after it
-            }
-        }
-#pragma unroll
-        for (int it = 0; it < MI; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * kMergeThreads);
-            if (k < j1) {
-                if (k >= j0) s_prod[k - j0] = av[it].x * xv[it].x;
-                if (k + 1 < j1) s_prod[k + 1 - j0] = av[it].y * xv[it].y;
-            }
-        }
-    }
-    __syncthreads();
-
-    // Thread-local merge-path search inside the tile.
-    const int td = min(t * kMergeItems, nitems);
-    int lo = max(0, td - (int)(j1 - j0)), hi = min(td, i1 - i0);
-    while (lo < hi) {
-        const int p = (lo + hi) >> 1;
-        if ((int64_t)s_rb[p + 1] <= j0 + td - p - 1) lo = p + 1;
-        else hi = p;
-    }
-    int ii = lo;
-    int64_t jj = j0 + td - lo;
-    double running = 0.0;
-    bool have = false, started = false;
-    int head_ii = -1;
-    double head_val = 0.0;
-    const int nmine = min(kMergeItems, nitems - td);
-    for (int it = 0; it < nmine; ++it) {
-        const int64_t rend = s_rb[ii + 1];
-        if (jj < rend) {
-            if (!have) {
-                started = (jj == s_rb[ii]);
-                running = 0.0;
-                if (ADD && started) running = z[CROW ? ridx[i0 + ii] : i0 + ii];
-                have = true;
-            }
-            running += s_prod[jj - j0];
-            ++jj;
-        } else {
-            if (!have) {
-                started = (jj == s_rb[ii]);  // empty row: its end is its first item
-                running = 0.0;
-                if (ADD && started) running = z[CROW ? ridx[i0 + ii] : i0 + ii];
-            }
-            if (started) {
-                y[CROW ? ridx[i0 + ii] : i0 + ii] = running;
-            } else {  // only the first row end of a lane can be a head
-                head_ii = ii;
-                head_val = running;
-            }
-            have = false;
-            ++ii;
-        }
-    }
-    s_tail_row[t] = have ? ii : -1;
-    s_tail_val[t] = running;
-    __syncthreads();
-
-    if (head_ii >= 0) {
-        int tf = t;
-        while (tf > 0 && s_tail_row[tf - 1] == head_ii) --tf;
-        double v;
-        if (tf < t) {
-            v = s_tail_val[tf];
-            for (int q = tf + 1; q < t; ++q) v += s_tail_val[q];
-            v += head_val;
-        } else {
-            v = head_val;
-        }
-        y[CROW ? ridx[i0 + head_ii] : i0 + head_ii] = v;
-    }
-    // Tile carry-out: the partial of the row left open at the tile's end.
-    const int tl = nitems > 0 ? (nitems - 1) / kMergeItems : 0;
-    if (t == tl) {
-        if (nitems > 0 && s_tail_row[tl] >= 0) {
-            const int row = s_tail_row[tl];
-            int tf = tl;
-            while (tf > 0 && s_tail_row[tf - 1] == row) --tf;
-            double v = s_tail_val[tf];
-            for (int q = tf + 1; q <= tl; ++q) v += s_tail_val[q];
-            carry_row[blockIdx.x] = make_int2(CROW ? ridx[i0 + row] : i0 + row, 0);
-            carry_val[blockIdx.x] = v;
-        } else {
-            carry_row[blockIdx.x] = make_int2(-1, 0);
-        }
-    }
-}
-
-// Adds tile carries into their rows. The first tile of each run of tiles
-// carrying into one row sums the run in tile order, then adds once.
-__global__ void k_merge_fixup(int ntiles, const int2 *__restrict__ carry_row,
-                              const double *__restrict__ carry_val, double *y) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= ntiles) return;
-    const int r = carry_row[b].x;
-    if (r < 0) return;
-    if (b > 0 && carry_row[b - 1].x == r) return;
-    double v = carry_val[b];
-    for (int q = b + 1; q < ntiles && carry_row[q].x == r; ++q) v += carry_val[q];
-    y[r] = y[r] + v;
 }
 
 // ------------------------------------------------------------ transpose
@@ -1971,44 +1798,14 @@ hipError_t launch_vector(const aijhip_mat &A, const double *x, const double *z, 
     return hipGetLastError();
 }
 
-hipError_t merge_plan_coords(const aijhip_mat &A, int2 *d_coord, int32_t n_tiles,
-                             hipStream_t s) {
-    const RowList L = row_list(A);
-    const int64_t K = A.nz;
-    hipLaunchKernelGGL(k_merge_coords, dim3(grid_for((int64_t)n_tiles + 1, 256)), dim3(256), 0, s,
-                       n_tiles, L.rai, L.nr, K, d_coord);
-    return hipGetLastError();
-}
-
-hipError_t launch_merge(const aijhip_mat &A, const double *x, const double *z, double *y,
-                        bool add, hipStream_t s) {
-    hipError_t e = compressed_prologue(A, z, y, add, s);
-    if (e != hipSuccess) return e;
-    const RowList L = row_list(A);
-    const Plan &P = A.plan;
-    if (L.nr == 0 || P.n_tiles == 0) return hipSuccess;
-    const dim3 g(P.n_tiles), b(kMergeThreads);
-#define AIJHIP_MERGE(ADD, CROW)                                                                 \
-    hipLaunchKernelGGL((k_spmv_merge<ADD, CROW>), g, b, 0, s, P.d_tile_coord, L.nr, L.rai,     \
-                       L.ridx, A.d_aj, A.d_aa, x, z, y, P.d_carry_row, P.d_carry_val)
-    if (add) { if (L.ridx) AIJHIP_MERGE(true, true); else AIJHIP_MERGE(true, false); }
-    else { if (L.ridx) AIJHIP_MERGE(false, true); else AIJHIP_MERGE(false, false); }
-#undef AIJHIP_MERGE
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_merge_fixup, dim3(grid_for(P.n_tiles, 256)), dim3(256), 0, s,
-                       P.n_tiles, P.d_carry_row, P.d_carry_val, y);
-    return hipGetLastError();
-}
-
 hipError_t launch_mult(const aijhip_mat &A, const double *x, const double *z, double *y,
                        bool add, hipStream_t s, const int *stop) {
     switch (A.plan.kernel) {
-        // the stop flag reaches the STREAM row blocks (the long-row, SCALAR,
-        // VECTOR and MERGE kernels ignore it: they recompute the same values)
+        // the stop flag reaches the STREAM row blocks (the long-row, SCALAR
+        // and VECTOR kernels ignore it: they recompute the same values)
         case AIJHIP_KERNEL_STREAM: return launch_stream(A, x, z, y, add, s, nullptr, stop);
         case AIJHIP_KERNEL_SCALAR: return launch_scalar(A, x, z, y, add, s);
         case AIJHIP_KERNEL_VECTOR: return launch_vector(A, x, z, y, add, s);
-        case AIJHIP_KERNEL_MERGE: return launch_merge(A, x, z, y, add, s);
         default: return hipErrorInvalidValue;
     }
 }

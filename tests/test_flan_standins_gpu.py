@@ -6,8 +6,8 @@ run at Flan_1565's scale against the C restatement of MatMult_SeqAIJ
 
   skewed  — `skewed_csr()` default size: 1,564,794 rows of 45-99 banded
             entries plus 1e-4 hub rows of 1e3-2e5 scattered entries (seed
-            1565); hub rows are longer than any STREAM block and are split
-            into segments.
+            1565); hub rows are longer than any STREAM block and are summed
+            by x column window (or 4096-entry segments).
   fem_hex — `fem_hex_csr()` default size: 81 x 80 x 80 hexahedral nodes, 3
             dofs per node (Flan_1565's structure), 81-entry interior rows.
 
@@ -75,16 +75,19 @@ def test_full_size_shape(standin):
         assert len(ai) - 1 == 81 * 80 * 80 * 3 and lens.max() == 81
 
 
-@pytest.mark.parametrize("mode", ["stream_exact", "stream_default", "merge"])
+@pytest.mark.parametrize("mode", ["stream_exact", "stream_default", "stream_segments"])
 def test_full_size_parity(pkg, standin, mode):
     name, ai, aj, aa, x, ref, absax = standin
     lens = np.diff(ai)
-    if mode == "merge":
-        y, info = _run(pkg, ai, aj, aa, x, "merge")
+    if mode == "stream_segments":  # long rows as 4096-entry segments instead of x windows
+        y, info = _run(pkg, ai, aj, aa, x, "stream", long_window=0)
+        assert info["long_windows"] == 0
     else:
         y, info = _run(pkg, ai, aj, aa, x, "stream", exact=1 if mode == "stream_exact" else 0)
+        if info["n_long_rows"]:  # the skewed stand-in's hub rows: by x window (automatic)
+            assert info["long_windows"] > 0
     print(f"\n{name} {mode}: rows {len(lens)} nnz {len(aj)} geometry {info['stream_geometry']} "
-          f"long rows {info['n_long_rows']}")
+          f"long rows {info['n_long_rows']} windows {info['long_windows']}")
     _bound_check(y, ref, lens, absax)
     cap = info["stream_nnz_cap"]
     if mode == "stream_exact":

@@ -2,7 +2,7 @@
 
 Bar: the STREAM and SCALAR kernels sum each row in PETSc's
 order without FMA, so they must be BIT-IDENTICAL to the CPU restatement.
-VECTOR / MERGE / long-row segments reorder the row sum and must meet the
+VECTOR and the long-row windows / segments reorder the row sum and must meet the
 componentwise fp64 bound |dy_i| <= 2 gamma(n_i) (|A||x|)_i (+ the |z| term),
 gamma(n) = n u / (1 - n u), u = 2^-53, plus ||dy||_inf / |||A||x|||_inf <= 1e-14.
 """
@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 BITEXACT = ("stream", "scalar")
-ALL_KERNELS = ("stream", "scalar", "vector", "merge")
+ALL_KERNELS = ("stream", "scalar", "vector")
 
 
 @pytest.fixture(scope="module")
@@ -513,6 +513,17 @@ def test_long_window_needs_sorted_rows(pkg, dev, coracle):
         A.mult(to_dev(x, dev), yd)
         torch.cuda.synchronize()
         check(yd.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True), ai, aj, aa, x, exact=False)
+
+
+def test_merge_kernel_withdrawn(pkg, dev):
+    """ABI 2 withdrew the explicit merge-path kernel (STREAM's planner is the
+    merge-path decomposition): set_kernel("merge") is refused and the handle
+    keeps its plan."""
+    g = golden("skewed_small")
+    with pkg.SeqAIJHIP(g["ai"], g["aj"], g["aa"], ncols=int(g["ncols"])) as A:
+        with pytest.raises(pkg.AIJHIPError, match="withdrawn"):
+            A.set_kernel("merge")
+        assert A.info()["kernel"] == "stream"
 
 
 @pytest.mark.parametrize("name", ["poisson16", "skewed_small", "compressed_small"])

@@ -94,7 +94,7 @@ def main():
         for g, nt in itertools.product(range(12), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
     if args.variants in ("kernels", "all"):
-        variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4}), ("merge", {})]
+        variants += [("scalar", {}), ("vector", {"lanes": 8}), ("vector", {"lanes": 4})]
     if args.variants == "default":  # the product's defaults only
         variants.append(("stream", {}))
     if args.variants == "rowsum":  # default plus the small geometries (medium-length rows)
@@ -139,8 +139,9 @@ def main():
     if args.variants == "patnt":  # row patterns: plain vs non-temporal aa loads
         for nt in (0, 1, 0, 1):
             variants.append(("stream", dict(row_patterns=1, nt_loads=nt)))
-    if args.variants == "merge":  # the merge-path kernel beside the automatic STREAM layout
-        variants += [("stream", {}), ("merge", {}), ("stream", dict(gather_sort=0, column_codes=0))]
+    if args.variants == "longwin":  # hub rows by x column window vs 4096-entry segments
+        for lw in (1, 0, 1, 0):
+            variants.append(("stream", dict(long_window=lw)))
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: XCD placement on / off
         for lx in (1, 0):
             variants.append(("stream", dict(long_xcd=lx)))
@@ -156,7 +157,7 @@ def main():
         for g in (1, 6):
             variants.append(("stream", dict(geometry=g, exact=1)))
         variants += [("vector", {"lanes": 16}), ("vector", {"lanes": 32}), ("vector", {"lanes": 64}),
-                     ("merge", {}), ("scalar", {})]
+                     ("scalar", {})]
 
     def configure(kind, opts):
         for k, v in opts.get("env", {}).items():  # read by the planner (the set_option calls below re-plan)
@@ -166,6 +167,7 @@ def main():
         A.set_option("exact", opts.get("exact", 0))
         A.set_option("x_tile", opts.get("x_tile", -1 if opts else 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
+        A.set_option("long_window", opts.get("long_window", -1))
         A.set_option("gather_sort", opts.get("gather_sort", -1))
         A.set_option("column_codes", opts.get("column_codes", -1))
         A.set_option("row_patterns", opts.get("row_patterns", -1))
