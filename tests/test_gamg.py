@@ -113,8 +113,11 @@ def test_gpu_cg_gamg_matches_oracle(pkg, N, norm):
 def test_gpu_vcycle_fused_smoothers_bitwise(pkg, monkeypatch):
     """The fused V-cycle smoothers (residual and Richardson+Jacobi step in the
     SpMV epilogue, default) and the unfused kernels (PCMG's separate
-    smoother, MatResidual and vector passes; AIJHIP_MG_UNFUSED=1) round
-    identically on one GPU: the whole CG+GAMG solve is bit-for-bit the same."""
+    smoother, MatResidual and vector passes; AIJHIP_MG_UNFUSED=1) round every
+    entry the same way on one GPU; only CG's z.z / z.r are summed in another
+    block order (the fused finest post-smoothing's STREAM blocks against the
+    vector grid), so the iterations are the same and the histories and
+    solutions agree to 1e-12 relative."""
     torch = pytest.importorskip("torch")
     assert torch.cuda.is_available()
     K = importlib.import_module("petsc-openacc_amd.ksp")
@@ -135,8 +138,8 @@ def test_gpu_vcycle_fused_smoothers_bitwise(pkg, monkeypatch):
                 out.append((ksp.its, np.array(ksp.history()), x.cpu().numpy()))
     for its, h, xv in out[1:]:
         assert its == out[0][0]
-        assert np.array_equal(h.view(np.uint64), out[0][1].view(np.uint64))
-        assert np.array_equal(xv.view(np.uint64), out[0][2].view(np.uint64))
+        np.testing.assert_allclose(h, out[0][1], rtol=1e-12, atol=1e-15 * out[0][1][0])
+        np.testing.assert_allclose(xv, out[0][2], rtol=1e-12, atol=1e-15)
 
 
 def test_oracle_vcycle_preconditions_cg():

@@ -26,16 +26,20 @@ __device__ __forceinline__ T ld(const T *p) {
     else return *p;
 }
 
-constexpr int kT = 512, kIters = 4, kCap = 4094;
+constexpr int kT = 512;
 
-template <int RUNG, bool NT>
+// ROWS rows per block (512: the product's geometry 6, four pair-iterations
+// per lane; 256: two pair-iterations, the flat read's best depth)
+template <int RUNG, bool NT, int ROWS = 512>
 __global__ __launch_bounds__(kT) void k_ladder(int32_t m, const int32_t *__restrict__ ai,
                                                const int32_t *__restrict__ aj, const double *__restrict__ aa,
                                                const double *__restrict__ x, double *__restrict__ y) {
+    constexpr int kIters = ROWS == 512 ? 4 : 2;
+    constexpr int kCap = 2 * kT * kIters - 2;
     __shared__ double prod[RUNG == 3 ? kCap : 1];
     const int t = threadIdx.x;
-    const int32_t row0 = (int32_t)blockIdx.x * kT;
-    const int32_t nrows = min(kT, m - row0);
+    const int32_t row0 = (int32_t)blockIdx.x * ROWS;
+    const int32_t nrows = min(ROWS, m - row0);
     const int64_t k0 = ai[row0], k1 = ai[row0 + nrows];
     const int r = row0 + min(t, nrows - 1);
     const int32_t rs = ai[r], re = ai[r + 1];
@@ -91,6 +95,58 @@ __global__ __launch_bounds__(kT) void k_ladder(int32_t m, const int32_t *__restr
     if (t < nrows) __builtin_nontemporal_store(s, y + r);
 }
 
+// rung 0b: the SpMV's five arrays streamed in the flat read's best shape —
+// per 512-lane block 2048 entries of aa (two 16-B loads per lane) and aj (one
+// 16-B load per lane), its share of the rows' ai and x (16-B loads) and of y
+// (16-B stores) — no CSR structure at all
+template <bool NT>
+__global__ __launch_bounds__(kT) void k_multi(int32_t m, int64_t nz, const int32_t *__restrict__ ai,
+                                              const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                                              const double *__restrict__ x, double *__restrict__ y) {
+    const int t = threadIdx.x;
+    const int64_t nb = (nz + 2047) / 2048, b = blockIdx.x;
+    const int64_t e0 = b * 2048;
+    const int64_t r0 = (b * m / nb) & ~int64_t(3), r1 = b + 1 == nb ? m : (((b + 1) * m / nb) & ~int64_t(3));
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const int64_t k = e0 + 2 * (t + u * kT);
+        if (k + 1 < nz) {
+            const f64x2 a = ld<NT>(reinterpret_cast<const f64x2 *>(aa + k));
+            s += a.x + a.y;
+        }
+    }
+    {
+        const int64_t k = e0 + 4 * t;
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        if (k + 3 < nz) {
+            const i32x4 c = ld<NT>(reinterpret_cast<const i32x4 *>(aj + k));
+            s += (double)(c.x ^ c.y ^ c.z ^ c.w);
+        }
+    }
+    const int64_t r = r0 + 4 * t;
+    typedef int i32x4 __attribute__((ext_vector_type(4)));
+    if (r + 3 < r1) {
+        const i32x4 q = ld<NT>(reinterpret_cast<const i32x4 *>(ai + r));
+        s += (double)(q.x + q.w);
+    }
+    const int64_t rx = r0 + 2 * t;
+    if (rx + 1 < r1) {
+        const f64x2 xv = *reinterpret_cast<const f64x2 *>(x + rx);
+        f64x2 o;
+        o.x = s + xv.x;
+        o.y = s + xv.y;
+        __builtin_nontemporal_store(o, reinterpret_cast<f64x2 *>(y + rx));
+    }
+    if (rx + 1 + 2 * kT < r1) {  // blocks of more than 1024 rows (never at 7 entries per row)
+        const f64x2 xv = *reinterpret_cast<const f64x2 *>(x + rx + 2 * kT);
+        f64x2 o;
+        o.x = s + xv.x;
+        o.y = s + xv.y;
+        __builtin_nontemporal_store(o, reinterpret_cast<f64x2 *>(y + rx + 2 * kT));
+    }
+}
+
 // rung 0: each array read once as flat 16-B tiles (two per lane), y written
 template <bool NT>
 __global__ __launch_bounds__(kT) void k_flat(int64_t n2, const f64x2 *__restrict__ v, double *out, int64_t nout) {
@@ -112,18 +168,31 @@ __global__ __launch_bounds__(kT) void k_flat(int64_t n2, const f64x2 *__restrict
 extern "C" {
 
 // y = a ladder rung over the Poisson CSR (device pointers); returns hipError_t
-int ladder_launch(int rung, int nt, int32_t m, const int32_t *ai, const int32_t *aj, const double *aa,
-                  const double *x, double *y, void *stream) {
+// rows 512 (four pair-iterations per lane) or 256 (two); rung 9 = k_multi
+int ladder_launch(int rung, int nt, int rows, int32_t m, int64_t nz, const int32_t *ai, const int32_t *aj,
+                  const double *aa, const double *x, double *y, void *stream) {
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const unsigned g = (unsigned)((m + kT - 1) / kT);
-#define L(R, N) hipLaunchKernelGGL((k_ladder<R, N>), dim3(g), dim3(kT), 0, s, m, ai, aj, aa, x, y)
-    switch (rung * 2 + (nt ? 1 : 0)) {
-        case 2: L(1, false); break;
-        case 3: L(1, true); break;
-        case 4: L(2, false); break;
-        case 5: L(2, true); break;
-        case 6: L(3, false); break;
-        case 7: L(3, true); break;
+    if (rung == 9) {
+        const unsigned g = (unsigned)((nz + 2047) / 2048);
+        if (nt) hipLaunchKernelGGL((k_multi<true>), dim3(g), dim3(kT), 0, s, m, nz, ai, aj, aa, x, y);
+        else hipLaunchKernelGGL((k_multi<false>), dim3(g), dim3(kT), 0, s, m, nz, ai, aj, aa, x, y);
+        return (int)hipGetLastError();
+    }
+    const unsigned g = (unsigned)((m + rows - 1) / rows);
+#define L(R, N, W) hipLaunchKernelGGL((k_ladder<R, N, W>), dim3(g), dim3(kT), 0, s, m, ai, aj, aa, x, y)
+    switch ((rows == 256 ? 8 : 0) + rung * 2 + (nt ? 1 : 0) - 2) {
+        case 0: L(1, false, 512); break;
+        case 1: L(1, true, 512); break;
+        case 2: L(2, false, 512); break;
+        case 3: L(2, true, 512); break;
+        case 4: L(3, false, 512); break;
+        case 5: L(3, true, 512); break;
+        case 8: L(1, false, 256); break;
+        case 9: L(1, true, 256); break;
+        case 10: L(2, false, 256); break;
+        case 11: L(2, true, 256); break;
+        case 12: L(3, false, 256); break;
+        case 13: L(3, true, 256); break;
         default: return (int)hipErrorInvalidValue;
     }
 #undef L

@@ -40,7 +40,8 @@ def main():
     args = ap.parse_args()
     L = build()
     P = ctypes.c_void_p
-    L.ladder_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int32, P, P, P, P, P, P]
+    L.ladder_launch.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int32, ctypes.c_int64, P, P, P, P,
+                                P, P]
     L.ladder_flat.argtypes = [ctypes.c_int, ctypes.c_int64, P, P, ctypes.c_int64, P]
     pkg = importlib.import_module("petsc-openacc_amd")
     dev = torch.device("cuda:0")
@@ -61,18 +62,21 @@ def main():
         elif name.startswith("flat"):
             rc = L.ladder_flat(int(name.endswith("nt")), flat.numel(), flat.data_ptr(), y.data_ptr(), m, sh)
             assert rc == 0
-        else:
-            rung, nt = int(name[4]), int(name.endswith("nt"))
-            rc = L.ladder_launch(rung, nt, m, d_ai, d_aj, d_aa, x.data_ptr(), y.data_ptr(), sh)
+        else:  # rungR[_256][_nt], multi[_nt]
+            rung = 9 if name.startswith("multi") else int(name[4])
+            nt, rows = int(name.endswith("nt")), 256 if "_256" in name else 512
+            rc = L.ladder_launch(rung, nt, rows, m, nnz, d_ai, d_aj, d_aa, x.data_ptr(), y.data_ptr(), sh)
             assert rc == 0, rc
 
-    variants = ["product", "flat", "flat_nt", "rung1", "rung1_nt", "rung2", "rung2_nt", "rung3", "rung3_nt"]
+    variants = ["product", "flat", "flat_nt", "multi", "multi_nt", "rung1", "rung1_nt", "rung1_256", "rung1_256_nt",
+                "rung2", "rung2_nt", "rung2_256_nt", "rung3", "rung3_nt", "rung3_256", "rung3_256_nt"]
     ref = torch.empty_like(y)
     A.mult(x, ref, s)
-    run("rung3")
-    torch.cuda.synchronize()
-    print(json.dumps({"check": "rung3 equals the product bit for bit", "equal": bool(torch.equal(ref, y))}),
-          flush=True)
+    for chk in ("rung3", "rung3_256_nt"):
+        run(chk)
+        torch.cuda.synchronize()
+        print(json.dumps({"check": f"{chk} equals the product bit for bit", "equal": bool(torch.equal(ref, y))}),
+              flush=True)
     print(json.dumps({"m": m, "nnz": nnz, "bytes": nbytes, "flat_bytes": flat.numel() * 8 + 8 * m}), flush=True)
     for rnd in range(args.rounds):
         for v in variants:
