@@ -80,6 +80,13 @@ int aijhip_ksp_set_up(aijhip_ksp_t ksp);
 /* KSPSolve: b, x device fp64[m]; x is overwritten (zeroed first unless the
  * initial guess is nonzero). Returns once the solve has finished. */
 int aijhip_ksp_solve(aijhip_ksp_t ksp, const double *b, double *x, void *stream);
+/* KSPSolve with HOST vectors b, x (fp64[m]; x is also read when the initial
+ * guess is nonzero): b goes up and x comes down once per solve, the whole
+ * solve runs on the device — the solve-level offload an unchanged PETSc
+ * caller with host Vecs reaches through a registered KSP type
+ * (petsc-openacc_amd/petsc/aijhip_ksp_petsc.c), instead of two PCIe copies per
+ * MatMult. Synchronous. */
+int aijhip_ksp_solve_host(aijhip_ksp_t ksp, const double *b, double *x);
 int aijhip_ksp_get_iteration_number(aijhip_ksp_t ksp, int32_t *its);
 int aijhip_ksp_get_residual_norm(aijhip_ksp_t ksp, double *rnorm);
 int aijhip_ksp_get_converged_reason(aijhip_ksp_t ksp, int *reason);

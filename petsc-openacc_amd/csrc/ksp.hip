@@ -140,6 +140,7 @@ struct aijhip_ksp {
     // (Those A/B forms were withdrawn in round 4.)
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
     double *d_hist = nullptr;
+    double *d_hb = nullptr, *d_hx = nullptr;  // aijhip_ksp_solve_host's device copies of b and x
     int32_t hist_cap = 0;
     CGState *d_state = nullptr;
     CGState *h_state = nullptr;  // pinned
@@ -172,6 +173,8 @@ void ksp_free(aijhip_ksp *K) {
     mg_free(K);
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
     hipFree(K->d_hist); hipFree(K->d_state);
+    hipFree(K->d_hb); hipFree(K->d_hx);
+    K->d_hb = K->d_hx = nullptr;
     if (K->h_state) hipHostFree(K->h_state);
     K->d_dinv = K->d_r = K->d_z = K->d_p = K->d_part = K->d_hist = nullptr;
     K->d_state = nullptr;
@@ -705,6 +708,31 @@ int aijhip_ksp_get_gamg_setup_path(aijhip_ksp_t K, int32_t cap, int32_t *path, i
         if (product_cols) product_cols[l] = K->setup_cols[l];
     }
     if (host_fallback) *host_fallback = K->setup_overflow ? 1 : 0;
+    return AIJHIP_OK;
+}
+
+int aijhip_ksp_solve_host(aijhip_ksp_t K, const double *b, double *x) {
+    if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
+    const int64_t m = K->A->m;
+    if (m > 0 && (!b || !x)) return kfail(AIJHIP_ERR_ARG, "NULL vector");
+    if (b == x) return kfail(AIJHIP_ERR_ARG, "b and x alias");
+    int rc = aijhip_ksp_set_up(K);
+    if (rc) return rc;
+    KDeviceGuard g(K->A->device);
+    hipError_t e = hipSuccess;
+    if (!K->d_hb && (e = hipMalloc(&K->d_hb, sizeof(double) * (size_t)std::max<int64_t>(m, 1))) != hipSuccess)
+        return khip(e, "KSPSolve host vectors");
+    if (!K->d_hx && (e = hipMalloc(&K->d_hx, sizeof(double) * (size_t)std::max<int64_t>(m, 1))) != hipSuccess)
+        return khip(e, "KSPSolve host vectors");
+    // b (and a nonzero initial guess) up once, x down once: 2 x 8m bytes over
+    // PCIe per solve instead of per MatMult (the reference's step-2 copies)
+    if (m > 0 && ((e = hipMemcpy(K->d_hb, b, sizeof(double) * (size_t)m, hipMemcpyHostToDevice)) != hipSuccess ||
+                  (K->guess_nonzero &&
+                   (e = hipMemcpy(K->d_hx, x, sizeof(double) * (size_t)m, hipMemcpyHostToDevice)) != hipSuccess)))
+        return khip(e, "KSPSolve b / x in");
+    if ((rc = aijhip_ksp_solve(K, K->d_hb, K->d_hx, nullptr))) return rc;
+    if (m > 0 && (e = hipMemcpy(x, K->d_hx, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost)) != hipSuccess)
+        return khip(e, "KSPSolve x out");
     return AIJHIP_OK;
 }
 

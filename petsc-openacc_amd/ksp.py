@@ -29,6 +29,7 @@ KSP_SYMBOLS = (
     "aijhip_ksp_get_residual_history", "aijhip_ksp_get_fused", "aijhip_ksp_destroy",
     "aijhip_ksp_set_gamg_params", "aijhip_ksp_get_pc_levels", "aijhip_ksp_get_pc_level",
     "aijhip_ksp_get_gamg_setup_path", "aijhip_ksp_get_host_syncs", "aijhip_ksp_get_iteration_bytes",
+    "aijhip_ksp_solve_host",
 )
 _P = ctypes.c_void_p
 _bound = False
@@ -47,6 +48,7 @@ def _lib():
         L.aijhip_ksp_set_initial_guess_nonzero.argtypes = [_P, ctypes.c_int]
         L.aijhip_ksp_set_up.argtypes = [_P]
         L.aijhip_ksp_solve.argtypes = [_P, _P, _P, _P]
+        L.aijhip_ksp_solve_host.argtypes = [_P, _P, _P]
         L.aijhip_ksp_get_iteration_number.argtypes = [_P, ctypes.POINTER(ctypes.c_int32)]
         L.aijhip_ksp_get_residual_norm.argtypes = [_P, ctypes.POINTER(ctypes.c_double)]
         L.aijhip_ksp_get_converged_reason.argtypes = [_P, ctypes.POINTER(ctypes.c_int)]
@@ -93,6 +95,14 @@ class KSPCG:
     def solve(self, b, x, stream=None):
         _pkg._check(_lib().aijhip_ksp_solve(self._h, _pkg._dev_ptr(b, self.A.m, "b"),
                                             _pkg._dev_ptr(x, self.A.m, "x"), _pkg._stream_handle(stream)))
+
+    def solve_host(self, b: np.ndarray, x: np.ndarray):
+        """KSPSolve with host arrays (aijhip_ksp_solve_host): b up and x down
+        once per solve, the solve itself on the device."""
+        b = np.ascontiguousarray(b, dtype=np.float64)
+        if x.dtype != np.float64 or not x.flags["C_CONTIGUOUS"] or len(x) < self.A.m or len(b) < self.A.m:
+            raise TypeError("solve_host: contiguous float64 arrays of the operator's size")
+        _pkg._check(_lib().aijhip_ksp_solve_host(self._h, b.ctypes.data, x.ctypes.data))
 
     @property
     def its(self) -> int:
@@ -249,6 +259,13 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
         t_solve = time.perf_counter() - t0
         its, reason, rnorm, syncs = ksp.its, ksp.reason, ksp.rnorm, ksp.host_syncs
         nb, nb_spmv, nb_l0 = ksp.iteration_bytes()
+        # the same solve from HOST b / x (aijhip_ksp_solve_host: the PETSc KSP
+        # type "cghip" for an unchanged caller with host Vecs)
+        xh = np.zeros(A.m)
+        t0 = time.perf_counter()
+        ksp.solve_host(rhs, xh)
+        t_host_solve = time.perf_counter() - t0
+        host_same = bool(np.array_equal(xh.view(np.uint64), x.cpu().numpy().view(np.uint64)))
     err = float((x.cpu() - torch.from_numpy(exact)).abs().max())
     # the same set-up again in this process (a caller that rebuilds the
     # hierarchy after new values): the first one above also pays one-time
@@ -262,6 +279,9 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
     return {"its": its, "reason": reason, "rnorm": rnorm, "max_err": err,
             "setup_s": round(t_setup, 3), "setup_again_s": round(t_again, 3), "setup_pc_s": round(t_host, 3),
             "solve_s": round(t_solve, 4), "first_solve_s": round(t_first, 4),
+            "solve_host_vectors": {"s": round(t_host_solve, 4), "bitwise_equal_device_solve": host_same,
+                                   "note": "aijhip_ksp_solve_host: b up and x down once per solve (the KSP type "
+                                           "cghip of the PETSc adapter for host Vecs), PCIe included"},
             "ms_per_iter": round(t_solve / max(its, 1) * 1e3, 4), "host_syncs": syncs,
             "time_to_solution_s": round(t_setup + t_solve, 3),
             "levels": [{"rows": r, "nnz": z} for r, z in zip(rows, nnz)],

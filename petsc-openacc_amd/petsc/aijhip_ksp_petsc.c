@@ -1,0 +1,204 @@
+/*
+ * aijhip_ksp_petsc.c — PETSc 3.7 KSP type "cghip": the whole KSPSolve of
+ * main_ksp.cpp:92-103 (CG with the reference's PC) on the MI355X through
+ * include/aijhip_ksp.h, for a caller whose Vecs stay on the host.
+ *
+ * NOT COMPILED IN THIS IMAGE (no PETSc here or on the GPU box); built into
+ * libaijhip_petsc.so beside aijhip_petsc.c when PETSC_DIR is set. The entry
+ * point it calls, aijhip_ksp_solve_host, is exercised through the same C ABI
+ * by tests/test_ksp.py::test_gpu_solve_host_vectors_equals_device_solve.
+ *
+ * Why: with the Mat adapter alone every MatMult of an unchanged caller moves
+ * x up and y down over PCIe (the reference's step-2 cost, 432 MB per 300^3
+ * MatMult, SURVEY §7 "Host-resident Vecs kill it"). Selecting this type in
+ * the options file (`-ksp_type cghip` beside configs/PETSc_SolverOptions_
+ * GAMG.info's other lines) moves b up and x down once per solve instead; the
+ * CG iteration, the PC (gamg / jacobi / none with PETSc's option names) and
+ * the convergence test run on the device (aijhip_ksp.h). main_ksp.cpp reads
+ * its, reason, rnorm and the history back through the usual KSP getters.
+ * Any other operator or PC falls back to PETSc's own KSPCG.
+ */
+#include <petsc/private/kspimpl.h>
+#include <petsc/private/pcimpl.h>
+
+#include "aijhip.h"
+#include "aijhip_gamg.h"
+#include "aijhip_ksp.h"
+
+/* aijhip_petsc.c: the device handle of a seqaij(hip) matrix, brought up to
+ * date with the host values; NULL for any other matrix. */
+PETSC_EXTERN PetscErrorCode AIJHIPGetHandle(Mat A, aijhip_mat_t *h);
+
+typedef struct {
+  aijhip_ksp_t     k;
+  aijhip_mat_t     h;     /* the handle k was set up on */
+  PetscObjectState state; /* the operator's state at that set-up */
+  int              pc;
+} KSP_CGHIP;
+
+static PetscErrorCode KSPCGHIPFree(KSP_CGHIP *c)
+{
+  PetscFunctionBegin;
+  if (c->k) aijhip_ksp_destroy(c->k);
+  c->k = NULL;
+  c->h = NULL;
+  PetscFunctionReturn(0);
+}
+
+/* The reference's PCs, by PETSc type name; -1: not offered on the device. */
+static PetscErrorCode KSPCGHIPPCType(KSP ksp, int *pc)
+{
+  PetscBool      is;
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  *pc = -1;
+  ierr = PetscObjectTypeCompare((PetscObject)ksp->pc, PCGAMG, &is);CHKERRQ(ierr);
+  if (is) { *pc = AIJHIP_PC_GAMG; PetscFunctionReturn(0); }
+  ierr = PetscObjectTypeCompare((PetscObject)ksp->pc, PCJACOBI, &is);CHKERRQ(ierr);
+  if (is) { *pc = AIJHIP_PC_JACOBI; PetscFunctionReturn(0); }
+  ierr = PetscObjectTypeCompare((PetscObject)ksp->pc, PCNONE, &is);CHKERRQ(ierr);
+  if (is) *pc = AIJHIP_PC_NONE;
+  PetscFunctionReturn(0);
+}
+
+/* PETSc's own CG for what the device path does not cover. */
+static PetscErrorCode KSPCGHIPFallBack(KSP ksp)
+{
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  ierr = PetscInfo(ksp, "cghip: operator or PC not on the device; using KSPCG\n");CHKERRQ(ierr);
+  ierr = KSPSetType(ksp, KSPCG);CHKERRQ(ierr);
+  ierr = KSPSetUp(ksp);CHKERRQ(ierr);
+  PetscFunctionReturn(0);
+}
+
+/* KSPSetUp (PCSetUp_GAMG included, timed by main_ksp.cpp as "create
+ * solver"): the device KSP on the operator's handle with the options file's
+ * PC settings. */
+static PetscErrorCode KSPSetUp_CGHIP(KSP ksp)
+{
+  KSP_CGHIP            *c = (KSP_CGHIP*)ksp->data;
+  Mat                  A;
+  aijhip_mat_t         h = NULL;
+  PetscObjectState     state;
+  aijhip_gamg_params_t gp;
+  PetscInt             iv;
+  PetscReal            rv;
+  PetscBool            set;
+  int                  pc, nt, rc;
+  PetscErrorCode       ierr;
+
+  PetscFunctionBegin;
+  ierr = KSPGetOperators(ksp, &A, NULL);CHKERRQ(ierr);
+  ierr = AIJHIPGetHandle(A, &h);CHKERRQ(ierr);
+  ierr = KSPCGHIPPCType(ksp, &pc);CHKERRQ(ierr);
+  if (!h || pc < 0) {
+    ierr = KSPCGHIPFallBack(ksp);CHKERRQ(ierr);
+    PetscFunctionReturn(0);
+  }
+  ierr = PetscObjectStateGet((PetscObject)A, &state);CHKERRQ(ierr);
+  if (c->k && c->h == h && c->state == state && c->pc == pc) PetscFunctionReturn(0);
+  ierr = KSPCGHIPFree(c);CHKERRQ(ierr);
+  rc = aijhip_ksp_create(h, &c->k);
+  if (!rc) rc = aijhip_ksp_set_pc_type(c->k, pc);
+  if (!rc && pc == AIJHIP_PC_GAMG) {
+    aijhip_gamg_params_default(&gp);
+    ierr = PetscOptionsGetReal(NULL, NULL, "-pc_gamg_threshold", &rv, &set);CHKERRQ(ierr);
+    if (set) gp.threshold = (double)rv;
+    ierr = PetscOptionsGetInt(NULL, NULL, "-pc_gamg_agg_nsmooths", &iv, &set);CHKERRQ(ierr);
+    if (set) gp.nsmooths = (int32_t)iv;
+    ierr = PetscOptionsGetInt(NULL, NULL, "-pc_gamg_coarse_eq_limit", &iv, &set);CHKERRQ(ierr);
+    if (set) gp.coarse_eq_limit = (int32_t)iv;
+    ierr = PetscOptionsGetInt(NULL, NULL, "-pc_mg_levels", &iv, &set);CHKERRQ(ierr);
+    if (set) gp.max_levels = (int32_t)iv;
+    rc = aijhip_ksp_set_gamg_params(c->k, &gp);
+  }
+  switch (ksp->normtype) {
+    case KSP_NORM_NONE:            nt = AIJHIP_KSP_NORM_NONE; break;
+    case KSP_NORM_UNPRECONDITIONED: nt = AIJHIP_KSP_NORM_UNPRECONDITIONED; break;
+    case KSP_NORM_NATURAL:         nt = AIJHIP_KSP_NORM_NATURAL; break;
+    default:                       nt = AIJHIP_KSP_NORM_PRECONDITIONED; break;
+  }
+  if (!rc) rc = aijhip_ksp_set_norm_type(c->k, nt);
+  if (!rc) rc = aijhip_ksp_set_tolerances(c->k, ksp->rtol, ksp->abstol, ksp->divtol, (int32_t)ksp->max_it);
+  if (!rc) rc = aijhip_ksp_set_up(c->k);
+  if (rc) SETERRQ1(PetscObjectComm((PetscObject)ksp), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
+  c->h = h;
+  c->state = state;
+  c->pc = pc;
+  PetscFunctionReturn(0);
+}
+
+/* KSPSolve: b up, the whole CG on the device, x down (aijhip_ksp_solve_host);
+ * then its, rnorm, reason and the residual history as KSPSolve_CG leaves
+ * them, and the monitors replayed from the history. */
+static PetscErrorCode KSPSolve_CGHIP(KSP ksp)
+{
+  KSP_CGHIP         *c = (KSP_CGHIP*)ksp->data;
+  const PetscScalar *b;
+  PetscScalar       *x;
+  int32_t           its, n = 0, i;
+  double            rnorm, *hist = NULL;
+  int               reason, rc;
+  PetscErrorCode    ierr;
+
+  PetscFunctionBegin;
+  ierr = KSPSetUp_CGHIP(ksp);CHKERRQ(ierr);
+  rc = aijhip_ksp_set_tolerances(c->k, ksp->rtol, ksp->abstol, ksp->divtol, (int32_t)ksp->max_it);
+  if (!rc) rc = aijhip_ksp_set_initial_guess_nonzero(c->k, ksp->guess_zero ? 0 : 1);
+  if (rc) SETERRQ1(PetscObjectComm((PetscObject)ksp), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
+  ierr = VecGetArrayRead(ksp->vec_rhs, &b);CHKERRQ(ierr);
+  ierr = VecGetArray(ksp->vec_sol, &x);CHKERRQ(ierr);
+  rc = aijhip_ksp_solve_host(c->k, b, x);
+  ierr = VecRestoreArrayRead(ksp->vec_rhs, &b);CHKERRQ(ierr);
+  ierr = VecRestoreArray(ksp->vec_sol, &x);CHKERRQ(ierr);
+  if (rc) SETERRQ1(PetscObjectComm((PetscObject)ksp), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
+  aijhip_ksp_get_iteration_number(c->k, &its);
+  aijhip_ksp_get_residual_norm(c->k, &rnorm);
+  aijhip_ksp_get_converged_reason(c->k, &reason); /* PETSc's KSPConvergedReason values */
+  ksp->its    = its;
+  ksp->rnorm  = rnorm;
+  ksp->reason = (KSPConvergedReason)reason;
+  ierr = PetscMalloc1(its + 2, &hist);CHKERRQ(ierr);
+  aijhip_ksp_get_residual_history(c->k, hist, its + 2, &n);
+  for (i = 0; i < n; ++i) {
+    ierr = KSPLogResidualHistory(ksp, hist[i]);CHKERRQ(ierr);
+    ierr = KSPMonitor(ksp, i, hist[i]);CHKERRQ(ierr);
+  }
+  ierr = PetscFree(hist);CHKERRQ(ierr);
+  PetscFunctionReturn(0);
+}
+
+static PetscErrorCode KSPDestroy_CGHIP(KSP ksp)
+{
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  ierr = KSPCGHIPFree((KSP_CGHIP*)ksp->data);CHKERRQ(ierr);
+  ierr = KSPDestroyDefault(ksp);CHKERRQ(ierr);
+  PetscFunctionReturn(0);
+}
+
+PETSC_EXTERN PetscErrorCode KSPCreate_CGHIP(KSP ksp)
+{
+  KSP_CGHIP      *c;
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  ierr = PetscNewLog(ksp, &c);CHKERRQ(ierr);
+  ksp->data = (void*)c;
+  /* KSPCG's norms and sides (left preconditioning only) */
+  ierr = KSPSetSupportedNorm(ksp, KSP_NORM_PRECONDITIONED, PC_LEFT, 3);CHKERRQ(ierr);
+  ierr = KSPSetSupportedNorm(ksp, KSP_NORM_UNPRECONDITIONED, PC_LEFT, 2);CHKERRQ(ierr);
+  ierr = KSPSetSupportedNorm(ksp, KSP_NORM_NATURAL, PC_LEFT, 2);CHKERRQ(ierr);
+  ierr = KSPSetSupportedNorm(ksp, KSP_NORM_NONE, PC_LEFT, 1);CHKERRQ(ierr);
+  ksp->ops->setup          = KSPSetUp_CGHIP;
+  ksp->ops->solve          = KSPSolve_CGHIP;
+  ksp->ops->destroy        = KSPDestroy_CGHIP;
+  ksp->ops->setfromoptions = NULL;
+  ksp->ops->buildsolution  = KSPBuildSolutionDefault;
+  ksp->ops->buildresidual  = KSPBuildResidualDefault;
+  PetscFunctionReturn(0);
+}

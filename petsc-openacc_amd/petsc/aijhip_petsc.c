@@ -39,9 +39,12 @@
  * matrix has at least -aijhip_transfer_min_nz entries (default 262144:
  * below that PETSc's own loop beats a PCIe round trip); smaller ones keep
  * PETSc's SeqAIJ (or Inode) bodies. A device Vec type is what removes the
- * PCIe traffic.
+ * PCIe traffic; the KSP type "cghip"
+ * (aijhip_ksp_petsc.c, registered below) removes it for the reference's
+ * solver by running the whole KSPSolve on the device.
  */
 #include <petsc/private/matimpl.h>
+#include <petscksp.h>
 #include <../src/mat/impls/aij/seq/aij.h>
 
 #include "aijhip.h"
@@ -193,6 +196,21 @@ static PetscErrorCode AIJHIPCurrent(Mat A, Mat_AIJHIP **out)
   PetscFunctionReturn(0);
 }
 
+/* The device handle of A brought up to date (aijhip_ksp_petsc.c's KSP type
+ * solves on it); NULL when A is not a matrix of this adapter. */
+PETSC_EXTERN PetscErrorCode AIJHIPGetHandle(Mat A, aijhip_mat_t *h)
+{
+  Mat_AIJHIP     *d;
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  *h = NULL;
+  if (A->ops->mult != AIJHIPMult) PetscFunctionReturn(0);
+  ierr = AIJHIPCurrent(A, &d);CHKERRQ(ierr);
+  *h = d->h;
+  PetscFunctionReturn(0);
+}
+
 /* zz = yy + A xx (MatMultAdd_SeqAIJ: each row sum starts from yy[i]). */
 static PetscErrorCode AIJHIPMultAdd(Mat A, Vec xx, Vec yy, Vec zz)
 {
@@ -328,12 +346,17 @@ PETSC_EXTERN PetscErrorCode MatCreate_SeqAIJHIP(Mat A)
 /* replace = PETSC_TRUE: every "seqaij" matrix uses the device MatMult and
  * keeps its type name (the reference's link-time patch reaches every SeqAIJ
  * the same way). */
+PETSC_EXTERN PetscErrorCode KSPCreate_CGHIP(KSP); /* aijhip_ksp_petsc.c */
+
 PETSC_EXTERN PetscErrorCode AIJHIPRegister(PetscBool replace)
 {
   PetscErrorCode ierr;
 
   PetscFunctionBegin;
   ierr = MatRegister("seqaijhip", MatCreate_SeqAIJHIP);CHKERRQ(ierr);
+  /* -ksp_type cghip: the whole KSPSolve on the device (host Vecs cross PCIe
+     once per solve, not per MatMult) */
+  ierr = KSPRegister("cghip", KSPCreate_CGHIP);CHKERRQ(ierr);
   if (replace) {
     type_name_seqaij = PETSC_TRUE;
     ierr = MatRegister(MATSEQAIJ, MatCreate_SeqAIJHIP);CHKERRQ(ierr);

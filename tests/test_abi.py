@@ -139,11 +139,15 @@ def test_petsc_adapter_binds_only_declared_symbols():
     tree, absent here) calls the library through the declared ABI alone, and
     its Makefile is a no-op without PETSC_DIR."""
     src = (ROOT / "petsc-openacc_amd" / "petsc" / "aijhip_petsc.c").read_text()
-    used = set(re.findall(r"\b(aijhip_\w+)\s*\(", src))
+    ksrc = (ROOT / "petsc-openacc_amd" / "petsc" / "aijhip_ksp_petsc.c").read_text()
+    used = set(re.findall(r"\b(aijhip_\w+)\s*\(", src + ksrc))
     assert {"aijhip_mat_create", "aijhip_mat_mult_host", "aijhip_mat_update_values",
             "aijhip_mat_assembly_end", "aijhip_mat_destroy", "aijhip_mat_mult_add_host",
             "aijhip_mat_mult_transpose_host"} <= used
+    assert {"aijhip_ksp_create", "aijhip_ksp_set_up", "aijhip_ksp_solve_host",
+            "aijhip_ksp_get_residual_history"} <= used  # the KSP type "cghip"
     assert used <= declared_functions()
+    assert 'KSPRegister("cghip", KSPCreate_CGHIP)' in src and "KSPSolve_CGHIP" in ksrc
     for sym in ("MatRegister", "MatCreate_SeqAIJ", "PetscDLLibraryRegister_aijhip_petsc",
                 "MatAssemblyEnd_SeqAIJ", "MatDestroy_SeqAIJ", "MatMult_SeqAIJ", "ops->multadd",
                 "ops->multtranspose", "-aijhip_transfer_min_nz"):

@@ -123,3 +123,30 @@ def test_gpu_cg_deterministic(pkg):
             xs.append(x.cpu().numpy())
     assert np.array_equal(xs[0].view(np.uint64), xs[1].view(np.uint64))
     A.destroy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pc,guess", [("gamg", False), ("jacobi", False), ("jacobi", True)])
+def test_gpu_solve_host_vectors_equals_device_solve(pkg, pc, guess):
+    """KSPSolve with host b / x (aijhip_ksp_solve_host: the solve-level
+    offload a registered PETSc KSP type uses, b up and x down once per
+    solve) is the device solve bit for bit, iterations and history too, with a
+    zero and with a nonzero initial guess."""
+    import torch
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    N = 20
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, _ = pkg.poisson_vectors(N)
+    x0 = pkg.splitmix_uniform(len(rhs), 3) if guess else np.zeros(len(rhs))
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        with K.KSPCG(A, rtol=1e-12, atol=1e-14, pc=pc, guess_nonzero=guess) as ksp:
+            b = torch.from_numpy(rhs).cuda()
+            xd = torch.from_numpy(x0.copy()).cuda()
+            ksp.solve(b, xd)
+            torch.cuda.synchronize()
+            its_d, hist_d, xdev = ksp.its, np.array(ksp.history()), xd.cpu().numpy()
+            xh = x0.copy()
+            ksp.solve_host(rhs, xh)
+            assert ksp.its == its_d
+            assert np.array_equal(np.array(ksp.history()).view(np.uint64), hist_d.view(np.uint64))
+            assert np.array_equal(xh.view(np.uint64), xdev.view(np.uint64))
