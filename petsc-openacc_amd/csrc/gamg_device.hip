@@ -131,21 +131,41 @@ __global__ void k_rows_unsorted(int32_t m, const int32_t *__restrict__ ai, const
     for (int64_t base = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * (64 / G); base < m;         \
          base += nw * (64 / G))
 
+// Also: flag[0] = 1 when a row's columns do not strictly increase (the
+// neighbouring entry's column is a neighbouring lane's load), and *updown +=
+// (strong entries above the diagonal) - (below it), one atomic per wavefront:
+// with every upper entry mirrored (k_strong_asymmetric) a zero tally makes S
+// symmetric (the mirror map is injective from the upper entries into the
+// lower ones; equal counts make it onto).
 template <int G>
 __global__ __launch_bounds__(256) void k_strong_direct_count(int32_t m, const int32_t *__restrict__ ai,
                                                              const int32_t *__restrict__ aj,
                                                              const double *__restrict__ aa,
                                                              const double *__restrict__ d, double theta,
-                                                             int32_t *cnt) {
+                                                             int32_t *cnt, int32_t *flag,
+                                                             unsigned long long *updown) {
+    long long ud = 0;
+    bool unsorted = false;
     AIJHIP_ROW_LANES {
         const int64_t i = base + lane / G;
         const bool on = i < m;
         const int32_t a0 = on ? ai[i] : 0, a1 = on ? ai[i + 1] : 0;
         int32_t c = 0;
-        for (int32_t k = a0 + l; k < a1; k += G) c += strong((int32_t)i, aj[k], aa[k], d, theta);
+        for (int32_t k = a0 + l; k < a1; k += G) {
+            const int32_t j = aj[k];
+            unsorted |= k > a0 && aj[k - 1] >= j;
+            if (strong((int32_t)i, j, aa[k], d, theta)) {
+                ++c;
+                ud += j > i ? 1 : -1;
+            }
+        }
         for (int o = G / 2; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
         if (on && l == 0) cnt[i] = c;
     }
+    (void)segmask;
+    for (int o = 32; o > 0; o >>= 1) ud += __shfl_xor(ud, o, 64);
+    if (__ballot(unsorted) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+    if (ud != 0 && (threadIdx.x & 63) == 0) atomicAdd(updown, (unsigned long long)ud);
 }
 
 // the strong entries in A's order: lanes take entries l, l + G, ... and
@@ -181,7 +201,8 @@ __global__ __launch_bounds__(256) void k_strong_direct_fill(int32_t m, const int
     }
 }
 
-// flag = 1 when some (i, j) of S has no (j, i)
+// flag = 1 when some (i, j) of S with j > i has no (j, i) (the entries below
+// the diagonal are covered by the tally of k_strong_direct_count)
 template <int G>
 __global__ __launch_bounds__(256) void k_strong_asymmetric(int32_t m, const int32_t *__restrict__ si,
                                                            const int32_t *__restrict__ sj, int32_t *flag) {
@@ -192,6 +213,7 @@ __global__ __launch_bounds__(256) void k_strong_asymmetric(int32_t m, const int3
         bool bad = false;
         for (int32_t k = si[i] + l; k < si[i + 1] && !bad; k += G) {
             const int32_t j = sj[k];
+            if (j < (int32_t)i) continue;
             const int32_t e = si[j + 1];
             int32_t lo = si[j], hi = e;
             while (lo < hi) {
@@ -971,20 +993,19 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
 int strength_direct(const aijhip_mat &A, const double *d, double theta, int32_t **si, int32_t **sj,
                     double **sval, int64_t *nzs, bool *ok) {
     const int32_t m = A.m;
-    const unsigned g256 = blocks_for(m, 256);
     int32_t *cnt = nullptr, *flag = nullptr;
-    int32_t h_flag = 0;
+    unsigned long long *updown = nullptr;  // flag (int32) and the tally, one allocation
+    struct { int32_t flag, pad; long long updown; } h = {0, 0, 0};
     hipError_t e;
     int rc = AIJHIP_OK;
     *ok = false;
     *si = *sj = nullptr;
     *sval = nullptr;
 #define DTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto done; } } while (0)
-    DTRY(dalloc(&flag, 1), "alloc");
-    DTRY(hipMemset(flag, 0, sizeof(int32_t)), "memset");
-    hipLaunchKernelGGL(k_rows_unsorted, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, flag);
-    DTRY(hipMemcpy(&h_flag, flag, sizeof(h_flag), hipMemcpyDeviceToHost), "read");
-    if (h_flag) goto done;
+    DTRY(dalloc(&updown, 2), "alloc");
+    flag = reinterpret_cast<int32_t *>(updown);
+    ++updown;
+    DTRY(hipMemset(flag, 0, 2 * sizeof(unsigned long long)), "memset");
     {
         // lanes per row: the mean row length rounded up to a power of two
         const double mean = m > 0 ? (double)A.nz / m : 1.0;
@@ -995,10 +1016,13 @@ int strength_direct(const aijhip_mat &A, const double *d, double theta, int32_t 
 #define AIJHIP_SD(GG)                                                                                         \
     case GG:                                                                                                  \
         hipLaunchKernelGGL((k_strong_direct_count<GG>), dim3(grid), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj,  \
-                           A.d_aa, d, theta, cnt);                                                            \
+                           A.d_aa, d, theta, cnt, flag, updown);                                              \
         break
         switch (G) { AIJHIP_SD(4); AIJHIP_SD(8); AIJHIP_SD(16); AIJHIP_SD(32); AIJHIP_SD(64); }
 #undef AIJHIP_SD
+        DTRY(hipGetLastError(), "strength kernels");
+        DTRY(hipMemcpy(&h, flag, sizeof(h), hipMemcpyDeviceToHost), "read");
+        if (h.flag || h.updown != 0) goto done;  // unsorted rows, or S cannot be symmetric
         DTRY(dalloc(si, (int64_t)m + 1), "alloc");
         DTRY(scan_offsets(cnt, m, *si, nzs), "scan");
         if (*nzs > INT32_MAX) { rc = AIJHIP_ERR_ARG; set_error("GAMG: strength graph exceeds int32"); goto done; }
@@ -1014,12 +1038,12 @@ int strength_direct(const aijhip_mat &A, const double *d, double theta, int32_t 
 #undef AIJHIP_SD
     }
     DTRY(hipGetLastError(), "strength kernels");
-    DTRY(hipMemcpy(&h_flag, flag, sizeof(h_flag), hipMemcpyDeviceToHost), "read");
-    *ok = h_flag == 0;
+    DTRY(hipMemcpy(&h.flag, flag, sizeof(h.flag), hipMemcpyDeviceToHost), "read");
+    *ok = h.flag == 0;
 done:
 #undef DTRY
     hipFree(cnt);
-    hipFree(flag);
+    hipFree(flag);  // (and the tally: one allocation)
     if (rc || !*ok) {
         hipFree(*si); hipFree(*sj); hipFree(*sval);
         *si = *sj = nullptr;
@@ -1395,8 +1419,7 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
                      std::chrono::duration<double>(t - t0).count());
         t0 = t;
     };
-    std::unique_lock<std::mutex> stage_lock;
-    Staging &stage = process_staging(stage_lock);
+    std::unique_lock<std::mutex> stage_lock;  // taken by the host pass only
     int rc = AIJHIP_OK;
     hipError_t e = hipSuccess;
     const unsigned g256 = blocks_for(m, 256);
@@ -1487,6 +1510,7 @@ strength_done:
         for (int c = 0; c < kChunks; ++c) slot = std::max<int64_t>(slot, (int64_t)h_off[c + 1] - h_off[c]);
         (void)hipHostFree(h_off);
         GTRY(e, "read S offsets");
+        Staging &stage = process_staging(stage_lock);
         GTRY(stage.reserve(sizeof(int32_t) * (2 * (size_t)m + 1 + 2 * (size_t)slot)), "pinned staging");
         lap("staging alloc");
         h_si = stage.i32();
@@ -1511,11 +1535,19 @@ strength_done:
             for (int c = 0; c < 2 && c < kChunks && e == hipSuccess; ++c) e = fetch(c);
             std::fill(agg, agg + m, -1);
             na = 0;
+            double t_wait = 0.0, t_pass = 0.0;  // (logged: copy-bound or pass-bound)
             for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
+                const auto w0 = std::chrono::steady_clock::now();
                 if ((e = hipEventSynchronize(ev[c & 1])) != hipSuccess) break;
+                const auto w1 = std::chrono::steady_clock::now();
                 na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_slot[c & 1], agg, na, h_si[r[c]]);
                 if (c + 2 < kChunks) e = fetch(c + 2);
+                t_wait += std::chrono::duration<double, std::milli>(w1 - w0).count();
+                t_pass += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w1).count();
             }
+            if (log)
+                std::fprintf(stderr, "gamg device level %zu host phase 1: %.1f MB of S, waits %.2f ms, pass %.2f ms\n",
+                             level, 4e-6 * (double)nzs, t_wait, t_pass);
             (void)hipStreamSynchronize(cs);
             for (hipEvent_t x : ev)
                 if (x) (void)hipEventDestroy(x);
@@ -1749,6 +1781,24 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     double *d_B = nullptr;
     if ((e = dalloc(&d_B, A0->m)) != hipSuccess) return herr(e, "alloc");
     hipLaunchKernelGGL(k_fill, dim3(blocks_for(A0->m, 256)), dim3(256), 0, nullptr, A0->m, 1.0, d_B);
+    // A finest level the device sweep aggregates leaves the first host pass
+    // to level 1: its pinned staging (S row chunks and ids, ~15 B per level-1
+    // row, ~2 B per finest row at aggregates of ~8) is reserved on a host
+    // thread meanwhile (6 ms of pinning at 300^3 on a first set-up)
+    std::thread prestage;
+    {
+        int32_t rounds = 0;
+        if (A0->m >= p.device_min_rows && device_phase1(A0->m, A0->nz - A0->m, &rounds))
+            prestage = std::thread([bytes = (size_t)A0->m * 5 / 2, device = A0->device] {
+                (void)hipSetDevice(device);
+                std::unique_lock<std::mutex> lock;
+                (void)process_staging(lock).reserve(bytes);
+            });
+    }
+    struct Joiner {
+        std::thread &t;
+        ~Joiner() { if (t.joinable()) t.join(); }
+    } prestage_join{prestage};
     lap("first kernel");
     while ((int32_t)levels.size() < p.max_levels && levels.back().A->m > p.coarse_eq_limit) {
         aijhip_mat &A = *levels.back().A;

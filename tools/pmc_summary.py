@@ -69,6 +69,13 @@ def main():
         if "TCC_HIT_sum" in cs and "TCC_MISS_sum" in cs:
             tot = cs["TCC_HIT_sum"] + cs["TCC_MISS_sum"]
             r["l2_hit_rate"] = cs["TCC_HIT_sum"] / tot if tot else None
+        if cs.get("SQ_WAVE_CYCLES"):
+            if "SQ_WAIT_ANY" in cs:
+                r["sq_wait_frac"] = cs["SQ_WAIT_ANY"] / cs["SQ_WAVE_CYCLES"]
+            if "SQ_ACTIVE_INST_ANY" in cs:
+                r["sq_active_inst_frac"] = cs["SQ_ACTIVE_INST_ANY"] / cs["SQ_WAVE_CYCLES"]
+        if cs.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_BANK_CONFLICT" in cs:
+            r["lds_bank_conflict_frac"] = cs["SQ_LDS_BANK_CONFLICT"] / cs["SQ_LDS_IDX_ACTIVE"]
         if "TCC_EA0_RDREQ_sum" in cs:
             r["ea_rd_bytes_64B"] = cs["TCC_EA0_RDREQ_sum"] * 64
         res[k] = r
