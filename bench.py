@@ -371,16 +371,17 @@ def flan_standins(pkg, dev, reps, cpu_sample):
     the same byte count in the same run:
       skewed — 1,564,794 rows of 45-99 banded entries plus 1e-4 hub rows of
                1e3-2e5 scattered entries (seed 1565): the merge-path
-               load-balance stress; STREAM (default: hub rows by x column
-               window), STREAM exact (PETSc's order in every row that fits a
-               block) and the hub rows as 4096-entry segments;
+               load-balance stress; STREAM (default: gather-ordered row
+               blocks, hub rows as 4096-entry segments), STREAM exact
+               (PETSc's order in every row that fits a block) and STREAM on
+               PETSc's aj as stored (stream_csr);
       fem_hex — Flan_1565's own structure: a hexahedral mesh of 81x80x80
                nodes, 3 dofs per node, 81-entry interior rows.
     Parity is the -m gpu tests' job (tests/test_flan_standins_gpu.py)."""
     import torch
     stream = torch.cuda.current_stream()
     out = {}
-    for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(), ("stream", "stream_exact", "stream_segments")),
+    for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(), ("stream", "stream_exact", "stream_csr")),
                                 ("fem_hex", lambda: pkg.fem_hex_csr(), ("stream",))):
         ai, aj, aa = make()
         m, nnz = len(ai) - 1, len(aj)
@@ -393,8 +394,8 @@ def flan_standins(pkg, dev, reps, cpu_sample):
             try:
                 if kern == "stream_exact":
                     A.set_option("exact", 1)
-                if kern == "stream_segments":  # hub rows as 4096-entry segments instead of x windows
-                    A.set_option("long_window", 0)
+                if kern == "stream_csr":  # aj as stored: no gather order
+                    A.set_option("gather_sort", 0)
                 info = A.info()
                 for _ in range(5):
                     A.mult(x, y, stream)
@@ -408,7 +409,7 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                          "csr_effective_GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
                          "geometry": info.get("stream_geometry"), "long_rows": info.get("n_long_rows"),
                          "column_codes": info.get("column_codes"), "gather_sorted": info.get("gather_sorted"),
-                         "row_patterns": info.get("row_patterns"), "long_windows": info.get("long_windows")}
+                         "row_patterns": info.get("row_patterns")}
         del x, y
         flat = read_ceiling(nbytes, dev)
         rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],

@@ -50,10 +50,11 @@
 extern "C" {
 #endif
 
-/* 2: aijhip_info_t gained long_windows and mult_layout_bytes; the A/B-only
- * options AIJHIP_OPT_XCD_REMAP / _PERSISTENT / _CLAMPED_LOADS /
- * _LONG_OVERLAP / _ROW_GROUP and AIJHIP_KERNEL_MERGE were withdrawn
- * (measured slower) and return AIJHIP_ERR_ARG. */
+/* 2: aijhip_info_t gained mult_layout_bytes and lost the fields of the
+ * withdrawn options; the A/B-only options AIJHIP_OPT_XCD_REMAP /
+ * _PERSISTENT / _CLAMPED_LOADS / _LONG_OVERLAP / _ROW_GROUP / _X_TILE /
+ * _LONG_WINDOW and AIJHIP_KERNEL_MERGE were withdrawn (measured slower,
+ * DESIGN.md §5) and return AIJHIP_ERR_ARG. */
 #define AIJHIP_ABI_VERSION 2
 
 enum {
@@ -105,14 +106,11 @@ typedef struct aijhip_info {
     int64_t mult_bytes;      /* algorithmic bytes per MatMult:
                                 12 nz + 4 (m+1) + 8 n + 8 m     */
     int32_t stream_geometry; /* AIJHIP_OPT_* values in effect                */
-    int32_t xcd_remap;
     int32_t nt_loads;
     int32_t stream_threads;  /* lanes / entries / rows per STREAM block      */
     int32_t stream_nnz_cap;
     int32_t stream_rows;
-    int32_t persistent;      /* workgroups per CU of the pipelined STREAM (0 = off) */
     int32_t exact;           /* AIJHIP_OPT_EXACT in effect                   */
-    int32_t x_tiled_blocks;  /* STREAM blocks gathering x from an LDS tile    */
     int32_t gather_sorted;   /* MatMult reads the gather-ordered copy of the
                                 row blocks (AIJHIP_OPT_GATHER_SORT): 1 with
                                 32-bit columns, 2 with 16-bit block-relative
@@ -124,9 +122,6 @@ typedef struct aijhip_info {
     int32_t row_patterns;    /* MatMult reads a pattern id per row instead of
                                 aj (AIJHIP_OPT_ROW_PATTERNS): the number of
                                 distinct column - row offset lists; 0 off    */
-    int32_t long_windows;    /* rows longer than a block summed by x column
-                                window (AIJHIP_OPT_LONG_WINDOW): the number
-                                of windows; 0 = 4096-entry segments        */
     int64_t mult_layout_bytes; /* compulsory bytes one MatMult of the plan in
                                 effect moves: mult_bytes for CSR (aj read);
                                 less where the plan reads column codes (10 B
@@ -184,13 +179,9 @@ enum {
                                        within the fp64 bound); shorter rows
                                        (7-pt Poisson, FEM rows) are bit-exact
                                        either way                           */
-    AIJHIP_OPT_X_TILE = 7,          /* 1: stage x in LDS for every block whose
-                                       columns span <= the block's LDS entries
-                                       (banded operators) and gather from
-                                       there; -1: only when half the blocks
-                                       fit; 0 (default, measured faster on
-                                       the skewed stand-in): gathers from
-                                       HBM/L2. Same results                   */
+    AIJHIP_OPT_X_TILE = 7,          /* withdrawn in ABI 2 (x staged in LDS per
+                                       row block, up to four column windows:
+                                       slower at every default geometry)     */
     AIJHIP_OPT_LONG_XCD = 8,        /* 1 (default): segments of long rows are
                                        launched so that XCD q (slot % 8)
                                        reduces those whose columns lie in the
@@ -232,17 +223,10 @@ enum {
                                        entries), else the automatic layout
                                        without them; costs 2 bytes per entry
                                        of device memory                      */
-    AIJHIP_OPT_LONG_WINDOW = 15,    /* rows longer than a STREAM block: 1 =
-                                       by x column window (each workgroup
-                                       stages 2048 x entries in LDS and sums
-                                       every long row's entries in that
-                                       window; the rows' window sums are added
-                                       in window order), 0 = 4096-entry
-                                       segments; -1 (default): windows when
-                                       the long rows are column-sorted, at
-                                       most 512 and >= 2048 of their entries
-                                       per window. Reordered, deterministic,
-                                       within the fp64 bound either way      */
+    AIJHIP_OPT_LONG_WINDOW = 15,    /* withdrawn in ABI 2 (long rows by x column
+                                       window staged in LDS: the hub rows no
+                                       faster than 4096-entry segments, their
+                                       window sums slower to finish)         */
     AIJHIP_OPT_ROW_PATTERNS = 14    /* short-row operands whose rows follow at
                                        most 256 distinct column - row offset
                                        lists (stencils): no per-entry column

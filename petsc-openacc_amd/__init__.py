@@ -32,10 +32,11 @@ if os.environ.get("AIJHIP_LIB"):
 
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
-OPTIONS = {"geometry": 1, "nt_loads": 3, "exact": 6, "x_tile": 7, "long_xcd": 8, "host_pipeline": 10,
-           "gather_sort": 12, "column_codes": 13, "row_patterns": 14, "long_window": 15}
+OPTIONS = {"geometry": 1, "nt_loads": 3, "exact": 6, "long_xcd": 8, "host_pipeline": 10,
+           "gather_sort": 12, "column_codes": 13, "row_patterns": 14}
 # withdrawn in ABI 2 (measured slower); the library refuses them
-WITHDRAWN_OPTIONS = {"xcd_remap": 2, "persistent": 4, "clamped": 5, "long_overlap": 9, "row_group": 11}
+WITHDRAWN_OPTIONS = {"xcd_remap": 2, "persistent": 4, "clamped": 5, "x_tile": 7, "long_overlap": 9, "row_group": 11,
+                     "long_window": 15}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 
@@ -70,11 +71,10 @@ class AIJInfo(ctypes.Structure):
         ("n_long_rows", ctypes.c_int32), ("device", ctypes.c_int32),
         ("device_bytes", ctypes.c_int64), ("mult_flops", ctypes.c_double),
         ("mult_bytes", ctypes.c_int64),
-        ("stream_geometry", ctypes.c_int32), ("xcd_remap", ctypes.c_int32), ("nt_loads", ctypes.c_int32),
+        ("stream_geometry", ctypes.c_int32), ("nt_loads", ctypes.c_int32),
         ("stream_threads", ctypes.c_int32), ("stream_nnz_cap", ctypes.c_int32), ("stream_rows", ctypes.c_int32),
-        ("persistent", ctypes.c_int32), ("exact", ctypes.c_int32), ("x_tiled_blocks", ctypes.c_int32),
-        ("gather_sorted", ctypes.c_int32), ("column_codes", ctypes.c_int32),
-        ("row_patterns", ctypes.c_int32), ("long_windows", ctypes.c_int32),
+        ("exact", ctypes.c_int32), ("gather_sorted", ctypes.c_int32), ("column_codes", ctypes.c_int32),
+        ("row_patterns", ctypes.c_int32),
         ("mult_layout_bytes", ctypes.c_int64),
     ]
 
@@ -250,7 +250,7 @@ class SeqAIJHIP:
 
     def set_option(self, option: str, value: int):
         """Speed-only STREAM knobs (include/aijhip.h AIJHIP_OPT_*): geometry,
-        nt_loads, exact, x_tile, long_xcd, host_pipeline, gather_sort,
+        nt_loads, exact, long_xcd, host_pipeline, gather_sort,
         column_codes, row_patterns. Results never depend on them."""
         code = OPTIONS.get(option, WITHDRAWN_OPTIONS.get(option))
         if code is None:

@@ -74,8 +74,6 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_longs);
     hipFree(P.d_partials);
     hipFree(P.d_segperm);
-    hipFree(P.d_wbnd);
-    hipFree(P.d_xwin);
     hipFree(P.d_saj);
     hipFree(P.d_saa);
     hipFree(P.d_sslot);
@@ -218,35 +216,9 @@ int plan_stream(aijhip_mat *A) {
     if (!blocks.empty() &&
         (e = hipMemcpy(P.d_blocks, blocks.data(), sizeof(BlockDesc) * blocks.size(), hipMemcpyHostToDevice)) != hipSuccess)
         return hipfail(e, "plan: upload blocks");
-    // x tiles (LDS-staged x, opt-in): where a block's columns span at most
-    // its LDS entries, x[lo, lo + span) is loaded coalesced and gathered
-    // from LDS (banded operators; never the 7-pt Poisson at scale, whose
-    // blocks span +-N^2 columns). Measured on the skewed stand-in: +3 % at
-    // geometry 6, -6 % at the default geometry 1, hence off by default.
-    P.n_xtiled = 0;
-    if (P.tune.xtile != 0 && !blocks.empty() && !A->compressed) {
-        std::vector<aijhip::XWin> xw(blocks.size());
-        aijhip::XWin *d_xw = nullptr;
-        if ((e = dmalloc(&d_xw, blocks.size(), &P.bytes)) != hipSuccess) return hipfail(e, "plan: alloc x windows");
-        if ((e = aijhip::block_x_windows(*A, P.d_blocks, P.n_blocks, G.nnz_cap, d_xw)) != hipSuccess ||
-            (e = hipMemcpy(xw.data(), d_xw, sizeof(aijhip::XWin) * xw.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
-            hipFree(d_xw);
-            return hipfail(e, "plan: x windows");
-        }
-        int32_t fit = 0;
-        for (const aijhip::XWin &w : xw) fit += w.n[0] >= 0;
-        if (P.tune.xtile == 1 || 2 * (int64_t)fit >= (int64_t)xw.size()) {
-            P.d_xwin = d_xw;
-            P.n_xtiled = fit;
-        } else {
-            hipFree(d_xw);
-            P.bytes -= (int64_t)sizeof(aijhip::XWin) * (int64_t)xw.size();
-        }
-    }
     // gather-ordered copy of the row blocks (Tuning::gsort): for the plain
-    // MatMult / MatMultAdd launch (not with the x tiles, which read the
-    // original order)
-    if (P.tune.gsort > 0 && !blocks.empty() && P.d_xwin == nullptr) {
+    // MatMult / MatMultAdd launch
+    if (P.tune.gsort > 0 && !blocks.empty()) {
         const size_t nzp = (size_t)A->nz + 2;
         if ((e = dmalloc(&P.d_saj, nzp, &P.bytes)) != hipSuccess || (e = dmalloc(&P.d_saa, nzp, &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_sslot, nzp, &P.bytes)) != hipSuccess ||
@@ -327,7 +299,7 @@ int plan_stream(aijhip_mat *A) {
     // geometry 6, plain full-row launches, no long rows
     const int32_t nrl = rai.empty() ? 0 : (int32_t)rai.size() - 1;
     if (P.tune.patterns > 0 && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed &&
-        A->nz <= (int64_t)kBatchMinMean * nrl && P.d_xwin == nullptr && P.d_sslot == nullptr) {
+        A->nz <= (int64_t)kBatchMinMean * nrl && P.d_sslot == nullptr) {
         bool ok = false;
         if ((e = aijhip::build_row_patterns(*A, P, &ok)) != hipSuccess) return hipfail(e, "plan: row patterns");
     }
@@ -336,7 +308,7 @@ int plan_stream(aijhip_mat *A) {
     // full-row launches: not with the x tiles or the gather order); when
     // some do not fit, they are launched from aj
     if (P.tune.codes > 0 && P.tune.geom == 6 && !blocks.empty() && P.d_pid == nullptr && !A->compressed &&
-        P.d_xwin == nullptr && P.d_sslot == nullptr) {
+        P.d_sslot == nullptr) {
         int32_t *d_cnt = nullptr;
         std::vector<int32_t> cnt(blocks.size());
         if ((e = dmalloc(&d_cnt, blocks.size(), nullptr)) != hipSuccess ||
@@ -396,13 +368,7 @@ int plan_stream(aijhip_mat *A) {
                 return hipfail(e, "plan: column codes");
         }
     }
-    bool windowed = false;
-    if (!longs.empty() && P.tune.long_window != 0) {
-        if ((e = aijhip::build_long_windows(*A, P, longs, P.tune.long_window > 0, &windowed)) != hipSuccess)
-            return hipfail(e, "plan: long-row windows");
-        if (windowed) P.n_segs = 0;
-    }
-    if (!longs.empty() && !windowed) {
+    if (!longs.empty()) {
         if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_partials, segs.size(), &P.bytes)) != hipSuccess)
@@ -496,7 +462,7 @@ int plan_build(aijhip_mat *A) {
             // short rows (a stencil: no per-entry column at all).
             const aijhip::Tuning &rq = A->requested_tune;
             if ((auto_codes || auto_patterns) && !A->compressed && rq.gsort <= 0 && (rq.geom < 0 || rq.geom == 6) &&
-                rq.xtile <= 0 && rq.nt <= 1) {
+                rq.nt <= 1) {
                 const aijhip::Tuning keep = P.tune;
                 if (auto_codes) P.tune.codes = 1;
                 if (auto_patterns) P.tune.patterns = 1;
@@ -884,6 +850,8 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_CLAMPED_LOADS:
         case AIJHIP_OPT_LONG_OVERLAP:
         case AIJHIP_OPT_ROW_GROUP:
+        case AIJHIP_OPT_X_TILE:
+        case AIJHIP_OPT_LONG_WINDOW:
             return fail(AIJHIP_ERR_ARG, "option " + std::to_string(option) +
                                             " was withdrawn in ABI 2 (measured slower; DESIGN.md §5)");
         case AIJHIP_OPT_NT_LOADS:
@@ -891,15 +859,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             t.nt = value;
             break;
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
-        case AIJHIP_OPT_X_TILE:
-            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "x_tile: -1 auto, 0 off, 1 on");
-            t.xtile = value;
-            break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
-        case AIJHIP_OPT_LONG_WINDOW:
-            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "long_window: -1 auto, 0 segments, 1 windows");
-            t.long_window = value;
-            break;
         case AIJHIP_OPT_HOST_PIPELINE:
             if (value < -1) return fail(AIJHIP_ERR_ARG, "host_pipeline: -1 auto, 0 serial, k > 0 chunk rows");
             t.host_chunk = value;
@@ -1097,18 +1057,14 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->mult_flops = 2.0 * (double)A->nz - (double)A->nonzerorowcnt;
     info->mult_bytes = 12 * A->nz + 4 * ((int64_t)A->m + 1) + 8 * (int64_t)A->n + 8 * (int64_t)A->m;
     info->stream_geometry = A->plan.tune.geom;
-    info->xcd_remap = 0;
     info->nt_loads = A->plan.tune.nt;
     info->stream_threads = aijhip::kStreamGeoms[A->plan.tune.geom].threads;
     info->stream_nnz_cap = aijhip::kStreamGeoms[A->plan.tune.geom].nnz_cap;
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
-    info->persistent = 0;
     info->exact = A->plan.tune.exact ? 1 : 0;
-    info->x_tiled_blocks = A->plan.n_xtiled;
     info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
     info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
     info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
-    info->long_windows = A->plan.d_wbnd != nullptr ? A->plan.n_win : 0;
     info->mult_layout_bytes = aijhip::mult_layout_bytes(*A);
     return AIJHIP_OK;
 }

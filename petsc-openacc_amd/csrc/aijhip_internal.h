@@ -54,28 +54,12 @@ constexpr int kMaxStreamNnzCap = 8192;
 // segments of at most kLongSegNnz entries, each summed by one workgroup.
 constexpr int kLongSegNnz = 4096;
 constexpr int kLongThreads = 256;
-// Windowed long rows (Tuning::long_window): x column windows of kWinCols
-// doubles staged in LDS, one workgroup per window; at most kWinMaxRows long
-// rows, their columns sorted.
-constexpr int kWinCols = 2048;
-constexpr int kWinMaxRows = 512;
 
 // One STREAM row block: rows [row0, row0+nrows) of the row list, entries
 // [k0, k0+nk) of aj/aa.
 struct BlockDesc {
     int32_t row0, nrows, k0, nk;
 };
-
-// LDS x tile of a row block (Tuning::xtile): up to kXWin column windows
-// [s[w], s[w] + n[w]) of x, ascending, staged one after another in the
-// block's LDS; n[0] < 0: the block gathers from global memory. A 7-point
-// stencil block has three (the planes below and above, its own plane +- N).
-constexpr int kXWin = 4;
-struct XWin {
-    int32_t s[kXWin], n[kXWin];
-};
-// Columns closer than this (in x entries) share a window.
-constexpr int kXWinGap = 64;
 
 // One segment of a long row: entries [k0, k0+nk), partial sum -> partials[seg].
 struct LongSeg {
@@ -101,18 +85,15 @@ struct RowList {
 // scattered long rows; plain loads except for those (non-temporal); hardware
 // round-robin block placement. The A/B-only variants measured slower
 // (XCD-contiguous placement, the persistent pipelined grid, clamped loads,
-// register row groups, a side stream for the long rows) were withdrawn in
-// ABI 2; profiles/r01-r03 keep their records.
+// register row groups, a side stream for the long rows, LDS x tiles, long
+// rows by x column window) were withdrawn in ABI 2; profiles/r01-r04 keep
+// their records.
 struct Tuning {
     int geom = -1;       // index into kStreamGeoms; -1 = by row length and gather locality (6 or 1)
     int nt = -1;         // matrix loads: -1 by gather locality (non-temporal for scattered long rows),
                          // 0 plain, 1 non-temporal
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
-    int xtile = 0;         // x staged in LDS per block (up to kXWin column windows): 0 off, 1 where
-                           // it fits, -1 when half the blocks fit
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
-    int long_window = -1;  // long rows by x column window (k_long_window) instead of segments: -1 auto
-                           // (sorted rows, >= 2048 long-row entries per window), 0 segments, 1 windows
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
@@ -177,15 +158,6 @@ struct Plan {
     // the s % 8-th eighth of x, so each XCD's L2 holds the x range its
     // scattered gathers hit (speed only; partials and their order unchanged)
     int32_t *d_segperm = nullptr;
-    // Tuning::long_window: per long row i and window w the first entry with
-    // column >= w kWinCols (n_win + 1 per row); then d_partials holds
-    // n_longs x n_win window sums and d_longs[i] = {orow, i n_win, n_win}
-    int32_t *d_wbnd = nullptr;
-    int32_t n_win = 0;
-    // x tiles: per block its column windows (XWin), or n[0] = -1 when they do
-    // not fit the block's LDS (gathers from global memory)
-    XWin *d_xwin = nullptr;
-    int32_t n_xtiled = 0;
     // Tuning::gsort: each row block's entries sorted by column (columns,
     // values) and their positions in the block (the products' LDS slots)
     int32_t *d_saj = nullptr;
@@ -288,17 +260,10 @@ hipError_t build_transpose(const aijhip_mat &A, int32_t **d_tai, int32_t **d_taj
                            double **d_taa, hipStream_t s);
 
 RowList row_list(const aijhip_mat &A);
-// Windowed long rows: *ok when every long row is sorted and (unless force)
-// the rows carry >= 2048 entries per window; fills P.d_wbnd / n_win,
-// P.d_longs and P.d_partials (the caller has not allocated them).
-hipError_t build_long_windows(const aijhip_mat &A, Plan &P, const std::vector<LongRow> &longs, bool force, bool *ok);
 // Per long-row segment: the column of its middle entry (synchronous).
 hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out);
 // Per STREAM block: min column and span (max - min + 1) of its entries.
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out);
-// Per STREAM block: its x column windows (k_block_xwindows), n[0] = -1 when
-// they are more than kXWin or span more than `cap` entries (synchronous).
-hipError_t block_x_windows(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int cap, XWin *d_out);
 // The gather-ordered copy of the plan's row blocks (Plan::d_saj/d_saa/
 // d_sslot, allocated by the caller); values_only: the values again, in the
 // order already built.

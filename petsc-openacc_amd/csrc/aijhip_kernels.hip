@@ -94,11 +94,10 @@ __device__ __forceinline__ void st_stream(double *p, double v) { __builtin_nonte
 // is formed in PETSc's order (or the deterministic multi-lane order); `seed`
 // starts it (MatMultAdd's z_i), `put` stores the row's result and adds to
 // the block's dot partials d[0..kDots).
-template <bool ADD, bool TILE = false>
+template <bool ADD>
 struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     static constexpr int kDots = 1;
     static constexpr bool kSeeded = ADD;
-    static constexpr bool kTile = TILE;  // x gathered from an LDS tile where the block fits
     const double *x, *z;
     double *y;
     bool dot;
@@ -117,7 +116,6 @@ template <bool NT>
 struct OpMgResid {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
-    static constexpr bool kTile = false;
     const double *x, *b;
     double *r;
     __device__ double gx(int32_t j) const { return x[j]; }
@@ -137,7 +135,6 @@ template <bool NT>
 struct OpMgPost {
     static constexpr int kDots = 2;
     static constexpr bool kSeeded = false;
-    static constexpr bool kTile = false;
     const double *t, *b, *dinv;
     double *x;
     bool dot;
@@ -159,7 +156,6 @@ struct OpMgPost {
 struct OpDinvMult {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
-    static constexpr bool kTile = false;
     const double *x, *dinv;
     double *y;
     __device__ double gx(int32_t j) const { return x[j]; }
@@ -197,8 +193,8 @@ template <int T, int CAP, int RPT, bool CROW, int NTMODE, class Op>
 __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const XWin *__restrict__ xwin,
-    const uint16_t *__restrict__ sslot, const int32_t *__restrict__ sbase) {
+    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const uint16_t *__restrict__ sslot,
+    const int32_t *__restrict__ sbase) {
     constexpr bool NT = (NTMODE & 1) != 0;
     // bit 3: gather-ordered blocks (Plan::d_saj/d_saa): aj/aa hold each
     // block's entries sorted by column, sslot their positions in the block,
@@ -215,7 +211,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     // start, size} and then the dictionaries. 10 bytes per entry instead of
     // 12; the products, their slots and the sums are the plain kernel's
     constexpr bool CODES = (NTMODE & 32) != 0;
-    static_assert(!(CODES && (S16 || SORTED || CROW || Op::kTile)), "column codes: plain full-row form only");
+    static_assert(!(CODES && (S16 || SORTED || CROW)), "column codes: plain full-row form only");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     __shared__ double prod[CAP];
@@ -321,52 +317,15 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
             if (k < k1) sv[it] = *reinterpret_cast<const uint32_t *>(sslot + k);
         }
     }
-    // x tile: the block's column windows (Plan::d_xwin) staged in LDS one
-    // after another (the products' space, free until the gathers are done)
-    // with coalesced loads; the gathers then read LDS instead of issuing
-    // scattered requests through L1/L2 (the plan decides per block).
-    XWin xw{};
-    if constexpr (Op::kTile) xw = xwin[b];
-    const bool tiled = Op::kTile && xw.n[0] >= 0;
-    int32_t wo[kXWin] = {};  // each window's first LDS slot
-    if constexpr (Op::kTile) {
-        if (tiled) {
-            int32_t o = 0;
-#pragma unroll
-            for (int w = 0; w < kXWin; ++w) {
-                wo[w] = o;
-                for (int32_t i = t; i < xw.n[w]; i += T) prod[o + i] = op.gx(xw.s[w] + i);
-                o += max(xw.n[w], 0);
-            }
-            __syncthreads();
-        }
-    }
-    // LDS slot of column c: the last window starting at or below it
-    auto tslot = [&](int32_t c) {
-        int32_t q = c - xw.s[0];
-#pragma unroll
-        for (int w = 1; w < kXWin; ++w)
-            if (xw.n[w] > 0 && c >= xw.s[w]) q = c - xw.s[w] + wo[w];
-        return q;
-    };
     if constexpr (!CODES) {  // (the coded form gathered with the decode above)
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
             if (k < k1) {
-                if (tiled) {
-                    // a pair's half outside the block (edge) reads slot 0, never stored
-                    xv[it].x = prod[k >= k0 ? tslot(cv[it].x) : 0];
-                    xv[it].y = prod[k + 1 < k1 ? tslot(cv[it].y) : 0];
-                } else {
-                    xv[it].x = op.gx(cv[it].x);
-                    xv[it].y = op.gx(cv[it].y);
-                }
+                xv[it].x = op.gx(cv[it].x);
+                xv[it].y = op.gx(cv[it].y);
             }
         }
-    }
-    if constexpr (Op::kTile) {
-        if (tiled) __syncthreads();  // every gather is done before the products overwrite the tile
     }
     // products into LDS; only the stores are predicated
 #pragma unroll
@@ -577,166 +536,6 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     }
 }
 
-// Windowed long rows (Plan::d_wbnd; Tuning::long_window): the hub rows of a
-// skewed operand scatter their gathers over all of x, one 128-B line per
-// entry, so the segment form above moves ~16x more L2 -> CU bytes for x than
-// for the matrix (the stand-in: 6.8 M hub entries, ~47 us against ~13 us of
-// their stream). Here workgroup w owns x's column window [w W, (w + 1) W),
-// loads it into LDS once with coalesced loads, and takes every long row's
-// entries whose columns fall in it (the rows' columns are sorted, so they are
-// one contiguous run per row: bnd[i (nw + 1) + w, + w + 1)). The runs are
-// walked as one flat list (prefix offsets in LDS), T * U entries per pass:
-// coalesced aa / aj loads, x from the LDS window, products to LDS, then per
-// row a wavefront sums the pass's slice (strided lanes + __shfl_down tree)
-// into acc[i] in pass order. partials[i nw + w] = the row's sum over the
-// window; k_long_finish adds them in window order. Deterministic (the lanes'
-// shares and the orders are fixed by the plan), reordered like the segments.
-template <int W, int T, int U>
-__global__ __launch_bounds__(T) void k_long_window(int32_t nl, int32_t nw, int32_t n, const int32_t *__restrict__ bnd,
-                                                   const int32_t *__restrict__ aj, const double *__restrict__ aa,
-                                                   const double *__restrict__ x, double *__restrict__ partials) {
-    __shared__ double xs[W];
-    __shared__ double prod[T * U];
-    __shared__ int32_t pre[kWinMaxRows + 1];
-    __shared__ int32_t kst[kWinMaxRows];
-    __shared__ double acc[kWinMaxRows];
-    __shared__ int32_t wtot[T / 64];
-    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    const int32_t w = (int32_t)blockIdx.x;
-    const int64_t c0 = (int64_t)w * W;
-    const int32_t cn = (int32_t)min<int64_t>(W, (int64_t)n - c0);
-    // the x window (16-B loads when x is 16-B aligned: W, c0 are even)
-    const bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
-    for (int32_t i = 2 * t; i < cn; i += 2 * T) {
-        if (i + 1 < cn && al) {
-            const f64x2 v = *reinterpret_cast<const f64x2 *>(x + c0 + i);
-            xs[i] = v.x;
-            xs[i + 1] = v.y;
-        } else if (i + 1 < cn) {
-            xs[i] = x[c0 + i];
-            xs[i + 1] = x[c0 + i + 1];
-        } else {
-            xs[i] = x[c0 + i];
-        }
-    }
-    // each row's run in this window; flat offsets by a block scan (rows
-    // T at a time, the running total carried in register `base`)
-    int32_t base = 0;
-    for (int32_t i0 = 0; i0 < nl; i0 += T) {
-        const int32_t i = i0 + t;
-        int32_t len = 0;
-        if (i < nl) {
-            const int32_t a = bnd[(int64_t)i * (nw + 1) + w], b = bnd[(int64_t)i * (nw + 1) + w + 1];
-            kst[i] = a;
-            len = b - a;
-            acc[i] = 0.0;
-        }
-        int32_t inc = len;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int32_t v = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += v;
-        }
-        if (lane == 63) wtot[wave] = inc;
-        __syncthreads();
-        int32_t off = base;
-        for (int q = 0; q < wave; ++q) off += wtot[q];
-        if (i < nl) pre[i] = off + inc - len;
-        for (int q = 0; q < T / 64; ++q) base += wtot[q];
-        __syncthreads();
-    }
-    if (t == 0) pre[nl] = base;
-    __syncthreads();
-    const int32_t E = base;
-    for (int32_t e0 = 0; e0 < E; e0 += T * U) {
-        double av[U];
-        int32_t cv[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t e = e0 + t + u * T;
-            if (e < E) {
-                int32_t lo = 0, hi = nl - 1;  // the row whose run holds flat entry e
-                while (lo < hi) {
-                    const int32_t mid = (lo + hi + 1) >> 1;
-                    if (pre[mid] <= e) lo = mid;
-                    else hi = mid - 1;
-                }
-                const int64_t k = (int64_t)kst[lo] + (e - pre[lo]);
-                av[u] = __builtin_nontemporal_load(aa + k);
-                cv[u] = __builtin_nontemporal_load(aj + k);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int32_t e = e0 + t + u * T;
-            if (e < E) prod[t + u * T] = av[u] * xs[cv[u] - c0];
-        }
-        __syncthreads();
-        // the rows whose runs meet [e0, e1): a wavefront each, in row order
-        const int32_t e1 = min(E, e0 + T * U);
-        int32_t r0 = 0, r1 = nl - 1;
-        {
-            int32_t lo = 0, hi = nl - 1;
-            while (lo < hi) {
-                const int32_t mid = (lo + hi + 1) >> 1;
-                if (pre[mid] <= e0) lo = mid;
-                else hi = mid - 1;
-            }
-            r0 = lo;
-            lo = 0, hi = nl - 1;
-            while (lo < hi) {
-                const int32_t mid = (lo + hi + 1) >> 1;
-                if (pre[mid] <= e1 - 1) lo = mid;
-                else hi = mid - 1;
-            }
-            r1 = lo;
-        }
-        for (int32_t i = r0 + wave; i <= r1; i += T / 64) {
-            const int32_t a = max(pre[i], e0) - e0, b = min(pre[i + 1], e1) - e0;
-            double s = 0.0;
-            for (int32_t j = a + lane; j < b; j += 64) s += prod[j];
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
-            if (lane == 0 && b > a) acc[i] += s;
-        }
-        __syncthreads();
-    }
-    for (int32_t i = t; i < nl; i += T) partials[(int64_t)i * nw + w] = acc[i];
-}
-
-// bnd[i (nw + 1) + w] = the first entry of long row rows[i] whose column is
-// >= w W (w = nw: the row's end); the row's columns must be sorted
-__global__ void k_window_bounds(int32_t nl, int32_t nw, int32_t W, const int32_t *__restrict__ rows,
-                                const int32_t *__restrict__ ai, const int32_t *__restrict__ aj, int32_t *bnd) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= (int64_t)nl * (nw + 1)) return;
-    const int32_t i = (int32_t)(g / (nw + 1)), w = (int32_t)(g - (int64_t)i * (nw + 1));
-    const int32_t r = rows[i];
-    int32_t lo = ai[r], hi = ai[r + 1];
-    if (w == nw) {
-        lo = hi;
-    } else {
-        const int64_t c = (int64_t)w * W;
-        while (lo < hi) {
-            const int32_t mid = lo + ((hi - lo) >> 1);
-            if ((int64_t)aj[mid] < c) lo = mid + 1;
-            else hi = mid;
-        }
-    }
-    bnd[g] = lo;
-}
-
-// long rows whose columns are not in ascending order (then: segments)
-__global__ void k_rows_unsorted(int32_t nl, const int32_t *__restrict__ rows, const int32_t *__restrict__ ai,
-                                const int32_t *__restrict__ aj, int *bad) {
-    const int32_t i = blockIdx.x;
-    if (i >= nl) return;
-    const int32_t r = rows[i];
-    int c = 0;
-    for (int32_t k = ai[r] + threadIdx.x; k + 1 < ai[r + 1]; k += blockDim.x) c += aj[k + 1] < aj[k];
-    if (c) atomicAdd(bad, c);
-}
-
 // One wavefront per long row: the lanes load 64 partials at once and the sum
 // runs through them in segment order by broadcast (a lane-per-row loop waited
 // on one dependent load per segment: 9 us for the stand-in's 119 hub rows).
@@ -887,69 +686,6 @@ __global__ __launch_bounds__(256) void k_block_xrange(const BlockDesc *__restric
     }
 }
 }  // namespace
-
-// x windows of a row block (Tuning::xtile): its columns sorted in LDS
-// (bitonic over the next power of two), split where two consecutive columns
-// are more than kXWinGap apart; up to kXWin windows whose lengths add up to
-// at most `cap` LDS entries, else n[0] = -1 (the block gathers from memory).
-template <int N>
-__global__ __launch_bounds__(256) void k_block_xwindows(const BlockDesc *__restrict__ blk,
-                                                        const int32_t *__restrict__ aj, int cap, XWin *out) {
-    __shared__ int32_t key[N];
-    __shared__ int32_t st[kXWin + 1];
-    __shared__ int32_t s_nc;
-    const BlockDesc d = blk[blockIdx.x];
-    const int t = threadIdx.x;
-    int n2 = 2;
-    while (n2 < d.nk) n2 <<= 1;
-    for (int i = t; i < n2; i += 256) key[i] = i < d.nk ? aj[(int64_t)d.k0 + i] : INT32_MAX;
-    __syncthreads();
-    for (int k = 2; k <= n2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < n2; i += 256) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const int32_t a = key[i], c = key[ixj];
-                    if ((a > c) == ((i & k) == 0)) {
-                        key[i] = c;
-                        key[ixj] = a;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    if (t < 64) {  // cluster starts, in order (wave 0)
-        int nc = 0;
-        for (int i0 = 0; i0 < d.nk; i0 += 64) {
-            const int i = i0 + t;
-            const bool f = i < d.nk && (i == 0 || (int64_t)key[i] - key[i - 1] > kXWinGap);
-            const unsigned long long msk = __ballot(f);
-            const int pos = nc + __popcll(msk & ((1ull << t) - 1ull));
-            if (f && pos <= kXWin) st[pos] = i;
-            nc += __popcll(msk);
-        }
-        if (t == 0) s_nc = nc;
-    }
-    __syncthreads();
-    if (t == 0) {
-        XWin w;
-        const int nc = s_nc;
-        int64_t tot = 0;
-        for (int q = 0; q < kXWin; ++q) {
-            if (q < nc && nc <= kXWin) {
-                const int a = st[q], e = q + 1 < nc ? st[q + 1] - 1 : d.nk - 1;
-                w.s[q] = key[a];
-                w.n[q] = key[e] - key[a] + 1;
-                tot += w.n[q];
-            } else {
-                w.s[q] = INT32_MAX;
-                w.n[q] = 0;
-            }
-        }
-        if (nc == 0 || nc > kXWin || tot > cap) w.n[0] = -1;
-        out[blockIdx.x] = w;
-    }
-}
 
 // Gather-ordered row blocks (Tuning::gsort): one workgroup sorts its
 // block's entries by column (ties by position; bitonic over the next power
@@ -1355,19 +1091,6 @@ hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_
     return launch_block_codes<true>(A, d_blk, nblk, nullptr, d_cmeta, d_code, kStreamGeoms[A.plan.tune.geom].nnz_cap);
 }
 
-hipError_t block_x_windows(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int cap, XWin *d_out) {
-    if (n_blocks <= 0) return hipSuccess;
-#define AIJHIP_XW(NN) \
-    hipLaunchKernelGGL(k_block_xwindows<NN>, dim3(n_blocks), dim3(256), 0, nullptr, d_blocks, A.d_aj, cap, d_out)
-    if (cap <= 1024) AIJHIP_XW(1024);
-    else if (cap <= 2048) AIJHIP_XW(2048);
-    else if (cap <= 4096) AIJHIP_XW(4096);
-    else AIJHIP_XW(8192);
-#undef AIJHIP_XW
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? hipDeviceSynchronize() : e;
-}
-
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out) {
     if (n_blocks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_block_xrange, dim3(n_blocks), dim3(256), 0, nullptr, d_blocks, A.d_aj, d_out);
@@ -1432,62 +1155,6 @@ __global__ __launch_bounds__(256) void k_seg_midcol(const LongSeg *__restrict__ 
     out[i] = s.nk > 0 ? aj[(int64_t)s.k0 + s.nk / 2] : 0;
 }
 
-hipError_t build_long_windows(const aijhip_mat &A, Plan &P, const std::vector<LongRow> &longs, bool force, bool *ok) {
-    *ok = false;
-    const int32_t nl = (int32_t)longs.size();
-    if (nl == 0 || nl > kWinMaxRows || A.compressed || A.n <= 0 || A.h_rai.empty()) return hipSuccess;
-    const int32_t nw = (int32_t)(((int64_t)A.n + kWinCols - 1) / kWinCols);
-    int64_t total = 0;
-    std::vector<int32_t> rows(nl);
-    for (int32_t i = 0; i < nl; ++i) {
-        rows[i] = longs[i].orow;
-        total += A.h_rai[rows[i] + 1] - A.h_rai[rows[i]];
-    }
-    // enough entries per window to pay for staging it (the skewed stand-in:
-    // ~8,800 per window; a few long rows over a wide x keep their segments)
-    if (!force && total < (int64_t)2048 * nw) return hipSuccess;
-    int32_t *d_rows = nullptr, *d_bnd = nullptr;
-    int *d_bad = nullptr, bad = 0;
-    hipError_t e;
-    auto done = [&](hipError_t r) {
-        hipFree(d_rows);
-        hipFree(d_bad);
-        if (!*ok) hipFree(d_bnd);
-        return r;
-    };
-    if ((e = hipMalloc(&d_rows, sizeof(int32_t) * nl)) != hipSuccess ||
-        (e = hipMalloc(&d_bad, sizeof(int))) != hipSuccess || (e = hipMemset(d_bad, 0, sizeof(int))) != hipSuccess ||
-        (e = hipMemcpy(d_rows, rows.data(), sizeof(int32_t) * nl, hipMemcpyHostToDevice)) != hipSuccess)
-        return done(e);
-    hipLaunchKernelGGL(k_rows_unsorted, dim3(nl), dim3(256), 0, nullptr, nl, d_rows, A.d_ai, A.d_aj, d_bad);
-    if ((e = hipGetLastError()) != hipSuccess || (e = hipMemcpy(&bad, d_bad, sizeof(int), hipMemcpyDeviceToHost)) !=
-                                                     hipSuccess)
-        return done(e);
-    if (bad) return done(hipSuccess);  // unsorted long rows: segments
-    const int64_t nb = (int64_t)nl * (nw + 1);
-    if ((e = hipMalloc(&d_bnd, sizeof(int32_t) * nb)) != hipSuccess) return done(e);
-    hipLaunchKernelGGL(k_window_bounds, dim3(grid_for(nb, 256)), dim3(256), 0, nullptr, nl, nw, kWinCols, d_rows,
-                       A.d_ai, A.d_aj, d_bnd);
-    std::vector<LongRow> lr(nl);
-    for (int32_t i = 0; i < nl; ++i) lr[i] = LongRow{longs[i].orow, i * nw, nw, 0};
-    if ((e = hipGetLastError()) != hipSuccess ||
-        (e = hipMalloc(&P.d_longs, sizeof(LongRow) * nl)) != hipSuccess ||
-        (e = hipMemcpy(P.d_longs, lr.data(), sizeof(LongRow) * nl, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMalloc(&P.d_partials, sizeof(double) * (size_t)nl * nw)) != hipSuccess ||
-        (e = hipDeviceSynchronize()) != hipSuccess) {
-        hipFree(P.d_longs);
-        hipFree(P.d_partials);
-        P.d_longs = nullptr;
-        P.d_partials = nullptr;
-        return done(e);
-    }
-    P.d_wbnd = d_bnd;
-    P.n_win = nw;
-    P.bytes += (int64_t)sizeof(int32_t) * nb + (int64_t)sizeof(LongRow) * nl + (int64_t)sizeof(double) * nl * nw;
-    *ok = true;
-    return done(hipSuccess);
-}
-
 hipError_t segment_mid_columns(const aijhip_mat &A, const LongSeg *d_segs, int32_t n_segs, int32_t *h_out) {
     if (n_segs <= 0) return hipSuccess;
     int32_t *d_out = nullptr;
@@ -1523,7 +1190,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
 #define AIJHIP_SL(ADD, CROW, NT)                                                                             \
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, NT, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
                        P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,             \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, nullptr);       \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr);       \
     return
     // Row patterns (Plan::d_pid; geometry 6, full-row lists, short rows)
     if constexpr (kGeom6) {
@@ -1549,11 +1216,11 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     if (nc > 0)                                                                                                   \
         hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, NTM, OpMult<ADD>>), dim3(nc), dim3(T), 0, s, cb, nc, \
                            (int)P.tune.exact, L.rai, nullptr, reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, \
-                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, P.d_cmeta);     \
+                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_cmeta);     \
     if (P.n_wblocks > 0)                                                                                          \
         hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, s, \
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,           \
-                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);                \
+                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);                \
     return
             if (add) {
                 if (P.tune.nt == 1) { AIJHIP_SC(true, 33); }
@@ -1575,11 +1242,11 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     if (nn > 0)                                                                                                \
         hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 16, OpMult<ADD>>), dim3(nn), dim3(T), 0, s, nb, nn, \
                            (int)P.tune.exact, L.rai, L.ridx, reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa, \
-                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, nullptr, P.d_sbase);  \
+                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sbase);  \
     if (P.n_wblocks > 0)                                                                                       \
         hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, s, \
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,         \
-                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr, nullptr);             \
+                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);             \
     return
         if (add && L.ridx) { AIJHIP_SS(true, true); }
         if (add) { AIJHIP_SS(true, false); }
@@ -1595,20 +1262,13 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
 #define AIJHIP_SS(ADD, CROW)                                                                                \
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 8, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
                        P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, L.ridx, P.d_saj, P.d_saa,          \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sslot, nullptr);   \
+                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, P.d_sslot, nullptr);   \
     return
         if (add && L.ridx) { AIJHIP_SS(true, true); }
         if (add) { AIJHIP_SS(true, false); }
         if (L.ridx) { AIJHIP_SS(false, true); }
         AIJHIP_SS(false, false);
 #undef AIJHIP_SS
-    }
-    // LDS x tiles: the plain full-row MatMult only
-    if (P.d_xwin && !add && !L.ridx && P.tune.nt != 1) {
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<false, true>>), dim3(P.n_blocks), dim3(T), 0,
-                           s, P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,
-                           OpMult<false, true>{x, z, y, dpart != nullptr}, dpart, stop, P.d_xwin, nullptr, nullptr);
-        return;
     }
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
     // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)
@@ -1656,7 +1316,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, 32, Op>), dim3(P.n_blocks),
                            dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,
-                           reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, op, dpart, stop, nullptr, nullptr,
+                           reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, op, dpart, stop, nullptr,
                            P.d_cmeta);
         return hipGetLastError();
     }
@@ -1665,7 +1325,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     case G:                                                                                                      \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_blocks),                      \
                            dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr, A.d_aj, \
-                           A.d_aa, op, dpart, stop, nullptr, nullptr, nullptr);                                  \
+                           A.d_aa, op, dpart, stop, nullptr, nullptr);                                  \
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
@@ -1687,8 +1347,8 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
     case G:                                                                                                      \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, OpMult<false>>), dim3(nb),                   \
                            dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks + b0, nb, (int)P.tune.exact, A.d_ai,  \
-                           nullptr, A.d_aj, A.d_aa, OpMult<false>{x, nullptr, y, false}, nullptr, nullptr,       \
-                           nullptr, nullptr, nullptr);                                                           \
+                           nullptr, A.d_aj, A.d_aa, OpMult<false>{x, nullptr, y, false}, nullptr, nullptr,      \
+                           nullptr, nullptr);                                                                    \
         break
     switch (P.tune.geom) {
         AIJHIP_BG(0); AIJHIP_BG(1); AIJHIP_BG(2); AIJHIP_BG(3); AIJHIP_BG(4);
@@ -1737,12 +1397,8 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     // long rows: segment partials, then their ordered sums (one stream: a
     // forked side stream measured neutral)
     if (P.n_longs > 0) {
-        if (P.d_wbnd)  // by x column window
-            hipLaunchKernelGGL((k_long_window<kWinCols, 512, 4>), dim3(P.n_win), dim3(512), 0, s, P.n_longs, P.n_win,
-                               A.n, P.d_wbnd, A.d_aj, A.d_aa, x, P.d_partials);
-        else
-            hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s, P.d_segs, A.d_aj, A.d_aa, x,
-                               P.d_partials, P.d_segperm);
+        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s, P.d_segs, A.d_aj, A.d_aa, x,
+                           P.d_partials, P.d_segperm);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
                                     P.d_partials, z, y);

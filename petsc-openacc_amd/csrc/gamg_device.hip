@@ -515,6 +515,10 @@ __global__ void k_narrow(int32_t n, const unsigned long long *__restrict__ w, in
 // alone — the same bits. Keys are claimed with an LDS compare-and-swap and
 // linear probing; values need no atomics. A_i's terms come in chunks of G
 // (one lane each: a_ik, k and B row k's extent) and are broadcast by shuffle.
+// Each lane loads its first entry of the next D steps' B rows together
+// before the first of them goes in (one load latency per D steps, not per
+// step: the coarse Galerkin rows take hundreds of steps of ~15-entry B rows);
+// the LDS order is unchanged.
 // Count mode: cnt[i] = distinct columns, or -1 when the table could pass T
 // (checked against an upper bound, recounted exactly only when it says so);
 // klass[i] = myclass when it fits. Write mode: the rows of myclass, their
@@ -527,10 +531,12 @@ __global__ __launch_bounds__(G *NG) void k_rowprod_hash(int32_t m, const int32_t
                                                         const int32_t *__restrict__ bj,
                                                         const double *__restrict__ ba, const int32_t *__restrict__ ci,
                                                         int32_t *cj, double *ca, int32_t *cnt, int32_t *klass,
-                                                        int32_t myclass, bool redo, bool pipe) {
+                                                        int32_t myclass, bool redo) {
     static_assert(G >= 1 && G <= 64 && 64 % G == 0, "a group lies within one wavefront");
     static_assert((T & (T - 1)) == 0 && T >= 2 * G, "power-of-two table, at least two slots per lane");
     constexpr int LOGT = __builtin_ctz(T);
+    constexpr int DM = WRITE ? 4 : 8;  // (write mode at 8: 82-98 VGPRs, 5 waves/SIMD; at 4: 58-76)
+    constexpr int D = G < DM ? G : DM;  // steps whose first entries are loaded together
     __shared__ int32_t s_key[NG * T];
     __shared__ double s_val[WRITE ? NG * T : 1];
     __shared__ int32_t s_ck[WRITE ? NG * T : 1];
@@ -579,43 +585,40 @@ __global__ __launch_bounds__(G *NG) void k_rowprod_hash(int32_t m, const int32_t
                 }
                 if (WRITE) val[h] += p;
             };
-            // B row k's first G entries are loaded one step ahead (software
-            // pipelined: the next row's load in flight while this one's
-            // products go into the table; the LDS order is unchanged)
-            int32_t nb0 = __shfl(q0, gbase, 64), nb1 = __shfl(q1, gbase, 64);
-            double nav = WRITE ? __shfl(a, gbase, 64) : 0.0;
-            int32_t nc = -1;
-            double nv = 0.0;
-            if (pipe && nb0 + l < nb1) {
-                nc = bj[nb0 + l];
-                if (WRITE) nv = ba[nb0 + l];
-            }
-            for (int t = 0; t < nk; ++t) {
-                const int32_t b0 = nb0, b1 = nb1, c0 = nc;
-                const double av = nav, v0 = nv;
-                if (t + 1 < nk) {
-                    nb0 = __shfl(q0, gbase + t + 1, 64);
-                    nb1 = __shfl(q1, gbase + t + 1, 64);
-                    if (WRITE) nav = __shfl(a, gbase + t + 1, 64);
-                    nc = -1;
-                    if (pipe && nb0 + l < nb1) {
-                        nc = bj[nb0 + l];
-                        if (WRITE) nv = ba[nb0 + l];
+            for (int t0 = 0; t0 < nk && !over; t0 += D) {
+                // steps t0 .. t0 + D - 1: extents, a_ik and this lane's first
+                // entry of each B row, all loads in flight together
+                int32_t pb0[D], pb1[D], pc[D];
+                double pa[D], pv[D];
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    const int src = gbase + (t0 + u < nk ? t0 + u : 0);
+                    pb0[u] = __shfl(q0, src, 64);
+                    pb1[u] = t0 + u < nk ? __shfl(q1, src, 64) : pb0[u];
+                    pa[u] = WRITE ? __shfl(a, src, 64) : 0.0;
+                    pc[u] = -1;
+                    pv[u] = 0.0;
+                    if (pb0[u] + l < pb1[u]) {
+                        pc[u] = bj[pb0[u] + l];
+                        if (WRITE) pv[u] = ba[pb0[u] + l];
                     }
                 }
-                const int len = b1 - b0;
-                if (bound + len > T - 1) {  // the table could fill: count exactly
-                    bound = group_sum(mine);
-                    if (bound + len > T - 1) {
-                        over = true;
-                        break;
+#pragma unroll
+                for (int u = 0; u < D; ++u) {
+                    if (t0 + u >= nk) break;  // group-uniform
+                    const int len = pb1[u] - pb0[u];
+                    if (bound + len > T - 1) {  // the table could fill: count exactly
+                        bound = group_sum(mine);
+                        if (bound + len > T - 1) {
+                            over = true;
+                            break;
+                        }
                     }
+                    bound += len;
+                    if (pc[u] >= 0) insert(pc[u], WRITE ? pa[u] * pv[u] : 0.0);
+                    for (int32_t q = pb0[u] + l + G; q < pb1[u]; q += G) insert(bj[q], WRITE ? pa[u] * ba[q] : 0.0);
+                    __builtin_amdgcn_wave_barrier();
                 }
-                bound += len;
-                // (pipelined: the first entry came with the previous step)
-                if (pipe && c0 >= 0) insert(c0, WRITE ? av * v0 : 0.0);
-                for (int32_t q = b0 + l + (pipe ? G : 0); q < b1; q += G) insert(bj[q], WRITE ? av * ba[q] : 0.0);
-                __builtin_amdgcn_wave_barrier();
             }
         }
         if (!WRITE) {
@@ -801,13 +804,12 @@ hipError_t rowprod_hash_pass(const DCsr &A, const DCsr &B, int32_t *cnt, int32_t
     constexpr int NG = hash_groups<G, T>();
     static_assert(NG * T * 16 <= 65536, "LDS per workgroup");
     const unsigned grid = (unsigned)std::min<int64_t>(blocks_for(A.m, NG), (int64_t)n_cu * 32);
-    constexpr bool pipe = true;  // the next B row's first entries loaded while the current one's go in (-10 %)
     if (!numeric)
         hipLaunchKernelGGL((k_rowprod_hash<G, T, NG, false>), dim3(grid), dim3(G * NG), 0, nullptr, A.m, A.ai, A.aj,
-                           A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, klass, myclass, redo, pipe);
+                           A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, klass, myclass, redo);
     else
         hipLaunchKernelGGL((k_rowprod_hash<G, T, NG, true>), dim3(grid), dim3(G * NG), 0, nullptr, A.m, A.ai, A.aj,
-                           A.aa, B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, klass, myclass, false, pipe);
+                           A.aa, B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, klass, myclass, false);
     return hipGetLastError();
 }
 

@@ -75,19 +75,17 @@ def test_full_size_shape(standin):
         assert len(ai) - 1 == 81 * 80 * 80 * 3 and lens.max() == 81
 
 
-@pytest.mark.parametrize("mode", ["stream_exact", "stream_default", "stream_segments"])
+@pytest.mark.parametrize("mode", ["stream_exact", "stream_default", "stream_csr"])
 def test_full_size_parity(pkg, standin, mode):
     name, ai, aj, aa, x, ref, absax = standin
     lens = np.diff(ai)
-    if mode == "stream_segments":  # long rows as 4096-entry segments instead of x windows
-        y, info = _run(pkg, ai, aj, aa, x, "stream", long_window=0)
-        assert info["long_windows"] == 0
+    if mode == "stream_csr":  # PETSc's aj as stored: no gather order, no column codes
+        y, info = _run(pkg, ai, aj, aa, x, "stream", gather_sort=0, column_codes=0, row_patterns=0)
+        assert info["gather_sorted"] == 0 and info["column_codes"] == 0
     else:
         y, info = _run(pkg, ai, aj, aa, x, "stream", exact=1 if mode == "stream_exact" else 0)
-        if info["n_long_rows"]:  # the skewed stand-in's hub rows: by x window (automatic)
-            assert info["long_windows"] > 0
     print(f"\n{name} {mode}: rows {len(lens)} nnz {len(aj)} geometry {info['stream_geometry']} "
-          f"long rows {info['n_long_rows']} windows {info['long_windows']}")
+          f"long rows {info['n_long_rows']} gather order {info['gather_sorted']} codes {info['column_codes']}")
     _bound_check(y, ref, lens, absax)
     cap = info["stream_nnz_cap"]
     if mode == "stream_exact":

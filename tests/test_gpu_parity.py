@@ -116,11 +116,11 @@ def test_stream_multilane_long_rows(pkg, dev, row_len):
 
 
 @pytest.mark.parametrize("geometry", [1, 6, 0, 9, 10])
-def test_stream_x_tile_banded(pkg, dev, geometry):
-    """x staged in LDS (x_tile=1) for blocks of a banded matrix: bit-exact,
-    and the blocks that do not fit (a row every 997 reaching five more
-    places of x: more windows than a block stages) fall back to gathers
-    from memory in the same launch."""
+def test_stream_banded_geometries(pkg, dev, geometry):
+    """A banded matrix of 10-40 entries per row (a row every 997 reaching
+    five far places of x) at every block geometry, PETSc's order: bit-exact.
+    (Geometries 9 and 10 were cut for the withdrawn LDS x tiles; they stay
+    selectable, speed-only.)"""
     rng = np.random.default_rng(11)
     m = 20000
     lens = rng.integers(10, 40, m)
@@ -135,27 +135,23 @@ def test_stream_x_tile_banded(pkg, dev, geometry):
     aj = np.concatenate(cols).astype(np.int32)
     aa = rng.uniform(-1, 1, len(aj))
     x = rng.uniform(-1, 1, m)
-    y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=1, x_tile=1, geometry=geometry)
-    assert 0 < info["x_tiled_blocks"] < info["n_blocks"]
+    y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=1, geometry=geometry, gather_sort=0)
+    assert info["stream_geometry"] == geometry
     assert_bits(y, seqaij.matmult(ai, aj, aa, x))
 
 
 @pytest.mark.parametrize("grid", [(16, 16, 16), (40, 40, 40), (300, 7, 5), (3, 200, 60)])
-def test_stream_x_windows_poisson(pkg, dev, coracle, grid):
-    """The 7-point operand's row blocks gather x from LDS windows (x_tile=1,
-    the CSR kernel reading aj): each block stages the planes below and above
-    and its own plane +- N (<= 4 windows); the result is PETSc's loop bit for
-    bit, and so is the plain gather."""
+def test_stream_csr_poisson(pkg, dev, coracle, grid):
+    """The CSR kernel (aj read, as the bench's headline) on boxes and thin
+    grids of the 7-point operand: PETSc's loop bit for bit."""
     ai, aj, aa = pkg.poisson_csr(*grid)
     m = len(ai) - 1
     x = pkg.splitmix_uniform(m, 17)
     ref = coracle.matmult(ai, aj, aa, x, omp=True)
-    y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", x_tile=1, row_patterns=0, column_codes=0)
-    assert info["x_tiled_blocks"] > 0 and info["row_patterns"] == 0 and info["column_codes"] == 0
+    y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", row_patterns=0, column_codes=0)
+    assert info["row_patterns"] == 0 and info["column_codes"] == 0 and info["gather_sorted"] == 0
+    assert info["mult_layout_bytes"] == info["mult_bytes"]
     assert_bits(y, ref)
-    y0, info0 = mult(pkg, dev, ai, aj, aa, m, x, "stream", x_tile=0, row_patterns=0, column_codes=0)
-    assert info0["x_tiled_blocks"] == 0
-    assert_bits(y0, ref)
 
 
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
@@ -442,22 +438,20 @@ def test_long_row_xcd_placement_is_speed_only(pkg, dev, coracle):
         assert_bits(yd.cpu().numpy(), wd.cpu().numpy())
 
 
-@pytest.mark.parametrize("force", [-1, 1])
-def test_long_rows_by_x_window(pkg, dev, coracle, force):
-    """Long rows summed by x column window (AIJHIP_OPT_LONG_WINDOW; automatic
-    on the skewed stand-in, whose hub rows are column-sorted): MatMult and
-    MatMultAdd within the fp64 bound, the same bits launch after launch, the
-    short rows bit-exact, and the same values as the segment form to the
-    bound; an MPIAIJ-style unaligned x (offset by one entry) too."""
+def test_long_row_segments_skewed(pkg, dev, coracle):
+    """Hub rows of the skewed stand-in as 4096-entry segments summed in
+    segment order: MatMult and MatMultAdd within the fp64 bound, the same bits
+    launch after launch, the short rows bit-exact; an MPIAIJ-style unaligned
+    x (offset by one entry) gives the same bits."""
     ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
     m = len(ai) - 1
     x = pkg.splitmix_uniform(m + 1, 7)
     z = pkg.splitmix_uniform(m, 8)
     ref = coracle.matmult(ai, aj, aa, x[:m], omp=True)
     short = np.diff(ai) <= 2048
-    with pkg.SeqAIJHIP(ai, aj, aa, exact=1, long_window=force) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, exact=1) as A:
         info = A.info()
-        assert info["n_long_rows"] > 0 and info["long_windows"] == (m + 2047) // 2048
+        assert info["n_long_rows"] > 0
         xd = to_dev(x, dev)
         zd = to_dev(z, dev)
         y1 = torch.full((m,), np.nan, dtype=torch.float64, device=dev)
@@ -478,16 +472,11 @@ def test_long_rows_by_x_window(pkg, dev, coracle, force):
         A.mult(xo[1:m + 1], y2)
         torch.cuda.synchronize()
         assert torch.equal(y1, y2)
-        A.set_option("long_window", 0)
-        assert A.info()["long_windows"] == 0
-        A.mult(xd, y2)
-        torch.cuda.synchronize()
-        check(y2.cpu().numpy(), ref, ai, aj, aa, x[:m], exact=False)
 
 
-def test_long_window_needs_sorted_rows(pkg, dev, coracle):
-    """A long row whose columns are not ascending keeps the segment form even
-    when windows are asked for (its window runs would not be contiguous)."""
+def test_long_rows_unsorted_columns(pkg, dev, coracle):
+    """Long rows whose columns are not ascending (one descending): the
+    segments take them in storage order, within the fp64 bound."""
     rng = np.random.default_rng(3)
     m = 50000
     lens = np.full(m, 5)
@@ -498,19 +487,11 @@ def test_long_window_needs_sorted_rows(pkg, dev, coracle):
     aj = np.concatenate(rows).astype(np.int32)
     aa = rng.uniform(-1, 1, ai[-1])
     x = rng.uniform(-1, 1, m)
-    with pkg.SeqAIJHIP(ai, aj, aa, long_window=1) as A:
-        assert A.info()["n_long_rows"] == 2 and A.info()["long_windows"] == 0
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        assert A.info()["n_long_rows"] == 2
         xd = to_dev(x, dev)
         yd = torch.empty(m, dtype=torch.float64, device=dev)
         A.mult(xd, yd)
-        torch.cuda.synchronize()
-        check(yd.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True), ai, aj, aa, x, exact=False)
-    rows[20000] = rows[20000][::-1].copy()
-    aj = np.concatenate(rows).astype(np.int32)
-    with pkg.SeqAIJHIP(ai, aj, aa, long_window=1) as A:
-        assert A.info()["long_windows"] == (m + 2047) // 2048  # forced: sorted now
-        yd = torch.empty(m, dtype=torch.float64, device=dev)
-        A.mult(to_dev(x, dev), yd)
         torch.cuda.synchronize()
         check(yd.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True), ai, aj, aa, x, exact=False)
 

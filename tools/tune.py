@@ -98,26 +98,13 @@ def main():
     if args.variants == "default":  # the product's defaults only
         variants.append(("stream", {}))
     if args.variants == "rowsum":  # default plus the small geometries (medium-length rows)
-        variants += [("stream", {})] + [("stream", dict(geometry=g, x_tile=xt)) for g in (0, 1, 6, 8) for xt in (0, -1)]
-    if args.variants == "xtile":
-        for g, xt in itertools.product((1, 6), (0, 1)):
-            variants.append(("stream", dict(geometry=g, x_tile=xt)))
-    if args.variants == "xwin":  # the CSR kernel (aj read) gathering x from LDS column windows vs from memory
-        for xt in (0, 1, 0, 1):
-            variants.append(("stream", dict(geometry=6, x_tile=xt, nt_loads=0, row_patterns=0, column_codes=0,
-                                            gather_sort=0)))
+        variants += [("stream", {})] + [("stream", dict(geometry=g)) for g in (0, 1, 6, 8)]
     if args.variants == "ntlong":  # non-temporal matrix loads for long-row operands, both automatic geometries
         for g, nt in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
     if args.variants == "ntgeom":  # non-temporal matrix loads x load depth (tools/read_sweep.hip: nt reads 6.8 TB/s)
         for g, nt in itertools.product((6, 11, 8, 0), (0, 1)):
             variants.append(("stream", dict(geometry=g, nt_loads=nt)))
-    if args.variants == "xtile_band":  # LDS x tiles of a +-2100-column band (geometries 9/10 fit it)
-        for g, xt in ((1, 0), (6, 0), (9, 0), (9, 1), (10, 0), (10, 1)):
-            variants.append(("stream", dict(geometry=g, x_tile=xt)))
-    if args.variants == "xtile_big":  # larger blocks amortise the tile load over more entries
-        for g, xt in ((1, 0), (7, 0), (7, 1), (4, 0), (4, 1), (6, 1)):
-            variants.append(("stream", dict(geometry=g, x_tile=xt)))
     if args.variants == "longxcd":
         for g, lx in itertools.product((1, 6), (0, 1)):
             variants.append(("stream", dict(geometry=g, long_xcd=lx)))
@@ -139,9 +126,6 @@ def main():
     if args.variants == "patnt":  # row patterns: plain vs non-temporal aa loads
         for nt in (0, 1, 0, 1):
             variants.append(("stream", dict(row_patterns=1, nt_loads=nt)))
-    if args.variants == "longwin":  # hub rows by x column window vs 4096-entry segments
-        for lw in (1, 0, 1, 0):
-            variants.append(("stream", dict(long_window=lw)))
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: XCD placement on / off
         for lx in (1, 0):
             variants.append(("stream", dict(long_xcd=lx)))
@@ -165,9 +149,7 @@ def main():
         A.set_kernel(kind, opts.get("lanes", 0))
         A.set_option("geometry", opts.get("geometry", -1))  # -1: the library's choice
         A.set_option("exact", opts.get("exact", 0))
-        A.set_option("x_tile", opts.get("x_tile", -1 if opts else 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
-        A.set_option("long_window", opts.get("long_window", -1))
         A.set_option("gather_sort", opts.get("gather_sort", -1))
         A.set_option("column_codes", opts.get("column_codes", -1))
         A.set_option("row_patterns", opts.get("row_patterns", -1))
@@ -201,7 +183,7 @@ def main():
                 maxdiff = float(np.max(np.abs(yy - ref_y)))
                 inf = A.info()
                 print(json.dumps({"variant": key, "bitwise_equal_first": same, "max_abs_diff": maxdiff,
-                                  "geometry": inf["stream_geometry"], "x_tiled_blocks": inf["x_tiled_blocks"],
+                                  "geometry": inf["stream_geometry"],
                                   "n_blocks": inf["n_blocks"]}), flush=True)
         for name, (fn, nb) in refs.items():
             time_launches(fn, 2, stream)
