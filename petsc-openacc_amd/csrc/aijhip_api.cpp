@@ -85,6 +85,9 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_cmeta);
     hipFree(P.d_pid);
     hipFree(P.d_ptab);
+    if (P.side) hipStreamDestroy(P.side);
+    if (P.ev_fork) hipEventDestroy(P.ev_fork);
+    if (P.ev_join) hipEventDestroy(P.ev_join);
     aijhip::host_pipe_free(P.hpipe);
     P = aijhip::Plan();
 }
@@ -402,6 +405,14 @@ int plan_stream(aijhip_mat *A) {
                     hipSuccess)
                 return hipfail(e, "plan: segment placement");
         }
+    }
+    // Tuning::overlap: a side stream and its two events for the wide blocks
+    // and the long rows (created once per plan that has them)
+    if (P.tune.overlap > 0 && (P.n_wblocks > 0 || P.n_longs > 0)) {
+        if ((e = hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming)) != hipSuccess)
+            return hipfail(e, "plan: side stream");
     }
     return AIJHIP_OK;
 }
@@ -848,7 +859,6 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_XCD_REMAP:
         case AIJHIP_OPT_PERSISTENT:
         case AIJHIP_OPT_CLAMPED_LOADS:
-        case AIJHIP_OPT_LONG_OVERLAP:
         case AIJHIP_OPT_ROW_GROUP:
         case AIJHIP_OPT_X_TILE:
         case AIJHIP_OPT_LONG_WINDOW:
@@ -860,6 +870,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             break;
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
+        case AIJHIP_OPT_LONG_OVERLAP:
+            if (value < 0 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: 0 off, 1 on");
+            t.overlap = value;
+            break;
         case AIJHIP_OPT_HOST_PIPELINE:
             if (value < -1) return fail(AIJHIP_ERR_ARG, "host_pipeline: -1 auto, 0 serial, k > 0 chunk rows");
             t.host_chunk = value;

@@ -94,6 +94,8 @@ struct Tuning {
                          // 0 plain, 1 non-temporal
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
+    int overlap = 0;       // MatMult / MatMultAdd with wide blocks or long rows: those launches on a
+                           // side stream concurrent with the row blocks (1), or after them (0)
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
@@ -158,6 +160,10 @@ struct Plan {
     // the s % 8-th eighth of x, so each XCD's L2 holds the x range its
     // scattered gathers hit (speed only; partials and their order unchanged)
     int32_t *d_segperm = nullptr;
+    // Tuning::overlap: the side stream the wide blocks and the long rows'
+    // segments run on, forked from / joined to the caller's by two events
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     // Tuning::gsort: each row block's entries sorted by column (columns,
     // values) and their positions in the block (the products' LDS slots)
     int32_t *d_saj = nullptr;

@@ -1185,7 +1185,7 @@ static hipError_t compressed_prologue(const aijhip_mat &A, const double *z, doub
 template <int T, int CAP, int RPT>
 static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L, const double *x,
                             const double *z, double *y, bool add, hipStream_t s, double *dpart,
-                            const int *stop) {
+                            const int *stop, hipStream_t sw) {  // sw: the wide blocks' stream
     constexpr bool kGeom6 = T == kStreamGeoms[6].threads && CAP == kStreamGeoms[6].nnz_cap && RPT == 1;
 #define AIJHIP_SL(ADD, CROW, NT)                                                                             \
     hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, NT, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
@@ -1218,7 +1218,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            (int)P.tune.exact, L.rai, nullptr, reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, \
                            OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_cmeta);     \
     if (P.n_wblocks > 0)                                                                                          \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, s, \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, sw, \
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,           \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);                \
     return
@@ -1244,7 +1244,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            (int)P.tune.exact, L.rai, L.ridx, reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa, \
                            OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sbase);  \
     if (P.n_wblocks > 0)                                                                                       \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, s, \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, sw, \
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,         \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);             \
     return
@@ -1381,11 +1381,34 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     if (e != hipSuccess) return e;
     const RowList L = row_list(A);
     const Plan &P = A.plan;
+    // Tuning::overlap: the long rows' segments and the wide blocks (the
+    // latency-bound launches) on the side stream, forked from s before any of
+    // them and joined back after; the row blocks on s meanwhile. Every launch
+    // writes its own rows of y, so the order between them is free.
+    const bool ovl = P.tune.overlap > 0 && P.side && !L.ridx && !dpart && !stop &&
+                     (P.n_wblocks > 0 || P.n_longs > 0);
+    hipStream_t sw = s;
+    if (ovl) {
+        if ((e = hipEventRecord(P.ev_fork, s)) != hipSuccess || (e = hipStreamWaitEvent(P.side, P.ev_fork, 0)) !=
+                                                                      hipSuccess)
+            return e;
+        sw = P.side;
+    }
+    // long rows: segment partials, then their ordered sums
+    if (P.n_longs > 0) {
+        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, sw, P.d_segs, A.d_aj, A.d_aa, x,
+                           P.d_partials, P.d_segperm);
+        if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, sw, P.d_longs, P.n_longs,
+                                    P.d_partials, z, y);
+        else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, sw, P.d_longs, P.n_longs,
+                                P.d_partials, z, y);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     // Every geometry is dispatched explicitly: the kernel's LDS size must be
     // the one the plan's row blocks were cut for.
     static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
     if (P.n_blocks > 0) {
-#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, P, L, x, z, y, add, s, dpart, stop); break
+#define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, P, L, x, z, y, add, s, dpart, stop, sw); break
         switch (P.tune.geom) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
             AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
@@ -1394,18 +1417,9 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
 #undef AIJHIP_SG
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    // long rows: segment partials, then their ordered sums (one stream: a
-    // forked side stream measured neutral)
-    if (P.n_longs > 0) {
-        hipLaunchKernelGGL(k_long_partial, dim3(P.n_segs), dim3(kLongThreads), 0, s, P.d_segs, A.d_aj, A.d_aa, x,
-                           P.d_partials, P.d_segperm);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
-                                    P.d_partials, z, y);
-        else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
-                                P.d_partials, z, y);
-        return hipGetLastError();
-    }
+    if (ovl && ((e = hipEventRecord(P.ev_join, P.side)) != hipSuccess || (e = hipStreamWaitEvent(s, P.ev_join, 0)) !=
+                                                                            hipSuccess))
+        return e;
     return hipSuccess;
 }
 

@@ -474,6 +474,30 @@ def test_long_row_segments_skewed(pkg, dev, coracle):
         assert torch.equal(y1, y2)
 
 
+@pytest.mark.parametrize("gather_sort", [-1, 0])
+def test_long_overlap_is_speed_only(pkg, dev, gather_sort):
+    """AIJHIP_OPT_LONG_OVERLAP: the hub segments and the wide blocks on a
+    side stream, concurrent with the row blocks: the same launches, so the
+    same bits as one stream, for MatMult and MatMultAdd, back to back."""
+    ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
+    m = len(ai) - 1
+    x = to_dev(pkg.splitmix_uniform(m, 7), dev)
+    z = to_dev(pkg.splitmix_uniform(m, 8), dev)
+    out = []
+    for ov in (0, 1):
+        with pkg.SeqAIJHIP(ai, aj, aa, gather_sort=gather_sort, long_overlap=ov) as A:
+            assert A.info()["n_long_rows"] > 0
+            y = torch.empty(m, dtype=torch.float64, device=dev)
+            w = torch.empty_like(y)
+            for _ in range(3):
+                A.mult(x, y)
+                A.mult_add(x, z, w)
+            torch.cuda.synchronize()
+            out.append((y.cpu().numpy(), w.cpu().numpy()))
+    assert_bits(out[0][0], out[1][0])
+    assert_bits(out[0][1], out[1][1])
+
+
 def test_long_rows_unsorted_columns(pkg, dev, coracle):
     """Long rows whose columns are not ascending (one descending): the
     segments take them in storage order, within the fp64 bound."""

@@ -126,6 +126,9 @@ def main():
     if args.variants == "patnt":  # row patterns: plain vs non-temporal aa loads
         for nt in (0, 1, 0, 1):
             variants.append(("stream", dict(row_patterns=1, nt_loads=nt)))
+    if args.variants == "overlap":  # hub segments + wide blocks on a side stream, concurrent with the row blocks
+        for ov in (0, 1, 0, 1):
+            variants.append(("stream", dict(long_overlap=ov)))
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: XCD placement on / off
         for lx in (1, 0):
             variants.append(("stream", dict(long_xcd=lx)))
@@ -150,6 +153,7 @@ def main():
         A.set_option("geometry", opts.get("geometry", -1))  # -1: the library's choice
         A.set_option("exact", opts.get("exact", 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
+        A.set_option("long_overlap", opts.get("long_overlap", 0))
         A.set_option("gather_sort", opts.get("gather_sort", -1))
         A.set_option("column_codes", opts.get("column_codes", -1))
         A.set_option("row_patterns", opts.get("row_patterns", -1))
