@@ -519,8 +519,9 @@ __global__ void k_narrow(int32_t n, const unsigned long long *__restrict__ w, in
 // before the first of them goes in (one load latency per D steps, not per
 // step: the coarse Galerkin rows take hundreds of steps of ~15-entry B rows);
 // the LDS order is unchanged.
-// Count mode: cnt[i] = distinct columns, or -1 when the table could pass T
-// (checked against an upper bound, recounted exactly only when it says so);
+// Count mode: cnt[i] = distinct columns, or -1 when they could pass keys_max
+// (< T; checked against an upper bound, recounted exactly only when it says
+// so);
 // klass[i] = myclass when it fits. Write mode: the rows of myclass, their
 // keys compacted and ranked (sorted columns) and written with the sums.
 template <int G, int T, int NG, bool WRITE>
@@ -531,7 +532,7 @@ __global__ __launch_bounds__(G *NG) void k_rowprod_hash(int32_t m, const int32_t
                                                         const int32_t *__restrict__ bj,
                                                         const double *__restrict__ ba, const int32_t *__restrict__ ci,
                                                         int32_t *cj, double *ca, int32_t *cnt, int32_t *klass,
-                                                        int32_t myclass, bool redo) {
+                                                        int32_t myclass, bool redo, int keys_max) {
     static_assert(G >= 1 && G <= 64 && 64 % G == 0, "a group lies within one wavefront");
     static_assert((T & (T - 1)) == 0 && T >= 2 * G, "power-of-two table, at least two slots per lane");
     constexpr int LOGT = __builtin_ctz(T);
@@ -607,9 +608,9 @@ __global__ __launch_bounds__(G *NG) void k_rowprod_hash(int32_t m, const int32_t
                 for (int u = 0; u < D; ++u) {
                     if (t0 + u >= nk) break;  // group-uniform
                     const int len = pb1[u] - pb0[u];
-                    if (bound + len > T - 1) {  // the table could fill: count exactly
+                    if (bound + len > keys_max) {  // the table could fill: count exactly
                         bound = group_sum(mine);
-                        if (bound + len > T - 1) {
+                        if (bound + len > keys_max) {
                             over = true;
                             break;
                         }
@@ -801,15 +802,20 @@ constexpr int hash_groups() {
 template <int G, int T>
 hipError_t rowprod_hash_pass(const DCsr &A, const DCsr &B, int32_t *cnt, int32_t *klass, int32_t myclass, bool redo,
                              const int32_t *ci, DCsr *C, bool numeric, int n_cu) {
+    // A product of few rows (a coarse level's: 744 at 300^3) leaves most CUs
+    // idle, and each group's time is its probes: at most half-full tables
+    // there (linear probing at load ~0.9 walks several slots per insert);
+    // many rows keep the fuller tables and their occupancy.
+    const int keys_max = A.m < 64 * n_cu ? T / 2 : T - 1;
     constexpr int NG = hash_groups<G, T>();
     static_assert(NG * T * 16 <= 65536, "LDS per workgroup");
     const unsigned grid = (unsigned)std::min<int64_t>(blocks_for(A.m, NG), (int64_t)n_cu * 32);
     if (!numeric)
         hipLaunchKernelGGL((k_rowprod_hash<G, T, NG, false>), dim3(grid), dim3(G * NG), 0, nullptr, A.m, A.ai, A.aj,
-                           A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, klass, myclass, redo);
+                           A.aa, B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt, klass, myclass, redo, keys_max);
     else
         hipLaunchKernelGGL((k_rowprod_hash<G, T, NG, true>), dim3(grid), dim3(G * NG), 0, nullptr, A.m, A.ai, A.aj,
-                           A.aa, B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, klass, myclass, false);
+                           A.aa, B.ai, B.aj, B.aa, ci, C->aj, C->aa, cnt, klass, myclass, false, keys_max);
     return hipGetLastError();
 }
 
@@ -937,10 +943,12 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
         };
         if ((e = dalloc(&klass, A.m)) != hipSuccess) return bail(e, "product classes");
         // the first table: the smallest above the mean products per row
-        // (their bound on the distinct columns), at most 64 slots; rows that
-        // overflow it are recounted with the next
+        // (their bound on the distinct columns; twice that for few rows),
+        // at most 64 slots (128); rows that overflow it are recounted with
+        // the next. The table size never changes the sums (traversal order)
         int first = 0;
-        while (first + 1 < kHashClasses && kHashT[first] <= std::min(per_row, 48.0)) ++first;
+        const int fill = A.m < 64 * n_cu ? 2 : 1;  // few rows: half-full tables (rowprod_hash_pass)
+        while (first + 1 < kHashClasses && kHashT[first] <= fill * std::min(per_row, 48.0)) ++first;
         int last = -1;
         for (int t = first; t < kHashClasses; ++t) {
             if ((e = rowprod_hash_class(t, hash_lanes(G, t), A, B, cnt, klass, t > first, nullptr, nullptr, false,

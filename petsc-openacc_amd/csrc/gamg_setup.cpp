@@ -382,17 +382,21 @@ namespace aijhip_gamg {
 int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const int32_t *sj, int32_t *agg,
                               int32_t na, int64_t sj0) {
     // The pass is a chain of dependent loads (row start, first column, its
-    // id): the ids of row i + 16's first two columns and row i + 32's columns
-    // are prefetched (300^3 level 1 on the build host: 75 -> 59 ms).
-    constexpr int32_t kAhead = 16;
+    // id): the ids of row i + 32's first two columns and row i + 64's columns
+    // are prefetched (300^3 level 1 on the build host: 75 -> 59 ms) — only
+    // for nodes still free now (an aggregated node stays aggregated and its
+    // row is never read; most are, so S is no longer streamed whole: a
+    // 148^3 27-point S on the build host 26.5 -> 16.1 ms, same aggregates).
+    constexpr int32_t kAhead = 32;
     for (int32_t i = r0; i < r1; ++i) {
         if (i + 2 * kAhead < r1) {
-            const int32_t *row = sj + (si[i + kAhead] - sj0);
-            if (si[i + kAhead + 1] - si[i + kAhead] >= 2) {
+            const int32_t ia = i + kAhead, ib = i + 2 * kAhead;
+            if (agg[ia] == -1 && si[ia + 1] - si[ia] >= 2) {
+                const int32_t *row = sj + (si[ia] - sj0);
                 __builtin_prefetch(&agg[row[0]], 0, 3);
                 __builtin_prefetch(&agg[row[1]], 0, 3);
             }
-            __builtin_prefetch(sj + (si[i + 2 * kAhead] - sj0), 0, 3);
+            if (agg[ib] == -1) __builtin_prefetch(sj + (si[ib] - sj0), 0, 3);
         }
         if (agg[i] != -1 || si[i] == si[i + 1]) continue;
         const int32_t *row = sj + (si[i] - sj0);
