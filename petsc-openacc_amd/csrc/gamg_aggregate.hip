@@ -20,15 +20,16 @@
 //           (all its lower neighbours are decided and none is a root: a
 //           root never decrements, so a node next to one never gets to 0).
 // Decisions are final, so the order in which concurrent lanes act cannot
-// change the outcome. Each round is two launches (roots mark, OUT nodes
-// count down); the rounds needed grow with the longest chain of roots the
-// natural order forces (about 2.35 N on an N^3 grid: 704 at 300^3). Deep
-// chains (a path graph needs m / 3 rounds) are handed back to the host pass
-// past a round budget. A workgroup gathers its list appends in LDS and
-// combines its count-downs per node in an LDS hash table, so the global
-// atomics are one per workgroup and pass on the list tails and one per
-// distinct node on the counts (the middle rounds, whose frontiers are the
-// largest, are where the time goes).
+// change the outcome. Each round is one launch (k_lf_round: OUT nodes count
+// down, and each new root is marked by the workgroup that made it); the
+// rounds needed grow with the longest chain of roots the natural order
+// forces (about 2.35 N on an N^3 grid: 704 at 300^3). Deep chains (a path
+// graph needs m / 3 rounds) are handed back to the host pass past a round
+// budget. A workgroup gathers its list appends in LDS and combines its
+// count-downs per node in an LDS hash table, so the global atomics are one
+// per workgroup and pass on the list tails and one per distinct node on the
+// counts (the middle rounds, whose frontiers are the largest, are where the
+// time goes).
 // Aggregate numbers follow the roots' index order (a scan), as the host's
 // counter does.
 //
@@ -224,50 +225,92 @@ __device__ __forceinline__ void group_walks(int32_t i, int l, bool on, const int
     }
 }
 
-// Round t, first half: the roots found last round mark the higher nodes
-// within two steps OUT. rstart[t] .. tails[0] are this round's roots (only
-// the second half appends roots, so tails[0] is stable here).
-__global__ __launch_bounds__(256) void k_lf_mark(int t, const int32_t *__restrict__ si,
-                                                 const int32_t *__restrict__ sj, int32_t *state,
-                                                 const int32_t *__restrict__ roots, int32_t *outs, unsigned *tails,
-                                                 unsigned *rstart, int pre) {
-    const unsigned lo = rstart[t], hi = tails[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0) rstart[t + 1] = hi;
-    if (lo >= hi) return;  // grid-uniform
-    __shared__ WgList L;
-    if (threadIdx.x == 0) L.n = 0;
-    __syncthreads();
+// Root appends (one element per lane; every lane of the workgroup calls it at
+// the same point) to the workgroup's LDS root list; past its capacity the
+// sweep is abandoned (*overflow: the host pass takes the level; never seen:
+// a workgroup's share of a round makes a few roots at most).
+__device__ __forceinline__ void wg_root(WgList &L, bool p, int32_t k, unsigned *overflow) {
+    const unsigned long long mask = __ballot(p);
+    if (!mask) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll(mask) - 1;
+    unsigned pos = 0;
+    if (lane == leader) pos = atomicAdd(&L.n, (unsigned)__popcll(mask));
+    pos = (unsigned)__shfl((int)pos, leader, 64);
+    if (p) {
+        const unsigned idx = pos + (unsigned)__popcll(mask & ((1ull << lane) - 1ull));
+        if (idx < (unsigned)kWgBuf) L.v[idx] = k;
+        else atomicOr(overflow, 1u);
+    }
+}
+
+// Roots R.v[0, nr) mark every higher node within two steps OUT (first
+// compare-and-swap wins), appended to `next` through the LDS list M; a
+// group per root. Workgroup-uniform (nr is read after a barrier).
+__device__ __forceinline__ void mark_roots(const WgList &R, unsigned nr, WgList &M, const int32_t *__restrict__ si,
+                                           const int32_t *__restrict__ sj, int32_t *state, int32_t *next,
+                                           unsigned *ntail) {
     const int l = threadIdx.x % kGroup;
-    const unsigned groups = gridDim.x * (blockDim.x / kGroup);
-    const unsigned g0 = blockIdx.x * (blockDim.x / kGroup) + threadIdx.x / kGroup;
-    // workgroup-uniform trip count (wg_flush synchronises the workgroup)
-    for (unsigned q0 = lo; q0 < hi; q0 += groups) {
-        const unsigned q = q0 + g0;
-        const bool on = q < hi;
-        const int32_t r = on ? roots[q] : 0;
-        group_walks(r, l, on, si, sj, state, pre != 0, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
+    const unsigned gpw = blockDim.x / kGroup, g = threadIdx.x / kGroup;
+    for (unsigned r0 = 0; r0 < nr; r0 += gpw) {
+        const bool on = r0 + g < nr;
+        const int32_t r = on ? R.v[r0 + g] : 0;
+        group_walks(r, l, on, si, sj, state, false, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
             bool p[kBatch2];
 #pragma unroll
             for (int u = 0; u < kBatch2; ++u)
                 p[u] = on && st[u] == kUndecided && atomicCAS(&state[k[u]], kUndecided, kOut) == kUndecided;
-            wg_add(L, p, k, outs, &tails[1]);
+            wg_add(M, p, k, next, ntail);
         });
-        wg_flush(L, outs, &tails[1]);
+        wg_flush(M, next, ntail);
     }
 }
 
-// Round t, second half: the nodes just marked OUT count down their higher
-// undecided nodes; a count reaching 0 makes a root for round t + 1.
-__global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restrict__ si,
+// Round 0's roots (the seeds, k_lf_seed) mark their higher nodes OUT into
+// out-list 0, which round 0 reads.
+__global__ __launch_bounds__(256) void k_lf_seed_mark(const int32_t *__restrict__ seeds, const unsigned *nseeds,
+                                                      const int32_t *__restrict__ si, const int32_t *__restrict__ sj,
+                                                      int32_t *state, int32_t *outs0, unsigned *tail0) {
+    __shared__ WgList R, M;
+    const unsigned n = *nseeds, gpw = blockDim.x / kGroup;
+    if (threadIdx.x == 0) M.n = 0;
+    for (unsigned b0 = blockIdx.x * gpw; b0 < n; b0 += gridDim.x * gpw) {  // grid-uniform per workgroup
+        const unsigned nr = min(gpw, n - b0);
+        __syncthreads();
+        for (unsigned i = threadIdx.x; i < nr; i += blockDim.x) R.v[i] = seeds[b0 + i];
+        __syncthreads();
+        mark_roots(R, nr, M, si, sj, state, outs0, tail0);
+    }
+}
+
+// Round t of the sweep, one launch. The OUT nodes of out-list t % 2
+// (marked in round t - 1) count down their higher undecided nodes; a count
+// reaching 0 makes a root, and the workgroup that made it marks its higher
+// nodes within two steps OUT at once, into out-list (t + 1) % 2 for round
+// t + 1. Marking inside the round is safe: a node a new root can mark has
+// that root among its lower two-step nodes, whose walk never counts down,
+// so no concurrent count-down can make it a root; decisions stay final and
+// only their timing moves (the roots are the same set). The two out-lists
+// alternate, so the list a round reads gets no appends while it runs;
+// ostart[t] = where round t's part of its list begins, recorded by round
+// t - 2. One launch per round instead of two (mark, then count).
+__global__ __launch_bounds__(256) void k_lf_round(int t, const int32_t *__restrict__ si,
                                                   const int32_t *__restrict__ sj, int32_t *state, int32_t *cnt,
-                                                  int32_t *roots, const int32_t *__restrict__ outs, unsigned *tails,
-                                                  unsigned *ostart, int pre) {
-    const unsigned lo = ostart[t], hi = tails[1];
-    if (blockIdx.x == 0 && threadIdx.x == 0) ostart[t + 1] = hi;
+                                                  int32_t *outs0, int32_t *outs1, unsigned *tails, unsigned *ostart,
+                                                  unsigned *overflow) {
+    const int P = t & 1;
+    const int32_t *outs = P ? outs1 : outs0;
+    int32_t *next = P ? outs0 : outs1;
+    unsigned *ntail = &tails[P ^ 1];
+    const unsigned lo = ostart[t], hi = tails[P];
+    if (blockIdx.x == 0 && threadIdx.x == 0) ostart[t + 2] = hi;
     if (lo >= hi) return;  // grid-uniform
-    __shared__ WgList L;
+    __shared__ WgList R, M;
     __shared__ WgCounts H;
-    if (threadIdx.x == 0) L.n = 0;
+    if (threadIdx.x == 0) {
+        R.n = 0;
+        M.n = 0;
+    }
     for (int s = threadIdx.x; s < kHash; s += blockDim.x) {
         H.key[s] = -1;
         H.n[s] = 0;
@@ -276,11 +319,11 @@ __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restri
     const int l = threadIdx.x % kGroup;
     const unsigned groups = gridDim.x * (blockDim.x / kGroup);
     const unsigned g0 = blockIdx.x * (blockDim.x / kGroup) + threadIdx.x / kGroup;
-    for (unsigned q0 = lo; q0 < hi; q0 += groups) {
+    for (unsigned q0 = lo; q0 < hi; q0 += groups) {  // workgroup-uniform trip count
         const unsigned q = q0 + g0;
         const bool on = q < hi;
         const int32_t j = on ? outs[q] : 0;
-        group_walks(j, l, on, si, sj, state, pre != 0, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
+        group_walks(j, l, on, si, sj, state, false, [&](const int32_t (&k)[kBatch2], const int32_t (&st)[kBatch2]) {
             bool p[kBatch2];
 #pragma unroll
             for (int u = 0; u < kBatch2; ++u) {
@@ -288,9 +331,10 @@ __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restri
                 if (on && st[u] == kUndecided && !wg_count_add(H, k[u])) p[u] = atomicSub(&cnt[k[u]], 1) == 1;
             }
 #pragma unroll
-            for (int u = 0; u < kBatch2; ++u)
+            for (int u = 0; u < kBatch2; ++u) {
                 if (p[u]) state[k[u]] = kRoot;
-            wg_add(L, p, k, roots, &tails[0]);
+                wg_root(R, p[u], k[u], overflow);
+            }
         });
         __syncthreads();
         // the combined count-downs: the one that brings a count to 0 (its old
@@ -306,9 +350,13 @@ __global__ __launch_bounds__(256) void k_lf_count(int t, const int32_t *__restri
                 H.key[s] = -1;
                 H.n[s] = 0;
             }
-            wg_add1(L, pr, key, roots, &tails[0]);
+            wg_root(R, pr, key, overflow);
         }
-        wg_flush(L, roots, &tails[0]);
+        __syncthreads();
+        mark_roots(R, min(R.n, (unsigned)kWgBuf), M, si, sj, state, next, ntail);
+        __syncthreads();
+        if (threadIdx.x == 0) R.n = 0;
+        __syncthreads();
     }
 }
 
@@ -394,14 +442,12 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     }
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     const unsigned grid = kRoundGrid;
-    // straight to the atomic, no read of a node's state first (a decided
-    // node's CAS fails; an OUT node's count never reaches 0, a root's gets no
-    // further walks): 5-10 % faster than pre-reading (fewer dependent loads)
-    constexpr int pre = 0;
     auto clk = std::chrono::steady_clock::now();
     hipStream_t s = nullptr;
-    int32_t *state = nullptr, *cnt = nullptr, *roots = nullptr, *outs = nullptr;
-    unsigned *tails = nullptr, *rstart = nullptr, *ostart = nullptr, *h_ctl = nullptr;
+    int32_t *state = nullptr, *cnt = nullptr, *roots = nullptr, *outs = nullptr, *outs1 = nullptr;
+    // tails: [0], [1] the out-lists' ends, [2] the seeds (round 0's roots),
+    // [3] the root-list overflow flag
+    unsigned *tails = nullptr, *ostart = nullptr, *h_ctl = nullptr;
     const unsigned g = blocks_for(m, 256);
     constexpr int kBatch = 32;  // rounds launched between two looks at the tails
     // s does not synchronise with the null stream, on which the strength
@@ -426,17 +472,18 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     if (e == hipSuccess) e = dalloc(&cnt, m);
     if (e == hipSuccess) e = dalloc(&roots, m);
     if (e == hipSuccess) e = dalloc(&outs, m);
+    if (e == hipSuccess) e = dalloc(&outs1, m);
     if (e == hipSuccess) e = dalloc(&tails, 4);
-    if (e == hipSuccess) e = dalloc(&rstart, (int64_t)max_rounds + kBatch + 2);
-    if (e == hipSuccess) e = dalloc(&ostart, (int64_t)max_rounds + kBatch + 2);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_ctl), sizeof(unsigned) * 4);
+    if (e == hipSuccess) e = dalloc(&ostart, (int64_t)max_rounds + kBatch + 3);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_ctl), sizeof(unsigned) * 8);
     mark("allocs");
     if (e == hipSuccess) e = hipMemsetAsync(tails, 0, sizeof(unsigned) * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(rstart, 0, sizeof(unsigned), s);
-    if (e == hipSuccess) e = hipMemsetAsync(ostart, 0, sizeof(unsigned), s);
+    if (e == hipSuccess) e = hipMemsetAsync(ostart, 0, sizeof(unsigned) * 2, s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_lf_init, dim3(g), dim3(256), 0, s, m, si, sj, state, cnt);
-        hipLaunchKernelGGL(k_lf_seed, dim3(g), dim3(256), 0, s, m, state, cnt, roots, tails);
+        hipLaunchKernelGGL(k_lf_seed, dim3(g), dim3(256), 0, s, m, state, cnt, roots, tails + 2);
+        hipLaunchKernelGGL(k_lf_seed_mark, dim3(grid), dim3(256), 0, s, roots, tails + 2, si, sj, state, outs,
+                           tails);
         e = hipGetLastError();
     }
     mark("launched");
@@ -451,20 +498,19 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     lap("init");
     int t = 0;
     while (e == hipSuccess && t < max_rounds) {
-        for (int b = 0; b < kBatch; ++b, ++t) {
-            hipLaunchKernelGGL(k_lf_mark, dim3(grid), dim3(256), 0, s, t, si, sj, state, roots, outs, tails,
-                               rstart, pre);
-            hipLaunchKernelGGL(k_lf_count, dim3(grid), dim3(256), 0, s, t, si, sj, state, cnt, roots, outs,
-                               tails, ostart, pre);
-        }
-        // finished when the last round found no new root: rstart[t] holds the
-        // root count the last mark launch saw
+        for (int b = 0; b < kBatch; ++b, ++t)
+            hipLaunchKernelGGL(k_lf_round, dim3(grid), dim3(256), 0, s, t, si, sj, state, cnt, outs, outs1, tails,
+                               ostart, tails + 3);
+        // finished when round t would find its part of its out-list empty
+        // (ostart[t], recorded by round t - 2, equals the list's end): no
+        // OUT node left to count down, so no root can follow
         if ((e = hipGetLastError()) != hipSuccess) break;
-        if ((e = hipMemcpyAsync(h_ctl, tails, sizeof(unsigned), hipMemcpyDeviceToHost, s)) != hipSuccess) break;
-        if ((e = hipMemcpyAsync(h_ctl + 1, rstart + t, sizeof(unsigned), hipMemcpyDeviceToHost, s)) != hipSuccess)
+        if ((e = hipMemcpyAsync(h_ctl, tails, sizeof(unsigned) * 4, hipMemcpyDeviceToHost, s)) != hipSuccess) break;
+        if ((e = hipMemcpyAsync(h_ctl + 4, ostart + t, sizeof(unsigned), hipMemcpyDeviceToHost, s)) != hipSuccess)
             break;
         if ((e = hipStreamSynchronize(s)) != hipSuccess) break;
-        if (h_ctl[0] == h_ctl[1]) {
+        if (h_ctl[3] != 0) break;  // a workgroup's root list overflowed: the host pass
+        if (h_ctl[t & 1] == h_ctl[4]) {
             *done = true;
             break;
         }
@@ -498,7 +544,7 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
     }
     lap("numbering");
     hipFree(state); hipFree(cnt); hipFree(roots); hipFree(outs);
-    hipFree(tails); hipFree(rstart); hipFree(ostart);
+    hipFree(outs1); hipFree(tails); hipFree(ostart);
     if (h_ctl) hipHostFree(h_ctl);
     // (s is the process's set-up stream: kept)
     return e;
