@@ -52,7 +52,7 @@ extern "C" {
 
 /* 2: aijhip_info_t gained mult_layout_bytes and lost the fields of the
  * withdrawn options; the A/B-only options AIJHIP_OPT_XCD_REMAP /
- * _PERSISTENT / _CLAMPED_LOADS / _LONG_OVERLAP / _ROW_GROUP / _X_TILE /
+ * _PERSISTENT / _CLAMPED_LOADS / _ROW_GROUP / _X_TILE /
  * _LONG_WINDOW and AIJHIP_KERNEL_MERGE were withdrawn (measured slower,
  * DESIGN.md §5) and return AIJHIP_ERR_ARG. */
 #define AIJHIP_ABI_VERSION 2
@@ -122,6 +122,11 @@ typedef struct aijhip_info {
     int32_t row_patterns;    /* MatMult reads a pattern id per row instead of
                                 aj (AIJHIP_OPT_ROW_PATTERNS): the number of
                                 distinct column - row offset lists; 0 off    */
+    int32_t long_overlap;    /* how the long rows' segments and the wide
+                                blocks run beside the row blocks: 0 after
+                                them, 1 on a side stream, 2 interleaved in
+                                one grid (AIJHIP_OPT_LONG_OVERLAP; fills the
+                                former padding word, layout unchanged)       */
     int64_t mult_layout_bytes; /* compulsory bytes one MatMult of the plan in
                                 effect moves: mult_bytes for CSR (aj read);
                                 less where the plan reads column codes (10 B
@@ -195,8 +200,14 @@ enum {
                                        download (step3/step4 analogue); k > 0:
                                        chunks of >= k rows; 0: the serial
                                        step-2 form. Same results              */
-    AIJHIP_OPT_LONG_OVERLAP = 9,    /* withdrawn in ABI 2 (a side stream for
-                                       the long-row segments measured neutral) */
+    AIJHIP_OPT_LONG_OVERLAP = 9,    /* operands with long rows: 0 the
+                                       segments and the wide blocks after the
+                                       row blocks; 1 on a side stream; 2 one
+                                       grid with the segments and wide blocks
+                                       interleaved among the row blocks
+                                       (plain or 16-bit gather-ordered
+                                       layouts, geometries 1 and 6). Same
+                                       results                                */
     AIJHIP_OPT_ROW_GROUP = 11,      /* withdrawn in ABI 2 (register row groups
                                        measured slower on every operand)     */
     AIJHIP_OPT_GATHER_SORT = 12,    /* MatMult / MatMultAdd from a copy of the

@@ -75,6 +75,7 @@ class AIJInfo(ctypes.Structure):
         ("stream_threads", ctypes.c_int32), ("stream_nnz_cap", ctypes.c_int32), ("stream_rows", ctypes.c_int32),
         ("exact", ctypes.c_int32), ("gather_sorted", ctypes.c_int32), ("column_codes", ctypes.c_int32),
         ("row_patterns", ctypes.c_int32),
+        ("long_overlap", ctypes.c_int32),
         ("mult_layout_bytes", ctypes.c_int64),
     ]
 

@@ -188,13 +188,17 @@ __device__ __forceinline__ double row_sum_seq(const double *p, int32_t n, double
     return s;
 }
 
+// One STREAM row block b of blk[0, nblk) by the T lanes of the calling
+// workgroup; prod (CAP doubles) and cdict (kCodeDictMax ints, column codes
+// only) are the workgroup's LDS. The body of k_spmv_stream and of the row
+// blocks of k_spmv_mixed.
 // NTMODE bit 0: non-temporal matrix loads (scattered long-row operands).
 template <int T, int CAP, int RPT, bool CROW, int NTMODE, class Op>
-__global__ __launch_bounds__(T) void k_spmv_stream(
-    const BlockDesc *__restrict__ blk, int nblk, int exact,
+__device__ __forceinline__ void stream_block(
+    const int b, const BlockDesc *__restrict__ blk, int nblk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const uint16_t *__restrict__ sslot,
-    const int32_t *__restrict__ sbase) {
+    const double *__restrict__ aa, const Op &op, double *dpart, const int *stop, const uint16_t *__restrict__ sslot,
+    const int32_t *__restrict__ sbase, double *prod, int32_t *cdict) {
     constexpr bool NT = (NTMODE & 1) != 0;
     // bit 3: gather-ordered blocks (Plan::d_saj/d_saa): aj/aa hold each
     // block's entries sorted by column, sslot their positions in the block,
@@ -214,9 +218,6 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     static_assert(!(CODES && (S16 || SORTED || CROW)), "column codes: plain full-row form only");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
-    __shared__ double prod[CAP];
-    __shared__ int32_t cdict[CODES ? kCodeDictMax : 1];
-    const int b = (int)blockIdx.x;
     const BlockDesc d = blk[b];
     int32_t nd = 0, dbase = 0;
     if constexpr (CODES) {
@@ -394,6 +395,18 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     }
 }
 
+template <int T, int CAP, int RPT, bool CROW, int NTMODE, class Op>
+__global__ __launch_bounds__(T) void k_spmv_stream(
+    const BlockDesc *__restrict__ blk, int nblk, int exact,
+    const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
+    const double *__restrict__ aa, Op op, double *dpart, const int *stop, const uint16_t *__restrict__ sslot,
+    const int32_t *__restrict__ sbase) {
+    __shared__ double prod[CAP];
+    __shared__ int32_t cdict[(NTMODE & 32) ? kCodeDictMax : 1];
+    stream_block<T, CAP, RPT, CROW, NTMODE, Op>((int)blockIdx.x, blk, nblk, exact, rai, ridx, aj, aa, op, dpart, stop,
+                                                sslot, sbase, prod, cdict);
+}
+
 // Row patterns (Tuning::patterns; short-row operands whose rows follow a
 // few column - row offset lists: stencils): the STREAM row blocks, but the
 // columns are not stored per entry. Each row has a pattern id (1 byte), the
@@ -480,23 +493,26 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
 // Segments of long rows: tree-reduced partial sums. A lane takes 16-B pairs
 // (aa as f64x2, aj as i32x2 from an even start, as the STREAM blocks do) at
 // pair stride kLongThreads and keeps U pairs in flight: a 4096-entry segment
-// is 2048 pairs, so every load and gather of the segment is issued before the
-// first product is needed (the previous form, 8 scalar entries per round,
+// is 2048 pairs (512 lanes x 4), so every load and gather of the segment is
+// issued before the first product is needed (the previous form, 8 scalar entries per round,
 // waited on two dependent latencies per round: 2.66 TB/s). The
 // lane's U partial sums are combined u = 0..U-1, then the wave tree, then the
 // waves in order: a fixed order.
-__global__ __launch_bounds__(kLongThreads) void k_long_partial(
-    const LongSeg *__restrict__ seg, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, const double *__restrict__ x,
-    double *__restrict__ partials, const int32_t *__restrict__ perm) {
-    constexpr int U = 8;
-    __shared__ double red[kLongThreads / 64];
-    const int32_t id = perm ? perm[blockIdx.x] : (int32_t)blockIdx.x;
+// The body, for the first kLongThreads lanes of the calling workgroup (any
+// further lanes only pass the barrier): k_long_partial, and the segments of
+// k_spmv_mixed's grid, with the same sums in the same order. red: >= 4 LDS doubles.
+__device__ __forceinline__ void long_segment(const int32_t id, const LongSeg *__restrict__ seg,
+                                             const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                                             const double *__restrict__ x, double *__restrict__ partials,
+                                             double *red) {
+    constexpr int U = kLongSegNnz / (2 * kLongThreads);  // pairs in flight per lane
+    static_assert(U >= 1, "a round of pairs must fit a segment");
     const LongSeg s = seg[id];
     const int t = threadIdx.x;
     double acc[U] = {};
     const int64_t k0 = s.k0, k1 = (int64_t)s.k0 + s.nk, kb = k0 & ~int64_t(1);
-    for (int64_t k = kb + 2 * t; k < k1; k += (int64_t)2 * U * kLongThreads) {
+    const int64_t kend = t < kLongThreads ? k1 : kb;  // lanes past kLongThreads take no pairs
+    for (int64_t k = kb + 2 * t; k < kend; k += (int64_t)2 * U * kLongThreads) {
         f64x2 a[U];
         i32x2 c[U];
 #pragma unroll
@@ -526,13 +542,50 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     for (int u = 1; u < U; ++u) v += acc[u];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
-    if ((t & 63) == 0) red[t >> 6] = v;
+    if ((t & 63) == 0 && t < kLongThreads) red[t >> 6] = v;
     __syncthreads();
     if (t == 0) {
         double r = red[0];
 #pragma unroll
         for (int w = 1; w < kLongThreads / 64; ++w) r += red[w];
         partials[id] = r;
+    }
+}
+
+__global__ __launch_bounds__(kLongThreads) void k_long_partial(
+    const LongSeg *__restrict__ seg, const int32_t *__restrict__ aj,
+    const double *__restrict__ aa, const double *__restrict__ x,
+    double *__restrict__ partials, const int32_t *__restrict__ perm) {
+    __shared__ double red[kLongThreads / 64];
+    long_segment(perm ? perm[blockIdx.x] : (int32_t)blockIdx.x, seg, aj, aa, x, partials, red);
+}
+
+// One grid for MatMult / MatMultAdd of an operand with long rows
+// (Tuning::overlap 2): the long rows' segments and the wide blocks are
+// interleaved with the row blocks in launch order (Plan::d_work: w >= 0 a
+// row block of nb[0, nn) or, past nn, of wb; w < 0 segment -1 - w), so the
+// latency-bound segment workgroups (scattered gathers) run beside the
+// streaming row blocks instead of as a phase of their own. Each part's
+// arithmetic is its own kernel's (stream_block, long_segment): the same
+// bits; k_long_finish sums the partials after this launch.
+template <int T, int CAP, int RPT, int NTM, bool ADD>
+__global__ __launch_bounds__(T) void k_spmv_mixed(
+    const int32_t *__restrict__ work, const BlockDesc *__restrict__ nb, int nn, const BlockDesc *__restrict__ wb,
+    int nw, int exact, const int32_t *__restrict__ rai, const int32_t *__restrict__ naj,
+    const double *__restrict__ naa, const int32_t *__restrict__ sbase, const int32_t *__restrict__ aj,
+    const double *__restrict__ aa, const LongSeg *__restrict__ segs, double *__restrict__ partials,
+    OpMult<ADD> op) {
+    static_assert(T >= kLongThreads, "a segment needs kLongThreads lanes");
+    __shared__ double prod[CAP];
+    const int32_t w = work[blockIdx.x];
+    if (w < 0) {
+        long_segment(-1 - w, segs, aj, aa, op.x, partials, prod);
+    } else if (w < nn) {
+        stream_block<T, CAP, RPT, false, NTM, OpMult<ADD>>(w, nb, nn, exact, rai, nullptr, naj, naa, op, nullptr,
+                                                           nullptr, nullptr, sbase, prod, nullptr);
+    } else {
+        stream_block<T, CAP, RPT, false, 0, OpMult<ADD>>(w - nn, wb, nw, exact, rai, nullptr, aj, aa, op, nullptr,
+                                                         nullptr, nullptr, nullptr, prod, nullptr);
     }
 }
 
@@ -1393,6 +1446,36 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
                                                                       hipSuccess)
             return e;
         sw = P.side;
+    }
+    // Tuning::overlap 2: one interleaved grid (Plan::d_work), then the sums
+    // of the long rows' partials
+    if (P.d_work && !L.ridx && !dpart && !stop) {
+        const bool s16 = P.d_sidx != nullptr;
+        const BlockDesc *nb = s16 && P.n_wblocks ? P.d_nblocks : P.d_blocks;
+        const int32_t nn = s16 && P.n_wblocks ? P.n_nblocks : P.n_blocks, nw = s16 ? P.n_wblocks : 0;
+        const int32_t *naj = s16 ? reinterpret_cast<const int32_t *>(P.d_sidx) : A.d_aj;
+        const double *naa = s16 ? P.d_saa : A.d_aa;
+#define AIJHIP_MX(G, NTM, ADD)                                                                                 \
+    hipLaunchKernelGGL((k_spmv_mixed<AIJHIP_GEOM(G), NTM, ADD>), dim3(P.n_work), dim3(kStreamGeoms[G].threads), 0, s, \
+                       P.d_work, nb, nn, P.d_wblocks, nw, (int)P.tune.exact, L.rai, naj, naa, P.d_sbase, A.d_aj, A.d_aa, \
+                       P.d_segs, P.d_partials, OpMult<ADD>{x, z, y, false})
+#define AIJHIP_MXG(G)                                                   \
+    if (s16) { if (add) AIJHIP_MX(G, 16, true); else AIJHIP_MX(G, 16, false); } \
+    else if (P.tune.nt == 1) { if (add) AIJHIP_MX(G, 1, true); else AIJHIP_MX(G, 1, false); } \
+    else { if (add) AIJHIP_MX(G, 0, true); else AIJHIP_MX(G, 0, false); }
+        if (P.tune.geom == 6) { AIJHIP_MXG(6); }
+        else if (P.tune.geom == 1) { AIJHIP_MXG(1); }
+        else return hipErrorInvalidValue;  // the planner builds d_work at geometries 1 and 6 only
+#undef AIJHIP_MXG
+#undef AIJHIP_MX
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (P.n_longs > 0) {
+            if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
+                                        P.d_partials, z, y);
+            else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
+                                    P.d_partials, z, y);
+        }
+        return hipGetLastError();
     }
     // long rows: segment partials, then their ordered sums
     if (P.n_longs > 0) {

@@ -126,8 +126,8 @@ def main():
     if args.variants == "patnt":  # row patterns: plain vs non-temporal aa loads
         for nt in (0, 1, 0, 1):
             variants.append(("stream", dict(row_patterns=1, nt_loads=nt)))
-    if args.variants == "overlap":  # hub segments + wide blocks on a side stream, concurrent with the row blocks
-        for ov in (0, 1, 0, 1):
+    if args.variants == "overlap":  # hub segments + wide blocks after, on a side stream, or in one interleaved grid
+        for ov in (0, 1, 2, 0, 1, 2):
             variants.append(("stream", dict(long_overlap=ov)))
     if args.variants == "gslong":  # hub-row segments beside the gather-ordered blocks: XCD placement on / off
         for lx in (1, 0):
