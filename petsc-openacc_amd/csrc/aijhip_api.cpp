@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -94,6 +95,7 @@ void free_plan(aijhip::Plan &P) {
 }
 
 void free_matrix(aijhip_mat *A) {
+    A->plan_gen = aijhip::next_plan_gen();
     free_plan(A->plan);
     hipFree(A->d_ai);
     hipFree(A->d_aj);
@@ -464,6 +466,7 @@ int plan_stream(aijhip_mat *A) {
 }
 
 int plan_build(aijhip_mat *A) {
+    A->plan_gen = aijhip::next_plan_gen();
     free_plan(A->plan);
     aijhip::Plan &P = A->plan;
     int kernel = A->requested_kernel;
@@ -726,6 +729,11 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
 
 namespace aijhip {
 void set_error(const std::string &msg) { g_err = msg; }
+
+uint64_t next_plan_gen() {
+    static std::atomic<uint64_t> gen{0};
+    return ++gen;
+}
 
 // hipGetDeviceCount costs milliseconds per call on this stack; the count of a
 // process does not change, so it is asked once.

@@ -212,6 +212,10 @@ struct Plan {
 
 struct aijhip_mat {
     int device = 0;
+    // changes whenever the device arrays or the plan are rebuilt (a fresh
+    // value of a process-wide counter): a captured HIP graph of launches on
+    // this handle is replayed only while it is unchanged (ksp.hip)
+    uint64_t plan_gen = 0;
     int n_cu = 256;  // compute units of the device
     int32_t m = 0, n = 0;
     int64_t nz = 0;
@@ -331,6 +335,9 @@ void host_pipe_free(HostPipe *p);
 // points at them (2 x *nbz doubles), else NULL.
 hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t s, const double **dots,
                          int *nbz, const int *stop = nullptr);
+
+// A fresh value for aijhip_mat::plan_gen.
+uint64_t next_plan_gen();
 
 // Compulsory bytes one MatMult under A's plan moves (aijhip_info_t.mult_layout_bytes).
 int64_t mult_layout_bytes(const aijhip_mat &A);

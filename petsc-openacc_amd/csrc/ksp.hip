@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <new>
 #include <string>
 #include <vector>
@@ -128,6 +129,8 @@ struct aijhip_ksp {
     int32_t max_it = 10000;
     aijhip_gamg_params_t gamg;
     bool set_up = false;
+    uint64_t a_gen = 0;  // the operator's plan generation at set-up: a re-planned
+                         // operator (options, MatAssemblyEnd) is set up again
     bool fused = false;
     int vec_grid = 0;
     // CG vector kernels store with the non-temporal hint (tools: CG+Jacobi
@@ -154,6 +157,14 @@ struct aijhip_ksp {
     int reason = 0;
     double rnorm = 0.0;
     std::vector<double> hist;
+    // One poll batch of iterations as a HIP graph (aijhip_ksp_solve):
+    // captured on `cap`, replayed on the caller's stream while gkey (x, the
+    // tolerances, every handle of the hierarchy and its plan generation)
+    // is unchanged; graphs_off after a capture failed (direct launches)
+    hipStream_t cap = nullptr;
+    hipGraphExec_t gexec = nullptr;
+    std::vector<uint64_t> gkey;
+    bool graphs_off = false;
 };
 
 namespace {
@@ -169,7 +180,14 @@ void mg_free(aijhip_ksp *K) {
     K->d_mgpart = nullptr;
 }
 
+void graph_free(aijhip_ksp *K) {
+    if (K->gexec) hipGraphExecDestroy(K->gexec);
+    K->gexec = nullptr;
+    K->gkey.clear();
+}
+
 void ksp_free(aijhip_ksp *K) {
+    graph_free(K);
     mg_free(K);
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
     hipFree(K->d_hist); hipFree(K->d_state);
@@ -448,7 +466,7 @@ int aijhip_ksp_set_initial_guess_nonzero(aijhip_ksp_t K, int flg) {
 int aijhip_ksp_set_up(aijhip_ksp_t K) {
     aijhip::Range range("KSPSetUp");
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
-    if (K->set_up) return AIJHIP_OK;
+    if (K->set_up && K->a_gen == K->A->plan_gen) return AIJHIP_OK;
     const auto t0 = std::chrono::steady_clock::now();
     aijhip_mat *A = K->A;
     KDeviceGuard g(A->device);
@@ -486,8 +504,81 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
     }
     K->setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     K->set_up = true;
+    K->a_gen = A->plan_gen;
     return AIJHIP_OK;
 }
+
+}  // extern "C"
+
+namespace {
+
+// What a captured batch depends on beyond the KSP's own buffers (which only
+// set-up reallocates, and set-up drops the graph): x, the batch length, the
+// tolerances (k_reduce_iter takes them by value) and every operator handle of
+// the iteration with its plan generation.
+std::vector<uint64_t> batch_key(const aijhip_ksp *K, const double *x, int batch, const CGParams &p) {
+    std::vector<uint64_t> k;
+    auto bits = [](double d) { uint64_t u; std::memcpy(&u, &d, sizeof u); return u; };
+    auto mat = [&](const aijhip_mat *M) {
+        k.push_back((uint64_t)(uintptr_t)M);
+        k.push_back(M ? M->plan_gen : 0);
+    };
+    k.push_back((uint64_t)(uintptr_t)x);
+    k.push_back((uint64_t)batch);
+    k.push_back((uint64_t)K->fused);
+    k.push_back(bits(p.rtol));
+    k.push_back(bits(p.abstol));
+    k.push_back(bits(p.dtol));
+    k.push_back((uint64_t)p.max_it);
+    k.push_back((uint64_t)p.normtype);
+    k.push_back((uint64_t)p.guess_zero);
+    k.push_back((uint64_t)p.pc);
+    mat(K->A);
+    for (const MGLevel &L : K->mg) {
+        mat(L.A);
+        mat(L.P);
+        mat(L.P ? L.P->transpose : nullptr);
+        k.push_back((uint64_t)L.fused);
+    }
+    return k;
+}
+
+// K->gexec holds `batch` iterations for the current key (captured now if it
+// does not): true, or false when capture is unavailable (then the caller
+// launches directly, and K never tries again).
+template <class F>
+bool batch_graph(aijhip_ksp *K, const double *x, int batch, const CGParams &p, F &iterate) {
+    std::vector<uint64_t> key = batch_key(K, x, batch, p);
+    if (K->gexec && key == K->gkey) return true;
+    graph_free(K);
+    if (!K->cap && hipStreamCreateWithFlags(&K->cap, hipStreamNonBlocking) != hipSuccess) {
+        K->cap = nullptr;
+        K->graphs_off = true;
+        (void)hipGetLastError();
+        return false;
+    }
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamBeginCapture(K->cap, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess) {
+        for (int j = 0; j < batch && e == hipSuccess; ++j) e = iterate(K->cap);
+        const hipError_t e2 = hipStreamEndCapture(K->cap, &g);  // always ends the capture
+        if (e == hipSuccess) e = e2;
+    }
+    if (e == hipSuccess && g) e = hipGraphInstantiate(&K->gexec, g, nullptr, nullptr, 0);
+    if (g) hipGraphDestroy(g);
+    if (e != hipSuccess || !K->gexec) {
+        K->gexec = nullptr;
+        K->graphs_off = true;
+        (void)hipGetLastError();
+        return false;
+    }
+    K->gkey = std::move(key);
+    return true;
+}
+
+}  // namespace
+
+extern "C" {
 
 int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     aijhip::Range range("KSPSolve");
@@ -524,10 +615,45 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     }
     hipLaunchKernelGGL(k_reduce_init, dim3(1), rt, 0, s, K->d_part, nb, K->d_state, K->d_hist, p);
     if ((e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve init");
-    // iterations in batches; every CG and V-cycle kernel is a no-op once
-    // `done` is set (AIJHIP_KSP_POLL overrides the batch, for A/B)
+    // One CG iteration (+ the V-cycle) on stream st; every kernel is a
+    // no-op once `done` is set.
+    auto iterate = [&](hipStream_t st) -> hipError_t {
+        hipError_t ie = hipSuccess;
+        hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
+        if (K->fused) {
+            ie = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, st);
+            if (ie == hipSuccess)
+                hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, st, K->d_part, A->plan.n_blocks, K->d_state);
+        } else {
+            ie = aijhip::launch_mult(*A, K->d_p, nullptr, K->d_z, false, st, &K->d_state->done);
+            hipLaunchKernelGGL(k_dot, vg, vt, 0, st, m, K->d_p, K->d_z, K->d_part, K->d_state);
+            hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, st, K->d_part, nb, K->d_state);
+        }
+        hipLaunchKernelGGL(k_update<true>, vg, vt, 0, st, m, K->d_r, K->d_z, K->d_dinv, K->d_part, K->d_state,
+                           K->pc, K->d_p, nullptr);
+        const double *pz = K->d_part;
+        int nbz = nb;
+        if (gamg && ie == hipSuccess) {
+            // z = B r; z.z and z.r come from the finest post-smoothing
+            // when it is fused, else from k_dots
+            bool dots = false;
+            ie = vcycle(K, K->d_r, K->d_z, st, K->d_mgpart, &dots, &K->d_state->done);
+            if (dots) {
+                pz = K->d_mgpart;
+                nbz = K->mg[0].A->plan.n_blocks;
+            } else {
+                hipLaunchKernelGGL(k_dots, vg, vt, 0, st, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
+            }
+        }
+        hipLaunchKernelGGL(k_reduce_iter, dim3(1), rt, 0, st, pz, nbz, K->d_part + 2 * nb, nb, K->d_state,
+                           K->d_hist, p);
+        return ie != hipSuccess ? ie : hipGetLastError();
+    };
+    // iterations in batches between polls (AIJHIP_KSP_POLL overrides the
+    // batch, for A/B); a whole batch is one HIP graph launch (batch_graph)
     int batch = 8;
     if (const char *v = std::getenv("AIJHIP_KSP_POLL")) batch = std::max(1, std::atoi(v));
+    const bool graphs = !K->graphs_off && !std::getenv("AIJHIP_KSP_NO_GRAPH");
     int32_t launched = 0;
     K->host_syncs = 0;
     for (;;) {
@@ -536,37 +662,13 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return khip(e, "KSPSolve poll");
         if (K->h_state->done || launched >= K->max_it) break;
-        for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched) {
-            hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
-            if (K->fused) {
-                e = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, s);
-                if (e == hipSuccess)
-                    hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, A->plan.n_blocks, K->d_state);
-            } else {
-                e = aijhip::launch_mult(*A, K->d_p, nullptr, K->d_z, false, s, &K->d_state->done);
-                hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
-                hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, s, K->d_part, nb, K->d_state);
-            }
-            hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
-                               K->d_state, K->pc, K->d_p, nullptr);
-            const double *pz = K->d_part;
-            int nbz = nb;
-            if (gamg && e == hipSuccess) {
-                // z = B r; z.z and z.r come from the finest post-smoothing
-                // when it is fused, else from k_dots
-                bool dots = false;
-                e = vcycle(K, K->d_r, K->d_z, s, K->d_mgpart, &dots, &K->d_state->done);
-                if (dots) {
-                    pz = K->d_mgpart;
-                    nbz = K->mg[0].A->plan.n_blocks;
-                } else {
-                    hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
-                }
-            }
-            hipLaunchKernelGGL(k_reduce_iter, dim3(1), rt, 0, s, pz, nbz, K->d_part + 2 * nb, nb, K->d_state,
-                               K->d_hist, p);
-            if (e != hipSuccess || (e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve iteration");
+        if (graphs && launched + batch <= K->max_it && batch_graph(K, x, batch, p, iterate)) {
+            if ((e = hipGraphLaunch(K->gexec, s)) != hipSuccess) return khip(e, "KSPSolve iteration graph");
+            launched += batch;
+            continue;
         }
+        for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched)
+            if ((e = iterate(s)) != hipSuccess) return khip(e, "KSPSolve iteration");
     }
     hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
     if ((e = hipGetLastError()) != hipSuccess ||
@@ -742,6 +844,7 @@ int aijhip_ksp_destroy(aijhip_ksp_t K) {
         KDeviceGuard g(K->A->device);
         (void)hipDeviceSynchronize();
         ksp_free(K);
+        if (K->cap) hipStreamDestroy(K->cap);
     }
     delete K;
     return AIJHIP_OK;

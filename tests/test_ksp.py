@@ -150,3 +150,52 @@ def test_gpu_solve_host_vectors_equals_device_solve(pkg, pc, guess):
             assert ksp.its == its_d
             assert np.array_equal(np.array(ksp.history()).view(np.uint64), hist_d.view(np.uint64))
             assert np.array_equal(xh.view(np.uint64), xdev.view(np.uint64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pc", ["gamg", "jacobi"])
+def test_gpu_solve_graph_replay_equals_direct_launches(pkg, monkeypatch, pc):
+    """A poll batch of iterations runs as one captured HIP graph
+    (aijhip_ksp_solve): the same kernels with the same arguments, so the
+    iterations, the residual history and x are the direct launches' bits. The
+    graph is re-captured when a tolerance or the operator's plan changes (a
+    re-planned operator is set up again), and a solve that stops mid-batch
+    leaves the rest of the batch as no-ops."""
+    import torch
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    N = 24
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, _ = pkg.poisson_vectors(N)
+    b = torch.from_numpy(rhs).cuda()
+
+    def run(ksp):
+        x = torch.zeros_like(b)
+        ksp.solve(b, x)
+        torch.cuda.synchronize()
+        return ksp.its, np.array(ksp.history()), x.cpu().numpy()
+
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        with K.KSPCG(A, rtol=1e-12, atol=1e-14, pc=pc) as ksp:
+            monkeypatch.setenv("AIJHIP_KSP_NO_GRAPH", "1")
+            ref = run(ksp)
+            monkeypatch.delenv("AIJHIP_KSP_NO_GRAPH")
+            for _ in range(2):  # captured, then replayed
+                got = run(ksp)
+                assert got[0] == ref[0]
+                assert np.array_equal(got[1].view(np.uint64), ref[1].view(np.uint64))
+                assert np.array_equal(got[2].view(np.uint64), ref[2].view(np.uint64))
+            ksp.set_tolerances(1e-6, 1e-14, 1e5, 10000)  # new key: captured again
+            monkeypatch.setenv("AIJHIP_KSP_NO_GRAPH", "1")
+            ref6 = run(ksp)
+            monkeypatch.delenv("AIJHIP_KSP_NO_GRAPH")
+            got6 = run(ksp)
+            assert got6[0] == ref6[0] < ref[0]
+            assert np.array_equal(got6[2].view(np.uint64), ref6[2].view(np.uint64))
+            # the operator re-planned (its plan generation changes): the KSP is
+            # set up again and the batch captured again
+            A.set_option("geometry", 1)
+            got1 = run(ksp)
+            monkeypatch.setenv("AIJHIP_KSP_NO_GRAPH", "1")
+            ref1 = run(ksp)
+            assert got1[0] == ref1[0]
+            assert np.array_equal(got1[2].view(np.uint64), ref1[2].view(np.uint64))

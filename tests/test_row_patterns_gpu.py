@@ -109,6 +109,35 @@ def test_many_patterns_fall_back(pkg, dev, coracle):
         assert_bits(y.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True))
 
 
+def test_many_patterns_plan_time_large(pkg, dev, coracle):
+    """a ~10^6-row random short-row operand (far more than 256
+    distinct offset lists) must leave the row-pattern attempt early (the
+    insert stops once the table has overflowed) instead of probing all 4096
+    slots for every row: the plan stays within seconds, the product the
+    oracle's."""
+    import time
+    rng = np.random.default_rng(21)
+    m, L = 1_000_000, 6
+    offs = -40 + rng.integers(0, 10, (m, 1)) + np.cumsum(rng.integers(1, 14, (m, L)), axis=1)
+    cols = np.arange(m)[:, None] + offs
+    keep = (cols >= 0) & (cols < m)
+    ai = np.concatenate([[0], np.cumsum(keep.sum(axis=1))]).astype(np.int32)
+    aj = cols[keep].astype(np.int32)
+    aa = rng.uniform(-1, 1, len(aj))
+    x = rng.uniform(-1, 1, m)
+    t0 = time.perf_counter()
+    with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=1) as A:
+        torch.cuda.synchronize()
+        t_plan = time.perf_counter() - t0
+        assert A.info()["row_patterns"] == 0
+        assert t_plan < 10.0, f"plan took {t_plan:.2f} s"
+        xd = to_dev(x, dev)
+        y = torch.empty(m, dtype=torch.float64, device=dev)
+        A.mult(xd, y)
+        torch.cuda.synchronize()
+        assert_bits(y.cpu().numpy(), coracle.matmult(ai, aj, aa, x, omp=True))
+
+
 def test_cg_and_gamg_with_patterns_bitwise(pkg, dev):
     """The solver path on a patterned operator: CG + Jacobi (the fused
     SpMV + p.w epilogue) and CG + GAMG (the fused V-cycle smoothers and the
