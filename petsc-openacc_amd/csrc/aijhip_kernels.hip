@@ -216,6 +216,15 @@ __device__ __forceinline__ void stream_block(
     // 12; the products, their slots and the sums are the plain kernel's
     constexpr bool CODES = (NTMODE & 32) != 0;
     static_assert(!(CODES && (S16 || SORTED || CROW)), "column codes: plain full-row form only");
+    // bit 6: phase 1 without branches: every lane loads its pairs (lanes past
+    // the block re-read the block's last pair) and gathers them, so the
+    // compiler issues all aj loads, then all aa loads, then all gathers, each
+    // group waiting only for what it needs. The predicated form compiles the
+    // per-pair `if`s to branches, and at each join the gathers wait for every
+    // earlier load, their own predecessors included (vmcnt(0) per pair: four
+    // gather round trips per lane instead of one).
+    constexpr bool BF = (NTMODE & 64) != 0;
+    static_assert(!(BF && (CODES || SORTED)), "branch-free phase 1: plain and 16-bit gather-ordered forms");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     const BlockDesc d = blk[b];
@@ -256,7 +265,17 @@ __device__ __forceinline__ void stream_block(
     f64x2 av[ITERS];
     i32x2 cv[ITERS];
     f64x2 xv[ITERS];
-    {
+    if constexpr (BF) {
+        if (d.nk > 0) {  // (block-uniform) the last pair start is then >= kb
+            const int64_t kl = (k1 - 1) & ~int64_t(1);
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it)
+                cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + min(kb + 2 * (int64_t)(t + it * T), kl)));
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it)
+                av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + min(kb + 2 * (int64_t)(t + it * T), kl)));
+        }
+    } else {
         uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
@@ -318,7 +337,15 @@ __device__ __forceinline__ void stream_block(
             if (k < k1) sv[it] = *reinterpret_cast<const uint32_t *>(sslot + k);
         }
     }
-    if constexpr (!CODES) {  // (the coded form gathered with the decode above)
+    if constexpr (BF) {  // every pair gathered (the clamped ones re-gather the last pair's columns)
+        if (d.nk > 0) {
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) {
+                xv[it].x = op.gx(cv[it].x);
+                xv[it].y = op.gx(cv[it].y);
+            }
+        }
+    } else if constexpr (!CODES) {  // (the coded form gathered with the decode above)
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
@@ -1291,9 +1318,9 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     if (P.d_sidx && (P.n_wblocks == 0 || !dpart)) {  // 16-bit columns and slots packed per pair
         const BlockDesc *nb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
         const int32_t nn = P.n_wblocks ? P.n_nblocks : P.n_blocks;
-#define AIJHIP_SS(ADD, CROW)                                                                                   \
+#define AIJHIP_SS(ADD, CROW, NTM)                                                                              \
     if (nn > 0)                                                                                                \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 16, OpMult<ADD>>), dim3(nn), dim3(T), 0, s, nb, nn, \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, NTM, OpMult<ADD>>), dim3(nn), dim3(T), 0, s, nb, nn, \
                            (int)P.tune.exact, L.rai, L.ridx, reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa, \
                            OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sbase);  \
     if (P.n_wblocks > 0)                                                                                       \
@@ -1301,10 +1328,15 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,         \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);             \
     return
-        if (add && L.ridx) { AIJHIP_SS(true, true); }
-        if (add) { AIJHIP_SS(true, false); }
-        if (L.ridx) { AIJHIP_SS(false, true); }
-        AIJHIP_SS(false, false);
+        if (add && L.ridx) { AIJHIP_SS(true, true, 16); }
+        if (P.tune.bf) {
+            if (add) { AIJHIP_SS(true, false, 80); }
+            if (L.ridx) { AIJHIP_SS(false, true, 80); }
+            AIJHIP_SS(false, false, 80);
+        }
+        if (add) { AIJHIP_SS(true, false, 16); }
+        if (L.ridx) { AIJHIP_SS(false, true, 16); }
+        AIJHIP_SS(false, false, 16);
 #undef AIJHIP_SS
     }
     if (P.d_sidx) {  // split plan, fused dot: the original arrays in one launch
@@ -1322,6 +1354,17 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         if (L.ridx) { AIJHIP_SS(false, true); }
         AIJHIP_SS(false, false);
 #undef AIJHIP_SS
+    }
+    // branch-free phase 1 (NTMODE bit 64, A/B: Tuning::bf)
+    if constexpr (kGeom6) {
+        if (P.tune.bf && !L.ridx) {
+            if (P.tune.nt == 1) {
+                if (add) { AIJHIP_SL(true, false, 65); }
+                AIJHIP_SL(false, false, 65);
+            }
+            if (add) { AIJHIP_SL(true, false, 64); }
+            AIJHIP_SL(false, false, 64);
+        }
     }
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
     // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)

@@ -17,6 +17,10 @@ timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout
     > "$OUT/pytest.log" 2>&1 && echo "pytest ok: $(tail -1 "$OUT/pytest.log")" \
     || { grep -E "FAIL|Error" "$OUT/pytest.log" | tail -20; tail -5 "$OUT/pytest.log"; exit 1; }
 bash tools/gpu_gamg_setup.sh "$TAG/gamg" || exit 1
+timeout -k 10 300 python -u tools/tune.py --variants bf --rounds 5 > "$OUT/bf_poisson.jsonl" 2>&1 \
+    && echo "bf poisson ok" && grep -h "bitwise\|us_median" "$OUT/bf_poisson.jsonl" | tail -7 || exit 1
+timeout -k 10 300 python -u tools/tune.py --matrix skewed --variants bf --rounds 3 > "$OUT/bf_skewed.jsonl" 2>&1 \
+    && echo "bf skewed ok" && grep -h "bitwise\|us_median" "$OUT/bf_skewed.jsonl" | tail -7 || exit 1
 timeout -k 10 300 python -u tools/tune.py --matrix skewed --variants overlap --rounds 5 > "$OUT/overlap.jsonl" 2>&1 \
     && echo "overlap ok" && grep us_median "$OUT/overlap.jsonl" | tail -6 || exit 1
 timeout -k 10 300 python -u bench.py --no-cg --no-gamg --no-host-vec --no-flan --no-cpu-baseline --steps 100 \
