@@ -538,30 +538,37 @@ __device__ __forceinline__ void long_segment(const int32_t id, const LongSeg *__
     const int t = threadIdx.x;
     double acc[U] = {};
     const int64_t k0 = s.k0, k1 = (int64_t)s.k0 + s.nk, kb = k0 & ~int64_t(1);
+    const int64_t kl = (k1 - 1) & ~int64_t(1);        // the segment's last pair (nk >= 1)
     const int64_t kend = t < kLongThreads ? k1 : kb;  // lanes past kLongThreads take no pairs
+    // Straight-line rounds: every pair slot loads (past the segment: its last
+    // pair again) and gathers, and the sums take only the segment's entries
+    // (selects). Predicated loads compiled to branches, and each gather
+    // then waited for all earlier loads: U x 2 dependent scattered round
+    // trips per round instead of one (the hub rows' 47 us in r03-r04).
     for (int64_t k = kb + 2 * t; k < kend; k += (int64_t)2 * U * kLongThreads) {
         f64x2 a[U];
         i32x2 c[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t kk = k + (int64_t)2 * u * kLongThreads;
-            if (kk < k1) {
-                a[u] = __builtin_nontemporal_load(reinterpret_cast<const f64x2 *>(aa + kk));
-                c[u] = __builtin_nontemporal_load(reinterpret_cast<const i32x2 *>(aj + kk));
-            }
-        }
+        for (int u = 0; u < U; ++u)
+            c[u] = __builtin_nontemporal_load(
+                reinterpret_cast<const i32x2 *>(aj + min(k + (int64_t)2 * u * kLongThreads, kl)));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            a[u] = __builtin_nontemporal_load(
+                reinterpret_cast<const f64x2 *>(aa + min(k + (int64_t)2 * u * kLongThreads, kl)));
         double x0[U], x1[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const int64_t kk = k + (int64_t)2 * u * kLongThreads;
-            x0[u] = (kk < k1 && kk >= k0) ? x[c[u].x] : 0.0;
-            x1[u] = (kk + 1 < k1) ? x[c[u].y] : 0.0;
+            x0[u] = x[c[u].x];
+            x1[u] = x[c[u].y];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t kk = k + (int64_t)2 * u * kLongThreads;
-            if (kk < k1 && kk >= k0) acc[u] += a[u].x * x0[u];
-            if (kk + 1 < k1) acc[u] += a[u].y * x1[u];
+            const double s0 = acc[u] + a[u].x * x0[u];
+            acc[u] = (kk < k1 && kk >= k0) ? s0 : acc[u];
+            const double s1 = acc[u] + a[u].y * x1[u];
+            acc[u] = (kk + 1 < k1) ? s1 : acc[u];
         }
     }
     double v = acc[0];
