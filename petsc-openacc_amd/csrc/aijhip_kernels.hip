@@ -224,7 +224,7 @@ __device__ __forceinline__ void stream_block(
     // earlier load, their own predecessors included (vmcnt(0) per pair: four
     // gather round trips per lane instead of one).
     constexpr bool BF = (NTMODE & 64) != 0;
-    static_assert(!(BF && (CODES || SORTED)), "branch-free phase 1: plain and 16-bit gather-ordered forms");
+    static_assert(!(BF && SORTED), "branch-free phase 1: plain, coded and 16-bit gather-ordered forms");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     const BlockDesc d = blk[b];
@@ -241,7 +241,10 @@ __device__ __forceinline__ void stream_block(
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
     // the block's offset dictionary, loaded ahead of the stream (to LDS below)
     int32_t dval[DPT];
-    if constexpr (CODES) {
+    if constexpr (CODES && BF) {  // unconditional (clamped) loads: no branch ahead of the stream's waits
+#pragma unroll
+        for (int i = 0; i < DPT; ++i) dval[i] = sbase[nd > 0 ? dbase + min(t + i * T, nd - 1) : 0];
+    } else if constexpr (CODES) {
 #pragma unroll
         for (int i = 0; i < DPT; ++i)
             if (t + i * T < nd) dval[i] = sbase[dbase + t + i * T];
@@ -266,14 +269,40 @@ __device__ __forceinline__ void stream_block(
     i32x2 cv[ITERS];
     f64x2 xv[ITERS];
     if constexpr (BF) {
-        if (d.nk > 0) {  // (block-uniform) the last pair start is then >= kb
-            const int64_t kl = (k1 - 1) & ~int64_t(1);
+        uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
+        const int64_t kl = (k1 - 1) & ~int64_t(1);  // the last pair start (>= kb when nk > 0)
+        if (d.nk > 0) {  // (block-uniform)
 #pragma unroll
-            for (int it = 0; it < ITERS; ++it)
-                cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + min(kb + 2 * (int64_t)(t + it * T), kl)));
+            for (int it = 0; it < ITERS; ++it) {
+                const int64_t k = min(kb + 2 * (int64_t)(t + it * T), kl);
+                if constexpr (CODES) cw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aj) + (k >> 1));
+                else cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
+            }
 #pragma unroll
             for (int it = 0; it < ITERS; ++it)
                 av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + min(kb + 2 * (int64_t)(t + it * T), kl)));
+        }
+        if constexpr (CODES) {
+#pragma unroll
+            for (int i = 0; i < DPT; ++i)
+                if (t + i * T < nd) cdict[t + i * T] = dval[i];
+            lds_barrier();
+            if (d.nk > 0) {
+                const int ib = code_index_bits(d.nrows);
+                const uint32_t im = (1u << ib) - 1u;
+                const int e0 = (int)(k0 - kb), ne = (int)(k1 - kb), el = (int)(kl - kb);
+#pragma unroll
+                for (int it = 0; it < ITERS; ++it) {
+                    const int e = min(2 * (t + it * T), el);  // the pair this lane loaded
+                    const uint32_t lo = cw[it] & 0xffffu, hi = cw[it] >> 16;
+                    int32_t c0 = d.row0 + (int32_t)(lo >> ib) + cdict[lo & im];
+                    int32_t c1 = d.row0 + (int32_t)(hi >> ib) + cdict[hi & im];
+                    if (e < e0) c0 = c1;
+                    if (e + 1 >= ne) c1 = c0;
+                    xv[it].x = op.gx(c0);
+                    xv[it].y = op.gx(c1);
+                }
+            }
         }
     } else {
         uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
@@ -337,7 +366,7 @@ __device__ __forceinline__ void stream_block(
             if (k < k1) sv[it] = *reinterpret_cast<const uint32_t *>(sslot + k);
         }
     }
-    if constexpr (BF) {  // every pair gathered (the clamped ones re-gather the last pair's columns)
+    if constexpr (BF && !CODES) {  // every pair gathered (the clamped ones re-gather the last pair's columns)
         if (d.nk > 0) {
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) {
@@ -345,7 +374,7 @@ __device__ __forceinline__ void stream_block(
                 xv[it].y = op.gx(cv[it].y);
             }
         }
-    } else if constexpr (!CODES) {  // (the coded form gathered with the decode above)
+    } else if constexpr (!CODES && !BF) {  // (the coded form gathered with the decode above)
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
@@ -1309,6 +1338,10 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,           \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);                \
     return
+            if (P.tune.bf) {
+                if (add) { AIJHIP_SC(true, 96); }
+                AIJHIP_SC(false, 96);
+            }
             if (add) {
                 if (P.tune.nt == 1) { AIJHIP_SC(true, 33); }
                 AIJHIP_SC(true, 32);

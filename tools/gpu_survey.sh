@@ -21,6 +21,8 @@ timeout -k 10 300 python -u tools/tune.py --variants bf --rounds 5 > "$OUT/bf_po
     && echo "bf poisson ok" && grep -h "bitwise\|us_median" "$OUT/bf_poisson.jsonl" | tail -7 || exit 1
 timeout -k 10 300 python -u tools/tune.py --matrix skewed --variants bf --rounds 3 > "$OUT/bf_skewed.jsonl" 2>&1 \
     && echo "bf skewed ok" && grep -h "bitwise\|us_median" "$OUT/bf_skewed.jsonl" | tail -7 || exit 1
+timeout -k 10 300 python -u tools/tune.py --matrix fem_hex --variants bfauto --rounds 3 > "$OUT/bf_fem.jsonl" 2>&1 \
+    && echo "bf fem ok" && grep -h "bitwise\|us_median" "$OUT/bf_fem.jsonl" | tail -7 || exit 1
 timeout -k 10 300 python -u tools/tune.py --matrix skewed --variants overlap --rounds 5 > "$OUT/overlap.jsonl" 2>&1 \
     && echo "overlap ok" && grep us_median "$OUT/overlap.jsonl" | tail -6 || exit 1
 timeout -k 10 300 python -u bench.py --no-cg --no-gamg --no-host-vec --no-flan --no-cpu-baseline --steps 100 \
