@@ -122,11 +122,11 @@ typedef struct aijhip_info {
     int32_t row_patterns;    /* MatMult reads a pattern id per row instead of
                                 aj (AIJHIP_OPT_ROW_PATTERNS): the number of
                                 distinct column - row offset lists; 0 off    */
-    int32_t long_overlap;    /* how the long rows' segments and the wide
-                                blocks run beside the row blocks: 0 after
-                                them, 1 on a side stream, 2 interleaved in
-                                one grid (AIJHIP_OPT_LONG_OVERLAP; fills the
-                                former padding word, layout unchanged)       */
+    int32_t long_overlap;    /* 1 when the long rows' segments and the wide
+                                blocks run on a side stream beside the row
+                                blocks (AIJHIP_OPT_LONG_OVERLAP), else 0
+                                (fills the former padding word, layout
+                                unchanged)                                    */
     int64_t mult_layout_bytes; /* compulsory bytes one MatMult of the plan in
                                 effect moves: mult_bytes for CSR (aj read);
                                 less where the plan reads column codes (10 B
@@ -202,11 +202,8 @@ enum {
                                        step-2 form. Same results              */
     AIJHIP_OPT_LONG_OVERLAP = 9,    /* operands with long rows: 0 the
                                        segments and the wide blocks after the
-                                       row blocks; 1 on a side stream; 2 one
-                                       grid with the segments and wide blocks
-                                       interleaved among the row blocks
-                                       (plain or 16-bit gather-ordered
-                                       layouts, geometries 1 and 6). Same
+                                       row blocks; 1 on a side stream beside
+                                       them (plain MatMult / MatMultAdd). Same
                                        results                                */
     AIJHIP_OPT_ROW_GROUP = 11,      /* withdrawn in ABI 2 (register row groups
                                        measured slower on every operand)     */

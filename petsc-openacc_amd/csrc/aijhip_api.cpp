@@ -75,7 +75,6 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_longs);
     hipFree(P.d_partials);
     hipFree(P.d_segperm);
-    hipFree(P.d_work);
     hipFree(P.d_saj);
     hipFree(P.d_saa);
     hipFree(P.d_sslot);
@@ -374,7 +373,6 @@ int plan_stream(aijhip_mat *A) {
                 return hipfail(e, "plan: column codes");
         }
     }
-    std::vector<int8_t> seg_class;  // per segment: the eighth of x its middle column lies in (long_xcd)
     if (!longs.empty()) {
         if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
@@ -408,51 +406,7 @@ int plan_stream(aijhip_mat *A) {
                 (e = hipMemcpy(P.d_segperm, perm.data(), sizeof(int32_t) * perm.size(), hipMemcpyHostToDevice)) !=
                     hipSuccess)
                 return hipfail(e, "plan: segment placement");
-            seg_class.assign(segs.size(), 0);
-            for (int32_t i = 0; i < P.n_segs; ++i) seg_class[i] = (int8_t)std::min<int64_t>(7, (int64_t)mid[i] * 8 / A->n);
         }
-    }
-    // Tuning::overlap 2: one grid, the segments and the wide blocks spread
-    // evenly among the row blocks (full-row plain or 16-bit gather-ordered
-    // layouts at geometry 1 or 6)
-    if (P.tune.overlap == 2 && (P.n_longs > 0 || P.n_wblocks > 0) && !A->compressed && P.d_code == nullptr &&
-        P.d_pid == nullptr && (P.d_sidx != nullptr || P.d_sslot == nullptr) && (P.tune.geom == 1 || P.tune.geom == 6)) {
-        const int32_t nw = P.d_sidx ? P.n_wblocks : 0;
-        const int32_t nn = P.d_sidx && P.n_wblocks ? P.n_nblocks : P.n_blocks;
-        const int64_t ns = (int64_t)P.n_segs + nw, N = ns + nn;
-        if (N > INT32_MAX) return fail(AIJHIP_ERR_ARG, "plan: grid too large");
-        std::vector<int32_t> work((size_t)N);
-        std::vector<char> special((size_t)N, 0);
-        for (int64_t i = 0; i < ns; ++i) special[(size_t)((2 * i + 1) * N / (2 * ns))] = 1;
-        // segments by the XCD eighth of their columns (all in one class without long_xcd)
-        std::vector<std::vector<int32_t>> part(8);
-        for (int32_t i = 0; i < P.n_segs; ++i) part[seg_class.empty() ? 0 : seg_class[i]].push_back(i);
-        std::vector<size_t> head(8, 0);
-        int32_t next_n = 0, next_w = 0;
-        for (int64_t p = 0; p < N; ++p) {
-            if (!special[(size_t)p]) {
-                work[(size_t)p] = next_n++;
-                continue;
-            }
-            int q = (int)(p & 7);
-            if (head[q] == part[q].size()) {
-                size_t best = 0;
-                for (int c = 0; c < 8; ++c)
-                    if (part[c].size() - head[c] > best) { best = part[c].size() - head[c]; q = c; }
-            }
-            // a wide block where no segment of this XCD's eighth is left, or in turn
-            const bool take_wide = next_w < nw && (head[q] == part[q].size() || (p & 1));
-            if (take_wide) work[(size_t)p] = nn + next_w++;
-            else work[(size_t)p] = -1 - part[q][head[q]++];
-        }
-        size_t placed = 0;
-        for (int c = 0; c < 8; ++c) placed += head[c];
-        if (next_n != nn || next_w != nw || placed != (size_t)P.n_segs)
-            return fail(AIJHIP_ERR_ARG, "plan: interleaved grid miscounted");
-        P.n_work = (int32_t)N;
-        if ((e = dmalloc(&P.d_work, work.size(), &P.bytes)) != hipSuccess ||
-            (e = hipMemcpy(P.d_work, work.data(), sizeof(int32_t) * work.size(), hipMemcpyHostToDevice)) != hipSuccess)
-            return hipfail(e, "plan: interleaved grid");
     }
     // Tuning::overlap: a side stream and its two events for the wide blocks
     // and the long rows (created once per plan that has them)
@@ -473,7 +427,6 @@ int plan_build(aijhip_mat *A) {
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
     P.tune = A->requested_tune;
-    if (const char *v = std::getenv("AIJHIP_STREAM_BF")) P.tune.bf = std::atoi(v);
     const bool auto_sort = P.tune.gsort < 0;
     const bool auto_codes = P.tune.codes < 0;
     const bool auto_patterns = P.tune.patterns < 0;
@@ -926,8 +879,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
         case AIJHIP_OPT_LONG_OVERLAP:
-            if (value < 0 || value > 2)
-                return fail(AIJHIP_ERR_ARG, "long_overlap: 0 off, 1 side stream, 2 one interleaved grid");
+            if (value < 0 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: 0 off, 1 side stream");
             t.overlap = value;
             break;
         case AIJHIP_OPT_HOST_PIPELINE:
@@ -1135,7 +1087,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
     info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
     info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
-    info->long_overlap = A->plan.d_work != nullptr ? 2 : (A->plan.side != nullptr ? 1 : 0);
+    info->long_overlap = A->plan.side != nullptr ? 1 : 0;
     info->mult_layout_bytes = aijhip::mult_layout_bytes(*A);
     return AIJHIP_OK;
 }

@@ -53,9 +53,7 @@ constexpr int kMaxStreamNnzCap = 8192;
 // A row longer than the geometry's nnz_cap leaves the STREAM blocks and is split into
 // segments of at most kLongSegNnz entries, each summed by one workgroup.
 constexpr int kLongSegNnz = 4096;
-// 512 lanes x 4 pairs in flight = one 4096-entry segment per round (the
-// width of the row blocks' workgroups, so k_spmv_mixed runs a segment with
-// every lane and the register budget of a row block)
+// 512 lanes x 4 pairs in flight = one 4096-entry segment per round
 constexpr int kLongThreads = 512;
 
 // One STREAM row block: rows [row0, row0+nrows) of the row list, entries
@@ -98,8 +96,7 @@ struct Tuning {
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
     int overlap = 0;       // MatMult / MatMultAdd with wide blocks or long rows: those launches on a
-                           // side stream concurrent with the row blocks (1), interleaved with the
-                           // row blocks in one grid (2, Plan::d_work), or after them (0)
+                           // side stream concurrent with the row blocks (1), or after them (0)
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
@@ -108,7 +105,6 @@ struct Tuning {
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
                            // offset lists are few), 0 off, 1 on
-    int bf = 0;            // A/B (AIJHIP_STREAM_BF=1): branch-free STREAM phase 1 (NTMODE bit 64)
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is
@@ -169,12 +165,6 @@ struct Plan {
     // segments run on, forked from / joined to the caller's by two events
     hipStream_t side = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    // Tuning::overlap 2: the launch order of k_spmv_mixed's grid (n_work
-    // entries: w >= 0 a row block, narrow then wide; w < 0 segment -1 - w),
-    // the segments and wide blocks spread evenly among the row blocks and
-    // each segment on the XCD of its columns (as d_segperm)
-    int32_t *d_work = nullptr;
-    int32_t n_work = 0;
     // Tuning::gsort: each row block's entries sorted by column (columns,
     // values) and their positions in the block (the products' LDS slots)
     int32_t *d_saj = nullptr;

@@ -190,8 +190,7 @@ __device__ __forceinline__ double row_sum_seq(const double *p, int32_t n, double
 
 // One STREAM row block b of blk[0, nblk) by the T lanes of the calling
 // workgroup; prod (CAP doubles) and cdict (kCodeDictMax ints, column codes
-// only) are the workgroup's LDS. The body of k_spmv_stream and of the row
-// blocks of k_spmv_mixed.
+// only) are the workgroup's LDS.
 // NTMODE bit 0: non-temporal matrix loads (scattered long-row operands).
 template <int T, int CAP, int RPT, bool CROW, int NTMODE, class Op>
 __device__ __forceinline__ void stream_block(
@@ -555,8 +554,7 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
 // lane's U partial sums are combined u = 0..U-1, then the wave tree, then the
 // waves in order: a fixed order.
 // The body, for the first kLongThreads lanes of the calling workgroup (any
-// further lanes only pass the barrier): k_long_partial, and the segments of
-// k_spmv_mixed's grid, with the same sums in the same order. red: >= 4 LDS doubles.
+// further lanes only pass the barrier). red: >= kLongThreads / 64 LDS doubles.
 __device__ __forceinline__ void long_segment(const int32_t id, const LongSeg *__restrict__ seg,
                                              const int32_t *__restrict__ aj, const double *__restrict__ aa,
                                              const double *__restrict__ x, double *__restrict__ partials,
@@ -621,35 +619,6 @@ __global__ __launch_bounds__(kLongThreads) void k_long_partial(
     double *__restrict__ partials, const int32_t *__restrict__ perm) {
     __shared__ double red[kLongThreads / 64];
     long_segment(perm ? perm[blockIdx.x] : (int32_t)blockIdx.x, seg, aj, aa, x, partials, red);
-}
-
-// One grid for MatMult / MatMultAdd of an operand with long rows
-// (Tuning::overlap 2): the long rows' segments and the wide blocks are
-// interleaved with the row blocks in launch order (Plan::d_work: w >= 0 a
-// row block of nb[0, nn) or, past nn, of wb; w < 0 segment -1 - w), so the
-// latency-bound segment workgroups (scattered gathers) run beside the
-// streaming row blocks instead of as a phase of their own. Each part's
-// arithmetic is its own kernel's (stream_block, long_segment): the same
-// bits; k_long_finish sums the partials after this launch.
-template <int T, int CAP, int RPT, int NTM, bool ADD>
-__global__ __launch_bounds__(T) void k_spmv_mixed(
-    const int32_t *__restrict__ work, const BlockDesc *__restrict__ nb, int nn, const BlockDesc *__restrict__ wb,
-    int nw, int exact, const int32_t *__restrict__ rai, const int32_t *__restrict__ naj,
-    const double *__restrict__ naa, const int32_t *__restrict__ sbase, const int32_t *__restrict__ aj,
-    const double *__restrict__ aa, const LongSeg *__restrict__ segs, double *__restrict__ partials,
-    OpMult<ADD> op) {
-    static_assert(T >= kLongThreads, "a segment needs kLongThreads lanes");
-    __shared__ double prod[CAP];
-    const int32_t w = work[blockIdx.x];
-    if (w < 0) {
-        long_segment(-1 - w, segs, aj, aa, op.x, partials, prod);
-    } else if (w < nn) {
-        stream_block<T, CAP, RPT, false, NTM, OpMult<ADD>>(w, nb, nn, exact, rai, nullptr, naj, naa, op, nullptr,
-                                                           nullptr, nullptr, sbase, prod, nullptr);
-    } else {
-        stream_block<T, CAP, RPT, false, 0, OpMult<ADD>>(w - nn, wb, nw, exact, rai, nullptr, aj, aa, op, nullptr,
-                                                         nullptr, nullptr, nullptr, prod, nullptr);
-    }
 }
 
 // One wavefront per long row: the lanes load 64 partials at once and the sum
@@ -1338,16 +1307,14 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,           \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);                \
     return
-            if (P.tune.bf) {
-                if (add) { AIJHIP_SC(true, 96); }
-                AIJHIP_SC(false, 96);
-            }
+            // branch-free phase 1 (bit 64): FEM stand-in 229.7 vs 253.5 us
+            // predicated (profiles/r04/s1/bf_fem.jsonl)
             if (add) {
-                if (P.tune.nt == 1) { AIJHIP_SC(true, 33); }
-                AIJHIP_SC(true, 32);
+                if (P.tune.nt == 1) { AIJHIP_SC(true, 97); }
+                AIJHIP_SC(true, 96);
             }
-            if (P.tune.nt == 1) { AIJHIP_SC(false, 33); }
-            AIJHIP_SC(false, 32);
+            if (P.tune.nt == 1) { AIJHIP_SC(false, 97); }
+            AIJHIP_SC(false, 96);
 #undef AIJHIP_SC
         }
     }
@@ -1368,15 +1335,12 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,         \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);             \
     return
-        if (add && L.ridx) { AIJHIP_SS(true, true, 16); }
-        if (P.tune.bf) {
-            if (add) { AIJHIP_SS(true, false, 80); }
-            if (L.ridx) { AIJHIP_SS(false, true, 80); }
-            AIJHIP_SS(false, false, 80);
-        }
-        if (add) { AIJHIP_SS(true, false, 16); }
-        if (L.ridx) { AIJHIP_SS(false, true, 16); }
-        AIJHIP_SS(false, false, 16);
+        // branch-free phase 1 (bit 64): skewed stand-in 331.9 vs 340.2 us
+        // predicated (profiles/r04/s1/bf_skewed.jsonl)
+        if (add && L.ridx) { AIJHIP_SS(true, true, 80); }
+        if (add) { AIJHIP_SS(true, false, 80); }
+        if (L.ridx) { AIJHIP_SS(false, true, 80); }
+        AIJHIP_SS(false, false, 80);
 #undef AIJHIP_SS
     }
     if (P.d_sidx) {  // split plan, fused dot: the original arrays in one launch
@@ -1395,17 +1359,10 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         AIJHIP_SS(false, false);
 #undef AIJHIP_SS
     }
-    // branch-free phase 1 (NTMODE bit 64, A/B: Tuning::bf)
-    if constexpr (kGeom6) {
-        if (P.tune.bf && !L.ridx) {
-            if (P.tune.nt == 1) {
-                if (add) { AIJHIP_SL(true, false, 65); }
-                AIJHIP_SL(false, false, 65);
-            }
-            if (add) { AIJHIP_SL(true, false, 64); }
-            AIJHIP_SL(false, false, 64);
-        }
-    }
+    // (the plain aj blocks keep the predicated phase 1: branch-free measured
+    // 505.9 vs 492.8 us at 300^3, profiles/r04/s1/bf_poisson.jsonl — for the
+    // 7-point rows the clamped lanes' extra loads and gathers cost more than
+    // the serialised gathers, which hit L1/L2)
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
     // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)
     if (P.tune.nt == 1 && !L.ridx) {
@@ -1450,7 +1407,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
         return hipGetLastError();
     }
     if (P.d_code && P.n_wblocks == 0 && P.tune.geom == 6) {  // column codes (the planner builds them at geometry 6)
-        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, 32, Op>), dim3(P.n_blocks),
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, 96, Op>), dim3(P.n_blocks),
                            dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,
                            reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, op, dpart, stop, nullptr,
                            P.d_cmeta);
@@ -1529,36 +1486,6 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
                                                                       hipSuccess)
             return e;
         sw = P.side;
-    }
-    // Tuning::overlap 2: one interleaved grid (Plan::d_work), then the sums
-    // of the long rows' partials
-    if (P.d_work && !L.ridx && !dpart && !stop) {
-        const bool s16 = P.d_sidx != nullptr;
-        const BlockDesc *nb = s16 && P.n_wblocks ? P.d_nblocks : P.d_blocks;
-        const int32_t nn = s16 && P.n_wblocks ? P.n_nblocks : P.n_blocks, nw = s16 ? P.n_wblocks : 0;
-        const int32_t *naj = s16 ? reinterpret_cast<const int32_t *>(P.d_sidx) : A.d_aj;
-        const double *naa = s16 ? P.d_saa : A.d_aa;
-#define AIJHIP_MX(G, NTM, ADD)                                                                                 \
-    hipLaunchKernelGGL((k_spmv_mixed<AIJHIP_GEOM(G), NTM, ADD>), dim3(P.n_work), dim3(kStreamGeoms[G].threads), 0, s, \
-                       P.d_work, nb, nn, P.d_wblocks, nw, (int)P.tune.exact, L.rai, naj, naa, P.d_sbase, A.d_aj, A.d_aa, \
-                       P.d_segs, P.d_partials, OpMult<ADD>{x, z, y, false})
-#define AIJHIP_MXG(G)                                                   \
-    if (s16) { if (add) AIJHIP_MX(G, 16, true); else AIJHIP_MX(G, 16, false); } \
-    else if (P.tune.nt == 1) { if (add) AIJHIP_MX(G, 1, true); else AIJHIP_MX(G, 1, false); } \
-    else { if (add) AIJHIP_MX(G, 0, true); else AIJHIP_MX(G, 0, false); }
-        if (P.tune.geom == 6) { AIJHIP_MXG(6); }
-        else if (P.tune.geom == 1) { AIJHIP_MXG(1); }
-        else return hipErrorInvalidValue;  // the planner builds d_work at geometries 1 and 6 only
-#undef AIJHIP_MXG
-#undef AIJHIP_MX
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (P.n_longs > 0) {
-            if (add) hipLaunchKernelGGL(k_long_finish<true>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
-                                        P.d_partials, z, y);
-            else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, s, P.d_longs, P.n_longs,
-                                    P.d_partials, z, y);
-        }
-        return hipGetLastError();
     }
     // long rows: segment partials, then their ordered sums
     if (P.n_longs > 0) {

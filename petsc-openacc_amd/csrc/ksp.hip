@@ -157,14 +157,6 @@ struct aijhip_ksp {
     int reason = 0;
     double rnorm = 0.0;
     std::vector<double> hist;
-    // One poll batch of iterations as a HIP graph (aijhip_ksp_solve):
-    // captured on `cap`, replayed on the caller's stream while gkey (x, the
-    // tolerances, every handle of the hierarchy and its plan generation)
-    // is unchanged; graphs_off after a capture failed (direct launches)
-    hipStream_t cap = nullptr;
-    hipGraphExec_t gexec = nullptr;
-    std::vector<uint64_t> gkey;
-    bool graphs_off = false;
 };
 
 namespace {
@@ -180,14 +172,7 @@ void mg_free(aijhip_ksp *K) {
     K->d_mgpart = nullptr;
 }
 
-void graph_free(aijhip_ksp *K) {
-    if (K->gexec) hipGraphExecDestroy(K->gexec);
-    K->gexec = nullptr;
-    K->gkey.clear();
-}
-
 void ksp_free(aijhip_ksp *K) {
-    graph_free(K);
     mg_free(K);
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
     hipFree(K->d_hist); hipFree(K->d_state);
@@ -508,78 +493,6 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
     return AIJHIP_OK;
 }
 
-}  // extern "C"
-
-namespace {
-
-// What a captured batch depends on beyond the KSP's own buffers (which only
-// set-up reallocates, and set-up drops the graph): x, the batch length, the
-// tolerances (k_reduce_iter takes them by value) and every operator handle of
-// the iteration with its plan generation.
-std::vector<uint64_t> batch_key(const aijhip_ksp *K, const double *x, int batch, const CGParams &p) {
-    std::vector<uint64_t> k;
-    auto bits = [](double d) { uint64_t u; std::memcpy(&u, &d, sizeof u); return u; };
-    auto mat = [&](const aijhip_mat *M) {
-        k.push_back((uint64_t)(uintptr_t)M);
-        k.push_back(M ? M->plan_gen : 0);
-    };
-    k.push_back((uint64_t)(uintptr_t)x);
-    k.push_back((uint64_t)batch);
-    k.push_back((uint64_t)K->fused);
-    k.push_back(bits(p.rtol));
-    k.push_back(bits(p.abstol));
-    k.push_back(bits(p.dtol));
-    k.push_back((uint64_t)p.max_it);
-    k.push_back((uint64_t)p.normtype);
-    k.push_back((uint64_t)p.guess_zero);
-    k.push_back((uint64_t)p.pc);
-    mat(K->A);
-    for (const MGLevel &L : K->mg) {
-        mat(L.A);
-        mat(L.P);
-        mat(L.P ? L.P->transpose : nullptr);
-        k.push_back((uint64_t)L.fused);
-    }
-    return k;
-}
-
-// K->gexec holds `batch` iterations for the current key (captured now if it
-// does not): true, or false when capture is unavailable (then the caller
-// launches directly, and K never tries again).
-template <class F>
-bool batch_graph(aijhip_ksp *K, const double *x, int batch, const CGParams &p, F &iterate) {
-    std::vector<uint64_t> key = batch_key(K, x, batch, p);
-    if (K->gexec && key == K->gkey) return true;
-    graph_free(K);
-    if (!K->cap && hipStreamCreateWithFlags(&K->cap, hipStreamNonBlocking) != hipSuccess) {
-        K->cap = nullptr;
-        K->graphs_off = true;
-        (void)hipGetLastError();
-        return false;
-    }
-    hipGraph_t g = nullptr;
-    hipError_t e = hipStreamBeginCapture(K->cap, hipStreamCaptureModeThreadLocal);
-    if (e == hipSuccess) {
-        for (int j = 0; j < batch && e == hipSuccess; ++j) e = iterate(K->cap);
-        const hipError_t e2 = hipStreamEndCapture(K->cap, &g);  // always ends the capture
-        if (e == hipSuccess) e = e2;
-    }
-    if (e == hipSuccess && g) e = hipGraphInstantiate(&K->gexec, g, nullptr, nullptr, 0);
-    if (g) hipGraphDestroy(g);
-    if (e != hipSuccess || !K->gexec) {
-        K->gexec = nullptr;
-        K->graphs_off = true;
-        (void)hipGetLastError();
-        return false;
-    }
-    K->gkey = std::move(key);
-    return true;
-}
-
-}  // namespace
-
-extern "C" {
-
 int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     aijhip::Range range("KSPSolve");
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
@@ -650,10 +563,12 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
         return ie != hipSuccess ? ie : hipGetLastError();
     };
     // iterations in batches between polls (AIJHIP_KSP_POLL overrides the
-    // batch, for A/B); a whole batch is one HIP graph launch (batch_graph)
+    // batch, for A/B). The kernels run back to back (a kernel trace of the
+    // 300^3 CG + GAMG solve: busy 0.996 of its span), and a batch replayed as
+    // one captured HIP graph measured slower (solve 0.194 vs 0.188 s, CG +
+    // Jacobi 0.331 vs 0.325 s per 400 iterations: profiles/r04/s1/graph_ab.txt)
     int batch = 8;
     if (const char *v = std::getenv("AIJHIP_KSP_POLL")) batch = std::max(1, std::atoi(v));
-    const bool graphs = !K->graphs_off && !std::getenv("AIJHIP_KSP_NO_GRAPH");
     int32_t launched = 0;
     K->host_syncs = 0;
     for (;;) {
@@ -662,11 +577,6 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             (e = hipStreamSynchronize(s)) != hipSuccess)
             return khip(e, "KSPSolve poll");
         if (K->h_state->done || launched >= K->max_it) break;
-        if (graphs && launched + batch <= K->max_it && batch_graph(K, x, batch, p, iterate)) {
-            if ((e = hipGraphLaunch(K->gexec, s)) != hipSuccess) return khip(e, "KSPSolve iteration graph");
-            launched += batch;
-            continue;
-        }
         for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched)
             if ((e = iterate(s)) != hipSuccess) return khip(e, "KSPSolve iteration");
     }
@@ -844,7 +754,6 @@ int aijhip_ksp_destroy(aijhip_ksp_t K) {
         KDeviceGuard g(K->A->device);
         (void)hipDeviceSynchronize();
         ksp_free(K);
-        if (K->cap) hipStreamDestroy(K->cap);
     }
     delete K;
     return AIJHIP_OK;

@@ -477,22 +477,19 @@ def test_long_row_segments_skewed(pkg, dev, coracle):
 @pytest.mark.parametrize("gather_sort,geometry,nt", [(-1, -1, -1), (0, -1, -1), (0, 1, 1), (0, 6, 0), (1, 6, -1)])
 def test_long_overlap_is_speed_only(pkg, dev, gather_sort, geometry, nt):
     """AIJHIP_OPT_LONG_OVERLAP: the hub segments and the wide blocks on a
-    side stream (1), or interleaved with the row blocks in one grid (2,
-    k_spmv_mixed): each part's arithmetic is its own kernel's, so the same
-    bits as one stream, for MatMult and MatMultAdd, back to back."""
+    side stream (1), concurrent with the row blocks: the same launches, so
+    the same bits as one stream, for MatMult and MatMultAdd, back to back."""
     ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
     m = len(ai) - 1
     x = to_dev(pkg.splitmix_uniform(m, 7), dev)
     z = to_dev(pkg.splitmix_uniform(m, 8), dev)
     out = []
-    for ov in (0, 1, 2):
+    for ov in (0, 1):
         with pkg.SeqAIJHIP(ai, aj, aa, gather_sort=gather_sort, long_overlap=ov, geometry=geometry,
                            nt_loads=nt) as A:
             inf = A.info()
             assert inf["n_long_rows"] > 0
-            # the one grid is built for the plain and 16-bit gather-ordered layouts
-            # (the 32-bit gather-ordered copy takes the side stream instead)
-            assert inf["long_overlap"] == (ov if ov < 2 or inf["gather_sorted"] in (0, 2) else 1)
+            assert inf["long_overlap"] == ov
             y = torch.empty(m, dtype=torch.float64, device=dev)
             w = torch.empty_like(y)
             for _ in range(3):
@@ -500,9 +497,8 @@ def test_long_overlap_is_speed_only(pkg, dev, gather_sort, geometry, nt):
                 A.mult_add(x, z, w)
             torch.cuda.synchronize()
             out.append((y.cpu().numpy(), w.cpu().numpy()))
-    for k in (1, 2):
-        assert_bits(out[0][0], out[k][0])
-        assert_bits(out[0][1], out[k][1])
+    assert_bits(out[0][0], out[1][0])
+    assert_bits(out[0][1], out[1][1])
 
 
 def test_long_rows_unsorted_columns(pkg, dev, coracle):

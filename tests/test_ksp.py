@@ -154,13 +154,12 @@ def test_gpu_solve_host_vectors_equals_device_solve(pkg, pc, guess):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("pc", ["gamg", "jacobi"])
-def test_gpu_solve_graph_replay_equals_direct_launches(pkg, monkeypatch, pc):
-    """A poll batch of iterations runs as one captured HIP graph
-    (aijhip_ksp_solve): the same kernels with the same arguments, so the
-    iterations, the residual history and x are the direct launches' bits. The
-    graph is re-captured when a tolerance or the operator's plan changes (a
-    re-planned operator is set up again), and a solve that stops mid-batch
-    leaves the rest of the batch as no-ops."""
+def test_gpu_replanned_operator_sets_up_again(pkg, pc):
+    """PCSetUp semantics on a changed operator: re-planning the handle
+    (set_option, MatAssemblyEnd) changes its plan generation, and the next
+    KSPSolve sets the KSP up again (Jacobi diagonal, the GAMG hierarchy, the
+    partial buffers sized by the new plan) instead of reading a stale plan:
+    the solve is a fresh KSP's bit for bit."""
     import torch
     K = importlib.import_module("petsc-openacc_amd.ksp")
     N = 24
@@ -174,28 +173,13 @@ def test_gpu_solve_graph_replay_equals_direct_launches(pkg, monkeypatch, pc):
         torch.cuda.synchronize()
         return ksp.its, np.array(ksp.history()), x.cpu().numpy()
 
-    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, geometry=6) as A:
         with K.KSPCG(A, rtol=1e-12, atol=1e-14, pc=pc) as ksp:
-            monkeypatch.setenv("AIJHIP_KSP_NO_GRAPH", "1")
-            ref = run(ksp)
-            monkeypatch.delenv("AIJHIP_KSP_NO_GRAPH")
-            for _ in range(2):  # captured, then replayed
-                got = run(ksp)
-                assert got[0] == ref[0]
-                assert np.array_equal(got[1].view(np.uint64), ref[1].view(np.uint64))
-                assert np.array_equal(got[2].view(np.uint64), ref[2].view(np.uint64))
-            ksp.set_tolerances(1e-6, 1e-14, 1e5, 10000)  # new key: captured again
-            monkeypatch.setenv("AIJHIP_KSP_NO_GRAPH", "1")
-            ref6 = run(ksp)
-            monkeypatch.delenv("AIJHIP_KSP_NO_GRAPH")
-            got6 = run(ksp)
-            assert got6[0] == ref6[0] < ref[0]
-            assert np.array_equal(got6[2].view(np.uint64), ref6[2].view(np.uint64))
-            # the operator re-planned (its plan generation changes): the KSP is
-            # set up again and the batch captured again
-            A.set_option("geometry", 1)
-            got1 = run(ksp)
-            monkeypatch.setenv("AIJHIP_KSP_NO_GRAPH", "1")
-            ref1 = run(ksp)
-            assert got1[0] == ref1[0]
-            assert np.array_equal(got1[2].view(np.uint64), ref1[2].view(np.uint64))
+            run(ksp)
+            A.set_option("geometry", 8)  # 256-row blocks instead of 512: a new plan, twice the partials
+            got = run(ksp)
+        with K.KSPCG(A, rtol=1e-12, atol=1e-14, pc=pc) as fresh:
+            ref = run(fresh)
+    assert got[0] == ref[0]
+    assert np.array_equal(got[1].view(np.uint64), ref[1].view(np.uint64))
+    assert np.array_equal(got[2].view(np.uint64), ref[2].view(np.uint64))

@@ -126,8 +126,8 @@ def main():
     if args.variants == "patnt":  # row patterns: plain vs non-temporal aa loads
         for nt in (0, 1, 0, 1):
             variants.append(("stream", dict(row_patterns=1, nt_loads=nt)))
-    if args.variants == "overlap":  # hub segments + wide blocks after, on a side stream, or in one interleaved grid
-        for ov in (0, 1, 2, 0, 1, 2):
+    if args.variants == "overlap":  # hub segments + wide blocks after the row blocks or on a side stream
+        for ov in (0, 1, 0, 1):
             variants.append(("stream", dict(long_overlap=ov)))
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
