@@ -21,7 +21,8 @@ def main():
     for f in Path(a.dir).rglob("*kernel_trace.csv"):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0][-60:]))
+                name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("aijhip::", "")
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0][-90:]))
     rows.sort()
     rows = rows[-a.last:]
     busy = sum(e - s for s, e, _ in rows)
