@@ -62,7 +62,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--grid", type=int, default=300, help="per-rank grid edge (N^3 rows per rank)")
     p.add_argument("--kernel", default="auto", choices=["auto", "stream", "scalar", "vector"])
-    p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..5 (default: library's)")
+    p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..12 (default: the library's)")
     p.add_argument("--nt", type=int, default=None, help="STREAM non-temporal matrix loads 0/1")
     p.add_argument("--layout", default="csr", choices=["csr", "auto"],
                    help="what the headline MatMult reads: csr = PETSc's aj/aa (the metric's CSR SpMV; default), "

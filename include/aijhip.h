@@ -164,7 +164,7 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 /* Speed-only knobs of the STREAM kernel; results are identical for every
  * setting. Re-plans on the device. */
 enum {
-    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..11: lanes / LDS entries / rows per block
+    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..12: lanes / LDS entries / rows per block
                                        (DESIGN.md §Kernels); -1 (default):
                                        6 for short rows, 1 for long rows    */
     AIJHIP_OPT_XCD_REMAP = 2,       /* withdrawn in ABI 2 (XCD-contiguous block

@@ -47,6 +47,7 @@ constexpr StreamGeom kStreamGeoms[] = {
     {512, 6142, 512},    // 9: 8 waves, 6 pair-iterations, 48 KiB: an x tile of a +-2100-column band fits
     {512, 8190, 512},    // 10: 8 waves, 8 pair-iterations, 64 KiB
     {512, 2046, 512},    // 11: 8 waves, 2 pair-iterations, 16 KiB
+    {512, 3070, 512},    // 12: 8 waves, 3 pair-iterations, 24 KiB (7-point blocks of ~438 rows: every lane 3 pairs)
 };
 constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
 constexpr int kMaxStreamNnzCap = 8192;
@@ -105,6 +106,7 @@ struct Tuning {
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
                            // offset lists are few), 0 off, 1 on
+    int bf = 0;            // A/B (AIJHIP_STREAM_BF=1): branch-free phase 1 for the plain aj blocks too
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is

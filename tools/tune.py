@@ -132,6 +132,11 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
+    if args.variants == "geo3":  # 3-pair-iteration blocks (geometry 12) vs 6, predicated and branch-free, aj layout
+        for rep in range(2):
+            for g, bf in ((6, "0"), (6, "1"), (12, "0"), (12, "1")):
+                variants.append(("stream", dict(geometry=g, row_patterns=0, column_codes=0,
+                                                env={"AIJHIP_STREAM_BF": bf})))
     if args.variants == "bfauto":  # branch-free phase 1 against the predicated form, the library's automatic layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(env={"AIJHIP_STREAM_BF": bf})))
