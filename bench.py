@@ -62,7 +62,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--grid", type=int, default=300, help="per-rank grid edge (N^3 rows per rank)")
     p.add_argument("--kernel", default="auto", choices=["auto", "stream", "scalar", "vector"])
-    p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..12 (default: the library's)")
+    p.add_argument("--geometry", type=int, default=None, help="STREAM geometry 0..11 (default: the library's)")
     p.add_argument("--nt", type=int, default=None, help="STREAM non-temporal matrix loads 0/1")
     p.add_argument("--layout", default="csr", choices=["csr", "auto"],
                    help="what the headline MatMult reads: csr = PETSc's aj/aa (the metric's CSR SpMV; default), "
@@ -372,7 +372,8 @@ def flan_standins(pkg, dev, reps, cpu_sample):
       skewed — 1,564,794 rows of 45-99 banded entries plus 1e-4 hub rows of
                1e3-2e5 scattered entries (seed 1565): the merge-path
                load-balance stress; STREAM (default: gather-ordered row
-               blocks, hub rows as 4096-entry segments), STREAM exact
+               blocks, hub rows as 4096-entry segments on a side stream
+               beside them; stream_serial: the segments after them), STREAM exact
                (PETSc's order in every row that fits a block) and STREAM on
                PETSc's aj as stored (stream_csr);
       fem_hex — Flan_1565's own structure: a hexahedral mesh of 81x80x80
@@ -381,7 +382,8 @@ def flan_standins(pkg, dev, reps, cpu_sample):
     import torch
     stream = torch.cuda.current_stream()
     out = {}
-    for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(), ("stream", "stream_exact", "stream_csr")),
+    for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(),
+                                 ("stream", "stream_serial", "stream_exact", "stream_csr")),
                                 ("fem_hex", lambda: pkg.fem_hex_csr(), ("stream",))):
         ai, aj, aa = make()
         m, nnz = len(ai) - 1, len(aj)
@@ -396,6 +398,8 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                     A.set_option("exact", 1)
                 if kern == "stream_csr":  # aj as stored: no gather order
                     A.set_option("gather_sort", 0)
+                if kern == "stream_serial":  # the long rows after the row blocks, not beside them
+                    A.set_option("long_overlap", 0)
                 info = A.info()
                 for _ in range(5):
                     A.mult(x, y, stream)
@@ -409,7 +413,7 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                          "csr_effective_GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
                          "geometry": info.get("stream_geometry"), "long_rows": info.get("n_long_rows"),
                          "column_codes": info.get("column_codes"), "gather_sorted": info.get("gather_sorted"),
-                         "row_patterns": info.get("row_patterns")}
+                         "row_patterns": info.get("row_patterns"), "long_overlap": info.get("long_overlap")}
         del x, y
         flat = read_ceiling(nbytes, dev)
         rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],

@@ -164,7 +164,7 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 /* Speed-only knobs of the STREAM kernel; results are identical for every
  * setting. Re-plans on the device. */
 enum {
-    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..12: lanes / LDS entries / rows per block
+    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..11: lanes / LDS entries / rows per block
                                        (DESIGN.md §Kernels); -1 (default):
                                        6 for short rows, 1 for long rows    */
     AIJHIP_OPT_XCD_REMAP = 2,       /* withdrawn in ABI 2 (XCD-contiguous block
@@ -202,8 +202,10 @@ enum {
                                        step-2 form. Same results              */
     AIJHIP_OPT_LONG_OVERLAP = 9,    /* operands with long rows: 0 the
                                        segments and the wide blocks after the
-                                       row blocks; 1 on a side stream beside
-                                       them (plain MatMult / MatMultAdd). Same
+                                       row blocks; 1 or -1 (default) on a side
+                                       stream beside them (plain MatMult /
+                                       MatMultAdd; forked from and joined to
+                                       the caller's stream by events). Same
                                        results                                */
     AIJHIP_OPT_ROW_GROUP = 11,      /* withdrawn in ABI 2 (register row groups
                                        measured slower on every operand)     */

@@ -410,7 +410,7 @@ int plan_stream(aijhip_mat *A) {
     }
     // Tuning::overlap: a side stream and its two events for the wide blocks
     // and the long rows (created once per plan that has them)
-    if (P.tune.overlap > 0 && (P.n_wblocks > 0 || P.n_longs > 0)) {
+    if (P.tune.overlap != 0 && (P.n_wblocks > 0 || P.n_longs > 0)) {
         if ((e = hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming)) != hipSuccess)
@@ -427,7 +427,6 @@ int plan_build(aijhip_mat *A) {
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
     P.tune = A->requested_tune;
-    if (const char *v = std::getenv("AIJHIP_STREAM_BF")) P.tune.bf = std::atoi(v);
     const bool auto_sort = P.tune.gsort < 0;
     const bool auto_codes = P.tune.codes < 0;
     const bool auto_patterns = P.tune.patterns < 0;
@@ -880,7 +879,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
         case AIJHIP_OPT_LONG_OVERLAP:
-            if (value < 0 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: 0 off, 1 side stream");
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: -1 auto (on), 0 off, 1 side stream");
             t.overlap = value;
             break;
         case AIJHIP_OPT_HOST_PIPELINE:

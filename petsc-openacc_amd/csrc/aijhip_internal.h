@@ -47,7 +47,6 @@ constexpr StreamGeom kStreamGeoms[] = {
     {512, 6142, 512},    // 9: 8 waves, 6 pair-iterations, 48 KiB: an x tile of a +-2100-column band fits
     {512, 8190, 512},    // 10: 8 waves, 8 pair-iterations, 64 KiB
     {512, 2046, 512},    // 11: 8 waves, 2 pair-iterations, 16 KiB
-    {512, 3070, 512},    // 12: 8 waves, 3 pair-iterations, 24 KiB (7-point blocks of ~438 rows: every lane 3 pairs)
 };
 constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
 constexpr int kMaxStreamNnzCap = 8192;
@@ -96,8 +95,9 @@ struct Tuning {
                          // 0 plain, 1 non-temporal
     bool exact = false;    // always sum rows sequentially (PETSc order), even long ones
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
-    int overlap = 0;       // MatMult / MatMultAdd with wide blocks or long rows: those launches on a
-                           // side stream concurrent with the row blocks (1), or after them (0)
+    int overlap = -1;      // MatMult / MatMultAdd with wide blocks or long rows: those launches on a
+                           // side stream concurrent with the row blocks (1; -1 auto = 1), or after
+                           // them (0). Skewed stand-in 299.0 vs 310.5 us (profiles/r04/s2/)
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
@@ -106,7 +106,6 @@ struct Tuning {
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
                            // offset lists are few), 0 off, 1 on
-    int bf = 0;            // A/B (AIJHIP_STREAM_BF=1): branch-free phase 1 for the plain aj blocks too
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is

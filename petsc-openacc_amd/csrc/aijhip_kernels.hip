@@ -1359,17 +1359,6 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         AIJHIP_SS(false, false);
 #undef AIJHIP_SS
     }
-    // branch-free phase 1 on the plain blocks (A/B: Tuning::bf; geometries 6 and 12)
-    if constexpr (kGeom6 || (T == kStreamGeoms[12].threads && CAP == kStreamGeoms[12].nnz_cap && RPT == 1)) {
-        if (P.tune.bf && !L.ridx) {
-            if (P.tune.nt == 1) {
-                if (add) { AIJHIP_SL(true, false, 65); }
-                AIJHIP_SL(false, false, 65);
-            }
-            if (add) { AIJHIP_SL(true, false, 64); }
-            AIJHIP_SL(false, false, 64);
-        }
-    }
     // (the plain aj blocks keep the predicated phase 1: branch-free measured
     // 505.9 vs 492.8 us at 300^3, profiles/r04/s1/bf_poisson.jsonl — for the
     // 7-point rows the clamped lanes' extra loads and gathers cost more than
@@ -1424,7 +1413,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
                            P.d_cmeta);
         return hipGetLastError();
     }
-    static_assert(kNumStreamGeoms == 13, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
 #define AIJHIP_OG(G)                                                                                             \
     case G:                                                                                                      \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_blocks),                      \
@@ -1434,7 +1423,6 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
         AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8); AIJHIP_OG(9); AIJHIP_OG(10); AIJHIP_OG(11);
-        AIJHIP_OG(12);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_OG
@@ -1447,7 +1435,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
     if (P.kernel != AIJHIP_KERNEL_STREAM || A.compressed || P.n_longs > 0 || b0 < 0 || b0 + nb > P.n_blocks)
         return hipErrorInvalidValue;
     if (nb <= 0) return hipSuccess;
-    static_assert(kNumStreamGeoms == 13, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
 #define AIJHIP_BG(G)                                                                                             \
     case G:                                                                                                      \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, OpMult<false>>), dim3(nb),                   \
@@ -1458,7 +1446,6 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
     switch (P.tune.geom) {
         AIJHIP_BG(0); AIJHIP_BG(1); AIJHIP_BG(2); AIJHIP_BG(3); AIJHIP_BG(4);
         AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8); AIJHIP_BG(9); AIJHIP_BG(10); AIJHIP_BG(11);
-        AIJHIP_BG(12);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_BG
@@ -1491,7 +1478,7 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     // latency-bound launches) on the side stream, forked from s before any of
     // them and joined back after; the row blocks on s meanwhile. Every launch
     // writes its own rows of y, so the order between them is free.
-    const bool ovl = P.tune.overlap > 0 && P.side && !L.ridx && !dpart && !stop &&
+    const bool ovl = P.tune.overlap != 0 && P.side && !L.ridx && !dpart && !stop &&
                      (P.n_wblocks > 0 || P.n_longs > 0);
     hipStream_t sw = s;
     if (ovl) {
@@ -1512,13 +1499,12 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     }
     // Every geometry is dispatched explicitly: the kernel's LDS size must be
     // the one the plan's row blocks were cut for.
-    static_assert(kNumStreamGeoms == 13, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
     if (P.n_blocks > 0) {
 #define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, P, L, x, z, y, add, s, dpart, stop, sw); break
         switch (P.tune.geom) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
             AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
-            AIJHIP_SG(12);
             default: return hipErrorInvalidValue;
         }
 #undef AIJHIP_SG

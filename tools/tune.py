@@ -132,11 +132,6 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
-    if args.variants == "geo3":  # 3-pair-iteration blocks (geometry 12) vs 6, predicated and branch-free, aj layout
-        for rep in range(2):
-            for g, bf in ((6, "0"), (6, "1"), (12, "0"), (12, "1")):
-                variants.append(("stream", dict(geometry=g, row_patterns=0, column_codes=0,
-                                                env={"AIJHIP_STREAM_BF": bf})))
     if args.variants == "bfauto":  # branch-free phase 1 against the predicated form, the library's automatic layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(env={"AIJHIP_STREAM_BF": bf})))
@@ -164,7 +159,7 @@ def main():
         A.set_option("geometry", opts.get("geometry", -1))  # -1: the library's choice
         A.set_option("exact", opts.get("exact", 0))
         A.set_option("long_xcd", opts.get("long_xcd", 1))
-        A.set_option("long_overlap", opts.get("long_overlap", 0))
+        A.set_option("long_overlap", opts.get("long_overlap", -1))
         A.set_option("gather_sort", opts.get("gather_sort", -1))
         A.set_option("column_codes", opts.get("column_codes", -1))
         A.set_option("row_patterns", opts.get("row_patterns", -1))
