@@ -550,6 +550,12 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # no launcher: start the N ranks here, before anything touches the GPU
         raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
+    # Exactly one line reaches stdout: everything else any layer prints there
+    # (gloo's "[Gloo] Rank 0 is connected ...", RCCL / HIP runtime notices)
+    # goes to stderr, and the JSON line is written to the saved descriptor.
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -968,7 +974,7 @@ def main():
                 "sample": f"{reps_all} whole-operand {G}^3 SpMVs, OpenMP static row blocks on {threads} threads, "
                           f"{t_all * 1e3:.1f} ms each; oracle/matmult_seqaij.c oracle_matmult_seqaij_omp",
             }
-        print(json.dumps(out), flush=True)
+        os.write(line_fd, (json.dumps(out) + "\n").encode())
 
     if distributed:
         dist.destroy_process_group()

@@ -1544,13 +1544,15 @@ strength_done:
             for (int z = 0; z < 2 && e == hipSuccess; ++z) e = hipEventCreateWithFlags(&ev[z], hipEventDisableTiming);
             for (int c = 0; c < 2 && c < kChunks && e == hipSuccess; ++c) e = fetch(c);
             std::fill(agg, agg + m, -1);
+            std::vector<uint64_t> taken(((size_t)m + 63) / 64, 0);
             na = 0;
             double t_wait = 0.0, t_pass = 0.0;  // (logged: copy-bound or pass-bound)
             for (int c = 0; c < kChunks && e == hipSuccess; ++c) {
                 const auto w0 = std::chrono::steady_clock::now();
                 if ((e = hipEventSynchronize(ev[c & 1])) != hipSuccess) break;
                 const auto w1 = std::chrono::steady_clock::now();
-                na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_slot[c & 1], agg, na, h_si[r[c]]);
+                na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_slot[c & 1], agg, taken.data(), na,
+                                                        h_si[r[c]]);
                 if (c + 2 < kChunks) e = fetch(c + 2);
                 t_wait += std::chrono::duration<double, std::milli>(w1 - w0).count();
                 t_pass += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w1).count();

@@ -18,11 +18,12 @@ namespace aijhip_gamg {
 // phase 3 roots aggregates at what is left (returns the final count).
 int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg);
 // The same pass over rows [r0, r1) (agg already holds rows < r0's result, -1
-// elsewhere; na = the count so far): a node reads only its own row of S, so
-// rows may arrive in order while earlier ones are processed.
+// elsewhere; taken: one bit per node, set exactly where agg != -1; na = the
+// count so far): a node reads only its own row of S, so rows may arrive in
+// order while earlier ones are processed.
 // (sj holds S's columns from entry sj0 on: sj[k - sj0] is entry k)
 int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const int32_t *sj, int32_t *agg,
-                              int32_t na, int64_t sj0 = 0);
+                              uint64_t *taken, int32_t na, int64_t sj0 = 0);
 int32_t aggregate_phase3(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t na);
 
 // Host continuation: the hierarchy below operator (m, ai, aj, aa) whose

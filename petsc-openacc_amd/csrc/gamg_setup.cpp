@@ -380,32 +380,32 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
 namespace aijhip_gamg {
 
 int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const int32_t *sj, int32_t *agg,
-                              int32_t na, int64_t sj0) {
-    // The pass is a chain of dependent loads (row start, first column, its
-    // id): the ids of row i + 32's first two columns and row i + 64's columns
-    // are prefetched (300^3 level 1 on the build host: 75 -> 59 ms) — only
-    // for nodes still free now (an aggregated node stays aggregated and its
-    // row is never read; most are, so S is no longer streamed whole: a
-    // 148^3 27-point S on the build host 26.5 -> 16.1 ms, same aggregates).
-    constexpr int32_t kAhead = 32;
+                              uint64_t *taken, int32_t na, int64_t sj0) {
+    // The pass is a chain of dependent loads (row start, its columns, their
+    // state). The state it tests is `taken`, one bit per node (agg[j] != -1):
+    // 400 KB for the 3.27 M nodes of 300^3's level 1, so the random tests hit
+    // the core's L2 instead of the 13 MB agg array; agg is only written. Rows
+    // of nodes still free are prefetched 64 ahead (an aggregated node's row
+    // is never read; most are, so S is not streamed whole).
+    constexpr int32_t kAhead = 64;
+    auto is_taken = [taken](int32_t j) { return (taken[j >> 6] >> (j & 63)) & 1u; };
+    auto take = [taken, agg](int32_t j, int32_t a) {
+        agg[j] = a;
+        taken[j >> 6] |= uint64_t(1) << (j & 63);
+    };
     for (int32_t i = r0; i < r1; ++i) {
-        if (i + 2 * kAhead < r1) {
-            const int32_t ia = i + kAhead, ib = i + 2 * kAhead;
-            if (agg[ia] == -1 && si[ia + 1] - si[ia] >= 2) {
-                const int32_t *row = sj + (si[ia] - sj0);
-                __builtin_prefetch(&agg[row[0]], 0, 3);
-                __builtin_prefetch(&agg[row[1]], 0, 3);
-            }
-            if (agg[ib] == -1) __builtin_prefetch(sj + (si[ib] - sj0), 0, 3);
+        if (i + kAhead < r1) {
+            const int32_t ib = i + kAhead;
+            if (!is_taken(ib)) __builtin_prefetch(sj + (si[ib] - sj0), 0, 3);
         }
-        if (agg[i] != -1 || si[i] == si[i + 1]) continue;
+        if (is_taken(i) || si[i] == si[i + 1]) continue;
         const int32_t *row = sj + (si[i] - sj0);
         const int32_t len = si[i + 1] - si[i];
         bool free_all = true;
-        for (int32_t k = 0; k < len && free_all; ++k) free_all = agg[row[k]] == -1;
+        for (int32_t k = 0; k < len && free_all; ++k) free_all = !is_taken(row[k]);
         if (!free_all) continue;
-        agg[i] = na;
-        for (int32_t k = 0; k < len; ++k) agg[row[k]] = na;
+        take(i, na);
+        for (int32_t k = 0; k < len; ++k) take(row[k], na);
         ++na;
     }
     return na;
@@ -413,7 +413,8 @@ int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const i
 
 int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg) {
     std::fill(agg, agg + m, -1);
-    return aggregate_phase1_rows(0, m, si, sj, agg, 0);
+    std::vector<uint64_t> taken(((size_t)m + 63) / 64, 0);
+    return aggregate_phase1_rows(0, m, si, sj, agg, taken.data(), 0);
 }
 
 int32_t aggregate_phase3(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t na) {
