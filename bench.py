@@ -401,7 +401,10 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                 if kern == "stream_serial":  # the long rows after the row blocks, not beside them
                     A.set_option("long_overlap", 0)
                 info = A.info()
-                for _ in range(5):
+                # warm-up of ~10 ms: the first leg follows the PCIe-bound host-vector
+                # leg, and with 5 launches it read 6-8 % slow (profiles/r04/bench_r04e.json
+                # vs s3/skewed_exact.jsonl)
+                for _ in range(30):
                     A.mult(x, y, stream)
                 mean, med, mn = time_launches(lambda: A.mult(x, y, stream), stream, reps)
             finally:
