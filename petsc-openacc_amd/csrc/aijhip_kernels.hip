@@ -224,12 +224,6 @@ __device__ __forceinline__ void stream_block(
     // gather round trips per lane instead of one).
     constexpr bool BF = (NTMODE & 64) != 0;
     static_assert(!(BF && SORTED), "branch-free phase 1: plain, coded and 16-bit gather-ordered forms");
-    // bit 7 (A/B): predicated loads, unconditional gathers (a lane past the
-    // block gathers x[0]): one gather round trip after
-    // the stream instead of a serialised one per pair, without the clamped
-    // lanes' extra aa / aj loads of the branch-free form
-    constexpr bool UG = (NTMODE & 128) != 0;
-    static_assert(!(UG && (BF || CODES || SORTED || S16)), "unconditional gathers: plain aj blocks");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     const BlockDesc d = blk[b];
@@ -377,15 +371,6 @@ __device__ __forceinline__ void stream_block(
             for (int it = 0; it < ITERS; ++it) {
                 xv[it].x = op.gx(cv[it].x);
                 xv[it].y = op.gx(cv[it].y);
-            }
-        }
-    } else if constexpr (UG) {
-        if (d.nk > 0) {  // (block-uniform: n >= 1 then, so x[0] exists)
-#pragma unroll
-            for (int it = 0; it < ITERS; ++it) {
-                const bool in = kb + 2 * (int64_t)(t + it * T) < k1;  // (the lane loaded cv[it])
-                xv[it].x = op.gx(in ? cv[it].x : 0);
-                xv[it].y = op.gx(in ? cv[it].y : 0);
             }
         }
     } else if constexpr (!CODES && !BF) {  // (the coded form gathered with the decode above)
@@ -1373,17 +1358,6 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         if (L.ridx) { AIJHIP_SS(false, true); }
         AIJHIP_SS(false, false);
 #undef AIJHIP_SS
-    }
-    // unconditional gathers on the plain blocks (A/B: Tuning::ug)
-    if constexpr (kGeom6) {
-        if (P.tune.ug && !L.ridx) {
-            if (P.tune.nt == 1) {
-                if (add) { AIJHIP_SL(true, false, 129); }
-                AIJHIP_SL(false, false, 129);
-            }
-            if (add) { AIJHIP_SL(true, false, 128); }
-            AIJHIP_SL(false, false, 128);
-        }
     }
     // (the plain aj blocks keep the predicated phase 1: branch-free measured
     // 505.9 vs 492.8 us at 300^3, profiles/r04/s1/bf_poisson.jsonl — for the

@@ -132,9 +132,6 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
-    if args.variants == "ug":  # unconditional gathers on the plain blocks (AIJHIP_STREAM_UG), aj layout
-        for ug in ("0", "1", "0", "1"):
-            variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_UG": ug})))
     if args.variants == "exact":  # PETSc's sequential row order in every block (exact) against the split sums
         for ex in (0, 1, 0, 1):
             variants.append(("stream", dict(exact=ex)))
