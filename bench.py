@@ -401,11 +401,14 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                 if kern == "stream_serial":  # the long rows after the row blocks, not beside them
                     A.set_option("long_overlap", 0)
                 info = A.info()
-                # warm-up of ~10 ms: the first leg follows the PCIe-bound host-vector
-                # leg, and with 5 launches it read 6-8 % slow (profiles/r04/bench_r04e.json
-                # vs s3/skewed_exact.jsonl)
-                for _ in range(30):
-                    A.mult(x, y, stream)
+                # warm-up of >= 50 ms of launches: the first leg follows the
+                # PCIe-bound host-vector leg, and after 5 launches it read 6-8 %
+                # slow (profiles/r04/bench_r04e.json vs s3/skewed_exact.jsonl)
+                t_w = time.perf_counter()
+                while time.perf_counter() - t_w < 0.05:
+                    for _ in range(10):
+                        A.mult(x, y, stream)
+                    torch.cuda.synchronize()
                 mean, med, mn = time_launches(lambda: A.mult(x, y, stream), stream, reps)
             finally:
                 A.destroy()

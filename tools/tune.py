@@ -132,6 +132,9 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
+    if args.variants == "geoms":  # the default plan at the geometries of 256 / 512 lanes and 2 / 4 pair-iterations
+        for g in (6, 8, 11, 0, 6, 8, 11, 0):
+            variants.append(("stream", dict(geometry=g)))
     if args.variants == "exact":  # PETSc's sequential row order in every block (exact) against the split sums
         for ex in (0, 1, 0, 1):
             variants.append(("stream", dict(exact=ex)))
