@@ -427,7 +427,6 @@ int plan_build(aijhip_mat *A) {
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
     P.tune = A->requested_tune;
-    if (const char *v = std::getenv("AIJHIP_STREAM_XP")) P.tune.xp = std::atoi(v);
     const bool auto_sort = P.tune.gsort < 0;
     const bool auto_codes = P.tune.codes < 0;
     const bool auto_patterns = P.tune.patterns < 0;

@@ -106,7 +106,6 @@ struct Tuning {
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
                            // offset lists are few), 0 off, 1 on
-    int xp = 0;            // A/B (AIJHIP_STREAM_XP=1): XCD-paired block order (NTMODE bit 256)
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is

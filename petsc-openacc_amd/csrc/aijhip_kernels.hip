@@ -458,20 +458,8 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     const int32_t *__restrict__ sbase) {
     __shared__ double prod[CAP];
     __shared__ int32_t cdict[(NTMODE & 32) ? kCodeDictMax : 1];
-    int b = (int)blockIdx.x;
-    if constexpr ((NTMODE & 256) != 0) {
-        // (A/B) XCD pairs: launch slot w runs on XCD w % 8 under round-robin
-        // placement; give each XCD two consecutive blocks in turn, so a
-        // block's +-1-row-band neighbour (the 7-point +-N x lines) shares its
-        // L2 while blocks a plane apart (176 = 2 x 88 blocks at 300^3) still do
-        const int full = nblk & ~15;
-        if (b < full) {
-            const int x = b & 7, k = b >> 3;
-            b = ((k >> 1) * 8 + x) * 2 + (k & 1);
-        }
-    }
-    stream_block<T, CAP, RPT, CROW, (NTMODE & 255), Op>(b, blk, nblk, exact, rai, ridx, aj, aa, op, dpart, stop,
-                                                        sslot, sbase, prod, cdict);
+    stream_block<T, CAP, RPT, CROW, NTMODE, Op>((int)blockIdx.x, blk, nblk, exact, rai, ridx, aj, aa, op, dpart, stop,
+                                                sslot, sbase, prod, cdict);
 }
 
 // Row patterns (Tuning::patterns; short-row operands whose rows follow a
@@ -1370,13 +1358,6 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
         if (L.ridx) { AIJHIP_SS(false, true); }
         AIJHIP_SS(false, false);
 #undef AIJHIP_SS
-    }
-    // XCD-paired block order on the plain blocks (A/B: Tuning::xp)
-    if constexpr (kGeom6) {
-        if (P.tune.xp && !L.ridx) {
-            if (add) { AIJHIP_SL(true, false, 256); }
-            AIJHIP_SL(false, false, 256);
-        }
     }
     // (the plain aj blocks keep the predicated phase 1: branch-free measured
     // 505.9 vs 492.8 us at 300^3, profiles/r04/s1/bf_poisson.jsonl — for the

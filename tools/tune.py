@@ -132,9 +132,6 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
-    if args.variants == "xp":  # XCD-paired block order (AIJHIP_STREAM_XP) against round-robin, aj layout
-        for xp in ("0", "1", "0", "1"):
-            variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_XP": xp})))
     if args.variants == "geoms":  # the default plan at the geometries of 256 / 512 lanes and 2 / 4 pair-iterations
         for g in (6, 8, 11, 0, 6, 8, 11, 0):
             variants.append(("stream", dict(geometry=g)))
