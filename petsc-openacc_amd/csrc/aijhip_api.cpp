@@ -799,7 +799,7 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
     A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
     if (!like) {  // the set-up's own operators: one copy of the entries, no code dictionaries or patterns
         A->requested_tune.gsort = 0;  // (plan time); block-relative columns where every block fits 2^16
-        A->requested_tune.codes = 2;
+        A->requested_tune.codes = std::getenv("AIJHIP_GAMG_REL0") ? 0 : 2;  // (A/B switch, temporary)
         A->requested_tune.patterns = 0;
     }
     aijhip::HostVec<int32_t> h_ai;

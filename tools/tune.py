@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--variants", default="stream")
-    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx", "skewed_blocksort", "fem_hex"])
+    ap.add_argument("--matrix", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "skewed_localx", "skewed_blocksort", "fem_hex", "banded"])
     ap.add_argument("--file", default=None, help="a MatrixMarket (.mtx) or PETSc binary operand, e.g. Flan_1565.mtx")
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
@@ -58,6 +58,15 @@ def main():
         ai, aj, aa = pkg.poisson_csr(args.grid)
     elif args.matrix == "fem_hex":  # Flan_1565's structure: hexahedral mesh, 3 dofs per node
         ai, aj, aa = pkg.fem_hex_csr()
+    elif args.matrix == "banded":  # 3 M rows of ~30 random columns within +-20000 (GAMG-coarse-like)
+        rng = np.random.default_rng(5)
+        m, w = 3_000_000, 30
+        c = np.sort(np.clip(np.arange(m)[:, None] + rng.integers(-20000, 20001, (m, w)), 0, m - 1), axis=1)
+        keep = np.ones_like(c, dtype=bool)
+        keep[:, 1:] = c[:, 1:] != c[:, :-1]
+        ai = np.concatenate([[0], np.cumsum(keep.sum(axis=1))]).astype(np.int32)
+        aj = c[keep].astype(np.int32)
+        aa = rng.uniform(-1, 1, len(aj))
     else:
         ai, aj, aa = pkg.skewed_csr()
         if args.matrix in ("skewed_nohub", "skewed_localx", "skewed_blocksort"):  # the FEM-like rows only (hub rows emptied)
@@ -132,6 +141,9 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
+    if args.variants == "rel":  # block-relative columns (column_codes auto) against aj, gather order off
+        for cc in (-1, 0, -1, 0):
+            variants.append(("stream", dict(gather_sort=0, row_patterns=0, column_codes=cc)))
     if args.variants == "geoms":  # the default plan at the geometries of 256 / 512 lanes and 2 / 4 pair-iterations
         for g in (6, 8, 11, 0, 6, 8, 11, 0):
             variants.append(("stream", dict(geometry=g)))
