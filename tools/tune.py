@@ -141,9 +141,11 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
-    if args.variants == "rel":  # block-relative columns (column_codes auto) against aj, gather order off
-        for cc in (-1, 0, -1, 0):
-            variants.append(("stream", dict(gather_sort=0, row_patterns=0, column_codes=cc)))
+    if args.variants == "rel":  # block-relative columns (column_codes auto, gather order off) against aj and the default
+        for rep in range(2):
+            variants += [("stream", dict(gather_sort=0, row_patterns=0, column_codes=-1)),
+                         ("stream", dict(gather_sort=0, row_patterns=0, column_codes=0)),
+                         ("stream", {})]
     if args.variants == "geoms":  # the default plan at the geometries of 256 / 512 lanes and 2 / 4 pair-iterations
         for g in (6, 8, 11, 0, 6, 8, 11, 0):
             variants.append(("stream", dict(geometry=g)))
