@@ -86,8 +86,6 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_cmeta);
     hipFree(P.d_pid);
     hipFree(P.d_ptab);
-    hipFree(P.d_rel);
-    hipFree(P.d_rbase);
     if (P.side) hipStreamDestroy(P.side);
     if (P.ev_fork) hipEventDestroy(P.ev_fork);
     if (P.ev_join) hipEventDestroy(P.ev_join);
@@ -314,7 +312,7 @@ int plan_stream(aijhip_mat *A) {
     // for the row blocks whose offset dictionaries fit (geometry 6, plain
     // full-row launches: not with the x tiles or the gather order); when
     // some do not fit, they are launched from aj
-    if (P.tune.codes == 1 && P.tune.geom == 6 && !blocks.empty() && P.d_pid == nullptr && !A->compressed &&
+    if (P.tune.codes > 0 && P.tune.geom == 6 && !blocks.empty() && P.d_pid == nullptr && !A->compressed &&
         P.d_sslot == nullptr) {
         int32_t *d_cnt = nullptr;
         std::vector<int32_t> cnt(blocks.size());
@@ -373,67 +371,6 @@ int plan_stream(aijhip_mat *A) {
                                                P.d_cmeta, P.d_code)) != hipSuccess ||
                 (e = hipDeviceSynchronize()) != hipSuccess)
                 return hipfail(e, "plan: column codes");
-        }
-    }
-    // block-relative 16-bit columns (Plan::d_rel): the automatic column
-    // layout of the final plan when the offset dictionaries did not fit (or
-    // were not tried) and no other layout was chosen, and the only one the
-    // GAMG set-up's own operators try (Tuning::codes 2: no dictionary pass at
-    // plan time), at the geometries the locality analysis picks for such
-    // operands (1 and 6); kept when the blocks spanning < 2^16 columns hold
-    // >= 90 % of the entries
-    if (((A->requested_tune.codes < 0 && P.tune.codes == 0) || P.tune.codes == 2) && P.d_code == nullptr &&
-        P.d_pid == nullptr &&
-        P.d_sslot == nullptr && P.d_sidx == nullptr && !A->compressed && (P.tune.geom == 1 || P.tune.geom == 6) &&
-        !blocks.empty() && A->n > 0) {
-        int2 *d_rng = nullptr;
-        std::vector<int2> rng(blocks.size());
-        if ((e = dmalloc(&d_rng, blocks.size(), nullptr)) != hipSuccess ||
-            (e = aijhip::block_column_ranges(*A, P.d_blocks, P.n_blocks, d_rng)) != hipSuccess ||
-            (e = hipMemcpy(rng.data(), d_rng, sizeof(int2) * rng.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
-            hipFree(d_rng);
-            return hipfail(e, "plan: block column ranges");
-        }
-        hipFree(d_rng);
-        int64_t narrow_nz = 0, nz_all = 0;
-        for (size_t b = 0; b < blocks.size(); ++b) {
-            nz_all += blocks[b].nk;
-            if (rng[b].y <= 65536) narrow_nz += blocks[b].nk;
-        }
-        if (narrow_nz > 0 && 10 * narrow_nz >= 9 * nz_all) {
-            std::vector<BlockDesc> nb, wb;
-            std::vector<int32_t> base;
-            for (size_t b = 0; b < blocks.size(); ++b) {
-                if (rng[b].y <= 65536) {
-                    nb.push_back(blocks[b]);
-                    base.push_back(rng[b].x);
-                } else {
-                    wb.push_back(blocks[b]);
-                }
-            }
-            const size_t nrel = (size_t)A->nz + 2;
-            if ((e = dmalloc(&P.d_rel, nrel, &P.bytes)) != hipSuccess ||
-                (e = hipMemset(P.d_rel, 0, sizeof(uint16_t) * nrel)) != hipSuccess ||
-                (e = dmalloc(&P.d_rbase, base.size(), &P.bytes)) != hipSuccess ||
-                (e = hipMemcpy(P.d_rbase, base.data(), sizeof(int32_t) * base.size(), hipMemcpyHostToDevice)) !=
-                    hipSuccess)
-                return hipfail(e, "plan: block-relative columns");
-            if (!wb.empty()) {
-                if ((e = dmalloc(&P.d_nblocks, nb.size(), &P.bytes)) != hipSuccess ||
-                    (e = dmalloc(&P.d_wblocks, wb.size(), &P.bytes)) != hipSuccess ||
-                    (e = hipMemcpy(P.d_nblocks, nb.data(), sizeof(BlockDesc) * nb.size(), hipMemcpyHostToDevice)) !=
-                        hipSuccess ||
-                    (e = hipMemcpy(P.d_wblocks, wb.data(), sizeof(BlockDesc) * wb.size(), hipMemcpyHostToDevice)) !=
-                        hipSuccess)
-                    return hipfail(e, "plan: block-relative block lists");
-                P.n_nblocks = (int32_t)nb.size();
-                P.n_wblocks = (int32_t)wb.size();
-                for (const BlockDesc &d : wb) P.nz_wide += d.nk;
-            }
-            if ((e = aijhip::rel16_write(*A, wb.empty() ? P.d_blocks : P.d_nblocks, (int32_t)nb.size(), P.d_rbase,
-                                         P.d_rel)) != hipSuccess ||
-                (e = hipDeviceSynchronize()) != hipSuccess)
-                return hipfail(e, "plan: block-relative columns");
         }
     }
     if (!longs.empty()) {
@@ -797,9 +734,9 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
     A->d_aj = d_aj;
     A->d_aa = d_aa;
     A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
-    if (!like) {  // the set-up's own operators: one copy of the entries, no code dictionaries or patterns
-        A->requested_tune.gsort = 0;  // (plan time); block-relative columns where every block fits 2^16
-        A->requested_tune.codes = std::getenv("AIJHIP_GAMG_REL0") ? 0 : 2;  // (A/B switch, temporary)
+    if (!like) {  // the set-up's own operators: one copy of the entries, no codes or patterns (plan time)
+        A->requested_tune.gsort = 0;
+        A->requested_tune.codes = 0;
         A->requested_tune.patterns = 0;
     }
     aijhip::HostVec<int32_t> h_ai;
@@ -851,8 +788,6 @@ int64_t mult_layout_bytes(const aijhip_mat &A) {
         return 8 * nz + rows + m + 4 * (int64_t)P.n_ptab + vec;
     if (P.d_code)  // coded entries 10 B, blocks launched from aj 12 B, the dictionaries
         return 10 * (nz - P.nz_wide) + 12 * P.nz_wide + rows + vec + 4 * P.n_cmeta;
-    if (P.d_rel)  // block-relative entries 10 B, blocks launched from aj 12 B, the block bases
-        return 10 * (nz - P.nz_wide) + 12 * P.nz_wide + rows + vec + 4 * (int64_t)(P.n_blocks - P.n_wblocks);
     if (P.d_sidx)  // 16-bit columns and slots per entry pair (4 B per entry), sorted values, block bases
         return 12 * nz + rows + vec + 4 * (int64_t)(P.n_blocks - P.n_wblocks);
     if (P.d_sslot)  // sorted 32-bit columns + sorted values + 16-bit slots
@@ -1150,7 +1085,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->stream_rows = aijhip::kStreamGeoms[A->plan.tune.geom].rows;
     info->exact = A->plan.tune.exact ? 1 : 0;
     info->gather_sorted = A->plan.d_sidx != nullptr ? 2 : (A->plan.d_sslot != nullptr ? 1 : 0);
-    info->column_codes = A->plan.d_code != nullptr ? 1 : (A->plan.d_rel != nullptr ? 2 : 0);
+    info->column_codes = A->plan.d_code != nullptr ? 1 : 0;
     info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
     info->long_overlap = A->plan.side != nullptr ? 1 : 0;
     info->mult_layout_bytes = aijhip::mult_layout_bytes(*A);

@@ -103,10 +103,7 @@ struct Tuning {
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
                            // (operands with scattered gathers, caller's handles), 0 off, 1 on
     int codes = -1;        // 16-bit column codes instead of aj (Plan::d_code): -1 auto (where the
-                           // blocks' offset dictionaries fit and gsort is off; else block-relative
-                           // columns, Plan::d_rel, where blocks span < 2^16), 0 off, 1 the
-                           // dictionary codes only, 2 the block-relative columns only (the GAMG
-                           // set-up's own operators; not settable through the ABI)
+                           // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
                            // offset lists are few), 0 off, 1 on
 };
@@ -197,14 +194,6 @@ struct Plan {
     // length << 16 per pattern, then the offsets); geometry 6, full rows
     uint8_t *d_pid = nullptr;
     int32_t *d_ptab = nullptr;
-    // Block-relative columns (automatic where the offset dictionaries of the
-    // column codes do not fit but a block's columns span < 2^16: GAMG's coarse
-    // operators and interpolations): entry k of a narrow block b holds
-    // aj[k] - d_rbase[b] in 16 bits (pairs read as one 4-B word), 10 B per
-    // entry; the narrow blocks are d_blocks, or d_nblocks with the others in
-    // d_wblocks (launched from aj), as for the codes
-    uint16_t *d_rel = nullptr;
-    int32_t *d_rbase = nullptr;
     int32_t n_ptab = 0, n_pat = 0;
     int32_t pat_dmax = 0;    // largest |column - row| offset in the table (the stencil's plane distance)
     int64_t bytes = 0;  // device bytes held by the plan
@@ -306,10 +295,6 @@ hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk
 // sets *ok; otherwise leaves them null.
 hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok);
 hipError_t column_code_counts(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt);
-// Block-relative columns of blocks d_blk[0, nblk) against their bases d_base
-// (Plan::d_rel; asynchronous on the null stream).
-hipError_t rel16_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, const int32_t *d_base,
-                       uint16_t *d_rel);
 hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cmeta,
                              uint16_t *d_code);
 // Distinct 128-B x lines per entry over a row sample (at most 65536 rows):

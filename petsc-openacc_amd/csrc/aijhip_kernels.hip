@@ -224,12 +224,6 @@ __device__ __forceinline__ void stream_block(
     // gather round trips per lane instead of one).
     constexpr bool BF = (NTMODE & 64) != 0;
     static_assert(!(BF && SORTED), "branch-free phase 1: plain, coded and 16-bit gather-ordered forms");
-    // bit 7: block-relative columns (Plan::d_rel, full-row lists, with bit 6):
-    // aj holds one 16-bit column - sbase[b] per entry, pairs read as one 4-B
-    // word; 10 bytes per entry
-    constexpr bool REL = (NTMODE & 128) != 0;
-    static_assert(!REL || (BF && !CODES && !S16 && !SORTED && !CROW), "block-relative columns: branch-free full rows");
-    constexpr bool WORDS = CODES || REL;  // a pair's columns come as one 32-bit word
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     const BlockDesc d = blk[b];
@@ -274,13 +268,13 @@ __device__ __forceinline__ void stream_block(
     i32x2 cv[ITERS];
     f64x2 xv[ITERS];
     if constexpr (BF) {
-        uint32_t cw[WORDS ? ITERS : 1];  // a pair's two codes / relative columns
+        uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
         const int64_t kl = (k1 - 1) & ~int64_t(1);  // the last pair start (>= kb when nk > 0)
         if (d.nk > 0) {  // (block-uniform)
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) {
                 const int64_t k = min(kb + 2 * (int64_t)(t + it * T), kl);
-                if constexpr (WORDS) cw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aj) + (k >> 1));
+                if constexpr (CODES) cw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aj) + (k >> 1));
                 else cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
             }
 #pragma unroll
@@ -302,25 +296,6 @@ __device__ __forceinline__ void stream_block(
                     const uint32_t lo = cw[it] & 0xffffu, hi = cw[it] >> 16;
                     int32_t c0 = d.row0 + (int32_t)(lo >> ib) + cdict[lo & im];
                     int32_t c1 = d.row0 + (int32_t)(hi >> ib) + cdict[hi & im];
-                    if (e < e0) c0 = c1;
-                    if (e + 1 >= ne) c1 = c0;
-                    xv[it].x = op.gx(c0);
-                    xv[it].y = op.gx(c1);
-                }
-            }
-        }
-        if constexpr (REL) {
-            if (d.nk > 0) {
-                const int32_t base = sbase[b];
-                const int e0 = (int)(k0 - kb), ne = (int)(k1 - kb), el = (int)(kl - kb);
-#pragma unroll
-                for (int it = 0; it < ITERS; ++it) {
-                    const int e = min(2 * (t + it * T), el);  // the pair this lane loaded
-                    int32_t c0 = base + (int32_t)(cw[it] & 0xffffu);
-                    int32_t c1 = base + (int32_t)(cw[it] >> 16);
-                    // a pair straddling a block edge carries the neighbour's
-                    // half, relative to the neighbour's base: that half gathers
-                    // this half's column (never stored)
                     if (e < e0) c0 = c1;
                     if (e + 1 >= ne) c1 = c0;
                     xv[it].x = op.gx(c0);
@@ -390,7 +365,7 @@ __device__ __forceinline__ void stream_block(
             if (k < k1) sv[it] = *reinterpret_cast<const uint32_t *>(sslot + k);
         }
     }
-    if constexpr (BF && !WORDS) {  // every pair gathered (the clamped ones re-gather the last pair's columns)
+    if constexpr (BF && !CODES) {  // every pair gathered (the clamped ones re-gather the last pair's columns)
         if (d.nk > 0) {
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) {
@@ -1201,23 +1176,6 @@ hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_
     return launch_block_codes<true>(A, d_blk, nblk, nullptr, d_cmeta, d_code, kStreamGeoms[A.plan.tune.geom].nnz_cap);
 }
 
-namespace {
-__global__ __launch_bounds__(256) void k_rel16_write(const BlockDesc *__restrict__ blk,
-                                                     const int32_t *__restrict__ base,
-                                                     const int32_t *__restrict__ aj, uint16_t *rel) {
-    const BlockDesc d = blk[blockIdx.x];
-    const int32_t b0 = base[blockIdx.x];
-    for (int64_t k = d.k0 + threadIdx.x; k < (int64_t)d.k0 + d.nk; k += 256) rel[k] = (uint16_t)(aj[k] - b0);
-}
-}  // namespace
-
-hipError_t rel16_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, const int32_t *d_base,
-                       uint16_t *d_rel) {
-    if (nblk <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rel16_write, dim3(nblk), dim3(256), 0, nullptr, d_blk, d_base, A.d_aj, d_rel);
-    return hipGetLastError();
-}
-
 hipError_t block_column_ranges(const aijhip_mat &A, const BlockDesc *d_blocks, int32_t n_blocks, int2 *d_out) {
     if (n_blocks <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_block_xrange, dim3(n_blocks), dim3(256), 0, nullptr, d_blocks, A.d_aj, d_out);
@@ -1360,33 +1318,6 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
 #undef AIJHIP_SC
         }
     }
-    // Block-relative columns (Plan::d_rel; geometries 1 and 6, full rows):
-    // MatMult, MatMultAdd and the CG dot when unsplit; a split plan's dot
-    // epilogue takes aj (its partials would come from two launches)
-    constexpr bool kGeom1 = T == kStreamGeoms[1].threads && CAP == kStreamGeoms[1].nnz_cap && RPT == 1;
-    if constexpr (kGeom6 || kGeom1) {
-        if (P.d_rel && !L.ridx && (P.n_wblocks == 0 || !dpart)) {
-            const BlockDesc *cb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
-            const int32_t nc = P.n_wblocks ? P.n_nblocks : P.n_blocks;
-#define AIJHIP_SR(ADD, NTM)                                                                                       \
-    if (nc > 0)                                                                                                   \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, NTM, OpMult<ADD>>), dim3(nc), dim3(T), 0, s, cb, nc, \
-                           (int)P.tune.exact, L.rai, nullptr, reinterpret_cast<const int32_t *>(P.d_rel), A.d_aa, \
-                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_rbase);     \
-    if (P.n_wblocks > 0)                                                                                          \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, sw, \
-                           P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,           \
-                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);                \
-    return
-            if (add) {
-                if (P.tune.nt == 1) { AIJHIP_SR(true, 193); }
-                AIJHIP_SR(true, 192);
-            }
-            if (P.tune.nt == 1) { AIJHIP_SR(false, 193); }
-            AIJHIP_SR(false, 192);
-#undef AIJHIP_SR
-        }
-    }
     // Gather-ordered blocks (Plan::d_sslot): the sorted copy, every variant
     // (MatMult / MatMultAdd, full or compressed rows, dot epilogue)
     // (with the narrow / wide split, the dot epilogue's partials would come
@@ -1480,24 +1411,6 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
                            dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,
                            reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, op, dpart, stop, nullptr,
                            P.d_cmeta);
-        return hipGetLastError();
-    }
-    if (P.d_rel && (P.tune.geom == 1 || P.tune.geom == 6) && (P.n_wblocks == 0 || !dpart)) {
-        // block-relative columns (narrow blocks) + the wide blocks from aj
-        const BlockDesc *cb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
-        const int32_t nc = P.n_wblocks ? P.n_nblocks : P.n_blocks;
-#define AIJHIP_OR(G, NTM)                                                                                       \
-    if (nc > 0)                                                                                                 \
-        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, NTM, Op>), dim3(nc), dim3(kStreamGeoms[G].threads), \
-                           0, s, cb, nc, ex, A.d_ai, nullptr, reinterpret_cast<const int32_t *>(P.d_rel), A.d_aa, op, \
-                           dpart, stop, nullptr, P.d_rbase);                                                     \
-    if (P.n_wblocks > 0)                                                                                        \
-        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_wblocks),                     \
-                           dim3(kStreamGeoms[G].threads), 0, s, P.d_wblocks, P.n_wblocks, ex, A.d_ai, nullptr,   \
-                           A.d_aj, A.d_aa, op, nullptr, stop, nullptr, nullptr)
-        if (P.tune.geom == 6) { AIJHIP_OR(6, 192); }
-        else { AIJHIP_OR(1, 192); }
-#undef AIJHIP_OR
         return hipGetLastError();
     }
     static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");

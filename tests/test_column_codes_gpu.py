@@ -172,76 +172,3 @@ def test_cg_and_gamg_with_codes_bitwise(pkg, dev):
         assert out[0][0] == out[1][0]
         assert_bits(out[0][1], out[1][1])
         assert_bits(out[0][2], out[1][2])
-
-
-def _banded_random(m, per_row, reach, seed, far_every=0):
-    """Sorted unique columns within +-reach of the diagonal (GAMG-coarse-like
-    rows: more distinct offsets per block than a code dictionary holds, but a
-    block's columns within 2^16); every far_every-th row also reaches column
-    0 and m - 1 (its block spans the whole x: launched from aj)."""
-    rng = np.random.default_rng(seed)
-    offs = rng.integers(-reach, reach + 1, (m, per_row))
-    cols = np.clip(np.arange(m)[:, None] + offs, 0, m - 1)
-    rows = []
-    for i in range(m):
-        c = np.unique(np.concatenate([cols[i], [i]]))
-        if far_every and i % far_every == 0:
-            c = np.unique(np.concatenate([c, [0, m - 1]]))
-        rows.append(c)
-    ai = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
-    aj = np.concatenate(rows).astype(np.int32)
-    aa = rng.uniform(-1, 1, len(aj))
-    return ai, aj, aa
-
-
-@pytest.mark.parametrize("far_every", [0, 997])
-def test_block_relative_columns_bitwise(pkg, dev, coracle, far_every):
-    """Block-relative 16-bit columns (info column_codes 2, 10 B per entry):
-    the automatic layout where the offset dictionaries overflow but each
-    block's columns span < 2^16 (GAMG's coarse operators). Unsplit, and split
-    (a far-reaching row every 997: those blocks from aj). MatMult and
-    MatMultAdd equal the aj kernel and the oracle bit for bit, also after new
-    values."""
-    ai, aj, aa = _banded_random(60000, 30, 20000, 5, far_every)
-    m = len(ai) - 1
-    x, z = pkg.splitmix_uniform(m, 42), pkg.splitmix_uniform(m, 7)
-    with pkg.SeqAIJHIP(ai, aj, aa, gather_sort=0) as A:  # (a caller's long rows default to the gather order)
-        info = A.info()
-        assert info["column_codes"] == 2 and info["row_patterns"] == 0 and info["gather_sorted"] == 0
-        assert info["mult_layout_bytes"] < info["mult_bytes"]
-        y2, w2 = products(A, x, z, dev)
-        assert_bits(y2, coracle.matmult(ai, aj, aa, x, omp=True))
-        A.set_option("column_codes", 0)
-        assert A.info()["column_codes"] == 0
-        y0, w0 = products(A, x, z, dev)
-        assert_bits(y2, y0)
-        assert_bits(w2, w0)
-        A.set_option("column_codes", -1)
-        aa2 = np.random.default_rng(6).uniform(-1, 1, len(aa))
-        A.update_values(aa2)
-        assert A.info()["column_codes"] == 2
-        y3, _ = products(A, x, z, dev)
-        assert_bits(y3, coracle.matmult(ai, aj, aa2, x, omp=True))
-
-
-def test_cg_and_gamg_with_block_relative_levels_bitwise(pkg, dev):
-    """CG + GAMG whose coarse operators and interpolations take the
-    block-relative columns (the default) against the same solve with every
-    level on aj (column_codes 0 on the fine handle, copied to its levels):
-    the fused smoothers, restriction and interpolation give the same
-    residual history and solution bit for bit."""
-    K = importlib.import_module("petsc-openacc_amd.ksp")
-    ai, aj, aa = pkg.poisson_csr(48)
-    rhs, _ = pkg.poisson_vectors(48, 48, 48)
-    b = torch.from_numpy(rhs).to(dev)
-    out = {}
-    for codes in (-1, 0):
-        with pkg.SeqAIJHIP(ai, aj, aa, column_codes=codes) as A:
-            x = torch.zeros_like(b)
-            with K.KSPCG(A, pc="gamg", rtol=1e-14, atol=1e-12) as ksp:
-                ksp.solve(b, x)
-                torch.cuda.synchronize()
-                out[codes] = (ksp.its, ksp.history(), x.cpu().numpy())
-    assert out[-1][0] == out[0][0]
-    assert_bits(out[-1][1], out[0][1])
-    assert_bits(out[-1][2], out[0][2])

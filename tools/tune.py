@@ -58,7 +58,7 @@ def main():
         ai, aj, aa = pkg.poisson_csr(args.grid)
     elif args.matrix == "fem_hex":  # Flan_1565's structure: hexahedral mesh, 3 dofs per node
         ai, aj, aa = pkg.fem_hex_csr()
-    elif args.matrix == "banded":  # 3 M rows of ~30 random columns within +-20000 (GAMG-coarse-like)
+    elif args.matrix == "banded":  # 3 M rows of ~30 random columns within +-20000 (GAMG-coarse-like scatter)
         rng = np.random.default_rng(5)
         m, w = 3_000_000, 30
         c = np.sort(np.clip(np.arange(m)[:, None] + rng.integers(-20000, 20001, (m, w)), 0, m - 1), axis=1)
@@ -141,11 +141,6 @@ def main():
     if args.variants == "bf":  # branch-free STREAM phase 1 (AIJHIP_STREAM_BF) against the predicated form, aj layout
         for bf in ("0", "1", "0", "1"):
             variants.append(("stream", dict(row_patterns=0, column_codes=0, env={"AIJHIP_STREAM_BF": bf})))
-    if args.variants == "rel":  # block-relative columns (column_codes auto, gather order off) against aj and the default
-        for rep in range(2):
-            variants += [("stream", dict(gather_sort=0, row_patterns=0, column_codes=-1)),
-                         ("stream", dict(gather_sort=0, row_patterns=0, column_codes=0)),
-                         ("stream", {})]
     if args.variants == "geoms":  # the default plan at the geometries of 256 / 512 lanes and 2 / 4 pair-iterations
         for g in (6, 8, 11, 0, 6, 8, 11, 0):
             variants.append(("stream", dict(geometry=g)))
