@@ -251,14 +251,6 @@ hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, do
 // Richardson+Jacobi step x = t + D^-1 (b - A t) (x != t) with optional
 // z.z / z.b partials (2 x n_blocks) for CG on the finest level.
 bool stream_mg_fusable(const aijhip_mat &A);
-// CG's p' = z + beta p with X += alpha pin fused into w = A p' (OpCgP,
-// aijhip_kernels.hip): p' for the rows into pout, the p'.w partials into
-// dpart[0..n_blocks); the scalars read from the device CG state (beta, alpha,
-// iteration index); *pcur = pidx once the launch ran. Same conditions as
-// stream_dot_fusable; pout, w must not alias z, pin.
-hipError_t launch_cg_pmult(const aijhip_mat &A, const double *z, const double *pin, double *pout, double *w, double *x,
-                           const double *beta, const double *alpha, const int32_t *iter, int32_t *pcur, int32_t pidx,
-                           double *dpart, const int *stop, hipStream_t s);
 // y = D^-1 A x in PETSc's row order (exact), for the GAMG set-up.
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s);
 // r = b - A x on a STREAM plan (residual in the SpMV epilogue).

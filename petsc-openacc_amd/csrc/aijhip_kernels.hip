@@ -101,7 +101,6 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     const double *x, *z;
     double *y;
     bool dot;
-    __device__ void prepare() {}
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int o) const { return ADD ? z[o] : 0.0; }
     __device__ void put(int o, double v, double *d) const {
@@ -119,7 +118,6 @@ struct OpMgResid {
     static constexpr bool kSeeded = false;
     const double *x, *b;
     double *r;
-    __device__ void prepare() {}
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int) const { return 0.0; }
     __device__ void put(int o, double v, double *) const {
@@ -140,7 +138,6 @@ struct OpMgPost {
     const double *t, *b, *dinv;
     double *x;
     bool dot;
-    __device__ void prepare() {}
     __device__ double gx(int32_t j) const { return t[j]; }
     __device__ double seed(int) const { return 0.0; }
     __device__ void put(int o, double v, double *d) const {
@@ -161,48 +158,9 @@ struct OpDinvMult {
     static constexpr bool kSeeded = false;
     const double *x, *dinv;
     double *y;
-    __device__ void prepare() {}
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int) const { return 0.0; }
     __device__ void put(int o, double v, double *) const { st_stream(y + o, dinv[o] * v); }
-};
-
-// KSPSolve_CG's direction update fused into its SpMV: p' = z + beta p (p' = z
-// at i = 0; VecAYPX, product first) is formed wherever the SpMV gathers it:
-// each row block recomputes the p' of the columns it reads from z and the
-// previous direction pin, so no block reads a p' another block writes; for
-// its own rows it stores p' into pout (the other buffer), applies the
-// previous iteration's X += a pin (as k_aypx, i > 0) and stores w = A p'
-// (w must not alias z or pin), with the p' . w partials. The same
-// operations on the same values as k_aypx + the SpMV: the same bits. The
-// scalars come from the device CG state (prepare(), after the stop test);
-// row 0's lane records which buffer now holds p (*pcur = pidx).
-struct OpCgP {
-    static constexpr int kDots = 1;
-    static constexpr bool kSeeded = false;
-    const double *z, *pin;
-    double *pout, *w, *x;
-    const double *sb, *sa;
-    const int32_t *si;
-    int32_t *pcur;
-    int32_t pidx;
-    double bb = 0.0, a = 0.0;
-    bool pf = true;
-    __device__ void prepare() {
-        bb = *sb;
-        a = *sa;
-        pf = *si == 0;
-    }
-    __device__ double gx(int32_t j) const { return pf ? z[j] : z[j] + bb * pin[j]; }
-    __device__ double seed(int) const { return 0.0; }
-    __device__ void put(int o, double v, double *d) const {
-        const double po = gx(o);
-        if (!pf) st_stream(x + o, x[o] + a * pin[o]);
-        st_stream(pout + o, po);
-        st_stream(w + o, v);
-        if (o == 0) *pcur = pidx;
-        d[0] += po * v;
-    }
 };
 
 // s + p[0] + p[1] + ... + p[n-1], added left to right (PETSc's order). The LDS
@@ -500,7 +458,6 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     const int32_t *__restrict__ sbase) {
     __shared__ double prod[CAP];
     __shared__ int32_t cdict[(NTMODE & 32) ? kCodeDictMax : 1];
-    op.prepare();
     stream_block<T, CAP, RPT, CROW, NTMODE, Op>((int)blockIdx.x, blk, nblk, exact, rai, ridx, aj, aa, op, dpart, stop,
                                                 sslot, sbase, prod, cdict);
 }
@@ -531,7 +488,6 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     const int b = (int)blockIdx.x;
     const BlockDesc d = blk[b];
     if ((stop ? *stop : 0) != 0 || d.nk < 0) return;
-    op.prepare();
     const int t = threadIdx.x;
     const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
     int32_t tv[TPT];
@@ -1506,12 +1462,6 @@ hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b,
                           double *dpart, hipStream_t s, bool nt, const int *stop) {
     if (nt) return launch_stream_op(A, OpMgPost<true>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
     return launch_stream_op(A, OpMgPost<false>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
-}
-
-hipError_t launch_cg_pmult(const aijhip_mat &A, const double *z, const double *pin, double *pout, double *w, double *x,
-                           const double *beta, const double *alpha, const int32_t *iter, int32_t *pcur, int32_t pidx,
-                           double *dpart, const int *stop, hipStream_t s) {
-    return launch_stream_op(A, OpCgP{z, pin, pout, w, x, beta, alpha, iter, pcur, pidx}, dpart, s, -1, stop);
 }
 
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s) {

@@ -20,7 +20,6 @@ struct CGState {
     double beta, betaold, dpi, dpiold, a, b, dp, rnorm0, ttol;
     int32_t its, reason, done, i;
     int32_t xpend;  // X += a P of the last completed iteration not applied yet
-    int32_t pcur;   // which of the two direction buffers holds P (the fused p-update SpMV, ksp.hip)
 };
 
 struct CGParams {

@@ -108,16 +108,6 @@ int khip(hipError_t e, const char *what) {
     return AIJHIP_ERR_HIP;
 }
 
-// k_final_x for the fused p-update: P is in the buffer the last launch wrote
-// (S->pcur).
-__global__ __launch_bounds__(kVecThreads) void k_final_xp(int64_t n, const double *__restrict__ p0,
-                                                          const double *__restrict__ p1, double *x, const CGState *S) {
-    if (!S->xpend) return;
-    const double a = S->a;
-    const double *p = S->pcur ? p1 : p0;
-    GRID_STRIDE(i, n) x[i] = x[i] + a * p[i];
-}
-
 struct MGLevel {
     aijhip_mat *A = nullptr;  // level 0: borrowed
     aijhip_mat *P = nullptr;  // interpolation from level l+1 (owned)
@@ -152,10 +142,6 @@ struct aijhip_ksp {
     // 0.392 s against 0.376 s per 400 iterations (profiles/r01/x_in_update/).
     // (Those A/B forms were withdrawn in round 4.)
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
-    // the fused p-update SpMV (pfused: aijhip::launch_cg_pmult): the second
-    // direction and z / w buffers, alternating by iteration parity
-    bool pfused = false;
-    double *d_p2 = nullptr, *d_zw = nullptr;
     double *d_hist = nullptr;
     double *d_hb = nullptr, *d_hx = nullptr;  // aijhip_ksp_solve_host's device copies of b and x
     int32_t hist_cap = 0;
@@ -189,8 +175,6 @@ void mg_free(aijhip_ksp *K) {
 void ksp_free(aijhip_ksp *K) {
     mg_free(K);
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
-    hipFree(K->d_p2); hipFree(K->d_zw);
-    K->d_p2 = K->d_zw = nullptr;
     hipFree(K->d_hist); hipFree(K->d_state);
     hipFree(K->d_hb); hipFree(K->d_hx);
     K->d_hb = K->d_hx = nullptr;
@@ -475,7 +459,6 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
     const int64_t m = A->m;
     const size_t vb = sizeof(double) * (size_t)std::max<int64_t>(m, 1);
     K->fused = aijhip::stream_dot_fusable(*A);
-    K->pfused = K->fused && !std::getenv("AIJHIP_CG_PSEP");  // (AIJHIP_CG_PSEP: the separate K1 pass, A/B)
     K->vec_grid = (int)vgrid(K, m).x;
     const int64_t nparts = std::max<int64_t>((int64_t)kNQ * K->vec_grid, K->fused ? A->plan.n_blocks : K->vec_grid);
     K->hist_cap = K->max_it + 2;
@@ -485,8 +468,7 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
         (e = hipMalloc(&K->d_part, sizeof(double) * (size_t)nparts)) != hipSuccess ||
         (e = hipMalloc(&K->d_hist, sizeof(double) * (size_t)K->hist_cap)) != hipSuccess ||
         (e = hipMalloc(&K->d_state, sizeof(CGState))) != hipSuccess ||
-        (e = hipHostMalloc(&K->h_state, sizeof(CGState), hipHostMallocDefault)) != hipSuccess ||
-        (K->pfused && ((e = hipMalloc(&K->d_p2, vb)) != hipSuccess || (e = hipMalloc(&K->d_zw, vb)) != hipSuccess))) {
+        (e = hipHostMalloc(&K->h_state, sizeof(CGState), hipHostMallocDefault)) != hipSuccess) {
         ksp_free(K);
         return khip(e, "ksp set-up allocation");
     }
@@ -548,38 +530,8 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     if ((e = hipGetLastError()) != hipSuccess) return khip(e, "KSPSolve init");
     // One CG iteration (+ the V-cycle) on stream st; every kernel is a
     // no-op once `done` is set.
-    auto iterate = [&](hipStream_t st, int32_t j) -> hipError_t {
+    auto iterate = [&](hipStream_t st) -> hipError_t {
         hipError_t ie = hipSuccess;
-        if (K->pfused) {
-            // K1 inside the SpMV: p' from z (buffer c) and p (buffer c) into
-            // the other p buffer, w = A p' into the other z buffer, which K4
-            // (Jacobi) / the V-cycle (GAMG) then overwrite with the new z
-            const int c = j & 1;
-            const double *zin = c ? K->d_zw : K->d_z, *pin = c ? K->d_p2 : K->d_p;
-            double *wz = c ? K->d_z : K->d_zw, *pout = c ? K->d_p : K->d_p2;
-            CGState *S = K->d_state;
-            ie = aijhip::launch_cg_pmult(*A, zin, pin, pout, wz, x, &S->b, &S->a, &S->i, &S->pcur, c ? 0 : 1,
-                                         K->d_part, &S->done, st);
-            if (ie == hipSuccess)
-                hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, st, K->d_part, A->plan.n_blocks, K->d_state);
-            hipLaunchKernelGGL(k_update<true>, vg, vt, 0, st, m, K->d_r, wz, K->d_dinv, K->d_part, K->d_state,
-                               K->pc, nullptr, nullptr);
-            const double *pz = K->d_part;
-            int nbz = nb;
-            if (gamg && ie == hipSuccess) {
-                bool dots = false;
-                ie = vcycle(K, K->d_r, wz, st, K->d_mgpart, &dots, &K->d_state->done);
-                if (dots) {
-                    pz = K->d_mgpart;
-                    nbz = K->mg[0].A->plan.n_blocks;
-                } else {
-                    hipLaunchKernelGGL(k_dots, vg, vt, 0, st, m, wz, K->d_r, K->d_part, 0, 1, K->d_state);
-                }
-            }
-            hipLaunchKernelGGL(k_reduce_iter, dim3(1), rt, 0, st, pz, nbz, K->d_part + 2 * nb, nb, K->d_state,
-                               K->d_hist, p);
-            return ie != hipSuccess ? ie : hipGetLastError();
-        }
         hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
         if (K->fused) {
             ie = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, st);
@@ -626,10 +578,9 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             return khip(e, "KSPSolve poll");
         if (K->h_state->done || launched >= K->max_it) break;
         for (int j = 0; j < batch && launched < K->max_it; ++j, ++launched)
-            if ((e = iterate(s, launched)) != hipSuccess) return khip(e, "KSPSolve iteration");
+            if ((e = iterate(s)) != hipSuccess) return khip(e, "KSPSolve iteration");
     }
-    if (K->pfused) hipLaunchKernelGGL(k_final_xp, vg, vt, 0, s, m, K->d_p, K->d_p2, x, K->d_state);
-    else hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
+    hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
     if ((e = hipGetLastError()) != hipSuccess ||
         (e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)
@@ -686,10 +637,8 @@ int aijhip_ksp_get_iteration_bytes(aijhip_ksp_t K, int64_t *bytes, int64_t *spmv
     const int64_t a0 = aijhip::mult_layout_bytes(*K->A);
     // CG: p = z + b p with x += a p (reads z, p, x; writes p, x), the SpMV
     // (p . w in its epilogue), the r update (Jacobi: reads r, w, D^-1,
-    // writes r, z; GAMG: reads r, w, writes r; z from the V-cycle). Fused
-    // p-update (pfused): the SpMV gathers z and p where the layout counts
-    // one vector, and writes p' and reads / writes x: 32 m beyond the layout
-    int64_t spmv = a0, vec = (K->pfused ? 32 : 40) * m + (K->pc == AIJHIP_PC_GAMG ? 24 * m : 40 * m);
+    // writes r, z; GAMG: reads r, w, writes r; z from the V-cycle)
+    int64_t spmv = a0, vec = 40 * m + (K->pc == AIJHIP_PC_GAMG ? 24 * m : 40 * m);
     if (!K->fused) vec += 16 * m;  // p . w in its own pass
     int64_t lev0 = a0 + vec;
     if (K->pc == AIJHIP_PC_GAMG) {

@@ -183,34 +183,3 @@ def test_gpu_replanned_operator_sets_up_again(pkg, pc):
     assert got[0] == ref[0]
     assert np.array_equal(got[1].view(np.uint64), ref[1].view(np.uint64))
     assert np.array_equal(got[2].view(np.uint64), ref[2].view(np.uint64))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("pc,layout", [("jacobi", "auto"), ("jacobi", "csr"), ("gamg", "auto")])
-def test_gpu_fused_p_update_equals_separate_pass(pkg, monkeypatch, pc, layout):
-    """KSPSolve_CG's K1 (p = z + beta p, X += a p) inside the SpMV (each
-    row block recomputes the p it gathers from z and the previous direction,
-    two alternating direction and z / w buffers) against the separate pass
-    (AIJHIP_CG_PSEP=1): iterations, residual history and x bit for bit, on
-    the row-pattern and the CSR layouts, stopping mid-batch."""
-    import torch
-    K = importlib.import_module("petsc-openacc_amd.ksp")
-    N = 30
-    ai, aj, aa = pkg.poisson_csr(N)
-    rhs, _ = pkg.poisson_vectors(N)
-    b = torch.from_numpy(rhs).cuda()
-    opts = {} if layout == "auto" else dict(row_patterns=0, column_codes=0)
-    out = {}
-    for sep in (False, True):
-        if sep:
-            monkeypatch.setenv("AIJHIP_CG_PSEP", "1")
-        with pkg.SeqAIJHIP(ai, aj, aa, **opts) as A:
-            with K.KSPCG(A, rtol=1e-12, atol=1e-14, pc=pc) as ksp:
-                x = torch.zeros_like(b)
-                ksp.solve(b, x)
-                torch.cuda.synchronize()
-                out[sep] = (ksp.its, np.array(ksp.history()), x.cpu().numpy())
-        monkeypatch.delenv("AIJHIP_CG_PSEP", raising=False)
-    assert out[False][0] == out[True][0] and out[False][0] % 8 != 0
-    assert np.array_equal(out[False][1].view(np.uint64), out[True][1].view(np.uint64))
-    assert np.array_equal(out[False][2].view(np.uint64), out[True][2].view(np.uint64))
