@@ -449,6 +449,17 @@ __global__ void k_div(int32_t m, const double *w, double nw, double *v) {
     if (i < m) v[i] = w[i] / nw;
 }
 
+// head[i][t] = row i's t-th column of S, or i past its end (the host phase-1
+// pass tests a free node's first columns from this dense array first)
+__global__ void k_phase1_head(int32_t m, const int32_t *__restrict__ si, const int32_t *__restrict__ sj,
+                              int32_t *__restrict__ head) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= (int64_t)m * aijhip_gamg::kPhase1Head) return;
+    const int32_t i = (int32_t)(q / aijhip_gamg::kPhase1Head), t = (int32_t)(q % aijhip_gamg::kPhase1Head);
+    const int64_t k = (int64_t)si[i] + t;
+    head[q] = k < si[i + 1] ? sj[k] : i;
+}
+
 __global__ void k_fill(int32_t m, double v, double *x) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) x[i] = v;
@@ -1439,7 +1450,7 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
     int32_t *tmp = nullptr, *si = nullptr, *sj = nullptr;
     unsigned long long *scan_tmp = nullptr;
     int64_t nzs = 0;
-    int32_t *h_si = nullptr, *agg = nullptr, *d_ph = nullptr;
+    int32_t *h_si = nullptr, *agg = nullptr, *d_ph = nullptr, *d_head = nullptr;
     int32_t *d_aggv = nullptr;  // the aggregates (device), handed to the prolongator
     unsigned long long *d_left = nullptr;
     int32_t na = 0;
@@ -1520,22 +1531,30 @@ strength_done:
         for (int c = 0; c < kChunks; ++c) slot = std::max<int64_t>(slot, (int64_t)h_off[c + 1] - h_off[c]);
         (void)hipHostFree(h_off);
         GTRY(e, "read S offsets");
+        constexpr int H = aijhip_gamg::kPhase1Head;
+        GTRY(dalloc(&d_head, (int64_t)m * H), "alloc");
+        hipLaunchKernelGGL(k_phase1_head, dim3(blocks_for((int64_t)m * H, 256)), dim3(256), 0, nullptr, m, si, sj,
+                           d_head);
         Staging &stage = process_staging(stage_lock);
-        GTRY(stage.reserve(sizeof(int32_t) * (2 * (size_t)m + 1 + 2 * (size_t)slot)), "pinned staging");
+        GTRY(stage.reserve(sizeof(int32_t) * ((2 + (size_t)H) * (size_t)m + 1 + 2 * (size_t)slot)), "pinned staging");
         lap("staging alloc");
         h_si = stage.i32();
         agg = h_si + m + 1;
-        int32_t *h_slot[2] = {agg + m, agg + m + slot};
+        int32_t *h_head = agg + m;
+        int32_t *h_slot[2] = {h_head + (size_t)H * m, h_head + (size_t)H * m + slot};
         GTRY(hipMemcpy(h_si, si, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToHost), "read S");
         lap("strength");
         {
             hipEvent_t ev[2] = {};
             hipStream_t cs = setup_stream(A.device, 1);
             if (!cs) GTRY(hipErrorOutOfMemory, "stream");
-            auto fetch = [&](int c) {  // chunk c into slot c % 2
+            auto fetch = [&](int c) {  // chunk c into slot c % 2 (its rows' heads first)
                 const int64_t a = h_si[r[c]], b = h_si[r[c + 1]];
                 hipError_t x = hipSuccess;
-                if (b > a)
+                if (r[c + 1] > r[c])
+                    x = hipMemcpyAsync(h_head + (size_t)H * r[c], d_head + (size_t)H * r[c],
+                                       sizeof(int32_t) * H * (size_t)(r[c + 1] - r[c]), hipMemcpyDeviceToHost, cs);
+                if (x == hipSuccess && b > a)
                     x = hipMemcpyAsync(h_slot[c & 1], sj + a, sizeof(int32_t) * (size_t)(b - a),
                                        hipMemcpyDeviceToHost, cs);
                 if (x == hipSuccess) x = hipEventRecord(ev[c & 1], cs);
@@ -1552,7 +1571,7 @@ strength_done:
                 if ((e = hipEventSynchronize(ev[c & 1])) != hipSuccess) break;
                 const auto w1 = std::chrono::steady_clock::now();
                 na = aijhip_gamg::aggregate_phase1_rows(r[c], r[c + 1], h_si, h_slot[c & 1], agg, taken.data(), na,
-                                                        h_si[r[c]]);
+                                                        h_si[r[c]], h_head);
                 if (c + 2 < kChunks) e = fetch(c + 2);
                 t_wait += std::chrono::duration<double, std::milli>(w1 - w0).count();
                 t_pass += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w1).count();
@@ -1584,7 +1603,7 @@ level_done:
     job.join();
     lap("emax joined");
     hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
-    hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left);
+    hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left); hipFree(d_head);
     lap("freed");
     if (emax_its > 0) {
         *emax = job.emax;
@@ -1794,14 +1813,14 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     // which spares a first set-up a 216 MB allocation and fill at 300^3 (5 ms)
     double *d_B = nullptr;
     // A finest level the device sweep aggregates leaves the first host pass
-    // to level 1: its pinned staging (S row chunks and ids, ~15 B per level-1
-    // row, ~2 B per finest row at aggregates of ~8) is reserved on a host
+    // to level 1: its pinned staging (S row chunks and ids and row heads,
+    // ~31 B per level-1 row, ~4 B per finest row at aggregates of ~8) is reserved on a host
     // thread meanwhile (6 ms of pinning at 300^3 on a first set-up)
     std::thread prestage;
     {
         int32_t rounds = 0;
         if (A0->m >= p.device_min_rows && device_phase1(A0->m, A0->nz - A0->m, &rounds))
-            prestage = std::thread([bytes = (size_t)A0->m * 5 / 2, device = A0->device] {
+            prestage = std::thread([bytes = (size_t)A0->m * 9 / 2, device = A0->device] {
                 (void)hipSetDevice(device);
                 std::unique_lock<std::mutex> lock;
                 (void)process_staging(lock).reserve(bytes);

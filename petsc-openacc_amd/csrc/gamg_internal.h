@@ -22,8 +22,12 @@ int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_
 // count so far): a node reads only its own row of S, so rows may arrive in
 // order while earlier ones are processed.
 // (sj holds S's columns from entry sj0 on: sj[k - sj0] is entry k)
+// head (optional): each row's first kPhase1Head columns (padded with the row's
+// own index), kPhase1Head per row from row 0; most free nodes meet a taken
+// neighbour among them, so their rows of sj are never read.
+constexpr int kPhase1Head = 4;
 int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const int32_t *sj, int32_t *agg,
-                              uint64_t *taken, int32_t na, int64_t sj0 = 0);
+                              uint64_t *taken, int32_t na, int64_t sj0 = 0, const int32_t *head = nullptr);
 int32_t aggregate_phase3(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t na);
 
 // Host continuation: the hierarchy below operator (m, ai, aj, aa) whose

@@ -380,25 +380,35 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
 namespace aijhip_gamg {
 
 int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const int32_t *sj, int32_t *agg,
-                              uint64_t *taken, int32_t na, int64_t sj0) {
+                              uint64_t *taken, int32_t na, int64_t sj0, const int32_t *head) {
     // The pass is a chain of dependent loads (row start, its columns, their
     // state). The state it tests is `taken`, one bit per node (agg[j] != -1):
     // 400 KB for the 3.27 M nodes of 300^3's level 1, so the random tests hit
     // the core's L2 instead of the 13 MB agg array; agg is only written. Rows
     // of nodes still free are prefetched 64 ahead (an aggregated node's row
-    // is never read; most are, so S is not streamed whole).
+    // is never read). With `head`, a free node first tests its row's first
+    // columns (the lowest: settled, mostly taken) from that dense array, and
+    // only the nodes they all leave free read their row of sj -- the order
+    // of the tests changes nothing (any taken neighbour rules the node out).
     constexpr int32_t kAhead = 64;
     auto is_taken = [taken](int32_t j) { return (taken[j >> 6] >> (j & 63)) & 1u; };
     auto take = [taken, agg](int32_t j, int32_t a) {
         agg[j] = a;
         taken[j >> 6] |= uint64_t(1) << (j & 63);
     };
+    auto head_free = [head, &is_taken](int32_t i) {
+        const int32_t *h = head + (size_t)i * kPhase1Head;
+        bool f = true;
+        for (int t = 0; t < kPhase1Head; ++t) f &= !is_taken(h[t]);
+        return f;
+    };
     for (int32_t i = r0; i < r1; ++i) {
-        if (i + kAhead < r1) {
+        if (!head && i + kAhead < r1) {  // (with heads, few rows are read: a host benchmark ran faster unprefetched)
             const int32_t ib = i + kAhead;
             if (!is_taken(ib)) __builtin_prefetch(sj + (si[ib] - sj0), 0, 3);
         }
         if (is_taken(i) || si[i] == si[i + 1]) continue;
+        if (head && !head_free(i)) continue;
         const int32_t *row = sj + (si[i] - sj0);
         const int32_t len = si[i + 1] - si[i];
         bool free_all = true;
