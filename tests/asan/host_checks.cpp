@@ -4,6 +4,7 @@
 // (gamg_setup.cpp) and the oracle's C MatMult, on small inputs including
 // ragged and degenerate ones. Built and run by tests/test_asan.py; exits
 // non-zero on a failed check, the sanitizers abort on a memory error.
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -12,6 +13,7 @@
 #include "aijhip.h"
 #include "aijhip_gamg.h"
 #include "aijhip_harness.h"
+#include "gamg_internal.h"
 
 extern "C" void oracle_matmult_seqaij(int32_t m, const int32_t *ai, const int32_t *aj, const double *aa,
                                       const double *x, double *y);
@@ -90,6 +92,52 @@ static void gamg_case(int n, int threads) {
     CHECK(aijhip_gamg_host_destroy(h) == AIJHIP_OK);
 }
 
+// The device set-up's host phase-1 pass (gamg_device.hip: S's rows arrive in
+// chunks, each chunk's columns in a buffer of its own, with the dense head
+// array of each row's first columns; the pass runs behind a look-ahead) gives
+// the plain sequential pass's aggregates on random symmetric graphs with
+// empty rows, for several chunk counts.
+static void phase1_case(int32_t m, int deg, uint64_t seed, int chunks) {
+    std::vector<std::vector<int32_t>> adj(m);
+    uint64_t z = seed;
+    auto next = [&z]() { z = z * 6364136223846793005ULL + 1442695040888963407ULL; return z >> 33; };
+    for (int32_t i = 0; i < m; ++i) {
+        if (next() % 7 == 0) continue;  // some rows stay empty unless a neighbour picks them
+        const int d = (int)(next() % (uint64_t)(2 * deg + 1));
+        for (int e = 0; e < d; ++e) {
+            const int32_t span = 1 + (int32_t)(next() % 3 == 0 ? m : 40);
+            int32_t j = i + (int32_t)(next() % (uint64_t)(2 * span + 1)) - span;
+            if (j < 0 || j >= m || j == i) continue;
+            adj[i].push_back(j);
+            adj[j].push_back(i);
+        }
+    }
+    std::vector<int32_t> si(m + 1, 0), sj;
+    for (int32_t i = 0; i < m; ++i) {
+        std::sort(adj[i].begin(), adj[i].end());
+        adj[i].erase(std::unique(adj[i].begin(), adj[i].end()), adj[i].end());
+        sj.insert(sj.end(), adj[i].begin(), adj[i].end());
+        si[i + 1] = (int32_t)sj.size();
+    }
+    std::vector<int32_t> ref(m), agg(m, -1);
+    const int32_t nref = aijhip_gamg::aggregate_phase1(m, si.data(), sj.data(), ref.data());
+    constexpr int H = aijhip_gamg::kPhase1Head;
+    std::vector<int32_t> head((size_t)m * H);
+    for (int32_t i = 0; i < m; ++i)
+        for (int t = 0; t < H; ++t) head[(size_t)i * H + t] = si[i] + t < si[i + 1] ? sj[si[i] + t] : i;
+    std::vector<uint64_t> taken(((size_t)m + 63) / 64, 0);
+    int32_t na = 0;
+    for (int c = 0; c < chunks; ++c) {
+        const int32_t r0 = (int32_t)((int64_t)m * c / chunks), r1 = (int32_t)((int64_t)m * (c + 1) / chunks);
+        std::vector<int32_t> slot(sj.begin() + si[r0], sj.begin() + si[r1]);  // the chunk's own buffer
+        na = aijhip_gamg::aggregate_phase1_rows(r0, r1, si.data(), slot.data(), agg.data(), taken.data(), na, si[r0],
+                                                head.data());
+    }
+    CHECK(na == nref);
+    CHECK(agg == ref);
+    for (int32_t i = 0; i < m; ++i) CHECK(((taken[i >> 6] >> (i & 63)) & 1u) == (agg[i] != -1));
+}
+
 int main() {
     poisson_case(6, 5, 4, 0, 4);
     poisson_case(7, 3, 9, 2, 6);
@@ -101,6 +149,11 @@ int main() {
     std::vector<int32_t> si(3001), sj(nnz);
     std::vector<double> sa(nnz);
     CHECK(aijhip_skewed_csr(3000, 1565, &nnz, si.data(), sj.data(), sa.data()) == AIJHIP_OK);
+    phase1_case(5000, 6, 1, 1);
+    phase1_case(5000, 6, 2, 7);
+    phase1_case(20000, 15, 3, 32);
+    phase1_case(300, 2, 4, 32);  // chunks shorter than the look-ahead
+    phase1_case(1, 0, 5, 1);
     gamg_case(10, 1);
     gamg_case(9, 4);
     CHECK(aijhip_poisson_nnz(0, 3, 3, 0, 3, &nnz) == AIJHIP_ERR_ARG);
