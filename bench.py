@@ -83,6 +83,9 @@ def parse():
     p.add_argument("--roofline-reps", type=int, default=50,
                    help="launches timed by HIP events for roofline.achieved (at least this many, SURVEY §8d)")
     p.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling 300^3 line")
+    p.add_argument("--strong-grid", type=int, default=None,
+                   help="edge of the strong-scaling operand (default: --grid); a one-GPU rehearsal of the N = 8 "
+                        "run keeps the strong line at 300^3 (38/37 planes per rank) with a small weak grid")
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
                         "(launch with torch.distributed.run): a one-GPU rehearsal of the N > 1 run")
@@ -171,13 +174,22 @@ def launch_ranks(n: int, argv, child=None, poll_s: float = 0.2) -> int:
     return rc
 
 
-def rank_record(rank, device, pci_bus, rows, nnz, ghosts, spmv_ms, diag_ms):
+def rank_record(rank, device, pci_bus, rows, nnz, ghosts, spmv_ms, diag_ms, paired=None):
     """One rank's entry of the N > 1 line: where it ran and how much of its
     distributed SpMV the exchange (+ the A_o product) adds on top of the
-    diagonal block alone."""
-    return {"rank": rank, "device": device, "pci_bus": pci_bus, "rows": rows, "nnz": nnz, "ghosts": ghosts,
-            "spmv_us_mean": round(spmv_ms * 1e3, 2), "diag_block_us_mean": round(diag_ms * 1e3, 2),
-            "halo_exposed_us": round((spmv_ms - diag_ms) * 1e3, 2)}
+    diagonal block alone. paired: the interleaved timing of halo_forms
+    (median per-round differences) — then
+    halo_exposed_us is that median, else the difference of the means."""
+    rec = {"rank": rank, "device": device, "pci_bus": pci_bus, "rows": rows, "nnz": nnz, "ghosts": ghosts,
+           "spmv_us_mean": round(spmv_ms * 1e3, 2), "diag_block_us_mean": round(diag_ms * 1e3, 2),
+           "halo_exposed_us": round((spmv_ms - diag_ms) * 1e3, 2)}
+    if paired is not None:
+        rec.update(spmv_us_median=round(paired["spmv_us_median"], 2),
+                   diag_block_us_median=round(paired["diag_us_median"], 2),
+                   halo_exposed_us=round(paired["diff_us_median"], 2),
+                   halo_exposed_iqr_us=[round(v, 2) for v in paired["diff_us_iqr"]],
+                   rounds=paired["rounds"])
+    return rec
 
 
 def distributed_block(world, backend, comm_info, timeout_s, ranks):
@@ -188,8 +200,9 @@ def distributed_block(world, backend, comm_info, timeout_s, ranks):
     return {"world_size": world, "backend": backend, "comm": comm_info["kind"],
             "rccl_version": comm_info["version"] or None, "comm_timeout_s": timeout_s, "ranks": ranks,
             "worst_rank": None if worst is None else worst["rank"],
-            "halo_hidden": "spmv_us_mean vs diag_block_us_mean per rank: the exchange runs on a second "
-                           "stream while A_d multiplies; halo_exposed_us is what it adds (A_o product included)"}
+            "halo_hidden": "per rank, A_d alone and the distributed SpMV launched in turn (interleaved rounds): the "
+                           "exchange runs on a second stream while A_d multiplies; halo_exposed_us is the median "
+                           "per-round difference, what it adds (A_o product and the fork / join included)"}
 
 
 def cpu_baseline(ai, aj, aa, x, seconds, all_cores=False):
@@ -423,8 +436,10 @@ def flan_standins(pkg, dev, reps, cpu_sample):
         del x, y
         flat = read_ceiling(nbytes, dev)
         rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],
-                                    "frac_of_ceiling": round(rec["stream"]["GBs"] / flat[0][0], 4),
-                                    "note": "the CSR byte count read once by aijhip_read_probe (mode 0)"}
+                                    "frac_of_ceiling": round(rec["stream"]["csr_effective_GBs"] / flat[0][0], 4),
+                                    "note": "the CSR byte count read once by aijhip_read_probe (mode 0); "
+                                            "frac_of_ceiling = the flat read's time / the stream launch's time "
+                                            "(the CSR bytes over both)"}
         if cpu_sample:
             t_cpu, reps_cpu, _ = cpu_baseline(ai, aj, aa, pkg.splitmix_uniform(m, 42), 3.0)
             rec["cpu_baseline"] = {"value": round(nbytes / t_cpu / 1e9, 3), "unit": "GB/s", "cores": 1,
@@ -450,21 +465,48 @@ def cpu_model():
 
 def halo_forms(op, x, stream, reps, rank, dev, m_loc, nnz_loc):
     """Per rank, what each exchange form adds on top of the diagonal block:
-    `reps` distributed SpMVs through the all-gather operator (op.native, built
-    with halo="allgather") and through its p2p twin (op.p2p_native(): same A_d,
-    ghost-numbered A_o, ncclSend/ncclRecv to the slab neighbours), against
-    the same launches of A_d alone. Returns {form: this rank's record}."""
+    distributed SpMVs through the all-gather operator (op.native, built with
+    halo="allgather") and through its p2p twin (op.p2p_native(): same A_d,
+    ghost-numbered A_o, ncclSend/ncclRecv to the slab neighbours), and A_d
+    alone, INTERLEAVED — one launch of each in turn for max(reps, 200) rounds,
+    HIP events on the compute stream around every launch, a 1.5 ms device
+    delay queued ahead of each round so the events time device work rather
+    than host enqueue overhead — so box drift hits the three alike; halo_exposed_us = the median over rounds of (form − A_d)
+    in the same round (two sequential means differed by
+    10 µs for the same operator). Returns {form: this rank's record}."""
     import torch
+    rounds = max(reps, 200)
     y = torch.empty(op.mloc, dtype=torch.float64, device=dev)
-    diag_us, _, _ = time_launches(lambda: op.A_d.mult(x, y, stream), stream, reps)
-    out = {}
+    fns = {"diag": lambda: op.A_d.mult(x, y, stream)}
     for form, nat in (("p2p", op.p2p_native()), ("allgather", op.native)):
-        for _ in range(3):
-            nat.mult(x, y, stream)
-        us, _, _ = time_launches(lambda: nat.mult(x, y, stream), stream, reps)
+        fns[form] = (lambda n: lambda: n.mult(x, y, stream))(nat)
+    for _ in range(3):
+        for f in fns.values():
+            f()
+    ev = {k: [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(rounds)]
+          for k in fns}
+    # a device delay ahead of every round: the round is fully enqueued before
+    # it runs, so the events time device work (fork / join included), not the
+    # host's launch overhead (RCCL's enqueue alone is tens of µs)
+    VL = importlib.import_module("petsc-openacc_amd.ksp")._veclib()
+    for i in range(rounds):
+        VL.aijhip_delay_probe(1500.0, stream.cuda_stream)
+        for k, f in fns.items():
+            a, b = ev[k][i]
+            a.record(stream)
+            f()
+            b.record(stream)
+    torch.cuda.synchronize()
+    us = {k: np.array([a.elapsed_time(b) for a, b in ev[k]]) * 1e3 for k in fns}
+    out = {}
+    for form in ("p2p", "allgather"):
+        d = us[form] - us["diag"]
+        paired = {"spmv_us_median": float(np.median(us[form])), "diag_us_median": float(np.median(us["diag"])),
+                  "diff_us_median": float(np.median(d)),
+                  "diff_us_iqr": [float(np.percentile(d, 25)), float(np.percentile(d, 75))], "rounds": rounds}
         out[form] = rank_record(rank, torch.cuda.current_device(),
                                 getattr(torch.cuda.get_device_properties(dev), "pci_bus_id", None), m_loc, nnz_loc,
-                                op.n_ghost, us / 1e3, diag_us / 1e3)
+                                op.n_ghost, float(np.mean(us[form])) / 1e3, float(np.mean(us["diag"])) / 1e3, paired)
     del y
     return out
 
@@ -759,7 +801,8 @@ def main():
 
     strong = None
     if distributed and not args.no_strong:
-        strong = guarded("strong_300", lambda: strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm))
+        G_s = args.strong_grid or G
+        strong = guarded("strong_300", lambda: strong_300(pkg, mpiaij, make_local, G_s, world, rank, dev, args, comm))
 
     # the solver legs run on the automatic layout (what a caller gets)
     if distributed and csr_forced:

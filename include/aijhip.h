@@ -40,6 +40,9 @@
  * objects are not thread-safe). Calls that take a `stream`
  * (a hipStream_t passed as void*, NULL = the legacy default stream) are
  * asynchronous with respect to the host; the ..._host variant synchronises.
+ * A handle's launches must not be in flight on two streams at once: the
+ * fork / join events of its side stream (AIJHIP_OPT_LONG_OVERLAP) are the
+ * handle's own, so a second caller stream would wait on the first's fork.
  */
 #ifndef AIJHIP_H
 #define AIJHIP_H
@@ -51,10 +54,8 @@ extern "C" {
 #endif
 
 /* 2: aijhip_info_t gained mult_layout_bytes and lost the fields of the
- * withdrawn options; the A/B-only options AIJHIP_OPT_XCD_REMAP /
- * _PERSISTENT / _CLAMPED_LOADS / _ROW_GROUP / _X_TILE /
- * _LONG_WINDOW and AIJHIP_KERNEL_MERGE were withdrawn (measured slower,
- * DESIGN.md §5) and return AIJHIP_ERR_ARG. */
+ * withdrawn A/B-only options; their option values and kernel 4 are reserved
+ * and return AIJHIP_ERR_ARG (measured slower). */
 #define AIJHIP_ABI_VERSION 2
 
 enum {
@@ -76,13 +77,8 @@ enum {
                                  `gang vector(32)` shape, step1 patch:19-21) */
     AIJHIP_KERNEL_VECTOR = 3, /* 2..64 lanes per row, __shfl tree reduction
                                  (64 = wavefront per row)                    */
-    AIJHIP_KERNEL_MERGE = 4   /* withdrawn in ABI 2 (aijhip_mat_set_kernel
-                                 returns AIJHIP_ERR_ARG): STREAM's planner
-                                 cuts the merge list of row ends and entries
-                                 into blocks of <= 512 rows and <= 4094
-                                 entries, rows longer than a block into x
-                                 windows or segments; an explicit merge-path
-                                 kernel measured 1.6x slower */
+    /* 4: reserved (the explicit merge-path kernel, withdrawn in ABI 2;
+       aijhip_mat_set_kernel returns AIJHIP_ERR_ARG) */
 };
 
 typedef struct aijhip_mat *aijhip_mat_t;
@@ -164,19 +160,16 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 /* Speed-only knobs of the STREAM kernel; results are identical for every
  * setting. Re-plans on the device. */
 enum {
-    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..11: lanes / LDS entries / rows per block
+    /* Values 2, 4, 5, 7, 11 and 15 (and kernel 4) are reserved:
+     * A/B-only variants withdrawn in ABI 2 (measured slower);
+     * setting them returns AIJHIP_ERR_ARG. */
+    AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..9: lanes / LDS entries / rows per block
                                        (DESIGN.md §Kernels); -1 (default):
                                        6 for short rows, 1 for long rows    */
-    AIJHIP_OPT_XCD_REMAP = 2,       /* withdrawn in ABI 2 (XCD-contiguous block
-                                       placement measured 3-10 % slower)     */
     AIJHIP_OPT_NT_LOADS = 3,        /* -1 (default): non-temporal for long rows
                                        with scattered gathers (the geometry-1
                                        operands), plain otherwise; 0 plain;
                                        1 non-temporal aa/aj loads            */
-    AIJHIP_OPT_PERSISTENT = 4,      /* withdrawn in ABI 2 (the persistent
-                                       pipelined STREAM measured 7-28 % slower) */
-    AIJHIP_OPT_CLAMPED_LOADS = 5,   /* withdrawn in ABI 2 (branch-free clamped
-                                       loads measured slower)                */
     AIJHIP_OPT_EXACT = 6,           /* 1: every row summed sequentially in
                                        PETSc's order. Default 0: row blocks
                                        whose mean row length exceeds 128 use
@@ -184,9 +177,6 @@ enum {
                                        within the fp64 bound); shorter rows
                                        (7-pt Poisson, FEM rows) are bit-exact
                                        either way                           */
-    AIJHIP_OPT_X_TILE = 7,          /* withdrawn in ABI 2 (x staged in LDS per
-                                       row block, up to four column windows:
-                                       slower at every default geometry)     */
     AIJHIP_OPT_LONG_XCD = 8,        /* 1 (default): segments of long rows are
                                        launched so that XCD q (slot % 8)
                                        reduces those whose columns lie in the
@@ -207,8 +197,6 @@ enum {
                                        MatMultAdd; forked from and joined to
                                        the caller's stream by events). Same
                                        results                                */
-    AIJHIP_OPT_ROW_GROUP = 11,      /* withdrawn in ABI 2 (register row groups
-                                       measured slower on every operand)     */
     AIJHIP_OPT_GATHER_SORT = 12,    /* MatMult / MatMultAdd from a copy of the
                                        row blocks with each block's entries
                                        sorted by column and their positions
@@ -233,10 +221,6 @@ enum {
                                        entries), else the automatic layout
                                        without them; costs 2 bytes per entry
                                        of device memory                      */
-    AIJHIP_OPT_LONG_WINDOW = 15,    /* withdrawn in ABI 2 (long rows by x column
-                                       window staged in LDS: the hub rows no
-                                       faster than 4096-entry segments, their
-                                       window sums slower to finish)         */
     AIJHIP_OPT_ROW_PATTERNS = 14    /* short-row operands whose rows follow at
                                        most 256 distinct column - row offset
                                        lists (stencils): no per-entry column

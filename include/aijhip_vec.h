@@ -52,6 +52,13 @@ int aijhip_vec_jacobi(int64_t n, const double *r, const double *dinv, double *z,
  * aligned. */
 int aijhip_read_probe(const double *d_buf, int64_t n, int mode, void *stream);
 
+/* Diagnostic: one wave on `stream` that finishes `us` microseconds after it
+ * starts (the device's constant-rate wall clock; 0 <= us <= 1e6). Queued
+ * ahead of timed launches it keeps the device busy while the host enqueues
+ * them, so HIP events around them time device work only, not host launch
+ * overhead (bench.py halo_forms, tools/halo_probe.py). */
+int aijhip_delay_probe(double us, void *stream);
+
 /* PCSetUp_Jacobi on A's rows: d_dinv[i] = 1 / (first stored a_ii, 0 -> 1). */
 int aijhip_mat_jacobi_inverse(aijhip_mat_t A, double *d_dinv, void *stream);
 

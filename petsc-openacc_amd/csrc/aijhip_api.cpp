@@ -94,7 +94,7 @@ void free_plan(aijhip::Plan &P) {
 }
 
 void free_matrix(aijhip_mat *A) {
-    A->plan_gen = aijhip::next_plan_gen();
+    A->plan_gen = A->values_gen = aijhip::next_plan_gen();
     free_plan(A->plan);
     hipFree(A->d_ai);
     hipFree(A->d_aj);
@@ -420,7 +420,7 @@ int plan_stream(aijhip_mat *A) {
 }
 
 int plan_build(aijhip_mat *A) {
-    A->plan_gen = aijhip::next_plan_gen();
+    A->plan_gen = A->values_gen = aijhip::next_plan_gen();
     free_plan(A->plan);
     aijhip::Plan &P = A->plan;
     int kernel = A->requested_kernel;
@@ -841,7 +841,7 @@ int aijhip_mat_create_from_device(int device, int32_t m, int32_t n, int64_t nz,
 int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes) {
     int rc = check_handle(A);
     if (rc) return rc;
-    if (kernel == AIJHIP_KERNEL_MERGE)
+    if (kernel == 4)  // reserved: the withdrawn MERGE kernel
         return fail(AIJHIP_ERR_ARG, "the MERGE kernel was withdrawn in ABI 2: STREAM's row blocks are the "
                                     "merge-path decomposition (DESIGN.md §5)");
     if (kernel < AIJHIP_KERNEL_AUTO || kernel > AIJHIP_KERNEL_VECTOR)
@@ -864,12 +864,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < -1 || value >= aijhip::kNumStreamGeoms) return fail(AIJHIP_ERR_ARG, "bad geometry");
             t.geom = value;
             break;
-        case AIJHIP_OPT_XCD_REMAP:
-        case AIJHIP_OPT_PERSISTENT:
-        case AIJHIP_OPT_CLAMPED_LOADS:
-        case AIJHIP_OPT_ROW_GROUP:
-        case AIJHIP_OPT_X_TILE:
-        case AIJHIP_OPT_LONG_WINDOW:
+        case 2: case 4: case 5: case 7: case 11: case 15:  // reserved (include/aijhip.h)
             return fail(AIJHIP_ERR_ARG, "option " + std::to_string(option) +
                                             " was withdrawn in ABI 2 (measured slower; DESIGN.md §5)");
         case AIJHIP_OPT_NT_LOADS:
@@ -920,6 +915,7 @@ int aijhip_mat_update_values(aijhip_mat_t A, const double *aa) {
     if (e == hipSuccess && A->plan.d_sslot)  // the gather-ordered copy of the values
         e = aijhip::build_gather_order(*A, A->plan, true);
     if (e != hipSuccess) return hipfail(e, "update values");
+    A->values_gen = aijhip::next_plan_gen();  // a set-up KSP redoes its PC set-up
     if (A->transpose) {  // A^T values are stale
         free_matrix(A->transpose);
         delete A->transpose;

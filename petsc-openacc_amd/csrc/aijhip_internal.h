@@ -44,10 +44,10 @@ constexpr StreamGeom kStreamGeoms[] = {
     {512, 4094, 512},    // 6: 8 waves, 4 pair-iterations (measured best)
     {1024, 8190, 1024},  // 7: 16 waves, 4 pair-iterations
     {256, 2046, 256},    // 8: 4 waves, 4 pair-iterations
-    {512, 6142, 512},    // 9: 8 waves, 6 pair-iterations, 48 KiB: an x tile of a +-2100-column band fits
-    {512, 8190, 512},    // 10: 8 waves, 8 pair-iterations, 64 KiB
-    {512, 2046, 512},    // 11: 8 waves, 2 pair-iterations, 16 KiB
+    {512, 2046, 512},    // 9: 8 waves, 2 pair-iterations, 16 KiB
 };
+// (Round 4's geometries of 6 and 8 pair-iterations, sized for the withdrawn
+// LDS x tiles, were removed in round 5; the 2-pair geometry is now 9.)
 constexpr int kNumStreamGeoms = sizeof(kStreamGeoms) / sizeof(kStreamGeoms[0]);
 constexpr int kMaxStreamNnzCap = 8192;
 // A row longer than the geometry's nnz_cap leaves the STREAM blocks and is split into
@@ -205,9 +205,14 @@ struct Plan {
 struct aijhip_mat {
     int device = 0;
     // changes whenever the device arrays or the plan are rebuilt (a fresh
-    // value of a process-wide counter): a captured HIP graph of launches on
-    // this handle is replayed only while it is unchanged (ksp.hip)
+    // value of a process-wide counter): a set-up KSP on this handle re-plans
+    // its fused launches when it moved (ksp.hip)
     uint64_t plan_gen = 0;
+    // changes whenever the values change (aijhip_mat_update_values, and
+    // every plan_gen change): a set-up KSP redoes its PC set-up (Jacobi's
+    // D^-1, the GAMG hierarchy) when it moved, as PETSc's PCSetUp does when
+    // the operator's state changed
+    uint64_t values_gen = 0;
     int n_cu = 256;  // compute units of the device
     int32_t m = 0, n = 0;
     int64_t nz = 0;

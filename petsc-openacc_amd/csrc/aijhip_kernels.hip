@@ -1413,7 +1413,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
                            P.d_cmeta);
         return hipGetLastError();
     }
-    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 10, "update the geometry dispatch");
 #define AIJHIP_OG(G)                                                                                             \
     case G:                                                                                                      \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_blocks),                      \
@@ -1422,7 +1422,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
-        AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8); AIJHIP_OG(9); AIJHIP_OG(10); AIJHIP_OG(11);
+        AIJHIP_OG(5); AIJHIP_OG(6); AIJHIP_OG(7); AIJHIP_OG(8); AIJHIP_OG(9);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_OG
@@ -1435,7 +1435,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
     if (P.kernel != AIJHIP_KERNEL_STREAM || A.compressed || P.n_longs > 0 || b0 < 0 || b0 + nb > P.n_blocks)
         return hipErrorInvalidValue;
     if (nb <= 0) return hipSuccess;
-    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
+    static_assert(kNumStreamGeoms == 10, "update the geometry dispatch");
 #define AIJHIP_BG(G)                                                                                             \
     case G:                                                                                                      \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, OpMult<false>>), dim3(nb),                   \
@@ -1445,7 +1445,7 @@ hipError_t launch_stream_blocks(const aijhip_mat &A, int32_t b0, int32_t nb, con
         break
     switch (P.tune.geom) {
         AIJHIP_BG(0); AIJHIP_BG(1); AIJHIP_BG(2); AIJHIP_BG(3); AIJHIP_BG(4);
-        AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8); AIJHIP_BG(9); AIJHIP_BG(10); AIJHIP_BG(11);
+        AIJHIP_BG(5); AIJHIP_BG(6); AIJHIP_BG(7); AIJHIP_BG(8); AIJHIP_BG(9);
         default: return hipErrorInvalidValue;
     }
 #undef AIJHIP_BG
@@ -1477,7 +1477,9 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     // Tuning::overlap: the long rows' segments and the wide blocks (the
     // latency-bound launches) on the side stream, forked from s before any of
     // them and joined back after; the row blocks on s meanwhile. Every launch
-    // writes its own rows of y, so the order between them is free.
+    // writes its own rows of y, so the order between them is free. The fork /
+    // join events live in the plan: a handle is used by one host thread at a
+    // time (include/aijhip.h, "Threading"), as PETSc's Mat is.
     const bool ovl = P.tune.overlap != 0 && P.side && !L.ridx && !dpart && !stop &&
                      (P.n_wblocks > 0 || P.n_longs > 0);
     hipStream_t sw = s;
@@ -1495,25 +1497,29 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
                                     P.d_partials, z, y);
         else hipLaunchKernelGGL(k_long_finish<false>, dim3(P.n_longs), dim3(64), 0, sw, P.d_longs, P.n_longs,
                                 P.d_partials, z, y);
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        e = hipGetLastError();
     }
     // Every geometry is dispatched explicitly: the kernel's LDS size must be
     // the one the plan's row blocks were cut for.
-    static_assert(kNumStreamGeoms == 12, "update the geometry dispatch");
-    if (P.n_blocks > 0) {
+    static_assert(kNumStreamGeoms == 10, "update the geometry dispatch");
+    if (e == hipSuccess && P.n_blocks > 0) {
 #define AIJHIP_SG(G) case G: stream_dispatch<AIJHIP_GEOM(G)>(A, P, L, x, z, y, add, s, dpart, stop, sw); break
         switch (P.tune.geom) {
             AIJHIP_SG(0); AIJHIP_SG(1); AIJHIP_SG(2); AIJHIP_SG(3); AIJHIP_SG(4);
-            AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9); AIJHIP_SG(10); AIJHIP_SG(11);
-            default: return hipErrorInvalidValue;
+            AIJHIP_SG(5); AIJHIP_SG(6); AIJHIP_SG(7); AIJHIP_SG(8); AIJHIP_SG(9);
+            default: e = hipErrorInvalidValue; break;
         }
 #undef AIJHIP_SG
-        if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (e == hipSuccess) e = hipGetLastError();
     }
-    if (ovl && ((e = hipEventRecord(P.ev_join, P.side)) != hipSuccess || (e = hipStreamWaitEvent(s, P.ev_join, 0)) !=
-                                                                            hipSuccess))
-        return e;
-    return hipSuccess;
+    // the join is recorded even after a failed launch, so the caller's stream
+    // never runs ahead of side-stream work that was already queued
+    if (ovl) {
+        const hipError_t j = hipEventRecord(P.ev_join, P.side);
+        const hipError_t w = j == hipSuccess ? hipStreamWaitEvent(s, P.ev_join, 0) : j;
+        if (e == hipSuccess) e = w;
+    }
+    return e;
 }
 
 hipError_t launch_scalar(const aijhip_mat &A, const double *x, const double *z, double *y,

@@ -131,6 +131,8 @@ struct aijhip_ksp {
     bool set_up = false;
     uint64_t a_gen = 0;  // the operator's plan generation at set-up: a re-planned
                          // operator (options, MatAssemblyEnd) is set up again
+    uint64_t v_gen = 0;  // its values generation: new values (aijhip_mat_update_values)
+                         // redo the PC set-up (D^-1, the GAMG hierarchy)
     bool fused = false;
     int vec_grid = 0;
     // CG vector kernels store with the non-temporal hint (tools: CG+Jacobi
@@ -451,7 +453,7 @@ int aijhip_ksp_set_initial_guess_nonzero(aijhip_ksp_t K, int flg) {
 int aijhip_ksp_set_up(aijhip_ksp_t K) {
     aijhip::Range range("KSPSetUp");
     if (!K) return kfail(AIJHIP_ERR_ARG, "NULL ksp");
-    if (K->set_up && K->a_gen == K->A->plan_gen) return AIJHIP_OK;
+    if (K->set_up && K->a_gen == K->A->plan_gen && K->v_gen == K->A->values_gen) return AIJHIP_OK;
     const auto t0 = std::chrono::steady_clock::now();
     aijhip_mat *A = K->A;
     KDeviceGuard g(A->device);
@@ -490,6 +492,7 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
     K->setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     K->set_up = true;
     K->a_gen = A->plan_gen;
+    K->v_gen = A->values_gen;
     return AIJHIP_OK;
 }
 

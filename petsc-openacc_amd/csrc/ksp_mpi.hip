@@ -450,7 +450,13 @@ namespace aijhip_mpi {
 
 // Start the ghost exchange on the exchange stream (ordered after everything
 // already enqueued on s, i.e. after x is written and the previous A_o
-// product has read the ghost vector).
+// product has read the ghost vector): the fork and the pack kernels. The
+// RCCL collective itself is enqueued by halo_finish — after the caller has
+// launched the diagonal block — because RCCL's host-side enqueue takes tens
+// of microseconds (hipExtLaunchKernel ~63 us median in profiles/r05/ of
+// round 5): issued first, it held back the A_d launch and the device
+// idled; issued second, A_d runs while the host is inside RCCL. The device
+// order is unchanged (the collective waits only for the fork).
 int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
     aijhip_comm *C = M->comm;
     if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
@@ -472,30 +478,7 @@ int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
     }
     if ((e = hipGetLastError()) != hipSuccess) return mhip(e, "halo pack");
     if (C->kind == AIJHIP_COMM_RCCL) {
-        const Rccl &R = rccl();
-        ncclResult_t r;
-        if (M->halo == AIJHIP_HALO_ALLGATHER) {
-            r = R.AllGather(M->d_sendbuf, M->d_ghost, (size_t)M->gather_len, ncclFloat64, C->nc, M->xs);
-            if (r != ncclSuccess) return nfail(r, "ncclAllGather");
-        } else {
-            if ((r = R.GroupStart()) != ncclSuccess) return nfail(r, "ncclGroupStart");
-            for (size_t q = 0; q < M->send_peer.size(); ++q) {
-                const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
-                const double *src = M->send_first[q] >= 0 ? x + M->send_first[q] : M->d_sendbuf + a;
-                if (n > 0 && (r = R.Send(src, (size_t)n, ncclFloat64, M->send_peer[q], C->nc, M->xs)) != ncclSuccess)
-                    break;
-            }
-            for (size_t p = 0; r == ncclSuccess && p < M->recv_peer.size(); ++p) {
-                const int64_t a = M->recv_off[p], n = M->recv_off[p + 1] - a;
-                if (n > 0 && (r = R.Recv(M->d_ghost + a, (size_t)n, ncclFloat64, M->recv_peer[p], C->nc, M->xs)) !=
-                                 ncclSuccess)
-                    break;
-            }
-            const ncclResult_t r2 = R.GroupEnd();
-            if (r != ncclSuccess) return nfail(r, "ncclSend/ncclRecv");
-            if (r2 != ncclSuccess) return nfail(r2, "ncclGroupEnd");
-        }
-        if ((e = hipEventRecord(M->ev_halo, M->xs)) != hipSuccess) return mhip(e, "halo event");
+        M->post_x = x;  // the collective is enqueued by halo_finish
     } else if (npack > 0) {
         if ((e = hipMemcpyAsync(M->h_send, M->d_sendbuf, sizeof(double) * (size_t)npack, hipMemcpyDeviceToHost,
                                 M->xs)) != hipSuccess)
@@ -504,12 +487,52 @@ int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
     return AIJHIP_OK;
 }
 
+namespace {
+
+// The RCCL collective of a posted exchange, on the exchange stream.
+int halo_send_rccl(aijhip_mpiaij *M) {
+    aijhip_comm *C = M->comm;
+    const double *x = M->post_x;
+    M->post_x = nullptr;
+    if (!x) return mfail(AIJHIP_ERR_STATE, "halo_finish without halo_post");
+    const Rccl &R = rccl();
+    ncclResult_t r;
+    if (M->halo == AIJHIP_HALO_ALLGATHER) {
+        r = R.AllGather(M->d_sendbuf, M->d_ghost, (size_t)M->gather_len, ncclFloat64, C->nc, M->xs);
+        if (r != ncclSuccess) return nfail(r, "ncclAllGather");
+    } else {
+        if ((r = R.GroupStart()) != ncclSuccess) return nfail(r, "ncclGroupStart");
+        for (size_t q = 0; q < M->send_peer.size(); ++q) {
+            const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
+            const double *src = M->send_first[q] >= 0 ? x + M->send_first[q] : M->d_sendbuf + a;
+            if (n > 0 && (r = R.Send(src, (size_t)n, ncclFloat64, M->send_peer[q], C->nc, M->xs)) != ncclSuccess)
+                break;
+        }
+        for (size_t p = 0; r == ncclSuccess && p < M->recv_peer.size(); ++p) {
+            const int64_t a = M->recv_off[p], n = M->recv_off[p + 1] - a;
+            if (n > 0 && (r = R.Recv(M->d_ghost + a, (size_t)n, ncclFloat64, M->recv_peer[p], C->nc, M->xs)) !=
+                             ncclSuccess)
+                break;
+        }
+        const ncclResult_t r2 = R.GroupEnd();
+        if (r != ncclSuccess) return nfail(r, "ncclSend/ncclRecv");
+        if (r2 != ncclSuccess) return nfail(r2, "ncclGroupEnd");
+    }
+    const hipError_t e = hipEventRecord(M->ev_halo, M->xs);
+    return e == hipSuccess ? AIJHIP_OK : mhip(e, "halo event");
+}
+
+}  // namespace
+
 // Finish the exchange (host transport: the callback, then the ghost upload)
 // and order s after it.
 int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
     aijhip_comm *C = M->comm;
     hipError_t e;
-    if (C->kind == AIJHIP_COMM_HOST) {
+    if (C->kind == AIJHIP_COMM_RCCL) {
+        const int rc = halo_send_rccl(M);
+        if (rc) return rc;
+    } else if (C->kind == AIJHIP_COMM_HOST) {
         const int64_t npack = M->halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send;
         int rc = wait_stream(C, M->xs);
         if (rc) return rc;
@@ -601,6 +624,10 @@ struct aijhip_kspmpi {
     int normtype = AIJHIP_KSP_NORM_PRECONDITIONED;
     int32_t poll = 8;
     bool set_up = false, fused = false;
+    // the blocks' plan and values generations at set-up: new values or a
+    // re-plan (on every rank: MatAssemblyEnd is collective) redo the set-up,
+    // as PETSc's PCSetUp does when the operator's state changed
+    uint64_t gens[4] = {0, 0, 0, 0};
     // PC GAMG = PETSc's -pc_type bjacobi -sub_pc_type gamg: a GAMG hierarchy of
     // this rank's diagonal block (a single-GPU KSP's set-up), one V-cycle per
     // application, no communication inside the preconditioner
@@ -639,8 +666,17 @@ void kspmpi_free(aijhip_kspmpi *K) {
     K->set_up = false;
 }
 
+void block_gens(const aijhip_mpiaij *M, uint64_t g[4]) {
+    g[0] = M->Ad->plan_gen;
+    g[1] = M->Ad->values_gen;
+    g[2] = M->Ao ? M->Ao->plan_gen : 0;
+    g[3] = M->Ao ? M->Ao->values_gen : 0;
+}
+
 int kspmpi_set_up(aijhip_kspmpi *K) {
-    if (K->set_up) return AIJHIP_OK;
+    uint64_t g[4];
+    block_gens(K->M, g);
+    if (K->set_up && std::equal(g, g + 4, K->gens)) return AIJHIP_OK;
     const auto t_setup = std::chrono::steady_clock::now();
     kspmpi_free(K);
     aijhip_mpiaij *M = K->M;
@@ -700,6 +736,7 @@ int kspmpi_set_up(aijhip_kspmpi *K) {
     }
     K->setup_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_setup).count();
     K->set_up = true;
+    std::copy(g, g + 4, K->gens);
     return AIJHIP_OK;
 }
 

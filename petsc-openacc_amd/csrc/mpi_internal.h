@@ -49,6 +49,7 @@ struct aijhip_mpiaij {
     double *h_send = nullptr, *h_ghost = nullptr;  // host transport staging (pinned)
     hipStream_t xs = nullptr;
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
+    const double *post_x = nullptr;  // RCCL: the x of the posted exchange, sent by halo_finish
     int o_grid = 1;
 };
 
@@ -67,8 +68,11 @@ int comm_allreduce_host(aijhip_comm *C, double *v, int32_t n);
 // Collective: every rank calls it with nranks-long vectors.
 int comm_sendrecv(aijhip_comm *C, const std::vector<std::vector<uint64_t>> &out,
                   std::vector<std::vector<uint64_t>> &in);
-// The ghost exchange of an operator (post on its exchange stream after `s`,
-// finish: `s` waits for the ghosts in M->d_ghost).
+// The ghost exchange of an operator: post = the fork from `s` and the pack
+// kernels on its exchange stream; the caller then launches the diagonal
+// product on `s`; finish = the RCCL collective (or the host transport's
+// exchange), then `s` waits for the ghosts in M->d_ghost. Every post is
+// followed by exactly one finish.
 int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s);
 int halo_finish(aijhip_mpiaij *M, hipStream_t s);
 // y = A_d x + A_o g (MatMult_MPIAIJ); part/opart/S/fused: the CG epilogue

@@ -247,6 +247,27 @@ int aijhip_read_probe(const double *d_buf, int64_t n, int mode, void *stream) {
     return vhip(hipGetLastError(), "read_probe");
 }
 
+// One wave that returns after `ticks` of the constant-rate wall clock (a
+// bounded loop: it exits on the clock whatever else runs).
+__global__ __launch_bounds__(64) void k_delay_probe(uint64_t ticks) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+int aijhip_delay_probe(double us, void *stream) {
+    if (!(us >= 0.0) || us > 1e6) return verr(AIJHIP_ERR_ARG, "delay_probe: 0 <= us <= 1e6");
+    static int khz = 0;  // wall-clock rate (kHz), queried once
+    if (khz == 0) {
+        int dev = 0, v = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev);
+        if (e != hipSuccess || v <= 0) return vhip(e != hipSuccess ? e : hipErrorInvalidValue, "delay_probe clock");
+        khz = v;
+    }
+    hipLaunchKernelGGL(k_delay_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, (uint64_t)(us * khz / 1000.0));
+    return vhip(hipGetLastError(), "delay_probe");
+}
+
 int aijhip_mat_jacobi_inverse(aijhip_mat_t A, double *d_dinv, void *stream) {
     if (!A || !d_dinv) return verr(AIJHIP_ERR_ARG, "mat_jacobi_inverse: NULL argument");
     if (A->m == 0) return AIJHIP_OK;

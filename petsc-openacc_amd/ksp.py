@@ -308,7 +308,7 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
 # or none.
 
 VEC_SYMBOLS = ("aijhip_vec_aypx", "aijhip_vec_dot", "aijhip_vec_cg_update", "aijhip_vec_jacobi",
-               "aijhip_mat_jacobi_inverse", "aijhip_read_probe")
+               "aijhip_mat_jacobi_inverse", "aijhip_read_probe", "aijhip_delay_probe")
 
 _vec_bound = False
 
@@ -326,6 +326,7 @@ def _veclib():
         L.aijhip_vec_jacobi.argtypes = [i64, _P, _P, _P, _P, _P]
         L.aijhip_mat_jacobi_inverse.argtypes = [_P, _P, _P]
         L.aijhip_read_probe.argtypes = [_P, i64, ctypes.c_int, _P]
+        L.aijhip_delay_probe.argtypes = [d, _P]
         _vec_bound = True
     return L
 

@@ -16,7 +16,13 @@
  * CG iteration, the PC (gamg / jacobi / none with PETSc's option names) and
  * the convergence test run on the device (aijhip_ksp.h). main_ksp.cpp reads
  * its, reason, rnorm and the history back through the usual KSP getters.
- * Any other operator or PC falls back to PETSc's own KSPCG.
+ * Any other operator or PC falls back to PETSc's own KSPCG, run as an inner
+ * KSP on the caller's operators and PC (this KSP never changes its own type,
+ * so nothing it owns is freed under a running solve).
+ *
+ * STATUS: not yet working code until it is compiled and run against PETSc
+ * 3.7 — the PETSc-facing half is written to the 3.7 headers but has never
+ * been built.
  */
 #include <petsc/private/kspimpl.h>
 #include <petsc/private/pcimpl.h>
@@ -31,9 +37,12 @@ PETSC_EXTERN PetscErrorCode AIJHIPGetHandle(Mat A, aijhip_mat_t *h);
 
 typedef struct {
   aijhip_ksp_t     k;
-  aijhip_mat_t     h;     /* the handle k was set up on */
-  PetscObjectState state; /* the operator's state at that set-up */
+  aijhip_mat_t     h;       /* the handle k was set up on */
+  PetscObjectState state;   /* the operator's state at that set-up */
   int              pc;
+  PC               user_pc; /* the caller's PC while ksp->pc is a PCNONE stand-in */
+  KSP              inner;   /* PETSc's KSPCG on the caller's PC: the fall-back */
+  PetscBool        fallback;
 } KSP_CGHIP;
 
 static PetscErrorCode KSPCGHIPFree(KSP_CGHIP *c)
@@ -45,32 +54,94 @@ static PetscErrorCode KSPCGHIPFree(KSP_CGHIP *c)
   PetscFunctionReturn(0);
 }
 
+/* The caller's PC: the one KSPGetPC handed out, even while ksp->pc is the
+ * stand-in. */
+static PC KSPCGHIPUserPC(KSP ksp)
+{
+  KSP_CGHIP *c = (KSP_CGHIP*)ksp->data;
+  return c->user_pc ? c->user_pc : ksp->pc;
+}
+
 /* The reference's PCs, by PETSc type name; -1: not offered on the device. */
 static PetscErrorCode KSPCGHIPPCType(KSP ksp, int *pc)
 {
+  PC             upc = KSPCGHIPUserPC(ksp);
   PetscBool      is;
   PetscErrorCode ierr;
 
   PetscFunctionBegin;
   *pc = -1;
-  ierr = PetscObjectTypeCompare((PetscObject)ksp->pc, PCGAMG, &is);CHKERRQ(ierr);
+  ierr = PetscObjectTypeCompare((PetscObject)upc, PCGAMG, &is);CHKERRQ(ierr);
   if (is) { *pc = AIJHIP_PC_GAMG; PetscFunctionReturn(0); }
-  ierr = PetscObjectTypeCompare((PetscObject)ksp->pc, PCJACOBI, &is);CHKERRQ(ierr);
+  ierr = PetscObjectTypeCompare((PetscObject)upc, PCJACOBI, &is);CHKERRQ(ierr);
   if (is) { *pc = AIJHIP_PC_JACOBI; PetscFunctionReturn(0); }
-  ierr = PetscObjectTypeCompare((PetscObject)ksp->pc, PCNONE, &is);CHKERRQ(ierr);
+  ierr = PetscObjectTypeCompare((PetscObject)upc, PCNONE, &is);CHKERRQ(ierr);
   if (is) *pc = AIJHIP_PC_NONE;
   PetscFunctionReturn(0);
 }
 
-/* PETSc's own CG for what the device path does not cover. */
+/* Device path: KSPSetUp calls PCSetUp(ksp->pc) after ops->setup, which for
+ * PCGAMG would build PETSc's host hierarchy beside the device one (inside
+ * main_ksp.cpp's timed "create solver"). Put a PCNONE stand-in in ksp->pc and
+ * keep the caller's PC (its type and options are what the device KSP reads). */
+static PetscErrorCode KSPCGHIPStandIn(KSP ksp)
+{
+  KSP_CGHIP      *c = (KSP_CGHIP*)ksp->data;
+  PC             none;
+  Mat            Amat, Pmat;
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  if (c->user_pc) PetscFunctionReturn(0);
+  ierr = PetscObjectReference((PetscObject)ksp->pc);CHKERRQ(ierr);
+  c->user_pc = ksp->pc;
+  ierr = PCGetOperators(c->user_pc, &Amat, &Pmat);CHKERRQ(ierr);
+  ierr = PCCreate(PetscObjectComm((PetscObject)ksp), &none);CHKERRQ(ierr);
+  ierr = PCSetType(none, PCNONE);CHKERRQ(ierr);
+  ierr = PCSetOperators(none, Amat, Pmat);CHKERRQ(ierr);
+  ierr = KSPSetPC(ksp, none);CHKERRQ(ierr); /* references none, releases the caller's (held above) */
+  ierr = PCDestroy(&none);CHKERRQ(ierr);
+  PetscFunctionReturn(0);
+}
+
+/* Give the caller's PC back to ksp->pc (the fall-back runs PETSc's CG on it). */
+static PetscErrorCode KSPCGHIPRestorePC(KSP ksp)
+{
+  KSP_CGHIP      *c = (KSP_CGHIP*)ksp->data;
+  PetscErrorCode ierr;
+
+  PetscFunctionBegin;
+  if (!c->user_pc) PetscFunctionReturn(0);
+  ierr = KSPSetPC(ksp, c->user_pc);CHKERRQ(ierr);
+  ierr = PCDestroy(&c->user_pc);CHKERRQ(ierr); /* drops the reference taken by KSPCGHIPStandIn */
+  PetscFunctionReturn(0);
+}
+
+/* PETSc's own CG for what the device path does not cover: an inner KSPCG on
+ * the caller's operators and PC, with this KSP's tolerances and norm. This
+ * KSP keeps its type (no KSPSetType from inside its own set-up or solve). */
 static PetscErrorCode KSPCGHIPFallBack(KSP ksp)
 {
+  KSP_CGHIP      *c = (KSP_CGHIP*)ksp->data;
+  Mat            Amat, Pmat;
   PetscErrorCode ierr;
 
   PetscFunctionBegin;
   ierr = PetscInfo(ksp, "cghip: operator or PC not on the device; using KSPCG\n");CHKERRQ(ierr);
-  ierr = KSPSetType(ksp, KSPCG);CHKERRQ(ierr);
-  ierr = KSPSetUp(ksp);CHKERRQ(ierr);
+  ierr = KSPCGHIPFree(c);CHKERRQ(ierr);
+  ierr = KSPCGHIPRestorePC(ksp);CHKERRQ(ierr);
+  if (!c->inner) {
+    ierr = KSPCreate(PetscObjectComm((PetscObject)ksp), &c->inner);CHKERRQ(ierr);
+    ierr = KSPSetType(c->inner, KSPCG);CHKERRQ(ierr);
+  }
+  ierr = KSPGetOperators(ksp, &Amat, &Pmat);CHKERRQ(ierr);
+  ierr = KSPSetOperators(c->inner, Amat, Pmat);CHKERRQ(ierr);
+  ierr = KSPSetPC(c->inner, ksp->pc);CHKERRQ(ierr);
+  ierr = KSPSetTolerances(c->inner, ksp->rtol, ksp->abstol, ksp->divtol, ksp->max_it);CHKERRQ(ierr);
+  ierr = KSPSetNormType(c->inner, ksp->normtype);CHKERRQ(ierr);
+  ierr = KSPSetInitialGuessNonzero(c->inner, ksp->guess_zero ? PETSC_FALSE : PETSC_TRUE);CHKERRQ(ierr);
+  ierr = KSPSetUp(c->inner);CHKERRQ(ierr);
+  c->fallback = PETSC_TRUE;
   PetscFunctionReturn(0);
 }
 
@@ -98,6 +169,8 @@ static PetscErrorCode KSPSetUp_CGHIP(KSP ksp)
     ierr = KSPCGHIPFallBack(ksp);CHKERRQ(ierr);
     PetscFunctionReturn(0);
   }
+  c->fallback = PETSC_FALSE;
+  ierr = KSPCGHIPStandIn(ksp);CHKERRQ(ierr);
   ierr = PetscObjectStateGet((PetscObject)A, &state);CHKERRQ(ierr);
   if (c->k && c->h == h && c->state == state && c->pc == pc) PetscFunctionReturn(0);
   ierr = KSPCGHIPFree(c);CHKERRQ(ierr);
@@ -145,7 +218,18 @@ static PetscErrorCode KSPSolve_CGHIP(KSP ksp)
   PetscErrorCode    ierr;
 
   PetscFunctionBegin;
+  /* values changed since the set-up (KSPSolve does not call ops->setup
+   * again for that): refresh the device KSP, or fall back */
   ierr = KSPSetUp_CGHIP(ksp);CHKERRQ(ierr);
+  if (c->fallback) {
+    ierr = KSPSetTolerances(c->inner, ksp->rtol, ksp->abstol, ksp->divtol, ksp->max_it);CHKERRQ(ierr);
+    ierr = KSPSetInitialGuessNonzero(c->inner, ksp->guess_zero ? PETSC_FALSE : PETSC_TRUE);CHKERRQ(ierr);
+    ierr = KSPSolve(c->inner, ksp->vec_rhs, ksp->vec_sol);CHKERRQ(ierr);
+    ierr = KSPGetIterationNumber(c->inner, &ksp->its);CHKERRQ(ierr);
+    ierr = KSPGetResidualNorm(c->inner, &ksp->rnorm);CHKERRQ(ierr);
+    ierr = KSPGetConvergedReason(c->inner, &ksp->reason);CHKERRQ(ierr);
+    PetscFunctionReturn(0);
+  }
   rc = aijhip_ksp_set_tolerances(c->k, ksp->rtol, ksp->abstol, ksp->divtol, (int32_t)ksp->max_it);
   if (!rc) rc = aijhip_ksp_set_initial_guess_nonzero(c->k, ksp->guess_zero ? 0 : 1);
   if (rc) SETERRQ1(PetscObjectComm((PetscObject)ksp), PETSC_ERR_LIB, "aijhip: %s", aijhip_last_error());
@@ -177,6 +261,8 @@ static PetscErrorCode KSPDestroy_CGHIP(KSP ksp)
 
   PetscFunctionBegin;
   ierr = KSPCGHIPFree((KSP_CGHIP*)ksp->data);CHKERRQ(ierr);
+  ierr = KSPCGHIPRestorePC(ksp);CHKERRQ(ierr);
+  ierr = KSPDestroy(&((KSP_CGHIP*)ksp->data)->inner);CHKERRQ(ierr);
   ierr = KSPDestroyDefault(ksp);CHKERRQ(ierr);
   PetscFunctionReturn(0);
 }

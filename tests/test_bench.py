@@ -53,6 +53,28 @@ def test_distributed_block_schema(bench):
     assert bench.distributed_block(1, "gloo", {"kind": "host", "version": 0}, 60.0, [])["rccl_version"] is None
 
 
+def test_rank_record_paired_median(bench):
+    """halo_forms' interleaved timing: halo_exposed_us is the median of the
+    per-round differences, not the difference of two separately timed means."""
+    paired = {"spmv_us_median": 470.5, "diag_us_median": 468.0, "diff_us_median": 1.25, "diff_us_iqr": [0.5, 2.0],
+              "rounds": 200}
+    rec = bench.rank_record(0, 0, 0x10, 27_000_000, 188_460_000, 0, 0.4810, 0.4690, paired)
+    assert rec["halo_exposed_us"] == 1.25 and rec["rounds"] == 200
+    assert rec["spmv_us_median"] == 470.5 and rec["diag_block_us_median"] == 468.0
+    assert rec["halo_exposed_iqr_us"] == [0.5, 2.0]
+    assert rec["spmv_us_mean"] == 481.0 and rec["diag_block_us_mean"] == 469.0
+
+
+def test_slab_bounds_strong_300_at_8(bench):
+    """The driver's N = 8 strong line splits 300 planes 38 x 4 + 37 x 4
+    (DMDA PETSC_DECIDE: the first 300 % 8 ranks take one more)."""
+    import importlib
+    mp_mod = importlib.import_module("petsc-openacc_amd.mpiaij")
+    b = [mp_mod.slab_bounds(300, 8, r) for r in range(8)]
+    assert [e - s for s, e in b] == [38, 38, 38, 38, 37, 37, 37, 37]
+    assert b[0][0] == 0 and b[-1][1] == 300 and all(b[i][1] == b[i + 1][0] for i in range(7))
+
+
 @pytest.mark.parametrize("name", ["bench_rehearse_n2_r02e.json", "bench_mpi_n1_r02e.json",
                                   "bench_rehearse_n2_r02j.json", "bench_mpi_n1_r02j.json",
                                   "bench_rehearse_n2_r02n.json", "bench_mpi_n1_r02n.json"])

@@ -142,6 +142,51 @@ def test_gpu_vcycle_fused_smoothers_bitwise(pkg, monkeypatch):
         np.testing.assert_allclose(xv, out[0][2], rtol=1e-10, atol=1e-12 * np.abs(out[0][2]).max())
 
 
+@pytest.mark.gpu
+def test_gpu_cg_gamg_fused_default_deterministic_and_values_update(pkg):
+    """The default (fused) CG + GAMG pinned bit for bit: two
+    solves on fresh handles give the same history and solution bits; and a
+    set-up KSP whose operator got new values (aijhip_mat_update_values, the
+    MatAssemblyEnd re-upload) redoes its PC set-up — its next solve equals, bit
+    for bit, a fresh KSP's on the new values (PETSc's PCSetUp on a changed
+    operator state), not the stale hierarchy's."""
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available()
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    N = 24
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, _ = pkg.poisson_vectors(N)
+    b = torch.from_numpy(rhs).cuda()
+    aa2 = aa * 2.0 + np.where(aj == np.repeat(np.arange(len(ai) - 1), np.diff(ai)), -1.0, 0.0)
+
+    def solve(vals, A=None, ksp=None):
+        own = A is None
+        A = A or pkg.SeqAIJHIP(ai, aj, vals)
+        ksp = ksp or K.KSPCG(A, pc="gamg", rtol=1e-14, atol=1e-12)
+        x = torch.empty_like(b)
+        ksp.solve(b, x)
+        r = (ksp.its, np.array(ksp.history()), x.cpu().numpy())
+        if own:
+            ksp.destroy()
+            A.destroy()
+        return r
+
+    def same(r, q):
+        assert r[0] == q[0]
+        assert np.array_equal(r[1].view(np.uint64), q[1].view(np.uint64))
+        assert np.array_equal(r[2].view(np.uint64), q[2].view(np.uint64))
+
+    first, again = solve(aa), solve(aa)
+    same(first, again)
+    fresh2 = solve(aa2)
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        with K.KSPCG(A, pc="gamg", rtol=1e-14, atol=1e-12) as ksp:
+            same(solve(aa, A, ksp), first)
+            A.update_values(aa2)
+            same(solve(aa2, A, ksp), fresh2)
+    assert fresh2[0] != first[0] or not np.array_equal(fresh2[2], first[2])
+
+
 def test_oracle_vcycle_preconditions_cg():
     ai, aj, aa, rhs, exact = seqaij.create_system(10, 10, 10)
     m = len(ai) - 1

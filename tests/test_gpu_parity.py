@@ -337,19 +337,34 @@ def test_stream_ordering_on_side_stream(pkg, dev):
         assert_bits(yd.cpu().numpy(), g["y"])
 
 
+def _csr_layout(A):
+    """The headline's layout: PETSc's aj / aa as stored (bench.py --layout
+    csr): no row patterns, no column codes."""
+    A.set_option("row_patterns", 0)
+    A.set_option("column_codes", 0)
+    info = A.info()
+    assert not info["row_patterns"] and not info["column_codes"] and not info.get("gather_sorted")
+    return info
+
+
+@pytest.mark.parametrize("layout", ["auto", "csr"])
 @pytest.mark.parametrize("N", [100, 300])
-def test_full_size_poisson_bitexact(pkg, dev, coracle, N):
+def test_full_size_poisson_bitexact(pkg, dev, coracle, N, layout):
     """BASELINE configs[0]/[1] operand at full size: STREAM vs the C oracle,
-    bit for bit, plus the size-independent properties A*1 = row sums and
-    linearity A(x + 2v) = Ax + 2Av (exact here: powers of two)."""
+    bit for bit, plus the size-independent property A*1 = row sums — in the
+    library's automatic layout (row patterns) and in the CSR layout the
+    headline `value` times (the timed kernel pinned at the
+    size it is timed)."""
     ai, aj, aa = pkg.poisson_csr(N)
     m = N ** 3
     x = pkg.splitmix_uniform(m, 42)
     ref = coracle.matmult(ai, aj, aa, x, omp=True)
     with pkg.SeqAIJHIP(ai, aj, aa) as A:
-        info = A.info()
+        info = _csr_layout(A) if layout == "csr" else A.info()
         assert info["kernel"] == "stream" and info["n_long_rows"] == 0
         assert info["nz"] == 7 * N ** 3 - 6 * N ** 2
+        if layout == "csr":  # the bytes the headline's roofline divides by
+            assert info["mult_layout_bytes"] == pkg.algorithmic_bytes(m, m, info["nz"])
         xd = to_dev(x, dev)
         yd = torch.empty_like(xd)
         A.mult(xd, yd)
@@ -381,6 +396,10 @@ def test_max_size_600_device_assembly_bitexact(pkg, dev, coracle):
         A.mult(xd, yd)
         torch.cuda.synchronize()
         y = yd.cpu().numpy()
+        _csr_layout(A)  # and the headline's CSR kernel on the same operand
+        A.mult(xd, yd)
+        torch.cuda.synchronize()
+        y_csr = yd.cpu().numpy()
         del xd, yd
     finally:
         A.destroy()
@@ -389,6 +408,7 @@ def test_max_size_600_device_assembly_bitexact(pkg, dev, coracle):
     ref = coracle.matmult(ai, aj, aa, x, omp=True)
     del ai, aj, aa
     assert_bits(y, ref)
+    assert_bits(y_csr, ref)
 
 
 def test_skewed_flan_standin_all_kernels(pkg, dev, coracle):
