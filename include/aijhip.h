@@ -55,8 +55,10 @@ extern "C" {
 
 /* 2: aijhip_info_t gained mult_layout_bytes and lost the fields of the
  * withdrawn A/B-only options; their option values and kernel 4 are reserved
- * and return AIJHIP_ERR_ARG (measured slower). */
-#define AIJHIP_ABI_VERSION 2
+ * and return AIJHIP_ERR_ARG (measured slower).
+ * 3: aijhip_gamg_params_t gained coarsen / square_graph / eig_ksp (PETSc
+ * 3.7's MIS coarsening and CG emax estimate as options). */
+#define AIJHIP_ABI_VERSION 3
 
 enum {
     AIJHIP_OK = 0,

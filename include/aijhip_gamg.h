@@ -10,9 +10,14 @@
  * aggregation; tentative prolongator from the near-null space (constant
  * vector on the finest level; the QR factors carry it down); one Jacobi
  * smoothing step P = (I - 1.4/emax D^-1 A) P0 (PCGAMGOptProlongator_AGG's
- * alpha = -1.4/emax); Galerkin coarse operator Pt A P. Aggregation is a
- * deterministic greedy pass in natural order (PETSc's MIS ordering is not
- * reproduced: GAMG iteration parity with PETSc is unpinned).
+ * alpha = -1.4/emax); Galerkin coarse operator Pt A P. Aggregation: a
+ * deterministic greedy pass in natural order (coarsen 0, the default), or
+ * PETSc 3.7's own agg coarsening restated (coarsen 1: a maximal independent
+ * set of the squared graph in a random order, aggregates smoothed — agg.c
+ * PCGAMGCoarsen_AGG / smoothAggs, mis.c; PETSc's random stream is not
+ * reproduced), with emax from a power iteration (eig_ksp 0) or from CG's
+ * Lanczos tridiagonal as PCGAMGOptProlongator_AGG does (eig_ksp 1). GAMG
+ * iteration parity with PETSc is unpinned either way (PETSc is absent).
  * The solve-phase V-cycle runs on the device inside aijhip_ksp
  * (AIJHIP_PC_GAMG), whose set-up builds the large levels on the device
  * (device_min_rows) with results identical to aijhip_gamg_build_host.
@@ -40,6 +45,14 @@ typedef struct aijhip_gamg_params {
                               * stays on the host); smaller ones on the host.
                               * 0 = every level on the device, INT32_MAX = all
                               * on the host. Same hierarchy either way.     */
+    /* ABI 3: */
+    int32_t coarsen;         /* 0: greedy aggregation (natural order);
+                              * 1: PETSc 3.7 agg's MIS (see above)          */
+    int32_t square_graph;    /* -pc_gamg_square_graph (1): coarsen 1 squares
+                              * the graph on this many levels from the finest */
+    int32_t eig_ksp;         /* emax(D^-1 A): 0 power iteration; 1 CG (Lanczos),
+                              * PETSc's estimate                             */
+    int32_t pad0;
 } aijhip_gamg_params_t;
 
 typedef struct aijhip_gamg_host *aijhip_gamg_host_t;

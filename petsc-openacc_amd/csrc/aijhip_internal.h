@@ -258,6 +258,8 @@ hipError_t launch_stream_dot(const aijhip_mat &A, const double *x, double *y, do
 bool stream_mg_fusable(const aijhip_mat &A);
 // y = D^-1 A x in PETSc's row order (exact), for the GAMG set-up.
 hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const double *x, double *y, hipStream_t s);
+// y = A x in PETSc's row order on a STREAM plan (exact; the GAMG set-up's CG estimate).
+hipError_t launch_mult_exact(const aijhip_mat &A, const double *x, double *y, hipStream_t s);
 // r = b - A x on a STREAM plan (residual in the SpMV epilogue).
 hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
                            bool nt, const int *stop = nullptr);

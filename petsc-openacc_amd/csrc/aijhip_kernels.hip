@@ -1468,6 +1468,10 @@ hipError_t launch_dinv_mult(const aijhip_mat &A, const double *dinv, const doubl
     return launch_stream_op(A, OpDinvMult{x, dinv, y}, nullptr, s, 1);  // PETSc row order
 }
 
+hipError_t launch_mult_exact(const aijhip_mat &A, const double *x, double *y, hipStream_t s) {
+    return launch_stream_op(A, OpMult<false>{x, nullptr, y, false}, nullptr, s, 1);  // PETSc row order
+}
+
 hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, double *y,
                          bool add, hipStream_t s, double *dpart, const int *stop) {
     hipError_t e = compressed_prologue(A, z, y, add, s);

@@ -427,9 +427,158 @@ hipError_t exclusive_sum(const int32_t *in, int32_t *out, int32_t n, hipStream_t
     return e;
 }
 
+// ---- PETSc 3.7 agg's MIS (gamg_internal.h aggregate_mis) on the device.
+// The sequential pass visits the nodes in key order and roots an aggregate
+// at every node no earlier root lies within reach of (G2: two steps of S
+// when squared, one otherwise), so the roots are the lexicographically-first
+// independent set of G2 by key, unique: node i is a root iff no lower-key
+// node within reach of it is one. Rounds decide it in place: an undecided
+// node that sees a lower-key root within reach is OUT; one whose lower-key
+// nodes within reach are all OUT is a root; otherwise it waits. Decisions
+// are final and depend only on final states, so a stale read only delays
+// one. With random keys the chains are short (tens of rounds, not the
+// natural order's 2.35 N).
+constexpr int32_t kMisUndecided = 0, kMisRoot = 1, kMisOut = 2, kMisSingle = 3;
+
+template <class F>
+__device__ __forceinline__ void for_reach(int32_t i, bool square, const int32_t *__restrict__ si,
+                                          const int32_t *__restrict__ sj, F f) {
+    const int32_t a1 = si[i + 1];
+    for (int32_t a = si[i]; a < a1; ++a) {
+        const int32_t j = sj[a];
+        if (!f(j)) return;
+        if (!square) continue;
+        const int32_t b1 = si[j + 1];
+        for (int32_t b = si[j]; b < b1; ++b) {
+            const int32_t k = sj[b];
+            if (k != i && !f(k)) return;
+        }
+    }
+}
+
+__global__ void k_mis_init(int32_t m, const int32_t *__restrict__ si, int32_t *state) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) state[i] = si[i] == si[i + 1] ? kMisSingle : kMisUndecided;
+}
+
+__global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__restrict__ si,
+                                                   const int32_t *__restrict__ sj, bool square, int32_t level,
+                                                   int32_t *state, unsigned long long *left) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool waits = false;
+    if (i < m && state[i] == kMisUndecided) {
+        const uint64_t ki = aijhip_gamg::mis_key(i, level);
+        bool out = false;
+        for_reach(i, square, si, sj, [&](int32_t w) {
+            const int32_t st = __builtin_nontemporal_load(state + w);  // (another lane may have decided it)
+            if ((st == kMisRoot || st == kMisUndecided) && aijhip_gamg::mis_key(w, level) < ki) {
+                if (st == kMisRoot) {
+                    out = true;
+                    return false;
+                }
+                waits = true;
+            }
+            return true;
+        });
+        if (out) state[i] = kMisOut;
+        else if (!waits) state[i] = kMisRoot;
+        else waits = true;
+    }
+    const unsigned long long nw = __popcll(__ballot(waits));
+    if ((threadIdx.x & 63) == 0 && nw) atomicAdd(left, nw);
+}
+
+// parent: a root itself; an OUT node the lowest-key root within reach (the
+// first root of the pass to take it), then (squared: smoothAggs) the
+// highest-index root among its S neighbours when it has one; singletons -1.
+// flag[i] = 1 for the roots (their scan numbers the aggregates).
+__global__ __launch_bounds__(256) void k_mis_parent(int32_t m, const int32_t *__restrict__ si,
+                                                    const int32_t *__restrict__ sj, bool square, int32_t level,
+                                                    const int32_t *__restrict__ state, int32_t *parent,
+                                                    int32_t *flag) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int32_t st = state[i];
+    flag[i] = st == kMisRoot;
+    if (st == kMisRoot) { parent[i] = i; return; }
+    if (st != kMisOut) { parent[i] = -1; return; }
+    int32_t best = -1;
+    uint64_t bk = ~0ull;
+    for_reach(i, square, si, sj, [&](int32_t w) {
+        if (state[w] == kMisRoot) {
+            const uint64_t kw = aijhip_gamg::mis_key(w, level);
+            if (kw < bk) { bk = kw; best = w; }
+        }
+        return true;
+    });
+    if (square) {
+        int32_t hi = -1;
+        for (int32_t a = si[i]; a < si[i + 1]; ++a) {
+            const int32_t j = sj[a];
+            if (state[j] == kMisRoot && j > hi) hi = j;
+        }
+        if (hi >= 0) best = hi;
+    }
+    parent[i] = best;
+}
+
+__global__ void k_mis_number(int32_t m, const int32_t *__restrict__ parent, const int32_t *__restrict__ cidx,
+                             int32_t *agg) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) agg[i] = parent[i] >= 0 ? cidx[parent[i]] : -1;
+}
+
 }  // namespace
 
 namespace aijhip_gamg {
+
+hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj, bool square, int32_t level,
+                                int32_t *agg, int32_t *na, int32_t *rounds) {
+    *na = 0;
+    *rounds = 0;
+    if (m == 0) return hipSuccess;
+    int32_t *state = nullptr, *parent = nullptr, *flag = nullptr, *cidx = nullptr;
+    unsigned long long *left = nullptr;
+    const unsigned g = blocks_for(m, 256);
+    hipError_t e = dalloc(&state, m);
+    if (e == hipSuccess) e = dalloc(&left, 1);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_mis_init, dim3(g), dim3(256), 0, nullptr, m, si, state);
+        e = hipGetLastError();
+    }
+    // every round decides at least the lowest-key undecided node, so m
+    // rounds always suffice; random keys need a few tens
+    for (int32_t r = 0; e == hipSuccess && r < m; ++r) {
+        unsigned long long h = 0;
+        if ((e = hipMemsetAsync(left, 0, sizeof(h), nullptr)) != hipSuccess) break;
+        hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, state, left);
+        if ((e = hipGetLastError()) != hipSuccess) break;
+        if ((e = hipMemcpy(&h, left, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) break;
+        *rounds = r + 1;
+        if (h == 0) break;
+    }
+    if (e == hipSuccess) e = dalloc(&parent, m);
+    if (e == hipSuccess) e = dalloc(&flag, m);
+    if (e == hipSuccess) e = dalloc(&cidx, m);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_mis_parent, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, state, parent,
+                           flag);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = exclusive_sum(flag, cidx, m, nullptr);
+    if (e == hipSuccess) {
+        int32_t lc = 0, lf = 0;
+        e = hipMemcpy(&lc, cidx + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(&lf, flag + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
+        *na = lc + lf;
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(k_mis_number, dim3(g), dim3(256), 0, nullptr, m, parent, cidx, agg);
+        e = hipGetLastError();
+    }
+    hipFree(state); hipFree(parent); hipFree(flag); hipFree(cidx); hipFree(left);
+    return e;
+}
 
 hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *sj, int32_t max_rounds,
                                    int32_t *phase1, int32_t *na, int32_t *rounds, bool *done) {

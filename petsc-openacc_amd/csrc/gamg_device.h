@@ -105,5 +105,9 @@ hipError_t aggregate_phase1_device(int32_t m, const int32_t *si, const int32_t *
 // the host, the result is scattered back. *na in: the count so far; out: the
 // final count.
 hipError_t aggregate_phase3_device(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg, int32_t *na);
+// PETSc 3.7 agg's MIS aggregates (gamg_internal.h aggregate_mis, node for
+// node) from the symmetric strength graph S: agg[0, m) in [-1, *na).
+hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj, bool square, int32_t level,
+                                int32_t *agg, int32_t *na, int32_t *rounds);
 
 }  // namespace aijhip_gamg

@@ -444,6 +444,43 @@ __global__ void k_block_dot(int64_t n, const double *__restrict__ a, double *par
     part[q] = s;
 }
 
+// one lane per 256-entry block: sum of a[i] * b[i], left to right
+__global__ void k_block_dot2(int64_t n, const double *__restrict__ a, const double *__restrict__ b, double *part) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i0 = q * kDotBlock;
+    if (i0 >= n) return;
+    const int64_t e = min(n, i0 + kDotBlock);
+    double s = 0.0;
+    for (int64_t i = i0; i < e; ++i) s += a[i] * b[i];
+    part[q] = s;
+}
+
+// CG's emax estimate (gamg_setup.cpp estimate_emax_cg): the start, r -= a w
+// with z = D^-1 r, and p = z + b p
+__global__ void k_cgest_start(int32_t m, const double *__restrict__ dinv, double *r, double *z, double *p) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double v = 2.0 * ((double)(mix64(0x5EEDULL + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL) >> 11) *
+                            (1.0 / 9007199254740992.0)) - 1.0;
+    r[i] = v;
+    z[i] = dinv[i] * v;
+    p[i] = z[i];
+}
+
+__global__ void k_cgest_update(int32_t m, double a, const double *__restrict__ w, const double *__restrict__ dinv,
+                               double *r, double *z) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double ri = r[i] - a * w[i];
+    r[i] = ri;
+    z[i] = dinv[i] * ri;
+}
+
+__global__ void k_cgest_dir(int32_t m, double b, const double *__restrict__ z, double *p) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) p[i] = z[i] + b * p[i];
+}
+
 __global__ void k_div(int32_t m, const double *w, double nw, double *v) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) v[i] = w[i] / nw;
@@ -485,7 +522,7 @@ __global__ void k_agg_norm(int32_t na, const int32_t *__restrict__ seg, const do
 // of count ones is count exactly, whatever the order)
 __global__ void k_agg_count(int32_t m, const int32_t *__restrict__ agg, int32_t *count) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) atomicAdd(&count[agg[i]], 1);
+    if (i < m && agg[i] >= 0) atomicAdd(&count[agg[i]], 1);  // (-1: MIS's removed singleton)
 }
 
 __global__ void k_agg_norm_count(int32_t na, const int32_t *__restrict__ count, double *Bc) {
@@ -497,8 +534,23 @@ __global__ void k_tentative(int32_t m, const int32_t *__restrict__ agg, const do
                             const double *__restrict__ Bc, double *p0) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    const double c = Bc[agg[i]];
+    const double c = agg[i] >= 0 ? Bc[agg[i]] : 0.0;
     p0[i] = c > 0.0 ? (B ? B[i] : 1.0) / c : 0.0;  // B == nullptr: the constant near-null space
+}
+
+// P0 with empty rows for the nodes no aggregate took (agg -1, MIS's removed
+// singletons): flag / scan, then the compacted entries.
+__global__ void k_member_flags(int32_t m, const int32_t *__restrict__ agg, int32_t *flag) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) flag[i] = agg[i] >= 0;
+}
+
+__global__ void k_member_compact(int32_t m, const int32_t *__restrict__ agg, const double *__restrict__ v,
+                                 const int32_t *__restrict__ ai, int32_t *aj, double *aa) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m || agg[i] < 0) return;
+    aj[ai[i]] = agg[i];
+    aa[ai[i]] = v ? v[i] : 1.0;
 }
 
 __global__ void k_iota(int32_t n, int32_t *v) {
@@ -695,6 +747,7 @@ __global__ __launch_bounds__(256) void k_rowprod_p0(int32_t m, const int32_t *__
     for (int32_t k = ai[i]; k < k1; ++k) {
         const int32_t j = aj[k];
         const int32_t c = agg[j];
+        if (c < 0) continue;  // an empty row of P0
         const double p = WRITE ? aa[k] * p0[j] : 0.0;
         bool hit = false;
 #pragma unroll
@@ -740,7 +793,7 @@ __global__ void k_prolong_len(int32_t m, const int32_t *__restrict__ ti, const i
                               const int32_t *__restrict__ agg, int32_t *len) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    bool has = false;
+    bool has = agg[i] < 0;  // (no P0 entry)
     for (int32_t k = ti[i]; k < ti[i + 1]; ++k) has |= tj[k] == agg[i];
     len[i] = ti[i + 1] - ti[i] + (has ? 0 : 1);
 }
@@ -752,8 +805,8 @@ __global__ void k_prolong_fill(int32_t m, const int32_t *__restrict__ ti, const 
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
     int32_t p = pi[i];
-    bool placed = false;
     const int32_t g = agg[i];
+    bool placed = g < 0;  // (no P0 entry to place)
     const double p0 = p0v[i];
     for (int32_t k = ti[i]; k < ti[i + 1]; ++k) {
         const int32_t c = tj[k];
@@ -792,6 +845,51 @@ hipError_t scan_offsets(const int32_t *cnt, int32_t m, int32_t *off, int64_t *to
     }
 done:
     hipFree(w); hipFree(o); hipFree(stmp);
+    return e;
+}
+
+// P0 (na columns) as a CSR: row i holds (agg[i], v[i]) (v nullptr: 1.0), or
+// nothing where agg[i] = -1 (MIS's removed singletons). Without such rows
+// the arrays are agg and v themselves (borrowed: *own false, only P0.ai
+// allocated); else compacted copies (*own true).
+hipError_t p0_csr(int32_t m, int32_t na, const int32_t *agg, const double *v, DCsr &P0, bool *own) {
+    P0 = DCsr();
+    P0.m = m;
+    P0.n = na;
+    *own = false;
+    unsigned long long *nfree = nullptr;
+    unsigned long long h = 0;
+    hipError_t e = dalloc(&nfree, 1);
+    if (e == hipSuccess) e = hipMemset(nfree, 0, sizeof(h));
+    if (e == hipSuccess && m > 0) {
+        hipLaunchKernelGGL(k_count_value, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, -1, nfree);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpy(&h, nfree, sizeof(h), hipMemcpyDeviceToHost);
+    hipFree(nfree);
+    if (e != hipSuccess) return e;
+    if ((e = dalloc(&P0.ai, (int64_t)m + 1)) != hipSuccess) return e;
+    if (h == 0 && v) {
+        hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, P0.ai);
+        P0.nz = m;
+        P0.aj = const_cast<int32_t *>(agg);
+        P0.aa = const_cast<double *>(v);
+        return hipGetLastError();
+    }
+    *own = true;
+    int32_t *flag = nullptr;
+    if ((e = dalloc(&flag, m)) == hipSuccess) {
+        if (m > 0) hipLaunchKernelGGL(k_member_flags, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, flag);
+        e = scan_offsets(flag, m, P0.ai, &P0.nz);
+    }
+    hipFree(flag);
+    if (e == hipSuccess && (e = dalloc(&P0.aj, P0.nz + 2)) == hipSuccess && (e = dalloc(&P0.aa, P0.nz + 2)) == hipSuccess &&
+        m > 0) {
+        hipLaunchKernelGGL(k_member_compact, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, v, P0.ai, P0.aj,
+                           P0.aa);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) P0.release();
     return e;
 }
 
@@ -876,7 +974,8 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used = nu
 // a row with more than kP0Cap distinct columns sends the whole product to
 // the general form (same bits either way).
 constexpr int kP0Cap = 8;
-int rowprod_p0(const DCsr &A, const DCsr &P0, DCsr &C, int n_cu, int *cols_used) {
+int rowprod_p0(const DCsr &A, const DCsr &P0, const int32_t *agg, const double *p0, DCsr &C, int n_cu,
+               int *cols_used) {
     // (rows of A longer than the list on average: the hash form directly)
     if (A.nz > (int64_t)kP0Cap * std::max<int32_t>(A.m, 1)) return rowprod(A, P0, C, n_cu, cols_used);
     C = DCsr();
@@ -888,7 +987,7 @@ int rowprod_p0(const DCsr &A, const DCsr &P0, DCsr &C, int n_cu, int *cols_used)
     if ((e = dalloc(&cnt, A.m)) != hipSuccess) return herr(e, "product counts");
     if (A.m > 0)
         hipLaunchKernelGGL((k_rowprod_p0<kP0Cap, false>), dim3(g), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           P0.aj, P0.aa, nullptr, nullptr, nullptr, cnt);
+                           agg, p0, nullptr, nullptr, nullptr, cnt);
     int32_t mn = 0;
     if ((e = hipGetLastError()) != hipSuccess || (e = min_of(cnt, A.m, &mn)) != hipSuccess) {
         hipFree(cnt);
@@ -910,7 +1009,7 @@ int rowprod_p0(const DCsr &A, const DCsr &P0, DCsr &C, int n_cu, int *cols_used)
     C.nz = total;
     if (A.m > 0)
         hipLaunchKernelGGL((k_rowprod_p0<kP0Cap, true>), dim3(g), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           P0.aj, P0.aa, C.ai, C.aj, C.aa, cnt);
+                           agg, p0, C.ai, C.aj, C.aa, cnt);
     e = hipGetLastError();
     hipFree(cnt);
     if (e != hipSuccess) {
@@ -1195,19 +1294,25 @@ hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B,
         hipFree(count);
         return e;
     }
-    if ((e = dalloc(&ai, (int64_t)m + 1)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, ai);
+    DCsr P0;
+    bool own = false;
+    if ((e = p0_csr(m, na, agg, B, P0, &own)) != hipSuccess) return e;
+    ai = P0.ai;
     {
         aijhip_mat v;  // non-owning view
         v.m = m;
         v.n = na;
-        v.nz = m;
-        v.d_ai = ai;
-        v.d_aj = const_cast<int32_t *>(agg);
-        v.d_aa = const_cast<double *>(B);
+        v.nz = P0.nz;
+        v.d_ai = P0.ai;
+        v.d_aj = P0.aj;
+        v.d_aa = P0.aa;
         e = aijhip::build_transpose(v, &tai, &taj, &taa, nullptr);
         v.d_ai = v.d_aj = nullptr;
         v.d_aa = nullptr;
+    }
+    if (own) {
+        hipFree(P0.aj);
+        hipFree(P0.aa);
     }
     if (e == hipSuccess) {
         if (na > 0) hipLaunchKernelGGL(k_agg_norm, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, tai, taa, Bc);
@@ -1216,6 +1321,19 @@ hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B,
     }
     hipFree(ai); hipFree(tai); hipFree(taj); hipFree(taa);
     return e;
+}
+
+// a . b in the host builder's blocked order (block sums on the device, then
+// summed left to right on the host)
+double host_blocked_dot(const double *d_a, const double *d_b, int64_t n, double *d_part, std::vector<double> &h_part,
+                        hipError_t *e) {
+    const int64_t nb = (n + kDotBlock - 1) / kDotBlock;
+    if (nb > 0) hipLaunchKernelGGL(k_block_dot2, dim3(blocks_for(nb, 64)), dim3(64), 0, nullptr, n, d_a, d_b, d_part);
+    h_part.resize((size_t)nb);
+    *e = nb > 0 ? hipMemcpy(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost) : hipSuccess;
+    double s = 0.0;
+    for (int64_t q = 0; q < nb; ++q) s += h_part[q];
+    return s;
 }
 
 double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vector<double> &h_part, hipError_t *e) {
@@ -1270,12 +1388,50 @@ DCsr view_of(const aijhip_mat &A) {
 // The power iteration for emax(D^-1 A) (10 steps from a fixed start, norms
 // summed on the host in 256-entry blocks: the host builder's order) on a
 // host thread of its own.
+// cg: CG's Lanczos estimate instead (gamg_setup.cpp estimate_emax_cg: the
+// same start, A p in PETSc's row order, the same blocked dots, the
+// tridiagonal's emax by the host's bisection).
 struct EmaxJob {
     std::thread th;
     double emax = 1.0;
     hipError_t e = hipSuccess;
-    double *v = nullptr, *w = nullptr, *part = nullptr;
-    void start(const aijhip_mat &A, const double *dinv, int its) {
+    double *v = nullptr, *w = nullptr, *part = nullptr, *r = nullptr, *z = nullptr;
+    void start(const aijhip_mat &A, const double *dinv, int its, bool cg = false) {
+        if (cg) {
+            th = std::thread([this, &A, dinv, its] {
+                (void)hipSetDevice(A.device);
+                const int32_t m = A.m;
+                const unsigned g256 = blocks_for(m, 256);
+                std::vector<double> h_part, alpha, beta;
+                if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
+                    (e = dalloc(&r, m)) != hipSuccess || (e = dalloc(&z, m)) != hipSuccess ||
+                    (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
+                    return;
+                if (m == 0) return;
+                double *p = v;
+                hipLaunchKernelGGL(k_cgest_start, dim3(g256), dim3(256), 0, nullptr, m, dinv, r, z, p);
+                double rz = host_blocked_dot(z, r, m, part, h_part, &e);
+                if (e != hipSuccess) return;
+                for (int it = 0; it < its; ++it) {
+                    if ((e = aijhip::launch_mult_exact(A, p, w, nullptr)) != hipSuccess) return;
+                    const double pw = host_blocked_dot(p, w, m, part, h_part, &e);
+                    if (e != hipSuccess) return;
+                    if (!(pw != 0.0 && rz != 0.0)) break;
+                    const double a = rz / pw;
+                    alpha.push_back(a);
+                    hipLaunchKernelGGL(k_cgest_update, dim3(g256), dim3(256), 0, nullptr, m, a, w, dinv, r, z);
+                    const double rzn = host_blocked_dot(z, r, m, part, h_part, &e);
+                    if (e != hipSuccess) return;
+                    const double b = rzn / rz;
+                    beta.push_back(b);
+                    hipLaunchKernelGGL(k_cgest_dir, dim3(g256), dim3(256), 0, nullptr, m, b, z, p);
+                    rz = rzn;
+                }
+                e = hipDeviceSynchronize();
+                if (e == hipSuccess && !alpha.empty()) emax = aijhip_gamg::lanczos_emax(alpha, beta);
+            });
+            return;
+        }
         th = std::thread([this, &A, dinv, its] {
             const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
             auto c0 = std::chrono::steady_clock::now();
@@ -1315,8 +1471,8 @@ struct EmaxJob {
         if (th.joinable()) th.join();
     }
     void release() {
-        hipFree(v); hipFree(w); hipFree(part);
-        v = w = part = nullptr;
+        hipFree(v); hipFree(w); hipFree(part); hipFree(r); hipFree(z);
+        v = w = part = r = z = nullptr;
     }
     ~EmaxJob() {
         join();
@@ -1497,9 +1653,20 @@ strength_done:
     // memory; the same aggregates either way. Phase 2 on the device; phase
     // 3 (sequential) over the nodes left.
     lap("strength kernels");
-    if (emax_its > 0) job.start(A, dinv, emax_its);
-    GTRY(dalloc(&d_ph, m), "alloc");
+    if (emax_its > 0) job.start(A, dinv, emax_its, p.eig_ksp == 1);
     GTRY(dalloc(&d_aggv, m), "alloc");
+    if (p.coarsen == 1) {  // PETSc 3.7 agg's MIS (gamg_aggregate.hip), node for node the host's
+        int32_t rounds = 0;
+        GTRY(aijhip_gamg::aggregate_mis_device(m, si, sj, (int32_t)level < p.square_graph, (int32_t)level, d_aggv,
+                                               &na, &rounds),
+             "MIS aggregation");
+        if (log)
+            std::fprintf(stderr, "gamg device level %zu MIS%s: %d rounds, %d aggregates\n", level,
+                         (int32_t)level < p.square_graph ? " (squared graph)" : "", rounds, na);
+        lap("aggregate");
+        goto level_done;
+    }
+    GTRY(dalloc(&d_ph, m), "alloc");
     GTRY(dalloc(&d_left, 1), "alloc");
     {
         int32_t max_rounds = 0;
@@ -1635,6 +1802,7 @@ int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, 
     double *d_p0 = nullptr, *d_Bc = nullptr;
     int32_t *plen = nullptr;
     DCsr P0, T;
+    bool p0_own = false;  // P0's aj / aa compacted copies (MIS singletons) rather than d_agg / d_p0
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](const char *what) {
@@ -1649,15 +1817,9 @@ int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, 
     GTRY(dalloc(&d_Bc, na), "alloc");
     GTRY(tentative(m, na, d_agg, d_B, d_Bc, d_p0, b_ones), "tentative prolongator");
     lap("tentative");
-    P0.m = m;
-    P0.n = na;
-    P0.nz = m;
-    GTRY(dalloc(&P0.ai, (int64_t)m + 1), "alloc");
-    hipLaunchKernelGGL(k_iota, dim3(blocks_for((int64_t)m + 1, 256)), dim3(256), 0, nullptr, m, P0.ai);
-    P0.aj = d_agg;
-    P0.aa = d_p0;
+    GTRY(p0_csr(m, na, d_agg, d_p0, P0, &p0_own), "tentative prolongator");
     if (nsmooths > 0) {
-        if ((rc = rowprod_p0(Av, P0, T, n_cu, cols_used))) goto done;
+        if ((rc = rowprod_p0(Av, P0, d_agg, d_p0, T, n_cu, cols_used))) goto done;
         lap("A*P0");
         P.m = m;
         P.n = na;
@@ -1674,17 +1836,21 @@ int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, 
     } else {
         P.m = m;
         P.n = na;
-        P.nz = m;
+        P.nz = P0.nz;
         GTRY(dalloc(&P.ai, (int64_t)m + 1), "alloc");
-        GTRY(dalloc(&P.aj, (int64_t)m + 2), "alloc");
-        GTRY(dalloc(&P.aa, (int64_t)m + 2), "alloc");
+        GTRY(dalloc(&P.aj, P0.nz + 2), "alloc");
+        GTRY(dalloc(&P.aa, P0.nz + 2), "alloc");
         GTRY(hipMemcpy(P.ai, P0.ai, sizeof(int32_t) * ((size_t)m + 1), hipMemcpyDeviceToDevice), "copy");
-        GTRY(hipMemcpy(P.aj, d_agg, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
-        GTRY(hipMemcpy(P.aa, d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToDevice), "copy");
+        GTRY(hipMemcpy(P.aj, P0.aj, sizeof(int32_t) * (size_t)P0.nz, hipMemcpyDeviceToDevice), "copy");
+        GTRY(hipMemcpy(P.aa, P0.aa, sizeof(double) * (size_t)P0.nz, hipMemcpyDeviceToDevice), "copy");
     }
 done:
 #undef GTRY
     hipFree(P0.ai);
+    if (p0_own) {
+        hipFree(P0.aj);
+        hipFree(P0.aa);
+    }
     hipFree(plen);
     T.release();
     lap("freed");
@@ -1819,7 +1985,7 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
     std::thread prestage;
     {
         int32_t rounds = 0;
-        if (A0->m >= p.device_min_rows && device_phase1(A0->m, A0->nz - A0->m, &rounds))
+        if (p.coarsen == 0 && A0->m >= p.device_min_rows && device_phase1(A0->m, A0->nz - A0->m, &rounds))
             prestage = std::thread([bytes = (size_t)A0->m * 9 / 2, device = A0->device] {
                 (void)hipSetDevice(device);
                 std::unique_lock<std::mutex> lock;

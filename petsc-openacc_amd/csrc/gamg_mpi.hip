@@ -688,6 +688,9 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
     aijhip_comm *C = M0->comm;
     if (M0->halo != AIJHIP_HALO_P2P)
         return mfail(AIJHIP_ERR_ARG, "distributed GAMG: the operator needs the p2p halo (AIJHIP_HALO_P2P)");
+    if (p.coarsen != 0 || p.eig_ksp != 0)  // (every rank refuses alike: the parameters are the caller's, collective)
+        return mfail(AIJHIP_ERR_ARG, "distributed GAMG: coarsen 1 / eig_ksp 1 (PETSc's MIS and CG estimate) are "
+                                     "single-GPU options");
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](size_t l, const char *what) {

@@ -219,6 +219,50 @@ double estimate_emax(const View &A, const std::vector<double> &dinv, int its, in
     return lam;
 }
 
+// emax(D^-1 A) from CG's Lanczos tridiagonal (PETSc 3.7's estimate for the
+// smoother: KSPCG + PC Jacobi, norm none, `its` iterations from x = 0 on a
+// random b, KSPComputeExtremeSingularValues; oracle/gamg.py
+// estimate_emax_cg): the same b as the power iteration's start (not
+// normalised), dots in the blocked order, w = A p summed in storage order.
+double estimate_emax_cg(const View &A, const std::vector<double> &dinv, int its, int nt) {
+    const int32_t m = A.m;
+    if (m == 0) return 1.0;
+    std::vector<double> r(m), z(m), p(m), w(m);
+#pragma omp parallel for schedule(static) num_threads(nt)
+    for (int32_t i = 0; i < m; ++i) {
+        r[i] = 2.0 * ((double)(mix64(0x5EEDULL + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL) >> 11) *
+                      (1.0 / 9007199254740992.0)) - 1.0;
+        z[i] = dinv[i] * r[i];
+        p[i] = z[i];
+    }
+    double rz = dot(z, r, nt);
+    std::vector<double> alpha, beta;
+    for (int it = 0; it < its; ++it) {
+#pragma omp parallel for schedule(static) num_threads(nt)
+        for (int32_t i = 0; i < m; ++i) {
+            double s = 0.0;
+            for (int32_t k = A.ai[i]; k < A.ai[i + 1]; ++k) s += A.aa[k] * p[A.aj[k]];
+            w[i] = s;
+        }
+        const double pw = dot(p, w, nt);
+        if (!(pw != 0.0 && rz != 0.0)) break;
+        const double a = rz / pw;
+        alpha.push_back(a);
+#pragma omp parallel for schedule(static) num_threads(nt)
+        for (int32_t i = 0; i < m; ++i) {
+            r[i] = r[i] - a * w[i];
+            z[i] = dinv[i] * r[i];
+        }
+        const double rzn = dot(z, r, nt);
+        const double b = rzn / rz;
+        beta.push_back(b);
+#pragma omp parallel for schedule(static) num_threads(nt)
+        for (int32_t i = 0; i < m; ++i) p[i] = z[i] + b * p[i];
+        rz = rzn;
+    }
+    return alpha.empty() ? 1.0 : aijhip_gamg::lanczos_emax(alpha, beta);
+}
+
 // C = A * B (CSR x CSR). Row-parallel; per row, each product is added into
 // its column's accumulator in (A entry, B entry) traversal order starting
 // from 0.0 (the order of scipy's csr_matmat), then columns sorted.
@@ -322,23 +366,27 @@ void transpose(const View &A, CSR &T, int nt) {
 void prolongator(const View &A, const std::vector<double> &dinv, const std::vector<int32_t> &agg,
                  int32_t na, const std::vector<double> &B, double alpha, int nsmooths, CSR &P,
                  std::vector<double> &Bc, int nt) {
+    // (agg[i] = -1: a node no aggregate took, MIS's removed singleton: an
+    // empty row of P0)
     const int32_t m = A.m;
     Bc.assign(na, 0.0);
-    for (int32_t i = 0; i < m; ++i) Bc[agg[i]] += B[i] * B[i];
+    for (int32_t i = 0; i < m; ++i)
+        if (agg[i] >= 0) Bc[agg[i]] += B[i] * B[i];
     for (int32_t a = 0; a < na; ++a) Bc[a] = std::sqrt(Bc[a]);
     CSR P0;
     P0.m = m;
     P0.n = na;
     P0.ai.resize((size_t)m + 1);
-    P0.aj.resize(m);
-    P0.aa.resize(m);
+    P0.ai[0] = 0;
+    for (int32_t i = 0; i < m; ++i) P0.ai[i + 1] = P0.ai[i] + (agg[i] >= 0 ? 1 : 0);
+    P0.aj.resize(P0.ai[m]);
+    P0.aa.resize(P0.ai[m]);
 #pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < m; ++i) {
-        P0.ai[i] = i;
-        P0.aj[i] = agg[i];
-        P0.aa[i] = Bc[agg[i]] > 0.0 ? B[i] / Bc[agg[i]] : 0.0;
+        if (agg[i] < 0) continue;
+        P0.aj[P0.ai[i]] = agg[i];
+        P0.aa[P0.ai[i]] = Bc[agg[i]] > 0.0 ? B[i] / Bc[agg[i]] : 0.0;
     }
-    P0.ai[m] = m;
     if (nsmooths <= 0) { P = std::move(P0); return; }
     CSR T;
     spgemm(A, view(P0), T, nt);
@@ -350,7 +398,8 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
     std::vector<int32_t> len(m);
 #pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < m; ++i) {
-        const bool has = std::binary_search(T.aj.begin() + T.ai[i], T.aj.begin() + T.ai[i + 1], agg[i]);
+        const bool has = agg[i] < 0 ||
+                         std::binary_search(T.aj.begin() + T.ai[i], T.aj.begin() + T.ai[i + 1], agg[i]);
         len[i] = (T.ai[i + 1] - T.ai[i]) + (has ? 0 : 1);
     }
     for (int32_t i = 0; i < m; ++i) P.ai[i + 1] = P.ai[i] + len[i];
@@ -359,9 +408,9 @@ void prolongator(const View &A, const std::vector<double> &dinv, const std::vect
 #pragma omp parallel for schedule(static) num_threads(nt)
     for (int32_t i = 0; i < m; ++i) {
         int64_t p = P.ai[i];
-        bool placed = false;
         const int32_t g = agg[i];
-        const double p0 = P0.aa[i];
+        bool placed = g < 0;  // (no P0 entry to place)
+        const double p0 = g < 0 ? 0.0 : P0.aa[P0.ai[i]];
         for (int32_t k = T.ai[i]; k < T.ai[i + 1]; ++k) {
             const int32_t c = T.aj[k];
             if (!placed && g < c) { P.aj[p] = g; P.aa[p] = p0; ++p; placed = true; }
@@ -444,6 +493,88 @@ int32_t aggregate_phase1_rows(int32_t r0, int32_t r1, const int32_t *si, const i
     return na;
 }
 
+int32_t aggregate_mis(int32_t m, const int32_t *si, const int32_t *sj, bool square, int32_t level, int32_t *agg) {
+    // the visiting order: ascending key (the key's low half is the node)
+    std::vector<uint64_t> order((size_t)m);
+    for (int32_t i = 0; i < m; ++i) order[i] = mis_key(i, level);
+    std::sort(order.begin(), order.end());
+    enum : int8_t { kNotDone = 0, kDeleted = 1, kSelected = 2, kRemoved = 3 };
+    std::vector<int8_t> state((size_t)m, kNotDone);
+    std::vector<int32_t> parent((size_t)m, -1);
+    for (const uint64_t key : order) {
+        const int32_t r = (int32_t)(uint32_t)key;
+        if (state[r] != kNotDone) continue;
+        if (si[r] == si[r + 1]) {  // G2 row = {r}: a singleton, removed
+            state[r] = kRemoved;
+            continue;
+        }
+        state[r] = kSelected;
+        parent[r] = r;
+        auto take = [&](int32_t j) {
+            if (state[j] == kNotDone) {
+                state[j] = kDeleted;
+                parent[j] = r;
+            }
+        };
+        for (int32_t a = si[r]; a < si[r + 1]; ++a) {  // G2 = G1 o G1, G1 = S + I
+            const int32_t u = sj[a];
+            take(u);
+            if (square)
+                for (int32_t b = si[u]; b < si[u + 1]; ++b) take(sj[b]);
+        }
+    }
+    if (square)  // smoothAggs
+        for (int32_t r = 0; r < m; ++r) {
+            if (state[r] != kSelected) continue;
+            for (int32_t a = si[r]; a < si[r + 1]; ++a) {
+                const int32_t j = sj[a];
+                if (state[j] == kDeleted && parent[j] != r) parent[j] = r;
+            }
+        }
+    std::vector<int32_t> cidx((size_t)m, -1);
+    int32_t na = 0;
+    for (int32_t i = 0; i < m; ++i)
+        if (state[i] == kSelected) cidx[i] = na++;
+    for (int32_t i = 0; i < m; ++i) agg[i] = parent[i] >= 0 ? cidx[parent[i]] : -1;
+    return na;
+}
+
+double tridiag_max_eig(const std::vector<double> &d, const std::vector<double> &e) {
+    const size_t n = d.size();
+    double lo = d[0], hi = d[0];
+    for (size_t k = 0; k < n; ++k) {
+        const double r = (k > 0 ? std::fabs(e[k - 1]) : 0.0) + (k + 1 < n ? std::fabs(e[k]) : 0.0);
+        lo = std::min(lo, d[k] - r);
+        hi = std::max(hi, d[k] + r);
+    }
+    auto below = [&](double x) {  // Sturm count of eigenvalues < x
+        size_t c = 0;
+        double q = 1.0;
+        for (size_t k = 0; k < n; ++k) {
+            q = (d[k] - x) - (k > 0 ? (e[k - 1] * e[k - 1]) / q : 0.0);
+            if (q == 0.0) q = -1e-300;
+            if (q < 0.0) ++c;
+        }
+        return c;
+    };
+    for (int it = 0; it < 200; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (!(lo < mid && mid < hi)) break;
+        if (below(mid) >= n) hi = mid;
+        else lo = mid;
+    }
+    return hi;
+}
+
+double lanczos_emax(const std::vector<double> &alpha, const std::vector<double> &beta) {
+    const size_t n = alpha.size();
+    std::vector<double> d(n), e(n > 0 ? n - 1 : 0);
+    d[0] = 1.0 / alpha[0];
+    for (size_t k = 1; k < n; ++k) d[k] = 1.0 / alpha[k] + beta[k - 1] / alpha[k - 1];
+    for (size_t k = 0; k + 1 < n; ++k) e[k] = std::sqrt(std::fabs(beta[k])) / alpha[k];
+    return tridiag_max_eig(d, e);
+}
+
 int32_t aggregate_phase1(int32_t m, const int32_t *si, const int32_t *sj, int32_t *agg) {
     std::fill(agg, agg + m, -1);
     std::vector<uint64_t> taken(((size_t)m + 63) / 64, 0);
@@ -484,6 +615,10 @@ int aijhip_gamg_params_default(aijhip_gamg_params_t *p) {
     p->eig_its = 10;
     p->threads = 0;
     p->device_min_rows = 20000;
+    p->coarsen = 0;
+    p->square_graph = 1;
+    p->eig_ksp = 0;
+    p->pad0 = 0;
     return AIJHIP_OK;
 }
 
@@ -498,7 +633,7 @@ int aijhip_gamg_build_host(int32_t m, const int32_t *ai, const int32_t *aj, cons
 }  // extern "C"
 
 int aijhip_gamg::build_host_nns(int32_t m, const int32_t *ai, const int32_t *aj, const double *aa, const double *B0,
-                                const aijhip_gamg_params_t &p, aijhip_gamg_host_t *out) {
+                                const aijhip_gamg_params_t &p, aijhip_gamg_host_t *out, int32_t level0) {
     if (!out || m < 0 || !ai || (ai[m] > 0 && (!aj || !aa))) return AIJHIP_ERR_ARG;
     *out = nullptr;
     if (p.max_levels < 1) return AIJHIP_ERR_ARG;
@@ -529,10 +664,20 @@ int aijhip_gamg::build_host_nns(int32_t m, const int32_t *ai, const int32_t *aj,
             lap("diagonal");
             strength_graph(cur, d, p.threshold, si, sj, nt);
             lap("strength");
-            const int32_t na = aggregate(cur, si, sj, agg);
+            const int32_t level = level0 + (int32_t)H->P.size();
+            int32_t na;
+            if (p.coarsen == 1) {
+                agg.resize(cur.m);
+                na = aijhip_gamg::aggregate_mis(cur.m, si.data(), sj.data(), level < p.square_graph, level,
+                                                agg.data());
+            } else {
+                na = aggregate(cur, si, sj, agg);
+            }
             lap("aggregate");
             if (na >= cur.m || na == 0) break;  // no coarsening
-            const double emax = p.nsmooths > 0 ? estimate_emax(cur, dinv, p.eig_its, nt) : 1.0;
+            const double emax = p.nsmooths <= 0 ? 1.0
+                                : p.eig_ksp == 1 ? estimate_emax_cg(cur, dinv, p.eig_its, nt)
+                                                 : estimate_emax(cur, dinv, p.eig_its, nt);
             lap("emax");
             CSR P;
             std::vector<double> Bc;

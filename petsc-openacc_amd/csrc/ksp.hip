@@ -249,7 +249,8 @@ int gamg_setup(aijhip_ksp *K) {
         }
         aijhip_gamg_params_t hp = K->gamg;
         hp.max_levels = K->gamg.max_levels - ((int32_t)dl.size() - 1);
-        rc = aijhip_gamg::build_host_nns(L.m, ai.data(), aj.data(), aa.data(), B.data(), hp, &H);
+        const int32_t nd_levels = (int32_t)dl.size();  // the host continues at level nd_levels - 1
+        rc = aijhip_gamg::build_host_nns(L.m, ai.data(), aj.data(), aa.data(), B.data(), hp, &H, nd_levels - 1);
         if (rc) {
             aijhip_gamg::free_device_levels(dl);
             return kfail(rc, "GAMG: host hierarchy set-up failed");

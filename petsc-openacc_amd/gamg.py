@@ -20,7 +20,8 @@ class GamgParams(ctypes.Structure):
     _fields_ = [("threshold", ctypes.c_double), ("coarse_eq_limit", ctypes.c_int32),
                 ("max_levels", ctypes.c_int32), ("nsmooths", ctypes.c_int32),
                 ("smooth_scale", ctypes.c_double), ("eig_its", ctypes.c_int32), ("threads", ctypes.c_int32),
-                ("device_min_rows", ctypes.c_int32)]
+                ("device_min_rows", ctypes.c_int32), ("coarsen", ctypes.c_int32), ("square_graph", ctypes.c_int32),
+                ("eig_ksp", ctypes.c_int32), ("pad0", ctypes.c_int32)]
 
 
 _P = ctypes.c_void_p

@@ -230,17 +230,19 @@ def bench_cg(pkg, A, nx, ny, nz, dev, iters=200):
                                  "passes, per iteration, over the measured wall time of the iterations"}}
 
 
-def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000):
+def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000, gamg=None, light=False):
     """The reference's solver configuration (CG + GAMG to atol 1e-12 / rtol
     1e-14, configs/cg_gamg.info) solved to convergence on the benchmark
     operand from x = 0: KSPSetUp (host hierarchy + uploads) and KSPSolve
     timed separately, the solve once warm (a second solve on the same
-    hierarchy, as a time-stepping caller would)."""
+    hierarchy, as a time-stepping caller would). gamg: the hierarchy's
+    parameters (aijhip_gamg_params_t fields); light: skip the host-vector
+    solve and the second set-up."""
     import torch
     rhs, exact = pkg.poisson_vectors(nx, ny, nz)
     b = torch.from_numpy(rhs).to(dev)
     x = torch.zeros_like(b)
-    with KSPCG(A, rtol=rtol, atol=atol, max_it=max_it, pc="gamg") as ksp:
+    with KSPCG(A, rtol=rtol, atol=atol, max_it=max_it, pc="gamg", gamg=gamg) as ksp:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ksp.set_up()
@@ -261,16 +263,30 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
         nb, nb_spmv, nb_l0 = ksp.iteration_bytes()
         # the same solve from HOST b / x (aijhip_ksp_solve_host: the PETSc KSP
         # type "cghip" for an unchanged caller with host Vecs)
-        xh = np.zeros(A.m)
-        t0 = time.perf_counter()
-        ksp.solve_host(rhs, xh)
-        t_host_solve = time.perf_counter() - t0
-        host_same = bool(np.array_equal(xh.view(np.uint64), x.cpu().numpy().view(np.uint64)))
+        t_host_solve, host_same = None, None
+        if not light:
+            xh = np.zeros(A.m)
+            t0 = time.perf_counter()
+            ksp.solve_host(rhs, xh)
+            t_host_solve = time.perf_counter() - t0
+            host_same = bool(np.array_equal(xh.view(np.uint64), x.cpu().numpy().view(np.uint64)))
     err = float((x.cpu() - torch.from_numpy(exact)).abs().max())
+    roof = {"bound": "hbm", "bytes_per_iter": nb, "spmv_bytes_per_iter": nb_spmv,
+            "finest_level_bytes_per_iter": nb_l0,
+            "achieved": round(nb * its / t_solve / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
+            "frac": round(nb * its / t_solve / 1e9 / 8000.0, 4),
+            "note": "aijhip_ksp_get_iteration_bytes (every SpMV of the hierarchy at its layout's "
+                    "bytes — A_l twice, P, P^T per level — plus CG's and the V-cycle's vector passes) "
+                    "x iterations / the solve's wall time (polls and launch gaps included)"}
+    if light:
+        return {"its": its, "reason": reason, "max_err": err, "setup_s": round(t_setup, 3),
+                "solve_s": round(t_solve, 4), "time_to_solution_s": round(t_setup + t_solve, 3),
+                "ms_per_iter": round(t_solve / max(its, 1) * 1e3, 4),
+                "levels": [{"rows": r, "nnz": z} for r, z in zip(rows, nnz)], "roofline": roof}
     # the same set-up again in this process (a caller that rebuilds the
     # hierarchy after new values): the first one above also pays one-time
     # costs (the set-up kernels' first launch, pinned staging)
-    with KSPCG(A, rtol=rtol, atol=atol, max_it=max_it, pc="gamg") as ksp2:
+    with KSPCG(A, rtol=rtol, atol=atol, max_it=max_it, pc="gamg", gamg=gamg) as ksp2:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ksp2.set_up()
@@ -285,13 +301,7 @@ def bench_cg_gamg(pkg, A, nx, ny, nz, dev, rtol=1e-14, atol=1e-12, max_it=10000)
             "ms_per_iter": round(t_solve / max(its, 1) * 1e3, 4), "host_syncs": syncs,
             "time_to_solution_s": round(t_setup + t_solve, 3),
             "levels": [{"rows": r, "nnz": z} for r, z in zip(rows, nnz)],
-            "roofline": {"bound": "hbm", "bytes_per_iter": nb, "spmv_bytes_per_iter": nb_spmv,
-                         "finest_level_bytes_per_iter": nb_l0,
-                         "achieved": round(nb * its / t_solve / 1e9, 1), "peak": 8000.0, "unit": "GB/s",
-                         "frac": round(nb * its / t_solve / 1e9 / 8000.0, 4),
-                         "note": "aijhip_ksp_get_iteration_bytes (every SpMV of the hierarchy at its layout's "
-                                 "bytes — A_l twice, P, P^T per level — plus CG's and the V-cycle's vector passes) "
-                                 "x iterations / the solve's wall time (polls and launch gaps included)"},
+            "roofline": roof,
             "options": "cg, gamg agg nsmooths 1 threshold 0, mg levels richardson(1)+jacobi, "
                        "coarse preonly+jacobi, rtol 1e-14 atol 1e-12"}
 

@@ -53,6 +53,71 @@ def test_host_hierarchy_matches_oracle_bitwise(pkg, dims):
             assert np.array_equal(mine.data, theirs.data)
 
 
+@pytest.mark.parametrize("dims", [(8, 8, 8), (12, 12, 12), (6, 7, 5), (16, 16, 16)])
+@pytest.mark.parametrize("eig_ksp", [0, 1])
+def test_host_mis_hierarchy_matches_oracle_bitwise(pkg, dims, eig_ksp):
+    """PETSc 3.7 agg's coarsening (coarsen 1: MIS on the squared graph at the
+    finest level, smoothAggs, then MIS on the graph; the reference point row
+    0 a removed singleton) and its CG emax estimate (eig_ksp 1): the C++ host
+    set-up equals the literal sequential restatement (oracle/gamg.py
+    aggregate_mis, estimate_emax_cg) bit for bit."""
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    ai, aj, aa = pkg.poisson_csr(*dims)
+    m = len(ai) - 1
+    A = sp.csr_matrix((aa, aj, ai), shape=(m, m))
+    lv = G.build_host(ai, aj, aa, coarse_eq_limit=20, coarsen=1, eig_ksp=eig_ksp)
+    ol = ogamg.build(A, coarse_eq_limit=20, coarsen=1, eig_ksp=eig_ksp)
+    assert len(lv) == len(ol) >= 2
+    assert lv[0]["agg"][0] == -1 and ol[0]["agg"][0] == -1  # row 0: only explicit zeros off the diagonal
+    for l in range(len(lv) - 1):
+        assert np.array_equal(lv[l]["agg"], ol[l]["agg"])
+        assert lv[l]["emax"] == ol[l]["emax"]
+        mc = lv[l + 1]["m"]
+        for mine, theirs in ((_csr(lv[l]["P"], (lv[l]["m"], mc)), ol[l]["P"]),
+                             (_csr(lv[l + 1]["A"], (mc, mc)), ol[l + 1]["A"])):
+            theirs = theirs.copy()
+            theirs.eliminate_zeros()
+            theirs.sort_indices()
+            assert np.array_equal(mine.indptr, theirs.indptr) and np.array_equal(mine.indices, theirs.indices)
+            assert np.array_equal(mine.data, theirs.data)
+
+
+def test_mis_aggregates_are_petsc_shaped():
+    """The restated MIS on the squared graph: roots pairwise more than two
+    steps apart in S, every other node (but the removed singletons) in the
+    aggregate of a root within two steps (one, after smoothAggs, when a root
+    is adjacent), aggregates numbered by their roots' order."""
+    ai, aj, aa, _, _ = seqaij.create_system(10, 10, 10)
+    m = len(ai) - 1
+    A = sp.csr_matrix((aa, aj, ai), shape=(m, m))
+    d = ogamg.first_diagonal(A)
+    S = ogamg.strength_graph(A, d, 0.0)
+    agg, na = ogamg.aggregate_mis(S, True, ogamg.mis_keys(m, 0))
+    G1 = (S + sp.identity(m, format="csr")).astype(bool).tocsr()
+    G2 = (G1.astype(np.int32) @ G1.astype(np.int32)).astype(bool).tocsr()
+    # the roots, by PETSc's rule (an undone node at its turn in key order)
+    isroot = np.zeros(m, bool)
+    keys = ogamg.mis_keys(m, 0)
+    order = np.argsort(keys, kind="stable")
+    taken = np.zeros(m, bool)
+    for v in order:
+        if taken[v] or S.indptr[v] == S.indptr[v + 1]:
+            continue
+        isroot[v] = True
+        taken[G2.indices[G2.indptr[v]:G2.indptr[v + 1]]] = True
+    r = np.flatnonzero(isroot)
+    assert len(r) == na and np.array_equal(agg[r], np.arange(na))
+    for v in r:  # independent in G2
+        nb = G2.indices[G2.indptr[v]:G2.indptr[v + 1]]
+        assert isroot[nb].sum() == 1
+    for v in np.flatnonzero(agg >= 0):
+        if isroot[v]:
+            continue
+        root = r[agg[v]]
+        assert G2[v, root]
+    assert np.all((agg == -1) == (np.diff(S.indptr) == 0))
+
+
 def test_host_hierarchy_thread_invariant(pkg):
     G = importlib.import_module("petsc-openacc_amd.gamg")
     ai, aj, aa = pkg.poisson_csr(16)
@@ -245,6 +310,27 @@ def test_gpu_device_setup_matches_host_bitwise(pkg, dims, params, agg, monkeypat
         monkeypatch.setenv("AIJHIP_GAMG_AGG", "device")
     ai, aj, aa = pkg.poisson_csr(*dims)
     _check_device_setup(pkg, ai, aj, aa, params)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,params", [
+    ((8, 8, 8), dict(coarse_eq_limit=20)),
+    ((12, 12, 12), dict(coarse_eq_limit=20, eig_ksp=1)),
+    ((6, 7, 5), dict(coarse_eq_limit=20)),
+    ((24, 24, 24), dict(eig_ksp=1)),
+    ((16, 16, 16), dict(square_graph=2, eig_ksp=1)),
+    ((40, 40, 40), dict(device_min_rows=20000, eig_ksp=1)),  # device level 0, host below
+])
+def test_gpu_device_mis_setup_matches_host_bitwise(pkg, dims, params):
+    """coarsen 1 (PETSc 3.7 agg's MIS, squared graph on the first
+    square_graph levels, smoothAggs; singletons removed) on the device — the
+    parallel rounds of gamg_aggregate.hip aggregate_mis_device — equals the
+    host builder's sequential pass (itself the oracle's, bit for bit), with
+    the CG emax estimate (eig_ksp 1) on the device too."""
+    ai, aj, aa = pkg.poisson_csr(*dims)
+    prm = dict(coarsen=1)
+    prm.update(params)
+    _check_device_setup(pkg, ai, aj, aa, prm)
 
 
 def _check_device_setup(pkg, ai, aj, aa, params):

@@ -166,6 +166,41 @@ def test_gpu_gamg_setup_300_matches_host_bitwise(pkg):
 
 
 @pytest.mark.gpu
+def test_gpu_mis_gamg_setup_100_matches_host_and_solves(pkg):
+    """PETSc 3.7's coarsening (coarsen 1 + the CG emax, eig_ksp 1) at 100^3:
+    the device set-up equals the host builder level for level, and CG + that
+    hierarchy converges to the reference's tolerances."""
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available()
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    G = importlib.import_module("petsc-openacc_amd.gamg")
+    N = 100
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, exact = pkg.poisson_vectors(N)
+    prm = dict(coarsen=1, eig_ksp=1)
+    lv = G.build_host(ai, aj, aa, **prm)
+    A = pkg.SeqAIJHIP(ai, aj, aa)
+    try:
+        with K.KSPCG(A, pc="gamg", gamg=prm, rtol=1e-14, atol=1e-12) as ksp:
+            ksp.set_up()
+            rows, nnz, _ = ksp.pc_levels()
+            print(f"\n100^3 MIS hierarchy rows {rows} nnz {nnz}")
+            assert rows == [L["m"] for L in lv] and rows[1] < rows[0] // 6
+            for l in range(1, len(lv)):
+                dai, daj, daa, _ = ksp.pc_level(l, "A")
+                hai, haj, haa = lv[l]["A"]
+                assert np.array_equal(dai, hai) and np.array_equal(daj, haj), l
+                assert np.array_equal(_bits(daa), _bits(haa)), l
+            b = torch.from_numpy(rhs).cuda()
+            x = torch.empty_like(b)
+            ksp.solve(b, x)
+            assert ksp.reason > 0 and ksp.its < 100, (ksp.its, ksp.reason)
+            assert np.abs(x.cpu().numpy() - exact).max() <= C_H2 / N ** 2
+    finally:
+        A.destroy()
+
+
+@pytest.mark.gpu
 def test_gpu_cg_gamg_100_configs0_vs_oracle(pkg):
     """configs[0] (100^3): the device solve against the oracle's CG
     (oracle/ksp_cg.py) preconditioned by the oracle's V-cycle
