@@ -4,12 +4,16 @@
 # halo forms), and rocprofv3 kernel statistics of the headline alone and of
 # the whole bench. Every GPU step has its own time limit; steps are chained so
 # the first failure ends the call (no retries).
-#   usage: tools/gpu_record.sh TAG [--no-tests] [--no-full-prof]
+#   usage: tools/gpu_record.sh TAG [--no-tests] [--no-full-prof] [--n8]
+# --n8: also the eight-rank rehearsal of the driver's N = 8 run on this one
+# GPU (--gpus 8 --rehearse-one-gpu: the self-launcher's 8 children, the
+# 38/37-plane strong_300 split, both halo forms, the distributed CG and
+# CG + GAMG legs) at a weak grid of 100^3 per rank.
 set -o pipefail
 TAG=${1:-record}; shift
-TESTS=1; FULLPROF=1
+TESTS=1; FULLPROF=1; N8=0
 for a in "$@"; do
-  case $a in --no-tests) TESTS=0 ;; --no-full-prof) FULLPROF=0 ;; esac
+  case $a in --no-tests) TESTS=0 ;; --no-full-prof) FULLPROF=0 ;; --n8) N8=1 ;; esac
 done
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
@@ -28,6 +32,11 @@ echo "bench ok"
 timeout -k 10 600 python -u bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --no-gamg \
     > "$OUT/bench_rehearse_n2.json" 2> "$OUT/bench_rehearse_n2.err" \
     && echo "rehearsal n2 ok" || { tail -20 "$OUT/bench_rehearse_n2.err"; exit 1; }
+if [ $N8 = 1 ]; then
+  timeout -k 10 900 python -u bench.py --gpus 8 --rehearse-one-gpu --grid 100 --strong-grid 300 --steps 20 \
+      --warmup 3 > "$OUT/bench_rehearse_n8.json" 2> "$OUT/bench_rehearse_n8.err" \
+      && echo "rehearsal n8 ok" || { tail -20 "$OUT/bench_rehearse_n8.err"; exit 1; }
+fi
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_headline" -o run --output-format csv \
     -- python3 bench.py --no-cg --no-gamg --no-host-vec --no-flan --no-cpu-baseline > "$OUT/bench_headline_prof.json" \
     2> "$OUT/bench_headline_prof.err" && echo "headline prof ok" || { tail -20 "$OUT/bench_headline_prof.err"; exit 1; }
