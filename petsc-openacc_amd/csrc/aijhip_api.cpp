@@ -412,8 +412,8 @@ int plan_stream(aijhip_mat *A) {
     // and the long rows (created once per plan that has them)
     if (P.tune.overlap != 0 && (P.n_wblocks > 0 || P.n_longs > 0)) {
         if ((e = hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&P.ev_fork, hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&P.ev_join, hipEventDisableTiming)) != hipSuccess)
+            (e = hipEventCreateWithFlags(&P.ev_fork, aijhip::sync_event_flags())) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&P.ev_join, aijhip::sync_event_flags())) != hipSuccess)
             return hipfail(e, "plan: side stream");
     }
     return AIJHIP_OK;
@@ -683,6 +683,14 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
 
 namespace aijhip {
 void set_error(const std::string &msg) { g_err = msg; }
+
+unsigned sync_event_flags() {
+    const char *v = std::getenv("AIJHIP_EVENT_FENCE");
+    unsigned f = hipEventDisableTiming;
+    if (v && std::strcmp(v, "device") == 0) f |= hipEventReleaseToDevice;
+    else if (v && std::strcmp(v, "none") == 0) f |= hipEventDisableSystemFence;
+    return f;
+}
 
 uint64_t next_plan_gen() {
     static std::atomic<uint64_t> gen{0};

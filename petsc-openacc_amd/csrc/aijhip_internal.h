@@ -338,6 +338,13 @@ hipError_t ksp_pc_vcycle(aijhip_ksp *K, const double *b, double *x, hipStream_t 
 // A fresh value for aijhip_mat::plan_gen.
 uint64_t next_plan_gen();
 
+// Flags of the library's cross-stream fork / join events (the MPIAIJ halo,
+// the long-row side stream): hipEventDisableTiming plus the release scope
+// AIJHIP_EVENT_FENCE selects at creation — "system" (HIP's default),
+// "device" (hipEventReleaseToDevice) or "none" (hipEventDisableSystemFence).
+// Both ends of every such edge are on one device.
+unsigned sync_event_flags();
+
 // Compulsory bytes one MatMult under A's plan moves (aijhip_info_t.mult_layout_bytes).
 int64_t mult_layout_bytes(const aijhip_mat &A);
 

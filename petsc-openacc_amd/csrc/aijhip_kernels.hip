@@ -168,12 +168,24 @@ struct OpDinvMult {
 // reads go out eight (then four) at a time ahead of their adds, so a lane's chain waits on
 // one read latency per eight entries instead of one per entry (FEM rows of
 // 50-100 entries are otherwise a serial LDS-latency chain on few lanes).
+// Software-pipelined (round 5): the next eight are read before this eight's
+// adds, so the chain waits on one LDS latency per row instead of one per
+// batch (rows of 45-99 entries: 6-12 batches). Same order, same bits.
 __device__ __forceinline__ double row_sum_seq(const double *p, int32_t n, double s) {
     int32_t k = 0;
-    for (; k + 8 <= n; k += 8) {
+    if (n >= 8) {
         double v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = p[k + i];
+        for (int i = 0; i < 8; ++i) v[i] = p[i];
+        for (k = 8; k + 8 <= n; k += 8) {
+            double w[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) w[i] = p[k + i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) s += v[i];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = w[i];
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i) s += v[i];
     }
@@ -225,13 +237,6 @@ __device__ __forceinline__ void stream_block(
     // gather round trips per lane instead of one).
     constexpr bool BF = (NTMODE & 64) != 0;
     static_assert(!(BF && SORTED), "branch-free phase 1: plain, coded and 16-bit gather-ordered forms");
-    // bit 7: phase 1 without branches through range-checked buffer loads (A/B,
-    // AIJHIP_STREAM_BUF=1; plain aj blocks only): the block's aa / aj pairs are
-    // loaded through descriptors that end at the block's last pair, so lanes
-    // past it read zeros without a memory request (no clamped duplicates as
-    // in BF) and no branch splits the loads from their gathers.
-    constexpr bool BUF = (NTMODE & 128) != 0;
-    static_assert(!(BUF && (BF || CODES || SORTED || S16)), "buffer phase 1: plain aj blocks only");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     const BlockDesc d = blk[b];
@@ -275,38 +280,7 @@ __device__ __forceinline__ void stream_block(
     f64x2 av[ITERS];
     i32x2 cv[ITERS];
     f64x2 xv[ITERS];
-    if constexpr (BUF) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        // the pair-rounded end stays inside the arrays' 2-entry tail pad
-        const int32_t npair = __builtin_amdgcn_readfirstlane((int32_t)((k1 - kb + 1) >> 1));
-        const double *abase = aa + kb;
-        const int32_t *jbase = aj + kb;
-        const __amdgpu_buffer_rsrc_t ra =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(abase), (short)0, npair * 16, 0x00020000);
-        const __amdgpu_buffer_rsrc_t rj =
-            __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t *>(jbase), (short)0, npair * 8, 0x00020000);
-        constexpr int kAux = NT ? 2 : 0;  // slc: the non-temporal hint
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int q = t + it * T;  // this lane's pair in the block
-            const u32x2 c = __builtin_amdgcn_raw_buffer_load_b64(rj, q * 8, 0, kAux);
-            cv[it] = i32x2{(int)c.x, (int)c.y};
-        }
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int q = t + it * T;
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(ra, q * 16, 0, kAux);
-            av[it] = f64x2{__builtin_bit_cast(double, (unsigned long long)v.x | ((unsigned long long)v.y << 32)),
-                           __builtin_bit_cast(double, (unsigned long long)v.z | ((unsigned long long)v.w << 32))};
-        }
-        // gathers for every lane (past the block: column 0, never stored)
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            xv[it].x = op.gx(cv[it].x);
-            xv[it].y = op.gx(cv[it].y);
-        }
-    } else if constexpr (BF) {
+    if constexpr (BF) {
         uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
         const int64_t kl = (k1 - 1) & ~int64_t(1);  // the last pair start (>= kb when nk > 0)
         if (d.nk > 0) {  // (block-uniform)
@@ -412,7 +386,7 @@ __device__ __forceinline__ void stream_block(
                 xv[it].y = op.gx(cv[it].y);
             }
         }
-    } else if constexpr (!CODES && !BF && !BUF) {  // (the coded / buffer forms gathered above)
+    } else if constexpr (!CODES && !BF) {  // (the coded form gathered with the decode above)
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
@@ -422,21 +396,9 @@ __device__ __forceinline__ void stream_block(
             }
         }
     }
-    // products into LDS; only the stores are predicated (BUF: not even they —
-    // a product outside the block goes to the trash slots prod[CAP..CAP+1],
-    // so no branch gives the compiler a place to sink the loads into)
-    if constexpr (BUF) {
+    // products into LDS; only the stores are predicated
 #pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            const int s0 = (k >= k0 && k < k1) ? (int)(k - k0) : CAP;
-            const int s1 = (k + 1 < k1) ? (int)(k + 1 - k0) : CAP + 1;
-            prod[s0] = av[it].x * xv[it].x;
-            prod[s1] = av[it].y * xv[it].y;
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < ITERS && !BUF; ++it) {
+    for (int it = 0; it < ITERS; ++it) {
         const int64_t k = kb + 2 * (int64_t)(t + it * T);
         if (k < k1) {
             const int s0 = (SORTED || S16) ? (int)(sv[it] & 0xffffu) : (int)(k - k0);
@@ -507,7 +469,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, Op op, double *dpart, const int *stop, const uint16_t *__restrict__ sslot,
     const int32_t *__restrict__ sbase) {
-    __shared__ double prod[(NTMODE & 128) ? CAP + 2 : CAP];  // (BUF: two trash slots)
+    __shared__ double prod[CAP];
     __shared__ int32_t cdict[(NTMODE & 32) ? kCodeDictMax : 1];
     stream_block<T, CAP, RPT, CROW, NTMODE, Op>((int)blockIdx.x, blk, nblk, exact, rai, ridx, aj, aa, op, dpart, stop,
                                                 sslot, sbase, prod, cdict);
@@ -1413,15 +1375,11 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // (the plain aj blocks keep the predicated phase 1: branch-free measured
     // 505.9 vs 492.8 us at 300^3, profiles/r04/s1/bf_poisson.jsonl — for the
     // 7-point rows the clamped lanes' extra loads and gathers cost more than
-    // the serialised gathers, which hit L1/L2)
-    // A/B: the buffer-load phase 1 (bit 7) on the plain full-row MatMult
-    // (read at every launch so one process can interleave the two forms)
-    const char *buf_env = std::getenv("AIJHIP_STREAM_BUF");
-    const bool buf_ab = buf_env && buf_env[0] == '1';
-    if (buf_ab && !L.ridx && !add) {
-        if (P.tune.nt == 1) { AIJHIP_SL(false, false, 129); }
-        AIJHIP_SL(false, false, 128);
-    }
+    // the serialised gathers, which hit L1/L2; round 5's straight-line form
+    // through range-checked buffer loads, whose ISA waits vmcnt(7..4) — one
+    // round trip for all eight gathers — measured 483.1 vs 469.8 us too,
+    // profiles/r05/b/ab_buf.jsonl: the gathers' serialisation is not what
+    // bounds this kernel)
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
     // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)
     if (P.tune.nt == 1 && !L.ridx) {

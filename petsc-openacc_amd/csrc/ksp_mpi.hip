@@ -942,8 +942,8 @@ int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o,
         (M->n_send > 0 && (e = hipMemcpy(M->d_send_rows, rows.data(), sizeof(int32_t) * (size_t)M->n_send,
                                          hipMemcpyHostToDevice)) != hipSuccess) ||
         (e = hipStreamCreateWithFlags(&M->xs, hipStreamNonBlocking)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&M->ev_x, hipEventDisableTiming)) != hipSuccess ||
-        (e = hipEventCreateWithFlags(&M->ev_halo, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&M->ev_x, aijhip::sync_event_flags())) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&M->ev_halo, aijhip::sync_event_flags())) != hipSuccess ||
         (M->pack_all && ((e = hipHostMalloc(&M->h_send, sizeof(double) * (size_t)nbuf, hipHostMallocDefault)) !=
                              hipSuccess ||
                          (e = hipHostMalloc(&M->h_ghost, sizeof(double) * (size_t)ng, hipHostMallocDefault)) !=

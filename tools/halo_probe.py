@@ -81,6 +81,9 @@ def main():
     ap.add_argument("--only", default=None, help="comma-separated variant subset (trace runs)")
     ap.add_argument("--preload-us", type=float, default=1500.0)
     ap.add_argument("--burst", type=int, default=100)
+    ap.add_argument("--graphs", type=int, default=0,
+                    help="also time HIP-graph replays of diag / p2p_self / ag_self (torch's capture_end segfaulted "
+                         "on them in round 5, profiles/r05/c/graph_diag.err)")
     args = ap.parse_args()
 
     import torch
@@ -143,6 +146,31 @@ def main():
             "p2p_self": lambda y: p2p_s.mult(x, y, stream),
             "ag_self": lambda y: ag_s.mult(x, y, stream),
         }
+        # the same launches captured once into a HIP graph and replayed
+        # (hipGraphLaunch: one host call instead of RCCL's enqueue per call)
+        graphs, gerr = {}, {}
+        if args.graphs:
+            for gname, base in (("diag", "diag"), ("p2p_self", "p2p_self"), ("ag_self", "ag_self")):
+                yg = torch.empty(m, dtype=torch.float64, device=dev)
+                try:
+                    g = torch.cuda.CUDAGraph()
+                    gs = torch.cuda.Stream()
+                    gs.wait_stream(stream)
+                    with torch.cuda.stream(gs):
+                        fn = {"diag": lambda y, st: op.A_d.mult(x, y, st),
+                              "p2p_self": lambda y, st: p2p_s.mult(x, y, st),
+                              "ag_self": lambda y, st: ag_s.mult(x, y, st)}[base]
+                        fn(yg, gs)  # warm-up outside the capture
+                        torch.cuda.synchronize()
+                        with torch.cuda.graph(g, stream=gs):
+                            fn(yg, torch.cuda.current_stream())
+                    torch.cuda.synchronize()
+                    graphs[gname + "_graph"] = (g, yg)
+                except Exception as e:  # noqa: BLE001
+                    gerr[gname + "_graph"] = repr(e)[:300]
+                    torch.cuda.synchronize()
+            for k, (g, yg) in graphs.items():
+                variants[k] = (lambda gg: lambda y: gg.replay())(g)
         if args.only:
             keep = set(args.only.split(","))
             variants = {k: v for k, v in variants.items() if k in keep}
@@ -189,6 +217,15 @@ def main():
                 rec[k]["minus_" + base + "_us_median"] = round(float(np.median(d)), 2)
                 rec[k]["minus_" + base + "_us_iqr"] = [round(float(np.percentile(d, 25)), 2),
                                                       round(float(np.percentile(d, 75)), 2)]
+        for k, base in (("diag_graph", "diag"), ("p2p_self_graph", "p2p_self"), ("ag_self_graph", "ag_self")):
+            if k in us and base in us:
+                rec[k]["minus_" + base + "_us_median"] = round(float(np.median(us[k] - us[base])), 2)
+        if gerr:
+            rec["graph_errors"] = gerr
+        for k, (g, yg) in graphs.items():
+            base = k[: -len("_graph")]
+            if base in ys:
+                rec[k]["bitwise_equal_" + base] = bool(torch.equal(yg, ys[base]))
         # bitwise: every distributed form against its diagonal block + A_o
         if "p2p_self" in ys and "ag_self" in ys:
             rec["self_forms_bitwise_equal"] = bool(torch.equal(ys["p2p_self"], ys["ag_self"]))
