@@ -52,6 +52,16 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
+# HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default)
+# round-robin: with the library's exchange and side streams, torch's and
+# RCCL's, a fifth stream shares a queue with the compute stream and its
+# "concurrent" work runs behind it. Measured (profiles/r05/e/): the skewed
+# stand-in's side-stream overlap 344 us at 4 queues (slower than serial, 325)
+# vs 313 us at 8; the halo's empty fork / join 29.5 vs 13.5 us. Set before
+# HIP initialises (the rank children inherit it); at least 8, a larger value stays.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md §Chip-level parameters (spec)
 
 
@@ -467,8 +477,9 @@ def halo_forms(op, x, stream, reps, rank, dev, m_loc, nnz_loc):
     """Per rank, what each exchange form adds on top of the diagonal block:
     distributed SpMVs through the all-gather operator (op.native, built with
     halo="allgather") and through its p2p twin (op.p2p_native(): same A_d,
-    ghost-numbered A_o, ncclSend/ncclRecv to the slab neighbours), and A_d
-    alone, INTERLEAVED — one launch of each in turn for max(reps, 200) rounds,
+    ghost-numbered A_o, ncclSend/ncclRecv to the slab neighbours), that twin
+    with the exchange in order on the compute stream (p2p_serial: no fork /
+    join events, aijhip_mpiaij_set_overlap 0), and A_d alone, INTERLEAVED — one launch of each in turn for max(reps, 200) rounds,
     HIP events on the compute stream around every launch, a 1.5 ms device
     delay queued ahead of each round so the events time device work rather
     than host enqueue overhead — so box drift hits the three alike; halo_exposed_us = the median over rounds of (form − A_d)
@@ -480,6 +491,13 @@ def halo_forms(op, x, stream, reps, rank, dev, m_loc, nnz_loc):
     fns = {"diag": lambda: op.A_d.mult(x, y, stream)}
     for form, nat in (("p2p", op.p2p_native()), ("allgather", op.native)):
         fns[form] = (lambda n: lambda: n.mult(x, y, stream))(nat)
+    p2p = op.p2p_native()
+
+    def p2p_serial():  # the p2p plan in order on the compute stream (no fork / join)
+        p2p.set_overlap(False)
+        p2p.mult(x, y, stream)
+        p2p.set_overlap(True)
+    fns["p2p_serial"] = p2p_serial
     for _ in range(3):
         for f in fns.values():
             f()
@@ -499,7 +517,7 @@ def halo_forms(op, x, stream, reps, rank, dev, m_loc, nnz_loc):
     torch.cuda.synchronize()
     us = {k: np.array([a.elapsed_time(b) for a, b in ev[k]]) * 1e3 for k in fns}
     out = {}
-    for form in ("p2p", "allgather"):
+    for form in ("p2p", "allgather", "p2p_serial"):
         d = us[form] - us["diag"]
         paired = {"spmv_us_median": float(np.median(us[form])), "diag_us_median": float(np.median(us["diag"])),
                   "diff_us_median": float(np.median(d)),
@@ -517,7 +535,7 @@ def gather_forms(mine, world):
     allr = [None] * world
     dist.all_gather_object(allr, mine)
     res = {}
-    for form in ("p2p", "allgather"):
+    for form in ("p2p", "allgather", "p2p_serial"):
         ranks = [r[form] for r in allr]
         worst = max(ranks, key=lambda q: q["halo_exposed_us"])
         res[form] = {"ranks": ranks, "worst_rank": worst["rank"], "worst_halo_exposed_us": worst["halo_exposed_us"]}

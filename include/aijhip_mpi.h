@@ -117,6 +117,13 @@ int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o,
  * handle's exchange stream while A_d multiplies on `stream`. x, y: device
  * fp64[mloc], distinct. */
 int aijhip_mpiaij_mult(aijhip_mpiaij_t M, const double *x, double *y, void *stream);
+/* RCCL exchange placement: 1 (default) on the operator's exchange stream
+ * beside A_d x (forked from and joined to the caller's stream by events); 0
+ * on the caller's stream in order — pack, A_d x, the collective, A_o g — with
+ * no cross-stream events (each fork / join costs ~6-13 us of device time on
+ * the MI355X, profiles/r05/; the serial form exposes the exchange instead).
+ * The host transport is unaffected. */
+int aijhip_mpiaij_set_overlap(aijhip_mpiaij_t M, int overlap);
 /* The ghost vector of the last mult (device fp64, *n entries), for tests. */
 int aijhip_mpiaij_get_ghost(aijhip_mpiaij_t M, const double **ghost, int64_t *n);
 int aijhip_mpiaij_destroy(aijhip_mpiaij_t M);

@@ -461,18 +461,23 @@ int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
     aijhip_comm *C = M->comm;
     if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
     hipError_t e;
-    if ((e = hipEventRecord(M->ev_x, s)) != hipSuccess || (e = hipStreamWaitEvent(M->xs, M->ev_x, 0)) != hipSuccess)
+    // serial (RCCL, overlap 0): everything on the caller's stream, in order
+    const bool serial = C->kind == AIJHIP_COMM_RCCL && !M->overlap;
+    const hipStream_t xs = serial ? s : M->xs;
+    M->post_s = xs;
+    if (!serial &&
+        ((e = hipEventRecord(M->ev_x, s)) != hipSuccess || (e = hipStreamWaitEvent(M->xs, M->ev_x, 0)) != hipSuccess))
         return mhip(e, "halo order");
     const int64_t npack = M->halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send;
     const int64_t nrows = M->send_off.empty() ? 0 : M->send_off.back();
     if (npack > 0 && (M->pack_all || M->halo == AIJHIP_HALO_ALLGATHER)) {
-        hipLaunchKernelGGL(k_pack, dim3(grid_of(npack, 1024)), dim3(256), 0, M->xs, nrows, npack, M->d_send_rows,
+        hipLaunchKernelGGL(k_pack, dim3(grid_of(npack, 1024)), dim3(256), 0, xs, nrows, npack, M->d_send_rows,
                            x, M->d_sendbuf);
     } else if (npack > 0) {  // RCCL p2p: only the non-contiguous peers are packed
         for (size_t q = 0; q < M->send_peer.size(); ++q) {
             if (M->send_first[q] >= 0) continue;
             const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
-            hipLaunchKernelGGL(k_pack, dim3(grid_of(n, 1024)), dim3(256), 0, M->xs, n, n, M->d_send_rows + a, x,
+            hipLaunchKernelGGL(k_pack, dim3(grid_of(n, 1024)), dim3(256), 0, xs, n, n, M->d_send_rows + a, x,
                                M->d_sendbuf + a);
         }
     }
@@ -489,28 +494,30 @@ int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
 
 namespace {
 
-// The RCCL collective of a posted exchange, on the exchange stream.
+// The RCCL collective of a posted exchange, on the stream halo_post chose
+// (the exchange stream, or the caller's in the serial form).
 int halo_send_rccl(aijhip_mpiaij *M) {
     aijhip_comm *C = M->comm;
     const double *x = M->post_x;
+    const hipStream_t xs = M->post_s;
     M->post_x = nullptr;
     if (!x) return mfail(AIJHIP_ERR_STATE, "halo_finish without halo_post");
     const Rccl &R = rccl();
     ncclResult_t r;
     if (M->halo == AIJHIP_HALO_ALLGATHER) {
-        r = R.AllGather(M->d_sendbuf, M->d_ghost, (size_t)M->gather_len, ncclFloat64, C->nc, M->xs);
+        r = R.AllGather(M->d_sendbuf, M->d_ghost, (size_t)M->gather_len, ncclFloat64, C->nc, xs);
         if (r != ncclSuccess) return nfail(r, "ncclAllGather");
     } else {
         if ((r = R.GroupStart()) != ncclSuccess) return nfail(r, "ncclGroupStart");
         for (size_t q = 0; q < M->send_peer.size(); ++q) {
             const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
             const double *src = M->send_first[q] >= 0 ? x + M->send_first[q] : M->d_sendbuf + a;
-            if (n > 0 && (r = R.Send(src, (size_t)n, ncclFloat64, M->send_peer[q], C->nc, M->xs)) != ncclSuccess)
+            if (n > 0 && (r = R.Send(src, (size_t)n, ncclFloat64, M->send_peer[q], C->nc, xs)) != ncclSuccess)
                 break;
         }
         for (size_t p = 0; r == ncclSuccess && p < M->recv_peer.size(); ++p) {
             const int64_t a = M->recv_off[p], n = M->recv_off[p + 1] - a;
-            if (n > 0 && (r = R.Recv(M->d_ghost + a, (size_t)n, ncclFloat64, M->recv_peer[p], C->nc, M->xs)) !=
+            if (n > 0 && (r = R.Recv(M->d_ghost + a, (size_t)n, ncclFloat64, M->recv_peer[p], C->nc, xs)) !=
                              ncclSuccess)
                 break;
         }
@@ -518,6 +525,7 @@ int halo_send_rccl(aijhip_mpiaij *M) {
         if (r != ncclSuccess) return nfail(r, "ncclSend/ncclRecv");
         if (r2 != ncclSuccess) return nfail(r2, "ncclGroupEnd");
     }
+    if (xs != M->xs) return AIJHIP_OK;  // serial: already in order on the caller's stream
     const hipError_t e = hipEventRecord(M->ev_halo, M->xs);
     return e == hipSuccess ? AIJHIP_OK : mhip(e, "halo event");
 }
@@ -530,8 +538,10 @@ int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
     aijhip_comm *C = M->comm;
     hipError_t e;
     if (C->kind == AIJHIP_COMM_RCCL) {
+        const bool serial = M->post_s == s && s != M->xs;
         const int rc = halo_send_rccl(M);
         if (rc) return rc;
+        if (serial) return AIJHIP_OK;  // (no join: one stream)
     } else if (C->kind == AIJHIP_COMM_HOST) {
         const int64_t npack = M->halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send;
         int rc = wait_stream(C, M->xs);
@@ -966,6 +976,13 @@ int aijhip_mpiaij_mult(aijhip_mpiaij_t M, const double *x, double *y, void *stre
     if (x == y) return mfail(AIJHIP_ERR_ARG, "x and y alias");
     DeviceGuard g(M->comm->device);
     return mpiaij_apply(M, x, y, reinterpret_cast<hipStream_t>(stream), nullptr, nullptr, nullptr, false);
+}
+
+int aijhip_mpiaij_set_overlap(aijhip_mpiaij_t M, int overlap) {
+    if (!M) return mfail(AIJHIP_ERR_ARG, "NULL matrix");
+    if (overlap < 0 || overlap > 1) return mfail(AIJHIP_ERR_ARG, "overlap: 0 (one stream) or 1 (exchange stream)");
+    M->overlap = overlap;
+    return AIJHIP_OK;
 }
 
 int aijhip_mpiaij_get_ghost(aijhip_mpiaij_t M, const double **ghost, int64_t *n) {

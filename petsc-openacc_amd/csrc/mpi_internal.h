@@ -50,6 +50,11 @@ struct aijhip_mpiaij {
     hipStream_t xs = nullptr;
     hipEvent_t ev_x = nullptr, ev_halo = nullptr;
     const double *post_x = nullptr;  // RCCL: the x of the posted exchange, sent by halo_finish
+    // RCCL: the exchange on its own stream beside A_d (1, default) or on the
+    // compute stream itself, in order (0: no fork / join events; the pack,
+    // A_d, the collective and A_o run one after another)
+    int overlap = 1;
+    hipStream_t post_s = nullptr;  // the stream the posted exchange runs on
     int o_grid = 1;
 };
 

@@ -10,8 +10,14 @@ from __future__ import annotations
 
 import ctypes
 import importlib
+import os
 import sys
 from pathlib import Path
+
+# the library's side / exchange streams each need a hardware queue of their
+# own (bench.py, profiles/r05/e/): set before HIP initialises
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np
 import pytest

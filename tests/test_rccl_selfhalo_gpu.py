@@ -82,6 +82,14 @@ def _worker(port, N, q):
                 op.mult(x, y)
                 op.mult(x, y)  # the ghost buffer and the send rows reused
                 torch.cuda.synchronize()
+                if kind == "rccl":  # the exchange in order on the compute stream: the same bits
+                    ys = torch.full_like(x, float("nan"))
+                    op.set_overlap(False)
+                    op.mult(x, ys)
+                    op.mult(x, ys)
+                    op.set_overlap(True)
+                    torch.cuda.synchronize()
+                    res["serial_equal"] = bool(torch.equal(ys, y))
                 runs = {}
                 for pc in ("jacobi", "none"):
                     xs = torch.full_like(b, float("nan"))
@@ -129,6 +137,7 @@ def test_gpu_rccl_self_exchange_paths_match_host_transport_bitwise():
     for name in ("p2p_contiguous", "p2p_scattered", "allgather"):
         res = r[name]
         yr, yh = res["rccl"]["y"], res["host"]["y"]
+        assert res["serial_equal"], name
         assert np.array_equal(yr.view(np.uint64), yh.view(np.uint64)), name
         assert np.array_equal(yr.view(np.uint64), res["device"].view(np.uint64)), name
         # A_d + A_o = A; the A_o part of each row is added after A_d's: rounding

@@ -2,7 +2,13 @@
 """What the release scope of the library's fork / join events costs
 (AIJHIP_EVENT_FENCE = system | device | none, read when an operator creates
 them). One process, one GPU, interleaved rounds, a device delay queued ahead
-of every round (device-only timing, tools/halo_probe.py):
+of every round (device-only timing, tools/halo_probe.py).
+
+--per-process: ONE fence mode per process (the environment's), one operator
+of each kind — several operators each with its own exchange / side stream in
+one process share HIP's hardware queues (GPU_MAX_HW_QUEUES, 4 by default)
+round-robin, so a stream may land on the compute stream's queue and
+serialise behind it (r05d's in-process comparison was confounded by that).
 
   halo   the one-rank RCCL operators of tools/halo_probe.py: the all-gather
          operator with no ghosts (fork + count-1 collective + join) and the
@@ -55,6 +61,8 @@ def main():
     ap.add_argument("--planes", type=int, nargs="+", default=[38, 300])
     ap.add_argument("--reps", type=int, default=100)
     ap.add_argument("--no-skewed", action="store_true")
+    ap.add_argument("--per-process", action="store_true",
+                    help="only the fence mode of AIJHIP_EVENT_FENCE (default system), one operator of each kind")
     args = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -70,6 +78,9 @@ def main():
     stream = torch.cuda.current_stream()
     dev = torch.device("cuda:0")
     G = args.grid
+    modes = MODES
+    if args.per_process:
+        modes = (os.environ.get("AIJHIP_EVENT_FENCE", "system"),)
 
     def local(a_i, a_j, a_a, ncols):
         A = pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols)
@@ -87,12 +98,15 @@ def main():
         Ad_s = local(dai, daj, daa, m)
         Ao_s = local(oai, oaj, oaa, len(Gh))
         ops, keep = {}, []
-        for mode in MODES:
+        env0 = os.environ.get("AIJHIP_EVENT_FENCE")
+        for mode in modes:
             os.environ["AIJHIP_EVENT_FENCE"] = mode
             Ao0 = None
             ops["ag_empty_" + mode] = C.NativeMPIAIJ(comm, Ad, Ao0, "allgather", [(-1, np.zeros(1, np.int64))], [], 1)
             ops["p2p_self_" + mode] = C.NativeMPIAIJ(comm, Ad_s, Ao_s, "p2p", [(0, Gh)], [(0, 0, len(Gh))], 0)
         os.environ.pop("AIJHIP_EVENT_FENCE", None)
+        if env0 is not None:
+            os.environ["AIJHIP_EVENT_FENCE"] = env0
         ys = {k: torch.empty(m, dtype=torch.float64, device=dev) for k in list(ops) + ["diag", "diag_s"]}
         variants = {"diag": lambda: Ad.mult(x, ys["diag"], stream), "diag_s": lambda: Ad_s.mult(x, ys["diag_s"], stream)}
         for k, op in ops.items():
@@ -103,8 +117,10 @@ def main():
             base = "diag" if k.startswith("ag_empty") or k == "diag" else "diag_s"
             rec[k] = {"us_median": round(float(np.median(v)), 2),
                       "minus_" + base + "_us_median": round(float(np.median(v - us[base])), 2)}
-        rec["bitwise"] = {k: bool(torch.equal(ys[k], ys["p2p_self_system"] if k.startswith("p2p") else ys["diag"]))
+        ref_p2p = "p2p_self_" + modes[0]
+        rec["bitwise"] = {k: bool(torch.equal(ys[k], ys[ref_p2p] if k.startswith("p2p") else ys["diag"]))
                           for k in ops}
+        rec["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
         print(json.dumps(rec), flush=True)
         for op in ops.values():
             op.destroy()
@@ -117,10 +133,13 @@ def main():
         m = len(ai) - 1
         x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
         mats = {}
-        for mode in MODES:
+        env0 = os.environ.get("AIJHIP_EVENT_FENCE")
+        for mode in modes:
             os.environ["AIJHIP_EVENT_FENCE"] = mode
             mats["stream_" + mode] = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="stream")
         os.environ.pop("AIJHIP_EVENT_FENCE", None)
+        if env0 is not None:
+            os.environ["AIJHIP_EVENT_FENCE"] = env0
         mats["serial"] = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="stream")
         mats["serial"].set_option("long_overlap", 0)
         ys = {k: torch.empty(m, dtype=torch.float64, device=dev) for k in mats}
@@ -130,6 +149,7 @@ def main():
         for k, v in us.items():
             rec[k] = {"us_median": round(float(np.median(v)), 2), "us_min": round(float(v.min()), 2)}
         rec["bitwise"] = {k: bool(torch.equal(ys[k], ys["serial"])) for k in mats}
+        rec["hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
         print(json.dumps(rec), flush=True)
         for A in mats.values():
             A.destroy()

@@ -11,6 +11,9 @@ of its per-round difference to the diagonal block launched in the same round:
   diag        A_d.mult alone (the operand's slab, --planes of --grid^2 rows)
   forkjoin    A_d.mult with an empty fork/join to a second stream around it
               (torch events: what the halo's two event edges cost by themselves)
+  rec_only / fork_only / join_done / join_fresh   its parts: an event record
+              on the compute stream; the fork alone; a wait on an event long
+              complete; a wait on one the idle side stream records now
   ag_empty    the MPIAIJ all-gather operator bench.py --mpi builds at N = 1
               (no ghosts; the count-0 ncclAllGather on the exchange stream)
   p2p_empty   its p2p twin (no ghosts: no exchange at all)
@@ -137,9 +140,35 @@ def main():
             e_join.record(side)
             stream.wait_event(e_join)
 
+        e_rec, e_pre = torch.cuda.Event(), torch.cuda.Event()
+        e_pre.record(side)  # recorded once on the idle side stream: complete
+        torch.cuda.synchronize()
+
+        def rec_only(y):  # an event recorded on the compute stream, nobody waits
+            e_rec.record(stream)
+            op.A_d.mult(x, y, stream)
+
+        def fork_only(y):
+            e_fork.record(stream)
+            side.wait_event(e_fork)
+            op.A_d.mult(x, y, stream)
+
+        def join_done(y):  # the compute stream waits on an event long complete
+            op.A_d.mult(x, y, stream)
+            stream.wait_event(e_pre)
+
+        def join_fresh(y):  # ... on one the idle side stream records now
+            op.A_d.mult(x, y, stream)
+            e_join.record(side)
+            stream.wait_event(e_join)
+
         variants = {
             "diag": lambda y: op.A_d.mult(x, y, stream),
             "forkjoin": forkjoin,
+            "rec_only": rec_only,
+            "fork_only": fork_only,
+            "join_done": join_done,
+            "join_fresh": join_fresh,
             "ag_empty": lambda y: op.native.mult(x, y, stream),
             "p2p_empty": lambda y: p2p0.mult(x, y, stream),
             "p2p_selfd": lambda y: Ad_s.mult(x, y, stream),
@@ -210,7 +239,8 @@ def main():
         for k in variants:
             rec[k] = {"us_median": round(float(np.median(us[k])), 2), "us_mean": round(float(np.mean(us[k])), 2),
                       "pipelined_us": round(pipe[k][0], 2), "host_us": round(pipe[k][1], 2)}
-        for k, base in (("forkjoin", "diag"), ("ag_empty", "diag"), ("p2p_empty", "diag"),
+        for k, base in (("forkjoin", "diag"), ("rec_only", "diag"), ("fork_only", "diag"), ("join_done", "diag"),
+                        ("join_fresh", "diag"), ("ag_empty", "diag"), ("p2p_empty", "diag"),
                         ("p2p_self", "p2p_selfd"), ("ag_self", "p2p_selfd")):
             if k in us and base in us:
                 d = us[k] - us[base]
