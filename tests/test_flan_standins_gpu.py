@@ -7,7 +7,7 @@ run at Flan_1565's scale against the C restatement of MatMult_SeqAIJ
   skewed  — `skewed_csr()` default size: 1,564,794 rows of 45-99 banded
             entries plus 1e-4 hub rows of 1e3-2e5 scattered entries (seed
             1565); hub rows are longer than any STREAM block and are summed
-            by x column window (or 4096-entry segments).
+            in 4096-entry segments (on a side stream beside the row blocks).
   fem_hex — `fem_hex_csr()` default size: 81 x 80 x 80 hexahedral nodes, 3
             dofs per node (Flan_1565's structure), 81-entry interior rows.
 
