@@ -115,12 +115,12 @@ def test_stream_multilane_long_rows(pkg, dev, row_len):
     assert_bits(y1, y_ref)
 
 
-@pytest.mark.parametrize("geometry", [1, 6, 0, 9, 10])
+@pytest.mark.parametrize("geometry", list(range(10)))
 def test_stream_banded_geometries(pkg, dev, geometry):
     """A banded matrix of 10-40 entries per row (a row every 997 reaching
     five far places of x) at every block geometry, PETSc's order: bit-exact.
-    (Geometries 9 and 10 were cut for the withdrawn LDS x tiles; they stay
-    selectable, speed-only.)"""
+    (Round 5 removed the two geometries cut for the withdrawn LDS x tiles;
+    the ten left are all selectable, speed-only, and 10 is refused.)"""
     rng = np.random.default_rng(11)
     m = 20000
     lens = rng.integers(10, 40, m)
@@ -138,6 +138,10 @@ def test_stream_banded_geometries(pkg, dev, geometry):
     y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=1, geometry=geometry, gather_sort=0)
     assert info["stream_geometry"] == geometry
     assert_bits(y, seqaij.matmult(ai, aj, aa, x))
+    if geometry == 9:
+        with pkg.SeqAIJHIP(ai, aj, aa) as A:
+            with pytest.raises(pkg.AIJHIPError):
+                A.set_option("geometry", 10)
 
 
 @pytest.mark.parametrize("grid", [(16, 16, 16), (40, 40, 40), (300, 7, 5), (3, 200, 60)])
