@@ -571,7 +571,7 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
             with pytest.raises(pkg.AIJHIPError, match="withdrawn"):
                 A.set_option(opt, 1)
         first = None
-        for geom in range(12):
+        for geom in range(10):
             for nt in (0, 1):
                 A.set_option("geometry", geom)
                 A.set_option("nt_loads", nt)
@@ -589,7 +589,7 @@ def test_stream_options_do_not_change_results(pkg, dev, name):
         # exact and default modes
         A.set_option("nt_loads", -1)
         short = np.diff(ai) <= 1024
-        for geom in range(12):
+        for geom in range(10):
             ys = {}
             for gs, ex in ((1, 1), (1, 0), (0, 0)):
                 A.set_option("geometry", geom)
