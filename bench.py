@@ -161,6 +161,7 @@ def launch_ranks(n: int, argv, child=None, poll_s: float = 0.2) -> int:
     for r, (cmd, env) in enumerate(plan):
         procs.append(subprocess.Popen(cmd, env=env, stdout=None if r == 0 else sys.stderr.fileno()))
     rc = 0
+    t0 = last = time.perf_counter()
     try:
         while True:
             codes = [p.poll() for p in procs]
@@ -171,6 +172,10 @@ def launch_ranks(n: int, argv, child=None, poll_s: float = 0.2) -> int:
             if all(c == 0 for c in codes):
                 break
             time.sleep(poll_s)
+            if time.perf_counter() - last >= 30.0:  # a heartbeat while the ranks start up (torch import, HIP init)
+                last = time.perf_counter()
+                running = sum(c is None for c in codes)
+                print(f"bench: {running} of {n} ranks running, {last - t0:.0f} s", file=sys.stderr, flush=True)
     finally:
         for p in procs:
             if p.poll() is None:
@@ -628,6 +633,12 @@ def main():
     pkg = importlib.import_module("petsc-openacc_amd")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    t_start = time.perf_counter()
+
+    def progress(msg):
+        """A line per leg on stderr (every rank): a long multi-rank run keeps
+        writing, and a stuck rank shows where it stopped."""
+        print(f"bench[{rank}/{world}] {time.perf_counter() - t_start:7.1f} s: {msg}", file=sys.stderr, flush=True)
     if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if not torch.cuda.is_available():
@@ -672,6 +683,7 @@ def main():
     planes = nz_global // world
     row_starts = np.array([r * planes * nx * ny for r in range(world + 1)], dtype=np.int64)
     z0, z1 = rank * planes, (rank + 1) * planes
+    progress(f"operand {nx}x{ny}x{nz_global}, planes {z0}..{z1}")
     t_setup = time.perf_counter()
     ai, aj, aa = pkg.poisson_csr(nx, ny, nz_global, z0, z1)
     m_loc = len(ai) - 1
@@ -721,9 +733,11 @@ def main():
     else:
         layout_bytes = info["mult_layout_bytes"]
 
+    progress("operator ready; warm-up")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    progress("timed steps")
 
     # per-launch HIP events on the stream the SpMV kernel runs on
     K = args.steps
@@ -750,6 +764,7 @@ def main():
     if distributed:
         # Evidence the exchange hides behind the diagonal block: both halo
         # forms against the same launches of A_d alone, per rank
+        progress("halo forms")
         mine = halo_forms(op, xd, stream, K, rank, dev, m_loc, nnz_loc)
         forms = gather_forms(mine, world)
         ranks = forms[args.halo]["ranks"]
@@ -805,6 +820,7 @@ def main():
     # raised alike on every rank (a bug, an allocation failure) is recorded
     # in the line instead of discarding the headline measurement.
     def guarded(name, fn):
+        progress(name)
         try:
             res, ok = fn(), 1.0
         except Exception as e:  # noqa: BLE001
@@ -949,6 +965,7 @@ def main():
         flan = guarded("flan_standin", lambda: flan_standins(pkg, dev, max(args.roofline_reps, 50),
                                                              not args.no_cpu_baseline))
 
+    progress("done; writing the line")
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
         mean_launch_s = float(np.mean(launch_ms)) / 1e3

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--its", type=int, default=50)
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--opt", action="append", default=[], help="set_option NAME=VALUE (repeatable)")
+    ap.add_argument("--gamg-opt", action="append", default=[],
+                    help="GAMG parameter NAME=VALUE (aijhip_gamg_params_t field, repeatable), e.g. coarsen=1")
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
     K = importlib.import_module("petsc-openacc_amd.ksp")
@@ -61,16 +63,17 @@ def main():
     rhs, _ = pkg.poisson_vectors(G)
     b = torch.from_numpy(rhs).to(dev)
     x = torch.zeros_like(b)
+    gp = {k: (float(v) if "." in v else int(v)) for k, v in (o.split("=") for o in args.gamg_opt)} or None
     if args.case == "gamg":
         # a first set-up in this process pays one-time costs (code objects of
         # the set-up kernels loaded on first launch); time a second one too
-        warm = K.KSPCG(A, rtol=1e-14, atol=1e-12, pc="gamg")
+        warm = K.KSPCG(A, rtol=1e-14, atol=1e-12, pc="gamg", gamg=gp)
         t0 = time.perf_counter()
         warm.set_up()
         torch.cuda.synchronize()
         print(f"gamg: first set-up in process {time.perf_counter() - t0:.3f} s")
         warm.destroy()
-        ksp = K.KSPCG(A, rtol=1e-14, atol=1e-12, pc="gamg")
+        ksp = K.KSPCG(A, rtol=1e-14, atol=1e-12, pc="gamg", gamg=gp)
     else:
         ksp = K.KSPCG(A, rtol=0.0, atol=0.0, max_it=args.its)
     t0 = time.perf_counter()
