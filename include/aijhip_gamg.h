@@ -40,9 +40,10 @@ typedef struct aijhip_gamg_params {
     int32_t eig_its;         /* iterations of the emax(D^-1 A) estimate (10) */
     int32_t threads;         /* host threads for set-up (0 = OpenMP default) */
     int32_t device_min_rows; /* KSP set-up: levels with at least this many rows
-                              * are built on the device (strength graph, emax,
-                              * smoothing, Galerkin product; the aggregation
-                              * stays on the host); smaller ones on the host.
+                              * (or 25 x as many entries) are built on the
+                              * device (strength graph, emax, aggregation,
+                              * smoothing, Galerkin product); smaller ones on
+                              * the host.
                               * 0 = every level on the device, INT32_MAX = all
                               * on the host. Same hierarchy either way.     */
     /* ABI 3: */

@@ -461,9 +461,12 @@ __global__ void k_mis_init(int32_t m, const int32_t *__restrict__ si, int32_t *s
     if (i < m) state[i] = si[i] == si[i + 1] ? kMisSingle : kMisUndecided;
 }
 
+// first: the first round, before any root exists — a lower-key node within
+// reach already means waiting, so the scan stops there (random keys: after
+// about two neighbours instead of all ~50 of a squared 7-point graph).
 __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__restrict__ si,
                                                    const int32_t *__restrict__ sj, bool square, int32_t level,
-                                                   int32_t *state, unsigned long long *left) {
+                                                   bool first, int32_t *state, unsigned long long *left) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool waits = false;
     if (i < m && state[i] == kMisUndecided) {
@@ -477,6 +480,7 @@ __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__r
                     return false;
                 }
                 waits = true;
+                if (first) return false;
             }
             return true;
         });
@@ -551,7 +555,7 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
     for (int32_t r = 0; e == hipSuccess && r < m; ++r) {
         unsigned long long h = 0;
         if ((e = hipMemsetAsync(left, 0, sizeof(h), nullptr)) != hipSuccess) break;
-        hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, state, left);
+        hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, r == 0, state, left);
         if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = hipMemcpy(&h, left, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) break;
         *rounds = r + 1;

@@ -1325,25 +1325,34 @@ hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B,
 
 // a . b in the host builder's blocked order (block sums on the device, then
 // summed left to right on the host)
+// (s: the emax job's own stream — its copies wait for its kernels only, not
+// for the aggregation the set-up thread runs meanwhile on the null stream)
 double host_blocked_dot(const double *d_a, const double *d_b, int64_t n, double *d_part, std::vector<double> &h_part,
-                        hipError_t *e) {
+                        hipError_t *e, hipStream_t s = nullptr) {
     const int64_t nb = (n + kDotBlock - 1) / kDotBlock;
-    if (nb > 0) hipLaunchKernelGGL(k_block_dot2, dim3(blocks_for(nb, 64)), dim3(64), 0, nullptr, n, d_a, d_b, d_part);
+    if (nb > 0) hipLaunchKernelGGL(k_block_dot2, dim3(blocks_for(nb, 64)), dim3(64), 0, s, n, d_a, d_b, d_part);
     h_part.resize((size_t)nb);
-    *e = nb > 0 ? hipMemcpy(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost) : hipSuccess;
-    double s = 0.0;
-    for (int64_t q = 0; q < nb; ++q) s += h_part[q];
-    return s;
+    *e = hipSuccess;
+    if (nb > 0 && (*e = hipMemcpyAsync(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, s)) ==
+                      hipSuccess)
+        *e = hipStreamSynchronize(s);
+    double sum = 0.0;
+    for (int64_t q = 0; q < nb; ++q) sum += h_part[q];
+    return sum;
 }
 
-double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vector<double> &h_part, hipError_t *e) {
+double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vector<double> &h_part, hipError_t *e,
+                         hipStream_t s = nullptr) {
     const int64_t nb = (n + kDotBlock - 1) / kDotBlock;
-    if (nb > 0) hipLaunchKernelGGL(k_block_dot, dim3(blocks_for(nb, 64)), dim3(64), 0, nullptr, n, d_v, d_part);
+    if (nb > 0) hipLaunchKernelGGL(k_block_dot, dim3(blocks_for(nb, 64)), dim3(64), 0, s, n, d_v, d_part);
     h_part.resize((size_t)nb);
-    *e = nb > 0 ? hipMemcpy(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost) : hipSuccess;
-    double s = 0.0;
-    for (int64_t q = 0; q < nb; ++q) s += h_part[q];
-    return std::sqrt(s);
+    *e = hipSuccess;
+    if (nb > 0 && (*e = hipMemcpyAsync(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, s)) ==
+                      hipSuccess)
+        *e = hipStreamSynchronize(s);
+    double sum = 0.0;
+    for (int64_t q = 0; q < nb; ++q) sum += h_part[q];
+    return std::sqrt(sum);
 }
 
 // Pinned host staging for the strength graph and the aggregates, grown as
@@ -1391,12 +1400,17 @@ DCsr view_of(const aijhip_mat &A) {
 // cg: CG's Lanczos estimate instead (gamg_setup.cpp estimate_emax_cg: the
 // same start, A p in PETSc's row order, the same blocked dots, the
 // tridiagonal's emax by the host's bisection).
+// Both run on the set-up's stream slot 2 (a queue of its own beside the
+// aggregation's kernels on the null stream), after `ready` (D^-1 written).
 struct EmaxJob {
     std::thread th;
     double emax = 1.0;
     hipError_t e = hipSuccess;
     double *v = nullptr, *w = nullptr, *part = nullptr, *r = nullptr, *z = nullptr;
-    void start(const aijhip_mat &A, const double *dinv, int its, bool cg = false) {
+    hipStream_t js = nullptr;
+    void start(const aijhip_mat &A, const double *dinv, int its, bool cg, hipEvent_t ready) {
+        js = aijhip_gamg::setup_stream(A.device, 2);
+        if (js && ready) e = hipStreamWaitEvent(js, ready, 0);
         if (cg) {
             th = std::thread([this, &A, dinv, its] {
                 (void)hipSetDevice(A.device);
@@ -1409,25 +1423,25 @@ struct EmaxJob {
                     return;
                 if (m == 0) return;
                 double *p = v;
-                hipLaunchKernelGGL(k_cgest_start, dim3(g256), dim3(256), 0, nullptr, m, dinv, r, z, p);
-                double rz = host_blocked_dot(z, r, m, part, h_part, &e);
+                hipLaunchKernelGGL(k_cgest_start, dim3(g256), dim3(256), 0, js, m, dinv, r, z, p);
+                double rz = host_blocked_dot(z, r, m, part, h_part, &e, js);
                 if (e != hipSuccess) return;
                 for (int it = 0; it < its; ++it) {
-                    if ((e = aijhip::launch_mult_exact(A, p, w, nullptr)) != hipSuccess) return;
-                    const double pw = host_blocked_dot(p, w, m, part, h_part, &e);
+                    if ((e = aijhip::launch_mult_exact(A, p, w, js)) != hipSuccess) return;
+                    const double pw = host_blocked_dot(p, w, m, part, h_part, &e, js);
                     if (e != hipSuccess) return;
                     if (!(pw != 0.0 && rz != 0.0)) break;
                     const double a = rz / pw;
                     alpha.push_back(a);
-                    hipLaunchKernelGGL(k_cgest_update, dim3(g256), dim3(256), 0, nullptr, m, a, w, dinv, r, z);
-                    const double rzn = host_blocked_dot(z, r, m, part, h_part, &e);
+                    hipLaunchKernelGGL(k_cgest_update, dim3(g256), dim3(256), 0, js, m, a, w, dinv, r, z);
+                    const double rzn = host_blocked_dot(z, r, m, part, h_part, &e, js);
                     if (e != hipSuccess) return;
                     const double b = rzn / rz;
                     beta.push_back(b);
-                    hipLaunchKernelGGL(k_cgest_dir, dim3(g256), dim3(256), 0, nullptr, m, b, z, p);
+                    hipLaunchKernelGGL(k_cgest_dir, dim3(g256), dim3(256), 0, js, m, b, z, p);
                     rz = rzn;
                 }
-                e = hipDeviceSynchronize();
+                e = hipStreamSynchronize(js);
                 if (e == hipSuccess && !alpha.empty()) emax = aijhip_gamg::lanczos_emax(alpha, beta);
             });
             return;
@@ -1450,20 +1464,21 @@ struct EmaxJob {
                 (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
                 return;
             mark("alloc");
-            hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, nullptr, m, v);
-            const double nv = host_blocked_norm(v, m, part, h_part, &e);
+            hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, js, m, v);
+            const double nv = host_blocked_norm(v, m, part, h_part, &e, js);
             if (e != hipSuccess) return;
             mark("start");
-            hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, v, nv, v);
+            hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, js, m, v, nv, v);
             for (int it = 0; it < its; ++it) {
-                if ((e = aijhip::launch_dinv_mult(A, dinv, v, w, nullptr)) != hipSuccess) return;
-                const double nw = host_blocked_norm(w, m, part, h_part, &e);
+                if ((e = aijhip::launch_dinv_mult(A, dinv, v, w, js)) != hipSuccess) return;
+                const double nw = host_blocked_norm(w, m, part, h_part, &e, js);
                 if (e != hipSuccess) return;
                 if (it == 0) mark("iteration 0");
                 if (!(nw > 0.0)) break;
                 emax = nw;
-                hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, nullptr, m, w, nw, v);
+                hipLaunchKernelGGL(k_div, dim3(g256), dim3(256), 0, js, m, w, nw, v);
             }
+            e = hipStreamSynchronize(js);
             mark("iterations");
         });
     }
@@ -1547,14 +1562,14 @@ bool device_phase1(int32_t m, int64_t nzs, int32_t *max_rounds) {
 namespace aijhip_gamg {
 
 // Process-wide set-up streams, per device and slot (0: the phase-1 sweep,
-// 1: the host pass's staging copies): created once, kept for the life of the
+// 1: the host pass's staging copies, 2: the emax job): created once, kept for the life of the
 // process like the pinned staging (a first stream creation costs ~5 ms on the
 // MI355X; set_pc_type(GAMG) makes them ahead of the set-up).
 hipStream_t setup_stream(int device, int slot) {
     static std::mutex mu;
     static std::vector<hipStream_t> *cache = new std::vector<hipStream_t>();
     std::lock_guard<std::mutex> g(mu);
-    const size_t k = (size_t)device * 2 + (size_t)(slot & 1);
+    const size_t k = (size_t)device * 3 + (size_t)std::min(std::max(slot, 0), 2);
     if (cache->size() <= k) cache->resize(k + 1, nullptr);
     if (!(*cache)[k]) {
         int cur = 0;
@@ -1615,6 +1630,7 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
     // emax(D^-1 A) needs only A: its power iteration runs from a second
     // host thread while this one stages S and aggregates on the CPU
     EmaxJob job;
+    hipEvent_t ev_dinv = nullptr;
 #define GTRY(call, what) do { if ((e = (call)) != hipSuccess) { rc = herr(e, what); goto level_done; } } while (0)
     GTRY(dalloc(&d, m), "alloc");
     GTRY(dalloc(&dinv, m), "alloc");
@@ -1653,7 +1669,15 @@ strength_done:
     // memory; the same aggregates either way. Phase 2 on the device; phase
     // 3 (sequential) over the nodes left.
     lap("strength kernels");
-    if (emax_its > 0) job.start(A, dinv, emax_its, p.eig_ksp == 1);
+    if (emax_its > 0) {  // (D^-1 is written on the null stream: the job's stream waits for it)
+        if (hipEventCreateWithFlags(&ev_dinv, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(ev_dinv, nullptr) != hipSuccess) {
+            if (ev_dinv) (void)hipEventDestroy(ev_dinv);
+            ev_dinv = nullptr;
+            GTRY(hipDeviceSynchronize(), "D^-1");
+        }
+        job.start(A, dinv, emax_its, p.eig_ksp == 1, ev_dinv);
+    }
     GTRY(dalloc(&d_aggv, m), "alloc");
     if (p.coarsen == 1) {  // PETSc 3.7 agg's MIS (gamg_aggregate.hip), node for node the host's
         int32_t rounds = 0;
@@ -1768,6 +1792,7 @@ strength_done:
 level_done:
 #undef GTRY
     job.join();
+    if (ev_dinv) (void)hipEventDestroy(ev_dinv);
     lap("emax joined");
     hipFree(cnt); hipFree(off); hipFree(pos); hipFree(tmp); hipFree(si); hipFree(sj);
     hipFree(sval); hipFree(scan_tmp); hipFree(d); hipFree(d_ph); hipFree(d_left); hipFree(d_head);
@@ -2001,7 +2026,10 @@ int build_device(aijhip_mat *A0, const aijhip_gamg_params_t &p, std::vector<Devi
         aijhip_mat &A = *levels.back().A;
         const int32_t m = A.m;
         aijhip::Range range("PCGAMG device level");
-        if (m < p.device_min_rows || !aijhip::stream_mg_fusable(A)) {
+        // the device while the level has device_min_rows rows or 25 x as many
+        // entries (PETSc's MIS hierarchy reaches a few thousand rows of ~200
+        // entries: 82 ms of host set-up at 300^3 against ~15 on the device)
+        if ((m < p.device_min_rows && A.nz < 25 * (int64_t)p.device_min_rows) || !aijhip::stream_mg_fusable(A)) {
             *more = true;  // the host takes it from here
             break;
         }
