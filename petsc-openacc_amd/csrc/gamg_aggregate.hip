@@ -438,7 +438,10 @@ hipError_t exclusive_sum(const int32_t *in, int32_t *out, int32_t n, hipStream_t
 // are final and depend only on final states, so a stale read only delays
 // one. With random keys the chains are short (tens of rounds, not the
 // natural order's 2.35 N).
-constexpr int32_t kMisUndecided = 0, kMisRoot = 1, kMisOut = 2, kMisSingle = 3;
+// one byte per node: a squared 7-point neighbourhood spans +-2 planes, 360 KB
+// of byte states against 1.4 MB of int32 ones (per-XCD L2: 4 MB)
+typedef uint8_t mis_state_t;
+constexpr mis_state_t kMisUndecided = 0, kMisRoot = 1, kMisOut = 2, kMisSingle = 3;
 
 template <class F>
 __device__ __forceinline__ void for_reach(int32_t i, bool square, const int32_t *__restrict__ si,
@@ -456,7 +459,7 @@ __device__ __forceinline__ void for_reach(int32_t i, bool square, const int32_t 
     }
 }
 
-__global__ void k_mis_init(int32_t m, const int32_t *__restrict__ si, int32_t *state) {
+__global__ void k_mis_init(int32_t m, const int32_t *__restrict__ si, mis_state_t *state) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) state[i] = si[i] == si[i + 1] ? kMisSingle : kMisUndecided;
 }
@@ -466,14 +469,14 @@ __global__ void k_mis_init(int32_t m, const int32_t *__restrict__ si, int32_t *s
 // about two neighbours instead of all ~50 of a squared 7-point graph).
 __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__restrict__ si,
                                                    const int32_t *__restrict__ sj, bool square, int32_t level,
-                                                   bool first, int32_t *state, unsigned long long *left) {
+                                                   bool first, mis_state_t *state, unsigned long long *left) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool waits = false;
     if (i < m && state[i] == kMisUndecided) {
         const uint64_t ki = aijhip_gamg::mis_key(i, level);
         bool out = false;
         for_reach(i, square, si, sj, [&](int32_t w) {
-            const int32_t st = __builtin_nontemporal_load(state + w);  // (another lane may have decided it)
+            const mis_state_t st = __builtin_nontemporal_load(state + w);  // (another lane may have decided it)
             if ((st == kMisRoot || st == kMisUndecided) && aijhip_gamg::mis_key(w, level) < ki) {
                 if (st == kMisRoot) {
                     out = true;
@@ -498,11 +501,11 @@ __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__r
 // flag[i] = 1 for the roots (their scan numbers the aggregates).
 __global__ __launch_bounds__(256) void k_mis_parent(int32_t m, const int32_t *__restrict__ si,
                                                     const int32_t *__restrict__ sj, bool square, int32_t level,
-                                                    const int32_t *__restrict__ state, int32_t *parent,
+                                                    const mis_state_t *__restrict__ state, int32_t *parent,
                                                     int32_t *flag) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
-    const int32_t st = state[i];
+    const mis_state_t st = state[i];
     flag[i] = st == kMisRoot;
     if (st == kMisRoot) { parent[i] = i; return; }
     if (st != kMisOut) { parent[i] = -1; return; }
@@ -541,7 +544,8 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
     *na = 0;
     *rounds = 0;
     if (m == 0) return hipSuccess;
-    int32_t *state = nullptr, *parent = nullptr, *flag = nullptr, *cidx = nullptr;
+    mis_state_t *state = nullptr;
+    int32_t *parent = nullptr, *flag = nullptr, *cidx = nullptr;
     unsigned long long *left = nullptr;
     const unsigned g = blocks_for(m, 256);
     hipError_t e = dalloc(&state, m);
@@ -552,13 +556,18 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
     }
     // every round decides at least the lowest-key undecided node, so m
     // rounds always suffice; random keys need a few tens
+    static const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     for (int32_t r = 0; e == hipSuccess && r < m; ++r) {
         unsigned long long h = 0;
+        const auto t0 = std::chrono::steady_clock::now();
         if ((e = hipMemsetAsync(left, 0, sizeof(h), nullptr)) != hipSuccess) break;
         hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, r == 0, state, left);
         if ((e = hipGetLastError()) != hipSuccess) break;
         if ((e = hipMemcpy(&h, left, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) break;
         *rounds = r + 1;
+        if (log)
+            std::fprintf(stderr, "  MIS round %d: %llu undecided, %.3f ms\n", r, h,
+                         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         if (h == 0) break;
     }
     if (e == hipSuccess) e = dalloc(&parent, m);
