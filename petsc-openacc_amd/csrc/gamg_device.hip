@@ -1327,31 +1327,44 @@ hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B,
 // summed left to right on the host)
 // (s: the emax job's own stream — its copies wait for its kernels only, not
 // for the aggregation the set-up thread runs meanwhile on the null stream)
-double host_blocked_dot(const double *d_a, const double *d_b, int64_t n, double *d_part, std::vector<double> &h_part,
+// Block partials come down into h_part: pinned (the emax job's) — a
+// pageable copy goes through the runtime's staging and, measured, kept the
+// job in step with the aggregation on the null stream (r05j: the CG estimate
+// was the level's critical path) — or a vector grown here (other callers).
+struct HostPart {
+    double *pinned = nullptr;
+    int64_t cap = 0;
+    std::vector<double> pageable;
+    double *get(int64_t nb) {
+        if (pinned && nb <= cap) return pinned;
+        pageable.resize((size_t)std::max<int64_t>(nb, 1));
+        return pageable.data();
+    }
+};
+
+double host_blocked_dot(const double *d_a, const double *d_b, int64_t n, double *d_part, HostPart &hp,
                         hipError_t *e, hipStream_t s = nullptr) {
     const int64_t nb = (n + kDotBlock - 1) / kDotBlock;
     if (nb > 0) hipLaunchKernelGGL(k_block_dot2, dim3(blocks_for(nb, 64)), dim3(64), 0, s, n, d_a, d_b, d_part);
-    h_part.resize((size_t)nb);
+    double *h = hp.get(nb);
     *e = hipSuccess;
-    if (nb > 0 && (*e = hipMemcpyAsync(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, s)) ==
-                      hipSuccess)
+    if (nb > 0 && (*e = hipMemcpyAsync(h, d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, s)) == hipSuccess)
         *e = hipStreamSynchronize(s);
     double sum = 0.0;
-    for (int64_t q = 0; q < nb; ++q) sum += h_part[q];
+    for (int64_t q = 0; q < nb; ++q) sum += h[q];
     return sum;
 }
 
-double host_blocked_norm(const double *d_v, int64_t n, double *d_part, std::vector<double> &h_part, hipError_t *e,
+double host_blocked_norm(const double *d_v, int64_t n, double *d_part, HostPart &hp, hipError_t *e,
                          hipStream_t s = nullptr) {
     const int64_t nb = (n + kDotBlock - 1) / kDotBlock;
     if (nb > 0) hipLaunchKernelGGL(k_block_dot, dim3(blocks_for(nb, 64)), dim3(64), 0, s, n, d_v, d_part);
-    h_part.resize((size_t)nb);
+    double *h = hp.get(nb);
     *e = hipSuccess;
-    if (nb > 0 && (*e = hipMemcpyAsync(h_part.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, s)) ==
-                      hipSuccess)
+    if (nb > 0 && (*e = hipMemcpyAsync(h, d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost, s)) == hipSuccess)
         *e = hipStreamSynchronize(s);
     double sum = 0.0;
-    for (int64_t q = 0; q < nb; ++q) sum += h_part[q];
+    for (int64_t q = 0; q < nb; ++q) sum += h[q];
     return std::sqrt(sum);
 }
 
@@ -1407,6 +1420,7 @@ struct EmaxJob {
     double emax = 1.0;
     hipError_t e = hipSuccess;
     double *v = nullptr, *w = nullptr, *part = nullptr, *r = nullptr, *z = nullptr;
+    double *h_pin = nullptr;  // pinned host partials
     hipStream_t js = nullptr;
     void start(const aijhip_mat &A, const double *dinv, int its, bool cg, hipEvent_t ready) {
         js = aijhip_gamg::setup_stream(A.device, 2);
@@ -1416,11 +1430,18 @@ struct EmaxJob {
                 (void)hipSetDevice(A.device);
                 const int32_t m = A.m;
                 const unsigned g256 = blocks_for(m, 256);
-                std::vector<double> h_part, alpha, beta;
+                std::vector<double> alpha, beta;
+                HostPart h_part;
+                const int64_t nb = (m + kDotBlock - 1) / kDotBlock;
                 if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
                     (e = dalloc(&r, m)) != hipSuccess || (e = dalloc(&z, m)) != hipSuccess ||
-                    (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
+                    (e = dalloc(&part, nb)) != hipSuccess)
                     return;
+                if (hipHostMalloc(reinterpret_cast<void **>(&h_pin), sizeof(double) * (size_t)std::max<int64_t>(nb, 1)) ==
+                    hipSuccess) {
+                    h_part.pinned = h_pin;
+                    h_part.cap = nb;
+                }
                 if (m == 0) return;
                 double *p = v;
                 hipLaunchKernelGGL(k_cgest_start, dim3(g256), dim3(256), 0, js, m, dinv, r, z, p);
@@ -1459,10 +1480,16 @@ struct EmaxJob {
             (void)hipSetDevice(A.device);
             const int32_t m = A.m;
             const unsigned g256 = blocks_for(m, 256);
-            std::vector<double> h_part;
+            HostPart h_part;
+            const int64_t nb = (m + kDotBlock - 1) / kDotBlock;
             if ((e = dalloc(&v, m)) != hipSuccess || (e = dalloc(&w, m)) != hipSuccess ||
-                (e = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
+                (e = dalloc(&part, nb)) != hipSuccess)
                 return;
+            if (hipHostMalloc(reinterpret_cast<void **>(&h_pin), sizeof(double) * (size_t)std::max<int64_t>(nb, 1)) ==
+                hipSuccess) {
+                h_part.pinned = h_pin;
+                h_part.cap = nb;
+            }
             mark("alloc");
             hipLaunchKernelGGL(k_power_start, dim3(g256), dim3(256), 0, js, m, v);
             const double nv = host_blocked_norm(v, m, part, h_part, &e, js);
@@ -1487,7 +1514,8 @@ struct EmaxJob {
     }
     void release() {
         hipFree(v); hipFree(w); hipFree(part); hipFree(r); hipFree(z);
-        v = w = part = r = z = nullptr;
+        if (h_pin) (void)hipHostFree(h_pin);
+        v = w = part = r = z = h_pin = nullptr;
     }
     ~EmaxJob() {
         join();
