@@ -476,7 +476,9 @@ __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__r
         const uint64_t ki = aijhip_gamg::mis_key(i, level);
         bool out = false;
         for_reach(i, square, si, sj, [&](int32_t w) {
-            const mis_state_t st = __builtin_nontemporal_load(state + w);  // (another lane may have decided it)
+            // a plain (cached) read: a state another lane decided this round
+            // may read stale, which only delays this node to the next round
+            const mis_state_t st = state[w];
             if ((st == kMisRoot || st == kMisUndecided) && aijhip_gamg::mis_key(w, level) < ki) {
                 if (st == kMisRoot) {
                     out = true;
