@@ -558,20 +558,35 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
     }
     // every round decides at least the lowest-key undecided node, so m
     // rounds always suffice; random keys need a few tens
+    // Rounds go out in batches of kBatch with one count read per batch (a
+    // round past the last is a no-op launch): the count comes back through
+    // pinned memory on the null stream's own copy, so the read waits for the
+    // rounds only — round 5's first form read it with a synchronous pageable
+    // hipMemcpy per round and measured ~5 ms a round, in step with the emax
+    // job on its other stream.
     static const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
-    for (int32_t r = 0; e == hipSuccess && r < m; ++r) {
-        unsigned long long h = 0;
+    constexpr int32_t kBatch = 4;
+    unsigned long long *h_left = nullptr;
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_left), sizeof(unsigned long long));
+    for (int32_t r0 = 0; e == hipSuccess && r0 < m; r0 += kBatch) {
         const auto t0 = std::chrono::steady_clock::now();
-        if ((e = hipMemsetAsync(left, 0, sizeof(h), nullptr)) != hipSuccess) break;
-        hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, r == 0, state, left);
-        if ((e = hipGetLastError()) != hipSuccess) break;
-        if ((e = hipMemcpy(&h, left, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) break;
-        *rounds = r + 1;
+        for (int32_t r = r0; r < r0 + kBatch && e == hipSuccess; ++r) {
+            if ((e = hipMemsetAsync(left, 0, sizeof(unsigned long long), nullptr)) != hipSuccess) break;
+            hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, r == 0, state,
+                               left);
+            e = hipGetLastError();
+        }
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(h_left, left, sizeof(unsigned long long), hipMemcpyDeviceToHost, nullptr);
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+        if (e != hipSuccess) break;
+        *rounds = r0 + kBatch;
         if (log)
-            std::fprintf(stderr, "  MIS round %d: %llu undecided, %.3f ms\n", r, h,
+            std::fprintf(stderr, "  MIS rounds %d-%d: %llu undecided after, %.3f ms\n", r0, r0 + kBatch - 1, *h_left,
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-        if (h == 0) break;
+        if (*h_left == 0) break;
     }
+    if (h_left) (void)hipHostFree(h_left);
     if (e == hipSuccess) e = dalloc(&parent, m);
     if (e == hipSuccess) e = dalloc(&flag, m);
     if (e == hipSuccess) e = dalloc(&cidx, m);
