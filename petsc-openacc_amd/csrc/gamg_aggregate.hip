@@ -459,27 +459,40 @@ __device__ __forceinline__ void for_reach(int32_t i, bool square, const int32_t 
     }
 }
 
-__global__ void k_mis_init(int32_t m, const int32_t *__restrict__ si, mis_state_t *state) {
+// hk[i]: the high word of mis_key(i, level) — its low word is i, so
+// mis_key(w) < mis_key(i) iff (hk[w], w) < (hk[i], i). Hashing once here
+// instead of per neighbour visit: the squared 7-point rounds were bound by the
+// 64-bit hash (~50 per node), ~5 ms a round at 300^3.
+__device__ __forceinline__ bool key_below(uint32_t hw, int32_t w, uint32_t hi, int32_t i) {
+    return hw < hi || (hw == hi && w < i);
+}
+
+__global__ void k_mis_init(int32_t m, int32_t level, const int32_t *__restrict__ si, mis_state_t *state,
+                           uint32_t *hk) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) state[i] = si[i] == si[i + 1] ? kMisSingle : kMisUndecided;
+    if (i < m) {
+        state[i] = si[i] == si[i + 1] ? kMisSingle : kMisUndecided;
+        hk[i] = static_cast<uint32_t>(aijhip_gamg::mis_key(i, level) >> 32);
+    }
 }
 
 // first: the first round, before any root exists — a lower-key node within
 // reach already means waiting, so the scan stops there (random keys: after
 // about two neighbours instead of all ~50 of a squared 7-point graph).
 __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__restrict__ si,
-                                                   const int32_t *__restrict__ sj, bool square, int32_t level,
-                                                   bool first, mis_state_t *state, unsigned long long *left) {
+                                                   const int32_t *__restrict__ sj, bool square,
+                                                   const uint32_t *__restrict__ hk, bool first, mis_state_t *state,
+                                                   unsigned long long *left) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool waits = false;
     if (i < m && state[i] == kMisUndecided) {
-        const uint64_t ki = aijhip_gamg::mis_key(i, level);
+        const uint32_t hi = hk[i];
         bool out = false;
         for_reach(i, square, si, sj, [&](int32_t w) {
             // a plain (cached) read: a state another lane decided this round
             // may read stale, which only delays this node to the next round
             const mis_state_t st = state[w];
-            if ((st == kMisRoot || st == kMisUndecided) && aijhip_gamg::mis_key(w, level) < ki) {
+            if ((st == kMisRoot || st == kMisUndecided) && key_below(hk[w], w, hi, i)) {
                 if (st == kMisRoot) {
                     out = true;
                     return false;
@@ -502,7 +515,8 @@ __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__r
 // highest-index root among its S neighbours when it has one; singletons -1.
 // flag[i] = 1 for the roots (their scan numbers the aggregates).
 __global__ __launch_bounds__(256) void k_mis_parent(int32_t m, const int32_t *__restrict__ si,
-                                                    const int32_t *__restrict__ sj, bool square, int32_t level,
+                                                    const int32_t *__restrict__ sj, bool square,
+                                                    const uint32_t *__restrict__ hk,
                                                     const mis_state_t *__restrict__ state, int32_t *parent,
                                                     int32_t *flag) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -512,11 +526,11 @@ __global__ __launch_bounds__(256) void k_mis_parent(int32_t m, const int32_t *__
     if (st == kMisRoot) { parent[i] = i; return; }
     if (st != kMisOut) { parent[i] = -1; return; }
     int32_t best = -1;
-    uint64_t bk = ~0ull;
+    uint32_t bh = 0;
     for_reach(i, square, si, sj, [&](int32_t w) {
         if (state[w] == kMisRoot) {
-            const uint64_t kw = aijhip_gamg::mis_key(w, level);
-            if (kw < bk) { bk = kw; best = w; }
+            const uint32_t hw = hk[w];
+            if (best < 0 || key_below(hw, w, bh, best)) { bh = hw; best = w; }
         }
         return true;
     });
@@ -547,13 +561,15 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
     *rounds = 0;
     if (m == 0) return hipSuccess;
     mis_state_t *state = nullptr;
+    uint32_t *hk = nullptr;
     int32_t *parent = nullptr, *flag = nullptr, *cidx = nullptr;
     unsigned long long *left = nullptr;
     const unsigned g = blocks_for(m, 256);
     hipError_t e = dalloc(&state, m);
+    if (e == hipSuccess) e = dalloc(&hk, m);
     if (e == hipSuccess) e = dalloc(&left, 1);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mis_init, dim3(g), dim3(256), 0, nullptr, m, si, state);
+        hipLaunchKernelGGL(k_mis_init, dim3(g), dim3(256), 0, nullptr, m, level, si, state, hk);
         e = hipGetLastError();
     }
     // every round decides at least the lowest-key undecided node, so m
@@ -572,7 +588,7 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
         const auto t0 = std::chrono::steady_clock::now();
         for (int32_t r = r0; r < r0 + kBatch && e == hipSuccess; ++r) {
             if ((e = hipMemsetAsync(left, 0, sizeof(unsigned long long), nullptr)) != hipSuccess) break;
-            hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, r == 0, state,
+            hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, hk, r == 0, state,
                                left);
             e = hipGetLastError();
         }
@@ -591,7 +607,7 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
     if (e == hipSuccess) e = dalloc(&flag, m);
     if (e == hipSuccess) e = dalloc(&cidx, m);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mis_parent, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, level, state, parent,
+        hipLaunchKernelGGL(k_mis_parent, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, hk, state, parent,
                            flag);
         e = hipGetLastError();
     }
@@ -606,7 +622,7 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
         hipLaunchKernelGGL(k_mis_number, dim3(g), dim3(256), 0, nullptr, m, parent, cidx, agg);
         e = hipGetLastError();
     }
-    hipFree(state); hipFree(parent); hipFree(flag); hipFree(cidx); hipFree(left);
+    hipFree(state); hipFree(hk); hipFree(parent); hipFree(flag); hipFree(cidx); hipFree(left);
     return e;
 }
 
