@@ -432,39 +432,35 @@ hipError_t exclusive_sum(const int32_t *in, int32_t *out, int32_t n, hipStream_t
 // at every node no earlier root lies within reach of (G2: two steps of S
 // when squared, one otherwise), so the roots are the lexicographically-first
 // independent set of G2 by key, unique: node i is a root iff no lower-key
-// node within reach of it is one. Rounds decide it in place: an undecided
-// node that sees a lower-key root within reach is OUT; one whose lower-key
-// nodes within reach are all OUT is a root; otherwise it waits. Decisions
-// are final and depend only on final states, so a stale read only delays
-// one. With random keys the chains are short (tens of rounds, not the
-// natural order's 2.35 N).
+// node within reach of it is one. Rounds decide it: an undecided node with a
+// root within reach is OUT (that root has the lower key: it was decided with
+// i undecided in its reach); one whose lower-key nodes within reach are all
+// OUT is a root; otherwise it waits. Decisions are final, so the rounds reach
+// the sequential pass's set whatever their number (random keys: ~16-20).
+//
+// A round is two flat one-hop passes rather than one two-hop walk: pass A
+// takes, for every node u, the minimum over its closed neighbourhood N[u] of
+// a value that is 0 for a root, key + 1 for an undecided node and all-ones
+// otherwise; pass B takes each undecided node's minimum over its neighbours'
+// pass-A values (squared) or its own (not) — that covers its reach and
+// itself — and decides: 0 → OUT, its own key + 1 → root, else it waits.
+// Round 5's first form walked the two-hop reach per lane (~50 visits, each a
+// dependent sj → state → key load chain): ~5 ms a round at 300^3 against
+// two neighbour-list passes' worth of bytes here.
 // one byte per node: a squared 7-point neighbourhood spans +-2 planes, 360 KB
 // of byte states against 1.4 MB of int32 ones (per-XCD L2: 4 MB)
 typedef uint8_t mis_state_t;
 constexpr mis_state_t kMisUndecided = 0, kMisRoot = 1, kMisOut = 2, kMisSingle = 3;
 
-template <class F>
-__device__ __forceinline__ void for_reach(int32_t i, bool square, const int32_t *__restrict__ si,
-                                          const int32_t *__restrict__ sj, F f) {
-    const int32_t a1 = si[i + 1];
-    for (int32_t a = si[i]; a < a1; ++a) {
-        const int32_t j = sj[a];
-        if (!f(j)) return;
-        if (!square) continue;
-        const int32_t b1 = si[j + 1];
-        for (int32_t b = si[j]; b < b1; ++b) {
-            const int32_t k = sj[b];
-            if (k != i && !f(k)) return;
-        }
-    }
+// hk[i]: the high word of mis_key(i, level); its low word is i.
+__device__ __forceinline__ uint64_t mis_key_of(uint32_t h, int32_t i) {
+    return (uint64_t)h << 32 | (uint32_t)i;
 }
 
-// hk[i]: the high word of mis_key(i, level) — its low word is i, so
-// mis_key(w) < mis_key(i) iff (hk[w], w) < (hk[i], i). Hashing once here
-// instead of per neighbour visit: the squared 7-point rounds were bound by the
-// 64-bit hash (~50 per node), ~5 ms a round at 300^3.
-__device__ __forceinline__ bool key_below(uint32_t hw, int32_t w, uint32_t hi, int32_t i) {
-    return hw < hi || (hw == hi && w < i);
+// roots = false: a round's decision value; true: a root's key (parents)
+__device__ __forceinline__ uint64_t mis_value(mis_state_t st, uint32_t h, int32_t w, bool roots) {
+    if (roots) return st == kMisRoot ? mis_key_of(h, w) : ~0ull;
+    return st == kMisRoot ? 0ull : st == kMisUndecided ? mis_key_of(h, w) + 1 : ~0ull;
 }
 
 __global__ void k_mis_init(int32_t m, int32_t level, const int32_t *__restrict__ si, mis_state_t *state,
@@ -476,34 +472,67 @@ __global__ void k_mis_init(int32_t m, int32_t level, const int32_t *__restrict__
     }
 }
 
-// first: the first round, before any root exists — a lower-key node within
-// reach already means waiting, so the scan stops there (random keys: after
-// about two neighbours instead of all ~50 of a squared 7-point graph).
-__global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__restrict__ si,
-                                                   const int32_t *__restrict__ sj, bool square,
-                                                   const uint32_t *__restrict__ hk, bool first, mis_state_t *state,
-                                                   unsigned long long *left) {
+// Pass A: amin[u] = min over N[u] of mis_value. Neighbour lists go four at a
+// time (clamped, so a repeat only re-reads the last one), their loads issued
+// together.
+__global__ __launch_bounds__(256) void k_mis_closed_min(int32_t m, const int32_t *__restrict__ si,
+                                                        const int32_t *__restrict__ sj,
+                                                        const uint32_t *__restrict__ hk,
+                                                        const mis_state_t *__restrict__ state, bool roots,
+                                                        uint64_t *__restrict__ amin) {
+    const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= m) return;
+    uint64_t best = mis_value(state[u], hk[u], u, roots);
+    const int32_t a0 = si[u], a1 = si[u + 1];
+    for (int32_t a = a0; a < a1; a += 4) {
+        int32_t j[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) j[q] = sj[min(a + q, a1 - 1)];
+        mis_state_t st[4];
+        uint32_t h[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            st[q] = state[j[q]];
+            h[q] = hk[j[q]];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) best = min(best, mis_value(st[q], h[q], j[q], roots));
+    }
+    amin[u] = best;
+}
+
+// min over i's neighbours of amin (squared reach), or amin[i] itself
+__device__ __forceinline__ uint64_t reach_min(int32_t i, bool square, const int32_t *__restrict__ si,
+                                              const int32_t *__restrict__ sj, const uint64_t *__restrict__ amin) {
+    if (!square) return amin[i];
+    uint64_t b = ~0ull;
+    const int32_t a0 = si[i], a1 = si[i + 1];
+    for (int32_t a = a0; a < a1; a += 4) {
+        int32_t j[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) j[q] = sj[min(a + q, a1 - 1)];
+        uint64_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = amin[j[q]];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b = min(b, v[q]);
+    }
+    return b;
+}
+
+// Pass B: the decisions (only this node's state is written; every read is
+// of pass A's output, so a round is the same whatever the lane order).
+__global__ __launch_bounds__(256) void k_mis_decide(int32_t m, const int32_t *__restrict__ si,
+                                                    const int32_t *__restrict__ sj, bool square,
+                                                    const uint32_t *__restrict__ hk,
+                                                    const uint64_t *__restrict__ amin, mis_state_t *state,
+                                                    unsigned long long *left) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     bool waits = false;
     if (i < m && state[i] == kMisUndecided) {
-        const uint32_t hi = hk[i];
-        bool out = false;
-        for_reach(i, square, si, sj, [&](int32_t w) {
-            // a plain (cached) read: a state another lane decided this round
-            // may read stale, which only delays this node to the next round
-            const mis_state_t st = state[w];
-            if ((st == kMisRoot || st == kMisUndecided) && key_below(hk[w], w, hi, i)) {
-                if (st == kMisRoot) {
-                    out = true;
-                    return false;
-                }
-                waits = true;
-                if (first) return false;
-            }
-            return true;
-        });
-        if (out) state[i] = kMisOut;
-        else if (!waits) state[i] = kMisRoot;
+        const uint64_t b = reach_min(i, square, si, sj, amin);
+        if (b == 0) state[i] = kMisOut;
+        else if (b == mis_key_of(hk[i], i) + 1) state[i] = kMisRoot;
         else waits = true;
     }
     const unsigned long long nw = __popcll(__ballot(waits));
@@ -511,12 +540,13 @@ __global__ __launch_bounds__(256) void k_mis_round(int32_t m, const int32_t *__r
 }
 
 // parent: a root itself; an OUT node the lowest-key root within reach (the
-// first root of the pass to take it), then (squared: smoothAggs) the
-// highest-index root among its S neighbours when it has one; singletons -1.
-// flag[i] = 1 for the roots (their scan numbers the aggregates).
+// first root of the pass to take it: amin over roots' keys, whose low word is
+// the root), then (squared: smoothAggs) the highest-index root among its S
+// neighbours when it has one; singletons -1. flag[i] = 1 for the roots
+// (their scan numbers the aggregates).
 __global__ __launch_bounds__(256) void k_mis_parent(int32_t m, const int32_t *__restrict__ si,
                                                     const int32_t *__restrict__ sj, bool square,
-                                                    const uint32_t *__restrict__ hk,
+                                                    const uint64_t *__restrict__ amin,
                                                     const mis_state_t *__restrict__ state, int32_t *parent,
                                                     int32_t *flag) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -525,15 +555,8 @@ __global__ __launch_bounds__(256) void k_mis_parent(int32_t m, const int32_t *__
     flag[i] = st == kMisRoot;
     if (st == kMisRoot) { parent[i] = i; return; }
     if (st != kMisOut) { parent[i] = -1; return; }
-    int32_t best = -1;
-    uint32_t bh = 0;
-    for_reach(i, square, si, sj, [&](int32_t w) {
-        if (state[w] == kMisRoot) {
-            const uint32_t hw = hk[w];
-            if (best < 0 || key_below(hw, w, bh, best)) { bh = hw; best = w; }
-        }
-        return true;
-    });
+    const uint64_t b = reach_min(i, square, si, sj, amin);  // an OUT node has a root within reach
+    int32_t best = static_cast<int32_t>(static_cast<uint32_t>(b));
     if (square) {
         int32_t hi = -1;
         for (int32_t a = si[i]; a < si[i + 1]; ++a) {
@@ -562,33 +585,32 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
     if (m == 0) return hipSuccess;
     mis_state_t *state = nullptr;
     uint32_t *hk = nullptr;
+    uint64_t *amin = nullptr;
     int32_t *parent = nullptr, *flag = nullptr, *cidx = nullptr;
-    unsigned long long *left = nullptr;
+    unsigned long long *left = nullptr, *h_left = nullptr;
     const unsigned g = blocks_for(m, 256);
     hipError_t e = dalloc(&state, m);
     if (e == hipSuccess) e = dalloc(&hk, m);
+    if (e == hipSuccess) e = dalloc(&amin, m);
     if (e == hipSuccess) e = dalloc(&left, 1);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_left), sizeof(unsigned long long));
     if (e == hipSuccess) {
         hipLaunchKernelGGL(k_mis_init, dim3(g), dim3(256), 0, nullptr, m, level, si, state, hk);
         e = hipGetLastError();
     }
-    // every round decides at least the lowest-key undecided node, so m
-    // rounds always suffice; random keys need a few tens
-    // Rounds go out in batches of kBatch with one count read per batch (a
-    // round past the last is a no-op launch): the count comes back through
-    // pinned memory on the null stream's own copy, so the read waits for the
-    // rounds only — round 5's first form read it with a synchronous pageable
-    // hipMemcpy per round and measured ~5 ms a round, in step with the emax
-    // job on its other stream.
+    // Every round decides at least the lowest-key undecided node, so m rounds
+    // always suffice. They go out in batches of kBatch with one count read
+    // per batch (a round past the last is a no-op), the count through pinned
+    // memory on the null stream's own copy, so the read waits for the rounds
+    // alone.
     static const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     constexpr int32_t kBatch = 4;
-    unsigned long long *h_left = nullptr;
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_left), sizeof(unsigned long long));
     for (int32_t r0 = 0; e == hipSuccess && r0 < m; r0 += kBatch) {
         const auto t0 = std::chrono::steady_clock::now();
         for (int32_t r = r0; r < r0 + kBatch && e == hipSuccess; ++r) {
             if ((e = hipMemsetAsync(left, 0, sizeof(unsigned long long), nullptr)) != hipSuccess) break;
-            hipLaunchKernelGGL(k_mis_round, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, hk, r == 0, state,
+            hipLaunchKernelGGL(k_mis_closed_min, dim3(g), dim3(256), 0, nullptr, m, si, sj, hk, state, false, amin);
+            hipLaunchKernelGGL(k_mis_decide, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, hk, amin, state,
                                left);
             e = hipGetLastError();
         }
@@ -602,12 +624,12 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
         if (*h_left == 0) break;
     }
-    if (h_left) (void)hipHostFree(h_left);
     if (e == hipSuccess) e = dalloc(&parent, m);
     if (e == hipSuccess) e = dalloc(&flag, m);
     if (e == hipSuccess) e = dalloc(&cidx, m);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mis_parent, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, hk, state, parent,
+        hipLaunchKernelGGL(k_mis_closed_min, dim3(g), dim3(256), 0, nullptr, m, si, sj, hk, state, true, amin);
+        hipLaunchKernelGGL(k_mis_parent, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, amin, state, parent,
                            flag);
         e = hipGetLastError();
     }
@@ -622,7 +644,8 @@ hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj,
         hipLaunchKernelGGL(k_mis_number, dim3(g), dim3(256), 0, nullptr, m, parent, cidx, agg);
         e = hipGetLastError();
     }
-    hipFree(state); hipFree(hk); hipFree(parent); hipFree(flag); hipFree(cidx); hipFree(left);
+    if (h_left) (void)hipHostFree(h_left);
+    hipFree(state); hipFree(hk); hipFree(amin); hipFree(parent); hipFree(flag); hipFree(cidx); hipFree(left);
     return e;
 }
 
