@@ -901,6 +901,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "row_patterns: -1 auto, 0 off, 1 on");
             t.patterns = value;
             break;
+        case AIJHIP_OPT_PIPELINE:
+            if (value < 0 || value > 8) return fail(AIJHIP_ERR_ARG, "pipeline: 0 off, 1..8 workgroups per CU");
+            t.pipe = value;
+            break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
