@@ -162,9 +162,9 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
 /* Speed-only knobs of the STREAM kernel; results are identical for every
  * setting. Re-plans on the device. */
 enum {
-    /* Values 2, 4, 5, 7, 11 and 15 (and kernel 4) are reserved:
-     * A/B-only variants withdrawn in ABI 2 (measured slower);
-     * setting them returns AIJHIP_ERR_ARG. */
+    /* Values 2, 4, 5, 7, 11, 15 and 16 (and kernel 4) are reserved:
+     * A/B-only variants withdrawn (measured slower); setting
+     * them returns AIJHIP_ERR_ARG. */
     AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..9: lanes / LDS entries / rows per block
                                        (DESIGN.md §Kernels); -1 (default):
                                        6 for short rows, 1 for long rows    */
@@ -223,7 +223,7 @@ enum {
                                        entries), else the automatic layout
                                        without them; costs 2 bytes per entry
                                        of device memory                      */
-    AIJHIP_OPT_ROW_PATTERNS = 14,   /* short-row operands whose rows follow at
+    AIJHIP_OPT_ROW_PATTERNS = 14    /* short-row operands whose rows follow at
                                        most 256 distinct column - row offset
                                        lists (stencils): no per-entry column
                                        at all — a pattern id per row (1 byte),
@@ -232,13 +232,6 @@ enum {
                                        sums. 1 on, 0 off, -1 (default): tried
                                        first where the mean row is at most 16
                                        entries; costs 1 byte per row          */
-    AIJHIP_OPT_PIPELINE = 16        /* plain aj row blocks (full-row lists, one
-                                       row per lane): 0 (default) one block
-                                       per workgroup; k > 0 a persistent grid
-                                       of k workgroups per CU, each with two
-                                       blocks in flight (the next block's aj /
-                                       aa loading while this one's gathers,
-                                       sums and stores run). Same bits.     */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

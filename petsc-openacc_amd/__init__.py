@@ -33,10 +33,10 @@ if os.environ.get("AIJHIP_LIB"):
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
 OPTIONS = {"geometry": 1, "nt_loads": 3, "exact": 6, "long_xcd": 8, "long_overlap": 9, "host_pipeline": 10,
-           "gather_sort": 12, "column_codes": 13, "row_patterns": 14, "pipeline": 16}
+           "gather_sort": 12, "column_codes": 13, "row_patterns": 14}
 # withdrawn in ABI 2 (measured slower); the library refuses them
 WITHDRAWN_OPTIONS = {"xcd_remap": 2, "persistent": 4, "clamped": 5, "x_tile": 7, "row_group": 11,
-                     "long_window": 15}
+                     "long_window": 15, "pipeline": 16}
 
 AIJHIP_OK, AIJHIP_ERR_ARG, AIJHIP_ERR_ALLOC, AIJHIP_ERR_HIP, AIJHIP_ERR_NODEVICE, AIJHIP_ERR_STATE = range(6)
 

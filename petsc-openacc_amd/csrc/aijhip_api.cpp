@@ -872,9 +872,9 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < -1 || value >= aijhip::kNumStreamGeoms) return fail(AIJHIP_ERR_ARG, "bad geometry");
             t.geom = value;
             break;
-        case 2: case 4: case 5: case 7: case 11: case 15:  // reserved (include/aijhip.h)
+        case 2: case 4: case 5: case 7: case 11: case 15: case 16:  // reserved (include/aijhip.h)
             return fail(AIJHIP_ERR_ARG, "option " + std::to_string(option) +
-                                            " was withdrawn in ABI 2 (measured slower; DESIGN.md §5)");
+                                            " was withdrawn (measured slower; DESIGN.md §5)");
         case AIJHIP_OPT_NT_LOADS:
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "nt_loads: -1 (auto), 0, 1");
             t.nt = value;
@@ -900,10 +900,6 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_ROW_PATTERNS:
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "row_patterns: -1 auto, 0 off, 1 on");
             t.patterns = value;
-            break;
-        case AIJHIP_OPT_PIPELINE:
-            if (value < 0 || value > 8) return fail(AIJHIP_ERR_ARG, "pipeline: 0 off, 1..8 workgroups per CU");
-            t.pipe = value;
             break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }

@@ -106,8 +106,6 @@ struct Tuning {
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
                            // offset lists are few), 0 off, 1 on
-    int pipe = 0;          // plain aj blocks: 0 one block per workgroup, k > 0 persistent grid of k
-                           // workgroups per CU with two blocks in flight (k_spmv_pipe)
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is

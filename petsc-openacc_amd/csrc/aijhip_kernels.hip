@@ -475,138 +475,6 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
                                                 sslot, sbase, prod, cdict);
 }
 
-// PIPE: the plain STREAM row blocks (full-row lists, one row per lane) with
-// two blocks in flight per workgroup. A persistent grid walks blocks b,
-// b + gridDim.x, ... (each block stays on the XCD the one-block-per-workgroup
-// launch puts it on: gridDim.x is a multiple of 8). While block b's x
-// gathers, products, barrier and row sums run, block b + gridDim.x's aj / aa
-// pairs and row extents are already loading: they are issued after b's
-// gathers, so the waits for the gathers leave them outstanding (the vector
-// memory counter retires in order), and they are branch-free (clamped to the
-// block's last pair) so no join drains them. The per-row sums are
-// stream_block's, in PETSc's order: same bits.
-// PRED: gathers predicated on the pair being in the block (else clamped
-// lanes re-gather the last pair's columns).
-template <int T, int CAP, bool NT, class Op>
-struct PipeBlock {
-    static constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
-    i32x2 cv[ITERS];
-    f64x2 av[ITERS];
-    int32_t rs, re;
-    BlockDesc d;
-    // the block's pairs (clamped to its last pair) and this lane's row extents
-    __device__ __forceinline__ void load(const BlockDesc &bd, const int32_t *__restrict__ rai,
-                                         const int32_t *__restrict__ aj, const double *__restrict__ aa) {
-        d = bd;
-        const int t = threadIdx.x;
-        const int64_t kb = (int64_t)d.k0 & ~int64_t(1);
-        const int64_t kl = ((int64_t)d.k0 + max(d.nk, 1) - 1) & ~int64_t(1);
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it)
-            cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + min(kb + 2 * (int64_t)(t + it * T), kl)));
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it)
-            av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + min(kb + 2 * (int64_t)(t + it * T), kl)));
-        const int r = d.row0 + min(t, max(d.nrows, 1) - 1);
-        rs = rai[r];
-        re = rai[r + 1];
-    }
-};
-
-// One pipelined step: block `cur` (loaded) is gathered, multiplied and
-// summed while block `nxt` loads. prod holds CAP + 2 doubles: the last pair
-// is the trash slot the out-of-block lanes store to, so every store and
-// every gather is unconditional (a predicated store lets the compiler sink
-// the gathers into it, and the branch join then waits for all loads).
-template <int T, int CAP, bool NT, class Op>
-__device__ __forceinline__ void pipe_step(PipeBlock<T, CAP, NT, Op> &cur, PipeBlock<T, CAP, NT, Op> &nxt,
-                                          const BlockDesc &dn, int b, int nblk, int exact,
-                                          const int32_t *__restrict__ rai, const int32_t *__restrict__ aj,
-                                          const double *__restrict__ aa, const Op &op, double *dpart, double *prod) {
-    constexpr int ITERS = PipeBlock<T, CAP, NT, Op>::ITERS;
-    const int t = threadIdx.x;
-    const BlockDesc &d = cur.d;
-    const int64_t k0 = d.k0, k1 = (int64_t)d.k0 + d.nk;
-    const int64_t kb = k0 & ~int64_t(1);
-    f64x2 xv[ITERS];
-#pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-        xv[it].x = op.gx(cur.cv[it].x);
-        xv[it].y = op.gx(cur.cv[it].y);
-    }
-    nxt.load(dn, rai, aj, aa);
-#pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-        const int64_t k = kb + 2 * (int64_t)(t + it * T);
-        const int s0 = (k >= k0 && k < k1) ? (int)(k - k0) : CAP;
-        const int s1 = (k + 1 < k1) ? (int)(k + 1 - k0) : CAP + 1;
-        prod[s0] = cur.av[it].x * xv[it].x;
-        prod[s1] = cur.av[it].y * xv[it].y;
-    }
-    lds_barrier();
-    double dv[Op::kDots > 0 ? Op::kDots : 1] = {};
-    const int nr = d.nrows;
-    int L = 1;
-    if (!exact && d.nk > kSplitMinMean * nr) {
-        const int cap = min(64, T / max(nr, 1));
-        while (L * 2 <= cap) L *= 2;
-    }
-    if (L == 1) {
-        if (t < nr) {
-            const int o = d.row0 + t;
-            double s = op.seed(o);
-            if (d.nk > kBatchMinMean * nr) s = row_sum_seq(prod + (cur.rs - k0), cur.re - cur.rs, s);
-            else
-                for (int32_t k = cur.rs; k < cur.re; ++k) s += prod[k - k0];
-            op.put(o, s, dv);
-        }
-    } else {
-        const int g = t / L, j = t - g * L;
-        const bool own = g < nr;
-        const int r = d.row0 + min(g, nr - 1);
-        const int32_t grs = rai[r], gre = rai[r + 1];
-        double s = 0.0;
-        if (own)
-            for (int32_t k = grs + j; k < gre; k += L) s += prod[k - k0];
-        for (int off = L >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-        if (own && j == 0) op.put(r, Op::kSeeded ? op.seed(r) + s : s, dv);
-    }
-    if (Op::kDots > 0 && dpart) {
-#pragma unroll
-        for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
-            const double v = block_sum<T>(dv[q], prod);
-            if (t == 0) dpart[(int64_t)q * nblk + b] = v;
-        }
-    }
-    lds_barrier();  // the row sums have read prod before the next products
-}
-
-template <int T, int CAP, bool NT, class Op>
-__global__ __launch_bounds__(T) void k_spmv_pipe(const BlockDesc *__restrict__ blk, int nblk, int exact,
-                                                 const int32_t *__restrict__ rai, const int32_t *__restrict__ aj,
-                                                 const double *__restrict__ aa, Op op, double *dpart,
-                                                 const int *stop) {
-    __shared__ double prod[CAP + 2];
-    if ((stop ? *stop : 0) != 0) return;
-    int b = (int)blockIdx.x;
-    if (b >= nblk) return;
-    const int stride = (int)gridDim.x;
-    // two register sets, alternating (no copies: a copy of a register with a
-    // load in flight would wait for the load)
-    PipeBlock<T, CAP, NT, Op> A, B;
-    A.load(blk[b], rai, aj, aa);
-    for (;;) {
-        int bn = b + stride;
-        pipe_step(A, B, blk[bn < nblk ? bn : b], b, nblk, exact, rai, aj, aa, op, dpart, prod);
-        if (bn >= nblk) break;
-        b = bn;
-        bn = b + stride;
-        pipe_step(B, A, blk[bn < nblk ? bn : b], b, nblk, exact, rai, aj, aa, op, dpart, prod);
-        if (bn >= nblk) break;
-        b = bn;
-    }
-}
-
 // Row patterns (Tuning::patterns; short-row operands whose rows follow a
 // few column - row offset lists: stencils): the STREAM row blocks, but the
 // columns are not stored per entry. Each row has a pattern id (1 byte), the
@@ -1512,28 +1380,13 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // round trip for all eight gathers — measured 483.1 vs 469.8 us too,
     // profiles/r05/b/ab_buf.jsonl: the gathers' serialisation is not what
     // bounds this kernel)
-    if constexpr (RPT == 1) {  // two blocks in flight per workgroup (Tuning::pipe workgroups per CU)
-        static const int cus = [] {
-            int dev = 0, n = 0;
-            (void)hipGetDevice(&dev);
-            return hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && n > 0 ? n
-                                                                                                                : 256;
-        }();
-        const int pipe = P.tune.pipe;
-        if (pipe != 0 && !L.ridx) {
-            const int g = std::min<int>(P.n_blocks, pipe * cus);
-#define AIJHIP_PP(ADD, NTB)                                                                                  \
-    hipLaunchKernelGGL((k_spmv_pipe<T, CAP, NTB, OpMult<ADD>>), dim3(g), dim3(T), 0, s, P.d_blocks,              \
-                       P.n_blocks, (int)P.tune.exact, L.rai, A.d_aj, A.d_aa, OpMult<ADD>{x, z, y, dpart != nullptr}, \
-                       dpart, stop);                                                                                \
-    return
-            const bool nt = P.tune.nt == 1;
-            if (add) { if (nt) { AIJHIP_PP(true, true); } AIJHIP_PP(true, false); }
-            if (nt) { AIJHIP_PP(false, true); }
-            AIJHIP_PP(false, false);
-#undef AIJHIP_PP
-        }
-    }
+    // (two blocks in flight per workgroup — a persistent grid loading block
+    // b + grid's aj / aa while block b gathers, sums and stores, with
+    // alternating register sets and unconditional LDS stores so that no wait
+    // drains the prefetch — measured 540-630 us vs 469 us at 300^3, bit-exact:
+    // at 87 VGPRs it holds 4-5 waves per SIMD against 8, and the hardware's
+    // four resident workgroups per CU overlap each other's phases better,
+    // profiles/r05/l/ab_pipe.jsonl; withdrawn, option 16 reserved)
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
     // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)
     if (P.tune.nt == 1 && !L.ridx) {

@@ -601,80 +601,100 @@ __global__ void k_mis_number(int32_t m, const int32_t *__restrict__ parent, cons
 
 namespace aijhip_gamg {
 
+// MIS scratch: stream-ordered allocations on the rounds' stream (hipFree
+// would wait for the whole device, the emax job's and the handle jobs' work
+// included)
+template <class T>
+hipError_t salloc(T **p, int64_t n, hipStream_t s) {
+    return hipMallocAsync(reinterpret_cast<void **>(p), sizeof(T) * (size_t)std::max<int64_t>(n, 1), s);
+}
+
 hipError_t aggregate_mis_device(int32_t m, const int32_t *si, const int32_t *sj, bool square, int32_t level,
                                 int32_t *agg, int32_t *na, int32_t *rounds) {
     *na = 0;
     *rounds = 0;
     if (m == 0) return hipSuccess;
+    // The rounds run on set-up stream slot 0 (the greedy sweep's), after the
+    // null stream's strength graph (an event, no host wait): round 5 measured
+    // a 15 ms stall of the level-1 rounds on the null stream while the handle
+    // job built P_0's plan (its copies and syncs go through the null stream).
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    hipStream_t ms = e == hipSuccess ? aijhip_gamg::setup_stream(dev, 0) : nullptr;
+    if (!ms) return e == hipSuccess ? hipErrorInvalidValue : e;
+    hipEvent_t ready = nullptr;
+    if ((e = hipEventCreateWithFlags(&ready, hipEventDisableTiming)) != hipSuccess) return e;
+    if ((e = hipEventRecord(ready, nullptr)) == hipSuccess) e = hipStreamWaitEvent(ms, ready, 0);
     mis_state_t *state = nullptr;
     uint32_t *hk = nullptr;
     uint64_t *amin = nullptr;
-    int32_t *parent = nullptr, *flag = nullptr, *cidx = nullptr;
-    unsigned long long *left = nullptr, *h_left = nullptr;
+    int32_t *parent = nullptr, *flag = nullptr, *cidx = nullptr, *tmp = nullptr;
+    unsigned long long *left = nullptr, *h_ctl = nullptr;  // h_ctl: [0] the count, [1] the aggregates
     unsigned *wcount = nullptr;
     const unsigned g = blocks_for(m, 256);
-    hipError_t e = dalloc(&state, m);
-    if (e == hipSuccess) e = dalloc(&hk, m);
-    if (e == hipSuccess) e = dalloc(&amin, m);
-    if (e == hipSuccess) e = dalloc(&left, 1);
-    if (e == hipSuccess) e = dalloc(&wcount, g);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&h_left), sizeof(unsigned long long));
+    if (e == hipSuccess) e = salloc(&state, m, ms);
+    if (e == hipSuccess) e = salloc(&hk, m, ms);
+    if (e == hipSuccess) e = salloc(&amin, m, ms);
+    if (e == hipSuccess) e = salloc(&left, 1, ms);
+    if (e == hipSuccess) e = salloc(&wcount, g, ms);
+    // pinned, one per host thread and never freed (hipHostFree waits for the device)
+    static thread_local unsigned long long *t_ctl = nullptr;
+    if (e == hipSuccess && !t_ctl) e = hipHostMalloc(reinterpret_cast<void **>(&t_ctl), 2 * sizeof(unsigned long long));
+    h_ctl = t_ctl;
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mis_init, dim3(g), dim3(256), 0, nullptr, m, level, si, state, hk);
+        hipLaunchKernelGGL(k_mis_init, dim3(g), dim3(256), 0, ms, m, level, si, state, hk);
         e = hipGetLastError();
     }
     // Every round decides at least the lowest-key undecided node, so m rounds
     // always suffice. They go out in batches of kBatch with one count read
     // per batch (a round past the last is a no-op), the count through pinned
-    // memory on the null stream's own copy, so the read waits for the rounds
-    // alone.
+    // memory.
     static const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     constexpr int32_t kBatch = 4;
     for (int32_t r0 = 0; e == hipSuccess && r0 < m; r0 += kBatch) {
         const auto t0 = std::chrono::steady_clock::now();
         for (int32_t r = r0; r < r0 + kBatch && e == hipSuccess; ++r) {
-            hipLaunchKernelGGL(k_mis_closed_min, dim3(g), dim3(256), 0, nullptr, m, si, sj, hk, state, false, amin);
-            hipLaunchKernelGGL(k_mis_decide, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, hk, amin, state,
-                               wcount);
+            hipLaunchKernelGGL(k_mis_closed_min, dim3(g), dim3(256), 0, ms, m, si, sj, hk, state, false, amin);
+            hipLaunchKernelGGL(k_mis_decide, dim3(g), dim3(256), 0, ms, m, si, sj, square, hk, amin, state, wcount);
             e = hipGetLastError();
         }
         if (e == hipSuccess) {
-            hipLaunchKernelGGL(k_mis_total, dim3(1), dim3(1024), 0, nullptr, wcount, (int32_t)g, left);
+            hipLaunchKernelGGL(k_mis_total, dim3(1), dim3(1024), 0, ms, wcount, (int32_t)g, left);
             e = hipGetLastError();
         }
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(h_left, left, sizeof(unsigned long long), hipMemcpyDeviceToHost, nullptr);
-        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+        if (e == hipSuccess) e = hipMemcpyAsync(h_ctl, left, sizeof(unsigned long long), hipMemcpyDeviceToHost, ms);
+        if (e == hipSuccess) e = hipStreamSynchronize(ms);
         if (e != hipSuccess) break;
         *rounds = r0 + kBatch;
         if (log)
-            std::fprintf(stderr, "  MIS rounds %d-%d: %llu undecided after, %.3f ms\n", r0, r0 + kBatch - 1, *h_left,
+            std::fprintf(stderr, "  MIS rounds %d-%d: %llu undecided after, %.3f ms\n", r0, r0 + kBatch - 1, h_ctl[0],
                          std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
-        if (*h_left == 0) break;
+        if (h_ctl[0] == 0) break;
     }
-    if (e == hipSuccess) e = dalloc(&parent, m);
-    if (e == hipSuccess) e = dalloc(&flag, m);
-    if (e == hipSuccess) e = dalloc(&cidx, m);
+    if (e == hipSuccess) e = salloc(&parent, m, ms);
+    if (e == hipSuccess) e = salloc(&flag, m, ms);
+    if (e == hipSuccess) e = salloc(&cidx, m, ms);
+    if (e == hipSuccess) e = salloc(&tmp, aijhip_dscan::scan_tmp_elems(m), ms);
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mis_closed_min, dim3(g), dim3(256), 0, nullptr, m, si, sj, hk, state, true, amin);
-        hipLaunchKernelGGL(k_mis_parent, dim3(g), dim3(256), 0, nullptr, m, si, sj, square, amin, state, parent,
-                           flag);
+        hipLaunchKernelGGL(k_mis_closed_min, dim3(g), dim3(256), 0, ms, m, si, sj, hk, state, true, amin);
+        hipLaunchKernelGGL(k_mis_parent, dim3(g), dim3(256), 0, ms, m, si, sj, square, amin, state, parent, flag);
         e = hipGetLastError();
     }
-    if (e == hipSuccess) e = exclusive_sum(flag, cidx, m, nullptr);
+    if (e == hipSuccess) e = aijhip_dscan::exclusive_scan(flag, cidx, (int64_t)m, tmp, ms);
     if (e == hipSuccess) {
-        int32_t lc = 0, lf = 0;
-        e = hipMemcpy(&lc, cidx + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
-        if (e == hipSuccess) e = hipMemcpy(&lf, flag + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost);
-        *na = lc + lf;
-    }
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(k_mis_number, dim3(g), dim3(256), 0, nullptr, m, parent, cidx, agg);
+        hipLaunchKernelGGL(k_mis_number, dim3(g), dim3(256), 0, ms, m, parent, cidx, agg);
         e = hipGetLastError();
     }
-    if (h_left) (void)hipHostFree(h_left);
-    hipFree(state); hipFree(hk); hipFree(amin); hipFree(parent); hipFree(flag); hipFree(cidx); hipFree(left);
-    hipFree(wcount);
+    int32_t *h_na = reinterpret_cast<int32_t *>(h_ctl + 1);  // [0] the last scan value, [1] the last flag
+    if (e == hipSuccess) e = hipMemcpyAsync(h_na, cidx + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost, ms);
+    if (e == hipSuccess) e = hipMemcpyAsync(h_na + 1, flag + (m - 1), sizeof(int32_t), hipMemcpyDeviceToHost, ms);
+    for (void *q : {(void *)state, (void *)hk, (void *)amin, (void *)parent, (void *)flag, (void *)cidx,
+                    (void *)tmp, (void *)left, (void *)wcount})
+        if (q) (void)hipFreeAsync(q, ms);
+    const hipError_t es = hipStreamSynchronize(ms);  // agg and the count are ready; the scratch went back
+    if (e == hipSuccess) e = es;
+    if (e == hipSuccess) *na = h_na[0] + h_na[1];
+    (void)hipEventDestroy(ready);
     return e;
 }
 

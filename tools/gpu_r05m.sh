@@ -1,16 +1,13 @@
 #!/bin/bash
 # Round 5: the MIS set-up after the per-workgroup round counts, and the
-# two-blocks-in-flight A/B on the headline operand.
+# (r05m: the rounds on their own stream).
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$ROOT/gpurun_out/r05l
+OUT=$ROOT/gpurun_out/r05m
 mkdir -p "$OUT"
 cd "$ROOT" || exit 1
 export TMPDIR=/tmp
 export GPU_MAX_HW_QUEUES=8
-timeout -k 10 300 python -u tools/ab_pipe.py > "$OUT/ab_pipe.jsonl" 2> "$OUT/ab_pipe.err" \
-    || { tail -30 "$OUT/ab_pipe.err"; exit 1; }
-cat "$OUT/ab_pipe.jsonl"
 timeout -k 10 300 python -u -m pytest tests/test_gamg.py -x -q -m gpu -k "mis" --timeout 300 --timeout-method thread \
     > "$OUT/pytest.log" 2>&1 || { tail -20 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
