@@ -10,14 +10,16 @@
  * aggregation; tentative prolongator from the near-null space (constant
  * vector on the finest level; the QR factors carry it down); one Jacobi
  * smoothing step P = (I - 1.4/emax D^-1 A) P0 (PCGAMGOptProlongator_AGG's
- * alpha = -1.4/emax); Galerkin coarse operator Pt A P. Aggregation: a
- * deterministic greedy pass in natural order (coarsen 0, the default), or
- * PETSc 3.7's own agg coarsening restated (coarsen 1: a maximal independent
- * set of the squared graph in a random order, aggregates smoothed — agg.c
- * PCGAMGCoarsen_AGG / smoothAggs, mis.c; PETSc's random stream is not
- * reproduced), with emax from a power iteration (eig_ksp 0) or from CG's
- * Lanczos tridiagonal as PCGAMGOptProlongator_AGG does (eig_ksp 1). GAMG
- * iteration parity with PETSc is unpinned either way (PETSc is absent).
+ * alpha = -1.4/emax); Galerkin coarse operator Pt A P. Aggregation:
+ * PETSc 3.7's own agg coarsening restated (coarsen 1, the default since
+ * round 5: a maximal independent set of the squared graph in a hashed random
+ * order, aggregates smoothed — agg.c PCGAMGCoarsen_AGG / smoothAggs, mis.c;
+ * PETSc's random stream is not reproduced) or a deterministic greedy pass in
+ * natural order (coarsen 0, the default through round 4), with emax from
+ * CG's Lanczos tridiagonal as PCGAMGOptProlongator_AGG does (eig_ksp 1, the
+ * default) or a power iteration (eig_ksp 0). GAMG iteration parity with
+ * PETSc is unpinned either way (PETSc is absent). The distributed set-up
+ * (aijhip_gamg_mpi) aggregates greedily.
  * The solve-phase V-cycle runs on the device inside aijhip_ksp
  * (AIJHIP_PC_GAMG), whose set-up builds the large levels on the device
  * (device_min_rows) with results identical to aijhip_gamg_build_host.
@@ -47,12 +49,12 @@ typedef struct aijhip_gamg_params {
                               * 0 = every level on the device, INT32_MAX = all
                               * on the host. Same hierarchy either way.     */
     /* ABI 3: */
-    int32_t coarsen;         /* 0: greedy aggregation (natural order);
-                              * 1: PETSc 3.7 agg's MIS (see above)          */
+    int32_t coarsen;         /* 1 (default): PETSc 3.7 agg's MIS (see above);
+                              * 0: greedy aggregation (natural order)       */
     int32_t square_graph;    /* -pc_gamg_square_graph (1): coarsen 1 squares
                               * the graph on this many levels from the finest */
-    int32_t eig_ksp;         /* emax(D^-1 A): 0 power iteration; 1 CG (Lanczos),
-                              * PETSc's estimate                             */
+    int32_t eig_ksp;         /* emax(D^-1 A): 1 (default) CG's Lanczos estimate,
+                              * PETSc's; 0 power iteration                   */
     int32_t pad0;
 } aijhip_gamg_params_t;
 

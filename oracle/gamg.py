@@ -280,11 +280,11 @@ def estimate_emax(A, dinv, its):
 
 
 def build(A, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smooth_scale=1.4, eig_its=10,
-          coarsen=0, square_graph=1, eig_ksp=0):
+          coarsen=1, square_graph=1, eig_ksp=1):
     """Returns a list of levels: dict(A, P, agg, emax) (P/agg absent on the
-    coarsest). coarsen 0: greedy aggregation in natural order; 1: PETSc's
-    MIS (squared graph on the first square_graph levels). eig_ksp 0: power
-    iteration; 1: CG Lanczos (PETSc's estimate)."""
+    coarsest). coarsen 1 (default): PETSc's MIS (squared graph on the first
+    square_graph levels); 0: greedy aggregation in natural order. eig_ksp 1
+    (default): CG Lanczos (PETSc's estimate); 0: power iteration."""
     A = sp.csr_matrix(A)
     levels = []
     B = np.ones(A.shape[0])

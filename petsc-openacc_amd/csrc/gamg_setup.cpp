@@ -615,9 +615,9 @@ int aijhip_gamg_params_default(aijhip_gamg_params_t *p) {
     p->eig_its = 10;
     p->threads = 0;
     p->device_min_rows = 20000;
-    p->coarsen = 0;
+    p->coarsen = 1;  // PETSc 3.7 agg's MIS (round 5: faster to solution than greedy)
     p->square_graph = 1;
-    p->eig_ksp = 0;
+    p->eig_ksp = 1;
     p->pad0 = 0;
     return AIJHIP_OK;
 }

@@ -7,7 +7,8 @@
 //            [-ksp_rtol R] [-ksp_atol A] [-ksp_max_it K] [-pc_type jacobi|none|gamg]
 //            [-ksp_norm_type preconditioned|unpreconditioned|natural]
 //            [-pc_gamg_threshold T] [-pc_gamg_agg_nsmooths S]
-//            [-pc_gamg_coarse_eq_limit C] [-pc_mg_levels L] [-aijhip_host_assembly]
+//            [-pc_gamg_coarse_eq_limit C] [-pc_mg_levels L] [-pc_gamg_square_graph G]
+//            [-aijhip_gamg_coarsen 1|0] [-aijhip_gamg_eig_ksp 1|0] [-aijhip_host_assembly]
 //
 // Options come from the command line and from a PETSc options file
 // (`-key value` per line, '#' comments; PetscOptionsInsertFile,
@@ -123,6 +124,11 @@ int main(int argc, char **argv) {
         gp.nsmooths = (int32_t)geti("-pc_gamg_agg_nsmooths", gp.nsmooths);
         gp.coarse_eq_limit = (int32_t)geti("-pc_gamg_coarse_eq_limit", gp.coarse_eq_limit);
         gp.max_levels = (int32_t)geti("-pc_mg_levels", gp.max_levels);
+        gp.square_graph = (int32_t)geti("-pc_gamg_square_graph", gp.square_graph);
+        // this build's extensions: 0 selects the greedy aggregation / the
+        // power-iteration emax of rounds 1-4 (PETSc has no such switch)
+        gp.coarsen = (int32_t)geti("-aijhip_gamg_coarsen", gp.coarsen);
+        gp.eig_ksp = (int32_t)geti("-aijhip_gamg_eig_ksp", gp.eig_ksp);
     }
     const std::string nts = gets("-ksp_norm_type", "preconditioned");
     const int normtype = nts == "unpreconditioned" ? AIJHIP_KSP_NORM_UNPRECONDITIONED

@@ -186,6 +186,13 @@ static PetscErrorCode KSPSetUp_CGHIP(KSP ksp)
     if (set) gp.coarse_eq_limit = (int32_t)iv;
     ierr = PetscOptionsGetInt(NULL, NULL, "-pc_mg_levels", &iv, &set);CHKERRQ(ierr);
     if (set) gp.max_levels = (int32_t)iv;
+    ierr = PetscOptionsGetInt(NULL, NULL, "-pc_gamg_square_graph", &iv, &set);CHKERRQ(ierr);
+    if (set) gp.square_graph = (int32_t)iv;
+    /* this library's extensions (0: the greedy aggregation / power-iteration emax) */
+    ierr = PetscOptionsGetInt(NULL, NULL, "-aijhip_gamg_coarsen", &iv, &set);CHKERRQ(ierr);
+    if (set) gp.coarsen = (int32_t)iv;
+    ierr = PetscOptionsGetInt(NULL, NULL, "-aijhip_gamg_eig_ksp", &iv, &set);CHKERRQ(ierr);
+    if (set) gp.eig_ksp = (int32_t)iv;
     rc = aijhip_ksp_set_gamg_params(c->k, &gp);
   }
   switch (ksp->normtype) {

@@ -37,8 +37,8 @@ def test_host_hierarchy_matches_oracle_bitwise(pkg, dims):
     ai, aj, aa = pkg.poisson_csr(*dims)
     m = len(ai) - 1
     A = sp.csr_matrix((aa, aj, ai), shape=(m, m))
-    lv = G.build_host(ai, aj, aa, coarse_eq_limit=20)
-    ol = ogamg.build(A, coarse_eq_limit=20)
+    lv = G.build_host(ai, aj, aa, coarse_eq_limit=20, coarsen=0, eig_ksp=0)  # greedy + power iteration
+    ol = ogamg.build(A, coarse_eq_limit=20, coarsen=0, eig_ksp=0)
     assert len(lv) == len(ol) >= 2
     for l in range(len(lv) - 1):
         assert np.array_equal(lv[l]["agg"], ol[l]["agg"])

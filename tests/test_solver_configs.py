@@ -24,9 +24,12 @@ from oracle import gamg as ogamg
 from oracle import ksp_cg
 
 TOL = dict(rtol=1e-14, atol=1e-12, max_it=10000)  # PETSc_SolverOptions_GAMG.info:2-4
-# Iteration counts of this build's CG+GAMG at the BASELINE sizes (measured on
-# MI355X, profiles/r02/); +-1 allows a reordered dot at the tolerance boundary.
-PINNED_ITS = {300: 57, 100: 47}
+# Iteration counts of this build's CG+GAMG at the BASELINE sizes with the
+# default hierarchy (PETSc 3.7 agg's MIS + CG emax since round 5: 53 at 300^3
+# measured on MI355X, profiles/r05/m/; 52 at 100^3 from the oracle CG over the
+# host hierarchy; the greedy hierarchy took 57 and 47); +-1 allows a
+# reordered dot at the tolerance boundary.
+PINNED_ITS = {300: 53, 100: 52}
 # Linf(x - exact) <= C_H2 * h^2: the 7-point scheme is second order; the
 # measured constant is ~6.6 at 300^3 and ~6.6 at 100^3.
 C_H2 = 8.0
@@ -93,7 +96,7 @@ def test_gpu_cg_gamg_300_configs2(pkg, coracle):
     assert err <= C_H2 / (N * N), err
     assert all(p == "device" for p, _ in path[:2]), path  # the two big levels are built on the GPU
     # the V-cycle honours the device stop flag: iterations go out in batches
-    # of 8 between host polls (57 iterations -> 8 polls + the final read)
+    # of 8 between host polls (53 iterations -> 7 polls + the final read)
     assert syncs <= 10, syncs
 
 
