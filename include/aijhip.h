@@ -172,13 +172,16 @@ enum {
                                        with scattered gathers (the geometry-1
                                        operands), plain otherwise; 0 plain;
                                        1 non-temporal aa/aj loads            */
-    AIJHIP_OPT_EXACT = 6,           /* 1: every row summed sequentially in
-                                       PETSc's order. Default 0: row blocks
-                                       whose mean row length exceeds 128 use
-                                       2..64 lanes per row (reordered sum,
-                                       within the fp64 bound); shorter rows
-                                       (7-pt Poisson, FEM rows) are bit-exact
-                                       either way                           */
+    AIJHIP_OPT_EXACT = 6,           /* 1: every row of the row blocks summed
+                                       sequentially in PETSc's order. Default
+                                       0: row blocks whose mean row length
+                                       exceeds 128 use 2..64 lanes per row
+                                       (reordered sum, within the fp64
+                                       bound); shorter rows (7-pt Poisson,
+                                       FEM rows) are bit-exact either way.
+                                       Rows longer than a block's entry cap
+                                       are split into segments either way
+                                       (deterministic, not PETSc's order)   */
     AIJHIP_OPT_LONG_XCD = 8,        /* 1 (default): segments of long rows are
                                        launched so that XCD q (slot % 8)
                                        reduces those whose columns lie in the
