@@ -8,10 +8,14 @@ computed globally:
 
   - rank r owns rows [starts[r], starts[r+1]) of every level;
   - aggregates are formed on each rank's diagonal block with oracle/gamg.py's
-    greedy aggregation, numbered rank by rank (coarse rows of rank r =
+    aggregation — PETSc's MIS (coarsen 1, the default: the block's graph,
+    squared on the first square_graph levels, keys at local indices) or the
+    greedy pass (coarsen 0) — numbered rank by rank (coarse rows of rank r =
     [cstarts[r], cstarts[r+1]));
-  - emax by power iteration on the global D^-1 A from oracle/gamg.py's start
-    vector at global indices;
+  - emax by CG's Lanczos estimate (eig_ksp 1, the default) or the power
+    iteration (0) on the global D^-1 A from oracle/gamg.py's start vector at
+    global indices (the device sums its dots rank by rank: equal to
+    rounding);
   - P0, P = P0 - 1.4/emax D^-1 A P0 and A_c = P^T A P over the whole operator;
   - the hierarchy stops where the single-GPU one does, with global counts.
 
@@ -28,10 +32,11 @@ from oracle import gamg as og
 
 
 def build(A, starts, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=1, smooth_scale=1.4, eig_its=10,
-          B=None):
+          B=None, coarsen=1, square_graph=1, eig_ksp=1, level0=0):
     """A: global operator; starts: row ownership (len = ranks + 1); B: the
     near-null space (ones). Returns a list of levels dict(A, P, starts, emax,
-    agg, Bc) in oracle/gamg.py's format (vcycle-compatible)."""
+    agg, Bc) in oracle/gamg.py's format (vcycle-compatible). level0: the
+    level index of A (the MIS keys' level)."""
     A = sp.csr_matrix(A)
     starts = np.asarray(starts, dtype=np.int64)
     levels = []
@@ -45,18 +50,27 @@ def build(A, starts, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=
             Ad = sp.csr_matrix(A[lo:hi, lo:hi])
             Ad.sort_indices()
             S = og.strength_graph(Ad, d[lo:hi], threshold)
-            agg, na = og.aggregate(Ad, S)
+            lvl = level0 + len(levels)
+            if coarsen == 1:
+                agg, na = og.aggregate_mis(S, lvl < square_graph, og.mis_keys(hi - lo, lvl))
+            else:
+                agg, na = og.aggregate(Ad, S)
             aggs.append(agg)
             nas.append(na)
         cstarts = np.concatenate([[0], np.cumsum(nas)]).astype(np.int64)
         NA = int(cstarts[-1])
         if NA == 0 or NA >= A.shape[0]:
             break
-        agg = np.concatenate([a + cstarts[r] for r, a in enumerate(aggs)])
-        emax = og.estimate_emax(A, dinv, eig_its) if nsmooths > 0 else 1.0
-        Bc = np.sqrt(np.bincount(agg, weights=B * B, minlength=NA))
-        p0 = np.where(Bc[agg] > 0, B / np.where(Bc[agg] > 0, Bc[agg], 1.0), 0.0)
-        P0 = sp.csr_matrix((p0, (np.arange(A.shape[0]), agg)), shape=(A.shape[0], NA))
+        agg = np.concatenate([np.where(a >= 0, a + cstarts[r], -1) for r, a in enumerate(aggs)])
+        if nsmooths > 0:
+            emax = og.estimate_emax_cg(A, dinv, eig_its) if eig_ksp == 1 else og.estimate_emax(A, dinv, eig_its)
+        else:
+            emax = 1.0
+        kept = agg >= 0  # MIS removes singletons: no aggregate, an empty row of P0
+        Bc = np.sqrt(np.bincount(agg[kept], weights=(B * B)[kept], minlength=NA))
+        aggk = np.where(kept, agg, 0)
+        p0 = np.where(kept & (Bc[aggk] > 0), B / np.where(Bc[aggk] > 0, Bc[aggk], 1.0), 0.0)
+        P0 = sp.csr_matrix((p0[kept], (np.arange(A.shape[0])[kept], agg[kept])), shape=(A.shape[0], NA))
         P = P0
         if nsmooths > 0:
             P = (-smooth_scale / emax) * (sp.diags(dinv) @ (A @ P0)) + P0

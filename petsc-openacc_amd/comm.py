@@ -306,10 +306,7 @@ class KSPCGMPINative:
         _pkg._check(L.aijhip_kspmpi_set_pc_type(self._h, K.PC_TYPES[pc]))
         if gamg:
             G = importlib.import_module("petsc-openacc_amd.gamg")
-            # the distributed hierarchy (pc "gamg") aggregates greedily unless
-            # asked otherwise (which it refuses: DESIGN.md §6)
-            base = dict(coarsen=0, eig_ksp=0) if pc == "gamg" else {}
-            self._gp = G.default_params(**{**base, **gamg})
+            self._gp = G.default_params(**gamg)
             _pkg._check(L.aijhip_kspmpi_set_gamg_params(self._h, ctypes.byref(self._gp)))
         _pkg._check(L.aijhip_kspmpi_set_norm_type(self._h, K.NORM_TYPES[norm]))
         _pkg._check(L.aijhip_kspmpi_set_poll_interval(self._h, int(poll)))

@@ -10,10 +10,15 @@
 //
 //   aggregates   local to each rank (PETSc's agg GAMG keeps aggregates on
 //                their owner too): the single-GPU steps (gamg_device.hip
-//                aggregate_level) on the diagonal block A_d;
-//   emax         power iteration on the distributed D^-1 A (MatMult_MPIAIJ +
-//                all-reduced norms), from the single-GPU start vector taken at
-//                global indices;
+//                aggregate_level) on the diagonal block A_d — PETSc's MIS
+//                (coarsen 1, the default; the graph of A_d, keys at local
+//                indices, so roots on either side of a rank boundary may
+//                be neighbours: PETSc's MIS also exchanges ghost states) or
+//                the greedy pass (coarsen 0);
+//   emax         CG's Lanczos estimate (eig_ksp 1, the default) or a power
+//                iteration on the distributed D^-1 A (MatMult_MPIAIJ +
+//                all-reduced dots), from the single-GPU start vector taken
+//                at global indices;
 //   P            = P0 + alpha D^-1 (A P0) over the whole operator: A_ext = [A_d |
 //                A_o] times P0 extended by its ghost rows (aggregate id and
 //                value of each ghost fine node, exchanged through the halo);
@@ -87,6 +92,44 @@ __global__ void k_sumsq_blocks(int64_t n, const double *__restrict__ a, double *
     part[q] = s;
 }
 
+__global__ void k_dot_blocks(int64_t n, const double *__restrict__ a, const double *__restrict__ b, double *part) {
+    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i0 = q * kDotBlock;
+    if (i0 >= n) return;
+    const int64_t e = min(n, i0 + kDotBlock);
+    double s = 0.0;
+    for (int64_t i = i0; i < e; ++i) s += a[i] * b[i];
+    part[q] = s;
+}
+
+// CG's emax estimate (gamg_setup.cpp estimate_emax_cg) on the distributed
+// operator: the start b at global indices (the power iteration's), r = b,
+// z = D^-1 r, p = z; r -= a w, z = D^-1 r; p = z + b p
+__global__ void k_cgest_start_off(int32_t m, int64_t off, const double *__restrict__ dinv, double *r, double *z,
+                                  double *p) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double v = 2.0 * ((double)(mix64d(0x5EEDULL + (uint64_t)(off + i + 1) * 0x9E3779B97F4A7C15ULL) >> 11) *
+                            (1.0 / 9007199254740992.0)) - 1.0;
+    r[i] = v;
+    z[i] = dinv[i] * v;
+    p[i] = z[i];
+}
+
+__global__ void k_cgest_update(int32_t m, double a, const double *__restrict__ w, const double *__restrict__ dinv,
+                               double *r, double *z) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double ri = r[i] - a * w[i];
+    r[i] = ri;
+    z[i] = dinv[i] * ri;
+}
+
+__global__ void k_cgest_dir(int32_t m, double b, const double *__restrict__ z, double *p) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) p[i] = z[i] + b * p[i];
+}
+
 __global__ void k_scale_by(int32_t m, const double *__restrict__ d, double *w) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < m) w[i] = d[i] * w[i];
@@ -97,9 +140,16 @@ __global__ void k_divide(int32_t m, const double *w, double nw, double *v) {
     if (i < m) v[i] = w[i] / nw;
 }
 
+// global coarse id of each node's aggregate; -1 for a node MIS removed
 __global__ void k_coarse_gid(int32_t m, int64_t off, const int32_t *__restrict__ agg, double *out) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) out[i] = (double)(off + agg[i]);
+    if (i < m) out[i] = agg[i] < 0 ? -1.0 : (double)(off + agg[i]);
+}
+
+__global__ void k_count_negative(int32_t m, const int32_t *__restrict__ agg, unsigned long long *n) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long c = __popcll(__ballot(i < m && agg[i] < 0));
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(n, c);
 }
 
 __global__ void k_iota32(int32_t n, int32_t *v) {
@@ -569,6 +619,25 @@ int halo_values(aijhip_mpiaij *M, const double *d_x, std::vector<double> &out) {
 }
 
 // sqrt of the sum over all ranks of the 256-blocked local sums of squares
+// sum a . b over the ranks: each rank's 256-entry block sums left to right,
+// then the ranks' sums (the same order as global_norm)
+int global_dot(aijhip_comm *C, const double *d_a, const double *d_b, int32_t m, double *d_part, double *out) {
+    const int64_t nb = (m + kDotBlock - 1) / kDotBlock;
+    std::vector<double> h((size_t)nb);
+    hipError_t e;
+    if (nb > 0) {
+        hipLaunchKernelGGL(k_dot_blocks, dim3(nblk(nb, 64)), dim3(64), 0, nullptr, (int64_t)m, d_a, d_b, d_part);
+        if ((e = hipMemcpy(h.data(), d_part, sizeof(double) * (size_t)nb, hipMemcpyDeviceToHost)) != hipSuccess)
+            return gerr(e, "dot");
+    }
+    double s = 0.0;
+    for (int64_t q = 0; q < nb; ++q) s += h[q];
+    int rc = aijhip_mpi::comm_allreduce_host(C, &s, 1);
+    if (rc) return rc;
+    *out = s;
+    return AIJHIP_OK;
+}
+
 int global_norm(aijhip_comm *C, const double *d_v, int32_t m, double *d_part, double *out) {
     const int64_t nb = (m + kDotBlock - 1) / kDotBlock;
     std::vector<double> h((size_t)nb);
@@ -688,9 +757,6 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
     aijhip_comm *C = M0->comm;
     if (M0->halo != AIJHIP_HALO_P2P)
         return mfail(AIJHIP_ERR_ARG, "distributed GAMG: the operator needs the p2p halo (AIJHIP_HALO_P2P)");
-    if (p.coarsen != 0 || p.eig_ksp != 0)  // (every rank refuses alike: the parameters are the caller's, collective)
-        return mfail(AIJHIP_ERR_ARG, "distributed GAMG: coarsen 1 / eig_ksp 1 (PETSc's MIS and CG estimate) are "
-                                     "single-GPU options");
     const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
     auto t0 = std::chrono::steady_clock::now();
     auto lap = [&](size_t l, const char *what) {
@@ -770,6 +836,44 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
                                    L.Ad->d_aa, dinv_e);
             emax_th = std::thread([&, dev = L.Ad->device]() {
                 (void)hipSetDevice(dev);
+                if (p.eig_ksp == 1) {  // CG's Lanczos estimate (PETSc's; gamg_setup.cpp estimate_emax_cg)
+                    double *r = nullptr, *z = nullptr, *pv = nullptr, *w = nullptr, *part = nullptr;
+                    hipError_t x;
+                    if ((x = dalloc(&r, m)) != hipSuccess || (x = dalloc(&z, m)) != hipSuccess ||
+                        (x = dalloc(&pv, m)) != hipSuccess || (x = dalloc(&w, m)) != hipSuccess ||
+                        (x = dalloc(&part, (m + kDotBlock - 1) / kDotBlock)) != hipSuccess)
+                        emax_rc = gerr(x, "alloc");
+                    std::vector<double> alpha, beta;
+                    double rz = 0.0;
+                    if (!emax_rc) {
+                        if (m > 0)
+                            hipLaunchKernelGGL(k_cgest_start_off, dim3(nblk(m)), dim3(256), 0, nullptr, m, L.rstart,
+                                               dinv_e, r, z, pv);
+                        emax_rc = global_dot(C, z, r, m, part, &rz);
+                    }
+                    for (int it = 0; !emax_rc && it < p.eig_its; ++it) {
+                        if ((emax_rc = aijhip_mpi::mpiaij_apply(L.op, pv, w, nullptr, nullptr, nullptr, nullptr, false)))
+                            break;
+                        double pw = 0.0;
+                        if ((emax_rc = global_dot(C, pv, w, m, part, &pw))) break;
+                        if (!(pw != 0.0 && rz != 0.0)) break;
+                        const double a = rz / pw;
+                        alpha.push_back(a);
+                        if (m > 0)
+                            hipLaunchKernelGGL(k_cgest_update, dim3(nblk(m)), dim3(256), 0, nullptr, m, a, w, dinv_e, r, z);
+                        double rzn = 0.0;
+                        if ((emax_rc = global_dot(C, z, r, m, part, &rzn))) break;
+                        const double b = rzn / rz;
+                        beta.push_back(b);
+                        if (m > 0) hipLaunchKernelGGL(k_cgest_dir, dim3(nblk(m)), dim3(256), 0, nullptr, m, b, z, pv);
+                        rz = rzn;
+                    }
+                    (void)hipStreamSynchronize(nullptr);
+                    if (!emax_rc && !alpha.empty()) emax = aijhip_gamg::lanczos_emax(alpha, beta);
+                    hipFree(r); hipFree(z); hipFree(pv); hipFree(w); hipFree(part);
+                    if (emax_rc) emax_err = aijhip_last_error();
+                    return;
+                }
                 double *v = nullptr, *w = nullptr, *part = nullptr;
                 hipError_t x;
                 if ((x = dalloc(&v, m)) != hipSuccess || (x = dalloc(&w, m)) != hipSuccess ||
@@ -851,7 +955,11 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
         const int32_t ng = (int32_t)L.ghost_gid.size();
         // extended coarse numbering E1: own aggregates, then the off-rank ones of the ghosts (sorted)
         std::vector<int64_t> e1_off;
-        for (int32_t s = 0; s < ng; ++s) e1_off.push_back((int64_t)g_agg[s]);
+        bool ghost_removed = false;  // a ghost fine node MIS removed (no aggregate)
+        for (int32_t s = 0; s < ng; ++s) {
+            if (g_agg[s] < 0) ghost_removed = true;
+            else e1_off.push_back((int64_t)g_agg[s]);
+        }
         std::sort(e1_off.begin(), e1_off.end());
         e1_off.erase(std::unique(e1_off.begin(), e1_off.end()), e1_off.end());
         auto e1_id = [&](int64_t gidc) -> int32_t {
@@ -875,8 +983,48 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
             Aext.n = m + ng;
         }
         lap(l, "A_ext");
-        // P0 extended by the ghost rows: rows m + ng, columns E1
-        if (!rc) {
+        // P0 extended by the ghost rows: rows m + ng, columns E1. A node MIS
+        // removed (agg -1, the single-GPU set-up's empty P0 row) has no
+        // entry: such levels (rare: isolated rows, e.g. the reference point
+        // row 0 at level 0) are compacted on the host; the others keep one
+        // entry per row, built on the device
+        bool local_removed = false;
+        if (!rc && m > 0) {
+            unsigned long long *d_n = nullptr, h_n = 0;
+            if ((e = dalloc(&d_n, 1)) != hipSuccess || (e = hipMemset(d_n, 0, sizeof(h_n))) != hipSuccess) {
+                rc = gerr(e, "alloc");
+            } else {
+                hipLaunchKernelGGL(k_count_negative, dim3(nblk(m)), dim3(256), 0, nullptr, m, d_agg, d_n);
+                if ((e = hipMemcpy(&h_n, d_n, sizeof(h_n), hipMemcpyDeviceToHost)) != hipSuccess) rc = gerr(e, "count");
+            }
+            hipFree(d_n);
+            local_removed = h_n > 0;
+        }
+        if (!rc && (local_removed || ghost_removed)) {
+            std::vector<int32_t> h_agg((size_t)m), ai, aj;
+            std::vector<double> h_p0((size_t)m), aa;
+            if (m > 0 && ((e = hipMemcpy(h_agg.data(), d_agg, sizeof(int32_t) * (size_t)m, hipMemcpyDeviceToHost)) !=
+                              hipSuccess ||
+                          (e = hipMemcpy(h_p0.data(), d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost)) !=
+                              hipSuccess))
+                rc = gerr(e, "P0 rows");
+            ai.push_back(0);
+            for (int32_t i = 0; i < m; ++i) {
+                if (h_agg[i] >= 0) {
+                    aj.push_back(h_agg[i]);
+                    aa.push_back(h_p0[i]);
+                }
+                ai.push_back((int32_t)aj.size());
+            }
+            for (int32_t s = 0; s < ng; ++s) {
+                if (g_agg[s] >= 0) {
+                    aj.push_back(e1_id((int64_t)g_agg[s]));
+                    aa.push_back(g_p0[s]);
+                }
+                ai.push_back((int32_t)aj.size());
+            }
+            if (!rc) rc = upload_csr(m + ng, na + (int32_t)e1_off.size(), ai, aj, aa, P0ext);
+        } else if (!rc) {
             std::vector<int32_t> gcol((size_t)ng);
             for (int32_t s = 0; s < ng; ++s) gcol[s] = e1_id((int64_t)g_agg[s]);
             P0ext.m = m + ng;
@@ -915,6 +1063,20 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
                                (e = hipMemcpy(aa.data(), d_p0, sizeof(double) * (size_t)m, hipMemcpyDeviceToHost)) !=
                                    hipSuccess)))
                     rc = gerr(e, "P0");
+                if (!rc && local_removed) {  // (MIS-removed nodes: empty rows)
+                    std::vector<int32_t> ci(1, 0), cj;
+                    std::vector<double> ca;
+                    for (int32_t i = 0; i < m; ++i) {
+                        if (aj[i] >= 0) {
+                            cj.push_back(aj[i]);
+                            ca.push_back(aa[i]);
+                        }
+                        ci.push_back((int32_t)cj.size());
+                    }
+                    ai.swap(ci);
+                    aj.swap(cj);
+                    aa.swap(ca);
+                }
                 if (!rc) rc = upload_csr(m, P0ext.n, ai, aj, aa, Plocal);
             }
         }

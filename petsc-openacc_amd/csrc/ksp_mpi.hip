@@ -726,13 +726,7 @@ int kspmpi_set_up(aijhip_kspmpi *K) {
     if (dist) {
         aijhip_gamg_params_t gp;
         if (K->gamg_set) gp = K->gamg;
-        else {
-            // the distributed build aggregates greedily (PETSc's MIS across
-            // ranks is not built: DESIGN.md §6)
-            aijhip_gamg_params_default(&gp);
-            gp.coarsen = 0;
-            gp.eig_ksp = 0;
-        }
+        else aijhip_gamg_params_default(&gp);
         K->dh = new (std::nothrow) aijhip_gamg_mpi::Hierarchy();
         int rc = K->dh ? aijhip_gamg_mpi::build(M, gp, *K->dh) : mfail(AIJHIP_ERR_ALLOC, "host allocation");
         if (rc) {

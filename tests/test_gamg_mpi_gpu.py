@@ -157,7 +157,7 @@ def test_gpu_gamg_across_ranks_matches_oracle(world, dims):
         if l + 1 == nl:
             break
         starts = [p[0] for p in parts] + [n_l]
-        sub = ogm.build(Al, starts, max_levels=2, coarse_eq_limit=0, B=B)
+        sub = ogm.build(Al, starts, max_levels=2, coarse_eq_limit=0, B=B, level0=l)  # (MIS keys and squaring by level)
         B = sub[0]["Bc"]
         n_c = g[0]["rows"][l + 1]
         assert sub[1]["A"].shape[0] == n_c, (l, sub[1]["A"].shape, n_c)

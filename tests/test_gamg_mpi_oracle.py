@@ -20,7 +20,7 @@ def _system(N):
 
 def test_one_rank_is_the_single_hierarchy():
     ai, aj, aa, rhs, A = _system(14)
-    single = og.build(A, coarsen=0, eig_ksp=0)  # the distributed build aggregates greedily
+    single = og.build(A)
     dist = ogm.build(A, [0, A.shape[0]])
     assert [L["A"].shape for L in single] == [L["A"].shape for L in dist]
     for s, d in zip(single, dist):
@@ -40,7 +40,7 @@ def test_slabs_keep_the_iteration_count():
         its[k] = ksp_cg.cg(ai, aj, aa, rhs, pc=lambda r: ogm.vcycle(L, r), **TOL)[1]
     # block Jacobi + a hierarchy per slab (no coupling) at 4 slabs, for contrast
     starts = [(r * N // 4) * N * N for r in range(4)] + [N ** 3]
-    blocks = [(lo, hi, og.build(sp.csr_matrix(A[lo:hi, lo:hi]), coarsen=0, eig_ksp=0)) for lo, hi in zip(starts[:-1], starts[1:])]
+    blocks = [(lo, hi, og.build(sp.csr_matrix(A[lo:hi, lo:hi]))) for lo, hi in zip(starts[:-1], starts[1:])]
 
     def bjacobi(r):
         return np.concatenate([og.vcycle(lv, r[lo:hi]) for lo, hi, lv in blocks])
