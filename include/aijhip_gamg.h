@@ -19,7 +19,8 @@
  * CG's Lanczos tridiagonal as PCGAMGOptProlongator_AGG does (eig_ksp 1, the
  * default) or a power iteration (eig_ksp 0). GAMG iteration parity with
  * PETSc is unpinned either way (PETSc is absent). The distributed set-up
- * (aijhip_gamg_mpi) aggregates greedily.
+ * (PCGAMG across ranks) takes the same parameters, its MIS on each rank's
+ * diagonal block.
  * The solve-phase V-cycle runs on the device inside aijhip_ksp
  * (AIJHIP_PC_GAMG), whose set-up builds the large levels on the device
  * (device_min_rows) with results identical to aijhip_gamg_build_host.
