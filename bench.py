@@ -90,6 +90,8 @@ def parse():
     p.add_argument("--cg-iters", type=int, default=200, help="CG iterations timed for cg.iters_per_s")
     p.add_argument("--no-host-vec", action="store_true", help="skip the host-vector MatMult timing")
     p.add_argument("--no-flan", action="store_true", help="skip the configs[4] Flan_1565 stand-in legs")
+    p.add_argument("--no-pmc", action="store_true",
+                   help="skip the live rocprofv3 --pmc passes for roofline.traffic (use the committed record)")
     p.add_argument("--roofline-reps", type=int, default=50,
                    help="launches timed by HIP events for roofline.achieved (at least this many, SURVEY §8d)")
     p.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling 300^3 line")
@@ -376,6 +378,57 @@ def pmc_traffic(rows, nnz, block):
     if rec.get("rows") != rows or rec.get("nnz") != nnz or rec.get("block") != block:
         return None, None
     return rec.get("hbm_traffic_bytes_per_launch"), rec.get("source")
+
+
+def live_pmc_traffic(grid, timeout_s=150):
+    """HBM bytes per launch of the headline kernel counted in THIS run: two
+    rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: one counter group
+    each, no other tracing) over a child process that launches the same CSR
+    kernel on the same operand (tools/prof_case.py poisson, row patterns and
+    column codes off, 10 launches), corrected as MI355X_MICROARCH.md's HBM
+    section prescribes for gfx950 (read bytes = 2 x FETCH_SIZE KiB, write
+    bytes = WRITE_SIZE KiB; tools/pmc_summary.py). The child runs in its own
+    process group, killed (SIGKILL) at the time limit. Returns (bytes, detail)
+    or (None, reason)."""
+    import shutil
+    import signal
+    import subprocess
+    import tempfile
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not on PATH"
+    got = {}
+    with tempfile.TemporaryDirectory(prefix="bench_pmc_", dir=os.environ.get("TMPDIR", "/tmp")) as td:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            out_dir = Path(td) / counter
+            cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", str(out_dir), "-o", "run", "--",
+                   sys.executable, str(ROOT / "tools" / "prof_case.py"), "poisson", "--grid", str(grid), "--its", "10",
+                   "--opt", "row_patterns=0", "--opt", "column_codes=0"]
+            with open(Path(td) / f"{counter}.log", "w") as log:
+                proc = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
+                try:
+                    proc.wait(timeout=timeout_s)
+                except subprocess.TimeoutExpired:
+                    os.killpg(proc.pid, signal.SIGKILL)
+                    proc.wait()
+                    return None, f"{counter} pass exceeded {timeout_s} s (killed)"
+            if proc.returncode != 0:
+                return None, f"{counter} pass exited {proc.returncode}"
+            vals = []
+            for f in out_dir.rglob("*counter_collection.csv"):
+                import csv
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        k = row.get("Kernel_Name", "")
+                        if "k_spmv_stream" in k and "OpMult<false>" in k and row.get("Counter_Name") == counter:
+                            vals.append(float(row["Counter_Value"]))
+            if not vals:
+                return None, f"{counter}: no k_spmv_stream dispatch in the record"
+            got[counter] = (float(np.mean(vals)), len(vals))
+    rd = 2.0 * got["FETCH_SIZE"][0] * 1024
+    wr = got["WRITE_SIZE"][0] * 1024
+    return int(rd + wr), {"read_bytes": int(rd), "write_bytes": int(wr),
+                          "dispatches": [got["FETCH_SIZE"][1], got["WRITE_SIZE"][1]]}
 
 
 def time_launches(fn, stream, reps):
@@ -965,6 +1018,11 @@ def main():
         flan = guarded("flan_standin", lambda: flan_standins(pkg, dev, max(args.roofline_reps, 50),
                                                              not args.no_cpu_baseline))
 
+    live_pmc = None
+    under_profiler = any(k.startswith("ROCPROF") for k in os.environ)  # (never nest a profiler)
+    if rank == 0 and world == 1 and not args.no_pmc and not args.no_cpu_baseline and not under_profiler:
+        progress("roofline.traffic: two rocprofv3 --pmc passes of the headline kernel")
+        live_pmc = guarded("pmc", lambda: live_pmc_traffic(G))
     progress("done; writing the line")
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9
@@ -973,6 +1031,15 @@ def main():
         block = {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "nt_loads", "column_codes",
                                       "row_patterns")}
         traffic, traffic_src = (None, None) if distributed else pmc_traffic(n_global, nnz_global, block)
+        pmc_detail = None
+        if isinstance(live_pmc, tuple) and live_pmc[0] is not None and not info.get("row_patterns") \
+                and not info.get("column_codes"):
+            traffic, pmc_detail = live_pmc
+            traffic_src = ("this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (one counter group each) of "
+                           "tools/prof_case.py poisson in the CSR layout, gfx950-corrected (2 x FETCH_SIZE KiB + "
+                           "WRITE_SIZE KiB), mean over the kernel's dispatches")
+        elif live_pmc is not None:
+            pmc_detail = {"live_pmc_failed": str(live_pmc[1] if isinstance(live_pmc, tuple) else live_pmc)}
         out = {
             "metric": "CSR SpMV effective HBM GB/s (300^3 7-pt Poisson, fp64 MatMult_SeqAIJ)",
             "value": round(value, 2),
@@ -1005,6 +1072,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
+                "traffic_detail": pmc_detail,
                 "kernel": ("k_spmv_stream (CSR: aj / aa pairs, x gathered, LDS row sums)"
                            if not (info.get("row_patterns") or info.get("column_codes")) else layout_name(info)),
                 "kernel_us_mean": round(mean_launch_s * 1e6, 2),
