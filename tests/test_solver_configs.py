@@ -233,6 +233,8 @@ def test_gpu_cg_gamg_100_configs0_vs_oracle(pkg):
     assert abs(its - its_o) <= 1 and abs(its - PINNED_ITS[N]) <= 1, (its, its_o)
     k = min(len(hist), len(hist_o))
     np.testing.assert_allclose(hist[:min(k, 10)], hist_o[:min(k, 10)], rtol=1e-7)
-    np.testing.assert_allclose(hist[:k], hist_o[:k], rtol=1e-4)
+    # (the last norms sit at ~1e-14 of the first, where the device's and the
+    # oracle's dot orders differ in the last bits: an absolute floor there)
+    np.testing.assert_allclose(hist[:k], hist_o[:k], rtol=1e-4, atol=1e-15 * hist_o[0])
     assert np.linalg.norm(x - xo) <= 1e-8 * np.linalg.norm(xo)
     assert err <= C_H2 / (N * N), err
