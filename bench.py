@@ -431,6 +431,19 @@ def live_pmc_traffic(grid, timeout_s=150):
                           "dispatches": [got["FETCH_SIZE"][1], got["WRITE_SIZE"][1]]}
 
 
+def launch_times(fn, stream, reps):
+    """Per-launch HIP events on `stream` around `reps` calls of fn(): the
+    launch times in us."""
+    import torch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) * 1e3 for a, b in ev]
+
+
 def time_launches(fn, stream, reps):
     """Per-launch HIP events on `stream` around `reps` calls of fn():
     (mean us, median us, min us)."""
@@ -472,16 +485,23 @@ def flan_standins(pkg, dev, reps, cpu_sample):
         x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
         y = torch.empty_like(x)
         rec = {"rows": m, "nnz": nnz, "max_row": int(np.diff(ai).max()), "bytes_per_spmv": nbytes}
-        for kern in kernels:
-            A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="stream")
-            try:
+        # every variant built first, then timed in interleaved rounds (10
+        # launches of each per round): a leg timed alone after another leg
+        # read up to 6 % apart from the same code (r05 records, skewed
+        # stream vs stream_exact)
+        mats, infos, times = {}, {}, {}
+        try:
+            for kern in kernels:
+                A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="stream")
+                mats[kern] = A
                 if kern == "stream_exact":
                     A.set_option("exact", 1)
                 if kern == "stream_csr":  # aj as stored: no gather order
                     A.set_option("gather_sort", 0)
                 if kern == "stream_serial":  # the long rows after the row blocks, not beside them
                     A.set_option("long_overlap", 0)
-                info = A.info()
+                infos[kern] = A.info()
+                times[kern] = []
                 # warm-up of >= 50 ms of launches: the first leg follows the
                 # PCIe-bound host-vector leg, and after 5 launches it read 6-8 %
                 # slow (profiles/r04/bench_r04e.json vs s3/skewed_exact.jsonl)
@@ -490,17 +510,25 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                     for _ in range(10):
                         A.mult(x, y, stream)
                     torch.cuda.synchronize()
-                mean, med, mn = time_launches(lambda: A.mult(x, y, stream), stream, reps)
-            finally:
+            for _ in range(max(8, reps // 10)):
+                for kern, A in mats.items():
+                    times[kern].extend(launch_times(lambda: A.mult(x, y, stream), stream, 10))
+        finally:
+            for A in mats.values():
                 A.destroy()
+        for kern in kernels:
+            info, us = infos[kern], np.array(times[kern])
+            mean, med, mn = float(np.mean(us)), float(np.median(us)), float(np.min(us))
             lb = info["mult_layout_bytes"]
             rec[kern] = {"us_mean": round(mean, 2), "us_median": round(med, 2), "us_min": round(mn, 2),
+                         "launches": int(len(us)),
                          "layout_bytes": lb, "GBs": round(lb / (mean * 1e-6) / 1e9, 1),
                          "frac": round(lb / (mean * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                          "csr_effective_GBs": round(nbytes / (mean * 1e-6) / 1e9, 1),
                          "geometry": info.get("stream_geometry"), "long_rows": info.get("n_long_rows"),
                          "column_codes": info.get("column_codes"), "gather_sorted": info.get("gather_sorted"),
-                         "row_patterns": info.get("row_patterns"), "long_overlap": info.get("long_overlap")}
+                         "row_patterns": info.get("row_patterns"), "long_overlap": info.get("long_overlap"),
+                         "exact": info.get("exact")}
         del x, y
         flat = read_ceiling(nbytes, dev)
         rec["ceiling_flat_read"] = {"GBs": flat[0][0], "us": flat[0][1],
@@ -988,6 +1016,12 @@ def main():
         greedy = ksp.bench_cg_gamg(pkg, A, nx, ny, nz_global, dev, gamg=dict(coarsen=0, eig_ksp=0), light=True)
         greedy["hierarchy"] = "greedy aggregation in natural order, power-iteration emax (coarsen 0, eig_ksp 0)"
         out["greedy_hierarchy"] = greedy
+        if "error" not in greedy:  # like for like: each hierarchy's second set-up in the process + its solve
+            out["hierarchy_comparison"] = {
+                "default_mis_s": round(out["setup_again_s"] + out["solve_s"], 4),
+                "greedy_s": round(greedy["setup_again_s"] + greedy["solve_s"], 4),
+                "note": "set-up again (warm: the first set-up of the process also pays one-time costs, and the "
+                        "greedy leg runs after the default one) + solve, seconds"}
         print(f"bench: CG+GAMG {out['its']} its, solve {out['solve_s']} s, set-up {out['setup_s']} s",
               file=sys.stderr, flush=True)
         # BASELINE configs[0] (100^3) on the device as well, beside its 1-core host solve
