@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round 5: kernel statistics of the whole bench (rocprofv3 --kernel-trace --stats).
+set -o pipefail
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/r05r
+mkdir -p "$OUT"
+cd "$ROOT" || exit 1
+export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run --output-format csv \
+    -- python3 bench.py --no-cpu-baseline --no-host-vec > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" \
+    && echo "full prof ok" || { tail -20 "$OUT/bench_prof.err"; exit 1; }
