@@ -1683,6 +1683,18 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
     GTRY(dalloc(&d, m), "alloc");
     GTRY(dalloc(&dinv, m), "alloc");
     hipLaunchKernelGGL(k_diag_dinv, dim3(g256), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, d, dinv);
+    // the emax job starts as soon as D^-1 is queued: it overlaps the strength
+    // graph as well as the aggregation (round 5: started after the strength
+    // graph, the level-0 CG estimate still held the level ~8 ms past the MIS)
+    if (emax_its > 0) {  // (D^-1 is written on the null stream: the job's stream waits for it)
+        if (hipEventCreateWithFlags(&ev_dinv, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(ev_dinv, nullptr) != hipSuccess) {
+            if (ev_dinv) (void)hipEventDestroy(ev_dinv);
+            ev_dinv = nullptr;
+            GTRY(hipDeviceSynchronize(), "D^-1");
+        }
+        job.start(A, dinv, emax_its, p.eig_ksp == 1, ev_dinv);
+    }
     {
         bool direct = false;  // S straight from A (sorted rows, symmetric strong pattern)
         if ((rc = strength_direct(A, d, p.threshold, &si, &sj, &sval, &nzs, &direct))) goto level_done;
@@ -1717,15 +1729,6 @@ strength_done:
     // memory; the same aggregates either way. Phase 2 on the device; phase
     // 3 (sequential) over the nodes left.
     lap("strength kernels");
-    if (emax_its > 0) {  // (D^-1 is written on the null stream: the job's stream waits for it)
-        if (hipEventCreateWithFlags(&ev_dinv, hipEventDisableTiming) != hipSuccess ||
-            hipEventRecord(ev_dinv, nullptr) != hipSuccess) {
-            if (ev_dinv) (void)hipEventDestroy(ev_dinv);
-            ev_dinv = nullptr;
-            GTRY(hipDeviceSynchronize(), "D^-1");
-        }
-        job.start(A, dinv, emax_its, p.eig_ksp == 1, ev_dinv);
-    }
     GTRY(dalloc(&d_aggv, m), "alloc");
     if (p.coarsen == 1) {  // PETSc 3.7 agg's MIS (gamg_aggregate.hip), node for node the host's
         int32_t rounds = 0;
