@@ -13,7 +13,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gamg.py -x -q -m gpu -k "mis" -
 tail -1 "$OUT/pytest.log"
 for rep in 1 2 3; do
   for case in mis greedy; do
-    if [ $case = mis ]; then opts="--gamg-opt coarsen=1 --gamg-opt eig_ksp=1"; else opts=""; fi
+    if [ $case = mis ]; then opts="--gamg-opt coarsen=1 --gamg-opt eig_ksp=1"; else opts="--gamg-opt coarsen=0 --gamg-opt eig_ksp=0"; fi
     AIJHIP_GAMG_LOG=1 timeout -k 10 200 python -u tools/prof_case.py gamg $opts > "$OUT/gamg_${case}_$rep.log" 2>&1 \
         || { tail -30 "$OUT/gamg_${case}_$rep.log"; exit 1; }
     echo "$case $rep: $(grep -E 'gamg: set-up' "$OUT/gamg_${case}_$rep.log")"
