@@ -214,35 +214,14 @@ __global__ __launch_bounds__(kVecThreads) void k_init(int64_t n, const double *_
 // anyway, before P is overwritten (same operation on every element, one
 // iteration later: X and P make one pass fewer per iteration).
 // x == nullptr: X += a P is applied in k_update instead (x_in_update).
-// Two elements per lane per step (i and i + stride, in that order): six
-// loads in flight per lane instead of three (round 5: the one-element loop
-// ran at ~5.2 TB/s against the update kernel's ~6.9).
 template <bool NT>
-__global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *__restrict__ z,
-                                                      double *__restrict__ p, double *__restrict__ x,
-                                                      const CGState *S) {
+__global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *__restrict__ z, double *p,
+                                                      double *x, const CGState *S) {
     if (S->done) return;
     const bool first = S->i == 0 || x == nullptr;
     const double bb = S->b, a = S->a;
     const bool p_first = S->i == 0;
-    const int64_t stride = (int64_t)gridDim.x * kVecThreads;
-    int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x;
-    for (; i + stride < n; i += 2 * stride) {
-        const int64_t j = i + stride;
-        const double pi = p[i], pj = p[j], zi = z[i], zj = z[j];
-        double xi = 0.0, xj = 0.0;
-        if (!first) {
-            xi = x[i];
-            xj = x[j];
-        }
-        if (!first) {
-            vst<NT>(x + i, xi + a * pi);
-            vst<NT>(x + j, xj + a * pj);
-        }
-        vst<NT>(p + i, p_first ? zi : zi + bb * pi);
-        vst<NT>(p + j, p_first ? zj : zj + bb * pj);
-    }
-    if (i < n) {
+    GRID_STRIDE(i, n) {
         const double pi = p[i];
         if (!first) vst<NT>(x + i, x[i] + a * pi);
         vst<NT>(p + i, p_first ? z[i] : z[i] + bb * pi);
@@ -297,17 +276,17 @@ __global__ __launch_bounds__(kVecThreads) void k_dots(int64_t n, const double *_
 // (GAMG: R.R only, Z follows from the V-cycle). VecAXPY(X, a, P) is deferred
 // to the next K1 (or k_final_x).
 template <bool NT>
-__global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *__restrict__ r, double *__restrict__ wz,
+__global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, double *wz,
                                                         const double *__restrict__ dinv, double *part,
                                                         const CGState *S, int pc,
-                                                        const double *__restrict__ p, double *__restrict__ x) {
+                                                        const double *__restrict__ p, double *x) {
     __shared__ double scratch[kVecThreads / 64];
     if (S->done) return;
     const double a = S->a, na = -S->a;
     double zz = 0.0, zr = 0.0, rr = 0.0;
-    // one element: the partials accumulate in the lane's element order
-    auto one = [&](int64_t i, double ri0, double wi) {
-        const double ri = ri0 + na * wi;  // VecAXPY(R, -a, W)
+    GRID_STRIDE(i, n) {
+        if (x) vst<NT>(x + i, x[i] + a * p[i]);  // VecAXPY(X, a, P) (x_in_update)
+        const double ri = r[i] + na * wz[i];  // VecAXPY(R, -a, W)
         vst<NT>(r + i, ri);
         rr += ri * ri;
         if (pc != AIJHIP_PC_GAMG) {
@@ -316,24 +295,6 @@ __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *__res
             zz += zi * zi;
             zr += zi * ri;
         }
-    };
-    // two elements per lane per step (i, then i + stride: the same order)
-    const int64_t stride = (int64_t)gridDim.x * kVecThreads;
-    int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x;
-    for (; i + stride < n; i += 2 * stride) {
-        const int64_t j = i + stride;
-        if (x) {
-            const double pi = p[i], pj = p[j], xi = x[i], xj = x[j];
-            vst<NT>(x + i, xi + a * pi);  // VecAXPY(X, a, P) (x_in_update)
-            vst<NT>(x + j, xj + a * pj);
-        }
-        const double ri = r[i], rj = r[j], wi = wz[i], wj = wz[j];
-        one(i, ri, wi);
-        one(j, rj, wj);
-    }
-    if (i < n) {
-        if (x) vst<NT>(x + i, x[i] + a * p[i]);
-        one(i, r[i], wz[i]);
     }
     const int nb = gridDim.x;
     double v;
