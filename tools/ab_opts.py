@@ -23,7 +23,7 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--case", default="poisson", choices=["poisson", "skewed", "fem_hex"])
+    ap.add_argument("--case", default="poisson", choices=["poisson", "skewed", "skewed_nohub", "fem_hex"])
     ap.add_argument("--grid", type=int, default=300)
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--per", type=int, default=10)
@@ -33,8 +33,14 @@ def main():
     dev = torch.device("cuda:0")
     if args.case == "poisson":
         ai, aj, aa = pkg.poisson_csr(args.grid)
-    elif args.case == "skewed":
+    elif args.case.startswith("skewed"):
         ai, aj, aa = pkg.skewed_csr()
+        if args.case == "skewed_nohub":  # the hub rows emptied (tools/prof_case.py)
+            import numpy as np
+            ln = np.diff(ai)
+            keep = np.repeat(ln <= 1000, ln)
+            ai = np.concatenate([[0], np.cumsum(np.where(ln <= 1000, ln, 0))]).astype(np.int32)
+            aj, aa = aj[keep], aa[keep]
     else:
         ai, aj, aa = pkg.fem_hex_csr()
     m = len(ai) - 1
