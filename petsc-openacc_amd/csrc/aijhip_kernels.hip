@@ -1280,6 +1280,14 @@ static hipError_t compressed_prologue(const aijhip_mat &A, const double *z, doub
     return hipSuccess;
 }
 
+// The wide blocks (few long rows of scattered columns each, split from the
+// narrow ones) on the branch-free phase 1 with non-temporal matrix loads:
+// with the predicated form each lane's eight scattered gathers waited on one
+// another (vmcnt(0) per pair), and a launch of a few dozen such blocks is
+// one block's latency — 29 us of the skewed stand-in's serial 331 us
+// (round 5, profiles/r05/x)
+constexpr int kWideMode = 64 | 1;
+
 template <int T, int CAP, int RPT>
 static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L, const double *x,
                             const double *z, double *y, bool add, hipStream_t s, double *dpart,
@@ -1316,7 +1324,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            (int)P.tune.exact, L.rai, nullptr, reinterpret_cast<const int32_t *>(P.d_code), A.d_aa, \
                            OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_cmeta);     \
     if (P.n_wblocks > 0)                                                                                          \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, sw, \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, kWideMode, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, sw, \
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,           \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);                \
     return
@@ -1344,7 +1352,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            (int)P.tune.exact, L.rai, L.ridx, reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa, \
                            OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop, nullptr, P.d_sbase);  \
     if (P.n_wblocks > 0)                                                                                       \
-        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, 0, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, sw, \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, CROW, kWideMode, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, sw, \
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,         \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);             \
     return
