@@ -175,7 +175,9 @@ enum {
     AIJHIP_OPT_EXACT = 6,           /* 1: every row of the row blocks summed
                                        sequentially in PETSc's order. Default
                                        0: row blocks whose mean row length
-                                       exceeds 128 use 2..64 lanes per row
+                                       exceeds 128 (and rows of more than
+                                       1024 entries, which get a block of
+                                       their own) use 2..64 lanes per row
                                        (reordered sum, within the fp64
                                        bound); shorter rows (7-pt Poisson,
                                        FEM rows) are bit-exact either way.

@@ -161,6 +161,13 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
         while (r < r1 && r - start < G.rows) {
             const int32_t l = rai[r + 1] - rai[r];
             if (l > G.nnz_cap || nk + l > G.nnz_cap) break;
+            if (l > kIsolateRowNnz) {  // a block of its own (see kIsolateRowNnz)
+                if (r == start) {
+                    nk = l;
+                    ++r;
+                }
+                break;
+            }
             nk += l;
             ++r;
         }

@@ -140,6 +140,12 @@ constexpr int kSplitMinMean = 128;
 // order, same bits). Measured (profiles/r01/rowsum/): FEM-structured stand-in
 // 310 -> 280 us at geometry 6, skewed stand-in 429 -> 405 us at geometry 1.
 constexpr int kBatchMinMean = 16;
+// A row longer than this (and within the block cap) gets a row block of its
+// own, so it is summed by 64 lanes (reordered; exact = 1 keeps one lane and
+// PETSc's order) instead of one lane's dependent chain holding its block of
+// short rows: the skewed stand-in's 40 rows of 1e3-4e3 scattered entries
+// made its wide blocks a 29 us launch (round 5, profiles/r05/x).
+constexpr int kIsolateRowNnz = 1024;
 // Automatic geometry for long rows (mean > 16): above this many distinct x
 // lines per entry the gathers count as scattered (geometry 1), below it they
 // run along lines (geometry 6). Measured: 7-pt 0.73, GAMG coarse operators
