@@ -128,6 +128,11 @@ int validate_csr(int32_t m, int32_t n, int64_t nz, const int32_t *ai, const int3
     return AIJHIP_OK;
 }
 
+int32_t isolate_row_nnz() {
+    const char *v = std::getenv("AIJHIP_ISOLATE_ROW_NNZ");
+    return v ? (int32_t)std::atoi(v) : aijhip::kIsolateRowNnz;
+}
+
 // CSR-stream row blocks over the handle's row list (h_rai): greedily pack
 // consecutive rows while the block holds <= nnz_cap entries and <= rows rows
 // of the chosen geometry. A longer row becomes a long row, split into
@@ -140,6 +145,9 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
     // segment length: 1024-16384 measured within 3 % on the skewed stand-in
     // (profiles/r03/longseg/)
     constexpr int64_t seg_nnz = kLongSegNnz;
+    // rows longer than this get a block of their own (kIsolateRowNnz;
+    // AIJHIP_ISOLATE_ROW_NNZ overrides it for A/B runs, 0 = never)
+    const int32_t isolate = isolate_row_nnz();
     int32_t r = r0;
     while (r < r1) {
         const int32_t len = rai[r + 1] - rai[r];
@@ -161,7 +169,7 @@ void plan_rows(const aijhip_mat *A, const aijhip::StreamGeom &G, const int32_t *
         while (r < r1 && r - start < G.rows) {
             const int32_t l = rai[r + 1] - rai[r];
             if (l > G.nnz_cap || nk + l > G.nnz_cap) break;
-            if (l > kIsolateRowNnz) {  // a block of its own (see kIsolateRowNnz)
+            if (isolate > 0 && l > isolate) {  // a block of its own (see kIsolateRowNnz)
                 if (r == start) {
                     nk = l;
                     ++r;

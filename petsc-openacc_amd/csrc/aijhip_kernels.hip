@@ -558,46 +558,60 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
     }
 }
 
-// Segments of long rows: tree-reduced partial sums. Lane t takes entries
-// k0 + t, k0 + t + kLongThreads, ... (U = 8 of a 4096-entry segment), so one
-// gather instruction of a wave reads 64 consecutive entries of the row: in
-// the hub rows' ascending, ~8-column-apart columns two lanes share each
-// 128-B line, half the L2 requests of the pair layout (lane t taking
-// entries 2t, 2t + 1, whose first gathers were 16 columns apart) — the
-// segments are bound by the L2 requests of their scattered gathers (round 5:
-// 44 us for 6.7 M entries). Every load and gather of the segment is issued
-// before the first product is needed; straight-line (clamped loads, selects
-// in the sums: predicated loads compiled to branches whose joins waited for
-// all earlier loads, the hub rows' 47 us in r03-r04). The lane's U partial
-// sums are combined u = 0..U-1, then the wave tree, then the waves in order:
-// a fixed order.
+// Segments of long rows: tree-reduced partial sums. (Round 5: lane t taking
+// entries k0 + t + 512u instead, so that one gather instruction reads 64
+// consecutive entries, measured 43.7 vs 44.9 us — the second gather of a
+// pair already hits L1; not kept.) A lane takes 16-B pairs
+// (aa as f64x2, aj as i32x2 from an even start, as the STREAM blocks do) at
+// pair stride kLongThreads and keeps U pairs in flight: a 4096-entry segment
+// is 2048 pairs (512 lanes x 4), so every load and gather of the segment is
+// issued before the first product is needed (the previous form, 8 scalar entries per round,
+// waited on two dependent latencies per round: 2.66 TB/s). The
+// lane's U partial sums are combined u = 0..U-1, then the wave tree, then the
+// waves in order: a fixed order.
 // The body, for the first kLongThreads lanes of the calling workgroup (any
 // further lanes only pass the barrier). red: >= kLongThreads / 64 LDS doubles.
 __device__ __forceinline__ void long_segment(const int32_t id, const LongSeg *__restrict__ seg,
                                              const int32_t *__restrict__ aj, const double *__restrict__ aa,
                                              const double *__restrict__ x, double *__restrict__ partials,
                                              double *red) {
-    constexpr int U = kLongSegNnz / kLongThreads;  // entries in flight per lane
-    static_assert(U >= 1, "a round of entries must fit a segment");
+    constexpr int U = kLongSegNnz / (2 * kLongThreads);  // pairs in flight per lane
+    static_assert(U >= 1, "a round of pairs must fit a segment");
     const LongSeg s = seg[id];
     const int t = threadIdx.x;
     double acc[U] = {};
-    const int64_t k0 = s.k0, k1 = (int64_t)s.k0 + s.nk;
-    const int64_t kl = k1 - 1;                        // the segment's last entry (nk >= 1)
-    const int64_t kend = t < kLongThreads ? k1 : k0;  // lanes past kLongThreads take no entries
-    for (int64_t k = k0 + t; k < kend; k += (int64_t)U * kLongThreads) {
-        int32_t c[U];
-        double a[U], xv[U];
+    const int64_t k0 = s.k0, k1 = (int64_t)s.k0 + s.nk, kb = k0 & ~int64_t(1);
+    const int64_t kl = (k1 - 1) & ~int64_t(1);        // the segment's last pair (nk >= 1)
+    const int64_t kend = t < kLongThreads ? k1 : kb;  // lanes past kLongThreads take no pairs
+    // Straight-line rounds: every pair slot loads (past the segment: its last
+    // pair again) and gathers, and the sums take only the segment's entries
+    // (selects). Predicated loads compiled to branches, and each gather
+    // then waited for all earlier loads: U x 2 dependent scattered round
+    // trips per round instead of one (the hub rows' 47 us in r03-r04).
+    for (int64_t k = kb + 2 * t; k < kend; k += (int64_t)2 * U * kLongThreads) {
+        f64x2 a[U];
+        i32x2 c[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) c[u] = __builtin_nontemporal_load(aj + min(k + (int64_t)u * kLongThreads, kl));
+        for (int u = 0; u < U; ++u)
+            c[u] = __builtin_nontemporal_load(
+                reinterpret_cast<const i32x2 *>(aj + min(k + (int64_t)2 * u * kLongThreads, kl)));
 #pragma unroll
-        for (int u = 0; u < U; ++u) a[u] = __builtin_nontemporal_load(aa + min(k + (int64_t)u * kLongThreads, kl));
-#pragma unroll
-        for (int u = 0; u < U; ++u) xv[u] = x[c[u]];
+        for (int u = 0; u < U; ++u)
+            a[u] = __builtin_nontemporal_load(
+                reinterpret_cast<const f64x2 *>(aa + min(k + (int64_t)2 * u * kLongThreads, kl)));
+        double x0[U], x1[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const double sv = acc[u] + a[u] * xv[u];
-            acc[u] = (k + (int64_t)u * kLongThreads < k1) ? sv : acc[u];
+            x0[u] = x[c[u].x];
+            x1[u] = x[c[u].y];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t kk = k + (int64_t)2 * u * kLongThreads;
+            const double s0 = acc[u] + a[u].x * x0[u];
+            acc[u] = (kk < k1 && kk >= k0) ? s0 : acc[u];
+            const double s1 = acc[u] + a[u].y * x1[u];
+            acc[u] = (kk + 1 < k1) ? s1 : acc[u];
         }
     }
     double v = acc[0];

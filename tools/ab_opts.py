@@ -47,10 +47,20 @@ def main():
     x = torch.from_numpy(pkg.splitmix_uniform(m, 42)).to(dev)
     variants = [json.loads(v) for v in args.variant] or [{}]
     mats, ys = [], []
+    import os
     for opts in variants:
+        env = opts.get("_env", {})  # planner environment knobs, e.g. AIJHIP_ISOLATE_ROW_NNZ, for this matrix only
+        saved = {k: os.environ.get(k) for k in env}
+        os.environ.update({k: str(v) for k, v in env.items()})
         A = pkg.SeqAIJHIP(ai, aj, aa, ncols=m, kernel="stream")
         for k, v in opts.items():
-            A.set_option(k, int(v))
+            if k != "_env":
+                A.set_option(k, int(v))
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         mats.append(A)
         ys.append(torch.empty(A.m, dtype=torch.float64, device=dev))
         print(f"ab_opts: {opts}: {A.info()}", file=sys.stderr, flush=True)
