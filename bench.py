@@ -466,8 +466,8 @@ def flan_standins(pkg, dev, reps, cpu_sample):
       skewed — 1,564,794 rows of 45-99 banded entries plus 1e-4 hub rows of
                1e3-2e5 scattered entries (seed 1565): the merge-path
                load-balance stress; STREAM (default: gather-ordered row
-               blocks, hub rows as 4096-entry segments on a side stream
-               beside them; stream_serial: the segments after them), STREAM exact
+               blocks, hub rows as 4096-entry segments after them;
+               stream_side: the segments on a side stream beside them), STREAM exact
                (PETSc's order in every row that fits a block) and STREAM on
                PETSc's aj as stored (stream_csr);
       fem_hex — Flan_1565's own structure: a hexahedral mesh of 81x80x80
@@ -477,7 +477,7 @@ def flan_standins(pkg, dev, reps, cpu_sample):
     stream = torch.cuda.current_stream()
     out = {}
     for name, make, kernels in (("skewed", lambda: pkg.skewed_csr(),
-                                 ("stream", "stream_serial", "stream_exact", "stream_csr")),
+                                 ("stream", "stream_side", "stream_exact", "stream_csr")),
                                 ("fem_hex", lambda: pkg.fem_hex_csr(), ("stream",))):
         ai, aj, aa = make()
         m, nnz = len(ai) - 1, len(aj)
@@ -498,8 +498,8 @@ def flan_standins(pkg, dev, reps, cpu_sample):
                     A.set_option("exact", 1)
                 if kern == "stream_csr":  # aj as stored: no gather order
                     A.set_option("gather_sort", 0)
-                if kern == "stream_serial":  # the long rows after the row blocks, not beside them
-                    A.set_option("long_overlap", 0)
+                if kern == "stream_side":  # the long rows on a side stream beside the row blocks
+                    A.set_option("long_overlap", 1)
                 infos[kern] = A.info()
                 times[kern] = []
                 # warm-up of >= 50 ms of launches: the first leg follows the

@@ -425,7 +425,7 @@ int plan_stream(aijhip_mat *A) {
     }
     // Tuning::overlap: a side stream and its two events for the wide blocks
     // and the long rows (created once per plan that has them)
-    if (P.tune.overlap != 0 && (P.n_wblocks > 0 || P.n_longs > 0)) {
+    if (P.tune.overlap > 0 && (P.n_wblocks > 0 || P.n_longs > 0)) {
         if ((e = hipStreamCreateWithFlags(&P.side, hipStreamNonBlocking)) != hipSuccess ||
             (e = hipEventCreateWithFlags(&P.ev_fork, aijhip::sync_event_flags())) != hipSuccess ||
             (e = hipEventCreateWithFlags(&P.ev_join, aijhip::sync_event_flags())) != hipSuccess)
@@ -897,7 +897,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
         case AIJHIP_OPT_LONG_OVERLAP:
-            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: -1 auto (on), 0 off, 1 side stream");
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: -1 auto (off), 0 off, 1 side stream");
             t.overlap = value;
             break;
         case AIJHIP_OPT_HOST_PIPELINE:

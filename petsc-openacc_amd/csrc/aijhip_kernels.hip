@@ -1519,7 +1519,7 @@ hipError_t launch_stream(const aijhip_mat &A, const double *x, const double *z, 
     // writes its own rows of y, so the order between them is free. The fork /
     // join events live in the plan: a handle is used by one host thread at a
     // time (include/aijhip.h, "Threading"), as PETSc's Mat is.
-    const bool ovl = P.tune.overlap != 0 && P.side && !L.ridx && !dpart && !stop &&
+    const bool ovl = P.tune.overlap > 0 && P.side && !L.ridx && !dpart && !stop &&
                      (P.n_wblocks > 0 || P.n_longs > 0);
     hipStream_t sw = s;
     if (ovl) {
