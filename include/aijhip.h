@@ -197,13 +197,14 @@ enum {
                                        download (step3/step4 analogue); k > 0:
                                        chunks of >= k rows; 0: the serial
                                        step-2 form. Same results              */
-    AIJHIP_OPT_LONG_OVERLAP = 9,    /* operands with long rows: 0 or -1
-                                       (default since round 5) the segments
-                                       and the wide blocks after the row
-                                       blocks; 1 on a side stream beside them
-                                       (plain MatMult / MatMultAdd; forked
-                                       from and joined to the caller's stream
-                                       by events). Same results             */
+    AIJHIP_OPT_LONG_OVERLAP = 9,    /* operands with long rows: 0 the
+                                       segments and the wide blocks after the
+                                       row blocks; 1 on a side stream beside
+                                       them (plain MatMult / MatMultAdd;
+                                       forked from and joined to the caller's
+                                       stream by events); -1 (default): 0,
+                                       or 1 with AIJHIP_OPT_EXACT. Same
+                                       results                              */
     AIJHIP_OPT_GATHER_SORT = 12,    /* MatMult / MatMultAdd from a copy of the
                                        row blocks with each block's entries
                                        sorted by column and their positions

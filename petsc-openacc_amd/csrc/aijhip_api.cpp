@@ -442,6 +442,11 @@ int plan_build(aijhip_mat *A) {
     if (kernel == AIJHIP_KERNEL_AUTO) kernel = AIJHIP_KERNEL_STREAM;
     P.kernel = kernel;
     P.tune = A->requested_tune;
+    // long rows after the row blocks, except in exact mode, where the rows
+    // of 1-4 K entries keep one lane's sequential sum and the side stream
+    // hides that chain (round 5: skewed stand-in default 310.7 vs 315.2 us
+    // side stream; exact 350.5 us after, profiles/r05/ad/)
+    if (P.tune.overlap < 0) P.tune.overlap = P.tune.exact ? 1 : 0;
     const bool auto_sort = P.tune.gsort < 0;
     const bool auto_codes = P.tune.codes < 0;
     const bool auto_patterns = P.tune.patterns < 0;
@@ -897,7 +902,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
         case AIJHIP_OPT_EXACT: t.exact = value != 0; break;
         case AIJHIP_OPT_LONG_XCD: t.long_xcd = value != 0; break;
         case AIJHIP_OPT_LONG_OVERLAP:
-            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: -1 auto (off), 0 off, 1 side stream");
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "long_overlap: -1 auto (off; on with exact), 0 off, 1 side stream");
             t.overlap = value;
             break;
         case AIJHIP_OPT_HOST_PIPELINE:

@@ -97,7 +97,7 @@ struct Tuning {
     bool long_xcd = true;  // long-row segments placed on the XCD that owns their column range
     int overlap = -1;      // MatMult / MatMultAdd with wide blocks or long rows: those launches on a
                            // side stream concurrent with the row blocks (1), or after them (0; -1
-                           // auto = 0 since round 5). Skewed stand-in r04: 299.0 vs 310.5 us
+                           // auto = 0 since round 5, 1 with exact). Skewed stand-in r04: 299.0 vs 310.5 us
                            // (profiles/r04/s2/); round 5, rows > 1024 in blocks of their own, the
                            // same box interleaved: side 315.1, serial 310.2 us (profiles/r05/ac/)
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
