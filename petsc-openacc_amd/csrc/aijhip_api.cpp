@@ -518,6 +518,7 @@ int plan_build(aijhip_mat *A) {
                 free_plan(A->plan);
                 P.kernel = kernel;
                 P.tune = req;
+                if (P.tune.overlap < 0) P.tune.overlap = P.tune.exact ? 1 : 0;
                 P.tune.gsort = 0;
                 if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
                 if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
