@@ -169,3 +169,57 @@ def test_launch_ranks_propagates_a_failure(bench, monkeypatch):
     import sys
     monkeypatch.setenv("FAIL_RANK", "1")
     assert bench.launch_ranks(2, [], child=[sys.executable, "-c", CHILD]) == 3
+
+
+def _fake_rocprof(tmp_path, body):
+    exe = tmp_path / "rocprofv3"
+    exe.write_text("#!/usr/bin/env python3\n" + body)
+    exe.chmod(0o755)
+    return exe
+
+
+_FAKE_OK = r'''
+import sys, pathlib
+a = sys.argv
+d = pathlib.Path(a[a.index("-d") + 1]); c = a[a.index("--pmc") + 1]
+d.mkdir(parents=True, exist_ok=True)
+v = {"FETCH_SIZE": 1000.0, "WRITE_SIZE": 300.0}[c]
+k = "void aijhip::(anonymous namespace)::k_spmv_stream<512, 4094, 1, false, 0, aijhip::(anonymous namespace)::OpMult<false> >(int)"
+with open(d / "run_counter_collection.csv", "w") as f:
+    f.write("Kernel_Name,Counter_Name,Counter_Value\n")
+    for i in range(10):
+        f.write('"%s",%s,%s\n' % (k, c, v + i))
+    f.write('"other_kernel(int)",%s,1e9\n' % c)
+'''
+
+
+def test_live_pmc_traffic_parses_the_passes(bench, tmp_path, monkeypatch):
+    """roofline.traffic from two --pmc passes: 2 x FETCH_SIZE KiB + WRITE_SIZE
+    KiB (MI355X_MICROARCH's gfx950 correction), mean over the headline
+    kernel's dispatches, other kernels ignored (a stand-in rocprofv3)."""
+    _fake_rocprof(tmp_path, _FAKE_OK)
+    monkeypatch.setenv("PATH", f"{tmp_path}:{__import__('os').environ['PATH']}")
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    traffic, detail = bench.live_pmc_traffic(300, timeout_s=60)
+    assert detail["read_bytes"] == int(2 * 1004.5 * 1024) and detail["write_bytes"] == int(304.5 * 1024)
+    assert traffic == detail["read_bytes"] + detail["write_bytes"] and detail["dispatches"] == [10, 10]
+
+
+def test_live_pmc_traffic_kills_a_hung_pass(bench, tmp_path, monkeypatch):
+    """A pass that hangs (rocprofv3's 'error code 38' behaviour) is killed with
+    its process group at the limit, and the bench falls back (None, reason)."""
+    _fake_rocprof(tmp_path, "import time\ntime.sleep(120)\n")
+    monkeypatch.setenv("PATH", f"{tmp_path}:{__import__('os').environ['PATH']}")
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    import time
+    t0 = time.time()
+    traffic, why = bench.live_pmc_traffic(300, timeout_s=2)
+    assert traffic is None and "killed" in why and time.time() - t0 < 30
+
+
+def test_live_pmc_traffic_failed_pass(bench, tmp_path, monkeypatch):
+    _fake_rocprof(tmp_path, "import sys\nsys.exit(3)\n")
+    monkeypatch.setenv("PATH", f"{tmp_path}:{__import__('os').environ['PATH']}")
+    monkeypatch.setenv("TMPDIR", str(tmp_path))
+    traffic, why = bench.live_pmc_traffic(300, timeout_s=30)
+    assert traffic is None and "exited 3" in why
