@@ -1128,10 +1128,10 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
         per_row = B.m > 0 ? (double)A.nz * ((double)bnz / (double)B.m) / std::max<int32_t>(A.m, 1) : 0.0;
         b_row = B.m > 0 ? (double)bnz / (double)B.m : 0.0;
     }
-    // short products (mean <= 24 per row) of many rows: the register form
+    // short products (mean <= 40 per row) of many rows: the register form
     // when every row's columns fit it (round 5: the finest level's A P,
     // 27 M rows x 24 products, 11.4 ms in the hash form)
-    if (per_row <= 24.0 && A.m >= 100000) {
+    if (per_row <= 40.0 && A.m >= 100000) {
         const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
         const auto t0 = std::chrono::steady_clock::now();
         const unsigned g = blocks_for(A.m, 256);
