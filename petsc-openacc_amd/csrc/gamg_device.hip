@@ -805,78 +805,6 @@ __global__ __launch_bounds__(256) void k_rowprod_p0(int32_t m, const int32_t *__
     }
 }
 
-// C = A * B for short products (the finest level's A P: 7 entries x ~3.4):
-// one lane per row, the row's distinct columns (at most CAP) in registers,
-// each product a_ik b_kj added to its column in traversal order (A's row,
-// then B's) from 0.0 — the hash form's order (k_rowprod_hash: one step per
-// A entry, a B row's columns distinct within the step), so the same bits;
-// sorted by rank on the way out. Count mode: cnt[i] = distinct columns, or
-// -1 past CAP (the hash forms take the product then).
-template <int CAP, bool WRITE>
-__global__ __launch_bounds__(256) void k_rowprod_regs(int32_t m, const int32_t *__restrict__ ai,
-                                                      const int32_t *__restrict__ aj, const double *__restrict__ aa,
-                                                      const int32_t *__restrict__ bi, const int32_t *__restrict__ bj,
-                                                      const double *__restrict__ ba, const int32_t *__restrict__ ci,
-                                                      int32_t *cj, double *ca, int32_t *cnt) {
-    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    int32_t col[CAP];
-    double val[WRITE ? CAP : 1];
-#pragma unroll
-    for (int e = 0; e < CAP; ++e) col[e] = -1;
-    if constexpr (WRITE) {
-#pragma unroll
-        for (int e = 0; e < CAP; ++e) val[e] = 0.0;
-    }
-    int n = 0;
-    bool over = false;
-    const int32_t k1 = ai[i + 1];
-    for (int32_t k = ai[i]; k < k1 && !over; ++k) {
-        const int32_t j = aj[k];
-        const double a = WRITE ? aa[k] : 0.0;
-        const int32_t q1 = bi[j + 1];
-        for (int32_t q = bi[j]; q < q1; ++q) {
-            const int32_t c = bj[q];
-            const double p = WRITE ? a * ba[q] : 0.0;
-            bool hit = false;
-#pragma unroll
-            for (int e = 0; e < CAP; ++e)
-                if (col[e] == c) {
-                    if constexpr (WRITE) val[e] += p;
-                    hit = true;
-                }
-            if (hit) continue;
-            if (n == CAP) {
-                over = true;
-                break;
-            }
-#pragma unroll
-            for (int e = 0; e < CAP; ++e)
-                if (e == n) {
-                    col[e] = c;
-                    if constexpr (WRITE) val[e] += p;  // from 0.0
-                }
-            ++n;
-        }
-    }
-    if (!WRITE) {
-        cnt[i] = over ? -1 : n;
-        return;
-    }
-    const int32_t o = ci[i];
-#pragma unroll
-    for (int e = 0; e < CAP; ++e) {
-        if (e < n) {
-            int r = 0;
-#pragma unroll
-            for (int z = 0; z < CAP; ++z) r += (z < n && col[z] < col[e]);
-            cj[o + r] = col[e];
-            if constexpr (WRITE) ca[o + r] = val[e];
-        }
-    }
-}
-constexpr int kRegsCap = 32;
-
 // P = alpha (D^-1 T) + P0 on the union pattern (gamg_setup.cpp prolongator):
 // lengths, then entries.
 __global__ void k_prolong_len(int32_t m, const int32_t *__restrict__ ti, const int32_t *__restrict__ tj,
@@ -1127,59 +1055,6 @@ int rowprod(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_used) {
         }
         per_row = B.m > 0 ? (double)A.nz * ((double)bnz / (double)B.m) / std::max<int32_t>(A.m, 1) : 0.0;
         b_row = B.m > 0 ? (double)bnz / (double)B.m : 0.0;
-    }
-    // short products (mean <= 40 per row) of many rows: the register form
-    // when every row's columns fit it (round 5: the finest level's A P,
-    // 27 M rows x 24 products, 11.4 ms in the hash form)
-    if (per_row <= 40.0 && A.m >= 100000) {
-        const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
-        const auto t0 = std::chrono::steady_clock::now();
-        const unsigned g = blocks_for(A.m, 256);
-        hipLaunchKernelGGL((k_rowprod_regs<kRegsCap, false>), dim3(g), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                           B.ai, B.aj, B.aa, nullptr, nullptr, nullptr, cnt);
-        int32_t mn = -1;
-        if ((e = hipGetLastError()) != hipSuccess || (e = min_of(cnt, A.m, &mn)) != hipSuccess) {
-            hipFree(cnt);
-            return herr(e, "symbolic product");
-        }
-        if (mn >= 0) {
-            int64_t total = 0;
-            if ((e = dalloc(&C.ai, (int64_t)A.m + 1)) != hipSuccess || (e = scan_offsets(cnt, A.m, C.ai, &total)) != hipSuccess) {
-                hipFree(cnt);
-                C.release();
-                return herr(e, "product rows");
-            }
-            if (total > INT32_MAX) {
-                hipFree(cnt);
-                C.release();
-                set_error("GAMG device set-up: product exceeds int32 indices");
-                return AIJHIP_ERR_ARG;
-            }
-            C.nz = total;
-            if ((e = dalloc(&C.aj, total + 2)) != hipSuccess || (e = dalloc(&C.aa, total + 2)) != hipSuccess ||
-                (e = hipMemset(C.aj + total, 0, 2 * sizeof(int32_t))) != hipSuccess ||
-                (e = hipMemset(C.aa + total, 0, 2 * sizeof(double))) != hipSuccess) {
-                hipFree(cnt);
-                C.release();
-                return herr(e, "product alloc");
-            }
-            hipLaunchKernelGGL((k_rowprod_regs<kRegsCap, true>), dim3(g), dim3(256), 0, nullptr, A.m, A.ai, A.aj, A.aa,
-                               B.ai, B.aj, B.aa, C.ai, C.aj, C.aa, cnt);
-            e = hipGetLastError();
-            hipFree(cnt);
-            if (e != hipSuccess) {
-                C.release();
-                return herr(e, "numeric product");
-            }
-            if (cols_used) *cols_used = std::max(*cols_used, kRegsCap);
-            if (log) {
-                (void)hipDeviceSynchronize();
-                std::fprintf(stderr, "  product %d x %d: %.0f products per row, B rows %.1f -> registers: %.2f ms\n",
-                             A.m, B.n, per_row, b_row,
-                             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3);
-            }
-            return AIJHIP_OK;
-        }
     }
     {
         // G lanes per row: B's mean row length rounded up to a power of two
