@@ -498,6 +498,51 @@ def test_long_row_segments_skewed(pkg, dev, coracle):
         assert torch.equal(y1, y2)
 
 
+def test_rows_over_1024_get_their_own_block(pkg, dev, coracle, monkeypatch):
+    """kIsolateRowNnz: a row of 1025..cap entries among short rows gets a row
+    block of its own (one block more than the plain greedy cut, which
+    AIJHIP_ISOLATE_ROW_NNZ=0 restores), summed by several lanes by default
+    (within the fp64 bound) and in PETSc's order with exact = 1 (bit-exact);
+    the short rows keep PETSc's order."""
+    rng = np.random.default_rng(1024)
+    m = 4000
+    lens = rng.integers(20, 60, m)
+    lens[[500, 501, 2600]] = (1500, 3000, 1025)  # inside the 4094-entry cap
+    ai = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    aj = np.concatenate([np.sort(rng.choice(m, size=l, replace=False)) for l in lens]).astype(np.int32)
+    aa = rng.uniform(-1, 1, ai[-1])
+    x = rng.uniform(-1, 1, m)
+    ref = coracle.matmult(ai, aj, aa, x)
+    short = lens <= 1024
+    blocks = {}
+    for iso in ("0", None):
+        if iso is None:
+            monkeypatch.delenv("AIJHIP_ISOLATE_ROW_NNZ", raising=False)
+        else:
+            monkeypatch.setenv("AIJHIP_ISOLATE_ROW_NNZ", iso)
+        for exact in (0, 1):
+            y, info = mult(pkg, dev, ai, aj, aa, m, x, "stream", exact=exact, gather_sort=0, geometry=6)
+            check(y, ref, ai, aj, aa, x, exact=False)
+            if exact:
+                assert_bits(y, ref)
+            elif iso is None:  # (without isolation a long row can lift its block's mean past 128)
+                assert_bits(y, ref, short)
+            blocks[(iso, exact)] = info["n_blocks"]
+    # isolating rows 500, 501 and 2600 adds blocks (a cut before and after each)
+    assert blocks[(None, 0)] > blocks[("0", 0)] and blocks[(None, 0)] == blocks[(None, 1)]
+
+
+def test_long_overlap_auto(pkg, dev):
+    """AIJHIP_OPT_LONG_OVERLAP -1 (default): the long rows after the row
+    blocks (no side stream), except in exact mode, whose 1-4 K-entry rows keep
+    one lane's sequential sum on the side stream."""
+    ai, aj, aa = pkg.skewed_csr(300000, seed=1565)
+    for exact, want in ((0, 0), (1, 1)):
+        with pkg.SeqAIJHIP(ai, aj, aa, exact=exact) as A:
+            inf = A.info()
+            assert inf["n_long_rows"] > 0 and inf["long_overlap"] == want, (exact, inf["long_overlap"])
+
+
 @pytest.mark.parametrize("gather_sort,geometry,nt", [(-1, -1, -1), (0, -1, -1), (0, 1, 1), (0, 6, 0), (1, 6, -1)])
 def test_long_overlap_is_speed_only(pkg, dev, gather_sort, geometry, nt):
     """AIJHIP_OPT_LONG_OVERLAP: the hub segments and the wide blocks on a
