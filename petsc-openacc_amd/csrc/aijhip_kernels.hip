@@ -1398,20 +1398,6 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // at 87 VGPRs it holds 4-5 waves per SIMD against 8, and the hardware's
     // four resident workgroups per CU overlap each other's phases better,
     // profiles/r05/l/ab_pipe.jsonl; withdrawn, option 16 reserved)
-    // (experiment) AIJHIP_PLAIN_BF=1: the plain full-row blocks on the
-    // branch-free phase 1
-    static const bool plain_bf = [] {
-        const char *v = std::getenv("AIJHIP_PLAIN_BF");
-        return v && std::atoi(v) != 0;
-    }();
-    if (plain_bf && !L.ridx) {
-        if (P.tune.nt == 1) {
-            if (add) { AIJHIP_SL(true, false, 65); }
-            AIJHIP_SL(false, false, 65);
-        }
-        if (add) { AIJHIP_SL(true, false, 64); }
-        AIJHIP_SL(false, false, 64);
-    }
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
     // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)
     if (P.tune.nt == 1 && !L.ridx) {
@@ -1463,20 +1449,11 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
         return hipGetLastError();
     }
     static_assert(kNumStreamGeoms == 10, "update the geometry dispatch");
-    static const bool plain_bf = [] {
-        const char *v = std::getenv("AIJHIP_PLAIN_BF");
-        return v && std::atoi(v) != 0;
-    }();
 #define AIJHIP_OG(G)                                                                                             \
     case G:                                                                                                      \
-        if (plain_bf)                                                                                            \
-            hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 64, Op>), dim3(P.n_blocks),                 \
-                               dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,  \
-                               A.d_aj, A.d_aa, op, dpart, stop, nullptr, nullptr);                       \
-        else                                                                                                     \
-            hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_blocks),                  \
-                               dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,  \
-                               A.d_aj, A.d_aa, op, dpart, stop, nullptr, nullptr);                       \
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_blocks),                      \
+                           dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr, A.d_aj, \
+                           A.d_aa, op, dpart, stop, nullptr, nullptr);                                  \
         break
     switch (P.tune.geom) {
         AIJHIP_OG(0); AIJHIP_OG(1); AIJHIP_OG(2); AIJHIP_OG(3); AIJHIP_OG(4);
