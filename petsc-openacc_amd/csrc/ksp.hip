@@ -536,14 +536,7 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     // no-op once `done` is set.
     auto iterate = [&](hipStream_t st) -> hipError_t {
         hipError_t ie = hipSuccess;
-        // (experiment) AIJHIP_VEC_NT=0: the CG vector kernels' stores through
-        // the caches (the next kernel may read them from the Infinity Cache)
-        static const bool vec_nt = [] {
-            const char *v = std::getenv("AIJHIP_VEC_NT");
-            return !v || std::atoi(v) != 0;
-        }();
-        if (vec_nt) hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
-        else hipLaunchKernelGGL(k_aypx<false>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
+        hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
         if (K->fused) {
             ie = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, st);
             if (ie == hipSuccess)
@@ -553,10 +546,6 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             hipLaunchKernelGGL(k_dot, vg, vt, 0, st, m, K->d_p, K->d_z, K->d_part, K->d_state);
             hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, st, K->d_part, nb, K->d_state);
         }
-        if (!vec_nt)
-            hipLaunchKernelGGL(k_update<false>, vg, vt, 0, st, m, K->d_r, K->d_z, K->d_dinv, K->d_part, K->d_state,
-                               K->pc, K->d_p, nullptr);
-        else
         hipLaunchKernelGGL(k_update<true>, vg, vt, 0, st, m, K->d_r, K->d_z, K->d_dinv, K->d_part, K->d_state,
                            K->pc, K->d_p, nullptr);
         const double *pz = K->d_part;
