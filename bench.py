@@ -380,16 +380,19 @@ def pmc_traffic(rows, nnz, block):
     return rec.get("hbm_traffic_bytes_per_launch"), rec.get("source")
 
 
-def live_pmc_traffic(grid, timeout_s=150):
-    """HBM bytes per launch of the headline kernel counted in THIS run: two
-    rocprofv3 --pmc passes (FETCH_SIZE, then WRITE_SIZE: one counter group
-    each, no other tracing) over a child process that launches the same CSR
-    kernel on the same operand (tools/prof_case.py poisson, row patterns and
-    column codes off, 10 launches), corrected as MI355X_MICROARCH.md's HBM
-    section prescribes for gfx950 (read bytes = 2 x FETCH_SIZE KiB, write
-    bytes = WRITE_SIZE KiB; tools/pmc_summary.py). The child runs in its own
-    process group, killed (SIGKILL) at the time limit. Returns (bytes, detail)
-    or (None, reason)."""
+def live_pmc_traffic(grid, timeout_s=150, case="poisson", opts=("row_patterns=0", "column_codes=0"), its=10):
+    """HBM bytes per MatMult counted in THIS run: two rocprofv3 --pmc passes
+    (FETCH_SIZE, then WRITE_SIZE: one counter group each, no other tracing)
+    over a child process that launches the same kernels on the same operand
+    (tools/prof_case.py CASE: `poisson` in the CSR layout — the headline —
+    or a Flan stand-in in its default layout; `its` MatMults), corrected as
+    MI355X_MICROARCH.md's HBM section prescribes for gfx950 (read bytes =
+    2 x FETCH_SIZE KiB, write bytes = WRITE_SIZE KiB; tools/pmc_summary.py),
+    summed over the MatMult's dispatches (row blocks, long-row segments and
+    their finish) and divided by `its`. The child runs in its own process
+    group, killed (SIGKILL) at the time limit. Returns (bytes, detail) or
+    (None, reason)."""
+    import csv
     import shutil
     import signal
     import subprocess
@@ -402,8 +405,9 @@ def live_pmc_traffic(grid, timeout_s=150):
         for counter in ("FETCH_SIZE", "WRITE_SIZE"):
             out_dir = Path(td) / counter
             cmd = [exe, "--pmc", counter, "--output-format", "csv", "-d", str(out_dir), "-o", "run", "--",
-                   sys.executable, str(ROOT / "tools" / "prof_case.py"), "poisson", "--grid", str(grid), "--its", "10",
-                   "--opt", "row_patterns=0", "--opt", "column_codes=0"]
+                   sys.executable, str(ROOT / "tools" / "prof_case.py"), case, "--grid", str(grid), "--its", str(its)]
+            for o in opts:
+                cmd += ["--opt", o]
             with open(Path(td) / f"{counter}.log", "w") as log:
                 proc = subprocess.Popen(cmd, stdout=log, stderr=subprocess.STDOUT, start_new_session=True)
                 try:
@@ -416,19 +420,19 @@ def live_pmc_traffic(grid, timeout_s=150):
                 return None, f"{counter} pass exited {proc.returncode}"
             vals = []
             for f in out_dir.rglob("*counter_collection.csv"):
-                import csv
                 with open(f) as fh:
                     for row in csv.DictReader(fh):
                         k = row.get("Kernel_Name", "")
-                        if "k_spmv_stream" in k and "OpMult<false>" in k and row.get("Counter_Name") == counter:
+                        spmv = ("k_spmv_stream" in k or "k_spmv_pattern" in k) and "OpMult<false>" in k
+                        if (spmv or "k_long_partial" in k or "k_long_finish" in k) and row.get("Counter_Name") == counter:
                             vals.append(float(row["Counter_Value"]))
             if not vals:
-                return None, f"{counter}: no k_spmv_stream dispatch in the record"
-            got[counter] = (float(np.mean(vals)), len(vals))
+                return None, f"{counter}: no MatMult dispatch in the record"
+            got[counter] = (float(np.sum(vals)) / its, len(vals))
     rd = 2.0 * got["FETCH_SIZE"][0] * 1024
     wr = got["WRITE_SIZE"][0] * 1024
     return int(rd + wr), {"read_bytes": int(rd), "write_bytes": int(wr),
-                          "dispatches": [got["FETCH_SIZE"][1], got["WRITE_SIZE"][1]]}
+                          "dispatches": [got["FETCH_SIZE"][1], got["WRITE_SIZE"][1]], "matmults": its}
 
 
 def launch_times(fn, stream, reps):
@@ -1057,6 +1061,18 @@ def main():
     if rank == 0 and world == 1 and not args.no_pmc and not args.no_cpu_baseline and not under_profiler:
         progress("roofline.traffic: two rocprofv3 --pmc passes of the headline kernel")
         live_pmc = guarded("pmc", lambda: live_pmc_traffic(G))
+        if isinstance(flan, dict) and "error" not in flan:  # the stand-ins' default MatMult
+            for name in ("skewed", "fem_hex"):
+                if isinstance(flan.get(name), dict) and "stream" in flan[name]:
+                    progress(f"flan_standin.{name}: two rocprofv3 --pmc passes")
+                    t = guarded(f"pmc_{name}", lambda n=name: live_pmc_traffic(G, case=n, opts=(), its=10))
+                    rec = flan[name]["stream"]
+                    if isinstance(t, tuple) and t[0] is not None:
+                        rec["traffic"], rec["traffic_detail"] = t
+                        rec["traffic_vs_layout_bytes"] = round(t[0] / rec["layout_bytes"], 4)
+                    else:
+                        rec["traffic"] = None
+                        rec["traffic_detail"] = {"live_pmc_failed": str(t[1] if isinstance(t, tuple) else t)}
     progress("done; writing the line")
     if rank == 0:
         value = bytes_global * K / elapsed / 1e9

@@ -23,7 +23,7 @@ sys.path.insert(0, str(ROOT))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("case", choices=["gamg", "jacobi", "skewed", "skewed_nohub", "poisson"])
+    ap.add_argument("case", choices=["gamg", "jacobi", "skewed", "skewed_nohub", "poisson", "fem_hex"])
     ap.add_argument("--exact", type=int, default=0)
     ap.add_argument("--grid", type=int, default=300)
     ap.add_argument("--its", type=int, default=50)
@@ -35,9 +35,11 @@ def main():
     pkg = importlib.import_module("petsc-openacc_amd")
     K = importlib.import_module("petsc-openacc_amd.ksp")
     dev = torch.device("cuda:0")
-    if args.case in ("skewed", "skewed_nohub", "poisson"):
+    if args.case in ("skewed", "skewed_nohub", "poisson", "fem_hex"):
         if args.case == "poisson":
             ai, aj, aa = pkg.poisson_csr(args.grid)
+        elif args.case == "fem_hex":
+            ai, aj, aa = pkg.fem_hex_csr()
         else:
             ai, aj, aa = pkg.skewed_csr()
         if args.case == "skewed_nohub":  # hub rows emptied (tools/tune.py)
