@@ -134,6 +134,29 @@ def test_round4_lines_have_no_fraction_above_one():
                 assert_fracs_at_most_one(json.loads(raw))
 
 
+@pytest.mark.parametrize("rec", ["af", "al", "ao"])
+def test_round5_records_keep_the_contract(rec):
+    """Round 5's closing records (the driver's command on a GPU box): one JSON
+    line with the contract's keys, a roofline with traffic counted in the run,
+    a CPU baseline, every fraction <= 1, the default GAMG hierarchy PETSc's
+    (53 iterations) beside the greedy one."""
+    import json
+    lines = [x for x in (ROOT / "profiles" / "r05" / rec / "bench.json").read_text().splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["dtype"] == "f64" and d["config"]["workload"].startswith("300^3")
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["traffic"] and r["traffic_source"].startswith("this run")
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
+    g = d["cg_gamg"]
+    assert g["its"] == 53 and g["greedy_hierarchy"]["its"] == 57
+    assert_fracs_at_most_one(d)
+
+
 def test_rank_plan_env_contract(bench):
     """`python bench.py --gpus N` without a launcher starts N ranks with the
     torch.distributed.run environment."""
