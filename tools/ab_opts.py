@@ -28,9 +28,12 @@ def main():
     ap.add_argument("--rounds", type=int, default=30)
     ap.add_argument("--per", type=int, default=10)
     ap.add_argument("--variant", action="append", default=[], help="JSON dict of set_option NAME: VALUE")
+    ap.add_argument("--dummy-streams", type=int, default=0,
+                    help="HIP streams created (and kept) before the matrices: moves the side stream's hardware queue")
     args = ap.parse_args()
     pkg = importlib.import_module("petsc-openacc_amd")
     dev = torch.device("cuda:0")
+    dummies = [torch.cuda.Stream(device=dev) for _ in range(args.dummy_streams)]  # noqa: F841 (kept alive)
     if args.case == "poisson":
         ai, aj, aa = pkg.poisson_csr(args.grid)
     elif args.case.startswith("skewed"):
