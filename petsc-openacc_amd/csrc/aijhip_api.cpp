@@ -447,7 +447,7 @@ int plan_build(aijhip_mat *A) {
     // hides that chain (round 5: skewed stand-in default 310.7 vs 315.2 us
     // side stream; exact 350.5 us after, profiles/r05/ad/)
     if (P.tune.overlap < 0) P.tune.overlap = P.tune.exact ? 1 : 0;
-    const bool auto_sort = P.tune.gsort < 0;
+    const bool auto_sort = P.tune.gsort < 0 && !A->setup_op;  // (a set-up operator keeps the 32-bit form)
     const bool auto_codes = P.tune.codes < 0;
     const bool auto_patterns = P.tune.patterns < 0;
     bool scattered = false;
@@ -763,8 +763,15 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
     A->d_aj = d_aj;
     A->d_aa = d_aa;
     A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
-    if (!like) {  // the set-up's own operators: one copy of the entries, no codes or patterns (plan time)
-        A->requested_tune.gsort = 0;
+    A->setup_op = like ? like->setup_op : true;
+    if (!like) {  // the set-up's own operators: no codes or patterns (plan time); the gather-ordered
+        // copy for long rows, 32-bit columns where the 16-bit form does not fit (GAMG's level 1
+        // and Pᵀ) — round 5, 300³ CG + GAMG: solve 0.1652-0.1656 s vs 0.1783-0.1791 unsorted,
+        // set-up 0.167 vs 0.156-0.162 s; sorting every operator 0.169-0.170 s (the finest P,
+        // short rows, runs slower sorted); profiles/r05/as/, at/. AIJHIP_SETUP_GSORT
+        // overrides (0 off, 1 every operator).
+        const char *gs = std::getenv("AIJHIP_SETUP_GSORT");
+        A->requested_tune.gsort = gs ? std::atoi(gs) : -1;
         A->requested_tune.codes = 0;
         A->requested_tune.patterns = 0;
     }

@@ -238,6 +238,9 @@ struct aijhip_mat {
     int requested_kernel = AIJHIP_KERNEL_AUTO;
     int requested_lanes = 0;
     aijhip::Tuning requested_tune;
+    // a set-up's own operator (GAMG levels, P, Pᵀ: adopt_device_csr): long
+    // rows keep the gather-ordered copy when its 16-bit form does not fit
+    bool setup_op = false;
     // host-vector staging for aijhip_mat_mult_host (allocated on first use)
     double *d_xstage = nullptr, *d_ystage = nullptr;
     hipStream_t host_stream = nullptr;

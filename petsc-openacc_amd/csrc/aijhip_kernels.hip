@@ -1448,8 +1448,23 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
                            P.d_cmeta);
         return hipGetLastError();
     }
+    // gather-ordered blocks: the products land in their storage slots, so the
+    // fused epilogues see the same sums as from aj / aa
+    if (P.d_sidx && P.n_wblocks == 0 && P.tune.geom == 6) {  // 16-bit columns (planned at geometry 6)
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, 80, Op>), dim3(P.n_blocks),
+                           dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,
+                           reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa, op, dpart, stop, nullptr,
+                           P.d_sbase);
+        return hipGetLastError();
+    }
+    if (P.d_sslot && P.d_saj && P.tune.geom == 6) {  // 32-bit sorted columns
+        hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, 8, Op>), dim3(P.n_blocks),
+                           dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,
+                           P.d_saj, P.d_saa, op, dpart, stop, P.d_sslot, nullptr);
+        return hipGetLastError();
+    }
     static_assert(kNumStreamGeoms == 10, "update the geometry dispatch");
-#define AIJHIP_OG(G)                                                                                             \
+#define AIJHIP_OG(G)                                                                                          \
     case G:                                                                                                      \
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(G), false, 0, Op>), dim3(P.n_blocks),                      \
                            dim3(kStreamGeoms[G].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr, A.d_aj, \

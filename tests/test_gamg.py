@@ -252,6 +252,37 @@ def test_gpu_cg_gamg_fused_default_deterministic_and_values_update(pkg):
     assert fresh2[0] != first[0] or not np.array_equal(fresh2[2], first[2])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("N", [24, 48])
+def test_gpu_cg_gamg_gather_ordered_levels_bitwise(pkg, N, monkeypatch):
+    """The set-up's operators (levels, P, Pᵀ) with the gather-ordered copy
+    (each block's entries sorted by column, products stored at their CSR
+    slots; the fused V-cycle launches take the sorted arrays too) — on long
+    rows (the default), on none (AIJHIP_SETUP_GSORT=0) or on every operator
+    (1) — solve bit for bit the same."""
+    torch = pytest.importorskip("torch")
+    assert torch.cuda.is_available()
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    ai, aj, aa = pkg.poisson_csr(N)
+    rhs, _ = pkg.poisson_vectors(N)
+    b = torch.from_numpy(rhs).cuda()
+    out = []
+    for gs in ("0", None, "1"):
+        if gs is None:
+            monkeypatch.delenv("AIJHIP_SETUP_GSORT", raising=False)
+        else:
+            monkeypatch.setenv("AIJHIP_SETUP_GSORT", gs)
+        with pkg.SeqAIJHIP(ai, aj, aa) as A:
+            x = torch.empty_like(b)
+            with K.KSPCG(A, pc="gamg", rtol=1e-14, atol=1e-12) as ksp:
+                ksp.solve(b, x)
+                out.append((ksp.its, np.array(ksp.history()), x.cpu().numpy()))
+    for its, h, xv in out[1:]:
+        assert its == out[0][0]
+        assert np.array_equal(h.view(np.uint64), out[0][1].view(np.uint64))
+        assert np.array_equal(xv.view(np.uint64), out[0][2].view(np.uint64))
+
+
 def test_oracle_vcycle_preconditions_cg():
     ai, aj, aa, rhs, exact = seqaij.create_system(10, 10, 10)
     m = len(ai) - 1

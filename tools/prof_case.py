@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--exact", type=int, default=0)
     ap.add_argument("--grid", type=int, default=300)
     ap.add_argument("--its", type=int, default=50)
+    ap.add_argument("--solves", type=int, default=1, help="solves timed after the set-up (gamg / jacobi)")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--opt", action="append", default=[], help="set_option NAME=VALUE (repeatable)")
     ap.add_argument("--gamg-opt", action="append", default=[],
@@ -85,7 +86,15 @@ def main():
     ksp.solve(b, x)
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    print(f"{args.case}: set-up {t1 - t0:.3f} s, solve {t2 - t1:.4f} s, its {ksp.its}, reason {ksp.reason}")
+    print(f"{args.case}: set-up {t1 - t0:.3f} s, solve {t2 - t1:.4f} s, its {ksp.its}, reason {ksp.reason}, "
+          f"x bits {int(x.view(torch.int64).sum()) & 0xffffffffffff:012x}")
+    for _ in range(args.solves - 1):  # the same solve again from x = 0
+        x.zero_()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ksp.solve(b, x)
+        torch.cuda.synchronize()
+        print(f"{args.case}: solve again {time.perf_counter() - t1:.4f} s")
     ksp.destroy()
     A.destroy()
 

@@ -4,7 +4,11 @@ count and mean duration, and the idle time between consecutive kernels
 (start of one minus end of the previous) over the last N kernels — the
 launch gaps a hipGraph or fewer launches would remove.
 
-    python3 tools/trace_gaps.py DIR [--last N]
+    python3 tools/trace_gaps.py DIR [--last N] [--span-ms MS] [--by-grid]
+
+--span-ms keeps the kernels that start in the trace's last MS milliseconds
+(a solve at the end of the run); --by-grid splits a kernel name by its grid
+size (the levels of a GAMG hierarchy launch the same kernels).
 """
 import argparse
 import csv
@@ -16,15 +20,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--last", type=int, default=1000)
+    ap.add_argument("--span-ms", type=float, default=0.0)
+    ap.add_argument("--by-grid", action="store_true")
     a = ap.parse_args()
     rows = []
     for f in Path(a.dir).rglob("*kernel_trace.csv"):
         with open(f) as fh:
             for r in csv.DictReader(fh):
                 name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("aijhip::", "")
-                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name.split("(")[0][-90:]))
+                name = name.split("(")[0][-90:]
+                if a.by_grid:
+                    name = f"{name} [grid {r['Grid_Size_X']}]"
+                rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
     rows.sort()
-    rows = rows[-a.last:]
+    if a.span_ms > 0:
+        rows = [q for q in rows if q[0] >= rows[-1][1] - a.span_ms * 1e6]
+    else:
+        rows = rows[-a.last:]
     busy = sum(e - s for s, e, _ in rows)
     span = rows[-1][1] - rows[0][0]
     gaps = defaultdict(list)
