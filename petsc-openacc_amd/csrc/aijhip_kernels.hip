@@ -789,46 +789,87 @@ __global__ __launch_bounds__(256) void k_block_xrange(const BlockDesc *__restric
 }  // namespace
 
 // Gather-ordered row blocks (Tuning::gsort): one workgroup sorts its
-// block's entries by column (ties by position; bitonic over the next power
-// of two) and writes the sorted columns, the values in that order and each
-// entry's position in the block. x is then gathered in column order — a
-// wave's 64 lanes read a few x lines instead of one per scattered node —
-// while the products land at their storage positions, so the row sums (and
-// their bits) are the unsorted kernel's.
-template <int N>
-__global__ __launch_bounds__(256) void k_block_gather_order(const BlockDesc *__restrict__ blk,
-                                                            const int32_t *__restrict__ aj,
-                                                            const double *__restrict__ aa, int32_t *saj,
-                                                            double *saa, uint16_t *sslot) {
+// block's entries by column (ties by position: the keys are unique) and
+// writes the sorted columns, the values in that order and each entry's
+// position in the block. x is then gathered in column order — a wave's 64
+// lanes read a few x lines instead of one per scattered node — while the
+// products land at their storage positions, so the row sums (and their bits)
+// are the unsorted kernel's.
+// The sort: bitonic over N keys, lane t holding keys [tE, tE + E) in
+// registers; the stages whose partner lies in another lane go through LDS
+// (one barrier each), the last log2(E) stages of every merge stay in
+// registers (round 5: the set-up's long-row operators are sorted by default,
+// and the LDS-only form — 256 lanes, every stage through LDS — took 17 ms of
+// the 300³ GAMG set-up).
+template <int E>
+__device__ __forceinline__ void bitonic_lane_stage(unsigned long long (&v)[E], int base, int k, int j) {
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int pe = e ^ j;
+        if (pe > e) {
+            const bool up = ((base + e) & k) == 0;
+            const unsigned long long a = v[e], b = v[pe];
+            if ((a > b) == up) {
+                v[e] = b;
+                v[pe] = a;
+            }
+        }
+    }
+}
+
+template <int N, int TB>
+__global__ __launch_bounds__(TB) void k_block_gather_order(const BlockDesc *__restrict__ blk,
+                                                           const int32_t *__restrict__ aj,
+                                                           const double *__restrict__ aa, int32_t *saj,
+                                                           double *saa, uint16_t *sslot) {
+    constexpr int E = N / TB;
+    static_assert(E >= 2 && (E & (E - 1)) == 0 && N <= 65536, "keys per lane: a power of two; 16-bit slots");
     __shared__ unsigned long long key[N];
     const BlockDesc d = blk[blockIdx.x];
-    const int t = threadIdx.x;
-    int n2 = 2;
-    while (n2 < d.nk) n2 <<= 1;
-    for (int i = t; i < n2; i += 256)
-        key[i] = i < d.nk ? ((unsigned long long)(uint32_t)aj[(int64_t)d.k0 + i] << 16) | (unsigned)i : ~0ull;
-    __syncthreads();
-    for (int k = 2; k <= n2; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = t; i < n2; i += 256) {
-                const int ixj = i ^ j;
-                if (ixj > i) {
-                    const unsigned long long a = key[i], b = key[ixj];
-                    if ((a > b) == ((i & k) == 0)) {
-                        key[i] = b;
-                        key[ixj] = a;
-                    }
+    const int t = threadIdx.x, base = t * E;
+    unsigned long long v[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = base + e;
+        v[e] = i < d.nk ? ((unsigned long long)(uint32_t)aj[(int64_t)d.k0 + i] << 16) | (unsigned)i : ~0ull;
+    }
+#pragma unroll
+    for (int k = 2; k <= E; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1) bitonic_lane_stage<E>(v, base, k, j);
+    for (int k = 2 * E; k <= N; k <<= 1) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) key[base + e] = v[e];
+        __syncthreads();
+        for (int j = k >> 1; j >= E; j >>= 1) {
+#pragma unroll
+            for (int q = 0; q < E / 2; ++q) {
+                const int p = t + q * TB;  // pair p: i has bit j clear, its partner i | j
+                const int i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), ixj = i | j;
+                const unsigned long long a = key[i], b = key[ixj];
+                if ((a > b) == ((i & k) == 0)) {
+                    key[i] = b;
+                    key[ixj] = a;
                 }
             }
             __syncthreads();
         }
-    for (int i = t; i < d.nk; i += 256) {
-        const unsigned long long v = key[i];
-        const int slot = (int)(v & 0xffffu);
-        const int64_t k = (int64_t)d.k0 + i;
-        saj[k] = (int32_t)(v >> 16);
-        sslot[k] = (uint16_t)slot;
-        saa[k] = aa[(int64_t)d.k0 + slot];
+#pragma unroll
+        for (int e = 0; e < E; ++e) v[e] = key[base + e];
+#pragma unroll
+        for (int j = E >> 1; j > 0; j >>= 1) bitonic_lane_stage<E>(v, base, k, j);
+        __syncthreads();  // every lane's reads done before the next merge's writes
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) {
+        const int i = base + e;
+        if (i < d.nk) {
+            const int slot = (int)(v[e] & 0xffffu);
+            const int64_t k = (int64_t)d.k0 + i;
+            saj[k] = (int32_t)(v[e] >> 16);
+            sslot[k] = (uint16_t)slot;
+            saa[k] = aa[(int64_t)d.k0 + slot];
+        }
     }
 }
 
@@ -954,8 +995,8 @@ hipError_t build_gather_order(const aijhip_mat &A, const Plan &P, bool values_on
     }
     const int cap = kStreamGeoms[P.tune.geom].nnz_cap;
 #define AIJHIP_GO(NN)                                                                                       \
-    hipLaunchKernelGGL(k_block_gather_order<NN>, dim3(P.n_blocks), dim3(256), 0, nullptr, P.d_blocks, A.d_aj, \
-                       A.d_aa, P.d_saj, P.d_saa, P.d_sslot)
+    hipLaunchKernelGGL((k_block_gather_order<NN, 512>), dim3(P.n_blocks), dim3(512), 0, nullptr, P.d_blocks, \
+                       A.d_aj, A.d_aa, P.d_saj, P.d_saa, P.d_sslot)
     if (cap <= 1024) AIJHIP_GO(1024);
     else if (cap <= 2048) AIJHIP_GO(2048);
     else if (cap <= 4096) AIJHIP_GO(4096);
