@@ -475,7 +475,8 @@ int plan_build(aijhip_mat *A) {
         // ordinary rows 342 -> 256, the FEM-structured one 287 -> 271
         // (profiles/r03/gsort_*.jsonl); the 7-pt Poisson (short rows) stays
         // unsorted (sorted: 551 vs 492 us). The set-up's own operators (GAMG
-        // levels: gsort 0) keep one copy of their entries.
+        // levels, P, Pᵀ; aijhip_mat::setup_op) take it for long rows too and
+        // keep the 32-bit sorted columns when the 16-bit form does not fit.
         if (P.tune.gsort < 0) P.tune.gsort = long_rows ? 1 : 0;
         const bool sorted = P.tune.gsort > 0;
         if (P.tune.geom < 0) P.tune.geom = (scattered && !sorted) ? 1 : 6;

@@ -102,8 +102,9 @@ struct Tuning {
                            // same box interleaved: side 315.1, serial 310.2 us (profiles/r05/ac/)
     int host_chunk = -1;   // host-vector MatMult: -1 pipelined in ~1M-row chunks, 0 serial (step-2 form),
                            // k > 0 pipelined in chunks of >= k rows
-    int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd): -1 auto
-                           // (operands with scattered gathers, caller's handles), 0 off, 1 on
+    int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd and the
+                           // fused V-cycle launches): -1 auto (long rows; a caller's handle only
+                           // in the 16-bit form), 0 off, 1 on
     int codes = -1;        // 16-bit column codes instead of aj (Plan::d_code): -1 auto (where the
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
