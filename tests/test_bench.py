@@ -134,7 +134,7 @@ def test_round4_lines_have_no_fraction_above_one():
                 assert_fracs_at_most_one(json.loads(raw))
 
 
-@pytest.mark.parametrize("rec", ["af", "al", "ao", "av"])
+@pytest.mark.parametrize("rec", ["af", "al", "ao", "av", "ax"])
 def test_round5_records_keep_the_contract(rec):
     """Round 5's closing records (the driver's command on a GPU box): one JSON
     line with the contract's keys, a roofline with traffic counted in the run,
