@@ -4,37 +4,42 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--grid 300] [--layout csr|auto]
 
 A step is one MatMult (y = A x) of the whole operand, inputs resident in HBM.
-N = 1: the BASELINE.json configs[1] workload — 300^3 Poisson CSR (27 M rows,
-188.46 M entries, fp64 values, int32 indices) on one MI355X.
-N > 1: one rank per GPU over RCCL. Launched by torch.distributed.run, or by
+The workload at every N is BASELINE.json configs[1]: 300^3 Poisson CSR (27 M
+rows, 188.46 M entries, fp64 values, int32 indices).
+N = 1: MatMult_SeqAIJ on one MI355X.
+N > 1: the SAME operand row-partitioned over N GPUs in balanced whole
+z-planes (strong scaling — the reference's own sweep, runs/single-node-
+scaling.pbs:56-67, `aprun -n 16/8/4/2/1 ... -da_grid_x 300`), one rank per
+GPU over RCCL: MatMult_MPIAIJ, the halo planes exchanged while the diagonal
+block multiplies (csrc/ksp_mpi.hip). Launched by torch.distributed.run, or by
 this script itself: `python bench.py --gpus N` with no WORLD_SIZE in the
 environment starts the N rank processes (before any GPU call) and prints rank
-0's line (the reference's rank sweep, runs/single-node-scaling.pbs:56-67, is
-its job script's; here the bench owns it). Weak scaling — every rank owns a
-300^3-row z-slab; the global grid doubles one axis per factor 2 of N (z, then
-y, then x): N = 2 is 300x300x600, N = 4 300x600x600, N = 8 the 600^3 grid of
-BASELINE configs[3] (75 planes of 600^2 per rank). The halo planes are
-exchanged over RCCL while the diagonal block multiplies (csrc/ksp_mpi.hip).
-The same line carries `strong_300`: the 300^3 operand itself row-partitioned
-over the N GPUs (the north star's "300^3 matrix at 1, 2, 4 and 8 GPUs"), and
-per rank the halo cost of both exchange forms (p2p send/recv, all-gather).
+0's line. Beside `value`, the `weak` block is BASELINE configs[3]: every rank
+a 300^3-row z-slab of a grid that doubles one axis per factor 2 of N (N = 8:
+the 600^3 grid), and per rank the halo cost of every exchange form.
 
 The headline MatMult reads PETSc's CSR as stored (ai / aj / aa; --layout
 csr, the default): the metric is a CSR SpMV. The library's automatic layout
 (row patterns for a stencil: no aj at all) is timed beside it in the
 `effective` block, on its own bytes, and is never `value`.
 
-value  = algorithmic bytes of all ranks x K / (max-over-ranks wall time of the
-         K timed steps), bytes per SpMV = 12 nnz + 4 (m+1) + 8 n + 8 m
-         (x and the matrix read once, y written once).
-roofline.achieved = the compulsory bytes of the layout the timed kernel reads
-         (aijhip_info_t.mult_layout_bytes: the CSR bytes above for --layout
-         csr) per launch / the mean duration of the launch, from HIP events
+value  = algorithmic bytes of the whole operand x K / (max-over-ranks wall
+         time of the K timed steps), bytes per SpMV = 12 nnz + 4 (m+1) + 8 n
+         + 8 m (x and the matrix read once, y written once).
+roofline.achieved = the compulsory bytes of the layout rank 0's timed launch
+         reads (aijhip_info_t.mult_layout_bytes: the CSR bytes above for
+         --layout csr) / the mean duration of the launch, from HIP events
          recorded around every launch on the stream it runs on; peak 8 TB/s
          (MI355X_MICROARCH.md). Every `frac` in the line is bytes the timed
          kernel moves / its time / 8 TB/s.
 cpu_baseline = the C restatement of PETSc's MatMult_SeqAIJ (oracle/, a port:
-         the reference cannot be built here) on 1 host core, bounded sample.
+         the reference cannot be built here) on 1 host core and on all the
+         process's threads, bounded samples of the whole 300^3 operand, rank
+         0 at every N.
+Every leg beside the headline has a wall budget (Legs): a leg that cannot
+fit in what is left of --wall-budget is recorded as {"error": "budget"}, and
+a leg still running at the deadline is cut the same way; the line is always
+printed.
 """
 from __future__ import annotations
 
@@ -44,6 +49,7 @@ import importlib
 import json
 import os
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -94,10 +100,12 @@ def parse():
                    help="skip the live rocprofv3 --pmc passes for roofline.traffic (use the committed record)")
     p.add_argument("--roofline-reps", type=int, default=50,
                    help="launches timed by HIP events for roofline.achieved (at least this many, SURVEY §8d)")
-    p.add_argument("--no-strong", action="store_true", help="N > 1: skip the strong-scaling 300^3 line")
-    p.add_argument("--strong-grid", type=int, default=None,
-                   help="edge of the strong-scaling operand (default: --grid); a one-GPU rehearsal of the N = 8 "
-                        "run keeps the strong line at 300^3 (38/37 planes per rank) with a small weak grid")
+    p.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling block (BASELINE configs[3])")
+    p.add_argument("--weak-grid", type=int, default=None,
+                   help="per-rank edge of the weak-scaling block (default: --grid; N = 8 -> 600^3)")
+    p.add_argument("--wall-budget", type=float, default=420.0,
+                   help="seconds from the start barrier after which no leg starts and a running leg is cut "
+                        "(the line is still printed; per-leg budgets in leg_budgets)")
     p.add_argument("--mpi", action="store_true",
                    help="take the multi-GPU code path (MPIAIJ, RCCL, distributed CG) even at N = 1 "
                         "(launch with torch.distributed.run): a one-GPU rehearsal of the N > 1 run")
@@ -632,45 +640,255 @@ def gather_forms(mine, world):
     return res
 
 
-def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm):
-    """The G^3 operand (300^3: BASELINE configs[1]) row-partitioned over all
-    ranks in balanced whole z-planes (DMDA PETSC_DECIDE), timed like the main
-    line: K distributed SpMVs between barriers, max over ranks. Strong
-    scaling: the total work is the N = 1 workload's. Both halo forms are
-    timed per rank (halo_forms); the headline form is --halo."""
+class Legs:
+    """Per-leg wall budgets and a hard deadline.
+
+    Every leg beside the headline runs through run(name, budget_s, fn): it
+    starts only if every rank still has at least budget_s of the run's wall
+    budget (--wall-budget, counted from the start barrier) left — the ranks
+    agree on the minimum, so all skip or all start — else it is recorded as
+    {"error": "budget"} and not started. A leg that is still running at the
+    deadline is cut by the watchdog: rank 0 writes the line built so far with
+    that leg as {"error": "budget"}, and every rank exits (the ranks share the
+    deadline, so none is left waiting in a collective). A heartbeat line on
+    stderr every 60 s names the leg each rank is in."""
+
+    def __init__(self, total_s, rank, world, distributed, dev, progress, line_fd):
+        self.total_s, self.rank, self.world, self.distributed, self.dev = total_s, rank, world, distributed, dev
+        self.progress, self.line_fd = progress, line_fd
+        self.t0 = time.time()
+        self.deadline = self.t0 + total_s
+        self.log = {}
+        self.current = None
+        self.out = None  # rank 0: the line built so far
+        self.headline_done = False
+        self._lock = threading.Lock()
+        self._written = False
+        self._timer = None
+
+    def remaining(self) -> float:
+        return self.deadline - time.time()
+
+    def _all_min(self, v: float) -> float:
+        if not self.distributed:
+            return v
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([v], dtype=torch.float64, device=self.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        return float(t.item())
+
+    def run(self, name, budget_s, fn, collective=True):
+        """collective=False: a leg one rank runs alone (no agreement)."""
+        rem = self._all_min(self.remaining()) if collective else self.remaining()
+        if rem < budget_s:
+            self.log[name] = {"budget_s": budget_s, "status": "skipped", "remaining_s": round(rem, 1)}
+            self.progress(f"{name}: skipped, {rem:.0f} s of the wall budget left < its {budget_s} s")
+            res = {"error": "budget", "budget_s": budget_s, "remaining_s": round(rem, 1),
+                   "note": "not started: less than this leg's budget was left of the run's --wall-budget"}
+        else:
+            self.current = name
+            t = time.perf_counter()
+            res = guarded_leg(name, fn, self.distributed and collective, self.dev, self.progress)
+            took = time.perf_counter() - t
+            self.current = None
+            self.log[name] = {"budget_s": budget_s, "took_s": round(took, 1),
+                              "status": "ok" if took <= budget_s else "over"}
+        if self.out is not None:
+            self.out[name] = res
+        return res
+
+    def summary(self, cut=None) -> dict:
+        d = {"wall_budget_s": self.total_s, "elapsed_s": round(time.time() - self.t0, 1), "legs": dict(self.log)}
+        if cut is not None:
+            d["legs"][cut] = {"status": "cut at the deadline"}
+        return d
+
+    def emit(self, obj) -> bool:
+        """Write the line (rank 0, exactly once)."""
+        with self._lock:
+            if self._written:
+                return False
+            self._written = True
+        os.write(self.line_fd, (json.dumps(obj) + "\n").encode())
+        return True
+
+    def arm(self):
+        """Start the watchdog and the heartbeat (daemon threads)."""
+        def fire():
+            cut = self.current
+            self.progress(f"wall budget ({self.total_s:.0f} s) reached in leg {cut!r}: writing the line and exiting")
+            if self.rank == 0:
+                if self.out is not None:
+                    part = dict(self.out)
+                    if cut is not None:
+                        part[cut] = {"error": "budget", "note": "cut at the run's --wall-budget deadline"}
+                    part["budget"] = self.summary(cut)
+                else:
+                    part = {"metric": METRIC, "value": None, "unit": "GB/s", "n_gpus": self.world,
+                            "error": "budget: the wall budget ran out before the headline was measured",
+                            "budget": self.summary(cut)}
+                self.emit(part)
+            sys.stderr.flush()
+            os._exit(0 if self.headline_done else 1)
+
+        self._timer = threading.Timer(max(0.0, self.remaining()), fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+        def beat():
+            while True:
+                time.sleep(60.0)
+                self.progress(f"heartbeat: in {self.current or 'the headline / between legs'}")
+        threading.Thread(target=beat, daemon=True).start()
+
+    def disarm(self):
+        if self._timer is not None:
+            self._timer.cancel()
+
+
+def guarded_leg(name, fn, distributed, dev, progress):
+    """Run one leg; an exception raised alike on every rank (a bug, an
+    allocation failure) is recorded in the line instead of discarding the
+    headline measurement, and every rank learns whether any rank failed, so
+    none waits on a peer that gave up."""
+    progress(name)
+    try:
+        res, ok = fn(), 1.0
+    except Exception as e:  # noqa: BLE001
+        print(f"bench: {name} failed: {e!r}", file=sys.stderr, flush=True)
+        res, ok = {"error": f"{type(e).__name__}: {e}"[:300]}, 0.0
+    if distributed:
+        import torch
+        import torch.distributed as dist
+        flag = torch.tensor([ok], dtype=torch.float64, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if float(flag.item()) < 1.0 and ok:
+            res = {"error": "failed on another rank"}
+    return res
+
+
+METRIC = "CSR SpMV effective HBM GB/s (300^3 7-pt Poisson, fp64 MatMult_SeqAIJ)"
+
+
+def slab_row_starts(mpiaij, dims, world):
+    """Balanced whole z-planes (DMDA PETSC_DECIDE over z, helper.cpp:31-36
+    with a 1x1xP process grid): (row_starts[world + 1], [(z0, z1)] per rank)."""
+    nx, ny, nz = dims
+    bounds = [mpiaij.slab_bounds(nz, world, r) for r in range(world)]
+    starts = np.array([b[0] * nx * ny for b in bounds] + [nx * ny * nz], dtype=np.int64)
+    return starts, bounds
+
+
+def headline_line(*, world, dims, nnz_global, K, warmup, elapsed_s, launch_us, layout_bytes, info, distributed,
+                  halo, x_kind, planes=None):
+    """The contract fields of the one JSON line (pure: tests/test_bench.py
+    checks it without a GPU). value = the whole operand's algorithmic bytes x
+    K / the max-over-ranks wall time of the K timed steps. At N > 1 the
+    operand is the same G^3 one row-partitioned over the N GPUs — strong
+    scaling, the reference's own sweep (runs/single-node-scaling.pbs:56-67:
+    aprun -n 1..16 ... -da_grid_x 300): `value` at every N is the metric's
+    300^3 MatMult, comparable across N. roofline = the layout bytes rank 0's
+    launch moves / the mean HIP-event time of its launches."""
+    nx, ny, nz = dims
+    n_global = nx * ny * nz
+    bytes_global = 12 * nnz_global + 4 * (n_global + 1) + 8 * n_global + 8 * n_global
+    launch_us = np.asarray(launch_us, dtype=np.float64)
+    mean_s = float(np.mean(launch_us)) * 1e-6
+    achieved = layout_bytes / mean_s / 1e9
+    value = bytes_global * K / elapsed_s / 1e9
+    csr = not (info.get("row_patterns") or info.get("column_codes"))
+    if distributed:
+        workload = (f"{nx}x{ny}x{nz} Poisson CSR MatMult row-partitioned over {world} GPU"
+                    f"{'s' if world > 1 else ''} in z-slabs of {planes} planes (BASELINE configs[1] strong-scaled, "
+                    f"the reference's 1-16 rank sweep at 300^3)")
+    else:
+        workload = f"{nx}x{ny}x{nz} Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])"
+    if nx == ny == nz:
+        workload = f"{nx}^3" + workload[len(f"{nx}x{ny}x{nz}"):]
+    block = {k: info.get(k) for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "nt_loads", "column_codes",
+                                      "row_patterns")}
+    return {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": warmup,
+        "ms_per_step": round(elapsed_s / K * 1e3, 4),
+        "ms_per_step_median_launch": round(float(np.median(launch_us[:K])) / 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": ("synthetic (generated 7-pt Poisson operand of helper.cpp; x = splitmix64 uniform[-1,1))"
+                 if x_kind == "uniform" else "synthetic (helper.cpp operand; x = generateExt field)"),
+        "config": {
+            "workload": workload, "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
+            "kernel": info.get("kernel"), "layout": layout_name(info), "halo": halo if distributed else None,
+            "block": block, "bytes_per_spmv": bytes_global, "flops_per_spmv_petsc": 2 * nnz_global - n_global,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "traffic_source": None,
+            "traffic_detail": None,
+            "kernel": ("k_spmv_stream (CSR: aj / aa pairs, x gathered, LDS row sums)" if csr else layout_name(info)),
+            "kernel_us_mean": round(mean_s * 1e6, 2),
+            "kernel_us_median": round(float(np.median(launch_us)), 2),
+            "kernel_us_min": round(float(np.min(launch_us)), 2),
+            "launches_timed": int(len(launch_us)),
+            "achieved_from_median": round(layout_bytes / (float(np.median(launch_us)) * 1e-6) / 1e9, 1),
+            "bytes_per_launch": layout_bytes,
+            "layout": layout_name(info),
+            "note": ("rank 0's distributed MatMult (exchange + A_d + A_o) on rank 0's bytes"
+                     if distributed else "bytes the timed kernel moves / mean HIP-event launch time"),
+        },
+    }
+
+
+def cpu_spmv_baselines(pkg, G, seconds):
+    """cpu_baseline (1 core) and cpu_baseline_all_cores (the OpenMP form on
+    every thread this process may use) of the oracle's MatMult_SeqAIJ loop on
+    the whole G^3 operand, x = the headline's splitmix x (a port: the
+    reference cannot be built here). Rank 0 only, at every N."""
+    ai, aj, aa = pkg.poisson_csr(G)
+    m = len(ai) - 1
+    x = pkg.splitmix_uniform(m, 42)
+    nbytes = pkg.algorithmic_bytes(m, m, len(aj))
+    t1, reps1, _ = cpu_baseline(ai, aj, aa, x, seconds)
+    tn, repsn, threads = cpu_baseline(ai, aj, aa, x, seconds / 2, all_cores=True)
+    one = {"value": round(nbytes / t1 / 1e9, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+           "sample": f"{reps1} whole-operand {G}^3 SpMVs on 1 core ({cpu_model()}), {t1 * 1e3:.1f} ms each; "
+                     f"oracle/matmult_seqaij.c"}
+    alln = {"value": round(nbytes / tn / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"{repsn} whole-operand {G}^3 SpMVs, OpenMP static row blocks on {threads} threads, "
+                      f"{tn * 1e3:.1f} ms each; oracle/matmult_seqaij.c oracle_matmult_seqaij_omp"}
+    return one, alln
+
+
+def build_dist_operator(pkg, mpiaij, make_local, dims, world, rank, dev, comm):
+    """This rank's z-slab of the nx x ny x nz operand as the native MPIAIJ
+    (built with the all-gather halo; its p2p twin shares A_d, so both exchange
+    forms run on one diagonal block). Returns (op, slab record)."""
     import torch
     import torch.distributed as dist
-    bounds = [mpiaij.slab_bounds(G, world, r) for r in range(world)]
-    row_starts = np.array([b[0] * G * G for b in bounds] + [G ** 3], dtype=np.int64)
+    row_starts, bounds = slab_row_starts(mpiaij, dims, world)
     z0, z1 = bounds[rank]
-    ai, aj, aa = pkg.poisson_csr(G, G, G, z0, z1)
-    nnz_loc = len(aj)
+    ai, aj, aa = pkg.poisson_csr(*dims, z0, z1)
     op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo="allgather", comm=comm)
-    nat = op.native if args.halo == "allgather" else op.p2p_native()
-    layout_local = op.A_d.info()["mult_layout_bytes"]
     nnz_t = torch.tensor([len(aj)], dtype=torch.float64, device=dev)
     dist.all_reduce(nnz_t)
-    nnz = int(nnz_t.item())
-    del ai, aj, aa
-    stream = torch.cuda.current_stream()
-    x = torch.from_numpy(pkg.splitmix_uniform(op.mloc, 42, int(row_starts[rank]))).to(dev)
-    y = torch.empty(op.mloc, dtype=torch.float64, device=dev)
-    for _ in range(args.warmup):
-        nat.mult(x, y, stream)
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        nat.mult(x, y, stream)
-    torch.cuda.synchronize()
-    dist.barrier()
-    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    dt = float(el.item()) / args.steps
-    forms = gather_forms(halo_forms(op, x, stream, max(args.steps, 20), rank, dev, op.mloc, nnz_loc), world)
-    nbytes = pkg.algorithmic_bytes(G ** 3, G ** 3, nnz)
-    lt = torch.tensor([float(layout_local)], dtype=torch.float64, device=dev)
-    dist.all_reduce(lt)
+    slab = {"z0": z0, "z1": z1, "row_starts": row_starts, "nnz_local": len(aj), "nnz_global": int(nnz_t.item()),
+            "csr": (ai, aj, aa)}
+    return op, slab
+
+
+def destroy_dist_operator(op):
     op.native.destroy()
     if op._twin is not None:
         op._twin[1].destroy()
@@ -679,13 +897,50 @@ def strong_300(pkg, mpiaij, make_local, G, world, rank, dev, args, comm):
     op.A_d.destroy()
     if op.A_o is not None:
         op.A_o.destroy()
-    return {"workload": f"{G}^3 Poisson CSR row-partitioned over {world} GPUs "
-                        f"({z1 - z0} of {G} z-planes on rank {rank})",
-            "scaling": "strong", "value": round(nbytes / dt / 1e9, 2), "unit": "GB/s",
-            # the bytes the ranks' diagonal blocks read (CSR with --layout csr)
-            # over N HBM peaks
+
+
+def weak_block(pkg, mpiaij, make_local, Gw, world, rank, dev, args, comm):
+    """BASELINE configs[3] (beside the headline, not
+    `value`): weak scaling, every rank a Gw^3-row z-slab of weak_grid(Gw, N)
+    (N = 8, Gw = 300: the 600^3 grid), timed like the headline — K
+    distributed MatMults between barriers, max over ranks — with both halo
+    forms per rank."""
+    import torch
+    import torch.distributed as dist
+    dims = weak_grid(Gw, world)
+    op, slab = build_dist_operator(pkg, mpiaij, make_local, dims, world, rank, dev, comm)
+    try:
+        nat = op.native if args.halo == "allgather" else op.p2p_native()
+        layout_local = op.A_d.info()["mult_layout_bytes"]
+        stream = torch.cuda.current_stream()
+        x = torch.from_numpy(pkg.splitmix_uniform(op.mloc, 42, int(slab["row_starts"][rank]))).to(dev)
+        y = torch.empty(op.mloc, dtype=torch.float64, device=dev)
+        for _ in range(args.warmup):
+            nat.mult(x, y, stream)
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            nat.mult(x, y, stream)
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dt = float(el.item()) / args.steps
+        forms = gather_forms(halo_forms(op, x, stream, max(args.steps, 20), rank, dev, op.mloc, slab["nnz_local"]),
+                             world)
+        lt = torch.tensor([float(layout_local)], dtype=torch.float64, device=dev)
+        dist.all_reduce(lt)
+        del x, y
+    finally:
+        destroy_dist_operator(op)
+    n = dims[0] * dims[1] * dims[2]
+    nbytes = pkg.algorithmic_bytes(n, n, slab["nnz_global"])
+    return {"workload": f"{dims[0]}x{dims[1]}x{dims[2]} Poisson CSR, {slab['z1'] - slab['z0']}-plane z-slab "
+                        f"({op.mloc} rows) per GPU (BASELINE configs[3] at N = 8)",
+            "scaling": "weak", "value": round(nbytes / dt / 1e9, 2), "unit": "GB/s",
             "frac": round(float(lt.item()) / dt / 1e9 / (HBM_PEAK_GBS * world), 4),
-            "ms_per_step": round(dt * 1e3, 4), "rows": G ** 3, "nnz": nnz, "halo": args.halo,
+            "ms_per_step": round(dt * 1e3, 4), "rows": n, "nnz": slab["nnz_global"], "halo": args.halo,
             "halo_forms": forms}
 
 
@@ -698,6 +953,17 @@ def layout_name(info) -> str:
     if info.get("gather_sorted"):
         return "gather-ordered copy of the CSR row blocks"
     return "CSR (PETSc's ai / aj / aa as stored)"
+
+
+def leg_budgets(distributed):
+    """Seconds each leg may need (a leg starts only with this much of the
+    wall budget left). Measured on MI355X (profiles/r05, r06): the N = 1 legs
+    take 2-25 s each; the distributed CG + GAMG set-up at 27 M rows per rank
+    is the largest (profiles/r06)."""
+    if distributed:
+        return {"cg": 60, "weak": 150, "cg_gamg": 240, "cpu_baseline": 60}
+    return {"cg": 60, "cg_gamg": 180, "host_vec": 60, "read_ceiling": 30, "flan_standin": 120, "pmc": 200,
+            "pmc_skewed": 120, "pmc_fem_hex": 120, "cpu_baseline": 60}
 
 
 def main():
@@ -762,27 +1028,15 @@ def main():
         C = importlib.import_module("petsc-openacc_amd.comm")
         comm = (C.Comm.host(device=local_rank, timeout_s=args.comm_timeout) if args.rehearse_one_gpu
                 else C.Comm.rccl(device=local_rank, timeout_s=args.comm_timeout))
+        dist.barrier()
+    legs = Legs(args.wall_budget, rank, world, distributed, dev, progress, line_fd)
+    legs.arm()
+    budget = leg_budgets(distributed)
 
     G = args.grid
-    nx, ny, nz_global = weak_grid(G, world) if distributed else (G, G, G)
-    planes = nz_global // world
-    row_starts = np.array([r * planes * nx * ny for r in range(world + 1)], dtype=np.int64)
-    z0, z1 = rank * planes, (rank + 1) * planes
-    progress(f"operand {nx}x{ny}x{nz_global}, planes {z0}..{z1}")
-    t_setup = time.perf_counter()
-    ai, aj, aa = pkg.poisson_csr(nx, ny, nz_global, z0, z1)
-    m_loc = len(ai) - 1
-    n_global = nx * ny * nz_global
-    nnz_loc = len(aj)
-
-    if args.x == "exact":
-        _, x_h = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
-    else:
-        x_h = pkg.splitmix_uniform(m_loc, 42, int(row_starts[rank]))
+    dims = (G, G, G)
     stream = torch.cuda.current_stream()
-    xd = torch.from_numpy(x_h).to(dev)
-    yd = torch.empty(m_loc, dtype=torch.float64, device=dev)
-
+    t_setup = time.perf_counter()
     if distributed:
         from importlib import import_module
         mpiaij = import_module("petsc-openacc_amd.mpiaij")
@@ -790,33 +1044,38 @@ def main():
         def make_local(a_i, a_j, a_a, ncols):
             return configure(pkg.SeqAIJHIP(a_i, a_j, a_a, ncols=ncols, device=local_rank, kernel=args.kernel))
 
-        # built with the all-gather halo; its p2p twin shares A_d, so both
-        # exchange forms are timed on one diagonal block (halo_forms)
-        op = mpiaij.MPIAIJ(ai, aj, aa, row_starts, make_local, pkg.split_rows, dev, halo="allgather", comm=comm)
+        op, slab = build_dist_operator(pkg, mpiaij, make_local, dims, world, rank, dev, comm)
+        z0, z1 = slab["z0"], slab["z1"]
+        progress(f"operand {G}^3 strong-scaled, planes {z0}..{z1}")
+        ai, aj, aa = slab.pop("csr")
+        m_loc, nnz_loc, nnz_global = op.mloc, slab["nnz_local"], slab["nnz_global"]
+        x_off = int(slab["row_starts"][rank])
         nat = op.native if args.halo == "allgather" else op.p2p_native()
         info = op.A_d.info()
-        step = lambda: nat.mult(xd, yd, stream)  # noqa: E731
-    else:
-        A = configure(pkg.SeqAIJHIP(ai, aj, aa, ncols=m_loc, device=local_rank, kernel=args.kernel))
-        info = A.info()
-        step = lambda: A.mult(xd, yd, stream)  # noqa: E731
-    torch.cuda.synchronize()
-    t_setup = time.perf_counter() - t_setup
-
-    # global algorithmic bytes per distributed SpMV (halo bytes not counted)
-    nnz_t = torch.tensor([nnz_loc], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(nnz_t)
-    nnz_global = int(nnz_t.item())
-    bytes_global = pkg.algorithmic_bytes(n_global, n_global, nnz_global)
-    bytes_local = pkg.algorithmic_bytes(m_loc, m_loc, nnz_loc)
-    # what the timed kernel moves: the layout's compulsory bytes (the CSR
-    # bytes above for --layout csr; distributed: A_d's layout + A_o as CSR)
-    if distributed:
+        # what the timed launch moves: A_d's layout + A_o as CSR (its rows, ghosts)
         layout_bytes = info["mult_layout_bytes"] + (pkg.algorithmic_bytes(m_loc, m_loc, op.nz_o) - 4 * (m_loc + 1)
                                                      - 16 * m_loc + 8 * op.n_ghost if op.nz_o else 0)
     else:
+        z0, z1 = 0, G
+        progress(f"operand {G}^3")
+        ai, aj, aa = pkg.poisson_csr(G)
+        m_loc = len(ai) - 1
+        nnz_loc = nnz_global = len(aj)
+        x_off = 0
+        A = configure(pkg.SeqAIJHIP(ai, aj, aa, ncols=m_loc, device=local_rank, kernel=args.kernel))
+        info = A.info()
         layout_bytes = info["mult_layout_bytes"]
+    planes = z1 - z0
+    if args.x == "exact":
+        _, x_h = pkg.poisson_vectors(G, G, G, z0, z1)
+    else:
+        x_h = pkg.splitmix_uniform(m_loc, 42, x_off)
+    xd = torch.from_numpy(x_h).to(dev)
+    yd = torch.empty(m_loc, dtype=torch.float64, device=dev)
+    step = (lambda: nat.mult(xd, yd, stream)) if distributed else (lambda: A.mult(xd, yd, stream))
+    torch.cuda.synchronize()
+    t_setup = time.perf_counter() - t_setup
+    bytes_local = pkg.algorithmic_bytes(m_loc, m_loc, nnz_loc)
 
     progress("operator ready; warm-up")
     for _ in range(args.warmup):
@@ -845,37 +1104,42 @@ def main():
     elapsed = float(el_t.item())
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
 
-    ranks = forms = None
-    if distributed:
-        # Evidence the exchange hides behind the diagonal block: both halo
-        # forms against the same launches of A_d alone, per rank
-        progress("halo forms")
-        mine = halo_forms(op, xd, stream, K, rank, dev, m_loc, nnz_loc)
-        forms = gather_forms(mine, world)
-        ranks = forms[args.halo]["ranks"]
-
     # roofline sample: at least --roofline-reps launches (SURVEY §8d asks
     # for the median of >= 50), the K timed ones plus more if K is smaller
     extra = max(0, args.roofline_reps - K)
-    if extra and not distributed:
-        ev_x = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(extra)]
-        for a, b in ev_x:
-            a.record(stream)
-            step()
-            b.record(stream)
-        torch.cuda.synchronize()
-        launch_ms = np.concatenate([launch_ms, [a.elapsed_time(b) for a, b in ev_x]])
+    if extra:
+        launch_ms = np.concatenate([launch_ms, np.array(launch_times(step, stream, extra)) / 1e3])
 
     # correctness spot-check of the timed output against a fresh multiply
     y_chk = yd.clone()
     step()
     torch.cuda.synchronize()
     stable = bool(torch.equal(y_chk, yd))
+    out = headline_line(world=world, dims=dims, nnz_global=nnz_global, K=K, warmup=args.warmup, elapsed_s=elapsed,
+                        launch_us=launch_ms * 1e3, layout_bytes=layout_bytes, info=info, distributed=distributed,
+                        halo=args.halo, x_kind=args.x, planes=planes)
+    out["result_stable"] = stable
+    out["setup_s"] = round(t_setup, 2)
+    legs.headline_done = True
+    if rank == 0:
+        legs.out = out
+
+    forms = None
+    if distributed:
+        # Evidence the exchange hides behind the diagonal block: both halo
+        # forms against the same launches of A_d alone, per rank
+        progress("halo forms")
+        forms = gather_forms(halo_forms(op, xd, stream, K, rank, dev, m_loc, nnz_loc), world)
+        out["aggregate_frac"] = round(out["value"] / (HBM_PEAK_GBS * world), 4)
+        out["distributed"] = distributed_block(world, dist.get_backend(), comm.info(), args.comm_timeout,
+                                               forms[args.halo]["ranks"])
+        out["distributed"]["halo_forms"] = forms
+        if args.rehearse_one_gpu:
+            out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
 
     # The library's automatic layout (row patterns for the stencil: no aj)
     # timed beside the CSR headline in the same run, on ITS bytes; its y must
     # be the headline's bits. It is not a CSR measurement and never `value`.
-    effective = None
     if not distributed and csr_forced:
         def effective_layout():
             set_layout(A, False)
@@ -899,29 +1163,7 @@ def main():
                     "note": "NOT a CSR SpMV: this layout does not read aj (the bytes it moves are bytes_per_launch; "
                             "frac is on those). csr_equivalent_GBs = the CSR bytes over the same time, for "
                             "comparison only. The CG / CG+GAMG legs below run on this layout."}
-        effective = effective_layout()
-
-    # The measurements beside the headline one are guarded: an exception
-    # raised alike on every rank (a bug, an allocation failure) is recorded
-    # in the line instead of discarding the headline measurement.
-    def guarded(name, fn):
-        progress(name)
-        try:
-            res, ok = fn(), 1.0
-        except Exception as e:  # noqa: BLE001
-            print(f"bench: {name} failed: {e!r}", file=sys.stderr, flush=True)
-            res, ok = {"error": f"{type(e).__name__}: {e}"[:300]}, 0.0
-        if distributed:  # every rank learns whether any rank failed, so none waits on a peer that gave up
-            flag = torch.tensor([ok], dtype=torch.float64, device=dev)
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if float(flag.item()) < 1.0 and ok:
-                res = {"error": "failed on another rank"}
-        return res
-
-    strong = None
-    if distributed and not args.no_strong:
-        G_s = args.strong_grid or G
-        strong = guarded("strong_300", lambda: strong_300(pkg, mpiaij, make_local, G_s, world, rank, dev, args, comm))
+        out["effective"] = effective_layout()
 
     # the solver legs run on the automatic layout (what a caller gets)
     if distributed and csr_forced:
@@ -932,17 +1174,17 @@ def main():
 
     def single_cg():
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
-        out = ksp.bench_cg(pkg, A, nx, ny, nz_global, dev, iters=args.cg_iters)
-        out["layout"] = solver_layout
+        res = ksp.bench_cg(pkg, A, G, G, G, dev, iters=args.cg_iters)
+        res["layout"] = solver_layout
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_cg_baseline(ai, aj, aa, pkg, nx, ny, nz_global)
-        return out
+            res["cpu_baseline"] = cpu_cg_baseline(ai, aj, aa, pkg, G, G, G)
+        return res
 
     def distributed_cg():
         # row-partitioned CG+Jacobi: dots all-reduced over RCCL
         # aijhip_kspmpi: scalar steps on the device, RCCL all-reduces of device
         # doubles on the compute stream, host polls every 8 iterations
-        rhs_h, _ = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
+        rhs_h, _ = pkg.poisson_vectors(G, G, G, z0, z1)
         b = torch.from_numpy(rhs_h).to(dev)
         xs = torch.zeros_like(b)
         cgm = C.KSPCGMPINative(nat, rtol=0.0, atol=0.0, max_it=5)
@@ -957,29 +1199,29 @@ def main():
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dt = float(el.item())
         its = cgm.its
-        out = {"iters": its, "seconds": round(dt, 4), "iters_per_s": round(its / dt, 2),
+        res = {"iters": its, "seconds": round(dt, 4), "iters_per_s": round(its / dt, 2),
                "ms_per_iter": round(dt / its * 1e3, 4), "pc": "jacobi (bjacobi+jacobi per rank)",
                "reductions": "2 all-reduces per iteration (" + ("host transport over gloo" if args.rehearse_one_gpu
                                                                  else "RCCL, device doubles") +
                              ("; skipped at one rank" if world == 1 else "") + ")",
                "host_syncs": cgm.host_syncs, "halo": args.halo, "solver": "aijhip_kspmpi (native)",
                "layout": solver_layout,
-               "workload": f"{nx}x{ny}x{nz_global} Poisson, {planes}-plane z-slab per GPU"}
+               "workload": f"{G}^3 Poisson, {planes}-plane z-slab on rank 0 of {world}"}
         cgm.destroy()
-        return out
+        return res
 
     def distributed_cg_gamg():
         # CG + PCGAMG across the ranks (csrc/gamg_mpi.hip: one distributed
         # hierarchy, as PETSc's agg GAMG on MPIAIJ), the reference's
         # tolerances, from x = 0; the hierarchy's level halos are p2p plans
-        rhs_h, exact_h = pkg.poisson_vectors(nx, ny, nz_global, z0, z1)
+        rhs_h, exact_h = pkg.poisson_vectors(G, G, G, z0, z1)
         b = torch.from_numpy(rhs_h).to(dev)
         xs = torch.zeros_like(b)
         kg = C.KSPCGMPINative(op.p2p_native(), rtol=1e-14, atol=1e-12, max_it=10000, pc="gamg")
         dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        kg.solve(b, xs)  # first solve: includes the per-rank GAMG set-up
+        kg.solve(b, xs)  # first solve: includes the GAMG set-up
         torch.cuda.synchronize()
         t_first = time.perf_counter() - t0
         xs.zero_()
@@ -996,152 +1238,102 @@ def main():
         err = torch.tensor([float((xs.cpu() - torch.from_numpy(exact_h)).abs().max())], dtype=torch.float64,
                            device=dev)
         dist.all_reduce(err, op=dist.ReduceOp.MAX)
-        out = {"its": kg.its, "reason": kg.reason, "rnorm": kg.rnorm, "max_err": float(err.item()),
+        res = {"its": kg.its, "reason": kg.reason, "rnorm": kg.rnorm, "max_err": float(err.item()),
                "setup_s": round(float(tt[0].item()) - float(tt[1].item()), 3), "solve_s": round(float(tt[1].item()), 4),
                "time_to_solution_s": round(float(tt[0].item()), 3),
                "ms_per_iter": round(float(tt[1].item()) / max(kg.its, 1) * 1e3, 3), "host_syncs": syncs,
                "levels": [{"rows": int(r), "nnz": int(z)} for r, z in zip(rows_l, nnz_l)],
                "pc": ("PCGAMG across ranks (aggregates per rank, P and Galerkin products over the MPIAIJ "
-                      "operator, csrc/gamg_mpi.hip)" if world > 1 else "PCGAMG (single-GPU set-up)"),
-               "options": "rtol 1e-14 atol 1e-12", "workload": f"{nx}x{ny}x{nz_global} Poisson",
+                      "operator, csrc/gamg_mpi.hip)" if world > 1 or os.environ.get("AIJHIP_GAMG_DIST") == "1"
+                      else "PCGAMG (single-GPU set-up)"),
+               "options": "rtol 1e-14 atol 1e-12", "workload": f"{G}^3 Poisson over {world} GPU(s)",
                "layout": solver_layout, "halo": "p2p (the p2p twin of the operator; shares A_d)"}
         kg.destroy()
-        return out
+        return res
 
     def single_cg_gamg():
         ksp = importlib.import_module("petsc-openacc_amd.ksp")
-        out = ksp.bench_cg_gamg(pkg, A, nx, ny, nz_global, dev)
-        out["layout"] = solver_layout
-        out["hierarchy"] = ("PETSc 3.7 agg restated (the default since round 5): MIS of the squared graph "
+        res = ksp.bench_cg_gamg(pkg, A, G, G, G, dev)
+        res["layout"] = solver_layout
+        res["hierarchy"] = ("PETSc 3.7 agg restated (the default since round 5): MIS of the squared graph "
                             "(finest level) in a hashed random order, smoothAggs, then MIS of the graph; emax "
                             "from CG's Lanczos tridiagonal (coarsen 1, eig_ksp 1)")
         # the greedy hierarchy beside it (the default through round 4; VERDICT
         # r04 item 5: both measured, the faster is the default)
-        greedy = ksp.bench_cg_gamg(pkg, A, nx, ny, nz_global, dev, gamg=dict(coarsen=0, eig_ksp=0), light=True)
+        greedy = ksp.bench_cg_gamg(pkg, A, G, G, G, dev, gamg=dict(coarsen=0, eig_ksp=0), light=True)
         greedy["hierarchy"] = "greedy aggregation in natural order, power-iteration emax (coarsen 0, eig_ksp 0)"
-        out["greedy_hierarchy"] = greedy
+        res["greedy_hierarchy"] = greedy
         if "error" not in greedy:  # like for like: each hierarchy's second set-up in the process + its solve
-            out["hierarchy_comparison"] = {
-                "default_mis_s": round(out["setup_again_s"] + out["solve_s"], 4),
+            res["hierarchy_comparison"] = {
+                "default_mis_s": round(res["setup_again_s"] + res["solve_s"], 4),
                 "greedy_s": round(greedy["setup_again_s"] + greedy["solve_s"], 4),
                 "note": "set-up again (warm: the first set-up of the process also pays one-time costs, and the "
                         "greedy leg runs after the default one) + solve, seconds"}
-        print(f"bench: CG+GAMG {out['its']} its, solve {out['solve_s']} s, set-up {out['setup_s']} s",
+        print(f"bench: CG+GAMG {res['its']} its, solve {res['solve_s']} s, set-up {res['setup_s']} s",
               file=sys.stderr, flush=True)
         # BASELINE configs[0] (100^3) on the device as well, beside its 1-core host solve
         s_ai, s_aj, s_aa = pkg.poisson_csr(100)
         with pkg.SeqAIJHIP(s_ai, s_aj, s_aa, device=local_rank) as A100:
             small = ksp.bench_cg_gamg(pkg, A100, 100, 100, 100, dev)
-        out["configs0_device"] = {k: small[k] for k in ("its", "reason", "max_err", "setup_s", "solve_s",
+        res["configs0_device"] = {k: small[k] for k in ("its", "reason", "max_err", "setup_s", "solve_s",
                                                         "time_to_solution_s")}
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_cg_gamg_baseline(ai, aj, aa, pkg, nx, ny, nz_global)
-        return out
+            res["cpu_baseline"] = cpu_cg_gamg_baseline(ai, aj, aa, pkg, G, G, G)
+        return res
 
-    cg = None
     if not args.no_cg:
-        cg = guarded("cg", distributed_cg if distributed else single_cg)
-    cg_gamg = None
+        legs.run("cg", budget["cg"], distributed_cg if distributed else single_cg)
+    if distributed and world > 1 and not args.no_weak:
+        legs.run("weak", budget["weak"],
+                 lambda: weak_block(pkg, mpiaij, make_local, args.weak_grid or G, world, rank, dev, args, comm))
     if not args.no_gamg:
-        cg_gamg = guarded("cg_gamg", distributed_cg_gamg if distributed else single_cg_gamg)
-    host_vec = None
-    if not distributed and not args.no_host_vec:
-        host_vec = guarded("host_vec", lambda: host_vec_mult(A, x_h))
-
-    ceiling = None
+        legs.run("cg_gamg", budget["cg_gamg"], distributed_cg_gamg if distributed else single_cg_gamg)
+    ceiling = flan = live_pmc = None
     if not distributed:
-        ceiling = guarded("read_ceiling", lambda: read_ceiling(bytes_local, dev))
-    flan = None
-    if not distributed and not args.no_flan:
-        flan = guarded("flan_standin", lambda: flan_standins(pkg, dev, max(args.roofline_reps, 50),
-                                                             not args.no_cpu_baseline))
+        if not args.no_host_vec:
+            legs.run("host_vec", budget["host_vec"], lambda: host_vec_mult(A, x_h))
+        ceiling = legs.run("read_ceiling", budget["read_ceiling"], lambda: read_ceiling(bytes_local, dev))
+        out.pop("read_ceiling", None)
+        if not args.no_flan:
+            flan = legs.run("flan_standin", budget["flan_standin"],
+                            lambda: flan_standins(pkg, dev, max(args.roofline_reps, 50), not args.no_cpu_baseline))
+        under_profiler = any(k.startswith("ROCPROF") for k in os.environ)  # (never nest a profiler)
+        if rank == 0 and not args.no_pmc and not args.no_cpu_baseline and not under_profiler:
+            progress("roofline.traffic: two rocprofv3 --pmc passes of the headline kernel")
+            live_pmc = legs.run("pmc", budget["pmc"], lambda: live_pmc_traffic(G))
+            out.pop("pmc", None)
+            if isinstance(flan, dict) and "error" not in flan:  # the stand-ins' default MatMult
+                for name in ("skewed", "fem_hex"):
+                    if isinstance(flan.get(name), dict) and "stream" in flan[name]:
+                        t = legs.run(f"pmc_{name}", budget[f"pmc_{name}"],
+                                     lambda n=name: live_pmc_traffic(G, case=n, opts=(), its=10))
+                        out.pop(f"pmc_{name}", None)
+                        rec = flan[name]["stream"]
+                        if isinstance(t, tuple) and t[0] is not None:
+                            rec["traffic"], rec["traffic_detail"] = t
+                            rec["traffic_vs_layout_bytes"] = round(t[0] / rec["layout_bytes"], 4)
+                        else:
+                            rec["traffic"] = None
+                            rec["traffic_detail"] = {"live_pmc_failed": str(t[1] if isinstance(t, tuple) else t)}
 
-    live_pmc = None
-    under_profiler = any(k.startswith("ROCPROF") for k in os.environ)  # (never nest a profiler)
-    if rank == 0 and world == 1 and not args.no_pmc and not args.no_cpu_baseline and not under_profiler:
-        progress("roofline.traffic: two rocprofv3 --pmc passes of the headline kernel")
-        live_pmc = guarded("pmc", lambda: live_pmc_traffic(G))
-        if isinstance(flan, dict) and "error" not in flan:  # the stand-ins' default MatMult
-            for name in ("skewed", "fem_hex"):
-                if isinstance(flan.get(name), dict) and "stream" in flan[name]:
-                    progress(f"flan_standin.{name}: two rocprofv3 --pmc passes")
-                    t = guarded(f"pmc_{name}", lambda n=name: live_pmc_traffic(G, case=n, opts=(), its=10))
-                    rec = flan[name]["stream"]
-                    if isinstance(t, tuple) and t[0] is not None:
-                        rec["traffic"], rec["traffic_detail"] = t
-                        rec["traffic_vs_layout_bytes"] = round(t[0] / rec["layout_bytes"], 4)
-                    else:
-                        rec["traffic"] = None
-                        rec["traffic_detail"] = {"live_pmc_failed": str(t[1] if isinstance(t, tuple) else t)}
     progress("done; writing the line")
-    if rank == 0:
-        value = bytes_global * K / elapsed / 1e9
-        mean_launch_s = float(np.mean(launch_ms)) / 1e3
-        achieved = layout_bytes / mean_launch_s / 1e9
-        block = {k: info[k] for k in ("stream_threads", "stream_nnz_cap", "stream_rows", "nt_loads", "column_codes",
-                                      "row_patterns")}
-        traffic, traffic_src = (None, None) if distributed else pmc_traffic(n_global, nnz_global, block)
-        pmc_detail = None
+    if distributed:
+        dist.barrier()
+    if rank == 0 and not distributed:
+        r = out["roofline"]
+        block = out["config"]["block"]
+        r["traffic"], r["traffic_source"] = pmc_traffic(G ** 3, nnz_global, block)
         if isinstance(live_pmc, tuple) and live_pmc[0] is not None and not info.get("row_patterns") \
                 and not info.get("column_codes"):
-            traffic, pmc_detail = live_pmc
-            traffic_src = ("this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (one counter group each) of "
-                           "tools/prof_case.py poisson in the CSR layout, gfx950-corrected (2 x FETCH_SIZE KiB + "
-                           "WRITE_SIZE KiB), mean over the kernel's dispatches")
+            r["traffic"], r["traffic_detail"] = live_pmc
+            r["traffic_source"] = ("this run: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (one counter group "
+                                   "each) of tools/prof_case.py poisson in the CSR layout, gfx950-corrected "
+                                   "(2 x FETCH_SIZE KiB + WRITE_SIZE KiB), mean over the kernel's dispatches")
         elif live_pmc is not None:
-            pmc_detail = {"live_pmc_failed": str(live_pmc[1] if isinstance(live_pmc, tuple) else live_pmc)}
-        out = {
-            "metric": "CSR SpMV effective HBM GB/s (300^3 7-pt Poisson, fp64 MatMult_SeqAIJ)",
-            "value": round(value, 2),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / K * 1e3, 4),
-            "ms_per_step_median_launch": round(float(np.median(launch_ms[:K])), 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (generated 7-pt Poisson operand of helper.cpp; x = splitmix64 uniform[-1,1))"
-            if args.x == "uniform" else "synthetic (helper.cpp operand; x = generateExt field)",
-            "config": {
-                "workload": f"{nx}x{ny}x{nz_global} Poisson CSR, {planes}-plane z-slab ({m_loc} rows) per GPU"
-                if distributed
-                else f"{G}^3 Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])",
-                "rows": n_global, "nnz": nnz_global, "index": "int32", "values": "fp64",
-                "kernel": info["kernel"], "layout": layout_name(info), "halo": args.halo if distributed else None,
-                "block": block,
-                "bytes_per_spmv": bytes_global, "flops_per_spmv_petsc": 2 * nnz_global - n_global,
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "traffic_detail": pmc_detail,
-                "kernel": ("k_spmv_stream (CSR: aj / aa pairs, x gathered, LDS row sums)"
-                           if not (info.get("row_patterns") or info.get("column_codes")) else layout_name(info)),
-                "kernel_us_mean": round(mean_launch_s * 1e6, 2),
-                "kernel_us_median": round(float(np.median(launch_ms)) * 1e3, 2),
-                "kernel_us_min": round(float(np.min(launch_ms)) * 1e3, 2),
-                "launches_timed": int(len(launch_ms)),
-                "achieved_from_median": round(layout_bytes / (float(np.median(launch_ms)) / 1e3) / 1e9, 1),
-                "bytes_per_launch": layout_bytes,
-                "layout": layout_name(info),
-                "note": ("rank 0's distributed MatMult (exchange + A_d + A_o) on rank 0's bytes"
-                         if distributed else "bytes the timed kernel moves / mean HIP-event launch time"),
-            },
-            "result_stable": stable,
-            "setup_s": round(t_setup, 2),
-        }
-        if effective is not None:
-            out["effective"] = effective
+            r["traffic_detail"] = {"live_pmc_failed": str(live_pmc[1] if isinstance(live_pmc, tuple) else live_pmc)}
         if isinstance(ceiling, dict) and "error" not in ceiling:  # same-run flat reads of the same bytes
-            out["roofline"]["ceiling_flat_read"] = {
+            achieved = r["achieved"]
+            r["ceiling_flat_read"] = {
                 "GBs": ceiling[0][0], "us": ceiling[0][1], "frac_of_ceiling": round(achieved / ceiling[0][0], 4),
                 "probe": "aijhip_read_probe mode 0: the SpMV's CSR byte count read once, non-temporal 16-B loads, "
                          "512-lane workgroups of two loads per lane (the fastest shape, tools/read_sweep.hip); "
@@ -1149,43 +1341,18 @@ def main():
                 "stream_shape_read": {"GBs": ceiling[1][0], "us": ceiling[1][1],
                                       "frac": round(achieved / ceiling[1][0], 4),
                                       "probe": "mode 1: plain loads, four per lane (the STREAM kernel's shape)"}}
-        if distributed:  # whole-job rate against N HBM peaks (roofline.frac: rank 0's launch alone)
-            out["aggregate_frac"] = round(value / (HBM_PEAK_GBS * world), 4)
-            out["distributed"] = distributed_block(world, dist.get_backend(), comm.info(), args.comm_timeout, ranks)
-            out["distributed"]["halo_forms"] = forms
-        if args.rehearse_one_gpu:
-            out["rehearsal"] = f"{world} ranks sharing cuda:0 over gloo: control flow only, not a scaling number"
-        if strong is not None:
-            out["strong_300"] = strong
-        if cg is not None:
-            out["cg"] = cg
-        if cg_gamg is not None:
-            out["cg_gamg"] = cg_gamg
-        if host_vec is not None:
-            out["host_vec"] = host_vec
-        if flan is not None:
-            out["flan_standin"] = flan
-        if not args.no_cpu_baseline and not distributed:
-            t_cpu, reps, _ = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds)
-            out["cpu_baseline"] = {
-                "value": round(bytes_local / t_cpu / 1e9, 3),
-                "unit": "GB/s",
-                "cores": 1,
-                "kind": "port",
-                "sample": f"{reps} whole-operand {G}^3 SpMVs on 1 core ({cpu_model()}), "
-                          f"{t_cpu * 1e3:.1f} ms each; oracle/matmult_seqaij.c",
-            }
-            t_all, reps_all, threads = cpu_baseline(ai, aj, aa, x_h, args.cpu_seconds / 2, all_cores=True)
-            out["cpu_baseline_all_cores"] = {
-                "value": round(bytes_local / t_all / 1e9, 3),
-                "unit": "GB/s",
-                "cores": threads,
-                "kind": "port",
-                "sample": f"{reps_all} whole-operand {G}^3 SpMVs, OpenMP static row blocks on {threads} threads, "
-                          f"{t_all * 1e3:.1f} ms each; oracle/matmult_seqaij.c oracle_matmult_seqaij_omp",
-            }
-        os.write(line_fd, (json.dumps(out) + "\n").encode())
-
+    # the host baselines last: at N > 1 the other ranks are done with the GPU
+    # by now, and rank 0 times the oracle on the whole G^3 operand
+    if rank == 0 and not args.no_cpu_baseline:
+        del ai, aj, aa
+        base = legs.run("cpu_baseline", budget["cpu_baseline"],
+                        lambda: cpu_spmv_baselines(pkg, G, args.cpu_seconds), collective=False)
+        if isinstance(base, tuple):
+            out["cpu_baseline"], out["cpu_baseline_all_cores"] = base
+    if rank == 0:
+        out["budget"] = legs.summary()
+        legs.emit(out)
+    legs.disarm()
     if distributed:
         dist.destroy_process_group()
 

@@ -246,3 +246,78 @@ def test_live_pmc_traffic_failed_pass(bench, tmp_path, monkeypatch):
     monkeypatch.setenv("TMPDIR", str(tmp_path))
     traffic, why = bench.live_pmc_traffic(300, timeout_s=30)
     assert traffic is None and "exited 3" in why
+
+
+def test_headline_line_n8_is_the_300_cubed_operand(bench):
+    """at N > 1 `value` is the metric's 300^3 MatMult
+    strong-scaled over the N GPUs (the reference's sweep), not a weak-scaled
+    larger grid: 27,000,000 rows, 188,460,000 entries, SURVEY §8d's bytes."""
+    info = {"kernel": "stream", "stream_threads": 512, "stream_nnz_cap": 4094, "stream_rows": 512, "nt_loads": 0,
+            "column_codes": 0, "row_patterns": 0, "gather_sorted": 0}
+    line = bench.headline_line(world=8, dims=(300, 300, 300), nnz_global=188_460_000, K=20, warmup=5,
+                               elapsed_s=20 * 70e-6, launch_us=[70.0] * 20, layout_bytes=350_190_000, info=info,
+                               distributed=True, halo="p2p", x_kind="uniform", planes=38)
+    c = line["config"]
+    assert c["rows"] == 27_000_000 and c["nnz"] == 188_460_000 and c["bytes_per_spmv"] == 2_801_520_004
+    assert c["workload"].startswith("300^3") and "over 8 GPUs" in c["workload"]
+    assert line["scaling"] == "strong" and line["n_gpus"] == 8
+    assert abs(line["value"] - 2_801_520_004 / 70e-6 / 1e9) < 0.01
+    assert abs(line["roofline"]["achieved"] - 350_190_000 / 70e-6 / 1e9) < 0.1
+    one = bench.headline_line(world=1, dims=(300, 300, 300), nnz_global=188_460_000, K=20, warmup=5,
+                              elapsed_s=20 * 480e-6, launch_us=[478.0] * 20, layout_bytes=2_801_520_004, info=info,
+                              distributed=False, halo="p2p", x_kind="uniform")
+    assert one["config"]["workload"].startswith("300^3 Poisson CSR MatMult_SeqAIJ (BASELINE configs[1])")
+    assert one["config"]["halo"] is None and one["scaling"] == "strong"
+    assert_fracs_at_most_one(line)
+    assert_fracs_at_most_one(one)
+
+
+def test_legs_skip_what_cannot_fit(bench):
+    """A leg starts only with its budget left (else {"error": "budget"}, the
+    function never called); a leg that ran is logged with its time."""
+    import os
+    calls = []
+    legs = bench.Legs(5.0, 0, 1, False, None, lambda m: None, os.dup(1))
+    legs.out = {}
+    r = legs.run("gamg", 60, lambda: calls.append(1))
+    assert r["error"] == "budget" and not calls and legs.out["gamg"] is r
+    assert legs.log["gamg"]["status"] == "skipped"
+    r = legs.run("cg", 1, lambda: {"iters": 3})
+    assert r == {"iters": 3} and legs.log["cg"]["status"] == "ok"
+    r = legs.run("bad", 1, lambda: 1 / 0)
+    assert r["error"].startswith("ZeroDivisionError")
+    s = legs.summary()
+    assert s["wall_budget_s"] == 5.0 and set(s["legs"]) == {"gamg", "cg", "bad"}
+
+
+WATCHDOG_CHILD = r'''
+import importlib.util, sys, time
+spec = importlib.util.spec_from_file_location("bench_mod", sys.argv[1])
+b = importlib.util.module_from_spec(spec); spec.loader.exec_module(b)
+legs = b.Legs(1.0, 0, 1, False, None, lambda m: print(m, file=sys.stderr), 1)
+legs.out = {"metric": b.METRIC, "value": 5000.0, "cg": {"iters": 200}}
+legs.headline_done = True
+legs.arm()
+legs.current = "cg_gamg"
+time.sleep(30)
+print("not reached")
+'''
+
+
+def test_watchdog_prints_the_line_and_exits(bench):
+    """A leg still running at the deadline: rank 0 writes the line so far with
+    that leg as {"error": "budget"} and the process exits 0 (the headline was
+    measured) well before the leg would have finished."""
+    import json
+    import subprocess
+    import sys
+    import time
+    t0 = time.time()
+    p = subprocess.run([sys.executable, "-c", WATCHDOG_CHILD, str(ROOT / "bench.py")], capture_output=True,
+                       text=True, timeout=60)
+    assert p.returncode == 0 and time.time() - t0 < 25
+    lines = [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1 and "not reached" not in p.stdout
+    d = lines[0]
+    assert d["value"] == 5000.0 and d["cg"] == {"iters": 200}
+    assert d["cg_gamg"]["error"] == "budget" and d["budget"]["legs"]["cg_gamg"]["status"] == "cut at the deadline"

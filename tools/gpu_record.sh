@@ -7,8 +7,8 @@
 #   usage: tools/gpu_record.sh TAG [--no-tests] [--no-full-prof] [--n8]
 # --n8: also the eight-rank rehearsal of the driver's N = 8 run on this one
 # GPU (--gpus 8 --rehearse-one-gpu: the self-launcher's 8 children, the
-# 38/37-plane strong_300 split, both halo forms, the distributed CG and
-# CG + GAMG legs) at a weak grid of 100^3 per rank.
+# 38/37-plane 300^3 strong split (the headline), both halo forms, the distributed CG and
+# CG + GAMG legs) with a weak block of 100^3 per rank.
 set -o pipefail
 TAG=${1:-record}; shift
 TESTS=1; FULLPROF=1; N8=0
@@ -34,7 +34,7 @@ timeout -k 10 600 python -u bench.py --gpus 2 --rehearse-one-gpu --steps 10 --wa
     > "$OUT/bench_rehearse_n2.json" 2> "$OUT/bench_rehearse_n2.err" \
     && echo "rehearsal n2 ok" || { tail -20 "$OUT/bench_rehearse_n2.err"; exit 1; }
 if [ $N8 = 1 ]; then
-  timeout -k 10 900 python -u bench.py --gpus 8 --rehearse-one-gpu --grid 100 --strong-grid 300 --steps 20 \
+  timeout -k 10 900 python -u bench.py --gpus 8 --rehearse-one-gpu --weak-grid 100 --steps 20 \
       --warmup 3 > "$OUT/bench_rehearse_n8.json" 2> "$OUT/bench_rehearse_n8.err" \
       && echo "rehearsal n8 ok" || { tail -20 "$OUT/bench_rehearse_n8.err"; exit 1; }
 fi
