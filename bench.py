@@ -594,7 +594,7 @@ def halo_forms(op, x, stream, reps, rank, dev, m_loc, nnz_loc):
     def p2p_serial():  # the p2p plan in order on the compute stream (no fork / join)
         p2p.set_overlap(False)
         p2p.mult(x, y, stream)
-        p2p.set_overlap(True)
+        p2p.set_overlap(None)  # back to the library's automatic choice
     fns["p2p_serial"] = p2p_serial
     for _ in range(3):
         for f in fns.values():

@@ -57,8 +57,11 @@ extern "C" {
  * withdrawn A/B-only options; their option values and kernel 4 are reserved
  * and return AIJHIP_ERR_ARG (measured slower).
  * 3: aijhip_gamg_params_t gained coarsen / square_graph / eig_ksp (PETSc
- * 3.7's MIS coarsening and CG emax estimate as options). */
-#define AIJHIP_ABI_VERSION 3
+ * 3.7's MIS coarsening and CG emax estimate as options).
+ * 4: aijhip_info_t gained hw_queues (the side streams' automatic choice
+ * follows it); aijhip_mpi.h gained aijhip_mpiaij_get_overlap and the
+ * automatic value -1 of aijhip_mpiaij_set_overlap. */
+#define AIJHIP_ABI_VERSION 4
 
 enum {
     AIJHIP_OK = 0,
@@ -133,6 +136,16 @@ typedef struct aijhip_info {
                                 more for the 32-bit gather-ordered copy
                                 (14 B per entry). x and the matrix read once,
                                 y written once (ABI 2)                        */
+    int32_t hw_queues;       /* hardware queues HIP maps the process's streams
+                                onto (GPU_MAX_HW_QUEUES, 4 when unset). With
+                                fewer than 8 the automatic choices keep every
+                                launch on the caller's stream: long rows after
+                                the row blocks (AIJHIP_OPT_LONG_OVERLAP -1,
+                                exact mode too), the MPIAIJ exchange in order
+                                (aijhip_mpiaij_set_overlap -1) — a side
+                                stream would share the compute stream's queue
+                                and run behind it (ABI 4)                     */
+    int32_t reserved0;
 } aijhip_info_t;
 
 /* Library / device. */
@@ -203,7 +216,9 @@ enum {
                                        them (plain MatMult / MatMultAdd;
                                        forked from and joined to the caller's
                                        stream by events); -1 (default): 0,
-                                       or 1 with AIJHIP_OPT_EXACT. Same
+                                       or 1 with AIJHIP_OPT_EXACT when the
+                                       process has >= 8 hardware queues
+                                       (aijhip_info_t.hw_queues). Same
                                        results                              */
     AIJHIP_OPT_GATHER_SORT = 12,    /* MatMult / MatMultAdd from a copy of the
                                        row blocks with each block's entries

@@ -117,13 +117,19 @@ int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o,
  * handle's exchange stream while A_d multiplies on `stream`. x, y: device
  * fp64[mloc], distinct. */
 int aijhip_mpiaij_mult(aijhip_mpiaij_t M, const double *x, double *y, void *stream);
-/* RCCL exchange placement: 1 (default) on the operator's exchange stream
- * beside A_d x (forked from and joined to the caller's stream by events); 0
- * on the caller's stream in order — pack, A_d x, the collective, A_o g — with
- * no cross-stream events (each fork / join costs ~6-13 us of device time on
- * the MI355X, profiles/r05/; the serial form exposes the exchange instead).
- * The host transport is unaffected. */
+/* RCCL exchange placement: 1 on the operator's exchange stream beside A_d x
+ * (forked from and joined to the caller's stream by events); 0 on the
+ * caller's stream in order — pack, A_d x, the collective, A_o g — with no
+ * cross-stream events (each fork / join costs ~6-13 us of device time on the
+ * MI355X, profiles/r05/; the serial form exposes the exchange instead); -1
+ * (the default at create): 1 when the process has at least 8 hardware queues
+ * (GPU_MAX_HW_QUEUES, aijhip_info_t.hw_queues), else 0 — with HIP's default
+ * 4 the exchange stream would share the compute stream's queue and run
+ * behind it (the fork / join then costs 29.5 us, profiles/r05/e/). The host
+ * transport is unaffected. */
 int aijhip_mpiaij_set_overlap(aijhip_mpiaij_t M, int overlap);
+/* The placement in effect (0 / 1) and the hardware-queue count it followed. */
+int aijhip_mpiaij_get_overlap(aijhip_mpiaij_t M, int32_t *overlap, int32_t *hw_queues);
 /* The ghost vector of the last mult (device fp64, *n entries), for tests. */
 int aijhip_mpiaij_get_ghost(aijhip_mpiaij_t M, const double **ghost, int64_t *n);
 int aijhip_mpiaij_destroy(aijhip_mpiaij_t M);

@@ -77,6 +77,7 @@ class AIJInfo(ctypes.Structure):
         ("row_patterns", ctypes.c_int32),
         ("long_overlap", ctypes.c_int32),
         ("mult_layout_bytes", ctypes.c_int64),
+        ("hw_queues", ctypes.c_int32), ("reserved0", ctypes.c_int32),
     ]
 
 

@@ -48,7 +48,7 @@ MPI_SYMBOLS = (
     "aijhip_kspmpi_get_iteration_number", "aijhip_kspmpi_get_residual_norm", "aijhip_kspmpi_get_converged_reason",
     "aijhip_kspmpi_get_residual_history", "aijhip_kspmpi_get_host_syncs", "aijhip_kspmpi_destroy",
     "aijhip_comm_set_host_sendrecv", "aijhip_kspmpi_get_pc_levels", "aijhip_kspmpi_get_setup_seconds",
-    "aijhip_kspmpi_get_pc_level", "aijhip_mpiaij_set_overlap",
+    "aijhip_kspmpi_get_pc_level", "aijhip_mpiaij_set_overlap", "aijhip_mpiaij_get_overlap",
 )
 _bound = False
 
@@ -69,6 +69,7 @@ def _lib():
         L.aijhip_mpiaij_create.argtypes = [_P, _P, _P, _i32, _i32, _P, _P, _P, _i32, _P, _P, _i32, ctypes.POINTER(_P)]
         L.aijhip_mpiaij_mult.argtypes = [_P, _P, _P, _P]
         L.aijhip_mpiaij_set_overlap.argtypes = [_P, ctypes.c_int]
+        L.aijhip_mpiaij_get_overlap.argtypes = [_P, ctypes.POINTER(_i32), ctypes.POINTER(_i32)]
         L.aijhip_mpiaij_get_ghost.argtypes = [_P, ctypes.POINTER(_P), ctypes.POINTER(_i64)]
         L.aijhip_mpiaij_destroy.argtypes = [_P]
         L.aijhip_kspmpi_create.argtypes = [_P, ctypes.POINTER(_P)]
@@ -263,10 +264,17 @@ class NativeMPIAIJ:
         _pkg._check(_lib().aijhip_mpiaij_mult(self._h, _pkg._dev_ptr(x, self.mloc, "x"),
                                               _pkg._dev_ptr(y, self.mloc, "y"), _pkg._stream_handle(stream)))
 
-    def set_overlap(self, overlap: bool):
-        """RCCL exchange on the exchange stream beside A_d (True, default) or
-        in order on the caller's stream (False: no fork / join events)."""
-        _pkg._check(_lib().aijhip_mpiaij_set_overlap(self._h, 1 if overlap else 0))
+    def set_overlap(self, overlap):
+        """RCCL exchange on the exchange stream beside A_d (True) or in order
+        on the caller's stream (False: no fork / join events); None: the
+        library's automatic choice (by the hardware-queue count, the default)."""
+        _pkg._check(_lib().aijhip_mpiaij_set_overlap(self._h, -1 if overlap is None else (1 if overlap else 0)))
+
+    def overlap(self):
+        """(placement in effect 0 / 1, the process's hardware queues)."""
+        o, q = _i32(), _i32()
+        _pkg._check(_lib().aijhip_mpiaij_get_overlap(self._h, ctypes.byref(o), ctypes.byref(q)))
+        return o.value, q.value
 
     def ghost(self):
         """(device pointer, length) of the ghost vector."""

@@ -446,7 +446,8 @@ int plan_build(aijhip_mat *A) {
     // of 1-4 K entries keep one lane's sequential sum and the side stream
     // hides that chain (round 5: skewed stand-in default 310.7 vs 315.2 us
     // side stream; exact 350.5 us after, profiles/r05/ad/)
-    if (P.tune.overlap < 0) P.tune.overlap = P.tune.exact ? 1 : 0;
+    // (with fewer hardware queues than a side stream needs, after them too)
+    if (P.tune.overlap < 0) P.tune.overlap = P.tune.exact && aijhip::hw_queues() >= aijhip::kOverlapMinQueues;
     const bool auto_sort = P.tune.gsort < 0 && !A->setup_op;  // (a set-up operator keeps the 32-bit form)
     const bool auto_codes = P.tune.codes < 0;
     const bool auto_patterns = P.tune.patterns < 0;
@@ -519,7 +520,8 @@ int plan_build(aijhip_mat *A) {
                 free_plan(A->plan);
                 P.kernel = kernel;
                 P.tune = req;
-                if (P.tune.overlap < 0) P.tune.overlap = P.tune.exact ? 1 : 0;
+                if (P.tune.overlap < 0)
+                    P.tune.overlap = P.tune.exact && aijhip::hw_queues() >= aijhip::kOverlapMinQueues;
                 P.tune.gsort = 0;
                 if (P.tune.geom < 0) P.tune.geom = scattered ? 1 : 6;
                 if (P.tune.nt < 0) P.tune.nt = scattered ? 1 : 0;
@@ -705,6 +707,15 @@ int create_impl(int device, int32_t m, int32_t n, int64_t nz, const int32_t *ai,
 
 namespace aijhip {
 void set_error(const std::string &msg) { g_err = msg; }
+
+int hw_queues() {
+    static const int q = [] {
+        const char *v = std::getenv("GPU_MAX_HW_QUEUES");
+        const int n = v ? std::atoi(v) : 0;
+        return n > 0 ? n : 4;
+    }();
+    return q;
+}
 
 unsigned sync_event_flags() {
     const char *v = std::getenv("AIJHIP_EVENT_FENCE");
@@ -1122,6 +1133,8 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->row_patterns = A->plan.d_pid != nullptr ? A->plan.n_pat : 0;
     info->long_overlap = A->plan.side != nullptr ? 1 : 0;
     info->mult_layout_bytes = aijhip::mult_layout_bytes(*A);
+    info->hw_queues = aijhip::hw_queues();
+    info->reserved0 = 0;
     return AIJHIP_OK;
 }
 

@@ -356,6 +356,16 @@ uint64_t next_plan_gen();
 // "device" (hipEventReleaseToDevice) or "none" (hipEventDisableSystemFence).
 // Both ends of every such edge are on one device.
 unsigned sync_event_flags();
+// The hardware queues HIP maps this process's streams onto: GPU_MAX_HW_QUEUES
+// as HIP reads it at initialisation, 4 (HIP's default) when unset. Streams
+// are dealt to the queues round-robin in creation order, so with fewer than
+// kOverlapMinQueues the library's second streams (the MPIAIJ exchange, the
+// long rows' side stream) share a queue with the compute stream beside
+// torch's and RCCL's, and their "concurrent" work runs behind it (measured,
+// profiles/r05/e/: the halo's empty fork / join 29.5 us at 4 queues vs 13.5
+// at 8; the skewed stand-in's side stream 344 us, slower than serial, at 4).
+int hw_queues();
+constexpr int kOverlapMinQueues = 8;
 
 // Compulsory bytes one MatMult under A's plan moves (aijhip_info_t.mult_layout_bytes).
 int64_t mult_layout_bytes(const aijhip_mat &A);

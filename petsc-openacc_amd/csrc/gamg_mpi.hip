@@ -1477,7 +1477,8 @@ static int transfer(aijhip_mpiaij *halo_op, const aijhip_mat *Bd, const aijhip_m
     int rc = exch ? aijhip_mpi::halo_post(halo_op, x, s) : AIJHIP_OK;
     if (rc) return rc;
     hipError_t e = aijhip::launch_mult(*Bd, x, z, y, add, s, stop);
-    if (e != hipSuccess) return gerr(e, "transfer product");
+    if (e != hipSuccess)
+        return exch ? aijhip_mpi::halo_abort(halo_op, s, gerr(e, "transfer product")) : gerr(e, "transfer product");
     if (exch && (rc = aijhip_mpi::halo_finish(halo_op, s))) return rc;
     if (Bo && (e = aijhip::launch_mult(*Bo, halo_op->d_ghost, y, y, true, s, stop)) != hipSuccess)
         return gerr(e, "transfer ghost product");
@@ -1517,7 +1518,7 @@ int vcycle(Hierarchy &H, const double *b0, double *x0, hipStream_t s, const int 
             const bool ex = exchanges(L.op);
             if (ex && (rc = aijhip_mpi::halo_post(L.op, X(l), s))) return rc;
             if ((e = aijhip::launch_mg_resid(*L.Ad, X(l), B(l), L.r, s, true, stop)) != hipSuccess)
-                return gerr(e, "residual");
+                return ex ? aijhip_mpi::halo_abort(L.op, s, gerr(e, "residual")) : gerr(e, "residual");
             if (ex && (rc = aijhip_mpi::halo_finish(L.op, s))) return rc;
             if ((rc = offdiag_axpy(L, nullptr, L.r, s, stop))) return rc;
         } else {  // MatMult_MPIAIJ, then the residual
@@ -1536,7 +1537,7 @@ int vcycle(Hierarchy &H, const double *b0, double *x0, hipStream_t s, const int 
             const bool ex = exchanges(L.op);
             if (ex && (rc = aijhip_mpi::halo_post(L.op, L.r, s))) return rc;
             if ((e = aijhip::launch_mg_post(*L.Ad, L.r, B(l), L.dinv, X(l), nullptr, s, true, stop)) != hipSuccess)
-                return gerr(e, "post-smoothing");
+                return ex ? aijhip_mpi::halo_abort(L.op, s, gerr(e, "post-smoothing")) : gerr(e, "post-smoothing");
             if (ex && (rc = aijhip_mpi::halo_finish(L.op, s))) return rc;
             if ((rc = offdiag_axpy(L, L.dinv, X(l), s, stop))) return rc;
         } else {

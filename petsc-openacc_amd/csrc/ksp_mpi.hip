@@ -435,6 +435,10 @@ int grid_of(int64_t n, int cap) {
 
 namespace {
 
+// aijhip_mpiaij_set_overlap(-1): the exchange stream only with a hardware
+// queue of its own to run on (aijhip::hw_queues)
+int auto_overlap() { return aijhip::hw_queues() >= aijhip::kOverlapMinQueues ? 1 : 0; }
+
 void mpiaij_free(aijhip_mpiaij *M) {
     hipFree(M->d_send_rows); hipFree(M->d_sendbuf); hipFree(M->d_ghost);
     if (M->h_send) hipHostFree(M->h_send);
@@ -489,6 +493,7 @@ int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
                                 M->xs)) != hipSuccess)
             return mhip(e, "halo staging");
     }
+    M->posted = true;
     return AIJHIP_OK;
 }
 
@@ -525,9 +530,7 @@ int halo_send_rccl(aijhip_mpiaij *M) {
         if (r != ncclSuccess) return nfail(r, "ncclSend/ncclRecv");
         if (r2 != ncclSuccess) return nfail(r2, "ncclGroupEnd");
     }
-    if (xs != M->xs) return AIJHIP_OK;  // serial: already in order on the caller's stream
-    const hipError_t e = hipEventRecord(M->ev_halo, M->xs);
-    return e == hipSuccess ? AIJHIP_OK : mhip(e, "halo event");
+    return AIJHIP_OK;
 }
 
 }  // namespace
@@ -537,11 +540,16 @@ int halo_send_rccl(aijhip_mpiaij *M) {
 int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
     aijhip_comm *C = M->comm;
     hipError_t e;
+    if (!M->posted) return mfail(AIJHIP_ERR_STATE, "halo_finish without halo_post");
+    M->posted = false;
     if (C->kind == AIJHIP_COMM_RCCL) {
-        const bool serial = M->post_s == s && s != M->xs;
         const int rc = halo_send_rccl(M);
         if (rc) return rc;
-        if (serial) return AIJHIP_OK;  // (no join: one stream)
+        // the serial form (the exchange enqueued on s itself): already in
+        // order, no join; otherwise s waits for the stream post chose — the
+        // stream recorded at post time, whatever stream finish is given
+        if (M->post_s == s) return AIJHIP_OK;
+        if ((e = hipEventRecord(M->ev_halo, M->post_s)) != hipSuccess) return mhip(e, "halo event");
     } else if (C->kind == AIJHIP_COMM_HOST) {
         const int64_t npack = M->halo == AIJHIP_HALO_ALLGATHER ? M->gather_len : M->n_send;
         int rc = wait_stream(C, M->xs);
@@ -595,6 +603,15 @@ int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
     return AIJHIP_OK;
 }
 
+int halo_abort(aijhip_mpiaij *M, hipStream_t s, int rc) {
+    if (M->posted) {
+        const std::string why = aijhip_last_error();  // keep the first failure's message
+        (void)halo_finish(M, s);
+        aijhip::set_error(why);
+    }
+    return rc;
+}
+
 // y = A_d x + A_o g; with dot: W = y and the p.w partials (p = x) into
 // part (A_d blocks, fused when A_d's plan allows) and opart (A_o rows).
 int mpiaij_apply(aijhip_mpiaij *M, const double *x, double *y, hipStream_t s, double *part, double *opart,
@@ -605,9 +622,10 @@ int mpiaij_apply(aijhip_mpiaij *M, const double *x, double *y, hipStream_t s, do
     int rc = exchange ? halo_post(M, x, s) : AIJHIP_OK;
     if (rc) return rc;
     hipError_t e;
-    if (part && fused) e = aijhip::launch_stream_dot(*M->Ad, x, y, part, S ? &S->done : nullptr, s);
+    if (M->fault_ad) e = hipErrorInvalidValue;
+    else if (part && fused) e = aijhip::launch_stream_dot(*M->Ad, x, y, part, S ? &S->done : nullptr, s);
     else e = aijhip::launch_mult(*M->Ad, x, nullptr, y, false, s, stop);
-    if (e != hipSuccess) return mhip(e, "A_d product");
+    if (e != hipSuccess) return exchange ? halo_abort(M, s, mhip(e, "A_d product")) : mhip(e, "A_d product");
     if (exchange && (rc = halo_finish(M, s))) return rc;
     if (M->Ao) {
         const aijhip::RowList L = aijhip::row_list(*M->Ao);
@@ -894,6 +912,8 @@ int aijhip_mpiaij_create(aijhip_comm_t comm, aijhip_mat_t A_d, aijhip_mat_t A_o,
     aijhip_mpiaij *M = new (std::nothrow) aijhip_mpiaij();
     if (!M) return mfail(AIJHIP_ERR_ALLOC, "host allocation");
     M->comm = comm; M->Ad = A_d; M->Ao = A_o; M->halo = halo; M->mloc = A_d->m;
+    M->overlap = auto_overlap();
+    if (const char *f = std::getenv("AIJHIP_FAULT_AD_RANK")) M->fault_ad = std::atoi(f) == comm->rank;
     auto bad = [&](const std::string &msg) {
         mpiaij_free(M);
         delete M;
@@ -980,8 +1000,17 @@ int aijhip_mpiaij_mult(aijhip_mpiaij_t M, const double *x, double *y, void *stre
 
 int aijhip_mpiaij_set_overlap(aijhip_mpiaij_t M, int overlap) {
     if (!M) return mfail(AIJHIP_ERR_ARG, "NULL matrix");
-    if (overlap < 0 || overlap > 1) return mfail(AIJHIP_ERR_ARG, "overlap: 0 (one stream) or 1 (exchange stream)");
-    M->overlap = overlap;
+    if (overlap < -1 || overlap > 1)
+        return mfail(AIJHIP_ERR_ARG, "overlap: -1 (automatic), 0 (one stream) or 1 (exchange stream)");
+    if (M->posted) return mfail(AIJHIP_ERR_STATE, "an exchange is posted");
+    M->overlap = overlap >= 0 ? overlap : auto_overlap();
+    return AIJHIP_OK;
+}
+
+int aijhip_mpiaij_get_overlap(aijhip_mpiaij_t M, int32_t *overlap, int32_t *hw_queues) {
+    if (!M) return mfail(AIJHIP_ERR_ARG, "NULL matrix");
+    if (overlap) *overlap = M->overlap;
+    if (hw_queues) *hw_queues = aijhip::hw_queues();
     return AIJHIP_OK;
 }
 

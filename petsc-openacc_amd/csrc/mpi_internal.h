@@ -55,7 +55,11 @@ struct aijhip_mpiaij {
     // A_d, the collective and A_o run one after another)
     int overlap = 1;
     hipStream_t post_s = nullptr;  // the stream the posted exchange runs on
+    bool posted = false;           // a halo_post not yet matched by its halo_finish
     int o_grid = 1;
+    // test hook (AIJHIP_FAULT_AD_RANK at create): this rank's A_d launch
+    // reports hipErrorInvalidValue, so the error paths after a post are tested
+    bool fault_ad = false;
 };
 
 namespace aijhip_mpi {
@@ -77,9 +81,14 @@ int comm_sendrecv(aijhip_comm *C, const std::vector<std::vector<uint64_t>> &out,
 // kernels on its exchange stream; the caller then launches the diagonal
 // product on `s`; finish = the RCCL collective (or the host transport's
 // exchange), then `s` waits for the ghosts in M->d_ghost. Every post is
-// followed by exactly one finish.
+// followed by exactly one finish — on an error path too (halo_abort): the
+// peers are already committed to the exchange, and a rank that skipped its
+// half would leave them blocked in the collective.
 int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s);
 int halo_finish(aijhip_mpiaij *M, hipStream_t s);
+// The error path after a successful halo_post: completes the exchange (its
+// result ignored) so no peer waits on this rank, and returns rc.
+int halo_abort(aijhip_mpiaij *M, hipStream_t s, int rc);
 // y = A_d x + A_o g (MatMult_MPIAIJ); part/opart/S/fused: the CG epilogue
 // (ksp_mpi.hip); stop: CG's flag for the products.
 int mpiaij_apply(aijhip_mpiaij *M, const double *x, double *y, hipStream_t s, double *part, double *opart,
