@@ -129,9 +129,10 @@ def _graph_rows(S):
     return G1
 
 
-def aggregate_mis(S, square, keys):
+def aggregate_mis(S, square, keys, return_roots=False):
     """PETSc's MIS aggregation (restated literally, sequential): returns
-    (agg, na), agg[i] = -1 for removed singletons."""
+    (agg, na), agg[i] = -1 for removed singletons (return_roots: and the
+    roots, ascending — aggregate c is rooted at roots[c])."""
     m = S.shape[0]
     G1 = _graph_rows(S)
     if square:
@@ -165,6 +166,8 @@ def aggregate_mis(S, square, keys):
     cidx = np.full(m, -1, np.int64)
     cidx[roots] = np.arange(len(roots))
     agg = np.where(parent >= 0, cidx[np.maximum(parent, 0)], -1)
+    if return_roots:
+        return agg, len(roots), roots
     return agg, len(roots)
 
 

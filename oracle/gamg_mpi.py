@@ -7,11 +7,18 @@ reference runs on 1-16 MPI ranks: /root/reference/runs/single-node-scaling.pbs
 computed globally:
 
   - rank r owns rows [starts[r], starts[r+1]) of every level;
-  - aggregates are formed on each rank's diagonal block with oracle/gamg.py's
-    aggregation — PETSc's MIS (coarsen 1, the default: the block's graph,
-    squared on the first square_graph levels, keys at local indices) or the
-    greedy pass (coarsen 0) — numbered rank by rank (coarse rows of rank r =
-    [cstarts[r], cstarts[r+1]));
+  - aggregates: PETSc's parallel MIS (coarsen 1, the default; mis.c
+    maxIndSetAgg exchanges ghost states every round, so roots on either side
+    of a rank boundary are independent and a node deleted by a root on
+    another rank joins that root's aggregate) restated as the
+    lexicographically-first MIS of the GLOBAL strength graph (squared on the
+    first square_graph levels) by keys at GLOBAL indices: oracle/gamg.py's
+    aggregate_mis on the whole operator, so the aggregates do not depend on
+    the partition; rank r owns the aggregates rooted in its rows (coarse rows
+    of rank r = [cstarts[r], cstarts[r+1]), the roots in natural order). The
+    source (PETSc 3.7.6 src/mat/coarsen/impls/mis/mis.c) is absent from
+    /root/reference (fetched by scripts/petsc.sh:37-41): parity unpinned.
+    The greedy pass (coarsen 0) stays on each rank's diagonal block;
   - emax by CG's Lanczos estimate (eig_ksp 1, the default) or the power
     iteration (0) on the global D^-1 A from oracle/gamg.py's start vector at
     global indices (the device sums its dots rank by rank: equal to
@@ -44,24 +51,28 @@ def build(A, starts, threshold=0.0, coarse_eq_limit=50, max_levels=10, nsmooths=
     while len(levels) + 1 < max_levels and A.shape[0] > coarse_eq_limit:
         d = og.first_diagonal(A)
         dinv = 1.0 / np.where(d == 0.0, 1.0, d)
-        aggs, nas = [], []
-        for r in range(len(starts) - 1):
-            lo, hi = starts[r], starts[r + 1]
-            Ad = sp.csr_matrix(A[lo:hi, lo:hi])
-            Ad.sort_indices()
-            S = og.strength_graph(Ad, d[lo:hi], threshold)
-            lvl = level0 + len(levels)
-            if coarsen == 1:
-                agg, na = og.aggregate_mis(S, lvl < square_graph, og.mis_keys(hi - lo, lvl))
-            else:
+        lvl = level0 + len(levels)
+        if coarsen == 1:  # the global MIS (partition-independent)
+            As = sp.csr_matrix(A)
+            As.sort_indices()
+            S = og.strength_graph(As, d, threshold)
+            agg, NA, roots = og.aggregate_mis(S, lvl < square_graph, og.mis_keys(A.shape[0], lvl), return_roots=True)
+            cstarts = np.searchsorted(roots, starts, side="left").astype(np.int64)
+        else:
+            aggs, nas = [], []
+            for r in range(len(starts) - 1):
+                lo, hi = starts[r], starts[r + 1]
+                Ad = sp.csr_matrix(A[lo:hi, lo:hi])
+                Ad.sort_indices()
+                S = og.strength_graph(Ad, d[lo:hi], threshold)
                 agg, na = og.aggregate(Ad, S)
-            aggs.append(agg)
-            nas.append(na)
-        cstarts = np.concatenate([[0], np.cumsum(nas)]).astype(np.int64)
+                aggs.append(agg)
+                nas.append(na)
+            cstarts = np.concatenate([[0], np.cumsum(nas)]).astype(np.int64)
+            agg = np.concatenate([np.where(a >= 0, a + cstarts[r], -1) for r, a in enumerate(aggs)])
         NA = int(cstarts[-1])
         if NA == 0 or NA >= A.shape[0]:
             break
-        agg = np.concatenate([np.where(a >= 0, a + cstarts[r], -1) for r, a in enumerate(aggs)])
         if nsmooths > 0:
             emax = og.estimate_emax_cg(A, dinv, eig_its) if eig_ksp == 1 else og.estimate_emax(A, dinv, eig_its)
         else:

@@ -73,8 +73,15 @@ void free_device_levels(std::vector<DeviceLevel> &levels);
 //  smooth_level: the tentative P0 from the near-null space B (Bc = the next
 //    level's) and P = P0 + alpha D^-1 (A P0), columns = agg ids;
 //  galerkin_level: A_c = P^T (A P) and P^T (ap_out: keep A P as well).
+//    keep_S: the strength graph (S of A's rows, symmetric, no diagonal) and
+//    the diagonal handed to the caller instead of aggregating (*d_agg NULL)
+struct StrengthGraph {
+    int32_t *si = nullptr, *sj = nullptr;
+    int64_t nz = 0;
+    double *d = nullptr;
+};
 int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_agg, int32_t *na, double **dinv,
-                    int emax_its, double *emax, hipError_t *emax_err, size_t level);
+                    int emax_its, double *emax, hipError_t *emax_err, size_t level, StrengthGraph *keep_S = nullptr);
 int smooth_level(const DCsr &Av, int32_t na, int32_t *d_agg, const double *d_B, const double *dinv, double alpha,
                  int nsmooths, int n_cu, double **d_p0, double **d_Bc, DCsr &P, int *cols_used,
                  bool b_ones = false);  // b_ones: d_B is all 1.0 (the finest level's near-null space)
@@ -87,6 +94,11 @@ int rowprod_device(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_us
 // B[i] / Bc[agg[i]] (device arrays).
 hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0,
                             bool b_ones = false);  // b_ones: B is all 1.0
+// Per aggregate the sum of B_i^2 over its members (agg[i] in [0, na); -1
+// not a member), in ascending member order: tentative_device's Bc before
+// the square root (B == nullptr or b_ones: the member counts).
+hipError_t aggregate_sumsq_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *s2,
+                                  bool b_ones = false);
 // P = P0 + alpha D^-1 T on the union pattern of T and P0 (P0: one entry per
 // row, column agg[i], value p0[i]); T's columns may extend past the local
 // aggregates (the distributed set-up's ghost coarse columns).

@@ -548,6 +548,25 @@ __global__ void k_agg_norm_count(int32_t na, const int32_t *__restrict__ count, 
     if (a < na) Bc[a] = sqrt((double)count[a]);
 }
 
+// the sums of squares themselves (the distributed set-up adds the members
+// other ranks hold before the square root): k_agg_norm / k_agg_norm_count
+// without it
+__global__ void k_agg_sumsq(int32_t na, const int32_t *__restrict__ seg, const double *__restrict__ bm, double *s2) {
+    const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= na) return;
+    double s = 0.0;
+    for (int32_t q = seg[a]; q < seg[a + 1]; ++q) {
+        const double b = bm[q];
+        s += b * b;
+    }
+    s2[a] = s;
+}
+
+__global__ void k_agg_count_d(int32_t na, const int32_t *__restrict__ count, double *s2) {
+    const int32_t a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a < na) s2[a] = (double)count[a];
+}
+
 __global__ void k_tentative(int32_t m, const int32_t *__restrict__ agg, const double *__restrict__ B,
                             const double *__restrict__ Bc, double *p0) {
     const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1295,7 +1314,8 @@ done:
 // the transpose of P0's pattern (one entry per row, column agg[i], value
 // B[i]): the library's stable transpose gives exactly that.
 hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0,
-                     bool b_ones = false) {
+                     bool b_ones = false, bool sumsq = false) {
+    // sumsq: Bc gets the sums of squares (no square root) and p0 is untouched
     if (m == 0) return hipSuccess;
     int32_t *ai = nullptr, *tai = nullptr, *taj = nullptr;
     double *taa = nullptr;
@@ -1305,8 +1325,13 @@ hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B,
         if ((e = dalloc(&count, std::max(na, 1))) != hipSuccess) return e;
         if ((e = hipMemset(count, 0, sizeof(int32_t) * (size_t)std::max(na, 1))) == hipSuccess) {
             hipLaunchKernelGGL(k_agg_count, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, count);
-            if (na > 0) hipLaunchKernelGGL(k_agg_norm_count, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, count, Bc);
-            hipLaunchKernelGGL(k_tentative, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, B, Bc, p0);
+            if (sumsq) {
+                if (na > 0) hipLaunchKernelGGL(k_agg_count_d, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, count, Bc);
+            } else {
+                if (na > 0)
+                    hipLaunchKernelGGL(k_agg_norm_count, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, count, Bc);
+                hipLaunchKernelGGL(k_tentative, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, B, Bc, p0);
+            }
             e = hipGetLastError();
         }
         hipFree(count);
@@ -1332,7 +1357,10 @@ hipError_t tentative(int32_t m, int32_t na, const int32_t *agg, const double *B,
         hipFree(P0.aj);
         hipFree(P0.aa);
     }
-    if (e == hipSuccess) {
+    if (e == hipSuccess && sumsq) {
+        if (na > 0) hipLaunchKernelGGL(k_agg_sumsq, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, tai, taa, Bc);
+        e = hipGetLastError();
+    } else if (e == hipSuccess) {
         if (na > 0) hipLaunchKernelGGL(k_agg_norm, dim3(blocks_for(na, 256)), dim3(256), 0, nullptr, na, tai, taa, Bc);
         hipLaunchKernelGGL(k_tentative, dim3(blocks_for(m, 256)), dim3(256), 0, nullptr, m, agg, B, Bc, p0);
         e = hipGetLastError();
@@ -1643,7 +1671,8 @@ void free_device_levels(std::vector<DeviceLevel> &levels) {
 // 0 the power iteration for emax(D^-1 A) runs on a second host thread
 // meanwhile (*emax on return).
 int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_agg_out, int32_t *na_out,
-                    double **dinv_out, int emax_its, double *emax, hipError_t *emax_err, size_t level) {
+                    double **dinv_out, int emax_its, double *emax, hipError_t *emax_err, size_t level,
+                    StrengthGraph *keep_S) {
     *d_agg_out = nullptr;
     *dinv_out = nullptr;
     *na_out = 0;
@@ -1723,6 +1752,15 @@ int aggregate_level(aijhip_mat &A, const aijhip_gamg_params_t &p, int32_t **d_ag
     if ((rc = strength_lists(A, cnt, off, tmp, nzs, n_cu, &si, &sj, &sval, &nzs))) goto level_done;
 strength_done:
     GTRY(hipGetLastError(), "strength kernels");
+    if (keep_S) {  // the distributed MIS aggregates across ranks itself (gamg_mpi.hip)
+        keep_S->si = si;
+        keep_S->sj = sj;
+        keep_S->nz = nzs;
+        keep_S->d = d;
+        si = sj = nullptr;
+        d = nullptr;
+        goto level_done;
+    }
     // ---- aggregation. Phase 1: the device sweep (gamg_aggregate.hip) on
     // large levels with a sparse S, else -- or when the sweep would run too
     // deep -- the sequential pass on the host from S staged in pinned
@@ -1998,6 +2036,11 @@ int rowprod_device(const DCsr &A, const DCsr &B, DCsr &C, int n_cu, int *cols_us
 hipError_t tentative_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *Bc, double *p0,
                             bool b_ones) {
     return tentative(m, na, agg, B, Bc, p0, b_ones);
+}
+
+hipError_t aggregate_sumsq_device(int32_t m, int32_t na, const int32_t *agg, const double *B, double *s2,
+                                  bool b_ones) {
+    return tentative(m, na, agg, B, s2, nullptr, b_ones, true);
 }
 
 int prolong_from_T(const DCsr &T, const int32_t *d_agg, const double *d_p0, const double *dinv, double alpha,

@@ -53,6 +53,7 @@
 
 #include "dscan.h"
 #include "gamg_device.h"
+#include "gamg_internal.h"
 #include "gamg_mpi.h"
 #include "mpi_internal.h"
 
@@ -306,6 +307,256 @@ __global__ __launch_bounds__(256) void k_offdiag_axpy(int32_t nr, const int32_t 
         for (int32_t k = rai[q]; k < rai[q + 1]; ++k) sum += aa[k] * g[aj[k]];
         y[o] = y[o] + (scale ? scale[o] : 1.0) * (-sum);
     }
+}
+
+
+// ---- PETSc's parallel MIS (mis.c maxIndSetAgg over an MPIAIJ graph: ghost
+// states exchanged every round), restated as the lexicographically-first
+// maximal independent set of the GLOBAL graph by a global key — the
+// single-GPU rule of gamg_aggregate.hip (aggregate_mis_device) with every
+// node's key taken at its global index, the graph G1 = S_d + S_o + I (the
+// strength graph of the diagonal block and of the off-diagonal block's ghost
+// columns) and each round's two one-hop passes reading the neighbours on
+// other ranks through the level's halo. Keys are unique, so the set, the
+// parents and the aggregates do not depend on the partition: at every rank
+// count the hierarchy is the single-GPU one (to the rounding of its sums).
+// Values travel through the fp64 halo as raw 64-bit patterns (copies only).
+typedef uint8_t dmis_t;
+constexpr dmis_t kDmUndecided = 0, kDmRoot = 1, kDmOut = 2, kDmSingle = 3;
+
+__device__ __forceinline__ uint64_t dm_key(uint32_t h, int64_t gid) { return (uint64_t)h << 32 | (uint32_t)gid; }
+// roots = false: a round's decision value (0 root, key + 1 undecided, all
+// ones otherwise); true: a root's key, else all ones (the parents' pass)
+__device__ __forceinline__ uint64_t dm_value(dmis_t st, uint32_t h, int64_t gid, bool roots) {
+    if (roots) return st == kDmRoot ? dm_key(h, gid) : ~0ull;
+    return st == kDmRoot ? 0ull : st == kDmUndecided ? dm_key(h, gid) + 1 : ~0ull;
+}
+__device__ __forceinline__ uint64_t dm_bits(double v) { return (uint64_t)__double_as_longlong(v); }
+__device__ __forceinline__ double dm_double(uint64_t v) { return __longlong_as_double((long long)v); }
+
+__global__ void k_dm_diag(int32_t m, const int32_t *__restrict__ ai, const int32_t *__restrict__ aj,
+                          const double *__restrict__ aa, double *d) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    double v = 0.0;
+    for (int32_t k = ai[i]; k < ai[i + 1]; ++k)
+        if (aj[k] == i) { v = aa[k]; break; }
+    d[i] = v;
+}
+
+// S_o: the off-diagonal block's strong entries (|a| > theta sqrt|d_i d_g|,
+// the single-GPU filter with the ghost's diagonal), full rows [0, m)
+__global__ void k_dm_so_count(int32_t nr, const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx,
+                              const double *__restrict__ aa, const double *__restrict__ d,
+                              const double *__restrict__ gd, const int32_t *__restrict__ aj, double theta,
+                              int32_t *cnt) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nr) return;
+    const int32_t i = ridx ? ridx[q] : q;
+    int32_t c = 0;
+    for (int32_t k = rai[q]; k < rai[q + 1]; ++k) c += fabs(aa[k]) > theta * sqrt(fabs(d[i] * gd[aj[k]]));
+    cnt[i] = c;
+}
+
+__global__ void k_dm_so_fill(int32_t nr, const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx,
+                             const double *__restrict__ aa, const double *__restrict__ d,
+                             const double *__restrict__ gd, const int32_t *__restrict__ aj, double theta,
+                             const int32_t *__restrict__ soi, int32_t *soj) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nr) return;
+    const int32_t i = ridx ? ridx[q] : q;
+    int32_t o = soi[i];
+    for (int32_t k = rai[q]; k < rai[q + 1]; ++k)
+        if (fabs(aa[k]) > theta * sqrt(fabs(d[i] * gd[aj[k]]))) soj[o++] = aj[k];
+}
+
+__global__ void k_dm_init(int32_t m, int64_t rstart, int32_t level, const int32_t *__restrict__ sdi,
+                          const int32_t *__restrict__ soi, dmis_t *state, uint32_t *hk) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    state[i] = (sdi[i] == sdi[i + 1] && soi[i] == soi[i + 1]) ? kDmSingle : kDmUndecided;
+    hk[i] = (uint32_t)(aijhip_gamg::mis_key((int32_t)(rstart + i), level) >> 32);
+}
+
+__global__ void k_dm_value(int32_t m, int64_t rstart, const dmis_t *__restrict__ state,
+                           const uint32_t *__restrict__ hk, bool roots, double *val) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) val[i] = dm_double(dm_value(state[i], hk[i], rstart + i, roots));
+}
+
+// pass A: amin[u] = min over u, its S_d neighbours and its S_o ghosts (their
+// values from the halo, gval) of the value
+__global__ __launch_bounds__(256) void k_dm_closed_min(int32_t m, int64_t rstart, const int32_t *__restrict__ sdi,
+                                                       const int32_t *__restrict__ sdj,
+                                                       const int32_t *__restrict__ soi,
+                                                       const int32_t *__restrict__ soj,
+                                                       const dmis_t *__restrict__ state,
+                                                       const uint32_t *__restrict__ hk,
+                                                       const double *__restrict__ gval, bool roots, double *amin) {
+    const int32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= m) return;
+    uint64_t best = dm_value(state[u], hk[u], rstart + u, roots);
+    for (int32_t a = sdi[u]; a < sdi[u + 1]; ++a) {
+        const int32_t j = sdj[a];
+        best = min(best, dm_value(state[j], hk[j], rstart + j, roots));
+    }
+    for (int32_t a = soi[u]; a < soi[u + 1]; ++a) best = min(best, dm_bits(gval[soj[a]]));
+    amin[u] = dm_double(best);
+}
+
+// min over i's neighbours (both blocks) of pass A's values (squared reach),
+// or i's own
+__device__ __forceinline__ uint64_t dm_reach(int32_t i, bool square, const int32_t *__restrict__ sdi,
+                                             const int32_t *__restrict__ sdj, const int32_t *__restrict__ soi,
+                                             const int32_t *__restrict__ soj, const double *__restrict__ amin,
+                                             const double *__restrict__ gamin) {
+    if (!square) return dm_bits(amin[i]);
+    uint64_t b = ~0ull;
+    for (int32_t a = sdi[i]; a < sdi[i + 1]; ++a) b = min(b, dm_bits(amin[sdj[a]]));
+    for (int32_t a = soi[i]; a < soi[i + 1]; ++a) b = min(b, dm_bits(gamin[soj[a]]));
+    return b;
+}
+
+// pass B: the decisions, and the workgroup's count of nodes still waiting
+__global__ __launch_bounds__(256) void k_dm_decide(int32_t m, int64_t rstart, const int32_t *__restrict__ sdi,
+                                                   const int32_t *__restrict__ sdj, const int32_t *__restrict__ soi,
+                                                   const int32_t *__restrict__ soj, bool square,
+                                                   const uint32_t *__restrict__ hk, const double *__restrict__ amin,
+                                                   const double *__restrict__ gamin, dmis_t *state,
+                                                   unsigned *wcount) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    bool waits = false;
+    if (i < m && state[i] == kDmUndecided) {
+        const uint64_t b = dm_reach(i, square, sdi, sdj, soi, soj, amin, gamin);
+        if (b == 0) state[i] = kDmOut;
+        else if (b == dm_key(hk[i], rstart + i) + 1) state[i] = kDmRoot;
+        else waits = true;
+    }
+    __shared__ unsigned wc[4];
+    const unsigned nw = (unsigned)__popcll(__ballot(waits));
+    if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = nw;
+    __syncthreads();
+    if (threadIdx.x == 0) wcount[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+__global__ __launch_bounds__(1024) void k_dm_total(const unsigned *__restrict__ wcount, int32_t n,
+                                                   unsigned long long *total) {
+    __shared__ unsigned long long part[16];
+    unsigned long long s = 0;
+    for (int32_t q = threadIdx.x; q < n; q += 1024) s += wcount[q];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_down(s, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < 16; ++w) t += part[w];
+        *total = t;
+    }
+}
+
+// smoothAggs' candidate: the highest global id among i's G1 neighbours that
+// are roots (S_d: the state; S_o: the ghost's root key from the halo), -1
+__global__ void k_dm_hiroot(int32_t m, int64_t rstart, const int32_t *__restrict__ sdi, const int32_t *__restrict__ sdj,
+                            const int32_t *__restrict__ soi, const int32_t *__restrict__ soj,
+                            const dmis_t *__restrict__ state, const double *__restrict__ grv,
+                            const int64_t *__restrict__ ggid, int64_t *hi) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    int64_t h = -1;
+    for (int32_t a = sdi[i]; a < sdi[i + 1]; ++a)
+        if (state[sdj[a]] == kDmRoot) h = max(h, rstart + sdj[a]);
+    for (int32_t a = soi[i]; a < soi[i + 1]; ++a)
+        if (dm_bits(grv[soj[a]]) != ~0ull) h = max(h, ggid[soj[a]]);
+    hi[i] = h;
+}
+
+// parent (global id): a root itself; an OUT node the lowest-key root within
+// reach (its key's low word), then (squared: smoothAggs) the highest-id root
+// among its G1 neighbours when it has one; otherwise -1. flag: the roots.
+__global__ void k_dm_parent(int32_t m, int64_t rstart, const int32_t *__restrict__ sdi,
+                            const int32_t *__restrict__ sdj, const int32_t *__restrict__ soi,
+                            const int32_t *__restrict__ soj, bool square, const double *__restrict__ amin,
+                            const double *__restrict__ gamin, const dmis_t *__restrict__ state,
+                            const int64_t *__restrict__ hi, int64_t *parent, int32_t *flag) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const dmis_t st = state[i];
+    flag[i] = st == kDmRoot;
+    if (st == kDmRoot) { parent[i] = rstart + i; return; }
+    if (st != kDmOut) { parent[i] = -1; return; }
+    int64_t p = (int64_t)(uint32_t)dm_reach(i, square, sdi, sdj, soi, soj, amin, gamin);
+    if (square && hi[i] >= 0) p = hi[i];
+    parent[i] = p;
+}
+
+// coarse ids: cg[i] = the coarse global id of i's aggregate (-1: removed);
+// agg[i] = its local aggregate (own roots), -1 otherwise; nodes whose root is
+// on another rank go to the list (node, parent gid) and get cg -2 for now
+__global__ void k_dm_coarse(int32_t m, int64_t rstart, int64_t cstart, const int64_t *__restrict__ parent,
+                            const int32_t *__restrict__ idx, double *cg, int32_t *agg, int32_t *rnode,
+                            int64_t *rpar, unsigned *rcount) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const int64_t p = parent[i];
+    if (p < 0) {
+        cg[i] = -1.0;
+        agg[i] = -1;
+    } else if (p >= rstart && p < rstart + m) {
+        const int32_t c = idx[p - rstart];
+        cg[i] = (double)(cstart + c);
+        agg[i] = c;
+    } else {
+        const unsigned k = atomicAdd(rcount, 1u);
+        rnode[k] = i;
+        rpar[k] = p;
+        cg[i] = -2.0;
+        agg[i] = -1;
+    }
+}
+
+__global__ void k_dm_gather_i32(int32_t n, const int32_t *__restrict__ at, const int32_t *__restrict__ v,
+                                int32_t *out) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) out[q] = v[at[q]];
+}
+
+__global__ void k_dm_gather_f64(int32_t n, const int32_t *__restrict__ at, const double *__restrict__ v, double *out) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) out[q] = v ? v[at[q]] : 1.0;
+}
+
+// s2[a[q]] += add[q] (distinct a per launch)
+__global__ void k_dm_add_at(int32_t n, const int32_t *__restrict__ a, const double *__restrict__ add, double *s2) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) s2[a[q]] = s2[a[q]] + add[q];
+}
+
+__global__ void k_dm_sqrt(int32_t n, double *v) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) v[q] = sqrt(v[q]);
+}
+
+// p0 of the nodes in own aggregates (k_tentative's formula), 0 elsewhere
+__global__ void k_dm_p0(int32_t m, const int32_t *__restrict__ agg, const double *__restrict__ B,
+                        const double *__restrict__ Bc, double *p0) {
+    const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const double c = agg[i] >= 0 ? Bc[agg[i]] : 0.0;
+    p0[i] = c > 0.0 ? (B ? B[i] : 1.0) / c : 0.0;
+}
+
+// the nodes in other ranks' aggregates: their coarse id and p0 (host-made)
+__global__ void k_dm_set_remote(int32_t n, const int32_t *__restrict__ node, const double *__restrict__ cgv,
+                                const double *__restrict__ p0v, double *cg, double *p0) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n) return;
+    cg[node[q]] = cgv[q];
+    p0[node[q]] = p0v[q];
+}
+
+__global__ void k_dm_set_i32(int32_t n, const int32_t *__restrict__ node, const int32_t *__restrict__ v, int32_t *x) {
+    const int32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q < n) x[node[q]] = v[q];
 }
 
 // ---------------------------------------------------------------- host side
@@ -655,6 +906,382 @@ int global_norm(aijhip_comm *C, const double *d_v, int32_t m, double *d_part, do
     return AIJHIP_OK;
 }
 
+
+// ---- the distributed MIS (coarsen 1; kernels k_dm_*): see the kernels'
+// comment. In: the level (handles, halo, ghost ids), its strength graph S_d
+// and diagonal from aggregate_level, the near-null space B. Out: the own
+// roots' count na and every rank's (cstarts), per local node the coarse
+// global id of its aggregate (cg, -1 removed), its local aggregate (agg: own
+// roots' aggregates, -1 otherwise), p0 = B_i / Bc, and the own aggregates'
+// Bc; on the host the local nodes whose aggregate is rooted on another rank
+// (PETSc's mis.c: a node deleted by a selected ghost joins that ghost's
+// aggregate, lid_parent_gid) with their coarse ids. Bc sums B^2 over the
+// members: its own in ascending order, then the other ranks' (each a sum in
+// their ascending order) in rank order.
+struct DistMis {
+    int32_t na = 0, rounds = 0;
+    std::vector<int64_t> cstarts;
+    double *d_cg = nullptr, *d_p0 = nullptr, *d_Bc = nullptr;
+    int32_t *d_agg = nullptr;
+    std::vector<int32_t> rnode;
+    std::vector<int64_t> rcg;
+    ~DistMis() { release(); }
+    void release() {
+        hipFree(d_cg); hipFree(d_p0); hipFree(d_Bc); hipFree(d_agg);
+        d_cg = d_p0 = d_Bc = nullptr;
+        d_agg = nullptr;
+    }
+};
+
+// the ghost values of d_x in M->d_ghost, ordered on the null stream
+int halo_device(aijhip_mpiaij *M, const double *d_x) {
+    int rc = aijhip_mpi::halo_post(M, d_x, nullptr);
+    if (!rc) rc = aijhip_mpi::halo_finish(M, nullptr);
+    return rc;
+}
+
+int dist_mis(aijhip_comm *C, aijhip_gamg_mpi::Level &L, const aijhip_gamg_params_t &p, int32_t level,
+             const aijhip_gamg::StrengthGraph &S, const double *d_B, bool b_ones, DistMis &out) {
+    const int32_t m = L.m, ng = (int32_t)L.ghost_gid.size();
+    const int P = C->nranks, me = C->rank;
+    const int64_t rstart = L.rstart, M = L.starts[P];
+    const bool square = level < p.square_graph;
+    const bool log = std::getenv("AIJHIP_GAMG_LOG") != nullptr;
+    aijhip_mpiaij *op = L.op;
+    const unsigned g = nblk(m);
+    int rc = AIJHIP_OK;
+    hipError_t e = hipSuccess;
+    double *gd = nullptr, *val = nullptr, *amin = nullptr;
+    int32_t *cnt = nullptr, *soi = nullptr, *soj = nullptr, *flag = nullptr, *idx = nullptr;
+    int32_t *rnode_d = nullptr;
+    int64_t *ggid = nullptr, *hi = nullptr, *parent = nullptr, *rpar_d = nullptr;
+    uint32_t *hk = nullptr;
+    dmis_t *state = nullptr;
+    unsigned *wcount = nullptr, *rcount = nullptr;
+    unsigned long long *left = nullptr;
+    int64_t nso = 0;
+#define DM(call, what) do { if ((e = (call)) != hipSuccess) { rc = gerr(e, what); goto done; } } while (0)
+#define DMRC(call) do { if ((rc = (call))) goto done; } while (0)
+    // ---- S_o: the ghosts' diagonal through the halo, then the filter
+    DM(dalloc(&gd, std::max(ng, 1)), "alloc");
+    DMRC(halo_device(op, S.d));
+    if (ng > 0) DM(hipMemcpyAsync(gd, op->d_ghost, sizeof(double) * (size_t)ng, hipMemcpyDeviceToDevice, nullptr), "copy");
+    DM(dalloc(&cnt, m), "alloc");
+    DM(hipMemsetAsync(cnt, 0, sizeof(int32_t) * (size_t)std::max(m, 1), nullptr), "memset");
+    if (L.Ao && ng > 0) {
+        const aijhip::RowList R = aijhip::row_list(*L.Ao);
+        if (R.nr > 0)
+            hipLaunchKernelGGL(k_dm_so_count, dim3(nblk(R.nr)), dim3(256), 0, nullptr, R.nr, R.rai, R.ridx,
+                               L.Ao->d_aa, S.d, gd, L.Ao->d_aj, p.threshold, cnt);
+        DMRC(scan_lengths(cnt, m, &soi, &nso));
+        DM(dalloc(&soj, std::max<int64_t>(nso, 1)), "alloc");
+        if (R.nr > 0)
+            hipLaunchKernelGGL(k_dm_so_fill, dim3(nblk(R.nr)), dim3(256), 0, nullptr, R.nr, R.rai, R.ridx,
+                               L.Ao->d_aa, S.d, gd, L.Ao->d_aj, p.threshold, soi, soj);
+    } else {
+        DMRC(scan_lengths(cnt, m, &soi, &nso));
+        DM(dalloc(&soj, 1), "alloc");
+    }
+    // ---- the rounds
+    DM(dalloc(&state, m), "alloc");
+    DM(dalloc(&hk, m), "alloc");
+    DM(dalloc(&val, m), "alloc");
+    DM(dalloc(&amin, m), "alloc");
+    DM(dalloc(&wcount, g), "alloc");
+    DM(dalloc(&left, 1), "alloc");
+    if (m > 0) hipLaunchKernelGGL(k_dm_init, dim3(g), dim3(256), 0, nullptr, m, rstart, level, S.si, soi, state, hk);
+    {
+        constexpr int32_t kBatch = 4;
+        bool done_all = false;
+        for (int64_t r0 = 0; !done_all && r0 <= M; r0 += kBatch) {
+            for (int32_t r = 0; r < kBatch; ++r) {
+                if (m > 0) hipLaunchKernelGGL(k_dm_value, dim3(g), dim3(256), 0, nullptr, m, rstart, state, hk, false, val);
+                DMRC(halo_device(op, val));
+                if (m > 0)
+                    hipLaunchKernelGGL(k_dm_closed_min, dim3(g), dim3(256), 0, nullptr, m, rstart, S.si, S.sj, soi, soj,
+                                       state, hk, op->d_ghost, false, amin);
+                DMRC(halo_device(op, amin));
+                if (m > 0)
+                    hipLaunchKernelGGL(k_dm_decide, dim3(g), dim3(256), 0, nullptr, m, rstart, S.si, S.sj, soi, soj,
+                                       square, hk, amin, op->d_ghost, state, wcount);
+            }
+            unsigned long long h_left = 0;
+            if (m > 0) {
+                hipLaunchKernelGGL(k_dm_total, dim3(1), dim3(1024), 0, nullptr, wcount, (int32_t)g, left);
+                DM(hipMemcpy(&h_left, left, sizeof(h_left), hipMemcpyDeviceToHost), "count");
+            }
+            double tot = (double)h_left;
+            DMRC(aijhip_mpi::comm_allreduce_host(C, &tot, 1));
+            out.rounds = (int32_t)(r0 + kBatch);
+            if (log)
+                std::fprintf(stderr, "[rank %d] distributed MIS level %d rounds %lld-%lld: %.0f undecided\n", me, level,
+                             (long long)r0, (long long)(r0 + kBatch - 1), tot);
+            done_all = tot == 0.0;
+        }
+        if (!done_all) {
+            rc = mfail(AIJHIP_ERR_STATE, "distributed GAMG: the MIS rounds did not finish");
+            goto done;
+        }
+    }
+    // ---- parents: the roots' keys within reach (and smoothAggs' neighbours)
+    DM(dalloc(&ggid, std::max(ng, 1)), "alloc");
+    if (ng > 0) DM(hipMemcpy(ggid, L.ghost_gid.data(), sizeof(int64_t) * (size_t)ng, hipMemcpyHostToDevice), "ghost ids");
+    DM(dalloc(&hi, m), "alloc");
+    DM(dalloc(&parent, m), "alloc");
+    DM(dalloc(&flag, m), "alloc");
+    if (m > 0) hipLaunchKernelGGL(k_dm_value, dim3(g), dim3(256), 0, nullptr, m, rstart, state, hk, true, val);
+    DMRC(halo_device(op, val));
+    if (m > 0) {
+        hipLaunchKernelGGL(k_dm_hiroot, dim3(g), dim3(256), 0, nullptr, m, rstart, S.si, S.sj, soi, soj, state,
+                           op->d_ghost, ggid, hi);
+        hipLaunchKernelGGL(k_dm_closed_min, dim3(g), dim3(256), 0, nullptr, m, rstart, S.si, S.sj, soi, soj, state, hk,
+                           op->d_ghost, true, amin);
+    }
+    DMRC(halo_device(op, amin));
+    if (m > 0)
+        hipLaunchKernelGGL(k_dm_parent, dim3(g), dim3(256), 0, nullptr, m, rstart, S.si, S.sj, soi, soj, square, amin,
+                           op->d_ghost, state, hi, parent, flag);
+    {
+        int64_t na64 = 0;
+        DMRC(scan_lengths(flag, m, &idx, &na64));
+        out.na = (int32_t)na64;
+    }
+    {
+        std::vector<int64_t> all;
+        DMRC(all_values(C, out.na, all));
+        out.cstarts.assign((size_t)P + 1, 0);
+        for (int q = 0; q < P; ++q) out.cstarts[q + 1] = out.cstarts[q] + all[q];
+    }
+    {
+        const int64_t cstart = out.cstarts[me];
+        DM(dalloc(&out.d_cg, m), "alloc");
+        DM(dalloc(&out.d_agg, m), "alloc");
+        DM(dalloc(&out.d_p0, m), "alloc");
+        DM(dalloc(&out.d_Bc, std::max(out.na, 1)), "alloc");
+        DM(dalloc(&rnode_d, m), "alloc");
+        DM(dalloc(&rpar_d, m), "alloc");
+        DM(dalloc(&rcount, 1), "alloc");
+        DM(hipMemset(rcount, 0, sizeof(unsigned)), "memset");
+        if (m > 0)
+            hipLaunchKernelGGL(k_dm_coarse, dim3(g), dim3(256), 0, nullptr, m, rstart, cstart, parent, idx, out.d_cg,
+                               out.d_agg, rnode_d, rpar_d, rcount);
+        unsigned nr = 0;
+        DM(hipMemcpy(&nr, rcount, sizeof(nr), hipMemcpyDeviceToHost), "remote count");
+        // own members' sums of squares, ascending (the single-GPU Bc before its root)
+        DM(aijhip_gamg::aggregate_sumsq_device(m, out.na, out.d_agg, b_ones ? nullptr : d_B, out.d_Bc, b_ones),
+           "aggregate sums");
+        // the members on this rank of other ranks' aggregates: sorted by node
+        std::vector<int32_t> rn(nr);
+        std::vector<int64_t> rp(nr);
+        std::vector<double> rb(nr, 1.0);
+        if (nr > 0) {
+            DM(hipMemcpy(rn.data(), rnode_d, sizeof(int32_t) * nr, hipMemcpyDeviceToHost), "remote nodes");
+            DM(hipMemcpy(rp.data(), rpar_d, sizeof(int64_t) * nr, hipMemcpyDeviceToHost), "remote parents");
+            std::vector<uint32_t> ord(nr);
+            std::iota(ord.begin(), ord.end(), 0u);
+            std::sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return rn[a] < rn[b]; });
+            std::vector<int32_t> rn2(nr);
+            std::vector<int64_t> rp2(nr);
+            for (unsigned k = 0; k < nr; ++k) { rn2[k] = rn[ord[k]]; rp2[k] = rp[ord[k]]; }
+            rn.swap(rn2);
+            rp.swap(rp2);
+            if (!b_ones) {  // B at those nodes
+                double *bv = nullptr;
+                DM(dalloc(&bv, nr), "alloc");
+                DM(hipMemcpy(rnode_d, rn.data(), sizeof(int32_t) * nr, hipMemcpyHostToDevice), "remote nodes");
+                hipLaunchKernelGGL(k_dm_gather_f64, dim3(nblk(nr)), dim3(256), 0, nullptr, (int32_t)nr, rnode_d, d_B, bv);
+                e = hipMemcpy(rb.data(), bv, sizeof(double) * nr, hipMemcpyDeviceToHost);
+                hipFree(bv);
+                if (e != hipSuccess) { rc = gerr(e, "remote B"); goto done; }
+            }
+        }
+        // requests: per owner, per parent (ascending) the sum of B^2 of its
+        // members here (in ascending node order)
+        std::vector<std::vector<uint64_t>> req((size_t)P), got;
+        std::vector<std::vector<int64_t>> asked((size_t)P);  // the parents asked of each owner, in order
+        {
+            std::vector<uint32_t> ord(nr);
+            std::iota(ord.begin(), ord.end(), 0u);
+            std::stable_sort(ord.begin(), ord.end(), [&](uint32_t a, uint32_t b) { return rp[a] < rp[b]; });
+            for (unsigned k = 0; k < nr;) {
+                const int64_t par = rp[ord[k]];
+                double s2 = 0.0;
+                unsigned j = k;
+                for (; j < nr && rp[ord[j]] == par; ++j) s2 += rb[ord[j]] * rb[ord[j]];
+                const int q = owner_of(L.starts, par);
+                uint64_t bits;
+                std::memcpy(&bits, &s2, 8);
+                req[q].push_back((uint64_t)par);
+                req[q].push_back(bits);
+                asked[q].push_back(par);
+                k = j;
+            }
+        }
+        DMRC(aijhip_mpi::comm_sendrecv(C, req, got));
+        // owner: the requested roots' local aggregates, the other ranks'
+        // contributions added (rank order), then Bc and the replies
+        std::vector<int32_t> rroot;  // every requested root (local index), in (rank, message) order
+        for (int q = 0; q < P; ++q) {
+            if (q == me) continue;
+            for (size_t k = 0; k + 1 < got[q].size(); k += 2) {
+                const int64_t par = (int64_t)got[q][k];
+                if (par < rstart || par >= rstart + m) {
+                    rc = mfail(AIJHIP_ERR_COMM, "distributed GAMG: a root request for another rank's node");
+                    goto done;
+                }
+                rroot.push_back((int32_t)(par - rstart));
+            }
+        }
+        std::vector<int32_t> ragg(rroot.size());
+        if (!rroot.empty()) {
+            int32_t *at = nullptr, *o = nullptr;
+            const int32_t n = (int32_t)rroot.size();
+            if ((e = dalloc(&at, n)) == hipSuccess && (e = dalloc(&o, n)) == hipSuccess &&
+                (e = hipMemcpy(at, rroot.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice)) == hipSuccess) {
+                hipLaunchKernelGGL(k_dm_gather_i32, dim3(nblk(n)), dim3(256), 0, nullptr, n, at, idx, o);
+                e = hipMemcpy(ragg.data(), o, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost);
+            }
+            hipFree(at);
+            hipFree(o);
+            if (e != hipSuccess) { rc = gerr(e, "requested roots"); goto done; }
+        }
+        {
+            // per aggregate the other ranks' sums, added in rank order
+            std::vector<std::pair<int32_t, double>> adds;
+            size_t t = 0;
+            for (int q = 0; q < P; ++q) {
+                if (q == me) continue;
+                for (size_t k = 0; k + 1 < got[q].size(); k += 2, ++t) {
+                    double v;
+                    std::memcpy(&v, &got[q][k + 1], 8);
+                    adds.emplace_back(ragg[t], v);
+                }
+            }
+            std::stable_sort(adds.begin(), adds.end(),
+                             [](const std::pair<int32_t, double> &a, const std::pair<int32_t, double> &b) {
+                                 return a.first < b.first;
+                             });
+            std::vector<int32_t> aa_i;
+            std::vector<double> aa_v;
+            for (size_t k = 0; k < adds.size();) {
+                double v = 0.0;
+                size_t j = k;
+                for (; j < adds.size() && adds[j].first == adds[k].first; ++j) v += adds[j].second;
+                aa_i.push_back(adds[k].first);
+                aa_v.push_back(v);
+                k = j;
+            }
+            if (!aa_i.empty()) {
+                int32_t *di = nullptr;
+                double *dv = nullptr;
+                const int32_t n = (int32_t)aa_i.size();
+                if ((e = dalloc(&di, n)) == hipSuccess && (e = dalloc(&dv, n)) == hipSuccess &&
+                    (e = hipMemcpy(di, aa_i.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice)) == hipSuccess &&
+                    (e = hipMemcpy(dv, aa_v.data(), sizeof(double) * (size_t)n, hipMemcpyHostToDevice)) == hipSuccess)
+                    hipLaunchKernelGGL(k_dm_add_at, dim3(nblk(n)), dim3(256), 0, nullptr, n, di, dv, out.d_Bc);
+                if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+                hipFree(di);
+                hipFree(dv);
+                if (e != hipSuccess) { rc = gerr(e, "remote sums"); goto done; }
+            }
+        }
+        if (out.na > 0) hipLaunchKernelGGL(k_dm_sqrt, dim3(nblk(out.na)), dim3(256), 0, nullptr, out.na, out.d_Bc);
+        if (m > 0)
+            hipLaunchKernelGGL(k_dm_p0, dim3(g), dim3(256), 0, nullptr, m, out.d_agg, b_ones ? nullptr : d_B, out.d_Bc,
+                               out.d_p0);
+        // replies: per request (in its order) the coarse id and Bc
+        std::vector<double> rbc(ragg.size());
+        if (!ragg.empty()) {
+            int32_t *at = nullptr;
+            double *o = nullptr;
+            const int32_t n = (int32_t)ragg.size();
+            if ((e = dalloc(&at, n)) == hipSuccess && (e = dalloc(&o, n)) == hipSuccess &&
+                (e = hipMemcpy(at, ragg.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice)) == hipSuccess) {
+                hipLaunchKernelGGL(k_dm_gather_f64, dim3(nblk(n)), dim3(256), 0, nullptr, n, at, out.d_Bc, o);
+                e = hipMemcpy(rbc.data(), o, sizeof(double) * (size_t)n, hipMemcpyDeviceToHost);
+            }
+            hipFree(at);
+            hipFree(o);
+            if (e != hipSuccess) { rc = gerr(e, "replies"); goto done; }
+        }
+        std::vector<std::vector<uint64_t>> rep((size_t)P), back;
+        {
+            size_t t = 0;
+            for (int q = 0; q < P; ++q) {
+                if (q == me) continue;
+                for (size_t k = 0; k + 1 < got[q].size(); k += 2, ++t) {
+                    uint64_t bits;
+                    std::memcpy(&bits, &rbc[t], 8);
+                    rep[q].push_back((uint64_t)(cstart + ragg[t]));
+                    rep[q].push_back(bits);
+                }
+            }
+        }
+        DMRC(aijhip_mpi::comm_sendrecv(C, rep, back));
+        // this rank's members of other ranks' aggregates: coarse id, p0
+        std::vector<int64_t> pcg;  // per parent asked (owner order, then ascending)
+        std::vector<double> pbc;
+        std::vector<int64_t> plist;
+        for (int q = 0; q < P; ++q) {
+            if (q == me) continue;
+            if (back[q].size() != 2 * asked[q].size()) {
+                rc = mfail(AIJHIP_ERR_COMM, "distributed GAMG: short root reply");
+                goto done;
+            }
+            for (size_t k = 0; k < asked[q].size(); ++k) {
+                plist.push_back(asked[q][k]);
+                pcg.push_back((int64_t)back[q][2 * k]);
+                double v;
+                std::memcpy(&v, &back[q][2 * k + 1], 8);
+                pbc.push_back(v);
+            }
+        }
+        std::vector<uint32_t> pord(plist.size());
+        std::iota(pord.begin(), pord.end(), 0u);
+        std::sort(pord.begin(), pord.end(), [&](uint32_t a, uint32_t b) { return plist[a] < plist[b]; });
+        out.rnode = rn;
+        out.rcg.assign(nr, -1);
+        std::vector<double> cgv(nr), p0v(nr);
+        for (unsigned k = 0; k < nr; ++k) {
+            const auto it = std::lower_bound(pord.begin(), pord.end(), rp[k],
+                                             [&](uint32_t a, int64_t v) { return plist[a] < v; });
+            if (it == pord.end() || plist[*it] != rp[k]) {
+                rc = mfail(AIJHIP_ERR_COMM, "distributed GAMG: a root without a reply");
+                goto done;
+            }
+            out.rcg[k] = pcg[*it];
+            cgv[k] = (double)pcg[*it];
+            const double c = pbc[*it];
+            p0v[k] = c > 0.0 ? rb[k] / c : 0.0;
+        }
+        if (nr > 0) {
+            double *dc = nullptr, *dp = nullptr;
+            if ((e = dalloc(&dc, nr)) == hipSuccess && (e = dalloc(&dp, nr)) == hipSuccess &&
+                (e = hipMemcpy(rnode_d, rn.data(), sizeof(int32_t) * nr, hipMemcpyHostToDevice)) == hipSuccess &&
+                (e = hipMemcpy(dc, cgv.data(), sizeof(double) * nr, hipMemcpyHostToDevice)) == hipSuccess &&
+                (e = hipMemcpy(dp, p0v.data(), sizeof(double) * nr, hipMemcpyHostToDevice)) == hipSuccess)
+                hipLaunchKernelGGL(k_dm_set_remote, dim3(nblk(nr)), dim3(256), 0, nullptr, (int32_t)nr, rnode_d, dc, dp,
+                                   out.d_cg, out.d_p0);
+            if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+            hipFree(dc);
+            hipFree(dp);
+            if (e != hipSuccess) { rc = gerr(e, "remote members"); goto done; }
+        }
+        if (log)
+            std::fprintf(stderr, "[rank %d] distributed MIS level %d: %d rounds, %d own aggregates, %u members of "
+                         "other ranks' aggregates\n", me, level, out.rounds, out.na, nr);
+    }
+    DM(hipGetLastError(), "distributed MIS");
+done:
+#undef DM
+#undef DMRC
+    hipFree(gd); hipFree(val); hipFree(amin); hipFree(cnt); hipFree(soi); hipFree(soj); hipFree(flag); hipFree(idx);
+    hipFree(rnode_d); hipFree(ggid); hipFree(hi); hipFree(parent); hipFree(rpar_d); hipFree(hk); hipFree(state);
+    hipFree(wcount); hipFree(rcount); hipFree(left);
+    if (rc) out.release();
+    return rc;
+}
+
 }  // namespace
 
 namespace aijhip_gamg_mpi {
@@ -899,15 +1526,38 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
                 if (emax_rc) emax_err = aijhip_last_error();
             });
         }
-        // ---- local aggregates
+        // ---- aggregates: PETSc's parallel MIS across the ranks (coarsen 1,
+        // dist_mis: the strength graph of A_d from the single-GPU steps, the
+        // rounds over the level's halo), or the greedy pass on each rank's
+        // diagonal block (coarsen 0; aggregates local)
         int32_t *d_agg = nullptr, na = 0;
         double *dinv = nullptr;
-        rc = aijhip_gamg::aggregate_level(*L.Ad, p, &d_agg, &na, &dinv, 0, nullptr, nullptr, l);
+        const bool dmis = p.coarsen == 1;
+        aijhip_gamg::StrengthGraph S;
+        DistMis DMo;
+        rc = aijhip_gamg::aggregate_level(*L.Ad, p, &d_agg, &na, &dinv, 0, nullptr, nullptr, l, dmis ? &S : nullptr);
         if (emax_th.joinable()) emax_th.join();
         hipFree(dinv_e);
         if (!rc && emax_rc) {
             rc = emax_rc;
             aijhip::set_error(emax_err);
+        }
+        if (dmis) {
+            // every rank's outcome so far, before the rounds' collectives
+            std::vector<int64_t> ok_all;
+            const int lrc = rc;
+            const int crc = all_values(C, lrc ? -1 : 0, ok_all);
+            bool peer = false;
+            if (!crc)
+                for (int64_t v : ok_all) peer = peer || v < 0;
+            if (!lrc && !crc && !peer) rc = dist_mis(C, L, p, (int32_t)l, S, d_B, l == 0, DMo);
+            else rc = lrc ? lrc : crc ? crc : mfail(AIJHIP_ERR_COMM, ("distributed GAMG: another rank failed at level " +
+                                                                    std::to_string(l)).c_str());
+            hipFree(S.si); hipFree(S.sj); hipFree(S.d);
+            hipFree(d_agg);
+            d_agg = DMo.d_agg;
+            DMo.d_agg = nullptr;
+            na = DMo.na;
         }
         // the level's first collective carries this rank's outcome (-1 =
         // failed): a failure on one rank (allocation, aggregation, emax) ends
@@ -942,11 +1592,17 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
         // ---- tentative prolongator and its ghost rows (aggregate gid, value)
         double *d_p0 = nullptr, *d_Bc = nullptr, *d_v = nullptr;
         std::vector<double> g_agg, g_p0;
-        if ((e = dalloc(&d_p0, m)) != hipSuccess || (e = dalloc(&d_Bc, na)) != hipSuccess ||
+        if (dmis) {  // (dist_mis made them: coarse ids cover the members of other ranks' aggregates)
+            d_p0 = DMo.d_p0;
+            d_Bc = DMo.d_Bc;
+            d_v = DMo.d_cg;
+            DMo.d_p0 = DMo.d_Bc = DMo.d_cg = nullptr;
+            rc = halo_values(L.op, d_v, g_agg);
+        } else if ((e = dalloc(&d_p0, m)) != hipSuccess || (e = dalloc(&d_Bc, na)) != hipSuccess ||
             (e = dalloc(&d_v, m)) != hipSuccess || (e = aijhip_gamg::tentative_device(m, na, d_agg, d_B, d_Bc, d_p0, l == 0)) !=
-                                                       hipSuccess)
+                                                       hipSuccess) {
             rc = gerr(e, "tentative prolongator");
-        if (!rc) {
+        } else {
             if (m > 0) hipLaunchKernelGGL(k_coarse_gid, dim3(nblk(m)), dim3(256), 0, nullptr, m, cstart, d_agg, d_v);
             rc = halo_values(L.op, d_v, g_agg);
         }
@@ -960,12 +1616,31 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
             if (g_agg[s] < 0) ghost_removed = true;
             else e1_off.push_back((int64_t)g_agg[s]);
         }
+        for (int64_t c : DMo.rcg) e1_off.push_back(c);  // this rank's members of other ranks' aggregates
         std::sort(e1_off.begin(), e1_off.end());
         e1_off.erase(std::unique(e1_off.begin(), e1_off.end()), e1_off.end());
         auto e1_id = [&](int64_t gidc) -> int32_t {
             if (gidc >= cstart && gidc < cstart + na) return (int32_t)(gidc - cstart);
             return na + (int32_t)(std::lower_bound(e1_off.begin(), e1_off.end(), gidc) - e1_off.begin());
         };
+        // their P0 column: the E1 slot of that aggregate
+        if (!rc && !DMo.rnode.empty()) {
+            const int32_t n = (int32_t)DMo.rnode.size();
+            std::vector<int32_t> col((size_t)n);
+            for (int32_t k = 0; k < n; ++k) col[k] = e1_id(DMo.rcg[k]);
+            int32_t *dn = nullptr, *dc = nullptr;
+            if ((e = dalloc(&dn, n)) != hipSuccess || (e = dalloc(&dc, n)) != hipSuccess ||
+                (e = hipMemcpy(dn, DMo.rnode.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice)) != hipSuccess ||
+                (e = hipMemcpy(dc, col.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice)) != hipSuccess)
+                rc = gerr(e, "P0 columns");
+            if (!rc) {
+                hipLaunchKernelGGL(k_dm_set_i32, dim3(nblk(n)), dim3(256), 0, nullptr, n, dn, dc, d_agg);
+                if ((e = hipStreamSynchronize(nullptr)) != hipSuccess) rc = gerr(e, "P0 columns");
+            }
+            hipFree(dn);
+            hipFree(dc);
+        }
+        DMo.release();
         // A_ext = [A_d | A_o] (ghost columns after the local ones)
         DCsr Aext, P0ext, T, Plocal;
         std::vector<int32_t> oai, oaj;

@@ -18,7 +18,10 @@
  * its, reason, rnorm and the history back through the usual KSP getters.
  * Any other operator or PC falls back to PETSc's own KSPCG, run as an inner
  * KSP on the caller's operators and PC (this KSP never changes its own type,
- * so nothing it owns is freed under a running solve).
+ * so nothing it owns is freed under a running solve). While the device path
+ * is active ksp->pc is a PCNONE stand-in (KSPCGHIPStandIn): KSPGetPC /
+ * PCView then show the stand-in, and the caller's PC is reachable again after
+ * a fall-back or KSPDestroy.
  *
  * STATUS: not yet working code until it is compiled and run against PETSc
  * 3.7 — the PETSc-facing half is written to the 3.7 headers but has never
@@ -104,15 +107,31 @@ static PetscErrorCode KSPCGHIPStandIn(KSP ksp)
   PetscFunctionReturn(0);
 }
 
-/* Give the caller's PC back to ksp->pc (the fall-back runs PETSc's CG on it). */
+/* Give the caller's PC back to ksp->pc (the fall-back runs PETSc's CG on it).
+ * A KSPSetOperators made after the stand-in went in reached the stand-in
+ * (ksp->pc), not the caller's PC: those operators move to the caller's PC
+ * here, so the fall-back and any later KSPGetPC see the current system. */
 static PetscErrorCode KSPCGHIPRestorePC(KSP ksp)
 {
   KSP_CGHIP      *c = (KSP_CGHIP*)ksp->data;
+  Mat            Amat = NULL, Pmat = NULL;
+  PetscBool      has = PETSC_FALSE;
   PetscErrorCode ierr;
 
   PetscFunctionBegin;
   if (!c->user_pc) PetscFunctionReturn(0);
+  ierr = PCGetOperatorsSet(ksp->pc, &has, NULL);CHKERRQ(ierr);
+  if (has) { /* held across KSPSetPC, which frees the stand-in and its references */
+    ierr = PCGetOperators(ksp->pc, &Amat, &Pmat);CHKERRQ(ierr);
+    ierr = PetscObjectReference((PetscObject)Amat);CHKERRQ(ierr);
+    ierr = PetscObjectReference((PetscObject)Pmat);CHKERRQ(ierr);
+  }
   ierr = KSPSetPC(ksp, c->user_pc);CHKERRQ(ierr);
+  if (has) {
+    ierr = PCSetOperators(c->user_pc, Amat, Pmat);CHKERRQ(ierr);
+    ierr = MatDestroy(&Amat);CHKERRQ(ierr);
+    ierr = MatDestroy(&Pmat);CHKERRQ(ierr);
+  }
   ierr = PCDestroy(&c->user_pc);CHKERRQ(ierr); /* drops the reference taken by KSPCGHIPStandIn */
   PetscFunctionReturn(0);
 }
@@ -129,7 +148,7 @@ static PetscErrorCode KSPCGHIPFallBack(KSP ksp)
   PetscFunctionBegin;
   ierr = PetscInfo(ksp, "cghip: operator or PC not on the device; using KSPCG\n");CHKERRQ(ierr);
   ierr = KSPCGHIPFree(c);CHKERRQ(ierr);
-  ierr = KSPCGHIPRestorePC(ksp);CHKERRQ(ierr);
+  ierr = KSPCGHIPRestorePC(ksp);CHKERRQ(ierr); /* (carries the current operators to the caller's PC) */
   if (!c->inner) {
     ierr = KSPCreate(PetscObjectComm((PetscObject)ksp), &c->inner);CHKERRQ(ierr);
     ierr = KSPSetType(c->inner, KSPCG);CHKERRQ(ierr);

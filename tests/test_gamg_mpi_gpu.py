@@ -231,3 +231,19 @@ def test_gpu_gamg_mpi_fused_smoothers_within_tolerance_of_petsc_order():
         h0 = b["hist"][0]
         np.testing.assert_allclose(a["hist"], b["hist"], rtol=1e-10, atol=1e-14 * h0)
         np.testing.assert_allclose(a["x"], b["x"], rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_gpu_gamg_across_ranks_is_partition_independent():
+    """PETSc's parallel MIS exchanges ghost states every round (VERDICT r05
+    item 4); restated as the global MIS by global keys, the device's
+    hierarchy at 2, 3 and 4 ranks has the one-rank distributed set-up's level
+    sizes and entry counts and CG takes the same iterations (no extra
+    aggregates along the slab boundaries)."""
+    dims = (12, 12, 24)
+    one = _run(1, dims, ("gamg",), env={"AIJHIP_GAMG_DIST": "1"})[0]["gamg"]
+    for world in (2, 3, 4):
+        g = _run(world, dims, ("gamg",))[0]["gamg"]
+        print(f"{world} ranks: levels {g['rows']} its {g['its']} (1 rank: {one['rows']} {one['its']})")
+        assert g["rows"] == one["rows"] and g["nnz"] == one["nnz"], world
+        assert g["its"] == one["its"], world
