@@ -247,8 +247,9 @@ int plan_stream(aijhip_mat *A) {
             (e = hipMemset(P.d_sslot, 0, sizeof(uint16_t) * nzp)) != hipSuccess ||
             (e = aijhip::build_gather_order(*A, P, false)) != hipSuccess)
             return hipfail(e, "plan: gather-ordered blocks");
-        // 16-bit columns when every block's columns span < 2^16 (banded
-        // operators): the packed form replaces the 32-bit sorted columns
+        // the packed form (20-bit columns and 12-bit slots, one word per
+        // entry) when the blocks' columns span < 2^20 and their caps fit the
+        // slots: it replaces the 32-bit sorted columns (12 B per entry, not 14)
         int32_t *d_base = nullptr, *d_span = nullptr;
         std::vector<int32_t> span((size_t)P.n_blocks);
         if ((e = dmalloc(&d_base, (size_t)P.n_blocks, nullptr)) != hipSuccess ||
@@ -260,15 +261,17 @@ int plan_stream(aijhip_mat *A) {
             return hipfail(e, "plan: gather-ordered spans");
         }
         hipFree(d_span);
-        // blocks whose columns span < 2^16 take the 16-bit form; when most
+        // blocks whose columns span < 2^20 take the packed form; when most
         // do, the others (a wide row within the block cap) are launched from
         // the original arrays
+        constexpr int32_t kNarrowSpan = 1 << aijhip::kPackedColBits;
+        const bool slots_fit = aijhip::kStreamGeoms[P.tune.geom].nnz_cap <= aijhip::kPackedMaxCap;
         int64_t narrow_nz = 0, nz_all = 0;
         for (size_t b = 0; b < blocks.size(); ++b) {
             nz_all += blocks[b].nk;
-            if (span[b] < 65536) narrow_nz += blocks[b].nk;
+            if (span[b] < kNarrowSpan) narrow_nz += blocks[b].nk;
         }
-        if (narrow_nz > 0 && 10 * narrow_nz >= 9 * nz_all) {
+        if (slots_fit && narrow_nz > 0 && 10 * narrow_nz >= 9 * nz_all) {
             std::vector<BlockDesc> nb, wb;
             std::vector<int32_t> nbase, base((size_t)P.n_blocks);
             if ((e = hipMemcpy(base.data(), d_base, sizeof(int32_t) * base.size(), hipMemcpyDeviceToHost)) != hipSuccess) {
@@ -276,7 +279,7 @@ int plan_stream(aijhip_mat *A) {
                 return hipfail(e, "plan: gather-ordered spans");
             }
             for (size_t b = 0; b < blocks.size(); ++b) {
-                if (span[b] < 65536) {
+                if (span[b] < kNarrowSpan) {
                     nb.push_back(blocks[b]);
                     nbase.push_back(base[b]);
                 } else {
@@ -284,13 +287,13 @@ int plan_stream(aijhip_mat *A) {
                 }
             }
             hipFree(d_base);
-            const size_t words = 4 * ((size_t)A->nz / 2 + 2);
+            const size_t words = (size_t)A->nz + 4;
             if ((e = dmalloc(&P.d_sidx, words, &P.bytes)) != hipSuccess ||
-                (e = hipMemset(P.d_sidx, 0, sizeof(uint16_t) * words)) != hipSuccess ||
+                (e = hipMemset(P.d_sidx, 0, sizeof(uint32_t) * words)) != hipSuccess ||
                 (e = dmalloc(&P.d_sbase, nbase.size(), &P.bytes)) != hipSuccess ||
                 (e = hipMemcpy(P.d_sbase, nbase.data(), sizeof(int32_t) * nbase.size(), hipMemcpyHostToDevice)) !=
                     hipSuccess)
-                return hipfail(e, "plan: gather-ordered 16-bit form");
+                return hipfail(e, "plan: gather-ordered packed form");
             if (!wb.empty()) {
                 if ((e = dmalloc(&P.d_nblocks, nb.size(), &P.bytes)) != hipSuccess ||
                     (e = dmalloc(&P.d_wblocks, wb.size(), &P.bytes)) != hipSuccess ||
@@ -306,7 +309,7 @@ int plan_stream(aijhip_mat *A) {
             if ((e = aijhip::pack_gather_order(P, wb.empty() ? P.d_blocks : P.d_nblocks, (int32_t)nb.size(), P.d_sbase,
                                                P.d_sidx)) != hipSuccess ||
                 (e = hipDeviceSynchronize()) != hipSuccess)
-                return hipfail(e, "plan: gather-ordered 16-bit form");
+                return hipfail(e, "plan: gather-ordered packed form");
             hipFree(P.d_saj);  // (d_sslot stays: it re-orders new values, aijhip_mat_update_values)
             P.bytes -= (int64_t)sizeof(int32_t) * (int64_t)nzp;
             P.d_saj = nullptr;
@@ -471,13 +474,13 @@ int plan_build(aijhip_mat *A) {
         }
         // Long rows on a caller's handle: the gather-ordered copy of the row
         // blocks (Tuning::gsort; x read in column order within a block, the
-        // sums unchanged) at geometry 6, plain loads, when its 16-bit form
+        // sums unchanged) at geometry 6, plain loads, when its packed form
         // fits (below) — measured: skewed stand-in 406 -> 325 us, its
         // ordinary rows 342 -> 256, the FEM-structured one 287 -> 271
         // (profiles/r03/gsort_*.jsonl); the 7-pt Poisson (short rows) stays
         // unsorted (sorted: 551 vs 492 us). The set-up's own operators (GAMG
         // levels, P, Pᵀ; aijhip_mat::setup_op) take it for long rows too and
-        // keep the 32-bit sorted columns when the 16-bit form does not fit.
+        // keep the 32-bit sorted columns when the packed form does not fit.
         if (P.tune.gsort < 0) P.tune.gsort = long_rows ? 1 : 0;
         const bool sorted = P.tune.gsort > 0;
         if (P.tune.geom < 0) P.tune.geom = (scattered && !sorted) ? 1 : 6;
@@ -513,8 +516,8 @@ int plan_build(aijhip_mat *A) {
             }
             int rc = plan_stream(A);
             if (!rc && auto_sort && P.tune.gsort > 0 && !P.d_sidx) {
-                // automatic and the 16-bit form did not fit (blocks spanning
-                // 2^16 columns and more): the original layout, the geometry
+                // automatic and the packed form did not fit (blocks spanning
+                // 2^20 columns and more): the original layout, the geometry
                 // and loads the gather locality picks without it
                 const aijhip::Tuning req = A->requested_tune;
                 free_plan(A->plan);
@@ -777,7 +780,7 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
     A->device_bytes = 4 * ((int64_t)m + 1) + 12 * (nz + 2);
     A->setup_op = like ? like->setup_op : true;
     if (!like) {  // the set-up's own operators: no codes or patterns (plan time); the gather-ordered
-        // copy for long rows, 32-bit columns where the 16-bit form does not fit (GAMG's level 1
+        // copy for long rows, 32-bit columns where the packed form does not fit (GAMG's level 1
         // and Pᵀ) — round 5, 300³ CG + GAMG: solve 0.1652-0.1656 s vs 0.1783-0.1791 unsorted,
         // set-up 0.167 vs 0.156-0.162 s; sorting every operator 0.169-0.170 s (the finest P,
         // short rows, runs slower sorted); profiles/r05/as/, at/. AIJHIP_SETUP_GSORT
@@ -836,7 +839,7 @@ int64_t mult_layout_bytes(const aijhip_mat &A) {
         return 8 * nz + rows + m + 4 * (int64_t)P.n_ptab + vec;
     if (P.d_code)  // coded entries 10 B, blocks launched from aj 12 B, the dictionaries
         return 10 * (nz - P.nz_wide) + 12 * P.nz_wide + rows + vec + 4 * P.n_cmeta;
-    if (P.d_sidx)  // 16-bit columns and slots per entry pair (4 B per entry), sorted values, block bases
+    if (P.d_sidx)  // packed columns and slots (4 B per entry), sorted values, block bases
         return 12 * nz + rows + vec + 4 * (int64_t)(P.n_blocks - P.n_wblocks);
     if (P.d_sslot)  // sorted 32-bit columns + sorted values + 16-bit slots
         return 14 * nz + rows + vec;

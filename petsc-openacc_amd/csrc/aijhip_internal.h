@@ -104,7 +104,7 @@ struct Tuning {
                            // k > 0 pipelined in chunks of >= k rows
     int gsort = -1;        // gather-ordered copy of the row blocks (MatMult / MatMultAdd and the
                            // fused V-cycle launches): -1 auto (long rows; a caller's handle only
-                           // in the 16-bit form), 0 off, 1 on
+                           // in the packed form), 0 off, 1 on
     int codes = -1;        // 16-bit column codes instead of aj (Plan::d_code): -1 auto (where the
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
@@ -180,10 +180,15 @@ struct Plan {
     int32_t *d_saj = nullptr;
     double *d_saa = nullptr;
     uint16_t *d_sslot = nullptr;
-    // ... or, when every block's columns span < 2^16, 16-bit columns
-    // (relative to the block's first, d_sbase) and slots packed four per
-    // entry pair in d_sidx (d_saj / d_sslot then freed): 12 bytes per entry
-    uint16_t *d_sidx = nullptr;
+    // ... or, when the blocks' columns span < 2^20 (kPackedColBits), one
+    // 32-bit word per entry in d_sidx: the column relative to the block's
+    // first (d_sbase) in the low 20 bits, the product slot (< 4096: block
+    // caps <= 4096 entries) in the high 12 (d_saj / d_sslot then freed):
+    // 12 bytes per entry with aa. (Round 5 packed 16-bit columns and 16-bit
+    // slots per entry pair: the same bytes, but blocks spanning 2^16 columns
+    // and more — the GAMG level-1 operator's and P^T's — fell back to the
+    // 32-bit sorted columns, 14 bytes per entry.)
+    uint32_t *d_sidx = nullptr;
     int32_t *d_sbase = nullptr;
     // ... and when only some blocks are that narrow (a wide row within the
     // block cap: the skewed stand-in's shorter hub rows), the narrow blocks
@@ -240,7 +245,7 @@ struct aijhip_mat {
     int requested_lanes = 0;
     aijhip::Tuning requested_tune;
     // a set-up's own operator (GAMG levels, P, Pᵀ: adopt_device_csr): long
-    // rows keep the gather-ordered copy when its 16-bit form does not fit
+    // rows keep the gather-ordered copy when its packed form does not fit
     bool setup_op = false;
     // host-vector staging for aijhip_mat_mult_host (allocated on first use)
     double *d_xstage = nullptr, *d_ystage = nullptr;
@@ -304,7 +309,9 @@ hipError_t gather_order_spans(const Plan &P, int32_t *d_base, int32_t *d_span);
 // The 16-bit packed form of the sorted columns and slots of blocks
 // d_blk[0, nblk) (d_base: their first columns, in that order).
 hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk, const int32_t *d_base,
-                             uint16_t *d_sidx);
+                             uint32_t *d_sidx);
+constexpr int kPackedColBits = 20;  // the packed gather-ordered form: 20-bit columns, 12-bit slots
+constexpr int kPackedMaxCap = 1 << (32 - kPackedColBits);  // slots < 4096: block caps up to 4096 entries
 // Column codes: pass 0 counts each block's distinct column - row offsets
 // into d_cnt[0, nblk); pass 1 (d_cmeta laid out by the caller) writes the
 // dictionaries and the codes of blocks d_blk[0, nblk).

@@ -216,10 +216,10 @@ __device__ __forceinline__ void stream_block(
     // block's entries sorted by column, sslot their positions in the block,
     // where the products go; the row sums below read them in storage order
     constexpr bool SORTED = (NTMODE & 8) != 0;
-    // bit 4: the same with 16-bit columns and slots packed per entry pair in
-    // aj's place (aj[k], aj[k+1] = cols | slots << 16 ... see pack below):
-    // one 8-B load per pair as in CSR, columns relative to the block's
-    // first (sbase[b]); 12 bytes per entry like the original arrays
+    // bit 4: the same with each entry's column (relative to the block's
+    // first, sbase[b]; 20 bits) and slot (12 bits) packed in one word in
+    // aj's place (k_pack_gather_order): one 8-B load per pair as in CSR, 12
+    // bytes per entry like the original arrays
     constexpr bool S16 = (NTMODE & 16) != 0;
     // bit 5: column codes (Plan::d_code, full-row lists only): aj holds one
     // 16-bit code per entry, (row - row0) << b | index into the block's
@@ -357,18 +357,19 @@ __device__ __forceinline__ void stream_block(
         }
     }
     uint32_t sv[(SORTED || S16) ? ITERS : 1];  // the pairs' product slots (two 16-bit positions)
-    if constexpr (S16) {  // unpack: .x = two 16-bit columns (block-relative), .y = two slots
-        // A pair straddling a block edge carries the neighbour's half,
+    if constexpr (S16) {  // unpack: .x, .y = the pair's words (column | slot << 20)
+        // A pair straddling a block edge carries the neighbour's word,
         // relative to the neighbour's first column: that half is gathered
         // (never stored) at this block's first column instead, which exists.
         const int32_t base = sbase[b];
+        constexpr uint32_t cm = (1u << kPackedColBits) - 1u;
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
-            const uint32_t c = (uint32_t)cv[it].x;
-            sv[it] = (uint32_t)cv[it].y;
-            cv[it].x = base + (k >= k0 && k < k1 ? (int32_t)(c & 0xffffu) : 0);
-            cv[it].y = base + (k + 1 < k1 ? (int32_t)(c >> 16) : 0);
+            const uint32_t w0 = (uint32_t)cv[it].x, w1 = (uint32_t)cv[it].y;
+            sv[it] = (w0 >> kPackedColBits) | ((w1 >> kPackedColBits) << 16);
+            cv[it].x = base + (k >= k0 && k < k1 ? (int32_t)(w0 & cm) : 0);
+            cv[it].y = base + (k + 1 < k1 ? (int32_t)(w1 & cm) : 0);
         }
     }
     if constexpr (SORTED) {
@@ -884,19 +885,18 @@ __global__ void k_block_col_span(const BlockDesc *__restrict__ blk, int32_t nblk
     span[b] = hi - lo;
 }
 
-// 16-bit form: entry k of pair p = k / 2 at half h = k % 2 -> column
-// (relative to the block's first) in sidx[4p + h], slot in sidx[4p + 2 + h];
-// a pair shared by two blocks gets one half from each
+// packed form: entry k -> sidx[k] = (column - the block's first) | slot <<
+// kPackedColBits (aj's layout: a pair shared by two blocks gets one word
+// from each)
 __global__ __launch_bounds__(256) void k_pack_gather_order(const BlockDesc *__restrict__ blk,
                                                            const int32_t *__restrict__ saj,
                                                            const uint16_t *__restrict__ sslot,
-                                                           const int32_t *__restrict__ base, uint16_t *sidx) {
+                                                           const int32_t *__restrict__ base, uint32_t *sidx) {
     const BlockDesc d = blk[blockIdx.x];
     const int32_t b0 = base[blockIdx.x];
     for (int i = threadIdx.x; i < d.nk; i += 256) {
-        const int64_t k = (int64_t)d.k0 + i, p = k >> 1, h = k & 1;
-        sidx[4 * p + h] = (uint16_t)(saj[k] - b0);
-        sidx[4 * p + 2 + h] = sslot[k];
+        const int64_t k = (int64_t)d.k0 + i;
+        sidx[k] = (uint32_t)(saj[k] - b0) | ((uint32_t)sslot[k] << kPackedColBits);
     }
 }
 
@@ -1013,7 +1013,7 @@ hipError_t gather_order_spans(const Plan &P, int32_t *d_base, int32_t *d_span) {
 }
 
 hipError_t pack_gather_order(const Plan &P, const BlockDesc *d_blk, int32_t nblk, const int32_t *d_base,
-                             uint16_t *d_sidx) {
+                             uint32_t *d_sidx) {
     if (nblk == 0) return hipSuccess;
     hipLaunchKernelGGL(k_pack_gather_order, dim3(nblk), dim3(256), 0, nullptr, d_blk, P.d_saj, P.d_sslot, d_base,
                        d_sidx);
@@ -1387,7 +1387,7 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // (MatMult / MatMultAdd, full or compressed rows, dot epilogue)
     // (with the narrow / wide split, the dot epilogue's partials would come
     // from two launches: the CG's fused product takes the original arrays)
-    if (P.d_sidx && (P.n_wblocks == 0 || !dpart)) {  // 16-bit columns and slots packed per pair
+    if (P.d_sidx && (P.n_wblocks == 0 || !dpart)) {  // packed columns and slots, a word per entry
         const BlockDesc *nb = P.n_wblocks ? P.d_nblocks : P.d_blocks;
         const int32_t nn = P.n_wblocks ? P.n_nblocks : P.n_blocks;
 #define AIJHIP_SS(ADD, CROW, NTM)                                                                              \
@@ -1491,7 +1491,7 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     }
     // gather-ordered blocks: the products land in their storage slots, so the
     // fused epilogues see the same sums as from aj / aa
-    if (P.d_sidx && P.n_wblocks == 0 && P.tune.geom == 6) {  // 16-bit columns (planned at geometry 6)
+    if (P.d_sidx && P.n_wblocks == 0 && P.tune.geom == 6) {  // packed columns (planned at geometry 6)
         hipLaunchKernelGGL((k_spmv_stream<AIJHIP_GEOM(6), false, 80, Op>), dim3(P.n_blocks),
                            dim3(kStreamGeoms[6].threads), 0, s, P.d_blocks, P.n_blocks, ex, A.d_ai, nullptr,
                            reinterpret_cast<const int32_t *>(P.d_sidx), P.d_saa, op, dpart, stop, nullptr,

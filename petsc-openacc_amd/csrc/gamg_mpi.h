@@ -23,8 +23,9 @@ struct Level {
     aijhip_mpiaij *op = nullptr;   // MatMult_MPIAIJ + the level's p2p halo (level 0: the caller's)
     std::vector<int64_t> ghost_gid;  // global row of every ghost slot
     // transfer to level l+1: P = [Pd | Po] (Po's columns: level l+1's ghost
-    // slots), R = P^T = [Pd^T (attached to Pd) | Ro] (Ro's columns: this
-    // level's ghost slots)
+    // slots); R = P^T as MatMultTranspose_MPIAIJ: Pd^T (attached to Pd) and
+    // Po^T (attached to Po) whose ghost-slot sums go back to their owners
+    // (Ro: unused since round 6, always NULL)
     aijhip_mat *Pd = nullptr, *Po = nullptr, *Ro = nullptr;
     double emax = 0.0;
     double *dinv = nullptr, *b = nullptr, *x = nullptr, *r = nullptr;

@@ -8,13 +8,14 @@
 // aggregation, prolongator smoothing and Galerkin products span the MPIAIJ
 // operator [ext]. The same structure here, MI355X-first:
 //
-//   aggregates   local to each rank (PETSc's agg GAMG keeps aggregates on
-//                their owner too): the single-GPU steps (gamg_device.hip
-//                aggregate_level) on the diagonal block A_d — PETSc's MIS
-//                (coarsen 1, the default; the graph of A_d, keys at local
-//                indices, so roots on either side of a rank boundary may
-//                be neighbours: PETSc's MIS also exchanges ghost states) or
-//                the greedy pass (coarsen 0);
+//   aggregates   PETSc's parallel MIS (coarsen 1, the default; dist_mis):
+//                ghost states exchanged every round over the level's halo,
+//                restated as the global MIS by global keys — roots on either
+//                side of a rank boundary are independent, a node taken by a
+//                root on another rank joins that aggregate (as mis.c's
+//                lid_parent_gid), and the aggregates are the single-GPU ones
+//                whatever the partition; or the greedy pass on each rank's
+//                diagonal block A_d (coarsen 0, aggregates local);
 //   emax         CG's Lanczos estimate (eig_ksp 1, the default) or a power
 //                iteration on the distributed D^-1 A (MatMult_MPIAIJ +
 //                all-reduced dots), from the single-GPU start vector taken
@@ -29,8 +30,9 @@
 //                that belong to other ranks' coarse nodes are sent to their
 //                owners and added there;
 //   level l+1    C_d (own columns) and C_o (ghost columns) with a p2p halo
-//                plan; P = [P_d | P_o] and R = P^T = [P_d^T | R_o], R_o built
-//                from the ghost fine rows of P.
+//                plan; P = [P_d | P_o]; R = P^T as MatMultTranspose_MPIAIJ
+//                (P_d^T r, and P_o^T r's ghost-slot sums added on their
+//                owners through level l+1's plan run backwards).
 // Bulk work (the large products, the transposes, the V-cycle) is on the
 // device; the host handles boundary-sized data (ghost rows, contributions).
 // The V-cycle is PETSc's multiplicative PCMG with the reference's options
@@ -1358,6 +1360,12 @@ struct PJob {
                 rc = e != hipSuccess ? gerr(e, "P^T") : aijhip::attach_transpose(Pd, ti, tj, ta);
             }
             if (!rc && po.nz > 0) rc = aijhip_gamg::make_level_handle(device, po, &Po);
+            if (!rc && Po) {  // P_o^T for the restriction's off-rank share (vcycle)
+                int32_t *ti = nullptr, *tj = nullptr;
+                double *ta = nullptr;
+                const hipError_t e = aijhip::build_transpose(*Po, &ti, &tj, &ta, nullptr);
+                rc = e != hipSuccess ? gerr(e, "P_o^T") : aijhip::attach_transpose(Po, ti, tj, ta);
+            }
             po.release();
             pd.release();
             if (rc) {
@@ -1613,8 +1621,9 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
         std::vector<int64_t> e1_off;
         bool ghost_removed = false;  // a ghost fine node MIS removed (no aggregate)
         for (int32_t s = 0; s < ng; ++s) {
-            if (g_agg[s] < 0) ghost_removed = true;
-            else e1_off.push_back((int64_t)g_agg[s]);
+            const int64_t ga = (int64_t)g_agg[s];
+            if (ga < 0) ghost_removed = true;
+            else if (ga < cstart || ga >= cstart + na) e1_off.push_back(ga);  // (a ghost may sit in an own aggregate)
         }
         for (int64_t c : DMo.rcg) e1_off.push_back(c);  // this rank's members of other ranks' aggregates
         std::sort(e1_off.begin(), e1_off.end());
@@ -1862,31 +1871,8 @@ int build(aijhip_mpiaij *M0, const aijhip_gamg_params_t &p, Hierarchy &H) {
                 hipLaunchKernelGGL(k_add_offset, dim3(nblk(ng)), dim3(256), 0, nullptr, ng, (int32_t)nzl, d_gi + 1,
                                    Pext.ai + m + 1);
             hipFree(d_gi);
-            // R_o rows (own coarse c): the ghost fine rows' entries in own
-            // columns, by slot (a counting pass, then the entries in (slot,
-            // entry) order; nothing when the rank has no ghosts)
-            if (!rc && ng > 0) {
-                std::vector<int32_t> ri((size_t)na + 1, 0);
-                for (int32_t s = 0; s < ng; ++s)
-                    for (int64_t c : gcols[s])
-                        if (c >= cstart && c < cstart + na) ++ri[c - cstart + 1];
-                for (int32_t c = 0; c < na; ++c) ri[c + 1] += ri[c];
-                std::vector<int32_t> rj((size_t)ri[na]), pos(ri.begin(), ri.end() - 1);
-                std::vector<double> ra((size_t)ri[na]);
-                for (int32_t s = 0; s < ng; ++s)
-                    for (size_t k = 0; k < gcols[s].size(); ++k) {
-                        const int64_t c = gcols[s][k];
-                        if (c < cstart || c >= cstart + na) continue;
-                        const int32_t q = pos[c - cstart]++;
-                        rj[q] = s;
-                        ra[q] = gvals[s][k];
-                    }
-                if (!rj.empty())
-                    rc = aijhip_mat_create(L.Ad->device, na, ng, (int64_t)rj.size(), ri.data(), rj.data(), ra.data(),
-                                           &L.Ro);
-            }
         }
-        lap(l, "P extended, R_o");
+        lap(l, "P extended");
         // ---- A P and P^T (A P)
         if (!rc) rc = aijhip_gamg::rowprod_device(Aext, Pext, AP, n_cu, &cols_used);
         Pext.release();
@@ -2160,6 +2146,25 @@ static int transfer(aijhip_mpiaij *halo_op, const aijhip_mat *Bd, const aijhip_m
     return AIJHIP_OK;
 }
 
+// MatRestrict as MatMultTranspose_MPIAIJ: b = P_d^T r, then P_o^T r (one
+// value per ghost coarse slot of level l+1, in that level's ghost vector)
+// sent back to the slots' owners and added (halo_reverse_add). An aggregate
+// may have members on other ranks up to two steps from its root (PETSc's
+// parallel MIS), and P's smoothing reaches one more, so the fine rows with
+// entries in a rank's coarse columns are not all ghosts of its level-l halo:
+// the sums travel with the coarse level's plan instead.
+static int restrict_to(const Level &L, Level &N, const double *r, double *b, hipStream_t s, const int *stop) {
+    hipError_t e = aijhip::launch_mult(*L.Pd->transpose, r, nullptr, b, false, s, stop);
+    if (e != hipSuccess) return gerr(e, "restriction");
+    aijhip_mpiaij *M = N.op;
+    if (M->n_send == 0 && M->n_ghost == 0) return AIJHIP_OK;
+    double *t = M->d_ghost;
+    if (L.Po && L.Po->transpose) e = aijhip::launch_mult(*L.Po->transpose, r, nullptr, t, false, s, stop);
+    else if (M->n_ghost > 0) e = hipMemsetAsync(t, 0, sizeof(double) * (size_t)M->n_ghost, s);
+    if (e != hipSuccess) return gerr(e, "restriction (off-rank share)");
+    return aijhip_mpi::halo_reverse_add(M, t, b, s);
+}
+
 // The A_o correction of a fused smoothing launch (after the halo landed).
 static int offdiag_axpy(const Level &L, const double *scale, double *y, hipStream_t s, const int *stop) {
     if (!L.Ao) return AIJHIP_OK;
@@ -2201,7 +2206,7 @@ int vcycle(Hierarchy &H, const double *b0, double *x0, hipStream_t s, const int 
             hipLaunchKernelGGL(k_mg_resid, grid(L.m), dim3(256), 0, s, (int64_t)L.m, B(l), L.r, stop);
         }
         // MatRestrict: b_{l+1} = P^T r = P_d^T r + R_o r_ghost
-        if ((rc = transfer(L.op, L.Pd->transpose, L.Ro, L.r, nullptr, H.lv[l + 1].b, false, s, stop))) return rc;
+        if ((rc = restrict_to(L, H.lv[l + 1], L.r, H.lv[l + 1].b, s, stop))) return rc;
     }
     for (int l = nl - 2; l >= 0; --l) {
         Level &L = H.lv[l];

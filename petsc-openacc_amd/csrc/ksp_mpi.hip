@@ -330,6 +330,13 @@ namespace {
 
 // ------------------------------------------------------------- kernels
 // Pack the send rows: buf[i] = x[rows[i]] (zero past n up to n_pad).
+// y[rows[k]] += v[k] over one peer's segment (rows distinct within it)
+__global__ __launch_bounds__(256) void k_add_rows(int64_t n, const int32_t *__restrict__ rows,
+                                                  const double *__restrict__ v, double *y) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k < n) y[rows[k]] = y[rows[k]] + v[k];
+}
+
 __global__ __launch_bounds__(256) void k_pack(int64_t n, int64_t n_pad, const int32_t *__restrict__ rows,
                                               const double *__restrict__ x, double *buf) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * 256)
@@ -601,6 +608,87 @@ int halo_finish(aijhip_mpiaij *M, hipStream_t s) {
     }
     if ((e = hipStreamWaitEvent(s, M->ev_halo, 0)) != hipSuccess) return mhip(e, "halo wait");
     return AIJHIP_OK;
+}
+
+// The exchange run backwards (PETSc's VecScatter SCATTER_REVERSE with
+// ADD_VALUES, as MatMultTranspose_MPIAIJ uses it): each ghost slot's value
+// goes to the slot's owner, which adds it to the row it sends for that slot
+// — per peer in the plan's order, so the sums' order is fixed. On `s`, in
+// order (no exchange stream). Collective over the operator's ranks.
+int halo_reverse_add(aijhip_mpiaij *M, const double *d_gvals, double *y, hipStream_t s) {
+    aijhip_comm *C = M->comm;
+    if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
+    if (M->halo != AIJHIP_HALO_P2P) return mfail(AIJHIP_ERR_ARG, "reverse exchange: p2p plans only");
+    if (M->posted) return mfail(AIJHIP_ERR_STATE, "reverse exchange while an exchange is posted");
+    hipError_t e;
+    if (C->kind == AIJHIP_COMM_RCCL) {
+        const Rccl &R = rccl();
+        ncclResult_t r;
+        if ((r = R.GroupStart()) != ncclSuccess) return nfail(r, "ncclGroupStart");
+        for (size_t p = 0; r == ncclSuccess && p < M->recv_peer.size(); ++p) {
+            const int64_t a = M->recv_off[p], n = M->recv_off[p + 1] - a;
+            if (n > 0) r = R.Send(d_gvals + a, (size_t)n, ncclFloat64, M->recv_peer[p], C->nc, s);
+        }
+        for (size_t q = 0; r == ncclSuccess && q < M->send_peer.size(); ++q) {
+            const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
+            if (n > 0) r = R.Recv(M->d_sendbuf + a, (size_t)n, ncclFloat64, M->send_peer[q], C->nc, s);
+        }
+        const ncclResult_t r2 = R.GroupEnd();
+        if (r != ncclSuccess) return nfail(r, "ncclSend/ncclRecv (reverse)");
+        if (r2 != ncclSuccess) return nfail(r2, "ncclGroupEnd (reverse)");
+    } else {
+        if (!C->hsr) return mfail(AIJHIP_ERR_STATE, "host transport without a sendrecv callback");
+        if (M->n_ghost > 0 &&
+            (e = hipMemcpyAsync(M->h_ghost, d_gvals, sizeof(double) * (size_t)M->n_ghost, hipMemcpyDeviceToHost, s)) !=
+                hipSuccess)
+            return mhip(e, "reverse exchange staging");
+        int rc = wait_stream(C, s);
+        if (rc) return rc;
+        std::vector<int32_t> sp, rp;
+        std::vector<int64_t> so{0}, ro{0};
+        std::vector<double> sb, rb;
+        const double *self = nullptr;
+        for (size_t p = 0; p < M->recv_peer.size(); ++p) {
+            if (M->recv_peer[p] == C->rank) {
+                self = M->h_ghost + M->recv_off[p];
+                continue;
+            }
+            sp.push_back(M->recv_peer[p]);
+            sb.insert(sb.end(), M->h_ghost + M->recv_off[p], M->h_ghost + M->recv_off[p + 1]);
+            so.push_back((int64_t)sb.size());
+        }
+        for (size_t q = 0; q < M->send_peer.size(); ++q) {
+            if (M->send_peer[q] == C->rank) continue;
+            rp.push_back(M->send_peer[q]);
+            ro.push_back(ro.back() + (M->send_off[q + 1] - M->send_off[q]));
+        }
+        rb.resize((size_t)ro.back());
+        if (C->hsr(C->ctx, (int32_t)sp.size(), sp.data(), so.data(), sb.data(), (int32_t)rp.size(), rp.data(),
+                   ro.data(), rb.data()) != 0) {
+            comm_abort(C);
+            return mfail(AIJHIP_ERR_COMM, "host sendrecv callback failed (reverse exchange)");
+        }
+        for (size_t q = 0, k = 0; q < M->send_peer.size(); ++q) {
+            const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
+            if (M->send_peer[q] == C->rank) {
+                if (n > 0 && self) std::memcpy(M->h_send + a, self, sizeof(double) * (size_t)n);
+            } else {
+                std::memcpy(M->h_send + a, rb.data() + ro[k], sizeof(double) * (size_t)n);
+                ++k;
+            }
+        }
+        if (M->n_send > 0 && (e = hipMemcpyAsync(M->d_sendbuf, M->h_send, sizeof(double) * (size_t)M->n_send,
+                                                 hipMemcpyHostToDevice, s)) != hipSuccess)
+            return mhip(e, "reverse exchange upload");
+    }
+    for (size_t q = 0; q < M->send_peer.size(); ++q) {
+        const int64_t a = M->send_off[q], n = M->send_off[q + 1] - a;
+        if (n > 0)
+            hipLaunchKernelGGL(k_add_rows, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, M->d_send_rows + a,
+                               M->d_sendbuf + a, y);
+    }
+    e = hipGetLastError();
+    return e == hipSuccess ? AIJHIP_OK : mhip(e, "reverse exchange add");
 }
 
 int halo_abort(aijhip_mpiaij *M, hipStream_t s, int rc) {

@@ -86,6 +86,10 @@ int comm_sendrecv(aijhip_comm *C, const std::vector<std::vector<uint64_t>> &out,
 // half would leave them blocked in the collective.
 int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s);
 int halo_finish(aijhip_mpiaij *M, hipStream_t s);
+// y[row] += the ghost values other ranks hold for this rank's rows: the
+// exchange backwards (VecScatter SCATTER_REVERSE, ADD_VALUES), on s, p2p
+// plans only. Collective.
+int halo_reverse_add(aijhip_mpiaij *M, const double *d_gvals, double *y, hipStream_t s);
 // The error path after a successful halo_post: completes the exchange (its
 // result ignored) so no peer waits on this rank, and returns rc.
 int halo_abort(aijhip_mpiaij *M, hipStream_t s, int rc);

@@ -667,11 +667,11 @@ def test_auto_geometry_follows_gather_locality(pkg, dev, coracle):
     geometry 6 for short rows that follow few offset lists (the 7-point
     stencil); column codes wherever the row blocks' offset dictionaries fit
     (the FEM rows); otherwise long rows -> the gather-ordered copy in its
-    16-bit form at geometry 6, and without it (gather_sort 0) long scattered
+    packed form at geometry 6, and without it (gather_sort 0) long scattered
     rows -> geometry 1. The gather-ordered product equals the unsorted one
     and the oracle bit for bit (rows within the block cap)."""
     cases = [(pkg.poisson_csr(12), 6, 0, 0, True, 6), (pkg.fem_hex_csr(21, 20, 19), 6, 0, 1, False, 6),
-             (pkg.skewed_csr(300000, seed=1565), 6, 2, 0, False, 1)]  # 2: 16-bit block-relative columns
+             (pkg.skewed_csr(300000, seed=1565), 6, 2, 0, False, 1)]  # 2: packed block-relative columns
     for (ai, aj, aa), geom, sorted_, codes, pats, geom_unsorted in cases:
         with pkg.SeqAIJHIP(ai, aj, aa) as A:
             info = A.info()
@@ -699,30 +699,31 @@ def test_auto_geometry_follows_gather_locality(pkg, dev, coracle):
 
 
 @pytest.mark.parametrize("wide,form", [(0, 2), (40, 1), (4999, 2)])
-def test_gather_sort_32_and_16_bit_columns(pkg, dev, coracle, wide, form):
-    """The gather-ordered copy with 16-bit block-relative columns (every
-    block's columns within 2^16), with 32-bit columns (a row every 40
-    reaching both ends of a 90,000-column x: every block wide), and split (a
+def test_gather_sort_32_bit_and_packed_columns(pkg, dev, coracle, wide, form):
+    """The gather-ordered copy in its packed form (a word per entry: the
+    column relative to the block's first in 20 bits, the product slot in 12;
+    every block's columns within 2^20), with 32-bit columns (a row every 40
+    reaching both ends of a 2^21-column x: every block wide), and split (a
     wide row every 4999: those blocks from the original arrays, the rest
-    16-bit): MatMult and MatMultAdd equal the unsorted kernel and the oracle
+    packed): MatMult and MatMultAdd equal the unsorted kernel and the oracle
     bit for bit (exact mode), and new values (aijhip_mat_update_values) reach
     the sorted copy."""
     rng = np.random.default_rng(21)
-    m = 90000
+    m, n = 90000, 1 << 21
     lens = rng.integers(40, 100, m)
     cols = []
     for i, l in enumerate(lens):
         lo, hi = max(0, i - 3000), min(m, i + 3000)
         c = np.sort(rng.choice(np.arange(lo, hi), size=l, replace=False))
         if wide and i % wide == 0:
-            c = np.unique(np.concatenate([c, [0, m - 1]]))
+            c = np.unique(np.concatenate([c, [0, n - 1]]))
         cols.append(c)
     ai = np.concatenate([[0], np.cumsum([len(c) for c in cols])]).astype(np.int32)
     aj = np.concatenate(cols).astype(np.int32)
     aa = rng.uniform(-1, 1, len(aj))
-    x = rng.uniform(-1, 1, m)
+    x = rng.uniform(-1, 1, n)
     z = rng.uniform(-1, 1, m)
-    with pkg.SeqAIJHIP(ai, aj, aa, exact=1, gather_sort=1) as A:
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, exact=1, gather_sort=1) as A:
         assert A.info()["gather_sorted"] == form
         xd, zd = to_dev(x, dev), to_dev(z, dev)
         y = torch.empty(m, dtype=torch.float64, device=dev)
