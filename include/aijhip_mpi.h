@@ -163,6 +163,15 @@ int aijhip_kspmpi_set_norm_type(aijhip_kspmpi_t K, int norm_type);
  * and every rank polls at the same iterations, so the collectives stay
  * matched. */
 int aijhip_kspmpi_set_poll_interval(aijhip_kspmpi_t K, int32_t iters);
+/* The poll batch (the iterations between two polls) captured once into a HIP
+ * graph and replayed with one launch: -1 (default) on with an RCCL
+ * communicator, 0 off, 1 on (RCCL only; the host transport waits on the host
+ * inside its exchanges). The same kernels and collectives in the same order:
+ * the results are the direct launches' bits. Re-captured when x, the poll
+ * interval, the tolerances / norm or the set-up change. */
+int aijhip_kspmpi_set_graph(aijhip_kspmpi_t K, int mode);
+/* Batches the last solve replayed from the graph. */
+int aijhip_kspmpi_get_graph_batches(aijhip_kspmpi_t K, int32_t *batches);
 /* KSPSolve from x = 0 (main_ksp.cpp: VecSet(lhs, 0)); b, x device
  * fp64[mloc]. Returns once the solve has finished on this rank. */
 int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *stream);

@@ -49,6 +49,7 @@ MPI_SYMBOLS = (
     "aijhip_kspmpi_get_residual_history", "aijhip_kspmpi_get_host_syncs", "aijhip_kspmpi_destroy",
     "aijhip_comm_set_host_sendrecv", "aijhip_kspmpi_get_pc_levels", "aijhip_kspmpi_get_setup_seconds",
     "aijhip_kspmpi_get_pc_level", "aijhip_mpiaij_set_overlap", "aijhip_mpiaij_get_overlap",
+    "aijhip_kspmpi_set_graph", "aijhip_kspmpi_get_graph_batches",
 )
 _bound = False
 
@@ -78,6 +79,8 @@ def _lib():
         L.aijhip_kspmpi_set_gamg_params.argtypes = [_P, _P]
         L.aijhip_kspmpi_set_norm_type.argtypes = [_P, ctypes.c_int]
         L.aijhip_kspmpi_set_poll_interval.argtypes = [_P, _i32]
+        L.aijhip_kspmpi_set_graph.argtypes = [_P, ctypes.c_int]
+        L.aijhip_kspmpi_get_graph_batches.argtypes = [_P, ctypes.POINTER(_i32)]
         L.aijhip_kspmpi_solve.argtypes = [_P, _P, _P, _P]
         L.aijhip_kspmpi_get_iteration_number.argtypes = [_P, ctypes.POINTER(_i32)]
         L.aijhip_kspmpi_get_residual_norm.argtypes = [_P, ctypes.POINTER(_d)]
@@ -301,10 +304,12 @@ class KSPCGMPINative:
     (bjacobi + jacobi per rank), every scalar decision on the device."""
 
     def __init__(self, op: NativeMPIAIJ, rtol=1e-5, atol=1e-50, dtol=1e5, max_it=10000, pc="jacobi",
-                 norm="preconditioned", poll: int = 8, gamg=None):
+                 norm="preconditioned", poll: int = 8, gamg=None, graph=None):
         """pc: "none", "jacobi" (bjacobi + jacobi), "gamg" (PCGAMG across the
         ranks: one distributed hierarchy) or "bjacobi_gamg" (a GAMG hierarchy
-        per rank's diagonal block); gamg = the GAMG parameters."""
+        per rank's diagonal block); gamg = the GAMG parameters; graph: the
+        poll batch replayed as a captured HIP graph (None: the library's
+        default, on over RCCL; False / True)."""
         K = importlib.import_module("petsc-openacc_amd.ksp")
         L = _lib()
         self.op = op
@@ -318,6 +323,15 @@ class KSPCGMPINative:
             _pkg._check(L.aijhip_kspmpi_set_gamg_params(self._h, ctypes.byref(self._gp)))
         _pkg._check(L.aijhip_kspmpi_set_norm_type(self._h, K.NORM_TYPES[norm]))
         _pkg._check(L.aijhip_kspmpi_set_poll_interval(self._h, int(poll)))
+        if graph is not None:
+            _pkg._check(L.aijhip_kspmpi_set_graph(self._h, 1 if graph else 0))
+
+    @property
+    def graph_batches(self) -> int:
+        """Poll batches the last solve replayed from its captured graph."""
+        v = _i32()
+        _pkg._check(_lib().aijhip_kspmpi_get_graph_batches(self._h, ctypes.byref(v)))
+        return v.value
 
     def set_tolerances(self, rtol, atol, dtol, max_it):
         self.max_it = int(max_it)

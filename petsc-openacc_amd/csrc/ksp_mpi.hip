@@ -26,6 +26,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -762,11 +763,26 @@ struct aijhip_kspmpi {
     int reason = 0;
     double rnorm = 0.0;
     std::vector<double> hist;
+    // The poll batch (poll iterations) captured once into a HIP graph and
+    // replayed by one hipGraphLaunch (aijhip_kspmpi_set_graph): the RCCL
+    // enqueues of the halo and the all-reduces (15-25 us of host time per
+    // call, profiles/r05/a/) leave the iteration. -1 auto (on with an RCCL
+    // communicator), 0 off, 1 on (RCCL only: the host transport waits).
+    int graph = -1;
+    hipStream_t gs = nullptr;  // the capture stream (the caller's may be the legacy one)
+    hipGraphExec_t gexec = nullptr;
+    const double *g_x = nullptr;  // what the captured batch baked in
+    int32_t g_poll = 0;
+    uint64_t g_key = 0;
+    int32_t graph_batches = 0;  // batches the last solve replayed
 };
 
 namespace {
 
 void kspmpi_free(aijhip_kspmpi *K) {
+    if (K->gexec) (void)hipGraphExecDestroy(K->gexec);
+    K->gexec = nullptr;
+    K->g_x = nullptr;
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
     hipFree(K->d_opart); hipFree(K->d_red); hipFree(K->d_hist); hipFree(K->d_state);
     if (K->h_state) hipHostFree(K->h_state);
@@ -1191,6 +1207,18 @@ int aijhip_kspmpi_set_poll_interval(aijhip_kspmpi_t K, int32_t iters) {
     return AIJHIP_OK;
 }
 
+int aijhip_kspmpi_set_graph(aijhip_kspmpi_t K, int mode) {
+    if (!K || mode < -1 || mode > 1) return mfail(AIJHIP_ERR_ARG, "graph: -1 auto, 0 off, 1 on");
+    K->graph = mode;
+    return AIJHIP_OK;
+}
+
+int aijhip_kspmpi_get_graph_batches(aijhip_kspmpi_t K, int32_t *batches) {
+    if (!K || !batches) return mfail(AIJHIP_ERR_ARG, "NULL argument");
+    *batches = K->graph_batches;
+    return AIJHIP_OK;
+}
+
 int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *stream) {
     aijhip::Range range("KSPSolve (MPIAIJ)");
     if (!K) return mfail(AIJHIP_ERR_ARG, "NULL ksp");
@@ -1234,6 +1262,57 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
     // in it (counting them twice broke conjugacy).
     double *opart = (have_o && K->fused) ? K->d_opart : nullptr;
     const int nob = opart ? M->o_grid : 0;
+    // one CG iteration on stream st (every kernel returns at once past the
+    // device stop flag; every collective is issued on every rank regardless)
+    auto iteration = [&](hipStream_t st) -> int {
+        int r;
+        hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
+        // W = A P with the p.w partials (W shares Z's storage)
+        if ((r = mpiaij_apply(M, K->d_p, K->d_z, st, K->d_part, opart, K->d_state, K->fused))) return r;
+        if (!K->fused) hipLaunchKernelGGL(k_dot, vg, vt, 0, st, m, K->d_p, K->d_z, K->d_part, K->d_state);
+        hipLaunchKernelGGL(k_local_dpi, dim3(1), rt, 0, st, K->d_part, K->n_dparts, opart, nob, K->d_red,
+                           K->d_state, multi ? 0 : 1);
+        if (multi) {
+            if ((r = comm_allreduce(C, K->d_red, 1, st))) return r;
+            hipLaunchKernelGGL(k_step_dpi, dim3(1), dim3(64), 0, st, K->d_red, K->d_state);
+        }
+        hipLaunchKernelGGL(k_update<true>, vg, vt, 0, st, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state, K->pc,
+                           K->d_p, nullptr);
+        if (gamg) {  // z = B r; z.z and z.r from the fused finest post-smoothing, else k_dots
+            const double *dots = nullptr;
+            int nbz = 0;
+            if ((r = pc_gamg_apply(K, st, &dots, &nbz, &K->d_state->done))) return r;
+            if (!dots) {
+                hipLaunchKernelGGL(k_dots, vg, vt, 0, st, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
+                dots = K->d_part;
+                nbz = nb;
+            }
+            hipLaunchKernelGGL(k_local_iter, dim3(1), rt, 0, st, dots, nbz, K->d_part + 2 * nb, nb, K->d_red,
+                               multi ? 0 : 1, K->d_state, K->d_hist, p);
+        } else {
+            hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, st, K->d_part, nb, 3, K->d_red, multi ? 0 : 2,
+                               K->d_state, K->d_hist, p);
+        }
+        if (multi) {
+            if ((r = comm_allreduce(C, K->d_red, 3, st))) return r;
+            hipLaunchKernelGGL(k_step_iter, dim3(1), dim3(64), 0, st, K->d_red, K->d_state, K->d_hist, p);
+        }
+        const hipError_t le = hipGetLastError();
+        return le == hipSuccess ? AIJHIP_OK : mhip(le, "KSPSolve iteration");
+    };
+    // the poll batch as a HIP graph: RCCL only (the host transport waits on
+    // the host inside the exchanges); captured on the handle's own stream
+    // and re-captured when what it baked in changes (x, the batch length,
+    // the tolerances and norm, the set-up)
+    const bool use_graph = C->kind == AIJHIP_COMM_RCCL && (K->graph == 1 || K->graph == -1);
+    uint64_t key = 1469598103934665603ULL;
+    for (double v : {p.rtol, p.abstol, p.dtol})
+        key = (key ^ std::hash<double>{}(v)) * 1099511628211ULL;
+    key = (key ^ (uint64_t)(uint32_t)p.max_it ^ ((uint64_t)(uint32_t)p.normtype << 32) ^
+           ((uint64_t)(uint32_t)p.pc << 40)) * 1099511628211ULL;
+    key = (key ^ K->gens[0] ^ (K->gens[1] << 1) ^ (K->gens[2] << 2) ^ (K->gens[3] << 3) ^
+           (uint64_t)(uintptr_t)K->d_state) * 1099511628211ULL;
+    K->graph_batches = 0;
     int32_t launched = 0;
     for (;;) {
         if ((e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess)
@@ -1241,40 +1320,36 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
         if ((rc = wait_stream(C, s))) return rc;
         if (K->h_state->done || launched >= K->max_it) break;
         const int32_t poll = K->poll;  // every CG and V-cycle kernel returns at once past the flag
-        for (int j = 0; j < poll && launched < K->max_it; ++j, ++launched) {
-            hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, s, m, K->d_z, K->d_p, x, K->d_state);
-            // W = A P with the p.w partials (W shares Z's storage)
-            if ((rc = mpiaij_apply(M, K->d_p, K->d_z, s, K->d_part, opart, K->d_state, K->fused))) return rc;
-            if (!K->fused) hipLaunchKernelGGL(k_dot, vg, vt, 0, s, m, K->d_p, K->d_z, K->d_part, K->d_state);
-            hipLaunchKernelGGL(k_local_dpi, dim3(1), rt, 0, s, K->d_part, K->n_dparts, opart, nob, K->d_red,
-                               K->d_state, multi ? 0 : 1);
-            if (multi) {
-                if ((rc = comm_allreduce(C, K->d_red, 1, s))) return rc;
-                hipLaunchKernelGGL(k_step_dpi, dim3(1), dim3(64), 0, s, K->d_red, K->d_state);
-            }
-            hipLaunchKernelGGL(k_update<true>, vg, vt, 0, s, m, K->d_r, K->d_z, dinv, K->d_part, K->d_state,
-                               K->pc, K->d_p, nullptr);
-            if (gamg) {  // z = B r; z.z and z.r from the fused finest post-smoothing, else k_dots
-                const double *dots = nullptr;
-                int nbz = 0;
-                if ((rc = pc_gamg_apply(K, s, &dots, &nbz, &K->d_state->done))) return rc;
-                if (!dots) {
-                    hipLaunchKernelGGL(k_dots, vg, vt, 0, s, m, K->d_z, K->d_r, K->d_part, 0, 1, K->d_state);
-                    dots = K->d_part;
-                    nbz = nb;
+        if (use_graph && K->max_it - launched >= poll) {
+            if (!K->gexec || K->g_x != x || K->g_poll != poll || K->g_key != key) {
+                if (K->gexec) (void)hipGraphExecDestroy(K->gexec);
+                K->gexec = nullptr;
+                if (!K->gs && (e = hipStreamCreateWithFlags(&K->gs, hipStreamNonBlocking)) != hipSuccess)
+                    return mhip(e, "KSPSolve capture stream");
+                if ((e = hipStreamBeginCapture(K->gs, hipStreamCaptureModeRelaxed)) != hipSuccess)
+                    return mhip(e, "KSPSolve capture");
+                int crc = AIJHIP_OK;
+                for (int j = 0; j < poll && !crc; ++j) crc = iteration(K->gs);
+                hipGraph_t graph = nullptr;
+                e = hipStreamEndCapture(K->gs, &graph);
+                if (!crc && e == hipSuccess) e = hipGraphInstantiate(&K->gexec, graph, nullptr, nullptr, 0);
+                if (graph) (void)hipGraphDestroy(graph);
+                if (crc) return crc;
+                if (e != hipSuccess) {
+                    K->gexec = nullptr;
+                    return mhip(e, "KSPSolve capture (end / instantiate)");
                 }
-                hipLaunchKernelGGL(k_local_iter, dim3(1), rt, 0, s, dots, nbz, K->d_part + 2 * nb, nb, K->d_red,
-                                   multi ? 0 : 1, K->d_state, K->d_hist, p);
-            } else {
-                hipLaunchKernelGGL(k_local_sums, dim3(1), rt, 0, s, K->d_part, nb, 3, K->d_red, multi ? 0 : 2,
-                                   K->d_state, K->d_hist, p);
+                K->g_x = x;
+                K->g_poll = poll;
+                K->g_key = key;
             }
-            if (multi) {
-                if ((rc = comm_allreduce(C, K->d_red, 3, s))) return rc;
-                hipLaunchKernelGGL(k_step_iter, dim3(1), dim3(64), 0, s, K->d_red, K->d_state, K->d_hist, p);
-            }
-            if ((e = hipGetLastError()) != hipSuccess) return mhip(e, "KSPSolve iteration");
+            if ((e = hipGraphLaunch(K->gexec, s)) != hipSuccess) return mhip(e, "KSPSolve graph launch");
+            launched += poll;
+            ++K->graph_batches;
+            continue;
         }
+        for (int j = 0; j < poll && launched < K->max_it; ++j, ++launched)
+            if ((rc = iteration(s))) return rc;
     }
     hipLaunchKernelGGL(k_final_x, vg, vt, 0, s, m, K->d_p, x, K->d_state);
     if ((e = hipGetLastError()) != hipSuccess ||
@@ -1393,6 +1468,7 @@ int aijhip_kspmpi_destroy(aijhip_kspmpi_t K) {
         DeviceGuard g(K->M->comm->device);
         (void)hipDeviceSynchronize();
         kspmpi_free(K);
+        if (K->gs) (void)hipStreamDestroy(K->gs);
     }
     delete K;
     return AIJHIP_OK;

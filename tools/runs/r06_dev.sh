@@ -22,5 +22,8 @@ for s in ${STEPS:-gamg_mpi parity bench}; do
     parity) step parity 300 python -u -m pytest tests/test_gpu_parity.py -x -v -k "gather or geometry" --timeout 200 --timeout-method thread ;;
     bench) step bench 400 python -u bench.py --no-flan --no-host-vec --no-pmc --steps 20 --warmup 5 ;;
     tests) step tests 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ;;
+    selfhalo) step selfhalo 300 python -u -m pytest tests/test_rccl_selfhalo_gpu.py tests/test_halo_errors_gpu.py -x -v --timeout 240 --timeout-method thread ;;
+    graph) step graph_probe 300 python -u tools/graph_probe.py ;;
+    graph_trace) step graph_trace 300 rocprofv3 --kernel-trace --hip-trace --stats -d "$OUT/graph_trace" -o run --output-format csv -- python3 tools/graph_probe.py --rounds 1 --its 160 ;;
   esac
 done
