@@ -164,9 +164,8 @@ int aijhip_kspmpi_set_norm_type(aijhip_kspmpi_t K, int norm_type);
  * matched. */
 int aijhip_kspmpi_set_poll_interval(aijhip_kspmpi_t K, int32_t iters);
 /* The poll batch (the iterations between two polls) captured once into a HIP
- * graph and replayed with one launch: -1 (default) on with an RCCL
- * communicator, 0 off, 1 on (RCCL only; the host transport waits on the host
- * inside its exchanges). The same kernels and collectives in the same order:
+ * graph and replayed with one launch: 0 off (default), 1 on (RCCL only; the
+ * host transport waits on the host inside its exchanges); -1 = the default. The same kernels and collectives in the same order:
  * the results are the direct launches' bits. Re-captured when x, the poll
  * interval, the tolerances / norm or the set-up change. */
 int aijhip_kspmpi_set_graph(aijhip_kspmpi_t K, int mode);

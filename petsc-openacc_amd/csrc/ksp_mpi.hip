@@ -766,9 +766,9 @@ struct aijhip_kspmpi {
     // The poll batch (poll iterations) captured once into a HIP graph and
     // replayed by one hipGraphLaunch (aijhip_kspmpi_set_graph): the RCCL
     // enqueues of the halo and the all-reduces (15-25 us of host time per
-    // call, profiles/r05/a/) leave the iteration. -1 auto (on with an RCCL
-    // communicator), 0 off, 1 on (RCCL only: the host transport waits).
-    int graph = -1;
+    // call, profiles/r05/a/) leave the iteration. 0 off (default), 1 on
+    // (RCCL only: the host transport waits on the host).
+    int graph = 0;
     hipStream_t gs = nullptr;  // the capture stream (the caller's may be the legacy one)
     hipGraphExec_t gexec = nullptr;
     const double *g_x = nullptr;  // what the captured batch baked in
@@ -1304,7 +1304,11 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
     // the host inside the exchanges); captured on the handle's own stream
     // and re-captured when what it baked in changes (x, the batch length,
     // the tolerances and norm, the set-up)
-    const bool use_graph = C->kind == AIJHIP_COMM_RCCL && (K->graph == 1 || K->graph == -1);
+    const bool use_graph = C->kind == AIJHIP_COMM_RCCL && K->graph == 1;  // (-1: the default, off)
+    static const bool gdbg = std::getenv("AIJHIP_GRAPH_DEBUG") != nullptr;
+    auto dbg = [&](const char *what) {
+        if (gdbg) std::fprintf(stderr, "[kspmpi graph, rank %d] %s\n", C->rank, what);
+    };
     uint64_t key = 1469598103934665603ULL;
     for (double v : {p.rtol, p.abstol, p.dtol})
         key = (key ^ std::hash<double>{}(v)) * 1099511628211ULL;
@@ -1318,6 +1322,7 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
         if ((e = hipMemcpyAsync(K->h_state, K->d_state, sizeof(CGState), hipMemcpyDeviceToHost, s)) != hipSuccess)
             return mhip(e, "KSPSolve poll");
         if ((rc = wait_stream(C, s))) return rc;
+        if (use_graph) dbg("polled");
         if (K->h_state->done || launched >= K->max_it) break;
         const int32_t poll = K->poll;  // every CG and V-cycle kernel returns at once past the flag
         if (use_graph && K->max_it - launched >= poll) {
@@ -1326,13 +1331,19 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
                 K->gexec = nullptr;
                 if (!K->gs && (e = hipStreamCreateWithFlags(&K->gs, hipStreamNonBlocking)) != hipSuccess)
                     return mhip(e, "KSPSolve capture stream");
+                dbg("begin capture");
                 if ((e = hipStreamBeginCapture(K->gs, hipStreamCaptureModeRelaxed)) != hipSuccess)
                     return mhip(e, "KSPSolve capture");
                 int crc = AIJHIP_OK;
-                for (int j = 0; j < poll && !crc; ++j) crc = iteration(K->gs);
+                for (int j = 0; j < poll && !crc; ++j) {
+                    crc = iteration(K->gs);
+                    dbg("iteration captured");
+                }
                 hipGraph_t graph = nullptr;
                 e = hipStreamEndCapture(K->gs, &graph);
+                dbg(e == hipSuccess ? "end capture" : "end capture failed");
                 if (!crc && e == hipSuccess) e = hipGraphInstantiate(&K->gexec, graph, nullptr, nullptr, 0);
+                dbg(e == hipSuccess ? "instantiated" : "instantiate failed");
                 if (graph) (void)hipGraphDestroy(graph);
                 if (crc) return crc;
                 if (e != hipSuccess) {
@@ -1344,6 +1355,7 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
                 K->g_key = key;
             }
             if ((e = hipGraphLaunch(K->gexec, s)) != hipSuccess) return mhip(e, "KSPSolve graph launch");
+            dbg("batch launched");
             launched += poll;
             ++K->graph_batches;
             continue;
