@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--its", type=int, default=400)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--ghosts", type=int, default=1, help="1: the boundary planes as self-ghosts (RCCL in the batch)")
+    ap.add_argument("--overlap", type=int, default=-1, help="exchange placement: -1 automatic, 0 serial, 1 side stream")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -61,6 +62,8 @@ def main():
         ghosts = np.zeros(0, np.int64)
         Ad, Ao = pkg.SeqAIJHIP(ai, aj, aa, ncols=m), None
         op = C.NativeMPIAIJ(comm, Ad, None, "p2p", [], [], 0)
+    if a.overlap >= 0:
+        op.set_overlap(bool(a.overlap))
     rhs, _ = pkg.poisson_vectors(G, G, nz)
     b = torch.from_numpy(rhs).to(dev)
     sols = {}
