@@ -126,6 +126,8 @@ def main():
         lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
         last = json.loads(lines[-1]) if lines else {"case": case, "stage": "none"}
         last["exit"] = r.returncode
+        if r.returncode:
+            last["stderr_tail"] = [x for x in r.stderr.splitlines() if x.strip()][-6:]
         print(json.dumps(last), flush=True)
 
 
