@@ -78,6 +78,8 @@ def run_case(case):
         op.mult(x, y)
         torch.cuda.synchronize()
         y_ref = y.clone()
+        y.fill_(float("nan"))
+        torch.cuda.synchronize()
     L = C._lib()
     rc = {}
     rc["begin"] = H.hipStreamBeginCapture(gs, 2)  # relaxed
@@ -98,8 +100,6 @@ def run_case(case):
         H.hipEventRecord(e2, xs)
         H.hipStreamWaitEvent(gs, e2, 0)
     else:
-        y.fill_(float("nan"))
-        torch.cuda.synchronize()
         rc["mult"] = L.aijhip_mpiaij_mult(op._h, P(x.data_ptr()), P(y.data_ptr()), gs)
     print(json.dumps({"case": case, "stage": "captured", **rc}), flush=True)
     g = P()
