@@ -469,12 +469,19 @@ namespace aijhip_mpi {
 // round 5): issued first, it held back the A_d launch and the device
 // idled; issued second, A_d runs while the host is inside RCCL. The device
 // order is unchanged (the collective waits only for the fork).
+// Set while aijhip_kspmpi_solve captures its poll batch: the exchanges are
+// captured in the serial form. Measured on this stack (tools/capture_probe.py,
+// profiles/r06/i/): grouped ncclSend / ncclRecv on a stream forked inside a
+// capture makes hipStreamEndCapture segfault (an all-reduce there, memsets
+// there, or the exchange on the capturing stream itself do not).
+thread_local bool g_capturing = false;
+
 int halo_post(aijhip_mpiaij *M, const double *x, hipStream_t s) {
     aijhip_comm *C = M->comm;
     if (C->aborted) return mfail(AIJHIP_ERR_COMM, "communicator aborted");
     hipError_t e;
-    // serial (RCCL, overlap 0): everything on the caller's stream, in order
-    const bool serial = C->kind == AIJHIP_COMM_RCCL && !M->overlap;
+    // serial (RCCL, overlap 0, or under capture): everything on the caller's stream, in order
+    const bool serial = C->kind == AIJHIP_COMM_RCCL && (!M->overlap || g_capturing);
     const hipStream_t xs = serial ? s : M->xs;
     M->post_s = xs;
     if (!serial &&
@@ -1335,10 +1342,12 @@ int aijhip_kspmpi_solve(aijhip_kspmpi_t K, const double *b, double *x, void *str
                 if ((e = hipStreamBeginCapture(K->gs, hipStreamCaptureModeRelaxed)) != hipSuccess)
                     return mhip(e, "KSPSolve capture");
                 int crc = AIJHIP_OK;
+                aijhip_mpi::g_capturing = true;
                 for (int j = 0; j < poll && !crc; ++j) {
                     crc = iteration(K->gs);
                     dbg("iteration captured");
                 }
+                aijhip_mpi::g_capturing = false;
                 hipGraph_t graph = nullptr;
                 e = hipStreamEndCapture(K->gs, &graph);
                 dbg(e == hipSuccess ? "end capture" : "end capture failed");
