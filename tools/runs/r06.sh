@@ -10,6 +10,9 @@
 #   rehearse_n2 — --gpus 2 --rehearse-one-gpu at 300^3 with CG + GAMG (13.5 M
 #                 rows per rank, host transport)
 #   default    — the driver's N = 1 command (python bench.py)
+#   rehearse_n8 — the driver's N = 8 line on one GPU: 8 ranks over gloo (host
+#                 transport), the 300^3 strong headline (38/37 planes), a 100^3
+#                 weak block, distributed CG and CG + GAMG
 #   tests      — pytest -m gpu + smoke()
 set -o pipefail
 MODE=${1:?mode}; TAG=${2:?tag}
@@ -34,6 +37,11 @@ case $MODE in
     timeout -k 10 1000 python -u bench.py --gpus 2 --rehearse-one-gpu --steps 10 --warmup 3 --wall-budget 900 \
         > "$OUT/bench_rehearse_n2.json" 2> "$OUT/bench_rehearse_n2.err" \
       && echo "rehearsal n2 ok" || { tail -20 "$OUT/bench_rehearse_n2.err"; exit 1; }
+    ;;
+  rehearse_n8)
+    timeout -k 10 1000 python -u bench.py --gpus 8 --rehearse-one-gpu --weak-grid 100 --steps 10 --warmup 3 \
+        --wall-budget 900 > "$OUT/bench_rehearse_n8.json" 2> "$OUT/bench_rehearse_n8.err" \
+      && echo "rehearsal n8 ok" || { tail -20 "$OUT/bench_rehearse_n8.err"; exit 1; }
     ;;
   tests)
     timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread \
