@@ -321,3 +321,33 @@ def test_watchdog_prints_the_line_and_exits(bench):
     d = lines[0]
     assert d["value"] == 5000.0 and d["cg"] == {"iters": 200}
     assert d["cg_gamg"]["error"] == "budget" and d["budget"]["legs"]["cg_gamg"]["status"] == "cut at the deadline"
+
+
+@pytest.mark.parametrize("rec,world", [("a/bench_mpi_n1_gamgdist.json", 1), ("e/bench_rehearse_n2.json", 2),
+                                       ("k/bench_rehearse_n8.json", 8)])
+def test_round6_distributed_records_measure_the_metric(rec, world):
+    """VERDICT r05 item 1, on the records this bench.py wrote on a GPU box
+    (profiles/r06/): the distributed line's `value` is the 300^3 operand
+    itself (27,000,000 rows, 188,460,000 entries) strong-scaled over the
+    ranks, the CPU baselines (1 core and all cores) are present at every N,
+    the weak block beside it at N > 1, every leg within the wall budget's
+    bookkeeping, and the distributed CG + GAMG at the full per-rank size
+    takes the single-GPU hierarchy's 53 iterations (PETSc's parallel MIS,
+    partition-independent)."""
+    import json
+    lines = [x for x in (ROOT / "profiles" / "r06" / rec).read_text().splitlines() if x.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == world and d["scaling"] == "strong"
+    c = d["config"]
+    assert c["rows"] == 27_000_000 and c["nnz"] == 188_460_000 and c["workload"].startswith("300^3")
+    assert d["cpu_baseline"]["cores"] == 1 and d["cpu_baseline"]["kind"] == "port"
+    assert d["cpu_baseline_all_cores"]["cores"] >= 1 and d["cpu_baseline_all_cores"]["value"] > 0
+    assert abs(d["value"] - c["bytes_per_spmv"] * d["steps"] / (d["ms_per_step"] * d["steps"] / 1e3) / 1e9) \
+        < 0.01 * d["value"]
+    if world > 1:
+        assert d["weak"]["scaling"] == "weak" and "error" not in d["weak"]
+    g = d["cg_gamg"]
+    assert g["its"] == 53 and [lv["rows"] for lv in g["levels"]][:3] == [27_000_000, 2_413_301, 183_694]
+    assert set(d["budget"]["legs"]) >= {"cg", "cg_gamg", "cpu_baseline"}
+    assert_fracs_at_most_one(d)
