@@ -87,6 +87,8 @@ def parse():
                    help="STREAM column codes -1 (library default: automatic) / 0 (aj) / 1")
     p.add_argument("--patterns", type=int, default=None,
                    help="STREAM row patterns -1 (library default: automatic) / 0 / 1")
+    p.add_argument("--templates", type=int, default=None,
+                   help="row templates (the patterns with the values) -1 (library default: automatic) / 0 / 1")
     p.add_argument("--halo", default="p2p", choices=["p2p", "allgather"])
     p.add_argument("--x", default="uniform", choices=["uniform", "exact"], help="x = splitmix(42) or generateExt")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="bound of the CPU baseline sample")
@@ -945,6 +947,9 @@ def weak_block(pkg, mpiaij, make_local, Gw, world, rank, dev, args, comm):
 
 
 def layout_name(info) -> str:
+    if info.get("row_templates"):
+        return (f"row templates ({info['row_patterns']} distinct rows, offsets and values, a 1-byte id per row: "
+                "the MatMult reads neither aj nor aa — a constant-coefficient stencil) — not CSR")
     if info.get("row_patterns"):
         return (f"row patterns ({info['row_patterns']} column - row offset lists, a 1-byte id per row, aa "
                 "verbatim, no column per entry; cf. PETSc's inode rows) — not CSR")
@@ -1004,8 +1009,9 @@ def main():
     def set_layout(mat, csr):
         """csr: the MatMult reads PETSc's aj (row patterns and column codes
         off); else the library's automatic layout (or what --codes /
-        --patterns force)."""
+        --patterns / --templates force)."""
         mat.set_option("column_codes", 0 if csr else (-1 if args.codes is None else args.codes))
+        mat.set_option("row_templates", -1 if args.templates is None else args.templates)
         mat.set_option("row_patterns", 0 if csr else (-1 if args.patterns is None else args.patterns))
 
     def configure(mat, csr=csr_forced):

@@ -60,8 +60,10 @@ extern "C" {
  * 3.7's MIS coarsening and CG emax estimate as options).
  * 4: aijhip_info_t gained hw_queues (the side streams' automatic choice
  * follows it); aijhip_mpi.h gained aijhip_mpiaij_get_overlap and the
- * automatic value -1 of aijhip_mpiaij_set_overlap. */
-#define AIJHIP_ABI_VERSION 4
+ * automatic value -1 of aijhip_mpiaij_set_overlap.
+ * 5: AIJHIP_OPT_ROW_TEMPLATES; aijhip_info_t's last word (reserved0) is
+ * row_templates (layout unchanged). */
+#define AIJHIP_ABI_VERSION 5
 
 enum {
     AIJHIP_OK = 0,
@@ -122,7 +124,9 @@ typedef struct aijhip_info {
                                 entry instead of 12); 0 off                  */
     int32_t row_patterns;    /* MatMult reads a pattern id per row instead of
                                 aj (AIJHIP_OPT_ROW_PATTERNS): the number of
-                                distinct column - row offset lists; 0 off    */
+                                distinct column - row offset lists (with
+                                row_templates: of distinct rows, offsets and
+                                values); 0 off                               */
     int32_t long_overlap;    /* 1 when the long rows' segments and the wide
                                 blocks run on a side stream beside the row
                                 blocks (AIJHIP_OPT_LONG_OVERLAP), else 0
@@ -145,7 +149,10 @@ typedef struct aijhip_info {
                                 (aijhip_mpiaij_set_overlap -1) — a side
                                 stream would share the compute stream's queue
                                 and run behind it (ABI 4)                     */
-    int32_t reserved0;
+    int32_t row_templates;   /* 1 when the row patterns carry the values too
+                                (AIJHIP_OPT_ROW_TEMPLATES): aa is not read
+                                by MatMult, else 0 (ABI 5; the former
+                                reserved word)                               */
 } aijhip_info_t;
 
 /* Library / device. */
@@ -244,7 +251,7 @@ enum {
                                        entries), else the automatic layout
                                        without them; costs 2 bytes per entry
                                        of device memory                      */
-    AIJHIP_OPT_ROW_PATTERNS = 14    /* short-row operands whose rows follow at
+    AIJHIP_OPT_ROW_PATTERNS = 14,   /* short-row operands whose rows follow at
                                        most 256 distinct column - row offset
                                        lists (stencils): no per-entry column
                                        at all — a pattern id per row (1 byte),
@@ -253,6 +260,17 @@ enum {
                                        sums. 1 on, 0 off, -1 (default): tried
                                        first where the mean row is at most 16
                                        entries; costs 1 byte per row          */
+    AIJHIP_OPT_ROW_TEMPLATES = 17   /* with row patterns: when the operand's rows
+                                       are at most 256 distinct (offsets,
+                                       values) lists — a constant-coefficient
+                                       stencil — the table holds the values
+                                       too and MatMult reads neither aj nor
+                                       aa: the row's id, x and y (the values
+                                       are the same bits, summed in the same
+                                       order: the same results). 1 on, 0 off,
+                                       -1 (default): tried before the plain
+                                       row patterns. aijhip_mat_update_values
+                                       re-plans (new values may not fit)     */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <tuple>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -86,6 +87,8 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_cmeta);
     hipFree(P.d_pid);
     hipFree(P.d_ptab);
+    hipFree(P.d_pval);
+    hipFree(P.d_tblocks);
     if (P.side) hipStreamDestroy(P.side);
     if (P.ev_fork) hipEventDestroy(P.ev_fork);
     if (P.ev_join) hipEventDestroy(P.ev_join);
@@ -323,9 +326,48 @@ int plan_stream(aijhip_mat *A) {
     const int32_t nrl = rai.empty() ? 0 : (int32_t)rai.size() - 1;
     if (P.tune.patterns > 0 && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed &&
         A->nz <= (int64_t)kBatchMinMean * nrl && P.d_sslot == nullptr) {
+        // with the values first (row templates: neither aj nor aa read), then
+        // the offsets alone
         bool ok = false;
-        if ((e = aijhip::build_row_patterns(*A, P, &ok)) != hipSuccess) return hipfail(e, "plan: row patterns");
+        if (P.tune.templates != 0 && (e = aijhip::build_row_patterns(*A, P, &ok, true)) != hipSuccess)
+            return hipfail(e, "plan: row templates");
+        if (!ok && (e = aijhip::build_row_patterns(*A, P, &ok, false)) != hipSuccess)
+            return hipfail(e, "plan: row patterns");
+        if (ok && P.d_pval) {
+            // the row templates' block order: a stencil's rows r and r +- D
+            // (D = the largest offset, a plane) share x lines, so the blocks
+            // go through the operand in column slabs of S rows of each plane,
+            // plane after plane within a slab: the x lines a block gathers
+            // from the planes either side are reused while they are still in
+            // the XCD's L2. k0 of the copy = the block's own index (its dot
+            // partial's slot; a template launch reads no entry range).
+            // S <= 8192 rows (profiles/r06/v, w: the CG SpMV's fetched bytes
+            // 0.62 GB in natural order, 0.60 / 0.52 / 0.44 GB at S = 16384 /
+            // 32768 / 8192; the times within a few per cent — the launch is
+            // bound by its gathers' latency, not its traffic)
+            const int64_t D = P.pat_dmax, split = 8192;
+            std::vector<int32_t> order(blocks.size());
+            for (size_t b = 0; b < blocks.size(); ++b) order[b] = (int32_t)b;
+            if (split > 0 && D > split) {
+                const int64_t ns = (D + split - 1) / split, S = (D + ns - 1) / ns;
+                auto key = [&](int32_t b) {
+                    const int64_t r = blocks[b].row0;
+                    return std::make_tuple((r % D) / S, r / D, r % D);
+                };
+                std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key(a) < key(b); });
+            }
+            std::vector<BlockDesc> tb(blocks.size());
+            for (size_t i = 0; i < order.size(); ++i) {
+                tb[i] = blocks[order[i]];
+                tb[i].k0 = order[i];
+            }
+            if ((e = dmalloc(&P.d_tblocks, tb.size(), &P.bytes)) != hipSuccess ||
+                (e = hipMemcpy(P.d_tblocks, tb.data(), sizeof(BlockDesc) * tb.size(), hipMemcpyHostToDevice)) !=
+                    hipSuccess)
+                return hipfail(e, "plan: template block order");
+        }
     }
+    P.tune.templates = P.d_pval != nullptr ? 1 : 0;
     // column codes (Tuning::codes): a 16-bit code per entry in aj's place
     // for the row blocks whose offset dictionaries fit (geometry 6, plain
     // full-row launches: not with the x tiles or the gather order); when
@@ -835,6 +877,8 @@ int64_t mult_layout_bytes(const aijhip_mat &A) {
     const int64_t rows = A.compressed ? (4 * ((int64_t)A.n_crow + 1) + 4 * (int64_t)A.n_crow) : 4 * (m + 1);
     const int64_t vec = 8 * n + 8 * m;
     if (P.kernel != AIJHIP_KERNEL_STREAM) return 12 * nz + rows + vec;
+    if (P.d_pid && P.d_pval)  // row templates: a template id per row, the table (offsets and values)
+        return m + 12 * (int64_t)P.n_ptab + vec;
     if (P.d_pid)  // aa, ai, a pattern id per row and the offset table
         return 8 * nz + rows + m + 4 * (int64_t)P.n_ptab + vec;
     if (P.d_code)  // coded entries 10 B, blocks launched from aj 12 B, the dictionaries
@@ -944,6 +988,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "row_patterns: -1 auto, 0 off, 1 on");
             t.patterns = value;
             break;
+        case AIJHIP_OPT_ROW_TEMPLATES:
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "row_templates: -1 auto, 0 off, 1 on");
+            t.templates = value;
+            break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -966,6 +1014,10 @@ int aijhip_mat_update_values(aijhip_mat_t A, const double *aa) {
     if (e == hipSuccess && A->plan.d_sslot)  // the gather-ordered copy of the values
         e = aijhip::build_gather_order(*A, A->plan, true);
     if (e != hipSuccess) return hipfail(e, "update values");
+    if (A->plan.d_pval) {  // row templates hold the old values: plan again (the new ones may not fit)
+        rc = plan_build(A);
+        if (rc) return rc;
+    }
     A->values_gen = aijhip::next_plan_gen();  // a set-up KSP redoes its PC set-up
     if (A->transpose) {  // A^T values are stale
         free_matrix(A->transpose);
@@ -1137,7 +1189,7 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->long_overlap = A->plan.side != nullptr ? 1 : 0;
     info->mult_layout_bytes = aijhip::mult_layout_bytes(*A);
     info->hw_queues = aijhip::hw_queues();
-    info->reserved0 = 0;
+    info->row_templates = A->plan.d_pval != nullptr ? 1 : 0;
     return AIJHIP_OK;
 }
 

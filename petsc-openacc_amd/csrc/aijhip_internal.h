@@ -109,6 +109,8 @@ struct Tuning {
                            // blocks' offset dictionaries fit and gsort is off), 0 off, 1 on
     int patterns = -1;     // row patterns instead of aj (Plan::d_pid): -1 auto (short rows whose
                            // offset lists are few), 0 off, 1 on
+    int templates = -1;    // with row patterns, the values in the table too (Plan::d_pval; a
+                           // constant-coefficient stencil): -1 auto (tried first), 0 off, 1 on
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is
@@ -210,6 +212,12 @@ struct Plan {
     int32_t *d_ptab = nullptr;
     int32_t n_ptab = 0, n_pat = 0;
     int32_t pat_dmax = 0;    // largest |column - row| offset in the table (the stencil's plane distance)
+    int32_t pat_maxlen = 0;  // longest pattern (entries)
+    // Tuning::templates: the values of each pattern's entries, indexed like
+    // the offsets in d_ptab (n_ptab doubles; the first n_pat unused): MatMult
+    // reads neither aj nor aa
+    double *d_pval = nullptr;
+    BlockDesc *d_tblocks = nullptr;  // the blocks in the template launch's order, k0 = the block's index
     int64_t bytes = 0;  // device bytes held by the plan
     HostPipe *hpipe = nullptr;  // built on the first host-vector MatMult
 };
@@ -318,8 +326,9 @@ constexpr int kPackedMaxCap = 1 << (32 - kPackedColBits);  // slots < 4096: bloc
 // Row patterns: when the operand's rows follow at most kPatMax distinct
 // column - row offset lists (64-bit hashes, verified entry by entry) whose
 // table fits kPatTableMax words, allocates and fills P.d_pid / P.d_ptab and
-// sets *ok; otherwise leaves them null.
-hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok);
+// sets *ok; otherwise leaves them null. values: the lists are (offset, value)
+// pairs (the value bits hashed and verified too) and P.d_pval is filled.
+hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok, bool values);
 hipError_t column_code_counts(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt);
 hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cmeta,
                              uint16_t *d_code);

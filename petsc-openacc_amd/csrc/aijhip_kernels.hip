@@ -94,7 +94,11 @@ __device__ __forceinline__ void st_stream(double *p, double v) { __builtin_nonte
 // What a STREAM launch gathers and writes. The row sum s_i = sum a_ij g(j)
 // is formed in PETSc's order (or the deterministic multi-lane order); `seed`
 // starts it (MatMultAdd's z_i), `put` stores the row's result and adds to
-// the block's dot partials d[0..kDots).
+// the block's dot partials d[0..kDots). `row` loads the row's other operands
+// (Row) so that a launch can issue them before the gathers (the row-template
+// kernel: with no matrix stream, a load issued after the sum is one more
+// latency per block); put(o, v, d) = put(o, v, d, row(o)), the same values —
+// the outputs never alias these inputs within a row.
 template <bool ADD>
 struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     static constexpr int kDots = 1;
@@ -102,12 +106,17 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     const double *x, *z;
     double *y;
     bool dot;
+    struct Row {
+        double xo;
+    };
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int o) const { return ADD ? z[o] : 0.0; }
-    __device__ void put(int o, double v, double *d) const {
+    __device__ Row row(int o) const { return {dot ? x[o] : 0.0}; }
+    __device__ void put(int o, double v, double *d, const Row &w) const {
         st_stream(y + o, v);
-        if (dot) d[0] += x[o] * v;
+        if (dot) d[0] += w.xo * v;
     }
+    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
 };
 
 // MatResidual with the SpMV: r_i = b_i + (-1) (A x)_i (SpMV + k_resid, same
@@ -119,13 +128,18 @@ struct OpMgResid {
     static constexpr bool kSeeded = false;
     const double *x, *b;
     double *r;
+    struct Row {
+        double bo;
+    };
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int) const { return 0.0; }
-    __device__ void put(int o, double v, double *) const {
-        const double ro = b[o] + (-1.0) * v;
+    __device__ Row row(int o) const { return {b[o]}; }
+    __device__ void put(int o, double v, double *, const Row &w) const {
+        const double ro = w.bo + (-1.0) * v;
         if constexpr (NT) st_stream(r + o, ro);
         else r[o] = ro;
     }
+    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
 };
 
 // V-cycle post-smoothing, one Richardson step with Jacobi from the guess t
@@ -139,18 +153,22 @@ struct OpMgPost {
     const double *t, *b, *dinv;
     double *x;
     bool dot;
+    struct Row {
+        double to, bo, dio;
+    };
     __device__ double gx(int32_t j) const { return t[j]; }
     __device__ double seed(int) const { return 0.0; }
-    __device__ void put(int o, double v, double *d) const {
-        const double bo = b[o];
-        const double xo = t[o] + 1.0 * (dinv[o] * (bo + (-1.0) * v));
+    __device__ Row row(int o) const { return {t[o], b[o], dinv[o]}; }
+    __device__ void put(int o, double v, double *d, const Row &w) const {
+        const double xo = w.to + 1.0 * (w.dio * (w.bo + (-1.0) * v));
         if constexpr (NT) st_stream(x + o, xo);
         else x[o] = xo;
         if (dot) {
             d[0] += xo * xo;
-            d[1] += xo * bo;
+            d[1] += xo * w.bo;
         }
     }
+    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
 };
 
 // y = D^-1 A x (the GAMG set-up's power iteration, gamg_setup.cpp dinv_apply).
@@ -159,9 +177,14 @@ struct OpDinvMult {
     static constexpr bool kSeeded = false;
     const double *x, *dinv;
     double *y;
+    struct Row {
+        double dio;
+    };
     __device__ double gx(int32_t j) const { return x[j]; }
     __device__ double seed(int) const { return 0.0; }
-    __device__ void put(int o, double v, double *) const { st_stream(y + o, dinv[o] * v); }
+    __device__ Row row(int o) const { return {dinv[o]}; }
+    __device__ void put(int o, double v, double *, const Row &w) const { st_stream(y + o, w.dio * v); }
+    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
 };
 
 // s + p[0] + p[1] + ... + p[n-1], added left to right (PETSc's order). The LDS
@@ -557,6 +580,291 @@ __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict_
             if (t == 0) dpart[(int64_t)q * gridDim.x + b] = v;
         }
     }
+}
+
+// Row templates (Tuning::templates; the row patterns of a constant-
+// coefficient stencil, values included): the table holds each template's
+// offsets and values (pval indexed like the offsets), staged in LDS once per
+// workgroup, and the launch streams only the 1-byte ids, x and y — neither
+// aj nor aa. One lane per row: s = seed, then s += value * x[r + offset] in
+// the row's storage order, the products and sums of k_spmv_pattern on the
+// same bits (the values are the row's own, verified bit for bit at plan
+// time). With no matrix stream a block's work is three dependent latencies
+// (descriptor, ids, gathers), so the workgroups are persistent: each takes
+// the row blocks b = first, first + step, ... with the next block's ids and
+// the one after's descriptor loaded while the current block gathers. xcd:
+// XCD q (workgroup g % 8) takes the q-th eighth of the blocks, so the x
+// planes a block gathers are in its own L2. dpart: one partial per block, as
+// the STREAM launches write them.
+template <int T, int R, class Op>
+__global__ __launch_bounds__(T) void k_spmv_template(const BlockDesc *__restrict__ blk, int nblk, int xcd,
+                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
+                                                     const double *__restrict__ pval, int ntab, int npat, Op op,
+                                                     double *dpart, const int *stop) {
+    constexpr int TPT = (kPatTableMax + T - 1) / T;
+    __shared__ int32_t tab[kPatTableMax];
+    __shared__ double val[kPatTableMax];
+    __shared__ double red[R * T / 64];
+    if ((stop ? *stop : 0) != 0) return;
+    const int t = threadIdx.x, G = (int)gridDim.x, g = (int)blockIdx.x;
+    int first = g, step = G, last = nblk;
+    if (xcd && G >= 8 && (G & 7) == 0) {
+        const int q = g & 7;
+        first = (int)((int64_t)nblk * q / 8) + (g >> 3);
+        step = G >> 3;
+        last = (int)((int64_t)nblk * (q + 1) / 8);
+    }
+    if (first >= last) return;
+#pragma unroll
+    for (int i = 0; i < TPT; ++i)
+        if (t + i * T < ntab) {
+            tab[t + i * T] = ptab[t + i * T];
+            val[t + i * T] = pval[t + i * T];
+        }
+    // lane t takes rows t, t + T, ... (R of them) of each block
+    BlockDesc d = blk[first], dn = d;
+    if (first + step < last) dn = blk[first + step];
+    int p[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) p[u] = pid[d.row0 + min(t + u * T, d.nrows - 1)];
+    __syncthreads();
+    for (int b = first; b < last; b += step) {
+        int pn[R] = {};
+        BlockDesc dnn = dn;
+        if (b + step < last) {
+#pragma unroll
+            for (int u = 0; u < R; ++u) pn[u] = pid[dn.row0 + min(t + u * T, dn.nrows - 1)];
+        }
+        if (b + 2 * step < last) dnn = blk[b + 2 * step];
+        if (d.nk >= 0) {
+            double dv[R][Op::kDots > 0 ? Op::kDots : 1] = {};
+            int r[R], st[R], n[R];
+            double s[R];
+            typename Op::Row rw[R];
+            int nmax = 0;
+#pragma unroll
+            for (int u = 0; u < R; ++u) {
+                const bool own = t + u * T < d.nrows;
+                r[u] = d.row0 + min(t + u * T, d.nrows - 1);
+                const int32_t pm = tab[min(p[u], npat - 1)];
+                st[u] = pm & 0xffff;
+                n[u] = own ? pm >> 16 : 0;
+                nmax = max(nmax, n[u]);
+                s[u] = op.seed(r[u]);
+                rw[u] = op.row(r[u]);  // issued with the gathers (r is a valid row for every lane)
+            }
+            for (int32_t j0 = 0; j0 < nmax; j0 += 8) {
+                double xv[R][8];
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (j0 + j < n[u]) xv[u][j] = op.gx(r[u] + tab[st[u] + j0 + j]);
+#pragma unroll
+                for (int u = 0; u < R; ++u)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j)
+                        if (j0 + j < n[u]) s[u] += val[st[u] + j0 + j] * xv[u][j];
+            }
+#pragma unroll
+            for (int u = 0; u < R; ++u)
+                if (t + u * T < d.nrows) op.put(r[u], s[u], dv[u], rw[u]);
+            if (Op::kDots > 0 && dpart) {
+                // block_sum<R * T> of the rows in block order: each wave's 64
+                // rows by the same shuffle tree, then the R * T / 64 wave sums
+                // in row order (the bits of a one-row-per-lane launch)
+#pragma unroll
+                for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
+                    lds_barrier();
+#pragma unroll
+                    for (int u = 0; u < R; ++u) {
+                        double v = dv[u][q];
+#pragma unroll
+                        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+                        if ((t & 63) == 0) red[u * (T / 64) + (t >> 6)] = v;
+                    }
+                    lds_barrier();
+                    if (t == 0) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int w = 0; w < R * T / 64; ++w) v += red[w];
+                        dpart[(int64_t)q * nblk + b] = v;
+                    }
+                }
+            }
+        }
+        d = dn;
+        dn = dnn;
+#pragma unroll
+        for (int u = 0; u < R; ++u) p[u] = pn[u];
+    }
+}
+
+// The same launch software-pipelined across a workgroup's blocks (one lane
+// per row; templates of at most kTmplFast entries): while block i is summed,
+// block i+1's gathers and row operands and block i+2's ids are in flight.
+// Two fixed register sets (A, B) take the blocks in turn — a register copy of
+// a load in flight would wait for it — each block's ids are loaded before the
+// previous block's gathers, and nothing that loads or stores is behind a
+// branch (a path-dependent count of loads in flight makes the compiler wait
+// for all of them): past the last block the descriptors repeat the last one
+// (its loads are issued again and not used), and a lane past a block's rows
+// takes the block's last row (it stores the same bits as that row's lane; its
+// dot terms are dropped); a workgroup with an odd number of blocks sums its
+// last block twice (the same bits, stored twice), so the loop body has no
+// branch for the compiler to sink a prefetch into. The templates' offsets and values sit in LDS 16-B
+// aligned and zero-padded to kTmplFast (an unused slot gathers x[r] and is
+// not summed). The sum is s = seed, s += value * x in storage order.
+constexpr int kTmplFast = 8;
+typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
+template <class Op>
+struct TmplStage {
+    int r, n, p;
+    double s;
+    typename Op::Row rw;
+    double xv[kTmplFast];
+};
+template <class Op>
+__device__ __forceinline__ void tmpl_issue(const Op &op, const BlockDesc &d, int pid, int npat, const int32_t *tab,
+                                           const int32_t *off8, TmplStage<Op> &g) {
+    g.r = d.row0 + min((int)threadIdx.x, d.nrows - 1);
+    g.p = min(pid, npat - 1);
+    const i32x4 o0 = *reinterpret_cast<const i32x4 *>(off8 + g.p * kTmplFast);
+    const i32x4 o1 = *reinterpret_cast<const i32x4 *>(off8 + g.p * kTmplFast + 4);
+    g.n = tab[g.p] >> 16;
+    g.s = op.seed(g.r);
+    g.rw = op.row(g.r);
+    g.xv[0] = op.gx(g.r + o0.x);
+    g.xv[1] = op.gx(g.r + o0.y);
+    g.xv[2] = op.gx(g.r + o0.z);
+    g.xv[3] = op.gx(g.r + o0.w);
+    g.xv[4] = op.gx(g.r + o1.x);
+    g.xv[5] = op.gx(g.r + o1.y);
+    g.xv[6] = op.gx(g.r + o1.z);
+    g.xv[7] = op.gx(g.r + o1.w);
+}
+template <int T, class Op>
+__device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, const TmplStage<Op> &g,
+                                            const double *val8, double *red, double *dpart, int nblk) {
+    const int t = threadIdx.x;
+    const f64x2 *v8 = reinterpret_cast<const f64x2 *>(val8 + g.p * kTmplFast);
+    const f64x2 v0 = v8[0], v1 = v8[1], v2 = v8[2], v3 = v8[3];
+    const double vv[kTmplFast] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
+    double s = g.s;
+#pragma unroll
+    for (int j = 0; j < kTmplFast; ++j)
+        if (j < g.n) s += vv[j] * g.xv[j];
+    double dd[Op::kDots > 0 ? Op::kDots : 1] = {};
+    op.put(g.r, s, dd, g.rw);
+    if (Op::kDots > 0 && dpart) {
+        const bool own = t < d.nrows;
+#pragma unroll
+        for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
+            const double v = block_sum<T>(own ? dd[q] : 0.0, red);
+            if (t == 0) dpart[(int64_t)q * nblk + d.k0] = v;
+        }
+    }
+}
+template <int T, class Op>
+__global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__restrict__ blk, int nblk,
+                                                          const uint8_t *__restrict__ pid,
+                                                          const int32_t *__restrict__ ptab,
+                                                          const double *__restrict__ pval, int ntab, int npat, Op op,
+                                                          double *dpart, const int *stop) {
+    constexpr int FPT = (kPatMax * kTmplFast + T - 1) / T;
+    __shared__ int32_t tab[kPatMax];
+    __shared__ __attribute__((aligned(16))) int32_t off8[kPatMax * kTmplFast];
+    __shared__ __attribute__((aligned(16))) double val8[kPatMax * kTmplFast];
+    __shared__ double red[T / 64];
+    if ((stop ? *stop : 0) != 0) return;
+    const int t = threadIdx.x, G = (int)gridDim.x, g = (int)blockIdx.x;
+    int first = g, step = G, last = nblk;
+    if (G >= 8 && (G & 7) == 0) {  // XCD q = g % 8 takes the q-th eighth of the blocks
+        const int q = g & 7;
+        first = (int)((int64_t)nblk * q / 8) + (g >> 3);
+        step = G >> 3;
+        last = (int)((int64_t)nblk * (q + 1) / 8);
+    }
+    if (first >= last) return;
+    const int lastb = first + (last - 1 - first) / step * step;  // this workgroup's last block
+    if (t < npat) tab[t] = ptab[t];
+#pragma unroll
+    for (int i = 0; i < FPT; ++i) {
+        const int e = t + i * T, pp = e / kTmplFast, j = e % kTmplFast;
+        if (pp < npat) {
+            const int32_t pm = ptab[pp], st = pm & 0xffff, n = pm >> 16;
+            off8[e] = j < n ? ptab[st + j] : 0;
+            val8[e] = j < n ? pval[st + j] : 0.0;
+        }
+    }
+    auto lane_row = [&](const BlockDesc &dd) { return dd.row0 + min(t, dd.nrows - 1); };
+    BlockDesc d0 = blk[first], d1 = blk[min(first + step, lastb)], d2 = blk[min(first + 2 * step, lastb)];
+    int pa = pid[lane_row(d0)];
+    int pb = pid[lane_row(d1)];
+    __syncthreads();
+    TmplStage<Op> A, B;
+    tmpl_issue(op, d0, pa, npat, tab, off8, A);
+    for (int b = first; b <= lastb; b += 2 * step) {
+        // block b (A); b + step's gathers into B; b + 2 step's ids
+        pa = pid[lane_row(d2)];
+        tmpl_issue(op, d1, pb, npat, tab, off8, B);
+        const BlockDesc d3 = blk[min(b + 3 * step, lastb)];
+        __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's sums wait
+        tmpl_finish<T>(op, d0, A, val8, red, dpart, nblk);
+        // block b + step (B; past lastb: lastb again, the same bits stored
+        // twice); b + 2 step's gathers into A; b + 3 step's ids
+        pb = pid[lane_row(d3)];
+        tmpl_issue(op, d2, pa, npat, tab, off8, A);
+        const BlockDesc d4 = blk[min(b + 4 * step, lastb)];
+        __builtin_amdgcn_sched_barrier(0);
+        tmpl_finish<T>(op, d1, B, val8, red, dpart, nblk);
+        d0 = d2;
+        d1 = d3;
+        d2 = d4;
+    }
+}
+
+// Row-template launch shapes. The pipelined kernel (templates of at most
+// kTmplFast entries) against the one below (2 rows per lane, no pipeline;
+// its fallback for longer templates), per launch inside the 300^3 CG + GAMG
+// solve (tools/runs/tmpl_ab.sh, profiles/r06/w; us): V-cycle post-smoothing
+// with CG's two dots 301 vs 476, residual 209 vs 237, CG's SpMV + dot 242 vs
+// 224; solve 0.1375 vs 0.1492 s (row patterns, aa read: 0.164 s). The one
+// below, plain MatMult in tools/ab_opts.py (profiles/r06/o, p): 2 rows per
+// lane 134 vs 142 us (1 row) and 160 (4 rows); 32 waves per CU 134 vs 142
+// (16); the XCD chunks 134 vs 143 (g % 8 interleaved); row patterns 342.
+constexpr int kTmplRows = 2;
+constexpr int kTmplThreads = kStreamGeoms[6].threads / kTmplRows;
+constexpr int kTmplWavesPerCu = 32;
+inline int template_grid(const aijhip_mat &A, int32_t nblk) {
+    int g = (int)std::min<int64_t>(nblk, (int64_t)A.n_cu * (kTmplWavesPerCu * 64 / kTmplThreads));
+    if (g >= 8) g &= ~7;
+    return g;
+}
+template <class Op>
+static void launch_template(const aijhip_mat &A, const Op &op, double *dpart, hipStream_t s, const int *stop) {
+    const Plan &P = A.plan;
+    static_assert(kStreamGeoms[6].rows == kTmplThreads * kTmplRows, "a block's rows = the lanes x kTmplRows");
+    if (P.pat_maxlen <= kTmplFast) {
+        // persistent: as many workgroups as fit on the device at once (the
+        // kernel's registers decide), a multiple of 8 for the XCD chunks
+        constexpr int TP = kStreamGeoms[6].threads;
+        static const int per_cu = [] {
+            int n = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_spmv_template_pipe<TP, Op>, TP, 0) != hipSuccess ||
+                n < 1)
+                n = 1;
+            return n;
+        }();
+        int g = (int)std::min<int64_t>(P.n_blocks, (int64_t)A.n_cu * per_cu);
+        if (g >= 8) g &= ~7;
+        hipLaunchKernelGGL((k_spmv_template_pipe<TP, Op>), dim3(g), dim3(TP), 0, s, P.d_tblocks, P.n_blocks, P.d_pid,
+                           P.d_ptab, P.d_pval, P.n_ptab, P.n_pat, op, dpart, stop);
+        return;
+    }
+    hipLaunchKernelGGL((k_spmv_template<kTmplThreads, kTmplRows, Op>), dim3(template_grid(A, P.n_blocks)),
+                       dim3(kTmplThreads), 0, s, P.d_blocks, P.n_blocks, 1, P.d_pid, P.d_ptab, P.d_pval, P.n_ptab,
+                       P.n_pat, op, dpart, stop);
 }
 
 // Segments of long rows: tree-reduced partial sums. (Round 5: lane t taking
@@ -1029,14 +1337,19 @@ __device__ __forceinline__ unsigned long long pat_mix(unsigned long long h) {
     return h ^ (h >> 31);
 }
 
-// 64-bit hash of each row's length and column - row offsets (never 0)
+// 64-bit hash of each row's length and column - row offsets (never 0); with
+// aa (row templates) the value bits of each entry too
 __global__ __launch_bounds__(256) void k_pat_hash(int32_t m, const int32_t *__restrict__ ai,
-                                                  const int32_t *__restrict__ aj, unsigned long long *hash) {
+                                                  const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                                                  unsigned long long *hash) {
     const int32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= m) return;
     const int32_t k0 = ai[r], k1 = ai[r + 1];
     unsigned long long h = pat_mix(0x9e3779b97f4a7c15ull + (unsigned long long)(k1 - k0));
-    for (int32_t k = k0; k < k1; ++k) h = pat_mix(h ^ (unsigned long long)(uint32_t)(aj[k] - r));
+    for (int32_t k = k0; k < k1; ++k) {
+        h = pat_mix(h ^ (unsigned long long)(uint32_t)(aj[k] - r));
+        if (aa) h = pat_mix(h ^ (unsigned long long)__double_as_longlong(aa[k]));
+    }
     hash[r] = h | 1ull;
 }
 
@@ -1093,29 +1406,38 @@ __global__ __launch_bounds__(256) void k_pat_assign(int32_t m, const unsigned lo
     if (__atomic_load_n(rep + lo, __ATOMIC_RELAXED) > r) atomicMin(rep + lo, r);
 }
 
-// The offsets of each pattern's first row (at most kPatTableMax per row)
+// The offsets (and with aa the values) of each pattern's first row (at most
+// kPatTableMax per row)
 __global__ void k_pat_rows(int npat, const int32_t *__restrict__ rep, const int32_t *__restrict__ ai,
-                           const int32_t *__restrict__ aj, int32_t *len, int32_t *off) {
+                           const int32_t *__restrict__ aj, const double *__restrict__ aa, int32_t *len, int32_t *off,
+                           double *val) {
     const int p = blockIdx.x;
     const int32_t r = rep[p], k0 = ai[r], n = ai[r + 1] - k0;
     if (threadIdx.x == 0) len[p] = n;
-    for (int j = threadIdx.x; j < n && j < kPatTableMax; j += blockDim.x) off[p * kPatTableMax + j] = aj[k0 + j] - r;
+    for (int j = threadIdx.x; j < n && j < kPatTableMax; j += blockDim.x) {
+        off[p * kPatTableMax + j] = aj[k0 + j] - r;
+        if (aa) val[p * kPatTableMax + j] = aa[k0 + j];
+    }
 }
 
-// Rows whose entries differ from their pattern's (a hash collision)
+// Rows whose entries differ from their pattern's (a hash collision); with
+// pval the value bits are compared too
 __global__ __launch_bounds__(256) void k_pat_verify(int32_t m, const int32_t *__restrict__ ai,
-                                                    const int32_t *__restrict__ aj, const uint8_t *__restrict__ pid,
-                                                    const int32_t *__restrict__ ptab, int *bad) {
+                                                    const int32_t *__restrict__ aj, const double *__restrict__ aa,
+                                                    const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,
+                                                    const double *__restrict__ pval, int *bad) {
     const int32_t r = blockIdx.x * 256 + threadIdx.x;
     if (r >= m) return;
     const int32_t pm = ptab[pid[r]], st = pm & 0xffff, len = pm >> 16;
     const int32_t k0 = ai[r], n = ai[r + 1] - k0;
     bool ok = n == len;
-    for (int32_t j = 0; ok && j < n; ++j) ok = aj[k0 + j] - r == ptab[st + j];
+    for (int32_t j = 0; ok && j < n; ++j)
+        ok = aj[k0 + j] - r == ptab[st + j] &&
+             (!pval || __double_as_longlong(aa[k0 + j]) == __double_as_longlong(pval[st + j]));
     if (!ok) atomicAdd(bad, 1);
 }
 
-hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
+hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok, bool values) {
     *ok = false;
     const int32_t m = A.m;
     if (m <= 0 || A.compressed) return hipSuccess;
@@ -1123,10 +1445,12 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
     unsigned long long *d_hash = nullptr, *d_table = nullptr, *d_sorted = nullptr;
     int *d_flag = nullptr;
     int32_t *d_rep = nullptr, *d_len = nullptr, *d_off = nullptr;
+    double *d_val = nullptr;
+    const double *vaa = values ? A.d_aa : nullptr;
     hipError_t e;
     auto done = [&](hipError_t r) {
         hipFree(d_hash); hipFree(d_table); hipFree(d_sorted); hipFree(d_flag);
-        hipFree(d_rep); hipFree(d_len); hipFree(d_off);
+        hipFree(d_rep); hipFree(d_len); hipFree(d_off); hipFree(d_val);
         return r;
     };
     if ((e = hipMalloc(&d_hash, sizeof(unsigned long long) * (size_t)m)) != hipSuccess ||
@@ -1135,7 +1459,7 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
         (e = hipMemset(d_table, 0, sizeof(unsigned long long) * kPatTableSlots)) != hipSuccess ||
         (e = hipMemset(d_flag, 0, sizeof(int) * 3)) != hipSuccess)
         return done(e);
-    hipLaunchKernelGGL(k_pat_hash, dim3(g), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, d_hash);
+    hipLaunchKernelGGL(k_pat_hash, dim3(g), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, vaa, d_hash);
     hipLaunchKernelGGL(k_pat_insert, dim3(g), dim3(256), 0, nullptr, m, d_hash, d_table, d_flag, d_flag + 2);
     std::vector<unsigned long long> table(kPatTableSlots);
     int flag[2] = {0, 0};
@@ -1155,13 +1479,15 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
         (e = hipMalloc(&d_rep, sizeof(int32_t) * npat)) != hipSuccess ||
         (e = hipMalloc(&d_len, sizeof(int32_t) * npat)) != hipSuccess ||
         (e = hipMalloc(&d_off, sizeof(int32_t) * (size_t)npat * kPatTableMax)) != hipSuccess ||
+        (values && (e = hipMalloc(&d_val, sizeof(double) * (size_t)npat * kPatTableMax)) != hipSuccess) ||
         (e = hipMalloc(&P.d_pid, (size_t)m + 256)) != hipSuccess ||
         (e = hipMemcpy(d_sorted, hs.data(), sizeof(unsigned long long) * npat, hipMemcpyHostToDevice)) !=
             hipSuccess ||
         (e = hipMemcpy(d_rep, rep_init.data(), sizeof(int32_t) * npat, hipMemcpyHostToDevice)) != hipSuccess)
         return done(e);
     hipLaunchKernelGGL(k_pat_assign, dim3(g), dim3(256), 0, nullptr, m, d_hash, d_sorted, npat, P.d_pid, d_rep);
-    hipLaunchKernelGGL(k_pat_rows, dim3(npat), dim3(64), 0, nullptr, npat, d_rep, A.d_ai, A.d_aj, d_len, d_off);
+    hipLaunchKernelGGL(k_pat_rows, dim3(npat), dim3(64), 0, nullptr, npat, d_rep, A.d_ai, A.d_aj, vaa, d_len, d_off,
+                       d_val);
     std::vector<int32_t> len(npat);
     if ((e = hipGetLastError()) != hipSuccess ||
         (e = hipMemcpy(len.data(), d_len, sizeof(int32_t) * npat, hipMemcpyDeviceToHost)) != hipSuccess)
@@ -1175,35 +1501,54 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok) {
         return done(hipSuccess);
     }
     std::vector<int32_t> off((size_t)npat * kPatTableMax);
-    if ((e = hipMemcpy(off.data(), d_off, sizeof(int32_t) * off.size(), hipMemcpyDeviceToHost)) != hipSuccess)
+    std::vector<double> val(values ? off.size() : 0);
+    if ((e = hipMemcpy(off.data(), d_off, sizeof(int32_t) * off.size(), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (values && (e = hipMemcpy(val.data(), d_val, sizeof(double) * val.size(), hipMemcpyDeviceToHost)) !=
+                       hipSuccess))
         return done(e);
     int32_t dmax = 0;
+    std::vector<double> tval(values ? npat : 0, 0.0);
     for (int p = 0; p < npat; ++p) {
         tab[p] = (int32_t)tab.size() | (len[p] << 16);
         for (int j = 0; j < len[p]; ++j) {
             const int32_t o = off[(size_t)p * kPatTableMax + j];
             tab.push_back(o);
+            if (values) tval.push_back(val[(size_t)p * kPatTableMax + j]);
             dmax = std::max(dmax, o < 0 ? -o : o);
         }
     }
     P.pat_dmax = dmax;
-    if ((e = hipMalloc(&P.d_ptab, sizeof(int32_t) * tab.size())) != hipSuccess ||
-        (e = hipMemcpy(P.d_ptab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice)) != hipSuccess)
-        return done(e);
-    hipLaunchKernelGGL(k_pat_verify, dim3(g), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, P.d_pid, P.d_ptab, d_flag + 1);
-    if ((e = hipGetLastError()) != hipSuccess ||
-        (e = hipMemcpy(flag, d_flag, sizeof(int) * 2, hipMemcpyDeviceToHost)) != hipSuccess)
-        return done(e);
-    if (flag[1] != 0) {  // a collision: keep aj
+    P.pat_maxlen = *std::max_element(len.begin(), len.end());
+    auto drop = [&]() {
         hipFree(P.d_pid);
         hipFree(P.d_ptab);
+        hipFree(P.d_pval);
         P.d_pid = nullptr;
         P.d_ptab = nullptr;
+        P.d_pval = nullptr;
+    };
+    if ((e = hipMalloc(&P.d_ptab, sizeof(int32_t) * tab.size())) != hipSuccess ||
+        (e = hipMemcpy(P.d_ptab, tab.data(), sizeof(int32_t) * tab.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        (values && ((e = hipMalloc(&P.d_pval, sizeof(double) * tval.size())) != hipSuccess ||
+                    (e = hipMemcpy(P.d_pval, tval.data(), sizeof(double) * tval.size(), hipMemcpyHostToDevice)) !=
+                        hipSuccess))) {
+        drop();
+        return done(e);
+    }
+    hipLaunchKernelGGL(k_pat_verify, dim3(g), dim3(256), 0, nullptr, m, A.d_ai, A.d_aj, A.d_aa, P.d_pid, P.d_ptab,
+                       P.d_pval, d_flag + 1);
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpy(flag, d_flag, sizeof(int) * 2, hipMemcpyDeviceToHost)) != hipSuccess) {
+        drop();
+        return done(e);
+    }
+    if (flag[1] != 0) {  // a collision: keep aj (and aa)
+        drop();
         return done(hipSuccess);
     }
     P.n_ptab = (int32_t)tab.size();
     P.n_pat = npat;
-    P.bytes += (int64_t)m + 256 + 4 * (int64_t)tab.size();
+    P.bytes += (int64_t)m + 256 + 4 * (int64_t)tab.size() + (values ? 8 * (int64_t)tval.size() : 0);
     *ok = true;
     return done(hipSuccess);
 }
@@ -1345,10 +1690,13 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // Row patterns (Plan::d_pid; geometry 6, full-row lists, short rows)
     if constexpr (kGeom6) {
         if (P.d_pid && !L.ridx) {
-#define AIJHIP_PT(ADD)                                                                                     \
-    hipLaunchKernelGGL((k_spmv_pattern<T, CAP, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, \
-                       L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,                                 \
-                       OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop);                                \
+#define AIJHIP_PT(ADD)                                                                                        \
+    if (P.d_pval)                                                                                             \
+        launch_template(A, OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, s, stop);                           \
+    else                                                                                                      \
+        hipLaunchKernelGGL((k_spmv_pattern<T, CAP, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, P.d_blocks, \
+                           L.rai, P.d_pid, P.d_ptab, P.n_ptab, P.n_pat, A.d_aa,                                 \
+                           OpMult<ADD>{x, z, y, dpart != nullptr}, dpart, stop);                                \
     return
             if (add) { AIJHIP_PT(true); }
             AIJHIP_PT(false);
@@ -1475,6 +1823,11 @@ static hipError_t launch_stream_op(const aijhip_mat &A, const Op &op, double *dp
     const Plan &P = A.plan;
     if (P.n_blocks == 0) return hipSuccess;
     const int ex = exact < 0 ? (int)P.tune.exact : exact;
+    if (P.d_pid && P.d_pval) {  // row templates (planned at geometry 6)
+        if (P.tune.geom != 6) return hipErrorInvalidValue;
+        launch_template(A, op, dpart, s, stop);
+        return hipGetLastError();
+    }
     if (P.d_pid) {  // row patterns (planned at geometry 6)
         if (P.tune.geom != 6) return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_spmv_pattern<kStreamGeoms[6].threads, kStreamGeoms[6].nnz_cap, Op>), dim3(P.n_blocks),

@@ -50,7 +50,7 @@ def test_library_is_gfx950_code_object(pkg):
 
 
 def test_abi_version(pkg):
-    assert pkg.lib().aijhip_abi_version() == 4
+    assert pkg.lib().aijhip_abi_version() == 5
 
 
 def test_create_validates_before_touching_the_device(pkg):
@@ -131,7 +131,7 @@ int main(void) {
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
-    assert out.stdout.split()[:2] == ["4", "50"]
+    assert out.stdout.split()[:2] == ["5", "50"]
 
 
 def test_petsc_adapter_binds_only_declared_symbols():

@@ -1,4 +1,6 @@
-"""Row patterns (AIJHIP_OPT_ROW_PATTERNS): for short-row operands whose rows
+"""Row patterns (AIJHIP_OPT_ROW_PATTERNS) and row templates
+(AIJHIP_OPT_ROW_TEMPLATES: the patterns with their values, for a constant-
+coefficient stencil; neither aj nor aa read): for short-row operands whose rows
 follow at most 256 distinct column - row offset lists (a stencil), the STREAM
 row blocks read no column per entry — a pattern id per row, the lists staged
 in LDS, x gathered by one lane per row. aa and the summation (s = seed, then
@@ -48,19 +50,31 @@ def products(A, x, z, dev):
 @pytest.mark.parametrize("dims", [(37, 37, 37), (20, 17, 13), (1, 9, 40), (300, 2, 3)])
 def test_poisson_patterns_bitwise(pkg, dev, coracle, dims):
     """7-point Poisson with the reference point (helper.cpp:161-279), cubes,
-    boxes and thin grids: the automatic layout takes row patterns (interior,
-    faces, edges, corners, the reference rows); MatMult and MatMultAdd equal
-    the oracle and the aj layout bit for bit, also after new values."""
+    boxes and thin grids: the automatic layout takes row templates (the
+    distinct rows, offsets and values: interior, faces, edges, corners, the
+    reference rows; AIJHIP_OPT_ROW_TEMPLATES), or with templates off row
+    patterns (the distinct offset lists). MatMult and MatMultAdd equal the
+    oracle and the aj layout bit for bit in all three, also after new values:
+    values that no longer fit the templates re-plan to the patterns, values
+    that do keep them."""
     ai, aj, aa = pkg.poisson_csr(*dims)
     m = len(ai) - 1
     x, z = pkg.splitmix_uniform(m, 42), pkg.splitmix_uniform(m, 7)
     rows = np.repeat(np.arange(m), np.diff(ai))
     lists = {tuple(aj[ai[i]:ai[i + 1]] - rows[ai[i]:ai[i + 1]]) for i in range(m)}  # the distinct offset lists
+    temps = {tuple(aj[ai[i]:ai[i + 1]] - rows[ai[i]:ai[i + 1]]) + tuple(aa[ai[i]:ai[i + 1]].view(np.uint64))
+             for i in range(m)}  # the distinct rows
     with pkg.SeqAIJHIP(ai, aj, aa) as A:
         info = A.info()
-        assert info["row_patterns"] == len(lists) and info["column_codes"] == 0
+        assert (info["row_templates"], info["row_patterns"], info["column_codes"]) == (1, len(temps), 0)
+        assert info["mult_layout_bytes"] == m + 12 * (len(temps) + sum(len(t) // 2 for t in temps)) + 16 * m
+        yt, wt = products(A, x, z, dev)
+        assert_bits(yt, coracle.matmult(ai, aj, aa, x, omp=True))
+        A.set_option("row_templates", 0)
+        assert (A.info()["row_templates"], A.info()["row_patterns"]) == (0, len(lists))
         y1, w1 = products(A, x, z, dev)
-        assert_bits(y1, coracle.matmult(ai, aj, aa, x, omp=True))
+        assert_bits(yt, y1)
+        assert_bits(wt, w1)
         A.set_option("row_patterns", 0)
         A.set_option("column_codes", 0)
         assert A.info()["row_patterns"] == 0
@@ -68,10 +82,82 @@ def test_poisson_patterns_bitwise(pkg, dev, coracle, dims):
         assert_bits(y1, y0)
         assert_bits(w1, w0)
         A.set_option("row_patterns", -1)
+        A.set_option("row_templates", -1)
+        assert A.info()["row_templates"] == 1
+        A.update_values(2.0 * aa)  # still one template per distinct row
+        assert A.info()["row_templates"] == 1
+        y3, _ = products(A, x, z, dev)
+        assert_bits(y3, coracle.matmult(ai, aj, 2.0 * aa, x, omp=True))
         aa2 = np.random.default_rng(5).uniform(-1, 1, len(aa))
-        A.update_values(aa2)  # the patterns do not depend on the values
+        A.update_values(aa2)  # the patterns do not depend on the values; the templates do
+        assert (A.info()["row_templates"], A.info()["row_patterns"]) == (0, len(lists))
         y2, _ = products(A, x, z, dev)
         assert_bits(y2, coracle.matmult(ai, aj, aa2, x, omp=True))
+
+
+def stencil27_csr(n):
+    """Constant-coefficient 27-point stencil on an n^3 grid (26 on the
+    diagonal, -1 off it): rows of up to 27 entries, 27 distinct rows."""
+    idx = np.arange(n ** 3).reshape(n, n, n)
+    rows, cols, vals = [], [], []
+    for dz in (-1, 0, 1):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                src = idx[max(0, -dz):n - max(0, dz), max(0, -dy):n - max(0, dy), max(0, -dx):n - max(0, dx)]
+                dst = idx[max(0, dz):n - max(0, -dz) or n, max(0, dy):n - max(0, -dy) or n,
+                          max(0, dx):n - max(0, -dx) or n]
+                rows.append(src.ravel())
+                cols.append(dst.ravel())
+                vals.append(np.full(src.size, 26.0 if (dz, dy, dx) == (0, 0, 0) else -1.0))
+    r, c, v = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
+    o = np.lexsort((c, r))
+    r, c, v = r[o], c[o], v[o]
+    ai = np.concatenate([[0], np.cumsum(np.bincount(r, minlength=n ** 3))]).astype(np.int32)
+    return ai, c.astype(np.int32), v
+
+
+@pytest.mark.parametrize("n", [12, 33])
+def test_templates_longer_than_the_fast_slots(pkg, dev, coracle, n):
+    """Row templates of 27 entries (a 27-point stencil): more than the
+    pipelined kernel's 8 fast slots, so the launch takes the 2-rows-per-lane
+    template kernel; MatMult / MatMultAdd bitwise the oracle's, and the same
+    as the row patterns (templates off)."""
+    ai, aj, aa = stencil27_csr(n)
+    m = n ** 3
+    x, z = pkg.splitmix_uniform(m, 3), pkg.splitmix_uniform(m, 4)
+    with pkg.SeqAIJHIP(ai, aj, aa) as A:
+        assert A.info()["row_templates"] == 1
+        yt, wt = products(A, x, z, dev)
+        assert_bits(yt, coracle.matmult(ai, aj, aa, x, omp=True))
+        A.set_option("row_templates", 0)
+        y1, w1 = products(A, x, z, dev)
+        assert_bits(yt, y1)
+        assert_bits(wt, w1)
+
+
+def test_templates_cg_dots_match_csr_on_odd_block_counts(pkg, dev):
+    """CG + Jacobi on operands whose persistent template grid leaves some
+    workgroups an odd number of row blocks (the last one summed twice) and
+    blocks shorter than 512 rows: the residual history and solution equal
+    the CSR layout's bit for bit (the fused SpMV + p.w partials per block)."""
+    K = importlib.import_module("petsc-openacc_amd.ksp")
+    for dims in ((23, 19, 17), (64, 64, 61)):
+        ai, aj, aa = pkg.poisson_csr(*dims)
+        rhs, _ = pkg.poisson_vectors(*dims)
+        b = torch.from_numpy(rhs).to(dev)
+        out = {}
+        for temps in (0, 1):
+            with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=temps, row_templates=temps, column_codes=0) as A:
+                assert A.info()["row_templates"] == temps
+                x = torch.zeros_like(b)
+                with K.KSPCG(A, pc="jacobi", rtol=1e-10, max_it=300) as ksp:
+                    ksp.set_up()
+                    ksp.solve(b, x)
+                    torch.cuda.synchronize()
+                    out[temps] = (ksp.its, ksp.history(), x.cpu().numpy())
+        assert out[0][0] == out[1][0]
+        assert_bits(out[0][1], out[1][1])
+        assert_bits(out[0][2], out[1][2])
 
 
 @pytest.mark.parametrize("name", GOLDEN_NAMES)
@@ -142,23 +228,26 @@ def test_cg_and_gamg_with_patterns_bitwise(pkg, dev):
     """The solver path on a patterned operator: CG + Jacobi (the fused
     SpMV + p.w epilogue) and CG + GAMG (the fused V-cycle smoothers and the
     set-up's power iteration on the fine level) give the aj run's residual
-    history and solution bit for bit."""
+    history and solution bit for bit, with row patterns and with row
+    templates."""
     K = importlib.import_module("petsc-openacc_amd.ksp")
     ai, aj, aa = pkg.poisson_csr(40)
     rhs, _ = pkg.poisson_vectors(40, 40, 40)
     b = torch.from_numpy(rhs).to(dev)
     for pc, kw in (("jacobi", dict(rtol=1e-10, max_it=500)), ("gamg", dict(rtol=1e-14, atol=1e-12))):
         out = {}
-        for pats in (0, 1):
-            with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=pats, column_codes=0) as A:
+        for pats, temps in ((0, 0), (1, 0), (1, 1)):
+            with pkg.SeqAIJHIP(ai, aj, aa, row_patterns=pats, row_templates=temps, column_codes=0) as A:
                 assert (A.info()["row_patterns"] > 0) == bool(pats)
+                assert A.info()["row_templates"] == temps
                 x = torch.zeros_like(b)
                 with K.KSPCG(A, pc=pc, **kw) as ksp:
                     ksp.set_up()
                     ksp.solve(b, x)
                     torch.cuda.synchronize()
                     assert ksp.fused
-                    out[pats] = (ksp.its, ksp.history(), x.cpu().numpy())
-        assert out[0][0] == out[1][0]
-        assert_bits(out[0][1], out[1][1])
-        assert_bits(out[0][2], out[1][2])
+                    out[pats, temps] = (ksp.its, ksp.history(), x.cpu().numpy())
+        for key in ((1, 0), (1, 1)):
+            assert out[0, 0][0] == out[key][0]
+            assert_bits(out[0, 0][1], out[key][1])
+            assert_bits(out[0, 0][2], out[key][2])
