@@ -55,7 +55,7 @@ extern "C" {
 
 /* 2: aijhip_info_t gained mult_layout_bytes and lost the fields of the
  * withdrawn A/B-only options; their option values and kernel 4 are reserved
- * and return AIJHIP_ERR_ARG (measured slower).
+ * and return AIJHIP_ERR_ARG (measured slower, profiles/README.md).
  * 3: aijhip_gamg_params_t gained coarsen / square_graph / eig_ksp (PETSc
  * 3.7's MIS coarsening and CG emax estimate as options).
  * 4: aijhip_info_t gained hw_queues (the side streams' automatic choice
@@ -74,7 +74,7 @@ enum {
     AIJHIP_ERR_STATE = 5     /* call not valid in the handle's current state */
 };
 
-/* SpMV kernel families (see DESIGN.md §Kernels). AUTO picks by row-length
+/* SpMV kernel families (see DESIGN.md §5). AUTO picks by row-length
  * statistics at assembly time. */
 enum {
     AIJHIP_KERNEL_AUTO = 0,
@@ -183,10 +183,10 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes);
  * setting. Re-plans on the device. */
 enum {
     /* Values 2, 4, 5, 7, 11, 15 and 16 (and kernel 4) are reserved:
-     * A/B-only variants withdrawn (measured slower); setting
+     * A/B-only variants withdrawn (measured slower; profiles/README.md); setting
      * them returns AIJHIP_ERR_ARG. */
     AIJHIP_OPT_STREAM_GEOMETRY = 1, /* 0..9: lanes / LDS entries / rows per block
-                                       (DESIGN.md §Kernels); -1 (default):
+                                       (DESIGN.md §5); -1 (default):
                                        6 for short rows, 1 for long rows    */
     AIJHIP_OPT_NT_LOADS = 3,        /* -1 (default): non-temporal for long rows
                                        with scattered gathers (the geometry-1

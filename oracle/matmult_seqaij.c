@@ -9,7 +9,7 @@
  * Parity status: PINNED ONLY BY RESTATEMENT. The reference holds no golden
  * vectors for MatMult_SeqAIJ and PETSc itself (which holds the original loop,
  * aij.c:1277-1335 [ext], cut out by /root/reference/scripts/petsc.sh:85-86) is
- * not in this image, so the reference cannot be built here (DESIGN.md §Oracle).
+ * not in this image, so the reference cannot be built here (DESIGN.md §3).
  * This restatement is cross-checked bit for bit against an independent numpy
  * restatement (oracle/seqaij.py) and against the committed fixtures in
  * tests/golden/ generated from it. "parity unpinned" w.r.t. a reference run.

@@ -34,7 +34,7 @@ KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
 OPTIONS = {"geometry": 1, "nt_loads": 3, "exact": 6, "long_xcd": 8, "long_overlap": 9, "host_pipeline": 10,
            "gather_sort": 12, "column_codes": 13, "row_patterns": 14, "row_templates": 17}
-# withdrawn in ABI 2 (measured slower); the library refuses them
+# withdrawn in ABI 2 (measured slower, profiles/README.md "Measured and withdrawn"); the library refuses them
 WITHDRAWN_OPTIONS = {"xcd_remap": 2, "persistent": 4, "clamped": 5, "x_tile": 7, "row_group": 11,
                      "long_window": 15, "pipeline": 16}
 

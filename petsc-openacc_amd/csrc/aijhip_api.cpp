@@ -938,7 +938,7 @@ int aijhip_mat_set_kernel(aijhip_mat_t A, int kernel, int lanes) {
     if (rc) return rc;
     if (kernel == 4)  // reserved: the withdrawn MERGE kernel
         return fail(AIJHIP_ERR_ARG, "the MERGE kernel was withdrawn in ABI 2: STREAM's row blocks are the "
-                                    "merge-path decomposition (DESIGN.md §5)");
+                                    "merge-path decomposition (DESIGN.md §4)");
     if (kernel < AIJHIP_KERNEL_AUTO || kernel > AIJHIP_KERNEL_VECTOR)
         return fail(AIJHIP_ERR_ARG, "unknown kernel " + std::to_string(kernel));
     DeviceGuard g(A->device);
@@ -961,7 +961,7 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             break;
         case 2: case 4: case 5: case 7: case 11: case 15: case 16:  // reserved (include/aijhip.h)
             return fail(AIJHIP_ERR_ARG, "option " + std::to_string(option) +
-                                            " was withdrawn (measured slower; DESIGN.md §5)");
+                                            " was withdrawn (measured slower; profiles/README.md)");
         case AIJHIP_OPT_NT_LOADS:
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "nt_loads: -1 (auto), 0, 1");
             t.nt = value;

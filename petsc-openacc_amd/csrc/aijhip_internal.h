@@ -25,7 +25,7 @@ struct Range {
     Range &operator=(const Range &) = delete;
 };
 
-// STREAM kernel geometries (DESIGN.md §Kernels): `threads` lanes per row
+// STREAM kernel geometries (DESIGN.md §5): `threads` lanes per row
 // block, up to `nnz_cap` products staged in LDS (8 B each) and up to
 // `rows` rows (rows / threads rows per lane in the reduction phase).
 struct StreamGeom {
@@ -81,7 +81,7 @@ struct RowList {
 };
 
 // Speed-only knobs (aijhip_mat_set_option); they never change results.
-// Defaults are the fastest measured on MI355X: geometry 6 for
+// Defaults are the fastest measured on MI355X (profiles/README.md): geometry 6 for
 // short rows and for long rows whose gathers run along x lines, geometry 1 for
 // scattered long rows; plain loads except for those (non-temporal); hardware
 // round-robin block placement. The A/B-only variants measured slower

@@ -512,7 +512,7 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
 // offsets; ntab entries in all (<= kPatTableMax). The row starts come from
 // ai (a scan of the patterns' lengths, branch-free 8-slot gathers, x[r +- 1]
 // from the neighbouring lanes, one 16-B LDS write per pair and XCD-chunked
-// block placement were all measured slower: DESIGN §5, profiles/r03/patterns/).
+// block placement were all measured slower: profiles/README.md, profiles/r03/patterns/).
 template <int T, int CAP, class Op>
 __global__ __launch_bounds__(T) void k_spmv_pattern(const BlockDesc *__restrict__ blk, const int32_t *__restrict__ rai,
                                                     const uint8_t *__restrict__ pid, const int32_t *__restrict__ ptab,

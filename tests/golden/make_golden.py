@@ -7,7 +7,7 @@ and PETSc is not in the image, so these fixtures come from the numpy
 restatement oracle/seqaij.py (cross-checked bit for bit against the C
 restatement oracle/matmult_seqaij.c by tests/test_oracle.py). They pin the
 oracle and the GPU path against regressions; they are NOT outputs of a
-reference run ("parity unpinned", DESIGN.md §Oracle).
+reference run ("parity unpinned", DESIGN.md §3).
 
 Each .npz holds: ai, aj, aa, ncols, x, y = A x, z, w = z + A x, xt, yt = A^T xt.
 """

@@ -95,41 +95,47 @@ def test_poisson_patterns_bitwise(pkg, dev, coracle, dims):
         assert_bits(y2, coracle.matmult(ai, aj, aa2, x, omp=True))
 
 
-def stencil27_csr(n):
-    """Constant-coefficient 27-point stencil on an n^3 grid (26 on the
-    diagonal, -1 off it): rows of up to 27 entries, 27 distinct rows."""
-    idx = np.arange(n ** 3).reshape(n, n, n)
+def box_stencil_csr(nz, ny, nx):
+    """Constant-coefficient box stencil (27 points in 3-D, 9 with nz = 1) on
+    an nz x ny x nx grid: the point count less one on the diagonal, -1 off
+    it; rows of up to 27 (9) entries."""
+    idx = np.arange(nz * ny * nx).reshape(nz, ny, nx)
     rows, cols, vals = [], [], []
-    for dz in (-1, 0, 1):
+    dzs = (-1, 0, 1) if nz > 1 else (0,)
+    npts = 9 * len(dzs)
+    for dz in dzs:
         for dy in (-1, 0, 1):
             for dx in (-1, 0, 1):
-                src = idx[max(0, -dz):n - max(0, dz), max(0, -dy):n - max(0, dy), max(0, -dx):n - max(0, dx)]
-                dst = idx[max(0, dz):n - max(0, -dz) or n, max(0, dy):n - max(0, -dy) or n,
-                          max(0, dx):n - max(0, -dx) or n]
+                def sl(d, n):
+                    return slice(max(0, -d), n - max(0, d)), slice(max(0, d), n - max(0, -d))
+                (sz, tz), (sy, ty), (sx, tx) = sl(dz, nz), sl(dy, ny), sl(dx, nx)
+                src, dst = idx[sz, sy, sx], idx[tz, ty, tx]
                 rows.append(src.ravel())
                 cols.append(dst.ravel())
-                vals.append(np.full(src.size, 26.0 if (dz, dy, dx) == (0, 0, 0) else -1.0))
+                vals.append(np.full(src.size, npts - 1.0 if (dz, dy, dx) == (0, 0, 0) else -1.0))
     r, c, v = np.concatenate(rows), np.concatenate(cols), np.concatenate(vals)
     o = np.lexsort((c, r))
     r, c, v = r[o], c[o], v[o]
-    ai = np.concatenate([[0], np.cumsum(np.bincount(r, minlength=n ** 3))]).astype(np.int32)
+    ai = np.concatenate([[0], np.cumsum(np.bincount(r, minlength=nz * ny * nx))]).astype(np.int32)
     return ai, c.astype(np.int32), v
 
 
-@pytest.mark.parametrize("n", [12, 33])
-def test_templates_longer_than_the_fast_slots(pkg, dev, coracle, n):
-    """Row templates of 27 entries (a 27-point stencil): more than the
-    pipelined kernel's 8 fast slots, so the launch takes the 2-rows-per-lane
-    template kernel; MatMult / MatMultAdd bitwise the oracle's, and the same
-    as the row patterns (templates off)."""
-    ai, aj, aa = stencil27_csr(n)
-    m = n ** 3
+@pytest.mark.parametrize("dims", [(1, 40, 37), (1, 700, 650)])
+def test_templates_longer_than_the_fast_slots(pkg, dev, coracle, dims):
+    """Row templates of 9 entries (a 2-D 9-point stencil; mean row <= 16, so
+    templates apply): more than the pipelined kernel's 8 fast slots, so the
+    launch takes the 2-rows-per-lane template kernel; MatMult / MatMultAdd
+    bitwise the oracle's and the row patterns' (templates off)."""
+    ai, aj, aa = box_stencil_csr(*dims)
+    m = len(ai) - 1
+    assert np.diff(ai).max() == 9
     x, z = pkg.splitmix_uniform(m, 3), pkg.splitmix_uniform(m, 4)
     with pkg.SeqAIJHIP(ai, aj, aa) as A:
         assert A.info()["row_templates"] == 1
         yt, wt = products(A, x, z, dev)
         assert_bits(yt, coracle.matmult(ai, aj, aa, x, omp=True))
         A.set_option("row_templates", 0)
+        assert A.info()["row_patterns"] > 0
         y1, w1 = products(A, x, z, dev)
         assert_bits(yt, y1)
         assert_bits(wt, w1)

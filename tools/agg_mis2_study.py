@@ -10,7 +10,7 @@ Variants: MIS-2 roots (Luby rounds on hashed priorities, distance-2 key
 maxima) + their strong neighbours, left-overs joined to the strongest
 aggregated neighbour; and the same plus a second MIS-2 round on the
 still-free nodes that have >= t free strong neighbours. Results in
-profiles/r02/agg_mis2_study.txt and DESIGN.md §9.
+profiles/r02/agg_mis2_study.txt.
 """
 import sys, time
 sys.path.insert(0, '.')

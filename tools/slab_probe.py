@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The parts of one rank's work at N = 8 strong scaling (300^3 over 8 GPUs:
 37-38 z-planes, 3.33-3.42 M rows per rank), measured on one GPU, for the
-N = 8 projection in DESIGN.md §8:
+N = 8 projection (profiles/r03/n8_projection/):
 
   - the diagonal block's SpMV (STREAM, HIP events, median of 100 launches);
   - the off-diagonal block (2 boundary planes, one entry per row,
