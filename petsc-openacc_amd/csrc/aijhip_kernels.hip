@@ -97,8 +97,8 @@ __device__ __forceinline__ void st_stream(double *p, double v) { __builtin_nonte
 // the block's dot partials d[0..kDots). `row` loads the row's other operands
 // (Row) so that a launch can issue them before the gathers (the row-template
 // kernel: with no matrix stream, a load issued after the sum is one more
-// latency per block); put(o, v, d) = put(o, v, d, row(o)), the same values —
-// the outputs never alias these inputs within a row.
+// latency per block) and put(o, v, d, row) takes them; put(o, v, d) loads
+// them itself, after the sum (the STREAM kernels' form).
 template <bool ADD>
 struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     static constexpr int kDots = 1;
@@ -116,7 +116,10 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
         st_stream(y + o, v);
         if (dot) d[0] += w.xo * v;
     }
-    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
+    __device__ void put(int o, double v, double *d) const {
+        st_stream(y + o, v);
+        if (dot) d[0] += x[o] * v;
+    }
 };
 
 // MatResidual with the SpMV: r_i = b_i + (-1) (A x)_i (SpMV + k_resid, same
@@ -139,7 +142,11 @@ struct OpMgResid {
         if constexpr (NT) st_stream(r + o, ro);
         else r[o] = ro;
     }
-    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
+    __device__ void put(int o, double v, double *) const {
+        const double ro = b[o] + (-1.0) * v;
+        if constexpr (NT) st_stream(r + o, ro);
+        else r[o] = ro;
+    }
 };
 
 // V-cycle post-smoothing, one Richardson step with Jacobi from the guess t
@@ -168,7 +175,16 @@ struct OpMgPost {
             d[1] += xo * w.bo;
         }
     }
-    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
+    __device__ void put(int o, double v, double *d) const {
+        const double bo = b[o];
+        const double xo = t[o] + 1.0 * (dinv[o] * (bo + (-1.0) * v));
+        if constexpr (NT) st_stream(x + o, xo);
+        else x[o] = xo;
+        if (dot) {
+            d[0] += xo * xo;
+            d[1] += xo * bo;
+        }
+    }
 };
 
 // y = D^-1 A x (the GAMG set-up's power iteration, gamg_setup.cpp dinv_apply).
@@ -184,7 +200,7 @@ struct OpDinvMult {
     __device__ double seed(int) const { return 0.0; }
     __device__ Row row(int o) const { return {dinv[o]}; }
     __device__ void put(int o, double v, double *, const Row &w) const { st_stream(y + o, w.dio * v); }
-    __device__ void put(int o, double v, double *d) const { put(o, v, d, row(o)); }
+    __device__ void put(int o, double v, double *) const { st_stream(y + o, dinv[o] * v); }
 };
 
 // s + p[0] + p[1] + ... + p[n-1], added left to right (PETSc's order). The LDS
@@ -708,11 +724,13 @@ __global__ __launch_bounds__(T) void k_spmv_template(const BlockDesc *__restrict
 // previous block's gathers, and nothing that loads or stores is behind a
 // branch (a path-dependent count of loads in flight makes the compiler wait
 // for all of them): past the last block the descriptors repeat the last one
-// (its loads are issued again and not used), and a lane past a block's rows
-// takes the block's last row (it stores the same bits as that row's lane; its
-// dot terms are dropped); a workgroup with an odd number of blocks sums its
-// last block twice (the same bits, stored twice), so the loop body has no
-// branch for the compiler to sink a prefetch into. The templates' offsets and values sit in LDS 16-B
+// (its loads are issued again and not used), a lane past a block's rows
+// loads the block's last row, and a workgroup with an odd number of blocks
+// sums its last block twice, so the loop body has no branch for the compiler
+// to sink a prefetch into. Only the stores are per lane (exec-masked): a lane
+// stores only its own row of a live block — the waves of a workgroup do not
+// run in step, so a duplicate's store could land after another wave already
+// stored that row and an in-place MatMultAdd (z = y) read it as its seed. The templates' offsets and values sit in LDS 16-B
 // aligned and zero-padded to kTmplFast (an unused slot gathers x[r] and is
 // not summed). The sum is s = seed, s += value * x in storage order.
 constexpr int kTmplFast = 8;
@@ -744,9 +762,10 @@ __device__ __forceinline__ void tmpl_issue(const Op &op, const BlockDesc &d, int
     g.xv[7] = op.gx(g.r + o1.w);
 }
 template <int T, class Op>
-__device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, const TmplStage<Op> &g,
+__device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, int live, const TmplStage<Op> &g,
                                             const double *val8, double *red, double *dpart, int nblk) {
     const int t = threadIdx.x;
+    const bool own = t < live;
     const f64x2 *v8 = reinterpret_cast<const f64x2 *>(val8 + g.p * kTmplFast);
     const f64x2 v0 = v8[0], v1 = v8[1], v2 = v8[2], v3 = v8[3];
     const double vv[kTmplFast] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
@@ -755,13 +774,12 @@ __device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, co
     for (int j = 0; j < kTmplFast; ++j)
         if (j < g.n) s += vv[j] * g.xv[j];
     double dd[Op::kDots > 0 ? Op::kDots : 1] = {};
-    op.put(g.r, s, dd, g.rw);
+    if (own) op.put(g.r, s, dd, g.rw);
     if (Op::kDots > 0 && dpart) {
-        const bool own = t < d.nrows;
 #pragma unroll
         for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
             const double v = block_sum<T>(own ? dd[q] : 0.0, red);
-            if (t == 0) dpart[(int64_t)q * nblk + d.k0] = v;
+            if (t == 0 && live > 0) dpart[(int64_t)q * nblk + d.k0] = v;
         }
     }
 }
@@ -810,14 +828,14 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
         tmpl_issue(op, d1, pb, npat, tab, off8, B);
         const BlockDesc d3 = blk[min(b + 3 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's sums wait
-        tmpl_finish<T>(op, d0, A, val8, red, dpart, nblk);
-        // block b + step (B; past lastb: lastb again, the same bits stored
-        // twice); b + 2 step's gathers into A; b + 3 step's ids
+        tmpl_finish<T>(op, d0, d0.nrows, A, val8, red, dpart, nblk);
+        // block b + step (B; past lastb: lastb again, loaded and summed but
+        // not stored); b + 2 step's gathers into A; b + 3 step's ids
         pb = pid[lane_row(d3)];
         tmpl_issue(op, d2, pa, npat, tab, off8, A);
         const BlockDesc d4 = blk[min(b + 4 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);
-        tmpl_finish<T>(op, d1, B, val8, red, dpart, nblk);
+        tmpl_finish<T>(op, d1, b + step <= lastb ? d1.nrows : 0, B, val8, red, dpart, nblk);
         d0 = d2;
         d1 = d3;
         d2 = d4;

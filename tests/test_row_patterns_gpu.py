@@ -141,6 +141,40 @@ def test_templates_longer_than_the_fast_slots(pkg, dev, coracle, dims):
         assert_bits(wt, w1)
 
 
+@pytest.mark.parametrize("m,n", [(119, 4), (250, 17), (1537, None), (70001, None)])
+def test_templates_inplace_mult_add(pkg, dev, coracle, m, n):
+    """In-place MatMultAdd (w = z, PCMG's x = x + P x_c) on row templates: a
+    coarse prolongator's shape (m x n, n < m, every row its own template) and
+    banded operators of one to 137 row blocks (a few value patterns). A lane
+    past a block's rows and the re-summed last block of a workgroup must not
+    store — another wave may already have updated that row, which an
+    in-place add reads as its seed. w equals z + A x bit for bit."""
+    rng = np.random.default_rng(m)
+    if n is not None:
+        rows = [np.unique(rng.integers(0, n, rng.integers(1, 4))) for _ in range(m)]
+        vals = [rng.uniform(-1, 1, len(c)) for c in rows]
+    else:
+        n = m
+        rows = [np.arange(max(0, i - 1), min(m, i + 2)) for i in range(m)]
+        pick = rng.integers(0, 3, m)
+        vals = [np.array([0.5, -1.0, 2.0, 0.25])[(pick[i] + np.arange(len(c))) % 4] for i, c in enumerate(rows)]
+    ai = np.concatenate([[0], np.cumsum([len(c) for c in rows])]).astype(np.int32)
+    aj = np.concatenate(rows).astype(np.int32)
+    aa = np.concatenate(vals)
+    x, z = rng.uniform(-1, 1, n), rng.uniform(-1, 1, m)
+    ref = coracle.matmult_add(ai, aj, aa, x, z)
+    with pkg.SeqAIJHIP(ai, aj, aa, ncols=n, row_patterns=1) as A:
+        assert A.info()["row_templates"] == 1
+        xd, zd = to_dev(x, dev), to_dev(z, dev)
+        w = zd.clone()
+        A.mult_add(xd, w, w)
+        w2 = torch.full_like(zd, np.nan)
+        A.mult_add(xd, zd, w2)
+        torch.cuda.synchronize()
+        assert_bits(w.cpu().numpy(), ref)
+        assert_bits(w2.cpu().numpy(), ref)
+
+
 def test_templates_cg_dots_match_csr_on_odd_block_counts(pkg, dev):
     """CG + Jacobi on operands whose persistent template grid leaves some
     workgroups an odd number of row blocks (the last one summed twice) and
