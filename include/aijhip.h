@@ -61,8 +61,9 @@ extern "C" {
  * 4: aijhip_info_t gained hw_queues (the side streams' automatic choice
  * follows it); aijhip_mpi.h gained aijhip_mpiaij_get_overlap and the
  * automatic value -1 of aijhip_mpiaij_set_overlap.
- * 5: AIJHIP_OPT_ROW_TEMPLATES; aijhip_info_t's last word (reserved0) is
- * row_templates (layout unchanged). */
+ * 5: AIJHIP_OPT_ROW_TEMPLATES and AIJHIP_OPT_VALUE_CODES; aijhip_info_t's
+ * former reserved0 is row_templates, and it gained value_codes (+ a
+ * reserved word). */
 #define AIJHIP_ABI_VERSION 5
 
 enum {
@@ -153,6 +154,10 @@ typedef struct aijhip_info {
                                 (AIJHIP_OPT_ROW_TEMPLATES): aa is not read
                                 by MatMult, else 0 (ABI 5; the former
                                 reserved word)                               */
+    int32_t value_codes;     /* the dictionary's size when MatMult reads a
+                                16-bit value code per entry instead of aa
+                                (AIJHIP_OPT_VALUE_CODES), else 0 (ABI 5)     */
+    int32_t reserved1;
 } aijhip_info_t;
 
 /* Library / device. */
@@ -260,7 +265,7 @@ enum {
                                        sums. 1 on, 0 off, -1 (default): tried
                                        first where the mean row is at most 16
                                        entries; costs 1 byte per row          */
-    AIJHIP_OPT_ROW_TEMPLATES = 17   /* with row patterns: when the operand's rows
+    AIJHIP_OPT_ROW_TEMPLATES = 17,  /* with row patterns: when the operand's rows
                                        are at most 256 distinct (offsets,
                                        values) lists — a constant-coefficient
                                        stencil — the table holds the values
@@ -271,6 +276,16 @@ enum {
                                        -1 (default): tried before the plain
                                        row patterns. aijhip_mat_update_values
                                        re-plans (new values may not fit)     */
+    AIJHIP_OPT_VALUE_CODES = 18     /* a 16-bit index per entry into a
+                                       dictionary of the operator's distinct
+                                       values (at most 512) in aa's place:
+                                       6 bytes per entry with aj or the packed
+                                       gather-ordered columns instead of 12;
+                                       the same bits. 1 on (where it fits),
+                                       0 off, -1 (default): on for the
+                                       set-up's own operators (GAMG's finest
+                                       P and P^T), off for a caller's handle.
+                                       aijhip_mat_update_values re-plans     */
 };
 int aijhip_mat_set_option(aijhip_mat_t A, int option, int value);
 

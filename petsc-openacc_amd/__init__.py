@@ -33,7 +33,8 @@ if os.environ.get("AIJHIP_LIB"):
 KERNELS = {"auto": 0, "stream": 1, "scalar": 2, "vector": 3, "merge": 4}
 KERNEL_NAMES = {v: k for k, v in KERNELS.items()}
 OPTIONS = {"geometry": 1, "nt_loads": 3, "exact": 6, "long_xcd": 8, "long_overlap": 9, "host_pipeline": 10,
-           "gather_sort": 12, "column_codes": 13, "row_patterns": 14, "row_templates": 17}
+           "gather_sort": 12, "column_codes": 13, "row_patterns": 14, "row_templates": 17,
+           "value_codes": 18}
 # withdrawn in ABI 2 (measured slower, profiles/README.md "Measured and withdrawn"); the library refuses them
 WITHDRAWN_OPTIONS = {"xcd_remap": 2, "persistent": 4, "clamped": 5, "x_tile": 7, "row_group": 11,
                      "long_window": 15, "pipeline": 16}
@@ -77,7 +78,8 @@ class AIJInfo(ctypes.Structure):
         ("row_patterns", ctypes.c_int32),
         ("long_overlap", ctypes.c_int32),
         ("mult_layout_bytes", ctypes.c_int64),
-        ("hw_queues", ctypes.c_int32), ("row_templates", ctypes.c_int32),
+        ("hw_queues", ctypes.c_int32), ("row_templates", ctypes.c_int32), ("value_codes", ctypes.c_int32),
+        ("reserved1", ctypes.c_int32),
     ]
 
 

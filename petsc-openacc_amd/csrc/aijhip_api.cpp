@@ -89,6 +89,9 @@ void free_plan(aijhip::Plan &P) {
     hipFree(P.d_ptab);
     hipFree(P.d_pval);
     hipFree(P.d_tblocks);
+    hipFree(P.d_vcode);
+    hipFree(P.d_svcode);
+    hipFree(P.d_vdict);
     if (P.side) hipStreamDestroy(P.side);
     if (P.ev_fork) hipEventDestroy(P.ev_fork);
     if (P.ev_join) hipEventDestroy(P.ev_join);
@@ -433,6 +436,20 @@ int plan_stream(aijhip_mat *A) {
                 return hipfail(e, "plan: column codes");
         }
     }
+    // value codes (Tuning::vcodes): a 16-bit index per entry into a
+    // dictionary of aa's distinct values, in aa's place, for operators of at
+    // most kVDictMax distinct values (GAMG's finest Pᵀ: ~370) read by the
+    // branch-free plain or packed gather-ordered blocks: 6 bytes per entry
+    // instead of 12, the same bits
+    // (automatic: the packed gather-ordered operators only — on the finest P's
+    // plain blocks the branch-free codes read ran 292 vs 274 us, r06/vc)
+    const bool want_vc = P.tune.vcodes > 0 || (P.tune.vcodes < 0 && A->setup_op && P.d_sidx != nullptr);
+    if (want_vc && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed && !P.d_pid &&
+        !P.d_code && (P.d_sslot == nullptr || P.d_sidx != nullptr) && P.n_wblocks == 0) {
+        bool ok = false;
+        if ((e = aijhip::build_value_codes(*A, P, &ok)) != hipSuccess) return hipfail(e, "plan: value codes");
+    }
+    P.tune.vcodes = (P.d_vcode || P.d_svcode) ? 1 : 0;
     if (!longs.empty()) {
         if ((e = dmalloc(&P.d_segs, segs.size(), &P.bytes)) != hipSuccess ||
             (e = dmalloc(&P.d_longs, longs.size(), &P.bytes)) != hipSuccess ||
@@ -829,6 +846,8 @@ int adopt_device_csr(int device, int32_t m, int32_t n, int64_t nz, int32_t *d_ai
         // overrides (0 off, 1 every operator).
         const char *gs = std::getenv("AIJHIP_SETUP_GSORT");
         A->requested_tune.gsort = gs ? std::atoi(gs) : -1;
+        const char *vc = std::getenv("AIJHIP_SETUP_VCODES");  // value codes: -1 (default) where they fit, 0 off
+        A->requested_tune.vcodes = vc ? std::atoi(vc) : -1;
         A->requested_tune.codes = 0;
         A->requested_tune.patterns = 0;
     }
@@ -883,6 +902,10 @@ int64_t mult_layout_bytes(const aijhip_mat &A) {
         return 8 * nz + rows + m + 4 * (int64_t)P.n_ptab + vec;
     if (P.d_code)  // coded entries 10 B, blocks launched from aj 12 B, the dictionaries
         return 10 * (nz - P.nz_wide) + 12 * P.nz_wide + rows + vec + 4 * P.n_cmeta;
+    if (P.d_sidx && P.d_svcode)  // packed columns and slots, value codes (6 B per entry), the dictionary
+        return 6 * nz + rows + vec + 4 * (int64_t)P.n_blocks + 8 * (int64_t)P.n_vdict;
+    if (P.d_vcode && !P.d_sslot)  // aj and value codes (6 B per entry), the dictionary
+        return 6 * nz + rows + vec + 8 * (int64_t)P.n_vdict;
     if (P.d_sidx)  // packed columns and slots (4 B per entry), sorted values, block bases
         return 12 * nz + rows + vec + 4 * (int64_t)(P.n_blocks - P.n_wblocks);
     if (P.d_sslot)  // sorted 32-bit columns + sorted values + 16-bit slots
@@ -992,6 +1015,10 @@ int aijhip_mat_set_option(aijhip_mat_t A, int option, int value) {
             if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "row_templates: -1 auto, 0 off, 1 on");
             t.templates = value;
             break;
+        case AIJHIP_OPT_VALUE_CODES:
+            if (value < -1 || value > 1) return fail(AIJHIP_ERR_ARG, "value_codes: -1 auto, 0 off, 1 on");
+            t.vcodes = value;
+            break;
         default: return fail(AIJHIP_ERR_ARG, "unknown option " + std::to_string(option));
     }
     DeviceGuard g(A->device);
@@ -1014,7 +1041,10 @@ int aijhip_mat_update_values(aijhip_mat_t A, const double *aa) {
     if (e == hipSuccess && A->plan.d_sslot)  // the gather-ordered copy of the values
         e = aijhip::build_gather_order(*A, A->plan, true);
     if (e != hipSuccess) return hipfail(e, "update values");
-    if (A->plan.d_pval) {  // row templates hold the old values: plan again (the new ones may not fit)
+    // templates / value codes hold the old values, and explicitly requested
+    // ones may fit the new values: plan again
+    if (A->plan.d_pval || A->plan.d_vcode || A->plan.d_svcode || A->requested_tune.vcodes > 0 ||
+        A->requested_tune.templates > 0) {
         rc = plan_build(A);
         if (rc) return rc;
     }
@@ -1190,6 +1220,8 @@ int aijhip_mat_get_info(aijhip_mat_t A, aijhip_info_t *info) {
     info->mult_layout_bytes = aijhip::mult_layout_bytes(*A);
     info->hw_queues = aijhip::hw_queues();
     info->row_templates = A->plan.d_pval != nullptr ? 1 : 0;
+    info->value_codes = (A->plan.d_vcode || A->plan.d_svcode) ? A->plan.n_vdict : 0;
+    info->reserved1 = 0;
     return AIJHIP_OK;
 }
 

@@ -111,6 +111,8 @@ struct Tuning {
                            // offset lists are few), 0 off, 1 on
     int templates = -1;    // with row patterns, the values in the table too (Plan::d_pval; a
                            // constant-coefficient stencil): -1 auto (tried first), 0 off, 1 on
+    int vcodes = -1;       // 16-bit value codes instead of aa (Plan::d_vcode): -1 auto (the set-up's own
+                           // operators, where <= kVDictMax distinct values), 0 off, 1 on
 };
 
 // Column codes (Tuning::codes): entry k of a row block starting at row0 is
@@ -125,6 +127,9 @@ constexpr int kCodeDictMax = 512;
 // lists per operand, their table (a start | length word per pattern, then
 // the offsets) at most kPatTableMax words, staged in LDS by every block.
 constexpr int kPatTableMax = 1024;
+// Value codes (Tuning::vcodes): at most kVDictMax distinct values, staged in
+// LDS by every block (4 KiB)
+constexpr int kVDictMax = 512;
 constexpr int kPatMax = 256;
 __host__ __device__ inline int code_index_bits(int nrows) {
     int rb = 0;
@@ -218,6 +223,12 @@ struct Plan {
     // reads neither aj nor aa
     double *d_pval = nullptr;
     BlockDesc *d_tblocks = nullptr;  // the blocks in the template launch's order, k0 = the block's index
+    // Tuning::vcodes: a 16-bit index per entry into d_vdict (n_vdict values),
+    // in aa's order (d_vcode) and, with the packed gather-ordered copy, in
+    // its order (d_svcode); nz + 2 each
+    uint16_t *d_vcode = nullptr, *d_svcode = nullptr;
+    double *d_vdict = nullptr;
+    int32_t n_vdict = 0;
     int64_t bytes = 0;  // device bytes held by the plan
     HostPipe *hpipe = nullptr;  // built on the first host-vector MatMult
 };
@@ -329,6 +340,11 @@ constexpr int kPackedMaxCap = 1 << (32 - kPackedColBits);  // slots < 4096: bloc
 // sets *ok; otherwise leaves them null. values: the lists are (offset, value)
 // pairs (the value bits hashed and verified too) and P.d_pval is filled.
 hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok, bool values);
+// Value codes: when aa holds at most kVDictMax distinct values (bit
+// patterns), fills P.d_vdict (sorted by bits) and P.d_vcode (and
+// P.d_svcode from P.d_saa when the packed gather-ordered copy exists) and
+// sets *ok; otherwise leaves them null.
+hipError_t build_value_codes(const aijhip_mat &A, Plan &P, bool *ok);
 hipError_t column_code_counts(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt);
 hipError_t column_code_write(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cmeta,
                              uint16_t *d_code);

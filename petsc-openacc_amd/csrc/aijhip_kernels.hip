@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "aijhip_internal.h"
@@ -249,7 +250,8 @@ __device__ __forceinline__ void stream_block(
     const int b, const BlockDesc *__restrict__ blk, int nblk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, const Op &op, double *dpart, const int *stop, const uint16_t *__restrict__ sslot,
-    const int32_t *__restrict__ sbase, double *prod, int32_t *cdict) {
+    const int32_t *__restrict__ sbase, double *prod, int32_t *cdict, const double *__restrict__ vdict, int nvd,
+    double *vlds) {
     constexpr bool NT = (NTMODE & 1) != 0;
     // bit 3: gather-ordered blocks (Plan::d_saj/d_saa): aj/aa hold each
     // block's entries sorted by column, sslot their positions in the block,
@@ -276,6 +278,13 @@ __device__ __forceinline__ void stream_block(
     // gather round trips per lane instead of one).
     constexpr bool BF = (NTMODE & 64) != 0;
     static_assert(!(BF && SORTED), "branch-free phase 1: plain, coded and 16-bit gather-ordered forms");
+    // bit 7: value codes (Plan::d_vcode, set-up operators with few distinct
+    // values, e.g. GAMG's finest P and P^T): `aa` holds a 16-bit index per
+    // entry (in the array's order, sorted or not) into the dictionary vdict
+    // (nvd <= kVDictMax values, staged in LDS): 6 bytes per entry read
+    // instead of 12 with the packed columns; the products are the same bits
+    constexpr bool VC = (NTMODE & 128) != 0;
+    static_assert(!VC || (BF && !CODES), "value codes: the branch-free plain or 16-bit gather-ordered forms");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     const BlockDesc d = blk[b];
@@ -301,6 +310,13 @@ __device__ __forceinline__ void stream_block(
             if (t + i * T < nd) dval[i] = sbase[dbase + t + i * T];
     }
 
+    constexpr int VPT = VC ? (kVDictMax + T - 1) / T : 1;  // dictionary values per lane
+    double vval[VPT];
+    if constexpr (VC) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) vval[i] = vdict[min(t + i * T, nvd - 1)];
+    }
+
     // Row extents and MatMultAdd seeds first: they overlap the stream below.
     int32_t rs[RPT], re[RPT], orow[RPT];
     double sum[RPT];
@@ -319,6 +335,7 @@ __device__ __forceinline__ void stream_block(
     f64x2 av[ITERS];
     i32x2 cv[ITERS];
     f64x2 xv[ITERS];
+    uint32_t vw[VC ? ITERS : 1] = {};  // value codes: a pair's two 16-bit indices
     if constexpr (BF) {
         uint32_t cw[CODES ? ITERS : 1];  // a pair's two codes
         const int64_t kl = (k1 - 1) & ~int64_t(1);  // the last pair start (>= kb when nk > 0)
@@ -329,9 +346,17 @@ __device__ __forceinline__ void stream_block(
                 if constexpr (CODES) cw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aj) + (k >> 1));
                 else cv[it] = ld_stream<NT>(reinterpret_cast<const i32x2 *>(aj + k));
             }
+            if constexpr (VC) {  // decoded just before the products (the gathers go out first)
 #pragma unroll
-            for (int it = 0; it < ITERS; ++it)
-                av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + min(kb + 2 * (int64_t)(t + it * T), kl)));
+                for (int it = 0; it < ITERS; ++it)
+                    vw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aa) +
+                                           (min(kb + 2 * (int64_t)(t + it * T), kl) >> 1));
+            } else {
+#pragma unroll
+                for (int it = 0; it < ITERS; ++it)
+                    av[it] = ld_stream<NT>(
+                        reinterpret_cast<const f64x2 *>(aa + min(kb + 2 * (int64_t)(t + it * T), kl)));
+            }
         }
         if constexpr (CODES) {
 #pragma unroll
@@ -436,6 +461,17 @@ __device__ __forceinline__ void stream_block(
             }
         }
     }
+    if constexpr (VC) {
+#pragma unroll
+        for (int i = 0; i < VPT; ++i)
+            if (t + i * T < nvd) vlds[t + i * T] = vval[i];
+        lds_barrier();
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            av[it].x = vlds[vw[it] & 0xffffu];
+            av[it].y = vlds[vw[it] >> 16];
+        }
+    }
     // products into LDS; only the stores are predicated
 #pragma unroll
     for (int it = 0; it < ITERS; ++it) {
@@ -508,11 +544,12 @@ __global__ __launch_bounds__(T) void k_spmv_stream(
     const BlockDesc *__restrict__ blk, int nblk, int exact,
     const int32_t *__restrict__ rai, const int32_t *__restrict__ ridx, const int32_t *__restrict__ aj,
     const double *__restrict__ aa, Op op, double *dpart, const int *stop, const uint16_t *__restrict__ sslot,
-    const int32_t *__restrict__ sbase) {
+    const int32_t *__restrict__ sbase, const double *__restrict__ vdict = nullptr, int nvd = 0) {
     __shared__ double prod[CAP];
     __shared__ int32_t cdict[(NTMODE & 32) ? kCodeDictMax : 1];
+    __shared__ double vlds[(NTMODE & 128) ? kVDictMax : 1];
     stream_block<T, CAP, RPT, CROW, NTMODE, Op>((int)blockIdx.x, blk, nblk, exact, rai, ridx, aj, aa, op, dpart, stop,
-                                                sslot, sbase, prod, cdict);
+                                                sslot, sbase, prod, cdict, vdict, nvd, vlds);
 }
 
 // Row patterns (Tuning::patterns; short-row operands whose rows follow a
@@ -1571,6 +1608,156 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok, bool value
     return done(hipSuccess);
 }
 
+// ---- value codes (Tuning::vcodes) ---------------------------------------
+// The distinct value bit patterns of aa into an open-addressing table of
+// kVTableSlots keys (key = bits ^ kVKeyXor; 0 = empty), read before any CAS
+// as k_pat_insert does; more than kVDictMax distinct raises `overflow`
+// (and every lane then leaves: a matrix of many values costs ~kVDictMax
+// inserts). A value whose key would be 0 raises it too.
+constexpr int kVTableSlots = 4096;
+constexpr unsigned long long kVKeyXor = 0x7ff4dead5a5a1234ull;
+__device__ __forceinline__ unsigned int vslot(unsigned long long key) {
+    return (unsigned int)(pat_mix(key) >> 20) & (kVTableSlots - 1);
+}
+__global__ __launch_bounds__(256) void k_vhash_insert(int64_t n, int64_t stride, const double *__restrict__ aa,
+                                                      unsigned long long *table, int *flags) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const unsigned long long key =
+        k < n ? ((unsigned long long)__double_as_longlong(aa[k * stride]) ^ kVKeyXor) : 0ull;
+    const unsigned long long kp = __shfl_up(key, 1, 64);
+    if (k >= n || ((threadIdx.x & 63) != 0 && kp == key)) return;
+    if (key == 0ull) {
+        atomicExch(flags, 1);
+        return;
+    }
+    if (__atomic_load_n(flags, __ATOMIC_RELAXED)) return;
+    unsigned int slot = vslot(key);
+    for (int probe = 0; probe < kVTableSlots; ++probe) {
+        const unsigned long long cur = __atomic_load_n(table + slot, __ATOMIC_RELAXED);
+        if (cur == key) return;
+        if (cur == 0ull) {
+            const unsigned long long prev = atomicCAS(table + slot, 0ull, key);
+            if (prev == key) return;
+            if (prev == 0ull) {
+                if (atomicAdd(flags + 1, 1) >= kVDictMax) atomicExch(flags, 1);
+                return;
+            }
+        }
+        if (__atomic_load_n(flags, __ATOMIC_RELAXED)) return;
+        slot = (slot + 1) & (kVTableSlots - 1);
+    }
+    atomicExch(flags, 1);
+}
+// Each entry's code: its key's slot, then the slot's dictionary index
+__global__ __launch_bounds__(256) void k_vcode_fill(int64_t n, const double *__restrict__ aa,
+                                                    const unsigned long long *__restrict__ table,
+                                                    const uint16_t *__restrict__ map, uint16_t *code, int *miss) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    const unsigned long long key = (unsigned long long)__double_as_longlong(aa[k]) ^ kVKeyXor;
+    unsigned int slot = vslot(key);
+    for (int probe = 0; probe < kVTableSlots; ++probe) {
+        if (table[slot] == key) {
+            code[k] = map[slot];
+            return;
+        }
+        slot = (slot + 1) & (kVTableSlots - 1);
+    }
+    atomicExch(miss, 1);
+}
+
+hipError_t build_value_codes(const aijhip_mat &A, Plan &P, bool *ok) {
+    *ok = false;
+    const int64_t nz = A.nz;
+    if (nz <= 0) return hipSuccess;
+    unsigned long long *d_table = nullptr;
+    int *d_flags = nullptr;
+    uint16_t *d_map = nullptr;
+    hipError_t e;
+    auto done = [&](hipError_t r) {
+        hipFree(d_table); hipFree(d_flags); hipFree(d_map);
+        return r;
+    };
+    auto drop = [&]() {
+        hipFree(P.d_vcode); hipFree(P.d_svcode); hipFree(P.d_vdict);
+        P.d_vcode = P.d_svcode = nullptr;
+        P.d_vdict = nullptr;
+        P.n_vdict = 0;
+    };
+    const unsigned g = (unsigned)((nz + 255) / 256);
+    if ((e = hipMalloc(&d_table, sizeof(unsigned long long) * kVTableSlots)) != hipSuccess ||
+        (e = hipMalloc(&d_flags, sizeof(int) * 3)) != hipSuccess ||
+        (e = hipMemset(d_table, 0, sizeof(unsigned long long) * kVTableSlots)) != hipSuccess ||
+        (e = hipMemset(d_flags, 0, sizeof(int) * 3)) != hipSuccess)
+        return done(e);
+    int flags[3] = {0, 0, 0};
+    // a strided sample of 4096 entries first: an operator of many values (a
+    // Galerkin product) is turned away by it after ~kVDictMax inserts (the
+    // full pass's lanes would all insert before the overflow is seen: 7.7 ms
+    // for a 1 M-entry operator, r06/vd)
+    if (nz > (int64_t)1 << 14) {
+        const int64_t ns = (int64_t)1 << 12, stride = nz / ns;
+        hipLaunchKernelGGL(k_vhash_insert, dim3((unsigned)(ns / 256)), dim3(256), 0, nullptr, ns, stride, A.d_aa,
+                           d_table, d_flags);
+        if ((e = hipGetLastError()) != hipSuccess ||
+            (e = hipMemcpy(flags, d_flags, sizeof(int) * 2, hipMemcpyDeviceToHost)) != hipSuccess)
+            return done(e);
+        if (flags[0]) return done(hipSuccess);
+    }
+    hipLaunchKernelGGL(k_vhash_insert, dim3(g), dim3(256), 0, nullptr, nz, (int64_t)1, A.d_aa, d_table, d_flags);
+    std::vector<unsigned long long> table(kVTableSlots);
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpy(flags, d_flags, sizeof(int) * 2, hipMemcpyDeviceToHost)) != hipSuccess)
+        return done(e);
+    if (flags[0] || flags[1] <= 0 || flags[1] > kVDictMax) return done(hipSuccess);
+    if ((e = hipMemcpy(table.data(), d_table, sizeof(unsigned long long) * kVTableSlots, hipMemcpyDeviceToHost)) !=
+        hipSuccess)
+        return done(e);
+    std::vector<unsigned long long> bits;  // the distinct values' bits, ascending: the same codes run to run
+    for (unsigned long long k : table)
+        if (k) bits.push_back(k ^ kVKeyXor);
+    std::sort(bits.begin(), bits.end());
+    std::vector<uint16_t> map(kVTableSlots, 0);
+    std::vector<double> dict(bits.size());
+    for (size_t i = 0; i < bits.size(); ++i) std::memcpy(&dict[i], &bits[i], sizeof(double));
+    for (int sl = 0; sl < kVTableSlots; ++sl)
+        if (table[sl])
+            map[sl] = (uint16_t)(std::lower_bound(bits.begin(), bits.end(), table[sl] ^ kVKeyXor) - bits.begin());
+    const size_t ncode = (size_t)nz + 2;
+    if ((e = hipMalloc(&d_map, sizeof(uint16_t) * kVTableSlots)) != hipSuccess ||
+        (e = hipMemcpy(d_map, map.data(), sizeof(uint16_t) * kVTableSlots, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMalloc(&P.d_vdict, sizeof(double) * dict.size())) != hipSuccess ||
+        (e = hipMemcpy(P.d_vdict, dict.data(), sizeof(double) * dict.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+        // the packed gather-ordered launches read the sorted copy's codes
+        // only; the plain blocks the original order's
+        (!P.d_saa && ((e = hipMalloc(&P.d_vcode, sizeof(uint16_t) * ncode)) != hipSuccess ||
+                      (e = hipMemset(P.d_vcode, 0, sizeof(uint16_t) * ncode)) != hipSuccess)) ||
+        (P.d_saa && ((e = hipMalloc(&P.d_svcode, sizeof(uint16_t) * ncode)) != hipSuccess ||
+                     (e = hipMemset(P.d_svcode, 0, sizeof(uint16_t) * ncode)) != hipSuccess))) {
+        drop();
+        return done(e);
+    }
+    if (!P.d_saa)
+        hipLaunchKernelGGL(k_vcode_fill, dim3(g), dim3(256), 0, nullptr, nz, A.d_aa, d_table, d_map, P.d_vcode,
+                           d_flags + 2);
+    else
+        hipLaunchKernelGGL(k_vcode_fill, dim3(g), dim3(256), 0, nullptr, nz, P.d_saa, d_table, d_map, P.d_svcode,
+                           d_flags + 2);
+    if ((e = hipGetLastError()) != hipSuccess ||
+        (e = hipMemcpy(flags + 2, d_flags + 2, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess) {
+        drop();
+        return done(e);
+    }
+    if (flags[2]) {  // (cannot happen: every value was inserted)
+        drop();
+        return done(hipSuccess);
+    }
+    P.n_vdict = (int32_t)dict.size();
+    P.bytes += (int64_t)(2 * ncode + 8 * dict.size());
+    *ok = true;
+    return done(hipSuccess);
+}
+
 template <bool WRITE>
 static hipError_t launch_block_codes(const aijhip_mat &A, const BlockDesc *d_blk, int32_t nblk, int32_t *d_cnt,
                                      int32_t *d_cmeta, uint16_t *d_code, int cap) {
@@ -1766,6 +1953,25 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
                            P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, L.ridx, A.d_aj, A.d_aa,         \
                            OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);             \
     return
+        // value codes (bit 128: 16-bit indices into the dictionary for aa)
+        if constexpr (kGeom6) {
+            if (P.d_svcode && !L.ridx) {
+#define AIJHIP_SV(ADD)                                                                                         \
+    if (nn > 0)                                                                                                \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 208, OpMult<ADD>>), dim3(nn), dim3(T), 0, s, nb, nn, \
+                           (int)P.tune.exact, L.rai, nullptr, reinterpret_cast<const int32_t *>(P.d_sidx),      \
+                           reinterpret_cast<const double *>(P.d_svcode), OpMult<ADD>{x, z, y, dpart != nullptr}, \
+                           dpart, stop, nullptr, P.d_sbase, P.d_vdict, P.n_vdict);                             \
+    if (P.n_wblocks > 0)                                                                                       \
+        hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, kWideMode, OpMult<ADD>>), dim3(P.n_wblocks), dim3(T), 0, \
+                           sw, P.d_wblocks, P.n_wblocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj, A.d_aa,     \
+                           OpMult<ADD>{x, z, y, false}, nullptr, stop, nullptr, nullptr);                      \
+    return
+                if (add) { AIJHIP_SV(true); }
+                AIJHIP_SV(false);
+#undef AIJHIP_SV
+            }
+        }
         // branch-free phase 1 (bit 64): skewed stand-in 331.9 vs 340.2 us
         // predicated (profiles/r04/s1/bf_skewed.jsonl)
         if (add && L.ridx) { AIJHIP_SS(true, true, 80); }
@@ -1805,6 +2011,21 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // at 87 VGPRs it holds 4-5 waves per SIMD against 8, and the hardware's
     // four resident workgroups per CU overlap each other's phases better,
     // profiles/r05/l/ab_pipe.jsonl; withdrawn, option 16 reserved)
+    // value codes on the plain blocks: the branch-free phase 1 (bit 64) with
+    // 16-bit indices into the dictionary for aa (bit 128)
+    if constexpr (kGeom6) {
+        if (P.d_vcode && !P.d_sslot && !L.ridx && P.n_wblocks == 0) {
+#define AIJHIP_PV(ADD)                                                                                     \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 192, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
+                       P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj,                  \
+                       reinterpret_cast<const double *>(P.d_vcode), OpMult<ADD>{x, z, y, dpart != nullptr}, \
+                       dpart, stop, nullptr, nullptr, P.d_vdict, P.n_vdict);                               \
+    return
+            if (add) { AIJHIP_PV(true); }
+            AIJHIP_PV(false);
+#undef AIJHIP_PV
+        }
+    }
     // non-temporal matrix loads: the plain full-row MatMult / MatMultAdd
     // (the compressed-row form, MPIAIJ's off-diagonal blocks, keeps plain loads)
     if (P.tune.nt == 1 && !L.ridx) {

@@ -19,6 +19,7 @@ step() {  # name, limit, command...
 for s in ${STEPS:-gamg_mpi parity bench}; do
   case $s in
     gamg_mpi) AIJHIP_GAMG_LOG=1 step gamg_mpi 600 python -u -m pytest tests/test_gamg_mpi_gpu.py -x -v -s --timeout 300 --timeout-method thread ;;
+    vcodes) step vcodes 400 python -u -m pytest tests/test_value_codes_gpu.py tests/test_gamg.py -x -v -m gpu --timeout 200 --timeout-method thread ;;
     patterns) step patterns 400 python -u -m pytest tests/test_row_patterns_gpu.py tests/test_ksp.py tests/test_solver_configs.py -x -v -m gpu --timeout 200 --timeout-method thread ;;
     parity) step parity 300 python -u -m pytest tests/test_gpu_parity.py -x -v -k "gather or geometry" --timeout 200 --timeout-method thread ;;
     bench) step bench 400 python -u bench.py --no-flan --no-host-vec --no-pmc --steps 20 --warmup 5 ;;
