@@ -438,12 +438,14 @@ int plan_stream(aijhip_mat *A) {
     }
     // value codes (Tuning::vcodes): a 16-bit index per entry into a
     // dictionary of aa's distinct values, in aa's place, for operators of at
-    // most kVDictMax distinct values (GAMG's finest Pᵀ: ~370) read by the
-    // branch-free plain or packed gather-ordered blocks: 6 bytes per entry
-    // instead of 12, the same bits
-    // (automatic: the packed gather-ordered operators only — on the finest P's
-    // plain blocks the branch-free codes read ran 292 vs 274 us, r06/vc)
-    const bool want_vc = P.tune.vcodes > 0 || (P.tune.vcodes < 0 && A->setup_op && P.d_sidx != nullptr);
+    // most kVDictMax distinct values (GAMG's finest P and Pᵀ: ~370) read by
+    // the plain or packed gather-ordered blocks: 6 bytes per entry instead of
+    // 12, the same bits
+    // (automatic for the set-up's operators; measured in the 300³ solve,
+    // profiles/r06/ve, vg: the finest Pᵀ 199 vs 275 us per launch, the finest
+    // P — plain blocks, predicated loads — 231 vs 277 us; solve 0.130 vs
+    // 0.1415 s; the many-valued operators are turned away by a sample)
+    const bool want_vc = P.tune.vcodes > 0 || (P.tune.vcodes < 0 && A->setup_op);
     if (want_vc && P.tune.geom == 6 && !blocks.empty() && longs.empty() && !A->compressed && !P.d_pid &&
         !P.d_code && (P.d_sslot == nullptr || P.d_sidx != nullptr) && P.n_wblocks == 0) {
         bool ok = false;

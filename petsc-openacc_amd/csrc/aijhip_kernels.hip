@@ -281,10 +281,12 @@ __device__ __forceinline__ void stream_block(
     // bit 7: value codes (Plan::d_vcode, set-up operators with few distinct
     // values, e.g. GAMG's finest P and P^T): `aa` holds a 16-bit index per
     // entry (in the array's order, sorted or not) into the dictionary vdict
-    // (nvd <= kVDictMax values, staged in LDS): 6 bytes per entry read
-    // instead of 12 with the packed columns; the products are the same bits
+    // (nvd <= kVDictMax values, staged in LDS; decoded after the gathers are
+    // issued): 6 bytes per entry read instead of 12 with aj or the packed
+    // columns; the products are the same bits
     constexpr bool VC = (NTMODE & 128) != 0;
-    static_assert(!VC || (BF && !CODES), "value codes: the branch-free plain or 16-bit gather-ordered forms");
+    static_assert(!VC || (!CODES && !SORTED && (BF || !S16)),
+                  "value codes: the plain (predicated or branch-free) or 16-bit gather-ordered forms");
     constexpr int ITERS = (CAP + 1 + 2 * T - 1) / (2 * T);
     constexpr int DPT = CODES ? (kCodeDictMax + T - 1) / T : 1;  // dictionary entries per lane
     const BlockDesc d = blk[b];
@@ -386,7 +388,8 @@ __device__ __forceinline__ void stream_block(
         for (int it = 0; it < ITERS; ++it) {
             const int64_t k = kb + 2 * (int64_t)(t + it * T);
             if (k < k1) {
-                av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
+                if constexpr (VC) vw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aa) + (k >> 1));
+                else av[it] = ld_stream<NT>(reinterpret_cast<const f64x2 *>(aa + k));
                 if constexpr (CODES)
                     cw[it] = ld_stream<NT>(reinterpret_cast<const uint32_t *>(aj) + (k >> 1));
                 else
@@ -2011,12 +2014,12 @@ static void stream_dispatch(const aijhip_mat &A, const Plan &P, const RowList &L
     // at 87 VGPRs it holds 4-5 waves per SIMD against 8, and the hardware's
     // four resident workgroups per CU overlap each other's phases better,
     // profiles/r05/l/ab_pipe.jsonl; withdrawn, option 16 reserved)
-    // value codes on the plain blocks: the branch-free phase 1 (bit 64) with
-    // 16-bit indices into the dictionary for aa (bit 128)
+    // value codes on the plain blocks: the predicated phase 1 with 16-bit
+    // indices into the dictionary for aa (bit 128)
     if constexpr (kGeom6) {
         if (P.d_vcode && !P.d_sslot && !L.ridx && P.n_wblocks == 0) {
 #define AIJHIP_PV(ADD)                                                                                     \
-    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 192, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
+    hipLaunchKernelGGL((k_spmv_stream<T, CAP, RPT, false, 128, OpMult<ADD>>), dim3(P.n_blocks), dim3(T), 0, s, \
                        P.d_blocks, P.n_blocks, (int)P.tune.exact, L.rai, nullptr, A.d_aj,                  \
                        reinterpret_cast<const double *>(P.d_vcode), OpMult<ADD>{x, z, y, dpart != nullptr}, \
                        dpart, stop, nullptr, nullptr, P.d_vdict, P.n_vdict);                               \
