@@ -166,6 +166,22 @@ __global__ void k_diag_inv(int m, const int32_t *__restrict__ ai, const int32_t 
     dinv[r] = 1.0 / d;
 }
 
+// PCSetUp_Jacobi on row templates: the diagonal of each template (its
+// first offset-0 entry, as k_diag_inv takes a row's), so that D^-1 of row i
+// is tdinv[pid[i]] — the same bits as k_diag_inv's dinv[i] (every row equals
+// its template bit for bit, verified at plan time).
+__global__ void k_tmpl_dinv(int npat, const int32_t *__restrict__ ptab, const double *__restrict__ pval,
+                            double *tdinv) {
+    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npat) return;
+    const int32_t pm = ptab[p], st = pm & 0xffff, n = pm >> 16;
+    double d = 0.0;
+    for (int32_t j = 0; j < n; ++j)
+        if (ptab[st + j] == 0) { d = pval[st + j]; break; }
+    if (d == 0.0) d = 1.0;
+    tdinv[p] = 1.0 / d;
+}
+
 #define GRID_STRIDE(i, n) \
     for (int64_t i = (int64_t)blockIdx.x * kVecThreads + threadIdx.x; i < (n); i += (int64_t)gridDim.x * kVecThreads)
 
@@ -214,17 +230,24 @@ __global__ __launch_bounds__(kVecThreads) void k_init(int64_t n, const double *_
 // anyway, before P is overwritten (same operation on every element, one
 // iteration later: X and P make one pass fewer per iteration).
 // x == nullptr: X += a P is applied in k_update instead (x_in_update).
-template <bool NT>
+// IZ (Jacobi on row templates): Z is not stored — z_i = D^-1_i r_i is formed
+// here from R and the template's D^-1 (tdinv[pid[i]]), the product k_update
+// formed for its dots: the same bits, one vector pass fewer per iteration.
+template <bool NT, bool IZ = false>
 __global__ __launch_bounds__(kVecThreads) void k_aypx(int64_t n, const double *__restrict__ z, double *p,
-                                                      double *x, const CGState *S) {
+                                                      double *x, const CGState *S,
+                                                      const double *__restrict__ r = nullptr,
+                                                      const uint8_t *__restrict__ pid = nullptr,
+                                                      const double *__restrict__ tdinv = nullptr) {
     if (S->done) return;
     const bool first = S->i == 0 || x == nullptr;
     const double bb = S->b, a = S->a;
     const bool p_first = S->i == 0;
     GRID_STRIDE(i, n) {
         const double pi = p[i];
+        const double zi = IZ ? tdinv[pid[i]] * r[i] : z[i];
         if (!first) vst<NT>(x + i, x[i] + a * pi);
-        vst<NT>(p + i, p_first ? z[i] : z[i] + bb * pi);
+        vst<NT>(p + i, p_first ? zi : zi + bb * pi);
     }
 }
 
@@ -275,11 +298,15 @@ __global__ __launch_bounds__(kVecThreads) void k_dots(int64_t n, const double *_
 // read before z[i] is written by the same lane); partials Z.Z, Z.R, R.R
 // (GAMG: R.R only, Z follows from the V-cycle). VecAXPY(X, a, P) is deferred
 // to the next K1 (or k_final_x).
-template <bool NT>
+// IZ (Jacobi on row templates): D^-1_i = tdinv[pid[i]] and Z is not
+// stored (k_aypx forms it again from R).
+template <bool NT, bool IZ = false>
 __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, double *wz,
                                                         const double *__restrict__ dinv, double *part,
                                                         const CGState *S, int pc,
-                                                        const double *__restrict__ p, double *x) {
+                                                        const double *__restrict__ p, double *x,
+                                                        const uint8_t *__restrict__ pid = nullptr,
+                                                        const double *__restrict__ tdinv = nullptr) {
     __shared__ double scratch[kVecThreads / 64];
     if (S->done) return;
     const double a = S->a, na = -S->a;
@@ -289,7 +316,11 @@ __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, do
         const double ri = r[i] + na * wz[i];  // VecAXPY(R, -a, W)
         vst<NT>(r + i, ri);
         rr += ri * ri;
-        if (pc != AIJHIP_PC_GAMG) {
+        if (IZ) {  // Jacobi on row templates
+            const double zi = tdinv[pid[i]] * ri;
+            zz += zi * zi;
+            zr += zi * ri;
+        } else if (pc != AIJHIP_PC_GAMG) {
             const double zi = pc == AIJHIP_PC_JACOBI ? dinv[i] * ri : ri;  // PCApply_Jacobi
             vst<NT>(wz + i, zi);
             zz += zi * zi;
@@ -298,7 +329,7 @@ __global__ __launch_bounds__(kVecThreads) void k_update(int64_t n, double *r, do
     }
     const int nb = gridDim.x;
     double v;
-    if (pc != AIJHIP_PC_GAMG) {
+    if (IZ || pc != AIJHIP_PC_GAMG) {
         v = bsum<kVecThreads>(zz, scratch); if (threadIdx.x == 0) part[0 * nb + blockIdx.x] = v;
         v = bsum<kVecThreads>(zr, scratch); if (threadIdx.x == 0) part[1 * nb + blockIdx.x] = v;
     }

@@ -144,6 +144,10 @@ struct aijhip_ksp {
     // 0.392 s against 0.376 s per 400 iterations (profiles/r01/x_in_update/).
     // (Those A/B forms were withdrawn in round 4.)
     double *d_dinv = nullptr, *d_r = nullptr, *d_z = nullptr, *d_p = nullptr, *d_part = nullptr;
+    // CG + Jacobi on row templates: D^-1 per template (d_tdinv, indexed by
+    // the operator's template ids) and Z not stored (k_aypx / k_update IZ)
+    double *d_tdinv = nullptr;
+    bool implicit_z = false;
     double *d_hist = nullptr;
     double *d_hb = nullptr, *d_hx = nullptr;  // aijhip_ksp_solve_host's device copies of b and x
     int32_t hist_cap = 0;
@@ -177,6 +181,9 @@ void mg_free(aijhip_ksp *K) {
 void ksp_free(aijhip_ksp *K) {
     mg_free(K);
     hipFree(K->d_dinv); hipFree(K->d_r); hipFree(K->d_z); hipFree(K->d_p); hipFree(K->d_part);
+    hipFree(K->d_tdinv);
+    K->d_tdinv = nullptr;
+    K->implicit_z = false;
     hipFree(K->d_hist); hipFree(K->d_state);
     hipFree(K->d_hb); hipFree(K->d_hx);
     K->d_hb = K->d_hx = nullptr;
@@ -483,6 +490,22 @@ int aijhip_ksp_set_up(aijhip_ksp_t K) {
             return khip(e, "PCSetUp_Jacobi");
         }
     }
+    // Jacobi on row templates: D^-1 per template, Z formed where it is read
+    // (AIJHIP_KSP_EXPLICIT_Z=1 keeps the stored Z, for A/B)
+    if (K->pc == AIJHIP_PC_JACOBI && m > 0 && A->plan.d_pid && A->plan.d_pval && !std::getenv("AIJHIP_KSP_EXPLICIT_Z")) {
+        const int np = A->plan.n_pat;
+        if ((e = hipMalloc(&K->d_tdinv, sizeof(double) * (size_t)np)) != hipSuccess) {
+            ksp_free(K);
+            return khip(e, "PCSetUp_Jacobi (templates)");
+        }
+        hipLaunchKernelGGL(k_tmpl_dinv, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, nullptr, np,
+                           A->plan.d_ptab, A->plan.d_pval, K->d_tdinv);
+        if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess) {
+            ksp_free(K);
+            return khip(e, "PCSetUp_Jacobi (templates)");
+        }
+        K->implicit_z = true;
+    }
     if (K->pc == AIJHIP_PC_GAMG) {
         const int rc = gamg_setup(K);
         if (rc) {
@@ -536,7 +559,11 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
     // no-op once `done` is set.
     auto iterate = [&](hipStream_t st) -> hipError_t {
         hipError_t ie = hipSuccess;
-        hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
+        if (K->implicit_z)
+            hipLaunchKernelGGL((k_aypx<true, true>), vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state, K->d_r,
+                               A->plan.d_pid, K->d_tdinv);
+        else
+            hipLaunchKernelGGL(k_aypx<true>, vg, vt, 0, st, m, K->d_z, K->d_p, x, K->d_state);
         if (K->fused) {
             ie = aijhip::launch_stream_dot(*A, K->d_p, K->d_z, K->d_part, &K->d_state->done, st);
             if (ie == hipSuccess)
@@ -546,8 +573,12 @@ int aijhip_ksp_solve(aijhip_ksp_t K, const double *b, double *x, void *stream) {
             hipLaunchKernelGGL(k_dot, vg, vt, 0, st, m, K->d_p, K->d_z, K->d_part, K->d_state);
             hipLaunchKernelGGL(k_reduce_dpi, dim3(1), rt, 0, st, K->d_part, nb, K->d_state);
         }
-        hipLaunchKernelGGL(k_update<true>, vg, vt, 0, st, m, K->d_r, K->d_z, K->d_dinv, K->d_part, K->d_state,
-                           K->pc, K->d_p, nullptr);
+        if (K->implicit_z)
+            hipLaunchKernelGGL((k_update<true, true>), vg, vt, 0, st, m, K->d_r, K->d_z, K->d_dinv, K->d_part,
+                               K->d_state, K->pc, K->d_p, nullptr, A->plan.d_pid, K->d_tdinv);
+        else
+            hipLaunchKernelGGL(k_update<true>, vg, vt, 0, st, m, K->d_r, K->d_z, K->d_dinv, K->d_part, K->d_state,
+                               K->pc, K->d_p, nullptr);
         const double *pz = K->d_part;
         int nbz = nb;
         if (gamg && ie == hipSuccess) {
@@ -642,7 +673,9 @@ int aijhip_ksp_get_iteration_bytes(aijhip_ksp_t K, int64_t *bytes, int64_t *spmv
     // CG: p = z + b p with x += a p (reads z, p, x; writes p, x), the SpMV
     // (p . w in its epilogue), the r update (Jacobi: reads r, w, D^-1,
     // writes r, z; GAMG: reads r, w, writes r; z from the V-cycle)
-    int64_t spmv = a0, vec = 40 * m + (K->pc == AIJHIP_PC_GAMG ? 24 * m : 40 * m);
+    // (Jacobi on row templates, Z not stored: p = z + b p reads r and a
+    // template id instead of z; the update reads r, w and an id, writes r)
+    int64_t spmv = a0, vec = K->implicit_z ? 41 * m + 25 * m : 40 * m + (K->pc == AIJHIP_PC_GAMG ? 24 * m : 40 * m);
     if (!K->fused) vec += 16 * m;  // p . w in its own pass
     int64_t lev0 = a0 + vec;
     if (K->pc == AIJHIP_PC_GAMG) {
