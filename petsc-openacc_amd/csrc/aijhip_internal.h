@@ -300,7 +300,8 @@ hipError_t launch_mult_exact(const aijhip_mat &A, const double *x, double *y, hi
 hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b, double *r, hipStream_t s,
                            bool nt, const int *stop = nullptr);
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
-                          double *dpart, hipStream_t s, bool nt, const int *stop = nullptr);
+                          double *dpart, hipStream_t s, bool nt, const int *stop = nullptr,
+                          const double *tdinv = nullptr);
 // Dispatch y = A x (or w = z + A x) through the handle's plan. stop: a device
 // flag (CG's `done`); STREAM row blocks return at once once it is set.
 hipError_t launch_mult(const aijhip_mat &A, const double *x, const double *z, double *y,

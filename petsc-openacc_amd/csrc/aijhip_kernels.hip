@@ -153,20 +153,24 @@ struct OpMgResid {
 // V-cycle post-smoothing, one Richardson step with Jacobi from the guess t
 // (SpMV + k_richardson): x_i = t_i + 1.0 (dinv_i (b_i + (-1) (A t)_i)); x
 // must not alias t. With dot, the finest level also yields CG's z.z and z.b
-// partials (z = x, b = CG's residual).
-template <bool NT>
+// partials (z = x, b = CG's residual). TD (row templates): D^-1 of row o is
+// tdinv[pid[o]], the template's (the same bits as dinv[o]).
+template <bool NT, bool TD = false>
 struct OpMgPost {
     static constexpr int kDots = 2;
     static constexpr bool kSeeded = false;
     const double *t, *b, *dinv;
     double *x;
     bool dot;
+    const uint8_t *pid = nullptr;
+    const double *tdinv = nullptr;
     struct Row {
         double to, bo, dio;
     };
+    __device__ double di(int o) const { return TD ? tdinv[pid[o]] : dinv[o]; }
     __device__ double gx(int32_t j) const { return t[j]; }
     __device__ double seed(int) const { return 0.0; }
-    __device__ Row row(int o) const { return {t[o], b[o], dinv[o]}; }
+    __device__ Row row(int o) const { return {t[o], b[o], di(o)}; }
     __device__ void put(int o, double v, double *d, const Row &w) const {
         const double xo = w.to + 1.0 * (w.dio * (w.bo + (-1.0) * v));
         if constexpr (NT) st_stream(x + o, xo);
@@ -178,7 +182,7 @@ struct OpMgPost {
     }
     __device__ void put(int o, double v, double *d) const {
         const double bo = b[o];
-        const double xo = t[o] + 1.0 * (dinv[o] * (bo + (-1.0) * v));
+        const double xo = t[o] + 1.0 * (di(o) * (bo + (-1.0) * v));
         if constexpr (NT) st_stream(x + o, xo);
         else x[o] = xo;
         if (dot) {
@@ -2145,7 +2149,10 @@ hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b
 }
 
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
-                          double *dpart, hipStream_t s, bool nt, const int *stop) {
+                          double *dpart, hipStream_t s, bool nt, const int *stop, const double *tdinv) {
+    if (tdinv && A.plan.d_pid && A.plan.d_pval)  // row templates: D^-1 per template
+        return launch_stream_op(A, OpMgPost<true, true>{t, b, dinv, x, dpart != nullptr, A.plan.d_pid, tdinv}, dpart,
+                                s, -1, stop);
     if (nt) return launch_stream_op(A, OpMgPost<true>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
     return launch_stream_op(A, OpMgPost<false>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
 }

@@ -83,6 +83,14 @@ __global__ __launch_bounds__(kVecThreads) void k_jacobi(int64_t n, const double 
     GRID_STRIDE(i, n) x[i] = dinv[i] * b[i];
 }
 
+// The same on row templates: D^-1 of row i is tdinv[pid[i]] (the same bits)
+__global__ __launch_bounds__(kVecThreads) void k_jacobi_t(int64_t n, const uint8_t *__restrict__ pid,
+                                                          const double *__restrict__ tdinv,
+                                                          const double *__restrict__ b, double *x, const int *stop) {
+    if (stop && *stop) return;
+    GRID_STRIDE(i, n) x[i] = tdinv[pid[i]] * b[i];
+}
+
 // MatResidual: r = b + (-1) r, where r holds A x on entry (VecAYPX(r,-1,b)).
 __global__ __launch_bounds__(kVecThreads) void k_resid(int64_t n, const double *__restrict__ b, double *r,
                                                        const int *stop) {
@@ -116,6 +124,7 @@ struct MGLevel {
     int32_t m = 0;
     int64_t nnz = 0;
     double *dinv = nullptr, *b = nullptr, *x = nullptr, *r = nullptr;
+    double *tdinv = nullptr;  // row templates (the finest level): D^-1 per template
 };
 
 }  // namespace
@@ -171,7 +180,7 @@ void mg_free(aijhip_ksp *K) {
     for (MGLevel &L : K->mg) {
         if (L.own_A) aijhip_mat_destroy(L.A);
         aijhip_mat_destroy(L.P);
-        hipFree(L.dinv); hipFree(L.b); hipFree(L.x); hipFree(L.r);
+        hipFree(L.dinv); hipFree(L.b); hipFree(L.x); hipFree(L.r); hipFree(L.tdinv);
     }
     K->mg.clear();
     hipFree(K->d_mgpart);
@@ -307,6 +316,16 @@ int gamg_setup(aijhip_ksp *K) {
         if (L.m > 0)
             hipLaunchKernelGGL(k_diag_inv, dim3((unsigned)((L.m + 255) / 256)), dim3(256), 0, nullptr, L.m,
                                L.A->d_ai, L.A->d_aj, L.A->d_aa, L.dinv);
+        // the finest level on row templates: D^-1 per template for its fused
+        // smoothing (pre-smoothing pass and post-smoothing epilogue read a
+        // template id instead of D^-1; AIJHIP_KSP_EXPLICIT_Z=1 keeps dinv)
+        if (l == 0 && L.m > 0 && L.A->plan.d_pid && L.A->plan.d_pval && !std::getenv("AIJHIP_KSP_EXPLICIT_Z")) {
+            const int np = L.A->plan.n_pat;
+            if ((e = hipMalloc(&L.tdinv, sizeof(double) * (size_t)np)) != hipSuccess)
+                return khip(e, "GAMG: template D^-1");
+            hipLaunchKernelGGL(k_tmpl_dinv, dim3((unsigned)((np + 255) / 256)), dim3(256), 0, nullptr, np,
+                               L.A->plan.d_ptab, L.A->plan.d_pval, L.tdinv);
+        }
     }
     // every restriction (P^T) exists before the first solve (the device
     // levels attached theirs during the set-up)
@@ -347,7 +366,10 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
         }
         if (L.fused) {
             // smoothd as a vector pass, then r = b - A x in the SpMV epilogue
-            hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
+            if (L.tdinv)
+                hipLaunchKernelGGL(k_jacobi_t, g, t, 0, s, (int64_t)L.m, L.A->plan.d_pid, L.tdinv, B(l), X(l), stop);
+            else
+                hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);
             if ((e = aijhip::launch_mg_resid(*L.A, X(l), B(l), L.r, s, true, stop)) != hipSuccess) return e;
         } else {
             hipLaunchKernelGGL(k_jacobi, g, t, 0, s, (int64_t)L.m, L.dinv, B(l), X(l), stop);  // smoothd
@@ -364,7 +386,7 @@ hipError_t vcycle(aijhip_ksp *K, const double *b0, double *x0, hipStream_t s, do
             // MatInterpolateAdd into the scratch: t = x + P x_c, then smoothu
             if ((e = aijhip::launch_mult(*L.P, X(l + 1), X(l), L.r, true, s, stop)) != hipSuccess) return e;
             double *dp = (l == 0 && dots) ? dots : nullptr;
-            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s, true, stop)) != hipSuccess)
+            if ((e = aijhip::launch_mg_post(*L.A, L.r, B(l), L.dinv, X(l), dp, s, true, stop, L.tdinv)) != hipSuccess)
                 return e;
             if (dp && dots_done) *dots_done = true;
         } else {
@@ -690,7 +712,9 @@ int aijhip_ksp_get_iteration_bytes(aijhip_ksp_t K, int64_t *bytes, int64_t *spmv
                 const int64_t la = aijhip::mult_layout_bytes(*L.A);
                 const int64_t lp = aijhip::mult_layout_bytes(*L.P);
                 const int64_t lt = L.P->transpose ? aijhip::mult_layout_bytes(*L.P->transpose) : lp;
-                if (L.fused)  // D^-1 b pass; r = b - A x (+ b); P^T r; t = x + P x_c (+ x); x = t + D^-1 (b - A t) (+ b, D^-1)
+                if (L.fused && L.tdinv)  // the same with a template id for D^-1 (two passes)
+                    sp = la + lt + lp + la, v = 17 * ml + 8 * ml + 8 * ml + 9 * ml;
+                else if (L.fused)  // D^-1 b pass; r = b - A x (+ b); P^T r; t = x + P x_c (+ x); x = t + D^-1 (b - A t) (+ b, D^-1)
                     sp = la + lt + lp + la, v = 24 * ml + 8 * ml + 8 * ml + 16 * ml;
                 else  // the same with the residual and Richardson passes separate
                     sp = la + lt + lp + la, v = 24 * ml + 24 * ml + 8 * ml + 40 * ml;
