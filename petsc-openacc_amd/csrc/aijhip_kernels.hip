@@ -779,16 +779,19 @@ __global__ __launch_bounds__(T) void k_spmv_template(const BlockDesc *__restrict
 // not summed). The sum is s = seed, s += value * x in storage order.
 constexpr int kTmplFast = 8;
 typedef int32_t i32x4 __attribute__((ext_vector_type(4)));
-template <class Op>
+// F: the gather slots a row takes (7 where every template has at most 7
+// entries — the 7-point operand: one load and two registers per stage fewer
+// — else kTmplFast)
+template <class Op, int F>
 struct TmplStage {
     int r, n, p;
     double s;
     typename Op::Row rw;
-    double xv[kTmplFast];
+    double xv[F];
 };
-template <class Op>
+template <class Op, int F>
 __device__ __forceinline__ void tmpl_issue(const Op &op, const BlockDesc &d, int pid, int npat, const int32_t *tab,
-                                           const int32_t *off8, TmplStage<Op> &g) {
+                                           const int32_t *off8, TmplStage<Op, F> &g) {
     g.r = d.row0 + min((int)threadIdx.x, d.nrows - 1);
     g.p = min(pid, npat - 1);
     const i32x4 o0 = *reinterpret_cast<const i32x4 *>(off8 + g.p * kTmplFast);
@@ -803,10 +806,10 @@ __device__ __forceinline__ void tmpl_issue(const Op &op, const BlockDesc &d, int
     g.xv[4] = op.gx(g.r + o1.x);
     g.xv[5] = op.gx(g.r + o1.y);
     g.xv[6] = op.gx(g.r + o1.z);
-    g.xv[7] = op.gx(g.r + o1.w);
+    if constexpr (F > 7) g.xv[7] = op.gx(g.r + o1.w);
 }
-template <int T, class Op>
-__device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, int live, const TmplStage<Op> &g,
+template <int T, class Op, int F>
+__device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, int live, const TmplStage<Op, F> &g,
                                             const double *val8, double *red, double *dpart, int nblk) {
     const int t = threadIdx.x;
     const bool own = t < live;
@@ -815,7 +818,7 @@ __device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, in
     const double vv[kTmplFast] = {v0.x, v0.y, v1.x, v1.y, v2.x, v2.y, v3.x, v3.y};
     double s = g.s;
 #pragma unroll
-    for (int j = 0; j < kTmplFast; ++j)
+    for (int j = 0; j < F; ++j)
         if (j < g.n) s += vv[j] * g.xv[j];
     double dd[Op::kDots > 0 ? Op::kDots : 1] = {};
     if (own) op.put(g.r, s, dd, g.rw);
@@ -827,7 +830,7 @@ __device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, in
         }
     }
 }
-template <int T, class Op>
+template <int T, int F, class Op>
 __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__restrict__ blk, int nblk,
                                                           const uint8_t *__restrict__ pid,
                                                           const int32_t *__restrict__ ptab,
@@ -864,7 +867,7 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
     int pa = pid[lane_row(d0)];
     int pb = pid[lane_row(d1)];
     __syncthreads();
-    TmplStage<Op> A, B;
+    TmplStage<Op, F> A, B;
     tmpl_issue(op, d0, pa, npat, tab, off8, A);
     for (int b = first; b <= lastb; b += 2 * step) {
         // block b (A); b + step's gathers into B; b + 2 step's ids
@@ -872,14 +875,14 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
         tmpl_issue(op, d1, pb, npat, tab, off8, B);
         const BlockDesc d3 = blk[min(b + 3 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's sums wait
-        tmpl_finish<T>(op, d0, d0.nrows, A, val8, red, dpart, nblk);
+        tmpl_finish<T, Op, F>(op, d0, d0.nrows, A, val8, red, dpart, nblk);
         // block b + step (B; past lastb: lastb again, loaded and summed but
         // not stored); b + 2 step's gathers into A; b + 3 step's ids
         pb = pid[lane_row(d3)];
         tmpl_issue(op, d2, pa, npat, tab, off8, A);
         const BlockDesc d4 = blk[min(b + 4 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);
-        tmpl_finish<T>(op, d1, b + step <= lastb ? d1.nrows : 0, B, val8, red, dpart, nblk);
+        tmpl_finish<T, Op, F>(op, d1, b + step <= lastb ? d1.nrows : 0, B, val8, red, dpart, nblk);
         d0 = d2;
         d1 = d3;
         d2 = d4;
@@ -903,6 +906,24 @@ inline int template_grid(const aijhip_mat &A, int32_t nblk) {
     if (g >= 8) g &= ~7;
     return g;
 }
+// (forcing 8 waves per SIMD, __launch_bounds__(512, 8), spills a few words
+// in most epilogues and ran slower: CG + Jacobi 1637-1644 vs 1832-1839 it/s,
+// solve 0.137 vs 0.125 s, profiles/r06/w8)
+template <int TP, int F, class Op>
+static void launch_template_pipe(const aijhip_mat &A, const Op &op, double *dpart, hipStream_t s, const int *stop) {
+    const Plan &P = A.plan;
+    static const int per_cu = [] {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_spmv_template_pipe<TP, F, Op>, TP, 0) != hipSuccess ||
+            n < 1)
+            n = 1;
+        return n;
+    }();
+    int g = (int)std::min<int64_t>(P.n_blocks, (int64_t)A.n_cu * per_cu);
+    if (g >= 8) g &= ~7;
+    hipLaunchKernelGGL((k_spmv_template_pipe<TP, F, Op>), dim3(g), dim3(TP), 0, s, P.d_tblocks, P.n_blocks, P.d_pid,
+                       P.d_ptab, P.d_pval, P.n_ptab, P.n_pat, op, dpart, stop);
+}
 template <class Op>
 static void launch_template(const aijhip_mat &A, const Op &op, double *dpart, hipStream_t s, const int *stop) {
     const Plan &P = A.plan;
@@ -911,17 +932,8 @@ static void launch_template(const aijhip_mat &A, const Op &op, double *dpart, hi
         // persistent: as many workgroups as fit on the device at once (the
         // kernel's registers decide), a multiple of 8 for the XCD chunks
         constexpr int TP = kStreamGeoms[6].threads;
-        static const int per_cu = [] {
-            int n = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_spmv_template_pipe<TP, Op>, TP, 0) != hipSuccess ||
-                n < 1)
-                n = 1;
-            return n;
-        }();
-        int g = (int)std::min<int64_t>(P.n_blocks, (int64_t)A.n_cu * per_cu);
-        if (g >= 8) g &= ~7;
-        hipLaunchKernelGGL((k_spmv_template_pipe<TP, Op>), dim3(g), dim3(TP), 0, s, P.d_tblocks, P.n_blocks, P.d_pid,
-                           P.d_ptab, P.d_pval, P.n_ptab, P.n_pat, op, dpart, stop);
+        if (P.pat_maxlen <= 7) launch_template_pipe<TP, 7>(A, op, dpart, s, stop);
+        else launch_template_pipe<TP, kTmplFast>(A, op, dpart, s, stop);
         return;
     }
     hipLaunchKernelGGL((k_spmv_template<kTmplThreads, kTmplRows, Op>), dim3(template_grid(A, P.n_blocks)),
