@@ -898,6 +898,13 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
 // below, plain MatMult in tools/ab_opts.py (profiles/r06/o, p): 2 rows per
 // lane 134 vs 142 us (1 row) and 160 (4 rows); 32 waves per CU 134 vs 142
 // (16); the XCD chunks 134 vs 143 (g % 8 interleaved); row patterns 342.
+// (A block's x[row0 - halo, row0 + nrows + halo) staged in LDS by coalesced
+// loads, the offsets within the halo read from it and only the neighbour
+// planes gathered — 3 window loads + 2 gathers a row for 7 gathers — was
+// bit-identical but slower for the plain MatMult, 169.4 / 170.0 vs 139.1 /
+// 141.1 us, and equal inside CG, 1841 / 1832 vs 1836 / 1828 it/s, in
+// alternating processes, profiles/r06/wa: the per-entry gathers are not what
+// bounds this kernel; withdrawn.)
 constexpr int kTmplRows = 2;
 constexpr int kTmplThreads = kStreamGeoms[6].threads / kTmplRows;
 constexpr int kTmplWavesPerCu = 32;
