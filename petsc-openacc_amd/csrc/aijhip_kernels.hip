@@ -104,6 +104,7 @@ template <bool ADD>
 struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     static constexpr int kDots = 1;
     static constexpr bool kSeeded = ADD;
+    static constexpr bool kTmplDiag = false;
     const double *x, *z;
     double *y;
     bool dot;
@@ -123,6 +124,20 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     }
 };
 
+// OpMult with the dot decided at compile time, for the pipelined template
+// launch: OpMult::row's load behind the runtime `dot` is a load behind a
+// branch, and the loop's waits then count for the path without it (one
+// load more waited for on the other)
+template <bool ADD, bool DOT>
+struct OpMultT : OpMult<ADD> {
+    using Row = typename OpMult<ADD>::Row;
+    __device__ Row row(int o) const { return {DOT ? this->x[o] : 0.0}; }
+    __device__ void put(int o, double v, double *d, const Row &w) const {
+        st_stream(this->y + o, v);
+        if (DOT) d[0] += w.xo * v;
+    }
+};
+
 // MatResidual with the SpMV: r_i = b_i + (-1) (A x)_i (SpMV + k_resid, same
 // roundings) — the second half of the pre-smoothing, after x = D^-1 b was
 // written by a vector pass.
@@ -130,6 +145,7 @@ template <bool NT>
 struct OpMgResid {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
+    static constexpr bool kTmplDiag = false;
     const double *x, *b;
     double *r;
     struct Row {
@@ -159,6 +175,7 @@ template <bool NT, bool TD = false>
 struct OpMgPost {
     static constexpr int kDots = 2;
     static constexpr bool kSeeded = false;
+    static constexpr bool kTmplDiag = TD;  // the pipelined template launch stages tdinv in LDS (row_td)
     const double *t, *b, *dinv;
     double *x;
     bool dot;
@@ -171,6 +188,7 @@ struct OpMgPost {
     __device__ double gx(int32_t j) const { return t[j]; }
     __device__ double seed(int) const { return 0.0; }
     __device__ Row row(int o) const { return {t[o], b[o], di(o)}; }
+    __device__ Row row_td(int o, double td) const { return {t[o], b[o], td}; }  // td = tdinv[pid[o]]
     __device__ void put(int o, double v, double *d, const Row &w) const {
         const double xo = w.to + 1.0 * (w.dio * (w.bo + (-1.0) * v));
         if constexpr (NT) st_stream(x + o, xo);
@@ -196,6 +214,7 @@ struct OpMgPost {
 struct OpDinvMult {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
+    static constexpr bool kTmplDiag = false;
     const double *x, *dinv;
     double *y;
     struct Row {
@@ -791,14 +810,17 @@ struct TmplStage {
 };
 template <class Op, int F>
 __device__ __forceinline__ void tmpl_issue(const Op &op, const BlockDesc &d, int pid, int npat, const int32_t *tab,
-                                           const int32_t *off8, TmplStage<Op, F> &g) {
+                                           const int32_t *off8, const double *tdl, TmplStage<Op, F> &g) {
     g.r = d.row0 + min((int)threadIdx.x, d.nrows - 1);
     g.p = min(pid, npat - 1);
     const i32x4 o0 = *reinterpret_cast<const i32x4 *>(off8 + g.p * kTmplFast);
     const i32x4 o1 = *reinterpret_cast<const i32x4 *>(off8 + g.p * kTmplFast + 4);
     g.n = tab[g.p] >> 16;
     g.s = op.seed(g.r);
-    g.rw = op.row(g.r);
+    // D^-1 per template from LDS (Op::kTmplDiag): tdinv[pid[r]] from global
+    // memory would wait for the id's load, and so for every load before it
+    if constexpr (Op::kTmplDiag) g.rw = op.row_td(g.r, tdl[g.p]);
+    else g.rw = op.row(g.r);
     g.xv[0] = op.gx(g.r + o0.x);
     g.xv[1] = op.gx(g.r + o0.y);
     g.xv[2] = op.gx(g.r + o0.z);
@@ -840,6 +862,7 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
     __shared__ int32_t tab[kPatMax];
     __shared__ __attribute__((aligned(16))) int32_t off8[kPatMax * kTmplFast];
     __shared__ __attribute__((aligned(16))) double val8[kPatMax * kTmplFast];
+    __shared__ double tdl[Op::kTmplDiag ? kPatMax : 1];
     __shared__ double red[T / 64];
     if ((stop ? *stop : 0) != 0) return;
     const int t = threadIdx.x, G = (int)gridDim.x, g = (int)blockIdx.x;
@@ -853,6 +876,9 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
     if (first >= last) return;
     const int lastb = first + (last - 1 - first) / step * step;  // this workgroup's last block
     if (t < npat) tab[t] = ptab[t];
+    if constexpr (Op::kTmplDiag) {
+        if (t < npat) tdl[t] = op.tdinv[t];
+    }
 #pragma unroll
     for (int i = 0; i < FPT; ++i) {
         const int e = t + i * T, pp = e / kTmplFast, j = e % kTmplFast;
@@ -868,18 +894,18 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
     int pb = pid[lane_row(d1)];
     __syncthreads();
     TmplStage<Op, F> A, B;
-    tmpl_issue(op, d0, pa, npat, tab, off8, A);
+    tmpl_issue(op, d0, pa, npat, tab, off8, tdl, A);
     for (int b = first; b <= lastb; b += 2 * step) {
         // block b (A); b + step's gathers into B; b + 2 step's ids
         pa = pid[lane_row(d2)];
-        tmpl_issue(op, d1, pb, npat, tab, off8, B);
+        tmpl_issue(op, d1, pb, npat, tab, off8, tdl, B);
         const BlockDesc d3 = blk[min(b + 3 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's sums wait
         tmpl_finish<T, Op, F>(op, d0, d0.nrows, A, val8, red, dpart, nblk);
         // block b + step (B; past lastb: lastb again, loaded and summed but
         // not stored); b + 2 step's gathers into A; b + 3 step's ids
         pb = pid[lane_row(d3)];
-        tmpl_issue(op, d2, pa, npat, tab, off8, A);
+        tmpl_issue(op, d2, pa, npat, tab, off8, tdl, A);
         const BlockDesc d4 = blk[min(b + 4 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);
         tmpl_finish<T, Op, F>(op, d1, b + step <= lastb ? d1.nrows : 0, B, val8, red, dpart, nblk);
@@ -946,6 +972,13 @@ static void launch_template(const aijhip_mat &A, const Op &op, double *dpart, hi
     hipLaunchKernelGGL((k_spmv_template<kTmplThreads, kTmplRows, Op>), dim3(template_grid(A, P.n_blocks)),
                        dim3(kTmplThreads), 0, s, P.d_blocks, P.n_blocks, 1, P.d_pid, P.d_ptab, P.d_pval, P.n_ptab,
                        P.n_pat, op, dpart, stop);
+}
+// MatMult / MatMultAdd: the dot as a compile-time choice (OpMultT)
+template <bool ADD>
+static void launch_template(const aijhip_mat &A, const OpMult<ADD> &op, double *dpart, hipStream_t s,
+                            const int *stop) {
+    if (op.dot) launch_template(A, OpMultT<ADD, true>{op}, dpart, s, stop);
+    else launch_template(A, OpMultT<ADD, false>{op}, dpart, s, stop);
 }
 
 // Segments of long rows: tree-reduced partial sums. (Round 5: lane t taking
