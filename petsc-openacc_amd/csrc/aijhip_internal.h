@@ -218,6 +218,7 @@ struct Plan {
     int32_t n_ptab = 0, n_pat = 0;
     int32_t pat_dmax = 0;    // largest |column - row| offset in the table (the stencil's plane distance)
     int32_t pat_maxlen = 0;  // longest pattern (entries)
+    bool tmpl_diag = false;  // every pattern has the offset 0 (the diagonal)
     // Tuning::templates: the values of each pattern's entries, indexed like
     // the offsets in d_ptab (n_ptab doubles; the first n_pat unused): MatMult
     // reads neither aj nor aa

@@ -105,6 +105,7 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
     static constexpr int kDots = 1;
     static constexpr bool kSeeded = ADD;
     static constexpr bool kTmplDiag = false;
+    static constexpr bool kXoFromSlot = false;
     const double *x, *z;
     double *y;
     bool dot;
@@ -128,10 +129,13 @@ struct OpMult {  // y = A x (+ z); optional x . y partials (CG's p . w)
 // launch: OpMult::row's load behind the runtime `dot` is a load behind a
 // branch, and the loop's waits then count for the path without it (one
 // load more waited for on the other)
-template <bool ADD, bool DOT>
+// (XS: the dot's x[o] taken from the row's gathered diagonal, every template
+// having one — Plan::tmpl_diag — so the stage carries no load of its own)
+template <bool ADD, bool DOT, bool XS = false>
 struct OpMultT : OpMult<ADD> {
     using Row = typename OpMult<ADD>::Row;
-    __device__ Row row(int o) const { return {DOT ? this->x[o] : 0.0}; }
+    static constexpr bool kXoFromSlot = DOT && XS;
+    __device__ Row row(int o) const { return {DOT && !XS ? this->x[o] : 0.0}; }
     __device__ void put(int o, double v, double *d, const Row &w) const {
         st_stream(this->y + o, v);
         if (DOT) d[0] += w.xo * v;
@@ -146,6 +150,7 @@ struct OpMgResid {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
     static constexpr bool kTmplDiag = false;
+    static constexpr bool kXoFromSlot = false;
     const double *x, *b;
     double *r;
     struct Row {
@@ -176,6 +181,7 @@ struct OpMgPost {
     static constexpr int kDots = 2;
     static constexpr bool kSeeded = false;
     static constexpr bool kTmplDiag = TD;  // the pipelined template launch stages tdinv in LDS (row_td)
+    static constexpr bool kXoFromSlot = false;
     const double *t, *b, *dinv;
     double *x;
     bool dot;
@@ -215,6 +221,7 @@ struct OpDinvMult {
     static constexpr int kDots = 0;
     static constexpr bool kSeeded = false;
     static constexpr bool kTmplDiag = false;
+    static constexpr bool kXoFromSlot = false;
     const double *x, *dinv;
     double *y;
     struct Row {
@@ -832,7 +839,8 @@ __device__ __forceinline__ void tmpl_issue(const Op &op, const BlockDesc &d, int
 }
 template <int T, class Op, int F>
 __device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, int live, const TmplStage<Op, F> &g,
-                                            const double *val8, double *red, double *dpart, int nblk) {
+                                            const double *val8, const int32_t *dsl, double *red, double *dpart,
+                                            int nblk) {
     const int t = threadIdx.x;
     const bool own = t < live;
     const f64x2 *v8 = reinterpret_cast<const f64x2 *>(val8 + g.p * kTmplFast);
@@ -843,7 +851,15 @@ __device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, in
     for (int j = 0; j < F; ++j)
         if (j < g.n) s += vv[j] * g.xv[j];
     double dd[Op::kDots > 0 ? Op::kDots : 1] = {};
-    if (own) op.put(g.r, s, dd, g.rw);
+    typename Op::Row rw = g.rw;
+    if constexpr (Op::kXoFromSlot) {  // x[r] = the gathered x of the template's diagonal slot
+        const int ds = dsl[g.p];
+        double xo = g.xv[0];
+#pragma unroll
+        for (int j = 1; j < F; ++j) xo = ds == j ? g.xv[j] : xo;
+        rw.xo = xo;
+    }
+    if (own) op.put(g.r, s, dd, rw);
     if (Op::kDots > 0 && dpart) {
 #pragma unroll
         for (int q = 0; q < (Op::kDots > 0 ? Op::kDots : 1); ++q) {
@@ -863,6 +879,7 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
     __shared__ __attribute__((aligned(16))) int32_t off8[kPatMax * kTmplFast];
     __shared__ __attribute__((aligned(16))) double val8[kPatMax * kTmplFast];
     __shared__ double tdl[Op::kTmplDiag ? kPatMax : 1];
+    __shared__ int32_t dsl[Op::kXoFromSlot ? kPatMax : 1];  // each template's diagonal slot
     __shared__ double red[T / 64];
     if ((stop ? *stop : 0) != 0) return;
     const int t = threadIdx.x, G = (int)gridDim.x, g = (int)blockIdx.x;
@@ -878,6 +895,15 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
     if (t < npat) tab[t] = ptab[t];
     if constexpr (Op::kTmplDiag) {
         if (t < npat) tdl[t] = op.tdinv[t];
+    }
+    if constexpr (Op::kXoFromSlot) {
+        if (t < npat) {
+            const int32_t pm = ptab[t], st = pm & 0xffff, n = pm >> 16;
+            int j0 = 0;
+            for (int j = n - 1; j >= 0; --j)
+                if (ptab[st + j] == 0) j0 = j;
+            dsl[t] = j0;
+        }
     }
 #pragma unroll
     for (int i = 0; i < FPT; ++i) {
@@ -901,14 +927,14 @@ __global__ __launch_bounds__(T) void k_spmv_template_pipe(const BlockDesc *__res
         tmpl_issue(op, d1, pb, npat, tab, off8, tdl, B);
         const BlockDesc d3 = blk[min(b + 3 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);  // B's loads issue before A's sums wait
-        tmpl_finish<T, Op, F>(op, d0, d0.nrows, A, val8, red, dpart, nblk);
+        tmpl_finish<T, Op, F>(op, d0, d0.nrows, A, val8, dsl, red, dpart, nblk);
         // block b + step (B; past lastb: lastb again, loaded and summed but
         // not stored); b + 2 step's gathers into A; b + 3 step's ids
         pb = pid[lane_row(d3)];
         tmpl_issue(op, d2, pa, npat, tab, off8, tdl, A);
         const BlockDesc d4 = blk[min(b + 4 * step, lastb)];
         __builtin_amdgcn_sched_barrier(0);
-        tmpl_finish<T, Op, F>(op, d1, b + step <= lastb ? d1.nrows : 0, B, val8, red, dpart, nblk);
+        tmpl_finish<T, Op, F>(op, d1, b + step <= lastb ? d1.nrows : 0, B, val8, dsl, red, dpart, nblk);
         d0 = d2;
         d1 = d3;
         d2 = d4;
@@ -977,7 +1003,9 @@ static void launch_template(const aijhip_mat &A, const Op &op, double *dpart, hi
 template <bool ADD>
 static void launch_template(const aijhip_mat &A, const OpMult<ADD> &op, double *dpart, hipStream_t s,
                             const int *stop) {
-    if (op.dot) launch_template(A, OpMultT<ADD, true>{op}, dpart, s, stop);
+    const Plan &P = A.plan;
+    if (op.dot && P.tmpl_diag && P.pat_maxlen <= kTmplFast) launch_template(A, OpMultT<ADD, true, true>{op}, dpart, s, stop);
+    else if (op.dot) launch_template(A, OpMultT<ADD, true>{op}, dpart, s, stop);
     else launch_template(A, OpMultT<ADD, false>{op}, dpart, s, stop);
 }
 
@@ -1633,6 +1661,12 @@ hipError_t build_row_patterns(const aijhip_mat &A, Plan &P, bool *ok, bool value
     }
     P.pat_dmax = dmax;
     P.pat_maxlen = *std::max_element(len.begin(), len.end());
+    P.tmpl_diag = true;  // every pattern has the offset 0
+    for (int p = 0; p < npat; ++p) {
+        bool has = false;
+        for (int j = 0; j < len[p]; ++j) has = has || off[(size_t)p * kPatTableMax + j] == 0;
+        P.tmpl_diag = P.tmpl_diag && has;
+    }
     auto drop = [&]() {
         hipFree(P.d_pid);
         hipFree(P.d_ptab);
