@@ -14,6 +14,8 @@
 #                 transport), the 300^3 strong headline (38/37 planes), a 100^3
 #                 weak block, distributed CG and CG + GAMG
 #   tests      — pytest -m gpu + smoke()
+#   final      — tests, then default, then the same bench under rocprofv3
+#                --kernel-trace --stats (--no-pmc: counters need their own runs)
 set -o pipefail
 MODE=${1:?mode}; TAG=${2:?tag}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -22,6 +24,13 @@ mkdir -p "$OUT"
 cd "$ROOT" || exit 1
 export TMPDIR=/tmp
 echo "box GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-unset}"
+if [ "$MODE" = final ]; then
+  bash "$ROOT/tools/runs/r06.sh" tests "$TAG" && bash "$ROOT/tools/runs/r06.sh" default "$TAG" || exit 1
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+      -- python3 bench.py --no-pmc > "$OUT/bench_profiled.json" 2> "$OUT/bench_profiled.err" \
+    && echo "profiled bench ok" || { tail -20 "$OUT/bench_profiled.err"; exit 1; }
+  exit 0
+fi
 case $MODE in
   default)
     timeout -k 10 600 python -u bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" \
