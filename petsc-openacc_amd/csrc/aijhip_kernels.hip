@@ -136,6 +136,7 @@ struct OpMultT : OpMult<ADD> {
     using Row = typename OpMult<ADD>::Row;
     static constexpr bool kXoFromSlot = DOT && XS;
     __device__ Row row(int o) const { return {DOT && !XS ? this->x[o] : 0.0}; }
+    __device__ void set_diag(Row &w, double xd) const { w.xo = xd; }
     __device__ void put(int o, double v, double *d, const Row &w) const {
         st_stream(this->y + o, v);
         if (DOT) d[0] += w.xo * v;
@@ -176,12 +177,14 @@ struct OpMgResid {
 // must not alias t. With dot, the finest level also yields CG's z.z and z.b
 // partials (z = x, b = CG's residual). TD (row templates): D^-1 of row o is
 // tdinv[pid[o]], the template's (the same bits as dinv[o]).
-template <bool NT, bool TD = false>
+template <bool NT, bool TD = false, bool XS = false>
 struct OpMgPost {
     static constexpr int kDots = 2;
     static constexpr bool kSeeded = false;
     static constexpr bool kTmplDiag = TD;  // the pipelined template launch stages tdinv in LDS (row_td)
-    static constexpr bool kXoFromSlot = false;
+    // XS (with TD, the pipelined template launch only): t[o] taken from the
+    // row's gathered diagonal slot (set_diag) instead of a load of its own
+    static constexpr bool kXoFromSlot = XS;
     const double *t, *b, *dinv;
     double *x;
     bool dot;
@@ -194,7 +197,8 @@ struct OpMgPost {
     __device__ double gx(int32_t j) const { return t[j]; }
     __device__ double seed(int) const { return 0.0; }
     __device__ Row row(int o) const { return {t[o], b[o], di(o)}; }
-    __device__ Row row_td(int o, double td) const { return {t[o], b[o], td}; }  // td = tdinv[pid[o]]
+    __device__ Row row_td(int o, double td) const { return {XS ? 0.0 : t[o], b[o], td}; }  // td = tdinv[pid[o]]
+    __device__ void set_diag(Row &w, double td) const { w.to = td; }
     __device__ void put(int o, double v, double *d, const Row &w) const {
         const double xo = w.to + 1.0 * (w.dio * (w.bo + (-1.0) * v));
         if constexpr (NT) st_stream(x + o, xo);
@@ -857,7 +861,7 @@ __device__ __forceinline__ void tmpl_finish(const Op &op, const BlockDesc &d, in
         double xo = g.xv[0];
 #pragma unroll
         for (int j = 1; j < F; ++j) xo = ds == j ? g.xv[j] : xo;
-        rw.xo = xo;
+        op.set_diag(rw, xo);
     }
     if (own) op.put(g.r, s, dd, rw);
     if (Op::kDots > 0 && dpart) {
@@ -2236,9 +2240,13 @@ hipError_t launch_mg_resid(const aijhip_mat &A, const double *x, const double *b
 
 hipError_t launch_mg_post(const aijhip_mat &A, const double *t, const double *b, const double *dinv, double *x,
                           double *dpart, hipStream_t s, bool nt, const int *stop, const double *tdinv) {
-    if (tdinv && A.plan.d_pid && A.plan.d_pval)  // row templates: D^-1 per template
+    if (tdinv && A.plan.d_pid && A.plan.d_pval) {  // row templates: D^-1 per template
+        if (A.plan.tmpl_diag && A.plan.pat_maxlen <= kTmplFast)  // the pipelined launch: t[r] from the diagonal slot
+            return launch_stream_op(A, OpMgPost<true, true, true>{t, b, dinv, x, dpart != nullptr, A.plan.d_pid, tdinv},
+                                    dpart, s, -1, stop);
         return launch_stream_op(A, OpMgPost<true, true>{t, b, dinv, x, dpart != nullptr, A.plan.d_pid, tdinv}, dpart,
                                 s, -1, stop);
+    }
     if (nt) return launch_stream_op(A, OpMgPost<true>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
     return launch_stream_op(A, OpMgPost<false>{t, b, dinv, x, dpart != nullptr}, dpart, s, -1, stop);
 }
